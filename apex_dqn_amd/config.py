@@ -1,0 +1,239 @@
+"""Typed configuration for the Ape-X engine.
+
+Accepts the reference ``parameters.json`` schema verbatim (four sections:
+``env_conf``, ``Actor``, ``Learner``, ``Replay_Memory`` --
+reference ``parameters.json:1-34``, consumed at ``main.py:29-33``) and adds an
+optional ``Runtime`` section for everything the reference hard-codes
+(learner T at ``main.py:46``, optimizer at ``learner.py:26``, the
+ExperienceBuffer gamma at ``actor.py:25``) or lacks entirely (device, world
+size, checkpointing, network variant, env backend).
+
+``--set Section.key=value`` overrides are parsed with JSON semantics
+(``--set Learner.replay_sample_size=512``,
+``--set env_conf.state_shape=[4,84,84]``).
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+import json
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence
+
+
+@dataclass
+class EnvConf:
+    state_shape: List[int] = field(default_factory=lambda: [1, 84, 84])
+    action_dim: int = 4
+    name: str = "RiverraidNoFrameskip-v4"
+
+
+@dataclass
+class ActorConf:
+    num_actors: int = 5
+    T: int = 50000
+    num_steps: int = 3
+    epsilon: float = 0.4
+    alpha: float = 7.0
+    gamma: float = 0.99
+    n_step_transition_batch_size: int = 5
+    Q_network_sync_freq: int = 500
+
+
+@dataclass
+class LearnerConf:
+    remove_old_xp_freq: int = 100
+    q_target_sync_freq: int = 2500
+    min_replay_mem_size: int = 20000
+    replay_sample_size: int = 32
+    load_saved_state: Any = False
+
+
+@dataclass
+class ReplayConf:
+    soft_capacity: int = 100000
+    priority_exponent: float = 0.6
+    importance_sampling_exponent: float = 0.4
+
+
+@dataclass
+class RuntimeConf:
+    """Extension section (not present in the reference; all optional)."""
+
+    device: str = "auto"            # "auto" | "cpu" | "cuda"
+    world_size: int = 1
+    dtype: str = "bf16"             # compute dtype on the GPU path
+    seed: int = 0
+    learner_T: int = 500000         # reference hard-codes 500000 (main.py:46)
+    network: str = "auto"           # "auto" | "nature64" | "nature32" | "mlp" | "impala"
+    env_backend: str = "auto"       # "auto" | "synthetic" | "cartpole" | "ale"
+    frame_stack: Optional[int] = None  # defaults to state_shape[0]
+    actors_per_rank: Optional[int] = None  # defaults to num_actors / world_size
+    obs_scale: float = 1.0 / 255.0  # uint8 -> float scale fed to conv nets
+    # optimizer: centered RMSprop as in the Ape-X paper (reference passes the
+    # decay 0.95 as weight_decay by mistake, learner.py:26).
+    lr: float = 0.00025 / 4
+    rms_decay: float = 0.95
+    rms_eps: float = 1.5e-7
+    centered_rmsprop: bool = True
+    grad_clip: float = 40.0
+    loss: str = "huber"             # "huber" | "mse" (0.5*delta^2, reference learner.py:48)
+    huber_delta: float = 1.0
+    priority_eps: float = 1e-6
+    use_is_weights: bool = True
+    ckpt_dir: Optional[str] = None
+    ckpt_freq: int = 0              # learner steps between checkpoints (0 = off)
+    metrics_path: Optional[str] = None
+    log_every: int = 100
+    param_publish_freq: int = 1     # learner steps between param publishes to actors
+    use_hip_kernels: bool = True    # GPU path: hand-written HIP kernels
+    use_graphs: bool = True         # GPU path: capture the learner step in a HIP graph
+    actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)
+    replay_capacity: Optional[int] = None  # physical capacity (default: soft_capacity * 1.25)
+    heartbeat_timeout: float = 60.0
+
+
+@dataclass
+class ApexConfig:
+    env_conf: EnvConf = field(default_factory=EnvConf)
+    Actor: ActorConf = field(default_factory=ActorConf)
+    Learner: LearnerConf = field(default_factory=LearnerConf)
+    Replay_Memory: ReplayConf = field(default_factory=ReplayConf)
+    Runtime: RuntimeConf = field(default_factory=RuntimeConf)
+
+    # ------------------------------------------------------------------ io
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any], strict: bool = False) -> "ApexConfig":
+        sections = {
+            "env_conf": EnvConf,
+            "Actor": ActorConf,
+            "Learner": LearnerConf,
+            "Replay_Memory": ReplayConf,
+            "Runtime": RuntimeConf,
+        }
+        kw = {}
+        for name, klass in sections.items():
+            raw = dict(d.get(name, {}) or {})
+            known = {f.name for f in dataclasses.fields(klass)}
+            unknown = set(raw) - known
+            if unknown and strict:
+                raise KeyError(f"unknown keys in section {name}: {sorted(unknown)}")
+            kw[name] = klass(**{k: v for k, v in raw.items() if k in known})
+        extra = set(d) - set(sections)
+        if extra and strict:
+            raise KeyError(f"unknown sections: {sorted(extra)}")
+        cfg = cls(**kw)
+        cfg.validate()
+        return cfg
+
+    @classmethod
+    def load(cls, path: str, overrides: Sequence[str] = ()) -> "ApexConfig":
+        with open(path, "r") as f:
+            d = json.load(f)
+        d = apply_overrides(d, overrides)
+        return cls.from_dict(d)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    def save(self, path: str) -> None:
+        with open(path, "w") as f:
+            json.dump(self.to_dict(), f, indent=2)
+
+    # ------------------------------------------------------------ derived
+    def validate(self) -> None:
+        ss = self.env_conf.state_shape
+        if not isinstance(ss, (list, tuple)) or len(ss) not in (1, 3):
+            raise ValueError(f"env_conf.state_shape must be [C,H,W] or [D], got {ss}")
+        if self.env_conf.action_dim < 1:
+            raise ValueError("env_conf.action_dim must be >= 1")
+        if self.Actor.num_actors < 1:
+            raise ValueError("Actor.num_actors must be >= 1")
+        if self.Actor.num_steps < 1:
+            raise ValueError("Actor.num_steps must be >= 1")
+        if not (0.0 <= self.Actor.gamma <= 1.0):
+            raise ValueError("Actor.gamma must be in [0,1]")
+        if self.Learner.replay_sample_size < 1:
+            raise ValueError("Learner.replay_sample_size must be >= 1")
+        if self.Runtime.world_size < 1:
+            raise ValueError("Runtime.world_size must be >= 1")
+        if self.Runtime.loss not in ("huber", "mse"):
+            raise ValueError("Runtime.loss must be 'huber' or 'mse'")
+        net = self.network
+        if net in ("nature64", "nature32", "impala") and len(ss) != 3:
+            raise ValueError(f"network {net} needs an image state_shape [C,H,W], got {ss}")
+        if net in ("nature64", "nature32") and tuple(ss[1:]) != (84, 84):
+            raise ValueError(f"NatureCNN expects 84x84 frames, got {ss}")
+
+    @property
+    def network(self) -> str:
+        if self.Runtime.network != "auto":
+            return self.Runtime.network
+        return "nature64" if len(self.env_conf.state_shape) == 3 else "mlp"
+
+    @property
+    def env_backend(self) -> str:
+        if self.Runtime.env_backend != "auto":
+            return self.Runtime.env_backend
+        name = self.env_conf.name.lower()
+        if "cartpole" in name:
+            return "cartpole"
+        if "synthetic" in name:
+            return "synthetic"
+        # Atari ids: use ALE when importable, otherwise a synthetic env of the same shape
+        try:  # pragma: no cover - ale_py is not installed in this image
+            import ale_py  # noqa: F401
+            return "ale"
+        except Exception:
+            return "synthetic"
+
+    @property
+    def frame_stack(self) -> int:
+        if self.Runtime.frame_stack is not None:
+            return int(self.Runtime.frame_stack)
+        ss = self.env_conf.state_shape
+        return int(ss[0]) if len(ss) == 3 else 1
+
+    @property
+    def replay_capacity(self) -> int:
+        if self.Runtime.replay_capacity is not None:
+            return int(self.Runtime.replay_capacity)
+        return int(self.Replay_Memory.soft_capacity * 1.25) + 1024
+
+    def copy(self) -> "ApexConfig":
+        return copy.deepcopy(self)
+
+
+def _parse_value(v: str) -> Any:
+    try:
+        return json.loads(v)
+    except (json.JSONDecodeError, ValueError):
+        low = v.lower()
+        if low in ("true", "false"):
+            return low == "true"
+        return v
+
+
+def apply_overrides(d: Dict[str, Any], overrides: Sequence[str]) -> Dict[str, Any]:
+    """Apply ``Section.key=value`` overrides to a raw config dict."""
+    d = copy.deepcopy(d)
+    for ov in overrides or ():
+        if "=" not in ov:
+            raise ValueError(f"override must be Section.key=value, got {ov!r}")
+        path, val = ov.split("=", 1)
+        parts = path.split(".")
+        if len(parts) != 2:
+            raise ValueError(f"override path must be Section.key, got {path!r}")
+        sec, key = parts
+        d.setdefault(sec, {})[key] = _parse_value(val)
+    return d
+
+
+def epsilon_ladder(num_actors: int, epsilon: float = 0.4, alpha: float = 7.0) -> List[float]:
+    """Per-actor exploration rates eps_i = eps^(1 + alpha*i/(N-1)).
+
+    Reference ``actor.py:111-114`` divides by zero for N=1 (defect A13); a
+    single actor gets the base epsilon here.
+    """
+    denom = max(num_actors - 1, 1)
+    return [float(epsilon ** (1.0 + alpha * i / denom)) for i in range(num_actors)]

@@ -1,0 +1,79 @@
+// Common helpers for the apex_dqn_amd CDNA4 (gfx950) kernels.
+// Written directly for HIP on gfx950: wave64 everywhere, no CUDA shims.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define APEX_EXPORT extern "C" __attribute__((visibility("default")))
+#define APEX_WAVE 64
+
+typedef uint16_t bf16_t;  // raw bf16 bits
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (NaN preserved)
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w = __shfl_xor(v, o, 64);
+    v = v > w ? v : w;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w = __shfl_xor(v, o, 64);
+    v = v < w ? v : w;
+  }
+  return v;
+}
+
+// inclusive prefix sum across the 64 lanes of a wave
+template <typename T>
+__device__ __forceinline__ T wave_inclusive_scan(T v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T w = __shfl_up(v, o, 64);
+    if (lane >= o) v += w;
+  }
+  return v;
+}
+
+// counter-based RNG (splitmix64 finaliser over (seed, counter, index))
+__device__ __forceinline__ uint64_t apex_mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ float apex_uniform(uint64_t seed, uint64_t ctr, uint64_t i) {
+  uint64_t r = apex_mix64(seed ^ apex_mix64(ctr * 0x100000001b3ull + i));
+  return (float)(r >> 40) * (1.0f / 16777216.0f);  // [0,1)
+}
+
+#define APEX_CHECK_LAUNCH() return (int)hipGetLastError()

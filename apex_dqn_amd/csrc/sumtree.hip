@@ -1,0 +1,266 @@
+// HBM-resident prioritized-replay shard: 64-ary sum-tree + record ring.
+//
+// Replaces the reference ReplayMemory (replay.py:8-84: dict priorities with an
+// O(N^2) recompute per add/update, O(B*N) sampling, FIFO list eviction) with a
+// tree whose fan-out equals the wavefront width: one wave descends one level
+// per coalesced 64-child load + wave prefix scan, so a 2^21-leaf shard is 4
+// dependent loads deep instead of 21 (binary tree).
+//
+// Layout: leaves = p^alpha (fp32, [cap]); internal levels k=1..L in one fp64
+// array (level k has ceil(n_{k-1}/64) nodes, root at level L).  Leaf writes
+// propagate fp64 deltas up with hardware fp64 atomics (no level-synchronous
+// passes, one launch); tree_rebuild re-derives every internal node exactly
+// from the leaves (run at the eviction cadence) so fp drift never accumulates.
+// Duplicate indices in one update batch: last occurrence wins (deterministic).
+#include "apex_common.h"
+
+struct TreeDesc {
+  float* leaf;
+  double* nodes;
+  int64_t off[8];
+  int64_t n[8];
+  int L;
+  uint32_t* min_bits;  // running min over positive leaves (float bits)
+};
+
+struct RecordDesc {
+  int32_t* obs;   // [cap, C] frame-ring slots of S_t's stack
+  int32_t* nxt;   // [cap, C] frame-ring slots of S_{t+n}'s stack
+  int32_t* act;   // [cap]
+  float* rew;     // [cap]
+  float* gam;     // [cap]
+  int32_t* gen;   // [cap] slot generation (bumped on every insert)
+  int C;
+  int64_t cap;
+};
+
+__device__ __forceinline__ void tree_set_leaf(const TreeDesc& t, int64_t i, float v) {
+  float old = t.leaf[i];
+  t.leaf[i] = v;
+  double d = (double)v - (double)old;
+  if (d != 0.0) {
+    int64_t node = i;
+    for (int k = 1; k <= t.L; ++k) {
+      node >>= 6;
+      atomicAdd(&t.nodes[t.off[k] + node], d);
+    }
+  }
+  if (v > 0.f) atomicMin(t.min_bits, __float_as_uint(v));
+}
+
+// mode 0: values are leaf values; mode 1: values are |td| -> (|td|+eps)^alpha,
+// skipping evicted leaves (leaf == 0) and slots re-used since sampling (gen).
+__global__ void tree_update_kernel(TreeDesc t, const int64_t* __restrict__ idx,
+                                   const float* __restrict__ values, int n, int mode,
+                                   float alpha, float eps, const int32_t* __restrict__ gen_expect,
+                                   const int32_t* __restrict__ gen, int dedupe,
+                                   uint64_t* ctr_to_bump) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ctr_to_bump != nullptr && i == 0) ctr_to_bump[0] += 1;
+  if (i >= n) return;
+  int64_t s = idx[i];
+  if (s < 0 || s >= t.n[0]) return;
+  if (dedupe) {
+    for (int j = i + 1; j < n; ++j)
+      if (idx[j] == s) return;  // a later write to the same leaf wins
+  }
+  float v = values[i];
+  if (mode == 1) {
+    if (t.leaf[s] <= 0.f) return;
+    if (gen_expect != nullptr && gen[s] != gen_expect[i]) return;
+    v = powf(fabsf(v) + eps, alpha);
+  }
+  tree_set_leaf(t, s, v);
+}
+
+// zero `count` leaves starting at ring slot `start` (FIFO eviction)
+__global__ void tree_zero_range_kernel(TreeDesc t, int64_t start, int64_t count) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  int64_t s = (start + i) % t.n[0];
+  if (t.leaf[s] != 0.f) tree_set_leaf(t, s, 0.f);
+}
+
+// scatter K staged records into ring slots start..start+K-1 (mod cap) and set
+// their leaves to (prio+eps)^alpha
+__global__ void replay_insert_kernel(TreeDesc t, RecordDesc r, int64_t start, int K,
+                                     const int32_t* __restrict__ s_obs,
+                                     const int32_t* __restrict__ s_nxt,
+                                     const int32_t* __restrict__ s_act,
+                                     const float* __restrict__ s_rew,
+                                     const float* __restrict__ s_gam,
+                                     const float* __restrict__ s_prio, float alpha, float eps) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= K) return;
+  int64_t s = (start + i) % r.cap;
+  for (int c = 0; c < r.C; ++c) {
+    r.obs[s * r.C + c] = s_obs[(int64_t)i * r.C + c];
+    r.nxt[s * r.C + c] = s_nxt[(int64_t)i * r.C + c];
+  }
+  r.act[s] = s_act[i];
+  r.rew[s] = s_rew[i];
+  r.gam[s] = s_gam[i];
+  r.gen[s] += 1;
+  tree_set_leaf(t, s, powf(fabsf(s_prio[i]) + eps, alpha));
+}
+
+// Stratified proportional sampling: one wave per sample, 64-ary descent.
+// Also gathers the sampled records and the IS weight
+//   w_i = ((p_i/total) / ratio_min)^-beta,  ratio_min = min_j p_j/total
+// (global over shards when `ratio_min_global` is given) -- max-normalised.
+__global__ void tree_sample_kernel(TreeDesc t, RecordDesc r, int B, uint64_t seed,
+                                   const uint64_t* __restrict__ ctr, float beta,
+                                   const float* __restrict__ ratio_min_global,
+                                   int64_t* __restrict__ out_idx, float* __restrict__ out_w,
+                                   int32_t* __restrict__ out_gen, int32_t* __restrict__ out_obs,
+                                   int32_t* __restrict__ out_nxt, int32_t* __restrict__ out_act,
+                                   float* __restrict__ out_rew, float* __restrict__ out_gam) {
+  const int lane = threadIdx.x & 63;
+  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (b >= B) return;
+  const double total = t.nodes[t.off[t.L]];
+  const float uu = apex_uniform(seed, ctr[0], (uint64_t)b);
+  double u = ((double)b + (double)uu) * (total / (double)B);
+  int64_t node = 0;
+  for (int k = t.L - 1; k >= 0; --k) {
+    int64_t child = node * 64 + lane;
+    double v = 0.0;
+    if (child < t.n[k]) v = (k == 0) ? (double)t.leaf[child] : t.nodes[t.off[k] + child];
+    double incl = wave_inclusive_scan(v, lane);
+    // first child whose inclusive prefix exceeds u; fall back to the last
+    // non-empty child when round-off pushes u past the subtree mass
+    uint64_t pass = __ballot(incl > u && v > 0.0);
+    uint64_t nonempty = __ballot(v > 0.0);
+    int sel;
+    if (pass) sel = __ffsll((unsigned long long)pass) - 1;
+    else sel = nonempty ? 63 - __clzll((long long)nonempty) : 0;
+    double excl = __shfl(incl - v, sel, 64);
+    u -= excl;
+    node = node * 64 + sel;
+  }
+  const int64_t s = node < t.n[0] ? node : t.n[0] - 1;
+  if (lane == 0) {
+    float p = t.leaf[s];
+    float ratio = ratio_min_global ? ratio_min_global[0]
+                                   : (float)((double)__uint_as_float(t.min_bits[0]) / total);
+    float pr = (float)((double)p / total);
+    float w = (p > 0.f && ratio > 0.f) ? powf(pr / ratio, -beta) : 0.f;
+    out_idx[b] = s;
+    out_w[b] = fminf(w, 1.0f);
+    out_gen[b] = r.gen[s];
+    out_act[b] = r.act[s];
+    out_rew[b] = r.rew[s];
+    out_gam[b] = r.gam[s];
+  }
+  for (int c = lane; c < r.C; c += 64) {
+    out_obs[(int64_t)b * r.C + c] = r.obs[s * r.C + c];
+    out_nxt[(int64_t)b * r.C + c] = r.nxt[s * r.C + c];
+  }
+}
+
+// Exact rebuild of one internal level from its children (wave per parent);
+// the leaf pass also recomputes the min over positive leaves.
+__global__ void tree_reduce_level_kernel(const float* __restrict__ leaf, const double* __restrict__ src,
+                                         int64_t nsrc, double* __restrict__ dst, int64_t ndst,
+                                         uint32_t* min_bits) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (p >= ndst) return;
+  int64_t c = p * 64 + lane;
+  double v = 0.0;
+  float mn = __uint_as_float(0x7f800000u);
+  if (c < nsrc) {
+    if (leaf) {
+      float f = leaf[c];
+      v = (double)f;
+      if (f > 0.f) mn = f;
+    } else {
+      v = src[c];
+    }
+  }
+  v = wave_sum(v);
+  if (leaf) mn = wave_min(mn);
+  if (lane == 0) {
+    dst[p] = v;
+    if (leaf && mn < __uint_as_float(0x7f800000u)) atomicMin(min_bits, __float_as_uint(mn));
+  }
+}
+
+__global__ void fill_u32_kernel(uint32_t* p, uint32_t v, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// gather stacked frames: out[b, c] = ring[slots[b, c]]  (uint8, frame_bytes each)
+__global__ void gather_frames_kernel(const uint8_t* __restrict__ ring, const int32_t* __restrict__ slots,
+                                     int nstack, int64_t frame_bytes, uint8_t* __restrict__ out) {
+  const int bc = blockIdx.x;  // one block per (sample, channel)
+  const int32_t s = slots[bc];
+  const uint4* src = reinterpret_cast<const uint4*>(ring + (int64_t)s * frame_bytes);
+  uint4* dst = reinterpret_cast<uint4*>(out + (int64_t)bc * frame_bytes);
+  const int64_t nv = frame_bytes / 16;
+  for (int64_t i = threadIdx.x; i < nv; i += blockDim.x) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------- launchers
+static inline int blocks_for(int64_t n, int t) { return (int)((n + t - 1) / t); }
+
+APEX_EXPORT int apex_tree_update(TreeDesc t, const int64_t* idx, const float* values, int n, int mode,
+                                 float alpha, float eps, const int32_t* gen_expect, const int32_t* gen,
+                                 int dedupe, uint64_t* ctr_to_bump, hipStream_t st) {
+  if (n <= 0 && ctr_to_bump == nullptr) return 0;
+  int nb = n > 0 ? blocks_for(n, 256) : 1;
+  tree_update_kernel<<<nb, 256, 0, st>>>(t, idx, values, n, mode, alpha, eps, gen_expect, gen, dedupe,
+                                         ctr_to_bump);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_tree_zero_range(TreeDesc t, int64_t start, int64_t count, hipStream_t st) {
+  if (count <= 0) return 0;
+  tree_zero_range_kernel<<<blocks_for(count, 256), 256, 0, st>>>(t, start, count);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_replay_insert(TreeDesc t, RecordDesc r, int64_t start, int K, const int32_t* s_obs,
+                                   const int32_t* s_nxt, const int32_t* s_act, const float* s_rew,
+                                   const float* s_gam, const float* s_prio, float alpha, float eps,
+                                   hipStream_t st) {
+  if (K <= 0) return 0;
+  replay_insert_kernel<<<blocks_for(K, 256), 256, 0, st>>>(t, r, start, K, s_obs, s_nxt, s_act, s_rew,
+                                                           s_gam, s_prio, alpha, eps);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_tree_sample(TreeDesc t, RecordDesc r, int B, uint64_t seed, const uint64_t* ctr,
+                                 float beta, const float* ratio_min_global, int64_t* out_idx, float* out_w,
+                                 int32_t* out_gen, int32_t* out_obs, int32_t* out_nxt, int32_t* out_act,
+                                 float* out_rew, float* out_gam, hipStream_t st) {
+  if (B <= 0) return 0;
+  const int waves_per_block = 4;
+  tree_sample_kernel<<<blocks_for(B, waves_per_block), 64 * waves_per_block, 0, st>>>(
+      t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
+      out_rew, out_gam);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_tree_rebuild(TreeDesc t, hipStream_t st) {
+  fill_u32_kernel<<<1, 64, 0, st>>>(t.min_bits, 0x7f800000u, 1);
+  for (int k = 1; k <= t.L; ++k) {
+    int64_t nd = t.n[k];
+    const int wpb = 4;
+    tree_reduce_level_kernel<<<blocks_for(nd, wpb), 64 * wpb, 0, st>>>(
+        k == 1 ? t.leaf : nullptr, k == 1 ? nullptr : t.nodes + t.off[k - 1], t.n[k - 1],
+        t.nodes + t.off[k], nd, t.min_bits);
+  }
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_gather_frames(const uint8_t* ring, const int32_t* slots, int n_slots, int nstack,
+                                   int64_t frame_bytes, uint8_t* out, hipStream_t st) {
+  if (n_slots <= 0) return 0;
+  if (frame_bytes % 16) return (int)hipErrorInvalidValue;
+  gather_frames_kernel<<<n_slots, 256, 0, st>>>(ring, slots, nstack, frame_bytes, out);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_abi_version() { return 1; }

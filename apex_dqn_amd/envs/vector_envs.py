@@ -1,0 +1,264 @@
+"""Vectorised environments.
+
+The reference builds a single ``gym.make(name)`` per actor with no wrappers
+(``env.py:3-4``) and preprocesses frames with a broken truncating reshape
+(``actor.py:117-119``, defect A14).  gym / ALE are not installed in this
+image (nor on the offline GPU box), so the engine ships:
+
+* ``CartPoleVec``   -- numpy CartPole-v1 dynamics for E envs (BASELINE config 1);
+* ``SyntheticAtariVec`` -- Atari-shaped (84x84 uint8 frame per step) env with
+  learnable dynamics, for the GPU configs on synthetic frames;
+* ``AtariPreprocess`` + ``ALEVec`` -- correct Atari preprocessing (gray,
+  area-resize to 84x84, frame-skip with max-pool, no-op starts, reward clip)
+  around ``ale_py`` when it is importable.
+
+All envs auto-reset: ``step`` returns the first observation of the next
+episode for envs that finished.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import numpy as np
+
+
+class CartPoleVec:
+    """CartPole-v1 (Barto, Sutton & Anderson) physics, vectorised."""
+
+    gravity = 9.8
+    masscart = 1.0
+    masspole = 0.1
+    total_mass = masscart + masspole
+    length = 0.5
+    polemass_length = masspole * length
+    force_mag = 10.0
+    tau = 0.02
+    theta_threshold = 12 * 2 * math.pi / 360
+    x_threshold = 2.4
+    max_steps = 500
+
+    obs_shape = (4,)
+    obs_dtype = np.float32
+    action_dim = 2
+    frame_based = False
+
+    def __init__(self, num_envs: int, seed: int = 0):
+        self.E = int(num_envs)
+        self.rng = np.random.default_rng(seed)
+        self.state = np.zeros((self.E, 4), np.float64)
+        self.t = np.zeros(self.E, np.int64)
+        self.ep_ret = np.zeros(self.E, np.float64)
+
+    def _reset_idx(self, idx):
+        self.state[idx] = self.rng.uniform(-0.05, 0.05, size=(len(idx), 4))
+        self.t[idx] = 0
+        self.ep_ret[idx] = 0.0
+
+    def reset(self) -> np.ndarray:
+        self._reset_idx(np.arange(self.E))
+        return self.state.astype(np.float32)
+
+    def step(self, actions: np.ndarray):
+        x, x_dot, th, th_dot = self.state.T
+        force = np.where(np.asarray(actions) == 1, self.force_mag, -self.force_mag)
+        cos, sin = np.cos(th), np.sin(th)
+        temp = (force + self.polemass_length * th_dot ** 2 * sin) / self.total_mass
+        th_acc = (self.gravity * sin - cos * temp) / (
+            self.length * (4.0 / 3.0 - self.masspole * cos ** 2 / self.total_mass))
+        x_acc = temp - self.polemass_length * th_acc * cos / self.total_mass
+        x = x + self.tau * x_dot
+        x_dot = x_dot + self.tau * x_acc
+        th = th + self.tau * th_dot
+        th_dot = th_dot + self.tau * th_acc
+        self.state = np.stack([x, x_dot, th, th_dot], axis=1)
+        self.t += 1
+        term = (np.abs(x) > self.x_threshold) | (np.abs(th) > self.theta_threshold)
+        trunc = self.t >= self.max_steps
+        done = term | trunc
+        rew = np.ones(self.E, np.float32)
+        self.ep_ret += rew
+        info = {"episode_return": np.where(done, self.ep_ret, np.nan),
+                "episode_length": np.where(done, self.t, -1), "truncated": trunc & ~term}
+        idx = np.nonzero(done)[0]
+        if len(idx):
+            self._reset_idx(idx)
+        return self.state.astype(np.float32), rew, done, info
+
+
+class SyntheticAtariVec:
+    """Atari-shaped synthetic env: one 84x84 uint8 frame per step.
+
+    Hidden state s in [0, S); the frame is a fixed random "sprite sheet" image
+    for s plus a moving bar, so a conv net can infer s.  Reward 1 when the
+    action equals s mod A.  Episodes end with probability ``p_end`` per step
+    or at ``max_len``.
+    """
+
+    obs_dtype = np.uint8
+    frame_based = True
+
+    def __init__(self, num_envs: int, action_dim: int = 6, seed: int = 0,
+                 num_states: int = 32, p_end: float = 0.01, max_len: int = 1000,
+                 frame_hw=(84, 84)):
+        self.E = int(num_envs)
+        self.action_dim = int(action_dim)
+        self.S = int(num_states)
+        self.rng = np.random.default_rng(seed)
+        h, w = frame_hw
+        self.obs_shape = (h, w)
+        bank_rng = np.random.default_rng(1234)
+        self.bank = bank_rng.integers(0, 64, size=(self.S, h, w), dtype=np.uint8)
+        for s in range(self.S):   # a bright block whose position encodes s
+            r0 = (s * 5) % (h - 12)
+            c0 = (s * 11) % (w - 12)
+            self.bank[s, r0:r0 + 12, c0:c0 + 12] = 200
+        self.p_end = float(p_end)
+        self.max_len = int(max_len)
+        self.s = np.zeros(self.E, np.int64)
+        self.t = np.zeros(self.E, np.int64)
+        self.ep_ret = np.zeros(self.E, np.float64)
+
+    def _frames(self) -> np.ndarray:
+        f = self.bank[self.s].copy()
+        col = (self.t * 3) % self.obs_shape[1]
+        f[np.arange(self.E), :, col] = 255
+        return f
+
+    def reset(self) -> np.ndarray:
+        self.s = self.rng.integers(0, self.S, size=self.E)
+        self.t[:] = 0
+        self.ep_ret[:] = 0
+        return self._frames()
+
+    def step(self, actions: np.ndarray):
+        actions = np.asarray(actions, np.int64)
+        rew = (actions == (self.s % self.action_dim)).astype(np.float32)
+        self.s = (self.s * 7 + actions + 1 + self.rng.integers(0, 2, size=self.E)) % self.S
+        self.t += 1
+        self.ep_ret += rew
+        done = (self.rng.random(self.E) < self.p_end) | (self.t >= self.max_len)
+        info = {"episode_return": np.where(done, self.ep_ret, np.nan),
+                "episode_length": np.where(done, self.t, -1)}
+        idx = np.nonzero(done)[0]
+        if len(idx):
+            self.s[idx] = self.rng.integers(0, self.S, size=len(idx))
+            self.t[idx] = 0
+            self.ep_ret[idx] = 0
+        return self._frames(), rew, done, info
+
+
+def _area_matrix(n_out: int, n_in: int) -> np.ndarray:
+    """Row-stochastic area-interpolation matrix (n_out, n_in)."""
+    m = np.zeros((n_out, n_in), np.float64)
+    scale = n_in / n_out
+    for i in range(n_out):
+        a, b = i * scale, (i + 1) * scale
+        j0, j1 = int(math.floor(a)), int(math.ceil(b))
+        for j in range(j0, min(j1, n_in)):
+            lo, hi = max(a, j), min(b, j + 1)
+            if hi > lo:
+                m[i, j] = (hi - lo) / scale
+    return m
+
+
+class AtariPreprocess:
+    """Gray-scale + area resize to 84x84 uint8 (fixes defect A14)."""
+
+    def __init__(self, in_hw=(210, 160), out_hw=(84, 84)):
+        self.ry = _area_matrix(out_hw[0], in_hw[0])
+        self.rx = _area_matrix(out_hw[1], in_hw[1])
+        self.w = np.array([0.299, 0.587, 0.114])
+
+    def __call__(self, rgb: np.ndarray) -> np.ndarray:
+        """rgb: (..., H, W, 3) uint8 -> (..., 84, 84) uint8."""
+        gray = rgb.astype(np.float64) @ self.w
+        out = np.einsum("oh,...hw,pw->...op", self.ry, gray, self.rx)
+        return np.clip(np.rint(out), 0, 255).astype(np.uint8)
+
+
+class ALEVec:  # pragma: no cover - ale_py is not available in this image
+    """Vectorised ALE with standard DQN wrappers (frame-skip 4 + max-pool,
+    up to 30 no-op starts, reward clipping, 84x84 gray)."""
+
+    obs_dtype = np.uint8
+    frame_based = True
+    obs_shape = (84, 84)
+
+    def __init__(self, game: str, num_envs: int, seed: int = 0, frame_skip: int = 4,
+                 noop_max: int = 30, clip_rewards: bool = True):
+        import ale_py  # noqa: F401
+        from ale_py import ALEInterface, roms
+        self.E = int(num_envs)
+        self.envs = []
+        name = game.replace("NoFrameskip-v4", "").replace("-v0", "")
+        snake = "".join("_" + c.lower() if c.isupper() else c for c in name).lstrip("_")
+        for i in range(self.E):
+            ale = ALEInterface()
+            ale.setInt("random_seed", seed + i)
+            ale.setFloat("repeat_action_probability", 0.0)
+            ale.loadROM(roms.get_rom_path(snake))
+            self.envs.append(ale)
+        self.actions = self.envs[0].getMinimalActionSet()
+        self.action_dim = len(self.actions)
+        self.pre = AtariPreprocess()
+        self.frame_skip, self.noop_max, self.clip = frame_skip, noop_max, clip_rewards
+        self.rng = np.random.default_rng(seed)
+        self.ep_ret = np.zeros(self.E)
+        self.ep_len = np.zeros(self.E, np.int64)
+
+    def _obs(self, i, buf):
+        return self.pre(np.maximum(buf[0], buf[1]))
+
+    def _reset_one(self, i):
+        ale = self.envs[i]
+        ale.reset_game()
+        for _ in range(int(self.rng.integers(0, self.noop_max + 1))):
+            ale.act(0)
+        f = ale.getScreenRGB()
+        return self.pre(f)
+
+    def reset(self):
+        return np.stack([self._reset_one(i) for i in range(self.E)])
+
+    def step(self, actions):
+        obs = np.zeros((self.E, 84, 84), np.uint8)
+        rew = np.zeros(self.E, np.float32)
+        done = np.zeros(self.E, bool)
+        ep_r = np.full(self.E, np.nan)
+        ep_l = np.full(self.E, -1)
+        for i, a in enumerate(actions):
+            ale = self.envs[i]
+            r, bufs = 0.0, []
+            for k in range(self.frame_skip):
+                r += ale.act(self.actions[int(a)])
+                if k >= self.frame_skip - 2:
+                    bufs.append(ale.getScreenRGB())
+                if ale.game_over():
+                    break
+            while len(bufs) < 2:
+                bufs.append(ale.getScreenRGB())
+            self.ep_ret[i] += r
+            self.ep_len[i] += 1
+            rew[i] = np.sign(r) if self.clip else r
+            if ale.game_over():
+                done[i] = True
+                ep_r[i], ep_l[i] = self.ep_ret[i], self.ep_len[i]
+                self.ep_ret[i], self.ep_len[i] = 0, 0
+                obs[i] = self._reset_one(i)
+            else:
+                obs[i] = self._obs(i, bufs)
+        return obs, rew, done, {"episode_return": ep_r, "episode_length": ep_l}
+
+
+def make_vec_env(backend: str, name: str, num_envs: int, action_dim: int,
+                 seed: int = 0, frame_hw: Optional[Tuple[int, int]] = None):
+    """Factory replacing ``make_local_env`` (``env.py:3-4``)."""
+    if backend == "cartpole":
+        return CartPoleVec(num_envs, seed=seed)
+    if backend == "synthetic":
+        return SyntheticAtariVec(num_envs, action_dim=action_dim, seed=seed,
+                                 frame_hw=frame_hw or (84, 84))
+    if backend == "ale":  # pragma: no cover
+        return ALEVec(name, num_envs, seed=seed)
+    raise ValueError(f"unknown env backend {backend!r}")

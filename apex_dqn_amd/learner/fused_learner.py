@@ -1,0 +1,239 @@
+"""MI355X learner for the dueling NatureCNN: one GPU-resident step.
+
+Per step (B = local batch), entirely on device, no host sync:
+
+  sample (64-ary sum-tree, IS weights)           csrc/sumtree.hip
+  gather S_t | S_{t+n} frame stacks (uint8)      csrc/sumtree.hip (or fused into conv1)
+  online fwd on 2B rows, target fwd on B rows    conv1/conv2/conv3/fc
+  DDQN target + Huber*IS loss + |delta| + dH     csrc/ddqn_head.hip
+  backward: heads, fc, conv3, conv2, conv1       head_wgrad / fc / conv dgrad+wgrad
+  (DP) flat-gradient all-reduce over RCCL        parallel/dist.py
+  grad-norm clip + centered RMSprop + bf16 pack  csrc/optimizer.hip
+  priority write-back (generation-checked)       csrc/sumtree.hip
+
+Periodic host work between steps: target sync (D2D copy, every
+``q_target_sync_freq``), FIFO eviction + exact tree rebuild (every
+``remove_old_xp_freq``), checkpoint (rank 0).
+
+Reference parity: ``Learner.learn`` / ``compute_loss_and_priorities`` /
+``update_Q`` (``learner.py:29-80``) with defects A16-A21, A30 fixed.
+The step can be captured once and replayed as a HIP graph (``use_graphs``).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Optional
+
+import torch
+
+from ..config import ApexConfig
+from ..models.dueling import DuellingDQN
+from ..models.flat_params import (FlatLayout, flat_to_reference_state, nature_segments,
+                                  reference_state_to_flat)
+from ..ops.fused_ops import HipBackend, TorchBackend
+from ..utils.checkpoint import load_checkpoint, save_checkpoint
+
+
+class FusedNatureLearner:
+    def __init__(self, cfg: ApexConfig, device, replay, comm=None, backend: Optional[str] = None,
+                 batch_size: Optional[int] = None):
+        self.cfg = cfg
+        self.rt = cfg.Runtime
+        self.device = torch.device(device)
+        self.replay = replay
+        self.comm = comm
+        self.C = cfg.frame_stack
+        self.A = int(cfg.env_conf.action_dim)
+        self.B = int(batch_size or cfg.Learner.replay_sample_size)
+        c1 = 32 if cfg.network == "nature32" else 64
+        if c1 != 64:
+            raise NotImplementedError("fused learner implements the reference 64-filter conv1")
+        if backend is None:
+            backend = "hip" if (self.device.type == "cuda" and self.rt.use_hip_kernels) else "torch"
+        self.ops = HipBackend() if backend == "hip" else TorchBackend(
+            torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        self.act_dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        d = self.device
+        self.layout = FlatLayout(nature_segments(self.C, self.A, c1))
+        n = self.layout.numel
+        self.p32 = torch.zeros(n, dtype=torch.float32, device=d)
+        self.pbf = torch.zeros(n, dtype=self.act_dtype, device=d)
+        self.g32 = torch.zeros(n, dtype=torch.float32, device=d)
+        self.rms_v = torch.zeros(n, dtype=torch.float32, device=d)
+        self.rms_m = torch.zeros(n, dtype=torch.float32, device=d)
+        self.t32 = torch.zeros(n, dtype=torch.float32, device=d)
+        self.tbf = torch.zeros(n, dtype=self.act_dtype, device=d)
+        self.P = self.layout.views(self.p32)
+        self.Pb = self.layout.views(self.pbf)
+        self.G = self.layout.views(self.g32)
+        self.T = self.layout.views(self.t32)
+        self.Tb = self.layout.views(self.tbf)
+        # random init identical in distribution to the reference module (torch default init)
+        init = DuellingDQN((self.C, 84, 84), self.A)
+        reference_state_to_flat(init.state_dict(), {k: v for k, v in self.P.items()})
+        if comm is not None and comm.world_size > 1:
+            comm.broadcast_flat(self.p32)
+        self.pbf.copy_(self.p32)
+        self.sync_target()
+        self.num_q_updates = 0
+        self._alloc(self.B)
+        self._graph = None
+        self._graph_ready = False
+        ls = cfg.Learner.load_saved_state
+        if ls:
+            self.load(ls)
+
+    # ------------------------------------------------------------- buffers
+    def _alloc(self, B: int) -> None:
+        d, ad = self.device, self.act_dtype
+        C = self.C
+        self.S = self.replay.alloc_sample_buffers(B)
+        self.slots = torch.zeros(2 * B, C, dtype=torch.int32, device=d)
+        self.frames = torch.zeros(2 * B, C, 84, 84, dtype=torch.uint8, device=d)
+        self.y1 = torch.zeros(2 * B, 20, 20, 64, dtype=ad, device=d)
+        self.y2 = torch.zeros(2 * B, 9, 9, 64, dtype=ad, device=d)
+        self.y3 = torch.zeros(2 * B, 7, 7, 64, dtype=ad, device=d)
+        self.h = torch.zeros(2 * B, 1024, dtype=ad, device=d)
+        self.y1t = torch.zeros(B, 20, 20, 64, dtype=ad, device=d)
+        self.y2t = torch.zeros(B, 9, 9, 64, dtype=ad, device=d)
+        self.y3t = torch.zeros(B, 7, 7, 64, dtype=ad, device=d)
+        self.ht = torch.zeros(B, 1024, dtype=ad, device=d)
+        self.dH = torch.zeros(B, 1024, dtype=ad, device=d)
+        self.dY3 = torch.zeros(B, 7, 7, 64, dtype=ad, device=d)
+        self.dY2 = torch.zeros(B, 9, 9, 64, dtype=ad, device=d)
+        self.dY1 = torch.zeros(B, 20, 20, 64, dtype=ad, device=d)
+        self.dhead = torch.zeros(B, self.A + 1, dtype=torch.float32, device=d)
+        self.td_abs = torch.zeros(B, dtype=torch.float32, device=d)
+        self.loss_b = torch.zeros(B, dtype=torch.float32, device=d)
+        self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
+        self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
+        # head-gradient region (zeroed by the head kernel, accumulated by head_wgrad)
+        o0 = self.layout.offsets["wv"]
+        o1 = self.layout.offsets["ba"] + self.A
+        self.g_head_region = self.g32[o0:o1]
+
+    # ------------------------------------------------------------ forward
+    def forward_online(self, frames, rows: int, y1, y2, y3, h, Pb):
+        ops, rt = self.ops, self.rt
+        ops.conv1_fwd(frames[:rows], Pb["w1"], Pb["b1"], rt.obs_scale, y1[:rows])
+        ops.conv_fwd(y1[:rows], Pb["w2"], Pb["b2"], 2, y2[:rows])
+        ops.conv_fwd(y2[:rows], Pb["w3"], Pb["b3"], 1, y3[:rows])
+        ops.fc_fwd(y3[:rows].reshape(rows, 3136), Pb["wfc"], Pb["bfc"], h[:rows])
+
+    def _head_params(self, V):
+        return {k: V[k] for k in ("wv", "bv", "wa", "ba")}
+
+    # ---------------------------------------------------------------- step
+    def _step_body(self, ratio_min: Optional[torch.Tensor] = None) -> None:
+        B, rt, ops = self.B, self.rt, self.ops
+        S = self.replay.sample(B, out=self.S, ratio_min_global=ratio_min)
+        self.slots[:B].copy_(S["obs"])
+        self.slots[B:].copy_(S["nxt"])
+        self.replay.gather_frames(self.slots, self.frames)
+        # online forward on [S_t ; S_tpn], target forward on S_tpn
+        self.forward_online(self.frames, 2 * B, self.y1, self.y2, self.y3, self.h, self.Pb)
+        self.forward_online(self.frames[B:], B, self.y1t, self.y2t, self.y3t, self.ht, self.Tb)
+        isw = S["weights"] if rt.use_is_weights else None
+        ops.head(self.h, self.ht, self._head_params(self.P), self._head_params(self.T), S["act"], S["rew"],
+                 S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / B, self.td_abs, self.loss_b,
+                 self.dH, self.dhead, zero=self.g_head_region)
+        ops.head_wgrad(self.h, self.dhead, self.G)
+        G, Pb = self.G, self.Pb
+        ops.fc_bwd(self.dH, self.y3[:B], Pb["wfc"], self.dY3, G["wfc"], G["bfc"])
+        ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2)
+        ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"])
+        ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1)
+        ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"])
+        ops.conv1_wgrad(self.dY1, self.frames[:B], rt.obs_scale, G["w1"], G["b1"])
+        if self.comm is not None and self.comm.world_size > 1:
+            self.comm.allreduce_flat(self.g32, average=True)
+        ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
+                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
+        self.replay.update_priorities(S["idx"], self.td_abs, S["gen"])
+
+    def step(self, ratio_min: Optional[torch.Tensor] = None) -> None:
+        """One learner update (asynchronous on the current stream)."""
+        if self.rt.use_graphs and self.device.type == "cuda":
+            if self._graph is None:
+                self._capture(ratio_min)
+            self._graph.replay()
+        else:
+            self._step_body(ratio_min)
+        self.num_q_updates += 1
+        L = self.cfg.Learner
+        if self.num_q_updates % L.q_target_sync_freq == 0:
+            self.sync_target()
+
+    def _capture(self, ratio_min) -> None:
+        # warm up on a side stream (allocator pools, library handles), then capture
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        snap = self._snapshot()
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._step_body(ratio_min)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._restore(snap)
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph):
+            self._step_body(ratio_min)
+        # capture recorded the step without executing it; state is as before
+
+    def _snapshot(self):
+        rp = self.replay
+        return [t.clone() for t in (self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes,
+                                    rp.min_bits, rp.ctr)]
+
+    def _restore(self, snap) -> None:
+        rp = self.replay
+        for dst, src in zip((self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes, rp.min_bits,
+                             rp.ctr), snap):
+            dst.copy_(src)
+
+    def sync_target(self) -> None:
+        self.t32.copy_(self.p32)
+        self.tbf.copy_(self.pbf)
+
+    # ------------------------------------------------------------ metrics
+    def last_metrics(self) -> Dict[str, float]:
+        return {"loss": float(self.loss_b.mean()), "td_abs_mean": float(self.td_abs.mean()),
+                "grad_norm": float(self.gnorm[0])}
+
+    def q_values(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        """Greedy-evaluation helper: q for a (N, C, 84, 84) uint8 batch."""
+        sd = self.reference_state_dict()
+        net = DuellingDQN((self.C, 84, 84), self.A).to(self.device)
+        net.load_state_dict(sd)
+        with torch.no_grad():
+            return net(frames_u8.to(self.device))[2]
+
+    # ------------------------------------------------------------- params
+    def reference_state_dict(self):
+        return flat_to_reference_state(self.P)
+
+    def load_reference_state_dict(self, sd) -> None:
+        reference_state_to_flat(sd, self.P)
+        self.pbf.copy_(self.p32)
+
+    def save(self, path: str) -> None:
+        tgt = flat_to_reference_state(self.T)
+        save_checkpoint(path, self.reference_state_dict(), Q_target_state=tgt,
+                        optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
+                        num_q_updates=self.num_q_updates, config=self.cfg.to_dict())
+
+    def load(self, path: str) -> bool:
+        ck = load_checkpoint(path)
+        if ck is None:
+            return False
+        self.load_reference_state_dict(ck["Q_state"])
+        if "Q_target_state" in ck:
+            reference_state_to_flat(ck["Q_target_state"], self.T)
+            self.tbf.copy_(self.t32)
+        else:
+            self.sync_target()
+        opt = ck.get("optimizer_state")
+        if isinstance(opt, dict) and "rms_v" in opt:
+            self.rms_v.copy_(opt["rms_v"])
+            self.rms_m.copy_(opt["rms_m"])
+        self.num_q_updates = int(ck.get("num_q_updates", 0))
+        self._graph = None
+        return True

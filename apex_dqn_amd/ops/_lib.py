@@ -1,0 +1,128 @@
+"""ctypes binding of ``libapex_kernels.so`` (C ABI, built in-tree by ``ops/build.py``).
+
+The library is loaded *after* torch so that its ``libamdhip64.so.7`` NEEDED
+entry resolves (by SONAME) to the HIP runtime torch already loaded: kernels
+then share torch's device context and run on torch's current stream
+(``torch.cuda.current_stream().cuda_stream``), so they are captured by
+``torch.cuda.graph`` like any torch op.
+
+On a GPU host a missing or stale library is an error (``require_kernels``),
+never a silent fallback: the torch implementations in ``ops/reference.py``
+exist only for CPU runs and as test oracles.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+from . import build as _build
+
+c_p = ctypes.c_void_p
+c_i = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_f = ctypes.c_float
+
+
+class TreeDesc(ctypes.Structure):
+    _fields_ = [("leaf", c_p), ("nodes", c_p), ("off", c_i64 * 8), ("n", c_i64 * 8), ("L", c_i),
+                ("min_bits", c_p)]
+
+
+class RecordDesc(ctypes.Structure):
+    _fields_ = [("obs", c_p), ("nxt", c_p), ("act", c_p), ("rew", c_p), ("gam", c_p), ("gen", c_p),
+                ("C", c_i), ("cap", c_i64)]
+
+
+class HeadParams(ctypes.Structure):
+    _fields_ = [("wv", c_p), ("bv", c_p), ("wa", c_p), ("ba", c_p)]
+
+
+class ConvDesc(ctypes.Structure):
+    """Implicit-GEMM conv problem (see csrc/conv_mfma.hip)."""
+    _fields_ = [("x", c_p), ("frame_slots", c_p), ("w", c_p), ("bias", c_p), ("y", c_p), ("mask", c_p),
+                ("N", c_i), ("H", c_i), ("W", c_i), ("Cin", c_i), ("OH", c_i), ("OW", c_i),
+                ("Cout", c_i), ("KH", c_i), ("KW", c_i), ("stride", c_i), ("mode", c_i),
+                ("relu", c_i), ("in_scale", c_f), ("ostride_h", c_i), ("ostride_w", c_i),
+                ("ooff_h", c_i), ("ooff_w", c_i), ("OHfull", c_i), ("OWfull", c_i),
+                ("pad_h", c_i), ("pad_w", c_i), ("tap_step", c_i)]
+
+
+_SIGS = {
+    "apex_abi_version": ([], c_i),
+    "apex_tree_update": ([TreeDesc, c_p, c_p, c_i, c_i, c_f, c_f, c_p, c_p, c_i, c_p, c_p], c_i),
+    "apex_tree_zero_range": ([TreeDesc, c_i64, c_i64, c_p], c_i),
+    "apex_replay_insert": ([TreeDesc, RecordDesc, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p],
+                           c_i),
+    "apex_tree_sample": ([TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                          c_p, c_p, c_p], c_i),
+    "apex_tree_rebuild": ([TreeDesc, c_p], c_i),
+    "apex_gather_frames": ([c_p, c_p, c_i, c_i, c_i64, c_p, c_p], c_i),
+    "apex_grad_sqnorm_partials": ([c_p, c_i64, c_p, c_p], c_i),
+    "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p], c_i),
+    "apex_cast_bf16": ([c_p, c_p, c_i64, c_p], c_i),
+    "apex_ddqn_head": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
+                        c_p, c_p, c_p, c_p, c_p, c_i, c_p], c_i),
+    "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_p], c_i),
+    "apex_actor_head": ([c_p, HeadParams, c_i, c_i, c_p, c_u64, c_p, c_p, c_p, c_p], c_i),
+}
+
+_LIB: Optional[ctypes.CDLL] = None
+_LOAD_ERROR: Optional[str] = None
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = args
+        fn.restype = res
+    # optional families declared by their own modules (conv / gemm)
+    from . import conv_sigs
+    conv_sigs.declare(lib)
+
+
+def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:
+    global _LIB, _LOAD_ERROR
+    if _LIB is not None:
+        return _LIB
+    path = _build.KERNEL_LIB
+    try:
+        if build_if_missing and not os.path.exists(path):
+            _build.build_kernels()
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        _declare(lib)
+        _LIB = lib
+    except Exception as e:  # pragma: no cover - depends on toolchain
+        _LOAD_ERROR = repr(e)
+        _LIB = None
+    return _LIB
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def require_kernels() -> ctypes.CDLL:
+    lib = load()
+    if lib is None:
+        raise RuntimeError(f"apex HIP kernel library unavailable: {_LOAD_ERROR}. "
+                           f"Run `python -m apex_dqn_amd.ops.build`.")
+    return lib
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")

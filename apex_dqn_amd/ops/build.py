@@ -1,0 +1,86 @@
+"""In-tree build of the native libraries (no JIT cache, no hipify).
+
+* ``libapex_kernels.so`` -- every ``csrc/*.hip`` compiled by ``hipcc
+  --offload-arch=gfx950`` into one shared library with a C ABI (ctypes).
+* ``libapex_runtime.so`` -- host C++ runtime (``csrc/runtime/*.cpp``: sum-tree,
+  n-step builder, frame ring bookkeeping) built with g++.
+
+Objects are rebuilt only when their source (or a header) is newer.  The
+libraries land in ``apex_dqn_amd/ops/_build/`` which ships to the GPU box
+with the repo snapshot (git-ignored, not gpurun-ignored).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from typing import List
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+CSRC = os.path.join(PKG, "csrc")
+OUT = os.path.join(HERE, "_build")
+KERNEL_LIB = os.path.join(OUT, "libapex_kernels.so")
+RUNTIME_LIB = os.path.join(OUT, "libapex_runtime.so")
+ARCH = os.environ.get("APEX_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-I", CSRC]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I", CSRC]
+
+
+def _newer(src_files: List[str], target: str) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in src_files)
+
+
+def _run(cmd: List[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
+
+
+def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.cuh"))
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(OUT, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer([s] + headers, o):
+            todo.append([HIPCC] + HIP_FLAGS + ["-c", s, "-o", o])
+    if todo:
+        with ThreadPoolExecutor(max_workers=jobs) as ex:
+            list(ex.map(_run, todo))
+    if force or todo or _newer(objs, KERNEL_LIB):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", KERNEL_LIB] + objs)
+    if verbose:
+        print(f"built {KERNEL_LIB} ({len(todo)} objects recompiled)")
+    return KERNEL_LIB
+
+
+def build_runtime(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    hdrs = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
+    if srcs and (force or _newer(srcs + hdrs, RUNTIME_LIB)):
+        _run(["g++"] + CXX_FLAGS + ["-shared", "-o", RUNTIME_LIB] + srcs + ["-lpthread"])
+        if verbose:
+            print(f"built {RUNTIME_LIB}")
+    return RUNTIME_LIB
+
+
+def build_all(force: bool = False, verbose: bool = True) -> None:
+    build_runtime(force=force, verbose=verbose)
+    build_kernels(force=force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)

@@ -1,0 +1,189 @@
+"""Backends for the fused NatureCNN learner step.
+
+``TorchBackend`` -- every op in PyTorch (CPU path, and the oracle);
+``HipBackend``   -- the MI355X path: hand-written gfx950 kernels from
+                    ``libapex_kernels.so`` for every op that has one.
+
+Both write into preallocated output buffers so a whole learner step can be
+captured in one HIP graph.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from . import _lib
+from . import reference as R
+
+
+class TorchBackend:
+    name = "torch"
+
+    def __init__(self, dtype=torch.float32):
+        self.dtype = dtype
+
+    # ------------------------------------------------------------- forward
+    def conv1_fwd(self, frames, w, b, scale, out):
+        out.copy_(R.conv1_fwd(frames, w, b, scale, self.dtype))
+
+    def conv_fwd(self, x, w, b, stride, out):
+        out.copy_(R.conv_fwd(x, w, b, stride, self.dtype))
+
+    def fc_fwd(self, x, w, b, out):
+        out.copy_(R.fc_fwd(x.reshape(x.shape[0], -1), w, b, self.dtype))
+
+    # ---------------------------------------------------------------- head
+    def head(self, Hon, Htg, Pon: Dict[str, torch.Tensor], Ptg: Dict[str, torch.Tensor], act, rew, gam, isw,
+             huber: bool, kappa: float, grad_scale: float, td_abs, loss, dH, dhead, q_out=None,
+             zero: Optional[torch.Tensor] = None):
+        B = act.shape[0]
+        A = Pon["wa"].shape[0]
+        Hon = Hon.float()
+        Htg = Htg.float()
+
+        def q_of(h, P):
+            v = h[:, :512] @ P["wv"].float() + P["bv"].float()
+            a = h[:, 512:] @ P["wa"].float().t() + P["ba"].float()
+            return v[:, None] + a - a.mean(1, keepdim=True)
+
+        q_t = q_of(Hon[:B], Pon)
+        q_n = q_of(Hon[B:2 * B], Pon)
+        q_g = q_of(Htg[:B], Ptg)
+        a_star = q_n.argmax(1)
+        G = rew.float() + gam.float() * q_g.gather(1, a_star[:, None]).squeeze(1)
+        q_sa = q_t.gather(1, act.long()[:, None]).squeeze(1)
+        delta = G - q_sa
+        ad = delta.abs()
+        if huber:
+            lval = torch.where(ad <= kappa, 0.5 * delta * delta, kappa * (ad - 0.5 * kappa))
+            dl = torch.where(ad <= kappa, delta, kappa * delta.sign())
+        else:
+            lval = 0.5 * delta * delta
+            dl = delta
+        w = isw.float() if isw is not None else torch.ones_like(delta)
+        dq = -w * dl * grad_scale
+        td_abs.copy_(ad)
+        loss.copy_(w * lval)
+        onehot = torch.nn.functional.one_hot(act.long(), A).float()
+        dadv = dq[:, None] * (onehot - 1.0 / A)
+        dhead[:, 0] = dq
+        dhead[:, 1:] = dadv
+        dv = dq[:, None] * Pon["wv"].float()[None, :]
+        da = dadv @ Pon["wa"].float()
+        dh = torch.cat([dv, da], 1) * (Hon[:B] > 0).float()
+        dH.copy_(dh)
+        if q_out is not None:
+            q_out.copy_(q_t)
+        if zero is not None:
+            zero.zero_()
+
+    def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor]):
+        B = dhead.shape[0]
+        h = Hon[:B].float()
+        g["wv"].add_(dhead[:, 0] @ h[:, :512])
+        g["bv"].add_(dhead[:, 0].sum().view(1))
+        g["wa"].add_(dhead[:, 1:].t() @ h[:, 512:])
+        g["ba"].add_(dhead[:, 1:].sum(0))
+
+    def actor_head(self, H, P, eps, gen: torch.Generator, q_out, a_out):
+        h = H.float()
+        v = h[:, :512] @ P["wv"].float() + P["bv"].float()
+        a = h[:, 512:] @ P["wa"].float().t() + P["ba"].float()
+        q = v[:, None] + a - a.mean(1, keepdim=True)
+        q_out.copy_(q)
+        E, A = q.shape
+        u = torch.rand(E, generator=gen, device="cpu").to(q.device)
+        r = torch.randint(0, A, (E,), generator=gen, device="cpu").to(q.device)
+        a_out.copy_(torch.where(u < eps, r, q.argmax(1)).to(a_out.dtype))
+
+    # ------------------------------------------------------------ backward
+    def fc_bwd(self, dh, x, w, dx_out, dw_out, db_out):
+        xf = x.reshape(x.shape[0], -1)
+        dx, dw, db = R.fc_bwd(dh, xf, w, xf, self.dtype)
+        dx_out.copy_(dx.reshape(dx_out.shape))
+        dw_out.copy_(dw)
+        db_out.copy_(db)
+
+    def conv_dgrad(self, dy, w, stride, x_src, dx_out):
+        dx_out.copy_(R.conv_dgrad(dy, w, tuple(x_src.shape), stride, x_src, self.dtype))
+
+    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out):
+        dw, db = R.conv_wgrad(dy, x, k, stride)
+        dw_out.copy_(dw)
+        db_out.copy_(db)
+
+    def conv1_wgrad(self, dy, frames, scale, dw_out, db_out):
+        dw, db = R.conv1_wgrad(dy, frames, scale)
+        dw_out.copy_(dw)
+        db_out.copy_(db)
+
+    # ----------------------------------------------------------- optimizer
+    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out):
+        norm = g32.double().pow(2).sum().sqrt().float()
+        coef = torch.clamp(clip / (norm + 1e-6), max=1.0) if clip > 0 else torch.ones_like(norm)
+        g = g32 * coef
+        v.mul_(alpha).add_((1 - alpha) * g * g)
+        if centered:
+            m.mul_(alpha).add_((1 - alpha) * g)
+            var = v - m * m
+        else:
+            var = v
+        p32.sub_(lr * g / (var.clamp_min(0).sqrt() + eps))
+        pbf.copy_(p32)
+        norm_out.copy_(norm.view(1))
+
+    def gather_frames(self, replay, slots, out):
+        replay.gather_frames(slots, out)
+
+
+class HipBackend(TorchBackend):
+    """MI355X backend.  Ops without a hand-written kernel yet run on torch
+    (MIOpen / hipBLASLt) in bf16; each kernel family switches on here as it
+    lands (``kernels`` lists what is native)."""
+
+    name = "hip"
+
+    def __init__(self, dtype=torch.bfloat16, native_conv: bool = True):
+        super().__init__(dtype)
+        self.lib = _lib.require_kernels()
+        self.native_conv = native_conv and hasattr(self.lib, "apex_conv_fwd")
+        self.kernels = ["replay", "head", "head_wgrad", "optimizer", "actor_head"]
+
+    @staticmethod
+    def _hp(P):
+        h = _lib.HeadParams()
+        h.wv, h.bv, h.wa, h.ba = (P["wv"].data_ptr(), P["bv"].data_ptr(), P["wa"].data_ptr(),
+                                  P["ba"].data_ptr())
+        return h
+
+    def head(self, Hon, Htg, Pon, Ptg, act, rew, gam, isw, huber, kappa, grad_scale, td_abs, loss, dH,
+             dhead, q_out=None, zero=None):
+        B = act.shape[0]
+        A = Pon["wa"].shape[0]
+        _lib.check(self.lib.apex_ddqn_head(
+            Hon.data_ptr(), Htg.data_ptr(), self._hp(Pon), self._hp(Ptg), act.data_ptr(), rew.data_ptr(),
+            gam.data_ptr(), _lib.ptr(isw), B, A, int(huber), float(kappa), float(grad_scale),
+            td_abs.data_ptr(), loss.data_ptr(), _lib.ptr(q_out), dH.data_ptr(), dhead.data_ptr(),
+            _lib.ptr(zero), 0 if zero is None else zero.numel(), _lib.stream_ptr()), "ddqn_head")
+
+    def head_wgrad(self, Hon, dhead, g):
+        B, A1 = dhead.shape
+        _lib.check(self.lib.apex_head_wgrad(Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(),
+                                            g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(),
+                                            _lib.stream_ptr()), "head_wgrad")
+
+    def actor_head(self, H, P, eps, ctr, seed, q_out, a_out):
+        E, A = q_out.shape
+        _lib.check(self.lib.apex_actor_head(H.data_ptr(), self._hp(P), E, A, eps.data_ptr(), int(seed),
+                                            ctr.data_ptr(), q_out.data_ptr(), a_out.data_ptr(),
+                                            _lib.stream_ptr()), "actor_head")
+
+    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out):
+        n = p32.numel()
+        st = _lib.stream_ptr()
+        _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), n, partials.data_ptr(), st), "sqnorm")
+        _lib.check(self.lib.apex_rmsprop_step(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
+                                              pbf.data_ptr(), n, partials.data_ptr(), float(lr), float(alpha),
+                                              float(eps), float(clip), int(centered), norm_out.data_ptr(), st),
+                   "rmsprop")

@@ -1,0 +1,332 @@
+"""HBM-resident prioritized replay shard (one per GPU rank).
+
+Storage per shard (sized for 288 GB HBM3E):
+* frame ring  uint8 [F, 84, 84]      -- each env frame stored once;
+* records     int32 [cap, C] x2      -- frame-ring slots of S_t / S_{t+n} stacks,
+              int32 act, fp32 R, fp32 Gamma, int32 generation;
+* sum-tree    64-ary (leaf fp32 = p^alpha, internal fp64) -- ``csrc/sumtree.hip``.
+
+Reference parity (``replay.py``): ``add`` -> :meth:`insert`, ``sample`` ->
+:meth:`sample`, ``set_priorities`` -> :meth:`update_priorities`,
+``remove_to_fit`` -> :meth:`remove_to_fit`, ``size`` -> :meth:`size`.
+
+All mutating kernels run on the caller's current stream (single writer per
+shard; SURVEY §5.2 race A24 is designed out).  Slot generations make a
+priority write-back for a slot that was overwritten after it was sampled a
+no-op; writes to evicted slots never resurrect them.
+
+On CPU (tests) the same class runs a torch implementation with identical
+semantics (exact recompute instead of fp64 deltas).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..ops import _lib
+
+
+def _tree_levels(cap: int):
+    sizes = [cap]
+    while sizes[-1] > 1:
+        sizes.append((sizes[-1] + 63) // 64)
+    return sizes  # sizes[0] = leaves, sizes[-1] = 1 (root)
+
+
+class GpuReplayShard:
+    def __init__(self, capacity: int, soft_capacity: int, frame_capacity: int, stack: int,
+                 frame_shape=(84, 84), alpha: float = 0.6, beta: float = 0.4, eps: float = 1e-6,
+                 device: torch.device = torch.device("cuda"), seed: int = 0, use_hip: Optional[bool] = None):
+        self.device = torch.device(device)
+        self.cap = int(capacity)
+        self.soft_capacity = int(min(soft_capacity, capacity))
+        self.F = int(frame_capacity)
+        self.C = int(stack)
+        self.frame_shape = tuple(frame_shape)
+        self.frame_bytes = int(np.prod(frame_shape))
+        self.alpha, self.beta, self.eps = float(alpha), float(beta), float(eps)
+        self.seed = int(seed)
+        on_gpu = self.device.type == "cuda"
+        self.use_hip = on_gpu if use_hip is None else bool(use_hip)
+        if self.use_hip:
+            self.lib = _lib.require_kernels()
+        d = self.device
+        self.sizes = _tree_levels(self.cap)
+        self.L = len(self.sizes) - 1
+        if self.L > 7:
+            raise ValueError("capacity too large for an 8-level 64-ary tree")
+        self.leaf = torch.zeros(self.cap, dtype=torch.float32, device=d)
+        n_int = sum(self.sizes[1:])
+        self.nodes = torch.zeros(max(n_int, 1), dtype=torch.float64, device=d)
+        self.offs = [0] * 8
+        o = 0
+        for k in range(1, self.L + 1):
+            self.offs[k] = o
+            o += self.sizes[k]
+        self.min_bits = torch.full((1,), 0x7f800000, dtype=torch.int32, device=d)
+        self.frames = torch.zeros((self.F,) + self.frame_shape, dtype=torch.uint8, device=d)
+        self.obs = torch.zeros(self.cap, self.C, dtype=torch.int32, device=d)
+        self.nxt = torch.zeros(self.cap, self.C, dtype=torch.int32, device=d)
+        self.act = torch.zeros(self.cap, dtype=torch.int32, device=d)
+        self.rew = torch.zeros(self.cap, dtype=torch.float32, device=d)
+        self.gam = torch.zeros(self.cap, dtype=torch.float32, device=d)
+        self.gen = torch.zeros(self.cap, dtype=torch.int32, device=d)
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=d)  # sampling RNG counter (device-side)
+        # host bookkeeping
+        self.head = 0          # next record slot
+        self.live = 0
+        self.frame_head = 0    # next frame sequence number
+        self.total_inserted = 0
+        self.min_frame_seq = np.full(self.cap, -1, np.int64)  # oldest frame referenced per slot
+        self._tdesc = None
+        self._rdesc = None
+
+    # ----------------------------------------------------------- descriptors
+    def tree_desc(self) -> "_lib.TreeDesc":
+        if self._tdesc is None:
+            t = _lib.TreeDesc()
+            t.leaf = self.leaf.data_ptr()
+            t.nodes = self.nodes.data_ptr()
+            for k in range(8):
+                t.off[k] = self.offs[k]
+                t.n[k] = self.sizes[k] if k < len(self.sizes) else 0
+            t.L = self.L
+            t.min_bits = self.min_bits.data_ptr()
+            self._tdesc = t
+        return self._tdesc
+
+    def record_desc(self) -> "_lib.RecordDesc":
+        if self._rdesc is None:
+            r = _lib.RecordDesc()
+            r.obs, r.nxt = self.obs.data_ptr(), self.nxt.data_ptr()
+            r.act, r.rew, r.gam, r.gen = (self.act.data_ptr(), self.rew.data_ptr(), self.gam.data_ptr(),
+                                          self.gen.data_ptr())
+            r.C, r.cap = self.C, self.cap
+            self._rdesc = r
+        return self._rdesc
+
+    def _stream(self):
+        return _lib.stream_ptr(self.device)
+
+    # --------------------------------------------------------------- insert
+    def append_frames(self, frames) -> np.ndarray:
+        """Store new frames (n, H, W) uint8; returns their sequence numbers."""
+        frames = torch.as_tensor(frames)
+        n = frames.shape[0]
+        seqs = self.frame_head + np.arange(n, dtype=np.int64)
+        start = self.frame_head % self.F
+        first = min(n, self.F - start)
+        src = frames.to(self.device, non_blocking=True)
+        self.frames[start:start + first].copy_(src[:first], non_blocking=True)
+        if first < n:
+            self.frames[:n - first].copy_(src[first:], non_blocking=True)
+        self.frame_head += n
+        return seqs
+
+    def insert(self, batch: Dict[str, np.ndarray]) -> np.ndarray:
+        """Insert n-step transitions whose S_t/S_tpn payloads are frame seqs (K, C)."""
+        K = len(batch["A_t"])
+        if K == 0:
+            return np.zeros(0, np.int64)
+        if K > self.cap:
+            raise ValueError("insert batch larger than replay capacity")
+        obs_seq = np.asarray(batch["S_t"], np.int64).reshape(K, self.C)
+        nxt_seq = np.asarray(batch["S_tpn"], np.int64).reshape(K, self.C)
+        slots = (self.head + np.arange(K)) % self.cap
+        self.min_frame_seq[slots] = np.minimum(obs_seq.min(1), nxt_seq.min(1))
+        d = self.device
+        s_obs = torch.from_numpy((obs_seq % self.F).astype(np.int32)).to(d, non_blocking=True)
+        s_nxt = torch.from_numpy((nxt_seq % self.F).astype(np.int32)).to(d, non_blocking=True)
+        s_act = torch.from_numpy(np.asarray(batch["A_t"], np.int32)).to(d, non_blocking=True)
+        s_rew = torch.from_numpy(np.asarray(batch["R"], np.float32)).to(d, non_blocking=True)
+        s_gam = torch.from_numpy(np.asarray(batch["Gamma"], np.float32)).to(d, non_blocking=True)
+        pr = batch.get("priority")
+        if pr is None:
+            pr = np.ones(K, np.float32)
+        s_pr = torch.from_numpy(np.asarray(pr, np.float32)).to(d, non_blocking=True)
+        if self.use_hip:
+            _lib.check(self.lib.apex_replay_insert(self.tree_desc(), self.record_desc(), self.head, K,
+                                                   s_obs.data_ptr(), s_nxt.data_ptr(), s_act.data_ptr(),
+                                                   s_rew.data_ptr(), s_gam.data_ptr(), s_pr.data_ptr(),
+                                                   self.alpha, self.eps, self._stream()), "replay_insert")
+        else:
+            ts = torch.from_numpy(slots).to(d)
+            self.obs[ts] = s_obs
+            self.nxt[ts] = s_nxt
+            self.act[ts] = s_act
+            self.rew[ts] = s_rew
+            self.gam[ts] = s_gam
+            self.gen[ts] += 1
+            self._torch_set_leaves(ts, (s_pr.abs().double() + self.eps) ** self.alpha)
+        self.head = int((self.head + K) % self.cap)
+        self.live = min(self.live + K, self.cap)
+        self.total_inserted += K
+        return slots
+
+    def size(self) -> int:
+        return int(self.live)
+
+    # ------------------------------------------------------------- sampling
+    def sample(self, B: int, out: Optional[Dict[str, torch.Tensor]] = None,
+               ratio_min_global: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        """Stratified proportional sample of B slots; IS weights max-normalised.
+
+        ``out`` (preallocated tensors) makes the call graph-capturable.
+        """
+        d = self.device
+        if out is None:
+            out = self.alloc_sample_buffers(B)
+        if self.use_hip:
+            _lib.check(self.lib.apex_tree_sample(
+                self.tree_desc(), self.record_desc(), B, self.seed, self.ctr.data_ptr(), self.beta,
+                _lib.ptr(ratio_min_global), out["idx"].data_ptr(), out["weights"].data_ptr(),
+                out["gen"].data_ptr(), out["obs"].data_ptr(), out["nxt"].data_ptr(), out["act"].data_ptr(),
+                out["rew"].data_ptr(), out["gam"].data_ptr(), self._stream()), "tree_sample")
+        else:
+            g = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + int(self.ctr.item()))
+            leaf = self.leaf.double().cpu()
+            total = leaf.sum()
+            u = (torch.arange(B, dtype=torch.float64) + torch.rand(B, generator=g, dtype=torch.float64)) * (
+                total / B)
+            c = torch.cumsum(leaf, 0)
+            idx = torch.searchsorted(c, u, right=True).clamp_(max=self.cap - 1)
+            # never return an empty leaf (round-off at the top of the range)
+            empty = leaf[idx] <= 0
+            if empty.any():
+                nz = torch.nonzero(leaf > 0).flatten()
+                idx[empty] = nz[-1]
+            p = leaf[idx]
+            pmin = leaf[leaf > 0].min()
+            ratio = float(ratio_min_global.item()) if ratio_min_global is not None else float(pmin / total)
+            w = ((p / total) / ratio) ** (-self.beta)
+            idx = idx.to(d)
+            out["idx"].copy_(idx)
+            out["weights"].copy_(w.clamp(max=1.0).float())
+            out["gen"].copy_(self.gen[idx])
+            out["obs"].copy_(self.obs[idx])
+            out["nxt"].copy_(self.nxt[idx])
+            out["act"].copy_(self.act[idx])
+            out["rew"].copy_(self.rew[idx])
+            out["gam"].copy_(self.gam[idx])
+        return out
+
+    def alloc_sample_buffers(self, B: int) -> Dict[str, torch.Tensor]:
+        d = self.device
+        return dict(idx=torch.zeros(B, dtype=torch.int64, device=d),
+                    weights=torch.zeros(B, dtype=torch.float32, device=d),
+                    gen=torch.zeros(B, dtype=torch.int32, device=d),
+                    obs=torch.zeros(B, self.C, dtype=torch.int32, device=d),
+                    nxt=torch.zeros(B, self.C, dtype=torch.int32, device=d),
+                    act=torch.zeros(B, dtype=torch.int32, device=d),
+                    rew=torch.zeros(B, dtype=torch.float32, device=d),
+                    gam=torch.zeros(B, dtype=torch.float32, device=d))
+
+    def gather_frames(self, slots: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """slots (B, C) int32 -> stacked frames (B, C, H, W) uint8."""
+        B = slots.shape[0]
+        if out is None:
+            out = torch.empty((B, self.C) + self.frame_shape, dtype=torch.uint8, device=self.device)
+        if self.use_hip:
+            _lib.check(self.lib.apex_gather_frames(self.frames.data_ptr(), slots.data_ptr(), B * self.C, self.C,
+                                                   self.frame_bytes, out.data_ptr(), self._stream()),
+                       "gather_frames")
+        else:
+            out.copy_(self.frames[slots.long()])
+        return out
+
+    # ------------------------------------------------------------ priorities
+    def update_priorities(self, idx: torch.Tensor, td_abs: torch.Tensor, gen: Optional[torch.Tensor] = None,
+                          bump_ctr: bool = True) -> None:
+        n = idx.numel()
+        if self.use_hip:
+            _lib.check(self.lib.apex_tree_update(self.tree_desc(), idx.data_ptr(), td_abs.data_ptr(), n, 1,
+                                                 self.alpha, self.eps, _lib.ptr(gen), self.gen.data_ptr(), 1,
+                                                 self.ctr.data_ptr() if bump_ctr else None, self._stream()),
+                       "tree_update")
+        else:
+            idx_c = idx.long()
+            keep = torch.ones(n, dtype=torch.bool, device=idx.device)
+            # last occurrence wins
+            for i in range(n):
+                if (idx_c[i + 1:] == idx_c[i]).any():
+                    keep[i] = False
+            keep &= self.leaf[idx_c] > 0
+            if gen is not None:
+                keep &= self.gen[idx_c] == gen
+            sel = idx_c[keep]
+            vals = (td_abs[keep].abs().double() + self.eps) ** self.alpha
+            self._torch_set_leaves(sel, vals)
+            if bump_ctr:
+                self.ctr += 1
+
+    def remove_to_fit(self) -> int:
+        """FIFO eviction to soft_capacity + drop slots whose frames were overwritten."""
+        excess = self.live - self.soft_capacity
+        n_ev = 0
+        if excess > 0:
+            oldest = (self.head - self.live) % self.cap
+            self._zero_range(oldest, excess)
+            self.live -= excess
+            n_ev += excess
+        # frame-ring guard: a live slot must not reference overwritten frames
+        frame_tail = self.frame_head - self.F
+        if frame_tail > 0 and self.live > 0:
+            oldest = (self.head - self.live) % self.cap
+            k = 0
+            while k < self.live and self.min_frame_seq[(oldest + k) % self.cap] < frame_tail:
+                k += 1
+            if k:
+                self._zero_range(oldest, k)
+                self.live -= k
+                n_ev += k
+        return n_ev
+
+    def rebuild(self) -> None:
+        """Exact recompute of all internal nodes and the min (drift guard)."""
+        if self.use_hip:
+            _lib.check(self.lib.apex_tree_rebuild(self.tree_desc(), self._stream()), "tree_rebuild")
+        else:
+            self._torch_rebuild()
+
+    # ------------------------------------------------------------ internals
+    def _zero_range(self, start: int, count: int) -> None:
+        if self.use_hip:
+            _lib.check(self.lib.apex_tree_zero_range(self.tree_desc(), int(start), int(count), self._stream()),
+                       "tree_zero_range")
+        else:
+            sl = torch.from_numpy((start + np.arange(count)) % self.cap).to(self.device)
+            self._torch_set_leaves(sl, torch.zeros(count, dtype=torch.float64, device=self.device))
+
+    def _torch_set_leaves(self, idx: torch.Tensor, vals: torch.Tensor) -> None:
+        self.leaf[idx] = vals.float()
+        self._torch_rebuild()
+
+    def _torch_rebuild(self) -> None:
+        prev = self.leaf.double()
+        for k in range(1, self.L + 1):
+            n = self.sizes[k]
+            pad = torch.zeros(n * 64, dtype=torch.float64, device=self.device)
+            pad[:prev.numel()] = prev
+            lvl = pad.view(n, 64).sum(1)
+            self.nodes[self.offs[k]:self.offs[k] + n] = lvl
+            prev = lvl
+        pos = self.leaf[self.leaf > 0]
+        mn = float(pos.min()) if pos.numel() else math.inf
+        self.min_bits.copy_(torch.tensor([mn], dtype=torch.float32).view(torch.int32))
+
+    # ---------------------------------------------------------------- stats
+    def total(self) -> float:
+        return float(self.nodes[self.offs[self.L]].item())
+
+    def min_leaf(self) -> float:
+        return float(self.min_bits.view(torch.float32).item())
+
+    def stats_tensor(self) -> torch.Tensor:
+        """(total, min_leaf, live) as fp32 for the cross-shard all-gather."""
+        t = self.nodes[self.offs[self.L]:self.offs[self.L] + 1].float()
+        m = self.min_bits.view(torch.float32)
+        n = torch.tensor([float(self.live)], device=self.device)
+        return torch.cat([t, m, n])

@@ -1,0 +1,132 @@
+#!/usr/bin/env python
+"""Headline benchmark: learner grad-steps/sec at batch 512 on 84x84x4 frames,
+dueling NatureCNN (BASELINE.json metric), on N MI355X of one node.
+
+One process per GPU (torchrun env vars).  Each rank owns an HBM replay shard
+prefilled with synthetic uint8 frames (no datasets on the box) and a
+data-parallel learner replica that takes a full batch of 512 from its shard
+(weak scaling: per-GPU work fixed).  A timed step is the complete learner
+update: prioritized sample + frame gather, online fwd on [S_t;S_t+n] and target
+fwd on S_t+n, DDQN/Huber/IS loss + priorities, full backward, RCCL gradient
+all-reduce (N>1), clip + centered RMSprop, priority write-back, plus the
+periodic target sync / FIFO eviction at their configured cadences.
+
+``value`` = whole-job batch-512 gradient steps per second
+          = N x (data-parallel steps/s)  (each DP step consumes N x 512 samples).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_STEPS_PER_S = 2.32  # BASELINE.md north-star row (reference learner compute, B=512, 4x84x84)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--actions", type=int, default=4)
+    ap.add_argument("--replay", type=int, default=100000, help="transitions per shard")
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--profile-phases", action="store_true")
+    args = ap.parse_args()
+
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.parallel.dist import Comm
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    comm = Comm.from_env(backend="nccl", device=device)
+
+    cfg = ApexConfig.from_dict({
+        "env_conf": {"state_shape": [4, 84, 84], "action_dim": args.actions, "name": "SyntheticPong"},
+        "Learner": {"replay_sample_size": args.batch, "q_target_sync_freq": 2500, "remove_old_xp_freq": 100,
+                    "min_replay_mem_size": 0},
+        "Replay_Memory": {"soft_capacity": args.replay},
+        "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
+                    "seed": 1234 + rank},
+    })
+    cap = args.replay
+    frames_cap = cap + 4096
+    replay = GpuReplayShard(cap, cap, frames_cap, 4, alpha=0.6, beta=0.4, device=device, seed=rank + 1)
+    # synthetic prefill: random frames straight into HBM + random n-step records
+    g = torch.Generator(device=device).manual_seed(1000 + rank)
+    replay.frames.copy_(torch.randint(0, 256, replay.frames.shape, generator=g, device=device,
+                                      dtype=torch.uint8))
+    replay.frame_head = frames_cap
+    rng = np.random.default_rng(rank)
+    chunk = 16384
+    for s in range(0, cap, chunk):
+        K = min(chunk, cap - s)
+        base = rng.integers(0, frames_cap - 8, size=K)
+        st = base[:, None] + np.arange(4)[None]
+        nx = st + 3
+        replay.insert(dict(S_t=st, S_tpn=nx, A_t=rng.integers(0, args.actions, K),
+                           R=rng.normal(size=K).astype(np.float32), Gamma=np.full(K, 0.99 ** 3, np.float32),
+                           priority=rng.random(K).astype(np.float32) + 0.01))
+    replay.rebuild()
+    learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
+    L = cfg.Learner
+
+    def one_step():
+        learner.step()
+        if learner.num_q_updates % L.remove_old_xp_freq == 0:
+            replay.remove_to_fit()
+            replay.rebuild()
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = comm.allreduce_scalar(dt, "max") if comm.active else dt
+    ms = 1e3 * dt / args.steps
+    dp_steps_per_s = args.steps / dt
+    value = dp_steps_per_s * world
+    m = learner.last_metrics()
+    if rank == 0:
+        out = {
+            "metric": "learner grad-steps/sec at batch 512, 84x84x4 dueling DQN",
+            "value": round(value, 2), "unit": "grad-steps/s (batch 512)", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_STEPS_PER_S, 2), "dtype": "bf16", "data": "synthetic",
+            "config": {"model": "dueling NatureCNN (reference DuellingDQN, conv1=64), 4x84x84, A=%d" % args.actions,
+                       "global_batch": args.batch * world, "seq_len": 1,
+                       "parallelism": "dp%d" % world, "per_gpu_batch": args.batch,
+                       "replay_per_gpu": cap, "backend": learner.ops.name,
+                       "hip_graphs": bool(learner.rt.use_graphs)},
+            "loss": round(m["loss"], 5), "grad_norm": round(m["grad_norm"], 5),
+        }
+        print(json.dumps(out), flush=True)
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    main()

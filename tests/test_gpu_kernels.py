@@ -1,0 +1,243 @@
+"""GPU numerics tests: each HIP kernel against a plain PyTorch fp32 reference
+of the same op (run on a real MI355X via gpurun: ``pytest -m gpu``)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _lib():
+    from apex_dqn_amd.ops import _lib as L
+    return L.require_kernels()
+
+
+def _fill_replay(rp, K, A=6, seed=0):
+    rng = np.random.default_rng(seed)
+    seqs = rp.append_frames(rng.integers(0, 255, (K + 8, 84, 84), dtype=np.uint8))
+    st = np.stack([seqs[i:i + 4] for i in range(K)])
+    nx = st + 3
+    pr = rng.random(K).astype(np.float32) * 3 + 0.01
+    batch = dict(S_t=st, S_tpn=nx, A_t=rng.integers(0, A, K), R=rng.normal(size=K).astype(np.float32),
+                 Gamma=np.full(K, 0.97, np.float32), priority=pr)
+    rp.insert(batch)
+    return batch
+
+
+def test_library_loads_on_gpu():
+    lib = _lib()
+    assert lib.apex_abi_version() >= 1
+
+
+def test_sumtree_insert_totals_and_rebuild():
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(5000, 5000, 6000, 4, device=DEV, alpha=0.6)
+    b = _fill_replay(rp, 4000)
+    torch.cuda.synchronize()
+    leaf = rp.leaf.double().cpu().numpy()
+    ref = (np.abs(b["priority"].astype(np.float64)) + 1e-6) ** 0.6
+    np.testing.assert_allclose(leaf[:4000], ref, rtol=2e-6)
+    assert abs(rp.total() - leaf.sum()) / leaf.sum() < 1e-9
+    assert abs(rp.min_leaf() - leaf[leaf > 0].min()) < 1e-7
+    tot = rp.total()
+    rp.rebuild()
+    assert abs(rp.total() - tot) / tot < 1e-9
+
+
+def test_sumtree_sample_stratified_and_weights():
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(100000, 100000, 100010, 4, device=DEV, alpha=0.6, beta=0.4)
+    _fill_replay(rp, 70000, seed=3)
+    B = 512
+    out = rp.sample(B)
+    torch.cuda.synchronize()
+    leaf = rp.leaf.double().cpu().numpy()
+    c = np.cumsum(leaf)
+    total = c[-1]
+    idx = out["idx"].cpu().numpy()
+    lo = c[idx] - leaf[idx]
+    hi = c[idx]
+    seg = total / B
+    b = np.arange(B)
+    # the sampled leaf's interval must intersect the b-th stratum
+    assert np.all(lo <= (b + 1) * seg * (1 + 1e-9)) and np.all(hi >= b * seg * (1 - 1e-9))
+    assert np.all(leaf[idx] > 0)
+    w = out["weights"].cpu().numpy()
+    pmin = leaf[leaf > 0].min()
+    np.testing.assert_allclose(w, (leaf[idx] / pmin) ** -0.4, rtol=1e-4)
+    # gathered records
+    np.testing.assert_array_equal(out["act"].cpu().numpy(), rp.act.cpu().numpy()[idx])
+    np.testing.assert_array_equal(out["obs"].cpu().numpy(), rp.obs.cpu().numpy()[idx])
+
+
+def test_sumtree_sampling_frequencies_proportional():
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(64 * 64, 64 * 64, 64 * 64 + 16, 4, device=DEV, alpha=1.0)
+    K = 300
+    b = _fill_replay(rp, K, seed=5)
+    counts = np.zeros(rp.cap)
+    for _ in range(200):
+        o = rp.sample(512)
+        rp.ctr += 1
+        counts += np.bincount(o["idx"].cpu().numpy(), minlength=rp.cap)
+    p = (b["priority"].astype(np.float64) + 1e-6)
+    p /= p.sum()
+    emp = counts[:K] / counts.sum()
+    assert np.abs(emp - p).max() < 3e-3
+
+
+def test_sumtree_update_duplicates_last_wins_and_generation():
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(1000, 1000, 1200, 4, device=DEV, alpha=1.0, eps=0.0)
+    _fill_replay(rp, 900)
+    idx = torch.tensor([5, 7, 5, 9, 5], dtype=torch.int64, device=DEV)
+    td = torch.tensor([1.0, 2.0, 3.0, 4.0, 7.0], device=DEV)
+    gen = rp.gen[idx].clone()
+    gen[3] += 1  # stale generation for slot 9 -> ignored
+    old9 = float(rp.leaf[9])
+    rp.update_priorities(idx, td, gen)
+    torch.cuda.synchronize()
+    assert float(rp.leaf[5]) == pytest.approx(7.0)
+    assert float(rp.leaf[7]) == pytest.approx(2.0)
+    assert float(rp.leaf[9]) == pytest.approx(old9)
+    leaf = rp.leaf.double().cpu().numpy()
+    assert abs(rp.total() - leaf.sum()) / leaf.sum() < 1e-9
+
+
+def test_sumtree_eviction_zeroes_and_no_resurrection():
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(1000, 600, 1200, 4, device=DEV)
+    _fill_replay(rp, 900)
+    n = rp.remove_to_fit()
+    torch.cuda.synchronize()
+    assert n == 300 and rp.size() == 600
+    leaf = rp.leaf.cpu().numpy()
+    assert np.all(leaf[:300] == 0) and np.all(leaf[300:900] > 0)
+    rp.update_priorities(torch.arange(0, 10, device=DEV), torch.ones(10, device=DEV), None)
+    torch.cuda.synchronize()
+    assert np.all(rp.leaf[:10].cpu().numpy() == 0)
+
+
+def test_gather_frames():
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(100, 100, 200, 4, device=DEV)
+    _fill_replay(rp, 50)
+    slots = torch.randint(0, 58, (16, 4), dtype=torch.int32, device=DEV)
+    out = rp.gather_frames(slots)
+    ref = rp.frames[slots.long()]
+    assert torch.equal(out, ref)
+
+
+def _head_inputs(B=64, A=6, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    Hon = torch.relu(torch.randn(2 * B, 1024, generator=g)).to(DEV, torch.bfloat16)
+    Htg = torch.relu(torch.randn(B, 1024, generator=g)).to(DEV, torch.bfloat16)
+
+    def P():
+        return {"wv": (torch.randn(512, generator=g) * 0.05).to(DEV), "bv": torch.randn(1, generator=g).to(DEV),
+                "wa": (torch.randn(A, 512, generator=g) * 0.05).to(DEV), "ba": torch.randn(A, generator=g).to(DEV)}
+    act = torch.randint(0, A, (B,), generator=g).to(DEV, torch.int32)
+    rew = torch.randn(B, generator=g).to(DEV)
+    gam = torch.full((B,), 0.97, device=DEV)
+    gam[::7] = 0.0
+    isw = torch.rand(B, generator=g).to(DEV)
+    return Hon, Htg, P(), P(), act, rew, gam, isw
+
+
+@pytest.mark.parametrize("huber", [True, False])
+@pytest.mark.parametrize("A", [4, 18])
+def test_ddqn_head_kernel_vs_torch(huber, A):
+    from apex_dqn_amd.ops.fused_ops import HipBackend, TorchBackend
+    B = 64
+    Hon, Htg, Pon, Ptg, act, rew, gam, isw = _head_inputs(B, A)
+    outs = {}
+    for name, be in (("hip", HipBackend()), ("ref", TorchBackend(torch.float32))):
+        td = torch.zeros(B, device=DEV)
+        loss = torch.zeros(B, device=DEV)
+        dH = torch.zeros(B, 1024, device=DEV, dtype=torch.bfloat16 if name == "hip" else torch.float32)
+        dhead = torch.zeros(B, A + 1, device=DEV)
+        q = torch.zeros(B, A, device=DEV)
+        be.head(Hon, Htg, Pon, Ptg, act, rew, gam, isw, huber, 1.0, 1.0 / B, td, loss, dH, dhead, q_out=q)
+        g = {"wv": torch.zeros(512, device=DEV), "bv": torch.zeros(1, device=DEV),
+             "wa": torch.zeros(A, 512, device=DEV), "ba": torch.zeros(A, device=DEV)}
+        be.head_wgrad(Hon, dhead, g)
+        outs[name] = (td, loss, dH.float(), dhead, q, g)
+    h, r = outs["hip"], outs["ref"]
+    torch.testing.assert_close(h[0], r[0], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(h[1], r[1], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(h[2], r[2], rtol=1e-2, atol=1e-6)
+    torch.testing.assert_close(h[3], r[3], rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(h[4], r[4], rtol=1e-4, atol=1e-4)
+    for k in ("wv", "bv", "wa", "ba"):
+        torch.testing.assert_close(h[5][k], r[5][k], rtol=1e-3, atol=1e-6)
+
+
+def test_rmsprop_kernel_vs_torch_optim():
+    from apex_dqn_amd.ops.fused_ops import HipBackend
+    n = 3333829 + 7
+    g = torch.Generator(device="cpu").manual_seed(1)
+    p0 = torch.randn(n, generator=g)
+    be = HipBackend()
+    p = p0.clone().to(DEV)
+    pbf = torch.zeros(n, dtype=torch.bfloat16, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    parts = torch.zeros(1024, dtype=torch.float64, device=DEV)
+    norm = torch.zeros(1, device=DEV)
+    tp = torch.nn.Parameter(p0.clone().to(DEV))
+    opt = torch.optim.RMSprop([tp], lr=2.5e-4, alpha=0.95, eps=1.5e-7, centered=True)
+    for it in range(3):
+        grad = (torch.randn(n, generator=g) * (0.1 if it else 0.001)).to(DEV)
+        be.optimizer(p, grad, v, m, pbf, 2.5e-4, 0.95, 1.5e-7, 40.0, True, parts, norm)
+        tp.grad = grad.clone()
+        torch.nn.utils.clip_grad_norm_([tp], 40.0)
+        opt.step()
+        torch.testing.assert_close(norm[0], grad.double().norm().float(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p, tp.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(pbf.float(), p, rtol=8e-3, atol=1e-6)
+
+
+def test_fused_learner_step_hip_vs_torch_backend():
+    """Whole learner step: HIP backend vs the torch (fp32) backend on identical state."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 64}, "Runtime": {"use_graphs": False}})
+    res = {}
+    for be in ("hip", "torch"):
+        torch.manual_seed(0)
+        rp = GpuReplayShard(2000, 2000, 2100, 4, device=DEV, seed=7)
+        _fill_replay(rp, 1500, seed=11)
+        L = FusedNatureLearner(cfg, DEV, rp, backend=be)
+        if be == "torch":
+            L.ops.dtype = torch.float32
+        L._step_body()
+        torch.cuda.synchronize()
+        res[be] = (L.reference_state_dict(), L.td_abs.clone(), L.g32.clone(), L.S["idx"].clone(),
+                   L.loss_b.clone())
+    # state_dict after step differs by optimizer; compare pre-step consistent things
+    assert torch.equal(res["hip"][3], res["torch"][3])
+    torch.testing.assert_close(res["hip"][1], res["torch"][1], rtol=5e-2, atol=5e-2)
+    gh, gt = res["hip"][2], res["torch"][2]
+    rel = (gh - gt).norm() / gt.norm()
+    assert rel < 5e-2, float(rel)
+
+
+def test_fused_learner_graph_replay_runs():
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 128}, "Runtime": {"use_graphs": True}})
+    rp = GpuReplayShard(4000, 4000, 4100, 4, device=DEV)
+    _fill_replay(rp, 3000)
+    L = FusedNatureLearner(cfg, DEV, rp, backend="hip")
+    for _ in range(5):
+        L.step()
+    torch.cuda.synchronize()
+    m = L.last_metrics()
+    assert np.isfinite(m["loss"]) and m["grad_norm"] > 0
+    assert L.num_q_updates == 5
