@@ -1,0 +1,535 @@
+// MFMA implicit-GEMM kernels for the dueling NatureCNN (gfx950, wave64).
+//
+// Reference compute: duelling_network.py:8-28 (3 convs + 2 stream FCs, run by
+// PyTorch-0.4 on the CPU) and learner.py:56 (autograd backward).  Here every
+// GEMM-shaped op of the learner step is one of two hand-written kernels:
+//
+//  igemm_fwd   C[M,N] = A[M,K] . B[N,K]^T  (+bias, *scale, ReLU | *mask)
+//              A-operand modes: 0 dense bf16 rows (fc fwd / fc dgrad),
+//                               1 NHWC bf16 implicit im2col (conv2/conv3 fwd,
+//                                 conv3 dgrad, conv2 dgrad per stride-parity class),
+//                               2 uint8 frames gathered straight from the replay
+//                                 frame ring by slot index (conv1 fwd: the frame
+//                                 stack is assembled in LDS, never in HBM).
+//  igemm_wgrad dW[Co,Kc] = sum_m dY[m,Co] . X[m,Kc]   (split over m, fp32 slabs),
+//              both operands read column-wise from LDS with ds_read_b64_tr_b16
+//              (the hardware transpose read), conv1 again gathering uint8 frames.
+//
+// Tiles: fwd 128x64x64 (4 waves, 32x64 per wave, v_mfma_f32_16x16x32_bf16);
+// wgrad 64x64 per block over 64-row reduction steps.  LDS images are XOR
+// swizzled so both the row reads (ds_read_b128) and the transposed reads are
+// bank-conflict free.  Global->LDS staging is register double-buffered: the
+// next tile's loads are issued before the current tile's MFMAs.
+#include "apex_common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+struct ConvDesc {
+  const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]; mode 2: u8 frame ring
+  const int32_t* frame_slots; // mode 2: [N][Cin] frame-ring slot per (image, stacked frame)
+  const bf16_t* w;            // B operand [Cout][K] (K contiguous), + cls * w_cls_stride
+  const float* bias;          // [Cout] or null
+  bf16_t* y;                  // output rows of ldy elements
+  const bf16_t* mask;         // optional ReLU mask source (same addressing as y): y = acc * (mask > 0)
+  int N, H, W, Cin;
+  int OH, OW, Cout, KH;
+  int KW, stride, pad_h, pad_w;
+  int mode, relu, ldy, ncls;
+  int ostride_h, ostride_w, OHfull, OWfull;
+  int K;
+  float in_scale;
+  int64_t w_cls_stride;
+};
+
+struct WgradDesc {
+  const bf16_t* dy;           // [Mred][ldd] rows = output pixels / samples
+  const void* x;              // mode 0: bf16 [Mred][ldx]; 1: NHWC bf16; 2: u8 frame ring
+  const int32_t* frame_slots;
+  float* slab;                // [nsplit][Co][Kc] fp32 partial sums
+  float* bias_slab;           // [nsplit][Co] (optional)
+  int N, H, W, Cin;
+  int OH, OW, KH, KW;
+  int stride, pad_h, pad_w, mode;
+  int Co, Kc, ldd, ldx;
+  int rows_per_split, Mred;
+};
+
+// 128-byte LDS rows, 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7):
+// a 16-lane ds_read_b128 group (16 rows, one chunk) hits 16 distinct 16-B slots.
+__device__ __forceinline__ int swz_row(int r, int c) { return (r << 7) + ((c ^ ((r >> 1) & 7)) << 4); }
+// transposed-read image: chunk16 c of row r at c ^ (s(r) << 1), s(r) = bit1(r) | bit3(r)<<1;
+// both ds_read_b64_tr_b16 halves (rows 8g+q, 8(g+1)+q) then cover 64 distinct banks.
+__device__ __forceinline__ int swz_tr(int r, int c) {
+  const int s = ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
+  return (r << 7) + ((c ^ (s << 1)) << 4);
+}
+
+__device__ __forceinline__ uint32_t u8pair_bf16(uint32_t v, int sh) {
+  // two consecutive bytes of v (starting at byte sh) -> two bf16 (exact: integers <= 255)
+  const uint32_t lo = __float_as_uint((float)((v >> (8 * sh)) & 0xffu)) >> 16;
+  const uint32_t hi = __float_as_uint((float)((v >> (8 * sh + 8)) & 0xffu)) >> 16;
+  return lo | (hi << 16);
+}
+
+__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint32_t lo, uint32_t hi) {
+  return make_uint4(u8pair_bf16(lo, 0), u8pair_bf16(lo, 2), u8pair_bf16(hi, 0), u8pair_bf16(hi, 2));
+}
+
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {
+  uint32_t lo = (v & 0x8000u) ? 0u : (v & 0xffffu);
+  uint32_t hi = (v & 0x80000000u) ? 0u : (v & 0xffff0000u);
+  return lo | hi;
+}
+
+__device__ __forceinline__ uint32_t mask_bf16x2(uint32_t v, uint32_t m) {
+  // keep v where the mask element is > 0 (sign clear and non-zero)
+  uint32_t lo = ((m & 0x8000u) == 0 && (m & 0x7fffu) != 0) ? (v & 0xffffu) : 0u;
+  uint32_t hi = ((m & 0x80000000u) == 0 && (m & 0x7fff0000u) != 0) ? (v & 0xffff0000u) : 0u;
+  return lo | hi;
+}
+
+// =====================================================================================
+// forward / dgrad implicit GEMM
+// =====================================================================================
+#define FWD_BM 128
+#define FWD_BN 64
+#define FWD_STAGE (FWD_BM * 128 + FWD_BN * 128)  // bytes per LDS buffer
+
+template <int MODE>
+__global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * FWD_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cls = blockIdx.z;
+  const int OHW = d.OH * d.OW;
+  const int M = d.N * OHW;
+  const int m0 = blockIdx.x * FWD_BM;
+  const int n0 = blockIdx.y * FWD_BN;
+  const bf16_t* __restrict__ wb = d.w + (int64_t)cls * d.w_cls_stride;
+  const int KT = d.K >> 6;
+  const int sc = tid & 7;
+  const int srow = tid >> 3;
+
+  // per-thread staging rows (4 A rows, 2 B rows)
+  bool a_ok[4];
+  int a_img[4], a_ih[4], a_iw[4];
+  const uint8_t* a_base[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + srow + 32 * i;
+    a_ok[i] = m < M;
+    const int mm = a_ok[i] ? m : 0;
+    const int img = mm / OHW, rem = mm - img * OHW;
+    const int oh = rem / d.OW, ow = rem - oh * d.OW;
+    a_img[i] = img;
+    a_ih[i] = oh * d.stride - d.pad_h;
+    a_iw[i] = ow * d.stride - d.pad_w;
+    if (MODE == 0) a_base[i] = (const uint8_t*)d.x + ((int64_t)mm * d.K) * 2;
+    else a_base[i] = nullptr;
+  }
+  uint4 ra[4], rb0, rb1;
+  const bf16_t* wrow0 = wb + (int64_t)(n0 + srow) * d.K + sc * 8;
+  const bf16_t* wrow1 = wrow0 + (int64_t)32 * d.K;
+
+  auto load_tile = [&](int kt) {
+    rb0 = *reinterpret_cast<const uint4*>(wrow0 + (kt << 6));
+    rb1 = *reinterpret_cast<const uint4*>(wrow1 + (kt << 6));
+    if (MODE == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        ra[i] = a_ok[i] ? *reinterpret_cast<const uint4*>(a_base[i] + ((kt << 6) + sc * 8) * 2)
+                        : make_uint4(0, 0, 0, 0);
+    } else if (MODE == 1) {
+      const int cpb = d.Cin >> 6;
+      const int tap = kt / cpb, cb = kt - tap * cpb;
+      const int kh = tap / d.KW, kw = tap - kh * d.KW;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
+        const bool ok = a_ok[i] && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
+        const bf16_t* src = (const bf16_t*)d.x +
+                            ((((int64_t)a_img[i] * d.H + ih) * d.W + iw) * d.Cin + (cb << 6) + sc * 8);
+        ra[i] = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+      }
+    } else {  // MODE 2: uint8 frames, K ordered (c, kh, kw), one frame per k-tile, chunk = kh
+      const int c = kt;
+      const int64_t fbytes = (int64_t)d.H * d.W;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (a_ok[i]) {
+          const int slot = d.frame_slots[a_img[i] * d.Cin + c];
+          const uint8_t* p = (const uint8_t*)d.x + slot * fbytes + (int64_t)(a_ih[i] + sc) * d.W + a_iw[i];
+          ra[i].x = *reinterpret_cast<const uint32_t*>(p);
+          ra[i].y = *reinterpret_cast<const uint32_t*>(p + 4);
+        } else {
+          ra[i].x = 0;
+          ra[i].y = 0;
+        }
+      }
+    }
+  };
+
+  auto write_tile = [&](int buf) {
+    uint8_t* As = smem + buf * FWD_STAGE;
+    uint8_t* Bs = As + FWD_BM * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = srow + 32 * i;
+      uint4 v = (MODE == 2) ? u8x8_to_bf16x8(ra[i].x, ra[i].y) : ra[i];
+      *reinterpret_cast<uint4*>(As + swz_row(r, sc)) = v;
+    }
+    *reinterpret_cast<uint4*>(Bs + swz_row(srow, sc)) = rb0;
+    *reinterpret_cast<uint4*>(Bs + swz_row(srow + 32, sc)) = rb1;
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load_tile(0);
+  write_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_tile(kt + 1);
+    const uint8_t* As = smem + cur * FWD_STAGE;
+    const uint8_t* Bs = As + FWD_BM * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 4 * s + (lane >> 4);
+      bf16x8 a[2], b[4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        a[mt] = *reinterpret_cast<const bf16x8*>(As + swz_row(32 * wv + 16 * mt + (lane & 15), c));
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        b[nt] = *reinterpret_cast<const bf16x8*>(Bs + swz_row(16 * nt + (lane & 15), c));
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+    }
+    if (kt + 1 < KT) write_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: scale + bias -> bf16 in LDS (per-wave 32x64 image), then
+  // coalesced 16-B row stores with ReLU or mask applied
+  uint8_t* Es = smem + wv * 4096;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int col = 16 * nt + (lane & 15);
+      const float bv = d.bias ? d.bias[n0 + col] : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = 16 * mt + 4 * (lane >> 4) + j;
+        *reinterpret_cast<bf16_t*>(Es + row * 128 + col * 2) = f32_to_bf16(acc[mt][nt][j] * d.in_scale + bv);
+      }
+    }
+  __syncthreads();
+  const int ooh = (d.ncls == 4) ? (cls >> 1) : 0;
+  const int oow = (d.ncls == 4) ? (cls & 1) : 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int row = 8 * p + (lane >> 3), ch = lane & 7;
+    const int m = m0 + 32 * wv + row;
+    if (m >= M) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(Es + row * 128 + ch * 16);
+    const int img = m / OHW, rem = m - img * OHW;
+    const int oh = rem / d.OW, ow = rem - oh * d.OW;
+    const int64_t orow = ((int64_t)img * d.OHfull + oh * d.ostride_h + ooh) * d.OWfull + ow * d.ostride_w + oow;
+    const int64_t off = orow * d.ldy + n0 + ch * 8;
+    if (d.mask) {
+      const uint4 mk = *reinterpret_cast<const uint4*>(d.mask + off);
+      v = make_uint4(mask_bf16x2(v.x, mk.x), mask_bf16x2(v.y, mk.y), mask_bf16x2(v.z, mk.z),
+                     mask_bf16x2(v.w, mk.w));
+    } else if (d.relu) {
+      v = make_uint4(relu_bf16x2(v.x), relu_bf16x2(v.y), relu_bf16x2(v.z), relu_bf16x2(v.w));
+    }
+    *reinterpret_cast<uint4*>(d.y + off) = v;
+  }
+}
+
+// =====================================================================================
+// weight gradient: dW[Co][Kc] partial over a slice of the reduction rows
+// =====================================================================================
+#define WG_BR 64                         // reduction rows per step
+#define WG_TILE (WG_BR * 128)            // one 64x64 bf16 operand image (8 KB)
+
+template <int MODE>
+__global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * WG_TILE + 256 * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int kct = blockIdx.x;            // 64-wide column tile of Kc
+  const int cot = blockIdx.y;            // 64-wide row tile of Co
+  const int split = blockIdx.z;
+  const int r_begin = split * d.rows_per_split;
+  const int r_end = min(d.Mred, r_begin + d.rows_per_split);
+  const int OHW = d.OH * d.OW;
+  const int sc = tid & 7, srow = tid >> 3;  // staging: rows srow, srow+32; chunk sc
+  const bool do_bias = d.bias_slab != nullptr && kct == 0;
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  // column-tile decode for the X operand
+  int tap = 0, cb = 0, kh = 0, kw = 0;
+  if (MODE == 1) {
+    const int cpb = d.Cin >> 6;
+    tap = kct / cpb;
+    cb = kct - tap * cpb;
+    kh = tap / d.KW;
+    kw = tap - kh * d.KW;
+  }
+  uint4 rdy[2], rx[2];
+
+  auto load_step = [&](int r0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = r0 + srow + 32 * i;
+      const bool ok = m < r_end;
+      rdy[i] = ok ? *reinterpret_cast<const uint4*>(d.dy + (int64_t)m * d.ldd + cot * 64 + sc * 8)
+                  : make_uint4(0, 0, 0, 0);
+      if (MODE == 0) {
+        rx[i] = ok ? *reinterpret_cast<const uint4*>((const bf16_t*)d.x + (int64_t)m * d.ldx + kct * 64 + sc * 8)
+                   : make_uint4(0, 0, 0, 0);
+      } else {
+        const int mm = ok ? m : 0;
+        const int img = mm / OHW, rem = mm - img * OHW;
+        const int oh = rem / d.OW, ow = rem - oh * d.OW;
+        if (MODE == 1) {
+          const int ih = oh * d.stride - d.pad_h + kh, iw = ow * d.stride - d.pad_w + kw;
+          const bool ok2 = ok && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
+          const bf16_t* src =
+              (const bf16_t*)d.x + ((((int64_t)img * d.H + ih) * d.W + iw) * d.Cin + (cb << 6) + sc * 8);
+          rx[i] = ok2 ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        } else {  // MODE 2: u8 frame of channel kct, chunk = kh row of 8 bytes
+          if (ok) {
+            const int slot = d.frame_slots[img * d.Cin + kct];
+            const uint8_t* p = (const uint8_t*)d.x + (int64_t)slot * d.H * d.W +
+                               (int64_t)(oh * d.stride + sc) * d.W + ow * d.stride;
+            rx[i].x = *reinterpret_cast<const uint32_t*>(p);
+            rx[i].y = *reinterpret_cast<const uint32_t*>(p + 4);
+          } else {
+            rx[i].x = 0;
+            rx[i].y = 0;
+          }
+        }
+      }
+    }
+  };
+
+  auto write_step = [&](int buf) {
+    uint8_t* Ds = smem + buf * 2 * WG_TILE;
+    uint8_t* Xs = Ds + WG_TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = srow + 32 * i;
+      *reinterpret_cast<uint4*>(Ds + swz_tr(r, sc)) = rdy[i];
+      uint4 xv = (MODE == 2) ? u8x8_to_bf16x8(rx[i].x, rx[i].y) : rx[i];
+      *reinterpret_cast<uint4*>(Xs + swz_tr(r, sc)) = xv;
+      if (do_bias) {
+        const uint32_t w4[4] = {rdy[i].x, rdy[i].y, rdy[i].z, rdy[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bsum[2 * j] += __uint_as_float(w4[j] << 16);
+          bsum[2 * j + 1] += __uint_as_float(w4[j] & 0xffff0000u);
+        }
+      }
+    }
+  };
+
+  // wave tile: 32 (Co) x 32 (Kc) = 2x2 MFMA 16x16 tiles
+  const int wco = (wv >> 1) * 32, wkc = (wv & 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read lane geometry: group g = lane>>4, within group q = (lane>>2)&3 (row), p = lane&3 (cols)
+  const int g = lane >> 4, q = (lane >> 2) & 3, pcol = lane & 3;
+
+  auto tr_frag = [&](const uint8_t* img, int kk, int col0) -> bf16x8 {
+    // 8 consecutive reduction rows (32kk + 8g .. +7) of column col0 + (lane & 15)
+    const int rA = 32 * kk + 8 * g + q;
+    const int cbyte = (col0 + 4 * pcol) * 2;  // byte offset of 4 columns inside the 128-B row
+    const int c16 = cbyte >> 4, within = cbyte & 15;
+    const lds_s16x4* pa = (const lds_s16x4*)(img + swz_tr(rA, c16) + within);
+    const lds_s16x4* pb = (const lds_s16x4*)(img + swz_tr(rA + 4, c16) + within);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pa));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pb));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  const int nsteps = (r_end - r_begin + WG_BR - 1) / WG_BR;
+  if (nsteps > 0) {
+    load_step(r_begin);
+    write_step(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int cur = st & 1;
+    if (st + 1 < nsteps) load_step(r_begin + (st + 1) * WG_BR);
+    const uint8_t* Ds = smem + cur * 2 * WG_TILE;
+    const uint8_t* Xs = Ds + WG_TILE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 a[2], b[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) a[t] = tr_frag(Ds, kk, wco + 16 * t);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) b[t] = tr_frag(Xs, kk, wkc + 16 * t);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < nsteps) write_step(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- store the fp32 partial tile: slab[split][co][kc]
+  float* slab = d.slab + (int64_t)split * d.Co * d.Kc;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = kct * 64 + wkc + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = cot * 64 + wco + 16 * i + 4 * (lane >> 4) + r;
+        slab[(int64_t)row * d.Kc + col] = acc[i][j][r];
+      }
+    }
+  if (do_bias) {
+    // reduce the per-thread column sums over threads sharing a chunk (lane bits 3..5, then waves)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = bsum[j];
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      bsum[j] = v;
+    }
+    float* red = reinterpret_cast<float*>(smem + 4 * WG_TILE);
+    if (lane < 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wv * 64 + lane * 8 + j] = bsum[j];
+    }
+    __syncthreads();
+    if (tid < 64) {
+      const float s = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
+      d.bias_slab[(int64_t)split * d.Co + cot * 64 + tid] = s;
+    }
+  }
+}
+
+// sum fp32 slabs over splits -> fp32 gradient (scaled), and the bias partials
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, int nsplit, int64_t n, float scale,
+                                   float* __restrict__ out, const float* __restrict__ bslab, int nb,
+                                   float* __restrict__ bout) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 * 4 < n) {
+    float4 s = make_float4(0, 0, 0, 0);
+    for (int k = 0; k < nsplit; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)k * n + i4 * 4);
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
+    *reinterpret_cast<float4*>(out + i4 * 4) = s;
+  }
+  if (bslab != nullptr && i4 < nb) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += bslab[(int64_t)k * nb + i4];
+    bout[i4] = s;
+  }
+}
+
+// Pack the bf16 weight copies the dgrad GEMMs read as their B operand:
+//  WfcT[n][k] = Wfc[k][n]                              (3136 x 1024, LDS-tiled transpose)
+//  W3TF[ci][kh][kw][co] = W3[co][2-kh][2-kw][ci]        (flipped + transposed; 64 x 576)
+//  W2T[cls=(p,q)][ci][a][b][co] = W2[co][p+2(1-a)][q+2(1-b)][ci]   (4 x 64 x 256)
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ src, int R, int C,
+                                                             bf16_t* __restrict__ dst) {
+  __shared__ bf16_t t[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i >> 6, c = i & 63;
+    if (r0 + r < R && c0 + c < C) t[r][c] = src[(int64_t)(r0 + r) * C + c0 + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int c = i >> 6, r = i & 63;
+    if (r0 + r < R && c0 + c < C) dst[(int64_t)(c0 + c) * R + r0 + r] = t[r][c];
+  }
+}
+
+__global__ void pack_conv_dgrad_weights_kernel(const bf16_t* __restrict__ w3, const bf16_t* __restrict__ w2,
+                                               bf16_t* __restrict__ w3tf, bf16_t* __restrict__ w2t) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n1 = 64LL * 576, n2 = 4LL * 64 * 256;
+  if (i < n1) {
+    const int ci = (int)(i / 576), r = (int)(i - (int64_t)ci * 576);
+    const int kh = r / 192, kw = (r / 64) % 3, co = r & 63;
+    w3tf[i] = w3[((co * 3 + (2 - kh)) * 3 + (2 - kw)) * 64 + ci];
+  } else if (i < n1 + n2) {
+    const int64_t j = i - n1;
+    const int cls = (int)(j / (64 * 256)), r = (int)(j - (int64_t)cls * 64 * 256);
+    const int ci = r / 256, r2 = r & 255;
+    const int a = r2 / 128, b = (r2 / 64) & 1, co = r2 & 63;
+    const int p = cls >> 1, qq = cls & 1;
+    const int kh = p + 2 * (1 - a), kw = qq + 2 * (1 - b);
+    w2t[j] = w2[((co * 4 + kh) * 4 + kw) * 64 + ci];
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
+  if ((d.K & 63) || (d.Cout & 63) || d.K <= 0) return (int)hipErrorInvalidValue;
+  if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
+  if (d.mode == 2 && (d.KH != 8 || d.KW != 8 || d.K != d.Cin * 64)) return (int)hipErrorInvalidValue;
+  const int M = d.N * d.OH * d.OW;
+  dim3 grid((M + FWD_BM - 1) / FWD_BM, d.Cout / FWD_BN, d.ncls > 0 ? d.ncls : 1);
+  if (d.mode == 0) igemm_fwd_kernel<0><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1) igemm_fwd_kernel<1><<<grid, 256, 0, st>>>(d);
+  else igemm_fwd_kernel<2><<<grid, 256, 0, st>>>(d);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_conv_wgrad(WgradDesc d, float* out, float* bout, int nsplit, float scale, hipStream_t st) {
+  if ((d.Kc & 63) || (d.Co & 63)) return (int)hipErrorInvalidValue;
+  if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
+  dim3 grid(d.Kc / 64, d.Co / 64, nsplit);
+  if (d.mode == 0) igemm_wgrad_kernel<0><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1) igemm_wgrad_kernel<1><<<grid, 256, 0, st>>>(d);
+  else igemm_wgrad_kernel<2><<<grid, 256, 0, st>>>(d);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (out != nullptr) {
+    const int64_t n = (int64_t)d.Co * d.Kc;
+    const int64_t nthreads = (n / 4 > d.Co ? n / 4 : d.Co);
+    slab_reduce_kernel<<<(int)((nthreads + 255) / 256), 256, 0, st>>>(d.slab, nsplit, n, scale, out,
+                                                                       d.bias_slab, d.bias_slab ? d.Co : 0, bout);
+  }
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_pack_dgrad_weights(const bf16_t* wfc, const bf16_t* w3, const bf16_t* w2, bf16_t* wfcT,
+                                        bf16_t* w3tf, bf16_t* w2t, hipStream_t st) {
+  transpose_bf16_kernel<<<dim3(3136 / 64, 1024 / 64), 256, 0, st>>>(wfc, 1024, 3136, wfcT);
+  const int64_t n = 64LL * 576 + 4LL * 64 * 256;
+  pack_conv_dgrad_weights_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(w3, w2, w3tf, w2t);
+  APEX_CHECK_LAUNCH();
+}

@@ -34,51 +34,86 @@ struct RecordDesc {
   int64_t cap;
 };
 
-__device__ __forceinline__ void tree_set_leaf(const TreeDesc& t, int64_t i, float v) {
-  float old = t.leaf[i];
-  t.leaf[i] = v;
-  double d = (double)v - (double)old;
-  if (d != 0.0) {
-    int64_t node = i;
-    for (int k = 1; k <= t.L; ++k) {
-      node >>= 6;
-      atomicAdd(&t.nodes[t.off[k] + node], d);
+// Write leaf values and propagate the deltas up the tree.  Must be called by
+// every lane of the wave (uniform control flow): lanes whose deltas target the
+// same node are summed with a wave reduction first, so a level receives one
+// fp64 atomic per distinct node per wave -- the root gets one per wave instead
+// of one per updated leaf (the contention that dominated a naive version).
+__device__ __forceinline__ void tree_write_and_propagate(const TreeDesc& t, bool act, int64_t i, float v) {
+  const int lane = threadIdx.x & 63;
+  double d = 0.0;
+  if (act) {
+    const float old = t.leaf[i];
+    t.leaf[i] = v;
+    d = (double)v - (double)old;
+  }
+  int64_t node = act ? i : 0;
+  uint64_t live = __ballot(act && d != 0.0);
+  for (int k = 1; k <= t.L && live; ++k) {
+    node >>= 6;
+    uint64_t pending = live;
+    while (pending) {
+      const int leader = __ffsll((unsigned long long)pending) - 1;
+      const int64_t ln = __shfl(node, leader, 64);
+      const bool mine = ((pending >> lane) & 1ull) && node == ln;
+      const double s = wave_sum(mine ? d : 0.0);
+      if (lane == leader) atomicAdd(&t.nodes[t.off[k] + ln], s);
+      pending &= ~__ballot(mine);
     }
   }
-  if (v > 0.f) atomicMin(t.min_bits, __float_as_uint(v));
+  // running min over positive leaves: one atomic per wave
+  float mv = (act && v > 0.f) ? v : __uint_as_float(0x7f800000u);
+  mv = wave_min(mv);
+  if (lane == 0 && mv < __uint_as_float(0x7f800000u)) atomicMin(t.min_bits, __float_as_uint(mv));
 }
 
 // mode 0: values are leaf values; mode 1: values are |td| -> (|td|+eps)^alpha,
 // skipping evicted leaves (leaf == 0) and slots re-used since sampling (gen).
+// Launched with whole waves; out-of-range threads take part as inactive lanes.
 __global__ void tree_update_kernel(TreeDesc t, const int64_t* __restrict__ idx,
                                    const float* __restrict__ values, int n, int mode,
                                    float alpha, float eps, const int32_t* __restrict__ gen_expect,
                                    const int32_t* __restrict__ gen, int dedupe,
                                    uint64_t* ctr_to_bump) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int64_t sidx[1024];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (ctr_to_bump != nullptr && i == 0) ctr_to_bump[0] += 1;
-  if (i >= n) return;
-  int64_t s = idx[i];
-  if (s < 0 || s >= t.n[0]) return;
-  if (dedupe) {
-    for (int j = i + 1; j < n; ++j)
-      if (idx[j] == s) return;  // a later write to the same leaf wins
+  const bool use_lds = dedupe && n <= 1024;
+  if (use_lds) {
+    for (int j = threadIdx.x; j < n; j += blockDim.x) sidx[j] = idx[j];
+    __syncthreads();
   }
-  float v = values[i];
-  if (mode == 1) {
-    if (t.leaf[s] <= 0.f) return;
-    if (gen_expect != nullptr && gen[s] != gen_expect[i]) return;
-    v = powf(fabsf(v) + eps, alpha);
+  bool act = i < n;
+  int64_t s = 0;
+  float v = 0.f;
+  if (act) {
+    s = idx[i];
+    act = s >= 0 && s < t.n[0];
   }
-  tree_set_leaf(t, s, v);
+  if (act && dedupe) {
+    for (int j = i + 1; j < n; ++j) {
+      const int64_t o = use_lds ? sidx[j] : idx[j];
+      if (o == s) { act = false; break; }  // a later write to the same leaf wins
+    }
+  }
+  if (act) {
+    v = values[i];
+    if (mode == 1) {
+      if (t.leaf[s] <= 0.f) act = false;
+      else if (gen_expect != nullptr && gen[s] != gen_expect[i]) act = false;
+      v = powf(fabsf(v) + eps, alpha);
+    }
+  }
+  tree_write_and_propagate(t, act, s, v);
 }
 
 // zero `count` leaves starting at ring slot `start` (FIFO eviction)
 __global__ void tree_zero_range_kernel(TreeDesc t, int64_t start, int64_t count) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  int64_t s = (start + i) % t.n[0];
-  if (t.leaf[s] != 0.f) tree_set_leaf(t, s, 0.f);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = i < count;
+  const int64_t s = act ? (start + i) % t.n[0] : 0;
+  if (act && t.leaf[s] == 0.f) act = false;
+  tree_write_and_propagate(t, act, s, 0.f);
 }
 
 // scatter K staged records into ring slots start..start+K-1 (mod cap) and set
@@ -90,18 +125,22 @@ __global__ void replay_insert_kernel(TreeDesc t, RecordDesc r, int64_t start, in
                                      const float* __restrict__ s_rew,
                                      const float* __restrict__ s_gam,
                                      const float* __restrict__ s_prio, float alpha, float eps) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= K) return;
-  int64_t s = (start + i) % r.cap;
-  for (int c = 0; c < r.C; ++c) {
-    r.obs[s * r.C + c] = s_obs[(int64_t)i * r.C + c];
-    r.nxt[s * r.C + c] = s_nxt[(int64_t)i * r.C + c];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < K;
+  const int64_t s = act ? (start + i) % r.cap : 0;
+  float v = 0.f;
+  if (act) {
+    for (int c = 0; c < r.C; ++c) {
+      r.obs[s * r.C + c] = s_obs[(int64_t)i * r.C + c];
+      r.nxt[s * r.C + c] = s_nxt[(int64_t)i * r.C + c];
+    }
+    r.act[s] = s_act[i];
+    r.rew[s] = s_rew[i];
+    r.gam[s] = s_gam[i];
+    r.gen[s] += 1;
+    v = powf(fabsf(s_prio[i]) + eps, alpha);
   }
-  r.act[s] = s_act[i];
-  r.rew[s] = s_rew[i];
-  r.gam[s] = s_gam[i];
-  r.gen[s] += 1;
-  tree_set_leaf(t, s, powf(fabsf(s_prio[i]) + eps, alpha));
+  tree_write_and_propagate(t, act, s, v);
 }
 
 // Stratified proportional sampling: one wave per sample, 64-ary descent.

@@ -112,12 +112,14 @@ class FusedNatureLearner:
         self.g_head_region = self.g32[o0:o1]
 
     # ------------------------------------------------------------ forward
-    def forward_online(self, frames, rows: int, y1, y2, y3, h, Pb):
+    def forward_online(self, slots, rows: int, y1, y2, y3, h, Pb, Pf, frames_buf):
+        """Forward of ``rows`` frame stacks: bf16 weights ``Pb``, fp32 biases ``Pf``."""
         ops, rt = self.ops, self.rt
-        ops.conv1_fwd(frames[:rows], Pb["w1"], Pb["b1"], rt.obs_scale, y1[:rows])
-        ops.conv_fwd(y1[:rows], Pb["w2"], Pb["b2"], 2, y2[:rows])
-        ops.conv_fwd(y2[:rows], Pb["w3"], Pb["b3"], 1, y3[:rows])
-        ops.fc_fwd(y3[:rows].reshape(rows, 3136), Pb["wfc"], Pb["bfc"], h[:rows])
+        ops.conv1_fwd_ring(self.replay.frames, slots[:rows], frames_buf, Pb["w1"], Pf["b1"], rt.obs_scale,
+                           y1[:rows])
+        ops.conv_fwd(y1[:rows], Pb["w2"], Pf["b2"], 2, y2[:rows])
+        ops.conv_fwd(y2[:rows], Pb["w3"], Pf["b3"], 1, y3[:rows])
+        ops.fc_fwd(y3[:rows].reshape(rows, 3136), Pb["wfc"], Pf["bfc"], h[:rows])
 
     def _head_params(self, V):
         return {k: V[k] for k in ("wv", "bv", "wa", "ba")}
@@ -125,13 +127,15 @@ class FusedNatureLearner:
     # ---------------------------------------------------------------- step
     def _step_body(self, ratio_min: Optional[torch.Tensor] = None) -> None:
         B, rt, ops = self.B, self.rt, self.ops
+        ops.prepare(self.Pb)
         S = self.replay.sample(B, out=self.S, ratio_min_global=ratio_min)
         self.slots[:B].copy_(S["obs"])
         self.slots[B:].copy_(S["nxt"])
-        self.replay.gather_frames(self.slots, self.frames)
-        # online forward on [S_t ; S_tpn], target forward on S_tpn
-        self.forward_online(self.frames, 2 * B, self.y1, self.y2, self.y3, self.h, self.Pb)
-        self.forward_online(self.frames[B:], B, self.y1t, self.y2t, self.y3t, self.ht, self.Tb)
+        # online forward on [S_t ; S_tpn], target forward on S_tpn; conv1 reads the
+        # uint8 frame stacks straight from the replay ring by slot
+        self.forward_online(self.slots, 2 * B, self.y1, self.y2, self.y3, self.h, self.Pb, self.P, self.frames)
+        self.forward_online(self.slots[B:], B, self.y1t, self.y2t, self.y3t, self.ht, self.Tb, self.T,
+                            self.frames[B:])
         isw = S["weights"] if rt.use_is_weights else None
         ops.head(self.h, self.ht, self._head_params(self.P), self._head_params(self.T), S["act"], S["rew"],
                  S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / B, self.td_abs, self.loss_b,
@@ -143,7 +147,8 @@ class FusedNatureLearner:
         ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"])
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1)
         ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"])
-        ops.conv1_wgrad(self.dY1, self.frames[:B], rt.obs_scale, G["w1"], G["b1"])
+        ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
+                             G["b1"])
         if self.comm is not None and self.comm.world_size > 1:
             self.comm.allreduce_flat(self.g32, average=True)
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,

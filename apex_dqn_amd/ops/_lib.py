@@ -42,13 +42,24 @@ class HeadParams(ctypes.Structure):
 
 
 class ConvDesc(ctypes.Structure):
-    """Implicit-GEMM conv problem (see csrc/conv_mfma.hip)."""
+    """Implicit-GEMM forward/dgrad problem (mirrors ``ConvDesc`` in csrc/conv_mfma.hip)."""
     _fields_ = [("x", c_p), ("frame_slots", c_p), ("w", c_p), ("bias", c_p), ("y", c_p), ("mask", c_p),
-                ("N", c_i), ("H", c_i), ("W", c_i), ("Cin", c_i), ("OH", c_i), ("OW", c_i),
-                ("Cout", c_i), ("KH", c_i), ("KW", c_i), ("stride", c_i), ("mode", c_i),
-                ("relu", c_i), ("in_scale", c_f), ("ostride_h", c_i), ("ostride_w", c_i),
-                ("ooff_h", c_i), ("ooff_w", c_i), ("OHfull", c_i), ("OWfull", c_i),
-                ("pad_h", c_i), ("pad_w", c_i), ("tap_step", c_i)]
+                ("N", c_i), ("H", c_i), ("W", c_i), ("Cin", c_i),
+                ("OH", c_i), ("OW", c_i), ("Cout", c_i), ("KH", c_i),
+                ("KW", c_i), ("stride", c_i), ("pad_h", c_i), ("pad_w", c_i),
+                ("mode", c_i), ("relu", c_i), ("ldy", c_i), ("ncls", c_i),
+                ("ostride_h", c_i), ("ostride_w", c_i), ("OHfull", c_i), ("OWfull", c_i),
+                ("K", c_i), ("in_scale", c_f), ("w_cls_stride", c_i64)]
+
+
+class WgradDesc(ctypes.Structure):
+    """Weight-gradient problem (mirrors ``WgradDesc`` in csrc/conv_mfma.hip)."""
+    _fields_ = [("dy", c_p), ("x", c_p), ("frame_slots", c_p), ("slab", c_p), ("bias_slab", c_p),
+                ("N", c_i), ("H", c_i), ("W", c_i), ("Cin", c_i),
+                ("OH", c_i), ("OW", c_i), ("KH", c_i), ("KW", c_i),
+                ("stride", c_i), ("pad_h", c_i), ("pad_w", c_i), ("mode", c_i),
+                ("Co", c_i), ("Kc", c_i), ("ldd", c_i), ("ldx", c_i),
+                ("rows_per_split", c_i), ("Mred", c_i)]
 
 
 _SIGS = {

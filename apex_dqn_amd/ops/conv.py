@@ -1,0 +1,169 @@
+"""Python launchers for the MFMA implicit-GEMM family (csrc/conv_mfma.hip).
+
+Every function writes into caller-provided buffers and launches on the
+current stream, so the whole learner step is graph-capturable.  Workspaces
+(wgrad split-K slabs) are cached per shape in ``Workspace``.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+
+class Workspace:
+    def __init__(self):
+        self.bufs: Dict[Tuple, torch.Tensor] = {}
+
+    def get(self, key, numel: int, device, dtype=torch.float32) -> torch.Tensor:
+        k = (key, numel, str(device), dtype)
+        t = self.bufs.get(k)
+        if t is None:
+            t = torch.empty(numel, dtype=dtype, device=device)
+            self.bufs[k] = t
+        return t
+
+
+def _conv_desc(**kw) -> "_lib.ConvDesc":
+    d = _lib.ConvDesc()
+    d.x = kw.get("x")
+    d.frame_slots = kw.get("frame_slots")
+    d.w = kw["w"]
+    d.bias = kw.get("bias")
+    d.y = kw["y"]
+    d.mask = kw.get("mask")
+    d.N, d.H, d.W, d.Cin = kw["N"], kw.get("H", 1), kw.get("W", 1), kw["Cin"]
+    d.OH, d.OW, d.Cout = kw.get("OH", 1), kw.get("OW", 1), kw["Cout"]
+    d.KH, d.KW = kw.get("KH", 1), kw.get("KW", 1)
+    d.stride, d.pad_h, d.pad_w = kw.get("stride", 1), kw.get("pad", 0), kw.get("pad", 0)
+    d.mode, d.relu = kw["mode"], int(kw.get("relu", 0))
+    d.ldy, d.ncls = kw.get("ldy", kw["Cout"]), kw.get("ncls", 1)
+    d.ostride_h = d.ostride_w = kw.get("ostride", 1)
+    d.OHfull, d.OWfull = kw.get("OHfull", d.OH), kw.get("OWfull", d.OW)
+    d.K = kw["K"]
+    d.in_scale = float(kw.get("scale", 1.0))
+    d.w_cls_stride = kw.get("w_cls_stride", 0)
+    return d
+
+
+def _launch_fwd(lib, d) -> None:
+    _lib.check(lib.apex_conv_fwd(d, _lib.stream_ptr()), "conv_fwd")
+
+
+def conv1_fwd_ring(lib, ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor,
+                   scale: float, out: torch.Tensor) -> None:
+    """conv1 (8x8 s4, C stacked frames -> 64) reading uint8 frames from the replay ring."""
+    N, C = slots.shape
+    H, W = ring.shape[1], ring.shape[2]
+    assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
+    d = _conv_desc(x=ring.data_ptr(), frame_slots=slots.data_ptr(), w=w1.data_ptr(), bias=b1.data_ptr(),
+                   y=out.data_ptr(), N=N, H=H, W=W, Cin=C, OH=20, OW=20, Cout=64, KH=8, KW=8, stride=4,
+                   mode=2, relu=1, K=C * 64, scale=scale)
+    _launch_fwd(lib, d)
+
+
+def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int, out: torch.Tensor) -> None:
+    """NHWC conv + bias + ReLU with OHWI weights (conv2 / conv3)."""
+    N, H, W, Cin = x.shape
+    Cout, KH, KW, _ = w.shape
+    OH, OW = out.shape[1], out.shape[2]
+    d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=b.data_ptr(), y=out.data_ptr(), N=N, H=H, W=W,
+                   Cin=Cin, OH=OH, OW=OW, Cout=Cout, KH=KH, KW=KW, stride=stride, mode=1, relu=1,
+                   K=KH * KW * Cin)
+    _launch_fwd(lib, d)
+
+
+def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
+              relu: bool = True, mask: Optional[torch.Tensor] = None) -> None:
+    """out[M,N] = act(x[M,K] @ w[N,K]^T + b)  (or * (mask > 0))."""
+    M, K = x.shape
+    Nc = w.shape[0]
+    assert w.shape[1] == K and out.shape == (M, Nc)
+    d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), mask=_lib.ptr(mask),
+                   N=M, Cin=K, Cout=Nc, mode=0, relu=relu and mask is None, K=K)
+    _launch_fwd(lib, d)
+
+
+def conv3_dgrad(lib, dy: torch.Tensor, w3tf: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
+    """dX2 (9x9) from dY3 (7x7): full correlation with the flipped/transposed 3x3 weights."""
+    N = dy.shape[0]
+    d = _conv_desc(x=dy.data_ptr(), w=w3tf.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=7, W=7,
+                   Cin=64, OH=9, OW=9, Cout=64, KH=3, KW=3, stride=1, pad=2, mode=1, K=576)
+    _launch_fwd(lib, d)
+
+
+def conv2_dgrad(lib, dy: torch.Tensor, w2t: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
+    """dX1 (20x20) from dY2 (9x9), 4x4 stride 2: four stride-parity classes, each a
+    2x2 stride-1 correlation (pad 1) writing every other output pixel."""
+    N = dy.shape[0]
+    d = _conv_desc(x=dy.data_ptr(), w=w2t.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
+                   Cin=64, OH=10, OW=10, Cout=64, KH=2, KW=2, stride=1, pad=1, mode=1, K=256, ncls=4,
+                   ostride=2, OHfull=20, OWfull=20, w_cls_stride=64 * 256)
+    _launch_fwd(lib, d)
+
+
+def _wg_desc(**kw) -> "_lib.WgradDesc":
+    d = _lib.WgradDesc()
+    d.dy, d.x, d.frame_slots = kw["dy"], kw["x"], kw.get("frame_slots")
+    d.slab, d.bias_slab = kw["slab"], kw.get("bias_slab")
+    d.N, d.H, d.W, d.Cin = kw.get("N", 1), kw.get("H", 1), kw.get("W", 1), kw.get("Cin", 64)
+    d.OH, d.OW, d.KH, d.KW = kw.get("OH", 1), kw.get("OW", 1), kw.get("KH", 1), kw.get("KW", 1)
+    d.stride, d.pad_h, d.pad_w, d.mode = kw.get("stride", 1), 0, 0, kw["mode"]
+    d.Co, d.Kc, d.ldd, d.ldx = kw["Co"], kw["Kc"], kw["ldd"], kw.get("ldx", 0)
+    d.rows_per_split, d.Mred = kw["rows_per_split"], kw["Mred"]
+    return d
+
+
+def _splits(Mred: int, per_img: int, target_rows: int) -> Tuple[int, int]:
+    imgs = max(1, target_rows // per_img)
+    rows = imgs * per_img
+    return (Mred + rows - 1) // rows, rows
+
+
+def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, stride: int,
+               dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1024) -> None:
+    """dW (OHWI, fp32) and db for an NHWC conv with 64 output channels."""
+    N, OH, OW, Co = dy.shape
+    _, H, W, Cin = x.shape
+    Kc = KH * KH * Cin
+    Mred = N * OH * OW
+    nsplit, rows = _splits(Mred, OH * OW, target_rows)
+    slab = ws.get(("wg", Co, Kc), nsplit * Co * Kc, dy.device)
+    bslab = ws.get(("wgb", Co), nsplit * Co, dy.device)
+    d = _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=slab.data_ptr(), bias_slab=bslab.data_ptr(), N=N,
+                 H=H, W=W, Cin=Cin, OH=OH, OW=OW, KH=KH, KW=KH, stride=stride, mode=1, Co=Co, Kc=Kc, ldd=Co,
+                 rows_per_split=rows, Mred=Mred)
+    _lib.check(lib.apex_conv_wgrad(d, dw_out.data_ptr(), db_out.data_ptr(), nsplit, 1.0, _lib.stream_ptr()),
+               "conv_wgrad")
+
+
+def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
+                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1600) -> None:
+    N, OH, OW, Co = dy.shape
+    C = slots.shape[1]
+    Kc = C * 64
+    Mred = N * OH * OW
+    nsplit, rows = _splits(Mred, OH * OW, target_rows)
+    slab = ws.get(("wg1", Co, Kc), nsplit * Co * Kc, dy.device)
+    bslab = ws.get(("wg1b", Co), nsplit * Co, dy.device)
+    d = _wg_desc(dy=dy.data_ptr(), x=ring.data_ptr(), frame_slots=slots.data_ptr(), slab=slab.data_ptr(),
+                 bias_slab=bslab.data_ptr(), N=N, H=ring.shape[1], W=ring.shape[2], Cin=C, OH=OH, OW=OW,
+                 KH=8, KW=8, stride=4, mode=2, Co=Co, Kc=Kc, ldd=Co, rows_per_split=rows, Mred=Mred)
+    _lib.check(lib.apex_conv_wgrad(d, dw_out.data_ptr(), db_out.data_ptr(), nsplit, float(scale),
+                                   _lib.stream_ptr()), "conv1_wgrad")
+
+
+def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor) -> None:
+    """dW[N,K] = dy[M,N]^T @ x[M,K] (fp32, written directly), db = sum_m dy."""
+    M, Nc = dy.shape
+    K = x.shape[1]
+    d = _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=dw_out.data_ptr(), bias_slab=db_out.data_ptr(),
+                 mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M)
+    _lib.check(lib.apex_conv_wgrad(d, None, None, 1, 1.0, _lib.stream_ptr()), "dense_wgrad")
+
+
+def pack_dgrad_weights(lib, wfc, w3, w2, wfcT, w3tf, w2t) -> None:
+    _lib.check(lib.apex_pack_dgrad_weights(wfc.data_ptr(), w3.data_ptr(), w2.data_ptr(), wfcT.data_ptr(),
+                                           w3tf.data_ptr(), w2t.data_ptr(), _lib.stream_ptr()), "pack")

@@ -10,12 +10,11 @@ c_f = ctypes.c_float
 
 
 def declare(lib: ctypes.CDLL) -> None:
-    from ._lib import ConvDesc
+    from ._lib import ConvDesc, WgradDesc
     sigs = {
         "apex_conv_fwd": ([ConvDesc, c_p], c_i),
-        "apex_conv_wgrad": ([ConvDesc, c_p, c_p, c_i, c_p], c_i),
-        "apex_gemm_bf16": ([c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p, c_i, c_f,
-                            c_p], c_i),
+        "apex_conv_wgrad": ([WgradDesc, c_p, c_p, c_i, c_f, c_p], c_i),
+        "apex_pack_dgrad_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(lib, name, None)

@@ -14,6 +14,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _lib
+from . import conv as C
 from . import reference as R
 
 
@@ -24,8 +25,17 @@ class TorchBackend:
         self.dtype = dtype
 
     # ------------------------------------------------------------- forward
+    def prepare(self, Pb) -> None:
+        """Per-step weight preparation (packed dgrad copies on the HIP path)."""
+
     def conv1_fwd(self, frames, w, b, scale, out):
         out.copy_(R.conv1_fwd(frames, w, b, scale, self.dtype))
+
+    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out):
+        """conv1 on frame stacks addressed by replay-ring slots (B, C)."""
+        frames = frames_buf[:slots.shape[0]]
+        frames.copy_(ring[slots.long()])
+        self.conv1_fwd(frames, w, b, scale, out)
 
     def conv_fwd(self, x, w, b, stride, out):
         out.copy_(R.conv_fwd(x, w, b, stride, self.dtype))
@@ -118,6 +128,9 @@ class TorchBackend:
         dw_out.copy_(dw)
         db_out.copy_(db)
 
+    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out):
+        self.conv1_wgrad(dy, frames_buf[:slots.shape[0]], scale, dw_out, db_out)
+
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out):
         norm = g32.double().pow(2).sum().sqrt().float()
@@ -149,6 +162,63 @@ class HipBackend(TorchBackend):
         self.lib = _lib.require_kernels()
         self.native_conv = native_conv and hasattr(self.lib, "apex_conv_fwd")
         self.kernels = ["replay", "head", "head_wgrad", "optimizer", "actor_head"]
+        if self.native_conv:
+            self.kernels += ["conv_fwd", "conv_dgrad", "conv_wgrad", "fc_fwd", "fc_bwd"]
+        self.ws = C.Workspace()
+        self._packed = None
+
+    # --------------------------------------------------- native conv family
+    def prepare(self, Pb) -> None:
+        if not self.native_conv:
+            return
+        if self._packed is None:
+            dev = Pb["wfc"].device
+            self._packed = dict(wfcT=torch.empty(3136, 1024, dtype=torch.bfloat16, device=dev),
+                                w3tf=torch.empty(64, 576, dtype=torch.bfloat16, device=dev),
+                                w2t=torch.empty(4, 64, 256, dtype=torch.bfloat16, device=dev))
+        k = self._packed
+        C.pack_dgrad_weights(self.lib, Pb["wfc"], Pb["w3"], Pb["w2"], k["wfcT"], k["w3tf"], k["w2t"])
+
+    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out):
+        if not self.native_conv:
+            return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out)
+        C.conv1_fwd_ring(self.lib, ring, slots, w, b, scale, out)
+
+    def conv_fwd(self, x, w, b, stride, out):
+        if not self.native_conv:
+            return super().conv_fwd(x, w, b, stride, out)
+        C.conv_fwd(self.lib, x, w, b, stride, out)
+
+    def fc_fwd(self, x, w, b, out):
+        if not self.native_conv:
+            return super().fc_fwd(x, w, b, out)
+        C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True)
+
+    def fc_bwd(self, dh, x, w, dx_out, dw_out, db_out):
+        if not self.native_conv:
+            return super().fc_bwd(dh, x, w, dx_out, dw_out, db_out)
+        xf = x.reshape(x.shape[0], -1)
+        C.dense_fwd(self.lib, dh, self._packed["wfcT"], None, dx_out.reshape(dh.shape[0], -1), relu=False,
+                    mask=xf)
+        C.dense_wgrad(self.lib, dh, xf, dw_out, db_out)
+
+    def conv_dgrad(self, dy, w, stride, x_src, dx_out):
+        if not self.native_conv:
+            return super().conv_dgrad(dy, w, stride, x_src, dx_out)
+        if stride == 1:
+            C.conv3_dgrad(self.lib, dy, self._packed["w3tf"], x_src, dx_out)
+        else:
+            C.conv2_dgrad(self.lib, dy, self._packed["w2t"], x_src, dx_out)
+
+    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out):
+        if not self.native_conv:
+            return super().conv_wgrad(dy, x, k, stride, dw_out, db_out)
+        C.conv_wgrad(self.lib, self.ws, dy, x, k, stride, dw_out, db_out)
+
+    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out):
+        if not self.native_conv:
+            return super().conv1_wgrad_ring(dy, ring, slots, frames_buf, scale, dw_out, db_out)
+        C.conv1_wgrad_ring(self.lib, self.ws, dy, ring, slots, scale, dw_out, db_out)
 
     @staticmethod
     def _hp(P):

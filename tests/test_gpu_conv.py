@@ -1,0 +1,173 @@
+"""MFMA implicit-GEMM kernels (csrc/conv_mfma.hip) vs plain PyTorch fp32
+references of the same ops, on bf16-rounded inputs."""
+import pytest
+import torch
+
+from apex_dqn_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _lib():
+    from apex_dqn_amd.ops import _lib as L
+    return L.require_kernels()
+
+
+def _bf(x):
+    return x.to(DEV, torch.bfloat16)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+def _maxrel(a, b):
+    return float((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("N", [3, 64])
+def test_conv1_fwd_from_ring(N):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(0)
+    ring = torch.randint(0, 256, (50, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    slots = torch.randint(0, 50, (N, 4), generator=g, dtype=torch.int32).to(DEV)
+    w = _bf(torch.randn(64, 4, 8, 8, generator=g) * 0.05)
+    b = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    out = torch.empty(N, 20, 20, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv1_fwd_ring(_lib(), ring, slots, w, b, 1 / 255.0, out)
+    frames = ring[slots.long()]
+    ref = R.conv1_fwd(frames, w.float(), b, 1 / 255.0)
+    assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,layer", [(5, 2), (64, 2), (7, 3), (64, 3)])
+def test_conv_fwd_nhwc(N, layer):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(layer * 100 + N)
+    if layer == 2:
+        x = _bf(torch.relu(torch.randn(N, 20, 20, 64, generator=g)))
+        w = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+        stride, oh = 2, 9
+    else:
+        x = _bf(torch.relu(torch.randn(N, 9, 9, 64, generator=g)))
+        w = _bf(torch.randn(64, 3, 3, 64, generator=g) * 0.04)
+        stride, oh = 1, 7
+    b = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    out = torch.empty(N, oh, oh, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv_fwd(_lib(), x, w, b, stride, out)
+    ref = R.conv_fwd(x.float(), w.float(), b, stride)
+    assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M", [64, 200, 1024])
+def test_dense_fwd_relu_and_mask(M):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(M)
+    x = _bf(torch.relu(torch.randn(M, 3136, generator=g)))
+    w = _bf(torch.randn(1024, 3136, generator=g) * 0.02)
+    b = (torch.randn(1024, generator=g) * 0.1).to(DEV)
+    out = torch.empty(M, 1024, dtype=torch.bfloat16, device=DEV)
+    C.dense_fwd(_lib(), x, w, b, out, relu=True)
+    ref = R.fc_fwd(x.float(), w.float(), b)
+    assert _rel(out, ref) < 1e-2
+    # masked (fc dgrad form): out = (dh @ WfcT^T) * (mask > 0)
+    dh = _bf(torch.randn(M, 1024, generator=g) * 0.01)
+    wT = _bf(torch.randn(3136, 1024, generator=g) * 0.02)
+    mask = _bf(torch.randn(M, 3136, generator=g))
+    out2 = torch.empty(M, 3136, dtype=torch.bfloat16, device=DEV)
+    C.dense_fwd(_lib(), dh, wT, None, out2, relu=False, mask=mask)
+    ref2 = (dh.float() @ wT.float().t()) * (mask.float() > 0)
+    assert _rel(out2, ref2) < 1e-2
+
+
+def test_pack_dgrad_weights():
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(3)
+    wfc = _bf(torch.randn(1024, 3136, generator=g))
+    w3 = _bf(torch.randn(64, 3, 3, 64, generator=g))
+    w2 = _bf(torch.randn(64, 4, 4, 64, generator=g))
+    wfcT = torch.empty(3136, 1024, dtype=torch.bfloat16, device=DEV)
+    w3tf = torch.empty(64, 576, dtype=torch.bfloat16, device=DEV)
+    w2t = torch.empty(4, 64, 256, dtype=torch.bfloat16, device=DEV)
+    C.pack_dgrad_weights(_lib(), wfc, w3, w2, wfcT, w3tf, w2t)
+    assert torch.equal(wfcT, wfc.t())
+    ref3 = w3.flip(1, 2).permute(3, 1, 2, 0).reshape(64, 576)
+    assert torch.equal(w3tf, ref3)
+    for cls in range(4):
+        p, q = cls >> 1, cls & 1
+        sub = w2[:, p::2, q::2, :].flip(1, 2)  # [co][a'][b'][ci] with a' = 1 - a
+        assert torch.equal(w2t[cls], sub.permute(3, 1, 2, 0).reshape(64, 256))
+
+
+@pytest.mark.parametrize("N", [3, 64])
+def test_conv_dgrad_layers(N):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N + 7)
+    lib = _lib()
+    w3 = _bf(torch.randn(64, 3, 3, 64, generator=g) * 0.04)
+    w2 = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+    wfc = _bf(torch.randn(1024, 3136, generator=g) * 0.02)
+    wfcT = torch.empty(3136, 1024, dtype=torch.bfloat16, device=DEV)
+    w3tf = torch.empty(64, 576, dtype=torch.bfloat16, device=DEV)
+    w2t = torch.empty(4, 64, 256, dtype=torch.bfloat16, device=DEV)
+    C.pack_dgrad_weights(lib, wfc, w3, w2, wfcT, w3tf, w2t)
+    # conv3 dgrad: dY3 (7x7) -> dX2 (9x9) masked by y2
+    dy3 = _bf(torch.randn(N, 7, 7, 64, generator=g))
+    y2 = _bf(torch.randn(N, 9, 9, 64, generator=g))
+    out = torch.empty(N, 9, 9, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv3_dgrad(lib, dy3, w3tf, y2, out)
+    ref = R.conv_dgrad(dy3.float(), w3.float(), (N, 9, 9, 64), 1, y2.float())
+    assert _rel(out, ref) < 1e-2
+    # conv2 dgrad: dY2 (9x9) -> dX1 (20x20), stride 2, masked by y1
+    dy2 = _bf(torch.randn(N, 9, 9, 64, generator=g))
+    y1 = _bf(torch.randn(N, 20, 20, 64, generator=g))
+    out1 = torch.empty(N, 20, 20, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv2_dgrad(lib, dy2, w2t, y1, out1)
+    ref1 = R.conv_dgrad(dy2.float(), w2.float(), (N, 20, 20, 64), 2, y1.float())
+    assert _rel(out1, ref1) < 1e-2
+
+
+@pytest.mark.parametrize("N", [3, 64])
+def test_conv_wgrad_layers(N):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N + 11)
+    lib = _lib()
+    ws = C.Workspace()
+    for KH, stride, hin, hout in ((3, 1, 9, 7), (4, 2, 20, 9)):
+        dy = _bf(torch.randn(N, hout, hout, 64, generator=g))
+        x = _bf(torch.relu(torch.randn(N, hin, hin, 64, generator=g)))
+        dw = torch.empty(64, KH, KH, 64, device=DEV)
+        db = torch.empty(64, device=DEV)
+        C.conv_wgrad(lib, ws, dy, x, KH, stride, dw, db, target_rows=256)
+        rdw, rdb = R.conv_wgrad(dy.float(), x.float(), KH, stride)
+        assert _rel(dw, rdw) < 5e-3, (KH, _rel(dw, rdw))
+        assert _rel(db, rdb) < 1e-4
+
+
+@pytest.mark.parametrize("N", [3, 32])
+def test_conv1_wgrad_from_ring(N):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N + 5)
+    ring = torch.randint(0, 256, (40, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    slots = torch.randint(0, 40, (N, 4), generator=g, dtype=torch.int32).to(DEV)
+    dy = _bf(torch.randn(N, 20, 20, 64, generator=g))
+    dw = torch.empty(64, 4, 8, 8, device=DEV)
+    db = torch.empty(64, device=DEV)
+    C.conv1_wgrad_ring(_lib(), C.Workspace(), dy, ring, slots, 1 / 255.0, dw, db, target_rows=800)
+    rdw, rdb = R.conv1_wgrad(dy.float(), ring[slots.long()], 1 / 255.0)
+    assert _rel(dw, rdw) < 5e-3
+    assert _rel(db, rdb) < 1e-4
+
+
+@pytest.mark.parametrize("M", [64, 512])
+def test_dense_wgrad(M):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(M + 1)
+    dh = _bf(torch.randn(M, 1024, generator=g))
+    x = _bf(torch.relu(torch.randn(M, 3136, generator=g)))
+    dw = torch.empty(1024, 3136, device=DEV)
+    db = torch.empty(1024, device=DEV)
+    C.dense_wgrad(_lib(), dh, x, dw, db)
+    assert _rel(dw, dh.float().t() @ x.float()) < 5e-3
+    assert _rel(db, dh.float().sum(0)) < 1e-4
