@@ -42,6 +42,10 @@ struct ConvDesc {
   int K;
   float in_scale;
   int64_t w_cls_stride;
+  const bf16_t* w2;           // weights for output rows >= m_switch (target network), or null
+  const float* bias2;
+  int m_switch;               // multiple of FWD_BM
+  int pad_;
 };
 
 struct WgradDesc {
@@ -98,6 +102,10 @@ __device__ __forceinline__ uint32_t mask_bf16x2(uint32_t v, uint32_t m) {
 #define FWD_BN 64
 #define FWD_STAGE (FWD_BM * 128 + FWD_BN * 128)  // bytes per LDS buffer
 
+struct FwdRegs {
+  uint4 a0, a1, a2, a3, b0, b1;
+};
+
 template <int MODE>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * FWD_STAGE];
@@ -107,7 +115,10 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const int M = d.N * OHW;
   const int m0 = blockIdx.x * FWD_BM;
   const int n0 = blockIdx.y * FWD_BN;
-  const bf16_t* __restrict__ wb = d.w + (int64_t)cls * d.w_cls_stride;
+  // online / target weight sets in one launch: the switch row is block-uniform
+  const bool second = d.w2 != nullptr && m0 >= d.m_switch;
+  const bf16_t* __restrict__ wb = (second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride;
+  const float* __restrict__ bias = second ? d.bias2 : d.bias;
   const int KT = d.K >> 6;
   const int sc = tid & 7;
   const int srow = tid >> 3;
@@ -115,7 +126,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   // per-thread staging rows (4 A rows, 2 B rows)
   bool a_ok[4];
   int a_img[4], a_ih[4], a_iw[4];
-  const uint8_t* a_base[4];
+  int a_slot[4][4];  // MODE 2: frame-ring slots of the row's image (C <= 4), read once up front
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + srow + 32 * i;
@@ -126,21 +137,24 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     a_img[i] = img;
     a_ih[i] = oh * d.stride - d.pad_h;
     a_iw[i] = ow * d.stride - d.pad_w;
-    if (MODE == 0) a_base[i] = (const uint8_t*)d.x + ((int64_t)mm * d.K) * 2;
-    else a_base[i] = nullptr;
+    if (MODE == 2) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a_slot[i][c] = (c < d.Cin) ? d.frame_slots[img * d.Cin + c] : 0;
+    }
   }
-  uint4 ra[4], rb0, rb1;
   const bf16_t* wrow0 = wb + (int64_t)(n0 + srow) * d.K + sc * 8;
   const bf16_t* wrow1 = wrow0 + (int64_t)32 * d.K;
 
-  auto load_tile = [&](int kt) {
-    rb0 = *reinterpret_cast<const uint4*>(wrow0 + (kt << 6));
-    rb1 = *reinterpret_cast<const uint4*>(wrow1 + (kt << 6));
+  auto load_tile = [&](int kt, FwdRegs& R) {
+    R.b0 = *reinterpret_cast<const uint4*>(wrow0 + (kt << 6));
+    R.b1 = *reinterpret_cast<const uint4*>(wrow1 + (kt << 6));
+    uint4 ra[4];
     if (MODE == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        ra[i] = a_ok[i] ? *reinterpret_cast<const uint4*>(a_base[i] + ((kt << 6) + sc * 8) * 2)
-                        : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        const bf16_t* src = (const bf16_t*)d.x + (int64_t)(m0 + srow + 32 * i) * d.K + (kt << 6) + sc * 8;
+        ra[i] = a_ok[i] ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+      }
     } else if (MODE == 1) {
       const int cpb = d.Cin >> 6;
       const int tap = kt / cpb, cb = kt - tap * cpb;
@@ -154,34 +168,31 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
         ra[i] = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
       }
     } else {  // MODE 2: uint8 frames, K ordered (c, kh, kw), one frame per k-tile, chunk = kh
-      const int c = kt;
       const int64_t fbytes = (int64_t)d.H * d.W;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (a_ok[i]) {
-          const int slot = d.frame_slots[a_img[i] * d.Cin + c];
-          const uint8_t* p = (const uint8_t*)d.x + slot * fbytes + (int64_t)(a_ih[i] + sc) * d.W + a_iw[i];
-          ra[i].x = *reinterpret_cast<const uint32_t*>(p);
-          ra[i].y = *reinterpret_cast<const uint32_t*>(p + 4);
-        } else {
-          ra[i].x = 0;
-          ra[i].y = 0;
-        }
+        const int slot = kt == 0 ? a_slot[i][0] : kt == 1 ? a_slot[i][1] : kt == 2 ? a_slot[i][2] : a_slot[i][3];
+        const uint8_t* p = (const uint8_t*)d.x + slot * fbytes + (int64_t)(a_ih[i] + sc) * d.W + a_iw[i];
+        ra[i].x = a_ok[i] ? *reinterpret_cast<const uint32_t*>(p) : 0u;
+        ra[i].y = a_ok[i] ? *reinterpret_cast<const uint32_t*>(p + 4) : 0u;
+        ra[i].z = ra[i].w = 0;
       }
     }
+    R.a0 = ra[0]; R.a1 = ra[1]; R.a2 = ra[2]; R.a3 = ra[3];
   };
 
-  auto write_tile = [&](int buf) {
+  auto write_tile = [&](int buf, const FwdRegs& R) {
     uint8_t* As = smem + buf * FWD_STAGE;
     uint8_t* Bs = As + FWD_BM * 128;
+    const uint4 ra[4] = {R.a0, R.a1, R.a2, R.a3};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = srow + 32 * i;
       uint4 v = (MODE == 2) ? u8x8_to_bf16x8(ra[i].x, ra[i].y) : ra[i];
       *reinterpret_cast<uint4*>(As + swz_row(r, sc)) = v;
     }
-    *reinterpret_cast<uint4*>(Bs + swz_row(srow, sc)) = rb0;
-    *reinterpret_cast<uint4*>(Bs + swz_row(srow + 32, sc)) = rb1;
+    *reinterpret_cast<uint4*>(Bs + swz_row(srow, sc)) = R.b0;
+    *reinterpret_cast<uint4*>(Bs + swz_row(srow + 32, sc)) = R.b1;
   };
 
   f32x4 acc[2][4];
@@ -190,13 +201,8 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  load_tile(0);
-  write_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load_tile(kt + 1);
-    const uint8_t* As = smem + cur * FWD_STAGE;
+  auto compute = [&](int buf) {
+    const uint8_t* As = smem + buf * FWD_STAGE;
     const uint8_t* Bs = As + FWD_BM * 128;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -214,8 +220,29 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
         for (int nt = 0; nt < 4; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
     }
-    if (kt + 1 < KT) write_tile(cur ^ 1);
+  };
+
+  // Software pipeline: two register stages + two LDS stages.  Tile t's global
+  // loads are issued two iterations before its MFMAs (prefetch distance 2), so
+  // an L2/Infinity-Cache hit is covered by ~2 k-tiles of MFMA work.
+  FwdRegs RA, RB;
+  load_tile(0, RA);
+  if (KT > 1) load_tile(1, RB);
+  write_tile(0, RA);
+  __syncthreads();
+  if (KT > 2) load_tile(2, RA);
+  for (int kt = 0; kt < KT; kt += 2) {
+    // even tile kt (LDS buf 0); its successor kt+1 sits in RB
+    compute(0);
+    if (kt + 1 < KT) write_tile(1, RB);
     __syncthreads();
+    if (kt + 3 < KT) load_tile(kt + 3, RB);
+    if (kt + 1 >= KT) break;
+    // odd tile kt+1 (LDS buf 1); its successor kt+2 sits in RA
+    compute(1);
+    if (kt + 2 < KT) write_tile(0, RA);
+    __syncthreads();
+    if (kt + 4 < KT) load_tile(kt + 4, RA);
   }
 
   // ---- epilogue: scale + bias -> bf16 in LDS (per-wave 32x64 image), then
@@ -226,7 +253,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int col = 16 * nt + (lane & 15);
-      const float bv = d.bias ? d.bias[n0 + col] : 0.f;
+      const float bv = bias ? bias[n0 + col] : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = 16 * mt + 4 * (lane >> 4) + j;
@@ -433,27 +460,40 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
   }
 }
 
-// sum fp32 slabs over splits -> fp32 gradient (scaled), and the bias partials
-__global__ void slab_reduce_kernel(const float* __restrict__ slab, int nsplit, int64_t n, float scale,
-                                   float* __restrict__ out, const float* __restrict__ bslab, int nb,
-                                   float* __restrict__ bout) {
-  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i4 * 4 < n) {
-    float4 s = make_float4(0, 0, 0, 0);
-    for (int k = 0; k < nsplit; ++k) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)k * n + i4 * 4);
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
+// sum fp32 slabs over splits -> fp32 gradient (scaled), and the bias partials.
+// Block = 64 float4 columns x 16 split-groups (1024 threads): each thread sums
+// every 16th split, then an LDS tree finishes -- 16x more loads in flight than
+// a thread-per-column loop over all splits.
+__global__ void __launch_bounds__(1024) slab_reduce_kernel(const float* __restrict__ slab, int nsplit, int64_t n,
+                                                           float scale, float* __restrict__ out,
+                                                           const float* __restrict__ bslab, int nb,
+                                                           float* __restrict__ bout) {
+  __shared__ float4 red[16][64];
+  const int lc = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t c4 = (int64_t)blockIdx.x * 64 + lc;
+  float4 s = make_float4(0, 0, 0, 0);
+  if (c4 * 4 < n) {
+    for (int k = grp; k < nsplit; k += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)k * n + c4 * 4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
-    *reinterpret_cast<float4*>(out + i4 * 4) = s;
   }
-  if (bslab != nullptr && i4 < nb) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += bslab[(int64_t)k * nb + i4];
-    bout[i4] = s;
+  red[grp][lc] = s;
+  __syncthreads();
+  if (grp == 0 && c4 * 4 < n) {
+    float4 a = red[0][lc];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) {
+      const float4 b = red[g][lc];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    a.x *= scale; a.y *= scale; a.z *= scale; a.w *= scale;
+    *reinterpret_cast<float4*>(out + c4 * 4) = a;
+  }
+  if (bslab != nullptr && blockIdx.x == 0 && threadIdx.x < nb) {
+    float b = 0.f;
+    for (int k = 0; k < nsplit; ++k) b += bslab[(int64_t)k * nb + threadIdx.x];
+    bout[threadIdx.x] = b;
   }
 }
 
@@ -499,7 +539,8 @@ __global__ void pack_conv_dgrad_weights_kernel(const bf16_t* __restrict__ w3, co
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if ((d.K & 63) || (d.Cout & 63) || d.K <= 0) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
-  if (d.mode == 2 && (d.KH != 8 || d.KW != 8 || d.K != d.Cin * 64)) return (int)hipErrorInvalidValue;
+  if (d.mode == 2 && (d.KH != 8 || d.KW != 8 || d.K != d.Cin * 64 || d.Cin > 4)) return (int)hipErrorInvalidValue;
+  if (d.w2 != nullptr && (d.m_switch % FWD_BM)) return (int)hipErrorInvalidValue;
   const int M = d.N * d.OH * d.OW;
   dim3 grid((M + FWD_BM - 1) / FWD_BM, d.Cout / FWD_BN, d.ncls > 0 ? d.ncls : 1);
   if (d.mode == 0) igemm_fwd_kernel<0><<<grid, 256, 0, st>>>(d);
@@ -519,9 +560,9 @@ APEX_EXPORT int apex_conv_wgrad(WgradDesc d, float* out, float* bout, int nsplit
   if (e != hipSuccess) return (int)e;
   if (out != nullptr) {
     const int64_t n = (int64_t)d.Co * d.Kc;
-    const int64_t nthreads = (n / 4 > d.Co ? n / 4 : d.Co);
-    slab_reduce_kernel<<<(int)((nthreads + 255) / 256), 256, 0, st>>>(d.slab, nsplit, n, scale, out,
-                                                                       d.bias_slab, d.bias_slab ? d.Co : 0, bout);
+    if (d.bias_slab != nullptr && d.Co > 1024) return (int)hipErrorInvalidValue;
+    slab_reduce_kernel<<<(int)((n / 4 + 63) / 64), 1024, 0, st>>>(d.slab, nsplit, n, scale, out, d.bias_slab,
+                                                                  d.bias_slab ? d.Co : 0, bout);
   }
   APEX_CHECK_LAUNCH();
 }

@@ -166,7 +166,7 @@ __global__ void __launch_bounds__(256) ddqn_head_kernel(
 }
 
 // head weight/bias gradients: dW[j][k] += sum_b dhead[b][j] * h[b][stream(j)][k]
-// grid: (A+1) rows x 2 column halves x batch slices of 64; fp32 atomics into a
+// grid: (A+1) rows x 2 column halves x batch slices of 16; fp32 atomics into a
 // region zeroed by ddqn_head_kernel.  Output layout = flat param layout:
 //   gwv[512] gbv[1] gwa[A*512] gba[A]
 __global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restrict__ Hon,
@@ -175,8 +175,8 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restric
                                                          float* __restrict__ gwa, float* __restrict__ gba) {
   const int j = blockIdx.x;            // 0 = value, 1..A = advantage j-1
   const int k = blockIdx.y * 256 + threadIdx.x;  // 0..511
-  const int b0 = blockIdx.z * 64;
-  const int b1 = min(B, b0 + 64);
+  const int b0 = blockIdx.z * 16;
+  const int b1 = min(B, b0 + 16);
   const int col = (j == 0 ? 0 : 512) + k;
   float acc = 0.f, accb = 0.f;
   for (int b = b0; b < b1; ++b) {
@@ -208,7 +208,7 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
 
 APEX_EXPORT int apex_head_wgrad(const bf16_t* Hon, const float* dhead, int B, int A, float* gwv, float* gbv,
                                 float* gwa, float* gba, hipStream_t st) {
-  dim3 grid(A + 1, 2, (B + 63) / 64);
+  dim3 grid(A + 1, 2, (B + 15) / 16);
   head_wgrad_kernel<<<grid, 256, 0, st>>>(Hon, dhead, B, A, gwv, gbv, gwa, gba);
   APEX_CHECK_LAUNCH();
 }

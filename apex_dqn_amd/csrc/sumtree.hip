@@ -34,68 +34,109 @@ struct RecordDesc {
   int64_t cap;
 };
 
-// Write leaf values and propagate the deltas up the tree.  Must be called by
-// every lane of the wave (uniform control flow): lanes whose deltas target the
-// same node are summed with a wave reduction first, so a level receives one
-// fp64 atomic per distinct node per wave -- the root gets one per wave instead
-// of one per updated leaf (the contention that dominated a naive version).
-__device__ __forceinline__ void tree_write_and_propagate(const TreeDesc& t, bool act, int64_t i, float v) {
-  const int lane = threadIdx.x & 63;
+// Write leaf values and propagate the deltas up the tree, block-cooperatively
+// (every thread of the block must call; contains __syncthreads):
+//  * levels with many nodes (k < kfirst): one fp64 global atomic per updated
+//    leaf -- random leaves rarely share a parent there;
+//  * the small top levels (k >= kfirst, <= TREE_LACC nodes in total): deltas are
+//    summed in LDS with ds_add_f64 first, then each touched node gets ONE global
+//    atomic per block -- the root sees #blocks atomics instead of #leaves.
+// The running min of positive leaves is reduced the same way.
+#define TREE_LACC 4096
+
+__device__ __forceinline__ void tree_block_update(const TreeDesc& t, bool act, int64_t i, float v,
+                                                  double* lacc, uint32_t* lmin, int kfirst) {
   double d = 0.0;
   if (act) {
     const float old = t.leaf[i];
     t.leaf[i] = v;
     d = (double)v - (double)old;
   }
-  int64_t node = act ? i : 0;
-  uint64_t live = __ballot(act && d != 0.0);
-  for (int k = 1; k <= t.L && live; ++k) {
-    node >>= 6;
-    uint64_t pending = live;
-    while (pending) {
-      const int leader = __ffsll((unsigned long long)pending) - 1;
-      const int64_t ln = __shfl(node, leader, 64);
-      const bool mine = ((pending >> lane) & 1ull) && node == ln;
-      const double s = wave_sum(mine ? d : 0.0);
-      if (lane == leader) atomicAdd(&t.nodes[t.off[k] + ln], s);
-      pending &= ~__ballot(mine);
+  int nsmall = 0;
+  for (int k = kfirst; k <= t.L; ++k) nsmall += (int)t.n[k];
+  for (int j = threadIdx.x; j < nsmall; j += blockDim.x) lacc[j] = 0.0;
+  if (threadIdx.x == 0) *lmin = 0x7f800000u;
+  __syncthreads();
+  if (act && d != 0.0) {
+    int64_t node = i;
+    int loff = 0;
+    for (int k = 1; k <= t.L; ++k) {
+      node >>= 6;
+      if (k < kfirst) {
+        atomicAdd(&t.nodes[t.off[k] + node], d);
+      } else {
+        atomicAdd(&lacc[loff + node], d);
+        loff += (int)t.n[k];
+      }
     }
   }
-  // running min over positive leaves: one atomic per wave
-  float mv = (act && v > 0.f) ? v : __uint_as_float(0x7f800000u);
-  mv = wave_min(mv);
-  if (lane == 0 && mv < __uint_as_float(0x7f800000u)) atomicMin(t.min_bits, __float_as_uint(mv));
+  if (act && v > 0.f) atomicMin(lmin, __float_as_uint(v));
+  __syncthreads();
+  int loff = 0;
+  for (int k = kfirst; k <= t.L; ++k) {
+    for (int j = threadIdx.x; j < t.n[k]; j += blockDim.x) {
+      const double a = lacc[loff + j];
+      if (a != 0.0) atomicAdd(&t.nodes[t.off[k] + j], a);
+    }
+    loff += (int)t.n[k];
+  }
+  if (threadIdx.x == 0 && *lmin != 0x7f800000u) atomicMin(t.min_bits, *lmin);
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
 }
 
 // mode 0: values are leaf values; mode 1: values are |td| -> (|td|+eps)^alpha,
 // skipping evicted leaves (leaf == 0) and slots re-used since sampling (gen).
-// Launched with whole waves; out-of-range threads take part as inactive lanes.
-__global__ void tree_update_kernel(TreeDesc t, const int64_t* __restrict__ idx,
-                                   const float* __restrict__ values, int n, int mode,
-                                   float alpha, float eps, const int32_t* __restrict__ gen_expect,
-                                   const int32_t* __restrict__ gen, int dedupe,
-                                   uint64_t* ctr_to_bump) {
-  __shared__ int64_t sidx[1024];
+// dedupe (single block, n <= 1024): last occurrence of an index wins, found with
+// an LDS hash table (atomicCAS insert + atomicMax of the position).
+__global__ void __launch_bounds__(1024) tree_update_kernel(TreeDesc t, const int64_t* __restrict__ idx,
+                                                           const float* __restrict__ values, int n, int mode,
+                                                           float alpha, float eps,
+                                                           const int32_t* __restrict__ gen_expect,
+                                                           const int32_t* __restrict__ gen, int dedupe,
+                                                           uint64_t* ctr_to_bump, int kfirst) {
+  __shared__ uint32_t hkey[2048];
+  __shared__ int32_t hval[2048];
+  __shared__ double lacc[TREE_LACC];
+  __shared__ uint32_t lmin;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (ctr_to_bump != nullptr && i == 0) ctr_to_bump[0] += 1;
-  const bool use_lds = dedupe && n <= 1024;
-  if (use_lds) {
-    for (int j = threadIdx.x; j < n; j += blockDim.x) sidx[j] = idx[j];
-    __syncthreads();
-  }
   bool act = i < n;
   int64_t s = 0;
-  float v = 0.f;
   if (act) {
     s = idx[i];
     act = s >= 0 && s < t.n[0];
   }
-  if (act && dedupe) {
-    for (int j = i + 1; j < n; ++j) {
-      const int64_t o = use_lds ? sidx[j] : idx[j];
-      if (o == s) { act = false; break; }  // a later write to the same leaf wins
+  if (dedupe) {  // host guarantees gridDim.x == 1 and n <= 1024
+    for (int j = threadIdx.x; j < 2048; j += blockDim.x) {
+      hkey[j] = 0u;
+      hval[j] = -1;
     }
+    __syncthreads();
+    int h = 0;
+    const uint32_t key = (uint32_t)s + 1u;
+    if (act) {
+      h = (int)(hash32(key) & 2047u);
+      while (true) {
+        const uint32_t old = atomicCAS(&hkey[h], 0u, key);
+        if (old == 0u || old == key) {
+          atomicMax(&hval[h], i);
+          break;
+        }
+        h = (h + 1) & 2047;
+      }
+    }
+    __syncthreads();
+    if (act && hval[h] != i) act = false;  // a later write to the same leaf wins
   }
+  float v = 0.f;
   if (act) {
     v = values[i];
     if (mode == 1) {
@@ -104,27 +145,33 @@ __global__ void tree_update_kernel(TreeDesc t, const int64_t* __restrict__ idx,
       v = powf(fabsf(v) + eps, alpha);
     }
   }
-  tree_write_and_propagate(t, act, s, v);
+  tree_block_update(t, act, s, v, lacc, &lmin, kfirst);
 }
 
 // zero `count` leaves starting at ring slot `start` (FIFO eviction)
-__global__ void tree_zero_range_kernel(TreeDesc t, int64_t start, int64_t count) {
+__global__ void __launch_bounds__(256) tree_zero_range_kernel(TreeDesc t, int64_t start, int64_t count,
+                                                              int kfirst) {
+  __shared__ double lacc[TREE_LACC];
+  __shared__ uint32_t lmin;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool act = i < count;
   const int64_t s = act ? (start + i) % t.n[0] : 0;
   if (act && t.leaf[s] == 0.f) act = false;
-  tree_write_and_propagate(t, act, s, 0.f);
+  tree_block_update(t, act, s, 0.f, lacc, &lmin, kfirst);
 }
 
 // scatter K staged records into ring slots start..start+K-1 (mod cap) and set
 // their leaves to (prio+eps)^alpha
-__global__ void replay_insert_kernel(TreeDesc t, RecordDesc r, int64_t start, int K,
-                                     const int32_t* __restrict__ s_obs,
-                                     const int32_t* __restrict__ s_nxt,
-                                     const int32_t* __restrict__ s_act,
-                                     const float* __restrict__ s_rew,
-                                     const float* __restrict__ s_gam,
-                                     const float* __restrict__ s_prio, float alpha, float eps) {
+__global__ void __launch_bounds__(256) replay_insert_kernel(TreeDesc t, RecordDesc r, int64_t start, int K,
+                                                            const int32_t* __restrict__ s_obs,
+                                                            const int32_t* __restrict__ s_nxt,
+                                                            const int32_t* __restrict__ s_act,
+                                                            const float* __restrict__ s_rew,
+                                                            const float* __restrict__ s_gam,
+                                                            const float* __restrict__ s_prio, float alpha,
+                                                            float eps, int kfirst) {
+  __shared__ double lacc[TREE_LACC];
+  __shared__ uint32_t lmin;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < K;
   const int64_t s = act ? (start + i) % r.cap : 0;
@@ -140,7 +187,18 @@ __global__ void replay_insert_kernel(TreeDesc t, RecordDesc r, int64_t start, in
     r.gen[s] += 1;
     v = powf(fabsf(s_prio[i]) + eps, alpha);
   }
-  tree_write_and_propagate(t, act, s, v);
+  tree_block_update(t, act, s, v, lacc, &lmin, kfirst);
+}
+
+// first level whose node count, summed with all levels above it, fits TREE_LACC
+static int tree_kfirst(const TreeDesc& t) {
+  int k = t.L;
+  int64_t sum = t.n[t.L];
+  while (k > 1 && sum + t.n[k - 1] <= TREE_LACC) {
+    sum += t.n[k - 1];
+    --k;
+  }
+  return k;
 }
 
 // Stratified proportional sampling: one wave per sample, 64-ary descent.
@@ -153,7 +211,8 @@ __global__ void tree_sample_kernel(TreeDesc t, RecordDesc r, int B, uint64_t see
                                    int64_t* __restrict__ out_idx, float* __restrict__ out_w,
                                    int32_t* __restrict__ out_gen, int32_t* __restrict__ out_obs,
                                    int32_t* __restrict__ out_nxt, int32_t* __restrict__ out_act,
-                                   float* __restrict__ out_rew, float* __restrict__ out_gam) {
+                                   float* __restrict__ out_rew, float* __restrict__ out_gam,
+                                   int32_t* __restrict__ out_nxt2) {
   const int lane = threadIdx.x & 63;
   const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (b >= B) return;
@@ -193,7 +252,9 @@ __global__ void tree_sample_kernel(TreeDesc t, RecordDesc r, int B, uint64_t see
   }
   for (int c = lane; c < r.C; c += 64) {
     out_obs[(int64_t)b * r.C + c] = r.obs[s * r.C + c];
-    out_nxt[(int64_t)b * r.C + c] = r.nxt[s * r.C + c];
+    const int32_t nv = r.nxt[s * r.C + c];
+    out_nxt[(int64_t)b * r.C + c] = nv;
+    if (out_nxt2) out_nxt2[(int64_t)b * r.C + c] = nv;
   }
 }
 
@@ -248,15 +309,17 @@ APEX_EXPORT int apex_tree_update(TreeDesc t, const int64_t* idx, const float* va
                                  float alpha, float eps, const int32_t* gen_expect, const int32_t* gen,
                                  int dedupe, uint64_t* ctr_to_bump, hipStream_t st) {
   if (n <= 0 && ctr_to_bump == nullptr) return 0;
-  int nb = n > 0 ? blocks_for(n, 256) : 1;
-  tree_update_kernel<<<nb, 256, 0, st>>>(t, idx, values, n, mode, alpha, eps, gen_expect, gen, dedupe,
-                                         ctr_to_bump);
+  if (dedupe && n > 1024) return (int)hipErrorInvalidValue;
+  const int threads = n <= 1024 ? ((n + 63) / 64) * 64 : 1024;
+  const int nb = n > 0 ? blocks_for(n, threads) : 1;
+  tree_update_kernel<<<nb, threads > 0 ? threads : 64, 0, st>>>(t, idx, values, n, mode, alpha, eps, gen_expect,
+                                                               gen, dedupe, ctr_to_bump, tree_kfirst(t));
   APEX_CHECK_LAUNCH();
 }
 
 APEX_EXPORT int apex_tree_zero_range(TreeDesc t, int64_t start, int64_t count, hipStream_t st) {
   if (count <= 0) return 0;
-  tree_zero_range_kernel<<<blocks_for(count, 256), 256, 0, st>>>(t, start, count);
+  tree_zero_range_kernel<<<blocks_for(count, 256), 256, 0, st>>>(t, start, count, tree_kfirst(t));
   APEX_CHECK_LAUNCH();
 }
 
@@ -266,19 +329,19 @@ APEX_EXPORT int apex_replay_insert(TreeDesc t, RecordDesc r, int64_t start, int 
                                    hipStream_t st) {
   if (K <= 0) return 0;
   replay_insert_kernel<<<blocks_for(K, 256), 256, 0, st>>>(t, r, start, K, s_obs, s_nxt, s_act, s_rew,
-                                                           s_gam, s_prio, alpha, eps);
+                                                           s_gam, s_prio, alpha, eps, tree_kfirst(t));
   APEX_CHECK_LAUNCH();
 }
 
 APEX_EXPORT int apex_tree_sample(TreeDesc t, RecordDesc r, int B, uint64_t seed, const uint64_t* ctr,
                                  float beta, const float* ratio_min_global, int64_t* out_idx, float* out_w,
                                  int32_t* out_gen, int32_t* out_obs, int32_t* out_nxt, int32_t* out_act,
-                                 float* out_rew, float* out_gam, hipStream_t st) {
+                                 float* out_rew, float* out_gam, int32_t* out_nxt2, hipStream_t st) {
   if (B <= 0) return 0;
   const int waves_per_block = 4;
   tree_sample_kernel<<<blocks_for(B, waves_per_block), 64 * waves_per_block, 0, st>>>(
       t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
-      out_rew, out_gam);
+      out_rew, out_gam, out_nxt2);
   APEX_CHECK_LAUNCH();
 }
 

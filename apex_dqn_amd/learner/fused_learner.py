@@ -86,17 +86,19 @@ class FusedNatureLearner:
     def _alloc(self, B: int) -> None:
         d, ad = self.device, self.act_dtype
         C = self.C
+        # rows [0,B) = S_t, [B,2B) = S_{t+n} (online net), [2B,3B) = S_{t+n} (target net):
+        # every forward layer is ONE launch over 3B images with the weight set
+        # switched at row 2B (block-uniform)
         self.S = self.replay.alloc_sample_buffers(B)
-        self.slots = torch.zeros(2 * B, C, dtype=torch.int32, device=d)
-        self.frames = torch.zeros(2 * B, C, 84, 84, dtype=torch.uint8, device=d)
-        self.y1 = torch.zeros(2 * B, 20, 20, 64, dtype=ad, device=d)
-        self.y2 = torch.zeros(2 * B, 9, 9, 64, dtype=ad, device=d)
-        self.y3 = torch.zeros(2 * B, 7, 7, 64, dtype=ad, device=d)
-        self.h = torch.zeros(2 * B, 1024, dtype=ad, device=d)
-        self.y1t = torch.zeros(B, 20, 20, 64, dtype=ad, device=d)
-        self.y2t = torch.zeros(B, 9, 9, 64, dtype=ad, device=d)
-        self.y3t = torch.zeros(B, 7, 7, 64, dtype=ad, device=d)
-        self.ht = torch.zeros(B, 1024, dtype=ad, device=d)
+        self.slots = torch.zeros(3 * B, C, dtype=torch.int32, device=d)
+        self.S["obs"] = self.slots[:B]
+        self.S["nxt"] = self.slots[B:2 * B]
+        self.frames = torch.zeros(3 * B, C, 84, 84, dtype=torch.uint8, device=d) if self.ops.name != "hip" \
+            else torch.zeros(1, C, 84, 84, dtype=torch.uint8, device=d)
+        self.y1 = torch.zeros(3 * B, 20, 20, 64, dtype=ad, device=d)
+        self.y2 = torch.zeros(3 * B, 9, 9, 64, dtype=ad, device=d)
+        self.y3 = torch.zeros(3 * B, 7, 7, 64, dtype=ad, device=d)
+        self.h = torch.zeros(3 * B, 1024, dtype=ad, device=d)
         self.dH = torch.zeros(B, 1024, dtype=ad, device=d)
         self.dY3 = torch.zeros(B, 7, 7, 64, dtype=ad, device=d)
         self.dY2 = torch.zeros(B, 9, 9, 64, dtype=ad, device=d)
@@ -112,14 +114,17 @@ class FusedNatureLearner:
         self.g_head_region = self.g32[o0:o1]
 
     # ------------------------------------------------------------ forward
-    def forward_online(self, slots, rows: int, y1, y2, y3, h, Pb, Pf, frames_buf):
-        """Forward of ``rows`` frame stacks: bf16 weights ``Pb``, fp32 biases ``Pf``."""
-        ops, rt = self.ops, self.rt
-        ops.conv1_fwd_ring(self.replay.frames, slots[:rows], frames_buf, Pb["w1"], Pf["b1"], rt.obs_scale,
-                           y1[:rows])
-        ops.conv_fwd(y1[:rows], Pb["w2"], Pf["b2"], 2, y2[:rows])
-        ops.conv_fwd(y2[:rows], Pb["w3"], Pf["b3"], 1, y3[:rows])
-        ops.fc_fwd(y3[:rows].reshape(rows, 3136), Pb["wfc"], Pf["bfc"], h[:rows])
+    def forward_all(self) -> None:
+        """Online net on rows [0,2B), target net on rows [2B,3B): one launch per layer.
+        bf16 weights (Pb / Tb), fp32 biases (P / T)."""
+        ops, rt, B = self.ops, self.rt, self.B
+        Pb, P, Tb, T = self.Pb, self.P, self.Tb, self.T
+        n = 3 * B
+        ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
+                           Tb["w1"], T["b1"], 2 * B)
+        ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B)
+        ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B)
+        ops.fc_fwd(self.y3.reshape(n, 3136), Pb["wfc"], P["bfc"], self.h, Tb["wfc"], T["bfc"], 2 * B)
 
     def _head_params(self, V):
         return {k: V[k] for k in ("wv", "bv", "wa", "ba")}
@@ -128,16 +133,13 @@ class FusedNatureLearner:
     def _step_body(self, ratio_min: Optional[torch.Tensor] = None) -> None:
         B, rt, ops = self.B, self.rt, self.ops
         ops.prepare(self.Pb)
-        S = self.replay.sample(B, out=self.S, ratio_min_global=ratio_min)
-        self.slots[:B].copy_(S["obs"])
-        self.slots[B:].copy_(S["nxt"])
-        # online forward on [S_t ; S_tpn], target forward on S_tpn; conv1 reads the
-        # uint8 frame stacks straight from the replay ring by slot
-        self.forward_online(self.slots, 2 * B, self.y1, self.y2, self.y3, self.h, self.Pb, self.P, self.frames)
-        self.forward_online(self.slots[B:], B, self.y1t, self.y2t, self.y3t, self.ht, self.Tb, self.T,
-                            self.frames[B:])
+        # the sampler writes the frame-ring slots of S_t / S_{t+n} (twice) into self.slots
+        S = self.replay.sample(B, out=self.S, ratio_min_global=ratio_min, nxt2=self.slots[2 * B:])
+        # conv1 reads the uint8 frame stacks straight from the replay ring by slot
+        self.forward_all()
         isw = S["weights"] if rt.use_is_weights else None
-        ops.head(self.h, self.ht, self._head_params(self.P), self._head_params(self.T), S["act"], S["rew"],
+        ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
+                 S["rew"],
                  S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / B, self.td_abs, self.loss_b,
                  self.dH, self.dhead, zero=self.g_head_region)
         ops.head_wgrad(self.h, self.dhead, self.G)

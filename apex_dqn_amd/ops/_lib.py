@@ -49,7 +49,8 @@ class ConvDesc(ctypes.Structure):
                 ("KW", c_i), ("stride", c_i), ("pad_h", c_i), ("pad_w", c_i),
                 ("mode", c_i), ("relu", c_i), ("ldy", c_i), ("ncls", c_i),
                 ("ostride_h", c_i), ("ostride_w", c_i), ("OHfull", c_i), ("OWfull", c_i),
-                ("K", c_i), ("in_scale", c_f), ("w_cls_stride", c_i64)]
+                ("K", c_i), ("in_scale", c_f), ("w_cls_stride", c_i64),
+                ("w2", c_p), ("bias2", c_p), ("m_switch", c_i), ("pad_", c_i)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -69,7 +70,7 @@ _SIGS = {
     "apex_replay_insert": ([TreeDesc, RecordDesc, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p],
                            c_i),
     "apex_tree_sample": ([TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                          c_p, c_p, c_p], c_i),
+                          c_p, c_p, c_p, c_p], c_i),
     "apex_tree_rebuild": ([TreeDesc, c_p], c_i),
     "apex_gather_frames": ([c_p, c_p, c_i, c_i, c_i64, c_p, c_p], c_i),
     "apex_grad_sqnorm_partials": ([c_p, c_i64, c_p, c_p], c_i),

@@ -45,7 +45,20 @@ def _conv_desc(**kw) -> "_lib.ConvDesc":
     d.K = kw["K"]
     d.in_scale = float(kw.get("scale", 1.0))
     d.w_cls_stride = kw.get("w_cls_stride", 0)
+    d.w2 = kw.get("w2")
+    d.bias2 = kw.get("bias2")
+    d.m_switch = kw.get("m_switch", 0)
     return d
+
+
+def _second(w2, b2, rows_first, per_row):
+    """Descriptor fields for a second weight set on rows >= rows_first (images)."""
+    if w2 is None:
+        return {}
+    m_switch = rows_first * per_row
+    if m_switch % 128:
+        raise ValueError("online/target split must fall on a 128-row tile boundary")
+    return dict(w2=w2.data_ptr(), bias2=_lib.ptr(b2), m_switch=m_switch)
 
 
 def _launch_fwd(lib, d) -> None:
@@ -53,36 +66,40 @@ def _launch_fwd(lib, d) -> None:
 
 
 def conv1_fwd_ring(lib, ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor,
-                   scale: float, out: torch.Tensor) -> None:
-    """conv1 (8x8 s4, C stacked frames -> 64) reading uint8 frames from the replay ring."""
+                   scale: float, out: torch.Tensor, w2=None, b2=None, rows_first: int = 0) -> None:
+    """conv1 (8x8 s4, C stacked frames -> 64) reading uint8 frames from the replay ring.
+    Rows >= ``rows_first`` use the second weight set (target network) when given."""
     N, C = slots.shape
     H, W = ring.shape[1], ring.shape[2]
     assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
     d = _conv_desc(x=ring.data_ptr(), frame_slots=slots.data_ptr(), w=w1.data_ptr(), bias=b1.data_ptr(),
                    y=out.data_ptr(), N=N, H=H, W=W, Cin=C, OH=20, OW=20, Cout=64, KH=8, KW=8, stride=4,
-                   mode=2, relu=1, K=C * 64, scale=scale)
+                   mode=2, relu=1, K=C * 64, scale=scale, **_second(w2, b2, rows_first, 400))
     _launch_fwd(lib, d)
 
 
-def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int, out: torch.Tensor) -> None:
+def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int, out: torch.Tensor,
+             w2=None, b2=None, rows_first: int = 0) -> None:
     """NHWC conv + bias + ReLU with OHWI weights (conv2 / conv3)."""
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     OH, OW = out.shape[1], out.shape[2]
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=b.data_ptr(), y=out.data_ptr(), N=N, H=H, W=W,
                    Cin=Cin, OH=OH, OW=OW, Cout=Cout, KH=KH, KW=KW, stride=stride, mode=1, relu=1,
-                   K=KH * KW * Cin)
+                   K=KH * KW * Cin, **_second(w2, b2, rows_first, OH * OW))
     _launch_fwd(lib, d)
 
 
 def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
-              relu: bool = True, mask: Optional[torch.Tensor] = None) -> None:
+              relu: bool = True, mask: Optional[torch.Tensor] = None, w2=None, b2=None,
+              rows_first: int = 0) -> None:
     """out[M,N] = act(x[M,K] @ w[N,K]^T + b)  (or * (mask > 0))."""
     M, K = x.shape
     Nc = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, Nc)
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), mask=_lib.ptr(mask),
-                   N=M, Cin=K, Cout=Nc, mode=0, relu=relu and mask is None, K=K)
+                   N=M, Cin=K, Cout=Nc, mode=0, relu=relu and mask is None, K=K,
+                   **_second(w2, b2, rows_first, 1))
     _launch_fwd(lib, d)
 
 
@@ -140,7 +157,7 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
 
 
 def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
-                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1600) -> None:
+                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 3200) -> None:
     N, OH, OW, Co = dy.shape
     C = slots.shape[1]
     Kc = C * 64

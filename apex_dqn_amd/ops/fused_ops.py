@@ -31,17 +31,31 @@ class TorchBackend:
     def conv1_fwd(self, frames, w, b, scale, out):
         out.copy_(R.conv1_fwd(frames, w, b, scale, self.dtype))
 
-    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out):
-        """conv1 on frame stacks addressed by replay-ring slots (B, C)."""
+    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0):
+        """conv1 on frame stacks addressed by replay-ring slots (N, C); rows >=
+        ``rows_first`` use the second weight set (w2, b2) when given."""
         frames = frames_buf[:slots.shape[0]]
         frames.copy_(ring[slots.long()])
-        self.conv1_fwd(frames, w, b, scale, out)
+        if w2 is None:
+            self.conv1_fwd(frames, w, b, scale, out)
+        else:
+            self.conv1_fwd(frames[:rows_first], w, b, scale, out[:rows_first])
+            self.conv1_fwd(frames[rows_first:], w2, b2, scale, out[rows_first:])
 
-    def conv_fwd(self, x, w, b, stride, out):
-        out.copy_(R.conv_fwd(x, w, b, stride, self.dtype))
+    def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0):
+        if w2 is None:
+            out.copy_(R.conv_fwd(x, w, b, stride, self.dtype))
+        else:
+            out[:rows_first].copy_(R.conv_fwd(x[:rows_first], w, b, stride, self.dtype))
+            out[rows_first:].copy_(R.conv_fwd(x[rows_first:], w2, b2, stride, self.dtype))
 
-    def fc_fwd(self, x, w, b, out):
-        out.copy_(R.fc_fwd(x.reshape(x.shape[0], -1), w, b, self.dtype))
+    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0):
+        x = x.reshape(x.shape[0], -1)
+        if w2 is None:
+            out.copy_(R.fc_fwd(x, w, b, self.dtype))
+        else:
+            out[:rows_first].copy_(R.fc_fwd(x[:rows_first], w, b, self.dtype))
+            out[rows_first:].copy_(R.fc_fwd(x[rows_first:], w2, b2, self.dtype))
 
     # ---------------------------------------------------------------- head
     def head(self, Hon, Htg, Pon: Dict[str, torch.Tensor], Ptg: Dict[str, torch.Tensor], act, rew, gam, isw,
@@ -179,20 +193,21 @@ class HipBackend(TorchBackend):
         k = self._packed
         C.pack_dgrad_weights(self.lib, Pb["wfc"], Pb["w3"], Pb["w2"], k["wfcT"], k["w3tf"], k["w2t"])
 
-    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out):
+    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0):
         if not self.native_conv:
-            return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out)
-        C.conv1_fwd_ring(self.lib, ring, slots, w, b, scale, out)
+            return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out, w2, b2, rows_first)
+        C.conv1_fwd_ring(self.lib, ring, slots, w, b, scale, out, w2, b2, rows_first)
 
-    def conv_fwd(self, x, w, b, stride, out):
+    def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0):
         if not self.native_conv:
-            return super().conv_fwd(x, w, b, stride, out)
-        C.conv_fwd(self.lib, x, w, b, stride, out)
+            return super().conv_fwd(x, w, b, stride, out, w2, b2, rows_first)
+        C.conv_fwd(self.lib, x, w, b, stride, out, w2, b2, rows_first)
 
-    def fc_fwd(self, x, w, b, out):
+    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0):
         if not self.native_conv:
-            return super().fc_fwd(x, w, b, out)
-        C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True)
+            return super().fc_fwd(x, w, b, out, w2, b2, rows_first)
+        C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True, w2=w2, b2=b2,
+                    rows_first=rows_first)
 
     def fc_bwd(self, dh, x, w, dx_out, dw_out, db_out):
         if not self.native_conv:

@@ -171,10 +171,12 @@ class GpuReplayShard:
 
     # ------------------------------------------------------------- sampling
     def sample(self, B: int, out: Optional[Dict[str, torch.Tensor]] = None,
-               ratio_min_global: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+               ratio_min_global: Optional[torch.Tensor] = None,
+               nxt2: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         """Stratified proportional sample of B slots; IS weights max-normalised.
 
-        ``out`` (preallocated tensors) makes the call graph-capturable.
+        ``out`` (preallocated tensors) makes the call graph-capturable; ``nxt2``
+        receives a second copy of the S_{t+n} frame slots (target-network rows).
         """
         d = self.device
         if out is None:
@@ -184,7 +186,7 @@ class GpuReplayShard:
                 self.tree_desc(), self.record_desc(), B, self.seed, self.ctr.data_ptr(), self.beta,
                 _lib.ptr(ratio_min_global), out["idx"].data_ptr(), out["weights"].data_ptr(),
                 out["gen"].data_ptr(), out["obs"].data_ptr(), out["nxt"].data_ptr(), out["act"].data_ptr(),
-                out["rew"].data_ptr(), out["gam"].data_ptr(), self._stream()), "tree_sample")
+                out["rew"].data_ptr(), out["gam"].data_ptr(), _lib.ptr(nxt2), self._stream()), "tree_sample")
         else:
             g = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + int(self.ctr.item()))
             leaf = self.leaf.double().cpu()
@@ -211,6 +213,8 @@ class GpuReplayShard:
             out["act"].copy_(self.act[idx])
             out["rew"].copy_(self.rew[idx])
             out["gam"].copy_(self.gam[idx])
+            if nxt2 is not None:
+                nxt2.copy_(out["nxt"])
         return out
 
     def alloc_sample_buffers(self, B: int) -> Dict[str, torch.Tensor]:

@@ -171,3 +171,33 @@ def test_dense_wgrad(M):
     C.dense_wgrad(_lib(), dh, x, dw, db)
     assert _rel(dw, dh.float().t() @ x.float()) < 5e-3
     assert _rel(db, dh.float().sum(0)) < 1e-4
+
+
+def test_fused_online_target_weight_switch():
+    """One launch over [online rows | target rows] equals two separate launches."""
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(21)
+    lib = _lib()
+    N1, N2 = 128, 64  # 128*81 rows is a multiple of the 128-row tile
+    x = _bf(torch.relu(torch.randn(N1 + N2, 20, 20, 64, generator=g)))
+    wa = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+    wb = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+    ba = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    bb = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    out = torch.empty(N1 + N2, 9, 9, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv_fwd(lib, x, wa, ba, 2, out, wb, bb, N1)
+    r1 = torch.empty(N1, 9, 9, 64, dtype=torch.bfloat16, device=DEV)
+    r2 = torch.empty(N2, 9, 9, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv_fwd(lib, x[:N1], wa, ba, 2, r1)
+    C.conv_fwd(lib, x[N1:], wb, bb, 2, r2)
+    assert torch.equal(out[:N1], r1) and torch.equal(out[N1:], r2)
+    # conv1 from the ring with the switch at a 400-row image boundary (N1*400 % 128 == 0)
+    ring = torch.randint(0, 256, (30, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    slots = torch.randint(0, 30, (N1 + N2, 4), generator=g, dtype=torch.int32).to(DEV)
+    w1a = _bf(torch.randn(64, 4, 8, 8, generator=g) * 0.05)
+    w1b = _bf(torch.randn(64, 4, 8, 8, generator=g) * 0.05)
+    o1 = torch.empty(N1 + N2, 20, 20, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv1_fwd_ring(lib, ring, slots, w1a, ba, 1 / 255.0, o1, w1b, bb, N1)
+    ref_a = R.conv1_fwd(ring[slots[:N1].long()], w1a.float(), ba, 1 / 255.0)
+    ref_b = R.conv1_fwd(ring[slots[N1:].long()], w1b.float(), bb, 1 / 255.0)
+    assert _rel(o1[:N1], ref_a) < 1e-2 and _rel(o1[N1:], ref_b) < 1e-2
