@@ -1,0 +1,147 @@
+"""GPU actor group: E environments, one batched forward through the learner's
+kernels, device-side epsilon-greedy, frames stored once in the replay ring.
+
+Reference: ``Actor.run`` (``actor.py:146-191``) -- per env step a batch-1 CPU
+forward, an epsilon-greedy draw (``:121-125``), an n-step buffer add and a
+pickled queue put every 5 transitions, a ``state_dict`` pull every 500 steps.
+Here one step of the group:
+
+  1. conv1 reads the group's current frame stacks from the replay ring by slot
+     (no stacking copy), conv2/conv3/fc, then ``actor_head`` computes q and the
+     epsilon-greedy action per env on the device (one launch, counter RNG);
+  2. one small D2H copy of (q, action) per env;
+  3. the vectorised envs step; each new frame is appended ONCE to the HBM
+     frame ring (uint8), observations are C frame sequence numbers;
+  4. the sliding-window n-step builder emits transitions with initial
+     priorities, inserted into the local replay shard by one kernel.
+
+The actor keeps its own parameter slot (bf16 weights + fp32 biases/heads),
+refreshed from the learner with a D2D copy every ``Q_network_sync_freq``
+steps (reference ``actor.py:189-191``).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..config import epsilon_ladder
+from .nstep import NStepBuilder
+
+
+class GpuActorGroup:
+    def __init__(self, cfg, learner, replay, env, num_envs: int, global_offset: int = 0,
+                 total_actors: Optional[int] = None, seed: int = 0):
+        self.cfg = cfg
+        self.learner = learner
+        self.replay = replay
+        self.env = env
+        self.E = int(num_envs)
+        self.C = learner.C
+        self.A = learner.A
+        self.ops = learner.ops
+        d = learner.device
+        self.device = d
+        a = cfg.Actor
+        total = total_actors or self.E
+        ladder = epsilon_ladder(total, a.epsilon, a.alpha)
+        self.eps = torch.tensor(ladder[global_offset:global_offset + self.E], dtype=torch.float32, device=d)
+        self.seed = int(seed) * 7919 + global_offset
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=d)
+        ad = learner.act_dtype
+        self.slots = torch.zeros(self.E, self.C, dtype=torch.int32, device=d)
+        self.frames_buf = torch.zeros(self.E, self.C, 84, 84, dtype=torch.uint8, device=d) \
+            if self.ops.name != "hip" else torch.zeros(1, self.C, 84, 84, dtype=torch.uint8, device=d)
+        self.y1 = torch.zeros(self.E, 20, 20, 64, dtype=ad, device=d)
+        self.y2 = torch.zeros(self.E, 9, 9, 64, dtype=ad, device=d)
+        self.y3 = torch.zeros(self.E, 7, 7, 64, dtype=ad, device=d)
+        self.h = torch.zeros(self.E, 1024, dtype=ad, device=d)
+        self.q = torch.zeros(self.E, self.A, dtype=torch.float32, device=d)
+        self.act = torch.zeros(self.E, dtype=torch.int32, device=d)
+        self.q_host = torch.zeros(self.E, self.A, dtype=torch.float32).pin_memory() \
+            if d.type == "cuda" else torch.zeros(self.E, self.A)
+        self.a_host = torch.zeros(self.E, dtype=torch.int32).pin_memory() \
+            if d.type == "cuda" else torch.zeros(self.E, dtype=torch.int32)
+        # actor parameter slot
+        self.p32 = learner.p32.clone()
+        self.pbf = learner.pbf.clone()
+        self.P = learner.layout.views(self.p32)
+        self.Pb = learner.layout.views(self.pbf)
+        self.builder = NStepBuilder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.payload: Optional[np.ndarray] = None
+        self.t = 0
+        self.episodes: List[tuple] = []
+        self.inserted = 0
+
+    # ---------------------------------------------------------------- params
+    def sync_params(self) -> None:
+        self.p32.copy_(self.learner.p32)
+        self.pbf.copy_(self.learner.pbf)
+
+    # --------------------------------------------------------------- acting
+    def _ingest(self, frames: np.ndarray, reset_mask: np.ndarray) -> np.ndarray:
+        seqs = self.replay.append_frames(frames)
+        if self.payload is None:
+            cur = np.repeat(seqs[:, None], self.C, axis=1)
+        else:
+            cur = np.concatenate([self.payload[:, 1:], seqs[:, None]], axis=1)
+            r = np.nonzero(reset_mask)[0]
+            if len(r):
+                cur[r] = seqs[r][:, None]
+        return cur
+
+    def reset(self) -> None:
+        self.payload = self._ingest(self.env.reset(), np.ones(self.E, bool))
+
+    def policy(self, payload: np.ndarray):
+        """Batched q + epsilon-greedy for the given frame-seq payload (E, C)."""
+        ops, P, Pb = self.ops, self.P, self.Pb
+        self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
+        ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
+                           self.cfg.Runtime.obs_scale, self.y1)
+        ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2)
+        ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3)
+        ops.fc_fwd(self.y3.reshape(self.E, 3136), Pb["wfc"], P["bfc"], self.h)
+        heads = {k: P[k] for k in ("wv", "bv", "wa", "ba")}
+        ops.actor_head(self.h, heads, self.eps, self.ctr, self.seed, self.q, self.act)
+        self.ctr += 1
+        self.q_host.copy_(self.q, non_blocking=True)
+        self.a_host.copy_(self.act, non_blocking=True)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        return self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64)
+
+    def step(self) -> int:
+        """One env step for all E envs; returns the number of transitions inserted."""
+        if self.payload is None:
+            self.reset()
+        q, actions = self.policy(self.payload)
+        frames, rew, done, info = self.env.step(actions)
+        prev = self.payload
+        self.payload = self._ingest(frames, done)
+        self.builder.step(prev, q, actions, rew, done, self.payload)
+        for e in np.nonzero(done)[0]:
+            self.episodes.append((int(self.builder.env_ids[e]), int(info["episode_length"][e]),
+                                  float(info["episode_return"][e])))
+        self.t += 1
+        if self.t % self.cfg.Actor.Q_network_sync_freq == 0:
+            self.sync_params()
+        n = 0
+        if self.builder.size >= self.cfg.Actor.n_step_transition_batch_size:
+            b = self.builder.get()
+            if b is not None:
+                self.replay.insert(b)
+                n = len(b["A_t"])
+                self.inserted += n
+        return n
+
+
+def make_gpu_actor_group(cfg, learner, replay, num_envs: int, rank: int = 0, world: int = 1,
+                         seed: int = 0) -> GpuActorGroup:
+    from ..envs.vector_envs import make_vec_env
+    total = max(cfg.Actor.num_actors, num_envs * world)
+    env = make_vec_env(cfg.env_backend, cfg.env_conf.name, num_envs, cfg.env_conf.action_dim,
+                       seed=seed + 1000 * rank)
+    return GpuActorGroup(cfg, learner, replay, env, num_envs, global_offset=rank * num_envs,
+                         total_actors=total, seed=seed + rank)

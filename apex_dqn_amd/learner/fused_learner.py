@@ -75,9 +75,17 @@ class FusedNatureLearner:
         self.pbf.copy_(self.p32)
         self.sync_target()
         self.num_q_updates = 0
+        self.world = comm.world_size if comm is not None else 1
         self._alloc(self.B)
-        self._graph = None
-        self._graph_ready = False
+        self._graphs = None
+        # cross-shard IS-weight normaliser: min over ranks of (min_i p_i / total)
+        self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
+        self.ratio_buf = torch.zeros(1, dtype=torch.float32, device=d)
+        self.ratio_min = None
+        self._ratio_work = None
+        if self.world > 1:
+            self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d)
+            self._init_ratio()
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
@@ -130,60 +138,130 @@ class FusedNatureLearner:
         return {k: V[k] for k in ("wv", "bv", "wa", "ba")}
 
     # ---------------------------------------------------------------- step
-    def _step_body(self, ratio_min: Optional[torch.Tensor] = None) -> None:
+    # The step is three segments.  With one rank they run back to back (one HIP
+    # graph).  With data parallelism the flat gradient is all-reduced in two
+    # buckets over RCCL: the fc+heads bucket (12.9 MB, ready after segment 1)
+    # is reduced on RCCL's stream WHILE segment 2 computes the conv backward on
+    # the compute stream; the small conv bucket follows; segment 3 (clip +
+    # RMSprop + priority write-back) waits for both.  Gradients are pre-scaled by
+    # 1/(B*world) in the head kernel, so the SUM all-reduce yields the mean.
+    def _seg1(self) -> None:
+        """sample, forward (online+target), loss/priorities, head + fc backward."""
         B, rt, ops = self.B, self.rt, self.ops
         ops.prepare(self.Pb)
         # the sampler writes the frame-ring slots of S_t / S_{t+n} (twice) into self.slots
-        S = self.replay.sample(B, out=self.S, ratio_min_global=ratio_min, nxt2=self.slots[2 * B:])
+        S = self.replay.sample(B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * B:])
         # conv1 reads the uint8 frame stacks straight from the replay ring by slot
         self.forward_all()
         isw = S["weights"] if rt.use_is_weights else None
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
-                 S["rew"],
-                 S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / B, self.td_abs, self.loss_b,
-                 self.dH, self.dhead, zero=self.g_head_region)
+                 S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
+                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
         ops.head_wgrad(self.h, self.dhead, self.G)
-        G, Pb = self.G, self.Pb
-        ops.fc_bwd(self.dH, self.y3[:B], Pb["wfc"], self.dY3, G["wfc"], G["bfc"])
+        ops.fc_bwd(self.dH, self.y3[:B], self.Pb["wfc"], self.dY3, self.G["wfc"], self.G["bfc"])
+
+    def _seg2(self) -> None:
+        """conv backward (dgrad + wgrad for conv3, conv2; wgrad for conv1)."""
+        B, rt, ops, G, Pb = self.B, self.rt, self.ops, self.G, self.Pb
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2)
         ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"])
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1)
         ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"])
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"])
-        if self.comm is not None and self.comm.world_size > 1:
-            self.comm.allreduce_flat(self.g32, average=True)
+
+    def _seg3(self) -> None:
+        """clip + centered RMSprop (+bf16 pack), priority write-back, shard stats."""
+        rt, ops = self.rt, self.ops
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
-        self.replay.update_priorities(S["idx"], self.td_abs, S["gen"])
+        self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
+        if self.world > 1:
+            # local min_i p_i / total for the global IS-weight normaliser (all-reduced MIN after the step)
+            rp = self.replay
+            tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float()
+            self.ratio_local.copy_(rp.min_bits.view(torch.float32) / tot)
 
-    def step(self, ratio_min: Optional[torch.Tensor] = None) -> None:
+    def _step_body(self) -> None:
+        self._seg1()
+        self._seg2()
+        self._seg3()
+
+    def _dp_step(self, graphs: bool) -> None:
+        import torch.distributed as dist
+        cut = self.layout.offsets["wfc"]
+        run = (lambda i: self._graphs[i].replay()) if graphs else (lambda i: (self._seg1, self._seg2,
+                                                                                self._seg3)[i]())
+        if self._ratio_work is not None:
+            self._ratio_work.wait()
+            self.ratio_min.copy_(self.ratio_buf)
+        run(0)
+        w_fc = dist.all_reduce(self.g32[cut:], op=dist.ReduceOp.SUM, async_op=True)
+        run(1)  # conv backward overlaps the fc/head bucket all-reduce
+        w_cv = dist.all_reduce(self.g32[:cut], op=dist.ReduceOp.SUM, async_op=True)
+        w_fc.wait()
+        w_cv.wait()
+        run(2)
+        self.ratio_buf.copy_(self.ratio_local)
+        self._ratio_work = dist.all_reduce(self.ratio_buf, op=dist.ReduceOp.MIN, async_op=True)
+
+    def step(self) -> None:
         """One learner update (asynchronous on the current stream)."""
-        if self.rt.use_graphs and self.device.type == "cuda":
-            if self._graph is None:
-                self._capture(ratio_min)
-            self._graph.replay()
+        graphs = self.rt.use_graphs and self.device.type == "cuda"
+        if graphs and self._graphs is None:
+            self._capture()
+        if self.world > 1:
+            self._dp_step(graphs)
+        elif graphs:
+            self._graphs[0].replay()
         else:
-            self._step_body(ratio_min)
+            self._step_body()
         self.num_q_updates += 1
         L = self.cfg.Learner
         if self.num_q_updates % L.q_target_sync_freq == 0:
             self.sync_target()
 
-    def _capture(self, ratio_min) -> None:
-        # warm up on a side stream (allocator pools, library handles), then capture
+    def _capture(self) -> None:
+        """Warm up on a side stream (allocator pools, workspaces), restore state,
+        then capture: one graph for a single rank, three segment graphs for DP."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         snap = self._snapshot()
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._step_body(ratio_min)
+                self._step_body()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._restore(snap)
-        self._graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._graph):
-            self._step_body(ratio_min)
+        torch.cuda.synchronize(self.device)
+        if self.world == 1:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step_body()
+            self._graphs = [g]
+        else:
+            self._graphs = []
+            for seg in (self._seg1, self._seg2, self._seg3):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    seg()
+                self._graphs.append(g)
         # capture recorded the step without executing it; state is as before
+
+    def _init_ratio(self) -> None:
+        import torch.distributed as dist
+        rp = self.replay
+        tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float().clamp_min(1e-30)
+        self.ratio_buf.copy_(rp.min_bits.view(torch.float32) / tot)
+        dist.all_reduce(self.ratio_buf, op=dist.ReduceOp.MIN)
+        self.ratio_min.copy_(self.ratio_buf)
+
+    def refresh_replay_stats(self) -> None:
+        """Re-derive the cross-shard IS normaliser (after inserts / eviction)."""
+        if self.world > 1:
+            if self._ratio_work is not None:
+                self._ratio_work.wait()
+                self._ratio_work = None
+            self._init_ratio()
 
     def _snapshot(self):
         rp = self.replay
@@ -242,5 +320,4 @@ class FusedNatureLearner:
             self.rms_v.copy_(opt["rms_v"])
             self.rms_m.copy_(opt["rms_m"])
         self.num_q_updates = int(ck.get("num_q_updates", 0))
-        self._graph = None
         return True

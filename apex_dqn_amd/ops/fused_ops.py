@@ -110,16 +110,18 @@ class TorchBackend:
         g["wa"].add_(dhead[:, 1:].t() @ h[:, 512:])
         g["ba"].add_(dhead[:, 1:].sum(0))
 
-    def actor_head(self, H, P, eps, gen: torch.Generator, q_out, a_out):
+    def actor_head(self, H, P, eps, ctr, seed, q_out, a_out):
+        """Dueling q + epsilon-greedy per row (the oracle of csrc actor_head_kernel)."""
         h = H.float()
         v = h[:, :512] @ P["wv"].float() + P["bv"].float()
         a = h[:, 512:] @ P["wa"].float().t() + P["ba"].float()
         q = v[:, None] + a - a.mean(1, keepdim=True)
         q_out.copy_(q)
         E, A = q.shape
-        u = torch.rand(E, generator=gen, device="cpu").to(q.device)
-        r = torch.randint(0, A, (E,), generator=gen, device="cpu").to(q.device)
-        a_out.copy_(torch.where(u < eps, r, q.argmax(1)).to(a_out.dtype))
+        gen = torch.Generator(device="cpu").manual_seed(int(seed) * 1000003 + int(ctr.item()))
+        u = torch.rand(E, generator=gen).to(q.device)
+        r = torch.randint(0, A, (E,), generator=gen).to(q.device)
+        a_out.copy_(torch.where(u < eps.to(q.device), r, q.argmax(1)).to(a_out.dtype))
 
     # ------------------------------------------------------------ backward
     def fc_bwd(self, dh, x, w, dx_out, dw_out, db_out):

@@ -117,12 +117,14 @@ class GpuReplayShard:
         frames = torch.as_tensor(frames)
         n = frames.shape[0]
         seqs = self.frame_head + np.arange(n, dtype=np.int64)
-        start = self.frame_head % self.F
-        first = min(n, self.F - start)
-        src = frames.to(self.device, non_blocking=True)
-        self.frames[start:start + first].copy_(src[:first], non_blocking=True)
-        if first < n:
-            self.frames[:n - first].copy_(src[first:], non_blocking=True)
+        skip = max(0, n - self.F)  # only the newest F frames survive a wrap
+        src = frames[skip:].to(self.device, non_blocking=True)
+        pos, k = (self.frame_head + skip) % self.F, 0
+        while k < src.shape[0]:
+            m = min(src.shape[0] - k, self.F - pos)
+            self.frames[pos:pos + m].copy_(src[k:k + m], non_blocking=True)
+            k += m
+            pos = 0
         self.frame_head += n
         return seqs
 

@@ -1,0 +1,117 @@
+"""Config surface, network definitions and checkpoint format (CPU)."""
+import json
+import os
+
+import pytest
+import torch
+
+from apex_dqn_amd.config import ApexConfig, apply_overrides, epsilon_ladder
+from apex_dqn_amd.models.dueling import REFERENCE_KEYS, DuellingDQN, MLPDuellingDQN, ImpalaDuellingDQN, build_network
+from apex_dqn_amd.models.flat_params import (FlatLayout, flat_to_reference_state, nature_segments,
+                                             reference_state_to_flat)
+from apex_dqn_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_PARAMS = os.path.join(ROOT, "configs", "reference_parameters.json")
+
+
+def test_reference_parameters_json_loads_verbatim():
+    cfg = ApexConfig.load(REF_PARAMS)
+    assert cfg.env_conf.state_shape == [1, 84, 84]
+    assert cfg.env_conf.action_dim == 4
+    assert cfg.Actor.num_actors == 5 and cfg.Actor.num_steps == 3
+    assert cfg.Learner.replay_sample_size == 32 and cfg.Learner.q_target_sync_freq == 2500
+    assert cfg.Replay_Memory.importance_sampling_exponent == 0.4
+    assert cfg.Runtime.learner_T == 500000  # reference main.py:46 hard-codes it
+    assert cfg.network == "nature64" and cfg.frame_stack == 1
+
+
+def test_all_shipped_configs_validate():
+    for f in os.listdir(os.path.join(ROOT, "configs")):
+        if f.endswith(".json"):
+            ApexConfig.load(os.path.join(ROOT, "configs", f))
+    ApexConfig.load(os.path.join(ROOT, "parameters.json"))
+
+
+def test_overrides_and_validation(tmp_path):
+    cfg = ApexConfig.load(REF_PARAMS, ["Learner.replay_sample_size=512", "env_conf.state_shape=[4,84,84]",
+                                       "Runtime.use_graphs=false"])
+    assert cfg.Learner.replay_sample_size == 512 and cfg.env_conf.state_shape == [4, 84, 84]
+    assert cfg.Runtime.use_graphs is False
+    with pytest.raises(ValueError):
+        apply_overrides({}, ["nodot=1"])
+    with pytest.raises(ValueError):
+        ApexConfig.from_dict({"env_conf": {"state_shape": [4, 64, 64]}})
+    with pytest.raises(ValueError):
+        ApexConfig.from_dict({"Actor": {"num_actors": 0}})
+    p = tmp_path / "c.json"
+    cfg.save(str(p))
+    assert ApexConfig.load(str(p)).Learner.replay_sample_size == 512
+
+
+def test_epsilon_ladder_matches_apex_and_single_actor():
+    e = epsilon_ladder(5, 0.4, 7)
+    assert e[0] == pytest.approx(0.4) and e[-1] == pytest.approx(0.4 ** 8)
+    assert all(a > b for a, b in zip(e, e[1:]))
+    assert epsilon_ladder(1, 0.4, 7) == [pytest.approx(0.4)]  # reference divides by zero (A13)
+
+
+@pytest.mark.parametrize("C,A,n", [(1, 4, 3321541), (4, 4, 3333829), (4, 18, 3341011)])
+def test_dueling_param_counts_match_reference(C, A, n):
+    net = DuellingDQN((C, 84, 84), A)
+    assert sum(p.numel() for p in net.parameters()) == n
+    assert tuple(net.state_dict().keys()) == REFERENCE_KEYS
+
+
+def test_dueling_combine_is_per_sample():
+    torch.manual_seed(0)
+    net = DuellingDQN((4, 84, 84), 6)
+    x = torch.randint(0, 255, (3, 4, 84, 84), dtype=torch.uint8)
+    v, a, q = net(x)
+    torch.testing.assert_close(q, v + a - a.mean(1, keepdim=True))
+    # same input gives the same q regardless of batch companions (reference A15 couples samples)
+    q1 = net(x[:1])[2]
+    torch.testing.assert_close(q1, q[:1], rtol=1e-5, atol=1e-5)
+
+
+def test_other_network_families_forward():
+    for kind, shape in (("mlp", [4]), ("impala", [4, 84, 84]), ("nature32", [4, 84, 84])):
+        net = build_network(kind, shape, 5)
+        x = torch.zeros((2,) + tuple(shape), dtype=torch.uint8 if len(shape) == 3 else torch.float32)
+        v, a, q = net(x)
+        assert q.shape == (2, 5) and v.shape == (2, 1)
+    assert isinstance(build_network("mlp", [4], 2), MLPDuellingDQN)
+    assert isinstance(build_network("impala", [4, 84, 84], 2), ImpalaDuellingDQN)
+
+
+def test_flat_params_roundtrip_and_forward_equivalence():
+    torch.manual_seed(1)
+    net = DuellingDQN((4, 84, 84), 6)
+    lay = FlatLayout(nature_segments(4, 6))
+    flat = torch.zeros(lay.numel)
+    V = lay.views(flat)
+    reference_state_to_flat(net.state_dict(), V)
+    sd = flat_to_reference_state(V)
+    for k, t in net.state_dict().items():
+        assert torch.equal(sd[k], t), k
+    assert lay.numel >= sum(p.numel() for p in net.parameters())
+    assert all(o % 64 == 0 for o in lay.offsets.values())
+
+
+def test_checkpoint_format_reference_compatible(tmp_path):
+    net = DuellingDQN((1, 84, 84), 4)
+    p = str(tmp_path / "ck.pt")
+    save_checkpoint(p, net.state_dict(), num_q_updates=7, config={"a": 1})
+    ck = torch.load(p, weights_only=True)  # reference learner.py:20-21 access pattern
+    net2 = DuellingDQN((1, 84, 84), 4)
+    net2.load_state_dict(ck["Q_state"])
+    for k in REFERENCE_KEYS:
+        assert torch.equal(net2.state_dict()[k], net.state_dict()[k])
+    assert ck["num_q_updates"] == 7
+    assert load_checkpoint(str(tmp_path / "missing.pt")) is None
+
+
+def test_params_file_is_json():
+    with open(os.path.join(ROOT, "parameters.json")) as f:
+        d = json.load(f)
+    assert set(d) >= {"env_conf", "Actor", "Learner", "Replay_Memory"}

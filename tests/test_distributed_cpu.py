@@ -1,0 +1,88 @@
+"""Data-parallel learner over gloo (CPU, world_size 2): the fake cluster.
+
+Checks that the bucketed, overlapped gradient all-reduce of the fused learner
+equals the mean of the per-rank gradients, that parameters stay bit-identical
+across ranks, and that the cross-shard IS normaliser is the global min.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from apex_dqn_amd.config import ApexConfig
+
+
+def _cfg():
+    return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
+                                 "Learner": {"replay_sample_size": 6},
+                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0}})
+
+
+def _replay(rank):
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(300, 300, 400, 4, device="cpu", seed=rank + 3)
+    rng = np.random.default_rng(100 + rank)
+    seqs = rp.append_frames(rng.integers(0, 255, (120, 84, 84), dtype=np.uint8))
+    K = 100
+    st = np.stack([seqs[i:i + 4] for i in range(K)])
+    rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 5, K), R=rng.normal(size=K),
+                   Gamma=np.full(K, 0.97), priority=rng.random(K) * (rank + 1)))
+    return rp
+
+
+def _worker(rank, world, path, q):
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.parallel.dist import Comm
+    torch.set_num_threads(2)
+    comm = Comm.init(rank, world, f"file://{path}", backend="gloo")
+    cfg = _cfg()
+    torch.manual_seed(1234 + rank)  # different local init: rank 0's params must be broadcast
+    rp = _replay(rank)
+    L = FusedNatureLearner(cfg, "cpu", rp, comm=comm)
+    ratio_global = float(L.ratio_min)
+    ratio_local0 = rp.min_leaf() / rp.total()
+    # local reference gradient on an identical replay copy, single rank, scale 1/B
+    torch.manual_seed(0)
+    rp2 = _replay(rank)
+    Lref = FusedNatureLearner(cfg, "cpu", rp2, comm=None)
+    Lref.p32.copy_(L.p32)
+    Lref.pbf.copy_(L.pbf)
+    Lref.sync_target()
+    Lref.ratio_min = L.ratio_min.clone()
+    Lref._seg1()
+    Lref._seg2()
+    g_local = Lref.g32.clone()
+    L.step()
+    g_dp = L.g32.clone()
+    gl = [torch.zeros_like(g_local) for _ in range(world)]
+    torch.distributed.all_gather(gl, g_local)
+    g_mean = torch.stack(gl).mean(0)
+    pl = [torch.zeros_like(L.p32) for _ in range(world)]
+    torch.distributed.all_gather(pl, L.p32.clone())
+    q.put((rank, float((g_dp - g_mean).abs().max()), float(g_mean.abs().max()),
+           float((pl[0] - pl[1]).abs().max()), ratio_global, ratio_local0))
+    comm.shutdown()
+
+
+@pytest.mark.slow
+def test_dp_learner_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "store")
+        procs = [ctx.Process(target=_worker, args=(r, world, path, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=240) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    ratios = [r[5] for r in res]
+    for rank, gerr, gmax, perr, ratio_g, _ in res:
+        assert gerr <= 1e-6 * max(gmax, 1e-6) + 1e-9, (rank, gerr, gmax)
+        assert perr == 0.0
+        assert ratio_g == pytest.approx(min(ratios), rel=1e-5)
