@@ -106,7 +106,21 @@ struct FwdRegs {
   uint4 a0, a1, a2, a3, b0, b1;
 };
 
-template <int MODE>
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16x2 (one v_cvt_pk_bf16_f32, round-to-nearest-even)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
+}
+
+// Epilogue image: 32 rows x 128 B per wave; 16-B chunk c of row r at c ^ ((r>>1)&7)
+__device__ __forceinline__ int epi_off(int r, int byte) {
+  return (r << 7) + ((((byte >> 4) ^ ((r >> 1) & 7))) << 4) + (byte & 15);
+}
+
+// MODE: A-operand source (0 dense, 1 NHWC implicit im2col, 2 legacy uint8 frames);
+// PAD: bounds-check im2col taps (padding / dgrad); pad==0 forward convs skip it.
+template <int MODE, bool PAD>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * FWD_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -123,10 +137,11 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const int sc = tid & 7;
   const int srow = tid >> 3;
 
-  // per-thread staging rows (4 A rows, 2 B rows)
+  // per-thread staging rows (4 A rows, 2 B rows): 64-bit row bases hoisted out of the k-loop
   bool a_ok[4];
-  int a_img[4], a_ih[4], a_iw[4];
-  int a_slot[4][4];  // MODE 2: frame-ring slots of the row's image (C <= 4), read once up front
+  int a_ih[4], a_iw[4];
+  const bf16_t* a_ptr[4];
+  int a_slot[4][4];  // MODE 2 only
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + srow + 32 * i;
@@ -134,16 +149,22 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     const int mm = a_ok[i] ? m : 0;
     const int img = mm / OHW, rem = mm - img * OHW;
     const int oh = rem / d.OW, ow = rem - oh * d.OW;
-    a_img[i] = img;
     a_ih[i] = oh * d.stride - d.pad_h;
     a_iw[i] = ow * d.stride - d.pad_w;
+    if (MODE == 0) a_ptr[i] = (const bf16_t*)d.x + (int64_t)mm * d.K + sc * 8;
+    else if (MODE == 1)
+      a_ptr[i] = (const bf16_t*)d.x + (((int64_t)img * d.H + a_ih[i]) * d.W + a_iw[i]) * d.Cin + sc * 8;
+    else a_ptr[i] = nullptr;
     if (MODE == 2) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) a_slot[i][c] = (c < d.Cin) ? d.frame_slots[img * d.Cin + c] : 0;
+      a_ih[i] = oh * d.stride;
+      a_iw[i] = ow * d.stride;
     }
   }
   const bf16_t* wrow0 = wb + (int64_t)(n0 + srow) * d.K + sc * 8;
   const bf16_t* wrow1 = wrow0 + (int64_t)32 * d.K;
+  const int cpb = d.Cin >> 6;
 
   auto load_tile = [&](int kt, FwdRegs& R) {
     R.b0 = *reinterpret_cast<const uint4*>(wrow0 + (kt << 6));
@@ -152,20 +173,24 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     if (MODE == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const bf16_t* src = (const bf16_t*)d.x + (int64_t)(m0 + srow + 32 * i) * d.K + (kt << 6) + sc * 8;
-        ra[i] = a_ok[i] ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        uint4 v = *reinterpret_cast<const uint4*>(a_ptr[i] + (kt << 6));
+        ra[i] = a_ok[i] ? v : make_uint4(0, 0, 0, 0);
       }
     } else if (MODE == 1) {
-      const int cpb = d.Cin >> 6;
+      // tap decode is wave-uniform (scalar); per row only a pointer add (+ bounds if PAD)
       const int tap = kt / cpb, cb = kt - tap * cpb;
       const int kh = tap / d.KW, kw = tap - kh * d.KW;
+      const int64_t toff = ((int64_t)kh * d.W + kw) * d.Cin + (cb << 6);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
-        const bool ok = a_ok[i] && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
-        const bf16_t* src = (const bf16_t*)d.x +
-                            ((((int64_t)a_img[i] * d.H + ih) * d.W + iw) * d.Cin + (cb << 6) + sc * 8);
-        ra[i] = ok ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        bool ok = a_ok[i];
+        if (PAD) {
+          const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
+          ok = ok && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
+        }
+        const bf16_t* src = ok ? a_ptr[i] + toff : (const bf16_t*)d.x;
+        const uint4 v = *reinterpret_cast<const uint4*>(src);
+        ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
       }
     } else {  // MODE 2: uint8 frames, K ordered (c, kh, kw), one frame per k-tile, chunk = kh
       const int64_t fbytes = (int64_t)d.H * d.W;
@@ -195,6 +220,9 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     *reinterpret_cast<uint4*>(Bs + swz_row(srow + 32, sc)) = R.b1;
   };
 
+  // acc[mt][nt] holds C^T (channels x pixels): lane (g = lane>>4, p = lane&15) owns
+  // channels 16nt + 4g + {0..3} of pixel 16mt + p -- 4 consecutive channels, so the
+  // epilogue packs them with v_cvt_pk_bf16_f32 into one 8-byte LDS write.
   f32x4 acc[2][4];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -218,7 +246,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
     }
   };
 
@@ -232,34 +260,36 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   __syncthreads();
   if (KT > 2) load_tile(2, RA);
   for (int kt = 0; kt < KT; kt += 2) {
-    // even tile kt (LDS buf 0); its successor kt+1 sits in RB
     compute(0);
     if (kt + 1 < KT) write_tile(1, RB);
     __syncthreads();
     if (kt + 3 < KT) load_tile(kt + 3, RB);
     if (kt + 1 >= KT) break;
-    // odd tile kt+1 (LDS buf 1); its successor kt+2 sits in RA
     compute(1);
     if (kt + 2 < KT) write_tile(0, RA);
     __syncthreads();
     if (kt + 4 < KT) load_tile(kt + 4, RA);
   }
 
-  // ---- epilogue: scale + bias -> bf16 in LDS (per-wave 32x64 image), then
-  // coalesced 16-B row stores with ReLU or mask applied
+  // ---- epilogue: (acc*scale + bias) -> bf16x4 per lane -> swizzled LDS image -> 16-B row stores
   uint8_t* Es = smem + wv * 4096;
+  const int g = lane >> 4, pl = lane & 15;
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int col = 16 * nt + (lane & 15);
-      const float bv = bias ? bias[n0 + col] : 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = 16 * mt + 4 * (lane >> 4) + j;
-        *reinterpret_cast<bf16_t*>(Es + row * 128 + col * 2) = f32_to_bf16(acc[mt][nt][j] * d.in_scale + bv);
-      }
+  for (int nt = 0; nt < 4; ++nt) {
+    const int ch = 16 * nt + 4 * g;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+      const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + ch);
+      b4[0] = bb.x; b4[1] = bb.y; b4[2] = bb.z; b4[3] = bb.w;
     }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const int row = 16 * mt + pl;
+      const uint2 v = make_uint2(cvt_pk_bf16(acc[mt][nt][0] * d.in_scale + b4[0], acc[mt][nt][1] * d.in_scale + b4[1]),
+                                 cvt_pk_bf16(acc[mt][nt][2] * d.in_scale + b4[2], acc[mt][nt][3] * d.in_scale + b4[3]));
+      *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) = v;
+    }
+  }
   __syncthreads();
   const int ooh = (d.ncls == 4) ? (cls >> 1) : 0;
   const int oow = (d.ncls == 4) ? (cls & 1) : 0;
@@ -268,7 +298,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     const int row = 8 * p + (lane >> 3), ch = lane & 7;
     const int m = m0 + 32 * wv + row;
     if (m >= M) continue;
-    uint4 v = *reinterpret_cast<const uint4*>(Es + row * 128 + ch * 16);
+    uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
     const int img = m / OHW, rem = m - img * OHW;
     const int oh = rem / d.OW, ow = rem - oh * d.OW;
     const int64_t orow = ((int64_t)img * d.OHfull + oh * d.ostride_h + ooh) * d.OWfull + ow * d.ostride_w + oow;
@@ -315,6 +345,25 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
   }
   uint4 rdy[2], rx[2];
 
+  // MODE 2 stages the X tile with a different lane map: lane = reduction row
+  // (64 consecutive output pixels), wave = 16-B s2d block (2 bf16 chunks), so one
+  // load instruction reads 64 consecutive blocks of one frame row (contiguous).
+  const int x2_row = tid & 63, x2_blk = tid >> 6;
+  uint4 rx2 = make_uint4(0, 0, 0, 0);
+  auto load_x2 = [&](int r0) {
+    const int m = r0 + x2_row;
+    rx2 = make_uint4(0, 0, 0, 0);
+    if (m < r_end) {
+      const int img = m / OHW, rem = m - img * OHW;
+      const int oh = rem / d.OW, ow = rem - oh * d.OW;
+      const int q = 4 * kct + x2_blk;
+      const int tap = q / d.Cin, c = q - tap * d.Cin;
+      const int slot = d.frame_slots[img * d.Cin + c];
+      rx2 = *reinterpret_cast<const uint4*>((const uint8_t*)d.x + (int64_t)slot * 7056 +
+                                             (((oh + (tap >> 1)) * 21 + ow + (tap & 1)) << 4));
+    }
+  };
+
   auto load_step = [&](int r0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -335,20 +384,10 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
           const bf16_t* src =
               (const bf16_t*)d.x + ((((int64_t)img * d.H + ih) * d.W + iw) * d.Cin + (cb << 6) + sc * 8);
           rx[i] = ok2 ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
-        } else {  // MODE 2: u8 frame of channel kct, chunk = kh row of 8 bytes
-          if (ok) {
-            const int slot = d.frame_slots[img * d.Cin + kct];
-            const uint8_t* p = (const uint8_t*)d.x + (int64_t)slot * d.H * d.W +
-                               (int64_t)(oh * d.stride + sc) * d.W + ow * d.stride;
-            rx[i].x = *reinterpret_cast<const uint32_t*>(p);
-            rx[i].y = *reinterpret_cast<const uint32_t*>(p + 4);
-          } else {
-            rx[i].x = 0;
-            rx[i].y = 0;
-          }
         }
       }
     }
+    if (MODE == 2) load_x2(r0);
   };
 
   auto write_step = [&](int buf) {
@@ -358,8 +397,12 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
     for (int i = 0; i < 2; ++i) {
       const int r = srow + 32 * i;
       *reinterpret_cast<uint4*>(Ds + swz_tr(r, sc)) = rdy[i];
-      uint4 xv = (MODE == 2) ? u8x8_to_bf16x8(rx[i].x, rx[i].y) : rx[i];
-      *reinterpret_cast<uint4*>(Xs + swz_tr(r, sc)) = xv;
+      if (MODE != 2) *reinterpret_cast<uint4*>(Xs + swz_tr(r, sc)) = rx[i];
+      if (MODE == 2 && i == 0) {
+        // 16 uint8 of one s2d block -> two 16-B bf16 chunks (2 x2_blk, 2 x2_blk + 1) of row x2_row
+        *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk)) = u8x8_to_bf16x8(rx2.x, rx2.y);
+        *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk + 1)) = u8x8_to_bf16x8(rx2.z, rx2.w);
+      }
       if (do_bias) {
         const uint32_t w4[4] = {rdy[i].x, rdy[i].y, rdy[i].z, rdy[i].w};
 #pragma unroll
@@ -543,9 +586,11 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.w2 != nullptr && (d.m_switch % FWD_BM)) return (int)hipErrorInvalidValue;
   const int M = d.N * d.OH * d.OW;
   dim3 grid((M + FWD_BM - 1) / FWD_BM, d.Cout / FWD_BN, d.ncls > 0 ? d.ncls : 1);
-  if (d.mode == 0) igemm_fwd_kernel<0><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1) igemm_fwd_kernel<1><<<grid, 256, 0, st>>>(d);
-  else igemm_fwd_kernel<2><<<grid, 256, 0, st>>>(d);
+  const bool pad = d.pad_h > 0 || d.pad_w > 0;
+  if (d.mode == 0) igemm_fwd_kernel<0, false><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1 && pad) igemm_fwd_kernel<1, true><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1) igemm_fwd_kernel<1, false><<<grid, 256, 0, st>>>(d);
+  else igemm_fwd_kernel<2, false><<<grid, 256, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }
 

@@ -78,6 +78,40 @@ def conv1_fwd_ring(lib, ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tenso
     _launch_fwd(lib, d)
 
 
+def pack_w1_s2d(lib, ws: "Workspace", w1: torch.Tensor, tag: str) -> torch.Tensor:
+    """OIHW conv1 weights -> s2d K order (cached buffer per tag, repacked every call)."""
+    C = w1.shape[1]
+    buf = ws.get(("w1s", tag), 64 * 64 * C, w1.device, torch.bfloat16)
+    _lib.check(lib.apex_s2d_pack_w1(w1.data_ptr(), buf.data_ptr(), C, _lib.stream_ptr()), "s2d_pack_w1")
+    return buf
+
+
+def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
+                  b1: torch.Tensor, scale: float, out: torch.Tensor, w2=None, b2=None, rows_first: int = 0,
+                  grid: int = 0) -> None:
+    """conv1 on the space-to-depth replay ring (persistent LDS-DMA kernel, csrc/conv1_s2d.hip)."""
+    N, C = slots.shape
+    assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
+    d = _lib.Conv1S2DDesc()
+    d.ring, d.slots, d.y = ring.data_ptr(), slots.data_ptr(), out.data_ptr()
+    d.w = pack_w1_s2d(lib, ws, w1, "a").data_ptr()
+    d.bias = b1.data_ptr()
+    if w2 is not None:
+        if (rows_first * 400) % 128:
+            raise ValueError("online/target split must fall on a 128-row tile boundary")
+        d.w2 = pack_w1_s2d(lib, ws, w2, "b").data_ptr()
+        d.bias2 = b2.data_ptr()
+        d.m_switch = rows_first * 400
+    zero = ws.get(("zero16",), 64, ring.device, torch.uint8)
+    if not getattr(ws, "_zeroed", False):
+        zero.zero_()
+        ws._zeroed = True
+    d.zero16 = zero.data_ptr()
+    d.scratch = ws.get(("scratch1k",), 2048, ring.device, torch.uint8).data_ptr()
+    d.N, d.C, d.in_scale = N, C, float(scale)
+    _lib.check(lib.apex_conv1_s2d_fwd(d, int(grid), _lib.stream_ptr()), "conv1_s2d_fwd")
+
+
 def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int, out: torch.Tensor,
              w2=None, b2=None, rows_first: int = 0) -> None:
     """NHWC conv + bias + ReLU with OHWI weights (conv2 / conv3)."""
@@ -165,11 +199,14 @@ def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, s
     nsplit, rows = _splits(Mred, OH * OW, target_rows)
     slab = ws.get(("wg1", Co, Kc), nsplit * Co * Kc, dy.device)
     bslab = ws.get(("wg1b", Co), nsplit * Co, dy.device)
+    tmp = ws.get(("wg1s", Co, Kc), Co * Kc, dy.device)  # dW in s2d K order
     d = _wg_desc(dy=dy.data_ptr(), x=ring.data_ptr(), frame_slots=slots.data_ptr(), slab=slab.data_ptr(),
                  bias_slab=bslab.data_ptr(), N=N, H=ring.shape[1], W=ring.shape[2], Cin=C, OH=OH, OW=OW,
                  KH=8, KW=8, stride=4, mode=2, Co=Co, Kc=Kc, ldd=Co, rows_per_split=rows, Mred=Mred)
-    _lib.check(lib.apex_conv_wgrad(d, dw_out.data_ptr(), db_out.data_ptr(), nsplit, float(scale),
+    _lib.check(lib.apex_conv_wgrad(d, tmp.data_ptr(), db_out.data_ptr(), nsplit, float(scale),
                                    _lib.stream_ptr()), "conv1_wgrad")
+    _lib.check(lib.apex_s2d_unpack_w1_grad(tmp.data_ptr(), dw_out.data_ptr(), C, _lib.stream_ptr()),
+               "s2d_unpack")
 
 
 def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor) -> None:

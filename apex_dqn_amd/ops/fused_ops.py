@@ -34,8 +34,10 @@ class TorchBackend:
     def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0):
         """conv1 on frame stacks addressed by replay-ring slots (N, C); rows >=
         ``rows_first`` use the second weight set (w2, b2) when given."""
+        from ..replay.gpu_replay import from_s2d
         frames = frames_buf[:slots.shape[0]]
-        frames.copy_(ring[slots.long()])
+        n, c = slots.shape
+        frames.copy_(from_s2d(ring[slots.long()].reshape(n * c, 84, 84)).reshape(n, c, 84, 84))
         if w2 is None:
             self.conv1_fwd(frames, w, b, scale, out)
         else:
@@ -198,7 +200,7 @@ class HipBackend(TorchBackend):
     def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0):
         if not self.native_conv:
             return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out, w2, b2, rows_first)
-        C.conv1_fwd_ring(self.lib, ring, slots, w, b, scale, out, w2, b2, rows_first)
+        C.conv1_s2d_fwd(self.lib, self.ws, ring, slots, w, b, scale, out, w2, b2, rows_first)
 
     def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0):
         if not self.native_conv:

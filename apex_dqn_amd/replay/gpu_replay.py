@@ -1,7 +1,9 @@
 """HBM-resident prioritized replay shard (one per GPU rank).
 
 Storage per shard (sized for 288 GB HBM3E):
-* frame ring  uint8 [F, 84, 84]      -- each env frame stored once;
+* frame ring  uint8 [F, 84, 84]      -- each env frame stored once, in space-to-depth(4)
+                                       byte order (21x21 blocks of 4x4 pixels, 16 B each) so
+                                       conv1 reads whole 16-B blocks by LDS-DMA;
 * records     int32 [cap, C] x2      -- frame-ring slots of S_t / S_{t+n} stacks,
               int32 act, fp32 R, fp32 Gamma, int32 generation;
 * sum-tree    64-ary (leaf fp32 = p^alpha, internal fp64) -- ``csrc/sumtree.hip``.
@@ -27,6 +29,18 @@ import numpy as np
 import torch
 
 from ..ops import _lib
+
+
+def to_s2d(x: torch.Tensor) -> torch.Tensor:
+    """(n, 84, 84) frames -> space-to-depth(4) byte layout [21][21][4][4], viewed as (n, 84, 84)."""
+    n = x.shape[0]
+    return x.reshape(n, 21, 4, 21, 4).permute(0, 1, 3, 2, 4).contiguous().reshape(n, 84, 84)
+
+
+def from_s2d(y: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`to_s2d` (the axis permutation is an involution)."""
+    n = y.shape[0]
+    return y.reshape(n, 21, 21, 4, 4).permute(0, 1, 3, 2, 4).contiguous().reshape(n, 84, 84)
 
 
 def _tree_levels(cap: int):
@@ -75,6 +89,7 @@ class GpuReplayShard:
         self.gam = torch.zeros(self.cap, dtype=torch.float32, device=d)
         self.gen = torch.zeros(self.cap, dtype=torch.int32, device=d)
         self.ctr = torch.zeros(1, dtype=torch.int64, device=d)  # sampling RNG counter (device-side)
+        self.zero16 = torch.zeros(64, dtype=torch.uint8, device=d)  # DMA source for padding rows
         # host bookkeeping
         self.head = 0          # next record slot
         self.live = 0
@@ -118,13 +133,20 @@ class GpuReplayShard:
         n = frames.shape[0]
         seqs = self.frame_head + np.arange(n, dtype=np.int64)
         skip = max(0, n - self.F)  # only the newest F frames survive a wrap
-        src = frames[skip:].to(self.device, non_blocking=True)
-        pos, k = (self.frame_head + skip) % self.F, 0
-        while k < src.shape[0]:
-            m = min(src.shape[0] - k, self.F - pos)
-            self.frames[pos:pos + m].copy_(src[k:k + m], non_blocking=True)
-            k += m
-            pos = 0
+        src = frames[skip:].to(self.device, non_blocking=True).contiguous()
+        start = (self.frame_head + skip) % self.F
+        if self.use_hip and self.frame_shape == (84, 84):
+            # s2d permutation + ring scatter (with wrap) in one kernel
+            _lib.check(self.lib.apex_s2d_frames(src.data_ptr(), self.frames.data_ptr(), src.shape[0], self.F,
+                                                start, self._stream()), "s2d_frames")
+        else:
+            src = to_s2d(src) if self.frame_shape == (84, 84) else src
+            pos, k = start, 0
+            while k < src.shape[0]:
+                m = min(src.shape[0] - k, self.F - pos)
+                self.frames[pos:pos + m].copy_(src[k:k + m], non_blocking=True)
+                k += m
+                pos = 0
         self.frame_head += n
         return seqs
 
@@ -231,16 +253,19 @@ class GpuReplayShard:
                     gam=torch.zeros(B, dtype=torch.float32, device=d))
 
     def gather_frames(self, slots: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """slots (B, C) int32 -> stacked frames (B, C, H, W) uint8."""
+        """slots (B, C) int32 -> stacked frames (B, C, H, W) uint8 in natural pixel order."""
         B = slots.shape[0]
-        if out is None:
-            out = torch.empty((B, self.C) + self.frame_shape, dtype=torch.uint8, device=self.device)
+        raw = torch.empty((B, self.C) + self.frame_shape, dtype=torch.uint8, device=self.device)
         if self.use_hip:
             _lib.check(self.lib.apex_gather_frames(self.frames.data_ptr(), slots.data_ptr(), B * self.C, self.C,
-                                                   self.frame_bytes, out.data_ptr(), self._stream()),
+                                                   self.frame_bytes, raw.data_ptr(), self._stream()),
                        "gather_frames")
         else:
-            out.copy_(self.frames[slots.long()])
+            raw.copy_(self.frames[slots.long()])
+        nat = from_s2d(raw.reshape(B * self.C, 84, 84)).reshape(raw.shape) if self.frame_shape == (84, 84) else raw
+        if out is None:
+            return nat
+        out.copy_(nat)
         return out
 
     # ------------------------------------------------------------ priorities

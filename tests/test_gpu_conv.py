@@ -30,13 +30,15 @@ def _maxrel(a, b):
 def test_conv1_fwd_from_ring(N):
     from apex_dqn_amd.ops import conv as C
     g = torch.Generator(device="cpu").manual_seed(0)
-    ring = torch.randint(0, 256, (50, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    raw = torch.randint(0, 256, (50, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    ring = to_s2d(raw)
     slots = torch.randint(0, 50, (N, 4), generator=g, dtype=torch.int32).to(DEV)
     w = _bf(torch.randn(64, 4, 8, 8, generator=g) * 0.05)
     b = (torch.randn(64, generator=g) * 0.1).to(DEV)
     out = torch.empty(N, 20, 20, 64, dtype=torch.bfloat16, device=DEV)
-    C.conv1_fwd_ring(_lib(), ring, slots, w, b, 1 / 255.0, out)
-    frames = ring[slots.long()]
+    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, w, b, 1 / 255.0, out)
+    frames = raw[slots.long()]
     ref = R.conv1_fwd(frames, w.float(), b, 1 / 255.0)
     assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
 
@@ -149,13 +151,15 @@ def test_conv_wgrad_layers(N):
 def test_conv1_wgrad_from_ring(N):
     from apex_dqn_amd.ops import conv as C
     g = torch.Generator(device="cpu").manual_seed(N + 5)
-    ring = torch.randint(0, 256, (40, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    raw = torch.randint(0, 256, (40, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    ring = to_s2d(raw)
     slots = torch.randint(0, 40, (N, 4), generator=g, dtype=torch.int32).to(DEV)
     dy = _bf(torch.randn(N, 20, 20, 64, generator=g))
     dw = torch.empty(64, 4, 8, 8, device=DEV)
     db = torch.empty(64, device=DEV)
     C.conv1_wgrad_ring(_lib(), C.Workspace(), dy, ring, slots, 1 / 255.0, dw, db, target_rows=800)
-    rdw, rdb = R.conv1_wgrad(dy.float(), ring[slots.long()], 1 / 255.0)
+    rdw, rdb = R.conv1_wgrad(dy.float(), raw[slots.long()], 1 / 255.0)
     assert _rel(dw, rdw) < 5e-3
     assert _rel(db, rdb) < 1e-4
 
@@ -192,12 +196,41 @@ def test_fused_online_target_weight_switch():
     C.conv_fwd(lib, x[N1:], wb, bb, 2, r2)
     assert torch.equal(out[:N1], r1) and torch.equal(out[N1:], r2)
     # conv1 from the ring with the switch at a 400-row image boundary (N1*400 % 128 == 0)
-    ring = torch.randint(0, 256, (30, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    raw = torch.randint(0, 256, (30, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    ring = to_s2d(raw)
     slots = torch.randint(0, 30, (N1 + N2, 4), generator=g, dtype=torch.int32).to(DEV)
     w1a = _bf(torch.randn(64, 4, 8, 8, generator=g) * 0.05)
     w1b = _bf(torch.randn(64, 4, 8, 8, generator=g) * 0.05)
     o1 = torch.empty(N1 + N2, 20, 20, 64, dtype=torch.bfloat16, device=DEV)
-    C.conv1_fwd_ring(lib, ring, slots, w1a, ba, 1 / 255.0, o1, w1b, bb, N1)
-    ref_a = R.conv1_fwd(ring[slots[:N1].long()], w1a.float(), ba, 1 / 255.0)
-    ref_b = R.conv1_fwd(ring[slots[N1:].long()], w1b.float(), bb, 1 / 255.0)
+    C.conv1_s2d_fwd(lib, C.Workspace(), ring, slots, w1a, ba, 1 / 255.0, o1, w1b, bb, N1)
+    ref_a = R.conv1_fwd(raw[slots[:N1].long()], w1a.float(), ba, 1 / 255.0)
+    ref_b = R.conv1_fwd(raw[slots[N1:].long()], w1b.float(), bb, 1 / 255.0)
     assert _rel(o1[:N1], ref_a) < 1e-2 and _rel(o1[N1:], ref_b) < 1e-2
+
+
+@pytest.mark.parametrize("C", [1, 2, 4])
+def test_conv1_s2d_frame_stacks_and_ring_layout(C):
+    """Other frame-stack depths (reference parameters.json uses C=1) + the s2d ring
+    written by the replay's append path."""
+    from apex_dqn_amd.ops import conv as Cv
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    g = torch.Generator(device="cpu").manual_seed(C)
+    rp = GpuReplayShard(64, 64, 80, C, device=DEV)
+    raw = torch.randint(0, 256, (70, 84, 84), generator=g, dtype=torch.uint8)
+    rp.append_frames(raw)
+    N = 37
+    slots = torch.randint(0, 70, (N, C), generator=g, dtype=torch.int32).to(DEV)
+    assert torch.equal(rp.gather_frames(slots).cpu(), raw[slots.long().cpu()])
+    w = _bf(torch.randn(64, C, 8, 8, generator=g) * 0.05)
+    b = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    out = torch.empty(N, 20, 20, 64, dtype=torch.bfloat16, device=DEV)
+    Cv.conv1_s2d_fwd(_lib(), Cv.Workspace(), rp.frames, slots, w, b, 1 / 255.0, out)
+    ref = R.conv1_fwd(raw[slots.long().cpu()].to(DEV), w.float(), b, 1 / 255.0)
+    assert _rel(out, ref) < 1e-2
+    dy = _bf(torch.randn(N, 20, 20, 64, generator=g))
+    dw = torch.empty(64, C, 8, 8, device=DEV)
+    db = torch.empty(64, device=DEV)
+    Cv.conv1_wgrad_ring(_lib(), Cv.Workspace(), dy, rp.frames, slots, 1 / 255.0, dw, db, target_rows=400)
+    rdw, _ = R.conv1_wgrad(dy.float(), raw[slots.long().cpu()].to(DEV), 1 / 255.0)
+    assert _rel(dw, rdw) < 5e-3

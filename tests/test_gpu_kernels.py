@@ -126,7 +126,8 @@ def test_gather_frames():
     _fill_replay(rp, 50)
     slots = torch.randint(0, 58, (16, 4), dtype=torch.int32, device=DEV)
     out = rp.gather_frames(slots)
-    ref = rp.frames[slots.long()]
+    from apex_dqn_amd.replay.gpu_replay import from_s2d
+    ref = from_s2d(rp.frames[slots.long()].reshape(64, 84, 84)).reshape(16, 4, 84, 84)
     assert torch.equal(out, ref)
 
 
