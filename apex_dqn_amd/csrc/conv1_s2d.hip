@@ -7,7 +7,7 @@
 // 16-byte LDS-DMA (global_load_lds_dwordx4) straight from the replay ring --
 // the frame stack is never materialised in HBM, and no VGPR staging or
 // ds_write is spent on it.  K order: k = ((tap*C + c)*16 + r4*4 + c4),
-// tap = 2a+b, so the weights are a K-permuted copy of OIHW w1.
+// tap = 2a+b: the kernel gathers that permutation of OIHW w1 into LDS itself.
 //
 // Forward: persistent workgroups (one per CU) keep both weight sets (online and
 // target network, 2 x 64 x 64C bf16) resident in LDS and stream 128-row A tiles
@@ -25,7 +25,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 struct Conv1S2DDesc {
   const uint8_t* ring;        // s2d frame ring [F][21][21][16]
   const int32_t* slots;       // [N][C]
-  const bf16_t* w;            // [64][64C] s2d K order (online)
+  const bf16_t* w;            // [64][C][8][8] OIHW (online)
   const bf16_t* w2;           // second set (target), or null
   const float* bias;
   const float* bias2;
@@ -93,6 +93,12 @@ __device__ __forceinline__ void sload_slots(const int32_t* p, int (&out)[4]) {
   }
 }
 
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
+}
+
 template <int C>
 __global__ void __launch_bounds__(256, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
   constexpr int NCH = 4 * C;             // 16-byte chunks (tap, frame) per A row
@@ -116,21 +122,30 @@ __global__ void __launch_bounds__(256, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
   const int ntiles = (M + S2D_ROWS - 1) / S2D_ROWS;
   const bool two = d.w2 != nullptr;
 
-  // ---- weights (both sets) -> LDS, chunk c of row n stored at c ^ (n & mask)
+  // ---- weights (both sets) -> LDS, chunk c of row n stored at c ^ (n & mask).
+  // Gathered straight from OIHW w1: s2d chunk c = (tap, frame) block q = c >> 1, kernel
+  // rows r4 = 2(c & 1) + {0, 1}; each is 4 contiguous kw taps (8 B) of the OIHW tensor.
   constexpr int WMASK = WCH >= 16 ? 15 : WCH - 1;
   for (int s = 0; s < (two ? 2 : 1); ++s) {
     const bf16_t* src = s ? d.w2 : d.w;
     for (int i = tid; i < 64 * WCH; i += 256) {
       const int n = i / WCH, c = i - n * WCH;
-      const uint4 v = *reinterpret_cast<const uint4*>(src + (int64_t)n * K + c * 8);
-      *reinterpret_cast<uint4*>(Wl + s * WSET + n * WROW + ((c ^ (n & WMASK)) << 4)) = v;
+      const int q = c >> 1, tap = q / C, ch = q - tap * C;
+      const int kh = 4 * (tap >> 1) + 2 * (c & 1), kw = 4 * (tap & 1);
+      const bf16_t* p = src + ((n * C + ch) * 8 + kh) * 8 + kw;
+      const uint2 lo = *reinterpret_cast<const uint2*>(p);
+      const uint2 hi = *reinterpret_cast<const uint2*>(p + 8);
+      *reinterpret_cast<uint4*>(Wl + s * WSET + n * WROW + ((c ^ (n & WMASK)) << 4)) =
+          make_uint4(lo.x, lo.y, hi.x, hi.y);
     }
   }
-  float bias_r[2][4];
+  // lane (g, p) owns output channels 16nt + 4g + {0..3} (swapped-operand MFMA below)
+  float4 bias4[2][4];
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
-    bias_r[0][nt] = d.bias[16 * nt + (lane & 15)];
-    bias_r[1][nt] = two ? d.bias2[16 * nt + (lane & 15)] : 0.f;
+    bias4[0][nt] = *reinterpret_cast<const float4*>(d.bias + 16 * nt + 4 * (lane >> 4));
+    bias4[1][nt] = two ? *reinterpret_cast<const float4*>(d.bias2 + 16 * nt + 4 * (lane >> 4))
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -213,33 +228,36 @@ __global__ void __launch_bounds__(256, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nt], af[mt], acc[mt][nt], 0, 0, 0);
     }
     // ---- epilogue: the wave's 32x64 bf16 output image (rows rho = 0..31, 128 B each)
-    // lives in its own consumed A rows: piece rho/4 = plane rho/4, rows [32wv, 32wv+32)
+    // lives in its own consumed A rows: piece rho/4 = plane rho/4, rows [32wv, 32wv+32).
+    // 16-B chunk c of row rho sits at c ^ ((rho >> 1) & 7) (conflict-free 8-B writes).
     auto eaddr = [&](int rho) -> uint8_t* {
       return EPI_IN_A ? A + (rho >> 2) * PLANE + 32 * wv * 16 + (rho & 3) * 128
                       : Al + S2D_STAGES * ATILE + wv * 4096 + rho * 128;
     };
+    auto eswz = [&](int rho, int byte) -> int { return (((byte >> 4) ^ ((rho >> 1) & 7)) << 4) + (byte & 15); };
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int nt = 0; nt < 4; ++nt) {
+      const float4 bv = second ? bias4[1][nt] : bias4[0][nt];
+      const int cb = 2 * (16 * nt + 4 * (lane >> 4));
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int col = 16 * nt + (lane & 15);
-        const float bv = second ? bias_r[1][nt] : bias_r[0][nt];
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int row = 16 * mt + 4 * (lane >> 4) + jj;
-          *reinterpret_cast<bf16_t*>(eaddr(row) + col * 2) = f32_to_bf16(acc[mt][nt][jj] * d.in_scale + bv);
-        }
+      for (int mt = 0; mt < 2; ++mt) {
+        const int row = 16 * mt + (lane & 15);
+        const f32x4 a = acc[mt][nt];
+        const uint2 v = make_uint2(cvt_pk_bf16(a[0] * d.in_scale + bv.x, a[1] * d.in_scale + bv.y),
+                                   cvt_pk_bf16(a[2] * d.in_scale + bv.z, a[3] * d.in_scale + bv.w));
+        *reinterpret_cast<uint2*>(eaddr(row) + eswz(row, cb)) = v;
       }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int row = 8 * p + (lane >> 3), ch = lane & 7;
       const int m = tile * S2D_ROWS + 32 * wv + row;
-      uint4 v = *reinterpret_cast<const uint4*>(eaddr(row) + ch * 16);
+      uint4 v = *reinterpret_cast<const uint4*>(eaddr(row) + eswz(row, ch * 16));
       v = make_uint4(relu2(v.x), relu2(v.y), relu2(v.z), relu2(v.w));
       // out-of-range rows store into a dummy (keeps the per-iteration store count fixed)
       bf16_t* dst = (m < M) ? d.y + (int64_t)m * 64 + ch * 8 : (bf16_t*)d.scratch + lane * 8;

@@ -45,7 +45,12 @@ struct ConvDesc {
   const bf16_t* w2;           // weights for output rows >= m_switch (target network), or null
   const float* bias2;
   int m_switch;               // multiple of FWD_BM
-  int pad_;
+  // B operand stored K-major (bt != 0): element (k, n) at w + koff(cls, k/64) + (k%64)*ldb + n.
+  // Lets the dgrad GEMMs read the natural weight tensors (no transposed / flipped copies):
+  // bt = 1: koff from the table koff[cls * KT + kt]; bt = 2: koff = kt * 64 * ldb.
+  int bt;
+  int ldb;
+  int koff[16];
 };
 
 struct WgradDesc {
@@ -95,6 +100,22 @@ __device__ __forceinline__ uint32_t mask_bf16x2(uint32_t v, uint32_t m) {
   return lo | hi;
 }
 
+// MFMA fragment of 8 consecutive K rows (32kk + 8(lane>>4) .. +7) of column col0 + (lane&15)
+// from a K-major 64x64 bf16 image stored with swz_tr (two ds_read_b64_tr_b16).
+__device__ __forceinline__ bf16x8 tr_frag8(const uint8_t* img, int kk, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, pcol = lane & 3;
+  const int rA = 32 * kk + 8 * g + q;
+  const int cbyte = (col0 + 4 * pcol) * 2;  // byte offset of 4 columns inside the 128-B row
+  const int c16 = cbyte >> 4, within = cbyte & 15;
+  const lds_s16x4* pa = (const lds_s16x4*)(img + swz_tr(rA, c16) + within);
+  const lds_s16x4* pb = (const lds_s16x4*)(img + swz_tr(rA + 4, c16) + within);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pa));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pb));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // =====================================================================================
 // forward / dgrad implicit GEMM
 // =====================================================================================
@@ -120,7 +141,8 @@ __device__ __forceinline__ int epi_off(int r, int byte) {
 
 // MODE: A-operand source (0 dense, 1 NHWC implicit im2col, 2 legacy uint8 frames);
 // PAD: bounds-check im2col taps (padding / dgrad); pad==0 forward convs skip it.
-template <int MODE, bool PAD>
+// BT: B operand K-major (d.bt), read through the LDS transpose path.
+template <int MODE, bool PAD, bool BT>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * FWD_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -162,13 +184,19 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
       a_iw[i] = ow * d.stride;
     }
   }
-  const bf16_t* wrow0 = wb + (int64_t)(n0 + srow) * d.K + sc * 8;
-  const bf16_t* wrow1 = wrow0 + (int64_t)32 * d.K;
+  const bf16_t* wrow0 = BT ? wb + (int64_t)srow * d.ldb + n0 + sc * 8 : wb + (int64_t)(n0 + srow) * d.K + sc * 8;
+  const bf16_t* wrow1 = wrow0 + (BT ? (int64_t)32 * d.ldb : (int64_t)32 * d.K);
   const int cpb = d.Cin >> 6;
 
   auto load_tile = [&](int kt, FwdRegs& R) {
-    R.b0 = *reinterpret_cast<const uint4*>(wrow0 + (kt << 6));
-    R.b1 = *reinterpret_cast<const uint4*>(wrow1 + (kt << 6));
+    if (BT) {
+      const int64_t ko = d.bt == 2 ? (int64_t)kt * 64 * d.ldb : (int64_t)d.koff[cls * KT + kt];
+      R.b0 = *reinterpret_cast<const uint4*>(wrow0 + ko);
+      R.b1 = *reinterpret_cast<const uint4*>(wrow1 + ko);
+    } else {
+      R.b0 = *reinterpret_cast<const uint4*>(wrow0 + (kt << 6));
+      R.b1 = *reinterpret_cast<const uint4*>(wrow1 + (kt << 6));
+    }
     uint4 ra[4];
     if (MODE == 0) {
 #pragma unroll
@@ -216,8 +244,8 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
       uint4 v = (MODE == 2) ? u8x8_to_bf16x8(ra[i].x, ra[i].y) : ra[i];
       *reinterpret_cast<uint4*>(As + swz_row(r, sc)) = v;
     }
-    *reinterpret_cast<uint4*>(Bs + swz_row(srow, sc)) = R.b0;
-    *reinterpret_cast<uint4*>(Bs + swz_row(srow + 32, sc)) = R.b1;
+    *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow, sc) : swz_row(srow, sc))) = R.b0;
+    *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow + 32, sc) : swz_row(srow + 32, sc))) = R.b1;
   };
 
   // acc[mt][nt] holds C^T (channels x pixels): lane (g = lane>>4, p = lane&15) owns
@@ -241,7 +269,8 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
         a[mt] = *reinterpret_cast<const bf16x8*>(As + swz_row(32 * wv + 16 * mt + (lane & 15), c));
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
-        b[nt] = *reinterpret_cast<const bf16x8*>(Bs + swz_row(16 * nt + (lane & 15), c));
+        b[nt] = BT ? tr_frag8(Bs, s, 16 * nt, lane)
+                   : *reinterpret_cast<const bf16x8*>(Bs + swz_row(16 * nt + (lane & 15), c));
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -320,7 +349,20 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 #define WG_BR 64                         // reduction rows per step
 #define WG_TILE (WG_BR * 128)            // one 64x64 bf16 operand image (8 KB)
 
-template <int MODE>
+struct WgRegs {
+  uint4 d0, d1, x0, x1;
+};
+
+// a / D with D a compile-time constant when DC != 0 (multiply-shift), else runtime
+template <int DC>
+__device__ __forceinline__ uint32_t udiv(uint32_t a, uint32_t d) {
+  return DC ? a / (uint32_t)DC : a / d;
+}
+
+// MODE: X-operand source (0 dense rows, 1 NHWC im2col, 2 s2d uint8 frame ring).
+// OWC/OHWC: output width / pixels per image as compile-time constants for the
+// learner's shapes (0 = read from the descriptor).
+template <int MODE, int OWC, int OHWC>
 __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[4 * WG_TILE + 256 * 4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -329,87 +371,91 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
   const int split = blockIdx.z;
   const int r_begin = split * d.rows_per_split;
   const int r_end = min(d.Mred, r_begin + d.rows_per_split);
-  const int OHW = d.OH * d.OW;
+  const uint32_t OW = OWC ? OWC : d.OW;
+  const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
   const int sc = tid & 7, srow = tid >> 3;  // staging: rows srow, srow+32; chunk sc
   const bool do_bias = d.bias_slab != nullptr && kct == 0;
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-  // column-tile decode for the X operand
-  int tap = 0, cb = 0, kh = 0, kw = 0;
+  // column-tile decode of the X operand (block-uniform)
+  int kh = 0, kw = 0;
+  int64_t xoff = 0;
   if (MODE == 1) {
     const int cpb = d.Cin >> 6;
-    tap = kct / cpb;
-    cb = kct - tap * cpb;
+    const int tap = kct / cpb, cb = kct - tap * cpb;
     kh = tap / d.KW;
     kw = tap - kh * d.KW;
+    xoff = ((int64_t)(kh - d.pad_h) * d.W + (kw - d.pad_w)) * d.Cin + (cb << 6) + sc * 8;
   }
-  uint4 rdy[2], rx[2];
-
-  // MODE 2 stages the X tile with a different lane map: lane = reduction row
-  // (64 consecutive output pixels), wave = 16-B s2d block (2 bf16 chunks), so one
-  // load instruction reads 64 consecutive blocks of one frame row (contiguous).
+  // MODE 2 stages X with lane = reduction row, wave = 16-B s2d block (2 bf16 chunks):
+  // one load instruction reads 64 consecutive blocks of one frame row.
   const int x2_row = tid & 63, x2_blk = tid >> 6;
-  uint4 rx2 = make_uint4(0, 0, 0, 0);
-  auto load_x2 = [&](int r0) {
-    const int m = r0 + x2_row;
-    rx2 = make_uint4(0, 0, 0, 0);
-    if (m < r_end) {
-      const int img = m / OHW, rem = m - img * OHW;
-      const int oh = rem / d.OW, ow = rem - oh * d.OW;
-      const int q = 4 * kct + x2_blk;
-      const int tap = q / d.Cin, c = q - tap * d.Cin;
-      const int slot = d.frame_slots[img * d.Cin + c];
-      rx2 = *reinterpret_cast<const uint4*>((const uint8_t*)d.x + (int64_t)slot * 7056 +
-                                             (((oh + (tap >> 1)) * 21 + ow + (tap & 1)) << 4));
-    }
-  };
+  int x2_c = 0, x2_off = 0;
+  if (MODE == 2) {
+    const int q = 4 * kct + x2_blk;
+    const int tap = q / d.Cin;
+    x2_c = q - tap * d.Cin;
+    x2_off = (((tap >> 1) * 21 + (tap & 1)) << 4);
+  }
+  const bf16_t* dyb = d.dy + cot * 64 + sc * 8;
 
-  auto load_step = [&](int r0) {
+  auto load_step = [&](int r0, WgRegs& R) {
+    uint4 rd[2], rx[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int m = r0 + srow + 32 * i;
       const bool ok = m < r_end;
-      rdy[i] = ok ? *reinterpret_cast<const uint4*>(d.dy + (int64_t)m * d.ldd + cot * 64 + sc * 8)
-                  : make_uint4(0, 0, 0, 0);
+      const int mm = ok ? m : r_begin;
+      const uint4 v = *reinterpret_cast<const uint4*>(dyb + (int64_t)mm * d.ldd);
+      rd[i] = ok ? v : make_uint4(0, 0, 0, 0);
       if (MODE == 0) {
-        rx[i] = ok ? *reinterpret_cast<const uint4*>((const bf16_t*)d.x + (int64_t)m * d.ldx + kct * 64 + sc * 8)
-                   : make_uint4(0, 0, 0, 0);
-      } else {
-        const int mm = ok ? m : 0;
-        const int img = mm / OHW, rem = mm - img * OHW;
-        const int oh = rem / d.OW, ow = rem - oh * d.OW;
-        if (MODE == 1) {
-          const int ih = oh * d.stride - d.pad_h + kh, iw = ow * d.stride - d.pad_w + kw;
-          const bool ok2 = ok && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
-          const bf16_t* src =
-              (const bf16_t*)d.x + ((((int64_t)img * d.H + ih) * d.W + iw) * d.Cin + (cb << 6) + sc * 8);
-          rx[i] = ok2 ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
-        }
+        const uint4 x = *reinterpret_cast<const uint4*>((const bf16_t*)d.x + (int64_t)mm * d.ldx + kct * 64 + sc * 8);
+        rx[i] = ok ? x : make_uint4(0, 0, 0, 0);
+      } else if (MODE == 1) {
+        const uint32_t img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
+        const uint32_t oh = udiv<OWC>(rem, OW), ow = rem - oh * OW;
+        const int ih = oh * d.stride + kh - d.pad_h, iw = ow * d.stride + kw - d.pad_w;
+        const bool ok2 = ok && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
+        const int64_t pix = ((int64_t)img * d.H + oh * d.stride) * d.W + ow * d.stride;
+        const bf16_t* src = ok2 ? (const bf16_t*)d.x + pix * d.Cin + xoff : (const bf16_t*)d.x;
+        const uint4 x = *reinterpret_cast<const uint4*>(src);
+        rx[i] = ok2 ? x : make_uint4(0, 0, 0, 0);
       }
     }
-    if (MODE == 2) load_x2(r0);
+    if (MODE == 2) {
+      const int m = r0 + x2_row;
+      const bool ok = m < r_end;
+      const uint32_t mm = ok ? m : r_begin;
+      const uint32_t img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
+      const uint32_t oh = udiv<OWC>(rem, OW), ow = rem - oh * OW;
+      const int slot = d.frame_slots[img * d.Cin + x2_c];
+      const uint4 x = *reinterpret_cast<const uint4*>((const uint8_t*)d.x + (int64_t)slot * 7056 +
+                                                      ((oh * 21 + ow) << 4) + x2_off);
+      rx[0] = ok ? x : make_uint4(0, 0, 0, 0);
+      rx[1] = rx[0];
+    }
+    R.d0 = rd[0]; R.d1 = rd[1]; R.x0 = rx[0]; R.x1 = rx[1];
   };
 
-  auto write_step = [&](int buf) {
+  auto write_step = [&](int buf, const WgRegs& R) {
     uint8_t* Ds = smem + buf * 2 * WG_TILE;
     uint8_t* Xs = Ds + WG_TILE;
+    *reinterpret_cast<uint4*>(Ds + swz_tr(srow, sc)) = R.d0;
+    *reinterpret_cast<uint4*>(Ds + swz_tr(srow + 32, sc)) = R.d1;
+    if (MODE != 2) {
+      *reinterpret_cast<uint4*>(Xs + swz_tr(srow, sc)) = R.x0;
+      *reinterpret_cast<uint4*>(Xs + swz_tr(srow + 32, sc)) = R.x1;
+    } else {
+      // 16 uint8 of one s2d block -> two 16-B bf16 chunks (2 x2_blk, 2 x2_blk + 1) of row x2_row
+      *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk)) = u8x8_to_bf16x8(R.x0.x, R.x0.y);
+      *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk + 1)) = u8x8_to_bf16x8(R.x0.z, R.x0.w);
+    }
+    if (do_bias) {
+      const uint32_t w8[8] = {R.d0.x, R.d0.y, R.d0.z, R.d0.w, R.d1.x, R.d1.y, R.d1.z, R.d1.w};
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = srow + 32 * i;
-      *reinterpret_cast<uint4*>(Ds + swz_tr(r, sc)) = rdy[i];
-      if (MODE != 2) *reinterpret_cast<uint4*>(Xs + swz_tr(r, sc)) = rx[i];
-      if (MODE == 2 && i == 0) {
-        // 16 uint8 of one s2d block -> two 16-B bf16 chunks (2 x2_blk, 2 x2_blk + 1) of row x2_row
-        *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk)) = u8x8_to_bf16x8(rx2.x, rx2.y);
-        *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk + 1)) = u8x8_to_bf16x8(rx2.z, rx2.w);
-      }
-      if (do_bias) {
-        const uint32_t w4[4] = {rdy[i].x, rdy[i].y, rdy[i].z, rdy[i].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          bsum[2 * j] += __uint_as_float(w4[j] << 16);
-          bsum[2 * j + 1] += __uint_as_float(w4[j] & 0xffff0000u);
-        }
+      for (int j = 0; j < 8; ++j) {
+        bsum[2 * (j & 3)] += __uint_as_float(w8[j] << 16);
+        bsum[2 * (j & 3) + 1] += __uint_as_float(w8[j] & 0xffff0000u);
       }
     }
   };
@@ -422,49 +468,45 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // transposed-read lane geometry: group g = lane>>4, within group q = (lane>>2)&3 (row), p = lane&3 (cols)
-  const int g = lane >> 4, q = (lane >> 2) & 3, pcol = lane & 3;
-
-  auto tr_frag = [&](const uint8_t* img, int kk, int col0) -> bf16x8 {
-    // 8 consecutive reduction rows (32kk + 8g .. +7) of column col0 + (lane & 15)
-    const int rA = 32 * kk + 8 * g + q;
-    const int cbyte = (col0 + 4 * pcol) * 2;  // byte offset of 4 columns inside the 128-B row
-    const int c16 = cbyte >> 4, within = cbyte & 15;
-    const lds_s16x4* pa = (const lds_s16x4*)(img + swz_tr(rA, c16) + within);
-    const lds_s16x4* pb = (const lds_s16x4*)(img + swz_tr(rA + 4, c16) + within);
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pa));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pb));
-    typedef short s16x8 __attribute__((ext_vector_type(8)));
-    s16x8 v = (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  };
-
-  const int nsteps = (r_end - r_begin + WG_BR - 1) / WG_BR;
-  if (nsteps > 0) {
-    load_step(r_begin);
-    write_step(0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    const int cur = st & 1;
-    if (st + 1 < nsteps) load_step(r_begin + (st + 1) * WG_BR);
-    const uint8_t* Ds = smem + cur * 2 * WG_TILE;
+  auto compute = [&](int buf) {
+    const uint8_t* Ds = smem + buf * 2 * WG_TILE;
     const uint8_t* Xs = Ds + WG_TILE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 a[2], b[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) a[t] = tr_frag(Ds, kk, wco + 16 * t);
+      for (int t = 0; t < 2; ++t) a[t] = tr_frag8(Ds, kk, wco + 16 * t, lane);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) b[t] = tr_frag(Xs, kk, wkc + 16 * t);
+      for (int t = 0; t < 2; ++t) b[t] = tr_frag8(Xs, kk, wkc + 16 * t, lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (st + 1 < nsteps) write_step(cur ^ 1);
+  };
+
+  // Same two-register-stage / two-LDS-stage pipeline as igemm_fwd: step t's global
+  // loads are issued two steps ahead of its MFMAs.
+  const int ns = (r_end - r_begin + WG_BR - 1) / WG_BR;
+  WgRegs RA, RB;
+  if (ns > 0) {
+    load_step(r_begin, RA);
+    if (ns > 1) load_step(r_begin + WG_BR, RB);
+    write_step(0, RA);
+  }
+  __syncthreads();
+  if (ns > 2) load_step(r_begin + 2 * WG_BR, RA);
+  for (int t = 0; t < ns; t += 2) {
+    compute(0);
+    if (t + 1 < ns) write_step(1, RB);
     __syncthreads();
+    if (t + 3 < ns) load_step(r_begin + (t + 3) * WG_BR, RB);
+    if (t + 1 >= ns) break;
+    compute(1);
+    if (t + 2 < ns) write_step(0, RA);
+    __syncthreads();
+    if (t + 4 < ns) load_step(r_begin + (t + 4) * WG_BR, RA);
   }
 
   // ---- store the fp32 partial tile: slab[split][co][kc]
@@ -503,40 +545,56 @@ __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
   }
 }
 
-// sum fp32 slabs over splits -> fp32 gradient (scaled), and the bias partials.
-// Block = 64 float4 columns x 16 split-groups (1024 threads): each thread sums
-// every 16th split, then an LDS tree finishes -- 16x more loads in flight than
-// a thread-per-column loop over all splits.
-__global__ void __launch_bounds__(1024) slab_reduce_kernel(const float* __restrict__ slab, int nsplit, int64_t n,
-                                                           float scale, float* __restrict__ out,
-                                                           const float* __restrict__ bslab, int nb,
-                                                           float* __restrict__ bout) {
-  __shared__ float4 red[16][64];
-  const int lc = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int64_t c4 = (int64_t)blockIdx.x * 64 + lc;
+// Sum the fp32 split-K slabs -> fp32 gradient (scaled) and the bias partials.
+// Block = 16 float4 columns x 16 split groups (256 threads): every thread keeps
+// its loads independent (nsplit/16 in flight), an LDS tree finishes, and the
+// grid has n/64 blocks so even the 16K-element conv1 gradient fills the chip.
+// The last ceil(nb/64) blocks reduce the bias slab the same way.
+// s2dC > 0: the slab is in conv1's space-to-depth K order (csrc/conv1_s2d.hip);
+// the store permutes it back to OIHW (each float4 = 4 consecutive kw: contiguous).
+__global__ void __launch_bounds__(256) slab_reduce_kernel(const float* __restrict__ slab, int nsplit, int64_t n,
+                                                          float scale, float* __restrict__ out,
+                                                          const float* __restrict__ bslab, int nb,
+                                                          float* __restrict__ bout, int s2dC, int Kc) {
+  __shared__ float4 red[16][16];
+  const int lc = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t nwb = (n / 4 + 15) / 16;
+  const bool bias = blockIdx.x >= nwb;
+  const float* src = bias ? bslab : slab;
+  const int64_t stride = bias ? nb : n;
+  const int64_t n4 = bias ? nb / 4 : n / 4;
+  const int64_t c4 = (bias ? (int64_t)(blockIdx.x - nwb) : (int64_t)blockIdx.x) * 16 + lc;
   float4 s = make_float4(0, 0, 0, 0);
-  if (c4 * 4 < n) {
+  if (c4 < n4) {
+#pragma unroll 4
     for (int k = grp; k < nsplit; k += 16) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + (int64_t)k * n + c4 * 4);
+      const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)k * stride + c4 * 4);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
   }
   red[grp][lc] = s;
   __syncthreads();
-  if (grp == 0 && c4 * 4 < n) {
+  if (grp == 0 && c4 < n4) {
     float4 a = red[0][lc];
 #pragma unroll
     for (int g = 1; g < 16; ++g) {
       const float4 b = red[g][lc];
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
+    if (bias) {
+      *reinterpret_cast<float4*>(bout + c4 * 4) = a;
+      return;
+    }
     a.x *= scale; a.y *= scale; a.z *= scale; a.w *= scale;
-    *reinterpret_cast<float4*>(out + c4 * 4) = a;
-  }
-  if (bslab != nullptr && blockIdx.x == 0 && threadIdx.x < nb) {
-    float b = 0.f;
-    for (int k = 0; k < nsplit; ++k) b += bslab[(int64_t)k * nb + threadIdx.x];
-    bout[threadIdx.x] = b;
+    int64_t o = c4 * 4;
+    if (s2dC > 0) {
+      const int64_t row = o / Kc;
+      const int k = (int)(o - row * Kc);
+      const int q = k >> 4, r4 = (k >> 2) & 3;
+      const int tap = q / s2dC, c = q - tap * s2dC;
+      o = row * Kc + (c * 8 + 4 * (tap >> 1) + r4) * 8 + 4 * (tap & 1);
+    }
+    *reinterpret_cast<float4*>(out + o) = a;
   }
 }
 
@@ -587,10 +645,14 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   const int M = d.N * d.OH * d.OW;
   dim3 grid((M + FWD_BM - 1) / FWD_BM, d.Cout / FWD_BN, d.ncls > 0 ? d.ncls : 1);
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
-  if (d.mode == 0) igemm_fwd_kernel<0, false><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1 && pad) igemm_fwd_kernel<1, true><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1) igemm_fwd_kernel<1, false><<<grid, 256, 0, st>>>(d);
-  else igemm_fwd_kernel<2, false><<<grid, 256, 0, st>>>(d);
+  if (d.bt == 1 && (d.K >> 6) * (d.ncls > 0 ? d.ncls : 1) > 16) return (int)hipErrorInvalidValue;
+  if (d.bt && d.mode == 2) return (int)hipErrorInvalidValue;
+  if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0) igemm_fwd_kernel<0, false, false><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1 && d.bt) igemm_fwd_kernel<1, true, true><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1 && pad) igemm_fwd_kernel<1, true, false><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1) igemm_fwd_kernel<1, false, false><<<grid, 256, 0, st>>>(d);
+  else igemm_fwd_kernel<2, false, false><<<grid, 256, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }
 
@@ -598,16 +660,21 @@ APEX_EXPORT int apex_conv_wgrad(WgradDesc d, float* out, float* bout, int nsplit
   if ((d.Kc & 63) || (d.Co & 63)) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
   dim3 grid(d.Kc / 64, d.Co / 64, nsplit);
-  if (d.mode == 0) igemm_wgrad_kernel<0><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1) igemm_wgrad_kernel<1><<<grid, 256, 0, st>>>(d);
-  else igemm_wgrad_kernel<2><<<grid, 256, 0, st>>>(d);
+  // learner shapes get compile-time output geometry (conv3 7x7, conv2 9x9, conv1 20x20)
+  if (d.mode == 0) igemm_wgrad_kernel<0, 1, 1><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1 && d.OH == 7 && d.OW == 7) igemm_wgrad_kernel<1, 7, 49><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1 && d.OH == 9 && d.OW == 9) igemm_wgrad_kernel<1, 9, 81><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 1) igemm_wgrad_kernel<1, 0, 0><<<grid, 256, 0, st>>>(d);
+  else if (d.OH == 20 && d.OW == 20) igemm_wgrad_kernel<2, 20, 400><<<grid, 256, 0, st>>>(d);
+  else igemm_wgrad_kernel<2, 0, 0><<<grid, 256, 0, st>>>(d);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   if (out != nullptr) {
     const int64_t n = (int64_t)d.Co * d.Kc;
-    if (d.bias_slab != nullptr && d.Co > 1024) return (int)hipErrorInvalidValue;
-    slab_reduce_kernel<<<(int)((n / 4 + 63) / 64), 1024, 0, st>>>(d.slab, nsplit, n, scale, out, d.bias_slab,
-                                                                  d.bias_slab ? d.Co : 0, bout);
+    const int nb = d.bias_slab ? d.Co : 0;
+    const int64_t blocks = (n / 4 + 15) / 16 + (nb / 4 + 15) / 16;
+    slab_reduce_kernel<<<(int)blocks, 256, 0, st>>>(d.slab, nsplit, n, scale, out, d.bias_slab, nb, bout,
+                                                    d.mode == 2 ? d.Cin : 0, d.Kc);
   }
   APEX_CHECK_LAUNCH();
 }

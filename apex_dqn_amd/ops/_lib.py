@@ -50,7 +50,8 @@ class ConvDesc(ctypes.Structure):
                 ("mode", c_i), ("relu", c_i), ("ldy", c_i), ("ncls", c_i),
                 ("ostride_h", c_i), ("ostride_w", c_i), ("OHfull", c_i), ("OWfull", c_i),
                 ("K", c_i), ("in_scale", c_f), ("w_cls_stride", c_i64),
-                ("w2", c_p), ("bias2", c_p), ("m_switch", c_i), ("pad_", c_i)]
+                ("w2", c_p), ("bias2", c_p), ("m_switch", c_i),
+                ("bt", c_i), ("ldb", c_i), ("koff", c_i * 16)]
 
 
 class WgradDesc(ctypes.Structure):

@@ -48,6 +48,9 @@ def _conv_desc(**kw) -> "_lib.ConvDesc":
     d.w2 = kw.get("w2")
     d.bias2 = kw.get("bias2")
     d.m_switch = kw.get("m_switch", 0)
+    d.bt, d.ldb = kw.get("bt", 0), kw.get("ldb", 0)
+    for i, v in enumerate(kw.get("koff", ())):
+        d.koff[i] = v
     return d
 
 
@@ -94,12 +97,12 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
     assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
     d = _lib.Conv1S2DDesc()
     d.ring, d.slots, d.y = ring.data_ptr(), slots.data_ptr(), out.data_ptr()
-    d.w = pack_w1_s2d(lib, ws, w1, "a").data_ptr()
+    d.w = w1.data_ptr()  # OIHW: the kernel gathers the s2d K order into LDS
     d.bias = b1.data_ptr()
     if w2 is not None:
         if (rows_first * 400) % 128:
             raise ValueError("online/target split must fall on a 128-row tile boundary")
-        d.w2 = pack_w1_s2d(lib, ws, w2, "b").data_ptr()
+        d.w2 = w2.data_ptr()
         d.bias2 = b2.data_ptr()
         d.m_switch = rows_first * 400
     zero = ws.get(("zero16",), 64, ring.device, torch.uint8)
@@ -137,21 +140,45 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
     _launch_fwd(lib, d)
 
 
-def conv3_dgrad(lib, dy: torch.Tensor, w3tf: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
-    """dX2 (9x9) from dY3 (7x7): full correlation with the flipped/transposed 3x3 weights."""
-    N = dy.shape[0]
-    d = _conv_desc(x=dy.data_ptr(), w=w3tf.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=7, W=7,
-                   Cin=64, OH=9, OW=9, Cout=64, KH=3, KW=3, stride=1, pad=2, mode=1, K=576)
+# K-major B-operand offsets for the dgrad GEMMs reading the natural OHWI weights.
+# conv3: k-tile = output tap t of the 3x3 correlation -> weight tap 8 - t (flipped).
+_KOFF3 = tuple((8 - t) * 64 for t in range(9))
+# conv2 parity class (p, q), k-tile (a, b) -> weight tap (p + 2(1-a), q + 2(1-b)).
+_KOFF2 = tuple(((p + 2 * (1 - a)) * 4 + (q + 2 * (1 - b))) * 64
+               for p in range(2) for q in range(2) for a in range(2) for b in range(2))
+
+
+def dense_dgrad(lib, dh: torch.Tensor, w: torch.Tensor, out: torch.Tensor, mask: torch.Tensor) -> None:
+    """out[M,K] = (dh[M,N] @ w[N,K]) * (mask > 0): the B operand is read K-major
+    straight from the natural [N][K] weight (no transposed copy)."""
+    M, Nn = dh.shape
+    K = w.shape[1]
+    assert w.shape[0] == Nn and out.shape == (M, K)
+    d = _conv_desc(x=dh.data_ptr(), w=w.data_ptr(), y=out.data_ptr(), mask=_lib.ptr(mask), N=M, Cin=Nn,
+                   Cout=K, mode=0, K=Nn, bt=2, ldb=K)
     _launch_fwd(lib, d)
 
 
-def conv2_dgrad(lib, dy: torch.Tensor, w2t: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
-    """dX1 (20x20) from dY2 (9x9), 4x4 stride 2: four stride-parity classes, each a
-    2x2 stride-1 correlation (pad 1) writing every other output pixel."""
+def conv3_dgrad(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
+    """dX2 (9x9) from dY3 (7x7): full correlation with the flipped 3x3 weights, read
+    K-major from the OHWI weight (co rows, ci columns)."""
     N = dy.shape[0]
-    d = _conv_desc(x=dy.data_ptr(), w=w2t.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
+    assert w3.shape == (64, 3, 3, 64)
+    d = _conv_desc(x=dy.data_ptr(), w=w3.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=7, W=7,
+                   Cin=64, OH=9, OW=9, Cout=64, KH=3, KW=3, stride=1, pad=2, mode=1, K=576,
+                   bt=1, ldb=576, koff=_KOFF3)
+    _launch_fwd(lib, d)
+
+
+def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
+    """dX1 (20x20) from dY2 (9x9), 4x4 stride 2: four stride-parity classes, each a
+    2x2 stride-1 correlation (pad 1) writing every other output pixel; weights read
+    K-major from the OHWI tensor per class."""
+    N = dy.shape[0]
+    assert w2.shape == (64, 4, 4, 64)
+    d = _conv_desc(x=dy.data_ptr(), w=w2.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
                    Cin=64, OH=10, OW=10, Cout=64, KH=2, KW=2, stride=1, pad=1, mode=1, K=256, ncls=4,
-                   ostride=2, OHfull=20, OWfull=20, w_cls_stride=64 * 256)
+                   ostride=2, OHfull=20, OWfull=20, bt=1, ldb=1024, koff=_KOFF2)
     _launch_fwd(lib, d)
 
 
@@ -174,9 +201,13 @@ def _splits(Mred: int, per_img: int, target_rows: int) -> Tuple[int, int]:
 
 
 def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, stride: int,
-               dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1024) -> None:
-    """dW (OHWI, fp32) and db for an NHWC conv with 64 output channels."""
+               dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 0) -> None:
+    """dW (OHWI, fp32) and db for an NHWC conv with 64 output channels.
+    ``target_rows``: reduction rows per split-K block (0 = tuned default: fewer
+    rows for the small 3x3 layer, whose 9 output tiles need more splits)."""
     N, OH, OW, Co = dy.shape
+    if target_rows <= 0:
+        target_rows = 512 if KH == 3 else 1024
     _, H, W, Cin = x.shape
     Kc = KH * KH * Cin
     Mred = N * OH * OW
@@ -191,7 +222,7 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
 
 
 def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
-                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 3200) -> None:
+                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1600) -> None:
     N, OH, OW, Co = dy.shape
     C = slots.shape[1]
     Kc = C * 64
@@ -199,14 +230,12 @@ def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, s
     nsplit, rows = _splits(Mred, OH * OW, target_rows)
     slab = ws.get(("wg1", Co, Kc), nsplit * Co * Kc, dy.device)
     bslab = ws.get(("wg1b", Co), nsplit * Co, dy.device)
-    tmp = ws.get(("wg1s", Co, Kc), Co * Kc, dy.device)  # dW in s2d K order
     d = _wg_desc(dy=dy.data_ptr(), x=ring.data_ptr(), frame_slots=slots.data_ptr(), slab=slab.data_ptr(),
                  bias_slab=bslab.data_ptr(), N=N, H=ring.shape[1], W=ring.shape[2], Cin=C, OH=OH, OW=OW,
                  KH=8, KW=8, stride=4, mode=2, Co=Co, Kc=Kc, ldd=Co, rows_per_split=rows, Mred=Mred)
-    _lib.check(lib.apex_conv_wgrad(d, tmp.data_ptr(), db_out.data_ptr(), nsplit, float(scale),
+    # the slab reduce permutes the s2d K order back to OIHW while storing
+    _lib.check(lib.apex_conv_wgrad(d, dw_out.data_ptr(), db_out.data_ptr(), nsplit, float(scale),
                                    _lib.stream_ptr()), "conv1_wgrad")
-    _lib.check(lib.apex_s2d_unpack_w1_grad(tmp.data_ptr(), dw_out.data_ptr(), C, _lib.stream_ptr()),
-               "s2d_unpack")
 
 
 def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor) -> None:

@@ -183,19 +183,10 @@ class HipBackend(TorchBackend):
         if self.native_conv:
             self.kernels += ["conv_fwd", "conv_dgrad", "conv_wgrad", "fc_fwd", "fc_bwd"]
         self.ws = C.Workspace()
-        self._packed = None
 
     # --------------------------------------------------- native conv family
-    def prepare(self, Pb) -> None:
-        if not self.native_conv:
-            return
-        if self._packed is None:
-            dev = Pb["wfc"].device
-            self._packed = dict(wfcT=torch.empty(3136, 1024, dtype=torch.bfloat16, device=dev),
-                                w3tf=torch.empty(64, 576, dtype=torch.bfloat16, device=dev),
-                                w2t=torch.empty(4, 64, 256, dtype=torch.bfloat16, device=dev))
-        k = self._packed
-        C.pack_dgrad_weights(self.lib, Pb["wfc"], Pb["w3"], Pb["w2"], k["wfcT"], k["w3tf"], k["w2t"])
+    # prepare(): nothing to do -- the dgrad GEMMs read the natural weight tensors
+    # K-major (transposed LDS reads) and conv1 reads OIHW w1 directly.
 
     def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0):
         if not self.native_conv:
@@ -217,17 +208,16 @@ class HipBackend(TorchBackend):
         if not self.native_conv:
             return super().fc_bwd(dh, x, w, dx_out, dw_out, db_out)
         xf = x.reshape(x.shape[0], -1)
-        C.dense_fwd(self.lib, dh, self._packed["wfcT"], None, dx_out.reshape(dh.shape[0], -1), relu=False,
-                    mask=xf)
+        C.dense_dgrad(self.lib, dh, w, dx_out.reshape(dh.shape[0], -1), xf)
         C.dense_wgrad(self.lib, dh, xf, dw_out, db_out)
 
     def conv_dgrad(self, dy, w, stride, x_src, dx_out):
         if not self.native_conv:
             return super().conv_dgrad(dy, w, stride, x_src, dx_out)
         if stride == 1:
-            C.conv3_dgrad(self.lib, dy, self._packed["w3tf"], x_src, dx_out)
+            C.conv3_dgrad(self.lib, dy, w, x_src, dx_out)
         else:
-            C.conv2_dgrad(self.lib, dy, self._packed["w2t"], x_src, dx_out)
+            C.conv2_dgrad(self.lib, dy, w, x_src, dx_out)
 
     def conv_wgrad(self, dy, x, k, stride, dw_out, db_out):
         if not self.native_conv:

@@ -46,10 +46,6 @@ def main():
     dY3 = rn(B, 7, 7, 64)
     dY2 = rn(B, 9, 9, 64)
     dY1 = rn(B, 20, 20, 64)
-    wfcT = torch.empty(3136, 1024, device=dev, dtype=bf)
-    w3tf = torch.empty(64, 576, device=dev, dtype=bf)
-    w2tt = torch.empty(4, 64, 256, device=dev, dtype=bf)
-    C.pack_dgrad_weights(lib, wfc, w3, w2, wfcT, w3tf, w2tt)
     ws = C.Workspace()
     gw = torch.empty(1024 * 3136, device=dev)
     gb = torch.empty(1024, device=dev)
@@ -61,19 +57,29 @@ def main():
         "conv3_fwd": (lambda: C.conv_fwd(lib, y2, w3, bias[:64], 1, y3, w3t, bias[:64], 2 * B), F(N3 * 49 * 64 * 576)),
         "fc_fwd": (lambda: C.dense_fwd(lib, y3.reshape(N3, 3136), wfc, bias, h, True, None, wfct, bias, 2 * B),
                    F(N3 * 1024 * 3136)),
-        "fc_dgrad": (lambda: C.dense_fwd(lib, dH, wfcT, None, dY3.reshape(B, 3136), False, y3[:B].reshape(B, 3136)),
+        "fc_dgrad": (lambda: C.dense_dgrad(lib, dH, wfc, dY3.reshape(B, 3136), y3[:B].reshape(B, 3136)),
                      F(B * 3136 * 1024)),
         "fc_wgrad": (lambda: C.dense_wgrad(lib, dH, y3[:B].reshape(B, 3136), gw.view(1024, 3136), gb),
                      F(B * 3136 * 1024)),
-        "conv3_dgrad": (lambda: C.conv3_dgrad(lib, dY3, w3tf, y2[:B], dY2), F(B * 81 * 64 * 576)),
+        "conv3_dgrad": (lambda: C.conv3_dgrad(lib, dY3, w3, y2[:B], dY2), F(B * 81 * 64 * 576)),
         "conv3_wgrad": (lambda: C.conv_wgrad(lib, ws, dY3, y2[:B], 3, 1, gw[:64 * 576].view(64, 3, 3, 64), gb[:64]),
                         F(B * 49 * 64 * 576)),
-        "conv2_dgrad": (lambda: C.conv2_dgrad(lib, dY2, w2tt, y1[:B], dY1), F(B * 400 * 64 * 256)),
+        "conv2_dgrad": (lambda: C.conv2_dgrad(lib, dY2, w2, y1[:B], dY1), F(B * 400 * 64 * 256)),
         "conv2_wgrad": (lambda: C.conv_wgrad(lib, ws, dY2, y1[:B], 4, 2, gw[:64 * 1024].view(64, 4, 4, 64), gb[:64]),
                         F(B * 81 * 64 * 1024)),
         "conv1_wgrad": (lambda: C.conv1_wgrad_ring(lib, ws, dY1, ring, slots[:B], 1 / 255., gw[:64 * 256].view(64, 4, 8, 8),
                                                    gb[:64]), F(B * 400 * 64 * 256)),
     }
+    # split-size variants of the weight-gradient kernels (rows of the reduction per block)
+    for tr in (256, 512, 2048):
+        ops[f"conv3_wgrad@{tr}"] = (lambda tr=tr: C.conv_wgrad(lib, ws, dY3, y2[:B], 3, 1, gw[:64 * 576].view(64, 3, 3, 64),
+                                                              gb[:64], target_rows=tr), F(B * 49 * 64 * 576))
+        ops[f"conv2_wgrad@{tr}"] = (lambda tr=tr: C.conv_wgrad(lib, ws, dY2, y1[:B], 4, 2, gw[:64 * 1024].view(64, 4, 4, 64),
+                                                              gb[:64], target_rows=tr), F(B * 81 * 64 * 1024))
+    for tr in (800, 1600, 6400):
+        ops[f"conv1_wgrad@{tr}"] = (lambda tr=tr: C.conv1_wgrad_ring(lib, ws, dY1, ring, slots[:B], 1 / 255.,
+                                                                    gw[:64 * 256].view(64, 4, 8, 8), gb[:64],
+                                                                    target_rows=tr), F(B * 400 * 64 * 256))
     total = 0.0
     for name, (fn, flops) in ops.items():
         if a.only and name not in a.only.split(","):
@@ -88,7 +94,8 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = 1e3 * e0.elapsed_time(e1) / a.iters
-        total += us
+        if "@" not in name:
+            total += us
         print(json.dumps({"op": name, "us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}), flush=True)
     print(json.dumps({"op": "TOTAL", "us": round(total, 1)}))
 

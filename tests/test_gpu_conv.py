@@ -81,6 +81,11 @@ def test_dense_fwd_relu_and_mask(M):
     C.dense_fwd(_lib(), dh, wT, None, out2, relu=False, mask=mask)
     ref2 = (dh.float() @ wT.float().t()) * (mask.float() > 0)
     assert _rel(out2, ref2) < 1e-2
+    # K-major B operand (fc dgrad straight from the natural [1024][3136] weight)
+    out3 = torch.empty(M, 3136, dtype=torch.bfloat16, device=DEV)
+    C.dense_dgrad(_lib(), dh, w, out3, mask)
+    ref3 = (dh.float() @ w.float()) * (mask.float() > 0)
+    assert _rel(out3, ref3) < 1e-2
 
 
 def test_pack_dgrad_weights():
@@ -109,23 +114,18 @@ def test_conv_dgrad_layers(N):
     lib = _lib()
     w3 = _bf(torch.randn(64, 3, 3, 64, generator=g) * 0.04)
     w2 = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
-    wfc = _bf(torch.randn(1024, 3136, generator=g) * 0.02)
-    wfcT = torch.empty(3136, 1024, dtype=torch.bfloat16, device=DEV)
-    w3tf = torch.empty(64, 576, dtype=torch.bfloat16, device=DEV)
-    w2t = torch.empty(4, 64, 256, dtype=torch.bfloat16, device=DEV)
-    C.pack_dgrad_weights(lib, wfc, w3, w2, wfcT, w3tf, w2t)
     # conv3 dgrad: dY3 (7x7) -> dX2 (9x9) masked by y2
     dy3 = _bf(torch.randn(N, 7, 7, 64, generator=g))
     y2 = _bf(torch.randn(N, 9, 9, 64, generator=g))
     out = torch.empty(N, 9, 9, 64, dtype=torch.bfloat16, device=DEV)
-    C.conv3_dgrad(lib, dy3, w3tf, y2, out)
+    C.conv3_dgrad(lib, dy3, w3, y2, out)
     ref = R.conv_dgrad(dy3.float(), w3.float(), (N, 9, 9, 64), 1, y2.float())
     assert _rel(out, ref) < 1e-2
     # conv2 dgrad: dY2 (9x9) -> dX1 (20x20), stride 2, masked by y1
     dy2 = _bf(torch.randn(N, 9, 9, 64, generator=g))
     y1 = _bf(torch.randn(N, 20, 20, 64, generator=g))
     out1 = torch.empty(N, 20, 20, 64, dtype=torch.bfloat16, device=DEV)
-    C.conv2_dgrad(lib, dy2, w2t, y1, out1)
+    C.conv2_dgrad(lib, dy2, w2, y1, out1)
     ref1 = R.conv_dgrad(dy2.float(), w2.float(), (N, 20, 20, 64), 2, y1.float())
     assert _rel(out1, ref1) < 1e-2
 
