@@ -32,6 +32,21 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// full-wave float sum without the LDS crossbar: DPP quad / row rotations reduce each
+// 16-lane row, four v_readlane finish.  Result is wave-uniform.
+#define APEX_DPP_ADD(v, ctrl)                                                                          \
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  APEX_DPP_ADD(v, 0xB1);   // quad_perm(1,0,3,2)
+  APEX_DPP_ADD(v, 0x4E);   // quad_perm(2,3,0,1)
+  APEX_DPP_ADD(v, 0x124);  // row_ror:4
+  APEX_DPP_ADD(v, 0x128);  // row_ror:8
+  return (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_max(T v) {
 #pragma unroll

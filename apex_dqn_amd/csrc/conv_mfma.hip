@@ -8,12 +8,11 @@
 //              A-operand modes: 0 dense bf16 rows (fc fwd / fc dgrad),
 //                               1 NHWC bf16 implicit im2col (conv2/conv3 fwd,
 //                                 conv3 dgrad, conv2 dgrad per stride-parity class),
-//                               2 uint8 frames gathered straight from the replay
-//                                 frame ring by slot index (conv1 fwd: the frame
-//                                 stack is assembled in LDS, never in HBM).
+//              (conv1 forward runs on the space-to-depth ring: csrc/conv1_s2d.hip);
+//              B operand row-major [N][K] or K-major (dgrad reads natural weights).
 //  igemm_wgrad dW[Co,Kc] = sum_m dY[m,Co] . X[m,Kc]   (split over m, fp32 slabs),
 //              both operands read column-wise from LDS with ds_read_b64_tr_b16
-//              (the hardware transpose read), conv1 again gathering uint8 frames.
+//              (the hardware transpose read); conv1 gathers uint8 s2d frame blocks.
 //
 // Tiles: fwd 128x64x64 (4 waves, 32x64 per wave, v_mfma_f32_16x16x32_bf16);
 // wgrad 64x64 per block over 64-row reduction steps.  LDS images are XOR
@@ -29,7 +28,7 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 struct ConvDesc {
   const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]; mode 2: u8 frame ring
-  const int32_t* frame_slots; // mode 2: [N][Cin] frame-ring slot per (image, stacked frame)
+  const int32_t* frame_slots; // unused (conv1 runs in csrc/conv1_s2d.hip)
   const bf16_t* w;            // B operand [Cout][K] (K contiguous), + cls * w_cls_stride
   const float* bias;          // [Cout] or null
   bf16_t* y;                  // output rows of ldy elements
@@ -139,8 +138,20 @@ __device__ __forceinline__ int epi_off(int r, int byte) {
   return (r << 7) + ((((byte >> 4) ^ ((r >> 1) & 7))) << 4) + (byte & 15);
 }
 
-// MODE: A-operand source (0 dense, 1 NHWC implicit im2col, 2 legacy uint8 frames);
-// PAD: bounds-check im2col taps (padding / dgrad); pad==0 forward convs skip it.
+// Raw buffer resource over a tensor (< 2 GB): loads with a 32-bit per-lane byte
+// offset (loop-invariant VGPR) + a scalar k-tile offset (SGPR), and an offset of
+// BUF_OOB reads zeros (hardware range check) -- no per-element selects or branches.
+#define BUF_OOB 0x80000000u
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7ffffff0, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+// MODE: A-operand source (0 dense rows, 1 NHWC implicit im2col).
+// PAD: im2col taps may fall outside the input (padding / dgrad): per-row tap
+//      validity bitmask, invalid taps read zeros through the buffer range check.
 // BT: B operand K-major (d.bt), read through the LDS transpose path.
 template <int MODE, bool PAD, bool BT>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
@@ -158,92 +169,83 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const int KT = d.K >> 6;
   const int sc = tid & 7;
   const int srow = tid >> 3;
+  const __amdgpu_buffer_rsrc_t ra_rs = buf_rsrc(d.x);
+  const __amdgpu_buffer_rsrc_t rb_rs = buf_rsrc(wb);
 
-  // per-thread staging rows (4 A rows, 2 B rows): 64-bit row bases hoisted out of the k-loop
-  bool a_ok[4];
-  int a_ih[4], a_iw[4];
-  const bf16_t* a_ptr[4];
-  int a_slot[4][4];  // MODE 2 only
+  // per-thread staging rows (4 A rows, 2 B rows): loop-invariant byte offsets.
+  // Rows past M are clamped to row 0 (their outputs are never stored).
+  uint32_t a_off[4], vmask[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + srow + 32 * i;
-    a_ok[i] = m < M;
-    const int mm = a_ok[i] ? m : 0;
-    const int img = mm / OHW, rem = mm - img * OHW;
-    const int oh = rem / d.OW, ow = rem - oh * d.OW;
-    a_ih[i] = oh * d.stride - d.pad_h;
-    a_iw[i] = ow * d.stride - d.pad_w;
-    if (MODE == 0) a_ptr[i] = (const bf16_t*)d.x + (int64_t)mm * d.K + sc * 8;
-    else if (MODE == 1)
-      a_ptr[i] = (const bf16_t*)d.x + (((int64_t)img * d.H + a_ih[i]) * d.W + a_iw[i]) * d.Cin + sc * 8;
-    else a_ptr[i] = nullptr;
-    if (MODE == 2) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) a_slot[i][c] = (c < d.Cin) ? d.frame_slots[img * d.Cin + c] : 0;
-      a_ih[i] = oh * d.stride;
-      a_iw[i] = ow * d.stride;
+    const int mm = m < M ? m : 0;
+    if (MODE == 0) {
+      a_off[i] = ((uint32_t)mm * d.K + sc * 8) * 2u;
+      vmask[i] = 0;
+    } else {
+      const int img = mm / OHW, rem = mm - img * OHW;
+      const int oh = rem / d.OW, ow = rem - oh * d.OW;
+      const int ih0 = oh * d.stride - d.pad_h, iw0 = ow * d.stride - d.pad_w;
+      // PAD: offset of the (possibly out-of-range) tap (0,0) pixel; taps add to it in VALU
+      a_off[i] = (uint32_t)(((img * d.H + ih0) * d.W + iw0) * d.Cin + sc * 8) * 2u;
+      uint32_t vm = 0;
+      if (PAD) {
+        for (int kh = 0; kh < d.KH; ++kh)
+          for (int kw = 0; kw < d.KW; ++kw) {
+            const int ih = ih0 + kh, iw = iw0 + kw;
+            if (ih >= 0 && ih < d.H && iw >= 0 && iw < d.W) vm |= 1u << (kh * d.KW + kw);
+          }
+      }
+      vmask[i] = vm;
     }
   }
-  const bf16_t* wrow0 = BT ? wb + (int64_t)srow * d.ldb + n0 + sc * 8 : wb + (int64_t)(n0 + srow) * d.K + sc * 8;
-  const bf16_t* wrow1 = wrow0 + (BT ? (int64_t)32 * d.ldb : (int64_t)32 * d.K);
+  const uint32_t b_off0 = BT ? (uint32_t)((srow * d.ldb + n0 + sc * 8) * 2) : (uint32_t)(((n0 + srow) * d.K + sc * 8) * 2);
+  const uint32_t b_off1 = b_off0 + (BT ? 64u * d.ldb : 64u * d.K);
   const int cpb = d.Cin >> 6;
 
-  auto load_tile = [&](int kt, FwdRegs& R) {
-    if (BT) {
-      const int64_t ko = d.bt == 2 ? (int64_t)kt * 64 * d.ldb : (int64_t)d.koff[cls * KT + kt];
-      R.b0 = *reinterpret_cast<const uint4*>(wrow0 + ko);
-      R.b1 = *reinterpret_cast<const uint4*>(wrow1 + ko);
-    } else {
-      R.b0 = *reinterpret_cast<const uint4*>(wrow0 + (kt << 6));
-      R.b1 = *reinterpret_cast<const uint4*>(wrow1 + (kt << 6));
-    }
+  // Tiles are loaded strictly in order (0, 1, 2, ... then KT-1 repeated), so the
+  // im2col tap decode is a scalar cursor advanced once per load: no integer
+  // division (which lowers to VALU and would make the offsets look divergent).
+  int lt = 0, c_cb = 0, c_kw = 0, c_kh = 0;
+  auto load_next = [&](FwdRegs& R) {
+    const int kt = lt;
+    const uint32_t bso = BT ? (uint32_t)(d.bt == 2 ? kt * 128 * d.ldb : 2 * d.koff[cls * KT + kt]) : (uint32_t)kt * 128u;
+    R.b0 = buf_ld16(rb_rs, b_off0, bso);
+    R.b1 = buf_ld16(rb_rs, b_off1, bso);
     uint4 ra[4];
     if (MODE == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint4 v = *reinterpret_cast<const uint4*>(a_ptr[i] + (kt << 6));
-        ra[i] = a_ok[i] ? v : make_uint4(0, 0, 0, 0);
-      }
-    } else if (MODE == 1) {
-      // tap decode is wave-uniform (scalar); per row only a pointer add (+ bounds if PAD)
-      const int tap = kt / cpb, cb = kt - tap * cpb;
-      const int kh = tap / d.KW, kw = tap - kh * d.KW;
-      const int64_t toff = ((int64_t)kh * d.W + kw) * d.Cin + (cb << 6);
+      for (int i = 0; i < 4; ++i) ra[i] = buf_ld16(ra_rs, a_off[i], (uint32_t)kt * 128u);
+    } else {
+      const int tap = c_kh * d.KW + c_kw;
+      const uint32_t toff = (uint32_t)(((c_kh * d.W + c_kw) * d.Cin + (c_cb << 6)) * 2);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        bool ok = a_ok[i];
         if (PAD) {
-          const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
-          ok = ok && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
+          const uint32_t vo = ((vmask[i] >> tap) & 1u) ? a_off[i] + toff : BUF_OOB;
+          ra[i] = buf_ld16(ra_rs, vo, 0);
+        } else {
+          ra[i] = buf_ld16(ra_rs, a_off[i], toff);
         }
-        const bf16_t* src = ok ? a_ptr[i] + toff : (const bf16_t*)d.x;
-        const uint4 v = *reinterpret_cast<const uint4*>(src);
-        ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
-      }
-    } else {  // MODE 2: uint8 frames, K ordered (c, kh, kw), one frame per k-tile, chunk = kh
-      const int64_t fbytes = (int64_t)d.H * d.W;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int slot = kt == 0 ? a_slot[i][0] : kt == 1 ? a_slot[i][1] : kt == 2 ? a_slot[i][2] : a_slot[i][3];
-        const uint8_t* p = (const uint8_t*)d.x + slot * fbytes + (int64_t)(a_ih[i] + sc) * d.W + a_iw[i];
-        ra[i].x = a_ok[i] ? *reinterpret_cast<const uint32_t*>(p) : 0u;
-        ra[i].y = a_ok[i] ? *reinterpret_cast<const uint32_t*>(p + 4) : 0u;
-        ra[i].z = ra[i].w = 0;
       }
     }
     R.a0 = ra[0]; R.a1 = ra[1]; R.a2 = ra[2]; R.a3 = ra[3];
+    if (lt < KT - 1) {
+      ++lt;
+      if (MODE == 1 && ++c_cb == cpb) {
+        c_cb = 0;
+        if (++c_kw == d.KW) { c_kw = 0; ++c_kh; }
+      }
+    }
   };
 
   auto write_tile = [&](int buf, const FwdRegs& R) {
     uint8_t* As = smem + buf * FWD_STAGE;
     uint8_t* Bs = As + FWD_BM * 128;
-    const uint4 ra[4] = {R.a0, R.a1, R.a2, R.a3};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = srow + 32 * i;
-      uint4 v = (MODE == 2) ? u8x8_to_bf16x8(ra[i].x, ra[i].y) : ra[i];
-      *reinterpret_cast<uint4*>(As + swz_row(r, sc)) = v;
-    }
+    *reinterpret_cast<uint4*>(As + swz_row(srow, sc)) = R.a0;
+    *reinterpret_cast<uint4*>(As + swz_row(srow + 32, sc)) = R.a1;
+    *reinterpret_cast<uint4*>(As + swz_row(srow + 64, sc)) = R.a2;
+    *reinterpret_cast<uint4*>(As + swz_row(srow + 96, sc)) = R.a3;
     *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow, sc) : swz_row(srow, sc))) = R.b0;
     *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow + 32, sc) : swz_row(srow + 32, sc))) = R.b1;
   };
@@ -279,26 +281,29 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     }
   };
 
-  // Software pipeline: two register stages + two LDS stages.  Tile t's global
-  // loads are issued two iterations before its MFMAs (prefetch distance 2), so
-  // an L2/Infinity-Cache hit is covered by ~2 k-tiles of MFMA work.
+  // Software pipeline: two register stages + two LDS stages, straight-line body.
+  // Tile t's global loads are issued two half-iterations before its MFMAs
+  // (prefetch distance 2); loads past the last tile re-read tile KT-1 (cache
+  // hits) so the body has no branches and the vmcnt waits stay partial.
   FwdRegs RA, RB;
-  load_tile(0, RA);
-  if (KT > 1) load_tile(1, RB);
+  load_next(RA);                        // tile 0
+  load_next(RB);                        // tile 1
   write_tile(0, RA);
   __syncthreads();
-  if (KT > 2) load_tile(2, RA);
-  for (int kt = 0; kt < KT; kt += 2) {
+  load_next(RA);                        // tile 2
+  int kt = 0;
+  for (; kt + 1 < KT; kt += 2) {
     compute(0);
-    if (kt + 1 < KT) write_tile(1, RB);
+    write_tile(1, RB);                  // tile kt+1
     __syncthreads();
-    if (kt + 3 < KT) load_tile(kt + 3, RB);
-    if (kt + 1 >= KT) break;
+    load_next(RB);                      // tile kt+3
     compute(1);
-    if (kt + 2 < KT) write_tile(0, RA);
+    write_tile(0, RA);                  // tile kt+2 (or a harmless duplicate)
     __syncthreads();
-    if (kt + 4 < KT) load_tile(kt + 4, RA);
+    load_next(RA);                      // tile kt+4
   }
+  if (kt < KT) compute(0);              // odd KT: last tile sits in buffer 0
+  __syncthreads();
 
   // ---- epilogue: (acc*scale + bias) -> bf16x4 per lane -> swizzled LDS image -> 16-B row stores
   uint8_t* Es = smem + wv * 4096;
@@ -640,19 +645,21 @@ __global__ void pack_conv_dgrad_weights_kernel(const bf16_t* __restrict__ w3, co
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if ((d.K & 63) || (d.Cout & 63) || d.K <= 0) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
-  if (d.mode == 2 && (d.KH != 8 || d.KW != 8 || d.K != d.Cin * 64 || d.Cin > 4)) return (int)hipErrorInvalidValue;
+  if (d.mode != 0 && d.mode != 1) return (int)hipErrorInvalidValue;
+  // buffer addressing: 32-bit byte offsets
+  const int64_t xbytes = d.mode == 0 ? (int64_t)d.N * d.K * 2 : (int64_t)d.N * d.H * d.W * d.Cin * 2;
+  if (xbytes >= 0x7ffffff0LL) return (int)hipErrorInvalidValue;
+  if (d.mode == 1 && (d.pad_h > 0 || d.pad_w > 0) && d.KH * d.KW > 32) return (int)hipErrorInvalidValue;
   if (d.w2 != nullptr && (d.m_switch % FWD_BM)) return (int)hipErrorInvalidValue;
   const int M = d.N * d.OH * d.OW;
   dim3 grid((M + FWD_BM - 1) / FWD_BM, d.Cout / FWD_BN, d.ncls > 0 ? d.ncls : 1);
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
   if (d.bt == 1 && (d.K >> 6) * (d.ncls > 0 ? d.ncls : 1) > 16) return (int)hipErrorInvalidValue;
-  if (d.bt && d.mode == 2) return (int)hipErrorInvalidValue;
   if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true><<<grid, 256, 0, st>>>(d);
   else if (d.mode == 0) igemm_fwd_kernel<0, false, false><<<grid, 256, 0, st>>>(d);
   else if (d.mode == 1 && d.bt) igemm_fwd_kernel<1, true, true><<<grid, 256, 0, st>>>(d);
   else if (d.mode == 1 && pad) igemm_fwd_kernel<1, true, false><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1) igemm_fwd_kernel<1, false, false><<<grid, 256, 0, st>>>(d);
-  else igemm_fwd_kernel<2, false, false><<<grid, 256, 0, st>>>(d);
+  else igemm_fwd_kernel<1, false, false><<<grid, 256, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }
 

@@ -1,5 +1,7 @@
 // Fused dueling heads + n-step double-DQN target + Huber/IS loss + priorities
-// + head backward.  One wavefront per sample.
+// + head backward.  One block of three waves per sample: each wave evaluates
+// one 1024-wide activation row (online S_t, online S_t+n, target S_t+n) and
+// the q-values meet in LDS; wave 0 finishes loss, priority and backward.
 //
 // Covers reference duelling_network.py:18-19,25-27 (value/advantage heads and
 // the dueling combine, with the per-sample advantage mean instead of the
@@ -60,12 +62,12 @@ __device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const H
       part[j + 1] = 0.f;
     }
   }
-  float v = wave_sum(part[0]) + P.bv[0];
+  float v = wave_sum_dpp(part[0]) + P.bv[0];
   float amean = 0.f;
 #pragma unroll
   for (int j = 0; j < HEAD_MAXA; ++j) {
     if (j < A) {
-      float a = wave_sum(part[j + 1]) + P.ba[j];
+      float a = wave_sum_dpp(part[j + 1]) + P.ba[j];
       part[j + 1] = a;
       amean += a;
     }
@@ -76,24 +78,40 @@ __device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const H
     if (j < A) q[j] = v + part[j + 1] - amean;
 }
 
-__global__ void __launch_bounds__(256) ddqn_head_kernel(
+__global__ void __launch_bounds__(192) ddqn_head_kernel(
     const bf16_t* __restrict__ Hon, const bf16_t* __restrict__ Htg, HeadParams Pon, HeadParams Ptg,
     const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
     bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n) {
-  const int lane = threadIdx.x & 63;
-  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  __shared__ float qs[2][HEAD_MAXA];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.x;
   // zero the head-gradient region that head_wgrad accumulates into (stream-ordered)
   if (zero_ptr != nullptr) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += gridDim.x * blockDim.x) zero_ptr[i] = 0.f;
   }
-  if (b >= B) return;
   float q_t[HEAD_MAXA], q_n[HEAD_MAXA], q_g[HEAD_MAXA];
-  float hv_t[8], ha_t[8], hv_x[8], ha_x[8];
-  head_row(Hon + (int64_t)b * 1024, Pon, A, lane, q_t, hv_t, ha_t);
-  head_row(Hon + (int64_t)(B + b) * 1024, Pon, A, lane, q_n, hv_x, ha_x);
-  head_row(Htg + (int64_t)b * 1024, Ptg, A, lane, q_g, hv_x, ha_x);
+  float hv_t[8], ha_t[8];
+  if (wv == 0) {
+    head_row(Hon + (int64_t)b * 1024, Pon, A, lane, q_t, hv_t, ha_t);
+  } else {
+    float hv_x[8], ha_x[8], q[HEAD_MAXA];
+    if (wv == 1) head_row(Hon + (int64_t)(B + b) * 1024, Pon, A, lane, q, hv_x, ha_x);
+    else head_row(Htg + (int64_t)b * 1024, Ptg, A, lane, q, hv_x, ha_x);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < HEAD_MAXA; ++j)
+        if (j < A) qs[wv - 1][j] = q[j];
+    }
+  }
+  __syncthreads();
+  if (wv != 0) return;
+#pragma unroll
+  for (int j = 0; j < HEAD_MAXA; ++j) {
+    q_n[j] = j < A ? qs[0][j] : 0.f;
+    q_g[j] = j < A ? qs[1][j] : 0.f;
+  }
   // double DQN: argmax from the online net, value from the target net
   int astar = 0;
   float best = -3.4e38f, qg_star = 0.f, q_sa = 0.f;
@@ -199,8 +217,7 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
                                float* loss, float* q_out, bf16_t* dH, float* dhead, float* zero_ptr,
                                int zero_n, hipStream_t st) {
   if (A < 1 || A > HEAD_MAXA || B < 1) return (int)hipErrorInvalidValue;
-  const int wpb = 4;
-  ddqn_head_kernel<<<(B + wpb - 1) / wpb, 64 * wpb, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A,
+  ddqn_head_kernel<<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A,
                                                             huber, kappa, grad_scale, td_abs, loss, q_out,
                                                             dH, dhead, zero_ptr, zero_n);
   APEX_CHECK_LAUNCH();

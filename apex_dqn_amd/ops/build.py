@@ -27,8 +27,13 @@ RUNTIME_LIB = os.path.join(OUT, "libapex_runtime.so")
 ARCH = os.environ.get("APEX_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in ArchVGPRs.  With the default
+# AGPR form the register allocator rotates the 32 accumulator registers
+# between the two pipeline halves of every GEMM main loop (44 v_accvgpr
+# moves per 32 MFMAs -- measured in the ISA); VGPR form makes the loops
+# MFMA + ds_read + buffer_load only.
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-             "-Wno-unused-result", "-I", CSRC]
+             "-mllvm", "-amdgpu-mfma-vgpr-form", "-Wno-unused-result", "-I", CSRC]
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-I", CSRC]
 
 
@@ -54,7 +59,7 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> 
     for s in srcs:
         o = os.path.join(OUT, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer([s] + headers, o):
+        if force or _newer([s] + headers + [os.path.abspath(__file__)], o):
             todo.append([HIPCC] + HIP_FLAGS + ["-c", s, "-o", o])
     if todo:
         with ThreadPoolExecutor(max_workers=jobs) as ex:

@@ -68,19 +68,6 @@ def _launch_fwd(lib, d) -> None:
     _lib.check(lib.apex_conv_fwd(d, _lib.stream_ptr()), "conv_fwd")
 
 
-def conv1_fwd_ring(lib, ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor, b1: torch.Tensor,
-                   scale: float, out: torch.Tensor, w2=None, b2=None, rows_first: int = 0) -> None:
-    """conv1 (8x8 s4, C stacked frames -> 64) reading uint8 frames from the replay ring.
-    Rows >= ``rows_first`` use the second weight set (target network) when given."""
-    N, C = slots.shape
-    H, W = ring.shape[1], ring.shape[2]
-    assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
-    d = _conv_desc(x=ring.data_ptr(), frame_slots=slots.data_ptr(), w=w1.data_ptr(), bias=b1.data_ptr(),
-                   y=out.data_ptr(), N=N, H=H, W=W, Cin=C, OH=20, OW=20, Cout=64, KH=8, KW=8, stride=4,
-                   mode=2, relu=1, K=C * 64, scale=scale, **_second(w2, b2, rows_first, 400))
-    _launch_fwd(lib, d)
-
-
 def pack_w1_s2d(lib, ws: "Workspace", w1: torch.Tensor, tag: str) -> torch.Tensor:
     """OIHW conv1 weights -> s2d K order (cached buffer per tag, repacked every call)."""
     C = w1.shape[1]
