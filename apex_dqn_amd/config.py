@@ -88,6 +88,8 @@ class RuntimeConf:
     param_publish_freq: int = 1     # learner steps between param publishes to actors
     use_hip_kernels: bool = True    # GPU path: hand-written HIP kernels
     use_graphs: bool = True         # GPU path: capture the learner step in a HIP graph
+    overlap_wgrad: bool = False     # weight-gradient GEMMs on a side stream beside the dgrad chain
+                                    # (measured slower on MI355X at B=512: the kernels contend)
     actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)
     replay_capacity: Optional[int] = None  # physical capacity (default: soft_capacity * 1.25)
     heartbeat_timeout: float = 60.0

@@ -32,6 +32,15 @@ __device__ __forceinline__ T wave_sum(T v) {
   return v;
 }
 
+// XCD-aware workgroup remap (bijective for any nwg): the dispatcher sends
+// workgroup i to XCD i % 8, each XCD with a private 4 MB L2.  Returned ids are
+// contiguous per XCD, so tiles that share operand rows (adjacent GEMM tiles,
+// the Kc blocks of one wgrad split, the tiles of one frame stack) hit one L2.
+__device__ __forceinline__ int xcd_swizzle(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 // full-wave float sum without the LDS crossbar: DPP quad / row rotations reduce each
 // 16-lane row, four v_readlane finish.  Result is wave-uniform.
 #define APEX_DPP_ADD(v, ctrl)                                                                          \

@@ -183,7 +183,8 @@ __global__ void __launch_bounds__(256, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
   };
 
   const int G = gridDim.x;
-  int tile = blockIdx.x;
+  // XCD-contiguous tile order: the ~3 tiles of one frame stack run on one L2
+  int tile = xcd_swizzle(blockIdx.x, G);
   if (tile < ntiles) issue_dma(tile, 0);
   if (tile + G < ntiles) issue_dma(tile + G, 1);
   int buf = 0;

@@ -75,11 +75,17 @@ __device__ __forceinline__ int swz_tr(int r, int c) {
   return (r << 7) + ((c ^ (s << 1)) << 4);
 }
 
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16x2 (one v_cvt_pk_bf16_f32, round-to-nearest-even)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
+}
+
 __device__ __forceinline__ uint32_t u8pair_bf16(uint32_t v, int sh) {
-  // two consecutive bytes of v (starting at byte sh) -> two bf16 (exact: integers <= 255)
-  const uint32_t lo = __float_as_uint((float)((v >> (8 * sh)) & 0xffu)) >> 16;
-  const uint32_t hi = __float_as_uint((float)((v >> (8 * sh + 8)) & 0xffu)) >> 16;
-  return lo | (hi << 16);
+  // two consecutive bytes of v (starting at byte sh) -> two bf16 (exact: integers <= 255):
+  // v_cvt_f32_ubyteN x2 + v_cvt_pk_bf16_f32
+  return cvt_pk_bf16((float)((v >> (8 * sh)) & 0xffu), (float)((v >> (8 * sh + 8)) & 0xffu));
 }
 
 __device__ __forceinline__ uint4 u8x8_to_bf16x8(uint32_t lo, uint32_t hi) {
@@ -126,12 +132,6 @@ struct FwdRegs {
   uint4 a0, a1, a2, a3, b0, b1;
 };
 
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-// two floats -> packed bf16x2 (one v_cvt_pk_bf16_f32, round-to-nearest-even)
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
-}
 
 // Epilogue image: 32 rows x 128 B per wave; 16-B chunk c of row r at c ^ ((r>>1)&7)
 __device__ __forceinline__ int epi_off(int r, int byte) {
@@ -157,11 +157,16 @@ template <int MODE, bool PAD, bool BT>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * FWD_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int cls = blockIdx.z;
+  // XCD-contiguous tile order: adjacent M tiles (overlapping im2col input rows) share an L2
+  const int wg = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                             gridDim.x * gridDim.y * gridDim.z);
+  const int bx = wg % gridDim.x, byz = wg / gridDim.x;
+  const int by = byz % gridDim.y, bz = byz / gridDim.y;
+  const int cls = bz;
   const int OHW = d.OH * d.OW;
   const int M = d.N * OHW;
-  const int m0 = blockIdx.x * FWD_BM;
-  const int n0 = blockIdx.y * FWD_BN;
+  const int m0 = bx * FWD_BM;
+  const int n0 = by * FWD_BN;
   // online / target weight sets in one launch: the switch row is block-uniform
   const bool second = d.w2 != nullptr && m0 >= d.m_switch;
   const bf16_t* __restrict__ wb = (second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride;
@@ -351,12 +356,21 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 // =====================================================================================
 // weight gradient: dW[Co][Kc] partial over a slice of the reduction rows
 // =====================================================================================
-#define WG_BR 64                         // reduction rows per step
-#define WG_TILE (WG_BR * 128)            // one 64x64 bf16 operand image (8 KB)
 
-struct WgRegs {
-  uint4 d0, d1, x0, x1;
-};
+// Design: a block owns CT x NT 64x64 output tiles (CT along Co, NT along Kc) of
+// one split-K slice; wave w owns tile (w / NT, w % NT), and all waves walk the
+// slice's reduction rows in 64-row steps.  Each step stages CT dY images and NT
+// X images (64 rows x 128 B each) in LDS once, so dY is read from L2 / Infinity
+// Cache Kc/(64 NT) times instead of Kc/64 times -- the wgrad GEMMs are bound by
+// those bytes (measured: 64x64 blocks re-read dY per Kc tile, ~170 MB for conv2),
+// not by MFMA or VALU.  All global reads are buffer loads: dY and dense X rows
+// are affine in the row index; im2col / s2d-ring X rows come from a per-block
+// LDS table of pixel byte offsets built in the prologue (rows past the split end
+// hold BUF_OOB -> zeros).  The bias gradient is 2 extra MFMAs per k-step against
+// an all-ones fragment, done by the waves owning Kc tile 0 -- no VALU sums.
+#define WG_ROWS 64
+#define WG_IMG 8192                     // one 64-row x 128-B operand image
+#define WG_TBL 4096                     // u32 row-offset table entries (16 KB)
 
 // a / D with D a compile-time constant when DC != 0 (multiply-shift), else runtime
 template <int DC>
@@ -364,189 +378,218 @@ __device__ __forceinline__ uint32_t udiv(uint32_t a, uint32_t d) {
   return DC ? a / (uint32_t)DC : a / d;
 }
 
-// MODE: X-operand source (0 dense rows, 1 NHWC im2col, 2 s2d uint8 frame ring).
-// OWC/OHWC: output width / pixels per image as compile-time constants for the
-// learner's shapes (0 = read from the descriptor).
-template <int MODE, int OWC, int OHWC>
+// MODE: X-operand source (0 dense rows, 1 NHWC im2col (pad 0), 2 s2d uint8 ring).
+// OWC/OHWC: output width / pixels per image as compile-time constants (0 = runtime);
+// only the prologue divides.  CT x NT (<= 4) output tiles per block; the block
+// always has 4 waves (all stage; waves past CT * NT do not compute).
+template <int MODE, int OWC, int OHWC, int CT, int NT>
 __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[4 * WG_TILE + 256 * 4];
+  static_assert(CT * NT <= 4, "at most 4 output tiles per block");
+  constexpr int NIMG = CT + NT;
+  constexpr int STAGE = NIMG * WG_IMG;
+  constexpr int NTHR = 256;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE + WG_TBL * 4];
+  uint32_t* tbl = reinterpret_cast<uint32_t*>(smem + 2 * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int kct = blockIdx.x;            // 64-wide column tile of Kc
-  const int cot = blockIdx.y;            // 64-wide row tile of Co
-  const int split = blockIdx.z;
+  // XCD-contiguous order: the Kc / Co blocks of one split (same dY rows, overlapping
+  // input pixels) and neighbouring splits run on one XCD's L2
+  const int wg = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                             gridDim.x * gridDim.y * gridDim.z);
+  const int bx = wg % gridDim.x, byz = wg / gridDim.x;
+  const int kcb = bx * NT;               // first 64-wide Kc tile of the block
+  const int cob = (byz % gridDim.y) * CT; // first 64-wide Co tile
+  const int split = byz / gridDim.y;
   const int r_begin = split * d.rows_per_split;
   const int r_end = min(d.Mred, r_begin + d.rows_per_split);
+  const int nst = (r_end - r_begin + WG_ROWS - 1) / WG_ROWS;
+  const int trows = nst * WG_ROWS;
   const uint32_t OW = OWC ? OWC : d.OW;
   const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
-  const int sc = tid & 7, srow = tid >> 3;  // staging: rows srow, srow+32; chunk sc
-  const bool do_bias = d.bias_slab != nullptr && kct == 0;
-  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-  // column-tile decode of the X operand (block-uniform)
-  int kh = 0, kw = 0;
-  int64_t xoff = 0;
+  // ---------------- prologue: per-row X pixel byte offsets (MODE 1 / 2)
   if (MODE == 1) {
-    const int cpb = d.Cin >> 6;
-    const int tap = kct / cpb, cb = kct - tap * cpb;
-    kh = tap / d.KW;
-    kw = tap - kh * d.KW;
-    xoff = ((int64_t)(kh - d.pad_h) * d.W + (kw - d.pad_w)) * d.Cin + (cb << 6) + sc * 8;
-  }
-  // MODE 2 stages X with lane = reduction row, wave = 16-B s2d block (2 bf16 chunks):
-  // one load instruction reads 64 consecutive blocks of one frame row.
-  const int x2_row = tid & 63, x2_blk = tid >> 6;
-  int x2_c = 0, x2_off = 0;
-  if (MODE == 2) {
-    const int q = 4 * kct + x2_blk;
-    const int tap = q / d.Cin;
-    x2_c = q - tap * d.Cin;
-    x2_off = (((tap >> 1) * 21 + (tap & 1)) << 4);
-  }
-  const bf16_t* dyb = d.dy + cot * 64 + sc * 8;
-
-  auto load_step = [&](int r0, WgRegs& R) {
-    uint4 rd[2], rx[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = r0 + srow + 32 * i;
-      const bool ok = m < r_end;
-      const int mm = ok ? m : r_begin;
-      const uint4 v = *reinterpret_cast<const uint4*>(dyb + (int64_t)mm * d.ldd);
-      rd[i] = ok ? v : make_uint4(0, 0, 0, 0);
-      if (MODE == 0) {
-        const uint4 x = *reinterpret_cast<const uint4*>((const bf16_t*)d.x + (int64_t)mm * d.ldx + kct * 64 + sc * 8);
-        rx[i] = ok ? x : make_uint4(0, 0, 0, 0);
-      } else if (MODE == 1) {
-        const uint32_t img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
+    for (int r = tid; r < trows; r += NTHR) {
+      const uint32_t m = r_begin + r;
+      uint32_t e = BUF_OOB;
+      if ((int)m < r_end) {
+        const uint32_t img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
         const uint32_t oh = udiv<OWC>(rem, OW), ow = rem - oh * OW;
-        const int ih = oh * d.stride + kh - d.pad_h, iw = ow * d.stride + kw - d.pad_w;
-        const bool ok2 = ok && ih >= 0 && ih < d.H && iw >= 0 && iw < d.W;
-        const int64_t pix = ((int64_t)img * d.H + oh * d.stride) * d.W + ow * d.stride;
-        const bf16_t* src = ok2 ? (const bf16_t*)d.x + pix * d.Cin + xoff : (const bf16_t*)d.x;
-        const uint4 x = *reinterpret_cast<const uint4*>(src);
-        rx[i] = ok2 ? x : make_uint4(0, 0, 0, 0);
+        e = (uint32_t)(((img * d.H + oh * d.stride) * d.W + ow * d.stride) * d.Cin) * 2u;
       }
+      tbl[r] = e;
     }
-    if (MODE == 2) {
-      const int m = r0 + x2_row;
-      const bool ok = m < r_end;
-      const uint32_t mm = ok ? m : r_begin;
-      const uint32_t img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
-      const uint32_t oh = udiv<OWC>(rem, OW), ow = rem - oh * OW;
-      const int slot = d.frame_slots[img * d.Cin + x2_c];
-      const uint4 x = *reinterpret_cast<const uint4*>((const uint8_t*)d.x + (int64_t)slot * 7056 +
-                                                      ((oh * 21 + ow) << 4) + x2_off);
-      rx[0] = ok ? x : make_uint4(0, 0, 0, 0);
-      rx[1] = rx[0];
-    }
-    R.d0 = rd[0]; R.d1 = rd[1]; R.x0 = rx[0]; R.x1 = rx[1];
-  };
-
-  auto write_step = [&](int buf, const WgRegs& R) {
-    uint8_t* Ds = smem + buf * 2 * WG_TILE;
-    uint8_t* Xs = Ds + WG_TILE;
-    *reinterpret_cast<uint4*>(Ds + swz_tr(srow, sc)) = R.d0;
-    *reinterpret_cast<uint4*>(Ds + swz_tr(srow + 32, sc)) = R.d1;
-    if (MODE != 2) {
-      *reinterpret_cast<uint4*>(Xs + swz_tr(srow, sc)) = R.x0;
-      *reinterpret_cast<uint4*>(Xs + swz_tr(srow + 32, sc)) = R.x1;
-    } else {
-      // 16 uint8 of one s2d block -> two 16-B bf16 chunks (2 x2_blk, 2 x2_blk + 1) of row x2_row
-      *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk)) = u8x8_to_bf16x8(R.x0.x, R.x0.y);
-      *reinterpret_cast<uint4*>(Xs + swz_tr(x2_row, 2 * x2_blk + 1)) = u8x8_to_bf16x8(R.x0.z, R.x0.w);
-    }
-    if (do_bias) {
-      const uint32_t w8[8] = {R.d0.x, R.d0.y, R.d0.z, R.d0.w, R.d1.x, R.d1.y, R.d1.z, R.d1.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        bsum[2 * (j & 3)] += __uint_as_float(w8[j] << 16);
-        bsum[2 * (j & 3) + 1] += __uint_as_float(w8[j] & 0xffff0000u);
+  } else if (MODE == 2) {
+    for (int i = tid; i < d.Cin * trows; i += NTHR) {
+      const int c = i / trows, r = i - c * trows;
+      const uint32_t m = r_begin + r;
+      uint32_t e = BUF_OOB;
+      if ((int)m < r_end) {
+        const uint32_t img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
+        const uint32_t oh = udiv<OWC>(rem, OW), ow = rem - oh * OW;
+        e = (uint32_t)d.frame_slots[img * d.Cin + c] * 7056u + ((oh * 21 + ow) << 4);
       }
+      tbl[i] = e;
     }
-  };
-
-  // wave tile: 32 (Co) x 32 (Kc) = 2x2 MFMA 16x16 tiles
-  const int wco = (wv >> 1) * 32, wkc = (wv & 1) * 32;
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int buf) {
-    const uint8_t* Ds = smem + buf * 2 * WG_TILE;
-    const uint8_t* Xs = Ds + WG_TILE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 a[2], b[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) a[t] = tr_frag8(Ds, kk, wco + 16 * t, lane);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) b[t] = tr_frag8(Xs, kk, wkc + 16 * t, lane);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // Same two-register-stage / two-LDS-stage pipeline as igemm_fwd: step t's global
-  // loads are issued two steps ahead of its MFMAs.
-  const int ns = (r_end - r_begin + WG_BR - 1) / WG_BR;
-  WgRegs RA, RB;
-  if (ns > 0) {
-    load_step(r_begin, RA);
-    if (ns > 1) load_step(r_begin + WG_BR, RB);
-    write_step(0, RA);
   }
   __syncthreads();
-  if (ns > 2) load_step(r_begin + 2 * WG_BR, RA);
-  for (int t = 0; t < ns; t += 2) {
-    compute(0);
-    if (t + 1 < ns) write_step(1, RB);
-    __syncthreads();
-    if (t + 3 < ns) load_step(r_begin + (t + 3) * WG_BR, RB);
-    if (t + 1 >= ns) break;
-    compute(1);
-    if (t + 2 < ns) write_step(0, RA);
-    __syncthreads();
-    if (t + 4 < ns) load_step(r_begin + (t + 4) * WG_BR, RA);
+
+  // ---------------- staging geometry (each image: 64 rows; thread rows srow, srow + 32; chunk sc)
+  const int sc = tid & 7, srow = tid >> 3;
+  const __amdgpu_buffer_rsrc_t dy_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(d.dy), (short)0, r_end * d.ldd * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t x_rs = MODE == 0
+      ? __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.x), (short)0, r_end * d.ldx * 2, 0x00020000)
+      : buf_rsrc(d.x);
+  const uint32_t dy_off = (uint32_t)(((r_begin + srow) * d.ldd + cob * 64 + sc * 8) * 2);
+  const uint32_t dy_r32 = (uint32_t)(32 * d.ldd * 2), dy_step = (uint32_t)(WG_ROWS * d.ldd * 2);
+  const uint32_t x_off = (uint32_t)(((r_begin + srow) * d.ldx + kcb * 64 + sc * 8) * 2);
+  const uint32_t x_r32 = (uint32_t)(32 * d.ldx * 2), x_step = (uint32_t)(WG_ROWS * d.ldx * 2);
+  // MODE 1: Kc tile t = (tap, channel block); tap shifts the pixel by (kh W + kw) Cin
+  uint32_t x_tap[NT];
+  // MODE 2: lane = row, wave = s2d block b of every Kc tile; frame c / tap per tile
+  int x2_tb[NT];
+  const int x2_row = lane, x2_b = wv;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    x_tap[t] = 0;
+    x2_tb[t] = 0;
+    if (MODE == 1) {
+      const int cpb = d.Cin >> 6, kt = kcb + t;
+      const int tap = kt / cpb, cb = kt - tap * cpb;
+      const int kh = tap / d.KW, kw = tap - kh * d.KW;
+      x_tap[t] = (uint32_t)(((kh * d.W + kw) * d.Cin + (cb << 6) + sc * 8) * 2);
+    } else if (MODE == 2) {
+      const int q = 4 * (kcb + t) + x2_b, tap = q / d.Cin, c = q - tap * d.Cin;
+      x2_tb[t] = c * trows;
+      x_tap[t] = (uint32_t)(((tap >> 1) * 21 + (tap & 1)) << 4);
+    }
   }
 
-  // ---- store the fp32 partial tile: slab[split][co][kc]
-  float* slab = d.slab + (int64_t)split * d.Co * d.Kc;
+  struct Regs {
+    uint4 dy[CT][2];
+    uint4 x[NT][2];
+  };
+
+  auto load_step = [&](int st, Regs& R) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int c = 0; c < CT; ++c) {
+      const uint32_t o = dy_off + st * dy_step + c * 128;
+      R.dy[c][0] = buf_ld16(dy_rs, o, 0);
+      R.dy[c][1] = buf_ld16(dy_rs, o + dy_r32, 0);
+    }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = kct * 64 + wkc + 16 * j + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = cot * 64 + wco + 16 * i + 4 * (lane >> 4) + r;
-        slab[(int64_t)row * d.Kc + col] = acc[i][j][r];
+    for (int t = 0; t < NT; ++t) {
+      if (MODE == 0) {
+        const uint32_t o = x_off + st * x_step + t * 128;
+        R.x[t][0] = buf_ld16(x_rs, o, 0);
+        R.x[t][1] = buf_ld16(x_rs, o + x_r32, 0);
+      } else if (MODE == 1) {
+        const uint32_t* tb = tbl + st * WG_ROWS + srow;
+        R.x[t][0] = buf_ld16(x_rs, tb[0] + x_tap[t], 0);
+        R.x[t][1] = buf_ld16(x_rs, tb[32] + x_tap[t], 0);
+      } else {
+        R.x[t][0] = buf_ld16(x_rs, tbl[x2_tb[t] + st * WG_ROWS + x2_row] + x_tap[t], 0);
       }
     }
-  if (do_bias) {
-    // reduce the per-thread column sums over threads sharing a chunk (lane bits 3..5, then waves)
+  };
+
+  // image i of stage stg: i < CT: dY co tile i; i >= CT: X kc tile i - CT
+  auto img = [&](int stg, int i) -> uint8_t* { return smem + stg * STAGE + i * WG_IMG; };
+
+  auto write_step = [&](int stg, const Regs& R) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = bsum[j];
-      v += __shfl_xor(v, 8, 64);
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      bsum[j] = v;
+    for (int c = 0; c < CT; ++c) {
+      *reinterpret_cast<uint4*>(img(stg, c) + swz_tr(srow, sc)) = R.dy[c][0];
+      *reinterpret_cast<uint4*>(img(stg, c) + swz_tr(srow + 32, sc)) = R.dy[c][1];
     }
-    float* red = reinterpret_cast<float*>(smem + 4 * WG_TILE);
-    if (lane < 8) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[wv * 64 + lane * 8 + j] = bsum[j];
+    for (int t = 0; t < NT; ++t) {
+      uint8_t* X = img(stg, CT + t);
+      if (MODE != 2) {
+        *reinterpret_cast<uint4*>(X + swz_tr(srow, sc)) = R.x[t][0];
+        *reinterpret_cast<uint4*>(X + swz_tr(srow + 32, sc)) = R.x[t][1];
+      } else {
+        // 16 uint8 of s2d block x2_b -> bf16 chunks 2 x2_b, 2 x2_b + 1 of row x2_row
+        *reinterpret_cast<uint4*>(X + swz_tr(x2_row, 2 * x2_b)) = u8x8_to_bf16x8(R.x[t][0].x, R.x[t][0].y);
+        *reinterpret_cast<uint4*>(X + swz_tr(x2_row, 2 * x2_b + 1)) = u8x8_to_bf16x8(R.x[t][0].z, R.x[t][0].w);
+      }
     }
+  };
+
+  const bool active = wv < CT * NT;
+  const int wc = active ? wv / NT : 0, wn = active ? wv - (wv / NT) * NT : 0;   // this wave's (co, kc) tile
+  const bool do_bias = active && d.bias_slab != nullptr && kcb + wn == 0;
+  // acc[i][j] = D[kc][co] (swapped operands): lane holds kc 16j + 4g + {0..3} of co 16i + (lane&15)
+  f32x4 acc[4][4], accb[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    accb[a] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
+
+  auto compute = [&](int stg) {
+    if (!active) return;
+    const uint8_t* D = img(stg, wc);
+    const uint8_t* X = img(stg, CT + wn);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[t] = tr_frag8(D, kk, 16 * t, lane);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) b[t] = tr_frag8(X, kk, 16 * t, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a[i], accb[i], 0, 0, 0);
+      }
+    }
+  };
+
+  // two register stages + two LDS stages, straight-line (loads past the end re-read
+  // the last step -- never computed)
+  Regs RA, RB;
+  const int SL = nst - 1;
+  if (nst > 0) {
+    load_step(0, RA);
+    load_step(min(1, SL), RB);
+    write_step(0, RA);
     __syncthreads();
-    if (tid < 64) {
-      const float s = red[tid] + red[64 + tid] + red[128 + tid] + red[192 + tid];
-      d.bias_slab[(int64_t)split * d.Co + cot * 64 + tid] = s;
+    load_step(min(2, SL), RA);
+    int st = 0;
+    for (; st + 1 < nst; st += 2) {
+      compute(0);
+      write_step(1, RB);
+      __syncthreads();
+      load_step(min(st + 3, SL), RB);
+      compute(1);
+      write_step(0, RA);
+      __syncthreads();
+      load_step(min(st + 4, SL), RA);
     }
+    if (st < nst) compute(0);
+  }
+
+  // ---------------- this wave's fp32 partial tile -> slab[split][co][kc] (float4 along kc)
+  if (!active) return;
+  const int g = lane >> 4, pl = lane & 15;
+  float* slab = d.slab + (int64_t)split * d.Co * d.Kc;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = (cob + wc) * 64 + 16 * i + pl;
+      *reinterpret_cast<f32x4*>(slab + (int64_t)co * d.Kc + (kcb + wn) * 64 + 16 * j + 4 * g) = acc[i][j];
+    }
+  if (do_bias && g == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d.bias_slab[(int64_t)split * d.Co + (cob + wc) * 64 + 16 * i + pl] = accb[i][0];
   }
 }
 
@@ -663,17 +706,58 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   APEX_CHECK_LAUNCH();
 }
 
+// Block shape: fewest re-read bytes -- X is read once per Co group (ct / CT
+// times), dY once per Kc group (kt / NT times); 4-tile shapes keep every wave busy.
+template <int MODE, int OWC, int OHWC>
+static void launch_wgrad(const WgradDesc& d, int nsplit, hipStream_t st) {
+  const int kt = d.Kc / 64, ct = d.Co / 64;
+  const double xb = (double)d.Kc, db = (double)d.Co;   // bytes per row, up to a common factor
+  struct Cand { int c, n; } cands[] = {{1, 4}, {2, 2}, {4, 1}, {1, 3}, {1, 1}};
+  int best = 4;
+  double bc = 1e300;
+  for (int i = 0; i < 5; ++i) {
+    const Cand c = cands[i];
+    if (kt % c.n || ct % c.c) continue;
+    const double cost = (double)(ct / c.c) * xb + (double)(kt / c.n) * db;
+    if (cost < bc) { bc = cost; best = i; }
+  }
+  const dim3 grid(kt / cands[best].n, ct / cands[best].c, nsplit);
+  switch (best) {
+    case 0: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 4><<<grid, 256, 0, st>>>(d); break;
+    case 1: igemm_wgrad_kernel<MODE, OWC, OHWC, 2, 2><<<grid, 256, 0, st>>>(d); break;
+    case 2: igemm_wgrad_kernel<MODE, OWC, OHWC, 4, 1><<<grid, 256, 0, st>>>(d); break;
+    case 3: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 3><<<grid, 256, 0, st>>>(d); break;
+    default: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 1><<<grid, 256, 0, st>>>(d); break;
+  }
+}
+
 APEX_EXPORT int apex_conv_wgrad(WgradDesc d, float* out, float* bout, int nsplit, float scale, hipStream_t st) {
   if ((d.Kc & 63) || (d.Co & 63)) return (int)hipErrorInvalidValue;
-  if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
-  dim3 grid(d.Kc / 64, d.Co / 64, nsplit);
+  if (d.mode == 1 && ((d.Cin & 63) || d.pad_h || d.pad_w)) return (int)hipErrorInvalidValue;
+  // per-block row-offset table capacity (rounded up to 64-row steps)
+  const int trows = (d.rows_per_split + WG_ROWS - 1) / WG_ROWS * WG_ROWS;
+  if (d.mode == 1 && trows > WG_TBL) return (int)hipErrorInvalidValue;
+  if (d.mode == 2 && (d.Cin * trows > WG_TBL || d.Cin > 4)) return (int)hipErrorInvalidValue;
+  if ((int64_t)d.Mred * d.ldd * 2 >= 0x7ffffff0LL) return (int)hipErrorInvalidValue;
+  if (d.mode == 0 && (int64_t)d.Mred * d.ldx * 2 >= 0x7ffffff0LL) return (int)hipErrorInvalidValue;
   // learner shapes get compile-time output geometry (conv3 7x7, conv2 9x9, conv1 20x20)
-  if (d.mode == 0) igemm_wgrad_kernel<0, 1, 1><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1 && d.OH == 7 && d.OW == 7) igemm_wgrad_kernel<1, 7, 49><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1 && d.OH == 9 && d.OW == 9) igemm_wgrad_kernel<1, 9, 81><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1) igemm_wgrad_kernel<1, 0, 0><<<grid, 256, 0, st>>>(d);
-  else if (d.OH == 20 && d.OW == 20) igemm_wgrad_kernel<2, 20, 400><<<grid, 256, 0, st>>>(d);
-  else igemm_wgrad_kernel<2, 0, 0><<<grid, 256, 0, st>>>(d);
+  if (d.mode == 0) launch_wgrad<0, 1, 1>(d, nsplit, st);
+  else if (d.mode == 1 && d.OH == 7 && d.OW == 7) launch_wgrad<1, 7, 49>(d, nsplit, st);
+  else if (d.mode == 1 && d.OH == 9 && d.OW == 9) launch_wgrad<1, 9, 81>(d, nsplit, st);
+  else if (d.mode == 1) launch_wgrad<1, 0, 0>(d, nsplit, st);
+  else {
+    // conv1: Kc = 64 C (C = 1, 2, 4 stacked frames) -> all Kc tiles in one block
+    const int kt = d.Kc / 64;
+    const dim3 grid(1, d.Co / 64, nsplit);
+    const bool fixed = d.OH == 20 && d.OW == 20;
+    if (kt == 4 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 4><<<grid, 256, 0, st>>>(d);
+    else if (kt == 2 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 2><<<grid, 256, 0, st>>>(d);
+    else if (kt == 1 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 1><<<grid, 256, 0, st>>>(d);
+    else if (kt == 4) igemm_wgrad_kernel<2, 0, 0, 1, 4><<<grid, 256, 0, st>>>(d);
+    else if (kt == 2) igemm_wgrad_kernel<2, 0, 0, 1, 2><<<grid, 256, 0, st>>>(d);
+    else if (kt == 1) igemm_wgrad_kernel<2, 0, 0, 1, 1><<<grid, 256, 0, st>>>(d);
+    else return (int)hipErrorInvalidValue;
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   if (out != nullptr) {

@@ -181,9 +181,14 @@ def _wg_desc(**kw) -> "_lib.WgradDesc":
     return d
 
 
-def _splits(Mred: int, per_img: int, target_rows: int) -> Tuple[int, int]:
-    imgs = max(1, target_rows // per_img)
-    rows = imgs * per_img
+_WG_ROWS = 64       # reduction rows per kernel step (csrc/conv_mfma.hip WG_ROWS)
+_WG_TBL = 4096      # per-block row-offset table entries (WG_TBL)
+
+
+def _splits(Mred: int, target_rows: int, max_rows: int) -> Tuple[int, int]:
+    """Split-K partition of the reduction rows: whole 64-row steps per block
+    (rows may straddle images -- the kernel's row table handles that)."""
+    rows = max(_WG_ROWS, min(max_rows, (target_rows // _WG_ROWS) * _WG_ROWS))
     return (Mred + rows - 1) // rows, rows
 
 
@@ -198,7 +203,7 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     _, H, W, Cin = x.shape
     Kc = KH * KH * Cin
     Mred = N * OH * OW
-    nsplit, rows = _splits(Mred, OH * OW, target_rows)
+    nsplit, rows = _splits(Mred, target_rows, _WG_TBL)
     slab = ws.get(("wg", Co, Kc), nsplit * Co * Kc, dy.device)
     bslab = ws.get(("wgb", Co), nsplit * Co, dy.device)
     d = _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=slab.data_ptr(), bias_slab=bslab.data_ptr(), N=N,
@@ -209,12 +214,12 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
 
 
 def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
-                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1600) -> None:
+                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1024) -> None:
     N, OH, OW, Co = dy.shape
     C = slots.shape[1]
     Kc = C * 64
     Mred = N * OH * OW
-    nsplit, rows = _splits(Mred, OH * OW, target_rows)
+    nsplit, rows = _splits(Mred, target_rows, _WG_TBL // C)
     slab = ws.get(("wg1", Co, Kc), nsplit * Co * Kc, dy.device)
     bslab = ws.get(("wg1b", Co), nsplit * Co, dy.device)
     d = _wg_desc(dy=dy.data_ptr(), x=ring.data_ptr(), frame_slots=slots.data_ptr(), slab=slab.data_ptr(),

@@ -127,11 +127,19 @@ class TorchBackend:
 
     # ------------------------------------------------------------ backward
     def fc_bwd(self, dh, x, w, dx_out, dw_out, db_out):
+        self.fc_dgrad(dh, x, w, dx_out)
+        self.fc_wgrad(dh, x, dw_out, db_out)
+
+    def fc_dgrad(self, dh, x, w, dx_out):
+        """dx = (dh @ w) * (x > 0) (x = the ReLU'd fc input)."""
         xf = x.reshape(x.shape[0], -1)
-        dx, dw, db = R.fc_bwd(dh, xf, w, xf, self.dtype)
+        dx, _, _ = R.fc_bwd(dh, xf, w, xf, self.dtype)
         dx_out.copy_(dx.reshape(dx_out.shape))
-        dw_out.copy_(dw)
-        db_out.copy_(db)
+
+    def fc_wgrad(self, dh, x, dw_out, db_out):
+        xf = x.reshape(x.shape[0], -1)
+        dw_out.copy_(dh.t().float() @ xf.float())
+        db_out.copy_(dh.float().sum(0))
 
     def conv_dgrad(self, dy, w, stride, x_src, dx_out):
         dx_out.copy_(R.conv_dgrad(dy, w, tuple(x_src.shape), stride, x_src, self.dtype))
@@ -204,12 +212,16 @@ class HipBackend(TorchBackend):
         C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True, w2=w2, b2=b2,
                     rows_first=rows_first)
 
-    def fc_bwd(self, dh, x, w, dx_out, dw_out, db_out):
+    def fc_dgrad(self, dh, x, w, dx_out):
         if not self.native_conv:
-            return super().fc_bwd(dh, x, w, dx_out, dw_out, db_out)
+            return super().fc_dgrad(dh, x, w, dx_out)
         xf = x.reshape(x.shape[0], -1)
         C.dense_dgrad(self.lib, dh, w, dx_out.reshape(dh.shape[0], -1), xf)
-        C.dense_wgrad(self.lib, dh, xf, dw_out, db_out)
+
+    def fc_wgrad(self, dh, x, dw_out, db_out):
+        if not self.native_conv:
+            return super().fc_wgrad(dh, x, dw_out, db_out)
+        C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out)
 
     def conv_dgrad(self, dy, w, stride, x_src, dx_out):
         if not self.native_conv:

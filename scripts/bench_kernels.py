@@ -71,12 +71,12 @@ def main():
                                                    gb[:64]), F(B * 400 * 64 * 256)),
     }
     # split-size variants of the weight-gradient kernels (rows of the reduction per block)
-    for tr in (256, 512, 2048):
+    for tr in (128, 256, 512, 1024):
         ops[f"conv3_wgrad@{tr}"] = (lambda tr=tr: C.conv_wgrad(lib, ws, dY3, y2[:B], 3, 1, gw[:64 * 576].view(64, 3, 3, 64),
                                                               gb[:64], target_rows=tr), F(B * 49 * 64 * 576))
         ops[f"conv2_wgrad@{tr}"] = (lambda tr=tr: C.conv_wgrad(lib, ws, dY2, y1[:B], 4, 2, gw[:64 * 1024].view(64, 4, 4, 64),
                                                               gb[:64], target_rows=tr), F(B * 81 * 64 * 1024))
-    for tr in (800, 1600, 6400):
+    for tr in (256, 512, 1024):
         ops[f"conv1_wgrad@{tr}"] = (lambda tr=tr: C.conv1_wgrad_ring(lib, ws, dY1, ring, slots[:B], 1 / 255.,
                                                                     gw[:64 * 256].view(64, 4, 8, 8), gb[:64],
                                                                     target_rows=tr), F(B * 400 * 64 * 256))
