@@ -66,7 +66,7 @@ class RuntimeConf:
     seed: int = 0
     learner_T: int = 500000         # reference hard-codes 500000 (main.py:46)
     network: str = "auto"           # "auto" | "nature64" | "nature32" | "mlp" | "impala"
-    env_backend: str = "auto"       # "auto" | "synthetic" | "cartpole" | "ale"
+    env_backend: str = "auto"       # "auto" | "synthetic" | "cartpole" | "ale" | "fake_ale"
     frame_stack: Optional[int] = None  # defaults to state_shape[0]
     actors_per_rank: Optional[int] = None  # defaults to num_actors / world_size
     obs_scale: float = 1.0 / 255.0  # uint8 -> float scale fed to conv nets

@@ -169,86 +169,166 @@ class AtariPreprocess:
         self.ry = _area_matrix(out_hw[0], in_hw[0])
         self.rx = _area_matrix(out_hw[1], in_hw[1])
         self.w = np.array([0.299, 0.587, 0.114])
+        self.ry32 = self.ry.astype(np.float32)
+        self.rxT32 = np.ascontiguousarray(self.rx.T.astype(np.float32))
 
     def __call__(self, rgb: np.ndarray) -> np.ndarray:
-        """rgb: (..., H, W, 3) uint8 -> (..., 84, 84) uint8."""
-        gray = rgb.astype(np.float64) @ self.w
-        out = np.einsum("oh,...hw,pw->...op", self.ry, gray, self.rx)
+        """rgb: (..., H, W, 3) uint8 -> (..., 84, 84) uint8 (two matmuls, no einsum)."""
+        gray = rgb.astype(np.float32) @ self.w.astype(np.float32)
+        out = np.matmul(np.matmul(self.ry32, gray), self.rxT32)
         return np.clip(np.rint(out), 0, 255).astype(np.uint8)
 
 
-class ALEVec:  # pragma: no cover - ale_py is not available in this image
-    """Vectorised ALE with standard DQN wrappers (frame-skip 4 + max-pool,
-    up to 30 no-op starts, reward clipping, 84x84 gray)."""
+class FakeALE:
+    """Deterministic stand-in for one ALE emulator (``ale_py.ALEInterface``
+    subset: act / getScreenRGB / game_over / reset_game / lives /
+    getMinimalActionSet).  A bright block moves with the actions over a
+    frame-indexed background; every 7th emulator frame pays a reward of
+    ``reward_scale`` (so clipping is observable), a life is lost every
+    ``life_frames`` frames and the game ends with the last life.  Lets the DQN
+    wrapper stack below run (and be tested) without ROMs."""
+
+    def __init__(self, seed: int = 0, lives: int = 3, life_frames: int = 60, reward_scale: float = 5.0,
+                 n_actions: int = 6):
+        self.rng = np.random.default_rng(seed)
+        self.max_lives, self.life_frames, self.reward_scale = lives, life_frames, reward_scale
+        self.n_actions = n_actions
+        self.frames_total = 0
+        self.reset_game()
+
+    def getMinimalActionSet(self):  # noqa: N802 - ALE naming
+        return list(range(self.n_actions))
+
+    def reset_game(self):
+        self.t = 0
+        self._lives = self.max_lives
+        self.x = int(self.rng.integers(10, 140))
+
+    def lives(self) -> int:
+        return self._lives
+
+    def game_over(self) -> bool:
+        return self._lives <= 0
+
+    def act(self, a: int) -> float:
+        if self.game_over():
+            return 0.0
+        self.t += 1
+        self.frames_total += 1
+        self.x = int(np.clip(self.x + (int(a) % 3 - 1) * 3, 0, 150))
+        if self.t % self.life_frames == 0:
+            self._lives -= 1
+        return self.reward_scale if self.t % 7 == 0 else 0.0
+
+    def getScreenRGB(self) -> np.ndarray:  # noqa: N802
+        img = np.full((210, 160, 3), (self.t * 3) % 256, np.uint8)
+        img[100:120, self.x:self.x + 10] = 255
+        img[5, :, 0] = self.t % 256  # per-frame marker (distinguishes the pooled frames)
+        return img
+
+
+class AtariWrapperVec:
+    """The standard DQN/Ape-X Atari preprocessing over any emulator exposing the
+    ALE interface (the reference calls plain ``gym.make`` with none of these,
+    ``env.py:3-4``):
+
+    * frame-skip ``k`` with the max over the last two raw frames (flicker);
+    * up to ``noop_max`` random no-op actions after every reset;
+    * optional FIRE after reset (games that wait for it);
+    * episodic life: ``done`` on a lost life (bootstrapping stops), the
+      emulator only resets on game over;
+    * reward clipping to sign(r);
+    * gray + area resize to 84x84 uint8 (``AtariPreprocess``).
+
+    ``info`` carries the UNCLIPPED game-episode return / length when a game
+    ends (``real_done``), NaN / -1 otherwise."""
 
     obs_dtype = np.uint8
     frame_based = True
     obs_shape = (84, 84)
 
-    def __init__(self, game: str, num_envs: int, seed: int = 0, frame_skip: int = 4,
-                 noop_max: int = 30, clip_rewards: bool = True):
-        import ale_py  # noqa: F401
-        from ale_py import ALEInterface, roms
-        self.E = int(num_envs)
-        self.envs = []
-        name = game.replace("NoFrameskip-v4", "").replace("-v0", "")
-        snake = "".join("_" + c.lower() if c.isupper() else c for c in name).lstrip("_")
-        for i in range(self.E):
-            ale = ALEInterface()
-            ale.setInt("random_seed", seed + i)
-            ale.setFloat("repeat_action_probability", 0.0)
-            ale.loadROM(roms.get_rom_path(snake))
-            self.envs.append(ale)
-        self.actions = self.envs[0].getMinimalActionSet()
+    def __init__(self, emulators, frame_skip: int = 4, noop_max: int = 30, clip_rewards: bool = True,
+                 episodic_life: bool = True, fire_reset: bool = False, seed: int = 0):
+        self.envs = list(emulators)
+        self.E = len(self.envs)
+        self.actions = list(self.envs[0].getMinimalActionSet())
         self.action_dim = len(self.actions)
         self.pre = AtariPreprocess()
-        self.frame_skip, self.noop_max, self.clip = frame_skip, noop_max, clip_rewards
+        self.frame_skip, self.noop_max, self.clip = int(frame_skip), int(noop_max), bool(clip_rewards)
+        self.episodic_life, self.fire_reset = bool(episodic_life), bool(fire_reset)
         self.rng = np.random.default_rng(seed)
         self.ep_ret = np.zeros(self.E)
         self.ep_len = np.zeros(self.E, np.int64)
+        self.lives = np.array([e.lives() for e in self.envs])
 
-    def _obs(self, i, buf):
-        return self.pre(np.maximum(buf[0], buf[1]))
-
-    def _reset_one(self, i):
-        ale = self.envs[i]
-        ale.reset_game()
+    def _reset_one(self, i: int) -> np.ndarray:
+        emu = self.envs[i]
+        emu.reset_game()
         for _ in range(int(self.rng.integers(0, self.noop_max + 1))):
-            ale.act(0)
-        f = ale.getScreenRGB()
-        return self.pre(f)
+            emu.act(self.actions[0])
+            if emu.game_over():
+                emu.reset_game()
+        if self.fire_reset and len(self.actions) > 1:
+            emu.act(self.actions[1])
+        self.lives[i] = emu.lives()
+        return self.pre(emu.getScreenRGB())
 
-    def reset(self):
+    def reset(self) -> np.ndarray:
+        self.ep_ret[:] = 0
+        self.ep_len[:] = 0
         return np.stack([self._reset_one(i) for i in range(self.E)])
 
     def step(self, actions):
         obs = np.zeros((self.E, 84, 84), np.uint8)
         rew = np.zeros(self.E, np.float32)
         done = np.zeros(self.E, bool)
+        real_done = np.zeros(self.E, bool)
         ep_r = np.full(self.E, np.nan)
         ep_l = np.full(self.E, -1)
         for i, a in enumerate(actions):
-            ale = self.envs[i]
-            r, bufs = 0.0, []
+            emu = self.envs[i]
+            r, last2 = 0.0, []
             for k in range(self.frame_skip):
-                r += ale.act(self.actions[int(a)])
+                r += emu.act(self.actions[int(a)])
                 if k >= self.frame_skip - 2:
-                    bufs.append(ale.getScreenRGB())
-                if ale.game_over():
+                    last2.append(emu.getScreenRGB())
+                if emu.game_over():
                     break
-            while len(bufs) < 2:
-                bufs.append(ale.getScreenRGB())
+            if not last2:
+                last2.append(emu.getScreenRGB())
+            frame = np.maximum(last2[0], last2[-1])
             self.ep_ret[i] += r
             self.ep_len[i] += 1
             rew[i] = np.sign(r) if self.clip else r
-            if ale.game_over():
-                done[i] = True
+            lives = emu.lives()
+            if emu.game_over():
+                done[i] = real_done[i] = True
                 ep_r[i], ep_l[i] = self.ep_ret[i], self.ep_len[i]
                 self.ep_ret[i], self.ep_len[i] = 0, 0
                 obs[i] = self._reset_one(i)
-            else:
-                obs[i] = self._obs(i, bufs)
-        return obs, rew, done, {"episode_return": ep_r, "episode_length": ep_l}
+                continue
+            if self.episodic_life and lives < self.lives[i]:
+                done[i] = True          # a lost life ends the transition chain, not the game
+            self.lives[i] = lives
+            obs[i] = self.pre(frame)
+        return obs, rew, done, {"episode_return": ep_r, "episode_length": ep_l, "real_done": real_done}
+
+
+class ALEVec(AtariWrapperVec):  # pragma: no cover - ale_py is not available in this image
+    """``AtariWrapperVec`` over real ALE emulators (``ale_py``), when importable."""
+
+    def __init__(self, game: str, num_envs: int, seed: int = 0, **kw):
+        from ale_py import ALEInterface, roms
+        name = game.replace("NoFrameskip-v4", "").replace("-v0", "")
+        snake = "".join("_" + c.lower() if c.isupper() else c for c in name).lstrip("_")
+        emus = []
+        for i in range(int(num_envs)):
+            ale = ALEInterface()
+            ale.setInt("random_seed", seed + i)
+            ale.setFloat("repeat_action_probability", 0.0)
+            ale.loadROM(roms.get_rom_path(snake))
+            emus.append(ale)
+        super().__init__(emus, seed=seed, **kw)
 
 
 def make_vec_env(backend: str, name: str, num_envs: int, action_dim: int,
@@ -259,6 +339,8 @@ def make_vec_env(backend: str, name: str, num_envs: int, action_dim: int,
     if backend == "synthetic":
         return SyntheticAtariVec(num_envs, action_dim=action_dim, seed=seed,
                                  frame_hw=frame_hw or (84, 84))
+    if backend == "fake_ale":
+        return AtariWrapperVec([FakeALE(seed=seed + i, n_actions=action_dim) for i in range(num_envs)], seed=seed)
     if backend == "ale":  # pragma: no cover
         return ALEVec(name, num_envs, seed=seed)
     raise ValueError(f"unknown env backend {backend!r}")
