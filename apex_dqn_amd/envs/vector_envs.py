@@ -335,7 +335,8 @@ def make_vec_env(backend: str, name: str, num_envs: int, action_dim: int,
                  seed: int = 0, frame_hw: Optional[Tuple[int, int]] = None):
     """Factory replacing ``make_local_env`` (``env.py:3-4``)."""
     if backend == "cartpole":
-        return CartPoleVec(num_envs, seed=seed)
+        from ..runtime import native
+        return native.NativeCartPoleVec(num_envs, seed=seed) if native.available() else CartPoleVec(num_envs, seed)
     if backend == "synthetic":
         return SyntheticAtariVec(num_envs, action_dim=action_dim, seed=seed,
                                  frame_hw=frame_hw or (84, 84))

@@ -17,6 +17,12 @@ import numpy as np
 from .sumtree import SumTree
 
 
+def _make_tree(cap: int) -> SumTree:
+    """C++ sum-tree (csrc/runtime) when the native runtime builds, numpy otherwise."""
+    from ..runtime.native import make_sum_tree
+    return make_sum_tree(cap)
+
+
 class PrioritizedReplay:
     def __init__(self, soft_capacity: int, priority_exponent: float = 0.6,
                  importance_sampling_exponent: float = 0.4, capacity: Optional[int] = None,
@@ -26,7 +32,7 @@ class PrioritizedReplay:
         self.alpha = float(priority_exponent)
         self.beta = float(importance_sampling_exponent)
         self.eps = float(priority_eps)
-        self.tree = SumTree(self.cap)
+        self.tree = _make_tree(self.cap)
         self.rng = np.random.default_rng(seed)
         self.storage: Dict[str, np.ndarray] = {}
         self.head = 0

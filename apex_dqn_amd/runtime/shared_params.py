@@ -28,9 +28,25 @@ class SharedParams:
         self.numel = off
         self.flat = torch.zeros(off, dtype=torch.float32).share_memory_()
         self.version = ctx.Value("q", 0, lock=False)
+        # native seqlock (csrc/runtime): release/acquire fences around the copy
+        from . import native
+        self.native = native.available()
+        if self.native:
+            self.seq = torch.zeros(1, dtype=torch.int64).share_memory_()
         self.publish(template)
 
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        if self.native:
+            from . import native
+            self.native = native.available()
+
     def publish(self, state: Dict[str, torch.Tensor]) -> None:
+        if self.native:
+            from .native import SeqLock
+            stage = torch.cat([state[k].detach().reshape(-1).float().cpu() for k, _, _ in self.spec])
+            SeqLock(self.seq, self.flat).write(stage)
+            return
         self.version.value += 1          # odd: writing
         for k, shape, off in self.spec:
             v = state[k]
@@ -39,6 +55,13 @@ class SharedParams:
 
     def read(self, last_version: int = -1):
         """Return (version, state_dict) or (last_version, None) if unchanged."""
+        if self.native:
+            from .native import SeqLock
+            snap = torch.empty_like(self.flat)
+            v = SeqLock(self.seq, self.flat).read_into(snap, last_version)
+            if v < 0:
+                return last_version, None
+            return v, {k: snap[off:off + math.prod(shape)].view(shape) for k, shape, off in self.spec}
         for _ in range(1000):
             v0 = self.version.value
             if v0 == last_version:
