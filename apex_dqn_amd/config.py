@@ -88,6 +88,12 @@ class RuntimeConf:
     param_publish_freq: int = 1     # learner steps between param publishes to actors
     use_hip_kernels: bool = True    # GPU path: hand-written HIP kernels
     use_graphs: bool = True         # GPU path: capture the learner step in a HIP graph
+    profile_phases: bool = False    # at every log interval, time one eager step per phase (CUDA events)
+    episode_lines_per_log: int = 4  # reference-format episode console lines per log interval (rank 0)
+    torch_profile_dir: Optional[str] = None  # torch.profiler (ROCm activities) trace of a few steps
+    torch_profile_start: int = 50   # first profiled learner step
+    torch_profile_steps: int = 5
+    resume: bool = True             # continue from ckpt_dir/checkpoint.pt when it exists (restarts)
     overlap_wgrad: bool = False     # weight-gradient GEMMs on a side stream beside the dgrad chain
                                     # (measured slower on MI355X at B=512: the kernels contend)
     actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)

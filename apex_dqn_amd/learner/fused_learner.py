@@ -158,18 +158,22 @@ class FusedNatureLearner:
         ops.prepare(self.Pb)
         # the sampler writes the frame-ring slots of S_t / S_{t+n} (twice) into self.slots
         S = self.replay.sample(B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * B:])
+        self._mark("sample")
         # conv1 reads the uint8 frame stacks straight from the replay ring by slot
         self.forward_all()
+        self._mark("forward")
         isw = S["weights"] if rt.use_is_weights else None
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
         ops.head_wgrad(self.h, self.dhead, self.G)
+        self._mark("head")
         with self._on_side():
             ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"])
         ops.fc_dgrad(self.dH, self.y3[:B], self.Pb["wfc"], self.dY3)
         if self.world > 1:
             self._join_side()   # the fc bucket all-reduce follows this segment
+        self._mark("fc_backward")
 
     def _seg2(self) -> None:
         """conv backward: the dgrad chain on the compute stream, conv3/conv2 wgrad on
@@ -184,6 +188,43 @@ class FusedNatureLearner:
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"])
         self._join_side()
+        self._mark("conv_backward")
+
+    # ------------------------------------------------------- phase timing
+    _marks = None
+
+    def _mark(self, name: str) -> None:
+        """Record a CUDA event at a phase boundary (eager profiling steps only)."""
+        if self._marks is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._marks.append((name, ev))
+
+    def profile_step(self) -> Dict[str, float]:
+        """Run ONE eager (un-graphed) learner step with CUDA events between its
+        phases; returns milliseconds per phase (sample, forward, head,
+        fc_backward, conv_backward, [allreduce_wait], optimizer, priorities) and
+        the total.  Counts as a normal update."""
+        if self.device.type != "cuda":
+            return {}
+        start = torch.cuda.Event(enable_timing=True)
+        start.record()
+        self._marks = []
+        try:
+            if self.world > 1:
+                self._dp_step(False)
+            else:
+                self._step_body()
+        finally:
+            marks, self._marks = self._marks, None
+        torch.cuda.synchronize(self.device)
+        out, prev = {}, start
+        for name, ev in marks:
+            out[name] = out.get(name, 0.0) + prev.elapsed_time(ev)
+            prev = ev
+        out["total"] = start.elapsed_time(prev)
+        self.num_q_updates += 1
+        return out
 
     def _on_side(self):
         """Context: launches go to the side stream, after everything queued so far on
@@ -202,7 +243,9 @@ class FusedNatureLearner:
         rt, ops = self.rt, self.ops
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
+        self._mark("optimizer")
         self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
+        self._mark("priorities")
         if self.world > 1:
             # local min_i p_i / total for the global IS-weight normaliser (all-reduced MIN after the step)
             rp = self.replay
@@ -228,6 +271,7 @@ class FusedNatureLearner:
         w_cv = dist.all_reduce(self.g32[:cut], op=dist.ReduceOp.SUM, async_op=True)
         w_fc.wait()
         w_cv.wait()
+        self._mark("allreduce_wait")
         run(2)
         self.ratio_buf.copy_(self.ratio_local)
         self._ratio_work = dist.all_reduce(self.ratio_buf, op=dist.ReduceOp.MIN, async_op=True)

@@ -35,6 +35,16 @@ def build_replay(cfg: ApexConfig, device, num_envs: int, seed: int = 0) -> GpuRe
                           seed=seed)
 
 
+def _start_torch_profiler(device):
+    """torch.profiler with CPU + GPU (roctracer on ROCm) activities."""
+    acts = [torch.profiler.ProfilerActivity.CPU]
+    if device.type == "cuda":
+        acts.append(torch.profiler.ProfilerActivity.CUDA)
+    p = torch.profiler.profile(activities=acts, record_shapes=False)
+    p.start()
+    return p
+
+
 def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                  metrics: Optional[MetricsLogger] = None, num_envs: Optional[int] = None,
                  actor_steps_per_update: int = 1, max_actor_steps: Optional[int] = None,
@@ -55,6 +65,15 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     max_actor_steps = max_actor_steps or 10 ** 12
     losses = []
     ckpt_path = os.path.join(rt.ckpt_dir, "checkpoint.pt") if rt.ckpt_dir else None
+    # restart after a learner-rank failure (torchrun --max-restarts / run_elastic):
+    # every rank resumes the same checkpoint, so the DP replicas stay identical
+    if ckpt_path and rt.resume and os.path.exists(ckpt_path):
+        learner.load(ckpt_path)
+        if metrics is not None:
+            metrics.log("resume", step=learner.num_q_updates, path=ckpt_path)
+    prof = None
+    n_ep_seen = 0
+    t_last, n_last, ins_last, steps_last = t0, learner.num_q_updates, 0, 0
     while learner.num_q_updates < learner_steps and actor_steps < max_actor_steps:
         for _ in range(actor_steps_per_update):
             group.step()
@@ -67,8 +86,15 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                 continue
             started = True
             learner.refresh_replay_stats()
+        if rt.torch_profile_dir and learner.num_q_updates == rt.torch_profile_start and prof is None:
+            prof = _start_torch_profiler(device)
         learner.step()
         n = learner.num_q_updates
+        if prof is not None and n >= rt.torch_profile_start + rt.torch_profile_steps:
+            prof.stop()
+            os.makedirs(rt.torch_profile_dir, exist_ok=True)
+            prof.export_chrome_trace(os.path.join(rt.torch_profile_dir, f"trace_rank{rank}.json"))
+            prof, rt.torch_profile_dir = None, None
         if n % L.remove_old_xp_freq == 0:
             replay.remove_to_fit()
             replay.rebuild()
@@ -77,12 +103,29 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
             m = learner.last_metrics()
             losses.append(m["loss"])
             if metrics is not None:
+                now = time.time()
+                dt = max(now - t_last, 1e-9)
+                eps_ = group.eps.float()
+                new_eps = group.episodes[n_ep_seen:]
                 rets = [r for (_, _, r) in group.episodes[-50:]]
+                lens = [ln for (_, ln, _) in group.episodes[-50:]]
                 metrics.log("learner", step=n, loss=m["loss"], td_abs=m["td_abs_mean"], grad_norm=m["grad_norm"],
+                            is_weight_mean=float(learner.S["weights"].mean()),
                             replay=replay.size(), actor_steps=actor_steps, inserted=group.inserted,
                             episodes=len(group.episodes),
                             mean_return=float(np.mean(rets)) if rets else float("nan"),
-                            steps_per_s=n / max(time.time() - t0, 1e-9))
+                            mean_ep_len=float(np.mean(lens)) if lens else float("nan"),
+                            eps_min=float(eps_.min()), eps_max=float(eps_.max()),
+                            grad_steps_per_s=(n - n_last) / dt,
+                            env_frames_per_s=(actor_steps - steps_last) * group.E * world / dt,
+                            inserts_per_s=(group.inserted - ins_last) * world / dt,
+                            steps_per_s=n / max(now - t0, 1e-9))
+                for (env_id, ep_len, ep_ret) in new_eps[:rt.episode_lines_per_log]:
+                    metrics.episode(env_id, actor_steps, ep_len, ep_ret)
+                n_ep_seen = len(group.episodes)
+                if rt.profile_phases and device.type == "cuda":
+                    metrics.log("phases_ms", step=n, **learner.profile_step())
+                t_last, n_last, ins_last, steps_last = time.time(), learner.num_q_updates, group.inserted, actor_steps
         if ckpt_path and rt.ckpt_freq and n % rt.ckpt_freq == 0 and rank == 0:
             learner.save(ckpt_path)
     if device.type == "cuda":

@@ -86,3 +86,42 @@ def test_dp_learner_gloo_world2():
         assert gerr <= 1e-6 * max(gmax, 1e-6) + 1e-9, (rank, gerr, gmax)
         assert perr == 0.0
         assert ratio_g == pytest.approx(min(ratios), rel=1e-5)
+
+
+def _elastic_target(comm, attempt, ckdir, out_dir, fail_at):
+    """2-rank gloo training; rank 1 crashes at learner step ``fail_at`` on the
+    first attempt (fault injection).  Checkpoints every 4 steps."""
+    from apex_dqn_amd.runtime.gpu_loop import train_frames
+    torch.set_num_threads(2)
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 4, "name": "Synthetic"},
+                                "Actor": {"num_actors": 8, "n_step_transition_batch_size": 4,
+                                          "Q_network_sync_freq": 5},
+                                "Learner": {"min_replay_mem_size": 40, "replay_sample_size": 8,
+                                            "remove_old_xp_freq": 4, "q_target_sync_freq": 5},
+                                "Replay_Memory": {"soft_capacity": 120},
+                                "Runtime": {"replay_capacity": 150, "log_every": 0, "use_graphs": False,
+                                            "ckpt_dir": ckdir, "ckpt_freq": 4}})
+    if attempt == 0 and comm.rank == 1:
+        import apex_dqn_amd.learner.fused_learner as fl
+        orig = fl.FusedNatureLearner.step
+
+        def faulty(self):
+            if self.num_q_updates == fail_at:
+                os._exit(17)          # hard crash of one learner rank
+            return orig(self)
+        fl.FusedNatureLearner.step = faulty
+    out = train_frames(cfg, "cpu", 12, comm=comm)
+    L = out["learner"]
+    torch.save({"n": L.num_q_updates, "p": L.p32.clone()}, os.path.join(out_dir, f"rank{comm.rank}.pt"))
+
+
+@pytest.mark.slow
+def test_elastic_restart_resumes_from_checkpoint():
+    from apex_dqn_amd.runtime.launch import run_elastic
+    with tempfile.TemporaryDirectory() as ck, tempfile.TemporaryDirectory() as out:
+        res = run_elastic(_elastic_target, 2, args=(ck, out, 6), max_restarts=2, timeout_s=600)
+        assert res["attempts"] == 2 and res["failures"][0]["ranks"][0][0] == 1
+        r0 = torch.load(os.path.join(out, "rank0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(out, "rank1.pt"), weights_only=True)
+        assert r0["n"] == r1["n"] == 12
+        assert torch.equal(r0["p"], r1["p"])   # replicas identical after the restart

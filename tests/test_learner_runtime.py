@@ -136,8 +136,17 @@ def test_gpu_loop_pipeline_on_cpu(tmp_path):
                                 "Replay_Memory": {"soft_capacity": 120},
                                 "Runtime": {"replay_capacity": 150, "log_every": 4, "use_graphs": False,
                                             "ckpt_dir": str(tmp_path), "ckpt_freq": 6}})
-    out = train_frames(cfg, "cpu", 12)
+    from apex_dqn_amd.utils.metrics import MetricsLogger
+    mpath = str(tmp_path / "m.jsonl")
+    ml = MetricsLogger(mpath)
+    out = train_frames(cfg, "cpu", 12, metrics=ml)
+    ml.close()
     assert out["learner"].num_q_updates == 12
+    import json
+    recs = [json.loads(x) for x in open(mpath)]
+    lrn = [r for r in recs if r["kind"] == "learner"]
+    assert lrn and all(k in lrn[-1] for k in ("loss", "grad_steps_per_s", "env_frames_per_s", "inserts_per_s",
+                                              "is_weight_mean", "eps_min", "eps_max", "mean_ep_len", "replay"))
     assert out["replay"].size() <= 120
     assert os.path.exists(os.path.join(str(tmp_path), "checkpoint.pt"))
     ck = torch.load(os.path.join(str(tmp_path), "checkpoint.pt"), weights_only=True)
