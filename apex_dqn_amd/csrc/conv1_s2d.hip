@@ -51,10 +51,10 @@ __device__ __forceinline__ bf16x8 u8x8_frag(uint2 v) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// ReLU on two packed bf16 (sign bits spread over their halves, then cleared)
 __device__ __forceinline__ uint32_t relu2(uint32_t v) {
-  uint32_t lo = (v & 0x8000u) ? 0u : (v & 0xffffu);
-  uint32_t hi = (v & 0x80000000u) ? 0u : (v & 0xffff0000u);
-  return lo | hi;
+  const uint32_t neg = ((v & 0x80008000u) >> 15) * 0xffffu;
+  return v & ~neg;
 }
 
 #define S2D_STAGES 3

@@ -92,17 +92,22 @@ __device__ __forceinline__ uint4 u8x8_to_bf16x8(uint32_t lo, uint32_t hi) {
   return make_uint4(u8pair_bf16(lo, 0), u8pair_bf16(lo, 2), u8pair_bf16(hi, 0), u8pair_bf16(hi, 2));
 }
 
+// ReLU on two packed bf16: zero the halves whose sign bit is set.
+// (v & 0x80008000) >> 15 marks negative halves with a 1 in their low bit; x 0xffff
+// spreads it over the half (v_mul_u32_u24, no carry between halves); v_bfi clears.
 __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {
-  uint32_t lo = (v & 0x8000u) ? 0u : (v & 0xffffu);
-  uint32_t hi = (v & 0x80000000u) ? 0u : (v & 0xffff0000u);
-  return lo | hi;
+  const uint32_t neg = ((v & 0x80008000u) >> 15) * 0xffffu;
+  return v & ~neg;
 }
 
+// dgrad ReLU mask: keep v's half where the producer activation m's half is > 0
+// (exact for any bf16 m): |m| + 0x7fff sets bit 15 of a half exactly when its
+// magnitude is non-zero (max 0xfffe: no carry into the next half); AND with the
+// inverted sign bits drops negative halves (and -0).  (A NaN half of m keeps v;
+// torch's m > 0 would drop it -- only reachable after the activations diverged.)
 __device__ __forceinline__ uint32_t mask_bf16x2(uint32_t v, uint32_t m) {
-  // keep v where the mask element is > 0 (sign clear and non-zero)
-  uint32_t lo = ((m & 0x8000u) == 0 && (m & 0x7fffu) != 0) ? (v & 0xffffu) : 0u;
-  uint32_t hi = ((m & 0x80000000u) == 0 && (m & 0x7fff0000u) != 0) ? (v & 0xffff0000u) : 0u;
-  return lo | hi;
+  const uint32_t pos = ((m & 0x7fff7fffu) + 0x7fff7fffu) & ~m & 0x80008000u;
+  return v & ((pos >> 15) * 0xffffu);
 }
 
 // MFMA fragment of 8 consecutive K rows (32kk + 8(lane>>4) .. +7) of column col0 + (lane&15)
@@ -149,11 +154,19 @@ __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t vof
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+// a / D with D a compile-time constant when DC != 0 (multiply-shift), else runtime
+template <int DC>
+__device__ __forceinline__ uint32_t udiv(uint32_t a, uint32_t d) {
+  return DC ? a / (uint32_t)DC : a / d;
+}
+
 // MODE: A-operand source (0 dense rows, 1 NHWC implicit im2col).
 // PAD: im2col taps may fall outside the input (padding / dgrad): per-row tap
 //      validity bitmask, invalid taps read zeros through the buffer range check.
 // BT: B operand K-major (d.bt), read through the LDS transpose path.
-template <int MODE, bool PAD, bool BT>
+// OWC / OHWC: output width / pixels per image as compile-time constants for the
+// learner's layers (0 = runtime), so the per-row div/mod is multiply-shift.
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * FWD_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -163,7 +176,8 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const int bx = wg % gridDim.x, byz = wg / gridDim.x;
   const int by = byz % gridDim.y, bz = byz / gridDim.y;
   const int cls = bz;
-  const int OHW = d.OH * d.OW;
+  const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
+  const uint32_t OWv = OWC ? OWC : d.OW;
   const int M = d.N * OHW;
   const int m0 = bx * FWD_BM;
   const int n0 = by * FWD_BN;
@@ -188,18 +202,18 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
       a_off[i] = ((uint32_t)mm * d.K + sc * 8) * 2u;
       vmask[i] = 0;
     } else {
-      const int img = mm / OHW, rem = mm - img * OHW;
-      const int oh = rem / d.OW, ow = rem - oh * d.OW;
+      const int img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
+      const int oh = udiv<OWC>(rem, OWv), ow = rem - oh * OWv;
       const int ih0 = oh * d.stride - d.pad_h, iw0 = ow * d.stride - d.pad_w;
       // PAD: offset of the (possibly out-of-range) tap (0,0) pixel; taps add to it in VALU
       a_off[i] = (uint32_t)(((img * d.H + ih0) * d.W + iw0) * d.Cin + sc * 8) * 2u;
       uint32_t vm = 0;
       if (PAD) {
-        for (int kh = 0; kh < d.KH; ++kh)
-          for (int kw = 0; kw < d.KW; ++kw) {
-            const int ih = ih0 + kh, iw = iw0 + kw;
-            if (ih >= 0 && ih < d.H && iw >= 0 && iw < d.W) vm |= 1u << (kh * d.KW + kw);
-          }
+        // valid taps form a rectangle [kh0, kh1) x [kw0, kw1): one row mask per kh
+        const int kh0 = max(0, -ih0), kh1 = min(d.KH, d.H - ih0);
+        const int kw0 = max(0, -iw0), kw1 = min(d.KW, d.W - iw0);
+        const uint32_t colbits = kw1 > kw0 ? ((1u << kw1) - 1u) & ~((1u << kw0) - 1u) : 0u;
+        for (int kh = kh0; kh < kh1; ++kh) vm |= colbits << (kh * d.KW);
       }
       vmask[i] = vm;
     }
@@ -338,8 +352,8 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     const int m = m0 + 32 * wv + row;
     if (m >= M) continue;
     uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
-    const int img = m / OHW, rem = m - img * OHW;
-    const int oh = rem / d.OW, ow = rem - oh * d.OW;
+    const int img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
+    const int oh = udiv<OWC>(rem, OWv), ow = rem - oh * OWv;
     const int64_t orow = ((int64_t)img * d.OHfull + oh * d.ostride_h + ooh) * d.OWfull + ow * d.ostride_w + oow;
     const int64_t off = orow * d.ldy + n0 + ch * 8;
     if (d.mask) {
@@ -371,12 +385,6 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 #define WG_ROWS 64
 #define WG_IMG 8192                     // one 64-row x 128-B operand image
 #define WG_TBL 4096                     // u32 row-offset table entries (16 KB)
-
-// a / D with D a compile-time constant when DC != 0 (multiply-shift), else runtime
-template <int DC>
-__device__ __forceinline__ uint32_t udiv(uint32_t a, uint32_t d) {
-  return DC ? a / (uint32_t)DC : a / d;
-}
 
 // MODE: X-operand source (0 dense rows, 1 NHWC im2col (pad 0), 2 s2d uint8 ring).
 // OWC/OHWC: output width / pixels per image as compile-time constants (0 = runtime);
@@ -698,11 +706,19 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   dim3 grid((M + FWD_BM - 1) / FWD_BM, d.Cout / FWD_BN, d.ncls > 0 ? d.ncls : 1);
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
   if (d.bt == 1 && (d.K >> 6) * (d.ncls > 0 ? d.ncls : 1) > 16) return (int)hipErrorInvalidValue;
-  if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 0) igemm_fwd_kernel<0, false, false><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1 && d.bt) igemm_fwd_kernel<1, true, true><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 1 && pad) igemm_fwd_kernel<1, true, false><<<grid, 256, 0, st>>>(d);
-  else igemm_fwd_kernel<1, false, false><<<grid, 256, 0, st>>>(d);
+  const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
+  if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true, 1, 1><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0) igemm_fwd_kernel<0, false, false, 1, 1><<<grid, 256, 0, st>>>(d);
+  else if (pad && d.bt) {
+    // dgrad: conv3 (9x9 out), conv2 per parity class (10x10 out)
+    if (g9) igemm_fwd_kernel<1, true, true, 9, 81><<<grid, 256, 0, st>>>(d);
+    else if (g10) igemm_fwd_kernel<1, true, true, 10, 100><<<grid, 256, 0, st>>>(d);
+    else igemm_fwd_kernel<1, true, true, 0, 0><<<grid, 256, 0, st>>>(d);
+  } else if (pad) igemm_fwd_kernel<1, true, false, 0, 0><<<grid, 256, 0, st>>>(d);
+  else if (d.bt) igemm_fwd_kernel<1, false, true, 0, 0><<<grid, 256, 0, st>>>(d);
+  else if (g9) igemm_fwd_kernel<1, false, false, 9, 81><<<grid, 256, 0, st>>>(d);   // conv2 fwd
+  else if (g7) igemm_fwd_kernel<1, false, false, 7, 49><<<grid, 256, 0, st>>>(d);   // conv3 fwd
+  else igemm_fwd_kernel<1, false, false, 0, 0><<<grid, 256, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }
 

@@ -84,7 +84,10 @@ class FusedNatureLearner:
         # (they only read dY / activations), captured into the same graph(s).  Off
         # by default: at B=512 the concurrent kernels contend for LDS-limited CU
         # slots and Infinity-Cache bandwidth (2680 vs 2832 steps/s measured).
-        self._side = torch.cuda.Stream(d) if (d.type == "cuda" and self.rt.overlap_wgrad) else None
+        # The side stream always carries the small latency-bound kernels that only
+        # need the head's outputs (head wgrad, priority write-back into the sum-tree):
+        # a few blocks each, they run beside the backward GEMMs instead of between them.
+        self._side = torch.cuda.Stream(d) if d.type == "cuda" else None
         # cross-shard IS-weight normaliser: min over ranks of (min_i p_i / total)
         self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
         self.ratio_buf = torch.zeros(1, dtype=torch.float32, device=d)
@@ -166,9 +169,11 @@ class FusedNatureLearner:
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
-        ops.head_wgrad(self.h, self.dhead, self.G)
         self._mark("head")
         with self._on_side():
+            ops.head_wgrad(self.h, self.dhead, self.G)
+            self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
+        with self._on_side(self.rt.overlap_wgrad):
             ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"])
         ops.fc_dgrad(self.dH, self.y3[:B], self.Pb["wfc"], self.dY3)
         if self.world > 1:
@@ -179,10 +184,10 @@ class FusedNatureLearner:
         """conv backward: the dgrad chain on the compute stream, conv3/conv2 wgrad on
         the side stream as soon as their dY is ready, conv1 wgrad last."""
         B, rt, ops, G, Pb = self.B, self.rt, self.ops, self.G, self.Pb
-        with self._on_side():
+        with self._on_side(rt.overlap_wgrad):
             ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"])
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2)
-        with self._on_side():
+        with self._on_side(rt.overlap_wgrad):
             ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"])
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1)
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
@@ -226,10 +231,10 @@ class FusedNatureLearner:
         self.num_q_updates += 1
         return out
 
-    def _on_side(self):
+    def _on_side(self, enabled: bool = True):
         """Context: launches go to the side stream, after everything queued so far on
-        the compute stream (fork).  No-op without a GPU."""
-        if self._side is None:
+        the compute stream (fork).  No-op without a GPU or when not ``enabled``."""
+        if self._side is None or not enabled:
             return contextlib.nullcontext()
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         return torch.cuda.stream(self._side)
@@ -239,13 +244,12 @@ class FusedNatureLearner:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
 
     def _seg3(self) -> None:
-        """clip + centered RMSprop (+bf16 pack), priority write-back, shard stats."""
+        """clip + centered RMSprop (+bf16 pack), shard stats (the priority write-back
+        ran on the side stream right after the head kernel)."""
         rt, ops = self.rt, self.ops
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
         self._mark("optimizer")
-        self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
-        self._mark("priorities")
         if self.world > 1:
             # local min_i p_i / total for the global IS-weight normaliser (all-reduced MIN after the step)
             rp = self.replay
