@@ -19,7 +19,6 @@
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-#define S2D_ROWS 128
 #define S2D_FRAME 7056
 
 struct Conv1S2DDesc {
@@ -45,11 +44,6 @@ __device__ __forceinline__ uint32_t bf16pair_from_f32(float lo, float hi) {
 // (float)(byte k of v): hipcc lowers this pattern to one v_cvt_f32_ubyte{k}
 __device__ __forceinline__ float ubyte(uint32_t v, int k) { return (float)((v >> (8 * k)) & 0xffu); }
 
-__device__ __forceinline__ bf16x8 u8x8_frag(uint2 v) {
-  const uint4 r = make_uint4(bf16pair_from_f32(ubyte(v.x, 0), ubyte(v.x, 1)), bf16pair_from_f32(ubyte(v.x, 2), ubyte(v.x, 3)),
-                             bf16pair_from_f32(ubyte(v.y, 0), ubyte(v.y, 1)), bf16pair_from_f32(ubyte(v.y, 2), ubyte(v.y, 3)));
-  return __builtin_bit_cast(bf16x8, r);
-}
 
 // ReLU on two packed bf16 (sign bits spread over their halves, then cleared)
 __device__ __forceinline__ uint32_t relu2(uint32_t v) {
@@ -57,7 +51,6 @@ __device__ __forceinline__ uint32_t relu2(uint32_t v) {
   return v & ~neg;
 }
 
-#define S2D_STAGES 3
 
 // 16-byte LDS-DMA issued from inline asm: hipcc does not track it, so it emits no
 // conservative vmcnt(0) before later ds_reads; completion is counted by hand with
@@ -99,172 +92,173 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
 }
 
+// ---------------------------------------------------------------------------
+// Image-resident forward.  A persistent workgroup (8 waves, one per CU)
+// walks whole images.  Per image:
+//   * its C uint8 frames (C x 7056 contiguous bytes in the ring) arrive in an
+//     LDS staging area by LDS-DMA, issued while the previous image computes;
+//   * every 16-byte s2d block is converted to bf16 ONCE, into 2C planes
+//     (frame c, half h) of 441 x 16 B (plane stride 7168 = 28 x 256 B, so the
+//     two halves read by one ds_read_b128 lane group never share banks);
+//   * the A fragment of (pixel p, tap (a,b), frame c, half h) is then a single
+//     ds_read_b128 at base(p) + lane-constant offset -- no conversion or address
+//     VALU per MFMA; the B fragments (weights, 2C x 4 per lane) live in VGPRs;
+//   * 25 row tiles of 16 pixels; wave pair (2p, 2p+1) takes tiles p, p+4, ...,
+//     each wave one half of the 64 output channels (half the B fragments per
+//     wave, so two waves fit per SIMD); the epilogue stages each tile through
+//     a wave-private LDS tile for 64-B row-half stores.
+// The 1/255 scale, bias and ReLU are applied in the epilogue; online/target
+// weights switch per image (m_switch is a multiple of 400 rows).
+#define C1_PLANE 7168
+#define C1_TILES 25
+#define C1_THREADS 512
+
 template <int C>
-__global__ void __launch_bounds__(256, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
-  constexpr int NCH = 4 * C;             // 16-byte chunks (tap, frame) per A row
-  constexpr int K = 64 * C;
-  constexpr int WROW = 2 * K;            // bytes per weight row (bf16)
-  constexpr int WCH = WROW / 16;         // 16-byte chunks per weight row
-  constexpr int PLANE = S2D_ROWS * 16;   // one chunk for all 128 rows
-  constexpr int ATILE = NCH * PLANE;
-  constexpr int WSET = 64 * WROW;
-  constexpr int NDMA = 2 * NCH / 4;      // DMA wave-instructions per wave per tile (64 rows each)
-  // A tile is CHUNK-MAJOR: plane j holds chunk j of all 128 rows.  One DMA
-  // wave-instruction = one (tap, frame) chunk of 64 consecutive output pixels,
-  // which are consecutive 16-B s2d blocks of one frame row: contiguous reads.
-  // (A row-major image would gather 64 scattered 16-B pieces per instruction.)
-  constexpr bool EPI_IN_A = NCH >= 8;    // wave's rows in 8 planes = 8 x 512 B = its 4 KB epilogue image
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * WSET + S2D_STAGES * ATILE + (EPI_IN_A ? 0 : 4 * 4096)];
-  uint8_t* Wl = smem;
-  uint8_t* Al = smem + 2 * WSET;
+__global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
+  constexpr int NW = C1_THREADS / 64;    // 8 waves: 2 per SIMD hide each other's epilogue / LDS latency
+  constexpr int IMG = 2 * C * C1_PLANE;
+  constexpr int NCHUNK = C * 441;        // 16-B s2d blocks per image
+  constexpr int NDMA = (NCHUNK + 63) / 64;
+  constexpr int NDW = (NDMA + NW - 1) / NW;   // DMA wave-instructions per wave
+  constexpr int STG = NDMA * 1024;       // u8 staging (lane-linear DMA pieces)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[IMG + STG + NW * 1024];
+  uint8_t* Pl = smem;
+  uint8_t* Sg = Pl + IMG;
+  uint8_t* Ep = Sg + STG;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int M = d.N * 400;
-  const int ntiles = (M + S2D_ROWS - 1) / S2D_ROWS;
+  const int g = lane >> 4, pl = lane & 15;
   const bool two = d.w2 != nullptr;
+  const int img_switch = two ? d.m_switch / 400 : 1 << 30;
 
-  // ---- weights (both sets) -> LDS, chunk c of row n stored at c ^ (n & mask).
-  // Gathered straight from OIHW w1: s2d chunk c = (tap, frame) block q = c >> 1, kernel
-  // rows r4 = 2(c & 1) + {0, 1}; each is 4 contiguous kw taps (8 B) of the OIHW tensor.
-  constexpr int WMASK = WCH >= 16 ? 15 : WCH - 1;
-  for (int s = 0; s < (two ? 2 : 1); ++s) {
-    const bf16_t* src = s ? d.w2 : d.w;
-    for (int i = tid; i < 64 * WCH; i += 256) {
-      const int n = i / WCH, c = i - n * WCH;
-      const int q = c >> 1, tap = q / C, ch = q - tap * C;
-      const int kh = 4 * (tap >> 1) + 2 * (c & 1), kw = 4 * (tap & 1);
-      const bf16_t* p = src + ((n * C + ch) * 8 + kh) * 8 + kw;
-      const uint2 lo = *reinterpret_cast<const uint2*>(p);
-      const uint2 hi = *reinterpret_cast<const uint2*>(p + 8);
-      *reinterpret_cast<uint4*>(Wl + s * WSET + n * WROW + ((c ^ (n & WMASK)) << 4)) =
-          make_uint4(lo.x, lo.y, hi.x, hi.y);
-    }
+  // wave pair (2 p, 2 p + 1) shares row tiles p, p+4, ...; wave w owns channels
+  // [32 (w & 1), 32 (w & 1) + 32) = n-tiles nt0, nt0 + 1: half the B fragments per wave
+  const int nt0 = 2 * (wv & 1);
+  float4 bv[2];                          // bias of the current weight set (channels 16 (nt0+j) + 4 g ..)
+  // lane-constant A offsets per k-step s: block q = 2s + (g >> 1) = (tap, frame c), half g & 1
+  int aoff[2 * C];
+#pragma unroll
+  for (int s = 0; s < 2 * C; ++s) {
+    const int q = 2 * s + (g >> 1), tap = q / C, c = q - tap * C;
+    aoff[s] = (2 * c + (g & 1)) * C1_PLANE + (((tap >> 1) * 21 + (tap & 1)) << 4);
   }
-  // lane (g, p) owns output channels 16nt + 4g + {0..3} (swapped-operand MFMA below)
-  float4 bias4[2][4];
+  // ---- B fragments of the current weight set in VGPRs (swapped-operand MFMA: lane
+  // (g, pl) supplies output channel n = 16 nt + pl, s2d K 32 s + 8 g .. +7), gathered
+  // from OIHW w1: 16-B K chunk c = 4 s + g is (tap, frame) block q = c >> 1, kernel
+  // rows r4 = 2 (c & 1) + {0, 1}, each 4 contiguous kw taps (8 B)
+  bf16x8 bfr[2 * C][2];
+  int cur_set = -1;
+  auto load_b = [&](int set) {
+    const bf16_t* W = set ? d.w2 : d.w;
+    const float* bsrc = set ? d.bias2 : d.bias;
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
-    bias4[0][nt] = *reinterpret_cast<const float4*>(d.bias + 16 * nt + 4 * (lane >> 4));
-    bias4[1][nt] = two ? *reinterpret_cast<const float4*>(d.bias2 + 16 * nt + 4 * (lane >> 4))
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // ---- A-tile DMA: wave wv issues instructions q = NDMA*wv .. +NDMA-1, each one
-  // (chunk j = q >> 1, half = q & 1) for rows 64*half + lane.  A tile spans at most
-  // two images; their C slots come from SCALAR loads (lgkmcnt, not vmcnt).
-  auto issue_dma = [&](int tile, int buf) {
-    const int img0 = __builtin_amdgcn_readfirstlane((tile * S2D_ROWS) / 400);
-    int s0[4], s1[4];
-    sload_slots<C>(d.slots + img0 * C, s0);
-    if (img0 + 1 < d.N) sload_slots<C>(d.slots + (img0 + 1) * C, s1);
-    else { s1[0] = s0[0]; s1[1] = s0[1]; s1[2] = s0[2]; s1[3] = s0[3]; }
+    for (int j = 0; j < 2; ++j) bv[j] = *reinterpret_cast<const float4*>(bsrc + 16 * (nt0 + j) + 4 * g);
 #pragma unroll
-    for (int i = 0; i < NDMA; ++i) {
-      const int q = NDMA * wv + i;
-      const int j = q >> 1, half = q & 1;
-      const int tap = j / C, c = j - tap * C;
-      const int r = 64 * half + lane;
-      const int m = tile * S2D_ROWS + r;
-      const uint8_t* src = d.zero16;
-      if (m < M) {
-        const int img = m / 400;
-        const int rem = m - img * 400;
-        const int oh = rem / 20, ow = rem - oh * 20;
-        int slot = s0[0];
+    for (int s = 0; s < 2 * C; ++s)
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc)
-          if (cc == c) slot = (img == img0) ? s0[cc] : s1[cc];
-        src = d.ring + (int64_t)slot * S2D_FRAME + (((oh + (tap >> 1)) * 21 + ow + (tap & 1)) << 4);
+      for (int nt = 0; nt < 2; ++nt) {
+        const int n = 16 * (nt0 + nt) + pl, c = 4 * s + g;
+        const int q = c >> 1, tap = q / C, ch = q - tap * C;
+        const int kh = 4 * (tap >> 1) + 2 * (c & 1), kw = 4 * (tap & 1);
+        const bf16_t* p = W + ((n * C + ch) * 8 + kh) * 8 + kw;
+        const uint2 lo = *reinterpret_cast<const uint2*>(p);
+        const uint2 hi = *reinterpret_cast<const uint2*>(p + 8);
+        bfr[s][nt] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
-      uint8_t* dst = Al + buf * ATILE + j * PLANE + half * 64 * 16;  // wave-uniform base
-      const uint32_t off = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)dst;
-      dma16(src, __builtin_amdgcn_readfirstlane(off));
+    cur_set = set;
+  };
+
+  // ---- LDS-DMA of one image's frames: chunk j = frame j / 441, block j % 441
+  auto issue_dma = [&](int img) {
+    int sl[4];
+    sload_slots<C>(d.slots + img * C, sl);
+#pragma unroll
+    for (int i = 0; i < NDW; ++i) {
+      const int k = wv * NDW + i;
+      if (k < NDMA) {
+        const int j = 64 * k + lane;
+        const uint8_t* src = d.zero16;
+        if (j < NCHUNK) {
+          const int c = j / 441, blk = j - c * 441;
+          int slot = sl[0];
+#pragma unroll
+          for (int cc = 1; cc < C; ++cc)
+            if (c == cc) slot = sl[cc];
+          src = d.ring + (int64_t)slot * S2D_FRAME + (blk << 4);
+        }
+        const uint32_t off = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(Sg + k * 1024);
+        dma16(src, __builtin_amdgcn_readfirstlane(off));
+      }
     }
   };
 
   const int G = gridDim.x;
-  // XCD-contiguous tile order: the ~3 tiles of one frame stack run on one L2
-  int tile = xcd_swizzle(blockIdx.x, G);
-  if (tile < ntiles) issue_dma(tile, 0);
-  if (tile + G < ntiles) issue_dma(tile + G, 1);
-  int buf = 0;
-  for (int it = 0; tile < ntiles; tile += G, ++it) {
-    // Wait until this tile's DMA group has landed.  Issue order per iteration is
-    // [DMA(tile+2G)][4 epilogue stores], so the VMEM ops younger than DMA(tile)
-    // are: only DMA(tile+G) at it=0, +4 stores at it=1, +8 after.
-    if (tile + G >= ntiles) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
-    else if (it == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA + 4) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA + 8) : "memory");
+  int img = blockIdx.x;
+  if (img < d.N) {
+    load_b(img >= img_switch ? 1 : 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    issue_dma(img);
+  }
+  uint8_t* E = Ep + wv * 1024;
+  for (int it = 0; img < d.N; img += G, ++it) {
+    // this wave's DMA(img) landed: younger VMEM ops are the previous image's
+    // epilogue stores (1 per row tile: 7 tiles for waves 0-1, 6 for the others)
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (wv < 2) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    // stage (buf+2)%3 was consumed two iterations ago by every wave: refill it
-    const int far = tile + 2 * G;
-    if (far < ntiles) issue_dma(far, buf == 0 ? 2 : buf - 1);
-    const bool second = two && tile * S2D_ROWS >= d.m_switch;
-    const uint8_t* W = Wl + (second ? WSET : 0);
-    uint8_t* A = Al + buf * ATILE;
-    f32x4 acc[2][4];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int g = lane >> 4;
-#pragma unroll
-    for (int s = 0; s < 2 * C; ++s) {
-      const int j = 2 * s + (g >> 1), h = g & 1;
-      bf16x8 af[2], bfr[4];
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int r = 32 * wv + 16 * mt + (lane & 15);
-        const uint2 v = *reinterpret_cast<const uint2*>(A + j * PLANE + r * 16 + h * 8);
-        af[mt] = u8x8_frag(v);
-      }
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int n = 16 * nt + (lane & 15);
-        const int c = 4 * s + g;
-        bfr[nt] = *reinterpret_cast<const bf16x8*>(W + n * WROW + ((c ^ (n & WMASK)) << 4));
-      }
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[nt], af[mt], acc[mt][nt], 0, 0, 0);
+    // ---- u8 staging -> bf16 planes (each block converted once)
+    for (int j = tid; j < NCHUNK; j += C1_THREADS) {
+      const uint4 v = *reinterpret_cast<const uint4*>(Sg + j * 16);
+      const int c = j / 441, blk = j - c * 441;
+      const uint4 lo = make_uint4(bf16pair_from_f32(ubyte(v.x, 0), ubyte(v.x, 1)), bf16pair_from_f32(ubyte(v.x, 2), ubyte(v.x, 3)),
+                                  bf16pair_from_f32(ubyte(v.y, 0), ubyte(v.y, 1)), bf16pair_from_f32(ubyte(v.y, 2), ubyte(v.y, 3)));
+      const uint4 hi = make_uint4(bf16pair_from_f32(ubyte(v.z, 0), ubyte(v.z, 1)), bf16pair_from_f32(ubyte(v.z, 2), ubyte(v.z, 3)),
+                                  bf16pair_from_f32(ubyte(v.w, 0), ubyte(v.w, 1)), bf16pair_from_f32(ubyte(v.w, 2), ubyte(v.w, 3)));
+      *reinterpret_cast<uint4*>(Pl + (2 * c) * C1_PLANE + blk * 16) = lo;
+      *reinterpret_cast<uint4*>(Pl + (2 * c + 1) * C1_PLANE + blk * 16) = hi;
     }
-    // ---- epilogue: the wave's 32x64 bf16 output image (rows rho = 0..31, 128 B each)
-    // lives in its own consumed A rows: piece rho/4 = plane rho/4, rows [32wv, 32wv+32).
-    // 16-B chunk c of row rho sits at c ^ ((rho >> 1) & 7) (conflict-free 8-B writes).
-    auto eaddr = [&](int rho) -> uint8_t* {
-      return EPI_IN_A ? A + (rho >> 2) * PLANE + 32 * wv * 16 + (rho & 3) * 128
-                      : Al + S2D_STAGES * ATILE + wv * 4096 + rho * 128;
-    };
-    auto eswz = [&](int rho, int byte) -> int { return (((byte >> 4) ^ ((rho >> 1) & 7)) << 4) + (byte & 15); };
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    // staging is free: prefetch the next image under this one's MFMAs
+    if (img + G < d.N) issue_dma(img + G);
+    const int set = img >= img_switch ? 1 : 0;
+    if (set != cur_set) {
+      // weight-set switch (once per block): reload, then restore the vmcnt invariant
+      load_b(set);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    for (int t = wv >> 1; t < C1_TILES; t += NW / 2) {
+      const int p = 16 * t + pl;
+      const int oh = p / 20, ow = p - 20 * oh;
+      const uint8_t* A = Pl + ((oh * 21 + ow) << 4);
+      f32x4 acc[2];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const float4 bv = second ? bias4[1][nt] : bias4[0][nt];
-      const int cb = 2 * (16 * nt + 4 * (lane >> 4));
+      for (int nt = 0; nt < 2; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int row = 16 * mt + (lane & 15);
-        const f32x4 a = acc[mt][nt];
-        const uint2 v = make_uint2(cvt_pk_bf16(a[0] * d.in_scale + bv.x, a[1] * d.in_scale + bv.y),
-                                   cvt_pk_bf16(a[2] * d.in_scale + bv.z, a[3] * d.in_scale + bv.w));
-        *reinterpret_cast<uint2*>(eaddr(row) + eswz(row, cb)) = v;
+      for (int s = 0; s < 2 * C; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + aoff[s]);
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][nt], a, acc[nt], 0, 0, 0);
+      }
+      // epilogue: lane holds channels 16 (nt0+nt) + 4 g .. +3 of pixel pl -> wave tile
+      // (16 rows x 64 B: 4 chunks, chunk c of row r at c ^ ((r >> 1) & 3)) -> one
+      // 16-B store per lane (rows of the output are 128 B: this wave writes one half)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x4 v = acc[nt];
+        const uint2 o = make_uint2(relu2(cvt_pk_bf16(v[0] * d.in_scale + bv[nt].x, v[1] * d.in_scale + bv[nt].y)),
+                                   relu2(cvt_pk_bf16(v[2] * d.in_scale + bv[nt].z, v[3] * d.in_scale + bv[nt].w)));
+        const int byte = 2 * (16 * nt + 4 * g);
+        *reinterpret_cast<uint2*>(E + pl * 64 + ((((byte >> 4) ^ ((pl >> 1) & 3))) << 4) + (byte & 15)) = o;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      {
+        const int row = lane >> 2, ch = lane & 3;
+        const uint4 v = *reinterpret_cast<const uint4*>(E + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4));
+        *reinterpret_cast<uint4*>(d.y + ((int64_t)img * 400 + 16 * t + row) * 64 + 32 * (wv & 1) + ch * 8) = v;
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int row = 8 * p + (lane >> 3), ch = lane & 7;
-      const int m = tile * S2D_ROWS + 32 * wv + row;
-      uint4 v = *reinterpret_cast<const uint4*>(eaddr(row) + eswz(row, ch * 16));
-      v = make_uint4(relu2(v.x), relu2(v.y), relu2(v.z), relu2(v.w));
-      // out-of-range rows store into a dummy (keeps the per-iteration store count fixed)
-      bf16_t* dst = (m < M) ? d.y + (int64_t)m * 64 + ch * 8 : (bf16_t*)d.scratch + lane * 8;
-      *reinterpret_cast<uint4*>(dst) = v;
-    }
-    buf = (buf == S2D_STAGES - 1) ? 0 : buf + 1;
+    __syncthreads();   // planes may be overwritten by the next conversion
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -311,14 +305,13 @@ __global__ void s2d_frames_kernel(const uint8_t* __restrict__ src, uint8_t* __re
 }
 
 APEX_EXPORT int apex_conv1_s2d_fwd(Conv1S2DDesc d, int grid, hipStream_t st) {
-  if (d.w2 != nullptr && (d.m_switch % S2D_ROWS)) return (int)hipErrorInvalidValue;
-  const int M = d.N * 400;
-  const int ntiles = (M + S2D_ROWS - 1) / S2D_ROWS;
-  if (grid <= 0 || grid > ntiles) grid = ntiles < 256 ? ntiles : 256;
+  if (d.w2 != nullptr && (d.m_switch % 400)) return (int)hipErrorInvalidValue;
+  if (d.N < 1) return 0;
+  if (grid <= 0 || grid > d.N) grid = d.N < 256 ? d.N : 256;
   switch (d.C) {
-    case 1: conv1_s2d_fwd_kernel<1><<<grid, 256, 0, st>>>(d); break;
-    case 2: conv1_s2d_fwd_kernel<2><<<grid, 256, 0, st>>>(d); break;
-    case 4: conv1_s2d_fwd_kernel<4><<<grid, 256, 0, st>>>(d); break;
+    case 1: conv1_s2d_fwd_kernel<1><<<grid, C1_THREADS, 0, st>>>(d); break;
+    case 2: conv1_s2d_fwd_kernel<2><<<grid, C1_THREADS, 0, st>>>(d); break;
+    case 4: conv1_s2d_fwd_kernel<4><<<grid, C1_THREADS, 0, st>>>(d); break;
     default: return (int)hipErrorInvalidValue;
   }
   APEX_CHECK_LAUNCH();

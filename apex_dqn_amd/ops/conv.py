@@ -87,8 +87,6 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
     d.w = w1.data_ptr()  # OIHW: the kernel gathers the s2d K order into LDS
     d.bias = b1.data_ptr()
     if w2 is not None:
-        if (rows_first * 400) % 128:
-            raise ValueError("online/target split must fall on a 128-row tile boundary")
         d.w2 = w2.data_ptr()
         d.bias2 = b2.data_ptr()
         d.m_switch = rows_first * 400
