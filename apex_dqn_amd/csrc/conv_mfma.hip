@@ -43,13 +43,15 @@ struct ConvDesc {
   int64_t w_cls_stride;
   const bf16_t* w2;           // weights for output rows >= m_switch (target network), or null
   const float* bias2;
-  int m_switch;               // multiple of FWD_BM
+  int m_switch;               // multiple of 128 rows
   // B operand stored K-major (bt != 0): element (k, n) at w + koff(cls, k/64) + (k%64)*ldb + n.
   // Lets the dgrad GEMMs read the natural weight tensors (no transposed / flipped copies):
   // bt = 1: koff from the table koff[cls * KT + kt]; bt = 2: koff = kt * 64 * ldb.
   int bt;
   int ldb;
   int koff[16];
+  int tile_hint;              // 0 auto, 1 BM=128, 2 BM=64
+  int order_hint;             // 0 auto, 1 M tiles fastest per XCD, 2 N tiles fastest
 };
 
 struct WgradDesc {
@@ -129,12 +131,11 @@ __device__ __forceinline__ bf16x8 tr_frag8(const uint8_t* img, int kk, int col0,
 // =====================================================================================
 // forward / dgrad implicit GEMM
 // =====================================================================================
-#define FWD_BM 128
 #define FWD_BN 64
-#define FWD_STAGE (FWD_BM * 128 + FWD_BN * 128)  // bytes per LDS buffer
 
 struct FwdRegs {
-  uint4 a0, a1, a2, a3, b0, b1;
+  uint4 a[4];
+  uint4 b0, b1;
 };
 
 
@@ -166,20 +167,38 @@ __device__ __forceinline__ uint32_t udiv(uint32_t a, uint32_t d) {
 // BT: B operand K-major (d.bt), read through the LDS transpose path.
 // OWC / OHWC: output width / pixels per image as compile-time constants for the
 // learner's layers (0 = runtime), so the per-row div/mod is multiply-shift.
-template <int MODE, bool PAD, bool BT, int OWC, int OHWC>
+// BM: rows per block (128: 32 per wave; 64: 16 per wave, for grids that would
+// otherwise leave CUs idle -- fc fwd/dgrad and the 7x7 / 9x9 layers).
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * FWD_STAGE];
+  constexpr int AR = BM / 32;            // A rows staged per thread
+  constexpr int MT = BM / 64;            // 16-row MFMA tiles per wave
+  constexpr int WR = BM / 4;             // output rows per wave
+  constexpr int STAGE = BM * 128 + FWD_BN * 128;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // XCD-contiguous tile order: adjacent M tiles (overlapping im2col input rows) share an L2
   const int wg = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                              gridDim.x * gridDim.y * gridDim.z);
-  const int bx = wg % gridDim.x, byz = wg / gridDim.x;
-  const int by = byz % gridDim.y, bz = byz / gridDim.y;
+  // order_hint 2 (set by the launcher): N tiles fastest, so an XCD keeps its few A
+  // panels in L2 and streams B (fc forward: A re-read once per N tile otherwise)
+  int bx, by, bz;
+  if (d.order_hint == 2) {
+    by = wg % gridDim.y;
+    const int r = wg / gridDim.y;
+    bx = r % gridDim.x;
+    bz = r / gridDim.x;
+  } else {
+    bx = wg % gridDim.x;
+    const int r = wg / gridDim.x;
+    by = r % gridDim.y;
+    bz = r / gridDim.y;
+  }
   const int cls = bz;
   const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
   const uint32_t OWv = OWC ? OWC : d.OW;
   const int M = d.N * OHW;
-  const int m0 = bx * FWD_BM;
+  const int m0 = bx * BM;
   const int n0 = by * FWD_BN;
   // online / target weight sets in one launch: the switch row is block-uniform
   const bool second = d.w2 != nullptr && m0 >= d.m_switch;
@@ -193,9 +212,9 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 
   // per-thread staging rows (4 A rows, 2 B rows): loop-invariant byte offsets.
   // Rows past M are clamped to row 0 (their outputs are never stored).
-  uint32_t a_off[4], vmask[4];
+  uint32_t a_off[AR], vmask[AR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < AR; ++i) {
     const int m = m0 + srow + 32 * i;
     const int mm = m < M ? m : 0;
     if (MODE == 0) {
@@ -231,24 +250,22 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     const uint32_t bso = BT ? (uint32_t)(d.bt == 2 ? kt * 128 * d.ldb : 2 * d.koff[cls * KT + kt]) : (uint32_t)kt * 128u;
     R.b0 = buf_ld16(rb_rs, b_off0, bso);
     R.b1 = buf_ld16(rb_rs, b_off1, bso);
-    uint4 ra[4];
     if (MODE == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ra[i] = buf_ld16(ra_rs, a_off[i], (uint32_t)kt * 128u);
+      for (int i = 0; i < AR; ++i) R.a[i] = buf_ld16(ra_rs, a_off[i], (uint32_t)kt * 128u);
     } else {
       const int tap = c_kh * d.KW + c_kw;
       const uint32_t toff = (uint32_t)(((c_kh * d.W + c_kw) * d.Cin + (c_cb << 6)) * 2);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < AR; ++i) {
         if (PAD) {
           const uint32_t vo = ((vmask[i] >> tap) & 1u) ? a_off[i] + toff : BUF_OOB;
-          ra[i] = buf_ld16(ra_rs, vo, 0);
+          R.a[i] = buf_ld16(ra_rs, vo, 0);
         } else {
-          ra[i] = buf_ld16(ra_rs, a_off[i], toff);
+          R.a[i] = buf_ld16(ra_rs, a_off[i], toff);
         }
       }
     }
-    R.a0 = ra[0]; R.a1 = ra[1]; R.a2 = ra[2]; R.a3 = ra[3];
     if (lt < KT - 1) {
       ++lt;
       if (MODE == 1 && ++c_cb == cpb) {
@@ -259,12 +276,10 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   };
 
   auto write_tile = [&](int buf, const FwdRegs& R) {
-    uint8_t* As = smem + buf * FWD_STAGE;
-    uint8_t* Bs = As + FWD_BM * 128;
-    *reinterpret_cast<uint4*>(As + swz_row(srow, sc)) = R.a0;
-    *reinterpret_cast<uint4*>(As + swz_row(srow + 32, sc)) = R.a1;
-    *reinterpret_cast<uint4*>(As + swz_row(srow + 64, sc)) = R.a2;
-    *reinterpret_cast<uint4*>(As + swz_row(srow + 96, sc)) = R.a3;
+    uint8_t* As = smem + buf * STAGE;
+    uint8_t* Bs = As + BM * 128;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) *reinterpret_cast<uint4*>(As + swz_row(srow + 32 * i, sc)) = R.a[i];
     *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow, sc) : swz_row(srow, sc))) = R.b0;
     *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow + 32, sc) : swz_row(srow + 32, sc))) = R.b1;
   };
@@ -272,28 +287,28 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   // acc[mt][nt] holds C^T (channels x pixels): lane (g = lane>>4, p = lane&15) owns
   // channels 16nt + 4g + {0..3} of pixel 16mt + p -- 4 consecutive channels, so the
   // epilogue packs them with v_cvt_pk_bf16_f32 into one 8-byte LDS write.
-  f32x4 acc[2][4];
+  f32x4 acc[MT][4];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MT; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](int buf) {
-    const uint8_t* As = smem + buf * FWD_STAGE;
-    const uint8_t* Bs = As + FWD_BM * 128;
+    const uint8_t* As = smem + buf * STAGE;
+    const uint8_t* Bs = As + BM * 128;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = 4 * s + (lane >> 4);
-      bf16x8 a[2], b[4];
+      bf16x8 a[MT], b[4];
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-        a[mt] = *reinterpret_cast<const bf16x8*>(As + swz_row(32 * wv + 16 * mt + (lane & 15), c));
+      for (int mt = 0; mt < MT; ++mt)
+        a[mt] = *reinterpret_cast<const bf16x8*>(As + swz_row(WR * wv + 16 * mt + (lane & 15), c));
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         b[nt] = BT ? tr_frag8(Bs, s, 16 * nt, lane)
                    : *reinterpret_cast<const bf16x8*>(Bs + swz_row(16 * nt + (lane & 15), c));
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
+      for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
@@ -325,7 +340,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   __syncthreads();
 
   // ---- epilogue: (acc*scale + bias) -> bf16x4 per lane -> swizzled LDS image -> 16-B row stores
-  uint8_t* Es = smem + wv * 4096;
+  uint8_t* Es = smem + wv * (WR * 128);
   const int g = lane >> 4, pl = lane & 15;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
@@ -336,7 +351,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
       b4[0] = bb.x; b4[1] = bb.y; b4[2] = bb.z; b4[3] = bb.w;
     }
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
+    for (int mt = 0; mt < MT; ++mt) {
       const int row = 16 * mt + pl;
       const uint2 v = make_uint2(cvt_pk_bf16(acc[mt][nt][0] * d.in_scale + b4[0], acc[mt][nt][1] * d.in_scale + b4[1]),
                                  cvt_pk_bf16(acc[mt][nt][2] * d.in_scale + b4[2], acc[mt][nt][3] * d.in_scale + b4[3]));
@@ -347,9 +362,9 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const int ooh = (d.ncls == 4) ? (cls >> 1) : 0;
   const int oow = (d.ncls == 4) ? (cls & 1) : 0;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < WR / 8; ++p) {
     const int row = 8 * p + (lane >> 3), ch = lane & 7;
-    const int m = m0 + 32 * wv + row;
+    const int m = m0 + WR * wv + row;
     if (m >= M) continue;
     uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
     const int img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
@@ -693,6 +708,24 @@ __global__ void pack_conv_dgrad_weights_kernel(const bf16_t* __restrict__ w3, co
 }
 
 // ------------------------------------------------------------------ launchers
+template <int BM>
+static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
+  const bool pad = d.pad_h > 0 || d.pad_w > 0;
+  const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
+  if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true, 1, 1, BM><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0) igemm_fwd_kernel<0, false, false, 1, 1, BM><<<grid, 256, 0, st>>>(d);
+  else if (pad && d.bt) {
+    // dgrad: conv3 (9x9 out), conv2 per parity class (10x10 out)
+    if (g9) igemm_fwd_kernel<1, true, true, 9, 81, BM><<<grid, 256, 0, st>>>(d);
+    else if (g10) igemm_fwd_kernel<1, true, true, 10, 100, BM><<<grid, 256, 0, st>>>(d);
+    else igemm_fwd_kernel<1, true, true, 0, 0, BM><<<grid, 256, 0, st>>>(d);
+  } else if (pad) igemm_fwd_kernel<1, true, false, 0, 0, BM><<<grid, 256, 0, st>>>(d);
+  else if (d.bt) igemm_fwd_kernel<1, false, true, 0, 0, BM><<<grid, 256, 0, st>>>(d);
+  else if (g9) igemm_fwd_kernel<1, false, false, 9, 81, BM><<<grid, 256, 0, st>>>(d);   // conv2 fwd
+  else if (g7) igemm_fwd_kernel<1, false, false, 7, 49, BM><<<grid, 256, 0, st>>>(d);   // conv3 fwd
+  else igemm_fwd_kernel<1, false, false, 0, 0, BM><<<grid, 256, 0, st>>>(d);
+}
+
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if ((d.K & 63) || (d.Cout & 63) || d.K <= 0) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
@@ -701,24 +734,21 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   const int64_t xbytes = d.mode == 0 ? (int64_t)d.N * d.K * 2 : (int64_t)d.N * d.H * d.W * d.Cin * 2;
   if (xbytes >= 0x7ffffff0LL) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.pad_h > 0 || d.pad_w > 0) && d.KH * d.KW > 32) return (int)hipErrorInvalidValue;
-  if (d.w2 != nullptr && (d.m_switch % FWD_BM)) return (int)hipErrorInvalidValue;
-  const int M = d.N * d.OH * d.OW;
-  dim3 grid((M + FWD_BM - 1) / FWD_BM, d.Cout / FWD_BN, d.ncls > 0 ? d.ncls : 1);
-  const bool pad = d.pad_h > 0 || d.pad_w > 0;
+  if (d.w2 != nullptr && (d.m_switch % 128)) return (int)hipErrorInvalidValue;
   if (d.bt == 1 && (d.K >> 6) * (d.ncls > 0 ? d.ncls : 1) > 16) return (int)hipErrorInvalidValue;
-  const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
-  if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true, 1, 1><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 0) igemm_fwd_kernel<0, false, false, 1, 1><<<grid, 256, 0, st>>>(d);
-  else if (pad && d.bt) {
-    // dgrad: conv3 (9x9 out), conv2 per parity class (10x10 out)
-    if (g9) igemm_fwd_kernel<1, true, true, 9, 81><<<grid, 256, 0, st>>>(d);
-    else if (g10) igemm_fwd_kernel<1, true, true, 10, 100><<<grid, 256, 0, st>>>(d);
-    else igemm_fwd_kernel<1, true, true, 0, 0><<<grid, 256, 0, st>>>(d);
-  } else if (pad) igemm_fwd_kernel<1, true, false, 0, 0><<<grid, 256, 0, st>>>(d);
-  else if (d.bt) igemm_fwd_kernel<1, false, true, 0, 0><<<grid, 256, 0, st>>>(d);
-  else if (g9) igemm_fwd_kernel<1, false, false, 9, 81><<<grid, 256, 0, st>>>(d);   // conv2 fwd
-  else if (g7) igemm_fwd_kernel<1, false, false, 7, 49><<<grid, 256, 0, st>>>(d);   // conv3 fwd
-  else igemm_fwd_kernel<1, false, false, 0, 0><<<grid, 256, 0, st>>>(d);
+  const int M = d.N * d.OH * d.OW;
+  const int ncls = d.ncls > 0 ? d.ncls : 1;
+  // 128-row tiles unless that leaves the chip under ~2.5 blocks per CU
+  const int64_t blocks128 = (int64_t)((M + 127) / 128) * (d.Cout / FWD_BN) * ncls;
+  const bool pad = d.pad_h > 0 || d.pad_w > 0;
+  // measured (scripts/bench_kernels.py sweep): 64-row tiles pay off for the dgrad
+  // GEMMs (K-major B): conv3/conv2 dgrad and fc dgrad; 128 for the forward GEMMs
+  bool bm64 = d.bt != 0 && (pad || blocks128 < 640);
+  if (d.tile_hint == 1) bm64 = false;
+  if (d.tile_hint == 2) bm64 = true;
+  if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
+  if (bm64) launch_fwd<64>(d, dim3((M + 63) / 64, d.Cout / FWD_BN, ncls), st);
+  else launch_fwd<128>(d, dim3((M + 127) / 128, d.Cout / FWD_BN, ncls), st);
   APEX_CHECK_LAUNCH();
 }
 

@@ -150,13 +150,14 @@ class FusedNatureLearner:
     # ---------------------------------------------------------------- step
     # The step is three segments.  With one rank they run back to back (one HIP
     # graph).  With data parallelism the flat gradient is all-reduced in two
-    # buckets over RCCL: the fc+heads bucket (12.9 MB, ready after segment 1)
-    # is reduced on RCCL's stream WHILE segment 2 computes the conv backward on
-    # the compute stream; the small conv bucket follows; segment 3 (clip +
-    # RMSprop + priority write-back) waits for both.  Gradients are pre-scaled by
-    # 1/(B*world) in the head kernel, so the SUM all-reduce yields the mean.
+    # buckets over RCCL: the fc+heads bucket (12.9 MB, complete once segment 1
+    # has produced the head and fc WEIGHT gradients) is reduced on RCCL's stream
+    # WHILE segment 2 runs the fc dgrad and the whole conv backward on the compute
+    # stream; the small conv bucket follows; segment 3 (clip + RMSprop) waits for
+    # both.  Gradients are pre-scaled by 1/(B*world) in the head kernel, so the SUM
+    # all-reduce yields the mean.
     def _seg1(self) -> None:
-        """sample, forward (online+target), loss/priorities, head + fc backward."""
+        """sample, forward (online+target), loss/priorities, head + fc weight gradients."""
         B, rt, ops = self.B, self.rt, self.ops
         ops.prepare(self.Pb)
         # the sampler writes the frame-ring slots of S_t / S_{t+n} (twice) into self.slots
@@ -175,15 +176,16 @@ class FusedNatureLearner:
             self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
         with self._on_side(self.rt.overlap_wgrad):
             ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"])
-        ops.fc_dgrad(self.dH, self.y3[:B], self.Pb["wfc"], self.dY3)
         if self.world > 1:
-            self._join_side()   # the fc bucket all-reduce follows this segment
-        self._mark("fc_backward")
+            self._join_side()   # the fc/heads bucket all-reduce starts right after this segment
+        self._mark("fc_wgrad")
 
     def _seg2(self) -> None:
-        """conv backward: the dgrad chain on the compute stream, conv3/conv2 wgrad on
-        the side stream as soon as their dY is ready, conv1 wgrad last."""
+        """fc dgrad + conv backward (with DP, all of it overlaps the fc/heads bucket
+        all-reduce): the dgrad chain, conv3/conv2 wgrad (side stream when
+        ``overlap_wgrad``), conv1 wgrad last."""
         B, rt, ops, G, Pb = self.B, self.rt, self.ops, self.G, self.Pb
+        ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3)
         with self._on_side(rt.overlap_wgrad):
             ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"])
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2)
@@ -208,7 +210,7 @@ class FusedNatureLearner:
     def profile_step(self) -> Dict[str, float]:
         """Run ONE eager (un-graphed) learner step with CUDA events between its
         phases; returns milliseconds per phase (sample, forward, head,
-        fc_backward, conv_backward, [allreduce_wait], optimizer, priorities) and
+        fc_wgrad, conv_backward (fc dgrad + convs), [allreduce_wait], optimizer) and
         the total.  Counts as a normal update."""
         if self.device.type != "cuda":
             return {}

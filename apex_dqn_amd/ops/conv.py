@@ -26,6 +26,14 @@ class Workspace:
         return t
 
 
+# launch-shape overrides for tuning sweeps (scripts/bench_kernels.py); 0 = kernel's choice
+_HINTS: Dict[str, int] = {}
+
+
+def set_launch_hints(tile: int = 0, order: int = 0) -> None:
+    _HINTS["tile"], _HINTS["order"] = int(tile), int(order)
+
+
 def _conv_desc(**kw) -> "_lib.ConvDesc":
     d = _lib.ConvDesc()
     d.x = kw.get("x")
@@ -49,6 +57,7 @@ def _conv_desc(**kw) -> "_lib.ConvDesc":
     d.bias2 = kw.get("bias2")
     d.m_switch = kw.get("m_switch", 0)
     d.bt, d.ldb = kw.get("bt", 0), kw.get("ldb", 0)
+    d.tile_hint, d.order_hint = _HINTS.get("tile", 0), _HINTS.get("order", 0)
     for i, v in enumerate(kw.get("koff", ())):
         d.koff[i] = v
     return d

@@ -80,6 +80,13 @@ def main():
         ops[f"conv1_wgrad@{tr}"] = (lambda tr=tr: C.conv1_wgrad_ring(lib, ws, dY1, ring, slots[:B], 1 / 255.,
                                                                     gw[:64 * 256].view(64, 4, 8, 8), gb[:64],
                                                                     target_rows=tr), F(B * 400 * 64 * 256))
+    # launch-shape sweep of the forward-family GEMMs (tile 1: BM=128, 2: BM=64; order 1: M fastest, 2: N fastest)
+    for tile in (1, 2):
+        for order in (1, 2):
+            for nm in ("fc_fwd", "fc_dgrad", "conv3_fwd", "conv2_fwd", "conv3_dgrad", "conv2_dgrad"):
+                fn, fl = ops[nm]
+                ops[f"{nm}@t{tile}o{order}"] = ((lambda fn=fn, tile=tile, order=order:
+                                                (C.set_launch_hints(tile, order), fn(), C.set_launch_hints())), fl)
     total = 0.0
     for name, (fn, flops) in ops.items():
         if a.only and name not in a.only.split(","):
