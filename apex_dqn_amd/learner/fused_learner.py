@@ -88,6 +88,12 @@ class FusedNatureLearner:
         # need the head's outputs (head wgrad, priority write-back into the sum-tree):
         # a few blocks each, they run beside the backward GEMMs instead of between them.
         self._side = torch.cuda.Stream(d) if d.type == "cuda" else None
+        # DP gradient payload: fp32 in place, or a bf16 copy (cast inside the captured
+        # segments, summed by RCCL in bf16, cast back before the optimizer)
+        if self.rt.allreduce_dtype not in ("fp32", "bf16"):
+            raise ValueError("Runtime.allreduce_dtype must be fp32 or bf16")
+        self._comm_bf16 = self.world > 1 and self.rt.allreduce_dtype == "bf16"
+        self.gcomm = torch.zeros(n, dtype=torch.bfloat16, device=d) if self._comm_bf16 else self.g32
         # cross-shard IS-weight normaliser: min over ranks of (min_i p_i / total)
         self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
         self.ratio_buf = torch.zeros(1, dtype=torch.float32, device=d)
@@ -178,6 +184,9 @@ class FusedNatureLearner:
             ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"])
         if self.world > 1:
             self._join_side()   # the fc/heads bucket all-reduce starts right after this segment
+            if self._comm_bf16:
+                cut = self.layout.offsets["wfc"]
+                self.gcomm[cut:].copy_(self.g32[cut:])
         self._mark("fc_wgrad")
 
     def _seg2(self) -> None:
@@ -195,6 +204,9 @@ class FusedNatureLearner:
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"])
         self._join_side()
+        if self._comm_bf16:
+            cut = self.layout.offsets["wfc"]
+            self.gcomm[:cut].copy_(self.g32[:cut])
         self._mark("conv_backward")
 
     # ------------------------------------------------------- phase timing
@@ -249,6 +261,8 @@ class FusedNatureLearner:
         """clip + centered RMSprop (+bf16 pack), shard stats (the priority write-back
         ran on the side stream right after the head kernel)."""
         rt, ops = self.rt, self.ops
+        if self._comm_bf16:
+            self.g32.copy_(self.gcomm)
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
         self._mark("optimizer")
@@ -272,9 +286,9 @@ class FusedNatureLearner:
             self._ratio_work.wait()
             self.ratio_min.copy_(self.ratio_buf)
         run(0)
-        w_fc = dist.all_reduce(self.g32[cut:], op=dist.ReduceOp.SUM, async_op=True)
+        w_fc = dist.all_reduce(self.gcomm[cut:], op=dist.ReduceOp.SUM, async_op=True)
         run(1)  # conv backward overlaps the fc/head bucket all-reduce
-        w_cv = dist.all_reduce(self.g32[:cut], op=dist.ReduceOp.SUM, async_op=True)
+        w_cv = dist.all_reduce(self.gcomm[:cut], op=dist.ReduceOp.SUM, async_op=True)
         w_fc.wait()
         w_cv.wait()
         self._mark("allreduce_wait")

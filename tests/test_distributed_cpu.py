@@ -15,10 +15,10 @@ import torch.multiprocessing as mp
 from apex_dqn_amd.config import ApexConfig
 
 
-def _cfg():
+def _cfg(ar="fp32"):
     return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
                                  "Learner": {"replay_sample_size": 6},
-                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0}})
+                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0, "allreduce_dtype": ar}})
 
 
 def _replay(rank):
@@ -33,12 +33,12 @@ def _replay(rank):
     return rp
 
 
-def _worker(rank, world, path, q):
+def _worker(rank, world, path, q, ar="fp32"):
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.parallel.dist import Comm
     torch.set_num_threads(2)
     comm = Comm.init(rank, world, f"file://{path}", backend="gloo")
-    cfg = _cfg()
+    cfg = _cfg(ar)
     torch.manual_seed(1234 + rank)  # different local init: rank 0's params must be broadcast
     rp = _replay(rank)
     L = FusedNatureLearner(cfg, "cpu", rp, comm=comm)
@@ -68,13 +68,14 @@ def _worker(rank, world, path, q):
 
 
 @pytest.mark.slow
-def test_dp_learner_gloo_world2():
+@pytest.mark.parametrize("ar", ["fp32", "bf16"])
+def test_dp_learner_gloo_world2(ar):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "store")
-        procs = [ctx.Process(target=_worker, args=(r, world, path, q)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, path, q, ar)) for r in range(world)]
         for p in procs:
             p.start()
         res = [q.get(timeout=240) for _ in range(world)]
@@ -82,8 +83,9 @@ def test_dp_learner_gloo_world2():
             p.join(timeout=60)
             assert p.exitcode == 0
     ratios = [r[5] for r in res]
+    tol = 1e-6 if ar == "fp32" else 1e-2          # bf16 payload: ~3 significant digits
     for rank, gerr, gmax, perr, ratio_g, _ in res:
-        assert gerr <= 1e-6 * max(gmax, 1e-6) + 1e-9, (rank, gerr, gmax)
+        assert gerr <= tol * max(gmax, 1e-6) + 1e-9, (rank, gerr, gmax)
         assert perr == 0.0
         assert ratio_g == pytest.approx(min(ratios), rel=1e-5)
 
