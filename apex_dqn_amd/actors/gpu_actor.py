@@ -137,11 +137,65 @@ class GpuActorGroup:
         return n
 
 
+class GraphActorGroup(GpuActorGroup):
+    """Actor group for ``GraphLearner`` networks (IMPALA-deep, nature32, ...): the
+    frame stacks are gathered from the replay ring on the device, the actor's own
+    network copy (refreshed every ``Q_network_sync_freq`` steps) runs in bf16, and
+    epsilon-greedy is drawn on the device; one small D2H copy per step."""
+
+    def __init__(self, cfg, learner, replay, env, num_envs: int, global_offset: int = 0,
+                 total_actors: Optional[int] = None, seed: int = 0):
+        import copy
+        self.cfg, self.learner, self.replay, self.env = cfg, learner, replay, env
+        self.E, self.C, self.A = int(num_envs), learner.C, learner.A
+        d = learner.device
+        self.device = d
+        a = cfg.Actor
+        total = total_actors or self.E
+        ladder = epsilon_ladder(total, a.epsilon, a.alpha)
+        self.eps = torch.tensor(ladder[global_offset:global_offset + self.E], dtype=torch.float32, device=d)
+        self.gen = torch.Generator(device=d)
+        self.gen.manual_seed(int(seed) * 7919 + global_offset)
+        self.slots = torch.zeros(self.E, self.C, dtype=torch.int32, device=d)
+        self.net = copy.deepcopy(learner.Q)
+        for p in self.net.parameters():
+            p.requires_grad_(False)
+        self.q_host = torch.zeros(self.E, self.A, dtype=torch.float32)
+        self.a_host = torch.zeros(self.E, dtype=torch.int64)
+        if d.type == "cuda":
+            self.q_host, self.a_host = self.q_host.pin_memory(), self.a_host.pin_memory()
+        self.builder = NStepBuilder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.payload = None
+        self.t = 0
+        self.episodes = []
+        self.inserted = 0
+
+    def sync_params(self) -> None:
+        with torch.no_grad():
+            for dst, src in zip(self.net.parameters(), self.learner.Q.parameters()):
+                dst.copy_(src)
+
+    def policy(self, payload: np.ndarray):
+        self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
+        frames = self.replay.gather_frames(self.slots)
+        q = self.learner.actor_forward(self.net, frames)
+        greedy = q.argmax(dim=1)
+        u = torch.rand(self.E, generator=self.gen, device=self.device)
+        rand_a = torch.randint(0, self.A, (self.E,), generator=self.gen, device=self.device)
+        act = torch.where(u < self.eps, rand_a, greedy)
+        self.q_host.copy_(q, non_blocking=True)
+        self.a_host.copy_(act, non_blocking=True)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        return self.q_host.numpy().copy(), self.a_host.numpy().copy()
+
+
 def make_gpu_actor_group(cfg, learner, replay, num_envs: int, rank: int = 0, world: int = 1,
                          seed: int = 0) -> GpuActorGroup:
     from ..envs.vector_envs import make_vec_env
     total = max(cfg.Actor.num_actors, num_envs * world)
     env = make_vec_env(cfg.env_backend, cfg.env_conf.name, num_envs, cfg.env_conf.action_dim,
                        seed=seed + 1000 * rank)
-    return GpuActorGroup(cfg, learner, replay, env, num_envs, global_offset=rank * num_envs,
-                         total_actors=total, seed=seed + rank)
+    cls = GraphActorGroup if getattr(learner, "kind", "") == "graph" else GpuActorGroup
+    return cls(cfg, learner, replay, env, num_envs, global_offset=rank * num_envs,
+               total_actors=total, seed=seed + rank)

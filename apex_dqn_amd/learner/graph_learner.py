@@ -1,0 +1,243 @@
+"""GPU-resident learner for any image network (IMPALA-deep ResNet, nature32, ...).
+
+The NatureCNN has the fully hand-written learner (``fused_learner.py``).  Every
+other image network runs here with the same GPU-first structure:
+
+* samples come from the HBM replay shard (``csrc/sumtree.hip`` sampling, frame
+  gather straight from the uint8 ring) -- no host round trip;
+* the network is a torch module whose parameters and gradients are VIEWS into
+  one flat fp32 buffer each, so the clip + centered RMSprop step is the fused
+  HIP optimizer kernel over the whole model (``csrc/optimizer.hip``) and the DP
+  all-reduce is one flat RCCL call;
+* forward/backward run in bf16 autocast (MIOpen / hipBLASLt convs and GEMMs);
+* the whole update -- sample, gather, 3 forwards, DDQN Huber*IS loss, backward,
+  optimizer, priority write-back -- is captured in ONE HIP graph (two segments
+  around the gradient all-reduce with data parallelism).
+
+Reference semantics are those of ``learner.py:29-80`` with the defects fixed
+(SURVEY Appendix A): terminal mask via Gamma, IS weights, Huber, centered
+RMSprop with decay 0.95, target sync every ``q_target_sync_freq`` steps.
+"""
+from __future__ import annotations
+
+import copy
+from typing import Dict, List, Optional
+
+import torch
+
+from ..config import ApexConfig
+from ..models.dueling import build_network
+from ..ops.fused_ops import HipBackend, TorchBackend
+from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from .losses import ddqn_loss
+
+
+def _flatten_module(module: torch.nn.Module, device) -> torch.Tensor:
+    """Move every parameter of ``module`` into one contiguous fp32 buffer (params
+    become views of it).  Returns the buffer."""
+    params = list(module.parameters())
+    n = sum(p.numel() for p in params)
+    flat = torch.zeros(n, dtype=torch.float32, device=device)
+    off = 0
+    for p in params:
+        k = p.numel()
+        flat[off:off + k].copy_(p.data.reshape(-1))
+        p.data = flat[off:off + k].view_as(p)
+        off += k
+    return flat
+
+
+class GraphLearner:
+    kind = "graph"
+
+    def __init__(self, cfg: ApexConfig, device, replay, comm=None, batch_size: Optional[int] = None):
+        self.cfg = cfg
+        self.rt = cfg.Runtime
+        self.device = torch.device(device)
+        self.replay = replay
+        self.comm = comm
+        self.world = comm.world_size if comm is not None else 1
+        self.C = cfg.frame_stack
+        self.A = int(cfg.env_conf.action_dim)
+        self.B = int(batch_size or cfg.Learner.replay_sample_size)
+        d = self.device
+        self.Q = build_network(cfg.network, cfg.env_conf.state_shape, self.A, obs_scale=self.rt.obs_scale).to(d)
+        self.p32 = _flatten_module(self.Q, d)
+        if comm is not None and comm.world_size > 1:
+            comm.broadcast_flat(self.p32)
+        self.g32 = torch.zeros_like(self.p32)
+        for p, g in zip(self.Q.parameters(), self._views(self.g32)):
+            p.grad = g
+        self.Q_target = copy.deepcopy(self.Q)
+        for p in self.Q_target.parameters():
+            p.requires_grad_(False)
+        self.t32 = _flatten_module(self.Q_target, d)
+        self.rms_v = torch.zeros_like(self.p32)
+        self.rms_m = torch.zeros_like(self.p32)
+        self.pbf = torch.zeros(self.p32.numel(), dtype=torch.bfloat16, device=d)
+        self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
+        self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
+        self.ops = HipBackend(native_conv=False) if (d.type == "cuda" and self.rt.use_hip_kernels) else \
+            TorchBackend(torch.float32)
+        self.S = replay.alloc_sample_buffers(self.B)
+        self.td_abs = torch.zeros(self.B, dtype=torch.float32, device=d)
+        self.loss_b = torch.zeros(1, dtype=torch.float32, device=d)
+        self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d) if self.world > 1 else None
+        if self.world > 1:
+            self._init_ratio()
+        self.num_q_updates = 0
+        self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
+        ls = cfg.Learner.load_saved_state
+        if ls:
+            self.load(ls)
+
+    def _views(self, flat: torch.Tensor) -> List[torch.Tensor]:
+        out, off = [], 0
+        for p in self.Q.parameters():
+            k = p.numel()
+            out.append(flat[off:off + k].view_as(p))
+            off += k
+        return out
+
+    # ---------------------------------------------------------------- step
+    def _forward_backward(self) -> None:
+        rt, B = self.rt, self.B
+        S = self.replay.sample(B, out=self.S, ratio_min_global=self.ratio_min)
+        obs = self.replay.gather_frames(S["obs"])
+        nxt = self.replay.gather_frames(S["nxt"])
+        self.g32.zero_()
+        # cache_enabled=False: autocast's weight-cast cache must not outlive a graph capture
+        amp = torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False) \
+            if self.device.type == "cuda" else torch.autocast(device_type="cpu", enabled=False)
+        with amp:
+            q_t = self.Q(obs)[2]
+            with torch.no_grad():
+                q_n = self.Q(nxt)[2]
+                q_g = self.Q_target(nxt)[2]
+        w = S["weights"] if rt.use_is_weights else None
+        loss, td = ddqn_loss(q_t.float(), q_n.float(), q_g.float(), S["act"], S["rew"], S["gam"], w,
+                             loss=rt.loss, kappa=rt.huber_delta)
+        (loss / self.world).backward()     # SUM all-reduce of 1/world-scaled grads = mean
+        self.td_abs.copy_(td)
+        self.loss_b.copy_(loss.detach().view(1))
+
+    def _apply(self) -> None:
+        rt = self.rt
+        self.ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
+                           rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
+        self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
+
+    def _allreduce(self) -> None:
+        import torch.distributed as dist
+        dist.all_reduce(self.g32, op=dist.ReduceOp.SUM)
+
+    def _capture(self) -> None:
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        snap = [t.clone() for t in (self.p32, self.rms_v, self.rms_m, self.replay.leaf, self.replay.nodes,
+                                    self.replay.min_bits, self.replay.ctr)]
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._forward_backward()
+                if self.world > 1:
+                    self._allreduce()
+                self._apply()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        for dst, src in zip((self.p32, self.rms_v, self.rms_m, self.replay.leaf, self.replay.nodes,
+                             self.replay.min_bits, self.replay.ctr), snap):
+            dst.copy_(src)
+        torch.cuda.synchronize(self.device)
+        segs = [self._forward_backward, self._apply] if self.world > 1 else \
+            [lambda: (self._forward_backward(), self._apply())]
+        self._graphs = []
+        for seg in segs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                seg()
+            self._graphs.append(g)
+
+    def step(self) -> None:
+        graphs = self.rt.use_graphs and self.device.type == "cuda"
+        if graphs and self._graphs is None:
+            self._capture()
+        if graphs:
+            self._graphs[0].replay()
+            if self.world > 1:
+                self._allreduce()
+                self._graphs[1].replay()
+        else:
+            self._forward_backward()
+            if self.world > 1:
+                self._allreduce()
+            self._apply()
+        if self.world > 1:
+            self._update_ratio()
+        self.num_q_updates += 1
+        if self.num_q_updates % self.cfg.Learner.q_target_sync_freq == 0:
+            self.sync_target()
+
+    # --------------------------------------------------- replay statistics
+    def _local_ratio(self) -> torch.Tensor:
+        rp = self.replay
+        tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float().clamp_min(1e-30)
+        return rp.min_bits.view(torch.float32) / tot
+
+    def _init_ratio(self) -> None:
+        import torch.distributed as dist
+        self.ratio_min.copy_(self._local_ratio())
+        dist.all_reduce(self.ratio_min, op=dist.ReduceOp.MIN)
+
+    _update_ratio = _init_ratio
+
+    def refresh_replay_stats(self) -> None:
+        if self.world > 1:
+            self._init_ratio()
+
+    def sync_target(self) -> None:
+        self.t32.copy_(self.p32)
+
+    # ------------------------------------------------------------- metrics
+    def last_metrics(self) -> Dict[str, float]:
+        return {"loss": float(self.loss_b[0]), "td_abs_mean": float(self.td_abs.mean()),
+                "grad_norm": float(self.gnorm[0])}
+
+    def profile_step(self) -> Dict[str, float]:
+        if self.device.type != "cuda":
+            return {}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.step()
+        e1.record()
+        torch.cuda.synchronize(self.device)
+        return {"total": e0.elapsed_time(e1)}
+
+    # ------------------------------------------------------------------ io
+    def actor_forward(self, net: torch.nn.Module, frames: torch.Tensor) -> torch.Tensor:
+        amp = torch.autocast(device_type="cuda", dtype=torch.bfloat16) if self.device.type == "cuda" \
+            else torch.autocast(device_type="cpu", enabled=False)
+        with torch.no_grad(), amp:
+            return net(frames)[2].float()
+
+    def save(self, path: str) -> None:
+        save_checkpoint(path, self.Q.state_dict(), Q_target_state=self.Q_target.state_dict(),
+                        optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
+                        num_q_updates=self.num_q_updates, config=self.cfg.to_dict())
+
+    def load(self, path: str) -> bool:
+        ck = load_checkpoint(path)
+        if ck is None:
+            return False
+        with torch.no_grad():
+            for p, v in zip(self.Q.state_dict().values(), ck["Q_state"].values()):
+                p.copy_(v)
+            if "Q_target_state" in ck:
+                for p, v in zip(self.Q_target.state_dict().values(), ck["Q_target_state"].values()):
+                    p.copy_(v)
+            else:
+                self.sync_target()
+            opt = ck.get("optimizer_state") or {}
+            if "rms_v" in opt:
+                self.rms_v.copy_(opt["rms_v"])
+                self.rms_m.copy_(opt["rms_m"])
+        self.num_q_updates = int(ck.get("num_q_updates", 0))
+        return True

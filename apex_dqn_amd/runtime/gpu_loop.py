@@ -56,7 +56,11 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     E = num_envs or cfg.Runtime.actors_per_rank or max(1, cfg.Actor.num_actors // world)
     torch.manual_seed(rt.seed)
     replay = build_replay(cfg, device, E, seed=rt.seed + rank)
-    learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=backend)
+    if cfg.network == "nature64":
+        learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=backend)
+    else:   # IMPALA-deep, nature32: graph-captured torch-autograd learner on the same HBM replay
+        from ..learner.graph_learner import GraphLearner
+        learner = GraphLearner(cfg, device, replay, comm=comm)
     group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed)
     min_local = max(L.min_replay_mem_size // world, L.replay_sample_size)
     started = False
@@ -111,6 +115,7 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                 lens = [ln for (_, ln, _) in group.episodes[-50:]]
                 metrics.log("learner", step=n, loss=m["loss"], td_abs=m["td_abs_mean"], grad_norm=m["grad_norm"],
                             is_weight_mean=float(learner.S["weights"].mean()),
+                            learner_kind=getattr(learner, "kind", "fused"),
                             replay=replay.size(), actor_steps=actor_steps, inserted=group.inserted,
                             episodes=len(group.episodes),
                             mean_return=float(np.mean(rets)) if rets else float("nan"),

@@ -53,7 +53,7 @@ def main(argv=None):
               "\n runtime:{}".format(d["env_conf"], d["Actor"], d["Learner"], d["Replay_Memory"], d["Runtime"]))
     metrics = MetricsLogger(args.metrics or cfg.Runtime.metrics_path, rank=rank, echo=True)
     mode = args.mode
-    image = len(cfg.env_conf.state_shape) == 3 and cfg.network in ("nature64",)
+    image = len(cfg.env_conf.state_shape) == 3 and cfg.network in ("nature64", "nature32", "impala")
     if mode == "auto":
         mode = "gpu" if (torch.cuda.is_available() and image) else "multiproc"
     if mode == "gpu":

@@ -121,3 +121,22 @@ def test_dp_learner_two_ranks_on_one_gpu(tmp_path):
     for rank, perr, finite, gnorm, ratio in res:
         assert perr == 0.0 and finite and gnorm > 0      # replicas bit-identical after 4 DP steps
     assert res[0][4] == res[1][4]                        # same global IS normaliser on both ranks
+
+
+def test_graph_learner_impala_with_hip_graph():
+    """IMPALA-deep on the GPU loop: HBM replay + graph-captured autograd learner."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.runtime.gpu_loop import train_frames
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Actor": {"num_actors": 16, "n_step_transition_batch_size": 16,
+                                          "Q_network_sync_freq": 10},
+                                "Learner": {"min_replay_mem_size": 300, "replay_sample_size": 64,
+                                            "remove_old_xp_freq": 10, "q_target_sync_freq": 20},
+                                "Replay_Memory": {"soft_capacity": 2000},
+                                "Runtime": {"replay_capacity": 2500, "log_every": 0, "use_graphs": True,
+                                            "network": "impala"}})
+    out = train_frames(cfg, DEV, 30)
+    L = out["learner"]
+    assert L.kind == "graph" and L.num_q_updates == 30 and L._graphs is not None
+    m = L.last_metrics()
+    assert np.isfinite(m["loss"]) and m["grad_norm"] > 0

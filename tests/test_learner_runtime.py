@@ -161,3 +161,26 @@ def test_main_cli_inline_cartpole():
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     assert '"learner_steps": 50' in r.stdout
+
+
+@pytest.mark.parametrize("net", ["impala", "nature32"])
+def test_graph_learner_loop_on_cpu(tmp_path, net):
+    """IMPALA-deep / nature32 run the GPU-resident loop with the graph learner
+    (HBM-replay API, flat-buffer params, fused optimizer path) -- CPU here."""
+    from apex_dqn_amd.runtime.gpu_loop import train_frames
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 4, "name": "Synthetic"},
+                                "Actor": {"num_actors": 6, "n_step_transition_batch_size": 6,
+                                          "Q_network_sync_freq": 5},
+                                "Learner": {"min_replay_mem_size": 40, "replay_sample_size": 8,
+                                            "remove_old_xp_freq": 4, "q_target_sync_freq": 5},
+                                "Replay_Memory": {"soft_capacity": 120},
+                                "Runtime": {"replay_capacity": 150, "log_every": 0, "use_graphs": False,
+                                            "network": net, "ckpt_dir": str(tmp_path), "ckpt_freq": 6}})
+    out = train_frames(cfg, "cpu", 8)
+    L = out["learner"]
+    assert L.kind == "graph" and L.num_q_updates == 8
+    assert np.isfinite(L.last_metrics()["loss"]) and L.last_metrics()["grad_norm"] > 0
+    # params are views of the flat buffer; the optimizer moved them
+    assert L.Q.state_dict()[next(iter(L.Q.state_dict()))].data_ptr() >= L.p32.data_ptr()
+    out2 = train_frames(cfg, "cpu", 10)          # resumes the step-6 checkpoint
+    assert out2["learner"].num_q_updates == 10
