@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
+                    help="nature64 = the headline fused-HIP learner; others use the graph learner")
     args = ap.parse_args()
 
     from apex_dqn_amd.config import ApexConfig
@@ -63,7 +65,7 @@ def main():
                     "min_replay_mem_size": 0},
         "Replay_Memory": {"soft_capacity": args.replay},
         "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
-                    "seed": 1234 + rank},
+                    "seed": 1234 + rank, "network": args.network},
     })
     cap = args.replay
     frames_cap = cap + 4096
@@ -84,7 +86,11 @@ def main():
                            R=rng.normal(size=K).astype(np.float32), Gamma=np.full(K, 0.99 ** 3, np.float32),
                            priority=rng.random(K).astype(np.float32) + 0.01))
     replay.rebuild()
-    learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
+    if args.network == "nature64":
+        learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
+    else:
+        from apex_dqn_amd.learner.graph_learner import GraphLearner
+        learner = GraphLearner(cfg, device, replay, comm=comm)
     L = cfg.Learner
 
     def one_step():
@@ -117,10 +123,12 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": round(value / BASELINE_STEPS_PER_S, 2), "dtype": "bf16", "data": "synthetic",
-            "config": {"model": "dueling NatureCNN (reference DuellingDQN, conv1=64), 4x84x84, A=%d" % args.actions,
+            "config": {"model": ("dueling NatureCNN (reference DuellingDQN, conv1=64), 4x84x84, A=%d" % args.actions
+                                  if args.network == "nature64" else
+                                  "dueling %s, 4x84x84, A=%d" % (args.network, args.actions)),
                        "global_batch": args.batch * world, "seq_len": 1,
                        "parallelism": "dp%d" % world, "per_gpu_batch": args.batch,
-                       "replay_per_gpu": cap, "backend": learner.ops.name,
+                       "replay_per_gpu": cap, "backend": getattr(learner, "kind", "fused") + "/" + learner.ops.name,
                        "hip_graphs": bool(learner.rt.use_graphs)},
             "loss": round(m["loss"], 5), "grad_norm": round(m["grad_norm"], 5),
         }
