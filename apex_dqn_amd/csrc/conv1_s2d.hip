@@ -14,10 +14,7 @@
 // (uint8, double-buffered, DMA of tile i+1 in flight under the MFMAs of tile i);
 // uint8 -> bf16 conversion happens at fragment-read time (values 0..255 are
 // exact in bf16; the 1/255 input scale is applied in the epilogue).
-#include "apex_common.h"
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+#include "mfma_common.h"
 
 #define S2D_FRAME 7056
 
@@ -34,63 +31,6 @@ struct Conv1S2DDesc {
   int N, C, m_switch;
   float in_scale;
 };
-
-// 8 uint8 (two dwords) -> 8 bf16: v_cvt_f32_ubyte{0..3} then one v_perm per pair
-// picks the high halves of two exact f32 integers (their low halves are zero).
-__device__ __forceinline__ uint32_t bf16pair_from_f32(float lo, float hi) {
-  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
-}
-
-// (float)(byte k of v): hipcc lowers this pattern to one v_cvt_f32_ubyte{k}
-__device__ __forceinline__ float ubyte(uint32_t v, int k) { return (float)((v >> (8 * k)) & 0xffu); }
-
-
-// ReLU on two packed bf16 (sign bits spread over their halves, then cleared)
-__device__ __forceinline__ uint32_t relu2(uint32_t v) {
-  const uint32_t neg = ((v & 0x80008000u) >> 15) * 0xffffu;
-  return v & ~neg;
-}
-
-
-// 16-byte LDS-DMA issued from inline asm: hipcc does not track it, so it emits no
-// conservative vmcnt(0) before later ds_reads; completion is counted by hand with
-// explicit s_waitcnt vmcnt(N) + s_barrier (M0 is written inside the statement).
-__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_off) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_off)
-               : "memory");
-}
-
-// Scalar (SMEM) load of the C frame slots of one image: counted by lgkmcnt, so it
-// never forces a vmcnt drain of the LDS-DMA in flight.  `p` must be wave-uniform.
-template <int C>
-__device__ __forceinline__ void sload_slots(const int32_t* p, int (&out)[4]) {
-  const uint64_t a = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int32_t* q = (const int32_t*)(((uint64_t)hi << 32) | lo);
-  if constexpr (C == 4) {
-    int __attribute__((ext_vector_type(4))) v;
-    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(q) : "memory");
-    out[0] = v[0]; out[1] = v[1]; out[2] = v[2]; out[3] = v[3];
-  } else if constexpr (C == 2) {
-    int __attribute__((ext_vector_type(2))) v;
-    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(q) : "memory");
-    out[0] = v[0]; out[1] = v[1]; out[2] = 0; out[3] = 0;
-  } else {
-    int v;
-    asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(q) : "memory");
-    out[0] = v; out[1] = 0; out[2] = 0; out[3] = 0;
-  }
-}
-
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
-}
 
 // ---------------------------------------------------------------------------
 // Image-resident forward.  A persistent workgroup (8 waves, one per CU)

@@ -19,12 +19,7 @@
 // swizzled so both the row reads (ds_read_b128) and the transposed reads are
 // bank-conflict free.  Global->LDS staging is register double-buffered: the
 // next tile's loads are issued before the current tile's MFMAs.
-#include "apex_common.h"
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+#include "mfma_common.h"
 
 struct ConvDesc {
   const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]; mode 2: u8 frame ring
@@ -67,67 +62,6 @@ struct WgradDesc {
   int rows_per_split, Mred;
 };
 
-// 128-byte LDS rows, 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7):
-// a 16-lane ds_read_b128 group (16 rows, one chunk) hits 16 distinct 16-B slots.
-__device__ __forceinline__ int swz_row(int r, int c) { return (r << 7) + ((c ^ ((r >> 1) & 7)) << 4); }
-// transposed-read image: chunk16 c of row r at c ^ (s(r) << 1), s(r) = bit1(r) | bit3(r)<<1;
-// both ds_read_b64_tr_b16 halves (rows 8g+q, 8(g+1)+q) then cover 64 distinct banks.
-__device__ __forceinline__ int swz_tr(int r, int c) {
-  const int s = ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
-  return (r << 7) + ((c ^ (s << 1)) << 4);
-}
-
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-// two floats -> packed bf16x2 (one v_cvt_pk_bf16_f32, round-to-nearest-even)
-__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
-}
-
-__device__ __forceinline__ uint32_t u8pair_bf16(uint32_t v, int sh) {
-  // two consecutive bytes of v (starting at byte sh) -> two bf16 (exact: integers <= 255):
-  // v_cvt_f32_ubyteN x2 + v_cvt_pk_bf16_f32
-  return cvt_pk_bf16((float)((v >> (8 * sh)) & 0xffu), (float)((v >> (8 * sh + 8)) & 0xffu));
-}
-
-__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint32_t lo, uint32_t hi) {
-  return make_uint4(u8pair_bf16(lo, 0), u8pair_bf16(lo, 2), u8pair_bf16(hi, 0), u8pair_bf16(hi, 2));
-}
-
-// ReLU on two packed bf16: zero the halves whose sign bit is set.
-// (v & 0x80008000) >> 15 marks negative halves with a 1 in their low bit; x 0xffff
-// spreads it over the half (v_mul_u32_u24, no carry between halves); v_bfi clears.
-__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t v) {
-  const uint32_t neg = ((v & 0x80008000u) >> 15) * 0xffffu;
-  return v & ~neg;
-}
-
-// dgrad ReLU mask: keep v's half where the producer activation m's half is > 0
-// (exact for any bf16 m): |m| + 0x7fff sets bit 15 of a half exactly when its
-// magnitude is non-zero (max 0xfffe: no carry into the next half); AND with the
-// inverted sign bits drops negative halves (and -0).  (A NaN half of m keeps v;
-// torch's m > 0 would drop it -- only reachable after the activations diverged.)
-__device__ __forceinline__ uint32_t mask_bf16x2(uint32_t v, uint32_t m) {
-  const uint32_t pos = ((m & 0x7fff7fffu) + 0x7fff7fffu) & ~m & 0x80008000u;
-  return v & ((pos >> 15) * 0xffffu);
-}
-
-// MFMA fragment of 8 consecutive K rows (32kk + 8(lane>>4) .. +7) of column col0 + (lane&15)
-// from a K-major 64x64 bf16 image stored with swz_tr (two ds_read_b64_tr_b16).
-__device__ __forceinline__ bf16x8 tr_frag8(const uint8_t* img, int kk, int col0, int lane) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, pcol = lane & 3;
-  const int rA = 32 * kk + 8 * g + q;
-  const int cbyte = (col0 + 4 * pcol) * 2;  // byte offset of 4 columns inside the 128-B row
-  const int c16 = cbyte >> 4, within = cbyte & 15;
-  const lds_s16x4* pa = (const lds_s16x4*)(img + swz_tr(rA, c16) + within);
-  const lds_s16x4* pb = (const lds_s16x4*)(img + swz_tr(rA + 4, c16) + within);
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pa));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pb));
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 v = (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
 // =====================================================================================
 // forward / dgrad implicit GEMM
 // =====================================================================================
@@ -142,23 +76,6 @@ struct FwdRegs {
 // Epilogue image: 32 rows x 128 B per wave; 16-B chunk c of row r at c ^ ((r>>1)&7)
 __device__ __forceinline__ int epi_off(int r, int byte) {
   return (r << 7) + ((((byte >> 4) ^ ((r >> 1) & 7))) << 4) + (byte & 15);
-}
-
-// Raw buffer resource over a tensor (< 2 GB): loads with a 32-bit per-lane byte
-// offset (loop-invariant VGPR) + a scalar k-tile offset (SGPR), and an offset of
-// BUF_OOB reads zeros (hardware range check) -- no per-element selects or branches.
-#define BUF_OOB 0x80000000u
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7ffffff0, 0x00020000);
-}
-__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-
-// a / D with D a compile-time constant when DC != 0 (multiply-shift), else runtime
-template <int DC>
-__device__ __forceinline__ uint32_t udiv(uint32_t a, uint32_t d) {
-  return DC ? a / (uint32_t)DC : a / d;
 }
 
 // MODE: A-operand source (0 dense rows, 1 NHWC implicit im2col).
@@ -813,6 +730,14 @@ APEX_EXPORT int apex_conv_wgrad(WgradDesc d, float* out, float* bout, int nsplit
     slab_reduce_kernel<<<(int)blocks, 256, 0, st>>>(d.slab, nsplit, n, scale, out, d.bias_slab, nb, bout,
                                                     d.mode == 2 ? d.Cin : 0, d.Kc);
   }
+  APEX_CHECK_LAUNCH();
+}
+
+// standalone split-K finalisation (used by csrc/conv1_wgrad.hip's per-block partials)
+APEX_EXPORT int apex_slab_reduce(const float* slab, int nsplit, int64_t n, float scale, float* out, const float* bslab,
+                                 int nb, float* bout, int s2dC, int Kc, hipStream_t st) {
+  const int64_t blocks = (n / 4 + 15) / 16 + (bslab ? (nb / 4 + 15) / 16 : 0);
+  slab_reduce_kernel<<<(int)blocks, 256, 0, st>>>(slab, nsplit, n, scale, out, bslab, bslab ? nb : 0, bout, s2dC, Kc);
   APEX_CHECK_LAUNCH();
 }
 

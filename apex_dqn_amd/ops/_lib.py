@@ -64,6 +64,12 @@ class WgradDesc(ctypes.Structure):
                 ("rows_per_split", c_i), ("Mred", c_i)]
 
 
+class Conv1WgDesc(ctypes.Structure):
+    """Image-resident conv1 weight gradient (mirrors ``Conv1WgDesc`` in csrc/conv1_wgrad.hip)."""
+    _fields_ = [("ring", c_p), ("slots", c_p), ("dy", c_p), ("slab", c_p), ("bias_slab", c_p), ("zero16", c_p),
+                ("N", c_i), ("C", c_i)]
+
+
 class Conv1S2DDesc(ctypes.Structure):
     """conv1 on the space-to-depth ring (mirrors ``Conv1S2DDesc`` in csrc/conv1_s2d.hip)."""
     _fields_ = [("ring", c_p), ("slots", c_p), ("w", c_p), ("w2", c_p), ("bias", c_p), ("bias2", c_p),
@@ -89,6 +95,8 @@ _SIGS = {
     "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_p], c_i),
     "apex_actor_head": ([c_p, HeadParams, c_i, c_i, c_p, c_u64, c_p, c_p, c_p, c_p], c_i),
     "apex_conv1_s2d_fwd": ([Conv1S2DDesc, c_i, c_p], c_i),
+    "apex_conv1_wgrad_img": ([Conv1WgDesc, c_i, c_p], c_i),
+    "apex_slab_reduce": ([c_p, c_i, c_i64, c_f, c_p, c_p, c_i, c_p, c_i, c_i, c_p], c_i),
     "apex_s2d_pack_w1": ([c_p, c_p, c_i, c_p], c_i),
     "apex_s2d_unpack_w1_grad": ([c_p, c_p, c_i, c_p], c_i),
     "apex_s2d_frames": ([c_p, c_p, c_i64, c_i64, c_i64, c_p], c_i),

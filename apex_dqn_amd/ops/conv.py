@@ -221,7 +221,34 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
 
 
 def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
-                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1024) -> None:
+                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, grid: int = 0) -> None:
+    """dW1 (OIHW fp32, x ``scale``) and db1 from dY1 (N, 20, 20, 64) and the uint8 frame
+    stacks addressed by ring slots: image-resident kernel (csrc/conv1_wgrad.hip), one
+    fp32 partial per workgroup, then the split-K reduce (s2d -> OIHW permuted store)."""
+    N, OH, OW, Co = dy.shape
+    C = slots.shape[1]
+    assert (OH, OW, Co) == (20, 20, 64) and slots.dtype == torch.int32 and dy.is_contiguous()
+    G = grid if grid > 0 else min(N, 256)
+    K = 64 * C
+    slab = ws.get(("wg1img", C, G), G * 64 * K, dy.device)
+    bslab = ws.get(("wg1imgb", G), G * 64, dy.device)
+    zero = ws.get(("zero16",), 64, ring.device, torch.uint8)
+    if not getattr(ws, "_zeroed", False):
+        zero.zero_()
+        ws._zeroed = True
+    d = _lib.Conv1WgDesc()
+    d.ring, d.slots, d.dy = ring.data_ptr(), slots.data_ptr(), dy.data_ptr()
+    d.slab, d.bias_slab, d.zero16 = slab.data_ptr(), bslab.data_ptr(), zero.data_ptr()
+    d.N, d.C = N, C
+    st = _lib.stream_ptr()
+    _lib.check(lib.apex_conv1_wgrad_img(d, G, st), "conv1_wgrad_img")
+    _lib.check(lib.apex_slab_reduce(slab.data_ptr(), G, 64 * K, float(scale), dw_out.data_ptr(), bslab.data_ptr(),
+                                    64, db_out.data_ptr(), C, K, st), "slab_reduce")
+
+
+def conv1_wgrad_ring_tiled(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
+                           scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1024) -> None:
+    """The generic tiled wgrad kernel in its s2d-ring mode (kept as a cross-check)."""
     N, OH, OW, Co = dy.shape
     C = slots.shape[1]
     Kc = C * 64

@@ -76,10 +76,13 @@ def main():
                                                               gb[:64], target_rows=tr), F(B * 49 * 64 * 576))
         ops[f"conv2_wgrad@{tr}"] = (lambda tr=tr: C.conv_wgrad(lib, ws, dY2, y1[:B], 4, 2, gw[:64 * 1024].view(64, 4, 4, 64),
                                                               gb[:64], target_rows=tr), F(B * 81 * 64 * 1024))
-    for tr in (256, 512, 1024):
-        ops[f"conv1_wgrad@{tr}"] = (lambda tr=tr: C.conv1_wgrad_ring(lib, ws, dY1, ring, slots[:B], 1 / 255.,
-                                                                    gw[:64 * 256].view(64, 4, 8, 8), gb[:64],
-                                                                    target_rows=tr), F(B * 400 * 64 * 256))
+    ops["conv1_wgrad@tiled"] = (lambda: C.conv1_wgrad_ring_tiled(lib, ws, dY1, ring, slots[:B], 1 / 255.,
+                                                                 gw[:64 * 256].view(64, 4, 8, 8), gb[:64]),
+                                F(B * 400 * 64 * 256))
+    for gr in (128, 512):
+        ops[f"conv1_wgrad@g{gr}"] = (lambda gr=gr: C.conv1_wgrad_ring(lib, ws, dY1, ring, slots[:B], 1 / 255.,
+                                                                     gw[:64 * 256].view(64, 4, 8, 8), gb[:64],
+                                                                     grid=gr), F(B * 400 * 64 * 256))
     # launch-shape sweep of the forward-family GEMMs (tile 1: BM=128, 2: BM=64; order 1: M fastest, 2: N fastest)
     for tile in (1, 2):
         for order in (1, 2):

@@ -147,8 +147,10 @@ def test_conv_wgrad_layers(N):
         assert _rel(db, rdb) < 1e-4
 
 
-@pytest.mark.parametrize("N", [3, 32])
-def test_conv1_wgrad_from_ring(N):
+@pytest.mark.parametrize("N,grid", [(3, 0), (32, 0), (32, 5), (9, 16)])
+def test_conv1_wgrad_from_ring(N, grid):
+    """Image-resident conv1 wgrad (several images per workgroup, idle workgroups)
+    and the tiled ring-mode wgrad, both against the fp32 autograd oracle."""
     from apex_dqn_amd.ops import conv as C
     g = torch.Generator(device="cpu").manual_seed(N + 5)
     from apex_dqn_amd.replay.gpu_replay import to_s2d
@@ -158,10 +160,13 @@ def test_conv1_wgrad_from_ring(N):
     dy = _bf(torch.randn(N, 20, 20, 64, generator=g))
     dw = torch.empty(64, 4, 8, 8, device=DEV)
     db = torch.empty(64, device=DEV)
-    C.conv1_wgrad_ring(_lib(), C.Workspace(), dy, ring, slots, 1 / 255.0, dw, db, target_rows=800)
+    C.conv1_wgrad_ring(_lib(), C.Workspace(), dy, ring, slots, 1 / 255.0, dw, db, grid=grid)
     rdw, rdb = R.conv1_wgrad(dy.float(), raw[slots.long()], 1 / 255.0)
     assert _rel(dw, rdw) < 5e-3
     assert _rel(db, rdb) < 1e-4
+    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
+    C.conv1_wgrad_ring_tiled(_lib(), C.Workspace(), dy, ring, slots, 1 / 255.0, dw2, db2, target_rows=800)
+    assert _rel(dw2, rdw) < 5e-3 and _rel(db2, rdb) < 1e-4
 
 
 @pytest.mark.parametrize("M", [64, 512])
@@ -231,6 +236,6 @@ def test_conv1_s2d_frame_stacks_and_ring_layout(C):
     dy = _bf(torch.randn(N, 20, 20, 64, generator=g))
     dw = torch.empty(64, C, 8, 8, device=DEV)
     db = torch.empty(64, device=DEV)
-    Cv.conv1_wgrad_ring(_lib(), Cv.Workspace(), dy, rp.frames, slots, 1 / 255.0, dw, db, target_rows=400)
+    Cv.conv1_wgrad_ring(_lib(), Cv.Workspace(), dy, rp.frames, slots, 1 / 255.0, dw, db)
     rdw, _ = R.conv1_wgrad(dy.float(), raw[slots.long().cpu()].to(DEV), 1 / 255.0)
     assert _rel(dw, rdw) < 5e-3
