@@ -120,6 +120,19 @@ APEX_EXPORT int apex_rmsprop_step(float* p, const float* g, float* v, float* m, 
   APEX_CHECK_LAUNCH();
 }
 
+// the same step with the clip norm taken from ``npart`` producer-written partials
+// (fc wgrad epilogue + grad_finalize blocks): no separate squared-norm pass
+APEX_EXPORT int apex_rmsprop_step_np(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
+                                     const double* partials, int npart, float lr, float alpha, float eps, float clip,
+                                     int centered, float* norm_out, hipStream_t st) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
+  if ((uintptr_t)pb & 7) return (int)hipErrorInvalidValue;
+  int nb = (int)((n / 4 + 255) / 256);
+  nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  rmsprop_kernel<<<nb, 256, 0, st>>>(p, g, v, m, pb, n, partials, npart, lr, alpha, eps, clip, centered, norm_out);
+  APEX_CHECK_LAUNCH();
+}
+
 APEX_EXPORT int apex_cast_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t st) {
   int nb = (int)((n + 255) / 256);
   nb = nb > 2048 ? 2048 : (nb < 1 ? 1 : nb);

@@ -94,6 +94,9 @@ class FusedNatureLearner:
             raise ValueError("Runtime.allreduce_dtype must be fp32 or bf16")
         self._comm_bf16 = self.world > 1 and self.rt.allreduce_dtype == "bf16"
         self.gcomm = torch.zeros(n, dtype=torch.bfloat16, device=d) if self._comm_bf16 else self.g32
+        # producer-summed clip norm: single rank only (with DP the norm is of the
+        # all-reduced gradient, so the separate squared-norm pass stays)
+        self._fuse_norm = self.world == 1 and self.ops.name == "hip" and getattr(self.ops, "native_conv", False)
         # cross-shard IS-weight normaliser: min over ranks of (min_i p_i / total)
         self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
         self.ratio_buf = torch.zeros(1, dtype=torch.float32, device=d)
@@ -131,6 +134,11 @@ class FusedNatureLearner:
         self.td_abs = torch.zeros(B, dtype=torch.float32, device=d)
         self.loss_b = torch.zeros(B, dtype=torch.float32, device=d)
         self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
+        # single rank, HIP: the clip norm is summed by the gradient producers (fc wgrad
+        # epilogue + grad_finalize blocks) instead of a separate pass over g32
+        self.norm_part = torch.zeros(8192, dtype=torch.float64, device=d)
+        self.norm_total = torch.zeros(1, dtype=torch.float64, device=d)
+        self._fc_slots = 0
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
         # head-gradient region (zeroed by the head kernel, accumulated by head_wgrad)
         o0 = self.layout.offsets["wv"]
@@ -181,7 +189,8 @@ class FusedNatureLearner:
             ops.head_wgrad(self.h, self.dhead, self.G)
             self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
         with self._on_side(self.rt.overlap_wgrad):
-            ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"])
+            self._fc_slots = ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"],
+                                          norm=(self.norm_part, 0) if self._fuse_norm else None) or 0
         if self.world > 1:
             self._join_side()   # the fc/heads bucket all-reduce starts right after this segment
             if self._comm_bf16:
@@ -194,16 +203,19 @@ class FusedNatureLearner:
         all-reduce): the dgrad chain, conv3/conv2 wgrad (side stream when
         ``overlap_wgrad``), conv1 wgrad last."""
         B, rt, ops, G, Pb = self.B, self.rt, self.ops, self.G, self.Pb
+        jobs = []    # split-K reductions, finalised in ONE launch at the end
         ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3)
         with self._on_side(rt.overlap_wgrad):
-            ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"])
+            ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"], jobs=jobs)
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2)
         with self._on_side(rt.overlap_wgrad):
-            ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"])
+            ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"], jobs=jobs)
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1)
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
-                             G["b1"])
-        self._join_side()
+                             G["b1"], jobs=jobs)
+        self._join_side()      # head wgrad (side stream) done: its region enters the norm
+        norm = dict(part=self.norm_part, slot0=self._fc_slots, total=self.norm_total) if self._fuse_norm else None
+        ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
         if self._comm_bf16:
             cut = self.layout.offsets["wfc"]
             self.gcomm[:cut].copy_(self.g32[:cut])
@@ -264,7 +276,8 @@ class FusedNatureLearner:
         if self._comm_bf16:
             self.g32.copy_(self.gcomm)
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
-                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
+                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
+                      norm_total=self.norm_total if self._fuse_norm else None)
         self._mark("optimizer")
         if self.world > 1:
             # local min_i p_i / total for the global IS-weight normaliser (all-reduced MIN after the step)

@@ -61,7 +61,19 @@ class WgradDesc(ctypes.Structure):
                 ("OH", c_i), ("OW", c_i), ("KH", c_i), ("KW", c_i),
                 ("stride", c_i), ("pad_h", c_i), ("pad_w", c_i), ("mode", c_i),
                 ("Co", c_i), ("Kc", c_i), ("ldd", c_i), ("ldx", c_i),
-                ("rows_per_split", c_i), ("Mred", c_i)]
+                ("rows_per_split", c_i), ("Mred", c_i), ("norm_part", c_p), ("norm_slot0", c_i), ("pad0", c_i)]
+
+
+class RedJob(ctypes.Structure):
+    """One split-K finalisation job (mirrors ``RedJob`` in csrc/conv_mfma.hip)."""
+    _fields_ = [("slab", c_p), ("bslab", c_p), ("out", c_p), ("bout", c_p), ("n", c_i64),
+                ("nsplit", c_i), ("nb", c_i), ("s2dC", c_i), ("Kc", c_i), ("scale", c_f), ("blk0", c_i)]
+
+
+class FinalizeDesc(ctypes.Structure):
+    """All split-K reductions of a step + squared-norm partials (``FinalizeDesc``)."""
+    _fields_ = [("job", RedJob * 4), ("njobs", c_i), ("nrm_n", c_i), ("nrm_ptr", c_p), ("norm_part", c_p),
+                ("norm_slot0", c_i), ("nblocks", c_i)]
 
 
 class Conv1WgDesc(ctypes.Structure):
@@ -90,6 +102,9 @@ _SIGS = {
     "apex_grad_sqnorm_partials": ([c_p, c_i64, c_p, c_p], c_i),
     "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p], c_i),
     "apex_cast_bf16": ([c_p, c_p, c_i64, c_p], c_i),
+    "apex_rmsprop_step_np": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p, c_p], c_i),
+    "apex_grad_finalize": ([FinalizeDesc, c_p], c_i),
+    "apex_norm_total": ([c_p, c_i, c_p, c_p], c_i),
     "apex_ddqn_head": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
                         c_p, c_p, c_p, c_p, c_p, c_i, c_p], c_i),
     "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_p], c_i),

@@ -185,6 +185,7 @@ def _wg_desc(**kw) -> "_lib.WgradDesc":
     d.stride, d.pad_h, d.pad_w, d.mode = kw.get("stride", 1), 0, 0, kw["mode"]
     d.Co, d.Kc, d.ldd, d.ldx = kw["Co"], kw["Kc"], kw["ldd"], kw.get("ldx", 0)
     d.rows_per_split, d.Mred = kw["rows_per_split"], kw["Mred"]
+    d.norm_part, d.norm_slot0 = kw.get("norm_part"), kw.get("norm_slot0", 0)
     return d
 
 
@@ -200,8 +201,9 @@ def _splits(Mred: int, target_rows: int, max_rows: int) -> Tuple[int, int]:
 
 
 def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, stride: int,
-               dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 0) -> None:
-    """dW (OHWI, fp32) and db for an NHWC conv with 64 output channels.
+               dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 0, jobs: Optional[list] = None) -> None:
+    """dW (OHWI, fp32) and db for an NHWC conv with 64 output channels.  With
+    ``jobs``, the split-K reduction is appended there for ``finalize_grads``.
     ``target_rows``: reduction rows per split-K block (0 = tuned default: fewer
     rows for the small 3x3 layer, whose 9 output tiles need more splits)."""
     N, OH, OW, Co = dy.shape
@@ -212,16 +214,22 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     Mred = N * OH * OW
     nsplit, rows = _splits(Mred, target_rows, _WG_TBL)
     slab = ws.get(("wg", Co, Kc), nsplit * Co * Kc, dy.device)
-    bslab = ws.get(("wgb", Co), nsplit * Co, dy.device)
+    bslab = ws.get(("wgb", Co, Kc), nsplit * Co, dy.device)
     d = _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=slab.data_ptr(), bias_slab=bslab.data_ptr(), N=N,
                  H=H, W=W, Cin=Cin, OH=OH, OW=OW, KH=KH, KW=KH, stride=stride, mode=1, Co=Co, Kc=Kc, ldd=Co,
                  rows_per_split=rows, Mred=Mred)
+    if jobs is not None:   # reduction deferred to one grad_finalize launch
+        _lib.check(lib.apex_conv_wgrad(d, None, None, nsplit, 1.0, _lib.stream_ptr()), "conv_wgrad")
+        jobs.append(dict(slab=slab, bslab=bslab, out=dw_out, bout=db_out, n=Co * Kc, nsplit=nsplit, nb=Co,
+                         s2dC=0, Kc=Kc, scale=1.0))
+        return
     _lib.check(lib.apex_conv_wgrad(d, dw_out.data_ptr(), db_out.data_ptr(), nsplit, 1.0, _lib.stream_ptr()),
                "conv_wgrad")
 
 
 def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
-                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, grid: int = 0) -> None:
+                     scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, grid: int = 0,
+                     jobs: Optional[list] = None) -> None:
     """dW1 (OIHW fp32, x ``scale``) and db1 from dY1 (N, 20, 20, 64) and the uint8 frame
     stacks addressed by ring slots: image-resident kernel (csrc/conv1_wgrad.hip), one
     fp32 partial per workgroup, then the split-K reduce (s2d -> OIHW permuted store)."""
@@ -242,6 +250,10 @@ def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, s
     d.N, d.C = N, C
     st = _lib.stream_ptr()
     _lib.check(lib.apex_conv1_wgrad_img(d, G, st), "conv1_wgrad_img")
+    if jobs is not None:
+        jobs.append(dict(slab=slab, bslab=bslab, out=dw_out, bout=db_out, n=64 * K, nsplit=G, nb=64, s2dC=C, Kc=K,
+                         scale=float(scale)))
+        return
     _lib.check(lib.apex_slab_reduce(slab.data_ptr(), G, 64 * K, float(scale), dw_out.data_ptr(), bslab.data_ptr(),
                                     64, db_out.data_ptr(), C, K, st), "slab_reduce")
 
@@ -264,13 +276,66 @@ def conv1_wgrad_ring_tiled(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Ten
                                    _lib.stream_ptr()), "conv1_wgrad")
 
 
-def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor) -> None:
-    """dW[N,K] = dy[M,N]^T @ x[M,K] (fp32, written directly), db = sum_m dy."""
+def wgrad_blocks(Co: int, Kc: int) -> int:
+    """Workgroups of one split of igemm_wgrad (mirrors launch_wgrad's tile-shape choice)."""
+    kt, ct = Kc // 64, Co // 64
+    best, bc = (1, 1), None
+    for c, n in ((1, 4), (2, 2), (4, 1), (1, 3), (1, 1)):
+        if kt % n or ct % c:
+            continue
+        cost = (ct // c) * Kc + (kt // n) * Co
+        if bc is None or cost < bc:
+            best, bc = (c, n), cost
+    return (kt // best[1]) * (ct // best[0])
+
+
+def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor,
+                norm: Optional[Tuple[torch.Tensor, int]] = None) -> int:
+    """dW[N,K] = dy[M,N]^T @ x[M,K] (fp32, written directly), db = sum_m dy.  With
+    ``norm = (partials, slot0)`` the kernel also writes 4 squared-norm partials per
+    workgroup; returns the number of slots used."""
     M, Nc = dy.shape
     K = x.shape[1]
+    extra = {} if norm is None else dict(norm_part=norm[0].data_ptr(), norm_slot0=int(norm[1]))
     d = _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=dw_out.data_ptr(), bias_slab=db_out.data_ptr(),
-                 mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M)
+                 mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M, **extra)
     _lib.check(lib.apex_conv_wgrad(d, None, None, 1, 1.0, _lib.stream_ptr()), "dense_wgrad")
+    return 4 * wgrad_blocks(Nc, K)
+
+
+def finalize_blocks(jobs: list, norm_range: Optional[torch.Tensor]) -> int:
+    n = sum((j["n"] // 4 + 15) // 16 + (j["nb"] // 4 + 15) // 16 for j in jobs)
+    return n + (1 if norm_range is not None else 0)
+
+
+def finalize_grads(lib, jobs: list, norm_range: Optional[torch.Tensor] = None, norm_part=None, slot0: int = 0,
+                   total=None) -> int:
+    """One launch for every deferred split-K reduction; with ``norm_part`` also the
+    squared-norm partials of everything it writes (+ ``norm_range``) into slots from
+    ``slot0``, then the grand total of ``norm_part[:slot0 + blocks]`` into ``total``
+    (one small kernel).  Returns the blocks used."""
+    d = _lib.FinalizeDesc()
+    assert len(jobs) <= 4
+    blk = 0
+    for i, j in enumerate(jobs):
+        J = d.job[i]
+        J.slab, J.bslab, J.out, J.bout = j["slab"].data_ptr(), j["bslab"].data_ptr(), j["out"].data_ptr(), \
+            j["bout"].data_ptr()
+        J.n, J.nsplit, J.nb, J.s2dC, J.Kc, J.scale, J.blk0 = j["n"], j["nsplit"], j["nb"], j["s2dC"], j["Kc"], \
+            j["scale"], blk
+        blk += (j["n"] // 4 + 15) // 16 + (j["nb"] // 4 + 15) // 16
+    d.njobs = len(jobs)
+    if norm_range is not None and norm_part is not None:
+        d.nrm_ptr, d.nrm_n = norm_range.data_ptr(), norm_range.numel()
+        blk += 1
+    d.nblocks = blk
+    if norm_part is not None:
+        d.norm_part, d.norm_slot0 = norm_part.data_ptr(), int(slot0)
+    _lib.check(lib.apex_grad_finalize(d, _lib.stream_ptr()), "grad_finalize")
+    if norm_part is not None and total is not None:
+        _lib.check(lib.apex_norm_total(norm_part.data_ptr(), int(slot0) + blk, total.data_ptr(), _lib.stream_ptr()),
+                   "norm_total")
+    return blk
 
 
 def pack_dgrad_weights(lib, wfc, w3, w2, wfcT, w3tf, w2t) -> None:

@@ -136,15 +136,19 @@ class TorchBackend:
         dx, _, _ = R.fc_bwd(dh, xf, w, xf, self.dtype)
         dx_out.copy_(dx.reshape(dx_out.shape))
 
-    def fc_wgrad(self, dh, x, dw_out, db_out):
+    def fc_wgrad(self, dh, x, dw_out, db_out, norm=None):
         xf = x.reshape(x.shape[0], -1)
         dw_out.copy_(dh.t().float() @ xf.float())
         db_out.copy_(dh.float().sum(0))
+        return 0
+
+    def finalize_grads(self, jobs, norm_range=None, norm=None) -> None:
+        """Deferred split-K reductions (the torch path computes gradients directly)."""
 
     def conv_dgrad(self, dy, w, stride, x_src, dx_out):
         dx_out.copy_(R.conv_dgrad(dy, w, tuple(x_src.shape), stride, x_src, self.dtype))
 
-    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out):
+    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None):
         dw, db = R.conv_wgrad(dy, x, k, stride)
         dw_out.copy_(dw)
         db_out.copy_(db)
@@ -154,11 +158,11 @@ class TorchBackend:
         dw_out.copy_(dw)
         db_out.copy_(db)
 
-    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out):
+    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out, jobs=None):
         self.conv1_wgrad(dy, frames_buf[:slots.shape[0]], scale, dw_out, db_out)
 
     # ----------------------------------------------------------- optimizer
-    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out):
+    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None):
         norm = g32.double().pow(2).sum().sqrt().float()
         coef = torch.clamp(clip / (norm + 1e-6), max=1.0) if clip > 0 else torch.ones_like(norm)
         g = g32 * coef
@@ -218,10 +222,18 @@ class HipBackend(TorchBackend):
         xf = x.reshape(x.shape[0], -1)
         C.dense_dgrad(self.lib, dh, w, dx_out.reshape(dh.shape[0], -1), xf)
 
-    def fc_wgrad(self, dh, x, dw_out, db_out):
+    def fc_wgrad(self, dh, x, dw_out, db_out, norm=None):
         if not self.native_conv:
             return super().fc_wgrad(dh, x, dw_out, db_out)
-        C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out)
+        return C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm=norm)
+
+    def finalize_grads(self, jobs, norm_range=None, norm=None) -> None:
+        if not jobs and norm is None:
+            return
+        if norm is None:
+            C.finalize_grads(self.lib, jobs)
+        else:
+            C.finalize_grads(self.lib, jobs, norm_range, norm["part"], norm["slot0"], norm["total"])
 
     def conv_dgrad(self, dy, w, stride, x_src, dx_out):
         if not self.native_conv:
@@ -231,15 +243,15 @@ class HipBackend(TorchBackend):
         else:
             C.conv2_dgrad(self.lib, dy, w, x_src, dx_out)
 
-    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out):
+    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None):
         if not self.native_conv:
             return super().conv_wgrad(dy, x, k, stride, dw_out, db_out)
-        C.conv_wgrad(self.lib, self.ws, dy, x, k, stride, dw_out, db_out)
+        C.conv_wgrad(self.lib, self.ws, dy, x, k, stride, dw_out, db_out, jobs=jobs)
 
-    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out):
+    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out, jobs=None):
         if not self.native_conv:
             return super().conv1_wgrad_ring(dy, ring, slots, frames_buf, scale, dw_out, db_out)
-        C.conv1_wgrad_ring(self.lib, self.ws, dy, ring, slots, scale, dw_out, db_out)
+        C.conv1_wgrad_ring(self.lib, self.ws, dy, ring, slots, scale, dw_out, db_out, jobs=jobs)
 
     @staticmethod
     def _hp(P):
@@ -270,9 +282,15 @@ class HipBackend(TorchBackend):
                                             ctr.data_ptr(), q_out.data_ptr(), a_out.data_ptr(),
                                             _lib.stream_ptr()), "actor_head")
 
-    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out):
+    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None):
         n = p32.numel()
         st = _lib.stream_ptr()
+        if norm_total is not None:   # squared norm already summed by the gradient producers
+            _lib.check(self.lib.apex_rmsprop_step_np(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
+                                                     pbf.data_ptr(), n, norm_total.data_ptr(), 1, float(lr),
+                                                     float(alpha), float(eps), float(clip), int(centered),
+                                                     norm_out.data_ptr(), st), "rmsprop_np")
+            return
         _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), n, partials.data_ptr(), st), "sqnorm")
         _lib.check(self.lib.apex_rmsprop_step(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
                                               pbf.data_ptr(), n, partials.data_ptr(), float(lr), float(alpha),

@@ -140,3 +140,29 @@ def test_graph_learner_impala_with_hip_graph():
     assert L.kind == "graph" and L.num_q_updates == 30 and L._graphs is not None
     m = L.last_metrics()
     assert np.isfinite(m["loss"]) and m["grad_norm"] > 0
+
+
+def test_fused_norm_equals_gradient_norm():
+    """Single-rank fused learner: the clip norm summed by the gradient producers
+    (fc wgrad epilogue partials + grad_finalize blocks + norm_total) must equal the
+    norm of the final flat gradient, step after step (graph replays)."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 256},
+                                "Runtime": {"use_graphs": True, "grad_clip": 1e-3}})
+    rp = GpuReplayShard(3000, 3000, 3600, 4, device=DEV, seed=5)
+    rng = np.random.default_rng(5)
+    seqs = rp.append_frames(rng.integers(0, 255, (2000, 84, 84), dtype=np.uint8))
+    K = 1800
+    st = np.stack([seqs[i:i + 4] for i in range(K)])
+    rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 6, K), R=rng.normal(size=K).astype(np.float32),
+                   Gamma=np.full(K, 0.97, np.float32), priority=rng.random(K).astype(np.float32) + 0.01))
+    L = FusedNatureLearner(cfg, DEV, rp)
+    assert L._fuse_norm
+    for _ in range(3):
+        L.step()
+        torch.cuda.synchronize()
+        true = float(L.g32.double().norm())
+        assert abs(float(L.gnorm[0]) - true) <= 1e-4 * true + 1e-12, (float(L.gnorm[0]), true)
