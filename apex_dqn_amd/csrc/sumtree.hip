@@ -14,6 +14,30 @@
 // Duplicate indices in one update batch: last occurrence wins (deterministic).
 #include "apex_common.h"
 
+// Bounds-checking debug build (SURVEY §5.2 "race / bounds detection"): built as a
+// separate library with -DAPEX_DEBUG_BOUNDS and selected by APEX_DEBUG_BOUNDS=1.
+// Every leaf / ring-slot / frame index a replay kernel dereferences is checked;
+// a violation bumps a per-site device counter, records the first bad index and
+// is clamped into range (or dropped) -- nothing traps, so a corrupt index shows
+// up as a readable error report instead of a GPU fault that resets the node.
+// Sites: 0 tree_update leaf, 1 replay_insert slot, 2 tree_sample leaf/record,
+// 3 gather_frames ring slot, 4 replay_insert frame-slot value, 5 zero_range slot.
+#define APEX_DBG_SITES 8
+#ifdef APEX_DEBUG_BOUNDS
+__device__ int apex_dbg_count[APEX_DBG_SITES];
+__device__ long long apex_dbg_first[APEX_DBG_SITES];
+__device__ __forceinline__ bool apex_dbg_ok(int64_t i, int64_t n, int site) {
+  if (i >= 0 && i < n) return true;
+  if (atomicAdd(&apex_dbg_count[site], 1) == 0) apex_dbg_first[site] = (long long)i;
+  return false;
+}
+#define APEX_DBG_OK(i, n, site) apex_dbg_ok((int64_t)(i), (int64_t)(n), site)
+#define APEX_DBG_CLAMP(i, n, site) (APEX_DBG_OK(i, n, site) ? (i) : ((i) < 0 ? 0 : (n) - 1))
+#else
+#define APEX_DBG_OK(i, n, site) true
+#define APEX_DBG_CLAMP(i, n, site) (i)
+#endif
+
 struct TreeDesc {
   float* leaf;
   double* nodes;
@@ -32,6 +56,7 @@ struct RecordDesc {
   int32_t* gen;   // [cap] slot generation (bumped on every insert)
   int C;
   int64_t cap;
+  int64_t nframes;  // frame-ring size (debug bounds checks of stored slots; 0 = unchecked)
 };
 
 // Write leaf values and propagate the deltas up the tree, block-cooperatively
@@ -112,7 +137,7 @@ __global__ void __launch_bounds__(1024) tree_update_kernel(TreeDesc t, const int
   int64_t s = 0;
   if (act) {
     s = idx[i];
-    act = s >= 0 && s < t.n[0];
+    act = APEX_DBG_OK(s, t.n[0], 0);
   }
   if (dedupe) {  // host guarantees gridDim.x == 1 and n <= 1024
     for (int j = threadIdx.x; j < 2048; j += blockDim.x) {
@@ -155,7 +180,8 @@ __global__ void __launch_bounds__(256) tree_zero_range_kernel(TreeDesc t, int64_
   __shared__ uint32_t lmin;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool act = i < count;
-  const int64_t s = act ? (start + i) % t.n[0] : 0;
+  int64_t s = act ? (start + i) % t.n[0] : 0;
+  s = APEX_DBG_CLAMP(s, t.n[0], 5);
   if (act && t.leaf[s] == 0.f) act = false;
   tree_block_update(t, act, s, 0.f, lacc, &lmin, kfirst);
 }
@@ -174,12 +200,20 @@ __global__ void __launch_bounds__(256) replay_insert_kernel(TreeDesc t, RecordDe
   __shared__ uint32_t lmin;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < K;
-  const int64_t s = act ? (start + i) % r.cap : 0;
+  int64_t s = act ? (start + i) % r.cap : 0;
+  s = APEX_DBG_CLAMP(s, r.cap < t.n[0] ? r.cap : t.n[0], 1);
   float v = 0.f;
   if (act) {
     for (int c = 0; c < r.C; ++c) {
-      r.obs[s * r.C + c] = s_obs[(int64_t)i * r.C + c];
-      r.nxt[s * r.C + c] = s_nxt[(int64_t)i * r.C + c];
+      const int32_t so = s_obs[(int64_t)i * r.C + c], sn = s_nxt[(int64_t)i * r.C + c];
+#ifdef APEX_DEBUG_BOUNDS
+      if (r.nframes > 0) {
+        APEX_DBG_OK(so, r.nframes, 4);
+        APEX_DBG_OK(sn, r.nframes, 4);
+      }
+#endif
+      r.obs[s * r.C + c] = so;
+      r.nxt[s * r.C + c] = sn;
     }
     r.act[s] = s_act[i];
     r.rew[s] = s_rew[i];
@@ -236,7 +270,8 @@ __global__ void tree_sample_kernel(TreeDesc t, RecordDesc r, int B, uint64_t see
     u -= excl;
     node = node * 64 + sel;
   }
-  const int64_t s = node < t.n[0] ? node : t.n[0] - 1;
+  int64_t s = node < t.n[0] ? node : t.n[0] - 1;
+  s = APEX_DBG_CLAMP(s, r.cap < t.n[0] ? r.cap : t.n[0], 2);
   if (lane == 0) {
     float p = t.leaf[s];
     float ratio = ratio_min_global ? ratio_min_global[0]
@@ -293,9 +328,15 @@ __global__ void fill_u32_kernel(uint32_t* p, uint32_t v, int64_t n) {
 
 // gather stacked frames: out[b, c] = ring[slots[b, c]]  (uint8, frame_bytes each)
 __global__ void gather_frames_kernel(const uint8_t* __restrict__ ring, const int32_t* __restrict__ slots,
-                                     int nstack, int64_t frame_bytes, uint8_t* __restrict__ out) {
+                                     int64_t nframes, int64_t frame_bytes, uint8_t* __restrict__ out) {
   const int bc = blockIdx.x;  // one block per (sample, channel)
-  const int32_t s = slots[bc];
+  int32_t s = slots[bc];
+#ifdef APEX_DEBUG_BOUNDS
+  if (!(s >= 0 && s < nframes)) {
+    if (threadIdx.x == 0) (void)APEX_DBG_OK(s, nframes, 3);
+    s = s < 0 ? 0 : (int32_t)(nframes - 1);
+  }
+#endif
   const uint4* src = reinterpret_cast<const uint4*>(ring + (int64_t)s * frame_bytes);
   uint4* dst = reinterpret_cast<uint4*>(out + (int64_t)bc * frame_bytes);
   const int64_t nv = frame_bytes / 16;
@@ -357,12 +398,46 @@ APEX_EXPORT int apex_tree_rebuild(TreeDesc t, hipStream_t st) {
   APEX_CHECK_LAUNCH();
 }
 
-APEX_EXPORT int apex_gather_frames(const uint8_t* ring, const int32_t* slots, int n_slots, int nstack,
+APEX_EXPORT int apex_gather_frames(const uint8_t* ring, const int32_t* slots, int n_slots, int64_t nframes,
                                    int64_t frame_bytes, uint8_t* out, hipStream_t st) {
   if (n_slots <= 0) return 0;
   if (frame_bytes % 16) return (int)hipErrorInvalidValue;
-  gather_frames_kernel<<<n_slots, 256, 0, st>>>(ring, slots, nstack, frame_bytes, out);
+  gather_frames_kernel<<<n_slots, 256, 0, st>>>(ring, slots, nframes, frame_bytes, out);
   APEX_CHECK_LAUNCH();
 }
 
-APEX_EXPORT int apex_abi_version() { return 1; }
+APEX_EXPORT int apex_abi_version() { return 2; }
+
+// 1 if this library was built with -DAPEX_DEBUG_BOUNDS
+APEX_EXPORT int apex_debug_bounds_enabled() {
+#ifdef APEX_DEBUG_BOUNDS
+  return 1;
+#else
+  return 0;
+#endif
+}
+
+// copy (and optionally reset) the per-site violation counters + first bad index
+APEX_EXPORT int apex_debug_errors(int* counts, long long* first, int reset) {
+#ifdef APEX_DEBUG_BOUNDS
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyFromSymbol(counts, HIP_SYMBOL(apex_dbg_count), sizeof(int) * APEX_DBG_SITES);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyFromSymbol(first, HIP_SYMBOL(apex_dbg_first), sizeof(long long) * APEX_DBG_SITES);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    int zc[APEX_DBG_SITES] = {0};
+    long long zf[APEX_DBG_SITES] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(apex_dbg_count), zc, sizeof(zc));
+    e = hipMemcpyToSymbol(HIP_SYMBOL(apex_dbg_first), zf, sizeof(zf));
+  }
+  return (int)e;
+#else
+  for (int i = 0; i < APEX_DBG_SITES; ++i) {
+    counts[i] = 0;
+    first[i] = 0;
+  }
+  return 0;
+#endif
+}

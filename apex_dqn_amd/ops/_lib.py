@@ -34,7 +34,7 @@ class TreeDesc(ctypes.Structure):
 
 class RecordDesc(ctypes.Structure):
     _fields_ = [("obs", c_p), ("nxt", c_p), ("act", c_p), ("rew", c_p), ("gam", c_p), ("gen", c_p),
-                ("C", c_i), ("cap", c_i64)]
+                ("C", c_i), ("cap", c_i64), ("nframes", c_i64)]
 
 
 class HeadParams(ctypes.Structure):
@@ -98,7 +98,9 @@ _SIGS = {
     "apex_tree_sample": ([TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                           c_p, c_p, c_p, c_p], c_i),
     "apex_tree_rebuild": ([TreeDesc, c_p], c_i),
-    "apex_gather_frames": ([c_p, c_p, c_i, c_i, c_i64, c_p, c_p], c_i),
+    "apex_gather_frames": ([c_p, c_p, c_i, c_i64, c_i64, c_p, c_p], c_i),
+    "apex_debug_bounds_enabled": ([], c_i),
+    "apex_debug_errors": ([c_p, c_p, c_i], c_i),
     "apex_grad_sqnorm_partials": ([c_p, c_i64, c_p, c_p], c_i),
     "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p], c_i),
     "apex_cast_bf16": ([c_p, c_p, c_i64, c_p], c_i),
@@ -137,10 +139,11 @@ def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:
     global _LIB, _LOAD_ERROR
     if _LIB is not None:
         return _LIB
-    path = _build.KERNEL_LIB
+    debug = debug_bounds_requested()
+    path = _build.KERNEL_DEBUG_LIB if debug else _build.KERNEL_LIB
     try:
         if build_if_missing and not os.path.exists(path):
-            _build.build_kernels()
+            _build.build_kernels(debug=debug)
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         _declare(lib)
         _LIB = lib
@@ -148,6 +151,27 @@ def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:
         _LOAD_ERROR = repr(e)
         _LIB = None
     return _LIB
+
+
+def debug_bounds_requested() -> bool:
+    """``APEX_DEBUG_BOUNDS=1`` selects the bounds-checking kernel library
+    (``libapex_kernels_debug.so``, built with ``-DAPEX_DEBUG_BOUNDS``)."""
+    return os.environ.get("APEX_DEBUG_BOUNDS", "0") not in ("", "0")
+
+
+DEBUG_SITES = ("tree_update.leaf", "replay_insert.slot", "tree_sample.slot", "gather_frames.frame",
+               "replay_insert.frame_value", "tree_zero_range.slot", "unused6", "unused7")
+
+
+def debug_errors(reset: bool = True) -> dict:
+    """Per-site bounds-violation counts of the debug library (synchronises the
+    device).  ``{site: (count, first_bad_index)}`` for sites with violations;
+    always empty for the release library."""
+    lib = require_kernels()
+    counts = (ctypes.c_int * 8)()
+    first = (ctypes.c_longlong * 8)()
+    check(lib.apex_debug_errors(ctypes.addressof(counts), ctypes.addressof(first), int(reset)), "debug_errors")
+    return {DEBUG_SITES[i]: (int(counts[i]), int(first[i])) for i in range(8) if counts[i]}
 
 
 def available() -> bool:

@@ -23,6 +23,7 @@ PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 OUT = os.path.join(HERE, "_build")
 KERNEL_LIB = os.path.join(OUT, "libapex_kernels.so")
+KERNEL_DEBUG_LIB = os.path.join(OUT, "libapex_kernels_debug.so")
 RUNTIME_LIB = os.path.join(OUT, "libapex_runtime.so")
 ARCH = os.environ.get("APEX_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -50,25 +51,35 @@ def _run(cmd: List[str]) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
 
 
-def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool = False) -> str:
+    """``debug=True`` builds ``libapex_kernels_debug.so`` with ``-DAPEX_DEBUG_BOUNDS``
+    (device-side index checks in the replay kernels, see csrc/sumtree.hip)."""
     os.makedirs(OUT, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.cuh"))
+    lib_path = KERNEL_DEBUG_LIB if debug else KERNEL_LIB
+    suffix = ".dbg.o" if debug else ".o"
+    flags = HIP_FLAGS + (["-DAPEX_DEBUG_BOUNDS"] if debug else [])
     objs = []
     todo = []
+    if debug:
+        build_kernels(force=force, jobs=jobs)  # sources without debug checks reuse the release objects
     for s in srcs:
-        o = os.path.join(OUT, os.path.basename(s) + ".o")
+        dbg_src = debug and "APEX_DEBUG_BOUNDS" in open(s).read()
+        o = os.path.join(OUT, os.path.basename(s) + (suffix if dbg_src else ".o"))
         objs.append(o)
+        if debug and not dbg_src:
+            continue
         if force or _newer([s] + headers + [os.path.abspath(__file__)], o):
-            todo.append([HIPCC] + HIP_FLAGS + ["-c", s, "-o", o])
+            todo.append([HIPCC] + flags + ["-c", s, "-o", o])
     if todo:
         with ThreadPoolExecutor(max_workers=jobs) as ex:
             list(ex.map(_run, todo))
-    if force or todo or _newer(objs, KERNEL_LIB):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", KERNEL_LIB] + objs)
+    if force or todo or _newer(objs, lib_path):
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib_path] + objs)
     if verbose:
-        print(f"built {KERNEL_LIB} ({len(todo)} objects recompiled)")
-    return KERNEL_LIB
+        print(f"built {lib_path} ({len(todo)} objects recompiled)")
+    return lib_path
 
 
 def build_runtime(force: bool = False, verbose: bool = False) -> str:
@@ -82,9 +93,11 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     return RUNTIME_LIB
 
 
-def build_all(force: bool = False, verbose: bool = True) -> None:
+def build_all(force: bool = False, verbose: bool = True, debug: bool = True) -> None:
     build_runtime(force=force, verbose=verbose)
     build_kernels(force=force, verbose=verbose)
+    if debug:
+        build_kernels(force=force, verbose=verbose, debug=True)
 
 
 if __name__ == "__main__":

@@ -119,7 +119,7 @@ class GpuReplayShard:
             r.obs, r.nxt = self.obs.data_ptr(), self.nxt.data_ptr()
             r.act, r.rew, r.gam, r.gen = (self.act.data_ptr(), self.rew.data_ptr(), self.gam.data_ptr(),
                                           self.gen.data_ptr())
-            r.C, r.cap = self.C, self.cap
+            r.C, r.cap, r.nframes = self.C, self.cap, self.F
             self._rdesc = r
         return self._rdesc
 
@@ -257,7 +257,7 @@ class GpuReplayShard:
         B = slots.shape[0]
         raw = torch.empty((B, self.C) + self.frame_shape, dtype=torch.uint8, device=self.device)
         if self.use_hip:
-            _lib.check(self.lib.apex_gather_frames(self.frames.data_ptr(), slots.data_ptr(), B * self.C, self.C,
+            _lib.check(self.lib.apex_gather_frames(self.frames.data_ptr(), slots.data_ptr(), B * self.C, self.F,
                                                    self.frame_bytes, raw.data_ptr(), self._stream()),
                        "gather_frames")
         else:
