@@ -30,51 +30,77 @@ struct Conv1S2DDesc {
   uint8_t* scratch;           // >= 1 KB dummy store target (rows past the end)
   int N, C, m_switch;
   float in_scale;
+  uint64_t* probe;            // optional phase timestamps (blocks < PROBE_BLOCKS), see mfma_common.h
 };
 
 // ---------------------------------------------------------------------------
 // Image-resident forward.  A persistent workgroup (8 waves, one per CU)
 // walks whole images.  Per image:
 //   * its C uint8 frames (C x 7056 contiguous bytes in the ring) arrive in an
-//     LDS staging area by LDS-DMA, issued while the previous image computes;
-//   * every 16-byte s2d block is converted to bf16 ONCE, into 2C planes
-//     (frame c, half h) of 441 x 16 B (plane stride 7168 = 28 x 256 B, so the
-//     two halves read by one ds_read_b128 lane group never share banks);
+//     LDS staging area by LDS-DMA;
+//   * every 16-byte s2d block is converted ONCE into 2C planes (frame c, half h)
+//     of 441 x 16 B (plane stride 7168 = 28 x 256 B) as f16 (1024 + x): one
+//     v_perm_b32 per two pixels (u8x8_to_f16off), exact; the offset adds
+//     1024 * sum_k w[n][k] to output channel n, folded into the epilogue bias;
 //   * the A fragment of (pixel p, tap (a,b), frame c, half h) is then a single
-//     ds_read_b128 at base(p) + lane-constant offset -- no conversion or address
-//     VALU per MFMA; the B fragments (weights, 2C x 4 per lane) live in VGPRs;
+//     ds_read_b128 at base(p) + lane-constant offset; the B fragments (weights
+//     converted to f16, 2C x 2 per lane) live in VGPRs; v_mfma_f32_16x16x32_f16;
 //   * 25 row tiles of 16 pixels; wave pair (2p, 2p+1) takes tiles p, p+4, ...,
-//     each wave one half of the 64 output channels (half the B fragments per
-//     wave, so two waves fit per SIMD); the epilogue stages each tile through
-//     a wave-private LDS tile for 64-B row-half stores.
-// The 1/255 scale, bias and ReLU are applied in the epilogue; online/target
-// weights switch per image (m_switch is a multiple of 400 rows).
+//     each wave one half of the 64 output channels (two waves fit per SIMD).
+// Pipelining (tuned with the PROBE phase stamps, scripts/probe_kernels.py):
+//   * planes are double-buffered: image i+1 is converted while image i computes;
+//   * each wave converts exactly the staging chunks its own LDS-DMA brought in,
+//     so the DMA -> convert hand-off is a per-wave vmcnt wait, no barrier, and
+//     no wait ever covers the epilogue stores (store acks cost microseconds);
+//   * waves 0-3 convert first and then compute, waves 4-7 compute first: every
+//     SIMD overlaps one wave's conversion with the other's MFMAs; the staging
+//     chunks are dealt so that the two waves with 7 tiles convert fewer chunks;
+//   * the epilogue is packed fp32 FMA (scale, bias), cvt_pk_bf16 and a packed
+//     int16 max (ReLU), stored straight from registers (two 8-byte stores).
+//   * weight sets are fetched with contiguous 16-B loads one image ahead, then
+//     installed through a swizzled LDS copy (a conflict-free fragment gather).
+// Online/target weights switch per image (m_switch is a multiple of 400 rows;
+// strided images make it at most one switch per block).
 #define C1_PLANE 7168
 #define C1_TILES 25
 #define C1_THREADS 512
+#define C1_MAXIMG 256   // images per workgroup (slot table in LDS)
+
+// staging instruction k (1 KB, 64 lanes x 16 B) belongs to the wave at position
+// k % 8 of the order 2,3,4,5,6,7,0,1: waves 0-1 (7 tiles) take the fewest
+__device__ __forceinline__ constexpr int c1_owner_pos(int w) { return (w + 6) & 7; }
+
+// LDS byte offset of the 8-byte piece (chunk q, half h) of the installed OIHW
+// weight copy: chunk low bits XOR the output channel, halves swapped on q bit 1,
+// so the per-lane fragment gather (16 channels x 4 K-chunks) is conflict-free.
+template <int C>
+__device__ __forceinline__ int c1_wswz(int q, int h) {
+  constexpr int NSH = 3 + (C == 4 ? 2 : (C == 2 ? 1 : 0));   // chunk -> output channel shift
+  return (((q & ~15) | ((q ^ (q >> NSH)) & 15)) << 4) + ((h ^ ((q >> 1) & 1)) << 3);
+}
 
 template <int C>
 __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
-  constexpr int NW = C1_THREADS / 64;    // 8 waves: 2 per SIMD hide each other's epilogue / LDS latency
+  constexpr int NW = C1_THREADS / 64;
   constexpr int IMG = 2 * C * C1_PLANE;
   constexpr int NCHUNK = C * 441;        // 16-B s2d blocks per image
   constexpr int NDMA = (NCHUNK + 63) / 64;
-  constexpr int NDW = (NDMA + NW - 1) / NW;   // DMA wave-instructions per wave
-  constexpr int STG = NDMA * 1024;       // u8 staging (lane-linear DMA pieces)
-  __shared__ __attribute__((aligned(16))) uint8_t smem[IMG + STG + NW * 1024];
-  uint8_t* Pl = smem;
-  uint8_t* Sg = Pl + IMG;
-  uint8_t* Ep = Sg + STG;
+  constexpr int NDW = (NDMA + NW - 1) / NW;   // max staging instructions per wave
+  constexpr int STG = NDMA * 1024;
+  static_assert(IMG >= 64 * 64 * C * 2 + 256, "weight install needs one plane buffer");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * IMG + STG];
+  __shared__ int32_t slot_tbl[C1_MAXIMG * C];   // this block's frame slots (prologue)
+  uint8_t* Sg = smem + 2 * IMG;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, pl = lane & 15;
   const bool two = d.w2 != nullptr;
   const int img_switch = two ? d.m_switch / 400 : 1 << 30;
-
-  // wave pair (2 p, 2 p + 1) shares row tiles p, p+4, ...; wave w owns channels
-  // [32 (w & 1), 32 (w & 1) + 32) = n-tiles nt0, nt0 + 1: half the B fragments per wave
+  const int pos = c1_owner_pos(wv);
+  const bool conv_first = wv < 4;        // group A: convert, then compute
+  const int ntiles = (wv >> 1) == 0 ? 7 : 6;
   const int nt0 = 2 * (wv & 1);
-  float4 bv[2];                          // bias of the current weight set (channels 16 (nt0+j) + 4 g ..)
-  // lane-constant A offsets per k-step s: block q = 2s + (g >> 1) = (tap, frame c), half g & 1
+  const int ndma_w = NDMA > pos ? (NDMA - pos + NW - 1) / NW : 0;   // this wave's DMA instructions / image
+  f32x2v bv[2][2];                       // epilogue bias (offset-corrected), channel pairs
   int aoff[2 * C];
 #pragma unroll
   for (int s = 0; s < 2 * C; ++s) {
@@ -84,14 +110,31 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
   // ---- B fragments of the current weight set in VGPRs (swapped-operand MFMA: lane
   // (g, pl) supplies output channel n = 16 nt + pl, s2d K 32 s + 8 g .. +7), gathered
   // from OIHW w1: 16-B K chunk c = 4 s + g is (tap, frame) block q = c >> 1, kernel
-  // rows r4 = 2 (c & 1) + {0, 1}, each 4 contiguous kw taps (8 B)
-  bf16x8 bfr[2 * C][2];
+  // rows r4 = 2 (c & 1) + {0, 1}, each 4 contiguous kw taps (8 B).
+  f16x8 bfr[2 * C][2];
+  uint4 wpf[C];
+  float4 bpf = make_float4(0.f, 0.f, 0.f, 0.f);
   int cur_set = -1;
-  auto load_b = [&](int set) {
-    const bf16_t* W = set ? d.w2 : d.w;
-    const float* bsrc = set ? d.bias2 : d.bias;
+  auto prefetch_w = [&](int set) {
+    const uint4* W = reinterpret_cast<const uint4*>(set ? d.w2 : d.w);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bv[j] = *reinterpret_cast<const float4*>(bsrc + 16 * (nt0 + j) + 4 * g);
+    for (int j = 0; j < C; ++j) wpf[j] = W[tid + C1_THREADS * j];
+    if (tid < 16) bpf = reinterpret_cast<const float4*>(set ? d.bias2 : d.bias)[tid];
+  };
+  // `younger`: VMEM ops this wave issued after the prefetch that need not finish
+  auto install_w = [&](uint8_t* L, int set, int younger) {   // every wave; L: a free plane buffer
+    vmcnt_le(younger);
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+      const int q = tid + C1_THREADS * j;
+      const uint4 v = wpf[j];
+      *reinterpret_cast<uint2*>(L + c1_wswz<C>(q, 0)) = make_uint2(v.x, v.y);
+      *reinterpret_cast<uint2*>(L + c1_wswz<C>(q, 1)) = make_uint2(v.z, v.w);
+    }
+    float* Lb = reinterpret_cast<float*>(L + 64 * 64 * C * 2);
+    if (tid < 16) reinterpret_cast<float4*>(Lb)[tid] = bpf;
+    __syncthreads();
+    float ws[2] = {0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 2 * C; ++s)
 #pragma unroll
@@ -99,26 +142,54 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
         const int n = 16 * (nt0 + nt) + pl, c = 4 * s + g;
         const int q = c >> 1, tap = q / C, ch = q - tap * C;
         const int kh = 4 * (tap >> 1) + 2 * (c & 1), kw = 4 * (tap & 1);
-        const bf16_t* p = W + ((n * C + ch) * 8 + kh) * 8 + kw;
-        const uint2 lo = *reinterpret_cast<const uint2*>(p);
-        const uint2 hi = *reinterpret_cast<const uint2*>(p + 8);
-        bfr[s][nt] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        const int p = ((n * C + ch) * 8 + kh) * 8 + kw;     // element offset, multiple of 4
+        const uint2 lo = *reinterpret_cast<const uint2*>(L + c1_wswz<C>(p >> 3, (p >> 2) & 1));
+        const uint2 hi = *reinterpret_cast<const uint2*>(L + c1_wswz<C>((p >> 3) + 1, (p >> 2) & 1));
+        const uint32_t wd[4] = {lo.x, lo.y, hi.x, hi.y};
+        f16x8 f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float a0 = __uint_as_float(wd[i] << 16), a1 = __uint_as_float(wd[i] & 0xffff0000u);
+          f[2 * i] = (_Float16)a0;
+          f[2 * i + 1] = (_Float16)a1;
+          ws[nt] += (float)f[2 * i] + (float)f[2 * i + 1];
+        }
+        bfr[s][nt] = f;
       }
+    // channel sums over the 4 K-chunk lanes, then the epilogue's channels 4 g + i
+    // fetch theirs: bias' = bias - 1024 * scale * sum_k w16[n][k]
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      float t = ws[nt];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      float c4[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c4[i] = __shfl(t, 4 * g + i, 64);
+      const float4 bb = *reinterpret_cast<const float4*>(Lb + 16 * (nt0 + nt) + 4 * g);
+      const float k = 1024.f * d.in_scale;
+      bv[nt][0] = (f32x2v){bb.x - k * c4[0], bb.y - k * c4[1]};
+      bv[nt][1] = (f32x2v){bb.z - k * c4[2], bb.w - k * c4[3]};
+    }
     cur_set = set;
+    __syncthreads();   // L is a plane buffer: free it for the next conversion
   };
 
-  // ---- LDS-DMA of one image's frames: chunk j = frame j / 441, block j % 441
-  auto issue_dma = [&](int img) {
-    int sl[4];
-    sload_slots<C>(d.slots + img * C, sl);
+  // ---- this wave's LDS-DMA share of one image: instructions k = pos + 8 j
+  auto issue_dma = [&](int img, int it_img) {
+    // slots from the LDS table: a scalar load here would expose its full memory
+    // latency (s_waitcnt lgkmcnt(0)) every image (~1400 clocks, PROBE-measured)
+    int sl[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int i = 0; i < NDW; ++i) {
-      const int k = wv * NDW + i;
+    for (int cc = 0; cc < C; ++cc) sl[cc] = slot_tbl[it_img * C + cc];
+#pragma unroll
+    for (int j = 0; j < NDW; ++j) {
+      const int k = pos + NW * j;
       if (k < NDMA) {
-        const int j = 64 * k + lane;
+        const int ch = 64 * k + lane;
         const uint8_t* src = d.zero16;
-        if (j < NCHUNK) {
-          const int c = j / 441, blk = j - c * 441;
+        if (ch < NCHUNK) {
+          const int c = ch / 441, blk = ch - c * 441;
           int slot = sl[0];
 #pragma unroll
           for (int cc = 1; cc < C; ++cc)
@@ -130,77 +201,112 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
       }
     }
   };
-
-  const int G = gridDim.x;
-  int img = blockIdx.x;
-  if (img < d.N) {
-    load_b(img >= img_switch ? 1 : 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    issue_dma(img);
-  }
-  uint8_t* E = Ep + wv * 1024;
-  for (int it = 0; img < d.N; img += G, ++it) {
-    // this wave's DMA(img) landed: younger VMEM ops are the previous image's
-    // epilogue stores (1 per row tile: 7 tiles for waves 0-1, 6 for the others)
-    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (wv < 2) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // ---- u8 staging -> bf16 planes (each block converted once)
-    for (int j = tid; j < NCHUNK; j += C1_THREADS) {
-      const uint4 v = *reinterpret_cast<const uint4*>(Sg + j * 16);
-      const int c = j / 441, blk = j - c * 441;
-      const uint4 lo = make_uint4(bf16pair_from_f32(ubyte(v.x, 0), ubyte(v.x, 1)), bf16pair_from_f32(ubyte(v.x, 2), ubyte(v.x, 3)),
-                                  bf16pair_from_f32(ubyte(v.y, 0), ubyte(v.y, 1)), bf16pair_from_f32(ubyte(v.y, 2), ubyte(v.y, 3)));
-      const uint4 hi = make_uint4(bf16pair_from_f32(ubyte(v.z, 0), ubyte(v.z, 1)), bf16pair_from_f32(ubyte(v.z, 2), ubyte(v.z, 3)),
-                                  bf16pair_from_f32(ubyte(v.w, 0), ubyte(v.w, 1)), bf16pair_from_f32(ubyte(v.w, 2), ubyte(v.w, 3)));
-      *reinterpret_cast<uint4*>(Pl + (2 * c) * C1_PLANE + blk * 16) = lo;
-      *reinterpret_cast<uint4*>(Pl + (2 * c + 1) * C1_PLANE + blk * 16) = hi;
+  // ---- convert this wave's own staging chunks into planes `P` (u8 -> f16 1024+x)
+  auto convert = [&](uint8_t* P) {
+#pragma unroll
+    for (int j = 0; j < NDW; ++j) {
+      const int k = pos + NW * j;
+      const int ch = 64 * k + lane;
+      if (k < NDMA && ch < NCHUNK) {
+        const uint4 v = *reinterpret_cast<const uint4*>(Sg + ch * 16);
+        const int c = ch / 441, blk = ch - c * 441;
+        *reinterpret_cast<uint4*>(P + (2 * c) * C1_PLANE + blk * 16) = u8x8_to_f16off(v.x, v.y);
+        *reinterpret_cast<uint4*>(P + (2 * c + 1) * C1_PLANE + blk * 16) = u8x8_to_f16off(v.z, v.w);
+      }
     }
-    __syncthreads();
-    // staging is free: prefetch the next image under this one's MFMAs
-    if (img + G < d.N) issue_dma(img + G);
-    const int set = img >= img_switch ? 1 : 0;
-    if (set != cur_set) {
-      // weight-set switch (once per block): reload, then restore the vmcnt invariant
-      load_b(set);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // staging reads retired before the next DMA may overwrite them
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  // ---- this wave's row tiles of image `img` from planes `P`; 2 stores per tile
+  auto compute = [&](const uint8_t* P, int img) {
     for (int t = wv >> 1; t < C1_TILES; t += NW / 2) {
       const int p = 16 * t + pl;
       const int oh = p / 20, ow = p - 20 * oh;
-      const uint8_t* A = Pl + ((oh * 21 + ow) << 4);
+      const uint8_t* A = P + ((oh * 21 + ow) << 4);
+      f16x8 a[2 * C];
+#pragma unroll
+      for (int s = 0; s < 2 * C; ++s) a[s] = *reinterpret_cast<const f16x8*>(A + aoff[s]);
       f32x4 acc[2];
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2 * C; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + aoff[s]);
+      for (int s = 0; s < 2 * C; ++s)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
-          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[s][nt], a, acc[nt], 0, 0, 0);
-      }
-      // epilogue: lane holds channels 16 (nt0+nt) + 4 g .. +3 of pixel pl -> wave tile
-      // (16 rows x 64 B: 4 chunks, chunk c of row r at c ^ ((r >> 1) & 3)) -> one
-      // 16-B store per lane (rows of the output are 128 B: this wave writes one half)
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[s][nt], a[s], acc[nt], 0, 0, 0);
+      // lane holds channels 16 (nt0+nt) + 4 g .. +3 of pixel p: one 8-byte store each
+      bf16_t* yrow = d.y + ((int64_t)img * 400 + p) * 64 + 16 * nt0 + 4 * g;
+      const f32x2v sc = {d.in_scale, d.in_scale};
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const f32x4 v = acc[nt];
-        const uint2 o = make_uint2(relu2(cvt_pk_bf16(v[0] * d.in_scale + bv[nt].x, v[1] * d.in_scale + bv[nt].y)),
-                                   relu2(cvt_pk_bf16(v[2] * d.in_scale + bv[nt].z, v[3] * d.in_scale + bv[nt].w)));
-        const int byte = 2 * (16 * nt + 4 * g);
-        *reinterpret_cast<uint2*>(E + pl * 64 + ((((byte >> 4) ^ ((pl >> 1) & 3))) << 4) + (byte & 15)) = o;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      {
-        const int row = lane >> 2, ch = lane & 3;
-        const uint4 v = *reinterpret_cast<const uint4*>(E + row * 64 + ((ch ^ ((row >> 1) & 3)) << 4));
-        *reinterpret_cast<uint4*>(d.y + ((int64_t)img * 400 + 16 * t + row) * 64 + 32 * (wv & 1) + ch * 8) = v;
+        const f32x2v v0 = (f32x2v){acc[nt][0], acc[nt][1]} * sc + bv[nt][0];
+        const f32x2v v1 = (f32x2v){acc[nt][2], acc[nt][3]} * sc + bv[nt][1];
+        const uint2 o = make_uint2(relu_pk16(cvt_pk_bf16(v0[0], v0[1])), relu_pk16(cvt_pk_bf16(v1[0], v1[1])));
+        *reinterpret_cast<uint2*>(yrow + 16 * nt) = o;
       }
     }
-    __syncthreads();   // planes may be overwritten by the next conversion
+  };
+  // wait for this wave's DMA(next): younger VMEM ops are the stores of one compute()
+  auto wait_dma = [&](bool exact0) {
+    if (exact0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (ntiles == 7) {
+      asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    }
+  };
+
+  const int G = gridDim.x;
+  int img = blockIdx.x;
+  if (img >= d.N) return;
+  // this block's frame slots -> LDS (host guarantees ceil(N / G) <= C1_MAXIMG)
+  for (int i = tid; i < C1_MAXIMG * C; i += C1_THREADS) {
+    const int im = blockIdx.x + (i / C) * G;
+    slot_tbl[i] = im < d.N ? d.slots[im * C + (i % C)] : 0;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // prologue: weights installed (via planes[1]), image 0 converted into planes[0],
+  // DMA of image 1 in flight
+  prefetch_w(img >= img_switch ? 1 : 0);
+  issue_dma(img, 0);
+  install_w(smem + IMG, img >= img_switch ? 1 : 0, 0);   // vmcnt(0): DMA(img) landed too
+  convert(smem);
+  if (img + G < d.N) issue_dma(img + G, 1);
+  __syncthreads();
+  for (int it = 0; img < d.N; img += G, ++it) {
+    PROBE(d.probe, NW, it, 0);
+    uint8_t* Pc = smem + (it & 1) * IMG;
+    uint8_t* Pn = smem + ((it & 1) ^ 1) * IMG;
+    const bool has_next = img + G < d.N;
+    const int set = img >= img_switch ? 1 : 0;
+    if (set != cur_set) install_w(Pn, set, 2 * ntiles + ndma_w);   // prefetched last iteration
+    // next image switches sets: fetch them now, hidden under this image's work
+    // (extra loads only make the vmcnt waits below more conservative)
+    if (has_next && (img + G >= img_switch ? 1 : 0) != set) prefetch_w(set ^ 1);
+    if (conv_first) {
+      if (has_next) wait_dma(it == 0);
+      PROBE(d.probe, NW, it, 1);
+      if (has_next) {
+        convert(Pn);
+        if (img + 2 * G < d.N) issue_dma(img + 2 * G, it + 2);
+      }
+      PROBE(d.probe, NW, it, 2);
+      compute(Pc, img);
+      PROBE(d.probe, NW, it, 3);
+    } else {
+      compute(Pc, img);
+      PROBE(d.probe, NW, it, 1);
+      if (has_next) wait_dma(false);
+      PROBE(d.probe, NW, it, 2);
+      if (has_next) {
+        convert(Pn);
+        if (img + 2 * G < d.N) issue_dma(img + 2 * G, it + 2);
+      }
+      PROBE(d.probe, NW, it, 3);
+    }
+    __syncthreads();   // planes[next] complete, planes[cur] free
+  }
 }
 
 // w1 [64][C][8][8] (OIHW) -> s2d K order [64][(tap*C + c)*16 + r4*4 + c4], tap = 2a + b,
@@ -248,6 +354,7 @@ APEX_EXPORT int apex_conv1_s2d_fwd(Conv1S2DDesc d, int grid, hipStream_t st) {
   if (d.w2 != nullptr && (d.m_switch % 400)) return (int)hipErrorInvalidValue;
   if (d.N < 1) return 0;
   if (grid <= 0 || grid > d.N) grid = d.N < 256 ? d.N : 256;
+  if ((d.N + grid - 1) / grid > C1_MAXIMG) grid = (d.N + C1_MAXIMG - 1) / C1_MAXIMG;
   switch (d.C) {
     case 1: conv1_s2d_fwd_kernel<1><<<grid, C1_THREADS, 0, st>>>(d); break;
     case 2: conv1_s2d_fwd_kernel<2><<<grid, C1_THREADS, 0, st>>>(d); break;

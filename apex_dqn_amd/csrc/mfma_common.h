@@ -9,6 +9,27 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+// uint8 pixels -> f16 (1024 + x), exact for x <= 1023: the f16 with exponent 2^10
+// and mantissa x.  Two bytes of `v` (b_i, b_{i+1}) become one f16 pair with a
+// single v_perm_b32 (bytes [b_i, 0x64, b_{i+1}, 0x64]); the +1024 offset is a
+// per-output-channel constant (1024 * sum of the channel's weights) removed in
+// the GEMM epilogue.  3x fewer VALU than cvt_f32_ubyte + cvt_pk_bf16.
+__device__ __forceinline__ uint32_t u8pair_f16off(uint32_t v, int hi) {
+  return __builtin_amdgcn_perm(0x64646464u, v, hi ? 0x04030402u : 0x04010400u);
+}
+__device__ __forceinline__ uint4 u8x8_to_f16off(uint32_t lo, uint32_t hi) {
+  return make_uint4(u8pair_f16off(lo, 0), u8pair_f16off(lo, 1), u8pair_f16off(hi, 0), u8pair_f16off(hi, 1));
+}
+// relu on two packed 16-bit floats (bf16 or f16): signed-int16 max with 0
+__device__ __forceinline__ uint32_t relu_pk16(uint32_t v) {
+  typedef short s16x2 __attribute__((ext_vector_type(2)));
+  const s16x2 x = __builtin_bit_cast(s16x2, v);
+  const s16x2 z = {0, 0};
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(x, z));
+}
 
 // 128-byte LDS rows, 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7):
 // a 16-lane ds_read_b128 group (16 rows, one chunk) hits 16 distinct 16-B slots.
@@ -114,6 +135,22 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_off) {
                : "memory");
 }
 
+// s_waitcnt vmcnt(n) for a run-time n (immediate operand: one branch per value;
+// n is wave-uniform, larger values clamp to 63 = no wait)
+__device__ __forceinline__ void vmcnt_le(int n) {
+#define APEX_VMCNT_CASE(k) \
+  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+  switch (n) {
+    APEX_VMCNT_CASE(0) APEX_VMCNT_CASE(1) APEX_VMCNT_CASE(2) APEX_VMCNT_CASE(3) APEX_VMCNT_CASE(4)
+    APEX_VMCNT_CASE(5) APEX_VMCNT_CASE(6) APEX_VMCNT_CASE(7) APEX_VMCNT_CASE(8) APEX_VMCNT_CASE(9)
+    APEX_VMCNT_CASE(10) APEX_VMCNT_CASE(11) APEX_VMCNT_CASE(12) APEX_VMCNT_CASE(13) APEX_VMCNT_CASE(14)
+    APEX_VMCNT_CASE(15) APEX_VMCNT_CASE(16) APEX_VMCNT_CASE(17) APEX_VMCNT_CASE(18) APEX_VMCNT_CASE(19)
+    APEX_VMCNT_CASE(20) APEX_VMCNT_CASE(21) APEX_VMCNT_CASE(22) APEX_VMCNT_CASE(23) APEX_VMCNT_CASE(24)
+    default: break;
+  }
+#undef APEX_VMCNT_CASE
+}
+
 // Scalar (SMEM) load of the C frame slots of one image: counted by lgkmcnt, so it
 // never forces a vmcnt drain of the LDS-DMA in flight.  `p` must be wave-uniform.
 template <int C>
@@ -137,4 +174,23 @@ __device__ __forceinline__ void sload_slots(const int32_t* p, int (&out)[4]) {
   }
 }
 
-
+// Phase probes for persistent kernels (diagnostic build only: compiled in with
+// -DAPEX_PROBE, i.e. in libapex_kernels_debug.so, selected by APEX_DEBUG_BOUNDS=1;
+// the release kernels carry no stamps, so their waits are unaffected).  With a
+// non-null buffer, lane 0 of every wave of the first PROBE_BLOCKS workgroups
+// stores s_memtime (shader clock) at point `pt` of iteration `it` ->
+// buf[((block * NW + wave) * PROBE_ITERS + it) * 4 + pt].  scripts/probe_kernels.py.
+#define PROBE_BLOCKS 4
+#define PROBE_ITERS 16
+#ifdef APEX_PROBE
+#define PROBE(buf, NW, it, pt)                                                                          \
+  do {                                                                                                  \
+    if ((buf) != nullptr && blockIdx.x < PROBE_BLOCKS && (it) < PROBE_ITERS && (threadIdx.x & 63) == 0) \
+      (buf)[((blockIdx.x * (NW) + (threadIdx.x >> 6)) * PROBE_ITERS + (it)) * 4 + (pt)] =                \
+          __builtin_amdgcn_s_memtime();                                                                 \
+  } while (0)
+#else
+#define PROBE(buf, NW, it, pt) \
+  do {                         \
+  } while (0)
+#endif

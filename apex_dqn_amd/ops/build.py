@@ -53,19 +53,21 @@ def _run(cmd: List[str]) -> None:
 
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool = False) -> str:
     """``debug=True`` builds ``libapex_kernels_debug.so`` with ``-DAPEX_DEBUG_BOUNDS``
-    (device-side index checks in the replay kernels, see csrc/sumtree.hip)."""
+    (device-side index checks in the replay kernels, see csrc/sumtree.hip) and
+    ``-DAPEX_PROBE`` (in-kernel phase stamps, csrc/mfma_common.h)."""
     os.makedirs(OUT, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.cuh"))
     lib_path = KERNEL_DEBUG_LIB if debug else KERNEL_LIB
     suffix = ".dbg.o" if debug else ".o"
-    flags = HIP_FLAGS + (["-DAPEX_DEBUG_BOUNDS"] if debug else [])
+    flags = HIP_FLAGS + (["-DAPEX_DEBUG_BOUNDS", "-DAPEX_PROBE"] if debug else [])
     objs = []
     todo = []
     if debug:
         build_kernels(force=force, jobs=jobs)  # sources without debug checks reuse the release objects
     for s in srcs:
-        dbg_src = debug and "APEX_DEBUG_BOUNDS" in open(s).read()
+        text = open(s).read()
+        dbg_src = debug and ("APEX_DEBUG_BOUNDS" in text or "PROBE(" in text)
         o = os.path.join(OUT, os.path.basename(s) + (suffix if dbg_src else ".o"))
         objs.append(o)
         if debug and not dbg_src:

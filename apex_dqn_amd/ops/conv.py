@@ -87,7 +87,7 @@ def pack_w1_s2d(lib, ws: "Workspace", w1: torch.Tensor, tag: str) -> torch.Tenso
 
 def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
                   b1: torch.Tensor, scale: float, out: torch.Tensor, w2=None, b2=None, rows_first: int = 0,
-                  grid: int = 0) -> None:
+                  grid: int = 0, probe: Optional[torch.Tensor] = None) -> None:
     """conv1 on the space-to-depth replay ring (persistent LDS-DMA kernel, csrc/conv1_s2d.hip)."""
     N, C = slots.shape
     assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
@@ -106,6 +106,8 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
     d.zero16 = zero.data_ptr()
     d.scratch = ws.get(("scratch1k",), 2048, ring.device, torch.uint8).data_ptr()
     d.N, d.C, d.in_scale = N, C, float(scale)
+    if probe is not None:
+        d.probe = probe.data_ptr()
     _lib.check(lib.apex_conv1_s2d_fwd(d, int(grid), _lib.stream_ptr()), "conv1_s2d_fwd")
 
 
