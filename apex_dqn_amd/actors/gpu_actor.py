@@ -138,7 +138,7 @@ class GpuActorGroup:
 
 
 class GraphActorGroup(GpuActorGroup):
-    """Actor group for ``GraphLearner`` networks (IMPALA-deep, nature32, ...): the
+    """Actor group for ``GraphLearner`` networks (IMPALA-deep): the
     frame stacks are gathered from the replay ring on the device, the actor's own
     network copy (refreshed every ``Q_network_sync_freq`` steps) runs in bf16, and
     epsilon-greedy is drawn on the device; one small D2H copy per step."""

@@ -46,16 +46,16 @@ class FusedNatureLearner:
         self.C = cfg.frame_stack
         self.A = int(cfg.env_conf.action_dim)
         self.B = int(batch_size or cfg.Learner.replay_sample_size)
-        c1 = 32 if cfg.network == "nature32" else 64
-        if c1 != 64:
-            raise NotImplementedError("fused learner implements the reference 64-filter conv1")
+        # nature32 (Nature DQN's 32-filter conv1) runs zero-padded to 64 filters on the
+        # same kernels (models/flat_params.py:reference_state_to_flat): exact math
+        self.c1 = 32 if cfg.network == "nature32" else 64
         if backend is None:
             backend = "hip" if (self.device.type == "cuda" and self.rt.use_hip_kernels) else "torch"
         self.ops = HipBackend() if backend == "hip" else TorchBackend(
             torch.bfloat16 if self.device.type == "cuda" else torch.float32)
         self.act_dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         d = self.device
-        self.layout = FlatLayout(nature_segments(self.C, self.A, c1))
+        self.layout = FlatLayout(nature_segments(self.C, self.A, 64))
         n = self.layout.numel
         self.p32 = torch.zeros(n, dtype=torch.float32, device=d)
         self.pbf = torch.zeros(n, dtype=self.act_dtype, device=d)
@@ -70,7 +70,7 @@ class FusedNatureLearner:
         self.T = self.layout.views(self.t32)
         self.Tb = self.layout.views(self.tbf)
         # random init identical in distribution to the reference module (torch default init)
-        init = DuellingDQN((self.C, 84, 84), self.A)
+        init = DuellingDQN((self.C, 84, 84), self.A, conv1_channels=self.c1)
         reference_state_to_flat(init.state_dict(), {k: v for k, v in self.P.items()})
         if comm is not None and comm.world_size > 1:
             comm.broadcast_flat(self.p32)
@@ -99,9 +99,10 @@ class FusedNatureLearner:
         self._fuse_norm = self.world == 1 and self.ops.name == "hip" and getattr(self.ops, "native_conv", False)
         # cross-shard IS-weight normaliser: min over ranks of (min_i p_i / total)
         self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
-        self.ratio_buf = torch.zeros(1, dtype=torch.float32, device=d)
+        self.ratio_buf = torch.zeros(2, 1, dtype=torch.float32, device=d)   # double-buffered (see _dp_step)
         self.ratio_min = None
-        self._ratio_work = None
+        self._ratio_work = [None, None]
+        self._ratio_k = 0
         if self.world > 1:
             self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d)
             self._init_ratio()
@@ -295,9 +296,18 @@ class FusedNatureLearner:
         cut = self.layout.offsets["wfc"]
         run = (lambda i: self._graphs[i].replay()) if graphs else (lambda i: (self._seg1, self._seg2,
                                                                                 self._seg3)[i]())
-        if self._ratio_work is not None:
-            self._ratio_work.wait()
-            self.ratio_min.copy_(self.ratio_buf)
+        # The IS normaliser all-reduced after step t-1 is consumed by step t+1, not
+        # step t: that tiny MIN all-reduce then completes under step t's compute
+        # (RCCL's stream already ran it before step t's gradient buckets) instead of
+        # sitting between seg3 and the next sample as a latency bubble.  The
+        # normaliser is a global per-step scale of the IS weights; one step of lag
+        # changes it by the few priorities one step rewrites.
+        k = self._ratio_k
+        prev = self._ratio_work[k]
+        if prev is not None:
+            prev.wait()
+            self.ratio_min.copy_(self.ratio_buf[k])
+            self._ratio_work[k] = None
         run(0)
         w_fc = dist.all_reduce(self.gcomm[cut:], op=dist.ReduceOp.SUM, async_op=True)
         run(1)  # conv backward overlaps the fc/head bucket all-reduce
@@ -306,8 +316,9 @@ class FusedNatureLearner:
         w_cv.wait()
         self._mark("allreduce_wait")
         run(2)
-        self.ratio_buf.copy_(self.ratio_local)
-        self._ratio_work = dist.all_reduce(self.ratio_buf, op=dist.ReduceOp.MIN, async_op=True)
+        self.ratio_buf[k].copy_(self.ratio_local)
+        self._ratio_work[k] = dist.all_reduce(self.ratio_buf[k], op=dist.ReduceOp.MIN, async_op=True)
+        self._ratio_k = 1 - k
 
     def step(self) -> None:
         """One learner update (asynchronous on the current stream)."""
@@ -355,16 +366,18 @@ class FusedNatureLearner:
         import torch.distributed as dist
         rp = self.replay
         tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float().clamp_min(1e-30)
-        self.ratio_buf.copy_(rp.min_bits.view(torch.float32) / tot)
-        dist.all_reduce(self.ratio_buf, op=dist.ReduceOp.MIN)
-        self.ratio_min.copy_(self.ratio_buf)
+        buf = self.ratio_buf[0]
+        buf.copy_(rp.min_bits.view(torch.float32) / tot)
+        dist.all_reduce(buf, op=dist.ReduceOp.MIN)
+        self.ratio_min.copy_(buf)
 
     def refresh_replay_stats(self) -> None:
         """Re-derive the cross-shard IS normaliser (after inserts / eviction)."""
         if self.world > 1:
-            if self._ratio_work is not None:
-                self._ratio_work.wait()
-                self._ratio_work = None
+            for i, w in enumerate(self._ratio_work):
+                if w is not None:
+                    w.wait()
+                    self._ratio_work[i] = None
             self._init_ratio()
 
     def _snapshot(self):
@@ -390,21 +403,21 @@ class FusedNatureLearner:
     def q_values(self, frames_u8: torch.Tensor) -> torch.Tensor:
         """Greedy-evaluation helper: q for a (N, C, 84, 84) uint8 batch."""
         sd = self.reference_state_dict()
-        net = DuellingDQN((self.C, 84, 84), self.A).to(self.device)
+        net = DuellingDQN((self.C, 84, 84), self.A, conv1_channels=self.c1).to(self.device)
         net.load_state_dict(sd)
         with torch.no_grad():
             return net(frames_u8.to(self.device))[2]
 
     # ------------------------------------------------------------- params
     def reference_state_dict(self):
-        return flat_to_reference_state(self.P)
+        return flat_to_reference_state(self.P, self.c1)
 
     def load_reference_state_dict(self, sd) -> None:
         reference_state_to_flat(sd, self.P)
         self.pbf.copy_(self.p32)
 
     def save(self, path: str) -> None:
-        tgt = flat_to_reference_state(self.T)
+        tgt = flat_to_reference_state(self.T, self.c1)
         save_checkpoint(path, self.reference_state_dict(), Q_target_state=tgt,
                         optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
                         num_q_updates=self.num_q_updates, config=self.cfg.to_dict())

@@ -58,15 +58,18 @@ class FlatLayout:
         return out
 
 
-def flat_to_reference_state(v: Dict[str, torch.Tensor]) -> "OrderedDict[str, torch.Tensor]":
-    """Engine layout -> reference DuellingDQN state_dict (fp32, CPU)."""
+def flat_to_reference_state(v: Dict[str, torch.Tensor], c1: int = 64) -> "OrderedDict[str, torch.Tensor]":
+    """Engine layout -> reference DuellingDQN state_dict (fp32, CPU).
+
+    ``c1`` < 64: the engine keeps conv1 zero-padded to 64 filters (see
+    ``reference_state_to_flat``); only the first ``c1`` filters are exported."""
     def fc_cols_to_chw(w):  # (512, 3136[h,w,c]) -> (512, 3136[c,h,w])
         return w.reshape(-1, 7, 7, 64).permute(0, 3, 1, 2).reshape(w.shape[0], 3136)
 
     sd = OrderedDict()
-    sd["layer1.0.weight"] = v["w1"].clone()
-    sd["layer1.0.bias"] = v["b1"].clone()
-    sd["layer2.0.weight"] = v["w2"].permute(0, 3, 1, 2).contiguous()
+    sd["layer1.0.weight"] = v["w1"][:c1].clone()
+    sd["layer1.0.bias"] = v["b1"][:c1].clone()
+    sd["layer2.0.weight"] = v["w2"][..., :c1].permute(0, 3, 1, 2).contiguous()
     sd["layer2.0.bias"] = v["b2"].clone()
     sd["layer3.0.weight"] = v["w3"].permute(0, 3, 1, 2).contiguous()
     sd["layer3.0.bias"] = v["b3"].clone()
@@ -82,14 +85,24 @@ def flat_to_reference_state(v: Dict[str, torch.Tensor]) -> "OrderedDict[str, tor
 
 
 def reference_state_to_flat(sd: Dict[str, torch.Tensor], v: Dict[str, torch.Tensor]) -> None:
-    """Reference state_dict -> engine layout (in place into the views ``v``)."""
+    """Reference state_dict -> engine layout (in place into the views ``v``).
+
+    A 32-filter conv1 (Nature DQN, ``network = "nature32"``) is stored
+    zero-padded to the engine's 64 filters: padded filters and the matching
+    conv2 input channels are exact zeros, so the padded activations are
+    ReLU(0) = 0, their gradients are exactly 0, and RMSprop (update ~ g) keeps
+    them at 0 -- the same math as the 32-filter net, run by the 64-filter kernels."""
     def fc_cols_to_hwc(w):
         return w.reshape(-1, 64, 7, 7).permute(0, 2, 3, 1).reshape(w.shape[0], 3136)
 
     with torch.no_grad():
-        v["w1"].copy_(sd["layer1.0.weight"])
-        v["b1"].copy_(sd["layer1.0.bias"])
-        v["w2"].copy_(sd["layer2.0.weight"].permute(0, 2, 3, 1))
+        c1 = sd["layer1.0.weight"].shape[0]
+        if c1 != v["w1"].shape[0]:
+            for k in ("w1", "b1", "w2"):
+                v[k].zero_()
+        v["w1"][:c1].copy_(sd["layer1.0.weight"])
+        v["b1"][:c1].copy_(sd["layer1.0.bias"])
+        v["w2"][..., :c1].copy_(sd["layer2.0.weight"].permute(0, 2, 3, 1))
         v["b2"].copy_(sd["layer2.0.bias"])
         v["w3"].copy_(sd["layer3.0.weight"].permute(0, 2, 3, 1))
         v["b3"].copy_(sd["layer3.0.bias"])

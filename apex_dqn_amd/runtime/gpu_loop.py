@@ -56,9 +56,9 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     E = num_envs or cfg.Runtime.actors_per_rank or max(1, cfg.Actor.num_actors // world)
     torch.manual_seed(rt.seed)
     replay = build_replay(cfg, device, E, seed=rt.seed + rank)
-    if cfg.network == "nature64":
+    if cfg.network in ("nature64", "nature32"):
         learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=backend)
-    else:   # IMPALA-deep, nature32: graph-captured torch-autograd learner on the same HBM replay
+    else:   # IMPALA-deep: graph-captured learner on the same HBM replay
         from ..learner.graph_learner import GraphLearner
         learner = GraphLearner(cfg, device, replay, comm=comm)
     group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed)

@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
-                    help="nature64 = the headline fused-HIP learner; others use the graph learner")
+                    help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala uses the graph learner")
     args = ap.parse_args()
 
     from apex_dqn_amd.config import ApexConfig
@@ -55,8 +55,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # one rank per GPU; the modulo only matters when rehearsing several ranks on
+    # fewer GPUs (device_count() does not initialise the GPU)
+    dev_idx = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_idx)
+    device = torch.device("cuda", dev_idx)
     comm = Comm.from_env(backend="nccl", device=device)
 
     cfg = ApexConfig.from_dict({
@@ -86,7 +89,7 @@ def main():
                            R=rng.normal(size=K).astype(np.float32), Gamma=np.full(K, 0.99 ** 3, np.float32),
                            priority=rng.random(K).astype(np.float32) + 0.01))
     replay.rebuild()
-    if args.network == "nature64":
+    if args.network in ("nature64", "nature32"):
         learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
     else:
         from apex_dqn_amd.learner.graph_learner import GraphLearner

@@ -57,6 +57,8 @@ def _worker(rank, world, path, q, ar="fp32"):
     g_local = Lref.g32.clone()
     L.step()
     g_dp = L.g32.clone()
+    for _ in range(3):      # exercises the double-buffered (one-step-lagged) IS normaliser
+        L.step()
     gl = [torch.zeros_like(g_local) for _ in range(world)]
     torch.distributed.all_gather(gl, g_local)
     g_mean = torch.stack(gl).mean(0)

@@ -10,11 +10,11 @@ from apex_dqn_amd.models.flat_params import flat_to_reference_state
 from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
 
 
-def _setup(loss="huber", A=6):
+def _setup(loss="huber", A=6, network="nature64"):
     torch.manual_seed(0)
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": A, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": 8},
-                                "Runtime": {"grad_clip": 40.0, "loss": loss}})
+                                "Runtime": {"grad_clip": 40.0, "loss": loss, "network": network}})
     rp = GpuReplayShard(400, 400, 600, 4, device="cpu")
     rng = np.random.default_rng(0)
     seqs = rp.append_frames(rng.integers(0, 255, (300, 84, 84), dtype=np.uint8))
@@ -28,8 +28,8 @@ def _setup(loss="huber", A=6):
     return cfg, rp
 
 
-def _check(loss):
-    cfg, rp = _setup(loss)
+def _check(loss, network="nature64"):
+    cfg, rp = _setup(loss, network=network)
     L = FusedNatureLearner(cfg, "cpu", rp)
     T = TorchLearner(cfg, "cpu")
     T.Q.load_state_dict(L.reference_state_dict())
@@ -45,9 +45,10 @@ def _check(loss):
     lref.backward()
     assert abs(float(lref) - float(L.loss_b.mean())) < 1e-5 * max(1.0, abs(float(lref)))
     torch.testing.assert_close(td, L.td_abs, rtol=1e-5, atol=1e-5)
-    gf = flat_to_reference_state(L.G)
+    gf = flat_to_reference_state(L.G, L.c1)
     for k, p in T.Q.named_parameters():
         torch.testing.assert_close(gf[k], p.grad, rtol=1e-4, atol=1e-7)
+    return L
 
 
 def test_fused_backward_matches_autograd_huber():
@@ -56,6 +57,19 @@ def test_fused_backward_matches_autograd_huber():
 
 def test_fused_backward_matches_autograd_mse():
     _check("mse")
+
+
+def test_nature32_runs_zero_padded_on_the_64_filter_path():
+    """Nature DQN's 32-filter conv1 is stored padded to 64 filters: the padded
+    gradients are exactly zero, so RMSprop keeps the padding at zero."""
+    L = _check("huber", network="nature32")
+    assert L.c1 == 32
+    assert torch.count_nonzero(L.G["w1"][32:]) == 0 and torch.count_nonzero(L.G["b1"][32:]) == 0
+    assert torch.count_nonzero(L.G["w2"][..., 32:]) == 0
+    L._seg3()
+    assert torch.count_nonzero(L.P["w1"][32:]) == 0 and torch.count_nonzero(L.P["w2"][..., 32:]) == 0
+    sd = L.reference_state_dict()
+    assert sd["layer1.0.weight"].shape[0] == 32 and sd["layer2.0.weight"].shape[1] == 32
 
 
 def test_fused_step_updates_params_and_priorities():
