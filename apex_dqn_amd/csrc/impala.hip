@@ -1,0 +1,555 @@
+// Small-channel 3x3 convolutions for the IMPALA-deep ResNet dueling Q-net
+// (BASELINE.json config 5; not in the reference, whose only network is the
+// NatureCNN of duelling_network.py:8-19).  gfx950, wave64, MFMA 16x16x32 bf16.
+//
+// Activation layout ("planar-16"): an activation of C channels is stored per
+// image as C/16 planes of [H][W][16] bf16, i.e. 32-byte pixel rows.  That row
+// width makes BOTH LDS reads the kernels need conflict-free without swizzles:
+//   * the im2col row fragment (ds_read_b128, 16 pixels x 16 B): pixel p's two
+//     16-B halves land on bank quads 2p, 2p+1 -- distinct for 16 consecutive
+//     pixels in every ds_read_b128 lane group;
+//   * the transposed fragment (ds_read_b64_tr_b16, 4 pixel rows x 16 channels
+//     per 16-lane group): a 32-lane half reads 8 consecutive pixel rows = 256
+//     contiguous bytes = all 64 banks once.
+//
+// sconv_fwd   one workgroup per (image, row band): the band's input rows (+1-row
+//             halo, zero-padded to (R+2) x (W+2)) are staged in LDS once (ReLU
+//             applied on the way in when the conv consumes relu(x)); outputs are
+//             computed on the flattened padded-width grid q = h (W+2) + w, so
+//             tap (kh, kw) of a 16-pixel M tile is the LDS row block at
+//             q + kh (W+2) + kw: a plain ds_read_b128 per K chunk, no index math.
+//             K = 9 taps x C_in in 32-wide chunks of two (tap, 16-ch plane)
+//             pairs; weights live in VGPRs as pre-packed MFMA fragments
+//             (sconv_pack).  Swapped operands (weights as A) give each lane 4
+//             consecutive output channels of one pixel -> one 8-byte store.
+//             Epilogue: *scale + bias, optional (* (mask > 0)), optional + add,
+//             optional ReLU -- covers the forward (bias, residual add) and the
+//             data gradient (mask = forward activation, add = skip gradient),
+//             which is the same correlation with transposed + flipped weights.
+// sconv_wgrad dW[co][ci][t] = sum over pixels dY[p][co] x[p + toff(t)][ci]: both
+//             operands through the transposed LDS read, reduction over 32-pixel
+//             chunks split across the 4 waves, summed in LDS; each workgroup writes
+//             one fp32 partial to a split-K slab, reduced by grad_finalize (conv_mfma.hip).
+// maxpool3s2  3x3 / stride 2 / pad 1 max pool (+ argmax codes for the backward);
+//             its backward is a gather (each input pixel sums the <= 4 window
+//             gradients whose argmax it is): no atomics.
+#include "mfma_common.h"
+
+struct SconvDesc {
+  const void* x;              // bf16 planar input, or (mode 2) the uint8 s2d frame ring
+  const int32_t* slots;       // mode 2: [N][4] frame-ring slots of each image
+  const bf16_t* wf;           // packed weight fragments (sconv_pack)
+  const bf16_t* wf2;          // second weight set for images >= n_switch (target net), or null
+  const float* bias;          // [C_out] or null
+  const float* bias2;
+  const bf16_t* add;          // added after the mask (output layout), or null
+  const bf16_t* mask;         // output multiplied by (mask > 0) (output layout), or null
+  bf16_t* y;                  // bf16 planar output
+  int64_t x_img, y_img;       // image strides (elements)
+  int64_t add_img, mask_img;
+  int N, n_switch;
+  int relu_in, relu_out;
+  float scale;                // applied to the accumulator before the bias
+  int pad0;
+};
+
+struct SconvWgDesc {
+  const bf16_t* dy;           // planar gradient of the conv output
+  const void* x;              // planar conv input (or mode 2: the frame ring)
+  const int32_t* slots;
+  float* slab;                // [nsplit][C_out * cin_real * 9] fp32 partials (OIHW order)
+  float* bslab;               // [nsplit][C_out]
+  int64_t dy_img, x_img;
+  int N, relu_in;
+  int imgs_per_group, cin_real;
+};
+
+__device__ __forceinline__ uint4 relu_u4(uint4 v) {
+  return make_uint4(relu_pk16(v.x), relu_pk16(v.y), relu_pk16(v.z), relu_pk16(v.w));
+}
+
+// Stage input rows [r0 - 1, r0 + R] x cols [-1, W] of image n (zero outside the
+// image) into P LDS planes of `plane_pix` 32-byte pixel rows; pixels past the
+// (R+2) x (W+2) block up to plane_pix are zeroed (M-tile overrun reads).
+// MODE 0: planar bf16; MODE 2: 4 uint8 frames from the space-to-depth ring
+// (csrc/conv1_s2d.hip layout) as channels 0..3 of a 16-channel plane.
+template <int P, int H, int W, int R, int MODE>
+__device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const void* x, int64_t x_img,
+                                           const int32_t* slots, int n, int r0, int relu, int tid, int nthr) {
+  constexpr int WP = W + 2, ROWS = R + 2, BLK = ROWS * WP;
+  if constexpr (MODE == 2) {
+    const uint8_t* ring = reinterpret_cast<const uint8_t*>(x);
+    const int32_t* sl = slots + (int64_t)n * 4;
+    const int64_t f0 = (int64_t)sl[0] * 7056, f1 = (int64_t)sl[1] * 7056;
+    const int64_t f2 = (int64_t)sl[2] * 7056, f3 = (int64_t)sl[3] * 7056;
+    for (int i = tid; i < BLK; i += nthr) {
+      const int lr = i / WP, c = i - lr * WP;
+      const int h = r0 - 1 + lr, w = c - 1;
+      uint4 lo = make_uint4(0, 0, 0, 0);
+      if (h >= 0 && h < H && w >= 0 && w < W) {
+        const int o = ((h >> 2) * 21 + (w >> 2)) * 16 + (h & 3) * 4 + (w & 3);
+        lo.x = cvt_pk_bf16((float)ring[f0 + o], (float)ring[f1 + o]);
+        lo.y = cvt_pk_bf16((float)ring[f2 + o], (float)ring[f3 + o]);
+      }
+      *reinterpret_cast<uint4*>(xs + i * 32) = lo;
+      *reinterpret_cast<uint4*>(xs + i * 32 + 16) = make_uint4(0, 0, 0, 0);
+    }
+  } else {
+    const bf16_t* xi = reinterpret_cast<const bf16_t*>(x) + (int64_t)n * x_img;
+    for (int i = tid; i < P * BLK * 2; i += nthr) {
+      const int hf = i & 1, pix = i >> 1;
+      const int p = pix / BLK, rem = pix - p * BLK;
+      const int lr = rem / WP, c = rem - lr * WP;
+      const int h = r0 - 1 + lr, w = c - 1;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (h >= 0 && h < H && w >= 0 && w < W) {
+        v = *reinterpret_cast<const uint4*>(xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+        if (relu) v = relu_u4(v);
+      }
+      *reinterpret_cast<uint4*>(xs + (p * plane_pix + rem) * 32 + hf * 16) = v;
+    }
+  }
+  const int slack = plane_pix - BLK;
+  for (int i = tid; i < P * slack * 2; i += nthr) {
+    const int p = i / (slack * 2), r = i - p * slack * 2;
+    *reinterpret_cast<uint4*>(xs + (p * plane_pix + BLK) * 32 + r * 16) = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// =====================================================================================
+// forward / data-gradient correlation
+// =====================================================================================
+template <int CIN, int COUT, int H, int W, int R, int MODE>
+__global__ void __launch_bounds__(256) sconv_fwd_kernel(SconvDesc d) {
+  constexpr int P = CIN / 16, NT = COUT / 16;
+  constexpr int WP = W + 2;
+  constexpr int PLANE = (R + 2) * WP + 18;     // + overrun of the last M tile's taps
+  constexpr int NCH = (9 * P + 1) / 2;         // 32-wide K chunks = pairs of (tap, plane)
+  constexpr int MROWS = R * WP;
+  constexpr int NTILE = (MROWS + 15) / 16;
+  __shared__ __attribute__((aligned(16))) uint8_t xs[P * PLANE * 32];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int band = blockIdx.x, n = blockIdx.y;
+  const int r0 = band * R;
+  const bool second = d.wf2 != nullptr && n >= d.n_switch;
+  const bf16_t* __restrict__ wf = second ? d.wf2 : d.wf;
+  const float* __restrict__ bias = second ? d.bias2 : d.bias;
+
+  // weight fragments first (L2-resident; overlap the staging loads)
+  bf16x8 wfr[NCH][NT];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      wfr[c][nt] = *reinterpret_cast<const bf16x8*>(wf + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
+
+  stage_rows<P, H, W, R, MODE>(xs, PLANE, d.x, d.x_img, d.slots, n, r0, d.relu_in, tid, 256);
+  __syncthreads();
+
+  // per-lane LDS byte offset of each K chunk: lane group kg = lane >> 4 reads
+  // pair 2c + (kg >> 1) (tap-major: pair = t * P + p), 16-B half (kg & 1)
+  const int kg = lane >> 4;
+  int aoff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int pair = 2 * c + (kg >> 1);
+    if (pair >= 9 * P) pair = 9 * P - 1;       // zero-weight K slot: any in-bounds read
+    const int t = pair / P, p = pair - (pair / P) * P;
+    const int toff = (t / 3) * WP + (t % 3);
+    aoff[c] = (p * PLANE + toff + (lane & 15)) * 32 + (kg & 1) * 16;
+  }
+  bf16_t* __restrict__ yi = d.y + (int64_t)n * d.y_img;
+  const bf16_t* __restrict__ addi = d.add ? d.add + (int64_t)n * d.add_img : nullptr;
+  const bf16_t* __restrict__ mski = d.mask ? d.mask + (int64_t)n * d.mask_img : nullptr;
+
+  for (int tile = wv; tile < NTILE; tile += 4) {
+    const int q0 = tile * 16;
+    bf16x8 xf[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) xf[c] = *reinterpret_cast<const bf16x8*>(xs + aoff[c] + q0 * 32);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[c][nt], xf[c], acc[nt], 0, 0, 0);
+    // lane: pixel q0 + (lane & 15), output channels nt*16 + 4 kg + {0..3}
+    const int q = q0 + (lane & 15);
+    const int lh = q / WP, w = q - (q / WP) * WP;
+    const int h = r0 + lh;
+    if (lh < R && w < W && h < H) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int co = nt * 16 + 4 * kg;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] * d.scale;
+        if (bias) {
+          const float4 b = *reinterpret_cast<const float4*>(bias + co);
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        const int64_t off = ((int64_t)(nt * H + h) * W + w) * 16 + 4 * kg;
+        if (mski) {
+          const uint2 m = *reinterpret_cast<const uint2*>(mski + off);
+          v[0] = bf16_to_f32(m.x & 0xffff) > 0.f ? v[0] : 0.f;
+          v[1] = bf16_to_f32(m.x >> 16) > 0.f ? v[1] : 0.f;
+          v[2] = bf16_to_f32(m.y & 0xffff) > 0.f ? v[2] : 0.f;
+          v[3] = bf16_to_f32(m.y >> 16) > 0.f ? v[3] : 0.f;
+        }
+        if (addi) {
+          const uint2 a = *reinterpret_cast<const uint2*>(addi + off);
+          v[0] += bf16_to_f32(a.x & 0xffff);
+          v[1] += bf16_to_f32(a.x >> 16);
+          v[2] += bf16_to_f32(a.y & 0xffff);
+          v[3] += bf16_to_f32(a.y >> 16);
+        }
+        if (d.relu_out) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        *reinterpret_cast<uint2*>(yi + off) = make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+      }
+    }
+  }
+}
+
+// =====================================================================================
+// weight gradient
+// =====================================================================================
+// MFMA operand from a transposed read of 32-byte pixel rows: lane (g = lane>>4,
+// i = lane&15) receives channel i of pixels 16h + 4g + {0..3} for h = 0, 1 --
+// the K order (k = 8g + 4h + r <-> pixel 16h + 4g + r) is the same for both
+// operands, and each 32-lane half reads 8 consecutive pixel rows per instruction.
+__device__ __forceinline__ bf16x8 tr_pix_frag(const uint8_t* plane, int pix0, int lane) {
+  const int g = lane >> 4, i = lane & 15, qq = i >> 2, pp = i & 3;
+  const lds_s16x4* pa = (const lds_s16x4*)(plane + (pix0 + 4 * g + qq) * 32 + 8 * pp);
+  const lds_s16x4* pb = (const lds_s16x4*)(plane + (pix0 + 16 + 4 * g + qq) * 32 + 8 * pp);
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pa));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(const_cast<lds_s16x4*>(pb));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = (s16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int CIN, int COUT, int H, int W, int R, int MODE>
+__global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
+  constexpr int P = CIN / 16, NT = COUT / 16;
+  constexpr int WP = W + 2;
+  constexpr int NQ = (R * WP + 31) / 32;             // 32-pixel reduction chunks per band
+  constexpr int DPIX = NQ * 32;                      // dY plane (zero past R x WP)
+  constexpr int XPIX = DPIX + 2 * WP + 2;            // x plane: covers every tap of every chunk
+  static_assert(XPIX >= (R + 2) * WP, "x plane too small");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[(NT * DPIX + P * XPIX) * 32];
+  uint8_t* dys = smem;
+  uint8_t* xs = smem + NT * DPIX * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int band = blockIdx.x, group = blockIdx.y;
+  const int r0 = band * R;
+  const int n_begin = group * d.imgs_per_group;
+  const int n_end = min(d.N, n_begin + d.imgs_per_group);
+
+  f32x4 acc[NT][9 * P], accb[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    accb[a] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int b = 0; b < 9 * P; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
+
+  for (int n = n_begin; n < n_end; ++n) {
+    // dY band: pixel q = lh * WP + w, zero for w >= W, rows past H / R, and q >= R * WP
+    const bf16_t* dyi = d.dy + (int64_t)n * d.dy_img;
+    for (int i = tid; i < NT * DPIX * 2; i += 256) {
+      const int hf = i & 1, pix = i >> 1;
+      const int p = pix / DPIX, q = pix - p * DPIX;
+      const int lh = q / WP, w = q - lh * WP;
+      const int h = r0 + lh;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (lh < R && w < W && h < H) v = *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+      *reinterpret_cast<uint4*>(dys + (p * DPIX + q) * 32 + hf * 16) = v;
+    }
+    stage_rows<P, H, W, R, MODE>(xs, XPIX, d.x, d.x_img, d.slots, n, r0, d.relu_in, tid, 256);
+    __syncthreads();
+    for (int j = wv; j < NQ; j += 4) {
+      const int qb = 32 * j;
+      bf16x8 a[NT];
+#pragma unroll
+      for (int ct = 0; ct < NT; ++ct) {
+        a[ct] = tr_pix_frag(dys + ct * DPIX * 32, qb, lane);
+        accb[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], ones, accb[ct], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = (t / 3) * WP + (t % 3);
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          const bf16x8 b = tr_pix_frag(xs + p * XPIX * 32, qb + toff, lane);
+#pragma unroll
+          for (int ct = 0; ct < NT; ++ct)
+            acc[ct][t * P + p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], b, acc[ct][t * P + p], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // the 4 waves' partials are summed through LDS (4 tiles per round) and the
+  // workgroup writes ONE partial: slab[split][co][ci][t] (OIHW order), split = band + bands * group
+  constexpr int T = NT * 9 * P;
+  const int split = group * gridDim.x + band;
+  const int KW9 = d.cin_real * 9;
+  float* __restrict__ slab = d.slab + (int64_t)split * COUT * KW9;
+  f32x4* red = reinterpret_cast<f32x4*>(smem);          // [wave][4 tiles][64 lanes]
+#pragma unroll
+  for (int base = 0; base < T; base += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u < T) red[(wv * 4 + u) * 64 + lane] = acc[(base + u) / (9 * P)][(base + u) % (9 * P)];
+    __syncthreads();
+    {
+      const int u = tid >> 6, l = tid & 63, tt = base + u;
+      if (tt < T) {
+        f32x4 v = red[u * 64 + l];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) v += red[(w * 4 + u) * 64 + l];
+        const int ct = tt / (9 * P), k = tt - ct * (9 * P);
+        const int t = k / P, p = k - (k / P) * P;
+        const int ci = p * 16 + (l & 15);
+        if (ci < d.cin_real) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) slab[(int64_t)(ct * 16 + 4 * (l >> 4) + r) * KW9 + ci * 9 + t] = v[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) {
+    red[wv * 64 + lane] = accb[ct];
+    __syncthreads();
+    if (tid < 64) {
+      f32x4 v = red[lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) v += red[w * 64 + lane];
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d.bslab[(int64_t)split * COUT + ct * 16 + 4 * (lane >> 4) + r] = v[r];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// =====================================================================================
+// 3x3 / stride 2 / pad 1 max pool on planar-16 tensors (+ backward)
+// =====================================================================================
+// one thread per (image, plane, output pixel, 8-channel half); argmax code = kh * 3 + kw
+// of the first maximum in window order (torch.max_pool2d's tie rule)
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restrict__ x, int64_t x_img, int P, int H,
+                                                          int W, int Ho, int Wo, bf16_t* __restrict__ y,
+                                                          int64_t y_img, uint8_t* __restrict__ amax, int N) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * P * Ho * Wo * 2;
+  if (idx >= total) return;
+  const int hf = (int)(idx & 1);
+  int64_t r = idx >> 1;
+  const int ow = (int)(r % Wo); r /= Wo;
+  const int oh = (int)(r % Ho); r /= Ho;
+  const int p = (int)(r % P);
+  const int n = (int)(r / P);
+  const bf16_t* xp = x + (int64_t)n * x_img + (int64_t)p * H * W * 16 + hf * 8;
+  float best[8];
+  int code[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) { best[c] = -INFINITY; code[c] = 0; }
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int h = 2 * oh - 1 + kh;
+    if (h < 0 || h >= H) continue;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int w = 2 * ow - 1 + kw;
+      if (w < 0 || w >= W) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(xp + ((int64_t)h * W + w) * 16);
+      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float f = bf16_to_f32((bf16_t)((u[c >> 1] >> (16 * (c & 1))) & 0xffff));
+        if (f > best[c]) { best[c] = f; code[c] = kh * 3 + kw; }
+      }
+    }
+  }
+  const int64_t o = (int64_t)n * y_img + (((int64_t)p * Ho + oh) * Wo + ow) * 16 + hf * 8;
+  // the max is one of the inputs: bf16 -> f32 -> bf16 is exact
+  *reinterpret_cast<uint4*>(y + o) = make_uint4(cvt_pk_bf16(best[0], best[1]), cvt_pk_bf16(best[2], best[3]),
+                                                cvt_pk_bf16(best[4], best[5]), cvt_pk_bf16(best[6], best[7]));
+  if (amax) {
+    const int64_t ao = ((((int64_t)n * P + p) * Ho + oh) * Wo + ow) * 16 + hf * 8;
+    uint2 cv;
+    cv.x = code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
+    cv.y = code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24);
+    *reinterpret_cast<uint2*>(amax + ao) = cv;
+  }
+}
+
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restrict__ dy, int64_t dy_img,
+                                                          const uint8_t* __restrict__ amax, int P, int H, int W,
+                                                          int Ho, int Wo, bf16_t* __restrict__ dx, int64_t dx_img,
+                                                          int N) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * P * H * W * 2;
+  if (idx >= total) return;
+  const int hf = (int)(idx & 1);
+  int64_t r = idx >> 1;
+  const int w = (int)(r % W); r /= W;
+  const int h = (int)(r % H); r /= H;
+  const int p = (int)(r % P);
+  const int n = (int)(r / P);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // windows oh with 2 oh - 1 <= h <= 2 oh + 1
+  const int oh0 = h / 2, oh1 = min(Ho - 1, (h + 1) / 2);
+  const int ow0 = w / 2, ow1 = min(Wo - 1, (w + 1) / 2);
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    const int kh = h - (2 * oh - 1);
+    if (kh < 0 || kh > 2) continue;
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int kw = w - (2 * ow - 1);
+      if (kw < 0 || kw > 2) continue;
+      const int want = kh * 3 + kw;
+      const int64_t po = (((int64_t)p * Ho + oh) * Wo + ow) * 16 + hf * 8;
+      const uint4 g = *reinterpret_cast<const uint4*>(dy + (int64_t)n * dy_img + po);
+      const uint2 cv = *reinterpret_cast<const uint2*>(amax + (int64_t)n * P * Ho * Wo * 16 + po);
+      const uint32_t gu[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int cd = ((c < 4 ? cv.x : cv.y) >> (8 * (c & 3))) & 0xff;
+        if (cd == want) acc[c] += bf16_to_f32((bf16_t)((gu[c >> 1] >> (16 * (c & 1))) & 0xffff));
+      }
+    }
+  }
+  const int64_t o = (int64_t)n * dx_img + (((int64_t)p * H + h) * W + w) * 16 + hf * 8;
+  *reinterpret_cast<uint4*>(dx + o) = make_uint4(cvt_pk_bf16(acc[0], acc[1]), cvt_pk_bf16(acc[2], acc[3]),
+                                                 cvt_pk_bf16(acc[4], acc[5]), cvt_pk_bf16(acc[6], acc[7]));
+}
+
+// =====================================================================================
+// weight fragment packing (OIHW bf16 master copy -> per-lane MFMA A fragments)
+// =====================================================================================
+// frag[c][nt][lane][j] = W'[co = nt*16 + (lane&15)][ci][t] for K chunk c, lane group
+// kg = lane>>4: pair = 2c + (kg>>1) = t * P + p, ci = p*16 + (kg&1)*8 + j (0 past 9P).
+// transpose = 1 packs the data-gradient correlation: W'[co'][ci'][t] = W[ci'][co'][8-t].
+struct PackJob {
+  const bf16_t* w;            // OIHW [cout][cin_real][3][3]
+  bf16_t* out;
+  int cin, cout;              // logical (multiples of 16; cin >= cin_real)
+  int cin_real, transpose;
+};
+struct PackDesc {
+  PackJob job[32];
+  int njobs;
+};
+
+__global__ void __launch_bounds__(256) sconv_pack_kernel(PackDesc d) {
+  const PackJob J = d.job[blockIdx.y];
+  const int Ci = J.transpose ? J.cout : J.cin, Co = J.transpose ? J.cin : J.cout;
+  const int P = Ci / 16, NT = Co / 16, NCH = (9 * P + 1) / 2;
+  const int total = NCH * NT * 512;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    const int j = e & 7, lane = (e >> 3) & 63, cn = e >> 9;
+    const int nt = cn % NT, c = cn / NT;
+    const int kg = lane >> 4, pair = 2 * c + (kg >> 1);
+    const int co = nt * 16 + (lane & 15);
+    bf16_t v = 0;
+    if (pair < 9 * P) {
+      const int t = pair / P, p = pair - (pair / P) * P;
+      const int ci = p * 16 + (kg & 1) * 8 + j;
+      if (J.transpose) {
+        if (co < J.cin_real) v = J.w[((int64_t)ci * J.cin_real + co) * 9 + (8 - t)];
+      } else if (ci < J.cin_real) {
+        v = J.w[((int64_t)co * J.cin_real + ci) * 9 + t];
+      }
+    }
+    J.out[e] = v;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+#define SCONV_SHAPES(X)      \
+  X(16, 16, 84, 84, 21, 2)   \
+  X(16, 16, 42, 42, 42, 0)   \
+  X(16, 32, 42, 42, 42, 0)   \
+  X(32, 16, 42, 42, 21, 0)   \
+  X(32, 32, 21, 21, 21, 0)   \
+  X(32, 32, 11, 11, 11, 0)
+
+APEX_EXPORT int apex_sconv_fwd(SconvDesc d, int cin, int cout, int H, int W, int mode, hipStream_t st) {
+  if (d.N <= 0) return 0;
+#define SCONV_FWD_CASE(CI, CO, HH, WW, RR, MM)                                                   \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) {                             \
+    sconv_fwd_kernel<CI, CO, HH, WW, RR, MM><<<dim3((HH + RR - 1) / RR, d.N), 256, 0, st>>>(d); \
+    APEX_CHECK_LAUNCH();                                                                         \
+  }
+  SCONV_SHAPES(SCONV_FWD_CASE)
+#undef SCONV_FWD_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+// wgrad bands (LDS: dY band + x band with halo; 2 workgroups per CU)
+#define SCONV_WG_SHAPES(X)   \
+  X(16, 16, 84, 84, 12, 2)   \
+  X(16, 16, 42, 42, 21, 0)   \
+  X(16, 32, 42, 42, 14, 0)   \
+  X(32, 32, 21, 21, 21, 0)   \
+  X(32, 32, 11, 11, 11, 0)
+
+APEX_EXPORT int apex_sconv_wgrad_bands(int cin, int cout, int H, int W, int mode) {
+#define SCONV_WG_BANDS(CI, CO, HH, WW, RR, MM) \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) return (HH + RR - 1) / RR;
+  SCONV_WG_SHAPES(SCONV_WG_BANDS)
+#undef SCONV_WG_BANDS
+  return 0;
+}
+
+APEX_EXPORT int apex_sconv_wgrad(SconvWgDesc d, int cin, int cout, int H, int W, int mode, int groups,
+                                 hipStream_t st) {
+  if (d.N <= 0 || groups <= 0) return (int)hipErrorInvalidValue;
+#define SCONV_WG_CASE(CI, CO, HH, WW, RR, MM)                                                       \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) {                                \
+    sconv_wgrad_kernel<CI, CO, HH, WW, RR, MM><<<dim3((HH + RR - 1) / RR, groups), 256, 0, st>>>(d); \
+    APEX_CHECK_LAUNCH();                                                                            \
+  }
+  SCONV_WG_SHAPES(SCONV_WG_CASE)
+#undef SCONV_WG_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+APEX_EXPORT int apex_maxpool_fwd(const bf16_t* x, int64_t x_img, int P, int H, int W, bf16_t* y, int64_t y_img,
+                                 uint8_t* amax, int N, hipStream_t st) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int64_t total = (int64_t)N * P * Ho * Wo * 2;
+  maxpool_fwd_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(x, x_img, P, H, W, Ho, Wo, y, y_img, amax, N);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_maxpool_bwd(const bf16_t* dy, int64_t dy_img, const uint8_t* amax, int P, int H, int W,
+                                 bf16_t* dx, int64_t dx_img, int N, hipStream_t st) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const int64_t total = (int64_t)N * P * H * W * 2;
+  maxpool_bwd_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(dy, dy_img, amax, P, H, W, Ho, Wo, dx, dx_img, N);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_sconv_pack(PackDesc d, hipStream_t st) {
+  if (d.njobs <= 0 || d.njobs > 32) return (int)hipErrorInvalidValue;
+  sconv_pack_kernel<<<dim3(8, d.njobs), 256, 0, st>>>(d);
+  APEX_CHECK_LAUNCH();
+}
+
+// packed fragment elements of one conv (for buffer sizing on the host)
+APEX_EXPORT int64_t apex_sconv_frag_elems(int cin, int cout) {
+  const int P = cin / 16, NT = cout / 16, NCH = (9 * P + 1) / 2;
+  return (int64_t)NCH * NT * 512;
+}

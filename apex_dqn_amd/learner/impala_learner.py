@@ -1,0 +1,462 @@
+"""MI355X learner for the IMPALA-deep ResNet dueling Q-net (BASELINE.json config 5).
+
+Same GPU-resident step as ``fused_learner.FusedNatureLearner`` (sample ->
+3-way forward -> fused DDQN head -> backward -> [DP all-reduce] -> clip +
+centered RMSprop -> priority write-back), with the trunk on the small-channel
+conv kernels of ``csrc/impala.hip``:
+
+  per stack s (channels 16 / 32 / 32, input 84 / 42 / 21 px):
+    c0 = conv3x3(x)              (stack 1: straight from the uint8 frame ring)
+    p  = maxpool3x3s2(c0)        (+ argmax codes for the backward)
+    ya = conv(relu(p));  ra = p  + conv(relu(ya))
+    yb = conv(relu(ra)); o  = ra + conv(relu(yb))
+  feat = relu(o_3) (planar, 3872 + 32 zero pad = 3904 per row)
+  h = relu(feat @ Wfc^T + b)   (value | advantage streams, 2 x 256)
+
+Backward per res block: the data gradient is the same correlation kernel with
+transposed + flipped weight fragments and a (producer > 0) mask epilogue, the
+skip gradient added in the same epilogue; weight gradients are image-tiled
+split-K partials finalised in one pass per four convs.
+
+Parameters live in one flat fp32 buffer in the kernels' layouts (conv OIHW,
+fc columns in planar order); ``state_dict()`` converts to the
+``ImpalaDuellingDQN`` module's keys.  Rows [0,B) = S_t and [B,2B) = S_{t+n}
+use the online weights, rows [2B,3B) = S_{t+n} the target weights, switched
+inside each launch.  Reference parity: ``learner.py:29-80`` semantics with the
+defects fixed, exactly as the NatureCNN learner.
+"""
+from __future__ import annotations
+
+import contextlib
+from collections import OrderedDict
+from typing import Dict, List, Optional
+
+import torch
+
+from ..config import ApexConfig
+from ..models.dueling import ImpalaDuellingDQN
+from ..models.flat_params import FlatLayout
+from ..ops.fused_ops import HipBackend, TorchBackend
+from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
+from ..utils.checkpoint import load_checkpoint, save_checkpoint
+
+CH = (16, 32, 32)
+HIDDEN = 256
+FEAT = 2 * 11 * 11 * 16          # 3872
+FEAT_LD = 3904                   # 61 x 64: the fc GEMM's K
+
+
+def _stack_dims():
+    out, cin, hw = [], 4, 84
+    for c in CH:
+        out.append((cin, c, hw, (hw + 1) // 2))
+        cin, hw = c, (hw + 1) // 2
+    return out   # (cin, cout, input hw, pooled hw)
+
+
+def fc_column_perm(device=None) -> torch.Tensor:
+    """torch flatten column j = c*121 + h*11 + w  ->  planar column of (c, h, w)."""
+    c = torch.arange(32).view(32, 1, 1)
+    h = torch.arange(11).view(1, 11, 1)
+    w = torch.arange(11).view(1, 1, 11)
+    k = ((c // 16) * 11 + h) * 176 + w * 16 + (c % 16)
+    return k.reshape(-1).to(device)
+
+
+class FusedImpalaLearner:
+    kind = "impala"
+
+    def __init__(self, cfg: ApexConfig, device, replay, comm=None, backend: Optional[str] = None,
+                 batch_size: Optional[int] = None):
+        self.cfg = cfg
+        self.rt = cfg.Runtime
+        self.device = torch.device(device)
+        self.replay = replay
+        self.comm = comm
+        self.world = comm.world_size if comm is not None else 1
+        self.C = cfg.frame_stack
+        if self.C != 4 or tuple(cfg.env_conf.state_shape[1:]) != (84, 84):
+            raise ValueError("the IMPALA kernels are built for 4 x 84 x 84 inputs")
+        self.A = int(cfg.env_conf.action_dim)
+        self.B = int(batch_size or cfg.Learner.replay_sample_size)
+        if backend is None:
+            backend = "hip" if (self.device.type == "cuda" and self.rt.use_hip_kernels) else "torch"
+        on_gpu = backend == "hip"
+        self.ops = HipBackend(native_conv=True) if on_gpu else TorchBackend(
+            torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+        self.iops = HipImpalaOps() if on_gpu else TorchImpalaOps()
+        self.act_dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        d = self.device
+
+        # ---- flat parameter layout (conv trunk first: the DP fc/heads bucket starts at wfc)
+        self.specs: List[List[ConvSpec]] = []
+        segs = []
+        for s, (cin, cout, hw, php) in enumerate(_stack_dims()):
+            convs = [ConvSpec(f"s{s}c0", max(cin, 16), cout, cin, hw, hw)]
+            for r in range(2):
+                for k in range(2):
+                    convs.append(ConvSpec(f"s{s}r{r}c{k}", cout, cout, cout, php, php))
+            for cs in convs:
+                segs += [(cs.name + ".w", (cs.cout, cs.cin_real, 3, 3)), (cs.name + ".b", (cs.cout,))]
+            self.specs.append(convs)
+        segs += [("wfc", (2 * HIDDEN, FEAT_LD)), ("bfc", (2 * HIDDEN,)), ("wv", (HIDDEN,)), ("bv", (1,)),
+                 ("wa", (self.A, HIDDEN)), ("ba", (self.A,))]
+        self.layout = FlatLayout(segs)
+        n = self.layout.numel
+        self.p32 = torch.zeros(n, dtype=torch.float32, device=d)
+        self.pbf = torch.zeros(n, dtype=self.act_dtype, device=d)
+        self.g32 = torch.zeros(n, dtype=torch.float32, device=d)
+        self.rms_v = torch.zeros(n, dtype=torch.float32, device=d)
+        self.rms_m = torch.zeros(n, dtype=torch.float32, device=d)
+        self.t32 = torch.zeros(n, dtype=torch.float32, device=d)
+        self.tbf = torch.zeros(n, dtype=self.act_dtype, device=d)
+        self.P = self.layout.views(self.p32)
+        self.Pb = self.layout.views(self.pbf)
+        self.G = self.layout.views(self.g32)
+        self.T = self.layout.views(self.t32)
+        self.Tb = self.layout.views(self.tbf)
+        self._perm = fc_column_perm(d)
+        for convs in self.specs:
+            for cs in convs:
+                cs.w, cs.b, cs.wb = self.P[cs.name + ".w"], self.P[cs.name + ".b"], self.Pb[cs.name + ".w"]
+                cs.extra["w_tgt"], cs.extra["b_tgt"] = self.Tb[cs.name + ".w"], self.T[cs.name + ".b"]
+                if on_gpu:
+                    cs.frag = torch.zeros(frag_elems(cs.cin, cs.cout), dtype=torch.bfloat16, device=d)
+                    cs.fragT = torch.zeros(frag_elems(cs.cout, cs.cin), dtype=torch.bfloat16, device=d)
+                    cs.frag_tgt = torch.zeros_like(cs.frag)
+        init = ImpalaDuellingDQN((self.C, 84, 84), self.A, channels=CH, hidden=HIDDEN)
+        self.load_module_state(init.state_dict(), self.P)
+        if comm is not None and comm.world_size > 1:
+            comm.broadcast_flat(self.p32)
+        self.pbf.copy_(self.p32)
+        self.num_q_updates = 0
+        self._alloc(self.B)
+        self.sync_target()
+        self._graphs = None
+        self._side = torch.cuda.Stream(d) if d.type == "cuda" else None
+        self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
+        self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
+        self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
+        self.ratio_buf = torch.zeros(2, 1, dtype=torch.float32, device=d)
+        self.ratio_min = None
+        self._ratio_work = [None, None]
+        self._ratio_k = 0
+        if self.world > 1:
+            self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d)
+            self._init_ratio()
+        ls = cfg.Learner.load_saved_state
+        if ls:
+            self.load(ls)
+
+    # ------------------------------------------------------------- buffers
+    def _alloc(self, B: int) -> None:
+        d, ad = self.device, self.act_dtype
+        N3 = 3 * B
+        self.S = self.replay.alloc_sample_buffers(B)
+        self.slots = torch.zeros(N3, self.C, dtype=torch.int32, device=d)
+        self.S["obs"] = self.slots[:B]
+        self.S["nxt"] = self.slots[B:2 * B]
+        self.fw, self.bw = [], []
+        self.feat = torch.zeros(N3, FEAT_LD, dtype=ad, device=d)     # pad columns stay 0
+        self.dfeat = torch.zeros(B, FEAT_LD, dtype=ad, device=d)
+        for s, (cin, cout, hw, php) in enumerate(_stack_dims()):
+            P = cout // 16
+            t = lambda n, h: torch.zeros(n, P, h, h, 16, dtype=ad, device=d)  # noqa: E731
+            f = dict(c0=t(N3, hw), p=t(N3, php), ya=t(N3, php), ra=t(N3, php), yb=t(N3, php),
+                     amax=torch.zeros(N3, P, php, php, 16, dtype=torch.uint8, device=d))
+            f["o"] = (self.feat[:, :FEAT].view(N3, P, php, php, 16) if s == 2 else t(N3, php))
+            self.fw.append(f)
+            b = dict(d_yb=t(B, php), d_ra=t(B, php), d_ya=t(B, php), d_p=t(B, php), d_c0=t(B, hw))
+            if s < 2:
+                b["d_o"] = t(B, php)    # gradient of this stack's output (the next stack's conv0 dgrad)
+            self.bw.append(b)
+        self.h = torch.zeros(N3, 2 * HIDDEN, dtype=ad, device=d)
+        self.dH = torch.zeros(B, 2 * HIDDEN, dtype=ad, device=d)
+        self.dhead = torch.zeros(B, self.A + 1, dtype=torch.float32, device=d)
+        self.td_abs = torch.zeros(B, dtype=torch.float32, device=d)
+        self.loss_b = torch.zeros(B, dtype=torch.float32, device=d)
+        o0 = self.layout.offsets["wv"]
+        o1 = self.layout.offsets["ba"] + self.A
+        self.g_head_region = self.g32[o0:o1]
+
+    # ------------------------------------------------------ weight packing
+    def _pack_online(self) -> None:
+        jobs = []
+        for convs in self.specs:
+            for i, cs in enumerate(convs):
+                jobs.append((cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, 0))
+                if not (cs.name == "s0c0"):
+                    jobs.append((cs.wb, cs.fragT, cs.cin, cs.cout, cs.cin_real, 1))
+        self.iops.pack(jobs)
+
+    def _pack_target(self) -> None:
+        self.iops.pack([(cs.extra["w_tgt"], cs.frag_tgt, cs.cin, cs.cout, cs.cin_real, 0)
+                        for convs in self.specs for cs in convs])
+
+    # ------------------------------------------------------------ forward
+    def forward_all(self) -> None:
+        """Online net on rows [0,2B), target net on rows [2B,3B)."""
+        io, B, rt = self.iops, self.B, self.rt
+        x = None
+        for s, convs in enumerate(self.specs):
+            f = self.fw[s]
+            c0, r0a, r0b, r1a, r1b = convs
+            tg = lambda cs: dict(second=cs.extra["b_tgt"], n_switch=2 * B)  # noqa: E731
+            if s == 0:
+                io.conv(None, c0, f["c0"], ring=self.replay.frames, slots=self.slots, scale=rt.obs_scale, **tg(c0))
+            else:
+                io.conv(x, c0, f["c0"], **tg(c0))
+            io.maxpool(f["c0"], f["p"], f["amax"])
+            io.conv(f["p"], r0a, f["ya"], relu_in=True, **tg(r0a))
+            io.conv(f["ya"], r0b, f["ra"], relu_in=True, add=f["p"], **tg(r0b))
+            io.conv(f["ra"], r1a, f["yb"], relu_in=True, **tg(r1a))
+            io.conv(f["yb"], r1b, f["o"], relu_in=True, add=f["ra"], relu_out=(s == 2), **tg(r1b))
+            x = f["o"]
+        self.ops.fc_fwd(self.feat, self.Pb["wfc"], self.P["bfc"], self.h, self.Tb["wfc"], self.T["bfc"], 2 * B)
+
+    def _head_params(self, V):
+        return {k: V[k] for k in ("wv", "bv", "wa", "ba")}
+
+    # ---------------------------------------------------------------- step
+    def _seg1(self) -> None:
+        B, rt, ops = self.B, self.rt, self.ops
+        self._pack_online()
+        S = self.replay.sample(B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * B:])
+        self.forward_all()
+        isw = S["weights"] if rt.use_is_weights else None
+        ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
+                 S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
+                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
+        with self._on_side():
+            ops.head_wgrad(self.h, self.dhead, self.G)
+            self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
+        ops.fc_wgrad(self.dH, self.feat[:B], self.G["wfc"], self.G["bfc"])
+        self._join_side()
+
+    def _seg2(self) -> None:
+        """fc data gradient, then the three stacks backwards."""
+        B, io, G = self.B, self.iops, self.G
+        self.ops.fc_dgrad(self.dH, self.feat[:B], self.Pb["wfc"], self.dfeat)
+        jobs: list = []
+        dO = self.dfeat[:, :FEAT].view(B, 2, 11, 11, 16)
+        for s in (2, 1, 0):
+            f, b = self.fw[s], self.bw[s]
+            c0, r0a, r0b, r1a, r1b = self.specs[s]
+            gw = lambda cs: (G[cs.name + ".w"], G[cs.name + ".b"])  # noqa: E731
+            io.conv(dO, r1b, b["d_yb"], transpose=True, mask=f["yb"][:B])
+            io.wgrad(dO, f["yb"][:B], r1b, *gw(r1b), jobs, relu_in=True)
+            io.conv(b["d_yb"], r1a, b["d_ra"], transpose=True, mask=f["ra"][:B], add=dO)
+            io.wgrad(b["d_yb"], f["ra"][:B], r1a, *gw(r1a), jobs, relu_in=True)
+            io.conv(b["d_ra"], r0b, b["d_ya"], transpose=True, mask=f["ya"][:B])
+            io.wgrad(b["d_ra"], f["ya"][:B], r0b, *gw(r0b), jobs, relu_in=True)
+            io.conv(b["d_ya"], r0a, b["d_p"], transpose=True, mask=f["p"][:B], add=b["d_ra"])
+            io.wgrad(b["d_ya"], f["p"][:B], r0a, *gw(r0a), jobs, relu_in=True)
+            io.maxpool_bwd(b["d_p"], f["amax"][:B], b["d_c0"])
+            if s == 0:
+                io.wgrad(b["d_c0"], None, c0, *gw(c0), jobs, ring=self.replay.frames, slots=self.slots[:B],
+                         scale=self.rt.obs_scale)
+            else:
+                prev = self.fw[s - 1]["o"][:B]
+                io.wgrad(b["d_c0"], prev, c0, *gw(c0), jobs)
+                dO = self.bw[s - 1]["d_o"]
+                io.conv(b["d_c0"], c0, dO, transpose=True)
+        io.finalize(jobs)
+
+    def _seg3(self) -> None:
+        rt, ops = self.rt, self.ops
+        ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
+                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
+        if self.world > 1:
+            rp = self.replay
+            tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float()
+            self.ratio_local.copy_(rp.min_bits.view(torch.float32) / tot)
+
+    def _step_body(self) -> None:
+        self._seg1()
+        self._seg2()
+        self._seg3()
+
+    def _on_side(self):
+        if self._side is None:
+            return contextlib.nullcontext()
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        return torch.cuda.stream(self._side)
+
+    def _join_side(self) -> None:
+        if self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+
+    def _dp_step(self, graphs: bool) -> None:
+        import torch.distributed as dist
+        cut = self.layout.offsets["wfc"]
+        run = (lambda i: self._graphs[i].replay()) if graphs else (lambda i: (self._seg1, self._seg2,
+                                                                                self._seg3)[i]())
+        k = self._ratio_k
+        if self._ratio_work[k] is not None:   # normaliser of step t-2 (see fused_learner._dp_step)
+            self._ratio_work[k].wait()
+            self.ratio_min.copy_(self.ratio_buf[k])
+            self._ratio_work[k] = None
+        run(0)
+        w_fc = dist.all_reduce(self.g32[cut:], op=dist.ReduceOp.SUM, async_op=True)
+        run(1)
+        w_cv = dist.all_reduce(self.g32[:cut], op=dist.ReduceOp.SUM, async_op=True)
+        w_fc.wait()
+        w_cv.wait()
+        run(2)
+        self.ratio_buf[k].copy_(self.ratio_local)
+        self._ratio_work[k] = dist.all_reduce(self.ratio_buf[k], op=dist.ReduceOp.MIN, async_op=True)
+        self._ratio_k = 1 - k
+
+    def step(self) -> None:
+        graphs = self.rt.use_graphs and self.device.type == "cuda"
+        if graphs and self._graphs is None:
+            self._capture()
+        if self.world > 1:
+            self._dp_step(graphs)
+        elif graphs:
+            self._graphs[0].replay()
+        else:
+            self._step_body()
+        self.num_q_updates += 1
+        if self.num_q_updates % self.cfg.Learner.q_target_sync_freq == 0:
+            self.sync_target()
+
+    def _capture(self) -> None:
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        snap = self._snapshot()
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._step_body()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._restore(snap)
+        torch.cuda.synchronize(self.device)
+        segs = [self._step_body] if self.world == 1 else [self._seg1, self._seg2, self._seg3]
+        self._graphs = []
+        for seg in segs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                seg()
+            self._graphs.append(g)
+
+    def _snapshot(self):
+        rp = self.replay
+        return [t.clone() for t in (self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes,
+                                    rp.min_bits, rp.ctr)]
+
+    def _restore(self, snap) -> None:
+        rp = self.replay
+        for dst, src in zip((self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes, rp.min_bits,
+                             rp.ctr), snap):
+            dst.copy_(src)
+
+    def _init_ratio(self) -> None:
+        import torch.distributed as dist
+        rp = self.replay
+        tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float().clamp_min(1e-30)
+        buf = self.ratio_buf[0]
+        buf.copy_(rp.min_bits.view(torch.float32) / tot)
+        dist.all_reduce(buf, op=dist.ReduceOp.MIN)
+        self.ratio_min.copy_(buf)
+
+    def refresh_replay_stats(self) -> None:
+        if self.world > 1:
+            for i, w in enumerate(self._ratio_work):
+                if w is not None:
+                    w.wait()
+                    self._ratio_work[i] = None
+            self._init_ratio()
+
+    def sync_target(self) -> None:
+        self.t32.copy_(self.p32)
+        self.tbf.copy_(self.pbf)
+        self._pack_target()
+
+    # ------------------------------------------------------------ metrics
+    def last_metrics(self) -> Dict[str, float]:
+        return {"loss": float(self.loss_b.mean()), "td_abs_mean": float(self.td_abs.mean()),
+                "grad_norm": float(self.gnorm[0])}
+
+    def profile_step(self) -> Dict[str, float]:
+        if self.device.type != "cuda":
+            return {}
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        self.step()
+        e1.record()
+        torch.cuda.synchronize(self.device)
+        return {"total": e0.elapsed_time(e1)}
+
+    # ------------------------------------------------------------- params
+    def module_state(self, V: Optional[Dict[str, torch.Tensor]] = None) -> "OrderedDict[str, torch.Tensor]":
+        """Engine layout -> ``ImpalaDuellingDQN.state_dict()`` (fp32, CPU)."""
+        V = self.P if V is None else V
+        sd = OrderedDict()
+        for s, convs in enumerate(self.specs):
+            names = ["conv", "res0.conv0", "res0.conv1", "res1.conv0", "res1.conv1"]
+            for nm, cs in zip(names, convs):
+                sd[f"stacks.{s}.{nm}.weight"] = V[cs.name + ".w"]
+                sd[f"stacks.{s}.{nm}.bias"] = V[cs.name + ".b"]
+        wfc = V["wfc"][:, self._perm]
+        sd["value_stream_layer.0.weight"] = wfc[:HIDDEN]
+        sd["value_stream_layer.0.bias"] = V["bfc"][:HIDDEN]
+        sd["advantage_stream_layer.0.weight"] = wfc[HIDDEN:]
+        sd["advantage_stream_layer.0.bias"] = V["bfc"][HIDDEN:]
+        sd["value.weight"] = V["wv"].view(1, HIDDEN)
+        sd["value.bias"] = V["bv"]
+        sd["advantage.weight"] = V["wa"]
+        sd["advantage.bias"] = V["ba"]
+        return OrderedDict((k, t.detach().float().cpu().clone()) for k, t in sd.items())
+
+    def load_module_state(self, sd, V: Optional[Dict[str, torch.Tensor]] = None) -> None:
+        V = self.P if V is None else V
+        with torch.no_grad():
+            for s, convs in enumerate(self.specs):
+                names = ["conv", "res0.conv0", "res0.conv1", "res1.conv0", "res1.conv1"]
+                for nm, cs in zip(names, convs):
+                    V[cs.name + ".w"].copy_(sd[f"stacks.{s}.{nm}.weight"])
+                    V[cs.name + ".b"].copy_(sd[f"stacks.{s}.{nm}.bias"])
+            wfc = torch.zeros_like(V["wfc"])
+            perm = self._perm.to(wfc.device)
+            wfc[:HIDDEN, perm] = sd["value_stream_layer.0.weight"].to(wfc)
+            wfc[HIDDEN:, perm] = sd["advantage_stream_layer.0.weight"].to(wfc)
+            V["wfc"].copy_(wfc)
+            V["bfc"][:HIDDEN].copy_(sd["value_stream_layer.0.bias"])
+            V["bfc"][HIDDEN:].copy_(sd["advantage_stream_layer.0.bias"])
+            V["wv"].copy_(sd["value.weight"].reshape(HIDDEN))
+            V["bv"].copy_(sd["value.bias"])
+            V["wa"].copy_(sd["advantage.weight"])
+            V["ba"].copy_(sd["advantage.bias"])
+
+    def state_dict(self):
+        return self.module_state()
+
+    def q_values(self, frames_u8: torch.Tensor) -> torch.Tensor:
+        net = ImpalaDuellingDQN((self.C, 84, 84), self.A, channels=CH, hidden=HIDDEN).to(self.device)
+        net.load_state_dict(self.module_state())
+        with torch.no_grad():
+            return net(frames_u8.to(self.device))[2]
+
+    def save(self, path: str) -> None:
+        save_checkpoint(path, self.module_state(), Q_target_state=self.module_state(self.T),
+                        optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
+                        num_q_updates=self.num_q_updates, config=self.cfg.to_dict())
+
+    def load(self, path: str) -> bool:
+        ck = load_checkpoint(path)
+        if ck is None:
+            return False
+        self.load_module_state(ck["Q_state"])
+        self.pbf.copy_(self.p32)
+        if "Q_target_state" in ck:
+            self.load_module_state(ck["Q_target_state"], self.T)
+            self.tbf.copy_(self.t32)
+            self._pack_target()
+        else:
+            self.sync_target()
+        opt = ck.get("optimizer_state")
+        if isinstance(opt, dict) and "rms_v" in opt:
+            self.rms_v.copy_(opt["rms_v"])
+            self.rms_m.copy_(opt["rms_m"])
+        self.num_q_updates = int(ck.get("num_q_updates", 0))
+        return True

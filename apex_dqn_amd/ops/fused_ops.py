@@ -68,9 +68,11 @@ class TorchBackend:
         Hon = Hon.float()
         Htg = Htg.float()
 
+        HS = Pon["wv"].numel()   # stream width (512 NatureCNN, 256 IMPALA)
+
         def q_of(h, P):
-            v = h[:, :512] @ P["wv"].float() + P["bv"].float()
-            a = h[:, 512:] @ P["wa"].float().t() + P["ba"].float()
+            v = h[:, :HS] @ P["wv"].float() + P["bv"].float()
+            a = h[:, HS:] @ P["wa"].float().t() + P["ba"].float()
             return v[:, None] + a - a.mean(1, keepdim=True)
 
         q_t = q_of(Hon[:B], Pon)
@@ -106,17 +108,19 @@ class TorchBackend:
 
     def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor]):
         B = dhead.shape[0]
+        HS = g["wv"].numel()
         h = Hon[:B].float()
-        g["wv"].add_(dhead[:, 0] @ h[:, :512])
+        g["wv"].add_(dhead[:, 0] @ h[:, :HS])
         g["bv"].add_(dhead[:, 0].sum().view(1))
-        g["wa"].add_(dhead[:, 1:].t() @ h[:, 512:])
+        g["wa"].add_(dhead[:, 1:].t() @ h[:, HS:])
         g["ba"].add_(dhead[:, 1:].sum(0))
 
     def actor_head(self, H, P, eps, ctr, seed, q_out, a_out):
         """Dueling q + epsilon-greedy per row (the oracle of csrc actor_head_kernel)."""
         h = H.float()
-        v = h[:, :512] @ P["wv"].float() + P["bv"].float()
-        a = h[:, 512:] @ P["wa"].float().t() + P["ba"].float()
+        HS = P["wv"].numel()
+        v = h[:, :HS] @ P["wv"].float() + P["bv"].float()
+        a = h[:, HS:] @ P["wa"].float().t() + P["ba"].float()
         q = v[:, None] + a - a.mean(1, keepdim=True)
         q_out.copy_(q)
         E, A = q.shape
@@ -268,19 +272,19 @@ class HipBackend(TorchBackend):
             Hon.data_ptr(), Htg.data_ptr(), self._hp(Pon), self._hp(Ptg), act.data_ptr(), rew.data_ptr(),
             gam.data_ptr(), _lib.ptr(isw), B, A, int(huber), float(kappa), float(grad_scale),
             td_abs.data_ptr(), loss.data_ptr(), _lib.ptr(q_out), dH.data_ptr(), dhead.data_ptr(),
-            _lib.ptr(zero), 0 if zero is None else zero.numel(), _lib.stream_ptr()), "ddqn_head")
+            _lib.ptr(zero), 0 if zero is None else zero.numel(), Pon["wv"].numel(), _lib.stream_ptr()), "ddqn_head")
 
     def head_wgrad(self, Hon, dhead, g):
         B, A1 = dhead.shape
         _lib.check(self.lib.apex_head_wgrad(Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(),
                                             g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(),
-                                            _lib.stream_ptr()), "head_wgrad")
+                                            g["wv"].numel(), _lib.stream_ptr()), "head_wgrad")
 
     def actor_head(self, H, P, eps, ctr, seed, q_out, a_out):
         E, A = q_out.shape
         _lib.check(self.lib.apex_actor_head(H.data_ptr(), self._hp(P), E, A, eps.data_ptr(), int(seed),
                                             ctr.data_ptr(), q_out.data_ptr(), a_out.data_ptr(),
-                                            _lib.stream_ptr()), "actor_head")
+                                            P["wv"].numel(), _lib.stream_ptr()), "actor_head")
 
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None):
         n = p32.numel()

@@ -1,0 +1,309 @@
+"""IMPALA-deep ResNet ops: HIP launchers (csrc/impala.hip) and the torch oracle.
+
+Activations are "planar-16" bf16 tensors: per image C/16 planes of [H][W][16]
+(shape ``(N, C/16, H, W, 16)``; the image stride may exceed the dense size, e.g.
+the FC input rows of 3904 = 2*11*11*16 + 32 zero pad elements).  Conv weights
+are OIHW ``(cout, cin_real, 3, 3)`` -- the torch ``nn.Conv2d`` layout -- and the
+HIP kernels read them as packed MFMA fragments (``pack``), re-packed from the
+bf16 master copy every step (online) or at target sync (target).
+
+``HipImpalaOps`` and ``TorchImpalaOps`` have the same methods; the torch one is
+the CPU path and the numerics oracle of every kernel (tests/test_impala.py).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+c_p, c_i, c_i64, c_f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+
+
+class SconvDesc(ctypes.Structure):
+    _fields_ = [("x", c_p), ("slots", c_p), ("wf", c_p), ("wf2", c_p), ("bias", c_p), ("bias2", c_p),
+                ("add", c_p), ("mask", c_p), ("y", c_p), ("x_img", c_i64), ("y_img", c_i64),
+                ("add_img", c_i64), ("mask_img", c_i64), ("N", c_i), ("n_switch", c_i),
+                ("relu_in", c_i), ("relu_out", c_i), ("scale", c_f), ("pad0", c_i)]
+
+
+class SconvWgDesc(ctypes.Structure):
+    _fields_ = [("dy", c_p), ("x", c_p), ("slots", c_p), ("slab", c_p), ("bslab", c_p),
+                ("dy_img", c_i64), ("x_img", c_i64), ("N", c_i), ("relu_in", c_i),
+                ("imgs_per_group", c_i), ("cin_real", c_i)]
+
+
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", c_p), ("out", c_p), ("cin", c_i), ("cout", c_i), ("cin_real", c_i), ("transpose", c_i)]
+
+
+class PackDesc(ctypes.Structure):
+    _fields_ = [("job", PackJob * 32), ("njobs", c_i)]
+
+
+_SIGS = {
+    "apex_sconv_fwd": ([SconvDesc, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_sconv_wgrad": ([SconvWgDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_sconv_wgrad_bands": ([c_i, c_i, c_i, c_i, c_i], c_i),
+    "apex_maxpool_fwd": ([c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_p], c_i),
+    "apex_maxpool_bwd": ([c_p, c_i64, c_p, c_i, c_i, c_i, c_p, c_i64, c_i, c_p], c_i),
+    "apex_sconv_pack": ([PackDesc, c_p], c_i),
+    "apex_sconv_frag_elems": ([c_i, c_i], c_i64),
+}
+
+
+def declare(lib: ctypes.CDLL) -> None:
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is not None:
+            fn.argtypes, fn.restype = args, res
+
+
+# ----------------------------------------------------------------- layouts
+def to_planar(x: torch.Tensor) -> torch.Tensor:
+    """(N, C, H, W) -> (N, C/16, H, W, 16)."""
+    N, C, H, W = x.shape
+    return x.reshape(N, C // 16, 16, H, W).permute(0, 1, 3, 4, 2).contiguous()
+
+
+def from_planar(x: torch.Tensor) -> torch.Tensor:
+    """(N, P, H, W, 16) -> (N, 16 P, H, W)."""
+    N, P, H, W, _ = x.shape
+    return x.permute(0, 1, 4, 2, 3).reshape(N, P * 16, H, W)
+
+
+def frag_elems(cin: int, cout: int) -> int:
+    P, NT = cin // 16, cout // 16
+    return ((9 * P + 1) // 2) * NT * 512
+
+
+def img_stride(t: torch.Tensor) -> int:
+    return int(t.stride(0))
+
+
+@dataclass
+class ConvSpec:
+    """One 3x3 / pad 1 conv of the trunk: logical channels (multiples of 16;
+    ``cin_real`` < ``cin`` for the 4-frame input), master views and fragments."""
+    name: str
+    cin: int
+    cout: int
+    cin_real: int
+    H: int
+    W: int
+    w: torch.Tensor = None          # fp32 master (view of the flat params)
+    b: torch.Tensor = None
+    wb: torch.Tensor = None         # bf16 compute copy (view)
+    frag: torch.Tensor = None       # forward fragments (online)
+    fragT: torch.Tensor = None      # data-gradient fragments (online)
+    frag_tgt: torch.Tensor = None   # forward fragments (target)
+    extra: Dict = field(default_factory=dict)
+
+
+# ------------------------------------------------------------------ HIP backend
+class HipImpalaOps:
+    name = "hip"
+
+    def __init__(self):
+        self.lib = _lib.require_kernels()
+        declare(self.lib)
+        self.ws: Dict = {}
+
+    def _buf(self, key, n, device, dtype=torch.float32):
+        t = self.ws.get(key)
+        if t is None or t.numel() < n:
+            t = torch.empty(n, dtype=dtype, device=device)
+            self.ws[key] = t
+        return t
+
+    # -- weights
+    def pack(self, jobs: List[tuple]) -> None:
+        """jobs: (w_bf16_oihw, out, cin, cout, cin_real, transpose)."""
+        for s in range(0, len(jobs), 32):
+            d = PackDesc()
+            chunk = jobs[s:s + 32]
+            for i, (w, out, cin, cout, cin_real, tr) in enumerate(chunk):
+                J = d.job[i]
+                J.w, J.out, J.cin, J.cout, J.cin_real, J.transpose = w.data_ptr(), out.data_ptr(), cin, cout, \
+                    cin_real, int(tr)
+            d.njobs = len(chunk)
+            _lib.check(self.lib.apex_sconv_pack(d, _lib.stream_ptr()), "sconv_pack")
+
+    # -- convs
+    def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
+             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None) -> None:
+        """y = epi(corr3x3(x', W')): W' = W (forward) or transposed + flipped (data
+        gradient); x' = relu(x) if relu_in; epi = *scale + bias, * (mask > 0), + add, relu."""
+        d = SconvDesc()
+        N = y.shape[0]
+        if ring is not None:
+            d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
+            mode = 2
+            assert slots.shape == (N, 4) and slots.dtype == torch.int32 and spec.cin == 16
+        else:
+            assert x.shape[0] == N
+            d.x, d.x_img = x.data_ptr(), img_stride(x)
+            mode = 0
+        d.wf = (spec.fragT if transpose else spec.frag).data_ptr()
+        if second is not None:
+            d.wf2 = spec.frag_tgt.data_ptr()
+            d.bias2 = second.data_ptr() if bias else None
+            d.n_switch = int(n_switch)
+        d.bias = spec.b.data_ptr() if (bias and not transpose) else None
+        if transpose:
+            d.bias2 = None
+        d.add, d.add_img = _lib.ptr(add), (img_stride(add) if add is not None else 0)
+        d.mask, d.mask_img = _lib.ptr(mask), (img_stride(mask) if mask is not None else 0)
+        d.y, d.y_img = y.data_ptr(), img_stride(y)
+        d.N, d.relu_in, d.relu_out, d.scale = N, int(relu_in), int(relu_out), float(scale)
+        cin, cout = (spec.cout, spec.cin) if transpose else (spec.cin, spec.cout)
+        _lib.check(self.lib.apex_sconv_fwd(d, cin, cout, spec.H, spec.W, mode, _lib.stream_ptr()),
+                   f"sconv_fwd[{spec.name}{'^T' if transpose else ''}]")
+
+    def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
+              groups: int = 0, scale: float = 1.0) -> None:
+        """gw = scale * sum dy (x) im2col(x') (x' = relu(x) if relu_in), gb = sum dy:
+        partials now, reduced by ``finalize(jobs)``."""
+        N = dy.shape[0]
+        mode = 2 if ring is not None else 0
+        bands = self.lib.apex_sconv_wgrad_bands(spec.cin, spec.cout, spec.H, spec.W, mode)
+        if bands <= 0:
+            raise ValueError(f"no wgrad kernel for {spec}")
+        n = spec.cout * spec.cin_real * 9
+        G = groups or max(1, min(N, 512 // bands))
+        while not groups and G > 32 and bands * G * n > (2 << 20):   # keep each slab <= 8 MB
+            G //= 2
+        ipg = (N + G - 1) // G
+        G = (N + ipg - 1) // ipg
+        nsplit = bands * G
+        slab = self._buf(("slab", spec.name), nsplit * n, dy.device)
+        bslab = self._buf(("bslab", spec.name), nsplit * spec.cout, dy.device)
+        d = SconvWgDesc()
+        d.dy, d.dy_img = dy.data_ptr(), img_stride(dy)
+        if ring is not None:
+            d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
+        else:
+            d.x, d.x_img = x.data_ptr(), img_stride(x)
+        d.slab, d.bslab = slab.data_ptr(), bslab.data_ptr()
+        d.N, d.relu_in, d.imgs_per_group, d.cin_real = N, int(relu_in), ipg, spec.cin_real
+        _lib.check(self.lib.apex_sconv_wgrad(d, spec.cin, spec.cout, spec.H, spec.W, mode, G, _lib.stream_ptr()),
+                   f"sconv_wgrad[{spec.name}]")
+        jobs.append(dict(slab=slab, bslab=bslab, out=gw, bout=gb, n=n, nsplit=nsplit, nb=spec.cout, s2dC=0, Kc=4,
+                         scale=float(scale)))
+
+    def finalize(self, jobs: list) -> None:
+        from . import conv as C
+        for s in range(0, len(jobs), 4):
+            C.finalize_grads(self.lib, jobs[s:s + 4])
+
+    # -- pooling
+    def maxpool(self, x, y, amax) -> None:
+        N, P, H, W, _ = x.shape
+        _lib.check(self.lib.apex_maxpool_fwd(x.data_ptr(), img_stride(x), P, H, W, y.data_ptr(), img_stride(y),
+                                             _lib.ptr(amax), N, _lib.stream_ptr()), "maxpool_fwd")
+
+    def maxpool_bwd(self, dy, amax, dx) -> None:
+        N, P, H, W, _ = dx.shape
+        _lib.check(self.lib.apex_maxpool_bwd(dy.data_ptr(), img_stride(dy), amax.data_ptr(), P, H, W, dx.data_ptr(),
+                                             img_stride(dx), N, _lib.stream_ptr()), "maxpool_bwd")
+
+
+# ---------------------------------------------------------------- torch oracle
+def ring_frames(ring: torch.Tensor, slots: torch.Tensor) -> torch.Tensor:
+    """(N, 4) slots into the space-to-depth ring -> (N, 4, 84, 84) uint8 frames."""
+    from ..replay.gpu_replay import from_s2d
+    raw = ring[slots.long().reshape(-1)]
+    return from_s2d(raw.reshape(-1, 84, 84)).reshape(slots.shape[0], slots.shape[1], 84, 84)
+
+
+class TorchImpalaOps:
+    """Same contract, plain torch (fp32 math, results cast to the output dtype)."""
+    name = "torch"
+
+    def pack(self, jobs) -> None:
+        pass
+
+    @staticmethod
+    def _w(spec: ConvSpec, transpose: bool, second: bool) -> torch.Tensor:
+        w = (spec.extra["w_tgt"] if second else spec.wb).float()
+        if spec.cin_real < spec.cin:
+            w = F.pad(w, (0, 0, 0, 0, 0, spec.cin - spec.cin_real))
+        if transpose:
+            w = w.transpose(0, 1).flip(2, 3)
+        return w
+
+    def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
+             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None) -> None:
+        N = y.shape[0]
+        if ring is not None:
+            xin = F.pad(ring_frames(ring, slots).float(), (0, 0, 0, 0, 0, 12))
+        else:
+            xin = from_planar(x.float())
+        if relu_in:
+            xin = xin.clamp_min(0)
+        outs = []
+        for lo, hi, sec in ((0, n_switch if second is not None else N, False), (n_switch, N, True)):
+            if hi <= lo or (sec and second is None):
+                continue
+            w = self._w(spec, transpose, sec)
+            b = None
+            if bias and not transpose:
+                b = (second if sec else spec.b).float()
+            o = F.conv2d(xin[lo:hi], w, None, padding=1) * scale
+            if b is not None:
+                o = o + b[None, :, None, None]
+            outs.append(o)
+        o = to_planar(torch.cat(outs))
+        if mask is not None:
+            o = o * (mask.float() > 0)
+        if add is not None:
+            o = o + add.float()
+        if relu_out:
+            o = o.clamp_min(0)
+        y.copy_(o.to(y.dtype))
+
+    def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
+              groups: int = 0, scale: float = 1.0) -> None:
+        if ring is not None:
+            xin = ring_frames(ring, slots).float()
+        else:
+            xin = from_planar(x.float())[:, :spec.cin_real]
+        if relu_in:
+            xin = xin.clamp_min(0)
+        g = from_planar(dy.float())
+        gw.copy_(torch.nn.grad.conv2d_weight(xin, gw.shape, g, padding=1) * scale)
+        gb.copy_(g.sum((0, 2, 3)))
+
+    def finalize(self, jobs) -> None:
+        pass
+
+    def maxpool(self, x, y, amax) -> None:
+        xn = from_planar(x.float())
+        o, idx = F.max_pool2d(xn, 3, 2, 1, return_indices=True)
+        y.copy_(to_planar(o).to(y.dtype))
+        if amax is not None:
+            H, W = xn.shape[2:]
+            Ho, Wo = o.shape[2:]
+            ih, iw = idx // W, idx % W
+            oh = torch.arange(Ho, device=x.device)[:, None]
+            ow = torch.arange(Wo, device=x.device)[None, :]
+            code = (ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1))
+            amax.copy_(to_planar(code).to(torch.uint8))
+
+    def maxpool_bwd(self, dy, amax, dx) -> None:
+        N, P, H, W, _ = dx.shape
+        g = from_planar(dy.float())
+        code = from_planar(amax.long())
+        Ho, Wo = g.shape[2:]
+        oh = torch.arange(Ho, device=dy.device)[:, None]
+        ow = torch.arange(Wo, device=dy.device)[None, :]
+        ih = 2 * oh - 1 + code // 3
+        iw = 2 * ow - 1 + code % 3
+        flat = (ih * W + iw).reshape(N, P * 16, -1)
+        out = torch.zeros(N, P * 16, H * W, dtype=torch.float32, device=dy.device)
+        out.scatter_add_(2, flat, g.reshape(N, P * 16, -1))
+        dx.copy_(to_planar(out.reshape(N, P * 16, H, W)).to(dx.dtype))

@@ -41,8 +41,10 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--graph-impala", action="store_true",
+                    help="IMPALA on the torch-autograd graph learner (MIOpen) instead of the HIP kernels")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
-                    help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala uses the graph learner")
+                    help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala.hip")
     args = ap.parse_args()
 
     from apex_dqn_amd.config import ApexConfig
@@ -91,6 +93,9 @@ def main():
     replay.rebuild()
     if args.network in ("nature64", "nature32"):
         learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
+    elif args.network == "impala" and not args.graph_impala:
+        from apex_dqn_amd.learner.impala_learner import FusedImpalaLearner
+        learner = FusedImpalaLearner(cfg, device, replay, comm=comm, backend=args.backend)
     else:
         from apex_dqn_amd.learner.graph_learner import GraphLearner
         learner = GraphLearner(cfg, device, replay, comm=comm)
