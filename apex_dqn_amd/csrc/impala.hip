@@ -44,7 +44,8 @@ struct SconvDesc {
   const float* bias2;
   const bf16_t* add;          // added after the mask (output layout), or null
   const bf16_t* mask;         // output multiplied by (mask > 0) (output layout), or null
-  bf16_t* y;                  // bf16 planar output
+  bf16_t* y;                  // bf16 planar output (pooled output when POOL)
+  void* mask_out;             // POOL: uint8 argmax codes [N][planes][Ho][Wo][16], or null
   int64_t x_img, y_img;       // image strides (elements)
   int64_t add_img, mask_img;
   int N, n_switch;
@@ -68,69 +69,105 @@ __device__ __forceinline__ uint4 relu_u4(uint4 v) {
   return make_uint4(relu_pk16(v.x), relu_pk16(v.y), relu_pk16(v.z), relu_pk16(v.w));
 }
 
-// Stage input rows [r0 - 1, r0 + R] x cols [-1, W] of image n (zero outside the
-// image) into P LDS planes of `plane_pix` 32-byte pixel rows; pixels past the
-// (R+2) x (W+2) block up to plane_pix are zeroed (M-tile overrun reads).
+// Stage SROWS input rows starting at global row `row0` (x cols [-1, W]; zero
+// outside the image) into P LDS planes of `plane_pix` 32-byte pixel rows; pixels
+// past the SROWS x (W+2) block up to plane_pix are zeroed (M-tile overrun reads).
 // MODE 0: planar bf16; MODE 2: 4 uint8 frames from the space-to-depth ring
 // (csrc/conv1_s2d.hip layout) as channels 0..3 of a 16-channel plane.
-template <int P, int H, int W, int R, int MODE>
+// Loads are issued in batches of BATCH per thread before any LDS store, so each
+// thread has BATCH global loads in flight instead of one load-use round trip.
+template <int P, int H, int W, int SROWS, int MODE, int NTHR, int BATCH>
 __device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const void* x, int64_t x_img,
-                                           const int32_t* slots, int n, int r0, int relu, int tid, int nthr) {
-  constexpr int WP = W + 2, ROWS = R + 2, BLK = ROWS * WP;
+                                           const int32_t* slots, int n, int row0, int relu, int tid) {
+  constexpr int WP = W + 2, BLK = SROWS * WP;
   if constexpr (MODE == 2) {
     const uint8_t* ring = reinterpret_cast<const uint8_t*>(x);
     const int32_t* sl = slots + (int64_t)n * 4;
     const int64_t f0 = (int64_t)sl[0] * 7056, f1 = (int64_t)sl[1] * 7056;
     const int64_t f2 = (int64_t)sl[2] * 7056, f3 = (int64_t)sl[3] * 7056;
-    for (int i = tid; i < BLK; i += nthr) {
-      const int lr = i / WP, c = i - lr * WP;
-      const int h = r0 - 1 + lr, w = c - 1;
-      uint4 lo = make_uint4(0, 0, 0, 0);
-      if (h >= 0 && h < H && w >= 0 && w < W) {
-        const int o = ((h >> 2) * 21 + (w >> 2)) * 16 + (h & 3) * 4 + (w & 3);
-        lo.x = cvt_pk_bf16((float)ring[f0 + o], (float)ring[f1 + o]);
-        lo.y = cvt_pk_bf16((float)ring[f2 + o], (float)ring[f3 + o]);
+    for (int base = 0; base < BLK; base += NTHR * BATCH) {
+      uint32_t b[BATCH][4];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int i = base + k * NTHR + tid;
+        const int lr = i / WP, c = i - (i / WP) * WP;
+        const int h = row0 + lr, w = c - 1;
+        b[k][0] = b[k][1] = b[k][2] = b[k][3] = 0;
+        if (i < BLK && h >= 0 && h < H && w >= 0 && w < W) {
+          const int o = ((h >> 2) * 21 + (w >> 2)) * 16 + (h & 3) * 4 + (w & 3);
+          b[k][0] = ring[f0 + o]; b[k][1] = ring[f1 + o]; b[k][2] = ring[f2 + o]; b[k][3] = ring[f3 + o];
+        }
       }
-      *reinterpret_cast<uint4*>(xs + i * 32) = lo;
-      *reinterpret_cast<uint4*>(xs + i * 32 + 16) = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int i = base + k * NTHR + tid;
+        if (i < BLK) {
+          const uint4 lo = make_uint4(cvt_pk_bf16((float)b[k][0], (float)b[k][1]),
+                                      cvt_pk_bf16((float)b[k][2], (float)b[k][3]), 0, 0);
+          *reinterpret_cast<uint4*>(xs + i * 32) = lo;
+          *reinterpret_cast<uint4*>(xs + i * 32 + 16) = make_uint4(0, 0, 0, 0);
+        }
+      }
     }
   } else {
     const bf16_t* xi = reinterpret_cast<const bf16_t*>(x) + (int64_t)n * x_img;
-    for (int i = tid; i < P * BLK * 2; i += nthr) {
-      const int hf = i & 1, pix = i >> 1;
-      const int p = pix / BLK, rem = pix - p * BLK;
-      const int lr = rem / WP, c = rem - lr * WP;
-      const int h = r0 - 1 + lr, w = c - 1;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (h >= 0 && h < H && w >= 0 && w < W) {
-        v = *reinterpret_cast<const uint4*>(xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
-        if (relu) v = relu_u4(v);
+    constexpr int NCK = P * BLK * 2;
+    for (int base = 0; base < NCK; base += NTHR * BATCH) {
+      uint4 v[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int i = base + k * NTHR + tid;
+        const int hf = i & 1, pix = i >> 1;
+        const int p = pix / BLK, rem = pix - (pix / BLK) * BLK;
+        const int lr = rem / WP, c = rem - (rem / WP) * WP;
+        const int h = row0 + lr, w = c - 1;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (i < NCK && h >= 0 && h < H && w >= 0 && w < W)
+          v[k] = *reinterpret_cast<const uint4*>(xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
       }
-      *reinterpret_cast<uint4*>(xs + (p * plane_pix + rem) * 32 + hf * 16) = v;
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int i = base + k * NTHR + tid;
+        const int hf = i & 1, pix = i >> 1;
+        const int p = pix / BLK, rem = pix - (pix / BLK) * BLK;
+        if (i < NCK) *reinterpret_cast<uint4*>(xs + (p * plane_pix + rem) * 32 + hf * 16) = relu ? relu_u4(v[k]) : v[k];
+      }
     }
   }
   const int slack = plane_pix - BLK;
-  for (int i = tid; i < P * slack * 2; i += nthr) {
+  for (int i = tid; i < P * slack * 2; i += NTHR) {
     const int p = i / (slack * 2), r = i - p * slack * 2;
     *reinterpret_cast<uint4*>(xs + (p * plane_pix + BLK) * 32 + r * 16) = make_uint4(0, 0, 0, 0);
   }
 }
 
 // =====================================================================================
-// forward / data-gradient correlation
+// forward / data-gradient correlation (+ fused 3x3/s2 max pool)
 // =====================================================================================
-template <int CIN, int COUT, int H, int W, int R, int MODE>
-__global__ void __launch_bounds__(256) sconv_fwd_kernel(SconvDesc d) {
+// POOL = 0: one workgroup computes output rows [R band, R band + R) and applies the
+//           bias / mask / add / ReLU epilogue straight to global memory.
+// POOL = 1: (R even) the workgroup computes conv rows [R band - 1, R band + R) into
+//           an LDS tile (rows outside the image = -inf), then max-pools them into
+//           pooled rows [R band / 2, R band / 2 + R / 2) + argmax codes: the
+//           full-resolution conv output never reaches HBM.
+template <int CIN, int COUT, int H, int W, int R, int MODE, int POOL>
+__global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
+  constexpr int NTHR = 512, NW = NTHR / 64;
   constexpr int P = CIN / 16, NT = COUT / 16;
   constexpr int WP = W + 2;
-  constexpr int PLANE = (R + 2) * WP + 18;     // + overrun of the last M tile's taps
+  constexpr int OROWS = POOL ? R + 1 : R;      // conv rows computed
+  constexpr int SROWS = OROWS + 2;             // staged input rows (1-row halo each side)
+  constexpr int PLANE = SROWS * WP + 18;       // + overrun of the last M tile's taps
   constexpr int NCH = (9 * P + 1) / 2;         // 32-wide K chunks = pairs of (tap, plane)
-  constexpr int MROWS = R * WP;
+  constexpr int MROWS = OROWS * WP;
   constexpr int NTILE = (MROWS + 15) / 16;
-  __shared__ __attribute__((aligned(16))) uint8_t xs[P * PLANE * 32];
+  constexpr int OPIX = POOL ? OROWS * W : 0;   // pool tile: conv pixels per output plane
+  static_assert(!POOL || (R % 2) == 0, "pooled bands need an even row count");
+  __shared__ __attribute__((aligned(16))) uint8_t xs[(P * PLANE + NT * OPIX) * 32];
+  uint8_t* ot = xs + P * PLANE * 32;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int band = blockIdx.x, n = blockIdx.y;
-  const int r0 = band * R;
+  const int o0 = POOL ? band * R - 1 : band * R;   // first conv output row of the band
   const bool second = d.wf2 != nullptr && n >= d.n_switch;
   const bf16_t* __restrict__ wf = second ? d.wf2 : d.wf;
   const float* __restrict__ bias = second ? d.bias2 : d.bias;
@@ -143,7 +180,7 @@ __global__ void __launch_bounds__(256) sconv_fwd_kernel(SconvDesc d) {
     for (int nt = 0; nt < NT; ++nt)
       wfr[c][nt] = *reinterpret_cast<const bf16x8*>(wf + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
 
-  stage_rows<P, H, W, R, MODE>(xs, PLANE, d.x, d.x_img, d.slots, n, r0, d.relu_in, tid, 256);
+  stage_rows<P, H, W, SROWS, MODE, NTHR, 8>(xs, PLANE, d.x, d.x_img, d.slots, n, o0 - 1, d.relu_in, tid);
   __syncthreads();
 
   // per-lane LDS byte offset of each K chunk: lane group kg = lane >> 4 reads
@@ -162,8 +199,23 @@ __global__ void __launch_bounds__(256) sconv_fwd_kernel(SconvDesc d) {
   const bf16_t* __restrict__ addi = d.add ? d.add + (int64_t)n * d.add_img : nullptr;
   const bf16_t* __restrict__ mski = d.mask ? d.mask + (int64_t)n * d.mask_img : nullptr;
 
-  for (int tile = wv; tile < NTILE; tile += 4) {
+  for (int tile = wv; tile < NTILE; tile += NW) {
     const int q0 = tile * 16;
+    // lane: pixel q0 + (lane & 15), output channels nt*16 + 4 kg + {0..3}
+    const int q = q0 + (lane & 15);
+    const int lh = q / WP, w = q - (q / WP) * WP;
+    const int h = o0 + lh;
+    const bool valid = lh < OROWS && w < W && (POOL || h < H);
+    // epilogue operands first: their latency hides under the fragment reads + MFMAs
+    uint2 am[NT], mm[NT];
+    if (!POOL && valid) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int64_t off = ((int64_t)(nt * H + h) * W + w) * 16 + 4 * kg;
+        if (addi) am[nt] = *reinterpret_cast<const uint2*>(addi + off);
+        if (mski) mm[nt] = *reinterpret_cast<const uint2*>(mski + off);
+      }
+    }
     bf16x8 xf[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) xf[c] = *reinterpret_cast<const bf16x8*>(xs + aoff[c] + q0 * 32);
@@ -175,41 +227,86 @@ __global__ void __launch_bounds__(256) sconv_fwd_kernel(SconvDesc d) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[c][nt], xf[c], acc[nt], 0, 0, 0);
-    // lane: pixel q0 + (lane & 15), output channels nt*16 + 4 kg + {0..3}
-    const int q = q0 + (lane & 15);
-    const int lh = q / WP, w = q - (q / WP) * WP;
-    const int h = r0 + lh;
-    if (lh < R && w < W && h < H) {
+    if (!valid) continue;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int co = nt * 16 + 4 * kg;
-        float v[4];
+    for (int nt = 0; nt < NT; ++nt) {
+      const int co = nt * 16 + 4 * kg;
+      float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] * d.scale;
-        if (bias) {
-          const float4 b = *reinterpret_cast<const float4*>(bias + co);
-          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-        }
-        const int64_t off = ((int64_t)(nt * H + h) * W + w) * 16 + 4 * kg;
-        if (mski) {
-          const uint2 m = *reinterpret_cast<const uint2*>(mski + off);
-          v[0] = bf16_to_f32(m.x & 0xffff) > 0.f ? v[0] : 0.f;
-          v[1] = bf16_to_f32(m.x >> 16) > 0.f ? v[1] : 0.f;
-          v[2] = bf16_to_f32(m.y & 0xffff) > 0.f ? v[2] : 0.f;
-          v[3] = bf16_to_f32(m.y >> 16) > 0.f ? v[3] : 0.f;
-        }
-        if (addi) {
-          const uint2 a = *reinterpret_cast<const uint2*>(addi + off);
-          v[0] += bf16_to_f32(a.x & 0xffff);
-          v[1] += bf16_to_f32(a.x >> 16);
-          v[2] += bf16_to_f32(a.y & 0xffff);
-          v[3] += bf16_to_f32(a.y >> 16);
-        }
-        if (d.relu_out) {
+      for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] * d.scale;
+      if (bias) {
+        const float4 b = *reinterpret_cast<const float4*>(bias + co);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (POOL) {
+        if (h < 0 || h >= H) v[0] = v[1] = v[2] = v[3] = -INFINITY;   // max-pool padding row
+        *reinterpret_cast<uint2*>(ot + ((nt * OROWS + lh) * W + w) * 32 + 8 * kg) =
+            make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+        continue;
+      }
+      if (mski) {
+        const uint2 m = mm[nt];
+        v[0] = bf16_to_f32(m.x & 0xffff) > 0.f ? v[0] : 0.f;
+        v[1] = bf16_to_f32(m.x >> 16) > 0.f ? v[1] : 0.f;
+        v[2] = bf16_to_f32(m.y & 0xffff) > 0.f ? v[2] : 0.f;
+        v[3] = bf16_to_f32(m.y >> 16) > 0.f ? v[3] : 0.f;
+      }
+      if (addi) {
+        const uint2 a = am[nt];
+        v[0] += bf16_to_f32(a.x & 0xffff);
+        v[1] += bf16_to_f32(a.x >> 16);
+        v[2] += bf16_to_f32(a.y & 0xffff);
+        v[3] += bf16_to_f32(a.y >> 16);
+      }
+      if (d.relu_out) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      const int64_t off = ((int64_t)(nt * H + h) * W + w) * 16 + 4 * kg;
+      *reinterpret_cast<uint2*>(yi + off) = make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+    }
+  }
+  if constexpr (POOL) {
+    // 3x3 / s2 / pad 1 max pool of the LDS conv tile: pooled rows band*R/2 + [0, R/2),
+    // one item per (plane, pooled pixel, 8-channel half); argmax code = kh*3 + kw of
+    // the first maximum in window order (torch.max_pool2d's rule)
+    constexpr int HO = (H + 1) / 2, WO = (W + 1) / 2, PR = R / 2;
+    __syncthreads();
+    uint8_t* __restrict__ am_out = reinterpret_cast<uint8_t*>(d.mask_out);
+    for (int it = tid; it < NT * PR * WO * 2; it += NTHR) {
+      const int hf = it & 1, r1 = it >> 1;
+      const int ow = r1 % WO, r2 = r1 / WO;
+      const int pr = r2 % PR, nt = r2 / PR;
+      const int oh = band * PR + pr;
+      if (oh >= HO) continue;
+      float best[8];
+      int code[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) { best[c] = -INFINITY; code[c] = 0; }
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int lr = 2 * pr + kh;            // conv row 2 oh - 1 + kh relative to o0
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int wc = 2 * ow - 1 + kw;
+          if (wc < 0 || wc >= W) continue;
+          const uint4 v = *reinterpret_cast<const uint4*>(ot + ((nt * OROWS + lr) * W + wc) * 32 + hf * 16);
+          const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const float f = bf16_to_f32((bf16_t)((u[c >> 1] >> (16 * (c & 1))) & 0xffff));
+            if (f > best[c]) { best[c] = f; code[c] = kh * 3 + kw; }
+          }
         }
-        *reinterpret_cast<uint2*>(yi + off) = make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+      }
+      const int64_t po = (((int64_t)nt * HO + oh) * WO + ow) * 16 + hf * 8;
+      *reinterpret_cast<uint4*>(yi + po) = make_uint4(cvt_pk_bf16(best[0], best[1]), cvt_pk_bf16(best[2], best[3]),
+                                                      cvt_pk_bf16(best[4], best[5]), cvt_pk_bf16(best[6], best[7]));
+      if (am_out) {
+        uint2 cv;
+        cv.x = code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
+        cv.y = code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24);
+        *reinterpret_cast<uint2*>(am_out + (int64_t)n * NT * HO * WO * 16 + po) = cv;
       }
     }
   }
@@ -262,16 +359,27 @@ __global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
   for (int n = n_begin; n < n_end; ++n) {
     // dY band: pixel q = lh * WP + w, zero for w >= W, rows past H / R, and q >= R * WP
     const bf16_t* dyi = d.dy + (int64_t)n * d.dy_img;
-    for (int i = tid; i < NT * DPIX * 2; i += 256) {
-      const int hf = i & 1, pix = i >> 1;
-      const int p = pix / DPIX, q = pix - p * DPIX;
-      const int lh = q / WP, w = q - lh * WP;
-      const int h = r0 + lh;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (lh < R && w < W && h < H) v = *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
-      *reinterpret_cast<uint4*>(dys + (p * DPIX + q) * 32 + hf * 16) = v;
+    constexpr int NDC = NT * DPIX * 2, DB = 4;
+    for (int base = 0; base < NDC; base += 256 * DB) {
+      uint4 v[DB];
+#pragma unroll
+      for (int k = 0; k < DB; ++k) {
+        const int i = base + k * 256 + tid;
+        const int hf = i & 1, pix = i >> 1;
+        const int p = pix / DPIX, q = pix - (pix / DPIX) * DPIX;
+        const int lh = q / WP, w = q - (q / WP) * WP;
+        const int h = r0 + lh;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (i < NDC && lh < R && w < W && h < H)
+          v[k] = *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+      }
+#pragma unroll
+      for (int k = 0; k < DB; ++k) {
+        const int i = base + k * 256 + tid;
+        if (i < NDC) *reinterpret_cast<uint4*>(dys + (i >> 1) * 32 + (i & 1) * 16) = v[k];
+      }
     }
-    stage_rows<P, H, W, R, MODE>(xs, XPIX, d.x, d.x_img, d.slots, n, r0, d.relu_in, tid, 256);
+    stage_rows<P, H, W, R + 2, MODE, 256, 4>(xs, XPIX, d.x, d.x_img, d.slots, n, r0 - 1, d.relu_in, tid);
     __syncthreads();
     for (int j = wv; j < NQ; j += 4) {
       const int qb = 32 * j;
@@ -477,20 +585,26 @@ __global__ void __launch_bounds__(256) sconv_pack_kernel(PackDesc d) {
 }
 
 // ------------------------------------------------------------------ launchers
-#define SCONV_SHAPES(X)      \
-  X(16, 16, 84, 84, 21, 2)   \
-  X(16, 16, 42, 42, 42, 0)   \
-  X(16, 32, 42, 42, 42, 0)   \
-  X(32, 16, 42, 42, 21, 0)   \
-  X(32, 32, 21, 21, 21, 0)   \
-  X(32, 32, 11, 11, 11, 0)
+#define SCONV_SHAPES(X)         \
+  X(16, 16, 84, 84, 10, 2, 1)   \
+  X(16, 32, 42, 42, 14, 0, 1)   \
+  X(32, 32, 21, 21, 22, 0, 1)   \
+  X(16, 16, 84, 84, 21, 2, 0)   \
+  X(16, 16, 42, 42, 42, 0, 0)   \
+  X(16, 32, 42, 42, 42, 0, 0)   \
+  X(32, 16, 42, 42, 21, 0, 0)   \
+  X(32, 32, 21, 21, 21, 0, 0)   \
+  X(32, 32, 11, 11, 11, 0, 0)
 
-APEX_EXPORT int apex_sconv_fwd(SconvDesc d, int cin, int cout, int H, int W, int mode, hipStream_t st) {
+// pool = 1: fused conv + 3x3/s2 max pool (d.y = pooled output, d.mask_out = argmax)
+APEX_EXPORT int apex_sconv_fwd(SconvDesc d, int cin, int cout, int H, int W, int mode, int pool, hipStream_t st) {
   if (d.N <= 0) return 0;
-#define SCONV_FWD_CASE(CI, CO, HH, WW, RR, MM)                                                   \
-  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) {                             \
-    sconv_fwd_kernel<CI, CO, HH, WW, RR, MM><<<dim3((HH + RR - 1) / RR, d.N), 256, 0, st>>>(d); \
-    APEX_CHECK_LAUNCH();                                                                         \
+  if (pool && (d.add || d.mask || d.relu_out)) return (int)hipErrorInvalidValue;
+#define SCONV_FWD_CASE(CI, CO, HH, WW, RR, MM, PP)                                                      \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM && pool == PP) {                      \
+    const int bands = PP ? ((HH + 1) / 2 + RR / 2 - 1) / (RR / 2) : (HH + RR - 1) / RR;                 \
+    sconv_fwd_kernel<CI, CO, HH, WW, RR, MM, PP><<<dim3(bands, d.N), 512, 0, st>>>(d);                  \
+    APEX_CHECK_LAUNCH();                                                                                \
   }
   SCONV_SHAPES(SCONV_FWD_CASE)
 #undef SCONV_FWD_CASE

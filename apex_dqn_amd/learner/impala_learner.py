@@ -6,8 +6,8 @@ centered RMSprop -> priority write-back), with the trunk on the small-channel
 conv kernels of ``csrc/impala.hip``:
 
   per stack s (channels 16 / 32 / 32, input 84 / 42 / 21 px):
-    c0 = conv3x3(x)              (stack 1: straight from the uint8 frame ring)
-    p  = maxpool3x3s2(c0)        (+ argmax codes for the backward)
+    p  = maxpool3x3s2(conv3x3(x))  one kernel (+ argmax codes for the backward);
+                                 stack 1 reads the uint8 frame ring directly
     ya = conv(relu(p));  ra = p  + conv(relu(ya))
     yb = conv(relu(ra)); o  = ra + conv(relu(yb))
   feat = relu(o_3) (planar, 3872 + 32 zero pad = 3904 per row)
@@ -162,7 +162,7 @@ class FusedImpalaLearner:
         for s, (cin, cout, hw, php) in enumerate(_stack_dims()):
             P = cout // 16
             t = lambda n, h: torch.zeros(n, P, h, h, 16, dtype=ad, device=d)  # noqa: E731
-            f = dict(c0=t(N3, hw), p=t(N3, php), ya=t(N3, php), ra=t(N3, php), yb=t(N3, php),
+            f = dict(p=t(N3, php), ya=t(N3, php), ra=t(N3, php), yb=t(N3, php),
                      amax=torch.zeros(N3, P, php, php, 16, dtype=torch.uint8, device=d))
             f["o"] = (self.feat[:, :FEAT].view(N3, P, php, php, 16) if s == 2 else t(N3, php))
             self.fw.append(f)
@@ -202,11 +202,11 @@ class FusedImpalaLearner:
             f = self.fw[s]
             c0, r0a, r0b, r1a, r1b = convs
             tg = lambda cs: dict(second=cs.extra["b_tgt"], n_switch=2 * B)  # noqa: E731
-            if s == 0:
-                io.conv(None, c0, f["c0"], ring=self.replay.frames, slots=self.slots, scale=rt.obs_scale, **tg(c0))
+            if s == 0:   # conv + max pool in one kernel, straight from the uint8 frame ring
+                io.conv_pool(None, c0, f["p"], f["amax"], ring=self.replay.frames, slots=self.slots,
+                             scale=rt.obs_scale, **tg(c0))
             else:
-                io.conv(x, c0, f["c0"], **tg(c0))
-            io.maxpool(f["c0"], f["p"], f["amax"])
+                io.conv_pool(x, c0, f["p"], f["amax"], **tg(c0))
             io.conv(f["p"], r0a, f["ya"], relu_in=True, **tg(r0a))
             io.conv(f["ya"], r0b, f["ra"], relu_in=True, add=f["p"], **tg(r0b))
             io.conv(f["ra"], r1a, f["yb"], relu_in=True, **tg(r1a))

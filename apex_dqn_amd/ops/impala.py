@@ -26,7 +26,7 @@ c_p, c_i, c_i64, c_f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_f
 
 class SconvDesc(ctypes.Structure):
     _fields_ = [("x", c_p), ("slots", c_p), ("wf", c_p), ("wf2", c_p), ("bias", c_p), ("bias2", c_p),
-                ("add", c_p), ("mask", c_p), ("y", c_p), ("x_img", c_i64), ("y_img", c_i64),
+                ("add", c_p), ("mask", c_p), ("y", c_p), ("mask_out", c_p), ("x_img", c_i64), ("y_img", c_i64),
                 ("add_img", c_i64), ("mask_img", c_i64), ("N", c_i), ("n_switch", c_i),
                 ("relu_in", c_i), ("relu_out", c_i), ("scale", c_f), ("pad0", c_i)]
 
@@ -46,7 +46,7 @@ class PackDesc(ctypes.Structure):
 
 
 _SIGS = {
-    "apex_sconv_fwd": ([SconvDesc, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_sconv_fwd": ([SconvDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
     "apex_sconv_wgrad": ([SconvWgDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
     "apex_sconv_wgrad_bands": ([c_i, c_i, c_i, c_i, c_i], c_i),
     "apex_maxpool_fwd": ([c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_p], c_i),
@@ -134,11 +134,21 @@ class HipImpalaOps:
             _lib.check(self.lib.apex_sconv_pack(d, _lib.stream_ptr()), "sconv_pack")
 
     # -- convs
+    def conv_pool(self, x, spec: ConvSpec, y, amax, *, second=None, n_switch=0, scale=1.0, ring=None,
+                  slots=None) -> None:
+        """y = maxpool3x3s2(conv3x3(x) * scale + b) (+ argmax codes): the fused stack-entry
+        kernel; the full-resolution conv output stays in LDS."""
+        self.conv(x, spec, y, second=second, n_switch=n_switch, scale=scale, ring=ring, slots=slots,
+                  _pool_amax=amax)
+
     def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
-             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None) -> None:
+             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None, _pool_amax=False) -> None:
         """y = epi(corr3x3(x', W')): W' = W (forward) or transposed + flipped (data
         gradient); x' = relu(x) if relu_in; epi = *scale + bias, * (mask > 0), + add, relu."""
         d = SconvDesc()
+        pool = _pool_amax is not False
+        if pool:
+            d.mask_out = _lib.ptr(_pool_amax)
         N = y.shape[0]
         if ring is not None:
             d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
@@ -161,8 +171,8 @@ class HipImpalaOps:
         d.y, d.y_img = y.data_ptr(), img_stride(y)
         d.N, d.relu_in, d.relu_out, d.scale = N, int(relu_in), int(relu_out), float(scale)
         cin, cout = (spec.cout, spec.cin) if transpose else (spec.cin, spec.cout)
-        _lib.check(self.lib.apex_sconv_fwd(d, cin, cout, spec.H, spec.W, mode, _lib.stream_ptr()),
-                   f"sconv_fwd[{spec.name}{'^T' if transpose else ''}]")
+        _lib.check(self.lib.apex_sconv_fwd(d, cin, cout, spec.H, spec.W, mode, int(pool), _lib.stream_ptr()),
+                   f"sconv_fwd[{spec.name}{'^T' if transpose else ''}{'+pool' if pool else ''}]")
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
               groups: int = 0, scale: float = 1.0) -> None:
@@ -235,6 +245,13 @@ class TorchImpalaOps:
         if transpose:
             w = w.transpose(0, 1).flip(2, 3)
         return w
+
+    def conv_pool(self, x, spec: ConvSpec, y, amax, *, second=None, n_switch=0, scale=1.0, ring=None,
+                  slots=None) -> None:
+        N = y.shape[0]
+        c0 = torch.zeros(N, spec.cout // 16, spec.H, spec.W, 16, dtype=y.dtype, device=y.device)
+        self.conv(x, spec, c0, second=second, n_switch=n_switch, scale=scale, ring=ring, slots=slots)
+        self.maxpool(c0, y, amax)
 
     def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
              bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None) -> None:

@@ -193,6 +193,14 @@ def test_gpu_sconv_ring_input():
     hops.conv(None, cs, y, **kw)
     tops.conv(None, cs, yr, **kw)
     torch.testing.assert_close(y.float(), yr.float(), rtol=2e-2, atol=3e-2)
+    # fused conv + max pool (+ argmax): same pooled values, codes consistent with the values
+    p, pr = (torch.zeros(5, 1, 42, 42, 16, dtype=torch.bfloat16, device=dev) for _ in range(2))
+    a, ar = (torch.zeros(5, 1, 42, 42, 16, dtype=torch.uint8, device=dev) for _ in range(2))
+    hops.conv_pool(None, cs, p, a, **kw)
+    tops.maxpool(y, pr, ar)
+    torch.testing.assert_close(p.float(), pr.float(), rtol=0, atol=0)
+    agree = (a == ar).float().mean().item()
+    assert agree > 0.999, agree
     # weight gradient from the ring (x scale)
     dy = torch.randn(5, 1, 84, 84, 16, device=dev).to(torch.bfloat16)
     gw, gb = torch.zeros(16, 4, 3, 3, device=dev), torch.zeros(16, device=dev)
@@ -229,6 +237,28 @@ def test_gpu_sconv_wgrad(cin, cout, H):
         scale = gwr.abs().max().item()
         torch.testing.assert_close(gw / scale, gwr / scale, rtol=0, atol=2e-3)
         torch.testing.assert_close(gb, gbr, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,H", [(16, 32, 42), (32, 32, 21)])
+def test_gpu_sconv_pool_fused(cin, cout, H):
+    from apex_dqn_amd.ops.impala import HipImpalaOps
+    dev = torch.device("cuda")
+    hops, tops = HipImpalaOps(), TorchImpalaOps()
+    N = 5
+    x = torch.randn(N, cin // 16, H, H, 16, device=dev).to(torch.bfloat16)
+    cs = _spec(cin, cout, H, dev)
+    _hip_pack(hops, cs, dev)
+    Ho = (H + 1) // 2
+    kw = dict(second=cs.extra["b_tgt"], n_switch=2)
+    y = torch.zeros(N, cout // 16, H, H, 16, dtype=torch.bfloat16, device=dev)
+    hops.conv(x, cs, y, **kw)
+    p, pr = (torch.zeros(N, cout // 16, Ho, Ho, 16, dtype=torch.bfloat16, device=dev) for _ in range(2))
+    a, ar = (torch.zeros(N, cout // 16, Ho, Ho, 16, dtype=torch.uint8, device=dev) for _ in range(2))
+    hops.conv_pool(x, cs, p, a, **kw)
+    tops.maxpool(y, pr, ar)          # pool of the (identically computed) unfused conv
+    torch.testing.assert_close(p.float(), pr.float(), rtol=0, atol=0)
+    assert (a == ar).float().mean().item() > 0.999
 
 
 @pytest.mark.gpu
