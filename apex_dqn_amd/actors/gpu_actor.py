@@ -190,12 +190,63 @@ class GraphActorGroup(GpuActorGroup):
         return self.q_host.numpy().copy(), self.a_host.numpy().copy()
 
 
+class ImpalaActorGroup(GpuActorGroup):
+    """Actor group for the hand-written IMPALA learner (``FusedImpalaLearner``):
+    the trunk runs on the learner's csrc/impala.hip kernels over the group's E
+    frame stacks (read straight from the replay ring by slot) with the group's
+    own parameter slot, then the ``actor_head`` kernel draws epsilon-greedy."""
+
+    def __init__(self, cfg, learner, replay, env, num_envs: int, global_offset: int = 0,
+                 total_actors: Optional[int] = None, seed: int = 0):
+        self.cfg, self.learner, self.replay, self.env = cfg, learner, replay, env
+        self.E, self.C, self.A = int(num_envs), learner.C, learner.A
+        self.ops = learner.ops
+        d = learner.device
+        self.device = d
+        a = cfg.Actor
+        total = total_actors or self.E
+        ladder = epsilon_ladder(total, a.epsilon, a.alpha)
+        self.eps = torch.tensor(ladder[global_offset:global_offset + self.E], dtype=torch.float32, device=d)
+        self.seed = int(seed) * 7919 + global_offset
+        self.ctr = torch.zeros(1, dtype=torch.int64, device=d)
+        self.slots = torch.zeros(self.E, self.C, dtype=torch.int32, device=d)
+        self.ps = learner.actor_param_set()
+        self.bufs = learner.alloc_trunk(self.E)
+        self.q = torch.zeros(self.E, self.A, dtype=torch.float32, device=d)
+        self.act = torch.zeros(self.E, dtype=torch.int32, device=d)
+        self.q_host = torch.zeros(self.E, self.A, dtype=torch.float32)
+        self.a_host = torch.zeros(self.E, dtype=torch.int32)
+        if d.type == "cuda":
+            self.q_host, self.a_host = self.q_host.pin_memory(), self.a_host.pin_memory()
+        self.builder = NStepBuilder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.payload = None
+        self.t = 0
+        self.episodes = []
+        self.inserted = 0
+
+    def sync_params(self) -> None:
+        self.learner.refresh_param_set(self.ps)
+
+    def policy(self, payload: np.ndarray):
+        self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
+        h = self.learner.trunk_forward(self.slots, self.ps, self.bufs)
+        heads = {k: self.ps["V"][k] for k in ("wv", "bv", "wa", "ba")}
+        self.ops.actor_head(h, heads, self.eps, self.ctr, self.seed, self.q, self.act)
+        self.ctr += 1
+        self.q_host.copy_(self.q, non_blocking=True)
+        self.a_host.copy_(self.act, non_blocking=True)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        return self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64)
+
+
 def make_gpu_actor_group(cfg, learner, replay, num_envs: int, rank: int = 0, world: int = 1,
                          seed: int = 0) -> GpuActorGroup:
     from ..envs.vector_envs import make_vec_env
     total = max(cfg.Actor.num_actors, num_envs * world)
     env = make_vec_env(cfg.env_backend, cfg.env_conf.name, num_envs, cfg.env_conf.action_dim,
                        seed=seed + 1000 * rank)
-    cls = GraphActorGroup if getattr(learner, "kind", "") == "graph" else GpuActorGroup
+    kind = getattr(learner, "kind", "")
+    cls = {"graph": GraphActorGroup, "impala": ImpalaActorGroup}.get(kind, GpuActorGroup)
     return cls(cfg, learner, replay, env, num_envs, global_offset=rank * num_envs,
                total_actors=total, seed=seed + rank)

@@ -214,6 +214,64 @@ class FusedImpalaLearner:
             x = f["o"]
         self.ops.fc_fwd(self.feat, self.Pb["wfc"], self.P["bfc"], self.h, self.Tb["wfc"], self.T["bfc"], 2 * B)
 
+    # ------------------------------------------------- actor-side inference
+    def actor_param_set(self) -> Dict:
+        """A private parameter slot for an actor group (fp32 + bf16 copies and, on
+        the HIP path, packed fragments); refreshed by ``refresh_param_set``."""
+        import dataclasses
+        p32, pbf = self.p32.clone(), self.pbf.clone()
+        V, Vb = self.layout.views(p32), self.layout.views(pbf)
+        specs = []
+        for convs in self.specs:
+            row = []
+            for cs in convs:
+                c2 = dataclasses.replace(cs, w=V[cs.name + ".w"], b=V[cs.name + ".b"], wb=Vb[cs.name + ".w"],
+                                         extra=dict(cs.extra))
+                if cs.frag is not None:
+                    c2.frag = torch.zeros_like(cs.frag)
+                    c2.fragT = c2.frag_tgt = None
+                row.append(c2)
+            specs.append(row)
+        ps = dict(p32=p32, pbf=pbf, V=V, Vb=Vb, specs=specs)
+        self.refresh_param_set(ps)
+        return ps
+
+    def refresh_param_set(self, ps: Dict) -> None:
+        ps["p32"].copy_(self.p32)
+        ps["pbf"].copy_(self.pbf)
+        self.iops.pack([(cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, 0) for row in ps["specs"] for cs in row])
+
+    def alloc_trunk(self, E: int) -> Dict:
+        d, ad = self.device, self.act_dtype
+        bufs = dict(stacks=[], feat=torch.zeros(E, FEAT_LD, dtype=ad, device=d),
+                    h=torch.zeros(E, 2 * HIDDEN, dtype=ad, device=d))
+        for s, (cin, cout, hw, php) in enumerate(_stack_dims()):
+            P = cout // 16
+            t = lambda: torch.zeros(E, P, php, php, 16, dtype=ad, device=d)  # noqa: E731
+            st = dict(p=t(), ya=t(), ra=t(), yb=t())
+            st["o"] = bufs["feat"][:, :FEAT].view(E, P, php, php, 16) if s == 2 else t()
+            bufs["stacks"].append(st)
+        return bufs
+
+    def trunk_forward(self, slots: torch.Tensor, ps: Dict, bufs: Dict) -> torch.Tensor:
+        """Stream activations h (E, 512) of the frame stacks at ``slots`` with the
+        parameter slot ``ps`` (actor inference: same kernels, no target rows)."""
+        io, x = self.iops, None
+        for s, convs in enumerate(ps["specs"]):
+            f = bufs["stacks"][s]
+            c0, r0a, r0b, r1a, r1b = convs
+            if s == 0:
+                io.conv_pool(None, c0, f["p"], None, ring=self.replay.frames, slots=slots, scale=self.rt.obs_scale)
+            else:
+                io.conv_pool(x, c0, f["p"], None)
+            io.conv(f["p"], r0a, f["ya"], relu_in=True)
+            io.conv(f["ya"], r0b, f["ra"], relu_in=True, add=f["p"])
+            io.conv(f["ra"], r1a, f["yb"], relu_in=True)
+            io.conv(f["yb"], r1b, f["o"], relu_in=True, add=f["ra"], relu_out=(s == 2))
+            x = f["o"]
+        self.ops.fc_fwd(bufs["feat"], ps["Vb"]["wfc"], ps["V"]["bfc"], bufs["h"])
+        return bufs["h"]
+
     def _head_params(self, V):
         return {k: V[k] for k in ("wv", "bv", "wa", "ba")}
 

@@ -104,6 +104,13 @@ class ConvSpec:
     extra: Dict = field(default_factory=dict)
 
 
+# weight-gradient launch shape: workgroups per conv (images are split into groups, one
+# fp32 partial per workgroup and band) and the cap on the partial slab (floats)
+import os as _os
+WGRAD_TUNING = {"target_wgs": int(_os.environ.get("APEX_IMPALA_WG_TARGET", "512")),
+                "slab_cap": int(_os.environ.get("APEX_IMPALA_SLAB_CAP", str(2 << 20)))}
+
+
 # ------------------------------------------------------------------ HIP backend
 class HipImpalaOps:
     name = "hip"
@@ -184,8 +191,8 @@ class HipImpalaOps:
         if bands <= 0:
             raise ValueError(f"no wgrad kernel for {spec}")
         n = spec.cout * spec.cin_real * 9
-        G = groups or max(1, min(N, 512 // bands))
-        while not groups and G > 32 and bands * G * n > (2 << 20):   # keep each slab <= 8 MB
+        G = groups or max(1, min(N, WGRAD_TUNING["target_wgs"] // bands))
+        while not groups and G > 32 and bands * G * n > WGRAD_TUNING["slab_cap"]:   # slab floats
             G //= 2
         ipg = (N + G - 1) // G
         G = (N + ipg - 1) // ipg

@@ -58,7 +58,10 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     replay = build_replay(cfg, device, E, seed=rt.seed + rank)
     if cfg.network in ("nature64", "nature32"):
         learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=backend)
-    else:   # IMPALA-deep: graph-captured learner on the same HBM replay
+    elif cfg.network == "impala" and cfg.Runtime.use_hip_kernels:   # csrc/impala.hip learner
+        from ..learner.impala_learner import FusedImpalaLearner
+        learner = FusedImpalaLearner(cfg, device, replay, comm=comm, backend=backend)
+    else:   # graph-captured torch-autograd learner on the same HBM replay
         from ..learner.graph_learner import GraphLearner
         learner = GraphLearner(cfg, device, replay, comm=comm)
     group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed)

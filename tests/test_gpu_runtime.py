@@ -123,8 +123,10 @@ def test_dp_learner_two_ranks_on_one_gpu(tmp_path):
     assert res[0][4] == res[1][4]                        # same global IS normaliser on both ranks
 
 
-def test_graph_learner_impala_with_hip_graph():
-    """IMPALA-deep on the GPU loop: HBM replay + graph-captured autograd learner."""
+@pytest.mark.parametrize("hip,kind", [(True, "impala"), (False, "graph")])
+def test_impala_loop_with_hip_graph(hip, kind):
+    """IMPALA-deep on the GPU loop (actors + HBM replay + graph-captured step): the
+    hand-written csrc/impala.hip learner, and the torch-autograd graph learner."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.runtime.gpu_loop import train_frames
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
@@ -134,10 +136,10 @@ def test_graph_learner_impala_with_hip_graph():
                                             "remove_old_xp_freq": 10, "q_target_sync_freq": 20},
                                 "Replay_Memory": {"soft_capacity": 2000},
                                 "Runtime": {"replay_capacity": 2500, "log_every": 0, "use_graphs": True,
-                                            "network": "impala"}})
+                                            "network": "impala", "use_hip_kernels": hip}})
     out = train_frames(cfg, DEV, 30)
     L = out["learner"]
-    assert L.kind == "graph" and L.num_q_updates == 30 and L._graphs is not None
+    assert L.kind == kind and L.num_q_updates == 30 and L._graphs is not None
     m = L.last_metrics()
     assert np.isfinite(m["loss"]) and m["grad_norm"] > 0
 

@@ -163,10 +163,12 @@ def test_main_cli_inline_cartpole():
     assert '"learner_steps": 50' in r.stdout
 
 
-@pytest.mark.parametrize("net", ["impala", "nature32"])
-def test_graph_learner_loop_on_cpu(tmp_path, net):
-    """IMPALA-deep / nature32 run the GPU-resident loop with the graph learner
-    (HBM-replay API, flat-buffer params, fused optimizer path) -- CPU here."""
+@pytest.mark.parametrize("net,hip,kind", [("impala", True, "impala"), ("impala", False, "graph"),
+                                           ("nature32", True, "fused")])
+def test_image_learner_loops_on_cpu(tmp_path, net, hip, kind):
+    """IMPALA-deep (hand-written learner or the graph learner) and nature32 (the
+    fused NatureCNN learner, conv1 zero-padded) run the GPU-resident loop with
+    the HBM-replay API, flat-buffer params and checkpoint resume -- CPU here."""
     from apex_dqn_amd.runtime.gpu_loop import train_frames
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 4, "name": "Synthetic"},
                                 "Actor": {"num_actors": 6, "n_step_transition_batch_size": 6,
@@ -175,12 +177,13 @@ def test_graph_learner_loop_on_cpu(tmp_path, net):
                                             "remove_old_xp_freq": 4, "q_target_sync_freq": 5},
                                 "Replay_Memory": {"soft_capacity": 120},
                                 "Runtime": {"replay_capacity": 150, "log_every": 0, "use_graphs": False,
-                                            "network": net, "ckpt_dir": str(tmp_path), "ckpt_freq": 6}})
+                                            "network": net, "ckpt_dir": str(tmp_path), "ckpt_freq": 6,
+                                            "use_hip_kernels": hip}})
     out = train_frames(cfg, "cpu", 8)
     L = out["learner"]
-    assert L.kind == "graph" and L.num_q_updates == 8
+    assert getattr(L, "kind", "fused") == kind and L.num_q_updates == 8
     assert np.isfinite(L.last_metrics()["loss"]) and L.last_metrics()["grad_norm"] > 0
-    # params are views of the flat buffer; the optimizer moved them
-    assert L.Q.state_dict()[next(iter(L.Q.state_dict()))].data_ptr() >= L.p32.data_ptr()
+    if kind == "graph":   # params are views of the flat buffer; the optimizer moved them
+        assert L.Q.state_dict()[next(iter(L.Q.state_dict()))].data_ptr() >= L.p32.data_ptr()
     out2 = train_frames(cfg, "cpu", 10)          # resumes the step-6 checkpoint
     assert out2["learner"].num_q_updates == 10
