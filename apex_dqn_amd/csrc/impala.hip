@@ -141,6 +141,42 @@ __device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const voi
   }
 }
 
+// MODE 3 staging: the 4 stacked uint8 frames as 4-channel bf16 pixels (8 bytes),
+// rows [row0, row0 + SROWS) x cols [-1, W] of image n, zero outside the image.
+// One item = 4 image pixels of one row: a dword per frame from the s2d ring
+// (4 horizontally adjacent pixels are 4 contiguous bytes), transposed in VGPRs.
+template <int H, int W, int SROWS, int NTHR>
+__device__ __forceinline__ void stage_ring4(uint8_t* xs, int plane_pix, const uint8_t* ring, const int32_t* slots,
+                                            int n, int row0, int tid) {
+  constexpr int WP = W + 2, G4 = W / 4;
+  static_assert(W % 4 == 0, "ring rows are s2d blocks of 4 pixels");
+  const int32_t* sl = slots + (int64_t)n * 4;
+  const int64_t f0 = (int64_t)sl[0] * 7056, f1 = (int64_t)sl[1] * 7056;
+  const int64_t f2 = (int64_t)sl[2] * 7056, f3 = (int64_t)sl[3] * 7056;
+  for (int i = tid; i < SROWS * G4; i += NTHR) {
+    const int lr = i / G4, g = i - (i / G4) * G4;
+    const int h = row0 + lr;
+    uint32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0;
+    if (h >= 0 && h < H) {
+      const int o = ((h >> 2) * 21 + g) * 16 + (h & 3) * 4;
+      u0 = *reinterpret_cast<const uint32_t*>(ring + f0 + o);
+      u1 = *reinterpret_cast<const uint32_t*>(ring + f1 + o);
+      u2 = *reinterpret_cast<const uint32_t*>(ring + f2 + o);
+      u3 = *reinterpret_cast<const uint32_t*>(ring + f3 + o);
+    }
+    uint8_t* dst = xs + (lr * WP + 4 * g + 1) * 8;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      *reinterpret_cast<uint2*>(dst + 8 * k) = make_uint2(cvt_pk_bf16(ubyte(u0, k), ubyte(u1, k)),
+                                                          cvt_pk_bf16(ubyte(u2, k), ubyte(u3, k)));
+  }
+  for (int i = tid; i < SROWS * 2; i += NTHR) {     // halo columns -1 and W
+    const int lr = i >> 1, c = (i & 1) ? WP - 1 : 0;
+    *reinterpret_cast<uint2*>(xs + (lr * WP + c) * 8) = make_uint2(0, 0);
+  }
+  for (int i = SROWS * WP + tid; i < plane_pix; i += NTHR) *reinterpret_cast<uint2*>(xs + i * 8) = make_uint2(0, 0);
+}
+
 // =====================================================================================
 // forward / data-gradient correlation (+ fused 3x3/s2 max pool)
 // =====================================================================================
@@ -150,6 +186,11 @@ __device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const voi
 //           an LDS tile (rows outside the image = -inf), then max-pools them into
 //           pooled rows [R band / 2, R band / 2 + R / 2) + argmax codes: the
 //           full-resolution conv output never reaches HBM.
+// MODE 3 (stack-1 input, 4 frames): K = 9 taps x 4 channels packed as tap PAIRS --
+//           lane group kg reads 16 B = pixels (kw0, kw0 + 1) x 4 channels of tap
+//           row kh (two ds_read_b64 on 8-byte pixels), so 2 K chunks cover the
+//           3x3 window (kw = 3 and the last half-chunk have zero weights) instead
+//           of 5 chunks of a 16-channel zero-padded image.
 template <int CIN, int COUT, int H, int W, int R, int MODE, int POOL>
 __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
   constexpr int NTHR = 512, NW = NTHR / 64;
@@ -157,14 +198,15 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
   constexpr int WP = W + 2;
   constexpr int OROWS = POOL ? R + 1 : R;      // conv rows computed
   constexpr int SROWS = OROWS + 2;             // staged input rows (1-row halo each side)
-  constexpr int PLANE = SROWS * WP + 18;       // + overrun of the last M tile's taps
-  constexpr int NCH = (9 * P + 1) / 2;         // 32-wide K chunks = pairs of (tap, plane)
+  constexpr int PLANE = SROWS * WP + 24;       // + overrun of the last M tile's taps
+  constexpr int PIXB = MODE == 3 ? 8 : 32;     // LDS bytes per staged pixel
+  constexpr int NCH = MODE == 3 ? 2 : (9 * P + 1) / 2;   // 32-wide K chunks
   constexpr int MROWS = OROWS * WP;
   constexpr int NTILE = (MROWS + 15) / 16;
   constexpr int OPIX = POOL ? OROWS * W : 0;   // pool tile: conv pixels per output plane
   static_assert(!POOL || (R % 2) == 0, "pooled bands need an even row count");
-  __shared__ __attribute__((aligned(16))) uint8_t xs[(P * PLANE + NT * OPIX) * 32];
-  uint8_t* ot = xs + P * PLANE * 32;
+  __shared__ __attribute__((aligned(16))) uint8_t xs[P * PLANE * PIXB + NT * OPIX * 32];
+  uint8_t* ot = xs + P * PLANE * PIXB;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int band = blockIdx.x, n = blockIdx.y;
   const int o0 = POOL ? band * R - 1 : band * R;   // first conv output row of the band
@@ -180,7 +222,10 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
     for (int nt = 0; nt < NT; ++nt)
       wfr[c][nt] = *reinterpret_cast<const bf16x8*>(wf + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
 
-  stage_rows<P, H, W, SROWS, MODE, NTHR, 8>(xs, PLANE, d.x, d.x_img, d.slots, n, o0 - 1, d.relu_in, tid);
+  if constexpr (MODE == 3)
+    stage_ring4<H, W, SROWS, NTHR>(xs, PLANE, reinterpret_cast<const uint8_t*>(d.x), d.slots, n, o0 - 1, tid);
+  else
+    stage_rows<P, H, W, SROWS, MODE, NTHR, 8>(xs, PLANE, d.x, d.x_img, d.slots, n, o0 - 1, d.relu_in, tid);
   __syncthreads();
 
   // per-lane LDS byte offset of each K chunk: lane group kg = lane >> 4 reads
@@ -189,6 +234,12 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
   int aoff[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
+    if (MODE == 3) {
+      // chunk 0: tap rows 0 (kg 0, 1) and 1 (kg 2, 3); chunk 1: row 2 (kg 0, 1), kg 2, 3 zero
+      const int kh = c == 0 ? (kg >> 1) : 2;
+      aoff[c] = (kh * WP + 2 * (kg & 1) + (lane & 15)) * 8;
+      continue;
+    }
     int pair = 2 * c + (kg >> 1);
     if (pair >= 9 * P) pair = 9 * P - 1;       // zero-weight K slot: any in-bounds read
     const int t = pair / P, p = pair - (pair / P) * P;
@@ -218,7 +269,15 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
     }
     bf16x8 xf[NCH];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) xf[c] = *reinterpret_cast<const bf16x8*>(xs + aoff[c] + q0 * 32);
+    for (int c = 0; c < NCH; ++c) {
+      if (MODE == 3) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(xs + aoff[c] + q0 * 8);
+        const uint2 hi = *reinterpret_cast<const uint2*>(xs + aoff[c] + q0 * 8 + 8);
+        xf[c] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      } else {
+        xf[c] = *reinterpret_cast<const bf16x8*>(xs + aoff[c] + q0 * 32);
+      }
+    }
     f32x4 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -562,8 +621,9 @@ struct PackDesc {
 
 __global__ void __launch_bounds__(256) sconv_pack_kernel(PackDesc d) {
   const PackJob J = d.job[blockIdx.y];
-  const int Ci = J.transpose ? J.cout : J.cin, Co = J.transpose ? J.cin : J.cout;
-  const int P = Ci / 16, NT = Co / 16, NCH = (9 * P + 1) / 2;
+  const bool tr = J.transpose == 1, ring = J.transpose == 2;
+  const int Ci = tr ? J.cout : J.cin, Co = tr ? J.cin : J.cout;
+  const int P = Ci / 16, NT = Co / 16, NCH = ring ? 2 : (9 * P + 1) / 2;
   const int total = NCH * NT * 512;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
     const int j = e & 7, lane = (e >> 3) & 63, cn = e >> 9;
@@ -571,10 +631,15 @@ __global__ void __launch_bounds__(256) sconv_pack_kernel(PackDesc d) {
     const int kg = lane >> 4, pair = 2 * c + (kg >> 1);
     const int co = nt * 16 + (lane & 15);
     bf16_t v = 0;
-    if (pair < 9 * P) {
+    if (ring) {
+      // tap-pair K (sconv_fwd MODE 3): kh from (chunk, kg), kw = 2 (kg & 1) + j / 4, channel j % 4
+      const int kh = c == 0 ? (kg >> 1) : (kg < 2 ? 2 : 3);
+      const int kw = 2 * (kg & 1) + (j >> 2), ch = j & 3;
+      if (kh < 3 && kw < 3 && ch < J.cin_real) v = J.w[((int64_t)co * J.cin_real + ch) * 9 + kh * 3 + kw];
+    } else if (pair < 9 * P) {
       const int t = pair / P, p = pair - (pair / P) * P;
       const int ci = p * 16 + (kg & 1) * 8 + j;
-      if (J.transpose) {
+      if (tr) {
         if (co < J.cin_real) v = J.w[((int64_t)ci * J.cin_real + co) * 9 + (8 - t)];
       } else if (ci < J.cin_real) {
         v = J.w[((int64_t)co * J.cin_real + ci) * 9 + t];
@@ -586,10 +651,10 @@ __global__ void __launch_bounds__(256) sconv_pack_kernel(PackDesc d) {
 
 // ------------------------------------------------------------------ launchers
 #define SCONV_SHAPES(X)         \
-  X(16, 16, 84, 84, 10, 2, 1)   \
+  X(16, 16, 84, 84, 10, 3, 1)   \
   X(16, 32, 42, 42, 14, 0, 1)   \
   X(32, 32, 21, 21, 22, 0, 1)   \
-  X(16, 16, 84, 84, 21, 2, 0)   \
+  X(16, 16, 84, 84, 21, 3, 0)   \
   X(16, 16, 42, 42, 42, 0, 0)   \
   X(16, 32, 42, 42, 42, 0, 0)   \
   X(32, 16, 42, 42, 21, 0, 0)   \

@@ -183,14 +183,18 @@ class FusedImpalaLearner:
     def _pack_online(self) -> None:
         jobs = []
         for convs in self.specs:
-            for i, cs in enumerate(convs):
-                jobs.append((cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, 0))
-                if not (cs.name == "s0c0"):
+            for cs in convs:
+                jobs.append((cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs)))
+                if cs.cin_real == cs.cin:   # the ring conv needs no data gradient
                     jobs.append((cs.wb, cs.fragT, cs.cin, cs.cout, cs.cin_real, 1))
         self.iops.pack(jobs)
 
+    @staticmethod
+    def _fwd_kind(cs: ConvSpec) -> int:
+        return 2 if cs.cin_real < cs.cin else 0     # 4-frame ring conv: tap-pair fragments
+
     def _pack_target(self) -> None:
-        self.iops.pack([(cs.extra["w_tgt"], cs.frag_tgt, cs.cin, cs.cout, cs.cin_real, 0)
+        self.iops.pack([(cs.extra["w_tgt"], cs.frag_tgt, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs))
                         for convs in self.specs for cs in convs])
 
     # ------------------------------------------------------------ forward
@@ -239,7 +243,8 @@ class FusedImpalaLearner:
     def refresh_param_set(self, ps: Dict) -> None:
         ps["p32"].copy_(self.p32)
         ps["pbf"].copy_(self.pbf)
-        self.iops.pack([(cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, 0) for row in ps["specs"] for cs in row])
+        self.iops.pack([(cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs))
+                        for row in ps["specs"] for cs in row])
 
     def alloc_trunk(self, E: int) -> Dict:
         d, ad = self.device, self.act_dtype

@@ -129,7 +129,9 @@ class HipImpalaOps:
 
     # -- weights
     def pack(self, jobs: List[tuple]) -> None:
-        """jobs: (w_bf16_oihw, out, cin, cout, cin_real, transpose)."""
+        """jobs: (w_bf16_oihw, out, cin, cout, cin_real, kind): kind 0 = forward
+        fragments, 1 = data-gradient (transposed + flipped), 2 = the 4-frame ring
+        conv's tap-pair layout."""
         for s in range(0, len(jobs), 32):
             d = PackDesc()
             chunk = jobs[s:s + 32]
@@ -157,10 +159,10 @@ class HipImpalaOps:
         if pool:
             d.mask_out = _lib.ptr(_pool_amax)
         N = y.shape[0]
-        if ring is not None:
+        if ring is not None:   # 4 frames from the s2d ring, tap-pair K (fragments packed with mode 2)
             d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
-            mode = 2
-            assert slots.shape == (N, 4) and slots.dtype == torch.int32 and spec.cin == 16
+            mode = 3
+            assert slots.shape == (N, 4) and slots.dtype == torch.int32 and spec.cin == 16 and not transpose
         else:
             assert x.shape[0] == N
             d.x, d.x_img = x.data_ptr(), img_stride(x)

@@ -131,8 +131,9 @@ def _hip_pack(hops, cs, dev):
     cs.frag = torch.zeros(frag_elems(cs.cin, cs.cout), dtype=torch.bfloat16, device=dev)
     cs.fragT = torch.zeros(frag_elems(cs.cout, cs.cin), dtype=torch.bfloat16, device=dev)
     cs.frag_tgt = torch.zeros_like(cs.frag)
-    jobs = [(cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, 0), (cs.extra["w_tgt"], cs.frag_tgt, cs.cin, cs.cout,
-                                                                 cs.cin_real, 0)]
+    kind = 2 if cs.cin_real < cs.cin else 0
+    jobs = [(cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, kind), (cs.extra["w_tgt"], cs.frag_tgt, cs.cin, cs.cout,
+                                                                    cs.cin_real, kind)]
     if cs.cin_real == cs.cin:
         jobs.append((cs.wb, cs.fragT, cs.cin, cs.cout, cs.cin_real, 1))
     hops.pack(jobs)
