@@ -372,6 +372,158 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
 }
 
 // =====================================================================================
+// fused residual block forward: out = x + conv1(relu(conv0(relu(x))))
+// =====================================================================================
+// One workgroup per (image, row band [r0, r0 + R)).  x rows [r0 - 2, r0 + R + 2)
+// are staged once; conv0 is evaluated on rows [r0 - 1, r0 + R + 1) into an LDS
+// image (rows outside the image stored as the zero padding conv1 reads); conv1
+// reads it, adds x from LDS and stores the block output.  The intermediate y =
+// conv0(.) goes to HBM only for the rows the backward needs (images < n_save,
+// own band rows) -- the unfused pair moved x, y, y, x, out through HBM.
+struct ResDesc {
+  const bf16_t* x;
+  const bf16_t* wf0; const bf16_t* wf0b;    // conv0 fragments (online, target)
+  const float* b0; const float* b0b;
+  const bf16_t* wf1; const bf16_t* wf1b;    // conv1 fragments
+  const float* b1; const float* b1b;
+  bf16_t* ysave;                            // conv0 output for images < n_save (or null)
+  bf16_t* out;
+  int64_t x_img, ysave_img, out_img;
+  int N, n_switch, n_save, relu_out;
+};
+
+// All M tiles of an OROWS x WP output grid from an LDS image of P planes (plane
+// stride PLANE pixels, LDS row 0 = output row -1), ReLU on the fragments when
+// `relu`; epi(lh, w, nt, kg, acc) for every lane-pixel of the grid.
+template <int P, int NT, int WP, int OROWS, int PLANE, int NTHR, typename Epi>
+__device__ __forceinline__ void conv_grid(const uint8_t* img, const bf16_t* __restrict__ wf, bool relu, int lane,
+                                          int wv, Epi epi) {
+  constexpr int NCH = (9 * P + 1) / 2, NW = NTHR / 64;
+  constexpr int NTILE = (OROWS * WP + 15) / 16;
+  bf16x8 wfr[NCH][NT];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+      wfr[c][nt] = *reinterpret_cast<const bf16x8*>(wf + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
+  const int kg = lane >> 4;
+  int aoff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int pair = 2 * c + (kg >> 1);
+    if (pair >= 9 * P) pair = 9 * P - 1;
+    const int t = pair / P, p = pair - (pair / P) * P;
+    aoff[c] = (p * PLANE + (t / 3) * WP + (t % 3) + (lane & 15)) * 32 + (kg & 1) * 16;
+  }
+  for (int tile = wv; tile < NTILE; tile += NW) {
+    const int q0 = tile * 16;
+    bf16x8 xf[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      uint4 v = *reinterpret_cast<const uint4*>(img + aoff[c] + q0 * 32);
+      if (relu) v = relu_u4(v);
+      xf[c] = __builtin_bit_cast(bf16x8, v);
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[c][nt], xf[c], acc[nt], 0, 0, 0);
+    const int q = q0 + (lane & 15);
+    const int lh = q / WP, w = q - (q / WP) * WP;
+    if (lh < OROWS) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) epi(lh, w, nt, kg, acc[nt]);
+    }
+  }
+}
+
+template <int C, int HW, int R>
+__global__ void __launch_bounds__(512) resblock_fwd_kernel(ResDesc d) {
+  constexpr int NTHR = 512, P = C / 16, NT = C / 16, WP = HW + 2;
+  constexpr int XROWS = R + 4, YROWS = R + 2;
+  constexpr int XPL = XROWS * WP + 24, YPL = YROWS * WP + 24;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[(P * XPL + P * YPL) * 32];
+  uint8_t* xs = smem;
+  uint8_t* ys = smem + P * XPL * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int band = blockIdx.x, n = blockIdx.y;
+  const int r0 = band * R;
+  const bool second = d.wf0b != nullptr && n >= d.n_switch;
+  stage_rows<P, HW, HW, XROWS, 0, NTHR, 8>(xs, XPL, d.x, d.x_img, nullptr, n, r0 - 2, 0, tid);
+  // conv1's zero padding: halo columns of every y row + the slack past the rows
+  for (int i = tid; i < P * YROWS * 2; i += NTHR) {
+    const int p = i / (YROWS * 2), r = i - p * YROWS * 2;
+    const int c = (r & 1) ? WP - 1 : 0;
+    *reinterpret_cast<uint4*>(ys + (p * YPL + (r >> 1) * WP + c) * 32) = make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(ys + (p * YPL + (r >> 1) * WP + c) * 32 + 16) = make_uint4(0, 0, 0, 0);
+  }
+  for (int i = tid; i < P * 24 * 2; i += NTHR) {
+    const int p = i / 48, r = i - p * 48;
+    *reinterpret_cast<uint4*>(ys + (p * YPL + YROWS * WP) * 32 + r * 16) = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+
+  // conv0 on rows r0 - 1 + lh, lh in [0, R + 2): LDS x row 0 = image row r0 - 2
+  {
+    const float* __restrict__ b0 = second ? d.b0b : d.b0;
+    const bool save = d.ysave != nullptr && n < d.n_save;
+    bf16_t* __restrict__ ysv = save ? d.ysave + (int64_t)n * d.ysave_img : nullptr;
+    conv_grid<P, NT, WP, YROWS, XPL, NTHR>(xs, second ? d.wf0b : d.wf0, true, lane, wv,
+      [&](int lh, int w, int nt, int kg, f32x4 a) {
+        if (w >= HW) return;                   // padded-width garbage columns
+        const int h = r0 - 1 + lh;
+        const bool inside = h >= 0 && h < HW;
+        const float4 b = *reinterpret_cast<const float4*>(b0 + nt * 16 + 4 * kg);
+        const uint2 v = inside ? make_uint2(cvt_pk_bf16(a[0] + b.x, a[1] + b.y), cvt_pk_bf16(a[2] + b.z, a[3] + b.w))
+                               : make_uint2(0, 0);
+        *reinterpret_cast<uint2*>(ys + (nt * YPL + lh * WP + w + 1) * 32 + 8 * kg) = v;
+        if (ysv != nullptr && lh >= 1 && lh <= R && h < HW)
+          *reinterpret_cast<uint2*>(ysv + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg) = v;
+      });
+  }
+  __syncthreads();
+  // conv1 on rows r0 + lh, lh in [0, R): LDS y row 0 = image row r0 - 1; + x, (ReLU)
+  {
+    const float* __restrict__ b1 = second ? d.b1b : d.b1;
+    bf16_t* __restrict__ oi = d.out + (int64_t)n * d.out_img;
+    const int relu_out = d.relu_out;
+    conv_grid<P, NT, WP, R, YPL, NTHR>(ys, second ? d.wf1b : d.wf1, true, lane, wv,
+      [&](int lh, int w, int nt, int kg, f32x4 a) {
+        const int h = r0 + lh;
+        if (w >= HW || h >= HW) return;
+        const float4 b = *reinterpret_cast<const float4*>(b1 + nt * 16 + 4 * kg);
+        const uint2 xv = *reinterpret_cast<const uint2*>(xs + (nt * XPL + (lh + 2) * WP + w + 1) * 32 + 8 * kg);
+        float v0 = a[0] + b.x + bf16_to_f32(xv.x & 0xffff), v1 = a[1] + b.y + bf16_to_f32(xv.x >> 16);
+        float v2 = a[2] + b.z + bf16_to_f32(xv.y & 0xffff), v3 = a[3] + b.w + bf16_to_f32(xv.y >> 16);
+        if (relu_out) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
+        *reinterpret_cast<uint2*>(oi + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg) =
+            make_uint2(cvt_pk_bf16(v0, v1), cvt_pk_bf16(v2, v3));
+      });
+  }
+}
+
+#define RESBLOCK_SHAPES(X) \
+  X(16, 42, 21)            \
+  X(32, 21, 21)            \
+  X(32, 11, 11)
+
+APEX_EXPORT int apex_resblock_fwd(ResDesc d, int C, int HW, hipStream_t st) {
+  if (d.N <= 0) return 0;
+#define RESBLOCK_CASE(CC, HH, RR)                                                           \
+  if (C == CC && HW == HH) {                                                                \
+    resblock_fwd_kernel<CC, HH, RR><<<dim3((HH + RR - 1) / RR, d.N), 512, 0, st>>>(d);      \
+    APEX_CHECK_LAUNCH();                                                                    \
+  }
+  RESBLOCK_SHAPES(RESBLOCK_CASE)
+#undef RESBLOCK_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+// =====================================================================================
 // weight gradient
 // =====================================================================================
 // MFMA operand from a transposed read of 32-byte pixel rows: lane (g = lane>>4,

@@ -8,8 +8,8 @@ conv kernels of ``csrc/impala.hip``:
   per stack s (channels 16 / 32 / 32, input 84 / 42 / 21 px):
     p  = maxpool3x3s2(conv3x3(x))  one kernel (+ argmax codes for the backward);
                                  stack 1 reads the uint8 frame ring directly
-    ya = conv(relu(p));  ra = p  + conv(relu(ya))
-    yb = conv(relu(ra)); o  = ra + conv(relu(yb))
+    ya = conv(relu(p));  ra = p  + conv(relu(ya))   one kernel per block (ya in
+    yb = conv(relu(ra)); o  = ra + conv(relu(yb))   LDS; kept in HBM for B rows)
   feat = relu(o_3) (planar, 3872 + 32 zero pad = 3904 per row)
   h = relu(feat @ Wfc^T + b)   (value | advantage streams, 2 x 256)
 
@@ -211,10 +211,11 @@ class FusedImpalaLearner:
                              scale=rt.obs_scale, **tg(c0))
             else:
                 io.conv_pool(x, c0, f["p"], f["amax"], **tg(c0))
-            io.conv(f["p"], r0a, f["ya"], relu_in=True, **tg(r0a))
-            io.conv(f["ya"], r0b, f["ra"], relu_in=True, add=f["p"], **tg(r0b))
-            io.conv(f["ra"], r1a, f["yb"], relu_in=True, **tg(r1a))
-            io.conv(f["yb"], r1b, f["o"], relu_in=True, add=f["ra"], relu_out=(s == 2), **tg(r1b))
+            # residual blocks: one kernel each; the mid activations are kept for the
+            # B training rows only (the backward's ReLU masks / weight-gradient inputs)
+            io.resblock(f["p"], r0a, r0b, f["ra"], ysave=f["ya"], n_save=B, target=True, n_switch=2 * B)
+            io.resblock(f["ra"], r1a, r1b, f["o"], ysave=f["yb"], n_save=B, target=True, n_switch=2 * B,
+                        relu_out=(s == 2))
             x = f["o"]
         self.ops.fc_fwd(self.feat, self.Pb["wfc"], self.P["bfc"], self.h, self.Tb["wfc"], self.T["bfc"], 2 * B)
 
@@ -269,10 +270,8 @@ class FusedImpalaLearner:
                 io.conv_pool(None, c0, f["p"], None, ring=self.replay.frames, slots=slots, scale=self.rt.obs_scale)
             else:
                 io.conv_pool(x, c0, f["p"], None)
-            io.conv(f["p"], r0a, f["ya"], relu_in=True)
-            io.conv(f["ya"], r0b, f["ra"], relu_in=True, add=f["p"])
-            io.conv(f["ra"], r1a, f["yb"], relu_in=True)
-            io.conv(f["yb"], r1b, f["o"], relu_in=True, add=f["ra"], relu_out=(s == 2))
+            io.resblock(f["p"], r0a, r0b, f["ra"])
+            io.resblock(f["ra"], r1a, r1b, f["o"], relu_out=(s == 2))
             x = f["o"]
         self.ops.fc_fwd(bufs["feat"], ps["Vb"]["wfc"], ps["V"]["bfc"], bufs["h"])
         return bufs["h"]

@@ -37,6 +37,12 @@ class SconvWgDesc(ctypes.Structure):
                 ("imgs_per_group", c_i), ("cin_real", c_i)]
 
 
+class ResDesc(ctypes.Structure):
+    _fields_ = [("x", c_p), ("wf0", c_p), ("wf0b", c_p), ("b0", c_p), ("b0b", c_p), ("wf1", c_p), ("wf1b", c_p),
+                ("b1", c_p), ("b1b", c_p), ("ysave", c_p), ("out", c_p), ("x_img", c_i64), ("ysave_img", c_i64),
+                ("out_img", c_i64), ("N", c_i), ("n_switch", c_i), ("n_save", c_i), ("relu_out", c_i)]
+
+
 class PackJob(ctypes.Structure):
     _fields_ = [("w", c_p), ("out", c_p), ("cin", c_i), ("cout", c_i), ("cin_real", c_i), ("transpose", c_i)]
 
@@ -52,6 +58,7 @@ _SIGS = {
     "apex_maxpool_fwd": ([c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_p], c_i),
     "apex_maxpool_bwd": ([c_p, c_i64, c_p, c_i, c_i, c_i, c_p, c_i64, c_i, c_p], c_i),
     "apex_sconv_pack": ([PackDesc, c_p], c_i),
+    "apex_resblock_fwd": ([ResDesc, c_i, c_i, c_p], c_i),
     "apex_sconv_frag_elems": ([c_i, c_i], c_i64),
 }
 
@@ -183,6 +190,24 @@ class HipImpalaOps:
         _lib.check(self.lib.apex_sconv_fwd(d, cin, cout, spec.H, spec.W, mode, int(pool), _lib.stream_ptr()),
                    f"sconv_fwd[{spec.name}{'^T' if transpose else ''}{'+pool' if pool else ''}]")
 
+    def resblock(self, x, c0: ConvSpec, c1: ConvSpec, out, *, ysave=None, n_save=0, target=False, n_switch=0,
+                 relu_out=False) -> None:
+        """out = x + conv1(relu(conv0(relu(x)))) (+ ReLU) in one kernel; conv0's output
+        goes to ``ysave`` for images < ``n_save`` only; images >= ``n_switch`` use the
+        target weights when ``target``."""
+        d = ResDesc()
+        d.x, d.x_img = x.data_ptr(), img_stride(x)
+        d.wf0, d.b0, d.wf1, d.b1 = c0.frag.data_ptr(), c0.b.data_ptr(), c1.frag.data_ptr(), c1.b.data_ptr()
+        if target:
+            d.wf0b, d.b0b = c0.frag_tgt.data_ptr(), c0.extra["b_tgt"].data_ptr()
+            d.wf1b, d.b1b = c1.frag_tgt.data_ptr(), c1.extra["b_tgt"].data_ptr()
+            d.n_switch = int(n_switch)
+        if ysave is not None:
+            d.ysave, d.ysave_img, d.n_save = ysave.data_ptr(), img_stride(ysave), int(n_save)
+        d.out, d.out_img = out.data_ptr(), img_stride(out)
+        d.N, d.relu_out = x.shape[0], int(relu_out)
+        _lib.check(self.lib.apex_resblock_fwd(d, c0.cin, c0.H, _lib.stream_ptr()), f"resblock_fwd[{c0.name}]")
+
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
               groups: int = 0, scale: float = 1.0) -> None:
         """gw = scale * sum dy (x) im2col(x') (x' = relu(x) if relu_in), gb = sum dy:
@@ -261,6 +286,16 @@ class TorchImpalaOps:
         c0 = torch.zeros(N, spec.cout // 16, spec.H, spec.W, 16, dtype=y.dtype, device=y.device)
         self.conv(x, spec, c0, second=second, n_switch=n_switch, scale=scale, ring=ring, slots=slots)
         self.maxpool(c0, y, amax)
+
+    def resblock(self, x, c0: ConvSpec, c1: ConvSpec, out, *, ysave=None, n_save=0, target=False, n_switch=0,
+                 relu_out=False) -> None:
+        y = torch.zeros(x.shape[0], c0.cout // 16, c0.H, c0.W, 16, dtype=out.dtype, device=out.device)
+        t0 = dict(second=c0.extra["b_tgt"], n_switch=n_switch) if target else {}
+        t1 = dict(second=c1.extra["b_tgt"], n_switch=n_switch) if target else {}
+        self.conv(x, c0, y, relu_in=True, **t0)
+        self.conv(y, c1, out, relu_in=True, add=x, relu_out=relu_out, **t1)
+        if ysave is not None:
+            ysave[:n_save].copy_(y[:n_save])
 
     def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
              bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None) -> None:

@@ -263,6 +263,28 @@ def test_gpu_sconv_pool_fused(cin, cout, H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("C,H", [(16, 42), (32, 21), (32, 11)])
+def test_gpu_resblock_fused(C, H):
+    from apex_dqn_amd.ops.impala import HipImpalaOps
+    dev = torch.device("cuda")
+    hops, tops = HipImpalaOps(), TorchImpalaOps()
+    N = 7
+    x = torch.randn(N, C // 16, H, H, 16, device=dev).to(torch.bfloat16)
+    c0, c1 = _spec(C, C, H, dev, seed=3), _spec(C, C, H, dev, seed=4)
+    _hip_pack(hops, c0, dev)
+    _hip_pack(hops, c1, dev)
+    for relu_out in (False, True):
+        out, outr = (torch.zeros(N, C // 16, H, H, 16, dtype=torch.bfloat16, device=dev) for _ in range(2))
+        ys, ysr = (torch.zeros(N, C // 16, H, H, 16, dtype=torch.bfloat16, device=dev) for _ in range(2))
+        kw = dict(n_save=4, target=True, n_switch=5, relu_out=relu_out)
+        hops.resblock(x, c0, c1, out, ysave=ys, **kw)
+        tops.resblock(x, c0, c1, outr, ysave=ysr, **kw)
+        torch.testing.assert_close(out.float(), outr.float(), rtol=3e-2, atol=5e-2)
+        torch.testing.assert_close(ys[:4].float(), ysr[:4].float(), rtol=2e-2, atol=3e-2)
+        assert torch.count_nonzero(ys[4:]) == 0          # rows past n_save are not written
+
+
+@pytest.mark.gpu
 def test_gpu_maxpool():
     from apex_dqn_amd.ops.impala import HipImpalaOps
     dev = torch.device("cuda")
