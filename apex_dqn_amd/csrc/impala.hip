@@ -58,8 +58,8 @@ struct SconvWgDesc {
   const bf16_t* dy;           // planar gradient of the conv output
   const void* x;              // planar conv input (or mode 2: the frame ring)
   const int32_t* slots;
-  float* slab;                // [nsplit][C_out * cin_real * 9] fp32 partials (OIHW order)
-  float* bslab;               // [nsplit][C_out]
+  float* slab;                // [nsplit][(C_out/16)(9 C_in/16) + C_out/16 tiles][64 lanes][4] fp32 partials
+  float* bslab;               // unused (bias partials are the slab's last tiles)
   int64_t dy_img, x_img;
   int N, relu_in;
   int imgs_per_group, cin_real;
@@ -616,50 +616,93 @@ __global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
   }
 
   // the 4 waves' partials are summed through LDS (4 tiles per round) and the
-  // workgroup writes ONE partial: slab[split][co][ci][t] (OIHW order), split = band + bands * group
-  constexpr int T = NT * 9 * P;
+  // workgroup writes ONE partial in accumulator order -- slab[split][tile][lane][4],
+  // tiles = the T weight tiles then NT bias tiles -- as coalesced 16-byte stores;
+  // sconv_wgrad_reduce sums the splits and scatters to OIHW.
+  constexpr int T = NT * 9 * P, TT = T + NT;
   const int split = group * gridDim.x + band;
-  const int KW9 = d.cin_real * 9;
-  float* __restrict__ slab = d.slab + (int64_t)split * COUT * KW9;
+  f32x4* __restrict__ slab = reinterpret_cast<f32x4*>(d.slab) + (int64_t)split * TT * 64;
   f32x4* red = reinterpret_cast<f32x4*>(smem);          // [wave][4 tiles][64 lanes]
 #pragma unroll
-  for (int base = 0; base < T; base += 4) {
+  for (int base = 0; base < TT; base += 4) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (base + u < T) red[(wv * 4 + u) * 64 + lane] = acc[(base + u) / (9 * P)][(base + u) % (9 * P)];
+    for (int u = 0; u < 4; ++u) {
+      const int tt = base + u;
+      if (tt < T) red[(wv * 4 + u) * 64 + lane] = acc[tt / (9 * P)][tt % (9 * P)];
+      else if (tt < TT) red[(wv * 4 + u) * 64 + lane] = accb[tt - T];
+    }
     __syncthreads();
     {
       const int u = tid >> 6, l = tid & 63, tt = base + u;
-      if (tt < T) {
+      if (tt < TT) {
         f32x4 v = red[u * 64 + l];
 #pragma unroll
         for (int w = 1; w < 4; ++w) v += red[(w * 4 + u) * 64 + l];
-        const int ct = tt / (9 * P), k = tt - ct * (9 * P);
-        const int t = k / P, p = k - (k / P) * P;
-        const int ci = p * 16 + (l & 15);
-        if (ci < d.cin_real) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) slab[(int64_t)(ct * 16 + 4 * (l >> 4) + r) * KW9 + ci * 9 + t] = v[r];
-        }
+        slab[tt * 64 + l] = v;
       }
     }
     __syncthreads();
   }
+}
+
+// Sum the split partials of every IMPALA conv weight gradient (one launch for
+// all jobs) and scatter them to the OIHW fp32 gradient (x scale) + bias.  A block
+// owns 16 float4 columns of one job's slab; 16 thread groups stride the splits.
+struct WgRedJob {
+  const float* slab;
+  float* out;
+  float* bout;
+  int nsplit, NT, P, cin_real;
+  float scale;
+  int blk0;
+};
+struct WgRedDesc {
+  WgRedJob job[16];
+  int njobs, nblocks;
+};
+
+__global__ void __launch_bounds__(256) sconv_wgrad_reduce_kernel(WgRedDesc d) {
+  __shared__ f32x4 red[16][16];
+  const int b = blockIdx.x;
+  int j = 0;
 #pragma unroll
-  for (int ct = 0; ct < NT; ++ct) {
-    red[wv * 64 + lane] = accb[ct];
-    __syncthreads();
-    if (tid < 64) {
-      f32x4 v = red[lane];
-#pragma unroll
-      for (int w = 1; w < 4; ++w) v += red[w * 64 + lane];
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) d.bslab[(int64_t)split * COUT + ct * 16 + 4 * (lane >> 4) + r] = v[r];
-      }
-    }
-    __syncthreads();
+  for (int k = 1; k < 16; ++k)
+    if (k < d.njobs && b >= d.job[k].blk0) j = k;
+  const WgRedJob& J = d.job[j];
+  const int T = J.NT * 9 * J.P, TT = T + J.NT;
+  const int lc = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int col = (b - J.blk0) * 16 + lc;               // float4 column = tile * 64 + lane
+  const f32x4* __restrict__ src = reinterpret_cast<const f32x4*>(J.slab);
+  const int64_t stride = (int64_t)TT * 64;
+  f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (col < TT * 64) {
+#pragma unroll 4
+    for (int k = grp; k < J.nsplit; k += 16) v += src[(int64_t)k * stride + col];
   }
+  red[grp][lc] = v;
+  __syncthreads();
+  if (grp != 0 || col >= TT * 64) return;
+#pragma unroll
+  for (int g2 = 1; g2 < 16; ++g2) v += red[g2][lc];
+  const int tt = col >> 6, l = col & 63, g = l >> 4, i = l & 15;
+  if (tt < T) {
+    const int ct = tt / (9 * J.P), k = tt - ct * (9 * J.P);
+    const int t = k / J.P, p = k - (k / J.P) * J.P;
+    const int ci = p * 16 + i;
+    if (ci < J.cin_real) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) J.out[((int64_t)(ct * 16 + 4 * g + r) * J.cin_real + ci) * 9 + t] = v[r] * J.scale;
+    }
+  } else if (i == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) J.bout[(tt - T) * 16 + 4 * g + r] = v[r];
+  }
+}
+
+APEX_EXPORT int apex_sconv_wgrad_reduce(WgRedDesc d, hipStream_t st) {
+  if (d.njobs <= 0 || d.njobs > 16 || d.nblocks <= 0) return (int)hipErrorInvalidValue;
+  sconv_wgrad_reduce_kernel<<<d.nblocks, 256, 0, st>>>(d);
+  APEX_CHECK_LAUNCH();
 }
 
 // =====================================================================================

@@ -43,6 +43,15 @@ class ResDesc(ctypes.Structure):
                 ("out_img", c_i64), ("N", c_i), ("n_switch", c_i), ("n_save", c_i), ("relu_out", c_i)]
 
 
+class WgRedJob(ctypes.Structure):
+    _fields_ = [("slab", c_p), ("out", c_p), ("bout", c_p), ("nsplit", c_i), ("NT", c_i), ("P", c_i),
+                ("cin_real", c_i), ("scale", c_f), ("blk0", c_i)]
+
+
+class WgRedDesc(ctypes.Structure):
+    _fields_ = [("job", WgRedJob * 16), ("njobs", c_i), ("nblocks", c_i)]
+
+
 class PackJob(ctypes.Structure):
     _fields_ = [("w", c_p), ("out", c_p), ("cin", c_i), ("cout", c_i), ("cin_real", c_i), ("transpose", c_i)]
 
@@ -59,6 +68,7 @@ _SIGS = {
     "apex_maxpool_bwd": ([c_p, c_i64, c_p, c_i, c_i, c_i, c_p, c_i64, c_i, c_p], c_i),
     "apex_sconv_pack": ([PackDesc, c_p], c_i),
     "apex_resblock_fwd": ([ResDesc, c_i, c_i, c_p], c_i),
+    "apex_sconv_wgrad_reduce": ([WgRedDesc, c_p], c_i),
     "apex_sconv_frag_elems": ([c_i, c_i], c_i64),
 }
 
@@ -217,7 +227,8 @@ class HipImpalaOps:
         bands = self.lib.apex_sconv_wgrad_bands(spec.cin, spec.cout, spec.H, spec.W, mode)
         if bands <= 0:
             raise ValueError(f"no wgrad kernel for {spec}")
-        n = spec.cout * spec.cin_real * 9
+        NT, P = spec.cout // 16, spec.cin // 16
+        n = (NT * 9 * P + NT) * 256          # partial floats per split (accumulator order)
         G = groups or max(1, min(N, WGRAD_TUNING["target_wgs"] // bands))
         while not groups and G > 32 and bands * G * n > WGRAD_TUNING["slab_cap"]:   # slab floats
             G //= 2
@@ -225,24 +236,32 @@ class HipImpalaOps:
         G = (N + ipg - 1) // ipg
         nsplit = bands * G
         slab = self._buf(("slab", spec.name), nsplit * n, dy.device)
-        bslab = self._buf(("bslab", spec.name), nsplit * spec.cout, dy.device)
         d = SconvWgDesc()
         d.dy, d.dy_img = dy.data_ptr(), img_stride(dy)
         if ring is not None:
             d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
         else:
             d.x, d.x_img = x.data_ptr(), img_stride(x)
-        d.slab, d.bslab = slab.data_ptr(), bslab.data_ptr()
+        d.slab = slab.data_ptr()
         d.N, d.relu_in, d.imgs_per_group, d.cin_real = N, int(relu_in), ipg, spec.cin_real
         _lib.check(self.lib.apex_sconv_wgrad(d, spec.cin, spec.cout, spec.H, spec.W, mode, G, _lib.stream_ptr()),
                    f"sconv_wgrad[{spec.name}]")
-        jobs.append(dict(slab=slab, bslab=bslab, out=gw, bout=gb, n=n, nsplit=nsplit, nb=spec.cout, s2dC=0, Kc=4,
-                         scale=float(scale)))
+        jobs.append(dict(slab=slab, out=gw, bout=gb, nsplit=nsplit, NT=NT, P=P, cin_real=spec.cin_real,
+                         scale=float(scale), cols=(NT * 9 * P + NT) * 64))
 
     def finalize(self, jobs: list) -> None:
-        from . import conv as C
-        for s in range(0, len(jobs), 4):
-            C.finalize_grads(self.lib, jobs[s:s + 4])
+        """One launch: sum every conv's split partials -> OIHW gradient + bias."""
+        for s0 in range(0, len(jobs), 16):
+            d = WgRedDesc()
+            blk = 0
+            for i, j in enumerate(jobs[s0:s0 + 16]):
+                J = d.job[i]
+                J.slab, J.out, J.bout = j["slab"].data_ptr(), j["out"].data_ptr(), j["bout"].data_ptr()
+                J.nsplit, J.NT, J.P, J.cin_real, J.scale, J.blk0 = j["nsplit"], j["NT"], j["P"], j["cin_real"], \
+                    j["scale"], blk
+                blk += (j["cols"] + 15) // 16
+            d.njobs, d.nblocks = min(16, len(jobs) - s0), blk
+            _lib.check(self.lib.apex_sconv_wgrad_reduce(d, _lib.stream_ptr()), "sconv_wgrad_reduce")
 
     # -- pooling
     def maxpool(self, x, y, amax) -> None:
