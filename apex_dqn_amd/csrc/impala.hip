@@ -52,6 +52,7 @@ struct SconvDesc {
   int relu_in, relu_out;
   float scale;                // applied to the accumulator before the bias
   int pad0;
+  const uint8_t* amax_in;     // MODE 4: argmax codes of the pooled gradient x (same image stride, bytes)
 };
 
 struct SconvWgDesc {
@@ -63,10 +64,52 @@ struct SconvWgDesc {
   int64_t dy_img, x_img;
   int N, relu_in;
   int imgs_per_group, cin_real;
+  const uint8_t* dy_amax;     // DYP: dy is the POOLED gradient, these its argmax codes (dy_img bytes/image)
 };
 
 __device__ __forceinline__ uint4 relu_u4(uint4 v) {
   return make_uint4(relu_pk16(v.x), relu_pk16(v.y), relu_pk16(v.z), relu_pk16(v.w));
+}
+
+// Gradient of a pre-pool conv output (h, w), channels 8 hf .. 8 hf + 7 of plane p,
+// from the pooled gradient dp and argmax codes am of one image (3x3 / s2 / pad 1):
+// the sum over the <= 4 windows whose argmax is (h, w).  The max-pool backward as
+// a gather, evaluated where the consumer stages its operand, so the
+// full-resolution gradient is never written to HBM.
+template <int H, int W>
+__device__ __forceinline__ uint4 pool_grad8(const bf16_t* __restrict__ dp, const uint8_t* __restrict__ am, int p,
+                                            int h, int w, int hf) {
+  // windows containing row h: oh = h >> 1 (tap row kh = 1 + (h & 1)) and, for odd h,
+  // oh + 1 (kh = 0); same for columns.  All four candidates are loaded up front
+  // (clamped address, masked out when absent): independent loads, no branches.
+  constexpr int HO = (H + 1) / 2, WO = (W + 1) / 2;
+  const int oha = h >> 1, owa = w >> 1;
+  const bool hb = (h & 1) && oha + 1 < HO, wb = (w & 1) && owa + 1 < WO;
+  const int kha = 1 + (h & 1), kwa = 1 + (w & 1);
+  const int ohs[2] = {oha, hb ? oha + 1 : oha}, ows[2] = {owa, wb ? owa + 1 : owa};
+  const int khs[2] = {kha, hb ? 0 : -16}, kws[2] = {kwa, wb ? 0 : -16};   // -16: never matches
+  uint4 g[4];
+  uint2 cv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t po = (((int64_t)p * HO + ohs[i >> 1]) * WO + ows[i & 1]) * 16 + hf * 8;
+    g[i] = *reinterpret_cast<const uint4*>(dp + po);
+    cv[i] = *reinterpret_cast<const uint2*>(am + po);
+  }
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int want = khs[i >> 1] * 3 + kws[i & 1];
+    const uint32_t gu[4] = {g[i].x, g[i].y, g[i].z, g[i].w};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int cd = (int)(((c < 4 ? cv[i].x : cv[i].y) >> (8 * (c & 3))) & 0xff);
+      const float gv = bf16_to_f32((bf16_t)((gu[c >> 1] >> (16 * (c & 1))) & 0xffff));
+      acc[c] += cd == want ? gv : 0.f;
+    }
+  }
+  return make_uint4(cvt_pk_bf16(acc[0], acc[1]), cvt_pk_bf16(acc[2], acc[3]), cvt_pk_bf16(acc[4], acc[5]),
+                    cvt_pk_bf16(acc[6], acc[7]));
 }
 
 // Stage SROWS input rows starting at global row `row0` (x cols [-1, W]; zero
@@ -78,7 +121,8 @@ __device__ __forceinline__ uint4 relu_u4(uint4 v) {
 // thread has BATCH global loads in flight instead of one load-use round trip.
 template <int P, int H, int W, int SROWS, int MODE, int NTHR, int BATCH>
 __device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const void* x, int64_t x_img,
-                                           const int32_t* slots, int n, int row0, int relu, int tid) {
+                                           const int32_t* slots, int n, int row0, int relu, int tid,
+                                           const uint8_t* amax = nullptr) {
   constexpr int WP = W + 2, BLK = SROWS * WP;
   if constexpr (MODE == 2) {
     const uint8_t* ring = reinterpret_cast<const uint8_t*>(x);
@@ -122,8 +166,12 @@ __device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const voi
         const int lr = rem / WP, c = rem - (rem / WP) * WP;
         const int h = row0 + lr, w = c - 1;
         v[k] = make_uint4(0, 0, 0, 0);
-        if (i < NCK && h >= 0 && h < H && w >= 0 && w < W)
-          v[k] = *reinterpret_cast<const uint4*>(xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+        if (i < NCK && h >= 0 && h < H && w >= 0 && w < W) {
+          if constexpr (MODE == 4)   // x = pooled gradient of this (pre-pool) tensor
+            v[k] = pool_grad8<H, W>(xi, amax + (int64_t)n * x_img, p, h, w, hf);
+          else
+            v[k] = *reinterpret_cast<const uint4*>(xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+        }
       }
 #pragma unroll
       for (int k = 0; k < BATCH; ++k) {
@@ -225,7 +273,8 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
   if constexpr (MODE == 3)
     stage_ring4<H, W, SROWS, NTHR>(xs, PLANE, reinterpret_cast<const uint8_t*>(d.x), d.slots, n, o0 - 1, tid);
   else
-    stage_rows<P, H, W, SROWS, MODE, NTHR, 8>(xs, PLANE, d.x, d.x_img, d.slots, n, o0 - 1, d.relu_in, tid);
+    stage_rows<P, H, W, SROWS, MODE, NTHR, 8>(xs, PLANE, d.x, d.x_img, d.slots, n, o0 - 1, d.relu_in, tid,
+                                              d.amax_in);
   __syncthreads();
 
   // per-lane LDS byte offset of each K chunk: lane group kg = lane >> 4 reads
@@ -541,7 +590,7 @@ __device__ __forceinline__ bf16x8 tr_pix_frag(const uint8_t* plane, int pix0, in
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int CIN, int COUT, int H, int W, int R, int MODE>
+template <int CIN, int COUT, int H, int W, int R, int MODE, int DYP>
 __global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
   constexpr int P = CIN / 16, NT = COUT / 16;
   constexpr int WP = W + 2;
@@ -582,7 +631,8 @@ __global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
         const int h = r0 + lh;
         v[k] = make_uint4(0, 0, 0, 0);
         if (i < NDC && lh < R && w < W && h < H)
-          v[k] = *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+          v[k] = DYP ? pool_grad8<H, W>(dyi, d.dy_amax + (int64_t)n * d.dy_img, p, h, w, hf)
+                     : *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
       }
 #pragma unroll
       for (int k = 0; k < DB; ++k) {
@@ -757,10 +807,10 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restri
   }
 }
 
+template <int H, int W>
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restrict__ dy, int64_t dy_img,
-                                                          const uint8_t* __restrict__ amax, int P, int H, int W,
-                                                          int Ho, int Wo, bf16_t* __restrict__ dx, int64_t dx_img,
-                                                          int N) {
+                                                          const uint8_t* __restrict__ amax, int P,
+                                                          bf16_t* __restrict__ dx, int64_t dx_img, int N) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)N * P * H * W * 2;
   if (idx >= total) return;
@@ -770,31 +820,9 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restri
   const int h = (int)(r % H); r /= H;
   const int p = (int)(r % P);
   const int n = (int)(r / P);
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // windows oh with 2 oh - 1 <= h <= 2 oh + 1
-  const int oh0 = h / 2, oh1 = min(Ho - 1, (h + 1) / 2);
-  const int ow0 = w / 2, ow1 = min(Wo - 1, (w + 1) / 2);
-  for (int oh = oh0; oh <= oh1; ++oh) {
-    const int kh = h - (2 * oh - 1);
-    if (kh < 0 || kh > 2) continue;
-    for (int ow = ow0; ow <= ow1; ++ow) {
-      const int kw = w - (2 * ow - 1);
-      if (kw < 0 || kw > 2) continue;
-      const int want = kh * 3 + kw;
-      const int64_t po = (((int64_t)p * Ho + oh) * Wo + ow) * 16 + hf * 8;
-      const uint4 g = *reinterpret_cast<const uint4*>(dy + (int64_t)n * dy_img + po);
-      const uint2 cv = *reinterpret_cast<const uint2*>(amax + (int64_t)n * P * Ho * Wo * 16 + po);
-      const uint32_t gu[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const int cd = ((c < 4 ? cv.x : cv.y) >> (8 * (c & 3))) & 0xff;
-        if (cd == want) acc[c] += bf16_to_f32((bf16_t)((gu[c >> 1] >> (16 * (c & 1))) & 0xffff));
-      }
-    }
-  }
-  const int64_t o = (int64_t)n * dx_img + (((int64_t)p * H + h) * W + w) * 16 + hf * 8;
-  *reinterpret_cast<uint4*>(dx + o) = make_uint4(cvt_pk_bf16(acc[0], acc[1]), cvt_pk_bf16(acc[2], acc[3]),
-                                                 cvt_pk_bf16(acc[4], acc[5]), cvt_pk_bf16(acc[6], acc[7]));
+  constexpr int64_t PIMG = (int64_t)((H + 1) / 2) * ((W + 1) / 2) * 16;
+  const uint4 v = pool_grad8<H, W>(dy + (int64_t)n * dy_img, amax + (int64_t)n * P * PIMG, p, h, w, hf);
+  *reinterpret_cast<uint4*>(dx + (int64_t)n * dx_img + (((int64_t)p * H + h) * W + w) * 16 + hf * 8) = v;
 }
 
 // =====================================================================================
@@ -853,6 +881,8 @@ __global__ void __launch_bounds__(256) sconv_pack_kernel(PackDesc d) {
   X(16, 16, 42, 42, 42, 0, 0)   \
   X(16, 32, 42, 42, 42, 0, 0)   \
   X(32, 16, 42, 42, 21, 0, 0)   \
+  X(32, 16, 42, 42, 21, 4, 0)   \
+  X(32, 32, 21, 21, 21, 4, 0)   \
   X(32, 32, 21, 21, 21, 0, 0)   \
   X(32, 32, 11, 11, 11, 0, 0)
 
@@ -872,15 +902,18 @@ APEX_EXPORT int apex_sconv_fwd(SconvDesc d, int cin, int cout, int H, int W, int
 }
 
 // wgrad bands (LDS: dY band + x band with halo; 2 workgroups per CU)
-#define SCONV_WG_SHAPES(X)   \
-  X(16, 16, 84, 84, 12, 2)   \
-  X(16, 16, 42, 42, 21, 0)   \
-  X(16, 32, 42, 42, 14, 0)   \
-  X(32, 32, 21, 21, 21, 0)   \
-  X(32, 32, 11, 11, 11, 0)
+#define SCONV_WG_SHAPES(X)      \
+  X(16, 16, 84, 84, 12, 2, 1)   \
+  X(16, 16, 84, 84, 12, 2, 0)   \
+  X(16, 16, 42, 42, 21, 0, 0)   \
+  X(16, 32, 42, 42, 14, 0, 1)   \
+  X(16, 32, 42, 42, 14, 0, 0)   \
+  X(32, 32, 21, 21, 21, 0, 1)   \
+  X(32, 32, 21, 21, 21, 0, 0)   \
+  X(32, 32, 11, 11, 11, 0, 0)
 
 APEX_EXPORT int apex_sconv_wgrad_bands(int cin, int cout, int H, int W, int mode) {
-#define SCONV_WG_BANDS(CI, CO, HH, WW, RR, MM) \
+#define SCONV_WG_BANDS(CI, CO, HH, WW, RR, MM, DP) \
   if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) return (HH + RR - 1) / RR;
   SCONV_WG_SHAPES(SCONV_WG_BANDS)
 #undef SCONV_WG_BANDS
@@ -890,10 +923,10 @@ APEX_EXPORT int apex_sconv_wgrad_bands(int cin, int cout, int H, int W, int mode
 APEX_EXPORT int apex_sconv_wgrad(SconvWgDesc d, int cin, int cout, int H, int W, int mode, int groups,
                                  hipStream_t st) {
   if (d.N <= 0 || groups <= 0) return (int)hipErrorInvalidValue;
-#define SCONV_WG_CASE(CI, CO, HH, WW, RR, MM)                                                       \
-  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) {                                \
-    sconv_wgrad_kernel<CI, CO, HH, WW, RR, MM><<<dim3((HH + RR - 1) / RR, groups), 256, 0, st>>>(d); \
-    APEX_CHECK_LAUNCH();                                                                            \
+#define SCONV_WG_CASE(CI, CO, HH, WW, RR, MM, DP)                                                       \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM && (d.dy_amax != nullptr) == (DP != 0)) { \
+    sconv_wgrad_kernel<CI, CO, HH, WW, RR, MM, DP><<<dim3((HH + RR - 1) / RR, groups), 256, 0, st>>>(d);   \
+    APEX_CHECK_LAUNCH();                                                                                \
   }
   SCONV_WG_SHAPES(SCONV_WG_CASE)
 #undef SCONV_WG_CASE
@@ -910,9 +943,12 @@ APEX_EXPORT int apex_maxpool_fwd(const bf16_t* x, int64_t x_img, int P, int H, i
 
 APEX_EXPORT int apex_maxpool_bwd(const bf16_t* dy, int64_t dy_img, const uint8_t* amax, int P, int H, int W,
                                  bf16_t* dx, int64_t dx_img, int N, hipStream_t st) {
-  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const int64_t total = (int64_t)N * P * H * W * 2;
-  maxpool_bwd_kernel<<<(int)((total + 255) / 256), 256, 0, st>>>(dy, dy_img, amax, P, H, W, Ho, Wo, dx, dx_img, N);
+  const int blocks = (int)((total + 255) / 256);
+  if (H == 84 && W == 84) maxpool_bwd_kernel<84, 84><<<blocks, 256, 0, st>>>(dy, dy_img, amax, P, dx, dx_img, N);
+  else if (H == 42 && W == 42) maxpool_bwd_kernel<42, 42><<<blocks, 256, 0, st>>>(dy, dy_img, amax, P, dx, dx_img, N);
+  else if (H == 21 && W == 21) maxpool_bwd_kernel<21, 21><<<blocks, 256, 0, st>>>(dy, dy_img, amax, P, dx, dx_img, N);
+  else return (int)hipErrorInvalidValue;
   APEX_CHECK_LAUNCH();
 }
 

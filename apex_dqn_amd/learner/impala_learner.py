@@ -79,6 +79,9 @@ class FusedImpalaLearner:
             raise ValueError("the IMPALA kernels are built for 4 x 84 x 84 inputs")
         self.A = int(cfg.env_conf.action_dim)
         self.B = int(batch_size or cfg.Learner.replay_sample_size)
+        # max-pool backward: gathered inside the consumers' staging (1) or materialised (0)
+        import os
+        self.fuse_pool_grad = os.environ.get("APEX_IMPALA_FUSE_POOLGRAD", "0") != "0"
         if backend is None:
             backend = "hip" if (self.device.type == "cuda" and self.rt.use_hip_kernels) else "torch"
         on_gpu = backend == "hip"
@@ -166,7 +169,9 @@ class FusedImpalaLearner:
                      amax=torch.zeros(N3, P, php, php, 16, dtype=torch.uint8, device=d))
             f["o"] = (self.feat[:, :FEAT].view(N3, P, php, php, 16) if s == 2 else t(N3, php))
             self.fw.append(f)
-            b = dict(d_yb=t(B, php), d_ra=t(B, php), d_ya=t(B, php), d_p=t(B, php), d_c0=t(B, hw))
+            b = dict(d_yb=t(B, php), d_ra=t(B, php), d_ya=t(B, php), d_p=t(B, php))
+            if not self.fuse_pool_grad:
+                b["d_c0"] = t(B, hw)
             if s < 2:
                 b["d_o"] = t(B, php)    # gradient of this stack's output (the next stack's conv0 dgrad)
             self.bw.append(b)
@@ -313,15 +318,22 @@ class FusedImpalaLearner:
             io.wgrad(b["d_ra"], f["ya"][:B], r0b, *gw(r0b), jobs, relu_in=True)
             io.conv(b["d_ya"], r0a, b["d_p"], transpose=True, mask=f["p"][:B], add=b["d_ra"])
             io.wgrad(b["d_ya"], f["p"][:B], r0a, *gw(r0a), jobs, relu_in=True)
-            io.maxpool_bwd(b["d_p"], f["amax"][:B], b["d_c0"])
+            am = f["amax"][:B]
+            if self.fuse_pool_grad:
+                # the max-pool backward is gathered by the two consumers while they stage
+                # their operand: the full-resolution gradient never reaches HBM
+                dc, kw_w, kw_c = b["d_p"], dict(dy_pool_amax=am), dict(pool_grad=am)
+            else:
+                io.maxpool_bwd(b["d_p"], am, b["d_c0"])
+                dc, kw_w, kw_c = b["d_c0"], {}, {}
             if s == 0:
-                io.wgrad(b["d_c0"], None, c0, *gw(c0), jobs, ring=self.replay.frames, slots=self.slots[:B],
-                         scale=self.rt.obs_scale)
+                io.wgrad(dc, None, c0, *gw(c0), jobs, ring=self.replay.frames, slots=self.slots[:B],
+                         scale=self.rt.obs_scale, **kw_w)
             else:
                 prev = self.fw[s - 1]["o"][:B]
-                io.wgrad(b["d_c0"], prev, c0, *gw(c0), jobs)
+                io.wgrad(dc, prev, c0, *gw(c0), jobs, **kw_w)
                 dO = self.bw[s - 1]["d_o"]
-                io.conv(b["d_c0"], c0, dO, transpose=True)
+                io.conv(dc, c0, dO, transpose=True, **kw_c)
         io.finalize(jobs)
 
     def _seg3(self) -> None:
