@@ -51,7 +51,7 @@ struct SconvDesc {
   int N, n_switch;
   int relu_in, relu_out;
   float scale;                // applied to the accumulator before the bias
-  int pad0;
+  int pad0;                   // POOL: argmax codes for images < pad0 only (0 = all)
   const uint8_t* amax_in;     // MODE 4: argmax codes of the pooled gradient x (same image stride, bytes)
 };
 
@@ -381,6 +381,8 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
     constexpr int HO = (H + 1) / 2, WO = (W + 1) / 2, PR = R / 2;
     __syncthreads();
     uint8_t* __restrict__ am_out = reinterpret_cast<uint8_t*>(d.mask_out);
+    // argmax codes only where a backward follows: images < pad0 (all when pad0 == 0)
+    const bool track = am_out != nullptr && (d.pad0 <= 0 || n < d.pad0);
     for (int it = tid; it < NT * PR * WO * 2; it += NTHR) {
       const int hf = it & 1, r1 = it >> 1;
       const int ow = r1 % WO, r2 = r1 / WO;
@@ -391,26 +393,46 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
       int code[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) { best[c] = -INFINITY; code[c] = 0; }
+      if (track) {
 #pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int lr = 2 * pr + kh;            // conv row 2 oh - 1 + kh relative to o0
+        for (int kh = 0; kh < 3; ++kh) {
+          const int lr = 2 * pr + kh;            // conv row 2 oh - 1 + kh relative to o0
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int wc = 2 * ow - 1 + kw;
-          if (wc < 0 || wc >= W) continue;
-          const uint4 v = *reinterpret_cast<const uint4*>(ot + ((nt * OROWS + lr) * W + wc) * 32 + hf * 16);
-          const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+          for (int kw = 0; kw < 3; ++kw) {
+            const int wc = 2 * ow - 1 + kw;
+            if (wc < 0 || wc >= W) continue;
+            const uint4 v = *reinterpret_cast<const uint4*>(ot + ((nt * OROWS + lr) * W + wc) * 32 + hf * 16);
+            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            const float f = bf16_to_f32((bf16_t)((u[c >> 1] >> (16 * (c & 1))) & 0xffff));
-            if (f > best[c]) { best[c] = f; code[c] = kh * 3 + kw; }
+            for (int c = 0; c < 8; ++c) {
+              const float f = bf16_to_f32((bf16_t)((u[c >> 1] >> (16 * (c & 1))) & 0xffff));
+              if (f > best[c]) { best[c] = f; code[c] = kh * 3 + kw; }
+            }
+          }
+        }
+      } else {
+        // no backward through these images: plain max, two channels per dword
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const int lr = 2 * pr + kh;
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int wc = 2 * ow - 1 + kw;
+            if (wc < 0 || wc >= W) continue;
+            const uint4 v = *reinterpret_cast<const uint4*>(ot + ((nt * OROWS + lr) * W + wc) * 32 + hf * 16);
+            const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              best[2 * c] = fmaxf(best[2 * c], __uint_as_float(u[c] << 16));
+              best[2 * c + 1] = fmaxf(best[2 * c + 1], __uint_as_float(u[c] & 0xffff0000u));
+            }
           }
         }
       }
       const int64_t po = (((int64_t)nt * HO + oh) * WO + ow) * 16 + hf * 8;
       *reinterpret_cast<uint4*>(yi + po) = make_uint4(cvt_pk_bf16(best[0], best[1]), cvt_pk_bf16(best[2], best[3]),
                                                       cvt_pk_bf16(best[4], best[5]), cvt_pk_bf16(best[6], best[7]));
-      if (am_out) {
+      if (track) {
         uint2 cv;
         cv.x = code[0] | (code[1] << 8) | (code[2] << 16) | (code[3] << 24);
         cv.y = code[4] | (code[5] << 8) | (code[6] << 16) | (code[7] << 24);

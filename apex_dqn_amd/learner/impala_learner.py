@@ -213,9 +213,9 @@ class FusedImpalaLearner:
             tg = lambda cs: dict(second=cs.extra["b_tgt"], n_switch=2 * B)  # noqa: E731
             if s == 0:   # conv + max pool in one kernel, straight from the uint8 frame ring
                 io.conv_pool(None, c0, f["p"], f["amax"], ring=self.replay.frames, slots=self.slots,
-                             scale=rt.obs_scale, **tg(c0))
+                             scale=rt.obs_scale, amax_rows=B, **tg(c0))
             else:
-                io.conv_pool(x, c0, f["p"], f["amax"], **tg(c0))
+                io.conv_pool(x, c0, f["p"], f["amax"], amax_rows=B, **tg(c0))
             # residual blocks: one kernel each; the mid activations are kept for the
             # B training rows only (the backward's ReLU masks / weight-gradient inputs)
             io.resblock(f["p"], r0a, r0b, f["ra"], ysave=f["ya"], n_save=B, target=True, n_switch=2 * B)

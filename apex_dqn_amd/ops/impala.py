@@ -161,11 +161,16 @@ class HipImpalaOps:
 
     # -- convs
     def conv_pool(self, x, spec: ConvSpec, y, amax, *, second=None, n_switch=0, scale=1.0, ring=None,
-                  slots=None) -> None:
-        """y = maxpool3x3s2(conv3x3(x) * scale + b) (+ argmax codes): the fused stack-entry
-        kernel; the full-resolution conv output stays in LDS."""
-        self.conv(x, spec, y, second=second, n_switch=n_switch, scale=scale, ring=ring, slots=slots,
-                  _pool_amax=amax)
+                  slots=None, amax_rows: int = 0) -> None:
+        """y = maxpool3x3s2(conv3x3(x) * scale + b) (+ argmax codes for images <
+        ``amax_rows``, all if 0): the fused stack-entry kernel; the full-resolution
+        conv output stays in LDS."""
+        self._amax_rows = int(amax_rows)
+        try:
+            self.conv(x, spec, y, second=second, n_switch=n_switch, scale=scale, ring=ring, slots=slots,
+                      _pool_amax=amax)
+        finally:
+            self._amax_rows = 0
 
     def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
              bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None, pool_grad=None,
@@ -178,6 +183,7 @@ class HipImpalaOps:
         pool = _pool_amax is not False
         if pool:
             d.mask_out = _lib.ptr(_pool_amax)
+            d.pad0 = getattr(self, "_amax_rows", 0)
         N = y.shape[0]
         if ring is not None:   # 4 frames from the s2d ring, tap-pair K (fragments packed with mode 2)
             d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
@@ -310,7 +316,7 @@ class TorchImpalaOps:
         return w
 
     def conv_pool(self, x, spec: ConvSpec, y, amax, *, second=None, n_switch=0, scale=1.0, ring=None,
-                  slots=None) -> None:
+                  slots=None, amax_rows: int = 0) -> None:
         N = y.shape[0]
         c0 = torch.zeros(N, spec.cout // 16, spec.H, spec.W, 16, dtype=y.dtype, device=y.device)
         self.conv(x, spec, c0, second=second, n_switch=n_switch, scale=scale, ring=ring, slots=slots)
