@@ -80,10 +80,10 @@ class FusedNatureLearner:
         self.world = comm.world_size if comm is not None else 1
         self._alloc(self.B)
         self._graphs = None
-        # optional: weight-gradient GEMMs on a side stream beside the dgrad chain
-        # (they only read dY / activations), captured into the same graph(s).  Off
-        # by default: at B=512 the concurrent kernels contend for LDS-limited CU
-        # slots and Infinity-Cache bandwidth (2680 vs 2832 steps/s measured).
+        # weight-gradient GEMMs on a side stream beside the dgrad chain (they only
+        # read dY / activations), captured into the same graph(s): on by default
+        # since the image-resident conv1 kernels (3315 -> 3385 steps/s measured; with
+        # the earlier kernels the concurrent GEMMs contended, 2680 vs 2832).
         # The side stream always carries the small latency-bound kernels that only
         # need the head's outputs (head wgrad, priority write-back into the sum-tree):
         # a few blocks each, they run beside the backward GEMMs instead of between them.
