@@ -47,6 +47,9 @@ struct ConvDesc {
   int koff[16];
   int tile_hint;              // 0 auto, 1 BM=128, 2 BM=64
   int order_hint;             // 0 auto, 1 M tiles fastest per XCD, 2 N tiles fastest
+  float* part;                // split-K (dense mode): fp32 partials [ksplit][M][ldy]
+  int ksplit;                 // > 1: blockIdx.z = K split; dense_splitk_reduce applies bias / ReLU
+  int pad1;
 };
 
 struct WgradDesc {
@@ -114,7 +117,10 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     by = r % gridDim.y;
     bz = r / gridDim.y;
   }
-  const int cls = bz;
+  // dense split-K: blockIdx.z is the K split (no weight classes in dense mode)
+  const bool splitk = MODE == 0 && d.ksplit > 1;
+  const int kz = splitk ? bz : 0;
+  const int cls = splitk ? 0 : bz;
   const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
   const uint32_t OWv = OWC ? OWC : d.OW;
   const int M = d.N * OHW;
@@ -124,7 +130,9 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const bool second = d.w2 != nullptr && m0 >= d.m_switch;
   const bf16_t* __restrict__ wb = (second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride;
   const float* __restrict__ bias = second ? d.bias2 : d.bias;
-  const int KT = d.K >> 6;
+  const int KT_all = d.K >> 6;
+  const int kt0 = splitk ? (kz * KT_all) / d.ksplit : 0;
+  const int KT = splitk ? ((kz + 1) * KT_all) / d.ksplit - kt0 : KT_all;
   const int sc = tid & 7;
   const int srow = tid >> 3;
   const __amdgpu_buffer_rsrc_t ra_rs = buf_rsrc(d.x);
@@ -138,7 +146,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     const int m = m0 + srow + 32 * i;
     const int mm = m < M ? m : 0;
     if (MODE == 0) {
-      a_off[i] = ((uint32_t)mm * d.K + sc * 8) * 2u;
+      a_off[i] = ((uint32_t)mm * d.K + sc * 8 + kt0 * 64) * 2u;
       vmask[i] = 0;
     } else {
       const int img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
@@ -157,7 +165,8 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
       vmask[i] = vm;
     }
   }
-  const uint32_t b_off0 = BT ? (uint32_t)((srow * d.ldb + n0 + sc * 8) * 2) : (uint32_t)(((n0 + srow) * d.K + sc * 8) * 2);
+  const uint32_t b_off0 = BT ? (uint32_t)((srow * d.ldb + n0 + sc * 8) * 2)
+                             : (uint32_t)(((n0 + srow) * d.K + sc * 8 + kt0 * 64) * 2);
   const uint32_t b_off1 = b_off0 + (BT ? 64u * d.ldb : 64u * d.K);
   const int cpb = d.Cin >> 6;
 
@@ -257,6 +266,21 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     load_next(RA);                      // tile kt+4
   }
   if (kt < KT) compute(0);              // odd KT: last tile sits in buffer 0
+  if (splitk) {
+    // fp32 partial tile straight from the accumulators (lane: 4 consecutive channels
+    // of one row per 16x16 block), reduced + biased + ReLU'd by dense_splitk_reduce
+    const int g = lane >> 4, pl = lane & 15;
+    float* __restrict__ part = d.part + (int64_t)kz * M * d.ldy;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = m0 + WR * wv + 16 * mt + pl;
+      if (m >= M) continue;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        *reinterpret_cast<f32x4*>(part + (int64_t)m * d.ldy + n0 + 16 * nt + 4 * g) = acc[mt][nt] * d.in_scale;
+    }
+    return;
+  }
   __syncthreads();
 
   // ---- epilogue: (acc*scale + bias) -> bf16x4 per lane -> swizzled LDS image -> 16-B row stores
@@ -666,6 +690,26 @@ static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
   else igemm_fwd_kernel<1, false, false, 0, 0, BM><<<grid, 256, 0, st>>>(d);
 }
 
+// out[m][n] = act(sum_z part[z][m][n] + bias[n]) as bf16 (bias2 for rows >= m_switch)
+__global__ void __launch_bounds__(256) dense_splitk_reduce_kernel(ConvDesc d, int M) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;      // 4 outputs per thread
+  const int n4 = d.Cout >> 2;
+  if (i >= (int64_t)M * n4) return;
+  const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
+  f32x4 v = *reinterpret_cast<const f32x4*>(d.part + (int64_t)m * d.ldy + n);
+  for (int z = 1; z < d.ksplit; ++z) v += *reinterpret_cast<const f32x4*>(d.part + ((int64_t)z * M + m) * d.ldy + n);
+  const float* bias = (d.w2 != nullptr && m >= d.m_switch) ? d.bias2 : d.bias;
+  if (bias) {
+    const float4 b = *reinterpret_cast<const float4*>(bias + n);
+    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+  }
+  if (d.relu) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+  }
+  *reinterpret_cast<uint2*>(d.y + (int64_t)m * d.ldy + n) = make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+}
+
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if ((d.K & 63) || (d.Cout & 63) || d.K <= 0) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
@@ -687,6 +731,14 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.tile_hint == 1) bm64 = false;
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
+  if (d.ksplit > 1) {
+    if (d.mode != 0 || d.bt || d.mask || d.part == nullptr || d.ksplit > (d.K >> 6)) return (int)hipErrorInvalidValue;
+    if (bm64) launch_fwd<64>(d, dim3((M + 63) / 64, d.Cout / FWD_BN, d.ksplit), st);
+    else launch_fwd<128>(d, dim3((M + 127) / 128, d.Cout / FWD_BN, d.ksplit), st);
+    const int64_t nthr = (int64_t)M * (d.Cout / 4);
+    dense_splitk_reduce_kernel<<<(int)((nthr + 255) / 256), 256, 0, st>>>(d, M);
+    APEX_CHECK_LAUNCH();
+  }
   if (bm64) launch_fwd<64>(d, dim3((M + 63) / 64, d.Cout / FWD_BN, ncls), st);
   else launch_fwd<128>(d, dim3((M + 127) / 128, d.Cout / FWD_BN, ncls), st);
   APEX_CHECK_LAUNCH();

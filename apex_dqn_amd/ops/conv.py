@@ -123,9 +123,22 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
     _launch_fwd(lib, d)
 
 
+# split-K of the dense forward GEMM (fc): the 1536 x 1024 output of the NatureCNN
+# learner is only 192 128x64 tiles for 256 CUs; splitting its K = 3136 fills the
+# chip, and one elementwise pass sums the fp32 partials + bias + ReLU (APEX_FC_KSPLIT)
+import os as _os
+DENSE_KSPLIT = int(_os.environ.get("APEX_FC_KSPLIT", "0"))   # 0 = auto
+
+
+def _dense_ksplit(M: int, Nc: int, K: int) -> int:
+    # auto = 1: measured on the learner step (B=512), split 2/3/4 did not beat the
+    # unsplit 192-tile launch (3314 / 3320 / 3293 / 3307 steps/s) -- kept as an option
+    return DENSE_KSPLIT or 1
+
+
 def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
               relu: bool = True, mask: Optional[torch.Tensor] = None, w2=None, b2=None,
-              rows_first: int = 0) -> None:
+              rows_first: int = 0, ws: Optional["Workspace"] = None) -> None:
     """out[M,N] = act(x[M,K] @ w[N,K]^T + b)  (or * (mask > 0))."""
     M, K = x.shape
     Nc = w.shape[0]
@@ -133,6 +146,10 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), mask=_lib.ptr(mask),
                    N=M, Cin=K, Cout=Nc, mode=0, relu=relu and mask is None, K=K,
                    **_second(w2, b2, rows_first, 1))
+    ks = _dense_ksplit(M, Nc, K) if (ws is not None and mask is None) else 1
+    if ks > 1:
+        part = ws.get(("dense_part", M, Nc), ks * M * Nc, x.device)
+        d.part, d.ksplit = part.data_ptr(), ks
     _launch_fwd(lib, d)
 
 

@@ -218,7 +218,7 @@ class HipBackend(TorchBackend):
         if not self.native_conv:
             return super().fc_fwd(x, w, b, out, w2, b2, rows_first)
         C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True, w2=w2, b2=b2,
-                    rows_first=rows_first)
+                    rows_first=rows_first, ws=self.ws)
 
     def fc_dgrad(self, dh, x, w, dx_out):
         if not self.native_conv:

@@ -88,6 +88,32 @@ def test_dense_fwd_relu_and_mask(M):
     assert _rel(out3, ref3) < 1e-2
 
 
+@pytest.mark.parametrize("ks", [2, 3, 4])
+def test_dense_fwd_split_k(ks):
+    """Split-K dense forward (fp32 partials + reduce/bias/ReLU pass) == unsplit, incl.
+    the online/target weight switch at a 128-row boundary."""
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(ks)
+    M = 768
+    x = _bf(torch.relu(torch.randn(M, 3136, generator=g)))
+    w = _bf(torch.randn(1024, 3136, generator=g) * 0.02)
+    w2 = _bf(torch.randn(1024, 3136, generator=g) * 0.02)
+    b = (torch.randn(1024, generator=g) * 0.1).to(DEV)
+    b2 = (torch.randn(1024, generator=g) * 0.1).to(DEV)
+    ref = torch.empty(M, 1024, dtype=torch.bfloat16, device=DEV)
+    C.dense_fwd(_lib(), x, w, b, ref, relu=True, w2=w2, b2=b2, rows_first=512)
+    old = C.DENSE_KSPLIT
+    C.DENSE_KSPLIT = ks
+    try:
+        out = torch.empty_like(ref)
+        C.dense_fwd(_lib(), x, w, b, out, relu=True, w2=w2, b2=b2, rows_first=512, ws=C.Workspace())
+    finally:
+        C.DENSE_KSPLIT = old
+    torch.testing.assert_close(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
+    exact = torch.cat([R.fc_fwd(x[:512].float(), w.float(), b), R.fc_fwd(x[512:].float(), w2.float(), b2)])
+    assert _rel(out, exact) < 1e-2
+
+
 def test_pack_dgrad_weights():
     from apex_dqn_amd.ops import conv as C
     g = torch.Generator(device="cpu").manual_seed(3)
