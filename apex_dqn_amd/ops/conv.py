@@ -73,6 +73,12 @@ def _second(w2, b2, rows_first, per_row):
     return dict(w2=w2.data_ptr(), bias2=_lib.ptr(b2), m_switch=m_switch)
 
 
+def _split_ok(w2, rows_first: int, per_row: int) -> bool:
+    """One launch can switch weight sets at rows_first only on a 128-row tile
+    boundary (the switch is block-uniform); otherwise the caller issues two."""
+    return w2 is None or (rows_first * per_row) % 128 == 0
+
+
 def _launch_fwd(lib, d) -> None:
     _lib.check(lib.apex_conv_fwd(d, _lib.stream_ptr()), "conv_fwd")
 
@@ -117,6 +123,10 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     OH, OW = out.shape[1], out.shape[2]
+    if not _split_ok(w2, rows_first, OH * OW):   # batch not tile-aligned: one launch per weight set
+        conv_fwd(lib, x[:rows_first], w, b, stride, out[:rows_first])
+        conv_fwd(lib, x[rows_first:], w2, b2, stride, out[rows_first:])
+        return
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=b.data_ptr(), y=out.data_ptr(), N=N, H=H, W=W,
                    Cin=Cin, OH=OH, OW=OW, Cout=Cout, KH=KH, KW=KW, stride=stride, mode=1, relu=1,
                    K=KH * KW * Cin, **_second(w2, b2, rows_first, OH * OW))
@@ -143,6 +153,11 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
     M, K = x.shape
     Nc = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, Nc)
+    if not _split_ok(w2, rows_first, 1):         # batch not tile-aligned: one launch per weight set
+        m1, m2 = (None, None) if mask is None else (mask[:rows_first], mask[rows_first:])
+        dense_fwd(lib, x[:rows_first], w, b, out[:rows_first], relu, m1, ws=ws)
+        dense_fwd(lib, x[rows_first:], w2, b2, out[rows_first:], relu, m2, ws=ws)
+        return
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), mask=_lib.ptr(mask),
                    N=M, Cin=K, Cout=Nc, mode=0, relu=relu and mask is None, K=K,
                    **_second(w2, b2, rows_first, 1))
