@@ -96,6 +96,9 @@ class RuntimeConf:
     resume: bool = True             # continue from ckpt_dir/checkpoint.pt when it exists (restarts)
     allreduce_dtype: str = "fp32"   # DP gradient all-reduce payload: "fp32" (exact) | "bf16" (half the bytes)
     overlap_wgrad: bool = True      # weight-gradient GEMMs on a side stream beside the dgrad chain (+2% measured)
+    presample: bool = False         # draw step t+1's batch inside step t beside the optimizer (fused learner;
+                                    # measured slower: the extra cross-stream graph edges cost more than
+                                    # the 9 us sample they hide, 3153 vs 3360 steps/s)
                                     # (measured slower on MI355X at B=512: the kernels contend)
     actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)
     replay_capacity: Optional[int] = None  # physical capacity (default: soft_capacity * 1.25)

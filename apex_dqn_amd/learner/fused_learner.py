@@ -106,6 +106,16 @@ class FusedNatureLearner:
         if self.world > 1:
             self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d)
             self._init_ratio()
+        # next-batch pre-sampling: the batch of step t+1 is drawn inside step t, on
+        # the side stream right after step t's priority write-back and its last read
+        # of the sample buffers (conv1 wgrad), so it overlaps the gradient
+        # finalisation + optimizer instead of heading step t+1.  Same draws as
+        # sampling at the head of t+1: the tree is identical (nothing device-side
+        # touches it in between); host-side mutations (inserts, eviction, rebuild)
+        # bump replay.version and force a fresh sample at the head of t+1.  Off by
+        # default: in the HIP graph the extra fork/join costs more than it hides.
+        self._presample = bool(self.rt.presample)
+        self._sample_ver = None
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
@@ -175,8 +185,9 @@ class FusedNatureLearner:
         """sample, forward (online+target), loss/priorities, head + fc weight gradients."""
         B, rt, ops = self.B, self.rt, self.ops
         ops.prepare(self.Pb)
-        # the sampler writes the frame-ring slots of S_t / S_{t+n} (twice) into self.slots
-        S = self.replay.sample(B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * B:])
+        if not self._presample or self._sample_ver != self.replay.version:
+            self._sample()
+        S = self.S
         self._mark("sample")
         # conv1 reads the uint8 frame stacks straight from the replay ring by slot
         self.forward_all()
@@ -199,6 +210,12 @@ class FusedNatureLearner:
                 self.gcomm[cut:].copy_(self.g32[cut:])
         self._mark("fc_wgrad")
 
+    def _sample(self) -> None:
+        """The sampler writes idx / IS weights / records and the frame-ring slots of
+        S_t, S_{t+n} (twice: online and target rows) into the step's buffers."""
+        self.replay.sample(self.B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * self.B:])
+        self._sample_ver = self.replay.version
+
     def _seg2(self) -> None:
         """fc dgrad + conv backward (with DP, all of it overlaps the fc/heads bucket
         all-reduce): the dgrad chain, conv3/conv2 wgrad (side stream when
@@ -215,11 +232,16 @@ class FusedNatureLearner:
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"], jobs=jobs)
         self._join_side()      # head wgrad (side stream) done: its region enters the norm
+        if self._presample:    # the last read of the sample buffers is done: draw step t+1's batch
+            with self._on_side():
+                self._sample()
         norm = dict(part=self.norm_part, slot0=self._fc_slots, total=self.norm_total) if self._fuse_norm else None
         ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
         if self._comm_bf16:
             cut = self.layout.offsets["wfc"]
             self.gcomm[:cut].copy_(self.g32[:cut])
+        if self.world > 1:
+            self._join_side()  # a graph segment must rejoin its forked streams
         self._mark("conv_backward")
 
     # ------------------------------------------------------- phase timing
@@ -279,6 +301,7 @@ class FusedNatureLearner:
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
                       norm_total=self.norm_total if self._fuse_norm else None)
+        self._join_side()      # the pre-sample of the next batch ran beside the optimizer
         self._mark("optimizer")
         if self.world > 1:
             # local min_i p_i / total for the global IS-weight normaliser (all-reduced MIN after the step)
@@ -325,6 +348,8 @@ class FusedNatureLearner:
         graphs = self.rt.use_graphs and self.device.type == "cuda"
         if graphs and self._graphs is None:
             self._capture()
+        if graphs and self._presample and self._sample_ver != self.replay.version:
+            self._sample()     # host-side replay mutation since the pre-sample: redraw
         if self.world > 1:
             self._dp_step(graphs)
         elif graphs:
@@ -347,6 +372,8 @@ class FusedNatureLearner:
                 self._step_body()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._restore(snap)
+        if self._presample:    # the graphs start from a drawn batch (their seg1 holds no sample)
+            self._sample()
         torch.cuda.synchronize(self.device)
         if self.world == 1:
             g = torch.cuda.CUDAGraph()

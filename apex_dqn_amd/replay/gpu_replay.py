@@ -95,6 +95,10 @@ class GpuReplayShard:
         self.live = 0
         self.frame_head = 0    # next frame sequence number
         self.total_inserted = 0
+        # bumped by every host-side mutation of the sampling state (inserts, frames,
+        # eviction, rebuild): a learner that samples its next batch ahead of time
+        # (inside the previous step) resamples when this changed in between
+        self.version = 0
         self.min_frame_seq = np.full(self.cap, -1, np.int64)  # oldest frame referenced per slot
         self._tdesc = None
         self._rdesc = None
@@ -129,6 +133,7 @@ class GpuReplayShard:
     # --------------------------------------------------------------- insert
     def append_frames(self, frames) -> np.ndarray:
         """Store new frames (n, H, W) uint8; returns their sequence numbers."""
+        self.version += 1
         frames = torch.as_tensor(frames)
         n = frames.shape[0]
         seqs = self.frame_head + np.arange(n, dtype=np.int64)
@@ -152,6 +157,7 @@ class GpuReplayShard:
 
     def insert(self, batch: Dict[str, np.ndarray]) -> np.ndarray:
         """Insert n-step transitions whose S_t/S_tpn payloads are frame seqs (K, C)."""
+        self.version += 1
         K = len(batch["A_t"])
         if K == 0:
             return np.zeros(0, np.int64)
@@ -295,6 +301,7 @@ class GpuReplayShard:
 
     def remove_to_fit(self) -> int:
         """FIFO eviction to soft_capacity + drop slots whose frames were overwritten."""
+        self.version += 1
         excess = self.live - self.soft_capacity
         n_ev = 0
         if excess > 0:
@@ -317,6 +324,7 @@ class GpuReplayShard:
 
     def rebuild(self) -> None:
         """Exact recompute of all internal nodes and the min (drift guard)."""
+        self.version += 1
         if self.use_hip:
             _lib.check(self.lib.apex_tree_rebuild(self.tree_desc(), self._stream()), "tree_rebuild")
         else:

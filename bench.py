@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--presample", action="store_true",
+                    help="draw step t+1's batch inside step t, beside the optimizer (default off)")
     ap.add_argument("--no-overlap-wgrad", action="store_true",
                     help="weight-gradient GEMMs serialised with the dgrad chain (default: side stream)")
     ap.add_argument("--graph-impala", action="store_true",
@@ -72,7 +74,8 @@ def main():
                     "min_replay_mem_size": 0},
         "Replay_Memory": {"soft_capacity": args.replay},
         "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
-                    "seed": 1234 + rank, "network": args.network, "overlap_wgrad": not args.no_overlap_wgrad},
+                    "seed": 1234 + rank, "network": args.network, "overlap_wgrad": not args.no_overlap_wgrad,
+                    "presample": args.presample},
     })
     cap = args.replay
     frames_cap = cap + 4096

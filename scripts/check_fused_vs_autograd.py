@@ -6,7 +6,7 @@ from apex_dqn_amd.learner.torch_learner import TorchLearner
 from apex_dqn_amd.learner.losses import ddqn_loss
 torch.manual_seed(0)
 cfg = ApexConfig.from_dict({"env_conf":{"state_shape":[4,84,84],"action_dim":6,"name":"Synthetic"},
-  "Learner":{"replay_sample_size":8}, "Runtime":{"grad_clip":40.0}})
+  "Learner":{"replay_sample_size":8}, "Runtime":{"grad_clip":40.0, "presample":False}})
 rp = GpuReplayShard(1000, 1000, 2000, 4, device="cpu")
 rng = np.random.default_rng(0)
 seqs = rp.append_frames(rng.integers(0,255,(300,84,84),dtype=np.uint8))

@@ -14,7 +14,8 @@ def _setup(loss="huber", A=6, network="nature64"):
     torch.manual_seed(0)
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": A, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": 8},
-                                "Runtime": {"grad_clip": 40.0, "loss": loss, "network": network}})
+                                "Runtime": {"grad_clip": 40.0, "loss": loss, "network": network,
+                                            "presample": False}})
     rp = GpuReplayShard(400, 400, 600, 4, device="cpu")
     rng = np.random.default_rng(0)
     seqs = rp.append_frames(rng.integers(0, 255, (300, 84, 84), dtype=np.uint8))
@@ -83,3 +84,30 @@ def test_fused_step_updates_params_and_priorities():
     idx = L.S["idx"]
     assert not torch.equal(leaf0[idx], rp.leaf[idx])
     assert L.num_q_updates == 1
+
+
+def test_presample_draws_the_same_batches():
+    """Drawing step t+1's batch inside step t (beside the optimizer) yields exactly the
+    batches of sampling at the head of each step, and host-side replay mutations in
+    between force a redraw."""
+    import copy
+    runs = {}
+    for pre in (False, True):
+        cfg, rp = _setup()
+        cfg = copy.deepcopy(cfg)
+        cfg.Runtime.presample = pre
+        torch.manual_seed(0)
+        L = FusedNatureLearner(cfg, "cpu", rp)
+        seen = []
+        for t in range(4):
+            if t == 2:                      # host-side mutation between steps
+                rp.remove_to_fit()
+                rp.rebuild()
+            L._seg1()
+            seen.append(L.S["idx"].clone())
+            L._seg2()
+            L._seg3()
+        runs[pre] = (seen, L.p32.clone())
+    for a, b in zip(runs[False][0], runs[True][0]):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(runs[False][1], runs[True][1], rtol=0, atol=0)

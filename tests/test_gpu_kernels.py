@@ -206,7 +206,8 @@ def test_fused_learner_step_hip_vs_torch_backend():
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
-                                "Learner": {"replay_sample_size": 64}, "Runtime": {"use_graphs": False}})
+                                "Learner": {"replay_sample_size": 64},
+                                "Runtime": {"use_graphs": False, "presample": False}})
     res = {}
     for be in ("hip", "torch"):
         torch.manual_seed(0)
