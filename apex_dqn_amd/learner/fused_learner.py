@@ -22,6 +22,7 @@ The step can be captured once and replayed as a HIP graph (``use_graphs``).
 from __future__ import annotations
 
 import contextlib
+import os
 
 from typing import Any, Dict, Optional
 
@@ -87,7 +88,7 @@ class FusedNatureLearner:
         # The side stream always carries the small latency-bound kernels that only
         # need the head's outputs (head wgrad, priority write-back into the sum-tree):
         # a few blocks each, they run beside the backward GEMMs instead of between them.
-        self._side = torch.cuda.Stream(d) if d.type == "cuda" else None
+        self._side = torch.cuda.Stream(d) if (d.type == "cuda" and os.environ.get("APEX_NO_SIDE_STREAM", "0") == "0") else None
         # DP gradient payload: fp32 in place, or a bf16 copy (cast inside the captured
         # segments, summed by RCCL in bf16, cast back before the optimizer)
         if self.rt.allreduce_dtype not in ("fp32", "bf16"):
