@@ -579,13 +579,16 @@ __global__ void __launch_bounds__(512) resblock_fwd_kernel(ResDesc d) {
 
 #define RESBLOCK_SHAPES(X) \
   X(16, 42, 21)            \
+  X(16, 42, 14)            \
+  X(16, 42, 11)            \
   X(32, 21, 21)            \
   X(32, 11, 11)
 
-APEX_EXPORT int apex_resblock_fwd(ResDesc d, int C, int HW, hipStream_t st) {
+// band rows R: 0 = default (the first listed for the shape)
+APEX_EXPORT int apex_resblock_fwd(ResDesc d, int C, int HW, int R, hipStream_t st) {
   if (d.N <= 0) return 0;
 #define RESBLOCK_CASE(CC, HH, RR)                                                           \
-  if (C == CC && HW == HH) {                                                                \
+  if (C == CC && HW == HH && (R == 0 || R == RR)) {                                         \
     resblock_fwd_kernel<CC, HH, RR><<<dim3((HH + RR - 1) / RR, d.N), 512, 0, st>>>(d);      \
     APEX_CHECK_LAUNCH();                                                                    \
   }

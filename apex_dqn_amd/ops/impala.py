@@ -67,7 +67,7 @@ _SIGS = {
     "apex_maxpool_fwd": ([c_p, c_i64, c_i, c_i, c_i, c_p, c_i64, c_p, c_i, c_p], c_i),
     "apex_maxpool_bwd": ([c_p, c_i64, c_p, c_i, c_i, c_i, c_p, c_i64, c_i, c_p], c_i),
     "apex_sconv_pack": ([PackDesc, c_p], c_i),
-    "apex_resblock_fwd": ([ResDesc, c_i, c_i, c_p], c_i),
+    "apex_resblock_fwd": ([ResDesc, c_i, c_i, c_i, c_p], c_i),
     "apex_sconv_wgrad_reduce": ([WgRedDesc, c_p], c_i),
     "apex_sconv_frag_elems": ([c_i, c_i], c_i64),
 }
@@ -126,6 +126,10 @@ class ConvSpec:
 import os as _os
 WGRAD_TUNING = {"target_wgs": int(_os.environ.get("APEX_IMPALA_WG_TARGET", "512")),
                 "slab_cap": int(_os.environ.get("APEX_IMPALA_SLAB_CAP", str(2 << 20)))}
+
+
+# fused residual block: rows per workgroup band per (channels, size); 0 = kernel default
+RESBLOCK_BANDS = {(16, 42): int(_os.environ.get("APEX_RESBLOCK_R16", "14"))}   # swept: 21 777, 14 786, 11 778
 
 
 # ------------------------------------------------------------------ HIP backend
@@ -228,7 +232,8 @@ class HipImpalaOps:
             d.ysave, d.ysave_img, d.n_save = ysave.data_ptr(), img_stride(ysave), int(n_save)
         d.out, d.out_img = out.data_ptr(), img_stride(out)
         d.N, d.relu_out = x.shape[0], int(relu_out)
-        _lib.check(self.lib.apex_resblock_fwd(d, c0.cin, c0.H, _lib.stream_ptr()), f"resblock_fwd[{c0.name}]")
+        R = RESBLOCK_BANDS.get((c0.cin, c0.H), 0)
+        _lib.check(self.lib.apex_resblock_fwd(d, c0.cin, c0.H, R, _lib.stream_ptr()), f"resblock_fwd[{c0.name}]")
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
               groups: int = 0, scale: float = 1.0, dy_pool_amax=None) -> None:
