@@ -95,11 +95,10 @@ class RuntimeConf:
     torch_profile_steps: int = 5
     resume: bool = True             # continue from ckpt_dir/checkpoint.pt when it exists (restarts)
     allreduce_dtype: str = "fp32"   # DP gradient all-reduce payload: "fp32" (exact) | "bf16" (half the bytes)
-    overlap_wgrad: bool = True      # weight-gradient GEMMs on a side stream beside the dgrad chain (+2% measured)
-    presample: bool = False         # draw step t+1's batch inside step t beside the optimizer (fused learner;
-                                    # measured slower: the extra cross-stream graph edges cost more than
-                                    # the 9 us sample they hide, 3153 vs 3360 steps/s)
-                                    # (measured slower on MI355X at B=512: the kernels contend)
+    overlap_wgrad: bool = False     # weight-gradient GEMMs on a side stream beside the dgrad chain (slower in the
+                                    # HIP graph since the tree kernels were fused: 3317 vs 3454 steps/s)
+    presample: bool = True          # draw step t+1's batch at the end of step t (fused learner; on the HIP
+                                    # backend inside the optimizer launch)
     actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)
     replay_capacity: Optional[int] = None  # physical capacity (default: soft_capacity * 1.25)
     heartbeat_timeout: float = 60.0

@@ -726,8 +726,10 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   const int64_t blocks128 = (int64_t)((M + 127) / 128) * (d.Cout / FWD_BN) * ncls;
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
   // measured (scripts/bench_kernels.py sweep): 64-row tiles pay off for the dgrad
-  // GEMMs (K-major B): conv3/conv2 dgrad and fc dgrad; 128 for the forward GEMMs
-  bool bm64 = d.bt != 0 && (pad || blocks128 < 640);
+  // GEMMs (K-major B): conv3/conv2 dgrad and fc dgrad; 128 for the conv forward
+  // GEMMs; 64 for a forward grid of < 1 block per CU (the fc: 192 -> 384 blocks,
+  // 3446 -> 3491 steps/s end to end)
+  bool bm64 = d.bt != 0 ? (pad || blocks128 < 640) : blocks128 < 256;
   if (d.tile_hint == 1) bm64 = false;
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;

@@ -19,90 +19,7 @@
 //   act int32, rew/gam/isw fp32
 // Outputs: td_abs[B], loss[B], q_t[B,A] (optional), dH[B,1024] bf16 (gradient
 // at the pre-ReLU stream outputs), dhead[B,1+A] fp32 (d value, d advantage).
-#include "apex_common.h"
-
-#define HEAD_MAXA 32
-
-struct HeadParams {
-  const float* wv;
-  const float* bv;
-  const float* wa;
-  const float* ba;
-};
-
-// NPL consecutive fp32 weights (16-B aligned: NPL is 4 or 8) as float4 loads
-template <int NPL>
-__device__ __forceinline__ void load_w(const float* __restrict__ p, float* w) {
-#pragma unroll
-  for (int k = 0; k < NPL; k += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(p + k);
-    w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
-  }
-}
-
-// bf16 elements k of a packed row chunk (k < 2 * dwords)
-__device__ __forceinline__ float bf16_at(const uint32_t* u, int k) {
-  return __uint_as_float((k & 1) ? (u[k >> 1] & 0xffff0000u) : (u[k >> 1] << 16));
-}
-
-// q-values of one 2*HS-wide activation row (HS = stream width: 512 NatureCNN, 256
-// IMPALA): lane holds cols lane*NPL..+NPL-1 of each stream, NPL = HS / 64
-template <int HS>
-__device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const HeadParams& P, int A,
-                                         int lane, float* q, float* hv, float* ha) {
-  constexpr int NPL = HS / 64;
-  uint32_t wv_[NPL / 2], wa_[NPL / 2];
-  if constexpr (NPL == 8) {
-    const uint4 rv = *reinterpret_cast<const uint4*>(row + lane * 8);
-    const uint4 ra = *reinterpret_cast<const uint4*>(row + HS + lane * 8);
-    wv_[0] = rv.x; wv_[1] = rv.y; wv_[2] = rv.z; wv_[3] = rv.w;
-    wa_[0] = ra.x; wa_[1] = ra.y; wa_[2] = ra.z; wa_[3] = ra.w;
-  } else {
-    const uint2 rv = *reinterpret_cast<const uint2*>(row + lane * 4);
-    const uint2 ra = *reinterpret_cast<const uint2*>(row + HS + lane * 4);
-    wv_[0] = rv.x; wv_[1] = rv.y;
-    wa_[0] = ra.x; wa_[1] = ra.y;
-  }
-#pragma unroll
-  for (int k = 0; k < NPL; ++k) {
-    hv[k] = bf16_at(wv_, k);
-    ha[k] = bf16_at(wa_, k);
-  }
-  float part[HEAD_MAXA + 1];
-  {
-    float w[NPL], s = 0.f;
-    load_w<NPL>(P.wv + lane * NPL, w);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) s += hv[k] * w[k];
-    part[0] = s;
-  }
-#pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
-    if (j < A) {
-      float w[NPL], s = 0.f;
-      load_w<NPL>(P.wa + j * HS + lane * NPL, w);
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) s += ha[k] * w[k];
-      part[j + 1] = s;
-    } else {
-      part[j + 1] = 0.f;
-    }
-  }
-  float v = wave_sum_dpp(part[0]) + P.bv[0];
-  float amean = 0.f;
-#pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
-    if (j < A) {
-      float a = wave_sum_dpp(part[j + 1]) + P.ba[j];
-      part[j + 1] = a;
-      amean += a;
-    }
-  }
-  amean /= (float)A;
-#pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j)
-    if (j < A) q[j] = v + part[j + 1] - amean;
-}
+#include "head_common.h"
 
 template <int HS>
 __global__ void __launch_bounds__(192) ddqn_head_kernel(
@@ -111,108 +28,9 @@ __global__ void __launch_bounds__(192) ddqn_head_kernel(
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
     bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n) {
-  __shared__ float qs[2][HEAD_MAXA];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b = blockIdx.x;
-  // zero the head-gradient region that head_wgrad accumulates into (stream-ordered)
-  if (zero_ptr != nullptr) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += gridDim.x * blockDim.x) zero_ptr[i] = 0.f;
-  }
-  constexpr int NPL = HS / 64, ROW = 2 * HS;
-  float q_t[HEAD_MAXA], q_n[HEAD_MAXA], q_g[HEAD_MAXA];
-  float hv_t[NPL], ha_t[NPL];
-  if (wv == 0) {
-    head_row<HS>(Hon + (int64_t)b * ROW, Pon, A, lane, q_t, hv_t, ha_t);
-  } else {
-    float hv_x[NPL], ha_x[NPL], q[HEAD_MAXA];
-    if (wv == 1) head_row<HS>(Hon + (int64_t)(B + b) * ROW, Pon, A, lane, q, hv_x, ha_x);
-    else head_row<HS>(Htg + (int64_t)b * ROW, Ptg, A, lane, q, hv_x, ha_x);
-    if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < HEAD_MAXA; ++j)
-        if (j < A) qs[wv - 1][j] = q[j];
-    }
-  }
-  __syncthreads();
-  if (wv != 0) return;
-#pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
-    q_n[j] = j < A ? qs[0][j] : 0.f;
-    q_g[j] = j < A ? qs[1][j] : 0.f;
-  }
-  // double DQN: argmax from the online net, value from the target net
-  int astar = 0;
-  float best = -3.4e38f, qg_star = 0.f, q_sa = 0.f;
-  const int a_b = act[b];
-#pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
-    if (j < A) {
-      if (q_n[j] > best) { best = q_n[j]; astar = j; qg_star = q_g[j]; }
-      if (j == a_b) q_sa = q_t[j];
-    }
-  }
-  (void)astar;
-  const float G = rew[b] + gam[b] * qg_star;
-  const float delta = G - q_sa;
-  const float ad = fabsf(delta);
-  float l, dl;
-  if (huber && ad > kappa) {
-    l = kappa * (ad - 0.5f * kappa);
-    dl = delta > 0.f ? kappa : -kappa;
-  } else {
-    l = 0.5f * delta * delta;
-    dl = delta;
-  }
-  const float w = isw ? isw[b] : 1.0f;
-  // d loss_mean / d q(S_t, a_b) = -w * dl / B  (grad_scale = 1/B)
-  const float dq = -w * dl * grad_scale;
-  if (lane == 0) {
-    td_abs[b] = ad;
-    loss[b] = w * l;
-    dhead[(int64_t)b * (A + 1)] = dq;
-  }
-  if (q_out != nullptr && lane < A) {
-    float qv = 0.f;
-#pragma unroll
-    for (int j = 0; j < HEAD_MAXA; ++j)
-      if (j == lane) qv = q_t[j];
-    q_out[(int64_t)b * A + lane] = qv;
-  }
-  const float invA = 1.0f / (float)A;
-  if (lane < A) dhead[(int64_t)b * (A + 1) + 1 + lane] = dq * ((lane == a_b ? 1.f : 0.f) - invA);
-  // back through the heads and the stream ReLUs
-  float dv[NPL], da[NPL], wvv[NPL];
-  load_w<NPL>(Pon.wv + lane * NPL, wvv);
-#pragma unroll
-  for (int k = 0; k < NPL; ++k) dv[k] = hv_t[k] > 0.f ? dq * wvv[k] : 0.f;
-  float colsum[NPL], wsel[NPL];
-#pragma unroll
-  for (int k = 0; k < NPL; ++k) { colsum[k] = 0.f; wsel[k] = 0.f; }
-  for (int j = 0; j < A; ++j) {
-    float wr[NPL];
-    load_w<NPL>(Pon.wa + j * HS + lane * NPL, wr);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const float ww = wr[k];
-      colsum[k] += ww;
-      if (j == a_b) wsel[k] = ww;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NPL; ++k) da[k] = ha_t[k] > 0.f ? dq * (wsel[k] - colsum[k] * invA) : 0.f;
-  if constexpr (NPL == 8) {
-    const uint4 ov = make_uint4(pack_bf16x2(dv[0], dv[1]), pack_bf16x2(dv[2], dv[3]), pack_bf16x2(dv[4], dv[5]),
-                                pack_bf16x2(dv[6], dv[7]));
-    const uint4 oa = make_uint4(pack_bf16x2(da[0], da[1]), pack_bf16x2(da[2], da[3]), pack_bf16x2(da[4], da[5]),
-                                pack_bf16x2(da[6], da[7]));
-    *reinterpret_cast<uint4*>(dH + (int64_t)b * ROW + lane * 8) = ov;
-    *reinterpret_cast<uint4*>(dH + (int64_t)b * ROW + HS + lane * 8) = oa;
-  } else {
-    *reinterpret_cast<uint2*>(dH + (int64_t)b * ROW + lane * 4) =
-        make_uint2(pack_bf16x2(dv[0], dv[1]), pack_bf16x2(dv[2], dv[3]));
-    *reinterpret_cast<uint2*>(dH + (int64_t)b * ROW + HS + lane * 4) =
-        make_uint2(pack_bf16x2(da[0], da[1]), pack_bf16x2(da[2], da[3]));
-  }
+  float ad;
+  (void)ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs, loss,
+                           q_out, dH, dhead, zero_ptr, zero_n, &ad);
 }
 
 // head weight/bias gradients: dW[j][k] += sum_b dhead[b][j] * h[b][stream(j)][k]

@@ -8,7 +8,7 @@
 //   v = a v + (1-a) g^2;  m = a m + (1-a) g;  p -= lr g / (sqrt(v - m^2) + eps))
 // and writes the bf16 compute copy that the MFMA kernels read, so no separate
 // cast kernel runs.  Memory-bound: 16 B read + 14 B written per parameter.
-#include "apex_common.h"
+#include "rmsprop_common.h"
 
 #define NPART 1024
 
@@ -30,73 +30,7 @@ __global__ void __launch_bounds__(256) sqnorm_partial_kernel(const float* __rest
   if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__device__ __forceinline__ float clip_coef_from_partials(const double* partials, int npart, float clip,
-                                                         float* sh) {
-  if (threadIdx.x < 64) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < npart; i += 64) s += partials[i];
-    s = wave_sum(s);
-    if (threadIdx.x == 0) {
-      float norm = (float)sqrt(s);
-      sh[0] = (clip > 0.f) ? fminf(1.0f, clip / (norm + 1e-6f)) : 1.0f;
-      sh[1] = norm;
-    }
-  }
-  __syncthreads();
-  return sh[0];
-}
-
-__global__ void __launch_bounds__(256) rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                      float* __restrict__ v, float* __restrict__ m,
-                                                      bf16_t* __restrict__ pb, int64_t n,
-                                                      const double* __restrict__ partials, int npart,
-                                                      float lr, float alpha, float eps, float clip,
-                                                      int centered, float* __restrict__ norm_out) {
-  __shared__ float sh[2];
-  const float coef = clip_coef_from_partials(partials, npart, clip, sh);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = sh[1];
-  const float a1 = 1.0f - alpha;
-  const int64_t n4 = n / 4;
-  float4* p4 = reinterpret_cast<float4*>(p);
-  const float4* g4 = reinterpret_cast<const float4*>(g);
-  float4* v4 = reinterpret_cast<float4*>(v);
-  float4* m4 = reinterpret_cast<float4*>(m);
-  uint2* pb4 = reinterpret_cast<uint2*>(pb);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 gg = g4[i], pp = p4[i], vv = v4[i], mm = centered ? m4[i] : make_float4(0, 0, 0, 0);
-    float gx[4] = {gg.x * coef, gg.y * coef, gg.z * coef, gg.w * coef};
-    float px[4] = {pp.x, pp.y, pp.z, pp.w};
-    float vx[4] = {vv.x, vv.y, vv.z, vv.w};
-    float mx[4] = {mm.x, mm.y, mm.z, mm.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      vx[j] = alpha * vx[j] + a1 * gx[j] * gx[j];
-      float var = vx[j];
-      if (centered) {
-        mx[j] = alpha * mx[j] + a1 * gx[j];
-        var = vx[j] - mx[j] * mx[j];
-      }
-      px[j] -= lr * gx[j] / (sqrtf(fmaxf(var, 0.f)) + eps);
-    }
-    p4[i] = make_float4(px[0], px[1], px[2], px[3]);
-    v4[i] = make_float4(vx[0], vx[1], vx[2], vx[3]);
-    if (centered) m4[i] = make_float4(mx[0], mx[1], mx[2], mx[3]);
-    pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
-  }
-  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float gg = g[i] * coef;
-    float vv = alpha * v[i] + a1 * gg * gg, var = vv;
-    v[i] = vv;
-    if (centered) {
-      float mm = alpha * m[i] + a1 * gg;
-      m[i] = mm;
-      var = vv - mm * mm;
-    }
-    float pp = p[i] - lr * gg / (sqrtf(fmaxf(var, 0.f)) + eps);
-    p[i] = pp;
-    pb[i] = f32_to_bf16(pp);
-  }
-}
+__global__ void __launch_bounds__(256) rmsprop_kernel(RmspropArgs a) { rmsprop_body(a, blockIdx.x, gridDim.x); }
 
 __global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -115,8 +49,8 @@ APEX_EXPORT int apex_rmsprop_step(float* p, const float* g, float* v, float* m, 
   if ((uintptr_t)pb & 7) return (int)hipErrorInvalidValue;
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
-  rmsprop_kernel<<<nb, 256, 0, st>>>(p, g, v, m, pb, n, partials, NPART, lr, alpha, eps, clip, centered,
-                                     norm_out);
+  rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, NPART, lr, alpha, eps, clip, centered,
+                                                 norm_out});
   APEX_CHECK_LAUNCH();
 }
 
@@ -129,7 +63,8 @@ APEX_EXPORT int apex_rmsprop_step_np(float* p, const float* g, float* v, float* 
   if ((uintptr_t)pb & 7) return (int)hipErrorInvalidValue;
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
-  rmsprop_kernel<<<nb, 256, 0, st>>>(p, g, v, m, pb, n, partials, npart, lr, alpha, eps, clip, centered, norm_out);
+  rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, npart, lr, alpha, eps, clip, centered,
+                                                 norm_out});
   APEX_CHECK_LAUNCH();
 }
 

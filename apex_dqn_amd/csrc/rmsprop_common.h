@@ -1,0 +1,97 @@
+// Centered RMSprop + global-norm clip + bf16 pack as a block-level device body
+// (rmsprop_body), shared by csrc/optimizer.hip (rmsprop_kernel) and by
+// csrc/sumtree.hip (rmsprop_sample_kernel: the optimizer launch also draws the
+// next step's prioritized batch in its first blocks).
+#pragma once
+#include "apex_common.h"
+
+// Clip coefficient from the squared-norm partials: every thread of the block sums a
+// fixed strided subset, then a fixed-order wave / LDS reduction -- deterministic.
+__device__ __forceinline__ float clip_coef_from_partials(const double* partials, int npart, float clip,
+                                                         float* sh) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < npart; i += blockDim.x) s += partials[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    const float norm = (float)sqrt(t);
+    sh[0] = (clip > 0.f) ? fminf(1.0f, clip / (norm + 1e-6f)) : 1.0f;
+    sh[1] = norm;
+  }
+  __syncthreads();
+  return sh[0];
+}
+
+struct RmspropArgs {
+  float* p;
+  const float* g;
+  float* v;
+  float* m;
+  bf16_t* pb;
+  int64_t n;
+  const double* partials;
+  int npart;
+  float lr, alpha, eps, clip;
+  int centered;
+  float* norm_out;
+};
+
+// one 256-thread block `bid` of `nblk` (grid-stride over float4 chunks)
+__device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int nblk) {
+  float* __restrict__ p = A_.p;
+  const float* __restrict__ g = A_.g;
+  float* __restrict__ v = A_.v;
+  float* __restrict__ m = A_.m;
+  bf16_t* __restrict__ pb = A_.pb;
+  const int64_t n = A_.n;
+  const float lr = A_.lr, alpha = A_.alpha, eps = A_.eps;
+  const int centered = A_.centered;
+  __shared__ float sh[2];
+  const float coef = clip_coef_from_partials(A_.partials, A_.npart, A_.clip, sh);
+  if (bid == 0 && threadIdx.x == 0 && A_.norm_out) A_.norm_out[0] = sh[1];
+  const float a1 = 1.0f - alpha;
+  const int64_t n4 = n / 4;
+  float4* p4 = reinterpret_cast<float4*>(p);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float4* v4 = reinterpret_cast<float4*>(v);
+  float4* m4 = reinterpret_cast<float4*>(m);
+  uint2* pb4 = reinterpret_cast<uint2*>(pb);
+  for (int64_t i = (int64_t)bid * blockDim.x + threadIdx.x; i < n4; i += (int64_t)nblk * blockDim.x) {
+    float4 gg = g4[i], pp = p4[i], vv = v4[i], mm = centered ? m4[i] : make_float4(0, 0, 0, 0);
+    float gx[4] = {gg.x * coef, gg.y * coef, gg.z * coef, gg.w * coef};
+    float px[4] = {pp.x, pp.y, pp.z, pp.w};
+    float vx[4] = {vv.x, vv.y, vv.z, vv.w};
+    float mx[4] = {mm.x, mm.y, mm.z, mm.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      vx[j] = alpha * vx[j] + a1 * gx[j] * gx[j];
+      float var = vx[j];
+      if (centered) {
+        mx[j] = alpha * mx[j] + a1 * gx[j];
+        var = vx[j] - mx[j] * mx[j];
+      }
+      px[j] -= lr * gx[j] / (sqrtf(fmaxf(var, 0.f)) + eps);
+    }
+    p4[i] = make_float4(px[0], px[1], px[2], px[3]);
+    v4[i] = make_float4(vx[0], vx[1], vx[2], vx[3]);
+    if (centered) m4[i] = make_float4(mx[0], mx[1], mx[2], mx[3]);
+    pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
+  }
+  for (int64_t i = n4 * 4 + (int64_t)bid * blockDim.x + threadIdx.x; i < n; i += (int64_t)nblk * blockDim.x) {
+    float gg = g[i] * coef;
+    float vv = alpha * v[i] + a1 * gg * gg, var = vv;
+    v[i] = vv;
+    if (centered) {
+      float mm = alpha * m[i] + a1 * gg;
+      m[i] = mm;
+      var = vv - mm * mm;
+    }
+    float pp = p[i] - lr * gg / (sqrtf(fmaxf(var, 0.f)) + eps);
+    p[i] = pp;
+    pb[i] = f32_to_bf16(pp);
+  }
+}

@@ -13,6 +13,8 @@
 // from the leaves (run at the eviction cadence) so fp drift never accumulates.
 // Duplicate indices in one update batch: last occurrence wins (deterministic).
 #include "apex_common.h"
+#include "head_common.h"
+#include "rmsprop_common.h"
 
 // Bounds-checking debug build (SURVEY §5.2 "race / bounds detection"): built as a
 // separate library with -DAPEX_DEBUG_BOUNDS and selected by APEX_DEBUG_BOUNDS=1.
@@ -239,16 +241,45 @@ static int tree_kfirst(const TreeDesc& t) {
 // Also gathers the sampled records and the IS weight
 //   w_i = ((p_i/total) / ratio_min)^-beta,  ratio_min = min_j p_j/total
 // (global over shards when `ratio_min_global` is given) -- max-normalised.
-__global__ void tree_sample_kernel(TreeDesc t, RecordDesc r, int B, uint64_t seed,
-                                   const uint64_t* __restrict__ ctr, float beta,
-                                   const float* __restrict__ ratio_min_global,
-                                   int64_t* __restrict__ out_idx, float* __restrict__ out_w,
-                                   int32_t* __restrict__ out_gen, int32_t* __restrict__ out_obs,
-                                   int32_t* __restrict__ out_nxt, int32_t* __restrict__ out_act,
-                                   float* __restrict__ out_rew, float* __restrict__ out_gam,
-                                   int32_t* __restrict__ out_nxt2) {
+struct SampleArgs {
+  TreeDesc t;
+  RecordDesc r;
+  int B;
+  uint64_t seed;
+  const uint64_t* ctr;
+  float beta;
+  const float* ratio_min_global;
+  int64_t* out_idx;
+  float* out_w;
+  int32_t* out_gen;
+  int32_t* out_obs;
+  int32_t* out_nxt;
+  int32_t* out_act;
+  float* out_rew;
+  float* out_gam;
+  int32_t* out_nxt2;
+};
+
+// block `bid` of 4 waves: samples 4 bid .. 4 bid + 3
+__device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
+  const TreeDesc& t = S.t;
+  const RecordDesc& r = S.r;
+  const int B = S.B;
+  const uint64_t seed = S.seed;
+  const uint64_t* __restrict__ ctr = S.ctr;
+  const float beta = S.beta;
+  const float* __restrict__ ratio_min_global = S.ratio_min_global;
+  int64_t* __restrict__ out_idx = S.out_idx;
+  float* __restrict__ out_w = S.out_w;
+  int32_t* __restrict__ out_gen = S.out_gen;
+  int32_t* __restrict__ out_obs = S.out_obs;
+  int32_t* __restrict__ out_nxt = S.out_nxt;
+  int32_t* __restrict__ out_act = S.out_act;
+  float* __restrict__ out_rew = S.out_rew;
+  float* __restrict__ out_gam = S.out_gam;
+  int32_t* __restrict__ out_nxt2 = S.out_nxt2;
   const int lane = threadIdx.x & 63;
-  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int b = (bid * blockDim.x + threadIdx.x) >> 6;
   if (b >= B) return;
   const double total = t.nodes[t.off[t.L]];
   const float uu = apex_uniform(seed, ctr[0], (uint64_t)b);
@@ -292,6 +323,8 @@ __global__ void tree_sample_kernel(TreeDesc t, RecordDesc r, int B, uint64_t see
     if (out_nxt2) out_nxt2[(int64_t)b * r.C + c] = nv;
   }
 }
+
+__global__ void __launch_bounds__(256) tree_sample_kernel(SampleArgs s) { tree_sample_body(s, blockIdx.x); }
 
 // Exact rebuild of one internal level from its children (wave per parent);
 // the leaf pass also recomputes the min over positive leaves.
@@ -343,6 +376,87 @@ __global__ void gather_frames_kernel(const uint8_t* __restrict__ ring, const int
   for (int64_t i = threadIdx.x; i < nv; i += blockDim.x) dst[i] = src[i];
 }
 
+// ------------------------------------------------- fused learner-step kernels
+// The priority write-back and the next batch's draw ride in launches that run
+// anyway, so the learner step has no separate latency-bound tree kernels on its
+// critical path (a lone tree_update / tree_sample launch is a few waves running
+// dependent global loads while the rest of the chip idles).
+
+struct PrioArgs {
+  TreeDesc t;
+  const int64_t* idx;        // sampled leaves of the batch [B]
+  const int32_t* gen_expect; // their slot generations at sampling time (or null)
+  const int32_t* gen;        // current slot generations
+  uint64_t* ctr_to_bump;     // sampler RNG counter (+1 per update batch, as tree_update)
+  float alpha, eps;
+  int B;
+};
+
+// ddqn_head + priority write-back.  Wave 0 of block b, after the head body, writes
+// leaf idx[b] = (|delta_b| + eps)^alpha unless a later sample of the batch has the
+// same leaf (last occurrence wins, as tree_update's dedupe), the slot was evicted
+// (leaf 0) or re-used since sampling (generation), then adds the fp64 delta to the
+// leaf's ancestors with hardware atomics and folds the value into the running min.
+template <int HS>
+__global__ void __launch_bounds__(192) ddqn_head_prio_kernel(
+    const bf16_t* __restrict__ Hon, const bf16_t* __restrict__ Htg, HeadParams Pon, HeadParams Ptg,
+    const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
+    const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
+    float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
+    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, PrioArgs pr) {
+  // wave 0 issues the write-back's loads (the leaf index, the dedupe scan of the
+  // later samples, the leaf and its generations) before the head body, so their
+  // latency hides under the head math instead of trailing it
+  const int lane = threadIdx.x & 63, b = blockIdx.x;
+  const TreeDesc& t = pr.t;
+  int64_t s = 0;
+  bool dup = false, live = false;
+  float old = 0.f;
+  if (threadIdx.x < 64) {
+    s = pr.idx[b];
+    for (int j0 = b + 1; j0 < pr.B; j0 += 512) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = j0 + 64 * k + lane;
+        if (j < pr.B) dup |= pr.idx[j] == s;
+      }
+    }
+    if (lane == 0 && APEX_DBG_OK(s, t.n[0], 0)) {
+      old = t.leaf[s];
+      live = old > 0.f && (pr.gen_expect == nullptr || pr.gen[s] == pr.gen_expect[b]);
+    }
+  }
+  float ad;
+  if (!ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs, loss,
+                          q_out, dH, dhead, zero_ptr, zero_n, &ad))
+    return;
+  if (b == 0 && lane == 0 && pr.ctr_to_bump != nullptr) pr.ctr_to_bump[0] += 1;
+  if (__ballot(dup) != 0ull || lane != 0 || !live) return;
+  const float v = powf(ad + pr.eps, pr.alpha);
+  t.leaf[s] = v;
+  const double d = (double)v - (double)old;
+  if (d != 0.0) {
+    int64_t node = s;
+    for (int k = 1; k <= t.L; ++k) {
+      node >>= 6;
+      atomicAdd(&t.nodes[t.off[k] + node], d);
+    }
+  }
+  if (v > 0.f) atomicMin(t.min_bits, __float_as_uint(v));
+}
+
+// optimizer + the next step's prioritized draw: blocks [0, nsb) sample, the rest
+// run the clip + centered RMSprop + bf16 pack over the flat parameters.  The tree
+// already holds this step's priorities (written by ddqn_head_prio_kernel), so the
+// draw equals the one a sample launch at the head of the next step would make.
+__global__ void __launch_bounds__(256) rmsprop_sample_kernel(RmspropArgs a, SampleArgs s, int nsb) {
+  if ((int)blockIdx.x < nsb) {
+    tree_sample_body(s, blockIdx.x);
+    return;
+  }
+  rmsprop_body(a, blockIdx.x - nsb, gridDim.x - nsb);
+}
+
 // ---------------------------------------------------------------- launchers
 static inline int blocks_for(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
@@ -381,8 +495,8 @@ APEX_EXPORT int apex_tree_sample(TreeDesc t, RecordDesc r, int B, uint64_t seed,
   if (B <= 0) return 0;
   const int waves_per_block = 4;
   tree_sample_kernel<<<blocks_for(B, waves_per_block), 64 * waves_per_block, 0, st>>>(
-      t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
-      out_rew, out_gam, out_nxt2);
+      SampleArgs{t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
+                 out_rew, out_gam, out_nxt2});
   APEX_CHECK_LAUNCH();
 }
 
@@ -440,4 +554,45 @@ APEX_EXPORT int apex_debug_errors(int* counts, long long* first, int reset) {
   }
   return 0;
 #endif
+}
+
+APEX_EXPORT int apex_ddqn_head_prio(const bf16_t* Hon, const bf16_t* Htg, HeadParams Pon, HeadParams Ptg,
+                                    const int32_t* act, const float* rew, const float* gam, const float* isw,
+                                    int B, int A, int huber, float kappa, float grad_scale, float* td_abs,
+                                    float* loss, float* q_out, bf16_t* dH, float* dhead, float* zero_ptr,
+                                    int zero_n, int hidden, TreeDesc t, const int64_t* idx,
+                                    const int32_t* gen_expect, const int32_t* gen, float alpha, float eps,
+                                    uint64_t* ctr_to_bump, hipStream_t st) {
+  if (A < 1 || A > HEAD_MAXA || B < 1 || idx == nullptr) return (int)hipErrorInvalidValue;
+  const PrioArgs pr{t, idx, gen_expect, gen, ctr_to_bump, alpha, eps, B};
+  if (hidden == 512)
+    ddqn_head_prio_kernel<512><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
+                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr);
+  else if (hidden == 256)
+    ddqn_head_prio_kernel<256><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
+                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr);
+  else
+    return (int)hipErrorInvalidValue;
+  APEX_CHECK_LAUNCH();
+}
+
+// rmsprop (clip norm from `npart` partials, as apex_rmsprop_step_np) + tree_sample of B
+APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
+                                    const double* partials, int npart, float lr, float alpha, float eps_opt,
+                                    float clip, int centered, float* norm_out, TreeDesc t, RecordDesc r, int B,
+                                    uint64_t seed, const uint64_t* ctr, float beta, const float* ratio_min_global,
+                                    int64_t* out_idx, float* out_w, int32_t* out_gen, int32_t* out_obs,
+                                    int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
+                                    int32_t* out_nxt2, hipStream_t st) {
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)pb & 7) || B < 1) return (int)hipErrorInvalidValue;
+  int nb = (int)((n / 4 + 255) / 256);
+  nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
+  const int nsb = blocks_for(B, 4);
+  rmsprop_sample_kernel<<<nb + nsb, 256, 0, st>>>(
+      RmspropArgs{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out},
+      SampleArgs{t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
+                 out_rew, out_gam, out_nxt2},
+      nsb);
+  APEX_CHECK_LAUNCH();
 }

@@ -81,14 +81,18 @@ class FusedNatureLearner:
         self.world = comm.world_size if comm is not None else 1
         self._alloc(self.B)
         self._graphs = None
-        # weight-gradient GEMMs on a side stream beside the dgrad chain (they only
-        # read dY / activations), captured into the same graph(s): on by default
-        # since the image-resident conv1 kernels (3315 -> 3385 steps/s measured; with
-        # the earlier kernels the concurrent GEMMs contended, 2680 vs 2832).
-        # The side stream always carries the small latency-bound kernels that only
-        # need the head's outputs (head wgrad, priority write-back into the sum-tree):
-        # a few blocks each, they run beside the backward GEMMs instead of between them.
-        self._side = torch.cuda.Stream(d) if (d.type == "cuda" and os.environ.get("APEX_NO_SIDE_STREAM", "0") == "0") else None
+        # Optional side stream for the weight-gradient GEMMs and the head wgrad
+        # (Runtime.overlap_wgrad, off by default).  In the captured HIP graph every
+        # cross-stream edge becomes an inter-queue signal wait of ~6-15 us and the
+        # runtime maps branches onto hardware queues its own way (the trace showed
+        # the dgrad chain queued behind side work), so one stream measured faster
+        # once the latency-bound tree kernels moved into the head / optimizer
+        # launches: 3454 vs 3317 steps/s (profiles/r1_step_kernels_*.md).
+        self._side = torch.cuda.Stream(d) if (d.type == "cuda" and self.rt.overlap_wgrad) else None
+        # clip norm: the optimizer launch sums the producers' squared-norm partials
+        # itself (no separate one-block total kernel); APEX_NORM_TOTAL=1 restores it
+        self._norm_total_kernel = os.environ.get("APEX_NORM_TOTAL", "0") == "1"
+        self._npart = 0
         # DP gradient payload: fp32 in place, or a bf16 copy (cast inside the captured
         # segments, summed by RCCL in bf16, cast back before the optimizer)
         if self.rt.allreduce_dtype not in ("fp32", "bf16"):
@@ -107,14 +111,15 @@ class FusedNatureLearner:
         if self.world > 1:
             self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d)
             self._init_ratio()
-        # next-batch pre-sampling: the batch of step t+1 is drawn inside step t, on
-        # the side stream right after step t's priority write-back and its last read
-        # of the sample buffers (conv1 wgrad), so it overlaps the gradient
-        # finalisation + optimizer instead of heading step t+1.  Same draws as
-        # sampling at the head of t+1: the tree is identical (nothing device-side
-        # touches it in between); host-side mutations (inserts, eviction, rebuild)
-        # bump replay.version and force a fresh sample at the head of t+1.  Off by
-        # default: in the HIP graph the extra fork/join costs more than it hides.
+        # next-batch pre-sampling: the batch of step t+1 is drawn at the end of step t,
+        # after the priority write-back -- on the HIP backend inside the optimizer
+        # launch (its first blocks run the sampler: csrc/sumtree.hip
+        # rmsprop_sample_kernel), so no lone latency-bound sample launch heads the
+        # step.  Same draws as sampling at the head of t+1: nothing device-side
+        # touches the tree in between; host-side mutations (inserts, eviction,
+        # rebuild) bump replay.version and force a fresh sample at the head of t+1.
+        # (The earlier side-stream variant lost: 3153 vs 3360 steps/s, the extra
+        # cross-stream graph edges cost more than the sample they hid.)
         self._presample = bool(self.rt.presample)
         self._sample_ver = None
         ls = cfg.Learner.load_saved_state
@@ -194,13 +199,15 @@ class FusedNatureLearner:
         self.forward_all()
         self._mark("forward")
         isw = S["weights"] if rt.use_is_weights else None
+        # the head kernel also writes the batch's priorities back into the sum-tree
+        # (HIP: one launch, csrc/sumtree.hip ddqn_head_prio_kernel)
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
-                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
+                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
+                 prio=(self.replay, S["idx"], S["gen"]))
         self._mark("head")
         with self._on_side():
             ops.head_wgrad(self.h, self.dhead, self.G)
-            self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
         with self._on_side(self.rt.overlap_wgrad):
             self._fc_slots = ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"],
                                           norm=(self.norm_part, 0) if self._fuse_norm else None) or 0
@@ -233,11 +240,9 @@ class FusedNatureLearner:
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"], jobs=jobs)
         self._join_side()      # head wgrad (side stream) done: its region enters the norm
-        if self._presample:    # the last read of the sample buffers is done: draw step t+1's batch
-            with self._on_side():
-                self._sample()
-        norm = dict(part=self.norm_part, slot0=self._fc_slots, total=self.norm_total) if self._fuse_norm else None
-        ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
+        norm = dict(part=self.norm_part, slot0=self._fc_slots,
+                    total=self.norm_total if self._norm_total_kernel else None) if self._fuse_norm else None
+        self._npart = ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
         if self._comm_bf16:
             cut = self.layout.offsets["wfc"]
             self.gcomm[:cut].copy_(self.g32[:cut])
@@ -299,16 +304,27 @@ class FusedNatureLearner:
         rt, ops = self.rt, self.ops
         if self._comm_bf16:
             self.g32.copy_(self.gcomm)
+        # with pre-sampling the optimizer launch also draws step t+1's batch (every
+        # read of this step's sample buffers is behind us)
+        nxt = (self.replay, self.B, self.S, self.ratio_min, self.slots[2 * self.B:]) if self._presample else None
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
-                      norm_total=self.norm_total if self._fuse_norm else None)
-        self._join_side()      # the pre-sample of the next batch ran beside the optimizer
+                      norm_total=self._norm_arg(), sample=nxt)
+        if self._presample:
+            self._sample_ver = self.replay.version
         self._mark("optimizer")
         if self.world > 1:
             # local min_i p_i / total for the global IS-weight normaliser (all-reduced MIN after the step)
             rp = self.replay
             tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float()
             self.ratio_local.copy_(rp.min_bits.view(torch.float32) / tot)
+
+    def _norm_arg(self):
+        """The optimizer's clip-norm source: None (it computes the norm of g32), the
+        one-value total, or (partials, count) summed inside the optimizer launch."""
+        if not self._fuse_norm:
+            return None
+        return self.norm_total if self._norm_total_kernel else (self.norm_part, self._npart)
 
     def _step_body(self) -> None:
         self._seg1()

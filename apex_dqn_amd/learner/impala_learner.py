@@ -136,7 +136,12 @@ class FusedImpalaLearner:
         self._alloc(self.B)
         self.sync_target()
         self._graphs = None
-        self._side = torch.cuda.Stream(d) if d.type == "cuda" else None
+        # one stream by default (see fused_learner: cross-stream edges in the HIP graph
+        # cost more than the overlap); the head kernel writes the priorities back and
+        # the optimizer launch draws the next batch (Runtime.presample)
+        self._side = torch.cuda.Stream(d) if (d.type == "cuda" and self.rt.overlap_wgrad) else None
+        self._presample = bool(self.rt.presample)
+        self._sample_ver = None
         self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
         self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
@@ -288,17 +293,23 @@ class FusedImpalaLearner:
     def _seg1(self) -> None:
         B, rt, ops = self.B, self.rt, self.ops
         self._pack_online()
-        S = self.replay.sample(B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * B:])
+        if not self._presample or self._sample_ver != self.replay.version:
+            self._sample()
+        S = self.S
         self.forward_all()
         isw = S["weights"] if rt.use_is_weights else None
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
-                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
+                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
+                 prio=(self.replay, S["idx"], S["gen"]))
         with self._on_side():
             ops.head_wgrad(self.h, self.dhead, self.G)
-            self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
         ops.fc_wgrad(self.dH, self.feat[:B], self.G["wfc"], self.G["bfc"])
         self._join_side()
+
+    def _sample(self) -> None:
+        self.replay.sample(self.B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * self.B:])
+        self._sample_ver = self.replay.version
 
     def _seg2(self) -> None:
         """fc data gradient, then the three stacks backwards."""
@@ -338,8 +349,11 @@ class FusedImpalaLearner:
 
     def _seg3(self) -> None:
         rt, ops = self.rt, self.ops
+        nxt = (self.replay, self.B, self.S, self.ratio_min, self.slots[2 * self.B:]) if self._presample else None
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
-                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
+                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm, sample=nxt)
+        if self._presample:
+            self._sample_ver = self.replay.version
         if self.world > 1:
             rp = self.replay
             tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float()
@@ -385,6 +399,8 @@ class FusedImpalaLearner:
         graphs = self.rt.use_graphs and self.device.type == "cuda"
         if graphs and self._graphs is None:
             self._capture()
+        if graphs and self._presample and self._sample_ver != self.replay.version:
+            self._sample()     # host-side replay mutation since the in-graph draw: redraw
         if self.world > 1:
             self._dp_step(graphs)
         elif graphs:
@@ -404,6 +420,8 @@ class FusedImpalaLearner:
                 self._step_body()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._restore(snap)
+        if self._presample:    # the graphs start from a drawn batch (their seg1 holds no sample)
+            self._sample()
         torch.cuda.synchronize(self.device)
         segs = [self._step_body] if self.world == 1 else [self._seg1, self._seg2, self._seg3]
         self._graphs = []

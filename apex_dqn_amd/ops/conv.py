@@ -366,7 +366,7 @@ def finalize_grads(lib, jobs: list, norm_range: Optional[torch.Tensor] = None, n
     if norm_part is not None:
         d.norm_part, d.norm_slot0 = norm_part.data_ptr(), int(slot0)
     _lib.check(lib.apex_grad_finalize(d, _lib.stream_ptr()), "grad_finalize")
-    if norm_part is not None and total is not None:
+    if norm_part is not None and total is not None:   # else the optimizer sums the partials itself
         _lib.check(lib.apex_norm_total(norm_part.data_ptr(), int(slot0) + blk, total.data_ptr(), _lib.stream_ptr()),
                    "norm_total")
     return blk

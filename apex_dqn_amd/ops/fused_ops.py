@@ -62,7 +62,9 @@ class TorchBackend:
     # ---------------------------------------------------------------- head
     def head(self, Hon, Htg, Pon: Dict[str, torch.Tensor], Ptg: Dict[str, torch.Tensor], act, rew, gam, isw,
              huber: bool, kappa: float, grad_scale: float, td_abs, loss, dH, dhead, q_out=None,
-             zero: Optional[torch.Tensor] = None):
+             zero: Optional[torch.Tensor] = None, prio=None):
+        """``prio = (replay, idx, gen)``: also write the batch's priorities back
+        (the HIP backend fuses it into the head kernel)."""
         B = act.shape[0]
         A = Pon["wa"].shape[0]
         Hon = Hon.float()
@@ -105,6 +107,8 @@ class TorchBackend:
             q_out.copy_(q_t)
         if zero is not None:
             zero.zero_()
+        if prio is not None:
+            prio[0].update_priorities(prio[1], td_abs, prio[2])
 
     def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor]):
         B = dhead.shape[0]
@@ -146,8 +150,9 @@ class TorchBackend:
         db_out.copy_(dh.float().sum(0))
         return 0
 
-    def finalize_grads(self, jobs, norm_range=None, norm=None) -> None:
+    def finalize_grads(self, jobs, norm_range=None, norm=None) -> int:
         """Deferred split-K reductions (the torch path computes gradients directly)."""
+        return 0
 
     def conv_dgrad(self, dy, w, stride, x_src, dx_out):
         dx_out.copy_(R.conv_dgrad(dy, w, tuple(x_src.shape), stride, x_src, self.dtype))
@@ -166,7 +171,16 @@ class TorchBackend:
         self.conv1_wgrad(dy, frames_buf[:slots.shape[0]], scale, dw_out, db_out)
 
     # ----------------------------------------------------------- optimizer
-    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None):
+    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
+                  sample=None):
+        """``sample = (replay, B, out, ratio_min_global, nxt2)``: also draw the next
+        batch after the update (the HIP backend fuses it into the optimizer launch)."""
+        self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out)
+        if sample is not None:
+            rp, B, out, ratio, nxt2 = sample
+            rp.sample(B, out=out, ratio_min_global=ratio, nxt2=nxt2)
+
+    def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out):
         norm = g32.double().pow(2).sum().sqrt().float()
         coef = torch.clamp(clip / (norm + 1e-6), max=1.0) if clip > 0 else torch.ones_like(norm)
         g = g32 * coef
@@ -231,13 +245,15 @@ class HipBackend(TorchBackend):
             return super().fc_wgrad(dh, x, dw_out, db_out)
         return C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm=norm)
 
-    def finalize_grads(self, jobs, norm_range=None, norm=None) -> None:
+    def finalize_grads(self, jobs, norm_range=None, norm=None) -> int:
+        """Returns the number of squared-norm partial slots written (``slot0`` + blocks)."""
         if not jobs and norm is None:
-            return
+            return 0
         if norm is None:
             C.finalize_grads(self.lib, jobs)
-        else:
-            C.finalize_grads(self.lib, jobs, norm_range, norm["part"], norm["slot0"], norm["total"])
+            return 0
+        return norm["slot0"] + C.finalize_grads(self.lib, jobs, norm_range, norm["part"], norm["slot0"],
+                                                norm.get("total"))
 
     def conv_dgrad(self, dy, w, stride, x_src, dx_out):
         if not self.native_conv:
@@ -265,14 +281,21 @@ class HipBackend(TorchBackend):
         return h
 
     def head(self, Hon, Htg, Pon, Ptg, act, rew, gam, isw, huber, kappa, grad_scale, td_abs, loss, dH,
-             dhead, q_out=None, zero=None):
+             dhead, q_out=None, zero=None, prio=None):
         B = act.shape[0]
         A = Pon["wa"].shape[0]
-        _lib.check(self.lib.apex_ddqn_head(
-            Hon.data_ptr(), Htg.data_ptr(), self._hp(Pon), self._hp(Ptg), act.data_ptr(), rew.data_ptr(),
-            gam.data_ptr(), _lib.ptr(isw), B, A, int(huber), float(kappa), float(grad_scale),
-            td_abs.data_ptr(), loss.data_ptr(), _lib.ptr(q_out), dH.data_ptr(), dhead.data_ptr(),
-            _lib.ptr(zero), 0 if zero is None else zero.numel(), Pon["wv"].numel(), _lib.stream_ptr()), "ddqn_head")
+        args = (Hon.data_ptr(), Htg.data_ptr(), self._hp(Pon), self._hp(Ptg), act.data_ptr(), rew.data_ptr(),
+                gam.data_ptr(), _lib.ptr(isw), B, A, int(huber), float(kappa), float(grad_scale),
+                td_abs.data_ptr(), loss.data_ptr(), _lib.ptr(q_out), dH.data_ptr(), dhead.data_ptr(),
+                _lib.ptr(zero), 0 if zero is None else zero.numel(), Pon["wv"].numel())
+        if prio is not None and prio[0].use_hip:
+            # priority write-back in the head kernel (csrc/sumtree.hip: ddqn_head_prio_kernel)
+            _lib.check(self.lib.apex_ddqn_head_prio(*args, *prio[0].prio_launch_args(prio[1], prio[2]),
+                                                    _lib.stream_ptr()), "ddqn_head_prio")
+            return
+        _lib.check(self.lib.apex_ddqn_head(*args, _lib.stream_ptr()), "ddqn_head")
+        if prio is not None:
+            prio[0].update_priorities(prio[1], td_abs, prio[2])
 
     def head_wgrad(self, Hon, dhead, g):
         B, A1 = dhead.shape
@@ -286,12 +309,34 @@ class HipBackend(TorchBackend):
                                             ctr.data_ptr(), q_out.data_ptr(), a_out.data_ptr(),
                                             P["wv"].numel(), _lib.stream_ptr()), "actor_head")
 
-    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None):
+    def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
+                  sample=None):
         n = p32.numel()
         st = _lib.stream_ptr()
+        if sample is not None and sample[0].use_hip:
+            # the next batch's draw rides in the optimizer launch (csrc/sumtree.hip: rmsprop_sample_kernel)
+            rp, B, out, ratio, nxt2 = sample
+            if norm_total is None:
+                _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), n, partials.data_ptr(), st), "sqnorm")
+                part, npart = partials, partials.numel()
+            elif isinstance(norm_total, tuple):   # (producer partials, count): summed in the launch
+                part, npart = norm_total
+            else:
+                part, npart = norm_total, 1
+            _lib.check(self.lib.apex_rmsprop_sample(
+                p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
+                float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
+                *rp.sample_launch_args(B, out, ratio, nxt2), st), "rmsprop_sample")
+            return
+        if sample is not None:
+            self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total)
+            rp, B, out, ratio, nxt2 = sample
+            rp.sample(B, out=out, ratio_min_global=ratio, nxt2=nxt2)
+            return
         if norm_total is not None:   # squared norm already summed by the gradient producers
+            part, npart = norm_total if isinstance(norm_total, tuple) else (norm_total, 1)
             _lib.check(self.lib.apex_rmsprop_step_np(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
-                                                     pbf.data_ptr(), n, norm_total.data_ptr(), 1, float(lr),
+                                                     pbf.data_ptr(), n, part.data_ptr(), npart, float(lr),
                                                      float(alpha), float(eps), float(clip), int(centered),
                                                      norm_out.data_ptr(), st), "rmsprop_np")
             return

@@ -247,6 +247,23 @@ class GpuReplayShard:
                 nxt2.copy_(out["nxt"])
         return out
 
+    def sample_launch_args(self, B: int, out: Dict[str, torch.Tensor],
+                           ratio_min_global: Optional[torch.Tensor] = None,
+                           nxt2: Optional[torch.Tensor] = None) -> tuple:
+        """The tree_sample arguments (TreeDesc .. out_nxt2) of :meth:`sample`, for
+        kernels that draw the batch inside another launch (``apex_rmsprop_sample``)."""
+        return (self.tree_desc(), self.record_desc(), B, self.seed, self.ctr.data_ptr(), self.beta,
+                _lib.ptr(ratio_min_global), out["idx"].data_ptr(), out["weights"].data_ptr(),
+                out["gen"].data_ptr(), out["obs"].data_ptr(), out["nxt"].data_ptr(), out["act"].data_ptr(),
+                out["rew"].data_ptr(), out["gam"].data_ptr(), _lib.ptr(nxt2))
+
+    def prio_launch_args(self, idx: torch.Tensor, gen: Optional[torch.Tensor] = None,
+                         bump_ctr: bool = True) -> tuple:
+        """The priority write-back arguments of :meth:`update_priorities` (TreeDesc, idx,
+        generations, alpha, eps, counter) for ``apex_ddqn_head_prio``."""
+        return (self.tree_desc(), idx.data_ptr(), _lib.ptr(gen), self.gen.data_ptr(), self.alpha, self.eps,
+                self.ctr.data_ptr() if bump_ctr else None)
+
     def alloc_sample_buffers(self, B: int) -> Dict[str, torch.Tensor]:
         d = self.device
         return dict(idx=torch.zeros(B, dtype=torch.int64, device=d),

@@ -41,10 +41,10 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--profile-phases", action="store_true")
-    ap.add_argument("--presample", action="store_true",
-                    help="draw step t+1's batch inside step t, beside the optimizer (default off)")
-    ap.add_argument("--no-overlap-wgrad", action="store_true",
-                    help="weight-gradient GEMMs serialised with the dgrad chain (default: side stream)")
+    ap.add_argument("--no-presample", action="store_true",
+                    help="sample at the head of each step instead of inside the previous step's optimizer launch")
+    ap.add_argument("--overlap-wgrad", action="store_true",
+                    help="weight-gradient GEMMs on a side stream beside the dgrad chain (default: one stream)")
     ap.add_argument("--graph-impala", action="store_true",
                     help="IMPALA on the torch-autograd graph learner (MIOpen) instead of the HIP kernels")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
@@ -74,8 +74,8 @@ def main():
                     "min_replay_mem_size": 0},
         "Replay_Memory": {"soft_capacity": args.replay},
         "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
-                    "seed": 1234 + rank, "network": args.network, "overlap_wgrad": not args.no_overlap_wgrad,
-                    "presample": args.presample},
+                    "seed": 1234 + rank, "network": args.network, "overlap_wgrad": args.overlap_wgrad,
+                    "presample": not args.no_presample},
     })
     cap = args.replay
     frames_cap = cap + 4096
