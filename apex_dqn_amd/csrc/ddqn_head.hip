@@ -34,30 +34,42 @@ __global__ void __launch_bounds__(192) ddqn_head_kernel(
 }
 
 // head weight/bias gradients: dW[j][k] += sum_b dhead[b][j] * h[b][stream(j)][k]
-// grid: (A+1) rows x HS/256 column blocks x batch slices of 16; fp32 atomics into a
-// region zeroed by ddqn_head_kernel.  Output layout = flat param layout:
-//   gwv[HS] gbv[1] gwa[A*HS] gba[A]
-__global__ void __launch_bounds__(256) head_wgrad_kernel(const bf16_t* __restrict__ Hon,
+// grid: (A+1) rows x HS/64 column chunks; block = 8 waves, lane = column, wave w
+// sums rows w, w+8, ...; the 8 wave partials meet in LDS and are added in a fixed
+// order -- no atomics, so the step is bitwise reproducible.  Output layout = flat
+// param layout: gwv[HS] gbv[1] gwa[A*HS] gba[A] (accumulated into, the region is
+// zeroed by ddqn_head_kernel).
+__global__ void __launch_bounds__(512) head_wgrad_kernel(const bf16_t* __restrict__ Hon,
                                                          const float* __restrict__ dhead, int B, int A,
                                                          float* __restrict__ gwv, float* __restrict__ gbv,
                                                          float* __restrict__ gwa, float* __restrict__ gba, int HS) {
+  __shared__ float red[8][65];
   const int j = blockIdx.x;            // 0 = value, 1..A = advantage j-1
-  const int k = blockIdx.y * 256 + threadIdx.x;  // 0..HS-1
-  const int b0 = blockIdx.z * 16;
-  const int b1 = min(B, b0 + 16);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = blockIdx.y * 64 + lane;  // 0..HS-1
   const int col = (j == 0 ? 0 : HS) + k;
   float acc = 0.f, accb = 0.f;
-  for (int b = b0; b < b1; ++b) {
+#pragma unroll 8
+  for (int b = w; b < B; b += 8) {
     const float d = dhead[(int64_t)b * (A + 1) + j];
     acc += d * bf16_to_f32(Hon[(int64_t)b * 2 * HS + col]);
     accb += d;
   }
-  if (j == 0) {
-    atomicAdd(&gwv[k], acc);
-    if (k == 0 && blockIdx.y == 0) atomicAdd(gbv, accb);
-  } else {
-    atomicAdd(&gwa[(j - 1) * HS + k], acc);
-    if (k == 0 && blockIdx.y == 0) atomicAdd(&gba[j - 1], accb);
+  red[w][lane] = acc;
+  if (lane == 0) red[w][64] = accb;
+  __syncthreads();
+  if (w != 0) return;
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s += red[q][lane];
+  if (j == 0) gwv[k] += s;
+  else gwa[(j - 1) * HS + k] += s;
+  if (lane == 0 && blockIdx.y == 0) {
+    float sb = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sb += red[q][64];
+    if (j == 0) gbv[0] += sb;
+    else gba[j - 1] += sb;
   }
 }
 
@@ -81,8 +93,8 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
 APEX_EXPORT int apex_head_wgrad(const bf16_t* Hon, const float* dhead, int B, int A, float* gwv, float* gbv,
                                 float* gwa, float* gba, int hidden, hipStream_t st) {
   if (hidden != 512 && hidden != 256) return (int)hipErrorInvalidValue;
-  dim3 grid(A + 1, hidden / 256, (B + 15) / 16);
-  head_wgrad_kernel<<<grid, 256, 0, st>>>(Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden);
+  dim3 grid(A + 1, hidden / 64);
+  head_wgrad_kernel<<<grid, 512, 0, st>>>(Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden);
   APEX_CHECK_LAUNCH();
 }
 

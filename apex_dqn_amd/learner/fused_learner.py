@@ -81,6 +81,7 @@ class FusedNatureLearner:
         self.world = comm.world_size if comm is not None else 1
         self._alloc(self.B)
         self._graphs = None
+        self._multi = None      # Runtime.graph_steps-step graph (steps())
         # Optional side stream for the weight-gradient GEMMs and the head wgrad
         # (Runtime.overlap_wgrad, off by default).  In the captured HIP graph every
         # cross-stream edge becomes an inter-queue signal wait of ~6-15 us and the
@@ -377,6 +378,40 @@ class FusedNatureLearner:
         L = self.cfg.Learner
         if self.num_q_updates % L.q_target_sync_freq == 0:
             self.sync_target()
+
+    def steps(self, n: int) -> None:
+        """``n`` learner updates.  On one rank with HIP graphs, chunks of
+        ``Runtime.graph_steps`` updates replay ONE graph holding that many steps
+        (each graph launch costs ~9 us of idle GPU at its boundary); chunks never
+        straddle a target-network sync.  Same updates as ``n`` calls of :meth:`step`."""
+        k = int(self.rt.graph_steps)
+        graphs = self.rt.use_graphs and self.device.type == "cuda"
+        if k <= 1 or not graphs or self.world > 1:
+            for _ in range(n):
+                self.step()
+            return
+        f = self.cfg.Learner.q_target_sync_freq
+        while n > 0:
+            to_sync = f - self.num_q_updates % f
+            if n < k or to_sync < k:
+                self.step()
+                n -= 1
+                continue
+            if self._graphs is None:
+                self._capture()
+            if self._multi is None:
+                self._multi = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize(self.device)
+                with torch.cuda.graph(self._multi):
+                    for _ in range(k):
+                        self._step_body()
+            if self._presample and self._sample_ver != self.replay.version:
+                self._sample()
+            self._multi.replay()
+            self.num_q_updates += k
+            n -= k
+            if self.num_q_updates % f == 0:
+                self.sync_target()
 
     def _capture(self) -> None:
         """Warm up on a side stream (allocator pools, workspaces), restore state,

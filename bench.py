@@ -45,6 +45,8 @@ def main():
                     help="sample at the head of each step instead of inside the previous step's optimizer launch")
     ap.add_argument("--overlap-wgrad", action="store_true",
                     help="weight-gradient GEMMs on a side stream beside the dgrad chain (default: one stream)")
+    ap.add_argument("--graph-steps", type=int, default=None,
+                    help="learner updates per HIP-graph launch (Runtime.graph_steps; 1 = one graph per update)")
     ap.add_argument("--graph-impala", action="store_true",
                     help="IMPALA on the torch-autograd graph learner (MIOpen) instead of the HIP kernels")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
@@ -75,7 +77,8 @@ def main():
         "Replay_Memory": {"soft_capacity": args.replay},
         "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
                     "seed": 1234 + rank, "network": args.network, "overlap_wgrad": args.overlap_wgrad,
-                    "presample": not args.no_presample},
+                    "presample": not args.no_presample,
+                    **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
     })
     cap = args.replay
     frames_cap = cap + 4096
@@ -106,20 +109,28 @@ def main():
         learner = GraphLearner(cfg, device, replay, comm=comm)
     L = cfg.Learner
 
-    def one_step():
-        learner.step()
-        if learner.num_q_updates % L.remove_old_xp_freq == 0:
-            replay.remove_to_fit()
-            replay.rebuild()
+    def run(n):
+        """n learner updates; the FIFO eviction + tree rebuild at its cadence runs
+        between graph launches (learners with ``steps`` replay multi-step graphs)."""
+        f = L.remove_old_xp_freq
+        while n > 0:
+            k = min(n, f - learner.num_q_updates % f)
+            if hasattr(learner, "steps"):
+                learner.steps(k)
+            else:
+                for _ in range(k):
+                    learner.step()
+            n -= k
+            if learner.num_q_updates % f == 0:
+                replay.remove_to_fit()
+                replay.rebuild()
 
-    for _ in range(args.warmup):
-        one_step()
+    run(args.warmup)
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
+    run(args.steps)
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
