@@ -33,45 +33,7 @@ __global__ void __launch_bounds__(192) ddqn_head_kernel(
                            q_out, dH, dhead, zero_ptr, zero_n, &ad);
 }
 
-// head weight/bias gradients: dW[j][k] += sum_b dhead[b][j] * h[b][stream(j)][k]
-// grid: (A+1) rows x HS/64 column chunks; block = 8 waves, lane = column, wave w
-// sums rows w, w+8, ...; the 8 wave partials meet in LDS and are added in a fixed
-// order -- no atomics, so the step is bitwise reproducible.  Output layout = flat
-// param layout: gwv[HS] gbv[1] gwa[A*HS] gba[A] (accumulated into, the region is
-// zeroed by ddqn_head_kernel).
-__global__ void __launch_bounds__(512) head_wgrad_kernel(const bf16_t* __restrict__ Hon,
-                                                         const float* __restrict__ dhead, int B, int A,
-                                                         float* __restrict__ gwv, float* __restrict__ gbv,
-                                                         float* __restrict__ gwa, float* __restrict__ gba, int HS) {
-  __shared__ float red[8][65];
-  const int j = blockIdx.x;            // 0 = value, 1..A = advantage j-1
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int k = blockIdx.y * 64 + lane;  // 0..HS-1
-  const int col = (j == 0 ? 0 : HS) + k;
-  float acc = 0.f, accb = 0.f;
-#pragma unroll 8
-  for (int b = w; b < B; b += 8) {
-    const float d = dhead[(int64_t)b * (A + 1) + j];
-    acc += d * bf16_to_f32(Hon[(int64_t)b * 2 * HS + col]);
-    accb += d;
-  }
-  red[w][lane] = acc;
-  if (lane == 0) red[w][64] = accb;
-  __syncthreads();
-  if (w != 0) return;
-  float s = 0.f;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) s += red[q][lane];
-  if (j == 0) gwv[k] += s;
-  else gwa[(j - 1) * HS + k] += s;
-  if (lane == 0 && blockIdx.y == 0) {
-    float sb = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) sb += red[q][64];
-    if (j == 0) gbv[0] += sb;
-    else gba[j - 1] += sb;
-  }
-}
+__global__ void __launch_bounds__(512) head_wgrad_kernel(HeadWgArgs h) { head_wgrad_body(h, blockIdx.x, blockIdx.y); }
 
 APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams Pon, HeadParams Ptg,
                                const int32_t* act, const float* rew, const float* gam, const float* isw,
@@ -94,7 +56,7 @@ APEX_EXPORT int apex_head_wgrad(const bf16_t* Hon, const float* dhead, int B, in
                                 float* gwa, float* gba, int hidden, hipStream_t st) {
   if (hidden != 512 && hidden != 256) return (int)hipErrorInvalidValue;
   dim3 grid(A + 1, hidden / 64);
-  head_wgrad_kernel<<<grid, 512, 0, st>>>(Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden);
+  head_wgrad_kernel<<<grid, 512, 0, st>>>(HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden});
   APEX_CHECK_LAUNCH();
 }
 

@@ -2,7 +2,8 @@
 // row (head_row) and the fused DDQN loss / priority / head-backward body
 // (ddqn_head_body), used by csrc/ddqn_head.hip (ddqn_head_kernel) and by
 // csrc/sumtree.hip (ddqn_head_prio_kernel: the same body + the priority
-// write-back into the sum-tree, so no separate tree_update launch).
+// write-back into the sum-tree), and the head weight gradient (head_wgrad_body,
+// also run by sumtree.hip head_wgrad_prio_kernel beside the tree update).
 #pragma once
 #include "apex_common.h"
 
@@ -203,4 +204,55 @@ __device__ __forceinline__ bool ddqn_head_body(
   }
   *ad_out = ad;
   return true;
+}
+
+// head weight/bias gradients: dW[j][k] += sum_b dhead[b][j] * h[b][stream(j)][k]
+// grid: (A+1) rows x HS/64 column chunks; block = 8 waves, lane = column, wave w
+// sums rows w, w+8, ...; the 8 wave partials meet in LDS and are added in a fixed
+// order -- no atomics, so the step is bitwise reproducible.  Output layout = flat
+// param layout: gwv[HS] gbv[1] gwa[A*HS] gba[A] (accumulated into, the region is
+// zeroed by ddqn_head_kernel).
+struct HeadWgArgs {
+  const bf16_t* Hon;
+  const float* dhead;
+  int B, A;
+  float* gwv;
+  float* gbv;
+  float* gwa;
+  float* gba;
+  int HS;
+};
+
+// block (j, chunk): 512 threads
+__device__ __forceinline__ void head_wgrad_body(const HeadWgArgs& h, int j, int chunk) {
+  const bf16_t* __restrict__ Hon = h.Hon;
+  const float* __restrict__ dhead = h.dhead;
+  const int B = h.B, A = h.A, HS = h.HS;
+  __shared__ float red[8][65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int k = chunk * 64 + lane;  // 0..HS-1
+  const int col = (j == 0 ? 0 : HS) + k;
+  float acc = 0.f, accb = 0.f;
+#pragma unroll 8
+  for (int b = w; b < B; b += 8) {
+    const float d = dhead[(int64_t)b * (A + 1) + j];
+    acc += d * bf16_to_f32(Hon[(int64_t)b * 2 * HS + col]);
+    accb += d;
+  }
+  red[w][lane] = acc;
+  if (lane == 0) red[w][64] = accb;
+  __syncthreads();
+  if (w != 0) return;
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s += red[q][lane];
+  if (j == 0) h.gwv[k] += s;
+  else h.gwa[(j - 1) * HS + k] += s;
+  if (lane == 0 && chunk == 0) {
+    float sb = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sb += red[q][64];
+    if (j == 0) h.gbv[0] += sb;
+    else h.gba[j - 1] += sb;
+  }
 }

@@ -446,6 +446,84 @@ __global__ void __launch_bounds__(192) ddqn_head_prio_kernel(
   if (v > 0.f) atomicMin(t.min_bits, __float_as_uint(v));
 }
 
+// Single-block priority write-back (tree_update mode 1 with dedupe) for n <= 1024
+// leaves, any block size: items tid, tid + blockDim, ...; the LDS hash keeps the
+// last occurrence of a duplicated leaf; every item's delta goes through the
+// block-aggregated tree_block_update (the root sees ONE atomic per item round).
+struct TreeUpdArgs {
+  TreeDesc t;
+  const int64_t* idx;
+  const float* td;           // |delta| per sample
+  const int32_t* gen_expect;
+  const int32_t* gen;
+  uint64_t* ctr_to_bump;
+  float alpha, eps;
+  int n, kfirst;
+};
+
+__device__ __forceinline__ void tree_update_block(const TreeUpdArgs& a) {
+  __shared__ uint32_t hkey[2048];
+  __shared__ int32_t hval[2048];
+  __shared__ double lacc[TREE_LACC];
+  __shared__ uint32_t lmin;
+  const TreeDesc& t = a.t;
+  const int nt = blockDim.x, R = (a.n + nt - 1) / nt;
+  if (a.ctr_to_bump != nullptr && threadIdx.x == 0) a.ctr_to_bump[0] += 1;
+  for (int j = threadIdx.x; j < 2048; j += nt) {
+    hkey[j] = 0u;
+    hval[j] = -1;
+  }
+  __syncthreads();
+  int64_t s[2];
+  int h[2];
+  for (int r = 0; r < R; ++r) {
+    const int i = threadIdx.x + r * nt;
+    s[r] = 0;
+    h[r] = -1;
+    if (i < a.n) {
+      s[r] = a.idx[i];
+      if (APEX_DBG_OK(s[r], t.n[0], 0)) {
+        const uint32_t key = (uint32_t)s[r] + 1u;
+        int hh = (int)(hash32(key) & 2047u);
+        while (true) {
+          const uint32_t old = atomicCAS(&hkey[hh], 0u, key);
+          if (old == 0u || old == key) {
+            atomicMax(&hval[hh], i);
+            break;
+          }
+          hh = (hh + 1) & 2047;
+        }
+        h[r] = hh;
+      }
+    }
+  }
+  __syncthreads();
+  for (int r = 0; r < R; ++r) {
+    const int i = threadIdx.x + r * nt;
+    bool act = h[r] >= 0 && hval[h[r]] == i;   // a later write to the same leaf wins
+    float v = 0.f;
+    if (act) {
+      if (t.leaf[s[r]] <= 0.f) act = false;
+      else if (a.gen_expect != nullptr && a.gen[s[r]] != a.gen_expect[i]) act = false;
+      v = powf(fabsf(a.td[i]) + a.eps, a.alpha);
+    }
+    tree_block_update(t, act, s[r], v, lacc, &lmin, a.kfirst);
+    __syncthreads();
+  }
+}
+
+// head weight gradient + priority write-back in one launch: block 0 runs the
+// single-block tree update (dispatched first, it is the long pole), blocks 1..
+// the (A+1) x HS/64 head_wgrad blocks.  Both only need the head kernel's outputs.
+__global__ void __launch_bounds__(512) head_wgrad_prio_kernel(HeadWgArgs hw, TreeUpdArgs tu) {
+  if (blockIdx.x == 0) {
+    tree_update_block(tu);
+    return;
+  }
+  const int b = blockIdx.x - 1, nch = hw.HS / 64;
+  head_wgrad_body(hw, b / nch, b - (b / nch) * nch);
+}
+
 // optimizer + the next step's prioritized draw: blocks [0, nsb) sample, the rest
 // run the clip + centered RMSprop + bf16 pack over the flat parameters.  The tree
 // already holds this step's priorities (written by ddqn_head_prio_kernel), so the
@@ -611,5 +689,17 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   if (nt == 1024) rmsprop_sample_kernel<1024><<<nb + nsb, 1024, 0, st>>>(ra, sa, nsb);
   else if (nt == 512) rmsprop_sample_kernel<512><<<nb + nsb, 512, 0, st>>>(ra, sa, nsb);
   else rmsprop_sample_kernel<256><<<nb + nsb, 256, 0, st>>>(ra, sa, nsb);
+  APEX_CHECK_LAUNCH();
+}
+
+APEX_EXPORT int apex_head_wgrad_prio(const bf16_t* Hon, const float* dhead, int B, int A, float* gwv, float* gbv,
+                                     float* gwa, float* gba, int hidden, TreeDesc t, const int64_t* idx,
+                                     const float* td, const int32_t* gen_expect, const int32_t* gen,
+                                     float alpha, float eps, uint64_t* ctr_to_bump, hipStream_t st) {
+  if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || idx == nullptr) return (int)hipErrorInvalidValue;
+  const int nblk = 1 + (A + 1) * (hidden / 64);
+  head_wgrad_prio_kernel<<<nblk, 512, 0, st>>>(
+      HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden},
+      TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)});
   APEX_CHECK_LAUNCH();
 }

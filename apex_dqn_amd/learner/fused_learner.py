@@ -29,6 +29,10 @@ from typing import Any, Dict, Optional
 import torch
 
 from ..config import ApexConfig
+
+# priority write-back: in the head-wgrad launch (one extra single-block tree update,
+# default) or in the head kernel itself (APEX_PRIO_IN_HEAD=1)
+_PRIO_IN_HEAD = os.environ.get("APEX_PRIO_IN_HEAD", "0") == "1"
 from ..models.dueling import DuellingDQN
 from ..models.flat_params import (FlatLayout, flat_to_reference_state, nature_segments,
                                   reference_state_to_flat)
@@ -200,15 +204,16 @@ class FusedNatureLearner:
         self.forward_all()
         self._mark("forward")
         isw = S["weights"] if rt.use_is_weights else None
-        # the head kernel also writes the batch's priorities back into the sum-tree
-        # (HIP: one launch, csrc/sumtree.hip ddqn_head_prio_kernel)
+        # the batch's priorities go back into the sum-tree from the head-wgrad launch
+        # (HIP: one extra block, csrc/sumtree.hip head_wgrad_prio_kernel)
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
-                 prio=(self.replay, S["idx"], S["gen"]))
+                 prio=(self.replay, S["idx"], S["gen"]) if _PRIO_IN_HEAD else None)
         self._mark("head")
         with self._on_side():
-            ops.head_wgrad(self.h, self.dhead, self.G)
+            ops.head_wgrad(self.h, self.dhead, self.G,
+                           prio=None if _PRIO_IN_HEAD else (self.replay, S["idx"], S["gen"], self.td_abs))
         with self._on_side(self.rt.overlap_wgrad):
             self._fc_slots = ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"],
                                           norm=(self.norm_part, 0) if self._fuse_norm else None) or 0

@@ -28,12 +28,17 @@ defects fixed, exactly as the NatureCNN learner.
 from __future__ import annotations
 
 import contextlib
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
 import torch
 
 from ..config import ApexConfig
+
+# priority write-back: in the head-wgrad launch (one extra single-block tree update,
+# default) or in the head kernel itself (APEX_PRIO_IN_HEAD=1)
+_PRIO_IN_HEAD = os.environ.get("APEX_PRIO_IN_HEAD", "0") == "1"
 from ..models.dueling import ImpalaDuellingDQN
 from ..models.flat_params import FlatLayout
 from ..ops.fused_ops import HipBackend, TorchBackend
@@ -301,9 +306,10 @@ class FusedImpalaLearner:
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
-                 prio=(self.replay, S["idx"], S["gen"]))
+                 prio=(self.replay, S["idx"], S["gen"]) if _PRIO_IN_HEAD else None)
         with self._on_side():
-            ops.head_wgrad(self.h, self.dhead, self.G)
+            ops.head_wgrad(self.h, self.dhead, self.G,
+                           prio=None if _PRIO_IN_HEAD else (self.replay, S["idx"], S["gen"], self.td_abs))
         ops.fc_wgrad(self.dH, self.feat[:B], self.G["wfc"], self.G["bfc"])
         self._join_side()
 

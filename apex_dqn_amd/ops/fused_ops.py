@@ -110,7 +110,11 @@ class TorchBackend:
         if prio is not None:
             prio[0].update_priorities(prio[1], td_abs, prio[2])
 
-    def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor]):
+    def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor], prio=None):
+        """``prio = (replay, idx, gen, td_abs)``: also write the batch's priorities back
+        (the HIP backend runs it as one extra block of the same launch)."""
+        if prio is not None:
+            prio[0].update_priorities(prio[1], prio[3], prio[2])
         B = dhead.shape[0]
         HS = g["wv"].numel()
         h = Hon[:B].float()
@@ -297,8 +301,18 @@ class HipBackend(TorchBackend):
         if prio is not None:
             prio[0].update_priorities(prio[1], td_abs, prio[2])
 
-    def head_wgrad(self, Hon, dhead, g):
+    def head_wgrad(self, Hon, dhead, g, prio=None):
         B, A1 = dhead.shape
+        if prio is not None and prio[0].use_hip and B <= 1024:
+            rp, idx, gen, td = prio
+            _lib.check(self.lib.apex_head_wgrad_prio(
+                Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(), g["bv"].data_ptr(),
+                g["wa"].data_ptr(), g["ba"].data_ptr(), g["wv"].numel(), rp.tree_desc(), idx.data_ptr(),
+                td.data_ptr(), _lib.ptr(gen), rp.gen.data_ptr(), rp.alpha, rp.eps, rp.ctr.data_ptr(),
+                _lib.stream_ptr()), "head_wgrad_prio")
+            return
+        if prio is not None:
+            prio[0].update_priorities(prio[1], prio[3], prio[2])
         _lib.check(self.lib.apex_head_wgrad(Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(),
                                             g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(),
                                             g["wv"].numel(), _lib.stream_ptr()), "head_wgrad")

@@ -345,3 +345,42 @@ def test_multi_step_graph_matches_single_step_graphs():
     assert torch.equal(res[1][3], res[4][3])
     for a, b in zip(res[1][:3], res[4][:3]):
         torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
+
+
+def test_head_wgrad_prio_matches_separate_launches():
+    """head_wgrad with the priority write-back as an extra block == head_wgrad +
+    tree_update (duplicates: last wins; stale generation / evicted: skipped)."""
+    from apex_dqn_amd.ops.fused_ops import HipBackend
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    B, A = 96, 6
+    Hon, Htg, Pon, Ptg, act, rew, gam, isw = _head_inputs(B, A, seed=4)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    idx = torch.randint(0, 300, (B,), generator=g).to(DEV)
+    idx[3] = idx[50] = idx[95] = 33
+    be = HipBackend()
+    td = torch.zeros(B, device=DEV)
+    outs = [td, torch.zeros(B, device=DEV), torch.zeros(B, 1024, device=DEV, dtype=torch.bfloat16),
+            torch.zeros(B, A + 1, device=DEV)]
+    be.head(Hon, Htg, Pon, Ptg, act, rew, gam, isw, True, 1.0, 1.0 / B, *outs)
+    res = {}
+    for fused in (False, True):
+        rp = GpuReplayShard(1000, 700, 1200, 4, device=DEV, alpha=0.6, eps=1e-6)
+        _fill_replay(rp, 900, seed=9)
+        rp.remove_to_fit()
+        gen = rp.gen[idx].clone()
+        gen[7] += 1
+        gr = {"wv": torch.zeros(512, device=DEV), "bv": torch.zeros(1, device=DEV),
+              "wa": torch.zeros(A, 512, device=DEV), "ba": torch.zeros(A, device=DEV)}
+        ctr0 = int(rp.ctr[0])
+        if fused:
+            be.head_wgrad(Hon, outs[3], gr, prio=(rp, idx, gen, td))
+        else:
+            be.head_wgrad(Hon, outs[3], gr)
+            rp.update_priorities(idx, td, gen)
+        torch.cuda.synchronize()
+        res[fused] = (gr, rp.leaf.clone(), rp.nodes.clone(), int(rp.min_bits[0]), int(rp.ctr[0]) - ctr0)
+    (g0, l0, n0, m0, c0), (g1, l1, n1, m1, c1) = res[False], res[True]
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k
+    assert torch.equal(l0, l1) and m0 == m1 and c0 == c1 == 1
+    torch.testing.assert_close(n1, n0, rtol=1e-12, atol=1e-9)
