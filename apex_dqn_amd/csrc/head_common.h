@@ -223,18 +223,18 @@ struct HeadWgArgs {
   int HS;
 };
 
-// block (j, chunk): 512 threads
+// block (j, chunk): any multiple of 64 threads up to 1024 (waves split the rows)
 __device__ __forceinline__ void head_wgrad_body(const HeadWgArgs& h, int j, int chunk) {
   const bf16_t* __restrict__ Hon = h.Hon;
   const float* __restrict__ dhead = h.dhead;
   const int B = h.B, A = h.A, HS = h.HS;
-  __shared__ float red[8][65];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ float red[16][65];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int k = chunk * 64 + lane;  // 0..HS-1
   const int col = (j == 0 ? 0 : HS) + k;
   float acc = 0.f, accb = 0.f;
 #pragma unroll 8
-  for (int b = w; b < B; b += 8) {
+  for (int b = w; b < B; b += nw) {
     const float d = dhead[(int64_t)b * (A + 1) + j];
     acc += d * bf16_to_f32(Hon[(int64_t)b * 2 * HS + col]);
     accb += d;
@@ -245,13 +245,15 @@ __device__ __forceinline__ void head_wgrad_body(const HeadWgArgs& h, int j, int 
   if (w != 0) return;
   float s = 0.f;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) s += red[q][lane];
+  for (int q = 0; q < 16; ++q)
+    if (q < nw) s += red[q][lane];
   if (j == 0) h.gwv[k] += s;
   else h.gwa[(j - 1) * HS + k] += s;
   if (lane == 0 && chunk == 0) {
     float sb = 0.f;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) sb += red[q][64];
+    for (int q = 0; q < 16; ++q)
+      if (q < nw) sb += red[q][64];
     if (j == 0) h.gbv[0] += sb;
     else h.gba[j - 1] += sb;
   }

@@ -15,6 +15,7 @@
 #include "apex_common.h"
 #include <stdlib.h>
 #include "head_common.h"
+#include "igemm_wgrad.h"
 #include "rmsprop_common.h"
 
 // Bounds-checking debug build (SURVEY §5.2 "race / bounds detection"): built as a
@@ -524,6 +525,26 @@ __global__ void __launch_bounds__(512) head_wgrad_prio_kernel(HeadWgArgs hw, Tre
   head_wgrad_body(hw, b / nch, b - (b / nch) * nch);
 }
 
+// fc weight gradient + head weight gradient + priority write-back in ONE launch
+// (all three only need the head kernel's outputs).  Block 0: the single-block tree
+// update (the latency-bound long pole, dispatched first); blocks 1..nhw: head
+// wgrad (4 waves each); from blk0 (a multiple of 8, so the XCD-contiguous tile
+// order of the GEMM part is preserved): the fc wgrad GEMM tiles (CT=4, NT=1, one
+// split, as launch_wgrad picks for the 1024 x 3136 fc).  The fc wgrad takes one
+// block per CU (96 KB LDS) and leaves ~60 CUs idle; the other two fill them.
+__global__ void __launch_bounds__(256) fc_wgrad_head_prio_kernel(WgradDesc d, int gx, int gy, HeadWgArgs hw,
+                                                                 TreeUpdArgs tu, int nhw, int blk0) {
+  const int b = blockIdx.x;
+  if (b == 0) {
+    tree_update_block(tu);
+  } else if (b <= nhw) {
+    const int nch = hw.HS / 64, q = b - 1;
+    head_wgrad_body(hw, q / nch, q - (q / nch) * nch);
+  } else if (b >= blk0) {
+    igemm_wgrad_body<0, 1, 1, 4, 1>(d, b - blk0, gx, gy, 1);
+  }
+}
+
 // optimizer + the next step's prioritized draw: blocks [0, nsb) sample, the rest
 // run the clip + centered RMSprop + bf16 pack over the flat parameters.  The tree
 // already holds this step's priorities (written by ddqn_head_prio_kernel), so the
@@ -701,5 +722,28 @@ APEX_EXPORT int apex_head_wgrad_prio(const bf16_t* Hon, const float* dhead, int 
   head_wgrad_prio_kernel<<<nblk, 512, 0, st>>>(
       HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden},
       TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)});
+  APEX_CHECK_LAUNCH();
+}
+
+// the fused launch above; returns hipErrorInvalidValue when the fc problem is not
+// the (CT=4, NT=1, single split, dense) shape it is compiled for -- the caller then
+// issues the three launches separately
+APEX_EXPORT int apex_fc_wgrad_head_prio(WgradDesc d, const bf16_t* Hon, const float* dhead, int B, int A,
+                                        float* gwv, float* gbv, float* gwa, float* gba, int hidden, TreeDesc t,
+                                        const int64_t* idx, const float* td, const int32_t* gen_expect,
+                                        const int32_t* gen, float alpha, float eps, uint64_t* ctr_to_bump,
+                                        hipStream_t st) {
+  if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || idx == nullptr) return (int)hipErrorInvalidValue;
+  if (d.mode != 0 || (d.Kc & 63) || (d.Co & 63) || d.rows_per_split < d.Mred) return (int)hipErrorInvalidValue;
+  if ((int64_t)d.Mred * d.ldd * 2 >= 0x7ffffff0LL || (int64_t)d.Mred * d.ldx * 2 >= 0x7ffffff0LL)
+    return (int)hipErrorInvalidValue;
+  const int kt = d.Kc / 64, ct = d.Co / 64;
+  if (wgrad_shape(kt, ct, d.Kc, d.Co) != 2) return (int)hipErrorInvalidValue;   // {CT,NT} = {4,1}
+  const int gx = kt, gy = ct / 4;
+  const int nhw = (A + 1) * (hidden / 64);
+  const int blk0 = (1 + nhw + 7) & ~7;
+  fc_wgrad_head_prio_kernel<<<blk0 + gx * gy, 256, 0, st>>>(
+      d, gx, gy, HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden},
+      TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)}, nhw, blk0);
   APEX_CHECK_LAUNCH();
 }

@@ -211,12 +211,18 @@ class FusedNatureLearner:
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
                  prio=(self.replay, S["idx"], S["gen"]) if _PRIO_IN_HEAD else None)
         self._mark("head")
-        with self._on_side():
-            ops.head_wgrad(self.h, self.dhead, self.G,
-                           prio=None if _PRIO_IN_HEAD else (self.replay, S["idx"], S["gen"], self.td_abs))
-        with self._on_side(self.rt.overlap_wgrad):
-            self._fc_slots = ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"],
-                                          norm=(self.norm_part, 0) if self._fuse_norm else None) or 0
+        prio = None if _PRIO_IN_HEAD else (self.replay, S["idx"], S["gen"], self.td_abs)
+        nrm = (self.norm_part, 0) if self._fuse_norm else None
+        if self._side is None:
+            # fc wgrad + head wgrad + priority write-back: one launch on the HIP backend
+            # (csrc/sumtree.hip fc_wgrad_head_prio_kernel)
+            self._fc_slots = ops.fc_head_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"], self.h,
+                                               self.dhead, self.G, prio, norm=nrm)
+        else:
+            with self._on_side():
+                ops.head_wgrad(self.h, self.dhead, self.G, prio=prio)
+            with self._on_side(self.rt.overlap_wgrad):
+                self._fc_slots = ops.fc_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"], norm=nrm) or 0
         if self.world > 1:
             self._join_side()   # the fc/heads bucket all-reduce starts right after this segment
             if self._comm_bf16:

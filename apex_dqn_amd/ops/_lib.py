@@ -117,6 +117,8 @@ _SIGS = {
                              c_p, c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
                               c_p, c_p], c_i),
+    "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,
+                                 c_p, c_f, c_f, c_p, c_p], c_i),
     "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p], c_i),
     "apex_actor_head": ([c_p, HeadParams, c_i, c_i, c_p, c_u64, c_p, c_p, c_p, c_i, c_p], c_i),
     "apex_conv1_s2d_fwd": ([Conv1S2DDesc, c_i, c_p], c_i),

@@ -327,18 +327,41 @@ def wgrad_blocks(Co: int, Kc: int) -> int:
     return (kt // best[1]) * (ct // best[0])
 
 
+def _dense_wgrad_desc(dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor,
+                      norm: Optional[Tuple[torch.Tensor, int]] = None):
+    M, Nc = dy.shape
+    K = x.shape[1]
+    extra = {} if norm is None else dict(norm_part=norm[0].data_ptr(), norm_slot0=int(norm[1]))
+    return _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=dw_out.data_ptr(), bias_slab=db_out.data_ptr(),
+                    mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M, **extra)
+
+
 def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor,
                 norm: Optional[Tuple[torch.Tensor, int]] = None) -> int:
     """dW[N,K] = dy[M,N]^T @ x[M,K] (fp32, written directly), db = sum_m dy.  With
     ``norm = (partials, slot0)`` the kernel also writes 4 squared-norm partials per
     workgroup; returns the number of slots used."""
-    M, Nc = dy.shape
-    K = x.shape[1]
-    extra = {} if norm is None else dict(norm_part=norm[0].data_ptr(), norm_slot0=int(norm[1]))
-    d = _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=dw_out.data_ptr(), bias_slab=db_out.data_ptr(),
-                 mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M, **extra)
+    d = _dense_wgrad_desc(dy, x, dw_out, db_out, norm)
     _lib.check(lib.apex_conv_wgrad(d, None, None, 1, 1.0, _lib.stream_ptr()), "dense_wgrad")
-    return 4 * wgrad_blocks(Nc, K)
+    return 4 * wgrad_blocks(dy.shape[1], x.shape[1])
+
+
+def dense_wgrad_head_prio(lib, dy, x, dw_out, db_out, norm, Hon, dhead, g, replay, idx, gen, td) -> Optional[int]:
+    """The fc weight gradient (as ``dense_wgrad``), the head weight gradient and the
+    priority write-back in one launch (csrc/sumtree.hip fc_wgrad_head_prio_kernel).
+    Returns the norm slots used, or None when the shape is not the fused kernel's
+    (nothing launched: the caller runs the three ops separately)."""
+    d = _dense_wgrad_desc(dy, x, dw_out, db_out, norm)
+    B, A1 = dhead.shape
+    rc = lib.apex_fc_wgrad_head_prio(d, Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(),
+                                     g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(), g["wv"].numel(),
+                                     replay.tree_desc(), idx.data_ptr(), td.data_ptr(), _lib.ptr(gen),
+                                     replay.gen.data_ptr(), replay.alpha, replay.eps, replay.ctr.data_ptr(),
+                                     _lib.stream_ptr())
+    if rc == 1:          # hipErrorInvalidValue: not the compiled shape
+        return None
+    _lib.check(rc, "fc_wgrad_head_prio")
+    return 4 * wgrad_blocks(dy.shape[1], x.shape[1])
 
 
 def finalize_blocks(jobs: list, norm_range: Optional[torch.Tensor]) -> int:

@@ -154,6 +154,12 @@ class TorchBackend:
         db_out.copy_(dh.float().sum(0))
         return 0
 
+    def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None) -> int:
+        """fc weight gradient + head weight gradient (+ the priority write-back,
+        ``prio = (replay, idx, gen, td_abs)``); returns the fc norm slots used."""
+        self.head_wgrad(Hon, dhead, g_head, prio=prio)
+        return self.fc_wgrad(dh, x, dw_out, db_out, norm=norm) or 0
+
     def finalize_grads(self, jobs, norm_range=None, norm=None) -> int:
         """Deferred split-K reductions (the torch path computes gradients directly)."""
         return 0
@@ -248,6 +254,15 @@ class HipBackend(TorchBackend):
         if not self.native_conv:
             return super().fc_wgrad(dh, x, dw_out, db_out)
         return C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm=norm)
+
+    def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None) -> int:
+        if self.native_conv and prio is not None and prio[0].use_hip:
+            rp, idx, gen, td = prio
+            r = C.dense_wgrad_head_prio(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm, Hon, dhead,
+                                        g_head, rp, idx, gen, td)
+            if r is not None:
+                return r
+        return super().fc_head_wgrad(dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm)
 
     def finalize_grads(self, jobs, norm_range=None, norm=None) -> int:
         """Returns the number of squared-norm partial slots written (``slot0`` + blocks)."""

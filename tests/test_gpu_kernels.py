@@ -384,3 +384,49 @@ def test_head_wgrad_prio_matches_separate_launches():
         assert torch.equal(g0[k], g1[k]), k
     assert torch.equal(l0, l1) and m0 == m1 and c0 == c1 == 1
     torch.testing.assert_close(n1, n0, rtol=1e-12, atol=1e-9)
+
+
+def test_fc_head_wgrad_prio_matches_separate_launches():
+    """fc wgrad + head wgrad + priority write-back in one launch == the three ops
+    launched separately (fc gradient, its squared-norm partials and the tree equal;
+    head gradient up to summation order)."""
+    from apex_dqn_amd.ops.fused_ops import HipBackend
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    B, A = 512, 4
+    Hon, Htg, Pon, Ptg, act, rew, gam, isw = _head_inputs(B, A, seed=8)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    dH = (torch.randn(B, 1024, generator=g) * 0.01).to(DEV, torch.bfloat16)
+    y3 = torch.relu(torch.randn(B, 3136, generator=g)).to(DEV, torch.bfloat16)
+    idx = torch.randint(0, 800, (B,), generator=g).to(DEV)
+    be = HipBackend()
+    td = torch.zeros(B, device=DEV)
+    outs = [td, torch.zeros(B, device=DEV), torch.zeros(B, 1024, device=DEV, dtype=torch.bfloat16),
+            torch.zeros(B, A + 1, device=DEV)]
+    be.head(Hon, Htg, Pon, Ptg, act, rew, gam, isw, True, 1.0, 1.0 / B, *outs)
+    res = {}
+    for fused in (False, True):
+        rp = GpuReplayShard(1000, 900, 1200, 4, device=DEV)
+        _fill_replay(rp, 1000, seed=9)
+        rp.remove_to_fit()
+        gen = rp.gen[idx].clone()
+        gw, gb = torch.zeros(1024, 3136, device=DEV), torch.zeros(1024, device=DEV)
+        gh = {"wv": torch.zeros(512, device=DEV), "bv": torch.zeros(1, device=DEV),
+              "wa": torch.zeros(A, 512, device=DEV), "ba": torch.zeros(A, device=DEV)}
+        part = torch.zeros(4096, dtype=torch.float64, device=DEV)
+        prio = (rp, idx, gen, td)
+        if fused:
+            n = be.fc_head_wgrad(dH, y3, gw, gb, Hon, outs[3], gh, prio, norm=(part, 0))
+        else:
+            be.head_wgrad(Hon, outs[3], gh, prio=prio)
+            n = be.fc_wgrad(dH, y3, gw, gb, norm=(part, 0))
+        torch.cuda.synchronize()
+        res[fused] = (n, gw, gb, gh, part, rp.leaf.clone(), rp.nodes.clone())
+    a, b = res[False], res[True]
+    assert a[0] == b[0] > 0
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2]) and torch.equal(a[4], b[4])
+    for k in a[3]:    # 4 vs 8 waves per head-wgrad block: different fixed summation order
+        torch.testing.assert_close(a[3][k], b[3][k], rtol=1e-5, atol=1e-7)
+    assert torch.equal(a[5], b[5])
+    torch.testing.assert_close(a[6], b[6], rtol=1e-12, atol=1e-9)
+    ref = dH.float().t() @ y3.float()
+    torch.testing.assert_close(b[1], ref, rtol=2e-2, atol=2e-3)
