@@ -1,0 +1,177 @@
+// conv2 of the dueling NatureCNN (4x4 stride 2, 64 -> 64 channels, 20x20 -> 9x9,
+// reference duelling_network.py:10-11) as an image-resident forward kernel.
+//
+// The generic implicit GEMM (csrc/conv_mfma.hip igemm_fwd) re-reads every input
+// pixel from L2 for each of the up-to-4 overlapping 4x4/s2 windows that use it and
+// re-stages the weights for every 128-row tile: ~255 MB of im2col operand traffic
+// per learner step for 79 MB of activations.  Here a persistent workgroup (8 waves,
+// one per CU) walks whole images:
+//   * the image (20 x 20 x 64 bf16 = 50 KB) is staged ONCE in LDS; the next image is
+//     prefetched into registers while the current one computes;
+//   * the weights never touch LDS: wave w holds the B fragments of its output-channel
+//     half (w & 1) and kernel row kh = w >> 1 (4 taps x 64 channels = K 256) in 64
+//     VGPRs, loaded once per weight set;
+//   * v_mfma_f32_32x32x16_bf16: 81 output pixels = 3 row tiles of 32, each wave runs
+//     3 x 16 MFMAs per image whose A fragments are single ds_read_b128 from the
+//     staged image (an output pixel's 8 channels of one tap are 16 contiguous bytes);
+//   * the four kernel-row partial sums meet in LDS (fp32, fixed order), then bias,
+//     ReLU, bf16 pack and 8-byte NHWC stores.
+// LDS image layout: column-parity planes (the stride-2 taps of one kw only touch one
+// parity), pixel (ih, iw) at slot ih * 10 + iw / 2 of plane iw & 1, 128 B per pixel,
+// 16-B channel chunk c stored at c ^ ((slot >> 1) & 7): the 16 lanes of a
+// ds_read_b128 phase (16 consecutive output pixels) mostly hit distinct bank groups.
+// Online / target weights switch per image (img_switch), so any batch works in one
+// launch.
+#include "mfma_common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct Conv2ImgDesc {
+  const bf16_t* x;      // [N][20][20][64] NHWC
+  const bf16_t* w;      // [64][4][4][64] OHWI (online)
+  const bf16_t* w2;     // second set (target) or null
+  const float* bias;
+  const float* bias2;
+  bf16_t* y;            // [N][9][9][64]
+  int N, img_switch;    // images >= img_switch use (w2, bias2)
+};
+
+#define C2_THREADS 512
+#define C2_IMG 51200            // staged image bytes
+#define C2_CHUNKS 3200          // 16-B chunks per image
+#define C2_PF 7                 // prefetch chunks per thread (ceil(3200 / 512))
+
+__device__ __forceinline__ int c2_lds_off(int ih, int iw, int c) {
+  const int slot = ih * 10 + (iw >> 1);
+  return ((((iw & 1) * 200 + slot)) << 7) + ((c ^ ((slot >> 1) & 7)) << 4);
+}
+
+__global__ void __launch_bounds__(C2_THREADS, 1) conv2_img_fwd_kernel(Conv2ImgDesc d) {
+  __shared__ __attribute__((aligned(16))) uint8_t simg[C2_IMG];
+  __shared__ __attribute__((aligned(16))) float red[8 * 3 * 32 * 32];   // 96 KB of partial tiles
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nh = wv & 1, kq = wv >> 1;          // output-channel half, kernel row kh
+  const int rr = lane & 31, kg = lane >> 5;     // A row in tile / 8-element K group
+  const int G = gridDim.x;
+  int img = blockIdx.x;
+  if (img >= d.N) return;
+
+  // prefetch registers: chunk q = tid + 512 i of the image (the last round: tid < 128)
+  uint4 pf0, pf1, pf2, pf3, pf4, pf5, pf6 = make_uint4(0, 0, 0, 0);
+  const bool last = tid < C2_CHUNKS - 6 * C2_THREADS;
+#define C2_PREFETCH(im)                                                                   \
+  {                                                                                       \
+    const uint4* src_ = reinterpret_cast<const uint4*>(d.x + (int64_t)(im) * (C2_IMG / 2)) + tid; \
+    pf0 = src_[0];                                                                        \
+    pf1 = src_[C2_THREADS];                                                               \
+    pf2 = src_[2 * C2_THREADS];                                                           \
+    pf3 = src_[3 * C2_THREADS];                                                           \
+    pf4 = src_[4 * C2_THREADS];                                                           \
+    pf5 = src_[5 * C2_THREADS];                                                           \
+    if (last) pf6 = src_[6 * C2_THREADS];                                                 \
+  }
+  // per m-tile: the output pixel of this lane's A row (rows past 80 repeat pixel 80)
+  int slot0[3];
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt) {
+    const int r = min(mt * 32 + rr, 80);
+    const int oh = r / 9, ow = r - oh * 9;
+    slot0[mt] = (2 * oh + kq) * 10 + ow;
+  }
+  bf16x8 bfr[16];
+  int cur_set = -1;
+  // LDS destinations of this thread's 7 chunks (fixed for every image)
+  int dst[C2_PF];
+#pragma unroll
+  for (int i = 0; i < C2_PF; ++i) {
+    const int q = min(tid + C2_THREADS * i, C2_CHUNKS - 1);
+    const int p = q >> 3, c = q & 7, ih = p / 20, iw = p - ih * 20;
+    dst[i] = c2_lds_off(ih, iw, c);
+  }
+
+  C2_PREFETCH(img);
+  for (; img < d.N; img += G) {
+    const int set = (d.w2 != nullptr && img >= d.img_switch) ? 1 : 0;
+    if (set != cur_set) {
+      const bf16_t* W = set ? d.w2 : d.w;
+      const int co = nh * 32 + rr;
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int kw = s >> 2, ci0 = ((s & 3) << 4) + kg * 8;
+        bfr[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(W + ((co * 4 + kq) * 4 + kw) * 64 + ci0));
+      }
+      cur_set = set;
+    }
+    __syncthreads();                       // previous image: compute + reduce reads done
+    *reinterpret_cast<uint4*>(simg + dst[0]) = pf0;
+    *reinterpret_cast<uint4*>(simg + dst[1]) = pf1;
+    *reinterpret_cast<uint4*>(simg + dst[2]) = pf2;
+    *reinterpret_cast<uint4*>(simg + dst[3]) = pf3;
+    *reinterpret_cast<uint4*>(simg + dst[4]) = pf4;
+    *reinterpret_cast<uint4*>(simg + dst[5]) = pf5;
+    if (last) *reinterpret_cast<uint4*>(simg + dst[6]) = pf6;
+    if (img + G < d.N) C2_PREFETCH(img + G);
+    __syncthreads();
+
+    f32x16 acc[3];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[mt][j] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int par = (s >> 2) & 1, c = ((s & 3) << 1) | kg;
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt) {
+        const int slot = slot0[mt] + (s >> 3);
+        const int off = ((par * 200 + slot) << 7) + ((c ^ ((slot >> 1) & 7)) << 4);
+        const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(simg + off));
+        acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[s], acc[mt], 0, 0, 0);
+      }
+    }
+    // partial tile of this kernel row -> LDS, [wave][tile][row][col] fp32
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int row = 8 * (j >> 2) + 4 * kg + (j & 3);
+        red[((wv * 3 + mt) * 32 + row) * 32 + rr] = acc[mt][j];
+      }
+    __syncthreads();
+    // reduce the 4 kernel rows (fixed order), bias, ReLU, bf16 pack, NHWC store:
+    // wave kq of channel half nh finishes tile rows 24 kq .. 24 kq + 23
+    const float* bias = set ? d.bias2 : d.bias;
+    const int c4 = (lane & 7) * 4;
+    const float4 bv = make_float4(bias[nh * 32 + c4], bias[nh * 32 + c4 + 1], bias[nh * 32 + c4 + 2],
+                                  bias[nh * 32 + c4 + 3]);
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int r = 24 * kq + 8 * it + (lane >> 3);
+      const int mt = r >> 5, row = r & 31;
+      float4 sum = bv;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(red + (((nh + 2 * q) * 3 + mt) * 32 + row) * 32 + c4);
+        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+      }
+      if (r < 81) {
+        const uint2 o = make_uint2(cvt_pk_bf16(fmaxf(sum.x, 0.f), fmaxf(sum.y, 0.f)),
+                                   cvt_pk_bf16(fmaxf(sum.z, 0.f), fmaxf(sum.w, 0.f)));
+        *reinterpret_cast<uint2*>(d.y + ((int64_t)img * 81 + r) * 64 + nh * 32 + c4) = o;
+      }
+    }
+  }
+#undef C2_PREFETCH
+}
+
+APEX_EXPORT int apex_conv2_img_fwd(Conv2ImgDesc d, int grid, hipStream_t st) {
+  if (d.N <= 0 || d.x == nullptr || d.w == nullptr || d.y == nullptr || d.bias == nullptr)
+    return (int)hipErrorInvalidValue;
+  if (d.w2 != nullptr && d.bias2 == nullptr) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)d.x | (uintptr_t)d.w | (uintptr_t)(d.w2 ? d.w2 : d.w)) & 15) return (int)hipErrorInvalidValue;
+  if ((uintptr_t)d.y & 7) return (int)hipErrorInvalidValue;
+  int G = grid > 0 ? grid : 256;
+  if (G > d.N) G = d.N;
+  conv2_img_fwd_kernel<<<G, C2_THREADS, 0, st>>>(d);
+  APEX_CHECK_LAUNCH();
+}

@@ -8,6 +8,8 @@ from __future__ import annotations
 
 from typing import Dict, Optional, Tuple
 
+import os as _os
+
 import torch
 
 from . import _lib
@@ -117,12 +119,38 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
     _lib.check(lib.apex_conv1_s2d_fwd(d, int(grid), _lib.stream_ptr()), "conv1_s2d_fwd")
 
 
+# conv2 (20x20x64 -> 9x9x64, 4x4/s2) on the image-resident kernel (csrc/conv2_img.hip);
+# APEX_CONV2_IMG=0 selects the generic implicit GEMM
+CONV2_IMG = _os.environ.get("APEX_CONV2_IMG", "1") != "0"
+
+
+def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
+                  w2=None, b2=None, rows_first: int = 0, grid: int = 0) -> None:
+    """conv2 + bias + ReLU, one persistent workgroup per CU walking whole images
+    (image staged once in LDS, weights in VGPRs); online/target switch per image."""
+    from .conv_sigs import Conv2ImgDesc
+    N = x.shape[0]
+    assert tuple(x.shape[1:]) == (20, 20, 64) and tuple(w.shape) == (64, 4, 4, 64) and tuple(out.shape) == (N, 9, 9, 64)
+    assert x.is_contiguous() and out.is_contiguous() and w.is_contiguous()
+    d = Conv2ImgDesc()
+    d.x, d.w, d.bias, d.y = x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr()
+    if w2 is not None:
+        assert w2.is_contiguous() and tuple(w2.shape) == (64, 4, 4, 64)
+        d.w2, d.bias2 = w2.data_ptr(), b2.data_ptr()
+    d.N, d.img_switch = N, int(rows_first) if w2 is not None else N
+    _lib.check(lib.apex_conv2_img_fwd(d, int(grid), _lib.stream_ptr()), "conv2_img_fwd")
+
+
 def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int, out: torch.Tensor,
              w2=None, b2=None, rows_first: int = 0) -> None:
     """NHWC conv + bias + ReLU with OHWI weights (conv2 / conv3)."""
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     OH, OW = out.shape[1], out.shape[2]
+    if CONV2_IMG and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
+            hasattr(lib, "apex_conv2_img_fwd"):
+        conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first)
+        return
     if not _split_ok(w2, rows_first, OH * OW):   # batch not tile-aligned: one launch per weight set
         conv_fwd(lib, x[:rows_first], w, b, stride, out[:rows_first])
         conv_fwd(lib, x[rows_first:], w2, b2, stride, out[rows_first:])
@@ -136,7 +164,6 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
 # split-K of the dense forward GEMM (fc): the 1536 x 1024 output of the NatureCNN
 # learner is only 192 128x64 tiles for 256 CUs; splitting its K = 3136 fills the
 # chip, and one elementwise pass sums the fp32 partials + bias + ReLU (APEX_FC_KSPLIT)
-import os as _os
 DENSE_KSPLIT = int(_os.environ.get("APEX_FC_KSPLIT", "0"))   # 0 = auto
 
 

@@ -1,4 +1,4 @@
-"""ctypes signatures of the conv / GEMM kernel family (csrc/conv_mfma.hip, csrc/gemm_mfma.hip)."""
+"""ctypes signatures of the conv / GEMM kernel family (csrc/conv_mfma.hip, csrc/conv2_img.hip)."""
 from __future__ import annotations
 
 import ctypes
@@ -9,9 +9,16 @@ c_i64 = ctypes.c_int64
 c_f = ctypes.c_float
 
 
+class Conv2ImgDesc(ctypes.Structure):
+    """Image-resident conv2 forward (mirrors ``Conv2ImgDesc`` in csrc/conv2_img.hip)."""
+    _fields_ = [("x", c_p), ("w", c_p), ("w2", c_p), ("bias", c_p), ("bias2", c_p), ("y", c_p),
+                ("N", c_i), ("img_switch", c_i)]
+
+
 def declare(lib: ctypes.CDLL) -> None:
     from ._lib import ConvDesc, WgradDesc
     sigs = {
+        "apex_conv2_img_fwd": ([Conv2ImgDesc, c_i, c_p], c_i),
         "apex_conv_fwd": ([ConvDesc, c_p], c_i),
         "apex_conv_wgrad": ([WgradDesc, c_p, c_p, c_i, c_f, c_p], c_i),
         "apex_pack_dgrad_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),

@@ -265,3 +265,22 @@ def test_conv1_s2d_frame_stacks_and_ring_layout(C):
     Cv.conv1_wgrad_ring(_lib(), Cv.Workspace(), dy, rp.frames, slots, 1 / 255.0, dw, db)
     rdw, _ = R.conv1_wgrad(dy.float(), raw[slots.long().cpu()].to(DEV), 1 / 255.0)
     assert _rel(dw, rdw) < 5e-3
+
+
+@pytest.mark.parametrize("N,grid,switch", [(37, 3, 20), (300, 0, 200), (1, 0, 1)])
+def test_conv2_image_resident_vs_torch(N, grid, switch):
+    """csrc/conv2_img.hip: several images per workgroup (grid < N), the online /
+    target weight switch inside a workgroup's image walk, vs the fp32 torch conv."""
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N)
+    x = _bf(torch.relu(torch.randn(N, 20, 20, 64, generator=g)))
+    wa = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+    wb = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+    ba = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    bb = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    out = torch.empty(N, 9, 9, 64, dtype=torch.bfloat16, device=DEV)
+    C.conv2_img_fwd(_lib(), x, wa, ba, out, wb, bb, switch, grid=grid)
+    ref = torch.cat([R.conv_fwd(x[:switch].float(), wa.float(), ba, 2),
+                     R.conv_fwd(x[switch:].float(), wb.float(), bb, 2)]) if switch < N else \
+        R.conv_fwd(x.float(), wa.float(), ba, 2)
+    assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
