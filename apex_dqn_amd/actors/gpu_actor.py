@@ -18,6 +18,14 @@ Here one step of the group:
 The actor keeps its own parameter slot (bf16 weights + fp32 biases/heads),
 refreshed from the learner with a D2D copy every ``Q_network_sync_freq``
 steps (reference ``actor.py:189-191``).
+
+Actor and learner overlap (the reference runs them as separate processes): the
+group's frame appends, inference and D2H copies run on its own stream, and
+``policy`` waits for that stream only, so the env stepping on the host and the
+actor's kernels proceed while the learner's step is still executing on the
+compute stream.  Transition inserts (records + sum-tree) stay on the compute
+stream -- single writer, stream-ordered with the learner's sampling and priority
+write-back -- after a wait on the actor stream for the frames they reference.
 """
 from __future__ import annotations
 
@@ -73,15 +81,45 @@ class GpuActorGroup:
         self.t = 0
         self.episodes: List[tuple] = []
         self.inserted = 0
+        self._init_stream()
+
+    # ---------------------------------------------------------------- stream
+    def _init_stream(self) -> None:
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+
+    def _on_stream(self):
+        import contextlib
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def _wait_stream(self) -> None:
+        """Host waits for the actor stream only (not for the learner's queued step)."""
+        if self.stream is not None:
+            self.stream.synchronize()
+
+    def _after_learner(self) -> None:
+        """Actor stream waits for everything queued on the compute stream so far."""
+        if self.stream is not None:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+
+    def _before_insert(self) -> None:
+        """Compute stream waits for the actor stream's frame appends."""
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
 
     # ---------------------------------------------------------------- params
     def sync_params(self) -> None:
+        self._after_learner()
+        with self._on_stream():
+            self._copy_params()
+
+    def _copy_params(self) -> None:
         self.p32.copy_(self.learner.p32)
         self.pbf.copy_(self.learner.pbf)
 
     # --------------------------------------------------------------- acting
     def _ingest(self, frames: np.ndarray, reset_mask: np.ndarray) -> np.ndarray:
-        seqs = self.replay.append_frames(frames)
+        with self._on_stream():
+            seqs = self.replay.append_frames(frames)
         if self.payload is None:
             cur = np.repeat(seqs[:, None], self.C, axis=1)
         else:
@@ -95,7 +133,13 @@ class GpuActorGroup:
         self.payload = self._ingest(self.env.reset(), np.ones(self.E, bool))
 
     def policy(self, payload: np.ndarray):
-        """Batched q + epsilon-greedy for the given frame-seq payload (E, C)."""
+        """Batched q + epsilon-greedy for the given frame-seq payload (E, C) (actor stream)."""
+        with self._on_stream():
+            self._policy(payload)
+        self._wait_stream()
+        return self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64)
+
+    def _policy(self, payload: np.ndarray):
         ops, P, Pb = self.ops, self.P, self.Pb
         self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
         ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
@@ -108,9 +152,6 @@ class GpuActorGroup:
         self.ctr += 1
         self.q_host.copy_(self.q, non_blocking=True)
         self.a_host.copy_(self.act, non_blocking=True)
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
-        return self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64)
 
     def step(self) -> int:
         """One env step for all E envs; returns the number of transitions inserted."""
@@ -131,6 +172,7 @@ class GpuActorGroup:
         if self.builder.size >= self.cfg.Actor.n_step_transition_batch_size:
             b = self.builder.get()
             if b is not None:
+                self._before_insert()
                 self.replay.insert(b)
                 n = len(b["A_t"])
                 self.inserted += n
@@ -169,13 +211,14 @@ class GraphActorGroup(GpuActorGroup):
         self.t = 0
         self.episodes = []
         self.inserted = 0
+        self._init_stream()
 
-    def sync_params(self) -> None:
+    def _copy_params(self) -> None:
         with torch.no_grad():
             for dst, src in zip(self.net.parameters(), self.learner.Q.parameters()):
                 dst.copy_(src)
 
-    def policy(self, payload: np.ndarray):
+    def _policy(self, payload: np.ndarray):
         self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
         frames = self.replay.gather_frames(self.slots)
         q = self.learner.actor_forward(self.net, frames)
@@ -185,9 +228,6 @@ class GraphActorGroup(GpuActorGroup):
         act = torch.where(u < self.eps, rand_a, greedy)
         self.q_host.copy_(q, non_blocking=True)
         self.a_host.copy_(act, non_blocking=True)
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
-        return self.q_host.numpy().copy(), self.a_host.numpy().copy()
 
 
 class ImpalaActorGroup(GpuActorGroup):
@@ -223,11 +263,12 @@ class ImpalaActorGroup(GpuActorGroup):
         self.t = 0
         self.episodes = []
         self.inserted = 0
+        self._init_stream()
 
-    def sync_params(self) -> None:
+    def _copy_params(self) -> None:
         self.learner.refresh_param_set(self.ps)
 
-    def policy(self, payload: np.ndarray):
+    def _policy(self, payload: np.ndarray):
         self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
         h = self.learner.trunk_forward(self.slots, self.ps, self.bufs)
         heads = {k: self.ps["V"][k] for k in ("wv", "bv", "wa", "ba")}
@@ -235,9 +276,6 @@ class ImpalaActorGroup(GpuActorGroup):
         self.ctr += 1
         self.q_host.copy_(self.q, non_blocking=True)
         self.a_host.copy_(self.act, non_blocking=True)
-        if self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
-        return self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64)
 
 
 def make_gpu_actor_group(cfg, learner, replay, num_envs: int, rank: int = 0, world: int = 1,

@@ -95,9 +95,13 @@ class GpuReplayShard:
         self.live = 0
         self.frame_head = 0    # next frame sequence number
         self.total_inserted = 0
-        # bumped by every host-side mutation of the sampling state (inserts, frames,
-        # eviction, rebuild): a learner that samples its next batch ahead of time
-        # (inside the previous step) resamples when this changed in between
+        # bumped by host-side mutations that can invalidate a batch drawn ahead of time
+        # (eviction, rebuild): a learner that samples its next batch inside the previous
+        # step resamples when this changed in between.  Inserts and frame appends do
+        # not: the early draw is then a proportional sample of the replay as of the end
+        # of the previous update (Ape-X's learner consumes prefetched batches the same
+        # way), its records are gathered copies, and a slot re-used before the priority
+        # write-back is caught by the generation check.
         self.version = 0
         self.min_frame_seq = np.full(self.cap, -1, np.int64)  # oldest frame referenced per slot
         self._tdesc = None
@@ -133,7 +137,6 @@ class GpuReplayShard:
     # --------------------------------------------------------------- insert
     def append_frames(self, frames) -> np.ndarray:
         """Store new frames (n, H, W) uint8; returns their sequence numbers."""
-        self.version += 1
         frames = torch.as_tensor(frames)
         n = frames.shape[0]
         seqs = self.frame_head + np.arange(n, dtype=np.int64)
@@ -157,7 +160,6 @@ class GpuReplayShard:
 
     def insert(self, batch: Dict[str, np.ndarray]) -> np.ndarray:
         """Insert n-step transitions whose S_t/S_tpn payloads are frame seqs (K, C)."""
-        self.version += 1
         K = len(batch["A_t"])
         if K == 0:
             return np.zeros(0, np.int64)
