@@ -72,7 +72,8 @@ class Comm:
 
     def barrier(self) -> None:
         if self.active:
-            if self.device is not None and torch.device(self.device).type == "cuda":
+            if (self.device is not None and torch.device(self.device).type == "cuda"
+                    and dist.get_backend(self.group) == "nccl"):
                 dist.barrier(device_ids=[torch.device(self.device).index or 0])
             else:
                 dist.barrier()

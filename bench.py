@@ -45,6 +45,8 @@ def main():
                     help="sample at the head of each step instead of inside the previous step's optimizer launch")
     ap.add_argument("--overlap-wgrad", action="store_true",
                     help="weight-gradient GEMMs on a side stream beside the dgrad chain (default: one stream)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (rehearsing several ranks on one GPU)")
     ap.add_argument("--graph-steps", type=int, default=None,
                     help="learner updates per HIP-graph launch (Runtime.graph_steps; 1 = one graph per update)")
     ap.add_argument("--graph-impala", action="store_true",
@@ -68,7 +70,7 @@ def main():
     dev_idx = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_idx)
     device = torch.device("cuda", dev_idx)
-    comm = Comm.from_env(backend="nccl", device=device)
+    comm = Comm.from_env(backend=args.dist_backend, device=device)
 
     cfg = ApexConfig.from_dict({
         "env_conf": {"state_shape": [4, 84, 84], "action_dim": args.actions, "name": "SyntheticPong"},

@@ -1,4 +1,4 @@
-"""Data-parallel learner over gloo (CPU, world_size 2): the fake cluster.
+"""Data-parallel learner over gloo (CPU, world_size 2 and 4): the fake cluster.
 
 Checks that the bucketed, overlapped gradient all-reduce of the fused learner
 equals the mean of the per-rank gradients, that parameters stay bit-identical
@@ -64,15 +64,14 @@ def _worker(rank, world, path, q, ar="fp32"):
     g_mean = torch.stack(gl).mean(0)
     pl = [torch.zeros_like(L.p32) for _ in range(world)]
     torch.distributed.all_gather(pl, L.p32.clone())
-    q.put((rank, float((g_dp - g_mean).abs().max()), float(g_mean.abs().max()),
-           float((pl[0] - pl[1]).abs().max()), ratio_global, ratio_local0))
+    perr = max(float((pl[0] - p).abs().max()) for p in pl[1:])
+    q.put((rank, float((g_dp - g_mean).abs().max()), float(g_mean.abs().max()), perr, ratio_global, ratio_local0))
     comm.shutdown()
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("ar", ["fp32", "bf16"])
-def test_dp_learner_gloo_world2(ar):
-    world = 2
+@pytest.mark.parametrize("ar,world", [("fp32", 2), ("bf16", 2), ("fp32", 4)])
+def test_dp_learner_gloo(ar, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as td:
