@@ -51,17 +51,32 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
   const float lr = A_.lr, alpha = A_.alpha, eps = A_.eps;
   const int centered = A_.centered;
   __shared__ float sh[2];
-  const float coef = clip_coef_from_partials(A_.partials, A_.npart, A_.clip, sh);
-  if (bid == 0 && threadIdx.x == 0 && A_.norm_out) A_.norm_out[0] = sh[1];
-  const float a1 = 1.0f - alpha;
   const int64_t n4 = n / 4;
   float4* p4 = reinterpret_cast<float4*>(p);
   const float4* g4 = reinterpret_cast<const float4*>(g);
   float4* v4 = reinterpret_cast<float4*>(v);
   float4* m4 = reinterpret_cast<float4*>(m);
   uint2* pb4 = reinterpret_cast<uint2*>(pb);
-  for (int64_t i = (int64_t)bid * blockDim.x + threadIdx.x; i < n4; i += (int64_t)nblk * blockDim.x) {
-    float4 gg = g4[i], pp = p4[i], vv = v4[i], mm = centered ? m4[i] : make_float4(0, 0, 0, 0);
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
+  // the first chunk's loads are in flight while the block sums the clip-norm
+  // partials, and every iteration prefetches the next chunk (one-deep pipeline)
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 gg = z4, pp = z4, vv = z4, mm = z4;
+  if (i < n4) {
+    gg = g4[i]; pp = p4[i]; vv = v4[i];
+    if (centered) mm = m4[i];
+  }
+  const float coef = clip_coef_from_partials(A_.partials, A_.npart, A_.clip, sh);
+  if (bid == 0 && threadIdx.x == 0 && A_.norm_out) A_.norm_out[0] = sh[1];
+  const float a1 = 1.0f - alpha;
+  for (; i < n4; i += stride) {
+    const int64_t inx = i + stride;
+    float4 gn = z4, pn = z4, vn = z4, mn = z4;
+    if (inx < n4) {
+      gn = g4[inx]; pn = p4[inx]; vn = v4[inx];
+      if (centered) mn = m4[inx];
+    }
     float gx[4] = {gg.x * coef, gg.y * coef, gg.z * coef, gg.w * coef};
     float px[4] = {pp.x, pp.y, pp.z, pp.w};
     float vx[4] = {vv.x, vv.y, vv.z, vv.w};
@@ -80,6 +95,7 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
     v4[i] = make_float4(vx[0], vx[1], vx[2], vx[3]);
     if (centered) m4[i] = make_float4(mx[0], mx[1], mx[2], mx[3]);
     pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
+    gg = gn; pp = pn; vv = vn; mm = mn;
   }
   for (int64_t i = n4 * 4 + (int64_t)bid * blockDim.x + threadIdx.x; i < n; i += (int64_t)nblk * blockDim.x) {
     float gg = g[i] * coef;
