@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from ..config import epsilon_ladder
-from .nstep import NStepBuilder
+from .nstep import make_nstep_builder
 
 
 class HostFrameStore:
@@ -75,7 +75,7 @@ class ActorGroup:
             self.mode = "state"
             obs_shape, obs_dtype = tuple(env.obs_shape), np.float32
         self.obs_builder = obs_builder
-        self.builder = NStepBuilder(self.E, n, gamma, obs_shape, obs_dtype,
+        self.builder = make_nstep_builder(self.E, n, gamma, obs_shape, obs_dtype,
                                     env_id_offset=global_actor_offset)
         self.t = 0
         self.episodes = []   # (env_id, ep_len, ep_return)

@@ -35,7 +35,7 @@ import numpy as np
 import torch
 
 from ..config import epsilon_ladder
-from .nstep import NStepBuilder
+from .nstep import make_nstep_builder
 
 
 class GpuActorGroup:
@@ -76,7 +76,7 @@ class GpuActorGroup:
         self.pbf = learner.pbf.clone()
         self.P = learner.layout.views(self.p32)
         self.Pb = learner.layout.views(self.pbf)
-        self.builder = NStepBuilder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
         self.payload: Optional[np.ndarray] = None
         self.t = 0
         self.episodes: List[tuple] = []
@@ -206,7 +206,7 @@ class GraphActorGroup(GpuActorGroup):
         self.a_host = torch.zeros(self.E, dtype=torch.int64)
         if d.type == "cuda":
             self.q_host, self.a_host = self.q_host.pin_memory(), self.a_host.pin_memory()
-        self.builder = NStepBuilder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
         self.payload = None
         self.t = 0
         self.episodes = []
@@ -258,7 +258,7 @@ class ImpalaActorGroup(GpuActorGroup):
         self.a_host = torch.zeros(self.E, dtype=torch.int32)
         if d.type == "cuda":
             self.q_host, self.a_host = self.q_host.pin_memory(), self.a_host.pin_memory()
-        self.builder = NStepBuilder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
         self.payload = None
         self.t = 0
         self.episodes = []

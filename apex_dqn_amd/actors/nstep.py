@@ -155,6 +155,17 @@ class NStepBuilder:
         return out
 
 
+def make_nstep_builder(num_envs: int, n: int, gamma: float, obs_shape, obs_dtype, env_id_offset: int = 0):
+    """The native builder (csrc/runtime/nstep.cpp) when the host runtime library is
+    available, else this numpy one (its test oracle).  APEX_NUMPY_NSTEP=1 forces numpy."""
+    import os
+    if os.environ.get("APEX_NUMPY_NSTEP", "0") != "1":
+        from ..runtime import native
+        if native.available():
+            return native.NativeNStepBuilder(num_envs, n, gamma, obs_shape, obs_dtype, env_id_offset)
+    return NStepBuilder(num_envs, n, gamma, obs_shape, obs_dtype, env_id_offset)
+
+
 def nstep_returns_reference(rewards, dones, gamma: float, n: int):
     """Slow scalar oracle for a single env trajectory (used by tests).
 

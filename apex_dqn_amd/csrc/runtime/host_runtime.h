@@ -36,3 +36,12 @@ APEX_RT_API void apex_rt_cp_step(double* state, int64_t* t, double* ep_ret, uint
 APEX_RT_API int64_t apex_rt_seqlock_write(uint64_t* seq, void* dst, const void* src, int64_t nbytes);
 APEX_RT_API int64_t apex_rt_seqlock_read(const uint64_t* seq, void* dst, const void* src, int64_t nbytes,
                                          int64_t last, int max_tries);
+
+// ---- sliding-window n-step transition builder (csrc/runtime/nstep.cpp)
+APEX_RT_API void* apex_rt_ns_create(int E, int n, double gamma, int obs_bytes, int64_t env_id_offset);
+APEX_RT_API void apex_rt_ns_destroy(void* h);
+APEX_RT_API int apex_rt_ns_step(void* h, const void* obs, const float* q, int A, const int64_t* actions,
+                                const float* rewards, const uint8_t* dones, const void* next_obs);
+APEX_RT_API int64_t apex_rt_ns_size(void* h);
+APEX_RT_API int64_t apex_rt_ns_take(void* h, int64_t max_items, void* obs, void* nxt, int64_t* act, float* R,
+                                    float* G, float* prio, int64_t* key, int64_t* env);

@@ -108,11 +108,58 @@ static int test_seqlock() {
   return 0;
 }
 
+// n-step builder: random episode ends, partial and full takes; every emitted
+// transition's discount is gamma^n or 0 and the buffers drain to empty
+static int test_nstep() {
+  const int E = 9, A = 4, n = 3;
+  void* h = apex_rt_ns_create(E, n, 0.99, 4 * sizeof(int64_t), 5);
+  CHECK(h != nullptr);
+  CHECK(apex_rt_ns_create(0, n, 0.99, 8, 0) == nullptr);
+  std::vector<int64_t> obs(E * 4), nxt(E * 4), act(E);
+  std::vector<float> q(E * A), rew(E);
+  std::vector<uint8_t> done(E);
+  uint64_t x = 0x1234567ull;
+  auto rnd = [&]() { x = x * 6364136223846793005ull + 1442695040888963407ull; return (uint32_t)(x >> 33); };
+  int64_t total = 0;
+  for (int t = 0; t < 500; ++t) {
+    for (int e = 0; e < E; ++e) {
+      for (int c = 0; c < 4; ++c) nxt[e * 4 + c] = rnd();
+      for (int a = 0; a < A; ++a) q[e * A + a] = (float)(rnd() % 100) * 0.01f;
+      act[e] = rnd() % A;
+      rew[e] = (float)(rnd() % 7) - 3.0f;
+      done[e] = (rnd() % 13) == 0;
+    }
+    CHECK(apex_rt_ns_step(h, obs.data(), q.data(), A, act.data(), rew.data(), done.data(), nxt.data()) == 0);
+    obs = nxt;
+    const int64_t sz = apex_rt_ns_size(h);
+    if (t % 5 == 4 && sz > 0) {
+      const int64_t k = (t % 10 == 9) ? -1 : sz / 2 + 1;
+      const int64_t m = k < 0 ? sz : k;
+      std::vector<int64_t> o(m * 4), nx(m * 4), a(m), key(m), env(m);
+      std::vector<float> R(m), G(m), pr(m);
+      const int64_t got = apex_rt_ns_take(h, k, o.data(), nx.data(), a.data(), R.data(), G.data(), pr.data(),
+                                          key.data(), env.data());
+      CHECK(got == m);
+      for (int64_t i = 0; i < got; ++i) {
+        CHECK(G[i] == 0.0f || std::fabs(G[i] - 0.970299f) < 1e-6f);
+        CHECK(env[i] >= 5 && env[i] < 5 + E && a[i] >= 0 && a[i] < A && pr[i] >= 0.0f);
+      }
+      total += got;
+    }
+  }
+  act[0] = A;  // out of range: rejected
+  CHECK(apex_rt_ns_step(h, obs.data(), q.data(), A, act.data(), rew.data(), done.data(), nxt.data()) == 1);
+  CHECK(total > 1000);
+  apex_rt_ns_destroy(h);
+  return 0;
+}
+
 int main() {
   CHECK(apex_rt_version() == 1);
   if (test_sumtree()) return 1;
   if (test_cartpole()) return 1;
   if (test_seqlock()) return 1;
+  if (test_nstep()) return 1;
   std::puts("runtime selftest OK");
   return 0;
 }

@@ -30,6 +30,11 @@ _SIGS = {
     "apex_rt_cp_step": ([c_p, c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_p], None),
     "apex_rt_seqlock_write": ([c_p, c_p, c_p, c_i64], c_i64),
     "apex_rt_seqlock_read": ([c_p, c_p, c_p, c_i64, c_i64, c_i], c_i64),
+    "apex_rt_ns_create": ([c_i, c_i, c_d, c_i, c_i64], c_p),
+    "apex_rt_ns_destroy": ([c_p], None),
+    "apex_rt_ns_step": ([c_p, c_p, c_p, c_i, c_p, c_p, c_p, c_p], c_i),
+    "apex_rt_ns_size": ([c_p], c_i64),
+    "apex_rt_ns_take": ([c_p, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i64),
 }
 
 
@@ -125,6 +130,57 @@ class NativeCartPoleVec(CartPoleVec):
         info = {"episode_return": self._iret.copy(), "episode_length": self._ilen.copy(),
                 "truncated": self._trunc.astype(bool)}
         return self._obs.copy(), self._rew.copy(), done, info
+
+
+class NativeNStepBuilder:
+    """``actors.nstep.NStepBuilder`` in C++ (csrc/runtime/nstep.cpp): same
+    semantics, emission order and ``get`` batches; observations are opaque
+    fixed-shape payloads of ``obs_dtype``."""
+
+    def __init__(self, num_envs: int, n: int, gamma: float, obs_shape, obs_dtype, env_id_offset: int = 0):
+        self.E, self.n, self.gamma = int(num_envs), int(n), float(gamma)
+        self.obs_shape = tuple(obs_shape)
+        self.obs_dtype = np.dtype(obs_dtype)
+        self._ob = int(np.prod(self.obs_shape)) * self.obs_dtype.itemsize
+        self.env_ids = np.arange(self.E, dtype=np.int64) + int(env_id_offset)
+        self._lib = lib()
+        self._h = self._lib.apex_rt_ns_create(self.E, self.n, self.gamma, self._ob, int(env_id_offset))
+        if not self._h:
+            raise ValueError("invalid n-step builder shape")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h and self._lib is not None:
+            self._lib.apex_rt_ns_destroy(h)
+
+    def step(self, obs, q, actions, rewards, dones, next_obs) -> None:
+        obs = np.ascontiguousarray(obs, self.obs_dtype)
+        nxt = np.ascontiguousarray(next_obs, self.obs_dtype)
+        q = np.ascontiguousarray(q, np.float32)
+        a = np.ascontiguousarray(actions, np.int64)
+        r = np.ascontiguousarray(rewards, np.float32)
+        d = np.ascontiguousarray(dones, np.uint8)
+        if self._lib.apex_rt_ns_step(self._h, _ptr(obs), _ptr(q), q.shape[1], _ptr(a), _ptr(r), _ptr(d),
+                                     _ptr(nxt)) != 0:
+            raise IndexError("action out of range")
+
+    @property
+    def size(self) -> int:
+        return int(self._lib.apex_rt_ns_size(self._h))
+
+    def get(self, max_items: Optional[int] = None):
+        k = self.size if max_items is None else min(self.size, int(max_items))
+        if self.size == 0:
+            return None
+        out = dict(S_t=np.empty((k,) + self.obs_shape, self.obs_dtype),
+                   S_tpn=np.empty((k,) + self.obs_shape, self.obs_dtype),
+                   A_t=np.empty(k, np.int64), R=np.empty(k, np.float32), Gamma=np.empty(k, np.float32),
+                   priority=np.empty(k, np.float32), key=np.empty(k, np.int64), env=np.empty(k, np.int64))
+        got = self._lib.apex_rt_ns_take(self._h, k, _ptr(out["S_t"]), _ptr(out["S_tpn"]), _ptr(out["A_t"]),
+                                        _ptr(out["R"]), _ptr(out["Gamma"]), _ptr(out["priority"]),
+                                        _ptr(out["key"]), _ptr(out["env"]))
+        assert got == k
+        return out
 
 
 class SeqLock:

@@ -96,7 +96,7 @@ def test_runtime_under_host_sanitizers(tmp_path):
     exe = str(tmp_path / "rt_selftest")
     cmd = ["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
            "-I", src, os.path.join(src, "tests", "runtime_selftest.cpp"), os.path.join(src, "host_runtime.cpp"),
-           "-lpthread", "-o", exe]
+           os.path.join(src, "nstep.cpp"), "-lpthread", "-o", exe]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
     # verify_asan_link_order=0: tolerate other preloaded libraries in the environment
@@ -104,3 +104,46 @@ def test_runtime_under_host_sanitizers(tmp_path):
                UBSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout + r.stderr)[-3000:]
+
+
+@pytest.mark.parametrize("obs_shape,dtype", [((4,), np.int64), ((4,), np.float32)])
+def test_native_nstep_builder_matches_numpy_oracle(obs_shape, dtype):
+    """csrc/runtime/nstep.cpp == actors/nstep.py (the oracle): same transitions, in the
+    same order, with the same keys / returns / discounts / initial priorities,
+    across random episode ends and partial takes."""
+    from apex_dqn_amd.actors.nstep import NStepBuilder
+    from apex_dqn_amd.runtime import native
+    if not native.available():
+        pytest.skip("native runtime unavailable")
+    E, A, n = 7, 5, 3
+    ref = NStepBuilder(E, n, 0.97, obs_shape, dtype, env_id_offset=11)
+    nat = native.NativeNStepBuilder(E, n, 0.97, obs_shape, dtype, env_id_offset=11)
+    rng = np.random.default_rng(3)
+    obs = rng.integers(0, 1000, (E,) + obs_shape).astype(dtype)
+    got_r, got_n = [], []
+    for t in range(200):
+        q = rng.normal(size=(E, A)).astype(np.float32)
+        a = rng.integers(0, A, E)
+        r = rng.normal(size=E).astype(np.float32)
+        d = rng.random(E) < 0.08
+        nxt = rng.integers(0, 1000, (E,) + obs_shape).astype(dtype)
+        ref.step(obs, q, a, r, d, nxt)
+        nat.step(obs, q, a, r, d, nxt)
+        assert ref.size == nat.size
+        if t % 7 == 6:
+            k = int(rng.integers(1, 40))
+            for lst, b in ((got_r, ref), (got_n, nat)):
+                out = b.get(k)
+                if out is not None:
+                    lst.append(out)
+        obs = nxt
+    for lst, b in ((got_r, ref), (got_n, nat)):
+        out = b.get()
+        if out is not None:
+            lst.append(out)
+    cat = lambda L, k: np.concatenate([o[k] for o in L])  # noqa: E731
+    for k in ("S_t", "S_tpn", "A_t", "key", "env"):
+        assert np.array_equal(cat(got_r, k), cat(got_n, k)), k
+    for k in ("R", "Gamma", "priority"):
+        np.testing.assert_allclose(cat(got_n, k), cat(got_r, k), rtol=1e-6, atol=1e-6)
+    assert len(cat(got_r, "A_t")) > 500
