@@ -38,7 +38,7 @@ struct WgradDesc {
 // an all-ones fragment, done by the waves owning Kc tile 0 -- no VALU sums.
 #define WG_ROWS 64
 #define WG_IMG 8192                     // one 64-row x 128-B operand image
-#define WG_TBL 4096                     // u32 row-offset table entries (16 KB)
+#define WG_TBL 1024                     // u32 row-offset table entries (4 KB; dense mode: none)
 
 // MODE: X-operand source (0 dense rows, 1 NHWC im2col (pad 0), 2 s2d uint8 ring).
 // OWC/OHWC: output width / pixels per image as compile-time constants (0 = runtime);
@@ -50,7 +50,9 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
   constexpr int NIMG = CT + NT;
   constexpr int STAGE = NIMG * WG_IMG;
   constexpr int NTHR = 256;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE + WG_TBL * 4];
+  // dense rows (MODE 0) need no row table: 80 KB for a 4-tile block, two blocks per CU
+  constexpr int TBL = MODE == 0 ? 0 : WG_TBL;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE + TBL * 4];
   uint32_t* tbl = reinterpret_cast<uint32_t*>(smem + 2 * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // XCD-contiguous order: the Kc / Co blocks of one split (same dY rows, overlapping

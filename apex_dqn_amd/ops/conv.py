@@ -252,7 +252,7 @@ def _wg_desc(**kw) -> "_lib.WgradDesc":
 
 _WG_ROWS_ENV = {3: int(_os.environ.get("APEX_WG_ROWS3", "0")), 4: int(_os.environ.get("APEX_WG_ROWS2", "0"))}
 _WG_ROWS = 64       # reduction rows per kernel step (csrc/conv_mfma.hip WG_ROWS)
-_WG_TBL = 4096      # per-block row-offset table entries (WG_TBL)
+_WG_TBL = 1024      # per-block row-offset table entries (WG_TBL)
 
 
 def _splits(Mred: int, target_rows: int, max_rows: int) -> Tuple[int, int]:
@@ -267,13 +267,14 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     """dW (OHWI, fp32) and db for an NHWC conv with 64 output channels.  With
     ``jobs``, the split-K reduction is appended there for ``finalize_grads``.
     ``target_rows``: reduction rows per split-K block (0 = tuned default: fewer
-    rows for the small 3x3 layer, whose 9 output tiles need more splits; 704 for
+    rows for the small 3x3 layer, whose 9 output tiles need more splits (384: two
+    68 KB blocks per CU); 704 for
     conv2 keeps its 4 x 59 blocks (96 KB LDS each, one per CU) in a single wave
     on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  APEX_WG_ROWS3 / APEX_WG_ROWS2
     override for sweeps."""
     N, OH, OW, Co = dy.shape
     if target_rows <= 0:
-        target_rows = _WG_ROWS_ENV.get(KH) or (512 if KH == 3 else 704)
+        target_rows = _WG_ROWS_ENV.get(KH) or (384 if KH == 3 else 704)
     _, H, W, Cin = x.shape
     Kc = KH * KH * Cin
     Mred = N * OH * OW
