@@ -268,9 +268,8 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     ``jobs``, the split-K reduction is appended there for ``finalize_grads``.
     ``target_rows``: reduction rows per split-K block (0 = tuned default: fewer
     rows for the small 3x3 layer, whose 9 output tiles need more splits (384: two
-    68 KB blocks per CU); 704 for
-    conv2 keeps its 4 x 59 blocks (96 KB LDS each, one per CU) in a single wave
-    on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  APEX_WG_ROWS3 / APEX_WG_ROWS2
+    68 KB blocks per CU); 704 for conv2 keeps its 4 x 59 blocks (84 KB LDS each,
+    one per CU) in a single wave on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  APEX_WG_ROWS3 / APEX_WG_ROWS2
     override for sweeps."""
     N, OH, OW, Co = dy.shape
     if target_rows <= 0:
