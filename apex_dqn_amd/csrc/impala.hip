@@ -836,15 +836,20 @@ template <int H, int W>
 __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restrict__ dy, int64_t dy_img,
                                                           const uint8_t* __restrict__ amax, int P,
                                                           bf16_t* __restrict__ dx, int64_t dx_img, int N) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = (int64_t)N * P * H * W * 2;
+  // 32-bit index math (the launcher checks N * P * H * W * 2 < 2^31): compile-time
+  // H / W divide by multiply-shift, no 64-bit division sequences
+  const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+  const uint32_t total = (uint32_t)N * (uint32_t)P * (uint32_t)(H * W * 2);
   if (idx >= total) return;
-  const int hf = (int)(idx & 1);
-  int64_t r = idx >> 1;
-  const int w = (int)(r % W); r /= W;
-  const int h = (int)(r % H); r /= H;
-  const int p = (int)(r % P);
-  const int n = (int)(r / P);
+  const int hf = (int)(idx & 1u);
+  uint32_t r = idx >> 1;
+  const uint32_t rw = r / (uint32_t)W;
+  const int w = (int)(r - rw * (uint32_t)W);
+  const uint32_t rh = rw / (uint32_t)H;
+  const int h = (int)(rw - rh * (uint32_t)H);
+  const uint32_t rp = rh / (uint32_t)P;
+  const int p = (int)(rh - rp * (uint32_t)P);
+  const int n = (int)rp;
   constexpr int64_t PIMG = (int64_t)((H + 1) / 2) * ((W + 1) / 2) * 16;
   const uint4 v = pool_grad8<H, W>(dy + (int64_t)n * dy_img, amax + (int64_t)n * P * PIMG, p, h, w, hf);
   *reinterpret_cast<uint4*>(dx + (int64_t)n * dx_img + (((int64_t)p * H + h) * W + w) * 16 + hf * 8) = v;
@@ -969,6 +974,7 @@ APEX_EXPORT int apex_maxpool_fwd(const bf16_t* x, int64_t x_img, int P, int H, i
 APEX_EXPORT int apex_maxpool_bwd(const bf16_t* dy, int64_t dy_img, const uint8_t* amax, int P, int H, int W,
                                  bf16_t* dx, int64_t dx_img, int N, hipStream_t st) {
   const int64_t total = (int64_t)N * P * H * W * 2;
+  if (total <= 0 || total >= 0x7fffff00LL) return (int)hipErrorInvalidValue;   // 32-bit kernel indexing
   const int blocks = (int)((total + 255) / 256);
   if (H == 84 && W == 84) maxpool_bwd_kernel<84, 84><<<blocks, 256, 0, st>>>(dy, dy_img, amax, P, dx, dx_img, N);
   else if (H == 42 && W == 42) maxpool_bwd_kernel<42, 42><<<blocks, 256, 0, st>>>(dy, dy_img, amax, P, dx, dx_img, N);
