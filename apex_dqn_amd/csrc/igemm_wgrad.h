@@ -50,11 +50,8 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
   constexpr int NIMG = CT + NT;
   constexpr int STAGE = NIMG * WG_IMG;
   constexpr int NTHR = 256;
-  // dense rows (MODE 0) need no row table, and neither does im2col with compile-time
-  // output geometry (MODE 1, OWC != 0: row offsets computed per load step with
-  // multiply-shift divisions): 80 KB for a 4-tile block, two blocks per CU
-  constexpr bool RTBL = MODE == 2 || (MODE == 1 && OWC == 0);
-  constexpr int TBL = RTBL ? WG_TBL : 0;
+  // dense rows (MODE 0) need no row table: 80 KB for a 4-tile block, two blocks per CU
+  constexpr int TBL = MODE == 0 ? 0 : WG_TBL;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE + TBL * 4];
   uint32_t* tbl = reinterpret_cast<uint32_t*>(smem + 2 * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -72,15 +69,8 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
   const uint32_t OW = OWC ? OWC : d.OW;
   const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
 
-  // X pixel byte offset of reduction row m (BUF_OOB past the split's end)
-  auto row_off = [&](uint32_t m) -> uint32_t {
-    if ((int)m >= r_end) return BUF_OOB;
-    const uint32_t img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
-    const uint32_t oh = udiv<OWC>(rem, OW), ow = rem - oh * OW;
-    return (uint32_t)(((img * d.H + oh * d.stride) * d.W + ow * d.stride) * d.Cin) * 2u;
-  };
   // ---------------- prologue: per-row X pixel byte offsets (MODE 1 / 2)
-  if (MODE == 1 && RTBL) {
+  if (MODE == 1) {
     for (int r = tid; r < trows; r += NTHR) {
       const uint32_t m = r_begin + r;
       uint32_t e = BUF_OOB;
@@ -156,14 +146,10 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
         const uint32_t o = x_off + st * x_step + t * 128;
         R.x[t][0] = buf_ld16(x_rs, o, 0);
         R.x[t][1] = buf_ld16(x_rs, o + x_r32, 0);
-      } else if (MODE == 1 && RTBL) {
+      } else if (MODE == 1) {
         const uint32_t* tb = tbl + st * WG_ROWS + srow;
         R.x[t][0] = buf_ld16(x_rs, tb[0] + x_tap[t], 0);
         R.x[t][1] = buf_ld16(x_rs, tb[32] + x_tap[t], 0);
-      } else if (MODE == 1) {
-        const uint32_t m0 = r_begin + st * WG_ROWS + srow;
-        R.x[t][0] = buf_ld16(x_rs, row_off(m0) + x_tap[t], 0);
-        R.x[t][1] = buf_ld16(x_rs, row_off(m0 + 32) + x_tap[t], 0);
       } else {
         R.x[t][0] = buf_ld16(x_rs, tbl[x2_tb[t] + st * WG_ROWS + x2_row] + x_tap[t], 0);
       }
