@@ -1,15 +1,17 @@
 """MI355X learner for the dueling NatureCNN: one GPU-resident step.
 
-Per step (B = local batch), entirely on device, no host sync:
+Per step (B = local batch), entirely on device, one stream, no host sync:
 
-  sample (64-ary sum-tree, IS weights)           csrc/sumtree.hip
-  gather S_t | S_{t+n} frame stacks (uint8)      csrc/sumtree.hip (or fused into conv1)
-  online fwd on 2B rows, target fwd on B rows    conv1/conv2/conv3/fc
+  online fwd on 2B rows, target fwd on B rows    conv1_s2d (reads the uint8 replay ring
+                                                 by slot) / conv2_img / conv3 / fc
   DDQN target + Huber*IS loss + |delta| + dH     csrc/ddqn_head.hip
-  backward: heads, fc, conv3, conv2, conv1       head_wgrad / fc / conv dgrad+wgrad
+  fc wgrad + head wgrad + priority write-back    ONE launch (csrc/sumtree.hip
+  (generation-checked, last writer wins)         fc_wgrad_head_prio_kernel)
+  backward: fc, conv3, conv2 dgrad+wgrad, conv1  csrc/conv_mfma.hip, conv1_wgrad.hip
+  wgrad, one split-K finalisation
   (DP) flat-gradient all-reduce over RCCL        parallel/dist.py
-  grad-norm clip + centered RMSprop + bf16 pack  csrc/optimizer.hip
-  priority write-back (generation-checked)       csrc/sumtree.hip
+  grad-norm clip + centered RMSprop + bf16 pack  ONE launch (csrc/sumtree.hip
+  + the NEXT step's prioritized sample           rmsprop_sample_kernel)
 
 Periodic host work between steps: target sync (D2D copy, every
 ``q_target_sync_freq``), FIFO eviction + exact tree rebuild (every
@@ -193,7 +195,8 @@ class FusedNatureLearner:
     # both.  Gradients are pre-scaled by 1/(B*world) in the head kernel, so the SUM
     # all-reduce yields the mean.
     def _seg1(self) -> None:
-        """sample, forward (online+target), loss/priorities, head + fc weight gradients."""
+        """(sample), forward (online+target), loss, head + fc weight gradients with the
+        priority write-back."""
         B, rt, ops = self.B, self.rt, self.ops
         ops.prepare(self.Pb)
         if not self._presample or self._sample_ver != self.replay.version:
@@ -251,7 +254,7 @@ class FusedNatureLearner:
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1)
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"], jobs=jobs)
-        self._join_side()      # head wgrad (side stream) done: its region enters the norm
+        self._join_side()      # (overlap_wgrad) side-stream wgrads done before the finalisation
         norm = dict(part=self.norm_part, slot0=self._fc_slots,
                     total=self.norm_total if self._norm_total_kernel else None) if self._fuse_norm else None
         self._npart = ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
@@ -311,8 +314,8 @@ class FusedNatureLearner:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
 
     def _seg3(self) -> None:
-        """clip + centered RMSprop (+bf16 pack), shard stats (the priority write-back
-        ran on the side stream right after the head kernel)."""
+        """clip + centered RMSprop (+bf16 pack) with the next batch's draw, shard stats
+        (DP)."""
         rt, ops = self.rt, self.ops
         if self._comm_bf16:
             self.g32.copy_(self.gcomm)
