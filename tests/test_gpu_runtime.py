@@ -198,3 +198,39 @@ def test_fused_learner_unaligned_batch(B):
     Lh.step()
     torch.cuda.synchronize()
     assert np.isfinite(Lh.last_metrics()["loss"])
+
+
+_BENCH_KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+               "vs_baseline", "dtype", "data", "config"}
+
+
+def _bench_json(stdout: str) -> dict:
+    import json
+    lines = [ln for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout[-2000:]
+    out = json.loads(lines[0])
+    assert _BENCH_KEYS <= set(out), set(out)
+    return out
+
+
+def test_bench_contract_one_gpu():
+    """bench.py prints exactly one JSON line with the driver's keys."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "30", "--warmup", "5",
+                        "--replay", "20000"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = _bench_json(r.stdout)
+    assert out["n_gpus"] == 1 and out["steps"] == 30 and out["value"] > 0
+    assert out["config"]["global_batch"] == 512 and out["dtype"] == "bf16"
+
+
+def test_bench_two_ranks_gloo_rehearsal():
+    """The driver's N>1 launch (torch.distributed.run, one rank per device) rehearsed
+    with 2 ranks on this one GPU over gloo: every DP code path of the bench runs and
+    rank 0 alone prints the whole-job JSON line (RCCL itself refuses 2 ranks on 1 GPU)."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "20", "--warmup", "5", "--replay", "20000",
+                        "--dist-backend", "gloo"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    out = _bench_json(r.stdout)
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1024 and out["config"]["parallelism"] == "dp2"
