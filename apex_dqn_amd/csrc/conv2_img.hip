@@ -175,3 +175,139 @@ APEX_EXPORT int apex_conv2_img_fwd(Conv2ImgDesc d, int grid, hipStream_t st) {
   conv2_img_fwd_kernel<<<G, C2_THREADS, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }
+
+// =====================================================================================
+// conv2 data gradient, image-resident: dX1[20][20][64] = (sum over taps of
+// dY2 * w2) * (y1 > 0) (backward of duelling_network.py:10-11, learner.py:56).
+// Output pixel (ih, iw) of stride-parity class (p, q) = (ih & 1, iw & 1) sees kernel
+// taps kh = p + 2a, kw = q + 2b (a, b in {0,1}) of dY2 pixel (i - a, j - b),
+// i = ih >> 1, j = iw >> 1: per class a 100 x 64 x 256 GEMM.  Wave w = (class
+// w >> 1, channel half w & 1) owns one outright -- no cross-wave reduction:
+//   * dY2 (9 x 9 x 64 bf16) is staged in LDS inside a zero ring (11 x 11 slots,
+//     chunk-swizzled), so out-of-range taps read zeros;
+//   * swapped operands: the weights are the MFMA A operand (32 input channels x
+//     16 K per fragment, gathered once per workgroup into 64 VGPRs), dY the B
+//     operand (one ds_read_b128 per 32 pixels x 8 channels),
+//     v_mfma_f32_32x32x16_bf16 -> each lane holds 4 runs of 4 channels of a pixel;
+//   * the bf16 results go through LDS so every pixel row (128 B) leaves in coalesced
+//     16-B stores, with the ReLU mask of y1 (coalesced 16-B loads) applied on the way.
+// =====================================================================================
+struct Conv2DgradImgDesc {
+  const bf16_t* dy;     // [N][9][9][64]
+  const bf16_t* w;      // [64 co][4][4][64 ci] OHWI
+  const bf16_t* mask;   // y1 [N][20][20][64] (ReLU mask source)
+  bf16_t* dx;           // [N][20][20][64]
+  int N;
+};
+
+#define C2D_SLOTS 121   // 11 x 11 padded dY slots, 128 B each
+
+__device__ __forceinline__ int c2d_off(int slot, int c) { return (slot << 7) + ((c ^ ((slot >> 1) & 7)) << 4); }
+
+__global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDesc d) {
+  __shared__ __attribute__((aligned(16))) uint8_t sdy[C2D_SLOTS * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sout[400 * 128];      // one output image, pixel rows
+  const bf16_t* __restrict__ dyp = d.dy;
+  const bf16_t* __restrict__ wp = d.w;
+  const bf16_t* __restrict__ mp = d.mask;
+  bf16_t* __restrict__ dxp = d.dx;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cls = wv >> 1, nh = wv & 1, p = cls >> 1, q = cls & 1;
+  const int rr = lane & 31, kg = lane >> 5;
+  for (int i = tid; i < C2D_SLOTS * 8; i += 512) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
+  // weight fragments: row = input channel ci = nh*32 + rr, K step s = (a, b, co group)
+  // (direct 2-byte gathers from L2, once per workgroup: staging them through LDS in
+  // coalesced rounds measured slower, 22.7 vs 18.8 us for 512 images)
+  bf16x8 wfr[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int a = (s >> 3) & 1, b = (s >> 2) & 1, co0 = ((s & 3) << 4) + kg * 8;
+    const int kh = p + 2 * a, kw = q + 2 * b, ci = nh * 32 + rr;
+    uint32_t u[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t lo = wp[((co0 + 2 * e) * 16 + kh * 4 + kw) * 64 + ci];
+      const uint32_t hi = wp[((co0 + 2 * e + 1) * 16 + kh * 4 + kw) * 64 + ci];
+      u[e] = lo | (hi << 16);
+    }
+    wfr[s] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
+  }
+  int pi[4], pj[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int r = min(t * 32 + rr, 99);
+    pi[t] = r / 10;
+    pj[t] = r - pi[t] * 10;
+  }
+  for (int img = blockIdx.x; img < d.N; img += gridDim.x) {
+    __syncthreads();   // previous image: LDS reads and output copy-out done
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(dyp + (int64_t)img * 81 * 64);
+      for (int k = tid; k < 81 * 8; k += 512) {
+        const int px = k >> 3, c = k & 7, oh = px / 9, ow = px - oh * 9;
+        *reinterpret_cast<uint4*>(sdy + c2d_off((oh + 1) * 11 + ow + 1, c)) = src[k];
+      }
+    }
+    __syncthreads();
+    f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int a = (s >> 3) & 1, b = (s >> 2) & 1, c = ((s & 3) << 1) | kg;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int slot = (pi[t] - a + 1) * 11 + (pj[t] - b + 1);
+        const bf16x8 x = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + c2d_off(slot, c)));
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfr[s], x, acc[t], 0, 0, 0);
+      }
+    }
+    // unmasked bf16 runs -> LDS output image (pixel-major, chunk-swizzled like sdy)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t * 32 + rr >= 100) continue;
+      const int ih = 2 * pi[t] + p, iw = 2 * pj[t] + q, px = ih * 20 + iw;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ch = nh * 32 + 8 * g + 4 * kg;      // 4 channels = 8 B, inside 16-B chunk ch >> 3
+        *reinterpret_cast<uint2*>(sout + c2d_off(px, ch >> 3) + (ch & 7) * 2) =
+            make_uint2(cvt_pk_bf16(acc[t][4 * g], acc[t][4 * g + 1]), cvt_pk_bf16(acc[t][4 * g + 2], acc[t][4 * g + 3]));
+      }
+    }
+    __syncthreads();
+    // coalesced copy-out with the ReLU mask of y1 applied per 16-B chunk (mask loads
+    // issued together, then the stores)
+    const uint4* msrc = reinterpret_cast<const uint4*>(mp + (int64_t)img * 400 * 64);
+    uint4* dst = reinterpret_cast<uint4*>(dxp + (int64_t)img * 400 * 64);
+    uint4 mv[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int k = tid + 512 * i;
+      if (k < 3200) mv[i] = msrc[k];
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int k = tid + 512 * i;
+      if (k < 3200) {
+        uint4 v = *reinterpret_cast<const uint4*>(sout + c2d_off(k >> 3, k & 7));
+        v.x = mask_bf16x2(v.x, mv[i].x);
+        v.y = mask_bf16x2(v.y, mv[i].y);
+        v.z = mask_bf16x2(v.z, mv[i].z);
+        v.w = mask_bf16x2(v.w, mv[i].w);
+        dst[k] = v;
+      }
+    }
+  }
+}
+
+APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t st) {
+  if (d.N <= 0 || d.dy == nullptr || d.w == nullptr || d.mask == nullptr || d.dx == nullptr)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)d.dy | (uintptr_t)d.w | (uintptr_t)d.mask | (uintptr_t)d.dx) & 15) return (int)hipErrorInvalidValue;
+  int G = grid > 0 ? grid : 256;
+  if (G > d.N) G = d.N;
+  conv2_dgrad_img_kernel<<<G, 512, 0, st>>>(d);
+  APEX_CHECK_LAUNCH();
+}

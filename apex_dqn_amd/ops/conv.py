@@ -225,12 +225,32 @@ def conv3_dgrad(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out
     _launch_fwd(lib, d)
 
 
+CONV2_DGRAD_IMG = _os.environ.get("APEX_CONV2_DGRAD_IMG", "1") != "0"
+
+
+def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor,
+                    grid: int = 0) -> None:
+    """conv2 data gradient on the image-resident kernel (csrc/conv2_img.hip): one wave
+    per (stride-parity class, channel half), dY staged in LDS inside a zero ring."""
+    from .conv_sigs import Conv2DgradImgDesc
+    N = dy.shape[0]
+    assert tuple(dy.shape) == (N, 9, 9, 64) and tuple(out.shape) == (N, 20, 20, 64)
+    assert tuple(mask.shape) == (N, 20, 20, 64) and tuple(w2.shape) == (64, 4, 4, 64)
+    assert dy.is_contiguous() and out.is_contiguous() and mask.is_contiguous() and w2.is_contiguous()
+    d = Conv2DgradImgDesc()
+    d.dy, d.w, d.mask, d.dx, d.N = dy.data_ptr(), w2.data_ptr(), mask.data_ptr(), out.data_ptr(), N
+    _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
+
+
 def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
     """dX1 (20x20) from dY2 (9x9), 4x4 stride 2: four stride-parity classes, each a
     2x2 stride-1 correlation (pad 1) writing every other output pixel; weights read
     K-major from the OHWI tensor per class."""
     N = dy.shape[0]
     assert w2.shape == (64, 4, 4, 64)
+    if CONV2_DGRAD_IMG and hasattr(lib, "apex_conv2_dgrad_img"):
+        conv2_dgrad_img(lib, dy, w2, mask, out)
+        return
     d = _conv_desc(x=dy.data_ptr(), w=w2.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
                    Cin=64, OH=10, OW=10, Cout=64, KH=2, KW=2, stride=1, pad=1, mode=1, K=256, ncls=4,
                    ostride=2, OHfull=20, OWfull=20, bt=1, ldb=1024, koff=_KOFF2)

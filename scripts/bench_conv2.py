@@ -29,6 +29,21 @@ def main():
     C.CONV2_IMG = False
     us = timed(lambda: C.conv_fwd(lib, x, w, b, 2, out, w2, b2, 2 * N // 3))
     print(json.dumps({"op": "conv2_fwd_igemm", "us": round(us, 2), "tflops": round(fl / us / 1e6, 1)}), flush=True)
+    B = N // 2       # 768: the per-image sweep below uses 256 / 512 / 768 of them
+    dy = torch.randn(B, 9, 9, 64, device=dev).to(torch.bfloat16)
+    y1 = torch.relu(torch.randn(B, 20, 20, 64, device=dev)).to(torch.bfloat16)
+    dx = torch.empty(B, 20, 20, 64, device=dev, dtype=torch.bfloat16)
+    fl2 = 2.0 * B * 400 * 64 * 256
+    C.CONV2_DGRAD_IMG = False
+    us = timed(lambda: C.conv2_dgrad(lib, dy, w, y1, dx))
+    print(json.dumps({"op": "conv2_dgrad_igemm", "us": round(us, 2), "tflops": round(fl2 / us / 1e6, 1)}), flush=True)
+    for nimg in (256, 512, 768):
+        us = timed(lambda: C.conv2_dgrad_img(lib, dy[:nimg], w, y1[:nimg], dx[:nimg], grid=256))
+        print(json.dumps({"op": "conv2_dgrad_img_n", "images": nimg, "us": round(us, 2)}), flush=True)
+    for grid in (256, 512):
+        us = timed(lambda: C.conv2_dgrad_img(lib, dy, w, y1, dx, grid=grid))
+        print(json.dumps({"op": "conv2_dgrad_img", "grid": grid, "us": round(us, 2),
+                          "tflops": round(fl2 / us / 1e6, 1)}), flush=True)
     for grid in (256, 128, 512, 768):
         us = timed(lambda: C.conv2_img_fwd(lib, x, w, b, out, w2, b2, 2 * N // 3, grid=grid))
         print(json.dumps({"op": "conv2_fwd_img", "grid": grid, "us": round(us, 2),

@@ -284,3 +284,18 @@ def test_conv2_image_resident_vs_torch(N, grid, switch):
                      R.conv_fwd(x[switch:].float(), wb.float(), bb, 2)]) if switch < N else \
         R.conv_fwd(x.float(), wa.float(), ba, 2)
     assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,grid", [(300, 0), (37, 5), (1, 0)])
+def test_conv2_dgrad_image_resident_vs_torch(N, grid):
+    """csrc/conv2_img.hip conv2_dgrad_img_kernel (several images per workgroup) vs the
+    fp32 torch conv-transpose, ReLU-masked by y1."""
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N + 7)
+    dy2 = _bf(torch.randn(N, 9, 9, 64, generator=g))
+    w2 = _bf(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+    y1 = _bf(torch.randn(N, 20, 20, 64, generator=g))
+    out = torch.full((N, 20, 20, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    C.conv2_dgrad_img(_lib(), dy2, w2, y1, out, grid=grid)
+    ref = R.conv_dgrad(dy2.float(), w2.float(), (N, 20, 20, 64), 2, y1.float())
+    assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
