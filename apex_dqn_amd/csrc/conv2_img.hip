@@ -300,6 +300,7 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
       }
     }
   }
+#undef C3_LOAD_DY
 }
 
 APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t st) {
@@ -309,5 +310,151 @@ APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t 
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
   conv2_dgrad_img_kernel<<<G, 512, 0, st>>>(d);
+  APEX_CHECK_LAUNCH();
+}
+
+// =====================================================================================
+// conv3 data gradient, image-resident: dX2[9][9][64] = (sum over the 3x3 taps of
+// dY3[ih - kh][iw - kw] * w3[co][kh][kw][ci]) * (y2 > 0)  (backward of
+// duelling_network.py:12-13): per image an 81 x 64 x 576 GEMM.  Six waves = 3 pixel
+// tiles (32 of the 81 pixels) x 2 channel halves; each owns its 32 x 32 output tile
+// over the full K (no reduction), with its 36 weight fragments (32 input channels x
+// 16 K) in 144 VGPRs, transposed once per workgroup through LDS.  dY3 (7 x 7 x 64)
+// sits in LDS inside a 2-pixel zero ring (the same 11 x 11 slot geometry as the conv2
+// kernel) and the next image's dY3 and this image's mask load under the MFMA chain;
+// results go through LDS and leave as coalesced 16-B rows with the y2 mask applied.
+// 512 images: 9.6 us vs 11.1 us for the implicit-GEMM dgrad (+1.4% steps/s A/B).
+// =====================================================================================
+struct Conv3DgradImgDesc {
+  const bf16_t* dy;     // [N][7][7][64]
+  const bf16_t* w;      // [64 co][3][3][64 ci] OHWI
+  const bf16_t* mask;   // y2 [N][9][9][64]
+  bf16_t* dx;           // [N][9][9][64]
+  int N;
+};
+
+#define C3_WROW 72   // padded co row of the transposed weight in LDS (144 B)
+
+__global__ void __launch_bounds__(384, 1) conv3_dgrad_img_kernel(Conv3DgradImgDesc d) {
+  __shared__ __attribute__((aligned(16))) uint8_t sdy[C2D_SLOTS * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sout[81 * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sw[9 * 64 * C3_WROW * 2];
+  const bf16_t* __restrict__ dyp = d.dy;
+  const bf16_t* __restrict__ wp = d.w;
+  const bf16_t* __restrict__ mp = d.mask;
+  bf16_t* __restrict__ dxp = d.dx;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int mt = wv >> 1, nh = wv & 1;
+  const int rr = lane & 31, kg = lane >> 5;
+  for (int i = tid; i < C2D_SLOTS * 8; i += 384) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
+  // dY3 of the first image is in flight while the weight gathers issue; every later
+  // image's dY3 (and this image's y2 mask) load under the previous MFMA chain.
+  uint4 dv0 = make_uint4(0, 0, 0, 0), dv1 = dv0, mv0 = dv0, mv1 = dv0;
+#define C3_LOAD_DY(IMG)                                                              \
+  {                                                                                  \
+    const uint4* src_ = reinterpret_cast<const uint4*>(dyp + (int64_t)(IMG) * 49 * 64); \
+    dv0 = src_[tid];                                                                 \
+    if (tid < 49 * 8 - 384) dv1 = src_[tid + 384];                                   \
+  }
+  if (blockIdx.x < d.N) C3_LOAD_DY(blockIdx.x);
+  // weight fragments: row = ci = nh*32 + rr; K step s = (tap s >> 2, co group s & 3).
+  // OHWI keeps ci contiguous but a fragment needs 8 consecutive co, so the weight is
+  // transposed once per workgroup through LDS: coalesced 16-B global loads (8 ci of one
+  // (co, tap); lanes run along co), 2-byte LDS writes into swt[tap][ci][co] (rows padded
+  // to 72 so the 16-B fragment reads below are conflict-free), then 36 16-B reads.  The
+  // direct 2-byte global gathers cost ~5 us per workgroup (288 per lane).
+  {
+    uint16_t* swt = reinterpret_cast<uint16_t*>(sw);
+    const uint4* wsrc = reinterpret_cast<const uint4*>(wp);
+    uint4 wv[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int q = tid + 384 * i, co = q & 63, r = q >> 6, tap = r >> 3, ci8 = r & 7;
+      wv[i] = wsrc[(co * 9 + tap) * 8 + ci8];
+    }
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int q = tid + 384 * i, co = q & 63, r = q >> 6, tap = r >> 3, ci8 = r & 7;
+      uint16_t* row = swt + (tap * 64 + ci8 * 8) * C3_WROW + co;
+      const uint32_t u[4] = {wv[i].x, wv[i].y, wv[i].z, wv[i].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        row[(2 * e) * C3_WROW] = (uint16_t)(u[e] & 0xffffu);
+        row[(2 * e + 1) * C3_WROW] = (uint16_t)(u[e] >> 16);
+      }
+    }
+  }
+  __syncthreads();
+  bf16x8 wfr[36];
+#pragma unroll
+  for (int s = 0; s < 36; ++s) {
+    const int tap = s >> 2, co0 = ((s & 3) << 4) + kg * 8, ci = nh * 32 + rr;
+    wfr[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sw + ((tap * 64 + ci) * C3_WROW + co0) * 2));
+  }
+  // this lane's output pixel (pixels past 80 repeat pixel 80, never stored)
+  const int pix = mt * 32 + rr, pc = min(pix, 80);
+  const int ih = pc / 9, iw = pc - ih * 9;
+  for (int img = blockIdx.x; img < d.N; img += gridDim.x) {
+    __syncthreads();   // previous image: LDS reads and output copy-out done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = tid + 384 * i;
+      if (k < 49 * 8) {
+        const int px = k >> 3, c = k & 7, oh = px / 7, ow = px - oh * 7;
+        *reinterpret_cast<uint4*>(sdy + c2d_off((oh + 2) * 11 + ow + 2, c)) = i ? dv1 : dv0;
+      }
+    }
+    __syncthreads();
+    {
+      const uint4* msrc = reinterpret_cast<const uint4*>(mp + (int64_t)img * 81 * 64);
+      mv0 = msrc[tid];
+      if (tid < 648 - 384) mv1 = msrc[tid + 384];
+    }
+    if (img + (int)gridDim.x < d.N) C3_LOAD_DY(img + gridDim.x);
+    f32x16 acc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 36; ++s) {
+      const int tap = s >> 2, kh = tap / 3, kw = tap - kh * 3, c = ((s & 3) << 1) | kg;
+      const int slot = (ih - kh + 2) * 11 + (iw - kw + 2);
+      const bf16x8 x = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + c2d_off(slot, c)));
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfr[s], x, acc, 0, 0, 0);
+    }
+    // D[ci][pixel]: lane holds pixel rr, channel rows 8 (j >> 2) + 4 kg + (j & 3)
+    if (pix < 81) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ch = nh * 32 + 8 * g + 4 * kg;
+        *reinterpret_cast<uint2*>(sout + c2d_off(pix, ch >> 3) + (ch & 7) * 2) =
+            make_uint2(cvt_pk_bf16(acc[4 * g], acc[4 * g + 1]), cvt_pk_bf16(acc[4 * g + 2], acc[4 * g + 3]));
+      }
+    }
+    __syncthreads();
+    uint4* dst = reinterpret_cast<uint4*>(dxp + (int64_t)img * 81 * 64);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = tid + 384 * i;
+      if (k < 648) {
+        uint4 v = *reinterpret_cast<const uint4*>(sout + c2d_off(k >> 3, k & 7));
+        const uint4 m = i ? mv1 : mv0;
+        v.x = mask_bf16x2(v.x, m.x);
+        v.y = mask_bf16x2(v.y, m.y);
+        v.z = mask_bf16x2(v.z, m.z);
+        v.w = mask_bf16x2(v.w, m.w);
+        dst[k] = v;
+      }
+    }
+  }
+#undef C3_LOAD_DY
+}
+
+APEX_EXPORT int apex_conv3_dgrad_img(Conv3DgradImgDesc d, int grid, hipStream_t st) {
+  if (d.N <= 0 || d.dy == nullptr || d.w == nullptr || d.mask == nullptr || d.dx == nullptr)
+    return (int)hipErrorInvalidValue;
+  if (((uintptr_t)d.dy | (uintptr_t)d.mask | (uintptr_t)d.dx) & 15) return (int)hipErrorInvalidValue;
+  int G = grid > 0 ? grid : 256;
+  if (G > d.N) G = d.N;
+  conv3_dgrad_img_kernel<<<G, 384, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }

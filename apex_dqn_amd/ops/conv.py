@@ -214,11 +214,31 @@ def dense_dgrad(lib, dh: torch.Tensor, w: torch.Tensor, out: torch.Tensor, mask:
     _launch_fwd(lib, d)
 
 
+CONV3_DGRAD_IMG = _os.environ.get("APEX_CONV3_DGRAD_IMG", "1") != "0"
+
+
+def conv3_dgrad_img(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out: torch.Tensor,
+                    grid: int = 0) -> None:
+    """conv3 data gradient on the image-resident kernel (csrc/conv2_img.hip): six waves
+    own 32-pixel x 32-channel output tiles over the full K, dY3 in LDS."""
+    from .conv_sigs import Conv3DgradImgDesc
+    N = dy.shape[0]
+    assert tuple(dy.shape) == (N, 7, 7, 64) and tuple(out.shape) == (N, 9, 9, 64)
+    assert tuple(mask.shape) == (N, 9, 9, 64) and tuple(w3.shape) == (64, 3, 3, 64)
+    assert dy.is_contiguous() and out.is_contiguous() and mask.is_contiguous() and w3.is_contiguous()
+    d = Conv3DgradImgDesc()
+    d.dy, d.w, d.mask, d.dx, d.N = dy.data_ptr(), w3.data_ptr(), mask.data_ptr(), out.data_ptr(), N
+    _lib.check(lib.apex_conv3_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv3_dgrad_img")
+
+
 def conv3_dgrad(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
     """dX2 (9x9) from dY3 (7x7): full correlation with the flipped 3x3 weights, read
     K-major from the OHWI weight (co rows, ci columns)."""
     N = dy.shape[0]
     assert w3.shape == (64, 3, 3, 64)
+    if CONV3_DGRAD_IMG and hasattr(lib, "apex_conv3_dgrad_img"):
+        conv3_dgrad_img(lib, dy, w3, mask, out)
+        return
     d = _conv_desc(x=dy.data_ptr(), w=w3.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=7, W=7,
                    Cin=64, OH=9, OW=9, Cout=64, KH=3, KW=3, stride=1, pad=2, mode=1, K=576,
                    bt=1, ldb=576, koff=_KOFF3)

@@ -20,11 +20,17 @@ class Conv2DgradImgDesc(ctypes.Structure):
     _fields_ = [("dy", c_p), ("w", c_p), ("mask", c_p), ("dx", c_p), ("N", c_i)]
 
 
+class Conv3DgradImgDesc(ctypes.Structure):
+    """Image-resident conv3 data gradient (mirrors ``Conv3DgradImgDesc`` in csrc/conv2_img.hip)."""
+    _fields_ = [("dy", c_p), ("w", c_p), ("mask", c_p), ("dx", c_p), ("N", c_i)]
+
+
 def declare(lib: ctypes.CDLL) -> None:
     from ._lib import ConvDesc, WgradDesc
     sigs = {
         "apex_conv2_img_fwd": ([Conv2ImgDesc, c_i, c_p], c_i),
         "apex_conv2_dgrad_img": ([Conv2DgradImgDesc, c_i, c_p], c_i),
+        "apex_conv3_dgrad_img": ([Conv3DgradImgDesc, c_i, c_p], c_i),
         "apex_conv_fwd": ([ConvDesc, c_p], c_i),
         "apex_conv_wgrad": ([WgradDesc, c_p, c_p, c_i, c_f, c_p], c_i),
         "apex_pack_dgrad_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),

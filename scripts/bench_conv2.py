@@ -44,6 +44,16 @@ def main():
         us = timed(lambda: C.conv2_dgrad_img(lib, dy, w, y1, dx, grid=grid))
         print(json.dumps({"op": "conv2_dgrad_img", "grid": grid, "us": round(us, 2),
                           "tflops": round(fl2 / us / 1e6, 1)}), flush=True)
+    dy3 = torch.randn(B, 7, 7, 64, device=dev).to(torch.bfloat16)
+    w3 = (torch.randn(64, 3, 3, 64, device=dev) * 0.04).to(torch.bfloat16)
+    y2 = torch.relu(torch.randn(B, 9, 9, 64, device=dev)).to(torch.bfloat16)
+    dx2 = torch.empty(B, 9, 9, 64, device=dev, dtype=torch.bfloat16)
+    C.CONV3_DGRAD_IMG = False
+    us = timed(lambda: C.conv3_dgrad(lib, dy3[:512], w3, y2[:512], dx2[:512]))
+    print(json.dumps({"op": "conv3_dgrad_igemm", "images": 512, "us": round(us, 2)}), flush=True)
+    for g3 in (256, 128, 512):
+        us = timed(lambda: C.conv3_dgrad_img(lib, dy3[:512], w3, y2[:512], dx2[:512], grid=g3))
+        print(json.dumps({"op": "conv3_dgrad_img", "images": 512, "grid": g3, "us": round(us, 2)}), flush=True)
     for grid in (256, 128, 512, 768):
         us = timed(lambda: C.conv2_img_fwd(lib, x, w, b, out, w2, b2, 2 * N // 3, grid=grid))
         print(json.dumps({"op": "conv2_fwd_img", "grid": grid, "us": round(us, 2),

@@ -299,3 +299,18 @@ def test_conv2_dgrad_image_resident_vs_torch(N, grid):
     C.conv2_dgrad_img(_lib(), dy2, w2, y1, out, grid=grid)
     ref = R.conv_dgrad(dy2.float(), w2.float(), (N, 20, 20, 64), 2, y1.float())
     assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,grid", [(300, 0), (37, 5), (1, 0)])
+def test_conv3_dgrad_image_resident_vs_torch(N, grid):
+    """csrc/conv2_img.hip conv3_dgrad_img_kernel vs the fp32 torch conv-transpose,
+    ReLU-masked by y2."""
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N + 11)
+    dy3 = _bf(torch.randn(N, 7, 7, 64, generator=g))
+    w3 = _bf(torch.randn(64, 3, 3, 64, generator=g) * 0.04)
+    y2 = _bf(torch.randn(N, 9, 9, 64, generator=g))
+    out = torch.full((N, 9, 9, 64), 7.0, dtype=torch.bfloat16, device=DEV)
+    C.conv3_dgrad_img(_lib(), dy3, w3, y2, out, grid=grid)
+    ref = R.conv_dgrad(dy3.float(), w3.float(), (N, 9, 9, 64), 1, y2.float())
+    assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
