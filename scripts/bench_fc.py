@@ -2,8 +2,12 @@
 what hipBLASLt (torch.matmul / addmm with ReLU epilogue) reaches on the same shapes as
 the fused igemm fc forward / data-gradient kernels."""
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timed(fn, iters=200):
@@ -36,3 +40,15 @@ for name, fn in [
 ]:
     us = timed(fn)
     print(json.dumps({"op": name, "us": round(us, 2)}), flush=True)
+
+# tile-count sensitivity of the fused fc forward (64-row tiles x 16 column tiles):
+# 256 / 384 / 512 / 768 workgroups on 256 CUs
+from apex_dqn_amd.ops import _lib, conv as C  # noqa: E402
+lib = _lib.require_kernels()
+xb = torch.relu(torch.randn(3072, 3136, device=dev)).to(bf)
+hb = torch.empty(3072, 1024, device=dev, dtype=bf)
+bias32 = torch.zeros(1024, device=dev)
+for M in (512, 1024, 1536, 2048, 3072):
+    us = timed(lambda: C.dense_fwd(lib, xb[:M], w, bias32, hb[:M], True))
+    print(json.dumps({"op": "igemm_fc_fwd", "M": M, "us": round(us, 2), "tflops": round(2 * M * 1024 * 3136 / us / 1e6, 1)}),
+          flush=True)
