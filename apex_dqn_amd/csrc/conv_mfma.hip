@@ -50,7 +50,7 @@ struct ConvDesc {
   int order_hint;             // 0 auto, 1 M tiles fastest per XCD, 2 N tiles fastest
   float* part;                // split-K (dense mode): fp32 partials [ksplit][M][ldy]
   int ksplit;                 // > 1: blockIdx.z = K split; dense_splitk_reduce applies bias / ReLU
-  int pad1;
+  int kgroups;                // 2: dense forward with two 4-wave K groups per block (see igemm_fwd_kernel)
 };
 
 
@@ -78,14 +78,23 @@ __device__ __forceinline__ int epi_off(int r, int byte) {
 // learner's layers (0 = runtime), so the per-row div/mod is multiply-shift.
 // BM: rows per block (128: 32 per wave; 64: 16 per wave, for grids that would
 // otherwise leave CUs idle -- fc fwd/dgrad and the 7x7 / 9x9 layers).
-template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM>
-__global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
+// KG: K groups per block (dense forward only).  KG = 2 runs two 4-wave pipelines
+// over the two halves of K in one 512-thread block, each with its own LDS stages,
+// and sums them through LDS before the epilogue: a grid of ~1.5 blocks per CU is
+// latency-bound per K step (one wave per SIMD), and this doubles the waves in
+// flight without split-K's fp32 partials in HBM.  Both halves must take the same
+// number of loop trips (barriers are block-wide): the host checks KT % 4 != 3.
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM, int KG = 1>
+__global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   constexpr int AR = BM / 32;            // A rows staged per thread
   constexpr int MT = BM / 64;            // 16-row MFMA tiles per wave
   constexpr int WR = BM / 4;             // output rows per wave
   constexpr int STAGE = BM * 128 + FWD_BN * 128;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  static_assert(KG == 1 || (MODE == 0 && !BT), "K groups: dense forward only");
+  __shared__ __attribute__((aligned(16))) uint8_t smem_all[KG * 2 * STAGE];
+  const int kgi = KG == 1 ? 0 : (int)(threadIdx.x >> 8);
+  uint8_t* const smem = smem_all + kgi * (2 * STAGE);
+  const int tid = threadIdx.x & 255, lane = tid & 63, wv = tid >> 6;
   // XCD-contiguous tile order: adjacent M tiles (overlapping im2col input rows) share an L2
   const int wg = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                              gridDim.x * gridDim.y * gridDim.z);
@@ -117,8 +126,12 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const bf16_t* __restrict__ wb = (second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride;
   const float* __restrict__ bias = second ? d.bias2 : d.bias;
   const int KT_all = d.K >> 6;
-  const int kt0 = splitk ? (kz * KT_all) / d.ksplit : 0;
-  const int KT = splitk ? ((kz + 1) * KT_all) / d.ksplit - kt0 : KT_all;
+  int kt0 = splitk ? (kz * KT_all) / d.ksplit : 0;
+  int KT = splitk ? ((kz + 1) * KT_all) / d.ksplit - kt0 : KT_all;
+  if (KG == 2) {
+    kt0 = kgi ? KT_all / 2 : 0;
+    KT = kgi ? KT_all - KT_all / 2 : KT_all / 2;
+  }
   const int sc = tid & 7;
   const int srow = tid >> 3;
   const __amdgpu_buffer_rsrc_t ra_rs = buf_rsrc(d.x);
@@ -252,6 +265,24 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
     load_next(RA);                      // tile kt+4
   }
   if (kt < KT) compute(0);              // odd KT: last tile sits in buffer 0
+  if constexpr (KG == 2) {
+    // group 1 hands its accumulators to group 0 through LDS (lane-major: conflict-free)
+    __syncthreads();
+    f32x4* red = reinterpret_cast<f32x4*>(smem_all);
+    if (kgi == 1) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) red[(mt * 4 + nt) * 256 + tid] = acc[mt][nt];
+    }
+    __syncthreads();
+    if (kgi == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] += red[(mt * 4 + nt) * 256 + tid];
+    }
+  }
   if (splitk) {
     // fp32 partial tile straight from the accumulators (lane: 4 consecutive channels
     // of one row per 16x16 block), reduced + biased + ReLU'd by dense_splitk_reduce
@@ -272,8 +303,10 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   // ---- epilogue: (acc*scale + bias) -> bf16x4 per lane -> swizzled LDS image -> 16-B row stores
   uint8_t* Es = smem + wv * (WR * 128);
   const int g = lane >> 4, pl = lane & 15;
+  const bool epi = KG == 1 || kgi == 0;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
+    if (!epi) break;
     const int ch = 16 * nt + 4 * g;
     float b4[4] = {0.f, 0.f, 0.f, 0.f};
     if (bias) {
@@ -295,7 +328,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   for (int p = 0; p < WR / 8; ++p) {
     const int row = 8 * p + (lane >> 3), ch = lane & 7;
     const int m = m0 + WR * wv + row;
-    if (m >= M) continue;
+    if (m >= M || !epi) continue;
     uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
     const int img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
     const int oh = udiv<OWC>(rem, OWv), ow = rem - oh * OWv;
@@ -416,6 +449,7 @@ static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
   const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
   if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true, 1, 1, BM><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0 && d.kgroups == 2 && d.ksplit <= 1) igemm_fwd_kernel<0, false, false, 1, 1, BM, 2><<<grid, 512, 0, st>>>(d);
   else if (d.mode == 0) igemm_fwd_kernel<0, false, false, 1, 1, BM><<<grid, 256, 0, st>>>(d);
   else if (pad && d.bt) {
     // dgrad: conv3 (9x9 out), conv2 per parity class (10x10 out)
@@ -472,6 +506,8 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.tile_hint == 1) bm64 = false;
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
+  // two K groups need equal loop trips in both halves (block-wide barriers)
+  if (d.kgroups == 2 && (d.mode != 0 || d.bt || ((d.K >> 6) & 3) == 3 || (d.K >> 6) < 4)) d.kgroups = 1;
   if (d.ksplit > 1) {
     if (d.mode != 0 || d.bt || d.mask || d.part == nullptr || d.ksplit > (d.K >> 6)) return (int)hipErrorInvalidValue;
     if (bm64) launch_fwd<64>(d, dim3((M + 63) / 64, d.Cout / FWD_BN, d.ksplit), st);

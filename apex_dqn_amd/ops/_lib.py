@@ -52,7 +52,7 @@ class ConvDesc(ctypes.Structure):
                 ("K", c_i), ("in_scale", c_f), ("w_cls_stride", c_i64),
                 ("w2", c_p), ("bias2", c_p), ("m_switch", c_i),
                 ("bt", c_i), ("ldb", c_i), ("koff", c_i * 16), ("tile_hint", c_i), ("order_hint", c_i),
-                ("part", c_p), ("ksplit", c_i), ("pad1", c_i)]
+                ("part", c_p), ("ksplit", c_i), ("kgroups", c_i)]
 
 
 class WgradDesc(ctypes.Structure):

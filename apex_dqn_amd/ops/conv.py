@@ -165,6 +165,8 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
 # learner is only 192 128x64 tiles for 256 CUs; splitting its K = 3136 fills the
 # chip, and one elementwise pass sums the fp32 partials + bias + ReLU (APEX_FC_KSPLIT)
 DENSE_KSPLIT = int(_os.environ.get("APEX_FC_KSPLIT", "0"))   # 0 = auto
+# fc forward: two 4-wave K groups per 512-thread block (csrc/conv_mfma.hip igemm_fwd KG)
+DENSE_KGROUPS = int(_os.environ.get("APEX_FC_KGROUPS", "1"))
 
 
 def _dense_ksplit(M: int, Nc: int, K: int) -> int:
@@ -192,6 +194,7 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
     if ks > 1:
         part = ws.get(("dense_part", M, Nc), ks * M * Nc, x.device)
         d.part, d.ksplit = part.data_ptr(), ks
+    d.kgroups = DENSE_KGROUPS
     _launch_fwd(lib, d)
 
 

@@ -52,3 +52,30 @@ for M in (512, 1024, 1536, 2048, 3072):
     us = timed(lambda: C.dense_fwd(lib, xb[:M], w, bias32, hb[:M], True))
     print(json.dumps({"op": "igemm_fc_fwd", "M": M, "us": round(us, 2), "tflops": round(2 * M * 1024 * 3136 / us / 1e6, 1)}),
           flush=True)
+
+# split-K variants (fp32 partials + dense_splitk_reduce) at the step's M = 1536
+ws = C.Workspace()
+for ks in (1, 2, 3, 4):
+    C.DENSE_KSPLIT = ks
+    us = timed(lambda: C.dense_fwd(lib, xb[:1536], w, bias32, hb[:1536], True, None, w2, bias32, 1024, ws=ws))
+    print(json.dumps({"op": "igemm_fc_fwd_2sets", "ksplit": ks, "us": round(us, 2)}), flush=True)
+C.DENSE_KSPLIT = 0
+
+# two K groups per block (512 threads) vs one
+for kgr in (1, 2):
+    C.DENSE_KGROUPS = kgr
+    for M in (1024, 1536):
+        us = timed(lambda: C.dense_fwd(lib, xb[:M], w, bias32, hb[:M], True, None, w2, bias32, 1024 if M > 1024 else 512))
+        print(json.dumps({"op": "igemm_fc_fwd_2sets", "kgroups": kgr, "M": M, "us": round(us, 2)}), flush=True)
+C.DENSE_KGROUPS = 1
+
+# tile shape x K groups (tile 1: BM=128, 2: BM=64) at the step's shape
+for tile in (1, 2):
+    for kgr in (1, 2):
+        C.DENSE_KGROUPS = kgr
+        C.set_launch_hints(tile, 0)
+        us = timed(lambda: C.dense_fwd(lib, xb[:1536], w, bias32, hb[:1536], True, None, w2, bias32, 1024))
+        print(json.dumps({"op": "igemm_fc_fwd_2sets", "tile": tile, "kgroups": kgr, "M": 1536, "us": round(us, 2)}),
+              flush=True)
+C.set_launch_hints()
+C.DENSE_KGROUPS = 1
