@@ -300,7 +300,6 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
       }
     }
   }
-#undef C3_LOAD_DY
 }
 
 APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t st) {
