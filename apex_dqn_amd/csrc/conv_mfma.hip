@@ -84,13 +84,16 @@ __device__ __forceinline__ int epi_off(int r, int byte) {
 // latency-bound per K step (one wave per SIMD), and this doubles the waves in
 // flight without split-K's fp32 partials in HBM.  Both halves must take the same
 // number of loop trips (barriers are block-wide): the host checks KT % 4 != 3.
-template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM, int KG = 1>
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM, int KG = 1, bool W22 = false, bool PF3 = false>
 __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   constexpr int AR = BM / 32;            // A rows staged per thread
   constexpr int MT = BM / 64;            // 16-row MFMA tiles per wave
   constexpr int WR = BM / 4;             // output rows per wave
   constexpr int STAGE = BM * 128 + FWD_BN * 128;
   static_assert(KG == 1 || (MODE == 0 && !BT), "K groups: dense forward only");
+  // W22: the four waves tile the 64 x 64 block as 2 x 2 (32 x 32 each) instead of
+  // 4 x 1 (16 x 64): 8 instead of 10 fragment reads per wave and K step
+  static_assert(!W22 || (BM == 64 && KG == 1 && MODE == 0 && !BT), "W22: dense 64-row tiles only");
   __shared__ __attribute__((aligned(16))) uint8_t smem_all[KG * 2 * STAGE];
   const int kgi = KG == 1 ? 0 : (int)(threadIdx.x >> 8);
   uint8_t* const smem = smem_all + kgi * (2 * STAGE);
@@ -224,6 +227,25 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   auto compute = [&](int buf) {
     const uint8_t* As = smem + buf * STAGE;
     const uint8_t* Bs = As + BM * 128;
+    if constexpr (W22) {
+      const int wm = wv >> 1, wn = wv & 1;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int c = 4 * s + (lane >> 4);
+        bf16x8 a[2], b[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          a[i] = *reinterpret_cast<const bf16x8*>(As + swz_row(32 * wm + 16 * i + (lane & 15), c));
+          b[i] = *reinterpret_cast<const bf16x8*>(Bs + swz_row(32 * wn + 16 * i + (lane & 15), c));
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[0][2 * mt + nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[0][2 * mt + nt], 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = 4 * s + (lane >> 4);
@@ -247,14 +269,53 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   // Tile t's global loads are issued two half-iterations before its MFMAs
   // (prefetch distance 2); loads past the last tile re-read tile KT-1 (cache
   // hits) so the body has no branches and the vmcnt waits stay partial.
+  int kt = 0;
+  if constexpr (PF3) {
+    // three register stages: tile t's loads are issued three compute steps ahead.
+    // Invariant at the loop head: tile kt in LDS buffer kt & 1, R1 / R2 hold tiles
+    // kt+1 / kt+2 (R0 is free); the body is unrolled by 3 so the sets stay static.
+    FwdRegs R0, R1, R2;
+    load_next(R0);
+    load_next(R1);
+    load_next(R2);
+    write_tile(0, R0);
+    __syncthreads();
+    load_next(R0);                      // tile 3
+    for (; kt + 2 < KT; kt += 3) {
+      const int b0 = kt & 1;
+      compute(b0);
+      write_tile(b0 ^ 1, R1);           // tile kt+1
+      __syncthreads();
+      load_next(R1);                    // tile kt+4
+      compute(b0 ^ 1);
+      write_tile(b0, R2);               // tile kt+2
+      __syncthreads();
+      load_next(R2);                    // tile kt+5
+      compute(b0);
+      write_tile(b0 ^ 1, R0);           // tile kt+3
+      __syncthreads();
+      load_next(R0);                    // tile kt+6
+      // rotate: R1 -> kt+4, R2 -> kt+5, R0 -> kt+6 are tiles kt'+1, kt'+2, kt'+3 of kt' = kt+3
+    }
+    if (kt < KT) {
+      compute(kt & 1);
+      if (kt + 1 < KT) {
+        write_tile((kt + 1) & 1, R1);
+        __syncthreads();
+        compute((kt + 1) & 1);
+      }
+    }
+    kt = KT;
+  }
   FwdRegs RA, RB;
+  if constexpr (!PF3) {
   load_next(RA);                        // tile 0
   load_next(RB);                        // tile 1
   write_tile(0, RA);
   __syncthreads();
   load_next(RA);                        // tile 2
-  int kt = 0;
-  for (; kt + 1 < KT; kt += 2) {
+  }
+  for (; !PF3 && kt + 1 < KT; kt += 2) {
     compute(0);
     write_tile(1, RB);                  // tile kt+1
     __syncthreads();
@@ -264,7 +325,7 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
     __syncthreads();
     load_next(RA);                      // tile kt+4
   }
-  if (kt < KT) compute(0);              // odd KT: last tile sits in buffer 0
+  if (!PF3 && kt < KT) compute(0);     // odd KT: last tile sits in buffer 0
   if constexpr (KG == 2) {
     // group 1 hands its accumulators to group 0 through LDS (lane-major: conflict-free)
     __syncthreads();
@@ -304,9 +365,30 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   uint8_t* Es = smem + wv * (WR * 128);
   const int g = lane >> 4, pl = lane & 15;
   const bool epi = KG == 1 || kgi == 0;
+  if constexpr (W22) {
+    // one 64-row image for the block (epi_off of the block row == the per-wave image
+    // the store loop below reads, since 16 wv is a multiple of 16)
+    const int wm = wv >> 1, wn = wv & 1;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int ch = 32 * wn + 16 * nt + 4 * g;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bias) {
+        const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + ch);
+        b4[0] = bb.x; b4[1] = bb.y; b4[2] = bb.z; b4[3] = bb.w;
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const f32x4 a4 = acc[0][2 * mt + nt];
+        const uint2 v = make_uint2(cvt_pk_bf16(a4[0] * d.in_scale + b4[0], a4[1] * d.in_scale + b4[1]),
+                                   cvt_pk_bf16(a4[2] * d.in_scale + b4[2], a4[3] * d.in_scale + b4[3]));
+        *reinterpret_cast<uint2*>(smem + epi_off(32 * wm + 16 * mt + pl, ch * 2)) = v;
+      }
+    }
+  }
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
-    if (!epi) break;
+    if (!epi || W22) break;
     const int ch = 16 * nt + 4 * g;
     float b4[4] = {0.f, 0.f, 0.f, 0.f};
     if (bias) {
@@ -450,6 +532,12 @@ static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
   const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
   if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true, 1, 1, BM><<<grid, 256, 0, st>>>(d);
   else if (d.mode == 0 && d.kgroups == 2 && d.ksplit <= 1) igemm_fwd_kernel<0, false, false, 1, 1, BM, 2><<<grid, 512, 0, st>>>(d);
+  else if (d.mode == 0 && BM == 64 && d.kgroups == 3 && d.ksplit <= 1)
+    igemm_fwd_kernel<0, false, false, 1, 1, 64, 1, true><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0 && BM == 64 && d.kgroups == 4 && d.ksplit <= 1)
+    igemm_fwd_kernel<0, false, false, 1, 1, 64, 1, true, true><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0 && BM == 64 && d.kgroups == 5 && d.ksplit <= 1)
+    igemm_fwd_kernel<0, false, false, 1, 1, 64, 1, false, true><<<grid, 256, 0, st>>>(d);
   else if (d.mode == 0) igemm_fwd_kernel<0, false, false, 1, 1, BM><<<grid, 256, 0, st>>>(d);
   else if (pad && d.bt) {
     // dgrad: conv3 (9x9 out), conv2 per parity class (10x10 out)
@@ -507,6 +595,8 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
   // two K groups need equal loop trips in both halves (block-wide barriers)
+  // 3: 2 x 2 wave tiling (W22); 4: W22 + three register stages (PF3); 5: PF3 only
+  if (d.kgroups >= 3 && (d.mode != 0 || d.bt)) d.kgroups = 1;
   if (d.kgroups == 2 && (d.mode != 0 || d.bt || ((d.K >> 6) & 3) == 3 || (d.K >> 6) < 4)) d.kgroups = 1;
   if (d.ksplit > 1) {
     if (d.mode != 0 || d.bt || d.mask || d.part == nullptr || d.ksplit > (d.K >> 6)) return (int)hipErrorInvalidValue;

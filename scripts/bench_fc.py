@@ -62,7 +62,7 @@ for ks in (1, 2, 3, 4):
 C.DENSE_KSPLIT = 0
 
 # two K groups per block (512 threads) vs one
-for kgr in (1, 2):
+for kgr in (1, 2, 3, 4, 5):
     C.DENSE_KGROUPS = kgr
     for M in (1024, 1536):
         us = timed(lambda: C.dense_fwd(lib, xb[:M], w, bias32, hb[:M], True, None, w2, bias32, 1024 if M > 1024 else 512))

@@ -316,8 +316,9 @@ def test_conv3_dgrad_image_resident_vs_torch(N, grid):
     assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("kgr", [2, 3, 4, 5])
 @pytest.mark.parametrize("M,K", [(1536, 3136), (200, 3136), (384, 3200)])
-def test_dense_fwd_two_k_groups(M, K):
+def test_dense_fwd_two_k_groups(M, K, kgr):
     """Dense forward with two 4-wave K groups per block (igemm_fwd KG = 2, partial
     tile summed through LDS) vs the fp32 torch reference, incl. the online/target
     weight switch, a ragged last row tile and K/64 = 50 (unequal-halves rule)."""
@@ -330,7 +331,7 @@ def test_dense_fwd_two_k_groups(M, K):
     b2 = (torch.randn(1024, generator=g) * 0.1).to(DEV)
     split = 1024 if M >= 1024 else 0
     old = C.DENSE_KGROUPS
-    C.DENSE_KGROUPS = 2
+    C.DENSE_KGROUPS = kgr    # 2: two K groups per block; 3: 2 x 2 waves; 4: + 3-deep prefetch; 5: prefetch only
     try:
         out = torch.empty(M, 1024, dtype=torch.bfloat16, device=DEV)
         if split:
