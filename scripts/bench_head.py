@@ -24,6 +24,7 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     Hon = torch.relu(torch.randn(2 * B, 1024, generator=g)).to(dev, torch.bfloat16)
     Htg = torch.relu(torch.randn(B, 1024, generator=g)).to(dev, torch.bfloat16)
+    Hsrc, Htsrc = Hon.clone(), Htg.clone()
 
     def P():
         return {"wv": (torch.randn(512, generator=g) * 0.05).to(dev), "bv": torch.randn(1, generator=g).to(dev),
@@ -52,7 +53,11 @@ def main():
                      ("head_prio", lambda: be.head(*args, zero=zero, prio=(rp, S["idx"], S["gen"]))),
                      ("head_wgrad", lambda: be.head_wgrad(Hon, dhead, gr)),
                      ("head_wgrad_prio", lambda: be.head_wgrad(Hon, dhead, gr, prio=(rp, S["idx"], S["gen"], td))),
-                     ("tree_update", lambda: rp.update_priorities(S["idx"], td, S["gen"]))]:
+                     ("tree_update", lambda: rp.update_priorities(S["idx"], td, S["gen"])),
+                     # the head right after a kernel that rewrote its inputs (as in the step,
+                     # where the fc forward produces them): minus "rewrite" = in-step cost
+                     ("rewrite", lambda: (Hon.copy_(Hsrc), Htg.copy_(Htsrc))),
+                     ("rewrite+head", lambda: (Hon.copy_(Hsrc), Htg.copy_(Htsrc), be.head(*args, zero=zero)))]:
         print(json.dumps({"op": name, "B": B, "us": round(timed(fn), 2)}), flush=True)
 
 
