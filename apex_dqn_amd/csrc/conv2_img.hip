@@ -361,7 +361,7 @@ __global__ void __launch_bounds__(384, 1) conv3_dgrad_img_kernel(Conv3DgradImgDe
   // transposed once per workgroup through LDS: coalesced 16-B global loads (8 ci of one
   // (co, tap); lanes run along co), 2-byte LDS writes into swt[tap][ci][co] (rows padded
   // to 72 so the 16-B fragment reads below are conflict-free), then 36 16-B reads.  The
-  // direct 2-byte global gathers cost ~5 us per workgroup (288 per lane).
+  // direct 2-byte global gathers (288 per lane) measured 10.6 vs 9.6 us for 512 images.
   {
     uint16_t* swt = reinterpret_cast<uint16_t*>(sw);
     const uint4* wsrc = reinterpret_cast<const uint4*>(wp);
