@@ -30,6 +30,7 @@ def main():
         return {"wv": (torch.randn(512, generator=g) * 0.05).to(dev), "bv": torch.randn(1, generator=g).to(dev),
                 "wa": (torch.randn(A, 512, generator=g) * 0.05).to(dev), "ba": torch.randn(A, generator=g).to(dev)}
     Pon, Ptg = P(), P()
+    Psrc, Ptsrc = {k: v.clone() for k, v in Pon.items()}, {k: v.clone() for k, v in Ptg.items()}
     act = torch.randint(0, A, (B,), generator=g).to(dev, torch.int32)
     rew, gam, isw = torch.randn(B, device=dev), torch.full((B,), 0.97, device=dev), torch.rand(B, device=dev)
     td, loss = torch.zeros(B, device=dev), torch.zeros(B, device=dev)
@@ -57,7 +58,12 @@ def main():
                      # the head right after a kernel that rewrote its inputs (as in the step,
                      # where the fc forward produces them): minus "rewrite" = in-step cost
                      ("rewrite", lambda: (Hon.copy_(Hsrc), Htg.copy_(Htsrc))),
-                     ("rewrite+head", lambda: (Hon.copy_(Hsrc), Htg.copy_(Htsrc), be.head(*args, zero=zero)))]:
+                     ("rewrite+head", lambda: (Hon.copy_(Hsrc), Htg.copy_(Htsrc), be.head(*args, zero=zero))),
+                     # ... and its head weights too (the optimizer rewrites them every step)
+                     ("rewrite_all", lambda: (Hon.copy_(Hsrc), Htg.copy_(Htsrc), [Pon[k].copy_(Psrc[k]) for k in Pon],
+                                              [Ptg[k].copy_(Ptsrc[k]) for k in Ptg])),
+                     ("rewrite_all+head", lambda: (Hon.copy_(Hsrc), Htg.copy_(Htsrc), [Pon[k].copy_(Psrc[k]) for k in Pon],
+                                                   [Ptg[k].copy_(Ptsrc[k]) for k in Ptg], be.head(*args, zero=zero)))]:
         print(json.dumps({"op": name, "B": B, "us": round(timed(fn), 2)}), flush=True)
 
 
