@@ -62,7 +62,8 @@ class RuntimeConf:
 
     device: str = "auto"            # "auto" | "cpu" | "cuda"
     world_size: int = 1
-    dtype: str = "bf16"             # compute dtype on the GPU path
+    dtype: str = "fp32"             # GPU learner precision: "fp32" (the reference's; split hi/lo bf16
+                                    # operands, 3 MFMAs per product) | "bf16" (bf16 operands)
     seed: int = 0
     learner_T: int = 500000         # reference hard-codes 500000 (main.py:46)
     network: str = "auto"           # "auto" | "nature64" | "nature32" | "mlp" | "impala"
@@ -95,8 +96,6 @@ class RuntimeConf:
     torch_profile_steps: int = 5
     resume: bool = True             # continue from ckpt_dir/checkpoint.pt when it exists (restarts)
     allreduce_dtype: str = "fp32"   # DP gradient all-reduce payload: "fp32" (exact) | "bf16" (half the bytes)
-    overlap_wgrad: bool = False     # weight-gradient GEMMs on a side stream beside the dgrad chain (slower in the
-                                    # HIP graph since the tree kernels were fused: 3317 vs 3454 steps/s)
     presample: bool = True          # draw step t+1's batch at the end of step t (fused learner; on the HIP
                                     # backend inside the optimizer launch)
     graph_steps: int = 10           # learner updates per HIP-graph launch in learner.steps(n) (1 rank;

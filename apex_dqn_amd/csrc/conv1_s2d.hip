@@ -31,6 +31,11 @@ struct Conv1S2DDesc {
   int N, C, m_switch;
   float in_scale;
   uint64_t* probe;            // optional phase timestamps (blocks < PROBE_BLOCKS), see mfma_common.h
+  // fp32-accurate ("split") mode when y_lo is set: the fp32 master weights (OIHW)
+  // are read instead of w / w2 and the output leaves as hi / lo bf16 planes
+  const float* w32;
+  const float* w2_32;
+  bf16_t* y_lo;
 };
 
 // ---------------------------------------------------------------------------
@@ -61,6 +66,11 @@ struct Conv1S2DDesc {
 //     installed through a swizzled LDS copy (a conflict-free fragment gather).
 // Online/target weights switch per image (m_switch is a multiple of 400 rows;
 // strided images make it at most one switch per block).
+// SPLIT (fp32-accurate): the pixels are exact in f16, the fp32 weights become
+// w = hi + lo * 2^-12 with hi = f16(w) and lo = f16((w - hi) * 2^12) (22
+// significant bits; the 2^12 keeps lo out of the f16 subnormals), gathered in two
+// install rounds; every fragment takes two MFMAs into two accumulators, combined
+// in fp32 in the epilogue, which writes the result as hi / lo bf16 planes.
 #define C1_PLANE 7168
 #define C1_TILES 25
 #define C1_THREADS 512
@@ -79,8 +89,11 @@ __device__ __forceinline__ int c1_wswz(int q, int h) {
   return (((q & ~15) | ((q ^ (q >> NSH)) & 15)) << 4) + ((h ^ ((q >> 1) & 1)) << 3);
 }
 
-template <int C>
+#define C1_LO_SCALE 4096.f
+
+template <int C, bool SPLIT>
 __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDesc d) {
+  constexpr int NST = SPLIT ? 4 : 2;     // epilogue stores per row tile (vmcnt accounting)
   constexpr int NW = C1_THREADS / 64;
   constexpr int IMG = 2 * C * C1_PLANE;
   constexpr int NCHUNK = C * 441;        // 16-B s2d blocks per image
@@ -111,51 +124,94 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
   // (g, pl) supplies output channel n = 16 nt + pl, s2d K 32 s + 8 g .. +7), gathered
   // from OIHW w1: 16-B K chunk c = 4 s + g is (tap, frame) block q = c >> 1, kernel
   // rows r4 = 2 (c & 1) + {0, 1}, each 4 contiguous kw taps (8 B).
-  f16x8 bfr[2 * C][2];
+  f16x8 bfr[2 * C][2], bfl[2 * C][2];
   uint4 wpf[C];
+  uint4 wpf32[SPLIT ? 2 * C : 1];        // SPLIT: the 8 fp32 weights of chunk q in two uint4
   float4 bpf = make_float4(0.f, 0.f, 0.f, 0.f);
   int cur_set = -1;
   auto prefetch_w = [&](int set) {
-    const uint4* W = reinterpret_cast<const uint4*>(set ? d.w2 : d.w);
+    if constexpr (SPLIT) {
+      const uint4* W = reinterpret_cast<const uint4*>(set ? d.w2_32 : d.w32);
 #pragma unroll
-    for (int j = 0; j < C; ++j) wpf[j] = W[tid + C1_THREADS * j];
+      for (int j = 0; j < C; ++j) {
+        wpf32[2 * j] = W[2 * (tid + C1_THREADS * j)];
+        wpf32[2 * j + 1] = W[2 * (tid + C1_THREADS * j) + 1];
+      }
+    } else {
+      const uint4* W = reinterpret_cast<const uint4*>(set ? d.w2 : d.w);
+#pragma unroll
+      for (int j = 0; j < C; ++j) wpf[j] = W[tid + C1_THREADS * j];
+    }
     if (tid < 16) bpf = reinterpret_cast<const float4*>(set ? d.bias2 : d.bias)[tid];
+  };
+  // SPLIT: f16 pair (hi or scaled lo part) of two fp32 weights, packed
+  auto f16pair = [&](uint32_t a, uint32_t b, int round) -> uint32_t {
+    const float fa = __uint_as_float(a), fb = __uint_as_float(b);
+    const _Float16 ha = (_Float16)fa, hb = (_Float16)fb;
+    f16x2v r;
+    if (round == 0) {
+      r = (f16x2v){ha, hb};
+    } else {
+      r = (f16x2v){(_Float16)((fa - (float)ha) * C1_LO_SCALE), (_Float16)((fb - (float)hb) * C1_LO_SCALE)};
+    }
+    return __builtin_bit_cast(uint32_t, r);
   };
   // `younger`: VMEM ops this wave issued after the prefetch that need not finish
   auto install_w = [&](uint8_t* L, int set, int younger) {   // every wave; L: a free plane buffer
-    vmcnt_le(younger);
-#pragma unroll
-    for (int j = 0; j < C; ++j) {
-      const int q = tid + C1_THREADS * j;
-      const uint4 v = wpf[j];
-      *reinterpret_cast<uint2*>(L + c1_wswz<C>(q, 0)) = make_uint2(v.x, v.y);
-      *reinterpret_cast<uint2*>(L + c1_wswz<C>(q, 1)) = make_uint2(v.z, v.w);
-    }
+    // SPLIT: the fp32 weights are fetched here, not one image ahead (their 8 C
+    // prefetch VGPRs would stay live across the loop and spill the 4-frame kernel)
+    if (SPLIT) prefetch_w(set);
+    vmcnt_le(SPLIT ? 0 : younger);
     float* Lb = reinterpret_cast<float*>(L + 64 * 64 * C * 2);
-    if (tid < 16) reinterpret_cast<float4*>(Lb)[tid] = bpf;
-    __syncthreads();
     float ws[2] = {0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 2 * C; ++s)
+    for (int round = 0; round < (SPLIT ? 2 : 1); ++round) {
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int n = 16 * (nt0 + nt) + pl, c = 4 * s + g;
-        const int q = c >> 1, tap = q / C, ch = q - tap * C;
-        const int kh = 4 * (tap >> 1) + 2 * (c & 1), kw = 4 * (tap & 1);
-        const int p = ((n * C + ch) * 8 + kh) * 8 + kw;     // element offset, multiple of 4
-        const uint2 lo = *reinterpret_cast<const uint2*>(L + c1_wswz<C>(p >> 3, (p >> 2) & 1));
-        const uint2 hi = *reinterpret_cast<const uint2*>(L + c1_wswz<C>((p >> 3) + 1, (p >> 2) & 1));
-        const uint32_t wd[4] = {lo.x, lo.y, hi.x, hi.y};
-        f16x8 f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float a0 = __uint_as_float(wd[i] << 16), a1 = __uint_as_float(wd[i] & 0xffff0000u);
-          f[2 * i] = (_Float16)a0;
-          f[2 * i + 1] = (_Float16)a1;
-          ws[nt] += (float)f[2 * i] + (float)f[2 * i + 1];
+      for (int j = 0; j < C; ++j) {
+        const int q = tid + C1_THREADS * j;
+        uint4 v = wpf[j];
+        if constexpr (SPLIT) {
+          const uint4 a = wpf32[2 * j], b = wpf32[2 * j + 1];
+          v = make_uint4(f16pair(a.x, a.y, round), f16pair(a.z, a.w, round), f16pair(b.x, b.y, round),
+                         f16pair(b.z, b.w, round));
         }
-        bfr[s][nt] = f;
+        *reinterpret_cast<uint2*>(L + c1_wswz<C>(q, 0)) = make_uint2(v.x, v.y);
+        *reinterpret_cast<uint2*>(L + c1_wswz<C>(q, 1)) = make_uint2(v.z, v.w);
       }
+      if (round == 0 && tid < 16) reinterpret_cast<float4*>(Lb)[tid] = bpf;
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < 2 * C; ++s)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int n = 16 * (nt0 + nt) + pl, c = 4 * s + g;
+          const int q = c >> 1, tap = q / C, ch = q - tap * C;
+          const int kh = 4 * (tap >> 1) + 2 * (c & 1), kw = 4 * (tap & 1);
+          const int p = ((n * C + ch) * 8 + kh) * 8 + kw;     // element offset, multiple of 4
+          const uint2 lo = *reinterpret_cast<const uint2*>(L + c1_wswz<C>(p >> 3, (p >> 2) & 1));
+          const uint2 hi = *reinterpret_cast<const uint2*>(L + c1_wswz<C>((p >> 3) + 1, (p >> 2) & 1));
+          const uint32_t wd[4] = {lo.x, lo.y, hi.x, hi.y};
+          f16x8 f;
+          if constexpr (SPLIT) {
+            // the LDS copy already holds f16 (hi, or lo * 2^12 in round 1)
+            f = __builtin_bit_cast(f16x8, make_uint4(wd[0], wd[1], wd[2], wd[3]));
+            const float sc = round == 0 ? 1.f : 1.f / C1_LO_SCALE;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ws[nt] += (float)f[i] * sc;
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float a0 = __uint_as_float(wd[i] << 16), a1 = __uint_as_float(wd[i] & 0xffff0000u);
+              f[2 * i] = (_Float16)a0;
+              f[2 * i + 1] = (_Float16)a1;
+              ws[nt] += (float)f[2 * i] + (float)f[2 * i + 1];
+            }
+          }
+          if (round == 0) bfr[s][nt] = f;
+          else bfl[s][nt] = f;
+        }
+      if (SPLIT && round == 0) __syncthreads();   // every gather done before round 1 rewrites L
+    }
     // channel sums over the 4 K-chunk lanes, then the epilogue's channels 4 g + i
     // fetch theirs: bias' = bias - 1024 * scale * sum_k w16[n][k]
 #pragma unroll
@@ -223,26 +279,47 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
       const int p = 16 * t + pl;
       const int oh = p / 20, ow = p - 20 * oh;
       const uint8_t* A = P + ((oh * 21 + ow) << 4);
-      f16x8 a[2 * C];
+      // (SPLIT: the fragments are read per K step -- all 2 C of them up front next to
+      // both weight sets would exceed the 256 VGPRs of two waves per SIMD)
+      constexpr int NA = SPLIT ? 1 : 2 * C;
+      f16x8 a[NA];
+      if (!SPLIT) {
 #pragma unroll
-      for (int s = 0; s < 2 * C; ++s) a[s] = *reinterpret_cast<const f16x8*>(A + aoff[s]);
-      f32x4 acc[2];
+        for (int s = 0; s < NA; ++s) a[s] = *reinterpret_cast<const f16x8*>(A + aoff[s]);
+      }
+      f32x4 acc[2], accl[2];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < 2; ++nt) acc[nt] = accl[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2 * C; ++s)
+      for (int s = 0; s < 2 * C; ++s) {
+        const f16x8 as = SPLIT ? *reinterpret_cast<const f16x8*>(A + aoff[s]) : a[SPLIT ? 0 : s];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[s][nt], a[s], acc[nt], 0, 0, 0);
+        for (int nt = 0; nt < 2; ++nt) {
+          acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfr[s][nt], as, acc[nt], 0, 0, 0);
+          if (SPLIT) accl[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bfl[s][nt], as, accl[nt], 0, 0, 0);
+        }
+      }
       // lane holds channels 16 (nt0+nt) + 4 g .. +3 of pixel p: one 8-byte store each
-      bf16_t* yrow = d.y + ((int64_t)img * 400 + p) * 64 + 16 * nt0 + 4 * g;
+      const int64_t yo = ((int64_t)img * 400 + p) * 64 + 16 * nt0 + 4 * g;
       const f32x2v sc = {d.in_scale, d.in_scale};
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const f32x2v v0 = (f32x2v){acc[nt][0], acc[nt][1]} * sc + bv[nt][0];
-        const f32x2v v1 = (f32x2v){acc[nt][2], acc[nt][3]} * sc + bv[nt][1];
-        const uint2 o = make_uint2(relu_pk16(cvt_pk_bf16(v0[0], v0[1])), relu_pk16(cvt_pk_bf16(v1[0], v1[1])));
-        *reinterpret_cast<uint2*>(yrow + 16 * nt) = o;
+        if constexpr (SPLIT) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[r] = fmaxf((acc[nt][r] + accl[nt][r] * (1.f / C1_LO_SCALE)) * d.in_scale + bv[nt][r >> 1][r & 1], 0.f);
+          uint32_t h01, l01, h23, l23;
+          split_pk_bf16(v[0], v[1], h01, l01);
+          split_pk_bf16(v[2], v[3], h23, l23);
+          *reinterpret_cast<uint2*>(d.y + yo + 16 * nt) = make_uint2(h01, h23);
+          *reinterpret_cast<uint2*>(d.y_lo + yo + 16 * nt) = make_uint2(l01, l23);
+        } else {
+          const f32x2v v0 = (f32x2v){acc[nt][0], acc[nt][1]} * sc + bv[nt][0];
+          const f32x2v v1 = (f32x2v){acc[nt][2], acc[nt][3]} * sc + bv[nt][1];
+          const uint2 o = make_uint2(relu_pk16(cvt_pk_bf16(v0[0], v0[1])), relu_pk16(cvt_pk_bf16(v1[0], v1[1])));
+          *reinterpret_cast<uint2*>(d.y + yo + 16 * nt) = o;
+        }
       }
     }
   };
@@ -251,9 +328,11 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
     if (exact0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (ntiles == 7) {
-      asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
+      if (SPLIT) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(14)" ::: "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      if (SPLIT) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     }
   };
 
@@ -268,7 +347,7 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
   __syncthreads();
   // prologue: weights installed (via planes[1]), image 0 converted into planes[0],
   // DMA of image 1 in flight
-  prefetch_w(img >= img_switch ? 1 : 0);
+  if (!SPLIT) prefetch_w(img >= img_switch ? 1 : 0);
   issue_dma(img, 0);
   install_w(smem + IMG, img >= img_switch ? 1 : 0, 0);   // vmcnt(0): DMA(img) landed too
   convert(smem);
@@ -280,10 +359,10 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
     uint8_t* Pn = smem + ((it & 1) ^ 1) * IMG;
     const bool has_next = img + G < d.N;
     const int set = img >= img_switch ? 1 : 0;
-    if (set != cur_set) install_w(Pn, set, 2 * ntiles + ndma_w);   // prefetched last iteration
+    if (set != cur_set) install_w(Pn, set, NST * ntiles + ndma_w);   // prefetched last iteration
     // next image switches sets: fetch them now, hidden under this image's work
     // (extra loads only make the vmcnt waits below more conservative)
-    if (has_next && (img + G >= img_switch ? 1 : 0) != set) prefetch_w(set ^ 1);
+    if (!SPLIT && has_next && (img + G >= img_switch ? 1 : 0) != set) prefetch_w(set ^ 1);
     if (conv_first) {
       if (has_next) wait_dma(it == 0);
       PROBE(d.probe, NW, it, 1);
@@ -355,11 +434,22 @@ APEX_EXPORT int apex_conv1_s2d_fwd(Conv1S2DDesc d, int grid, hipStream_t st) {
   if (d.N < 1) return 0;
   if (grid <= 0 || grid > d.N) grid = d.N < 256 ? d.N : 256;
   if ((d.N + grid - 1) / grid > C1_MAXIMG) grid = (d.N + C1_MAXIMG - 1) / C1_MAXIMG;
-  switch (d.C) {
-    case 1: conv1_s2d_fwd_kernel<1><<<grid, C1_THREADS, 0, st>>>(d); break;
-    case 2: conv1_s2d_fwd_kernel<2><<<grid, C1_THREADS, 0, st>>>(d); break;
-    case 4: conv1_s2d_fwd_kernel<4><<<grid, C1_THREADS, 0, st>>>(d); break;
-    default: return (int)hipErrorInvalidValue;
+  const bool split = d.y_lo != nullptr;
+  if (split && (d.w32 == nullptr || (d.w2 != nullptr && d.w2_32 == nullptr))) return (int)hipErrorInvalidValue;
+  if (split) {
+    switch (d.C) {
+      case 1: conv1_s2d_fwd_kernel<1, true><<<grid, C1_THREADS, 0, st>>>(d); break;
+      case 2: conv1_s2d_fwd_kernel<2, true><<<grid, C1_THREADS, 0, st>>>(d); break;
+      case 4: conv1_s2d_fwd_kernel<4, true><<<grid, C1_THREADS, 0, st>>>(d); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+  } else {
+    switch (d.C) {
+      case 1: conv1_s2d_fwd_kernel<1, false><<<grid, C1_THREADS, 0, st>>>(d); break;
+      case 2: conv1_s2d_fwd_kernel<2, false><<<grid, C1_THREADS, 0, st>>>(d); break;
+      case 4: conv1_s2d_fwd_kernel<4, false><<<grid, C1_THREADS, 0, st>>>(d); break;
+      default: return (int)hipErrorInvalidValue;
+    }
   }
   APEX_CHECK_LAUNCH();
 }

@@ -18,6 +18,12 @@
 // gradient is 2 extra MFMAs per k-step against an all-ones fragment (K-quarter 0
 // waves).  dW is read from L2/HBM exactly once per image (vs once per 64-wide
 // K tile in the generic wgrad); each block writes one fp32 partial to the slab.
+//
+// SPLIT (fp32-accurate mode, dy_lo set): the frames are exact in bf16 and dY comes
+// as hi + lo planes -- two MFMAs per fragment pair.  Both dY planes do not fit in
+// LDS next to the frame planes, so an image's pixels run in two halves (224 + 192
+// rows, the last 16 zero): per half both dY planes are LDS-DMA'd (rows past pixel
+// 399 read the zero block), and the next image's frames stream in under half 1.
 #include "mfma_common.h"
 
 #define C1W_PLANE 7168
@@ -31,9 +37,10 @@ struct Conv1WgDesc {
   float* bias_slab;           // [gridDim.x][64]
   const uint8_t* zero16;      // 16 zero bytes (DMA filler)
   int N, C;
+  const bf16_t* dy_lo;        // split mode: lo plane of dY (else null)
 };
 
-template <int C>
+template <int C, bool SPLIT>
 __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1WgDesc d) {
   constexpr int K = 64 * C;
   constexpr int IMG = 2 * C * C1W_PLANE;
@@ -42,10 +49,12 @@ __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1Wg
   constexpr int NW = C1W_THREADS / 64;
   constexpr int NDW = (NDMA + NW - 1) / NW;
   constexpr int STG = NDMA * 1024;
-  constexpr int DYR = 416;               // dY rows: 400 + 16 zero rows (13 k-steps of 32)
+  // dY rows per LDS plane: 400 + 16 zero rows (13 k-steps of 32); SPLIT: one half
+  // (224 rows = 7 k-steps, the second half 192) per plane, two planes
+  constexpr int DYR = SPLIT ? 224 : 416;
   constexpr int NDY = 400 * 128 / 1024;  // dY DMA wave-instructions (8 rows each)
   constexpr int NDYW = (NDY + NW - 1) / NW;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[IMG + STG + DYR * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t smem[IMG + STG + (SPLIT ? 2 : 1) * DYR * 128];
   uint8_t* Pl = smem;
   uint8_t* Sg = Pl + IMG;
   uint8_t* Dy = Sg + STG;
@@ -54,8 +63,10 @@ __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1Wg
   const int wc = wv & 1, wk = wv >> 1;   // co tiles 2wc, 2wc+1; K tiles C*wk .. C*wk + C-1
 
   // zero dY rows 400..415 once (never written by the DMA)
-  for (int i = tid; i < 16 * 128 / 16; i += C1W_THREADS)
-    *reinterpret_cast<uint4*>(Dy + 400 * 128 + i * 16) = make_uint4(0, 0, 0, 0);
+  if (!SPLIT) {
+    for (int i = tid; i < 16 * 128 / 16; i += C1W_THREADS)
+      *reinterpret_cast<uint4*>(Dy + 400 * 128 + i * 16) = make_uint4(0, 0, 0, 0);
+  }
 
   // per-lane constant part of the X fragment address of each of this wave's K tiles:
   // tile t = (tap, frame c) block; lane reads k = 4 pcol .. +3 -> half pcol >> 1, +8 B for pcol & 1
@@ -104,6 +115,30 @@ __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1Wg
       }
     }
   };
+  // SPLIT: rows [224 h, 224 h + 224) of both dY planes (28 + 28 DMA instructions over
+  // the 8 waves; local row = global row - 224 h keeps swz_tr's row bits, 224 % 16 == 0)
+  constexpr int NDYS = 2 * DYR * 128 / 1024;
+  constexpr int NDYSW = (NDYS + NW - 1) / NW;
+  auto issue_dy_half = [&](int img, int h) {
+#pragma unroll
+    for (int i = 0; i < NDYSW; ++i) {
+      const int k = wv * NDYSW + i;
+      if (k < NDYS) {
+        const int pln = k / (NDYS / 2), kk = k - pln * (NDYS / 2);
+        const int r = 8 * kk + (lane >> 3), pc = lane & 7;
+        const int s = ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
+        const int c = pc ^ (s << 1);
+        const int gr = DYR * h + r;
+        const uint8_t* src = d.zero16;
+        if (gr < 400) src = reinterpret_cast<const uint8_t*>((pln ? d.dy_lo : d.dy) + ((int64_t)img * 400 + gr) * 64 + c * 8);
+        const uint32_t off =
+            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(Dy + pln * DYR * 128 + kk * 1024);
+        dma16(src, __builtin_amdgcn_readfirstlane(off));
+      }
+    }
+  };
+  // frame-DMA instructions this wave issues per image (vmcnt accounting of SPLIT)
+  const int nfr_w = NDMA > wv * NDW ? min(NDW, NDMA - wv * NDW) : 0;
 
   f32x4 acc[2][C], accb[2];
 #pragma unroll
@@ -114,30 +149,20 @@ __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1Wg
   }
   const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
 
-  const int G = gridDim.x;
-  int img = blockIdx.x;
-  if (img < d.N) issue_frames(img);
-  for (; img < d.N; img += G) {
-    issue_dy(img);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // frames(img) + dY(img) of this wave
-    __builtin_amdgcn_s_barrier();
-    for (int j = tid; j < NCHUNK; j += C1W_THREADS) {
-      const uint4 v = *reinterpret_cast<const uint4*>(Sg + j * 16);
-      const int c = j / 441, blk = j - c * 441;
-      *reinterpret_cast<uint4*>(Pl + (2 * c) * C1W_PLANE + blk * 16) = u8x8_to_bf16x8(v.x, v.y);
-      *reinterpret_cast<uint4*>(Pl + (2 * c + 1) * C1W_PLANE + blk * 16) = u8x8_to_bf16x8(v.z, v.w);
-    }
-    __syncthreads();
-    if (img + G < d.N) issue_frames(img + G);            // staging is free again
+  // k-steps [ks0, ks1) of the image, dY rows from plane `DyH` (row 32 ks - rbase)
+  auto compute_steps = [&](int ks0, int ks1, int rbase) {
 #pragma unroll 1
-    for (int ks = 0; ks < DYR / 32; ++ks) {
-      // pixels of this lane's two transposed reads (clamped: rows >= 400 carry dY = 0)
+    for (int ks = ks0; ks < ks1; ++ks) {
       const int p0 = min(32 * ks + 8 * g + q, 399), p1 = min(32 * ks + 8 * g + q + 4, 399);
       const int oh0 = p0 / 20, oh1 = p1 / 20;
       const int b0 = ((oh0 * 21 + p0 - 20 * oh0) << 4), b1 = ((oh1 * 21 + p1 - 20 * oh1) << 4);
-      bf16x8 a[2], b[C];
+      const int lk = ks - rbase / 32;
+      bf16x8 a[2], al[2], b[C];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = tr_frag8(Dy, ks, 16 * (2 * wc + i), lane);
+      for (int i = 0; i < 2; ++i) {
+        a[i] = tr_frag8(Dy, lk, 16 * (2 * wc + i), lane);
+        if (SPLIT) al[i] = tr_frag8(Dy + DYR * 128, lk, 16 * (2 * wc + i), lane);
+      }
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         const lds_s16x4* pa = (const lds_s16x4*)(Pl + b0 + xoff[j]);
@@ -151,12 +176,56 @@ __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1Wg
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < C; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < C; ++j) {
+          if (SPLIT) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], al[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        }
       if (wk == 0) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a[i], accb[i], 0, 0, 0);
+        for (int i = 0; i < 2; ++i) {
+          if (SPLIT) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, al[i], accb[i], 0, 0, 0);
+          accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a[i], accb[i], 0, 0, 0);
+        }
       }
     }
+  };
+  auto convert_frames = [&]() {
+    for (int j = tid; j < NCHUNK; j += C1W_THREADS) {
+      const uint4 v = *reinterpret_cast<const uint4*>(Sg + j * 16);
+      const int c = j / 441, blk = j - c * 441;
+      *reinterpret_cast<uint4*>(Pl + (2 * c) * C1W_PLANE + blk * 16) = u8x8_to_bf16x8(v.x, v.y);
+      *reinterpret_cast<uint4*>(Pl + (2 * c + 1) * C1W_PLANE + blk * 16) = u8x8_to_bf16x8(v.z, v.w);
+    }
+  };
+
+  const int G = gridDim.x;
+  int img = blockIdx.x;
+  if (img < d.N) issue_frames(img);
+  if constexpr (SPLIT) {
+    for (; img < d.N; img += G) {
+      issue_dy_half(img, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // frames(img) + dY half 0 of this wave
+      __builtin_amdgcn_s_barrier();
+      convert_frames();
+      __syncthreads();
+      compute_steps(0, DYR / 32, 0);
+      __syncthreads();                                    // dY planes and staging free
+      issue_dy_half(img, 1);
+      if (img + G < d.N) issue_frames(img + G);           // lands under half 1
+      vmcnt_le(img + G < d.N ? nfr_w : 0);                // dY half 1 of this wave
+      __builtin_amdgcn_s_barrier();
+      compute_steps(DYR / 32, 13, DYR);
+      __syncthreads();                                    // planes and dY may be overwritten
+    }
+  }
+  for (; !SPLIT && img < d.N; img += G) {
+    issue_dy(img);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // frames(img) + dY(img) of this wave
+    __builtin_amdgcn_s_barrier();
+    convert_frames();
+    __syncthreads();
+    if (img + G < d.N) issue_frames(img + G);            // staging is free again
+    compute_steps(0, DYR / 32, 0);
     __syncthreads();   // planes and dY image may be overwritten
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -180,11 +249,20 @@ __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1Wg
 APEX_EXPORT int apex_conv1_wgrad_img(Conv1WgDesc d, int grid, hipStream_t st) {
   if (d.N < 1) return 0;
   if (grid <= 0) return (int)hipErrorInvalidValue;
-  switch (d.C) {
-    case 1: conv1_wgrad_img_kernel<1><<<grid, C1W_THREADS, 0, st>>>(d); break;
-    case 2: conv1_wgrad_img_kernel<2><<<grid, C1W_THREADS, 0, st>>>(d); break;
-    case 4: conv1_wgrad_img_kernel<4><<<grid, C1W_THREADS, 0, st>>>(d); break;
-    default: return (int)hipErrorInvalidValue;
+  if (d.dy_lo != nullptr) {
+    switch (d.C) {
+      case 1: conv1_wgrad_img_kernel<1, true><<<grid, C1W_THREADS, 0, st>>>(d); break;
+      case 2: conv1_wgrad_img_kernel<2, true><<<grid, C1W_THREADS, 0, st>>>(d); break;
+      case 4: conv1_wgrad_img_kernel<4, true><<<grid, C1W_THREADS, 0, st>>>(d); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+  } else {
+    switch (d.C) {
+      case 1: conv1_wgrad_img_kernel<1, false><<<grid, C1W_THREADS, 0, st>>>(d); break;
+      case 2: conv1_wgrad_img_kernel<2, false><<<grid, C1W_THREADS, 0, st>>>(d); break;
+      case 4: conv1_wgrad_img_kernel<4, false><<<grid, C1W_THREADS, 0, st>>>(d); break;
+      default: return (int)hipErrorInvalidValue;
+    }
   }
   APEX_CHECK_LAUNCH();
 }

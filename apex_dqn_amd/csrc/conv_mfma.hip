@@ -23,7 +23,7 @@
 #include "igemm_wgrad.h"
 
 struct ConvDesc {
-  const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]; mode 2: u8 frame ring
+  const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]
   const int32_t* frame_slots; // unused (conv1 runs in csrc/conv1_s2d.hip)
   const bf16_t* w;            // B operand [Cout][K] (K contiguous), + cls * w_cls_stride
   const float* bias;          // [Cout] or null
@@ -48,9 +48,12 @@ struct ConvDesc {
   int koff[16];
   int tile_hint;              // 0 auto, 1 BM=128, 2 BM=64
   int order_hint;             // 0 auto, 1 M tiles fastest per XCD, 2 N tiles fastest
-  float* part;                // split-K (dense mode): fp32 partials [ksplit][M][ldy]
-  int ksplit;                 // > 1: blockIdx.z = K split; dense_splitk_reduce applies bias / ReLU
-  int kgroups;                // 2: dense forward with two 4-wave K groups per block (see igemm_fwd_kernel)
+  // fp32-accurate ("split") mode, all four set: the lo planes of A, B (both weight
+  // sets) and the output; every operand is hi + lo (csrc/mfma_common.h split_pk_bf16)
+  const bf16_t* x_lo;
+  const bf16_t* w_lo;
+  const bf16_t* w2_lo;
+  bf16_t* y_lo;
 };
 
 
@@ -62,6 +65,8 @@ struct ConvDesc {
 struct FwdRegs {
   uint4 a[4];
   uint4 b0, b1;
+  uint4 al[4];                // SPLIT: lo planes of the same rows
+  uint4 bl0, bl1;
 };
 
 
@@ -78,26 +83,21 @@ __device__ __forceinline__ int epi_off(int r, int byte) {
 // learner's layers (0 = runtime), so the per-row div/mod is multiply-shift.
 // BM: rows per block (128: 32 per wave; 64: 16 per wave, for grids that would
 // otherwise leave CUs idle -- fc fwd/dgrad and the 7x7 / 9x9 layers).
-// KG: K groups per block (dense forward only).  KG = 2 runs two 4-wave pipelines
-// over the two halves of K in one 512-thread block, each with its own LDS stages,
-// and sums them through LDS before the epilogue: a grid of ~1.5 blocks per CU is
-// latency-bound per K step (one wave per SIMD), and this doubles the waves in
-// flight without split-K's fp32 partials in HBM.  Both halves must take the same
-// number of loop trips (barriers are block-wide): the host checks KT % 4 != 3.
-template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM, int KG = 1, bool W22 = false, bool PF3 = false>
-__global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
+// SPLIT: fp32-accurate mode.  Every stage holds the hi AND lo planes of both
+// operand tiles (the same staging addresses, a second buffer resource), each
+// fragment pair takes three MFMAs (hi.hi + lo.hi + hi.lo into one fp32
+// accumulator), and the epilogue writes the fp32 result as hi / lo bf16 planes
+// (ReLU applied in fp32 before the split: a ReLU on the lo plane alone would be
+// wrong; the dgrad mask zeroes both planes).
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM, bool SPLIT>
+__global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   constexpr int AR = BM / 32;            // A rows staged per thread
   constexpr int MT = BM / 64;            // 16-row MFMA tiles per wave
   constexpr int WR = BM / 4;             // output rows per wave
-  constexpr int STAGE = BM * 128 + FWD_BN * 128;
-  static_assert(KG == 1 || (MODE == 0 && !BT), "K groups: dense forward only");
-  // W22: the four waves tile the 64 x 64 block as 2 x 2 (32 x 32 each) instead of
-  // 4 x 1 (16 x 64): 8 instead of 10 fragment reads per wave and K step
-  static_assert(!W22 || (BM == 64 && KG == 1 && MODE == 0 && !BT), "W22: dense 64-row tiles only");
-  __shared__ __attribute__((aligned(16))) uint8_t smem_all[KG * 2 * STAGE];
-  const int kgi = KG == 1 ? 0 : (int)(threadIdx.x >> 8);
-  uint8_t* const smem = smem_all + kgi * (2 * STAGE);
-  const int tid = threadIdx.x & 255, lane = tid & 63, wv = tid >> 6;
+  constexpr int HALF = BM * 128 + FWD_BN * 128;   // one precision plane of a stage
+  constexpr int STAGE = SPLIT ? 2 * HALF : HALF;
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // XCD-contiguous tile order: adjacent M tiles (overlapping im2col input rows) share an L2
   const int wg = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                              gridDim.x * gridDim.y * gridDim.z);
@@ -115,10 +115,7 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
     by = r % gridDim.y;
     bz = r / gridDim.y;
   }
-  // dense split-K: blockIdx.z is the K split (no weight classes in dense mode)
-  const bool splitk = MODE == 0 && d.ksplit > 1;
-  const int kz = splitk ? bz : 0;
-  const int cls = splitk ? 0 : bz;
+  const int cls = bz;
   const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
   const uint32_t OWv = OWC ? OWC : d.OW;
   const int M = d.N * OHW;
@@ -128,17 +125,14 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   const bool second = d.w2 != nullptr && m0 >= d.m_switch;
   const bf16_t* __restrict__ wb = (second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride;
   const float* __restrict__ bias = second ? d.bias2 : d.bias;
-  const int KT_all = d.K >> 6;
-  int kt0 = splitk ? (kz * KT_all) / d.ksplit : 0;
-  int KT = splitk ? ((kz + 1) * KT_all) / d.ksplit - kt0 : KT_all;
-  if (KG == 2) {
-    kt0 = kgi ? KT_all / 2 : 0;
-    KT = kgi ? KT_all - KT_all / 2 : KT_all / 2;
-  }
+  const int KT = d.K >> 6;
   const int sc = tid & 7;
   const int srow = tid >> 3;
   const __amdgpu_buffer_rsrc_t ra_rs = buf_rsrc(d.x);
   const __amdgpu_buffer_rsrc_t rb_rs = buf_rsrc(wb);
+  const __amdgpu_buffer_rsrc_t ra_lo = buf_rsrc(SPLIT ? d.x_lo : d.x);
+  const __amdgpu_buffer_rsrc_t rb_lo =
+      buf_rsrc(SPLIT ? (second ? d.w2_lo : d.w_lo) + (int64_t)cls * d.w_cls_stride : wb);
 
   // per-thread staging rows (4 A rows, 2 B rows): loop-invariant byte offsets.
   // Rows past M are clamped to row 0 (their outputs are never stored).
@@ -148,7 +142,7 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
     const int m = m0 + srow + 32 * i;
     const int mm = m < M ? m : 0;
     if (MODE == 0) {
-      a_off[i] = ((uint32_t)mm * d.K + sc * 8 + kt0 * 64) * 2u;
+      a_off[i] = ((uint32_t)mm * d.K + sc * 8) * 2u;
       vmask[i] = 0;
     } else {
       const int img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
@@ -168,7 +162,7 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
     }
   }
   const uint32_t b_off0 = BT ? (uint32_t)((srow * d.ldb + n0 + sc * 8) * 2)
-                             : (uint32_t)(((n0 + srow) * d.K + sc * 8 + kt0 * 64) * 2);
+                             : (uint32_t)(((n0 + srow) * d.K + sc * 8) * 2);
   const uint32_t b_off1 = b_off0 + (BT ? 64u * d.ldb : 64u * d.K);
   const int cpb = d.Cin >> 6;
 
@@ -181,9 +175,16 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
     const uint32_t bso = BT ? (uint32_t)(d.bt == 2 ? kt * 128 * d.ldb : 2 * d.koff[cls * KT + kt]) : (uint32_t)kt * 128u;
     R.b0 = buf_ld16(rb_rs, b_off0, bso);
     R.b1 = buf_ld16(rb_rs, b_off1, bso);
+    if (SPLIT) {
+      R.bl0 = buf_ld16(rb_lo, b_off0, bso);
+      R.bl1 = buf_ld16(rb_lo, b_off1, bso);
+    }
     if (MODE == 0) {
 #pragma unroll
-      for (int i = 0; i < AR; ++i) R.a[i] = buf_ld16(ra_rs, a_off[i], (uint32_t)kt * 128u);
+      for (int i = 0; i < AR; ++i) {
+        R.a[i] = buf_ld16(ra_rs, a_off[i], (uint32_t)kt * 128u);
+        if (SPLIT) R.al[i] = buf_ld16(ra_lo, a_off[i], (uint32_t)kt * 128u);
+      }
     } else {
       const int tap = c_kh * d.KW + c_kw;
       const uint32_t toff = (uint32_t)(((c_kh * d.W + c_kw) * d.Cin + (c_cb << 6)) * 2);
@@ -192,8 +193,10 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
         if (PAD) {
           const uint32_t vo = ((vmask[i] >> tap) & 1u) ? a_off[i] + toff : BUF_OOB;
           R.a[i] = buf_ld16(ra_rs, vo, 0);
+          if (SPLIT) R.al[i] = buf_ld16(ra_lo, vo, 0);
         } else {
           R.a[i] = buf_ld16(ra_rs, a_off[i], toff);
+          if (SPLIT) R.al[i] = buf_ld16(ra_lo, a_off[i], toff);
         }
       }
     }
@@ -213,6 +216,14 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
     for (int i = 0; i < AR; ++i) *reinterpret_cast<uint4*>(As + swz_row(srow + 32 * i, sc)) = R.a[i];
     *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow, sc) : swz_row(srow, sc))) = R.b0;
     *reinterpret_cast<uint4*>(Bs + (BT ? swz_tr(srow + 32, sc) : swz_row(srow + 32, sc))) = R.b1;
+    if (SPLIT) {
+      uint8_t* Al = As + HALF;
+      uint8_t* Bl = Bs + HALF;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) *reinterpret_cast<uint4*>(Al + swz_row(srow + 32 * i, sc)) = R.al[i];
+      *reinterpret_cast<uint4*>(Bl + (BT ? swz_tr(srow, sc) : swz_row(srow, sc))) = R.bl0;
+      *reinterpret_cast<uint4*>(Bl + (BT ? swz_tr(srow + 32, sc) : swz_row(srow + 32, sc))) = R.bl1;
+    }
   };
 
   // acc[mt][nt] holds C^T (channels x pixels): lane (g = lane>>4, p = lane&15) owns
@@ -227,41 +238,33 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   auto compute = [&](int buf) {
     const uint8_t* As = smem + buf * STAGE;
     const uint8_t* Bs = As + BM * 128;
-    if constexpr (W22) {
-      const int wm = wv >> 1, wn = wv & 1;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int c = 4 * s + (lane >> 4);
-        bf16x8 a[2], b[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          a[i] = *reinterpret_cast<const bf16x8*>(As + swz_row(32 * wm + 16 * i + (lane & 15), c));
-          b[i] = *reinterpret_cast<const bf16x8*>(Bs + swz_row(32 * wn + 16 * i + (lane & 15), c));
-        }
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
-            acc[0][2 * mt + nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[0][2 * mt + nt], 0, 0, 0);
-      }
-      return;
-    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = 4 * s + (lane >> 4);
-      bf16x8 a[MT], b[4];
+      bf16x8 a[MT], b[4], al[MT], bl[4];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int mt = 0; mt < MT; ++mt) {
         a[mt] = *reinterpret_cast<const bf16x8*>(As + swz_row(WR * wv + 16 * mt + (lane & 15), c));
+        if (SPLIT) al[mt] = *reinterpret_cast<const bf16x8*>(As + HALF + swz_row(WR * wv + 16 * mt + (lane & 15), c));
+      }
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
+      for (int nt = 0; nt < 4; ++nt) {
         b[nt] = BT ? tr_frag8(Bs, s, 16 * nt, lane)
                    : *reinterpret_cast<const bf16x8*>(Bs + swz_row(16 * nt + (lane & 15), c));
+        if (SPLIT)
+          bl[nt] = BT ? tr_frag8(Bs + HALF, s, 16 * nt, lane)
+                      : *reinterpret_cast<const bf16x8*>(Bs + HALF + swz_row(16 * nt + (lane & 15), c));
+      }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
+        for (int nt = 0; nt < 4; ++nt) {
+          if (SPLIT) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[nt], a[mt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], al[mt], acc[mt][nt], 0, 0, 0);
+          }
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+        }
     }
   };
 
@@ -269,53 +272,14 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   // Tile t's global loads are issued two half-iterations before its MFMAs
   // (prefetch distance 2); loads past the last tile re-read tile KT-1 (cache
   // hits) so the body has no branches and the vmcnt waits stay partial.
-  int kt = 0;
-  if constexpr (PF3) {
-    // three register stages: tile t's loads are issued three compute steps ahead.
-    // Invariant at the loop head: tile kt in LDS buffer kt & 1, R1 / R2 hold tiles
-    // kt+1 / kt+2 (R0 is free); the body is unrolled by 3 so the sets stay static.
-    FwdRegs R0, R1, R2;
-    load_next(R0);
-    load_next(R1);
-    load_next(R2);
-    write_tile(0, R0);
-    __syncthreads();
-    load_next(R0);                      // tile 3
-    for (; kt + 2 < KT; kt += 3) {
-      const int b0 = kt & 1;
-      compute(b0);
-      write_tile(b0 ^ 1, R1);           // tile kt+1
-      __syncthreads();
-      load_next(R1);                    // tile kt+4
-      compute(b0 ^ 1);
-      write_tile(b0, R2);               // tile kt+2
-      __syncthreads();
-      load_next(R2);                    // tile kt+5
-      compute(b0);
-      write_tile(b0 ^ 1, R0);           // tile kt+3
-      __syncthreads();
-      load_next(R0);                    // tile kt+6
-      // rotate: R1 -> kt+4, R2 -> kt+5, R0 -> kt+6 are tiles kt'+1, kt'+2, kt'+3 of kt' = kt+3
-    }
-    if (kt < KT) {
-      compute(kt & 1);
-      if (kt + 1 < KT) {
-        write_tile((kt + 1) & 1, R1);
-        __syncthreads();
-        compute((kt + 1) & 1);
-      }
-    }
-    kt = KT;
-  }
   FwdRegs RA, RB;
-  if constexpr (!PF3) {
   load_next(RA);                        // tile 0
   load_next(RB);                        // tile 1
   write_tile(0, RA);
   __syncthreads();
   load_next(RA);                        // tile 2
-  }
-  for (; !PF3 && kt + 1 < KT; kt += 2) {
+  int kt = 0;
+  for (; kt + 1 < KT; kt += 2) {
     compute(0);
     write_tile(1, RB);                  // tile kt+1
     __syncthreads();
@@ -325,70 +289,17 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
     __syncthreads();
     load_next(RA);                      // tile kt+4
   }
-  if (!PF3 && kt < KT) compute(0);     // odd KT: last tile sits in buffer 0
-  if constexpr (KG == 2) {
-    // group 1 hands its accumulators to group 0 through LDS (lane-major: conflict-free)
-    __syncthreads();
-    f32x4* red = reinterpret_cast<f32x4*>(smem_all);
-    if (kgi == 1) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) red[(mt * 4 + nt) * 256 + tid] = acc[mt][nt];
-    }
-    __syncthreads();
-    if (kgi == 0) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] += red[(mt * 4 + nt) * 256 + tid];
-    }
-  }
-  if (splitk) {
-    // fp32 partial tile straight from the accumulators (lane: 4 consecutive channels
-    // of one row per 16x16 block), reduced + biased + ReLU'd by dense_splitk_reduce
-    const int g = lane >> 4, pl = lane & 15;
-    float* __restrict__ part = d.part + (int64_t)kz * M * d.ldy;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int m = m0 + WR * wv + 16 * mt + pl;
-      if (m >= M) continue;
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        *reinterpret_cast<f32x4*>(part + (int64_t)m * d.ldy + n0 + 16 * nt + 4 * g) = acc[mt][nt] * d.in_scale;
-    }
-    return;
-  }
+  if (kt < KT) compute(0);              // odd KT: last tile sits in buffer 0
   __syncthreads();
 
   // ---- epilogue: (acc*scale + bias) -> bf16x4 per lane -> swizzled LDS image -> 16-B row stores
+  // (SPLIT: a second image for the lo plane right after the BM-row hi image)
   uint8_t* Es = smem + wv * (WR * 128);
+  uint8_t* El = smem + BM * 128 + wv * (WR * 128);
   const int g = lane >> 4, pl = lane & 15;
-  const bool epi = KG == 1 || kgi == 0;
-  if constexpr (W22) {
-    // one 64-row image for the block (epi_off of the block row == the per-wave image
-    // the store loop below reads, since 16 wv is a multiple of 16)
-    const int wm = wv >> 1, wn = wv & 1;
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int ch = 32 * wn + 16 * nt + 4 * g;
-      float b4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (bias) {
-        const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + ch);
-        b4[0] = bb.x; b4[1] = bb.y; b4[2] = bb.z; b4[3] = bb.w;
-      }
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const f32x4 a4 = acc[0][2 * mt + nt];
-        const uint2 v = make_uint2(cvt_pk_bf16(a4[0] * d.in_scale + b4[0], a4[1] * d.in_scale + b4[1]),
-                                   cvt_pk_bf16(a4[2] * d.in_scale + b4[2], a4[3] * d.in_scale + b4[3]));
-        *reinterpret_cast<uint2*>(smem + epi_off(32 * wm + 16 * mt + pl, ch * 2)) = v;
-      }
-    }
-  }
+  const bool relu32 = SPLIT && d.relu && d.mask == nullptr;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt) {
-    if (!epi || W22) break;
     const int ch = 16 * nt + 4 * g;
     float b4[4] = {0.f, 0.f, 0.f, 0.f};
     if (bias) {
@@ -398,9 +309,22 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int row = 16 * mt + pl;
-      const uint2 v = make_uint2(cvt_pk_bf16(acc[mt][nt][0] * d.in_scale + b4[0], acc[mt][nt][1] * d.in_scale + b4[1]),
-                                 cvt_pk_bf16(acc[mt][nt][2] * d.in_scale + b4[2], acc[mt][nt][3] * d.in_scale + b4[3]));
-      *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) = v;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[mt][nt][r] * d.in_scale + b4[r];
+        if (relu32) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (SPLIT) {
+        uint32_t h01, l01, h23, l23;
+        split_pk_bf16(v[0], v[1], h01, l01);
+        split_pk_bf16(v[2], v[3], h23, l23);
+        *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(El + epi_off(row, ch * 2)) = make_uint2(l01, l23);
+      } else {
+        *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) =
+            make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+      }
     }
   }
   __syncthreads();
@@ -410,8 +334,10 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
   for (int p = 0; p < WR / 8; ++p) {
     const int row = 8 * p + (lane >> 3), ch = lane & 7;
     const int m = m0 + WR * wv + row;
-    if (m >= M || !epi) continue;
+    if (m >= M) continue;
     uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
+    uint4 vl = make_uint4(0, 0, 0, 0);
+    if (SPLIT) vl = *reinterpret_cast<const uint4*>(El + epi_off(row, ch * 16));
     const int img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
     const int oh = udiv<OWC>(rem, OWv), ow = rem - oh * OWv;
     const int64_t orow = ((int64_t)img * d.OHfull + oh * d.ostride_h + ooh) * d.OWfull + ow * d.ostride_w + oow;
@@ -420,18 +346,22 @@ __global__ void __launch_bounds__(256 * KG) igemm_fwd_kernel(ConvDesc d) {
       const uint4 mk = *reinterpret_cast<const uint4*>(d.mask + off);
       v = make_uint4(mask_bf16x2(v.x, mk.x), mask_bf16x2(v.y, mk.y), mask_bf16x2(v.z, mk.z),
                      mask_bf16x2(v.w, mk.w));
-    } else if (d.relu) {
+      if (SPLIT)
+        vl = make_uint4(mask_bf16x2(vl.x, mk.x), mask_bf16x2(vl.y, mk.y), mask_bf16x2(vl.z, mk.z),
+                        mask_bf16x2(vl.w, mk.w));
+    } else if (d.relu && !SPLIT) {
       v = make_uint4(relu_bf16x2(v.x), relu_bf16x2(v.y), relu_bf16x2(v.z), relu_bf16x2(v.w));
     }
     *reinterpret_cast<uint4*>(d.y + off) = v;
+    if (SPLIT) *reinterpret_cast<uint4*>(d.y_lo + off) = vl;
   }
 }
 
 // weight gradient: csrc/igemm_wgrad.h (igemm_wgrad_body)
-template <int MODE, int OWC, int OHWC, int CT, int NT>
+template <int MODE, int OWC, int OHWC, int CT, int NT, int SP>
 __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
-  igemm_wgrad_body<MODE, OWC, OHWC, CT, NT>(d, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
-                                            gridDim.x, gridDim.y, gridDim.z);
+  igemm_wgrad_body<MODE, OWC, OHWC, CT, NT, SP>(d, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                                                gridDim.x, gridDim.y, gridDim.z);
 }
 
 // Sum the fp32 split-K slabs -> fp32 gradient (scaled) and the bias partials.
@@ -526,49 +456,22 @@ __global__ void pack_conv_dgrad_weights_kernel(const bf16_t* __restrict__ w3, co
 }
 
 // ------------------------------------------------------------------ launchers
-template <int BM>
+template <int BM, bool SPLIT>
 static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
   const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
-  if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true, 1, 1, BM><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 0 && d.kgroups == 2 && d.ksplit <= 1) igemm_fwd_kernel<0, false, false, 1, 1, BM, 2><<<grid, 512, 0, st>>>(d);
-  else if (d.mode == 0 && BM == 64 && d.kgroups == 3 && d.ksplit <= 1)
-    igemm_fwd_kernel<0, false, false, 1, 1, 64, 1, true><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 0 && BM == 64 && d.kgroups == 4 && d.ksplit <= 1)
-    igemm_fwd_kernel<0, false, false, 1, 1, 64, 1, true, true><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 0 && BM == 64 && d.kgroups == 5 && d.ksplit <= 1)
-    igemm_fwd_kernel<0, false, false, 1, 1, 64, 1, false, true><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 0) igemm_fwd_kernel<0, false, false, 1, 1, BM><<<grid, 256, 0, st>>>(d);
+  if (d.mode == 0 && d.bt) igemm_fwd_kernel<0, false, true, 1, 1, BM, SPLIT><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0) igemm_fwd_kernel<0, false, false, 1, 1, BM, SPLIT><<<grid, 256, 0, st>>>(d);
   else if (pad && d.bt) {
     // dgrad: conv3 (9x9 out), conv2 per parity class (10x10 out)
-    if (g9) igemm_fwd_kernel<1, true, true, 9, 81, BM><<<grid, 256, 0, st>>>(d);
-    else if (g10) igemm_fwd_kernel<1, true, true, 10, 100, BM><<<grid, 256, 0, st>>>(d);
-    else igemm_fwd_kernel<1, true, true, 0, 0, BM><<<grid, 256, 0, st>>>(d);
-  } else if (pad) igemm_fwd_kernel<1, true, false, 0, 0, BM><<<grid, 256, 0, st>>>(d);
-  else if (d.bt) igemm_fwd_kernel<1, false, true, 0, 0, BM><<<grid, 256, 0, st>>>(d);
-  else if (g9) igemm_fwd_kernel<1, false, false, 9, 81, BM><<<grid, 256, 0, st>>>(d);   // conv2 fwd
-  else if (g7) igemm_fwd_kernel<1, false, false, 7, 49, BM><<<grid, 256, 0, st>>>(d);   // conv3 fwd
-  else igemm_fwd_kernel<1, false, false, 0, 0, BM><<<grid, 256, 0, st>>>(d);
-}
-
-// out[m][n] = act(sum_z part[z][m][n] + bias[n]) as bf16 (bias2 for rows >= m_switch)
-__global__ void __launch_bounds__(256) dense_splitk_reduce_kernel(ConvDesc d, int M) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;      // 4 outputs per thread
-  const int n4 = d.Cout >> 2;
-  if (i >= (int64_t)M * n4) return;
-  const int m = (int)(i / n4), n = (int)(i - (int64_t)m * n4) * 4;
-  f32x4 v = *reinterpret_cast<const f32x4*>(d.part + (int64_t)m * d.ldy + n);
-  for (int z = 1; z < d.ksplit; ++z) v += *reinterpret_cast<const f32x4*>(d.part + ((int64_t)z * M + m) * d.ldy + n);
-  const float* bias = (d.w2 != nullptr && m >= d.m_switch) ? d.bias2 : d.bias;
-  if (bias) {
-    const float4 b = *reinterpret_cast<const float4*>(bias + n);
-    v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-  }
-  if (d.relu) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
-  }
-  *reinterpret_cast<uint2*>(d.y + (int64_t)m * d.ldy + n) = make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+    if (g9) igemm_fwd_kernel<1, true, true, 9, 81, BM, SPLIT><<<grid, 256, 0, st>>>(d);
+    else if (g10) igemm_fwd_kernel<1, true, true, 10, 100, BM, SPLIT><<<grid, 256, 0, st>>>(d);
+    else igemm_fwd_kernel<1, true, true, 0, 0, BM, SPLIT><<<grid, 256, 0, st>>>(d);
+  } else if (pad) igemm_fwd_kernel<1, true, false, 0, 0, BM, SPLIT><<<grid, 256, 0, st>>>(d);
+  else if (d.bt) igemm_fwd_kernel<1, false, true, 0, 0, BM, SPLIT><<<grid, 256, 0, st>>>(d);
+  else if (g9) igemm_fwd_kernel<1, false, false, 9, 81, BM, SPLIT><<<grid, 256, 0, st>>>(d);   // conv2 fwd
+  else if (g7) igemm_fwd_kernel<1, false, false, 7, 49, BM, SPLIT><<<grid, 256, 0, st>>>(d);   // conv3 fwd
+  else igemm_fwd_kernel<1, false, false, 0, 0, BM, SPLIT><<<grid, 256, 0, st>>>(d);
 }
 
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
@@ -581,6 +484,10 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.mode == 1 && (d.pad_h > 0 || d.pad_w > 0) && d.KH * d.KW > 32) return (int)hipErrorInvalidValue;
   if (d.w2 != nullptr && (d.m_switch % 128)) return (int)hipErrorInvalidValue;
   if (d.bt == 1 && (d.K >> 6) * (d.ncls > 0 ? d.ncls : 1) > 16) return (int)hipErrorInvalidValue;
+  // split mode: every lo plane present (and the target set's when there is one)
+  const bool split = d.x_lo != nullptr;
+  if (split && (d.w_lo == nullptr || d.y_lo == nullptr || (d.w2 != nullptr && d.w2_lo == nullptr)))
+    return (int)hipErrorInvalidValue;
   const int M = d.N * d.OH * d.OW;
   const int ncls = d.ncls > 0 ? d.ncls : 1;
   // 128-row tiles unless that leaves the chip under ~2.5 blocks per CU
@@ -589,42 +496,47 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   // measured (scripts/bench_kernels.py sweep): 64-row tiles pay off for the dgrad
   // GEMMs (K-major B): conv3/conv2 dgrad and fc dgrad; 128 for the conv forward
   // GEMMs; 64 for a forward grid of < 1 block per CU (the fc: 192 -> 384 blocks,
-  // 3446 -> 3491 steps/s end to end)
-  bool bm64 = d.bt != 0 ? (pad || blocks128 < 640) : blocks128 < 256;
+  // 3446 -> 3491 steps/s end to end).  Split mode doubles the LDS stages (96 KB
+  // at 128 rows: one block per CU), so it takes 64-row tiles throughout.
+  bool bm64 = split ? true : (d.bt != 0 ? (pad || blocks128 < 640) : blocks128 < 256);
   if (d.tile_hint == 1) bm64 = false;
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
-  // two K groups need equal loop trips in both halves (block-wide barriers)
-  // 3: 2 x 2 wave tiling (W22); 4: W22 + three register stages (PF3); 5: PF3 only
-  if (d.kgroups >= 3 && (d.mode != 0 || d.bt)) d.kgroups = 1;
-  if (d.kgroups == 2 && (d.mode != 0 || d.bt || ((d.K >> 6) & 3) == 3 || (d.K >> 6) < 4)) d.kgroups = 1;
-  if (d.ksplit > 1) {
-    if (d.mode != 0 || d.bt || d.mask || d.part == nullptr || d.ksplit > (d.K >> 6)) return (int)hipErrorInvalidValue;
-    if (bm64) launch_fwd<64>(d, dim3((M + 63) / 64, d.Cout / FWD_BN, d.ksplit), st);
-    else launch_fwd<128>(d, dim3((M + 127) / 128, d.Cout / FWD_BN, d.ksplit), st);
-    const int64_t nthr = (int64_t)M * (d.Cout / 4);
-    dense_splitk_reduce_kernel<<<(int)((nthr + 255) / 256), 256, 0, st>>>(d, M);
-    APEX_CHECK_LAUNCH();
+  const dim3 g64((M + 63) / 64, d.Cout / FWD_BN, ncls), g128((M + 127) / 128, d.Cout / FWD_BN, ncls);
+  if (split) {
+    if (bm64) launch_fwd<64, true>(d, g64, st);
+    else launch_fwd<128, true>(d, g128, st);
+  } else {
+    if (bm64) launch_fwd<64, false>(d, g64, st);
+    else launch_fwd<128, false>(d, g128, st);
   }
-  if (bm64) launch_fwd<64>(d, dim3((M + 63) / 64, d.Cout / FWD_BN, ncls), st);
-  else launch_fwd<128>(d, dim3((M + 127) / 128, d.Cout / FWD_BN, ncls), st);
   APEX_CHECK_LAUNCH();
 }
 
 // Block shape: fewest re-read bytes -- X is read once per Co group (ct / CT
 // times), dY once per Kc group (kt / NT times); 4-tile shapes keep every wave busy.
-template <int MODE, int OWC, int OHWC>
+template <int MODE, int OWC, int OHWC, int SP>
 static void launch_wgrad(const WgradDesc& d, int nsplit, hipStream_t st) {
   const int kt = d.Kc / 64, ct = d.Co / 64;
-  const int best = wgrad_shape(kt, ct, d.Kc, d.Co);
-  const WgShape cands[] = {{1, 4}, {2, 2}, {4, 1}, {1, 3}, {1, 1}};
+  const int best = wgrad_shape(kt, ct, d.Kc, d.Co, SP);
+  const WgShape cands[WG_NSHAPES] = {{1, 4}, {2, 2}, {4, 1}, {1, 3}, {1, 1}, {1, 2}, {2, 1}};
   const dim3 grid(kt / cands[best].n, ct / cands[best].c, nsplit);
-  switch (best) {
-    case 0: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 4><<<grid, 256, 0, st>>>(d); break;
-    case 1: igemm_wgrad_kernel<MODE, OWC, OHWC, 2, 2><<<grid, 256, 0, st>>>(d); break;
-    case 2: igemm_wgrad_kernel<MODE, OWC, OHWC, 4, 1><<<grid, 256, 0, st>>>(d); break;
-    case 3: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 3><<<grid, 256, 0, st>>>(d); break;
-    default: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 1><<<grid, 256, 0, st>>>(d); break;
+  if constexpr (SP == 0) {
+    switch (best) {
+      case 0: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 4, 0><<<grid, 256, 0, st>>>(d); break;
+      case 1: igemm_wgrad_kernel<MODE, OWC, OHWC, 2, 2, 0><<<grid, 256, 0, st>>>(d); break;
+      case 2: igemm_wgrad_kernel<MODE, OWC, OHWC, 4, 1, 0><<<grid, 256, 0, st>>>(d); break;
+      case 3: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 3, 0><<<grid, 256, 0, st>>>(d); break;
+      default: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 1, 0><<<grid, 256, 0, st>>>(d); break;
+    }
+  } else {
+    switch (best) {
+      case 1: igemm_wgrad_kernel<MODE, OWC, OHWC, 2, 2, SP><<<grid, 256, 0, st>>>(d); break;
+      case 3: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 3, SP><<<grid, 256, 0, st>>>(d); break;
+      case 5: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 2, SP><<<grid, 256, 0, st>>>(d); break;
+      case 6: igemm_wgrad_kernel<MODE, OWC, OHWC, 2, 1, SP><<<grid, 256, 0, st>>>(d); break;
+      default: igemm_wgrad_kernel<MODE, OWC, OHWC, 1, 1, SP><<<grid, 256, 0, st>>>(d); break;
+    }
   }
 }
 
@@ -637,22 +549,42 @@ APEX_EXPORT int apex_conv_wgrad(WgradDesc d, float* out, float* bout, int nsplit
   if (d.mode == 2 && (d.Cin * trows > WG_TBL || d.Cin > 4)) return (int)hipErrorInvalidValue;
   if ((int64_t)d.Mred * d.ldd * 2 >= 0x7ffffff0LL) return (int)hipErrorInvalidValue;
   if (d.mode == 0 && (int64_t)d.Mred * d.ldx * 2 >= 0x7ffffff0LL) return (int)hipErrorInvalidValue;
+  // split mode: dY lo plane; X lo plane too except for the exact uint8 frames (mode 2)
+  const bool split = d.dy_lo != nullptr;
+  if (split && d.mode != 2 && d.x_lo == nullptr) return (int)hipErrorInvalidValue;
   // learner shapes get compile-time output geometry (conv3 7x7, conv2 9x9, conv1 20x20)
-  if (d.mode == 0) launch_wgrad<0, 1, 1>(d, nsplit, st);
-  else if (d.mode == 1 && d.OH == 7 && d.OW == 7) launch_wgrad<1, 7, 49>(d, nsplit, st);
-  else if (d.mode == 1 && d.OH == 9 && d.OW == 9) launch_wgrad<1, 9, 81>(d, nsplit, st);
-  else if (d.mode == 1) launch_wgrad<1, 0, 0>(d, nsplit, st);
-  else {
+  if (d.mode == 0) {
+    if (split) launch_wgrad<0, 1, 1, 1>(d, nsplit, st);
+    else launch_wgrad<0, 1, 1, 0>(d, nsplit, st);
+  } else if (d.mode == 1 && d.OH == 7 && d.OW == 7) {
+    if (split) launch_wgrad<1, 7, 49, 1>(d, nsplit, st);
+    else launch_wgrad<1, 7, 49, 0>(d, nsplit, st);
+  } else if (d.mode == 1 && d.OH == 9 && d.OW == 9) {
+    if (split) launch_wgrad<1, 9, 81, 1>(d, nsplit, st);
+    else launch_wgrad<1, 9, 81, 0>(d, nsplit, st);
+  } else if (d.mode == 1) {
+    if (split) launch_wgrad<1, 0, 0, 1>(d, nsplit, st);
+    else launch_wgrad<1, 0, 0, 0>(d, nsplit, st);
+  } else if (split) {
+    // conv1 in split mode: dY hi + lo against the exact frames (20 x 20 output only)
+    const int kt = d.Kc / 64;
+    const dim3 grid(1, d.Co / 64, nsplit);
+    if (d.OH != 20 || d.OW != 20) return (int)hipErrorInvalidValue;
+    if (kt == 4) igemm_wgrad_kernel<2, 20, 400, 1, 4, 2><<<grid, 256, 0, st>>>(d);
+    else if (kt == 2) igemm_wgrad_kernel<2, 20, 400, 1, 2, 2><<<grid, 256, 0, st>>>(d);
+    else if (kt == 1) igemm_wgrad_kernel<2, 20, 400, 1, 1, 2><<<grid, 256, 0, st>>>(d);
+    else return (int)hipErrorInvalidValue;
+  } else {
     // conv1: Kc = 64 C (C = 1, 2, 4 stacked frames) -> all Kc tiles in one block
     const int kt = d.Kc / 64;
     const dim3 grid(1, d.Co / 64, nsplit);
     const bool fixed = d.OH == 20 && d.OW == 20;
-    if (kt == 4 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 4><<<grid, 256, 0, st>>>(d);
-    else if (kt == 2 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 2><<<grid, 256, 0, st>>>(d);
-    else if (kt == 1 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 1><<<grid, 256, 0, st>>>(d);
-    else if (kt == 4) igemm_wgrad_kernel<2, 0, 0, 1, 4><<<grid, 256, 0, st>>>(d);
-    else if (kt == 2) igemm_wgrad_kernel<2, 0, 0, 1, 2><<<grid, 256, 0, st>>>(d);
-    else if (kt == 1) igemm_wgrad_kernel<2, 0, 0, 1, 1><<<grid, 256, 0, st>>>(d);
+    if (kt == 4 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 4, 0><<<grid, 256, 0, st>>>(d);
+    else if (kt == 2 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 2, 0><<<grid, 256, 0, st>>>(d);
+    else if (kt == 1 && fixed) igemm_wgrad_kernel<2, 20, 400, 1, 1, 0><<<grid, 256, 0, st>>>(d);
+    else if (kt == 4) igemm_wgrad_kernel<2, 0, 0, 1, 4, 0><<<grid, 256, 0, st>>>(d);
+    else if (kt == 2) igemm_wgrad_kernel<2, 0, 0, 1, 2, 0><<<grid, 256, 0, st>>>(d);
+    else if (kt == 1) igemm_wgrad_kernel<2, 0, 0, 1, 1, 0><<<grid, 256, 0, st>>>(d);
     else return (int)hipErrorInvalidValue;
   }
   hipError_t e = hipGetLastError();

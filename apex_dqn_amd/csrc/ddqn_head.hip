@@ -27,10 +27,10 @@ __global__ void __launch_bounds__(192) ddqn_head_kernel(
     const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
-    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n) {
+    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, HeadLo lo) {
   float ad;
   (void)ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs, loss,
-                           q_out, dH, dhead, zero_ptr, zero_n, &ad);
+                           q_out, dH, dhead, zero_ptr, zero_n, &ad, lo);
 }
 
 __global__ void __launch_bounds__(512) head_wgrad_kernel(HeadWgArgs h) { head_wgrad_body(h, blockIdx.x, blockIdx.y); }
@@ -39,24 +39,25 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
                                const int32_t* act, const float* rew, const float* gam, const float* isw,
                                int B, int A, int huber, float kappa, float grad_scale, float* td_abs,
                                float* loss, float* q_out, bf16_t* dH, float* dhead, float* zero_ptr,
-                               int zero_n, int hidden, hipStream_t st) {
+                               int zero_n, int hidden, HeadLo lo, hipStream_t st) {
   if (A < 1 || A > HEAD_MAXA || B < 1) return (int)hipErrorInvalidValue;
+  if (lo.Hon != nullptr && (lo.Htg == nullptr || lo.dH == nullptr)) return (int)hipErrorInvalidValue;
   if (hidden == 512)
     ddqn_head_kernel<512><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale,
-                                             td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n);
+                                             td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo);
   else if (hidden == 256)
     ddqn_head_kernel<256><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale,
-                                             td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n);
+                                             td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo);
   else
     return (int)hipErrorInvalidValue;
   APEX_CHECK_LAUNCH();
 }
 
 APEX_EXPORT int apex_head_wgrad(const bf16_t* Hon, const float* dhead, int B, int A, float* gwv, float* gbv,
-                                float* gwa, float* gba, int hidden, hipStream_t st) {
+                                float* gwa, float* gba, int hidden, const bf16_t* Hon_lo, hipStream_t st) {
   if (hidden != 512 && hidden != 256) return (int)hipErrorInvalidValue;
   dim3 grid(A + 1, hidden / 64);
-  head_wgrad_kernel<<<grid, 512, 0, st>>>(HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden});
+  head_wgrad_kernel<<<grid, 512, 0, st>>>(HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden, Hon_lo});
   APEX_CHECK_LAUNCH();
 }
 
@@ -71,7 +72,7 @@ __global__ void __launch_bounds__(256) actor_head_kernel(const bf16_t* __restric
   const int e = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (e >= E) return;
   float q[HEAD_MAXA], hv[HS / 64], ha[HS / 64];
-  head_row<HS>(H + (int64_t)e * 2 * HS, P, A, lane, q, hv, ha);
+  head_row<HS>(H + (int64_t)e * 2 * HS, nullptr, P, A, lane, q, hv, ha);
   int best = 0;
   float bq = -3.4e38f;
 #pragma unroll

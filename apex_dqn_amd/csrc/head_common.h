@@ -16,6 +16,14 @@ struct HeadParams {
   const float* ba;
 };
 
+// fp32-accurate ("split") mode: lo planes of the stream activations (online,
+// target) and of the stream gradient dH; all null in bf16 mode
+struct HeadLo {
+  const bf16_t* Hon;
+  const bf16_t* Htg;
+  bf16_t* dH;
+};
+
 // NPL consecutive fp32 weights (16-B aligned: NPL is 4 or 8) as float4 loads
 template <int NPL>
 __device__ __forceinline__ void load_w(const float* __restrict__ p, float* w) {
@@ -33,9 +41,9 @@ __device__ __forceinline__ float bf16_at(const uint32_t* u, int k) {
 
 // q-values of one 2*HS-wide activation row (HS = stream width: 512 NatureCNN, 256
 // IMPALA): lane holds cols lane*NPL..+NPL-1 of each stream, NPL = HS / 64
+// NPL bf16 of each stream of one row -> fp32 (lane's columns)
 template <int HS>
-__device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const HeadParams& P, int A,
-                                         int lane, float* q, float* hv, float* ha) {
+__device__ __forceinline__ void load_row_streams(const bf16_t* __restrict__ row, int lane, float* hv, float* ha) {
   constexpr int NPL = HS / 64;
   uint32_t wv_[NPL / 2], wa_[NPL / 2];
   if constexpr (NPL == 8) {
@@ -53,6 +61,24 @@ __device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const H
   for (int k = 0; k < NPL; ++k) {
     hv[k] = bf16_at(wv_, k);
     ha[k] = bf16_at(wa_, k);
+  }
+}
+
+// q-values of one row; `row_lo` (split mode, else null) adds the lo plane: the
+// activations are then fp32-accurate (hi + lo)
+template <int HS>
+__device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const bf16_t* __restrict__ row_lo,
+                                         const HeadParams& P, int A, int lane, float* q, float* hv, float* ha) {
+  constexpr int NPL = HS / 64;
+  load_row_streams<HS>(row, lane, hv, ha);
+  if (row_lo != nullptr) {
+    float lv[NPL], la[NPL];
+    load_row_streams<HS>(row_lo, lane, lv, la);
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      hv[k] += lv[k];
+      ha[k] += la[k];
+    }
   }
   float part[HEAD_MAXA + 1];
   {
@@ -99,7 +125,7 @@ __device__ __forceinline__ bool ddqn_head_body(
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
     bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n,
-    float* ad_out) {
+    float* ad_out, HeadLo lo) {
   __shared__ float qs[2][HEAD_MAXA];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.x;
@@ -110,12 +136,16 @@ __device__ __forceinline__ bool ddqn_head_body(
   constexpr int NPL = HS / 64, ROW = 2 * HS;
   float q_t[HEAD_MAXA], q_n[HEAD_MAXA], q_g[HEAD_MAXA];
   float hv_t[NPL], ha_t[NPL];
+  const bool split = lo.Hon != nullptr;
   if (wv == 0) {
-    head_row<HS>(Hon + (int64_t)b * ROW, Pon, A, lane, q_t, hv_t, ha_t);
+    head_row<HS>(Hon + (int64_t)b * ROW, split ? lo.Hon + (int64_t)b * ROW : nullptr, Pon, A, lane, q_t, hv_t, ha_t);
   } else {
     float hv_x[NPL], ha_x[NPL], q[HEAD_MAXA];
-    if (wv == 1) head_row<HS>(Hon + (int64_t)(B + b) * ROW, Pon, A, lane, q, hv_x, ha_x);
-    else head_row<HS>(Htg + (int64_t)b * ROW, Ptg, A, lane, q, hv_x, ha_x);
+    if (wv == 1)
+      head_row<HS>(Hon + (int64_t)(B + b) * ROW, split ? lo.Hon + (int64_t)(B + b) * ROW : nullptr, Pon, A, lane, q,
+                   hv_x, ha_x);
+    else
+      head_row<HS>(Htg + (int64_t)b * ROW, split ? lo.Htg + (int64_t)b * ROW : nullptr, Ptg, A, lane, q, hv_x, ha_x);
     if (lane == 0) {
 #pragma unroll
       for (int j = 0; j < HEAD_MAXA; ++j)
@@ -189,7 +219,28 @@ __device__ __forceinline__ bool ddqn_head_body(
   }
 #pragma unroll
   for (int k = 0; k < NPL; ++k) da[k] = ha_t[k] > 0.f ? dq * (wsel[k] - colsum[k] * invA) : 0.f;
-  if constexpr (NPL == 8) {
+  if (split) {
+    // fp32 dH -> hi / lo planes (NPL consecutive columns per stream: 2 per dword)
+    uint32_t vh[NPL / 2], vl[NPL / 2], ah[NPL / 2], al[NPL / 2];
+#pragma unroll
+    for (int k = 0; k < NPL / 2; ++k) {
+      split_pk_bf16_h(dv[2 * k], dv[2 * k + 1], vh[k], vl[k]);
+      split_pk_bf16_h(da[2 * k], da[2 * k + 1], ah[k], al[k]);
+    }
+    bf16_t* o[2] = {dH + (int64_t)b * ROW, lo.dH + (int64_t)b * ROW};
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+      const uint32_t* V = pl ? vl : vh;
+      const uint32_t* Av = pl ? al : ah;
+      if constexpr (NPL == 8) {
+        *reinterpret_cast<uint4*>(o[pl] + lane * 8) = make_uint4(V[0], V[1], V[2], V[3]);
+        *reinterpret_cast<uint4*>(o[pl] + HS + lane * 8) = make_uint4(Av[0], Av[1], Av[2], Av[3]);
+      } else {
+        *reinterpret_cast<uint2*>(o[pl] + lane * 4) = make_uint2(V[0], V[1]);
+        *reinterpret_cast<uint2*>(o[pl] + HS + lane * 4) = make_uint2(Av[0], Av[1]);
+      }
+    }
+  } else if constexpr (NPL == 8) {
     const uint4 ov = make_uint4(pack_bf16x2(dv[0], dv[1]), pack_bf16x2(dv[2], dv[3]), pack_bf16x2(dv[4], dv[5]),
                                 pack_bf16x2(dv[6], dv[7]));
     const uint4 oa = make_uint4(pack_bf16x2(da[0], da[1]), pack_bf16x2(da[2], da[3]), pack_bf16x2(da[4], da[5]),
@@ -221,6 +272,7 @@ struct HeadWgArgs {
   float* gwa;
   float* gba;
   int HS;
+  const bf16_t* Hon_lo;      // split mode: lo plane of Hon (else null)
 };
 
 // block (j, chunk): any multiple of 64 threads up to 1024 (waves split the rows)
@@ -233,11 +285,22 @@ __device__ __forceinline__ void head_wgrad_body(const HeadWgArgs& h, int j, int 
   const int k = chunk * 64 + lane;  // 0..HS-1
   const int col = (j == 0 ? 0 : HS) + k;
   float acc = 0.f, accb = 0.f;
+  const bf16_t* __restrict__ Hlo = h.Hon_lo;
+  if (Hlo != nullptr) {
 #pragma unroll 8
-  for (int b = w; b < B; b += nw) {
-    const float d = dhead[(int64_t)b * (A + 1) + j];
-    acc += d * bf16_to_f32(Hon[(int64_t)b * 2 * HS + col]);
-    accb += d;
+    for (int b = w; b < B; b += nw) {
+      const float d = dhead[(int64_t)b * (A + 1) + j];
+      const int64_t o = (int64_t)b * 2 * HS + col;
+      acc += d * (bf16_to_f32(Hon[o]) + bf16_to_f32(Hlo[o]));
+      accb += d;
+    }
+  } else {
+#pragma unroll 8
+    for (int b = w; b < B; b += nw) {
+      const float d = dhead[(int64_t)b * (A + 1) + j];
+      acc += d * bf16_to_f32(Hon[(int64_t)b * 2 * HS + col]);
+      accb += d;
+    }
   }
   red[w][lane] = acc;
   if (lane == 0) red[w][64] = accb;

@@ -19,6 +19,10 @@ struct WgradDesc {
   double* norm_part;          // optional: per-wave sum of squares of this (final) gradient tile
   int norm_slot0;             // first slot; slot = norm_slot0 + 4 * linear block + wave
   int pad0;
+  // fp32-accurate ("split") mode: lo planes of dY and X (x_lo null for the exact
+  // uint8 frames of mode 2); see igemm_wgrad_body's SP
+  const bf16_t* dy_lo;
+  const void* x_lo;
 };
 
 // =====================================================================================
@@ -44,10 +48,15 @@ struct WgradDesc {
 // OWC/OHWC: output width / pixels per image as compile-time constants (0 = runtime);
 // only the prologue divides.  CT x NT (<= 4) output tiles per block; the block
 // always has 4 waves (all stage; waves past CT * NT do not compute).
-template <int MODE, int OWC, int OHWC, int CT, int NT>
+// SP: fp32-accurate operands.  0: bf16; 1: dY and X both hi + lo (three MFMAs per
+// fragment pair: hi.hi + lo.hi + hi.lo); 2: dY hi + lo, X exact in bf16 (uint8
+// frames: two MFMAs).  The lo images sit after the hi images of each stage.
+template <int MODE, int OWC, int OHWC, int CT, int NT, int SP = 0>
 __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, int gx, int gy, int gz) {
   static_assert(CT * NT <= 4, "at most 4 output tiles per block");
-  constexpr int NIMG = CT + NT;
+  static_assert(SP != 1 || MODE != 2, "mode 2 X is exact: SP = 2");
+  constexpr int NLO = SP == 0 ? 0 : (SP == 1 ? CT + NT : CT);
+  constexpr int NIMG = CT + NT + NLO;
   constexpr int STAGE = NIMG * WG_IMG;
   constexpr int NTHR = 256;
   // dense rows (MODE 0) need no row table: 80 KB for a 4-tile block, two blocks per CU
@@ -103,6 +112,12 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
   const __amdgpu_buffer_rsrc_t x_rs = MODE == 0
       ? __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(d.x), (short)0, r_end * d.ldx * 2, 0x00020000)
       : buf_rsrc(d.x);
+  const __amdgpu_buffer_rsrc_t dyl_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(SP ? d.dy_lo : d.dy), (short)0, r_end * d.ldd * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xl_rs = MODE == 0
+      ? __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(SP == 1 ? d.x_lo : d.x), (short)0, r_end * d.ldx * 2,
+                                          0x00020000)
+      : buf_rsrc(SP == 1 ? d.x_lo : d.x);
   const uint32_t dy_off = (uint32_t)(((r_begin + srow) * d.ldd + cob * 64 + sc * 8) * 2);
   const uint32_t dy_r32 = (uint32_t)(32 * d.ldd * 2), dy_step = (uint32_t)(WG_ROWS * d.ldd * 2);
   const uint32_t x_off = (uint32_t)(((r_begin + srow) * d.ldx + kcb * 64 + sc * 8) * 2);
@@ -131,6 +146,8 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
   struct Regs {
     uint4 dy[CT][2];
     uint4 x[NT][2];
+    uint4 dyl[CT][2];
+    uint4 xl[NT][2];
   };
 
   auto load_step = [&](int st, Regs& R) {
@@ -139,6 +156,10 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
       const uint32_t o = dy_off + st * dy_step + c * 128;
       R.dy[c][0] = buf_ld16(dy_rs, o, 0);
       R.dy[c][1] = buf_ld16(dy_rs, o + dy_r32, 0);
+      if (SP) {
+        R.dyl[c][0] = buf_ld16(dyl_rs, o, 0);
+        R.dyl[c][1] = buf_ld16(dyl_rs, o + dy_r32, 0);
+      }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -146,17 +167,26 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
         const uint32_t o = x_off + st * x_step + t * 128;
         R.x[t][0] = buf_ld16(x_rs, o, 0);
         R.x[t][1] = buf_ld16(x_rs, o + x_r32, 0);
+        if (SP == 1) {
+          R.xl[t][0] = buf_ld16(xl_rs, o, 0);
+          R.xl[t][1] = buf_ld16(xl_rs, o + x_r32, 0);
+        }
       } else if (MODE == 1) {
         const uint32_t* tb = tbl + st * WG_ROWS + srow;
         R.x[t][0] = buf_ld16(x_rs, tb[0] + x_tap[t], 0);
         R.x[t][1] = buf_ld16(x_rs, tb[32] + x_tap[t], 0);
+        if (SP == 1) {
+          R.xl[t][0] = buf_ld16(xl_rs, tb[0] + x_tap[t], 0);
+          R.xl[t][1] = buf_ld16(xl_rs, tb[32] + x_tap[t], 0);
+        }
       } else {
         R.x[t][0] = buf_ld16(x_rs, tbl[x2_tb[t] + st * WG_ROWS + x2_row] + x_tap[t], 0);
       }
     }
   };
 
-  // image i of stage stg: i < CT: dY co tile i; i >= CT: X kc tile i - CT
+  // image i of stage stg: i < CT: dY co tile i; i >= CT: X kc tile i - CT; then the
+  // lo planes: CT + NT + c = dY lo tile c, 2 CT + NT + t = X lo tile t
   auto img = [&](int stg, int i) -> uint8_t* { return smem + stg * STAGE + i * WG_IMG; };
 
   auto write_step = [&](int stg, const Regs& R) {
@@ -164,6 +194,10 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
     for (int c = 0; c < CT; ++c) {
       *reinterpret_cast<uint4*>(img(stg, c) + swz_tr(srow, sc)) = R.dy[c][0];
       *reinterpret_cast<uint4*>(img(stg, c) + swz_tr(srow + 32, sc)) = R.dy[c][1];
+      if (SP) {
+        *reinterpret_cast<uint4*>(img(stg, CT + NT + c) + swz_tr(srow, sc)) = R.dyl[c][0];
+        *reinterpret_cast<uint4*>(img(stg, CT + NT + c) + swz_tr(srow + 32, sc)) = R.dyl[c][1];
+      }
     }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -171,6 +205,11 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
       if (MODE != 2) {
         *reinterpret_cast<uint4*>(X + swz_tr(srow, sc)) = R.x[t][0];
         *reinterpret_cast<uint4*>(X + swz_tr(srow + 32, sc)) = R.x[t][1];
+        if (SP == 1) {
+          uint8_t* XL = img(stg, 2 * CT + NT + t);
+          *reinterpret_cast<uint4*>(XL + swz_tr(srow, sc)) = R.xl[t][0];
+          *reinterpret_cast<uint4*>(XL + swz_tr(srow + 32, sc)) = R.xl[t][1];
+        }
       } else {
         // 16 uint8 of s2d block x2_b -> bf16 chunks 2 x2_b, 2 x2_b + 1 of row x2_row
         *reinterpret_cast<uint4*>(X + swz_tr(x2_row, 2 * x2_b)) = u8x8_to_bf16x8(R.x[t][0].x, R.x[t][0].y);
@@ -196,21 +235,35 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
     if (!active) return;
     const uint8_t* D = img(stg, wc);
     const uint8_t* X = img(stg, CT + wn);
+    const uint8_t* DL = img(stg, CT + NT + wc);
+    const uint8_t* XL = img(stg, 2 * CT + NT + wn);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 a[4], b[4];
+      bf16x8 a[4], b[4], al[4], bl[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = tr_frag8(D, kk, 16 * t, lane);
+      for (int t = 0; t < 4; ++t) {
+        a[t] = tr_frag8(D, kk, 16 * t, lane);
+        if (SP) al[t] = tr_frag8(DL, kk, 16 * t, lane);
+      }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) b[t] = tr_frag8(X, kk, 16 * t, lane);
+      for (int t = 0; t < 4; ++t) {
+        b[t] = tr_frag8(X, kk, 16 * t, lane);
+        if (SP == 1) bl[t] = tr_frag8(XL, kk, 16 * t, lane);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < 4; ++j) {
+          if (SP) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], al[i], acc[i][j], 0, 0, 0);
+          if (SP == 1) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], a[i], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+        }
       if (do_bias) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a[i], accb[i], 0, 0, 0);
+        for (int i = 0; i < 4; ++i) {
+          if (SP) accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, al[i], accb[i], 0, 0, 0);
+          accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a[i], accb[i], 0, 0, 0);
+        }
       }
     }
   };
@@ -278,15 +331,21 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
 
 // Block shape choice (host): fewest re-read bytes -- X is read once per Co group
 // (ct / CT times), dY once per Kc group (kt / NT times); 4-tile shapes keep every
-// wave busy.  Index into {CT,NT} = {1,4} {2,2} {4,1} {1,3} {1,1}.
+// wave busy.  Index into {CT,NT} = {1,4} {2,2} {4,1} {1,3} {1,1} {1,2} {2,1}.
+// Split mode doubles the images per stage, so only shapes with CT + NT <= 4
+// (2 CT + NT <= 6 with SP = 2's exact X) fit two stages in LDS next to the row table.
 struct WgShape { int c, n; };
-static inline int wgrad_shape(int kt, int ct, int Kc, int Co) {
-  const WgShape cands[] = {{1, 4}, {2, 2}, {4, 1}, {1, 3}, {1, 1}};
+#define WG_NSHAPES 7
+static inline int wgrad_shape(int kt, int ct, int Kc, int Co, int sp = 0) {
+  const WgShape cands[WG_NSHAPES] = {{1, 4}, {2, 2}, {4, 1}, {1, 3}, {1, 1}, {1, 2}, {2, 1}};
   int best = 4;
   double bc = 1e300;
-  for (int i = 0; i < 5; ++i) {
+  for (int i = 0; i < WG_NSHAPES; ++i) {
     const WgShape c = cands[i];
     if (kt % c.n || ct % c.c) continue;
+    if (sp == 1 && c.c + c.n > 4) continue;
+    if (sp == 2 && 2 * c.c + c.n > 6) continue;
+    if (sp == 0 && i >= 5) continue;     // the 3-tile shapes are for split mode only
     const double cost = (double)(ct / c.c) * (double)Kc + (double)(kt / c.n) * (double)Co;
     if (cost < bc) { bc = cost; best = i; }
   }

@@ -46,6 +46,15 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){lo, hi}, bf16x2v));
 }
 
+// fp32-accurate ("split") operands: v = hi + lo with hi = bf16(v), lo = bf16(v - hi),
+// both round-to-nearest-even (v - hi is exact in fp32).  A product of two split
+// operands is hi*hi + hi*lo + lo*hi (the lo*lo term is below 2^-16 relative):
+// three bf16 MFMAs with fp32 accumulation instead of one fp32 MFMA at 1/16 the rate.
+__device__ __forceinline__ void split_pk_bf16(float a, float b, uint32_t& hi, uint32_t& lo) {
+  hi = cvt_pk_bf16(a, b);
+  lo = cvt_pk_bf16(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+
 __device__ __forceinline__ uint32_t u8pair_bf16(uint32_t v, int sh) {
   // two consecutive bytes of v (starting at byte sh) -> two bf16 (exact: integers <= 255):
   // v_cvt_f32_ubyteN x2 + v_cvt_pk_bf16_f32
@@ -146,6 +155,9 @@ __device__ __forceinline__ void vmcnt_le(int n) {
     APEX_VMCNT_CASE(10) APEX_VMCNT_CASE(11) APEX_VMCNT_CASE(12) APEX_VMCNT_CASE(13) APEX_VMCNT_CASE(14)
     APEX_VMCNT_CASE(15) APEX_VMCNT_CASE(16) APEX_VMCNT_CASE(17) APEX_VMCNT_CASE(18) APEX_VMCNT_CASE(19)
     APEX_VMCNT_CASE(20) APEX_VMCNT_CASE(21) APEX_VMCNT_CASE(22) APEX_VMCNT_CASE(23) APEX_VMCNT_CASE(24)
+    APEX_VMCNT_CASE(25) APEX_VMCNT_CASE(26) APEX_VMCNT_CASE(27) APEX_VMCNT_CASE(28) APEX_VMCNT_CASE(29)
+    APEX_VMCNT_CASE(30) APEX_VMCNT_CASE(31) APEX_VMCNT_CASE(32) APEX_VMCNT_CASE(33) APEX_VMCNT_CASE(34)
+    APEX_VMCNT_CASE(35) APEX_VMCNT_CASE(36)
     default: break;
   }
 #undef APEX_VMCNT_CASE

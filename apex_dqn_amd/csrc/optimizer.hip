@@ -32,9 +32,14 @@ __global__ void __launch_bounds__(256) sqnorm_partial_kernel(const float* __rest
 
 __global__ void __launch_bounds__(256) rmsprop_kernel(RmspropArgs a) { rmsprop_body(a, blockIdx.x, gridDim.x); }
 
-__global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    y[i] = f32_to_bf16(x[i]);
+// fp32 -> bf16 copy; with `lo` also the residual plane (x = y + lo: fp32-accurate mode)
+__global__ void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, bf16_t* __restrict__ lo,
+                                 int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bf16_t h = f32_to_bf16(x[i]);
+    y[i] = h;
+    if (lo != nullptr) lo[i] = f32_to_bf16(x[i] - bf16_to_f32(h));
+  }
 }
 
 APEX_EXPORT int apex_grad_sqnorm_partials(const float* g, int64_t n, double* partials, hipStream_t st) {
@@ -44,13 +49,13 @@ APEX_EXPORT int apex_grad_sqnorm_partials(const float* g, int64_t n, double* par
 
 APEX_EXPORT int apex_rmsprop_step(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
                                   const double* partials, float lr, float alpha, float eps, float clip,
-                                  int centered, float* norm_out, hipStream_t st) {
+                                  int centered, float* norm_out, bf16_t* pb_lo, hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
-  if ((uintptr_t)pb & 7) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)pb | (uintptr_t)pb_lo) & 7) return (int)hipErrorInvalidValue;
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, NPART, lr, alpha, eps, clip, centered,
-                                                 norm_out});
+                                                 norm_out, pb_lo});
   APEX_CHECK_LAUNCH();
 }
 
@@ -58,19 +63,19 @@ APEX_EXPORT int apex_rmsprop_step(float* p, const float* g, float* v, float* m, 
 // (fc wgrad epilogue + grad_finalize blocks): no separate squared-norm pass
 APEX_EXPORT int apex_rmsprop_step_np(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
                                      const double* partials, int npart, float lr, float alpha, float eps, float clip,
-                                     int centered, float* norm_out, hipStream_t st) {
+                                     int centered, float* norm_out, bf16_t* pb_lo, hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
-  if ((uintptr_t)pb & 7) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)pb | (uintptr_t)pb_lo) & 7) return (int)hipErrorInvalidValue;
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, npart, lr, alpha, eps, clip, centered,
-                                                 norm_out});
+                                                 norm_out, pb_lo});
   APEX_CHECK_LAUNCH();
 }
 
-APEX_EXPORT int apex_cast_bf16(const float* x, bf16_t* y, int64_t n, hipStream_t st) {
+APEX_EXPORT int apex_cast_bf16(const float* x, bf16_t* y, int64_t n, bf16_t* lo, hipStream_t st) {
   int nb = (int)((n + 255) / 256);
   nb = nb > 2048 ? 2048 : (nb < 1 ? 1 : nb);
-  cast_bf16_kernel<<<nb, 256, 0, st>>>(x, y, n);
+  cast_bf16_kernel<<<nb, 256, 0, st>>>(x, y, lo, n);
   APEX_CHECK_LAUNCH();
 }

@@ -38,6 +38,7 @@ struct RmspropArgs {
   float lr, alpha, eps, clip;
   int centered;
   float* norm_out;
+  bf16_t* pb_lo;     // fp32-accurate mode: lo plane of the bf16 copy (p = pb + pb_lo), else null
 };
 
 // one 256-thread block `bid` of `nblk` (grid-stride over float4 chunks)
@@ -47,6 +48,7 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
   float* __restrict__ v = A_.v;
   float* __restrict__ m = A_.m;
   bf16_t* __restrict__ pb = A_.pb;
+  bf16_t* __restrict__ pbl = A_.pb_lo;
   const int64_t n = A_.n;
   const float lr = A_.lr, alpha = A_.alpha, eps = A_.eps;
   const int centered = A_.centered;
@@ -57,6 +59,7 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
   float4* v4 = reinterpret_cast<float4*>(v);
   float4* m4 = reinterpret_cast<float4*>(m);
   uint2* pb4 = reinterpret_cast<uint2*>(pb);
+  uint2* pbl4 = reinterpret_cast<uint2*>(pbl);
   const int64_t stride = (int64_t)nblk * blockDim.x;
   int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   // the first chunk's loads are in flight while the block sums the clip-norm
@@ -94,7 +97,15 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
     p4[i] = make_float4(px[0], px[1], px[2], px[3]);
     v4[i] = make_float4(vx[0], vx[1], vx[2], vx[3]);
     if (centered) m4[i] = make_float4(mx[0], mx[1], mx[2], mx[3]);
-    pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
+    if (pbl != nullptr) {
+      uint32_t h01, l01, h23, l23;
+      split_pk_bf16_h(px[0], px[1], h01, l01);
+      split_pk_bf16_h(px[2], px[3], h23, l23);
+      pb4[i] = make_uint2(h01, h23);
+      pbl4[i] = make_uint2(l01, l23);
+    } else {
+      pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
+    }
     gg = gn; pp = pn; vv = vn; mm = mn;
   }
   for (int64_t i = n4 * 4 + (int64_t)bid * blockDim.x + threadIdx.x; i < n; i += (int64_t)nblk * blockDim.x) {
@@ -109,5 +120,6 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
     float pp = p[i] - lr * gg / (sqrtf(fmaxf(var, 0.f)) + eps);
     p[i] = pp;
     pb[i] = f32_to_bf16(pp);
+    if (pbl != nullptr) pbl[i] = f32_to_bf16(pp - bf16_to_f32(pb[i]));
   }
 }

@@ -405,7 +405,8 @@ __global__ void __launch_bounds__(192) ddqn_head_prio_kernel(
     const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
-    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, PrioArgs pr) {
+    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, PrioArgs pr,
+    HeadLo lo) {
   // wave 0 issues the write-back's loads (the leaf index, the dedupe scan of the
   // later samples, the leaf and its generations) before the head body, so their
   // latency hides under the head math instead of trailing it
@@ -430,7 +431,7 @@ __global__ void __launch_bounds__(192) ddqn_head_prio_kernel(
   }
   float ad;
   if (!ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs, loss,
-                          q_out, dH, dhead, zero_ptr, zero_n, &ad))
+                          q_out, dH, dhead, zero_ptr, zero_n, &ad, lo))
     return;
   if (b == 0 && lane == 0 && pr.ctr_to_bump != nullptr) pr.ctr_to_bump[0] += 1;
   if (__ballot(dup) != 0ull || lane != 0 || !live) return;
@@ -448,9 +449,11 @@ __global__ void __launch_bounds__(192) ddqn_head_prio_kernel(
 }
 
 // Single-block priority write-back (tree_update mode 1 with dedupe) for n <= 1024
-// leaves, any block size: items tid, tid + blockDim, ...; the LDS hash keeps the
-// last occurrence of a duplicated leaf; every item's delta goes through the
-// block-aggregated tree_block_update (the root sees ONE atomic per item round).
+// leaves and n <= TU_MAXR * blockDim (the launchers check both): items tid,
+// tid + blockDim, ...; the LDS hash keeps the last occurrence of a duplicated leaf;
+// every item's delta goes through the block-aggregated tree_block_update (the root
+// sees ONE atomic per item round).
+#define TU_MAXR 4
 struct TreeUpdArgs {
   TreeDesc t;
   const int64_t* idx;
@@ -475,9 +478,11 @@ __device__ __forceinline__ void tree_update_block(const TreeUpdArgs& a) {
     hval[j] = -1;
   }
   __syncthreads();
-  int64_t s[2];
-  int h[2];
-  for (int r = 0; r < R; ++r) {
+  int64_t s[TU_MAXR];
+  int h[TU_MAXR];
+#pragma unroll
+  for (int r = 0; r < TU_MAXR; ++r) {
+    if (r >= R) break;
     const int i = threadIdx.x + r * nt;
     s[r] = 0;
     h[r] = -1;
@@ -499,7 +504,9 @@ __device__ __forceinline__ void tree_update_block(const TreeUpdArgs& a) {
     }
   }
   __syncthreads();
-  for (int r = 0; r < R; ++r) {
+#pragma unroll
+  for (int r = 0; r < TU_MAXR; ++r) {
+    if (r >= R) break;
     const int i = threadIdx.x + r * nt;
     bool act = h[r] >= 0 && hval[h[r]] == i;   // a later write to the same leaf wins
     float v = 0.f;
@@ -529,9 +536,11 @@ __global__ void __launch_bounds__(512) head_wgrad_prio_kernel(HeadWgArgs hw, Tre
 // (all three only need the head kernel's outputs).  Block 0: the single-block tree
 // update (the latency-bound long pole, dispatched first); blocks 1..nhw: head
 // wgrad (4 waves each); from blk0 (a multiple of 8, so the XCD-contiguous tile
-// order of the GEMM part is preserved): the fc wgrad GEMM tiles (CT=4, NT=1, one
-// split, as launch_wgrad picks for the 1024 x 3136 fc).  The fc wgrad takes one
-// block per CU (96 KB LDS) and leaves ~60 CUs idle; the other two fill them.
+// order of the GEMM part is preserved): the fc wgrad GEMM tiles (one split, the
+// shape launch_wgrad picks for the 1024 x 3136 fc: CT=4, NT=1 in bf16; CT=2, NT=1
+// in split mode, whose doubled images leave room for the tree update's LDS).  The
+// fc wgrad takes one block per CU and leaves CUs idle; the other two fill them.
+template <int SP>
 __global__ void __launch_bounds__(256) fc_wgrad_head_prio_kernel(WgradDesc d, int gx, int gy, HeadWgArgs hw,
                                                                  TreeUpdArgs tu, int nhw, int blk0) {
   const int b = blockIdx.x;
@@ -541,7 +550,7 @@ __global__ void __launch_bounds__(256) fc_wgrad_head_prio_kernel(WgradDesc d, in
     const int nch = hw.HS / 64, q = b - 1;
     head_wgrad_body(hw, q / nch, q - (q / nch) * nch);
   } else if (b >= blk0) {
-    igemm_wgrad_body<0, 1, 1, 4, 1>(d, b - blk0, gx, gy, 1);
+    igemm_wgrad_body<0, 1, 1, SP ? 2 : 4, 1, SP>(d, b - blk0, gx, gy, 1);
   }
 }
 
@@ -663,15 +672,16 @@ APEX_EXPORT int apex_ddqn_head_prio(const bf16_t* Hon, const bf16_t* Htg, HeadPa
                                     float* loss, float* q_out, bf16_t* dH, float* dhead, float* zero_ptr,
                                     int zero_n, int hidden, TreeDesc t, const int64_t* idx,
                                     const int32_t* gen_expect, const int32_t* gen, float alpha, float eps,
-                                    uint64_t* ctr_to_bump, hipStream_t st) {
+                                    uint64_t* ctr_to_bump, HeadLo lo, hipStream_t st) {
   if (A < 1 || A > HEAD_MAXA || B < 1 || idx == nullptr) return (int)hipErrorInvalidValue;
+  if (lo.Hon != nullptr && (lo.Htg == nullptr || lo.dH == nullptr)) return (int)hipErrorInvalidValue;
   const PrioArgs pr{t, idx, gen_expect, gen, ctr_to_bump, alpha, eps, B};
   if (hidden == 512)
     ddqn_head_prio_kernel<512><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
-                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr);
+                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr, lo);
   else if (hidden == 256)
     ddqn_head_prio_kernel<256><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
-                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr);
+                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr, lo);
   else
     return (int)hipErrorInvalidValue;
   APEX_CHECK_LAUNCH();
@@ -684,9 +694,9 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     uint64_t seed, const uint64_t* ctr, float beta, const float* ratio_min_global,
                                     int64_t* out_idx, float* out_w, int32_t* out_gen, int32_t* out_obs,
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
-                                    int32_t* out_nxt2, hipStream_t st) {
+                                    int32_t* out_nxt2, bf16_t* pb_lo, hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
-  if (((uintptr_t)pb & 7) || B < 1) return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)pb | (uintptr_t)pb_lo) & 7) || B < 1) return (int)hipErrorInvalidValue;
   // block size APEX_OPT_THREADS (256 / 512 / 1024), grid capped at APEX_OPT_BLOCKS:
   // every block first sums the ~2.6 K clip-norm partials, so fewer, fatter blocks
   // cut those L2 reads (measured 512 x 512: 3543-3576 steps/s vs 3497-3520 at
@@ -704,7 +714,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   int nb = (int)((n / 4 + nt - 1) / nt);
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
   const int nsb = blocks_for(B, nt / 64);
-  const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out};
+  const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo};
   const SampleArgs sa{t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt,
                       out_act, out_rew, out_gam, out_nxt2};
   if (nt == 1024) rmsprop_sample_kernel<1024><<<nb + nsb, 1024, 0, st>>>(ra, sa, nsb);
@@ -716,11 +726,14 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
 APEX_EXPORT int apex_head_wgrad_prio(const bf16_t* Hon, const float* dhead, int B, int A, float* gwv, float* gbv,
                                      float* gwa, float* gba, int hidden, TreeDesc t, const int64_t* idx,
                                      const float* td, const int32_t* gen_expect, const int32_t* gen,
-                                     float alpha, float eps, uint64_t* ctr_to_bump, hipStream_t st) {
-  if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || idx == nullptr) return (int)hipErrorInvalidValue;
+                                     float alpha, float eps, uint64_t* ctr_to_bump, const bf16_t* Hon_lo,
+                                     hipStream_t st) {
+  // the single-block tree update holds TU_MAXR items per thread
+  if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || B > TU_MAXR * 512 || idx == nullptr)
+    return (int)hipErrorInvalidValue;
   const int nblk = 1 + (A + 1) * (hidden / 64);
   head_wgrad_prio_kernel<<<nblk, 512, 0, st>>>(
-      HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden},
+      HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden, Hon_lo},
       TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)});
   APEX_CHECK_LAUNCH();
 }
@@ -732,18 +745,24 @@ APEX_EXPORT int apex_fc_wgrad_head_prio(WgradDesc d, const bf16_t* Hon, const fl
                                         float* gwv, float* gbv, float* gwa, float* gba, int hidden, TreeDesc t,
                                         const int64_t* idx, const float* td, const int32_t* gen_expect,
                                         const int32_t* gen, float alpha, float eps, uint64_t* ctr_to_bump,
-                                        hipStream_t st) {
-  if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || idx == nullptr) return (int)hipErrorInvalidValue;
+                                        const bf16_t* Hon_lo, hipStream_t st) {
+  // 256-thread blocks: the single-block tree update holds TU_MAXR items per thread
+  if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || B > TU_MAXR * 256 || idx == nullptr)
+    return (int)hipErrorInvalidValue;
   if (d.mode != 0 || (d.Kc & 63) || (d.Co & 63) || d.rows_per_split < d.Mred) return (int)hipErrorInvalidValue;
   if ((int64_t)d.Mred * d.ldd * 2 >= 0x7ffffff0LL || (int64_t)d.Mred * d.ldx * 2 >= 0x7ffffff0LL)
     return (int)hipErrorInvalidValue;
+  const bool split = d.dy_lo != nullptr;
+  if (split && (d.x_lo == nullptr || Hon_lo == nullptr)) return (int)hipErrorInvalidValue;
   const int kt = d.Kc / 64, ct = d.Co / 64;
-  if (wgrad_shape(kt, ct, d.Kc, d.Co) != 2) return (int)hipErrorInvalidValue;   // {CT,NT} = {4,1}
-  const int gx = kt, gy = ct / 4;
+  // the compiled shape: {CT,NT} = {4,1} (index 2) in bf16, {2,1} (index 6) in split mode
+  if (wgrad_shape(kt, ct, d.Kc, d.Co, split ? 1 : 0) != (split ? 6 : 2)) return (int)hipErrorInvalidValue;
+  const int gx = kt, gy = ct / (split ? 2 : 4);
   const int nhw = (A + 1) * (hidden / 64);
   const int blk0 = (1 + nhw + 7) & ~7;
-  fc_wgrad_head_prio_kernel<<<blk0 + gx * gy, 256, 0, st>>>(
-      d, gx, gy, HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden},
-      TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)}, nhw, blk0);
+  const HeadWgArgs hw{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden, Hon_lo};
+  const TreeUpdArgs tu{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)};
+  if (split) fc_wgrad_head_prio_kernel<1><<<blk0 + gx * gy, 256, 0, st>>>(d, gx, gy, hw, tu, nhw, blk0);
+  else fc_wgrad_head_prio_kernel<0><<<blk0 + gx * gy, 256, 0, st>>>(d, gx, gy, hw, tu, nhw, blk0);
   APEX_CHECK_LAUNCH();
 }

@@ -9,7 +9,10 @@ other image network runs here with the same GPU-first structure:
   one flat fp32 buffer each, so the clip + centered RMSprop step is the fused
   HIP optimizer kernel over the whole model (``csrc/optimizer.hip``) and the DP
   all-reduce is one flat RCCL call;
-* forward/backward run in bf16 autocast (MIOpen / hipBLASLt convs and GEMMs);
+* forward/backward run in fp32 (``Runtime.dtype = fp32``, the reference's precision) or
+  bf16 autocast (``bf16``) on MIOpen / hipBLASLt convs and GEMMs -- the vendor-library
+  baseline the hand-written NatureCNN learner is measured against (``bench.py
+  --learner graph``);
 * the whole update -- sample, gather, 3 forwards, DDQN Huber*IS loss, backward,
   optimizer, priority write-back -- is captured in ONE HIP graph (two segments
   around the gradient all-reduce with data parallelism).
@@ -79,6 +82,9 @@ class GraphLearner:
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
         self.ops = HipBackend(native_conv=False) if (d.type == "cuda" and self.rt.use_hip_kernels) else \
             TorchBackend(torch.float32)
+        # fp32: plain fp32 library kernels (gfx950 has no xf32 / TF32 path); bf16: autocast
+        self.amp_dtype = torch.bfloat16 if (d.type == "cuda" and self.rt.dtype == "bf16") else None
+        self.graph_captures = 0
         self.S = replay.alloc_sample_buffers(self.B)
         self.td_abs = torch.zeros(self.B, dtype=torch.float32, device=d)
         self.loss_b = torch.zeros(1, dtype=torch.float32, device=d)
@@ -107,8 +113,8 @@ class GraphLearner:
         nxt = self.replay.gather_frames(S["nxt"])
         self.g32.zero_()
         # cache_enabled=False: autocast's weight-cast cache must not outlive a graph capture
-        amp = torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False) \
-            if self.device.type == "cuda" else torch.autocast(device_type="cpu", enabled=False)
+        amp = torch.autocast(device_type="cuda", dtype=self.amp_dtype, cache_enabled=False) \
+            if self.amp_dtype is not None else torch.autocast(device_type=self.device.type, enabled=False)
         with amp:
             q_t = self.Q(obs)[2]
             with torch.no_grad():
@@ -155,6 +161,13 @@ class GraphLearner:
             with torch.cuda.graph(g):
                 seg()
             self._graphs.append(g)
+            self.graph_captures += 1
+
+    def prepare_graphs(self, multi: bool = True) -> int:
+        """Capture the step's graphs now (outside any timed region)."""
+        if self.rt.use_graphs and self.device.type == "cuda" and self._graphs is None:
+            self._capture()
+        return self.graph_captures
 
     def step(self) -> None:
         graphs = self.rt.use_graphs and self.device.type == "cuda"
@@ -213,8 +226,8 @@ class GraphLearner:
 
     # ------------------------------------------------------------------ io
     def actor_forward(self, net: torch.nn.Module, frames: torch.Tensor) -> torch.Tensor:
-        amp = torch.autocast(device_type="cuda", dtype=torch.bfloat16) if self.device.type == "cuda" \
-            else torch.autocast(device_type="cpu", enabled=False)
+        amp = torch.autocast(device_type="cuda", dtype=self.amp_dtype) if self.amp_dtype is not None \
+            else torch.autocast(device_type=self.device.type, enabled=False)
         with torch.no_grad(), amp:
             return net(frames)[2].float()
 

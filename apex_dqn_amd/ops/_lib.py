@@ -41,6 +41,11 @@ class HeadParams(ctypes.Structure):
     _fields_ = [("wv", c_p), ("bv", c_p), ("wa", c_p), ("ba", c_p)]
 
 
+class HeadLo(ctypes.Structure):
+    """Split-mode lo planes of the head's activations / gradient (``HeadLo``, csrc/head_common.h)."""
+    _fields_ = [("Hon", c_p), ("Htg", c_p), ("dH", c_p)]
+
+
 class ConvDesc(ctypes.Structure):
     """Implicit-GEMM forward/dgrad problem (mirrors ``ConvDesc`` in csrc/conv_mfma.hip)."""
     _fields_ = [("x", c_p), ("frame_slots", c_p), ("w", c_p), ("bias", c_p), ("y", c_p), ("mask", c_p),
@@ -52,7 +57,7 @@ class ConvDesc(ctypes.Structure):
                 ("K", c_i), ("in_scale", c_f), ("w_cls_stride", c_i64),
                 ("w2", c_p), ("bias2", c_p), ("m_switch", c_i),
                 ("bt", c_i), ("ldb", c_i), ("koff", c_i * 16), ("tile_hint", c_i), ("order_hint", c_i),
-                ("part", c_p), ("ksplit", c_i), ("kgroups", c_i)]
+                ("x_lo", c_p), ("w_lo", c_p), ("w2_lo", c_p), ("y_lo", c_p)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -62,7 +67,8 @@ class WgradDesc(ctypes.Structure):
                 ("OH", c_i), ("OW", c_i), ("KH", c_i), ("KW", c_i),
                 ("stride", c_i), ("pad_h", c_i), ("pad_w", c_i), ("mode", c_i),
                 ("Co", c_i), ("Kc", c_i), ("ldd", c_i), ("ldx", c_i),
-                ("rows_per_split", c_i), ("Mred", c_i), ("norm_part", c_p), ("norm_slot0", c_i), ("pad0", c_i)]
+                ("rows_per_split", c_i), ("Mred", c_i), ("norm_part", c_p), ("norm_slot0", c_i), ("pad0", c_i),
+                ("dy_lo", c_p), ("x_lo", c_p)]
 
 
 class RedJob(ctypes.Structure):
@@ -80,14 +86,14 @@ class FinalizeDesc(ctypes.Structure):
 class Conv1WgDesc(ctypes.Structure):
     """Image-resident conv1 weight gradient (mirrors ``Conv1WgDesc`` in csrc/conv1_wgrad.hip)."""
     _fields_ = [("ring", c_p), ("slots", c_p), ("dy", c_p), ("slab", c_p), ("bias_slab", c_p), ("zero16", c_p),
-                ("N", c_i), ("C", c_i)]
+                ("N", c_i), ("C", c_i), ("dy_lo", c_p)]
 
 
 class Conv1S2DDesc(ctypes.Structure):
     """conv1 on the space-to-depth ring (mirrors ``Conv1S2DDesc`` in csrc/conv1_s2d.hip)."""
     _fields_ = [("ring", c_p), ("slots", c_p), ("w", c_p), ("w2", c_p), ("bias", c_p), ("bias2", c_p),
                 ("y", c_p), ("zero16", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("m_switch", c_i),
-                ("in_scale", c_f), ("probe", c_p)]
+                ("in_scale", c_f), ("probe", c_p), ("w32", c_p), ("w2_32", c_p), ("y_lo", c_p)]
 
 
 _SIGS = {
@@ -103,23 +109,25 @@ _SIGS = {
     "apex_debug_bounds_enabled": ([], c_i),
     "apex_debug_errors": ([c_p, c_p, c_i], c_i),
     "apex_grad_sqnorm_partials": ([c_p, c_i64, c_p, c_p], c_i),
-    "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p], c_i),
-    "apex_cast_bf16": ([c_p, c_p, c_i64, c_p], c_i),
-    "apex_rmsprop_step_np": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p, c_p], c_i),
+    "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p], c_i),
+    "apex_cast_bf16": ([c_p, c_p, c_i64, c_p, c_p], c_i),
+    "apex_rmsprop_step_np": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p],
+                             c_i),
     "apex_grad_finalize": ([FinalizeDesc, c_p], c_i),
     "apex_norm_total": ([c_p, c_i, c_p, c_p], c_i),
     "apex_ddqn_head": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
-                        c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
+                        c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, c_p], c_i),
     "apex_ddqn_head_prio": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
-                             c_p, c_p, c_p, c_p, c_p, c_i, c_i, TreeDesc, c_p, c_p, c_p, c_f, c_f, c_p, c_p], c_i),
+                             c_p, c_p, c_p, c_p, c_p, c_i, c_i, TreeDesc, c_p, c_p, c_p, c_f, c_f, c_p, HeadLo, c_p],
+                            c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p], c_i),
+                             c_p, c_p, c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
-                              c_p, c_p], c_i),
+                              c_p, c_p, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,
-                                 c_p, c_f, c_f, c_p, c_p], c_i),
-    "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p], c_i),
+                                 c_p, c_f, c_f, c_p, c_p, c_p], c_i),
+    "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p], c_i),
     "apex_actor_head": ([c_p, HeadParams, c_i, c_i, c_p, c_u64, c_p, c_p, c_p, c_i, c_p], c_i),
     "apex_conv1_s2d_fwd": ([Conv1S2DDesc, c_i, c_p], c_i),
     "apex_conv1_wgrad_img": ([Conv1WgDesc, c_i, c_p], c_i),
@@ -202,6 +210,13 @@ def stream_ptr(device: Optional[torch.device] = None) -> int:
 
 def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
+
+
+def head_lo(Hon_lo=None, Htg_lo=None, dH_lo=None) -> HeadLo:
+    """Split-mode lo planes for the head kernels (all None in bf16 mode)."""
+    lo = HeadLo()
+    lo.Hon, lo.Htg, lo.dH = ptr(Hon_lo), ptr(Htg_lo), ptr(dH_lo)
+    return lo
 
 
 def check(rc: int, what: str) -> None:

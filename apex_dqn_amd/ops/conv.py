@@ -62,7 +62,17 @@ def _conv_desc(**kw) -> "_lib.ConvDesc":
     d.tile_hint, d.order_hint = _HINTS.get("tile", 0), _HINTS.get("order", 0)
     for i, v in enumerate(kw.get("koff", ())):
         d.koff[i] = v
+    # fp32-accurate ("split") mode: lo planes of A, B (both weight sets) and the output
+    d.x_lo, d.w_lo, d.w2_lo, d.y_lo = kw.get("x_lo"), kw.get("w_lo"), kw.get("w2_lo"), kw.get("y_lo")
     return d
+
+
+def _lo(x_lo=None, w_lo=None, w2_lo=None, out_lo=None) -> dict:
+    """Descriptor fields of split mode (every tensor given, or none)."""
+    if x_lo is None:
+        return {}
+    assert w_lo is not None and out_lo is not None
+    return dict(x_lo=x_lo.data_ptr(), w_lo=w_lo.data_ptr(), w2_lo=_lib.ptr(w2_lo), y_lo=out_lo.data_ptr())
 
 
 def _second(w2, b2, rows_first, per_row):
@@ -95,8 +105,11 @@ def pack_w1_s2d(lib, ws: "Workspace", w1: torch.Tensor, tag: str) -> torch.Tenso
 
 def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
                   b1: torch.Tensor, scale: float, out: torch.Tensor, w2=None, b2=None, rows_first: int = 0,
-                  grid: int = 0, probe: Optional[torch.Tensor] = None) -> None:
-    """conv1 on the space-to-depth replay ring (persistent LDS-DMA kernel, csrc/conv1_s2d.hip)."""
+                  grid: int = 0, probe: Optional[torch.Tensor] = None, w32: Optional[torch.Tensor] = None,
+                  w2_32: Optional[torch.Tensor] = None, out_lo: Optional[torch.Tensor] = None) -> None:
+    """conv1 on the space-to-depth replay ring (persistent LDS-DMA kernel, csrc/conv1_s2d.hip).
+    Split mode (``out_lo`` given): the fp32 master weights ``w32`` / ``w2_32`` (OIHW) are
+    read and the output leaves as hi (``out``) / lo (``out_lo``) bf16 planes."""
     N, C = slots.shape
     assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
     d = _lib.Conv1S2DDesc()
@@ -116,6 +129,9 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
     d.N, d.C, d.in_scale = N, C, float(scale)
     if probe is not None:
         d.probe = probe.data_ptr()
+    if out_lo is not None:
+        assert w32 is not None and w32.dtype == torch.float32 and (w2 is None or w2_32 is not None)
+        d.w32, d.w2_32, d.y_lo = w32.data_ptr(), _lib.ptr(w2_32), out_lo.data_ptr()
     _lib.check(lib.apex_conv1_s2d_fwd(d, int(grid), _lib.stream_ptr()), "conv1_s2d_fwd")
 
 
@@ -142,59 +158,50 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
 
 
 def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int, out: torch.Tensor,
-             w2=None, b2=None, rows_first: int = 0) -> None:
-    """NHWC conv + bias + ReLU with OHWI weights (conv2 / conv3)."""
+             w2=None, b2=None, rows_first: int = 0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None) -> None:
+    """NHWC conv + bias + ReLU with OHWI weights (conv2 / conv3).  Split mode
+    (``x_lo`` ... ``out_lo``): fp32-accurate operands as hi + lo bf16 planes."""
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     OH, OW = out.shape[1], out.shape[2]
-    if CONV2_IMG and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
+    split = x_lo is not None
+    if CONV2_IMG and not split and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
             hasattr(lib, "apex_conv2_img_fwd"):
         conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first)
         return
     if not _split_ok(w2, rows_first, OH * OW):   # batch not tile-aligned: one launch per weight set
-        conv_fwd(lib, x[:rows_first], w, b, stride, out[:rows_first])
-        conv_fwd(lib, x[rows_first:], w2, b2, stride, out[rows_first:])
+        r = rows_first
+        conv_fwd(lib, x[:r], w, b, stride, out[:r], x_lo=None if not split else x_lo[:r], w_lo=w_lo,
+                 out_lo=None if not split else out_lo[:r])
+        conv_fwd(lib, x[r:], w2, b2, stride, out[r:], x_lo=None if not split else x_lo[r:], w_lo=w2_lo,
+                 out_lo=None if not split else out_lo[r:])
         return
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=b.data_ptr(), y=out.data_ptr(), N=N, H=H, W=W,
                    Cin=Cin, OH=OH, OW=OW, Cout=Cout, KH=KH, KW=KW, stride=stride, mode=1, relu=1,
-                   K=KH * KW * Cin, **_second(w2, b2, rows_first, OH * OW))
+                   K=KH * KW * Cin, **_second(w2, b2, rows_first, OH * OW), **_lo(x_lo, w_lo, w2_lo, out_lo))
     _launch_fwd(lib, d)
-
-
-# split-K of the dense forward GEMM (fc): the 1536 x 1024 output of the NatureCNN
-# learner is only 192 128x64 tiles for 256 CUs; splitting its K = 3136 fills the
-# chip, and one elementwise pass sums the fp32 partials + bias + ReLU (APEX_FC_KSPLIT)
-DENSE_KSPLIT = int(_os.environ.get("APEX_FC_KSPLIT", "0"))   # 0 = auto
-# fc forward: two 4-wave K groups per 512-thread block (csrc/conv_mfma.hip igemm_fwd KG)
-DENSE_KGROUPS = int(_os.environ.get("APEX_FC_KGROUPS", "1"))
-
-
-def _dense_ksplit(M: int, Nc: int, K: int) -> int:
-    # auto = 1: measured on the learner step (B=512), split 2/3/4 did not beat the
-    # unsplit 192-tile launch (3314 / 3320 / 3293 / 3307 steps/s) -- kept as an option
-    return DENSE_KSPLIT or 1
 
 
 def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], out: torch.Tensor,
               relu: bool = True, mask: Optional[torch.Tensor] = None, w2=None, b2=None,
-              rows_first: int = 0, ws: Optional["Workspace"] = None) -> None:
-    """out[M,N] = act(x[M,K] @ w[N,K]^T + b)  (or * (mask > 0))."""
+              rows_first: int = 0, ws: Optional["Workspace"] = None, x_lo=None, w_lo=None, w2_lo=None,
+              out_lo=None) -> None:
+    """out[M,N] = act(x[M,K] @ w[N,K]^T + b)  (or * (mask > 0)); split mode with the lo planes."""
     M, K = x.shape
     Nc = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, Nc)
     if not _split_ok(w2, rows_first, 1):         # batch not tile-aligned: one launch per weight set
-        m1, m2 = (None, None) if mask is None else (mask[:rows_first], mask[rows_first:])
-        dense_fwd(lib, x[:rows_first], w, b, out[:rows_first], relu, m1, ws=ws)
-        dense_fwd(lib, x[rows_first:], w2, b2, out[rows_first:], relu, m2, ws=ws)
+        r = rows_first
+        m1, m2 = (None, None) if mask is None else (mask[:r], mask[r:])
+        sp = x_lo is not None
+        dense_fwd(lib, x[:r], w, b, out[:r], relu, m1, ws=ws, x_lo=x_lo[:r] if sp else None, w_lo=w_lo,
+                  out_lo=out_lo[:r] if sp else None)
+        dense_fwd(lib, x[r:], w2, b2, out[r:], relu, m2, ws=ws, x_lo=x_lo[r:] if sp else None, w_lo=w2_lo,
+                  out_lo=out_lo[r:] if sp else None)
         return
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), mask=_lib.ptr(mask),
                    N=M, Cin=K, Cout=Nc, mode=0, relu=relu and mask is None, K=K,
-                   **_second(w2, b2, rows_first, 1))
-    ks = _dense_ksplit(M, Nc, K) if (ws is not None and mask is None) else 1
-    if ks > 1:
-        part = ws.get(("dense_part", M, Nc), ks * M * Nc, x.device)
-        d.part, d.ksplit = part.data_ptr(), ks
-    d.kgroups = DENSE_KGROUPS
+                   **_second(w2, b2, rows_first, 1), **_lo(x_lo, w_lo, w2_lo, out_lo))
     _launch_fwd(lib, d)
 
 
@@ -206,14 +213,15 @@ _KOFF2 = tuple(((p + 2 * (1 - a)) * 4 + (q + 2 * (1 - b))) * 64
                for p in range(2) for q in range(2) for a in range(2) for b in range(2))
 
 
-def dense_dgrad(lib, dh: torch.Tensor, w: torch.Tensor, out: torch.Tensor, mask: torch.Tensor) -> None:
+def dense_dgrad(lib, dh: torch.Tensor, w: torch.Tensor, out: torch.Tensor, mask: torch.Tensor, dh_lo=None,
+                w_lo=None, out_lo=None) -> None:
     """out[M,K] = (dh[M,N] @ w[N,K]) * (mask > 0): the B operand is read K-major
     straight from the natural [N][K] weight (no transposed copy)."""
     M, Nn = dh.shape
     K = w.shape[1]
     assert w.shape[0] == Nn and out.shape == (M, K)
     d = _conv_desc(x=dh.data_ptr(), w=w.data_ptr(), y=out.data_ptr(), mask=_lib.ptr(mask), N=M, Cin=Nn,
-                   Cout=K, mode=0, K=Nn, bt=2, ldb=K)
+                   Cout=K, mode=0, K=Nn, bt=2, ldb=K, **_lo(dh_lo, w_lo, None, out_lo))
     _launch_fwd(lib, d)
 
 
@@ -234,17 +242,18 @@ def conv3_dgrad_img(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor,
     _lib.check(lib.apex_conv3_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv3_dgrad_img")
 
 
-def conv3_dgrad(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
+def conv3_dgrad(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out: torch.Tensor, dy_lo=None,
+                w_lo=None, out_lo=None) -> None:
     """dX2 (9x9) from dY3 (7x7): full correlation with the flipped 3x3 weights, read
     K-major from the OHWI weight (co rows, ci columns)."""
     N = dy.shape[0]
     assert w3.shape == (64, 3, 3, 64)
-    if CONV3_DGRAD_IMG and hasattr(lib, "apex_conv3_dgrad_img"):
+    if CONV3_DGRAD_IMG and dy_lo is None and hasattr(lib, "apex_conv3_dgrad_img"):
         conv3_dgrad_img(lib, dy, w3, mask, out)
         return
     d = _conv_desc(x=dy.data_ptr(), w=w3.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=7, W=7,
                    Cin=64, OH=9, OW=9, Cout=64, KH=3, KW=3, stride=1, pad=2, mode=1, K=576,
-                   bt=1, ldb=576, koff=_KOFF3)
+                   bt=1, ldb=576, koff=_KOFF3, **_lo(dy_lo, w_lo, None, out_lo))
     _launch_fwd(lib, d)
 
 
@@ -265,18 +274,19 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 
-def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor) -> None:
+def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor, dy_lo=None,
+                w_lo=None, out_lo=None) -> None:
     """dX1 (20x20) from dY2 (9x9), 4x4 stride 2: four stride-parity classes, each a
     2x2 stride-1 correlation (pad 1) writing every other output pixel; weights read
     K-major from the OHWI tensor per class."""
     N = dy.shape[0]
     assert w2.shape == (64, 4, 4, 64)
-    if CONV2_DGRAD_IMG and hasattr(lib, "apex_conv2_dgrad_img"):
+    if CONV2_DGRAD_IMG and dy_lo is None and hasattr(lib, "apex_conv2_dgrad_img"):
         conv2_dgrad_img(lib, dy, w2, mask, out)
         return
     d = _conv_desc(x=dy.data_ptr(), w=w2.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
                    Cin=64, OH=10, OW=10, Cout=64, KH=2, KW=2, stride=1, pad=1, mode=1, K=256, ncls=4,
-                   ostride=2, OHfull=20, OWfull=20, bt=1, ldb=1024, koff=_KOFF2)
+                   ostride=2, OHfull=20, OWfull=20, bt=1, ldb=1024, koff=_KOFF2, **_lo(dy_lo, w_lo, None, out_lo))
     _launch_fwd(lib, d)
 
 
@@ -290,6 +300,7 @@ def _wg_desc(**kw) -> "_lib.WgradDesc":
     d.Co, d.Kc, d.ldd, d.ldx = kw["Co"], kw["Kc"], kw["ldd"], kw.get("ldx", 0)
     d.rows_per_split, d.Mred = kw["rows_per_split"], kw["Mred"]
     d.norm_part, d.norm_slot0 = kw.get("norm_part"), kw.get("norm_slot0", 0)
+    d.dy_lo, d.x_lo = kw.get("dy_lo"), kw.get("x_lo")    # split mode (x_lo null for the exact frames)
     return d
 
 
@@ -306,7 +317,8 @@ def _splits(Mred: int, target_rows: int, max_rows: int) -> Tuple[int, int]:
 
 
 def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, stride: int,
-               dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 0, jobs: Optional[list] = None) -> None:
+               dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 0, jobs: Optional[list] = None,
+               dy_lo=None, x_lo=None) -> None:
     """dW (OHWI, fp32) and db for an NHWC conv with 64 output channels.  With
     ``jobs``, the split-K reduction is appended there for ``finalize_grads``.
     ``target_rows``: reduction rows per split-K block (0 = tuned default: fewer
@@ -325,7 +337,7 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     bslab = ws.get(("wgb", Co, Kc), nsplit * Co, dy.device)
     d = _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=slab.data_ptr(), bias_slab=bslab.data_ptr(), N=N,
                  H=H, W=W, Cin=Cin, OH=OH, OW=OW, KH=KH, KW=KH, stride=stride, mode=1, Co=Co, Kc=Kc, ldd=Co,
-                 rows_per_split=rows, Mred=Mred)
+                 rows_per_split=rows, Mred=Mred, dy_lo=_lib.ptr(dy_lo), x_lo=_lib.ptr(x_lo))
     if jobs is not None:   # reduction deferred to one grad_finalize launch
         _lib.check(lib.apex_conv_wgrad(d, None, None, nsplit, 1.0, _lib.stream_ptr()), "conv_wgrad")
         jobs.append(dict(slab=slab, bslab=bslab, out=dw_out, bout=db_out, n=Co * Kc, nsplit=nsplit, nb=Co,
@@ -337,10 +349,11 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
 
 def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
                      scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, grid: int = 0,
-                     jobs: Optional[list] = None) -> None:
+                     jobs: Optional[list] = None, dy_lo: Optional[torch.Tensor] = None) -> None:
     """dW1 (OIHW fp32, x ``scale``) and db1 from dY1 (N, 20, 20, 64) and the uint8 frame
     stacks addressed by ring slots: image-resident kernel (csrc/conv1_wgrad.hip), one
-    fp32 partial per workgroup, then the split-K reduce (s2d -> OIHW permuted store)."""
+    fp32 partial per workgroup, then the split-K reduce (s2d -> OIHW permuted store).
+    Split mode (``dy_lo``): dY hi + lo against the exact frames (two MFMAs per fragment)."""
     N, OH, OW, Co = dy.shape
     C = slots.shape[1]
     assert (OH, OW, Co) == (20, 20, 64) and slots.dtype == torch.int32 and dy.is_contiguous()
@@ -356,6 +369,7 @@ def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, s
     d.ring, d.slots, d.dy = ring.data_ptr(), slots.data_ptr(), dy.data_ptr()
     d.slab, d.bias_slab, d.zero16 = slab.data_ptr(), bslab.data_ptr(), zero.data_ptr()
     d.N, d.C = N, C
+    d.dy_lo = _lib.ptr(dy_lo)
     st = _lib.stream_ptr()
     _lib.check(lib.apex_conv1_wgrad_img(d, G, st), "conv1_wgrad_img")
     if jobs is not None:
@@ -367,8 +381,12 @@ def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, s
 
 
 def conv1_wgrad_ring_tiled(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, slots: torch.Tensor,
-                           scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 1024) -> None:
-    """The generic tiled wgrad kernel in its s2d-ring mode (kept as a cross-check)."""
+                           scale: float, dw_out: torch.Tensor, db_out: torch.Tensor, target_rows: int = 0,
+                           jobs: Optional[list] = None, dy_lo: Optional[torch.Tensor] = None) -> None:
+    """The generic tiled wgrad kernel in its s2d-ring mode: the split-mode conv1 weight
+    gradient (``dy_lo``) and a cross-check of the image-resident bf16 kernel."""
+    if target_rows <= 0:
+        target_rows = 800 if dy_lo is not None else 1024
     N, OH, OW, Co = dy.shape
     C = slots.shape[1]
     Kc = C * 64
@@ -378,18 +396,30 @@ def conv1_wgrad_ring_tiled(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Ten
     bslab = ws.get(("wg1b", Co), nsplit * Co, dy.device)
     d = _wg_desc(dy=dy.data_ptr(), x=ring.data_ptr(), frame_slots=slots.data_ptr(), slab=slab.data_ptr(),
                  bias_slab=bslab.data_ptr(), N=N, H=ring.shape[1], W=ring.shape[2], Cin=C, OH=OH, OW=OW,
-                 KH=8, KW=8, stride=4, mode=2, Co=Co, Kc=Kc, ldd=Co, rows_per_split=rows, Mred=Mred)
+                 KH=8, KW=8, stride=4, mode=2, Co=Co, Kc=Kc, ldd=Co, rows_per_split=rows, Mred=Mred,
+                 dy_lo=_lib.ptr(dy_lo))
+    if jobs is not None:   # reduction (s2d -> OIHW permuted store) deferred to grad_finalize
+        _lib.check(lib.apex_conv_wgrad(d, None, None, nsplit, 1.0, _lib.stream_ptr()), "conv1_wgrad")
+        jobs.append(dict(slab=slab, bslab=bslab, out=dw_out, bout=db_out, n=Co * Kc, nsplit=nsplit, nb=Co, s2dC=C,
+                         Kc=Kc, scale=float(scale)))
+        return
     # the slab reduce permutes the s2d K order back to OIHW while storing
     _lib.check(lib.apex_conv_wgrad(d, dw_out.data_ptr(), db_out.data_ptr(), nsplit, float(scale),
                                    _lib.stream_ptr()), "conv1_wgrad")
 
 
-def wgrad_blocks(Co: int, Kc: int) -> int:
-    """Workgroups of one split of igemm_wgrad (mirrors launch_wgrad's tile-shape choice)."""
+_WG_SHAPES = ((1, 4), (2, 2), (4, 1), (1, 3), (1, 1), (1, 2), (2, 1))
+
+
+def wgrad_blocks(Co: int, Kc: int, sp: int = 0) -> int:
+    """Workgroups of one split of igemm_wgrad (mirrors csrc/igemm_wgrad.h wgrad_shape:
+    ``sp`` 1 = split mode with both operands split, 2 = dY split / exact X)."""
     kt, ct = Kc // 64, Co // 64
     best, bc = (1, 1), None
-    for c, n in ((1, 4), (2, 2), (4, 1), (1, 3), (1, 1)):
+    for i, (c, n) in enumerate(_WG_SHAPES):
         if kt % n or ct % c:
+            continue
+        if (sp == 1 and c + n > 4) or (sp == 2 and 2 * c + n > 6) or (sp == 0 and i >= 5):
             continue
         cost = (ct // c) * Kc + (kt // n) * Co
         if bc is None or cost < bc:
@@ -398,40 +428,42 @@ def wgrad_blocks(Co: int, Kc: int) -> int:
 
 
 def _dense_wgrad_desc(dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor,
-                      norm: Optional[Tuple[torch.Tensor, int]] = None):
+                      norm: Optional[Tuple[torch.Tensor, int]] = None, dy_lo=None, x_lo=None):
     M, Nc = dy.shape
     K = x.shape[1]
     extra = {} if norm is None else dict(norm_part=norm[0].data_ptr(), norm_slot0=int(norm[1]))
     return _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=dw_out.data_ptr(), bias_slab=db_out.data_ptr(),
-                    mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M, **extra)
+                    mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M, dy_lo=_lib.ptr(dy_lo),
+                    x_lo=_lib.ptr(x_lo), **extra)
 
 
 def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor,
-                norm: Optional[Tuple[torch.Tensor, int]] = None) -> int:
+                norm: Optional[Tuple[torch.Tensor, int]] = None, dy_lo=None, x_lo=None) -> int:
     """dW[N,K] = dy[M,N]^T @ x[M,K] (fp32, written directly), db = sum_m dy.  With
     ``norm = (partials, slot0)`` the kernel also writes 4 squared-norm partials per
-    workgroup; returns the number of slots used."""
-    d = _dense_wgrad_desc(dy, x, dw_out, db_out, norm)
+    workgroup; returns the number of slots used.  Split mode: ``dy_lo`` and ``x_lo``."""
+    d = _dense_wgrad_desc(dy, x, dw_out, db_out, norm, dy_lo, x_lo)
     _lib.check(lib.apex_conv_wgrad(d, None, None, 1, 1.0, _lib.stream_ptr()), "dense_wgrad")
-    return 4 * wgrad_blocks(dy.shape[1], x.shape[1])
+    return 4 * wgrad_blocks(dy.shape[1], x.shape[1], 1 if dy_lo is not None else 0)
 
 
-def dense_wgrad_head_prio(lib, dy, x, dw_out, db_out, norm, Hon, dhead, g, replay, idx, gen, td) -> Optional[int]:
+def dense_wgrad_head_prio(lib, dy, x, dw_out, db_out, norm, Hon, dhead, g, replay, idx, gen, td, dy_lo=None,
+                          x_lo=None, Hon_lo=None) -> Optional[int]:
     """The fc weight gradient (as ``dense_wgrad``), the head weight gradient and the
     priority write-back in one launch (csrc/sumtree.hip fc_wgrad_head_prio_kernel).
     Returns the norm slots used, or None when the shape is not the fused kernel's
     (nothing launched: the caller runs the three ops separately)."""
-    d = _dense_wgrad_desc(dy, x, dw_out, db_out, norm)
+    d = _dense_wgrad_desc(dy, x, dw_out, db_out, norm, dy_lo, x_lo)
     B, A1 = dhead.shape
     rc = lib.apex_fc_wgrad_head_prio(d, Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(),
                                      g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(), g["wv"].numel(),
                                      replay.tree_desc(), idx.data_ptr(), td.data_ptr(), _lib.ptr(gen),
                                      replay.gen.data_ptr(), replay.alpha, replay.eps, replay.ctr.data_ptr(),
-                                     _lib.stream_ptr())
+                                     _lib.ptr(Hon_lo), _lib.stream_ptr())
     if rc == 1:          # hipErrorInvalidValue: not the compiled shape
         return None
     _lib.check(rc, "fc_wgrad_head_prio")
-    return 4 * wgrad_blocks(dy.shape[1], x.shape[1])
+    return 4 * wgrad_blocks(dy.shape[1], x.shape[1], 1 if dy_lo is not None else 0)
 
 
 def finalize_blocks(jobs: list, norm_range: Optional[torch.Tensor]) -> int:

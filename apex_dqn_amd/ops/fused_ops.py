@@ -6,6 +6,15 @@
 
 Both write into preallocated output buffers so a whole learner step can be
 captured in one HIP graph.
+
+fp32-accurate ("split") mode: every activation, gradient and bf16 weight copy
+comes as a hi plane (the usual tensor) plus a ``*_lo`` plane with
+``value = hi + lo`` (csrc/mfma_common.h ``split_pk_bf16``).  The HIP kernels run
+three bf16 MFMAs per fragment pair (hi.hi + lo.hi + hi.lo, fp32 accumulation); the
+torch backend emulates the mode by joining the planes into fp32, computing in
+fp32 and splitting the outputs again, so the learner's split plumbing runs (and is
+tested) on the CPU.  Without ``*_lo`` arguments every op is the plain bf16 / fp32
+op of before.
 """
 from __future__ import annotations
 
@@ -18,6 +27,18 @@ from . import conv as C
 from . import reference as R
 
 
+def join(hi: torch.Tensor, lo: Optional[torch.Tensor]) -> torch.Tensor:
+    """hi (+ lo) as fp32."""
+    return hi.float() if lo is None else hi.float() + lo.float()
+
+
+def split_into(v: torch.Tensor, hi: torch.Tensor, lo: Optional[torch.Tensor]) -> None:
+    """Write fp32 ``v`` as hi = round(v), lo = round(v - hi) (or just hi when lo is None)."""
+    hi.copy_(v.reshape(hi.shape))
+    if lo is not None:
+        lo.copy_((v.reshape(hi.shape).float() - hi.float()))
+
+
 class TorchBackend:
     name = "torch"
 
@@ -26,49 +47,64 @@ class TorchBackend:
 
     # ------------------------------------------------------------- forward
     def prepare(self, Pb) -> None:
-        """Per-step weight preparation (packed dgrad copies on the HIP path)."""
+        """Per-step weight preparation (nothing on either backend: the dgrad GEMMs read
+        the natural weight tensors)."""
 
-    def conv1_fwd(self, frames, w, b, scale, out):
-        out.copy_(R.conv1_fwd(frames, w, b, scale, self.dtype))
+    def conv1_fwd(self, frames, w, b, scale, out, out_lo=None):
+        dt = torch.float32 if out_lo is not None else self.dtype
+        split_into(R.conv1_fwd(frames, w, b, scale, dt), out, out_lo)
 
-    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0):
+    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0, w32=None,
+                       w2_32=None, out_lo=None):
         """conv1 on frame stacks addressed by replay-ring slots (N, C); rows >=
-        ``rows_first`` use the second weight set (w2, b2) when given."""
+        ``rows_first`` use the second weight set (w2, b2) when given.  Split mode reads
+        the fp32 master weights ``w32`` / ``w2_32``."""
         from ..replay.gpu_replay import from_s2d
         frames = frames_buf[:slots.shape[0]]
         n, c = slots.shape
         frames.copy_(from_s2d(ring[slots.long()].reshape(n * c, 84, 84)).reshape(n, c, 84, 84))
+        wa, wb = (w32, w2_32) if out_lo is not None else (w, w2)
         if w2 is None:
-            self.conv1_fwd(frames, w, b, scale, out)
+            self.conv1_fwd(frames, wa, b, scale, out, out_lo)
         else:
-            self.conv1_fwd(frames[:rows_first], w, b, scale, out[:rows_first])
-            self.conv1_fwd(frames[rows_first:], w2, b2, scale, out[rows_first:])
+            r = rows_first
+            self.conv1_fwd(frames[:r], wa, b, scale, out[:r], None if out_lo is None else out_lo[:r])
+            self.conv1_fwd(frames[r:], wb, b2, scale, out[r:], None if out_lo is None else out_lo[r:])
 
-    def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0):
+    def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
+                 out_lo=None):
+        dt = torch.float32 if x_lo is not None else self.dtype
+        xf = join(x, x_lo) if x_lo is not None else x
         if w2 is None:
-            out.copy_(R.conv_fwd(x, w, b, stride, self.dtype))
+            split_into(R.conv_fwd(xf, join(w, w_lo), b, stride, dt), out, out_lo)
         else:
-            out[:rows_first].copy_(R.conv_fwd(x[:rows_first], w, b, stride, self.dtype))
-            out[rows_first:].copy_(R.conv_fwd(x[rows_first:], w2, b2, stride, self.dtype))
+            r = rows_first
+            split_into(R.conv_fwd(xf[:r], join(w, w_lo), b, stride, dt), out[:r], None if out_lo is None else out_lo[:r])
+            split_into(R.conv_fwd(xf[r:], join(w2, w2_lo), b2, stride, dt), out[r:],
+                       None if out_lo is None else out_lo[r:])
 
-    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0):
+    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None):
+        dt = torch.float32 if x_lo is not None else self.dtype
         x = x.reshape(x.shape[0], -1)
+        xf = join(x, x_lo.reshape(x.shape)) if x_lo is not None else x
         if w2 is None:
-            out.copy_(R.fc_fwd(x, w, b, self.dtype))
+            split_into(R.fc_fwd(xf, join(w, w_lo), b, dt), out, out_lo)
         else:
-            out[:rows_first].copy_(R.fc_fwd(x[:rows_first], w, b, self.dtype))
-            out[rows_first:].copy_(R.fc_fwd(x[rows_first:], w2, b2, self.dtype))
+            r = rows_first
+            split_into(R.fc_fwd(xf[:r], join(w, w_lo), b, dt), out[:r], None if out_lo is None else out_lo[:r])
+            split_into(R.fc_fwd(xf[r:], join(w2, w2_lo), b2, dt), out[r:], None if out_lo is None else out_lo[r:])
 
     # ---------------------------------------------------------------- head
     def head(self, Hon, Htg, Pon: Dict[str, torch.Tensor], Ptg: Dict[str, torch.Tensor], act, rew, gam, isw,
              huber: bool, kappa: float, grad_scale: float, td_abs, loss, dH, dhead, q_out=None,
-             zero: Optional[torch.Tensor] = None, prio=None):
+             zero: Optional[torch.Tensor] = None, prio=None, lo=None):
         """``prio = (replay, idx, gen)``: also write the batch's priorities back
-        (the HIP backend fuses it into the head kernel)."""
+        (the HIP backend fuses it into the head kernel).  ``lo = (Hon_lo, Htg_lo,
+        dH_lo)`` in split mode."""
         B = act.shape[0]
         A = Pon["wa"].shape[0]
-        Hon = Hon.float()
-        Htg = Htg.float()
+        Hon = join(Hon, None if lo is None else lo[0])
+        Htg = join(Htg, None if lo is None else lo[1])
 
         HS = Pon["wv"].numel()   # stream width (512 NatureCNN, 256 IMPALA)
 
@@ -102,7 +138,7 @@ class TorchBackend:
         dv = dq[:, None] * Pon["wv"].float()[None, :]
         da = dadv @ Pon["wa"].float()
         dh = torch.cat([dv, da], 1) * (Hon[:B] > 0).float()
-        dH.copy_(dh)
+        split_into(dh, dH, None if lo is None else lo[2])
         if q_out is not None:
             q_out.copy_(q_t)
         if zero is not None:
@@ -110,14 +146,14 @@ class TorchBackend:
         if prio is not None:
             prio[0].update_priorities(prio[1], td_abs, prio[2])
 
-    def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor], prio=None):
+    def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor], prio=None, Hon_lo=None):
         """``prio = (replay, idx, gen, td_abs)``: also write the batch's priorities back
         (the HIP backend runs it as one extra block of the same launch)."""
         if prio is not None:
             prio[0].update_priorities(prio[1], prio[3], prio[2])
         B = dhead.shape[0]
         HS = g["wv"].numel()
-        h = Hon[:B].float()
+        h = join(Hon[:B], None if Hon_lo is None else Hon_lo[:B])
         g["wv"].add_(dhead[:, 0] @ h[:, :HS])
         g["bv"].add_(dhead[:, 0].sum().view(1))
         g["wa"].add_(dhead[:, 1:].t() @ h[:, HS:])
@@ -142,55 +178,66 @@ class TorchBackend:
         self.fc_dgrad(dh, x, w, dx_out)
         self.fc_wgrad(dh, x, dw_out, db_out)
 
-    def fc_dgrad(self, dh, x, w, dx_out):
+    def fc_dgrad(self, dh, x, w, dx_out, dh_lo=None, w_lo=None, dx_lo=None):
         """dx = (dh @ w) * (x > 0) (x = the ReLU'd fc input)."""
         xf = x.reshape(x.shape[0], -1)
+        if dh_lo is not None:
+            dx = (join(dh, dh_lo) @ join(w, w_lo)) * (xf > 0).float()
+            split_into(dx, dx_out, dx_lo)
+            return
         dx, _, _ = R.fc_bwd(dh, xf, w, xf, self.dtype)
         dx_out.copy_(dx.reshape(dx_out.shape))
 
-    def fc_wgrad(self, dh, x, dw_out, db_out, norm=None):
-        xf = x.reshape(x.shape[0], -1)
-        dw_out.copy_(dh.t().float() @ xf.float())
-        db_out.copy_(dh.float().sum(0))
+    def fc_wgrad(self, dh, x, dw_out, db_out, norm=None, dh_lo=None, x_lo=None):
+        xf = join(x.reshape(x.shape[0], -1), None if x_lo is None else x_lo.reshape(x.shape[0], -1))
+        dhf = join(dh, dh_lo)
+        dw_out.copy_(dhf.t() @ xf)
+        db_out.copy_(dhf.sum(0))
         return 0
 
-    def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None) -> int:
+    def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None, dh_lo=None, x_lo=None,
+                      Hon_lo=None) -> int:
         """fc weight gradient + head weight gradient (+ the priority write-back,
         ``prio = (replay, idx, gen, td_abs)``); returns the fc norm slots used."""
-        self.head_wgrad(Hon, dhead, g_head, prio=prio)
-        return self.fc_wgrad(dh, x, dw_out, db_out, norm=norm) or 0
+        self.head_wgrad(Hon, dhead, g_head, prio=prio, Hon_lo=Hon_lo)
+        return self.fc_wgrad(dh, x, dw_out, db_out, norm=norm, dh_lo=dh_lo, x_lo=x_lo) or 0
 
     def finalize_grads(self, jobs, norm_range=None, norm=None) -> int:
         """Deferred split-K reductions (the torch path computes gradients directly)."""
         return 0
 
-    def conv_dgrad(self, dy, w, stride, x_src, dx_out):
+    def conv_dgrad(self, dy, w, stride, x_src, dx_out, dy_lo=None, w_lo=None, dx_lo=None):
+        if dy_lo is not None:
+            dx = R.conv_dgrad(join(dy, dy_lo), join(w, w_lo), tuple(x_src.shape), stride, x_src, torch.float32)
+            split_into(dx, dx_out, dx_lo)
+            return
         dx_out.copy_(R.conv_dgrad(dy, w, tuple(x_src.shape), stride, x_src, self.dtype))
 
-    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None):
-        dw, db = R.conv_wgrad(dy, x, k, stride)
+    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None, dy_lo=None, x_lo=None):
+        dw, db = R.conv_wgrad(join(dy, dy_lo), join(x, x_lo), k, stride)
         dw_out.copy_(dw)
         db_out.copy_(db)
 
-    def conv1_wgrad(self, dy, frames, scale, dw_out, db_out):
-        dw, db = R.conv1_wgrad(dy, frames, scale)
+    def conv1_wgrad(self, dy, frames, scale, dw_out, db_out, dy_lo=None):
+        dw, db = R.conv1_wgrad(join(dy, dy_lo), frames, scale)
         dw_out.copy_(dw)
         db_out.copy_(db)
 
-    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out, jobs=None):
-        self.conv1_wgrad(dy, frames_buf[:slots.shape[0]], scale, dw_out, db_out)
+    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out, jobs=None, dy_lo=None):
+        self.conv1_wgrad(dy, frames_buf[:slots.shape[0]], scale, dw_out, db_out, dy_lo=dy_lo)
 
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None):
+                  sample=None, pb_lo=None):
         """``sample = (replay, B, out, ratio_min_global, nxt2)``: also draw the next
-        batch after the update (the HIP backend fuses it into the optimizer launch)."""
-        self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out)
+        batch after the update (the HIP backend fuses it into the optimizer launch).
+        ``pb_lo``: split mode, the lo plane of the bf16 copy."""
+        self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo)
         if sample is not None:
             rp, B, out, ratio, nxt2 = sample
             rp.sample(B, out=out, ratio_min_global=ratio, nxt2=nxt2)
 
-    def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out):
+    def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo=None):
         norm = g32.double().pow(2).sum().sqrt().float()
         coef = torch.clamp(clip / (norm + 1e-6), max=1.0) if clip > 0 else torch.ones_like(norm)
         g = g32 * coef
@@ -201,7 +248,7 @@ class TorchBackend:
         else:
             var = v
         p32.sub_(lr * g / (var.clamp_min(0).sqrt() + eps))
-        pbf.copy_(p32)
+        split_into(p32, pbf, pb_lo)
         norm_out.copy_(norm.view(1))
 
     def gather_frames(self, replay, slots, out):
@@ -209,9 +256,8 @@ class TorchBackend:
 
 
 class HipBackend(TorchBackend):
-    """MI355X backend.  Ops without a hand-written kernel yet run on torch
-    (MIOpen / hipBLASLt) in bf16; each kernel family switches on here as it
-    lands (``kernels`` lists what is native)."""
+    """MI355X backend: the hand-written gfx950 kernels (``kernels`` lists the op
+    families).  A missing kernel library is an error (``_lib.require_kernels``)."""
 
     name = "hip"
 
@@ -225,44 +271,52 @@ class HipBackend(TorchBackend):
         self.ws = C.Workspace()
 
     # --------------------------------------------------- native conv family
-    # prepare(): nothing to do -- the dgrad GEMMs read the natural weight tensors
-    # K-major (transposed LDS reads) and conv1 reads OIHW w1 directly.
-
-    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0):
+    def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0, w32=None,
+                       w2_32=None, out_lo=None):
         if not self.native_conv:
-            return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out, w2, b2, rows_first)
-        C.conv1_s2d_fwd(self.lib, self.ws, ring, slots, w, b, scale, out, w2, b2, rows_first)
+            return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out, w2, b2, rows_first, w32, w2_32,
+                                          out_lo)
+        C.conv1_s2d_fwd(self.lib, self.ws, ring, slots, w, b, scale, out, w2, b2, rows_first, w32=w32, w2_32=w2_32,
+                        out_lo=out_lo)
 
-    def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0):
+    def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
+                 out_lo=None):
         if not self.native_conv:
-            return super().conv_fwd(x, w, b, stride, out, w2, b2, rows_first)
-        C.conv_fwd(self.lib, x, w, b, stride, out, w2, b2, rows_first)
+            return super().conv_fwd(x, w, b, stride, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
+        C.conv_fwd(self.lib, x, w, b, stride, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo,
+                   out_lo=out_lo)
 
-    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0):
+    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None):
         if not self.native_conv:
-            return super().fc_fwd(x, w, b, out, w2, b2, rows_first)
+            return super().fc_fwd(x, w, b, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
         C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True, w2=w2, b2=b2,
-                    rows_first=rows_first, ws=self.ws)
+                    rows_first=rows_first, ws=self.ws,
+                    x_lo=None if x_lo is None else x_lo.reshape(x.shape[0], -1), w_lo=w_lo, w2_lo=w2_lo,
+                    out_lo=out_lo)
 
-    def fc_dgrad(self, dh, x, w, dx_out):
+    def fc_dgrad(self, dh, x, w, dx_out, dh_lo=None, w_lo=None, dx_lo=None):
         if not self.native_conv:
-            return super().fc_dgrad(dh, x, w, dx_out)
+            return super().fc_dgrad(dh, x, w, dx_out, dh_lo, w_lo, dx_lo)
         xf = x.reshape(x.shape[0], -1)
-        C.dense_dgrad(self.lib, dh, w, dx_out.reshape(dh.shape[0], -1), xf)
+        C.dense_dgrad(self.lib, dh, w, dx_out.reshape(dh.shape[0], -1), xf, dh_lo=dh_lo, w_lo=w_lo,
+                      out_lo=None if dx_lo is None else dx_lo.reshape(dh.shape[0], -1))
 
-    def fc_wgrad(self, dh, x, dw_out, db_out, norm=None):
+    def fc_wgrad(self, dh, x, dw_out, db_out, norm=None, dh_lo=None, x_lo=None):
         if not self.native_conv:
-            return super().fc_wgrad(dh, x, dw_out, db_out)
-        return C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm=norm)
+            return super().fc_wgrad(dh, x, dw_out, db_out, dh_lo=dh_lo, x_lo=x_lo)
+        return C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm=norm, dy_lo=dh_lo,
+                             x_lo=None if x_lo is None else x_lo.reshape(x.shape[0], -1))
 
-    def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None) -> int:
+    def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None, dh_lo=None, x_lo=None,
+                      Hon_lo=None) -> int:
         if self.native_conv and prio is not None and prio[0].use_hip:
             rp, idx, gen, td = prio
             r = C.dense_wgrad_head_prio(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm, Hon, dhead,
-                                        g_head, rp, idx, gen, td)
+                                        g_head, rp, idx, gen, td, dy_lo=dh_lo,
+                                        x_lo=None if x_lo is None else x_lo.reshape(x.shape[0], -1), Hon_lo=Hon_lo)
             if r is not None:
                 return r
-        return super().fc_head_wgrad(dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm)
+        return super().fc_head_wgrad(dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm, dh_lo, x_lo, Hon_lo)
 
     def finalize_grads(self, jobs, norm_range=None, norm=None) -> int:
         """Returns the number of squared-norm partial slots written (``slot0`` + blocks)."""
@@ -274,23 +328,23 @@ class HipBackend(TorchBackend):
         return norm["slot0"] + C.finalize_grads(self.lib, jobs, norm_range, norm["part"], norm["slot0"],
                                                 norm.get("total"))
 
-    def conv_dgrad(self, dy, w, stride, x_src, dx_out):
+    def conv_dgrad(self, dy, w, stride, x_src, dx_out, dy_lo=None, w_lo=None, dx_lo=None):
         if not self.native_conv:
-            return super().conv_dgrad(dy, w, stride, x_src, dx_out)
+            return super().conv_dgrad(dy, w, stride, x_src, dx_out, dy_lo, w_lo, dx_lo)
         if stride == 1:
-            C.conv3_dgrad(self.lib, dy, w, x_src, dx_out)
+            C.conv3_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo)
         else:
-            C.conv2_dgrad(self.lib, dy, w, x_src, dx_out)
+            C.conv2_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo)
 
-    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None):
+    def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None, dy_lo=None, x_lo=None):
         if not self.native_conv:
-            return super().conv_wgrad(dy, x, k, stride, dw_out, db_out)
-        C.conv_wgrad(self.lib, self.ws, dy, x, k, stride, dw_out, db_out, jobs=jobs)
+            return super().conv_wgrad(dy, x, k, stride, dw_out, db_out, dy_lo=dy_lo, x_lo=x_lo)
+        C.conv_wgrad(self.lib, self.ws, dy, x, k, stride, dw_out, db_out, jobs=jobs, dy_lo=dy_lo, x_lo=x_lo)
 
-    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out, jobs=None):
+    def conv1_wgrad_ring(self, dy, ring, slots, frames_buf, scale, dw_out, db_out, jobs=None, dy_lo=None):
         if not self.native_conv:
-            return super().conv1_wgrad_ring(dy, ring, slots, frames_buf, scale, dw_out, db_out)
-        C.conv1_wgrad_ring(self.lib, self.ws, dy, ring, slots, scale, dw_out, db_out, jobs=jobs)
+            return super().conv1_wgrad_ring(dy, ring, slots, frames_buf, scale, dw_out, db_out, dy_lo=dy_lo)
+        C.conv1_wgrad_ring(self.lib, self.ws, dy, ring, slots, scale, dw_out, db_out, jobs=jobs, dy_lo=dy_lo)
 
     @staticmethod
     def _hp(P):
@@ -300,23 +354,24 @@ class HipBackend(TorchBackend):
         return h
 
     def head(self, Hon, Htg, Pon, Ptg, act, rew, gam, isw, huber, kappa, grad_scale, td_abs, loss, dH,
-             dhead, q_out=None, zero=None, prio=None):
+             dhead, q_out=None, zero=None, prio=None, lo=None):
         B = act.shape[0]
         A = Pon["wa"].shape[0]
         args = (Hon.data_ptr(), Htg.data_ptr(), self._hp(Pon), self._hp(Ptg), act.data_ptr(), rew.data_ptr(),
                 gam.data_ptr(), _lib.ptr(isw), B, A, int(huber), float(kappa), float(grad_scale),
                 td_abs.data_ptr(), loss.data_ptr(), _lib.ptr(q_out), dH.data_ptr(), dhead.data_ptr(),
                 _lib.ptr(zero), 0 if zero is None else zero.numel(), Pon["wv"].numel())
+        hl = _lib.head_lo(*(lo if lo is not None else (None, None, None)))
         if prio is not None and prio[0].use_hip:
             # priority write-back in the head kernel (csrc/sumtree.hip: ddqn_head_prio_kernel)
-            _lib.check(self.lib.apex_ddqn_head_prio(*args, *prio[0].prio_launch_args(prio[1], prio[2]),
+            _lib.check(self.lib.apex_ddqn_head_prio(*args, *prio[0].prio_launch_args(prio[1], prio[2]), hl,
                                                     _lib.stream_ptr()), "ddqn_head_prio")
             return
-        _lib.check(self.lib.apex_ddqn_head(*args, _lib.stream_ptr()), "ddqn_head")
+        _lib.check(self.lib.apex_ddqn_head(*args, hl, _lib.stream_ptr()), "ddqn_head")
         if prio is not None:
             prio[0].update_priorities(prio[1], td_abs, prio[2])
 
-    def head_wgrad(self, Hon, dhead, g, prio=None):
+    def head_wgrad(self, Hon, dhead, g, prio=None, Hon_lo=None):
         B, A1 = dhead.shape
         if prio is not None and prio[0].use_hip and B <= 1024:
             rp, idx, gen, td = prio
@@ -324,13 +379,13 @@ class HipBackend(TorchBackend):
                 Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(), g["bv"].data_ptr(),
                 g["wa"].data_ptr(), g["ba"].data_ptr(), g["wv"].numel(), rp.tree_desc(), idx.data_ptr(),
                 td.data_ptr(), _lib.ptr(gen), rp.gen.data_ptr(), rp.alpha, rp.eps, rp.ctr.data_ptr(),
-                _lib.stream_ptr()), "head_wgrad_prio")
+                _lib.ptr(Hon_lo), _lib.stream_ptr()), "head_wgrad_prio")
             return
         if prio is not None:
             prio[0].update_priorities(prio[1], prio[3], prio[2])
         _lib.check(self.lib.apex_head_wgrad(Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(),
                                             g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(),
-                                            g["wv"].numel(), _lib.stream_ptr()), "head_wgrad")
+                                            g["wv"].numel(), _lib.ptr(Hon_lo), _lib.stream_ptr()), "head_wgrad")
 
     def actor_head(self, H, P, eps, ctr, seed, q_out, a_out):
         E, A = q_out.shape
@@ -339,9 +394,10 @@ class HipBackend(TorchBackend):
                                             P["wv"].numel(), _lib.stream_ptr()), "actor_head")
 
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None):
+                  sample=None, pb_lo=None):
         n = p32.numel()
         st = _lib.stream_ptr()
+        lo = _lib.ptr(pb_lo)
         if sample is not None and sample[0].use_hip:
             # the next batch's draw rides in the optimizer launch (csrc/sumtree.hip: rmsprop_sample_kernel)
             rp, B, out, ratio, nxt2 = sample
@@ -355,10 +411,11 @@ class HipBackend(TorchBackend):
             _lib.check(self.lib.apex_rmsprop_sample(
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
-                *rp.sample_launch_args(B, out, ratio, nxt2), st), "rmsprop_sample")
+                *rp.sample_launch_args(B, out, ratio, nxt2), lo, st), "rmsprop_sample")
             return
         if sample is not None:
-            self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total)
+            self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,
+                           pb_lo=pb_lo)
             rp, B, out, ratio, nxt2 = sample
             rp.sample(B, out=out, ratio_min_global=ratio, nxt2=nxt2)
             return
@@ -367,10 +424,15 @@ class HipBackend(TorchBackend):
             _lib.check(self.lib.apex_rmsprop_step_np(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
                                                      pbf.data_ptr(), n, part.data_ptr(), npart, float(lr),
                                                      float(alpha), float(eps), float(clip), int(centered),
-                                                     norm_out.data_ptr(), st), "rmsprop_np")
+                                                     norm_out.data_ptr(), lo, st), "rmsprop_np")
             return
         _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), n, partials.data_ptr(), st), "sqnorm")
         _lib.check(self.lib.apex_rmsprop_step(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
                                               pbf.data_ptr(), n, partials.data_ptr(), float(lr), float(alpha),
-                                              float(eps), float(clip), int(centered), norm_out.data_ptr(), st),
+                                              float(eps), float(clip), int(centered), norm_out.data_ptr(), lo, st),
                    "rmsprop")
+
+    def cast_bf16(self, x32, hi, lo=None) -> None:
+        """hi = bf16(x32) (and lo = bf16(x32 - hi)) with one kernel."""
+        _lib.check(self.lib.apex_cast_bf16(x32.data_ptr(), hi.data_ptr(), x32.numel(), _lib.ptr(lo),
+                                           _lib.stream_ptr()), "cast_bf16")

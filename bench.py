@@ -11,6 +11,18 @@ fwd on S_t+n, DDQN/Huber/IS loss + priorities, full backward, RCCL gradient
 all-reduce (N>1), clip + centered RMSprop, priority write-back, plus the
 periodic target sync / FIFO eviction at their configured cadences.
 
+Precision: ``--dtype fp32`` (default) matches the reference learner
+(``learner.py:37-38`` computes in fp32): the hand-written kernels run split
+hi/lo bf16 operands (three MFMAs per product, fp32 accumulation; see
+learner/fused_learner.py).  The JSON's ``value`` is that fp32 number; unless
+``--no-bf16-extra``, the same run also times the bf16-operand learner and reports
+it as ``value_bf16``.
+
+Timing: ``--warmup`` untimed updates, then every HIP graph the timed region
+replays is captured (``learner.prepare_graphs``: state-preserving, no updates),
+then EXACTLY ``--steps`` updates between barrier + synchronize brackets; the
+max over ranks is reported.  ``graph_captures_in_timed`` must be 0.
+
 ``value`` = whole-job batch-512 gradient steps per second
           = N x (data-parallel steps/s)  (each DP step consumes N x 512 samples).
 """
@@ -27,68 +39,18 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-BASELINE_STEPS_PER_S = 2.32  # BASELINE.md north-star row (reference learner compute, B=512, 4x84x84)
+BASELINE_STEPS_PER_S = 2.32  # BASELINE.md north-star row (reference learner compute, B=512, 4x84x84, fp32 CPU)
+METRIC = "learner grad-steps/sec at batch 512, 84x84x4 dueling DQN"
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=512)
-    ap.add_argument("--actions", type=int, default=4)
-    ap.add_argument("--replay", type=int, default=100000, help="transitions per shard")
-    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
-    ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--profile-phases", action="store_true")
-    ap.add_argument("--no-presample", action="store_true",
-                    help="sample at the head of each step instead of inside the previous step's optimizer launch")
-    ap.add_argument("--overlap-wgrad", action="store_true",
-                    help="weight-gradient GEMMs on a side stream beside the dgrad chain (default: one stream)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (rehearsing several ranks on one GPU)")
-    ap.add_argument("--graph-steps", type=int, default=None,
-                    help="learner updates per HIP-graph launch (Runtime.graph_steps; 1 = one graph per update)")
-    ap.add_argument("--graph-impala", action="store_true",
-                    help="IMPALA on the torch-autograd graph learner (MIOpen) instead of the HIP kernels")
-    ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
-                    help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala.hip")
-    args = ap.parse_args()
-
-    from apex_dqn_amd.config import ApexConfig
-    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
-    from apex_dqn_amd.parallel.dist import Comm
+def make_replay(args, device, rank):
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU")
-    # one rank per GPU; the modulo only matters when rehearsing several ranks on
-    # fewer GPUs (device_count() does not initialise the GPU)
-    dev_idx = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(dev_idx)
-    device = torch.device("cuda", dev_idx)
-    comm = Comm.from_env(backend=args.dist_backend, device=device)
-
-    cfg = ApexConfig.from_dict({
-        "env_conf": {"state_shape": [4, 84, 84], "action_dim": args.actions, "name": "SyntheticPong"},
-        "Learner": {"replay_sample_size": args.batch, "q_target_sync_freq": 2500, "remove_old_xp_freq": 100,
-                    "min_replay_mem_size": 0},
-        "Replay_Memory": {"soft_capacity": args.replay},
-        "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
-                    "seed": 1234 + rank, "network": args.network, "overlap_wgrad": args.overlap_wgrad,
-                    "presample": not args.no_presample,
-                    **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
-    })
     cap = args.replay
     frames_cap = cap + 4096
     replay = GpuReplayShard(cap, cap, frames_cap, 4, alpha=0.6, beta=0.4, device=device, seed=rank + 1)
     # synthetic prefill: random frames straight into HBM + random n-step records
     g = torch.Generator(device=device).manual_seed(1000 + rank)
-    replay.frames.copy_(torch.randint(0, 256, replay.frames.shape, generator=g, device=device,
-                                      dtype=torch.uint8))
+    replay.frames.copy_(torch.randint(0, 256, replay.frames.shape, generator=g, device=device, dtype=torch.uint8))
     replay.frame_head = frames_cap
     rng = np.random.default_rng(rank)
     chunk = 16384
@@ -101,14 +63,32 @@ def main():
                            R=rng.normal(size=K).astype(np.float32), Gamma=np.full(K, 0.99 ** 3, np.float32),
                            priority=rng.random(K).astype(np.float32) + 0.01))
     replay.rebuild()
-    if args.network in ("nature64", "nature32"):
-        learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
-    elif args.network == "impala" and not args.graph_impala:
-        from apex_dqn_amd.learner.impala_learner import FusedImpalaLearner
-        learner = FusedImpalaLearner(cfg, device, replay, comm=comm, backend=args.backend)
-    else:
+    return replay
+
+
+def make_learner(args, dtype, device, comm, rank, replay):
+    from apex_dqn_amd.config import ApexConfig
+    cfg = ApexConfig.from_dict({
+        "env_conf": {"state_shape": [4, 84, 84], "action_dim": args.actions, "name": "SyntheticPong"},
+        "Learner": {"replay_sample_size": args.batch, "q_target_sync_freq": 2500, "remove_old_xp_freq": 100,
+                    "min_replay_mem_size": 0},
+        "Replay_Memory": {"soft_capacity": args.replay},
+        "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
+                    "seed": 1234 + rank, "network": args.network, "dtype": dtype,
+                    "presample": not args.no_presample,
+                    **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
+    })
+    if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
         from apex_dqn_amd.learner.graph_learner import GraphLearner
-        learner = GraphLearner(cfg, device, replay, comm=comm)
+        return cfg, GraphLearner(cfg, device, replay, comm=comm)
+    if args.network in ("nature64", "nature32"):
+        from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+        return cfg, FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
+    from apex_dqn_amd.learner.impala_learner import FusedImpalaLearner
+    return cfg, FusedImpalaLearner(cfg, device, replay, comm=comm, backend=args.backend)
+
+
+def measure(cfg, learner, replay, comm, warmup: int, steps: int) -> dict:
     L = cfg.Learner
 
     def run(n):
@@ -126,38 +106,115 @@ def main():
             if learner.num_q_updates % f == 0:
                 replay.remove_to_fit()
                 replay.rebuild()
+                if hasattr(learner, "refresh_replay_stats"):
+                    learner.refresh_replay_stats()
 
-    run(args.warmup)
+    run(warmup)
+    # every graph the timed region replays, captured now (no learner updates)
+    caps = learner.prepare_graphs() if hasattr(learner, "prepare_graphs") else 0
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.steps)
+    run(steps)
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, "max") if comm.active else dt
+    caps_after = getattr(learner, "graph_captures", 0)
+    return dict(dt=dt, prep_graph_captures=int(caps), graph_captures_in_timed=int(caps_after - caps),
+                metrics=learner.last_metrics())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--actions", type=int, default=4)
+    ap.add_argument("--replay", type=int, default=100000, help="transitions per shard")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="learner precision of the headline value (fp32 = the reference's)")
+    ap.add_argument("--no-bf16-extra", action="store_true",
+                    help="skip the extra bf16-operand measurement (value_bf16)")
+    ap.add_argument("--learner", default="fused", choices=["fused", "graph"],
+                    help="fused = hand-written HIP learner; graph = torch autograd on MIOpen / hipBLASLt "
+                         "(the vendor-library baseline)")
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-presample", action="store_true",
+                    help="sample at the head of each step instead of inside the previous step's optimizer launch")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (rehearsing several ranks on one GPU)")
+    ap.add_argument("--graph-steps", type=int, default=None,
+                    help="learner updates per HIP-graph launch (Runtime.graph_steps; 1 = one graph per update)")
+    ap.add_argument("--graph-impala", action="store_true",
+                    help="IMPALA on the torch-autograd graph learner (MIOpen) instead of the HIP kernels")
+    ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
+                    help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala.hip")
+    args = ap.parse_args()
+
+    from apex_dqn_amd.parallel.dist import Comm
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    # one rank per GPU; the modulo only matters when rehearsing several ranks on
+    # fewer GPUs (device_count() does not initialise the GPU)
+    dev_idx = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_idx)
+    device = torch.device("cuda", dev_idx)
+    comm = Comm.from_env(backend=args.dist_backend, device=device)
+
+    replay = make_replay(args, device, rank)
+    cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay)
+    res = measure(cfg, learner, replay, comm, args.warmup, args.steps)
+    extra = None
+    if not args.no_bf16_extra and args.dtype == "fp32":
+        del learner
+        torch.cuda.empty_cache()
+        cfg_b, learner_b = make_learner(args, "bf16", device, comm, rank, replay)
+        extra = measure(cfg_b, learner_b, replay, comm, args.warmup, args.steps)
+        learner = learner_b
+    dt = res["dt"]
     ms = 1e3 * dt / args.steps
-    dp_steps_per_s = args.steps / dt
-    value = dp_steps_per_s * world
-    m = learner.last_metrics()
+    value = args.steps / dt * world
+    m = res["metrics"]
     if rank == 0:
+        kind = getattr(learner, "kind", "fused")
+        ops = getattr(learner, "ops", None)
         out = {
-            "metric": "learner grad-steps/sec at batch 512, 84x84x4 dueling DQN",
+            "metric": METRIC,
             "value": round(value, 2), "unit": "grad-steps/s (batch 512)", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_STEPS_PER_S, 2), "dtype": "bf16", "data": "synthetic",
+            "vs_baseline": round(value / BASELINE_STEPS_PER_S, 2), "dtype": args.dtype, "data": "synthetic",
             "config": {"model": ("dueling NatureCNN (reference DuellingDQN, conv1=64), 4x84x84, A=%d" % args.actions
                                   if args.network == "nature64" else
                                   "dueling %s, 4x84x84, A=%d" % (args.network, args.actions)),
                        "global_batch": args.batch * world, "seq_len": 1,
                        "parallelism": "dp%d" % world, "per_gpu_batch": args.batch,
-                       "replay_per_gpu": cap, "backend": getattr(learner, "kind", "fused") + "/" + learner.ops.name,
-                       "hip_graphs": bool(learner.rt.use_graphs)},
+                       "replay_per_gpu": args.replay,
+                       "learner": kind + ("/" + ops.name if ops is not None and args.learner == "fused" else
+                                          "/torch-autograd"),
+                       "hip_graphs": not args.no_graphs},
+            "math": ("fp32 master weights, gradients and optimizer; GEMM operands as bf16 hi + lo "
+                     "(hi*hi + lo*hi + hi*lo MFMAs, fp32 accumulation)" if args.dtype == "fp32"
+                     and args.learner == "fused" else
+                     ("torch fp32 (MIOpen / hipBLASLt)" if args.learner == "graph" and args.dtype == "fp32" else
+                      "bf16 operands, fp32 accumulation / master weights / optimizer")),
+            "prep_graph_captures": res["prep_graph_captures"],
+            "graph_captures_in_timed": res["graph_captures_in_timed"],
             "loss": round(m["loss"], 5), "grad_norm": round(m["grad_norm"], 5),
         }
+        if extra is not None:
+            out["value_bf16"] = round(args.steps / extra["dt"] * world, 2)
+            out["ms_per_step_bf16"] = round(1e3 * extra["dt"] / args.steps, 4)
+            out["graph_captures_in_timed_bf16"] = extra["graph_captures_in_timed"]
         print(json.dumps(out), flush=True)
     comm.shutdown()
 

@@ -53,29 +53,23 @@ for M in (512, 1024, 1536, 2048, 3072):
     print(json.dumps({"op": "igemm_fc_fwd", "M": M, "us": round(us, 2), "tflops": round(2 * M * 1024 * 3136 / us / 1e6, 1)}),
           flush=True)
 
-# split-K variants (fp32 partials + dense_splitk_reduce) at the step's M = 1536
-ws = C.Workspace()
-for ks in (1, 2, 3, 4):
-    C.DENSE_KSPLIT = ks
-    us = timed(lambda: C.dense_fwd(lib, xb[:1536], w, bias32, hb[:1536], True, None, w2, bias32, 1024, ws=ws))
-    print(json.dumps({"op": "igemm_fc_fwd_2sets", "ksplit": ks, "us": round(us, 2)}), flush=True)
-C.DENSE_KSPLIT = 0
-
-# two K groups per block (512 threads) vs one
-for kgr in (1, 2, 3, 4, 5):
-    C.DENSE_KGROUPS = kgr
-    for M in (1024, 1536):
-        us = timed(lambda: C.dense_fwd(lib, xb[:M], w, bias32, hb[:M], True, None, w2, bias32, 1024 if M > 1024 else 512))
-        print(json.dumps({"op": "igemm_fc_fwd_2sets", "kgroups": kgr, "M": M, "us": round(us, 2)}), flush=True)
-C.DENSE_KGROUPS = 1
-
-# tile shape x K groups (tile 1: BM=128, 2: BM=64) at the step's shape
+# tile shape (1: BM=128, 2: BM=64) at the step's shape, both weight sets in one launch
 for tile in (1, 2):
-    for kgr in (1, 2):
-        C.DENSE_KGROUPS = kgr
-        C.set_launch_hints(tile, 0)
-        us = timed(lambda: C.dense_fwd(lib, xb[:1536], w, bias32, hb[:1536], True, None, w2, bias32, 1024))
-        print(json.dumps({"op": "igemm_fc_fwd_2sets", "tile": tile, "kgroups": kgr, "M": 1536, "us": round(us, 2)}),
-              flush=True)
+    C.set_launch_hints(tile, 0)
+    us = timed(lambda: C.dense_fwd(lib, xb[:1536], w, bias32, hb[:1536], True, None, w2, bias32, 1024))
+    print(json.dumps({"op": "igemm_fc_fwd_2sets", "tile": tile, "M": 1536, "us": round(us, 2)}), flush=True)
 C.set_launch_hints()
-C.DENSE_KGROUPS = 1
+
+# fp32 accuracy: the split (hi + lo bf16, 3 MFMAs) fc forward vs the library's fp32 GEMM
+x32 = torch.relu(torch.randn(1536, 3136, device=dev))
+w32 = torch.randn(1024, 3136, device=dev) * 0.02
+xh, wh = x32.to(bf), w32.to(bf)
+xl, wl = (x32 - xh.float()).to(bf), (w32 - wh.float()).to(bf)
+hh, hl = torch.empty(1536, 1024, device=dev, dtype=bf), torch.empty(1536, 1024, device=dev, dtype=bf)
+us = timed(lambda: C.dense_fwd(lib, xh, wh, bias32, hh, True, x_lo=xl, w_lo=wl, out_lo=hl))
+ref = torch.relu(x32.double() @ w32.double().t())
+err = float(((hh.float() + hl.float()).double() - ref).norm() / ref.norm())
+us_lib = timed(lambda: torch.relu(torch.nn.functional.linear(x32, w32)))
+err_lib = float((torch.relu(torch.nn.functional.linear(x32, w32)).double() - ref).norm() / ref.norm())
+print(json.dumps({"op": "fc_fwd_fp32_split_vs_hipblaslt_fp32", "M": 1536, "split_us": round(us, 2),
+                  "split_rel_err": err, "lib_fp32_us": round(us_lib, 2), "lib_rel_err": err_lib}), flush=True)

@@ -111,3 +111,36 @@ def test_presample_draws_the_same_batches():
     for a, b in zip(runs[False][0], runs[True][0]):
         assert torch.equal(a, b)
     torch.testing.assert_close(runs[False][1], runs[True][1], rtol=0, atol=0)
+
+
+def test_split_mode_plumbing_matches_fp32_autograd():
+    """fp32-accurate split mode (hi + lo bf16 planes for every weight copy, activation
+    and gradient; the torch backend emulates the HIP kernels' contract on the CPU):
+    the whole-step gradients match fp32 autograd to <= 1e-4 relative per segment, so
+    every lo plane is routed to the right op."""
+    cfg, rp = _setup("huber")
+    L = FusedNatureLearner(cfg, "cpu", rp, split=True)
+    assert L.split and L.pbf.dtype == torch.bfloat16 and L.y1_lo is not None
+    # hi + lo reproduce the fp32 master weights far better than bf16 alone
+    err_hi = (L.pbf.float() - L.p32).abs().max()
+    err_split = (L.pbf.float() + L.pbf_lo.float() - L.p32).abs().max()
+    assert err_split < err_hi / 100
+    T = TorchLearner(cfg, "cpu")
+    T.Q.load_state_dict(L.reference_state_dict())
+    T.Q_target.load_state_dict(L.reference_state_dict())
+    L._seg1()
+    L._seg2()
+    B, S = L.B, L.S
+    batch = dict(S_t=L.frames[:B], S_tpn=L.frames[B:2 * B], A_t=S["act"], R=S["rew"], Gamma=S["gam"],
+                 weights=S["weights"])
+    lref, td = T.compute_loss_and_priorities(batch)
+    T.optimizer.zero_grad()
+    lref.backward()
+    torch.testing.assert_close(td, L.td_abs, rtol=1e-4, atol=1e-4)
+    gf = flat_to_reference_state(L.G, L.c1)
+    for k, p in T.Q.named_parameters():
+        rel = float((gf[k] - p.grad).norm() / (p.grad.norm() + 1e-30))
+        assert rel < 1e-4, (k, rel)
+    # the optimizer rewrites both planes: hi + lo == fp32 master to ~2^-17 relative
+    L._seg3()
+    torch.testing.assert_close(L.pbf.float() + L.pbf_lo.float(), L.p32, rtol=2e-5, atol=1e-9)

@@ -88,32 +88,6 @@ def test_dense_fwd_relu_and_mask(M):
     assert _rel(out3, ref3) < 1e-2
 
 
-@pytest.mark.parametrize("ks", [2, 3, 4])
-def test_dense_fwd_split_k(ks):
-    """Split-K dense forward (fp32 partials + reduce/bias/ReLU pass) == unsplit, incl.
-    the online/target weight switch at a 128-row boundary."""
-    from apex_dqn_amd.ops import conv as C
-    g = torch.Generator(device="cpu").manual_seed(ks)
-    M = 768
-    x = _bf(torch.relu(torch.randn(M, 3136, generator=g)))
-    w = _bf(torch.randn(1024, 3136, generator=g) * 0.02)
-    w2 = _bf(torch.randn(1024, 3136, generator=g) * 0.02)
-    b = (torch.randn(1024, generator=g) * 0.1).to(DEV)
-    b2 = (torch.randn(1024, generator=g) * 0.1).to(DEV)
-    ref = torch.empty(M, 1024, dtype=torch.bfloat16, device=DEV)
-    C.dense_fwd(_lib(), x, w, b, ref, relu=True, w2=w2, b2=b2, rows_first=512)
-    old = C.DENSE_KSPLIT
-    C.DENSE_KSPLIT = ks
-    try:
-        out = torch.empty_like(ref)
-        C.dense_fwd(_lib(), x, w, b, out, relu=True, w2=w2, b2=b2, rows_first=512, ws=C.Workspace())
-    finally:
-        C.DENSE_KSPLIT = old
-    torch.testing.assert_close(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
-    exact = torch.cat([R.fc_fwd(x[:512].float(), w.float(), b), R.fc_fwd(x[512:].float(), w2.float(), b2)])
-    assert _rel(out, exact) < 1e-2
-
-
 def test_pack_dgrad_weights():
     from apex_dqn_amd.ops import conv as C
     g = torch.Generator(device="cpu").manual_seed(3)
@@ -314,34 +288,3 @@ def test_conv3_dgrad_image_resident_vs_torch(N, grid):
     C.conv3_dgrad_img(_lib(), dy3, w3, y2, out, grid=grid)
     ref = R.conv_dgrad(dy3.float(), w3.float(), (N, 9, 9, 64), 1, y2.float())
     assert _rel(out, ref) < 1e-2 and _maxrel(out, ref) < 2e-2
-
-
-@pytest.mark.parametrize("kgr", [2, 3, 4, 5])
-@pytest.mark.parametrize("M,K", [(1536, 3136), (200, 3136), (384, 3200)])
-def test_dense_fwd_two_k_groups(M, K, kgr):
-    """Dense forward with two 4-wave K groups per block (igemm_fwd KG = 2, partial
-    tile summed through LDS) vs the fp32 torch reference, incl. the online/target
-    weight switch, a ragged last row tile and K/64 = 50 (unequal-halves rule)."""
-    from apex_dqn_amd.ops import conv as C
-    g = torch.Generator(device="cpu").manual_seed(M + K)
-    x = _bf(torch.relu(torch.randn(M, K, generator=g)))
-    w = _bf(torch.randn(1024, K, generator=g) * 0.02)
-    w2 = _bf(torch.randn(1024, K, generator=g) * 0.02)
-    b = (torch.randn(1024, generator=g) * 0.1).to(DEV)
-    b2 = (torch.randn(1024, generator=g) * 0.1).to(DEV)
-    split = 1024 if M >= 1024 else 0
-    old = C.DENSE_KGROUPS
-    C.DENSE_KGROUPS = kgr    # 2: two K groups per block; 3: 2 x 2 waves; 4: + 3-deep prefetch; 5: prefetch only
-    try:
-        out = torch.empty(M, 1024, dtype=torch.bfloat16, device=DEV)
-        if split:
-            C.dense_fwd(_lib(), x, w, b, out, relu=True, w2=w2, b2=b2, rows_first=split)
-        else:
-            C.dense_fwd(_lib(), x, w, b, out, relu=True)
-    finally:
-        C.DENSE_KGROUPS = old
-    if split:
-        exact = torch.cat([R.fc_fwd(x[:split].float(), w.float(), b), R.fc_fwd(x[split:].float(), w2.float(), b2)])
-    else:
-        exact = R.fc_fwd(x.float(), w.float(), b)
-    assert _rel(out, exact) < 1e-2

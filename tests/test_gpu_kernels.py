@@ -271,19 +271,21 @@ def test_rmsprop_kernel_vs_torch_optim():
 
 
 def test_fused_learner_step_hip_vs_torch_backend():
-    """Whole learner step: HIP backend vs the torch (fp32) backend on identical state."""
+    """Whole learner step, bf16-operand mode: HIP backend vs the torch (fp32) backend on
+    identical state (loose: bf16 operands; the fp32 split mode has its 1e-3 test in
+    tests/test_gpu_split.py)."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": 64},
-                                "Runtime": {"use_graphs": False, "presample": False}})
+                                "Runtime": {"use_graphs": False, "presample": False, "dtype": "bf16"}})
     res = {}
     for be in ("hip", "torch"):
         torch.manual_seed(0)
         rp = GpuReplayShard(2000, 2000, 2100, 4, device=DEV, seed=7)
         _fill_replay(rp, 1500, seed=11)
-        L = FusedNatureLearner(cfg, DEV, rp, backend=be)
+        L = FusedNatureLearner(cfg, DEV, rp, backend=be, split=False)
         if be == "torch":
             L.ops.dtype = torch.float32
         L._step_body()

@@ -191,7 +191,7 @@ def test_fused_learner_unaligned_batch(B):
         torch.manual_seed(0)
         return FusedNatureLearner(cfg, DEV, rp, backend=backend)
     Lh, Lt = make("hip"), make("torch")
-    Lt.p32.copy_(Lh.p32); Lt.pbf.copy_(Lh.pbf); Lt.sync_target()
+    Lt.p32.copy_(Lh.p32); Lt._refresh_bf16(); Lt.sync_target()
     Lh._step_body(); Lt._step_body()
     torch.cuda.synchronize()
     torch.testing.assert_close(Lh.td_abs, Lt.td_abs, rtol=5e-2, atol=5e-2)
@@ -214,13 +214,19 @@ def _bench_json(stdout: str) -> dict:
 
 
 def test_bench_contract_one_gpu():
-    """bench.py prints exactly one JSON line with the driver's keys."""
+    """bench.py prints exactly one JSON line with the driver's keys; the headline is
+    the fp32 (reference-precision) learner, bf16 rides along as value_bf16, and no
+    HIP graph is captured inside either timed window (warmup 5 < graph_steps 10:
+    the 10-update graph is captured by prepare_graphs, before the clock starts)."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "30", "--warmup", "5",
                         "--replay", "20000"], capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     out = _bench_json(r.stdout)
     assert out["n_gpus"] == 1 and out["steps"] == 30 and out["value"] > 0
-    assert out["config"]["global_batch"] == 512 and out["dtype"] == "bf16"
+    assert out["config"]["global_batch"] == 512 and out["dtype"] == "fp32"
+    assert out["value_bf16"] > 0
+    assert out["graph_captures_in_timed"] == 0 and out["graph_captures_in_timed_bf16"] == 0
+    assert out["prep_graph_captures"] == 2
 
 
 def test_bench_two_ranks_gloo_rehearsal():
@@ -230,7 +236,8 @@ def test_bench_two_ranks_gloo_rehearsal():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29541", os.path.join(ROOT, "bench.py"),
                         "--gpus", "2", "--steps", "20", "--warmup", "5", "--replay", "20000",
-                        "--dist-backend", "gloo"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+                        "--dist-backend", "gloo", "--no-bf16-extra"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     out = _bench_json(r.stdout)
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1024 and out["config"]["parallelism"] == "dp2"

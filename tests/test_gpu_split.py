@@ -1,0 +1,314 @@
+"""fp32-accurate ("split") mode of every learner kernel vs fp64 PyTorch references.
+
+Operands are fp32 tensors passed as hi + lo bf16 planes (value = hi + lo); the
+kernels run hi.hi + lo.hi + hi.lo bf16 MFMAs with fp32 accumulation (conv1: exact
+uint8 pixels x f16 hi + scaled-lo weights) and write fp32-accurate outputs as hi / lo
+planes again.  Tolerance 1e-4 relative (norm-wise) -- plain bf16 operands sit at
+~3e-3 on the same data, so these tests separate the two paths by > 10x.
+"""
+import numpy as np
+import pytest
+import torch
+
+from apex_dqn_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+TOL = 1e-4
+
+
+def _lib():
+    from apex_dqn_amd.ops import _lib as L
+    return L.require_kernels()
+
+
+def _split(x32):
+    """fp32 (any device) -> (hi, lo) bf16 planes on the GPU."""
+    x32 = x32.to(DEV, torch.float32)
+    hi = x32.to(torch.bfloat16)
+    lo = (x32 - hi.float()).to(torch.bfloat16)
+    return hi, lo
+
+
+def _join(hi, lo):
+    return hi.double() + lo.double()
+
+
+def _rel(a, b):
+    """norm-wise relative error, computed in fp64 on the CPU"""
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _c(t):
+    """fp64 CPU copy for the reference computations"""
+    return t.detach().double().cpu()
+
+
+def _empty2(*shape):
+    return (torch.empty(*shape, dtype=torch.bfloat16, device=DEV),
+            torch.empty(*shape, dtype=torch.bfloat16, device=DEV))
+
+
+def test_split_planes_represent_fp32():
+    x = torch.randn(1 << 16) * 3
+    hi, lo = _split(x)
+    assert _rel(_join(hi, lo).cpu(), x.double()) < 5e-6      # ~2^-17 per element (measured 2.4e-6)
+    assert _rel(hi.double().cpu(), x.double()) > 1e-3         # bf16 alone: ~2^-9
+
+
+@pytest.mark.parametrize("N,switch", [(64, 0), (200, 128)])
+def test_conv1_split_fwd(N, switch):
+    from apex_dqn_amd.ops import conv as C
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    g = torch.Generator(device="cpu").manual_seed(N)
+    raw = torch.randint(0, 256, (60, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    ring = to_s2d(raw)
+    slots = torch.randint(0, 60, (N, 4), generator=g, dtype=torch.int32).to(DEV)
+    wa32 = (torch.randn(64, 4, 8, 8, generator=g) * 0.05).to(DEV)
+    wb32 = (torch.randn(64, 4, 8, 8, generator=g) * 0.05).to(DEV)
+    wa32[0, 0, 0, :4] = torch.tensor([1e-5, -3e-7, 2e-9, 0.0])   # tiny weights (f16 subnormal range)
+    ba = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    bb = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    hi, lo = _empty2(N, 20, 20, 64)
+    two = dict(w2=wb32.to(torch.bfloat16), b2=bb, rows_first=switch, w2_32=wb32) if switch else {}
+    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, wa32.to(torch.bfloat16), ba, 1 / 255.0, hi,
+                    w32=wa32, out_lo=lo, **two)
+    frames = _c(raw[slots.long()])
+    if switch:
+        ref = torch.cat([R.conv1_fwd(frames[:switch], _c(wa32), _c(ba), 1 / 255.0, torch.float64),
+                         R.conv1_fwd(frames[switch:], _c(wb32), _c(bb), 1 / 255.0, torch.float64)])
+    else:
+        ref = R.conv1_fwd(frames, _c(wa32), _c(ba), 1 / 255.0, torch.float64)
+    assert _rel(_join(hi, lo), ref) < TOL
+
+
+@pytest.mark.parametrize("layer", [2, 3])
+def test_conv_split_fwd_with_weight_switch(layer):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(layer)
+    N1, N2 = 128, 64
+    if layer == 2:
+        x = torch.relu(torch.randn(N1 + N2, 20, 20, 64, generator=g))
+        wa, wb = torch.randn(64, 4, 4, 64, generator=g) * 0.03, torch.randn(64, 4, 4, 64, generator=g) * 0.03
+        stride, oh = 2, 9
+    else:
+        x = torch.relu(torch.randn(N1 + N2, 9, 9, 64, generator=g))
+        wa, wb = torch.randn(64, 3, 3, 64, generator=g) * 0.04, torch.randn(64, 3, 3, 64, generator=g) * 0.04
+        stride, oh = 1, 7
+    ba, bb = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    xh, xl = _split(x)
+    wah, wal = _split(wa)
+    wbh, wbl = _split(wb)
+    hi, lo = _empty2(N1 + N2, oh, oh, 64)
+    C.conv_fwd(_lib(), xh, wah, ba, stride, hi, wbh, bb, N1, x_lo=xl, w_lo=wal, w2_lo=wbl, out_lo=lo)
+    xd = _c(x)
+    ref = torch.cat([R.conv_fwd(xd[:N1], _c(wa), _c(ba), stride, torch.float64),
+                     R.conv_fwd(xd[N1:], _c(wb), _c(bb), stride, torch.float64)])
+    assert _rel(_join(hi, lo), ref) < TOL
+    # ReLU applied in fp32 before the split: no negative hi + lo anywhere
+    assert float(_join(hi, lo).min()) >= 0.0
+
+
+@pytest.mark.parametrize("M", [200, 1536])
+def test_dense_split_fwd_dgrad_wgrad(M):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(M)
+    lib = _lib()
+    x = torch.relu(torch.randn(M, 3136, generator=g))
+    w = torch.randn(1024, 3136, generator=g) * 0.02
+    b = (torch.randn(1024, generator=g) * 0.1).to(DEV)
+    xh, xl = _split(x)
+    wh, wl = _split(w)
+    hi, lo = _empty2(M, 1024)
+    C.dense_fwd(lib, xh, wh, b, hi, relu=True, x_lo=xl, w_lo=wl, out_lo=lo)
+    ref = R.fc_fwd(_c(x), _c(w), _c(b), torch.float64)
+    assert _rel(_join(hi, lo), ref) < TOL
+    # data gradient: (dh @ w) * (mask > 0), the natural weight read K-major
+    dh = torch.randn(M, 1024, generator=g) * 0.01
+    dhh, dhl = _split(dh)
+    mask = torch.randn(M, 3136, generator=g).to(DEV, torch.bfloat16)
+    gh, gl = _empty2(M, 3136)
+    C.dense_dgrad(lib, dhh, wh, gh, mask, dh_lo=dhl, w_lo=wl, out_lo=gl)
+    ref2 = (_c(dh) @ _c(w)) * (_c(mask) > 0)
+    assert _rel(_join(gh, gl), ref2) < TOL
+    # weight gradient
+    dw = torch.empty(1024, 3136, device=DEV)
+    db = torch.empty(1024, device=DEV)
+    C.dense_wgrad(lib, dhh, xh, dw, db, dy_lo=dhl, x_lo=xl)
+    assert _rel(dw, _c(dh).t() @ _c(x)) < TOL
+    assert _rel(db, _c(dh).sum(0)) < TOL
+
+
+@pytest.mark.parametrize("N", [3, 64])
+def test_conv_split_dgrad(N):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N + 7)
+    lib = _lib()
+    w3, w2 = torch.randn(64, 3, 3, 64, generator=g) * 0.04, torch.randn(64, 4, 4, 64, generator=g) * 0.03
+    dy3, dy2 = torch.randn(N, 7, 7, 64, generator=g), torch.randn(N, 9, 9, 64, generator=g)
+    y2 = torch.randn(N, 9, 9, 64, generator=g).to(DEV, torch.bfloat16)
+    y1 = torch.randn(N, 20, 20, 64, generator=g).to(DEV, torch.bfloat16)
+    (w3h, w3l), (w2h, w2l), (d3h, d3l), (d2h, d2l) = _split(w3), _split(w2), _split(dy3), _split(dy2)
+    h3, l3 = _empty2(N, 9, 9, 64)
+    C.conv3_dgrad(lib, d3h, w3h, y2, h3, dy_lo=d3l, w_lo=w3l, out_lo=l3)
+    ref3 = R.conv_dgrad(_c(dy3), _c(w3), (N, 9, 9, 64), 1, _c(y2), torch.float64)
+    assert _rel(_join(h3, l3), ref3) < TOL
+    h1, l1 = _empty2(N, 20, 20, 64)
+    C.conv2_dgrad(lib, d2h, w2h, y1, h1, dy_lo=d2l, w_lo=w2l, out_lo=l1)
+    ref1 = R.conv_dgrad(_c(dy2), _c(w2), (N, 20, 20, 64), 2, _c(y1), torch.float64)
+    assert _rel(_join(h1, l1), ref1) < TOL
+
+
+@pytest.mark.parametrize("N", [3, 64])
+def test_conv_split_wgrad(N):
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N + 11)
+    lib = _lib()
+    ws = C.Workspace()
+    for KH, stride, hin, hout in ((3, 1, 9, 7), (4, 2, 20, 9)):
+        dy = torch.randn(N, hout, hout, 64, generator=g)
+        x = torch.relu(torch.randn(N, hin, hin, 64, generator=g))
+        (dyh, dyl), (xh, xl) = _split(dy), _split(x)
+        dw = torch.empty(64, KH, KH, 64, device=DEV)
+        db = torch.empty(64, device=DEV)
+        jobs = []
+        C.conv_wgrad(lib, ws, dyh, xh, KH, stride, dw, db, jobs=jobs, dy_lo=dyl, x_lo=xl)
+        C.finalize_grads(lib, jobs)
+        rdw = torch.nn.grad.conv2d_weight(_c(x).permute(0, 3, 1, 2), (64, 64, KH, KH), _c(dy).permute(0, 3, 1, 2),
+                                          stride=stride).permute(0, 2, 3, 1)
+        rdb = _c(dy).sum((0, 1, 2))
+        assert _rel(dw, rdw) < TOL, (KH, _rel(dw, rdw))
+        assert _rel(db, rdb) < TOL
+
+
+@pytest.mark.parametrize("N,grid", [(3, 0), (64, 0), (37, 5)])
+def test_conv1_split_wgrad(N, grid):
+    from apex_dqn_amd.ops import conv as C
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    g = torch.Generator(device="cpu").manual_seed(N + 5)
+    raw = torch.randint(0, 256, (40, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    ring = to_s2d(raw)
+    slots = torch.randint(0, 40, (N, 4), generator=g, dtype=torch.int32).to(DEV)
+    dy = torch.randn(N, 20, 20, 64, generator=g)
+    dyh, dyl = _split(dy)
+    dw = torch.empty(64, 4, 8, 8, device=DEV)
+    db = torch.empty(64, device=DEV)
+    C.conv1_wgrad_ring(_lib(), C.Workspace(), dyh, ring, slots, 1 / 255.0, dw, db, grid=grid, dy_lo=dyl)
+    x = _c(raw[slots.long()]) / 255.0
+    rdw = torch.nn.grad.conv2d_weight(x, (64, 4, 8, 8), _c(dy).permute(0, 3, 1, 2), stride=4)
+    assert _rel(dw, rdw) < TOL
+    assert _rel(db, _c(dy).sum((0, 1, 2))) < TOL
+
+
+def test_head_split_matches_fp32_torch():
+    """ddqn_head / head_wgrad with lo planes == the torch backend on the joined fp32
+    activations (the split-mode head contract)."""
+    from apex_dqn_amd.ops.fused_ops import HipBackend, TorchBackend
+    B, A = 64, 6
+    g = torch.Generator(device="cpu").manual_seed(2)
+    H = torch.relu(torch.randn(3 * B, 1024, generator=g))
+    Hh, Hl = _split(H)
+    P = {"wv": (torch.randn(512, generator=g) * 0.05).to(DEV), "bv": torch.zeros(1, device=DEV),
+         "wa": (torch.randn(A, 512, generator=g) * 0.05).to(DEV), "ba": (torch.randn(A, generator=g) * 0.1).to(DEV)}
+    Pt = {k: (v * 0.9).contiguous() for k, v in P.items()}
+    act = torch.randint(0, A, (B,), generator=g, dtype=torch.int32).to(DEV)
+    rew = torch.randn(B, generator=g).to(DEV)
+    gam = torch.full((B,), 0.97, device=DEV)
+    isw = torch.rand(B, generator=g).to(DEV)
+    res = {}
+    for name, be in (("hip", HipBackend()), ("torch", TorchBackend(torch.float32))):
+        td, loss = torch.zeros(B, device=DEV), torch.zeros(B, device=DEV)
+        dHh, dHl = _empty2(B, 1024)
+        dhead = torch.zeros(B, A + 1, device=DEV)
+        be.head(Hh[:2 * B], Hh[2 * B:], P, Pt, act, rew, gam, isw, True, 1.0, 1.0 / B, td, loss, dHh, dhead,
+                lo=(Hl[:2 * B], Hl[2 * B:], dHl))
+        gr = {"wv": torch.zeros(512, device=DEV), "bv": torch.zeros(1, device=DEV),
+              "wa": torch.zeros(A, 512, device=DEV), "ba": torch.zeros(A, device=DEV)}
+        be.head_wgrad(Hh, dhead, gr, Hon_lo=Hl)
+        torch.cuda.synchronize()
+        res[name] = (td, loss, _join(dHh, dHl), dhead, gr)
+    a, b = res["hip"], res["torch"]
+    for x, y in zip(a[:4], b[:4]):
+        assert _rel(x, y) < 1e-5
+    for k in a[4]:
+        assert _rel(a[4][k], b[4][k]) < 1e-5, k
+
+
+def test_rmsprop_writes_split_copy():
+    from apex_dqn_amd.ops.fused_ops import HipBackend
+    n = 100_003
+    g = torch.Generator(device="cpu").manual_seed(1)
+    p = torch.randn(n, generator=g).to(DEV)
+    gr = (torch.randn(n, generator=g) * 0.1).to(DEV)
+    v, m = torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    hi, lo = _empty2(n)
+    parts, norm = torch.zeros(1024, dtype=torch.float64, device=DEV), torch.zeros(1, device=DEV)
+    HipBackend().optimizer(p, gr, v, m, hi, 2.5e-4, 0.95, 1.5e-7, 40.0, True, parts, norm, pb_lo=lo)
+    torch.cuda.synchronize()
+    assert _rel(_join(hi, lo), p.double()) < 5e-6     # ~2^-17 per element (measured 2.4e-6)
+    assert torch.equal(hi, p.to(torch.bfloat16))
+
+
+def _fp64_reference_grads(L):
+    """Gradients of the learner's batch (S, frames from the ring) under fp64 CPU
+    autograd of the reference DuellingDQN module (weights = the learner's fp32 master
+    copy, target = its target copy): the oracle of the whole-step test."""
+    from apex_dqn_amd.models.dueling import DuellingDQN
+    from apex_dqn_amd.models.flat_params import flat_to_reference_state
+    B, S, rt = L.B, L.S, L.rt
+    Q = DuellingDQN((4, 84, 84), L.A).double()
+    Qt = DuellingDQN((4, 84, 84), L.A).double()
+    Q.load_state_dict({k: v.double() for k, v in L.reference_state_dict().items()})
+    Qt.load_state_dict({k: v.double() for k, v in flat_to_reference_state(L.T).items()})
+    fr = lambda slots: _c(L.replay.gather_frames(slots)) * rt.obs_scale      # noqa: E731
+    s_t, s_n = fr(S["obs"]), fr(S["nxt"])
+    with torch.no_grad():
+        a_star = Q(s_n)[2].argmax(1, keepdim=True)
+        G = _c(S["rew"]) + _c(S["gam"]) * Qt(s_n)[2].gather(1, a_star).squeeze(1)
+    q_sa = Q(s_t)[2].gather(1, S["act"].long().cpu().view(-1, 1)).squeeze(1)
+    delta = G - q_sa
+    a = delta.abs()
+    per = torch.where(a <= 1.0, 0.5 * delta * delta, a - 0.5)
+    loss = (per * _c(S["weights"])).mean()
+    loss.backward()
+    return {k: p.grad for k, p in Q.named_parameters()}, a.detach()
+
+
+def test_whole_step_fp32_split_matches_fp64_oracle():
+    """The whole fused learner step in its default fp32 (split) mode: every gradient
+    segment within 1e-3 relative (norm-wise) of fp64 CPU autograd on the same batch;
+    the bf16-operand mode and the torch fp32 backend (MIOpen / hipBLASLt) are measured
+    against the same oracle and printed for comparison."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.models.flat_params import flat_to_reference_state
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    errs_all = {}
+    for mode, be, dtype in (("fp32_split", "hip", "fp32"), ("bf16", "hip", "bf16"), ("torch_fp32", "torch", "fp32")):
+        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                    "Learner": {"replay_sample_size": 128},
+                                    "Runtime": {"use_graphs": False, "presample": False, "dtype": dtype}})
+        torch.manual_seed(0)
+        rp = GpuReplayShard(2000, 2000, 2100, 4, device=DEV, seed=7)
+        rng = np.random.default_rng(11)
+        seqs = rp.append_frames(rng.integers(0, 255, (1800, 84, 84), dtype=np.uint8))
+        K = 1500
+        st = np.stack([seqs[i:i + 4] for i in range(K)])
+        rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 6, K), R=rng.normal(size=K) * 2,
+                       Gamma=np.where(rng.random(K) < 0.1, 0.0, 0.97), priority=rng.random(K)))
+        L = FusedNatureLearner(cfg, DEV, rp, backend=be)
+        assert L.split == (mode == "fp32_split")
+        L._seg1()
+        L._seg2()
+        torch.cuda.synchronize()
+        ref, td_ref = _fp64_reference_grads(L)
+        g = flat_to_reference_state(L.G)
+        errs_all[mode] = {k: _rel(g[k], ref[k]) for k in ref}
+        errs_all[mode]["td_abs"] = _rel(L.td_abs, td_ref)
+    for mode, e in errs_all.items():
+        print(f"per-segment relative grad error vs fp64 ({mode}):", {k: f"{v:.2e}" for k, v in e.items()})
+    e = errs_all["fp32_split"]
+    assert max(e.values()) < 1e-3, e
+    # the split path is a different precision class from the bf16-operand path
+    assert max(e.values()) < 0.2 * max(errs_all["bf16"].values())
