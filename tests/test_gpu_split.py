@@ -251,35 +251,57 @@ def test_rmsprop_writes_split_copy():
 
 
 def _fp64_reference_grads(L):
-    """Gradients of the learner's batch (S, frames from the ring) under fp64 CPU
-    autograd of the reference DuellingDQN module (weights = the learner's fp32 master
-    copy, target = its target copy): the oracle of the whole-step test."""
+    """Gradients of the learner's batch under fp64 CPU autograd of the dueling network
+    (weights = the learner's fp32 master copy, target = its target copy), evaluated in
+    the learner's ReLU activation region: the S_t rows use the learner's own ReLU masks,
+    so the oracle is the exact gradient of the same piecewise-linear function.  (A
+    pre-activation within ~1e-6 of zero can flip its ReLU under any finite precision; one
+    flipped element moves a norm-wise layer gradient by ~1e-3.)  Returns (grads keyed like
+    the reference state_dict, |delta|, number of mask flips vs an fp64 forward)."""
+    import torch.nn.functional as F
     from apex_dqn_amd.models.dueling import DuellingDQN
     from apex_dqn_amd.models.flat_params import flat_to_reference_state
     B, S, rt = L.B, L.S, L.rt
-    Q = DuellingDQN((4, 84, 84), L.A).double()
+    sd = {k: v.double().requires_grad_(True) for k, v in L.reference_state_dict().items()}
     Qt = DuellingDQN((4, 84, 84), L.A).double()
-    Q.load_state_dict({k: v.double() for k, v in L.reference_state_dict().items()})
     Qt.load_state_dict({k: v.double() for k, v in flat_to_reference_state(L.T).items()})
+    Qn = DuellingDQN((4, 84, 84), L.A).double()
+    Qn.load_state_dict({k: v.detach() for k, v in sd.items()})
     fr = lambda slots: _c(L.replay.gather_frames(slots)) * rt.obs_scale      # noqa: E731
     s_t, s_n = fr(S["obs"]), fr(S["nxt"])
+    nchw = lambda t: (_c(t[:B]) > 0).double().permute(0, 3, 1, 2)            # noqa: E731
+    m1, m2, m3 = nchw(L.y1), nchw(L.y2), nchw(L.y3)
+    mh = (_c(L.h[:B]) > 0).double()
+    p1 = F.conv2d(s_t, sd["layer1.0.weight"], sd["layer1.0.bias"], stride=4)
+    p2 = F.conv2d(p1 * m1, sd["layer2.0.weight"], sd["layer2.0.bias"], stride=2)
+    p3 = F.conv2d(p2 * m2, sd["layer3.0.weight"], sd["layer3.0.bias"])
+    flat = (p3 * m3).reshape(B, 3136)
+    hv = F.linear(flat, sd["value_stream_layer.0.weight"], sd["value_stream_layer.0.bias"]) * mh[:, :512]
+    ha = F.linear(flat, sd["advantage_stream_layer.0.weight"], sd["advantage_stream_layer.0.bias"]) * mh[:, 512:]
+    v = F.linear(hv, sd["value.weight"], sd["value.bias"])
+    adv = F.linear(ha, sd["advantage.weight"], sd["advantage.bias"])
+    q = v + adv - adv.mean(1, keepdim=True)
     with torch.no_grad():
-        a_star = Q(s_n)[2].argmax(1, keepdim=True)
+        a_star = Qn(s_n)[2].argmax(1, keepdim=True)
         G = _c(S["rew"]) + _c(S["gam"]) * Qt(s_n)[2].gather(1, a_star).squeeze(1)
-    q_sa = Q(s_t)[2].gather(1, S["act"].long().cpu().view(-1, 1)).squeeze(1)
+        # ReLU decisions of a plain fp64 forward that differ from the learner's (informational)
+        f1 = F.relu(p1)
+        f2 = F.relu(F.conv2d(f1, sd["layer2.0.weight"], sd["layer2.0.bias"], stride=2))
+        flips = int(((p1 > 0).double() != m1).sum()) + int(((f2 > 0).double() != m2).sum())
+    q_sa = q.gather(1, S["act"].long().cpu().view(-1, 1)).squeeze(1)
     delta = G - q_sa
     a = delta.abs()
     per = torch.where(a <= 1.0, 0.5 * delta * delta, a - 0.5)
     loss = (per * _c(S["weights"])).mean()
     loss.backward()
-    return {k: p.grad for k, p in Q.named_parameters()}, a.detach()
+    return {k: t.grad for k, t in sd.items()}, a.detach(), flips
 
 
 def test_whole_step_fp32_split_matches_fp64_oracle():
     """The whole fused learner step in its default fp32 (split) mode: every gradient
-    segment within 1e-3 relative (norm-wise) of fp64 CPU autograd on the same batch;
-    the bf16-operand mode and the torch fp32 backend (MIOpen / hipBLASLt) are measured
-    against the same oracle and printed for comparison."""
+    segment within 1e-3 relative (norm-wise; measured ~1e-5) of fp64 CPU autograd on the
+    same batch in the same ReLU region; the bf16-operand mode and the torch fp32 backend
+    (MIOpen / hipBLASLt) are measured against the same oracle and printed."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.models.flat_params import flat_to_reference_state
@@ -302,10 +324,11 @@ def test_whole_step_fp32_split_matches_fp64_oracle():
         L._seg1()
         L._seg2()
         torch.cuda.synchronize()
-        ref, td_ref = _fp64_reference_grads(L)
+        ref, td_ref, flips = _fp64_reference_grads(L)
         g = flat_to_reference_state(L.G)
         errs_all[mode] = {k: _rel(g[k], ref[k]) for k in ref}
         errs_all[mode]["td_abs"] = _rel(L.td_abs, td_ref)
+        print(f"{mode}: {flips} conv ReLU decisions differ from a plain fp64 forward")
     for mode, e in errs_all.items():
         print(f"per-segment relative grad error vs fp64 ({mode}):", {k: f"{v:.2e}" for k, v in e.items()})
     e = errs_all["fp32_split"]
