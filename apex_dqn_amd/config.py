@@ -18,7 +18,7 @@ import copy
 import dataclasses
 import json
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 
 @dataclass
@@ -101,7 +101,8 @@ class RuntimeConf:
     graph_steps: int = 10           # learner updates per HIP-graph launch in learner.steps(n) (1 rank;
                                     # 10 divides the default eviction cadence: 3505 vs 3472 steps/s at 4)
     actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)
-    replay_capacity: Optional[int] = None  # physical capacity (default: soft_capacity * 1.25)
+    replay_capacity: Optional[int] = None  # physical capacity, global over the ranks' shards
+                                           # (default: soft_capacity * 1.25 + 1024)
     heartbeat_timeout: float = 60.0
 
 
@@ -211,6 +212,18 @@ class ApexConfig:
         if self.Runtime.replay_capacity is not None:
             return int(self.Runtime.replay_capacity)
         return int(self.Replay_Memory.soft_capacity * 1.25) + 1024
+
+    def shard_capacity(self, world: int) -> Tuple[int, int]:
+        """(soft, physical) transitions held by ONE of ``world`` replay shards: the
+        global FIFO bound ``Replay_Memory.soft_capacity`` (``replay.py:71-80``) split
+        evenly, ceil-rounded; the physical ring keeps the configured headroom."""
+        w = max(int(world), 1)
+        soft = -(-int(self.Replay_Memory.soft_capacity) // w)
+        if self.Runtime.replay_capacity is not None:
+            phys = -(-int(self.Runtime.replay_capacity) // w)
+        else:
+            phys = int(soft * 1.25) + 1024
+        return soft, max(phys, soft)
 
     def copy(self) -> "ApexConfig":
         return copy.deepcopy(self)

@@ -241,8 +241,21 @@ static int tree_kfirst(const TreeDesc& t) {
 
 // Stratified proportional sampling: one wave per sample, 64-ary descent.
 // Also gathers the sampled records and the IS weight
-//   w_i = ((p_i/total) / ratio_min)^-beta,  ratio_min = min_j p_j/total
-// (global over shards when `ratio_min_global` is given) -- max-normalised.
+//   w_i = (N P(i) / max_j N P(j))^-beta = (p_i / min_j p_j)^-beta   (max-normalised).
+//
+// Sharded mode (`shard_stats` set: the all-gathered (total, min p) of the W shards,
+// fp64 [W][2]): ONE global stratified draw over the concatenation of the shards'
+// mass intervals, identical on every rank (same seed, same counter, same gathered
+// totals summed in the same order), so every global draw lands in exactly one
+// shard and an item's sampling probability is p_i / sum_all p -- the single
+// prioritized replay of the reference (replay.py:44-57) spread over W GPUs.
+// Rank r takes the draws in its interval [c_{r-1}, c_r): slot b of the local batch
+// holds the b-th of them.  The global batch is M = min(W B, floor((B - 2) sum / max
+// T_r)) draws, so no interval catches more than B (an interval of length T spans at
+// most floor(T M / sum) + 2 strata); unused slots get weight 0 and generation -1
+// (their priority write-back is dropped).  IS weights use the global minimum:
+// w = (p / p_min)^-beta * (W B / M), the last factor turning the head's 1/(W B)
+// gradient scale into the 1/M mean over the draws actually taken.
 struct SampleArgs {
   TreeDesc t;
   RecordDesc r;
@@ -250,7 +263,6 @@ struct SampleArgs {
   uint64_t seed;
   const uint64_t* ctr;
   float beta;
-  const float* ratio_min_global;
   int64_t* out_idx;
   float* out_w;
   int32_t* out_gen;
@@ -260,6 +272,9 @@ struct SampleArgs {
   float* out_rew;
   float* out_gam;
   int32_t* out_nxt2;
+  const double* shard_stats;   // sharded mode: [W][2] (total, min p) of every shard, or null
+  int shard_rank, shard_world;
+  uint64_t shard_seed;         // common to all ranks (the local `seed` is per shard)
 };
 
 // block `bid` of 4 waves: samples 4 bid .. 4 bid + 3
@@ -270,7 +285,6 @@ __device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
   const uint64_t seed = S.seed;
   const uint64_t* __restrict__ ctr = S.ctr;
   const float beta = S.beta;
-  const float* __restrict__ ratio_min_global = S.ratio_min_global;
   int64_t* __restrict__ out_idx = S.out_idx;
   float* __restrict__ out_w = S.out_w;
   int32_t* __restrict__ out_gen = S.out_gen;
@@ -284,8 +298,48 @@ __device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
   const int b = (bid * blockDim.x + threadIdx.x) >> 6;
   if (b >= B) return;
   const double total = t.nodes[t.off[t.L]];
-  const float uu = apex_uniform(seed, ctr[0], (uint64_t)b);
-  double u = ((double)b + (double)uu) * (total / (double)B);
+  double u;
+  bool valid = true;
+  float wscale = 1.f, pmin_g = 0.f;
+  if (S.shard_stats != nullptr) {
+    const int W = S.shard_world, r = S.shard_rank;
+    double sum = 0.0, c0 = 0.0, tmax = 0.0;
+    float pm = __uint_as_float(0x7f800000u);
+    for (int q = 0; q < W; ++q) {
+      const double Tq = S.shard_stats[2 * q];
+      if (q < r) c0 += Tq;
+      sum += Tq;
+      tmax = fmax(tmax, Tq);
+      const float mq = (float)S.shard_stats[2 * q + 1];
+      if (Tq > 0.0 && mq > 0.f) pm = fminf(pm, mq);
+    }
+    const double Tr = S.shard_stats[2 * r];
+    const double c1 = c0 + Tr;
+    int64_t M = 0;
+    if (tmax > 0.0) {
+      const double mb = floor((double)(B - 2) * sum / tmax);
+      M = (int64_t)fmin((double)W * (double)B, fmax(mb, 0.0));
+    }
+    const uint64_t cc = ctr[0];
+    double ul = 0.0;
+    if (M > 0 && Tr > 0.0) {
+      const double delta = sum / (double)M;
+      int64_t j0 = (int64_t)floor(c0 / delta);
+      if (((double)j0 + (double)apex_uniform(S.shard_seed, cc, (uint64_t)j0)) * delta < c0) ++j0;
+      const int64_t j = j0 + b;
+      const double uj = ((double)j + (double)apex_uniform(S.shard_seed, cc, (uint64_t)j)) * delta;
+      valid = j < M && uj < c1;
+      ul = uj - c0;
+      wscale = (float)((double)W * (double)B / (double)M);
+    } else {
+      valid = false;
+    }
+    u = valid ? fmin(fmax(ul, 0.0), total) : 0.0;
+    pmin_g = pm;
+  } else {
+    const float uu = apex_uniform(seed, ctr[0], (uint64_t)b);
+    u = ((double)b + (double)uu) * (total / (double)B);
+  }
   int64_t node = 0;
   for (int k = t.L - 1; k >= 0; --k) {
     int64_t child = node * 64 + lane;
@@ -307,13 +361,13 @@ __device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
   s = APEX_DBG_CLAMP(s, r.cap < t.n[0] ? r.cap : t.n[0], 2);
   if (lane == 0) {
     float p = t.leaf[s];
-    float ratio = ratio_min_global ? ratio_min_global[0]
-                                   : (float)((double)__uint_as_float(t.min_bits[0]) / total);
-    float pr = (float)((double)p / total);
-    float w = (p > 0.f && ratio > 0.f) ? powf(pr / ratio, -beta) : 0.f;
+    // (p / p_min)^-beta <= 1 (p_min global over the shards in sharded mode), times
+    // the global-batch correction
+    const float pmin = S.shard_stats != nullptr ? pmin_g : __uint_as_float(t.min_bits[0]);
+    const float w = (valid && p > 0.f && pmin > 0.f) ? fminf(powf(p / pmin, -beta), 1.0f) * wscale : 0.f;
     out_idx[b] = s;
-    out_w[b] = fminf(w, 1.0f);
-    out_gen[b] = r.gen[s];
+    out_w[b] = w;
+    out_gen[b] = valid ? r.gen[s] : -1;
     out_act[b] = r.act[s];
     out_rew[b] = r.rew[s];
     out_gam[b] = r.gam[s];
@@ -599,14 +653,17 @@ APEX_EXPORT int apex_replay_insert(TreeDesc t, RecordDesc r, int64_t start, int 
 }
 
 APEX_EXPORT int apex_tree_sample(TreeDesc t, RecordDesc r, int B, uint64_t seed, const uint64_t* ctr,
-                                 float beta, const float* ratio_min_global, int64_t* out_idx, float* out_w,
+                                 float beta, int64_t* out_idx, float* out_w,
                                  int32_t* out_gen, int32_t* out_obs, int32_t* out_nxt, int32_t* out_act,
-                                 float* out_rew, float* out_gam, int32_t* out_nxt2, hipStream_t st) {
+                                 float* out_rew, float* out_gam, int32_t* out_nxt2, const double* shard_stats,
+                                 int shard_rank, int shard_world, uint64_t shard_seed, hipStream_t st) {
   if (B <= 0) return 0;
+  if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
+    return (int)hipErrorInvalidValue;
   const int waves_per_block = 4;
   tree_sample_kernel<<<blocks_for(B, waves_per_block), 64 * waves_per_block, 0, st>>>(
-      SampleArgs{t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
-                 out_rew, out_gam, out_nxt2});
+      SampleArgs{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
+                 out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed});
   APEX_CHECK_LAUNCH();
 }
 
@@ -691,10 +748,13 @@ APEX_EXPORT int apex_ddqn_head_prio(const bf16_t* Hon, const bf16_t* Htg, HeadPa
 APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
                                     const double* partials, int npart, float lr, float alpha, float eps_opt,
                                     float clip, int centered, float* norm_out, TreeDesc t, RecordDesc r, int B,
-                                    uint64_t seed, const uint64_t* ctr, float beta, const float* ratio_min_global,
+                                    uint64_t seed, const uint64_t* ctr, float beta,
                                     int64_t* out_idx, float* out_w, int32_t* out_gen, int32_t* out_obs,
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
-                                    int32_t* out_nxt2, bf16_t* pb_lo, hipStream_t st) {
+                                    int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
+                                    uint64_t shard_seed, bf16_t* pb_lo, hipStream_t st) {
+  if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
+    return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
   if ((((uintptr_t)pb | (uintptr_t)pb_lo) & 7) || B < 1) return (int)hipErrorInvalidValue;
   // block size APEX_OPT_THREADS (256 / 512 / 1024), grid capped at APEX_OPT_BLOCKS:
@@ -715,8 +775,8 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
   const int nsb = blocks_for(B, nt / 64);
   const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo};
-  const SampleArgs sa{t, r, B, seed, ctr, beta, ratio_min_global, out_idx, out_w, out_gen, out_obs, out_nxt,
-                      out_act, out_rew, out_gam, out_nxt2};
+  const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
+                      out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed};
   if (nt == 1024) rmsprop_sample_kernel<1024><<<nb + nsb, 1024, 0, st>>>(ra, sa, nsb);
   else if (nt == 512) rmsprop_sample_kernel<512><<<nb + nsb, 512, 0, st>>>(ra, sa, nsb);
   else rmsprop_sample_kernel<256><<<nb + nsb, 256, 0, st>>>(ra, sa, nsb);

@@ -46,6 +46,15 @@ from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
 
 
+def _enable_sharding(replay, comm, rt) -> None:
+    """Turn the rank-local replay into one shard of the global replay (idempotent)."""
+    if not replay.sharded:
+        replay.enable_sharding(comm.rank, comm.world_size, shard_seed=(int(rt.seed) << 20) ^ 0x5EED,
+                               group=comm.group)
+    if not rt.use_is_weights:
+        replay.beta = 0.0
+
+
 class FusedNatureLearner:
     kind = "fused"
 
@@ -124,12 +133,16 @@ class FusedNatureLearner:
         # write squared-norm partials of the values they store, the optimizer launch sums
         # them.  With DP the norm is of the all-reduced gradient: the optimizer's own pass.
         self._fuse_norm = self.world == 1 and self.ops.name == "hip" and getattr(self.ops, "native_conv", False)
-        # cross-shard IS-weight normaliser: min over ranks of (min_i p_i / total), reduced
-        # inside every DP step right after the priority write-back (exact, no lag)
-        self.ratio_min = None
+        # DP: the rank-local replay shards form ONE prioritized replay (replay/gpu_replay.py
+        # enable_sharding): every step all-gathers the shards' (sum p^alpha, min p^alpha)
+        # right after the priority write-back and the next batch is one global draw,
+        # identical on every rank, of which each rank keeps the part in its own shard.
+        # Rows drawn elsewhere carry IS weight 0, so the IS weights always enter the loss
+        # (with use_is_weights off: beta = 0, i.e. weights 0 / W B / M only).
+        self._isw = bool(self.rt.use_is_weights) or self.world > 1
         if self.world > 1:
-            self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d)
-            self._init_ratio()
+            _enable_sharding(replay, comm, self.rt)
+            replay.gather_shard_stats()
         # DP step as ONE captured graph including the RCCL collectives (backend nccl);
         # gloo (CPU tests, one-GPU rehearsals) cannot be captured: eager DP steps
         self._dp_graphs = self.world > 1 and cuda and self._backend_name() == "nccl"
@@ -240,7 +253,7 @@ class FusedNatureLearner:
         # conv1 reads the uint8 frame stacks straight from the replay ring by slot
         self.forward_all()
         self._mark("forward")
-        isw = S["weights"] if rt.use_is_weights else None
+        isw = S["weights"] if self._isw else None
         sp = self.split
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
@@ -263,7 +276,7 @@ class FusedNatureLearner:
     def _sample(self) -> None:
         """The sampler writes idx / IS weights / records and the frame-ring slots of
         S_t, S_{t+n} (twice: online and target rows) into the step's buffers."""
-        self.replay.sample(self.B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * self.B:])
+        self.replay.sample(self.B, out=self.S, nxt2=self.slots[2 * self.B:])
         self._sample_ver = self.replay.version
 
     def _seg2(self) -> None:
@@ -334,7 +347,7 @@ class FusedNatureLearner:
             self.g32.copy_(self.gcomm)
         # with pre-sampling the optimizer launch also draws step t+1's batch (every
         # read of this step's sample buffers is behind us)
-        nxt = (self.replay, self.B, self.S, self.ratio_min, self.slots[2 * self.B:]) if self._presample else None
+        nxt = (self.replay, self.B, self.S, self.slots[2 * self.B:]) if self._presample else None
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else None, sample=nxt,
@@ -348,24 +361,17 @@ class FusedNatureLearner:
         self._seg2()
         self._seg3()
 
-    def _local_ratio(self, out: torch.Tensor) -> None:
-        """out = min_i p_i / total of this shard (device-side, capturable)."""
-        rp = self.replay
-        tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float().clamp_min(1e-30)
-        torch.div(rp.min_bits.view(torch.float32), tot, out=out)
-
     def _dp_body(self) -> None:
         """One data-parallel step (graph-capturable with RCCL): the fc/heads gradient
-        bucket and the IS normaliser (MIN over shards of min p / total, taken after
-        this step's priority write-back, consumed by the next batch's draw inside the
-        optimizer launch) are reduced while the conv backward runs; the conv bucket
-        follows; the optimizer waits for all three."""
+        bucket and the shard statistics (every shard's sum / min p^alpha, taken after
+        this step's priority write-back, consumed by the next batch's global draw
+        inside the optimizer launch) are exchanged while the conv backward runs; the
+        conv bucket follows; the optimizer waits for all three."""
         import torch.distributed as dist
         cut = self.layout.offsets["wfc"]
         self._seg1()
-        self._local_ratio(self.ratio_min)
         w_fc = dist.all_reduce(self.gcomm[cut:], op=dist.ReduceOp.SUM, async_op=True)
-        w_r = dist.all_reduce(self.ratio_min, op=dist.ReduceOp.MIN, async_op=True)
+        w_r = self.replay.gather_shard_stats(async_op=True)
         self._seg2()     # conv backward overlaps the fc/head bucket all-reduce
         w_cv = dist.all_reduce(self.gcomm[:cut], op=dist.ReduceOp.SUM, async_op=True)
         w_fc.wait()
@@ -466,28 +472,22 @@ class FusedNatureLearner:
         self.graph_captures += 1
         # capture recorded the step without executing it; state is as before
 
-    def _init_ratio(self) -> None:
-        import torch.distributed as dist
-        self._local_ratio(self.ratio_min)
-        dist.all_reduce(self.ratio_min, op=dist.ReduceOp.MIN)
-
     def refresh_replay_stats(self) -> None:
-        """Re-derive the cross-shard IS normaliser (after host-side inserts / eviction;
-        a collective: every rank calls it at the same point)."""
+        """Re-gather the shard statistics (after host-side inserts / eviction; a
+        collective: every rank calls it at the same point)."""
         if self.world > 1:
-            self._init_ratio()
+            self.replay.gather_shard_stats()
 
     def _snapshot(self):
         rp = self.replay
         return [t.clone() for t in (self.p32, self._pbf_all, self.rms_v, self.rms_m, rp.leaf, rp.nodes,
-                                    rp.min_bits, rp.ctr)] + ([self.ratio_min.clone()] if self.ratio_min is not None
-                                                             else [])
+                                    rp.min_bits, rp.ctr)] + ([rp.shard_stats.clone()] if rp.sharded else [])
 
     def _restore(self, snap) -> None:
         rp = self.replay
         dst = [self.p32, self._pbf_all, self.rms_v, self.rms_m, rp.leaf, rp.nodes, rp.min_bits, rp.ctr]
-        if self.ratio_min is not None:
-            dst.append(self.ratio_min)
+        if rp.sharded:
+            dst.append(rp.shard_stats)
         for t, src in zip(dst, snap):
             t.copy_(src)
 

@@ -32,6 +32,7 @@ from ..config import ApexConfig
 from ..models.dueling import build_network
 from ..ops.fused_ops import HipBackend, TorchBackend
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from .fused_learner import _enable_sharding
 from .losses import ddqn_loss
 
 
@@ -88,9 +89,11 @@ class GraphLearner:
         self.S = replay.alloc_sample_buffers(self.B)
         self.td_abs = torch.zeros(self.B, dtype=torch.float32, device=d)
         self.loss_b = torch.zeros(1, dtype=torch.float32, device=d)
-        self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d) if self.world > 1 else None
+        # DP: one global prioritized replay over the rank shards (see fused_learner)
+        self._isw = bool(self.rt.use_is_weights) or self.world > 1
         if self.world > 1:
-            self._init_ratio()
+            _enable_sharding(replay, comm, self.rt)
+            replay.gather_shard_stats()
         self.num_q_updates = 0
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None
         ls = cfg.Learner.load_saved_state
@@ -108,7 +111,7 @@ class GraphLearner:
     # ---------------------------------------------------------------- step
     def _forward_backward(self) -> None:
         rt, B = self.rt, self.B
-        S = self.replay.sample(B, out=self.S, ratio_min_global=self.ratio_min)
+        S = self.replay.sample(B, out=self.S)
         obs = self.replay.gather_frames(S["obs"])
         nxt = self.replay.gather_frames(S["nxt"])
         self.g32.zero_()
@@ -120,7 +123,7 @@ class GraphLearner:
             with torch.no_grad():
                 q_n = self.Q(nxt)[2]
                 q_g = self.Q_target(nxt)[2]
-        w = S["weights"] if rt.use_is_weights else None
+        w = S["weights"] if self._isw else None
         loss, td = ddqn_loss(q_t.float(), q_n.float(), q_g.float(), S["act"], S["rew"], S["gam"], w,
                              loss=rt.loss, kappa=rt.huber_delta)
         (loss / self.world).backward()     # SUM all-reduce of 1/world-scaled grads = mean
@@ -184,27 +187,15 @@ class GraphLearner:
                 self._allreduce()
             self._apply()
         if self.world > 1:
-            self._update_ratio()
+            self.replay.gather_shard_stats()
         self.num_q_updates += 1
         if self.num_q_updates % self.cfg.Learner.q_target_sync_freq == 0:
             self.sync_target()
 
     # --------------------------------------------------- replay statistics
-    def _local_ratio(self) -> torch.Tensor:
-        rp = self.replay
-        tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float().clamp_min(1e-30)
-        return rp.min_bits.view(torch.float32) / tot
-
-    def _init_ratio(self) -> None:
-        import torch.distributed as dist
-        self.ratio_min.copy_(self._local_ratio())
-        dist.all_reduce(self.ratio_min, op=dist.ReduceOp.MIN)
-
-    _update_ratio = _init_ratio
-
     def refresh_replay_stats(self) -> None:
         if self.world > 1:
-            self._init_ratio()
+            self.replay.gather_shard_stats()
 
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)

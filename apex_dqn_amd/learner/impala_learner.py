@@ -44,6 +44,7 @@ from ..models.flat_params import FlatLayout
 from ..ops.fused_ops import HipBackend, TorchBackend
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from .fused_learner import _enable_sharding
 
 CH = (16, 32, 32)
 HIDDEN = 256
@@ -150,14 +151,11 @@ class FusedImpalaLearner:
         self._sample_ver = None
         self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
-        self.ratio_local = torch.zeros(1, dtype=torch.float32, device=d)
-        self.ratio_buf = torch.zeros(2, 1, dtype=torch.float32, device=d)
-        self.ratio_min = None
-        self._ratio_work = [None, None]
-        self._ratio_k = 0
+        # DP: one global prioritized replay over the rank shards (see fused_learner)
+        self._isw = bool(self.rt.use_is_weights) or self.world > 1
         if self.world > 1:
-            self.ratio_min = torch.zeros(1, dtype=torch.float32, device=d)
-            self._init_ratio()
+            _enable_sharding(replay, comm, self.rt)
+            replay.gather_shard_stats()
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
@@ -303,7 +301,7 @@ class FusedImpalaLearner:
             self._sample()
         S = self.S
         self.forward_all()
-        isw = S["weights"] if rt.use_is_weights else None
+        isw = S["weights"] if self._isw else None
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
@@ -315,7 +313,7 @@ class FusedImpalaLearner:
         self._join_side()
 
     def _sample(self) -> None:
-        self.replay.sample(self.B, out=self.S, ratio_min_global=self.ratio_min, nxt2=self.slots[2 * self.B:])
+        self.replay.sample(self.B, out=self.S, nxt2=self.slots[2 * self.B:])
         self._sample_ver = self.replay.version
 
     def _seg2(self) -> None:
@@ -356,15 +354,11 @@ class FusedImpalaLearner:
 
     def _seg3(self) -> None:
         rt, ops = self.rt, self.ops
-        nxt = (self.replay, self.B, self.S, self.ratio_min, self.slots[2 * self.B:]) if self._presample else None
+        nxt = (self.replay, self.B, self.S, self.slots[2 * self.B:]) if self._presample else None
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm, sample=nxt)
         if self._presample:
             self._sample_ver = self.replay.version
-        if self.world > 1:
-            rp = self.replay
-            tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float()
-            self.ratio_local.copy_(rp.min_bits.view(torch.float32) / tot)
 
     def _step_body(self) -> None:
         self._seg1()
@@ -386,21 +380,17 @@ class FusedImpalaLearner:
         cut = self.layout.offsets["wfc"]
         run = (lambda i: self._graphs[i].replay()) if graphs else (lambda i: (self._seg1, self._seg2,
                                                                                 self._seg3)[i]())
-        k = self._ratio_k
-        if self._ratio_work[k] is not None:   # normaliser of step t-2 (see fused_learner._dp_step)
-            self._ratio_work[k].wait()
-            self.ratio_min.copy_(self.ratio_buf[k])
-            self._ratio_work[k] = None
         run(0)
+        # shard statistics after this step's priority write-back: the next global draw
+        # (inside the optimizer launch) sees exactly the trees it samples from
+        w_st = self.replay.gather_shard_stats(async_op=True)
         w_fc = dist.all_reduce(self.g32[cut:], op=dist.ReduceOp.SUM, async_op=True)
         run(1)
         w_cv = dist.all_reduce(self.g32[:cut], op=dist.ReduceOp.SUM, async_op=True)
+        w_st.wait()
         w_fc.wait()
         w_cv.wait()
         run(2)
-        self.ratio_buf[k].copy_(self.ratio_local)
-        self._ratio_work[k] = dist.all_reduce(self.ratio_buf[k], op=dist.ReduceOp.MIN, async_op=True)
-        self._ratio_k = 1 - k
 
     def step(self) -> None:
         graphs = self.rt.use_graphs and self.device.type == "cuda"
@@ -448,30 +438,17 @@ class FusedImpalaLearner:
     def _snapshot(self):
         rp = self.replay
         return [t.clone() for t in (self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes,
-                                    rp.min_bits, rp.ctr)]
+                                    rp.min_bits, rp.ctr)] + ([rp.shard_stats.clone()] if rp.sharded else [])
 
     def _restore(self, snap) -> None:
         rp = self.replay
         for dst, src in zip((self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes, rp.min_bits,
-                             rp.ctr), snap):
+                             rp.ctr) + ((rp.shard_stats,) if rp.sharded else ()), snap):
             dst.copy_(src)
-
-    def _init_ratio(self) -> None:
-        import torch.distributed as dist
-        rp = self.replay
-        tot = rp.nodes[rp.offs[rp.L]:rp.offs[rp.L] + 1].float().clamp_min(1e-30)
-        buf = self.ratio_buf[0]
-        buf.copy_(rp.min_bits.view(torch.float32) / tot)
-        dist.all_reduce(buf, op=dist.ReduceOp.MIN)
-        self.ratio_min.copy_(buf)
 
     def refresh_replay_stats(self) -> None:
         if self.world > 1:
-            for i, w in enumerate(self._ratio_work):
-                if w is not None:
-                    w.wait()
-                    self._ratio_work[i] = None
-            self._init_ratio()
+            self.replay.gather_shard_stats()
 
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)

@@ -103,7 +103,7 @@ _SIGS = {
     "apex_replay_insert": ([TreeDesc, RecordDesc, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p],
                            c_i),
     "apex_tree_sample": ([TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                          c_p, c_p, c_p, c_p], c_i),
+                          c_p, c_p, c_p, c_i, c_i, c_u64, c_p], c_i),
     "apex_tree_rebuild": ([TreeDesc, c_p], c_i),
     "apex_gather_frames": ([c_p, c_p, c_i, c_i64, c_i64, c_p, c_p], c_i),
     "apex_debug_bounds_enabled": ([], c_i),
@@ -121,8 +121,8 @@ _SIGS = {
                              c_p, c_p, c_p, c_p, c_p, c_i, c_i, TreeDesc, c_p, c_p, c_p, c_f, c_f, c_p, HeadLo, c_p],
                             c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
-                             TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p, c_p], c_i),
+                             TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                             c_p, c_p, c_i, c_i, c_u64, c_p, c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
                               c_p, c_p, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,

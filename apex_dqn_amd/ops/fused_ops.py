@@ -229,13 +229,13 @@ class TorchBackend:
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
                   sample=None, pb_lo=None):
-        """``sample = (replay, B, out, ratio_min_global, nxt2)``: also draw the next
+        """``sample = (replay, B, out, nxt2)``: also draw the next
         batch after the update (the HIP backend fuses it into the optimizer launch).
         ``pb_lo``: split mode, the lo plane of the bf16 copy."""
         self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo)
         if sample is not None:
-            rp, B, out, ratio, nxt2 = sample
-            rp.sample(B, out=out, ratio_min_global=ratio, nxt2=nxt2)
+            rp, B, out, nxt2 = sample
+            rp.sample(B, out=out, nxt2=nxt2)
 
     def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo=None):
         norm = g32.double().pow(2).sum().sqrt().float()
@@ -400,7 +400,7 @@ class HipBackend(TorchBackend):
         lo = _lib.ptr(pb_lo)
         if sample is not None and sample[0].use_hip:
             # the next batch's draw rides in the optimizer launch (csrc/sumtree.hip: rmsprop_sample_kernel)
-            rp, B, out, ratio, nxt2 = sample
+            rp, B, out, nxt2 = sample
             if norm_total is None:
                 _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), n, partials.data_ptr(), st), "sqnorm")
                 part, npart = partials, partials.numel()
@@ -411,13 +411,13 @@ class HipBackend(TorchBackend):
             _lib.check(self.lib.apex_rmsprop_sample(
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
-                *rp.sample_launch_args(B, out, ratio, nxt2), lo, st), "rmsprop_sample")
+                *rp.sample_launch_args(B, out, nxt2), lo, st), "rmsprop_sample")
             return
         if sample is not None:
             self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,
                            pb_lo=pb_lo)
-            rp, B, out, ratio, nxt2 = sample
-            rp.sample(B, out=out, ratio_min_global=ratio, nxt2=nxt2)
+            rp, B, out, nxt2 = sample
+            rp.sample(B, out=out, nxt2=nxt2)
             return
         if norm_total is not None:   # squared norm already summed by the gradient producers
             part, npart = norm_total if isinstance(norm_total, tuple) else (norm_total, 1)

@@ -17,8 +17,20 @@ shard; SURVEY §5.2 race A24 is designed out).  Slot generations make a
 priority write-back for a slot that was overwritten after it was sampled a
 no-op; writes to evicted slots never resurrect them.
 
+Data parallelism (:meth:`enable_sharding`): the W shards are ONE prioritized
+replay.  Each step the shards all-gather their (sum p^alpha, min p^alpha) and run
+one global stratified draw -- identical on every rank -- over the concatenated
+mass intervals; rank r keeps the draws that land in its interval.  An item's
+sampling probability is p_i / sum over ALL shards, exactly as in the reference's
+single ``ReplayMemory.sample`` (``replay.py:44-57``), the per-rank batch varies
+with the shard's share of the mass (fixed B-row buffers, unused rows carry IS
+weight 0), and IS weights are normalised by the global minimum priority.  Each
+shard holds ``ceil(soft_capacity / W)`` transitions, so the global FIFO bound is
+the reference's ``soft_capacity`` (``replay.py:71-80``).
+
 On CPU (tests) the same class runs a torch implementation with identical
-semantics (exact recompute instead of fp64 deltas).
+semantics (exact recompute instead of fp64 deltas; the same counter-based
+uniforms as the kernel, so the global draw is bit-identical).
 """
 from __future__ import annotations
 
@@ -41,6 +53,62 @@ def from_s2d(y: torch.Tensor) -> torch.Tensor:
     """Inverse of :func:`to_s2d` (the axis permutation is an involution)."""
     n = y.shape[0]
     return y.reshape(n, 21, 21, 4, 4).permute(0, 1, 3, 2, 4).contiguous().reshape(n, 84, 84)
+
+
+_MASK64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(z: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser (csrc/apex_common.h ``apex_mix64``), wrapping uint64 math."""
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def apex_uniform(seed: int, ctr: int, idx) -> np.ndarray:
+    """The kernels' counter-based uniform in [0, 1) (``apex_uniform``), float32."""
+    i = np.asarray(idx, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        inner = _mix64(np.uint64(ctr & 0xFFFFFFFFFFFFFFFF) * np.uint64(0x100000001B3) + i)
+    r = _mix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ inner)
+    return (r >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def global_draw(stats: np.ndarray, rank: int, B: int, seed: int, ctr: int):
+    """The sharded sampler's global stratified draw as seen by ``rank`` (mirror of
+    csrc/sumtree.hip ``tree_sample_body``): returns (u_local (B,) float64, valid (B,)
+    bool, wscale, pmin_global) for the all-gathered ``stats`` [W, 2] = (total, min p)."""
+    W = stats.shape[0]
+    sm = c0 = tmax = 0.0
+    pm = math.inf
+    for q in range(W):
+        tq = float(stats[q, 0])
+        if q < rank:
+            c0 += tq
+        sm += tq
+        tmax = max(tmax, tq)
+        mq = float(np.float32(stats[q, 1]))
+        if tq > 0.0 and mq > 0.0:
+            pm = min(pm, mq)
+    tr = float(stats[rank, 0])
+    c1 = c0 + tr
+    M = int(min(W * B, max(math.floor((B - 2) * sm / tmax), 0))) if tmax > 0.0 else 0
+    u = np.zeros(B, np.float64)
+    valid = np.zeros(B, bool)
+    wscale = 1.0
+    if M > 0 and tr > 0.0:
+        delta = sm / M
+        j0 = int(math.floor(c0 / delta))
+        if (j0 + float(apex_uniform(seed, ctr, j0))) * delta < c0:
+            j0 += 1
+        j = j0 + np.arange(B, dtype=np.int64)
+        uj = (j.astype(np.float64) + apex_uniform(seed, ctr, j).astype(np.float64)) * delta
+        valid = (j < M) & (uj < c1)
+        u = np.where(valid, uj - c0, 0.0)
+        wscale = float(np.float32(W * B / M))
+    return u, valid, wscale, pm
 
 
 def _tree_levels(cap: int):
@@ -106,6 +174,42 @@ class GpuReplayShard:
         self.min_frame_seq = np.full(self.cap, -1, np.int64)  # oldest frame referenced per slot
         self._tdesc = None
         self._rdesc = None
+        # sharding (enable_sharding): all-gathered (total, min p) of every shard, fp64
+        self.shard_rank, self.shard_world, self.shard_seed, self.shard_group = 0, 1, 0, None
+        self.local_stats = None
+        self.shard_stats = None
+
+    # -------------------------------------------------------------- sharding
+    def enable_sharding(self, rank: int, world: int, shard_seed: int, group=None) -> None:
+        """Make this shard part of ONE global prioritized replay over ``world`` ranks
+        (see the module docstring).  ``shard_seed`` must be equal on every rank;
+        the sampling counter ``ctr`` advances in lock-step with the DP updates."""
+        d = self.device
+        self.shard_rank, self.shard_world = int(rank), int(world)
+        self.shard_seed, self.shard_group = int(shard_seed), group
+        self.local_stats = torch.zeros(2, dtype=torch.float64, device=d)
+        self.shard_stats = torch.zeros(2 * self.shard_world, dtype=torch.float64, device=d)
+
+    @property
+    def sharded(self) -> bool:
+        return self.shard_stats is not None
+
+    def gather_shard_stats(self, async_op: bool = False):
+        """All-gather every shard's (sum p^alpha, min p^alpha) into ``shard_stats``
+        (a collective; device-side, HIP-graph capturable over RCCL).  Call it after
+        the last tree mutation that the next draw must see."""
+        import torch.distributed as dist
+        root = self.offs[self.L]
+        self.local_stats[0:1].copy_(self.nodes[root:root + 1])
+        self.local_stats[1:2].copy_(self.min_bits.view(torch.float32))
+        if dist.get_backend(self.shard_group) == "nccl":
+            return dist.all_gather_into_tensor(self.shard_stats, self.local_stats, group=self.shard_group,
+                                               async_op=async_op)
+        # gloo (CPU tests, one-GPU rehearsals; its all_gather takes no CUDA tensors): a
+        # SUM all-reduce of the rank-placed rows, exact (every other row is zero)
+        self.shard_stats.zero_()
+        self.shard_stats[2 * self.shard_rank:2 * self.shard_rank + 2].copy_(self.local_stats)
+        return dist.all_reduce(self.shard_stats, op=dist.ReduceOp.SUM, group=self.shard_group, async_op=async_op)
 
     # ----------------------------------------------------------- descriptors
     def tree_desc(self) -> "_lib.TreeDesc":
@@ -203,9 +307,10 @@ class GpuReplayShard:
 
     # ------------------------------------------------------------- sampling
     def sample(self, B: int, out: Optional[Dict[str, torch.Tensor]] = None,
-               ratio_min_global: Optional[torch.Tensor] = None,
                nxt2: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
-        """Stratified proportional sample of B slots; IS weights max-normalised.
+        """Stratified proportional sample of B slots; IS weights max-normalised
+        (globally over the shards once :meth:`enable_sharding` ran: then rows whose
+        global draw fell in another shard carry weight 0 and generation -1).
 
         ``out`` (preallocated tensors) makes the call graph-capturable; ``nxt2``
         receives a second copy of the S_{t+n} frame slots (target-network rows).
@@ -213,51 +318,57 @@ class GpuReplayShard:
         d = self.device
         if out is None:
             out = self.alloc_sample_buffers(B)
+        if self.sharded and B < 3:
+            raise ValueError("sharded sampling needs B >= 3")
         if self.use_hip:
-            _lib.check(self.lib.apex_tree_sample(
-                self.tree_desc(), self.record_desc(), B, self.seed, self.ctr.data_ptr(), self.beta,
-                _lib.ptr(ratio_min_global), out["idx"].data_ptr(), out["weights"].data_ptr(),
-                out["gen"].data_ptr(), out["obs"].data_ptr(), out["nxt"].data_ptr(), out["act"].data_ptr(),
-                out["rew"].data_ptr(), out["gam"].data_ptr(), _lib.ptr(nxt2), self._stream()), "tree_sample")
+            _lib.check(self.lib.apex_tree_sample(*self.sample_launch_args(B, out, nxt2), self._stream()),
+                       "tree_sample")
+            return out
+        leaf = self.leaf.double().cpu()
+        total = leaf.sum()
+        ctr = int(self.ctr.item())
+        valid = np.ones(B, bool)
+        wscale = 1.0
+        if self.sharded:
+            st = self.shard_stats.double().cpu().numpy().reshape(self.shard_world, 2)
+            u, valid, wscale, pmin = global_draw(st, self.shard_rank, B, self.shard_seed, ctr)
+            u = torch.from_numpy(u).clamp_(0.0, float(total))
         else:
-            g = torch.Generator(device="cpu").manual_seed(self.seed * 1000003 + int(self.ctr.item()))
-            leaf = self.leaf.double().cpu()
-            total = leaf.sum()
-            u = (torch.arange(B, dtype=torch.float64) + torch.rand(B, generator=g, dtype=torch.float64)) * (
-                total / B)
-            c = torch.cumsum(leaf, 0)
-            idx = torch.searchsorted(c, u, right=True).clamp_(max=self.cap - 1)
-            # never return an empty leaf (round-off at the top of the range)
-            empty = leaf[idx] <= 0
-            if empty.any():
-                nz = torch.nonzero(leaf > 0).flatten()
-                idx[empty] = nz[-1]
-            p = leaf[idx]
-            pmin = leaf[leaf > 0].min()
-            ratio = float(ratio_min_global.item()) if ratio_min_global is not None else float(pmin / total)
-            w = ((p / total) / ratio) ** (-self.beta)
-            idx = idx.to(d)
-            out["idx"].copy_(idx)
-            out["weights"].copy_(w.clamp(max=1.0).float())
-            out["gen"].copy_(self.gen[idx])
-            out["obs"].copy_(self.obs[idx])
-            out["nxt"].copy_(self.nxt[idx])
-            out["act"].copy_(self.act[idx])
-            out["rew"].copy_(self.rew[idx])
-            out["gam"].copy_(self.gam[idx])
-            if nxt2 is not None:
-                nxt2.copy_(out["nxt"])
+            uu = torch.from_numpy(apex_uniform(self.seed, ctr, np.arange(B))).double()
+            u = (torch.arange(B, dtype=torch.float64) + uu) * (total / B)
+            pos = leaf[leaf > 0]
+            pmin = float(np.float32(pos.min())) if pos.numel() else 0.0
+        c = torch.cumsum(leaf, 0)
+        idx = torch.searchsorted(c, u, right=True).clamp_(max=self.cap - 1)
+        # never return an empty leaf (round-off at the top of the range)
+        empty = leaf[idx] <= 0
+        if empty.any():
+            nz = torch.nonzero(leaf > 0).flatten()
+            idx[empty] = nz[-1] if nz.numel() else 0
+        p = leaf[idx].float()
+        vt = torch.from_numpy(valid)
+        w = torch.where(vt & (p > 0) & (pmin > 0), (p / max(pmin, 1e-38)).pow(-self.beta).clamp(max=1.0),
+                        torch.zeros_like(p)) * wscale
+        idx = idx.to(d)
+        out["idx"].copy_(idx)
+        out["weights"].copy_(w.float())
+        out["gen"].copy_(torch.where(vt.to(d), self.gen[idx], torch.full_like(self.gen[idx], -1)))
+        out["obs"].copy_(self.obs[idx])
+        out["nxt"].copy_(self.nxt[idx])
+        out["act"].copy_(self.act[idx])
+        out["rew"].copy_(self.rew[idx])
+        out["gam"].copy_(self.gam[idx])
+        if nxt2 is not None:
+            nxt2.copy_(out["nxt"])
         return out
 
-    def sample_launch_args(self, B: int, out: Dict[str, torch.Tensor],
-                           ratio_min_global: Optional[torch.Tensor] = None,
-                           nxt2: Optional[torch.Tensor] = None) -> tuple:
-        """The tree_sample arguments (TreeDesc .. out_nxt2) of :meth:`sample`, for
+    def sample_launch_args(self, B: int, out: Dict[str, torch.Tensor], nxt2: Optional[torch.Tensor] = None) -> tuple:
+        """The tree_sample arguments (TreeDesc .. shard_seed) of :meth:`sample`, for
         kernels that draw the batch inside another launch (``apex_rmsprop_sample``)."""
         return (self.tree_desc(), self.record_desc(), B, self.seed, self.ctr.data_ptr(), self.beta,
-                _lib.ptr(ratio_min_global), out["idx"].data_ptr(), out["weights"].data_ptr(),
-                out["gen"].data_ptr(), out["obs"].data_ptr(), out["nxt"].data_ptr(), out["act"].data_ptr(),
-                out["rew"].data_ptr(), out["gam"].data_ptr(), _lib.ptr(nxt2))
+                out["idx"].data_ptr(), out["weights"].data_ptr(), out["gen"].data_ptr(), out["obs"].data_ptr(),
+                out["nxt"].data_ptr(), out["act"].data_ptr(), out["rew"].data_ptr(), out["gam"].data_ptr(),
+                _lib.ptr(nxt2), _lib.ptr(self.shard_stats), self.shard_rank, self.shard_world, self.shard_seed)
 
     def prio_launch_args(self, idx: torch.Tensor, gen: Optional[torch.Tensor] = None,
                          bump_ctr: bool = True) -> tuple:
@@ -381,10 +492,3 @@ class GpuReplayShard:
 
     def min_leaf(self) -> float:
         return float(self.min_bits.view(torch.float32).item())
-
-    def stats_tensor(self) -> torch.Tensor:
-        """(total, min_leaf, live) as fp32 for the cross-shard all-gather."""
-        t = self.nodes[self.offs[self.L]:self.offs[self.L] + 1].float()
-        m = self.min_bits.view(torch.float32)
-        n = torch.tensor([float(self.live)], device=self.device)
-        return torch.cat([t, m, n])

@@ -25,12 +25,14 @@ from ..replay.gpu_replay import GpuReplayShard
 from ..utils.metrics import MetricsLogger
 
 
-def build_replay(cfg: ApexConfig, device, num_envs: int, seed: int = 0) -> GpuReplayShard:
+def build_replay(cfg: ApexConfig, device, num_envs: int, seed: int = 0, world: int = 1) -> GpuReplayShard:
+    """This rank's shard of the global replay: ``soft_capacity / world`` transitions
+    (the learners turn the shards into one prioritized replay, replay/gpu_replay.py)."""
     rm = cfg.Replay_Memory
-    cap = cfg.replay_capacity
+    soft, cap = cfg.shard_capacity(world)
     n, C = cfg.Actor.num_steps, cfg.frame_stack
     frame_cap = int(cap * 1.25) + (n + C + 4) * num_envs + 64
-    return GpuReplayShard(cap, rm.soft_capacity, frame_cap, C, alpha=rm.priority_exponent,
+    return GpuReplayShard(cap, soft, frame_cap, C, alpha=rm.priority_exponent,
                           beta=rm.importance_sampling_exponent, eps=cfg.Runtime.priority_eps, device=device,
                           seed=seed)
 
@@ -55,7 +57,7 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     rt, L = cfg.Runtime, cfg.Learner
     E = num_envs or cfg.Runtime.actors_per_rank or max(1, cfg.Actor.num_actors // world)
     torch.manual_seed(rt.seed)
-    replay = build_replay(cfg, device, E, seed=rt.seed + rank)
+    replay = build_replay(cfg, device, E, seed=rt.seed + rank, world=world)
     if cfg.network in ("nature64", "nature32"):
         learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=backend)
     elif cfg.network == "impala" and cfg.Runtime.use_hip_kernels:   # csrc/impala.hip learner

@@ -1,8 +1,9 @@
 """Data-parallel learner over gloo (CPU, world_size 2 and 4): the fake cluster.
 
 Checks that the bucketed, overlapped gradient all-reduce of the fused learner
-equals the mean of the per-rank gradients, that parameters stay bit-identical
-across ranks, and that the cross-shard IS normaliser is the global min.
+equals the mean of the per-rank gradients on the same globally drawn batches,
+that parameters stay bit-identical across ranks, and that the shards' statistics
+are all-gathered (one global prioritized replay, replay/gpu_replay.py).
 """
 import os
 import tempfile
@@ -42,22 +43,29 @@ def _worker(rank, world, path, q, ar="fp32"):
     torch.manual_seed(1234 + rank)  # different local init: rank 0's params must be broadcast
     rp = _replay(rank)
     L = FusedNatureLearner(cfg, "cpu", rp, comm=comm)
-    ratio_global = float(L.ratio_min)
-    ratio_local0 = rp.min_leaf() / rp.total()
-    # local reference gradient on an identical replay copy, single rank, scale 1/B
+    stats = rp.shard_stats.view(world, 2).clone()
+    own = (rp.total(), rp.min_leaf())
+    # the global draw of step 1 (what L.step() consumes: presampled, version unchanged)
+    L._sample()
+    # local reference gradient on an identical replay copy and the SAME batch, single
+    # rank, scale 1/B: the DP gradient is the mean of these over the ranks
     torch.manual_seed(0)
     rp2 = _replay(rank)
     Lref = FusedNatureLearner(cfg, "cpu", rp2, comm=None)
     Lref.p32.copy_(L.p32)
     Lref.pbf.copy_(L.pbf)
     Lref.sync_target()
-    Lref.ratio_min = L.ratio_min.clone()
+    for k, v in L.S.items():
+        Lref.S[k].copy_(v)
+    Lref.slots.copy_(L.slots)
+    Lref._sample_ver = rp2.version
     Lref._seg1()
     Lref._seg2()
     g_local = Lref.g32.clone()
+    n_valid = int((L.S["gen"] >= 0).sum())
     L.step()
     g_dp = L.g32.clone()
-    for _ in range(3):      # exercises the double-buffered (one-step-lagged) IS normaliser
+    for _ in range(3):
         L.step()
     gl = [torch.zeros_like(g_local) for _ in range(world)]
     torch.distributed.all_gather(gl, g_local)
@@ -65,7 +73,8 @@ def _worker(rank, world, path, q, ar="fp32"):
     pl = [torch.zeros_like(L.p32) for _ in range(world)]
     torch.distributed.all_gather(pl, L.p32.clone())
     perr = max(float((pl[0] - p).abs().max()) for p in pl[1:])
-    q.put((rank, float((g_dp - g_mean).abs().max()), float(g_mean.abs().max()), perr, ratio_global, ratio_local0))
+    q.put((rank, float((g_dp - g_mean).abs().max()), float(g_mean.abs().max()), perr, stats.numpy(),
+           own, n_valid))
     comm.shutdown()
 
 
@@ -83,12 +92,18 @@ def test_dp_learner_gloo(ar, world):
         for p in procs:
             p.join(timeout=60)
             assert p.exitcode == 0
-    ratios = [r[5] for r in res]
     tol = 1e-6 if ar == "fp32" else 1e-2          # bf16 payload: ~3 significant digits
-    for rank, gerr, gmax, perr, ratio_g, _ in res:
+    res.sort(key=lambda r: r[0])
+    own = np.array([r[5] for r in res])
+    for rank, gerr, gmax, perr, stats, _, _ in res:
         assert gerr <= tol * max(gmax, 1e-6) + 1e-9, (rank, gerr, gmax)
         assert perr == 0.0
-        assert ratio_g == pytest.approx(min(ratios), rel=1e-5)
+        # every rank holds every shard's (total, min p) in rank order
+        np.testing.assert_allclose(stats, own, rtol=1e-6)
+    # every one of the M global draws landed in exactly one shard
+    B, T = 6, own[:, 0]
+    M = min(world * B, int(np.floor((B - 2) * T.sum() / T.max())))
+    assert sum(r[6] for r in res) == M
 
 
 def _elastic_target(comm, attempt, ckdir, out_dir, fail_at):

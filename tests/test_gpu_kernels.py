@@ -88,6 +88,38 @@ def test_sumtree_sampling_frequencies_proportional():
     assert np.abs(emp - p).max() < 3e-3
 
 
+def test_sharded_sample_hip_matches_global_draw():
+    """csrc/sumtree.hip sharded mode vs replay/gpu_replay.py ``global_draw``: same
+    strata, same owner shard per draw, IS weights with the global min and W B / M."""
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard, global_draw
+    W, B, seed, ctr = 3, 64, 11, 5
+    rps = [GpuReplayShard(4096, 4096, 4200, 4, device=DEV, alpha=0.6, beta=0.4, seed=r) for r in range(W)]
+    for r, rp in enumerate(rps):
+        _fill_replay(rp, 700 + 900 * r, seed=r)
+    stats = torch.tensor([[rp.total(), rp.min_leaf()] for rp in rps], dtype=torch.float64)
+    n_valid = 0
+    for r, rp in enumerate(rps):
+        rp.enable_sharding(r, W, seed)
+        rp.shard_stats.copy_(stats.reshape(-1))
+        rp.ctr.fill_(ctr)
+        out = rp.sample(B)
+        torch.cuda.synchronize()
+        u, valid, wscale, pmin = global_draw(stats.numpy(), r, B, seed, ctr)
+        gen = out["gen"].cpu().numpy()
+        np.testing.assert_array_equal(gen >= 0, valid)
+        n_valid += int(valid.sum())
+        leaf = rp.leaf.double().cpu().numpy()
+        c = np.cumsum(leaf)
+        idx = out["idx"].cpu().numpy()[valid]
+        tol = 1e-9 * c[-1]
+        assert np.all(c[idx] - leaf[idx] <= u[valid] + tol) and np.all(u[valid] < c[idx] + tol)
+        w = out["weights"].cpu().numpy()
+        np.testing.assert_allclose(w[valid], np.minimum((leaf[idx] / pmin) ** -0.4, 1.0) * wscale, rtol=1e-5)
+        assert np.all(w[~valid] == 0)
+    T = stats[:, 0].numpy()
+    assert n_valid == min(W * B, int(np.floor((B - 2) * T.sum() / T.max())))
+
+
 def test_sumtree_update_duplicates_last_wins_and_generation():
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
     rp = GpuReplayShard(1000, 1000, 1200, 4, device=DEV, alpha=1.0, eps=0.0)

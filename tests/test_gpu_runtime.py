@@ -74,7 +74,8 @@ def _dp_gpu_worker(rank, world, path, q):
     """One rank of a 2-process data-parallel learner sharing cuda:0 (gloo carries
     the CUDA-tensor all-reduces; RCCL refuses two ranks on one GPU).  Exercises the
     DP step exactly as on a node: three captured HIP-graph segments, async bucket
-    all-reduces waited on the compute stream, the MIN-reduced IS normaliser."""
+    all-reduces waited on the compute stream, the all-gathered shard statistics of
+    the global prioritized replay."""
     import numpy as np
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
@@ -101,7 +102,7 @@ def _dp_gpu_worker(rank, world, path, q):
     pl = [torch.zeros_like(L.p32) for _ in range(world)]
     torch.distributed.all_gather(pl, L.p32.clone())
     ok_finite = bool(torch.isfinite(L.p32).all())
-    q.put((rank, float((pl[0] - pl[1]).abs().max()), ok_finite, float(L.gnorm[0]), float(L.ratio_min[0])))
+    q.put((rank, float((pl[0] - pl[1]).abs().max()), ok_finite, float(L.gnorm[0]), rp.shard_stats.cpu().tolist()))
     comm.shutdown()
 
 
@@ -120,7 +121,7 @@ def test_dp_learner_two_ranks_on_one_gpu(tmp_path):
         assert p.exitcode == 0
     for rank, perr, finite, gnorm, ratio in res:
         assert perr == 0.0 and finite and gnorm > 0      # replicas bit-identical after 4 DP steps
-    assert res[0][4] == res[1][4]                        # same global IS normaliser on both ranks
+    assert res[0][4] == res[1][4]                        # same shard statistics on both ranks
 
 
 @pytest.mark.parametrize("hip,kind", [(True, "impala"), (False, "graph")])
