@@ -136,7 +136,8 @@ class ActorGroup:
         prev = self.payload
         self.payload = self._ingest(obs, done)
         self.builder.step(prev, q, actions, rew, done, self.payload)
-        d = np.nonzero(done)[0]
+        # real game overs only (episodic-life terminals carry NaN / -1 episode info)
+        d = np.nonzero(info.get("real_done", done))[0]
         for e in d:
             self.episodes.append((int(self.builder.env_ids[e]), int(info["episode_length"][e]),
                                   float(info["episode_return"][e])))

@@ -26,6 +26,9 @@ actor's kernels proceed while the learner's step is still executing on the
 compute stream.  Transition inserts (records + sum-tree) stay on the compute
 stream -- single writer, stream-ordered with the learner's sampling and priority
 write-back -- after a wait on the actor stream for the frames they reference.
+The compute stream is the one current when the group is built, so the group can
+step on its own host thread (runtime/actor_thread.py) while the learner thread
+replays its graphs on that stream.
 """
 from __future__ import annotations
 
@@ -77,6 +80,7 @@ class GpuActorGroup:
         self.P = learner.layout.views(self.p32)
         self.Pb = learner.layout.views(self.pbf)
         self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.global_offset = global_offset
         self.payload: Optional[np.ndarray] = None
         self.t = 0
         self.episodes: List[tuple] = []
@@ -85,7 +89,15 @@ class GpuActorGroup:
 
     # ---------------------------------------------------------------- stream
     def _init_stream(self) -> None:
-        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        cuda = self.device.type == "cuda"
+        self.stream = torch.cuda.Stream(self.device) if cuda else None
+        # the learner's stream: inserts go there from whichever thread steps the group
+        self.compute_stream = torch.cuda.current_stream(self.device) if cuda else None
+
+    def _on_compute(self):
+        import contextlib
+        return torch.cuda.stream(self.compute_stream) if self.compute_stream is not None \
+            else contextlib.nullcontext()
 
     def _on_stream(self):
         import contextlib
@@ -99,12 +111,12 @@ class GpuActorGroup:
     def _after_learner(self) -> None:
         """Actor stream waits for everything queued on the compute stream so far."""
         if self.stream is not None:
-            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+            self.stream.wait_stream(self.compute_stream)
 
     def _before_insert(self) -> None:
         """Compute stream waits for the actor stream's frame appends."""
         if self.stream is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            self.compute_stream.wait_stream(self.stream)
 
     # ---------------------------------------------------------------- params
     def sync_params(self) -> None:
@@ -115,6 +127,13 @@ class GpuActorGroup:
     def _copy_params(self) -> None:
         self.p32.copy_(self.learner.p32)
         self.pbf.copy_(self.learner.pbf)
+
+    def reset_episodes(self) -> None:
+        """Drop the partial n-step windows and start fresh episodes (actor restart)."""
+        a = self.cfg.Actor
+        self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64,
+                                          env_id_offset=self.global_offset)
+        self.payload = None
 
     # --------------------------------------------------------------- acting
     def _ingest(self, frames: np.ndarray, reset_mask: np.ndarray) -> np.ndarray:
@@ -162,7 +181,9 @@ class GpuActorGroup:
         prev = self.payload
         self.payload = self._ingest(frames, done)
         self.builder.step(prev, q, actions, rew, done, self.payload)
-        for e in np.nonzero(done)[0]:
+        # an episode ends at a real game over; with episodic-life wrappers a lost
+        # life is a terminal for the n-step targets only (its info is NaN / -1)
+        for e in np.nonzero(info.get("real_done", done))[0]:
             self.episodes.append((int(self.builder.env_ids[e]), int(info["episode_length"][e]),
                                   float(info["episode_return"][e])))
         self.t += 1
@@ -173,7 +194,8 @@ class GpuActorGroup:
             b = self.builder.get()
             if b is not None:
                 self._before_insert()
-                self.replay.insert(b)
+                with self._on_compute():
+                    self.replay.insert(b)
                 n = len(b["A_t"])
                 self.inserted += n
         return n
@@ -207,6 +229,7 @@ class GraphActorGroup(GpuActorGroup):
         if d.type == "cuda":
             self.q_host, self.a_host = self.q_host.pin_memory(), self.a_host.pin_memory()
         self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.global_offset = global_offset
         self.payload = None
         self.t = 0
         self.episodes = []
@@ -259,6 +282,7 @@ class ImpalaActorGroup(GpuActorGroup):
         if d.type == "cuda":
             self.q_host, self.a_host = self.q_host.pin_memory(), self.a_host.pin_memory()
         self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
+        self.global_offset = global_offset
         self.payload = None
         self.t = 0
         self.episodes = []

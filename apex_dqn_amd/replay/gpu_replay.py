@@ -35,6 +35,7 @@ uniforms as the kernel, so the global draw is bit-identical).
 from __future__ import annotations
 
 import math
+import threading
 from typing import Dict, Optional
 
 import numpy as np
@@ -172,6 +173,10 @@ class GpuReplayShard:
         # write-back is caught by the generation check.
         self.version = 0
         self.min_frame_seq = np.full(self.cap, -1, np.int64)  # oldest frame referenced per slot
+        # host-state lock: an actor thread appends / inserts while the learner thread
+        # evicts (runtime/actor_thread.py); the kernels each section enqueues land on the
+        # stream in the order the sections run
+        self.lock = threading.RLock()
         self._tdesc = None
         self._rdesc = None
         # sharding (enable_sharding): all-gathered (total, min p) of every shard, fp64
@@ -241,6 +246,21 @@ class GpuReplayShard:
     # --------------------------------------------------------------- insert
     def append_frames(self, frames) -> np.ndarray:
         """Store new frames (n, H, W) uint8; returns their sequence numbers."""
+        with self.lock:
+            return self._append_frames_locked(frames)
+
+    def insert(self, batch: Dict[str, np.ndarray]) -> np.ndarray:
+        """Insert n-step transitions whose S_t/S_tpn payloads are frame seqs (K, C)."""
+        with self.lock:
+            return self._insert_locked(batch)
+
+    def remove_to_fit(self) -> int:
+        """FIFO eviction to soft_capacity + drop slots whose frames were overwritten."""
+        with self.lock:
+            return self._remove_to_fit_locked()
+
+    def _append_frames_locked(self, frames) -> np.ndarray:
+        """Store new frames (n, H, W) uint8; returns their sequence numbers."""
         frames = torch.as_tensor(frames)
         n = frames.shape[0]
         seqs = self.frame_head + np.arange(n, dtype=np.int64)
@@ -262,7 +282,7 @@ class GpuReplayShard:
         self.frame_head += n
         return seqs
 
-    def insert(self, batch: Dict[str, np.ndarray]) -> np.ndarray:
+    def _insert_locked(self, batch: Dict[str, np.ndarray]) -> np.ndarray:
         """Insert n-step transitions whose S_t/S_tpn payloads are frame seqs (K, C)."""
         K = len(batch["A_t"])
         if K == 0:
@@ -429,7 +449,7 @@ class GpuReplayShard:
             if bump_ctr:
                 self.ctr += 1
 
-    def remove_to_fit(self) -> int:
+    def _remove_to_fit_locked(self) -> int:
         """FIFO eviction to soft_capacity + drop slots whose frames were overwritten."""
         self.version += 1
         excess = self.live - self.soft_capacity

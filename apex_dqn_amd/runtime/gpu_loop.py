@@ -11,9 +11,11 @@ checkpoints, JSONL metrics, synchronized start across ranks.
 """
 from __future__ import annotations
 
+import collections
 import os
+import sys
 import time
-from typing import Any, Dict, Optional
+from typing import Any, Deque, Dict, Optional
 
 import numpy as np
 import torch
@@ -50,7 +52,15 @@ def _start_torch_profiler(device):
 def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                  metrics: Optional[MetricsLogger] = None, num_envs: Optional[int] = None,
                  actor_steps_per_update: int = 1, max_actor_steps: Optional[int] = None,
-                 backend: Optional[str] = None) -> Dict[str, Any]:
+                 backend: Optional[str] = None, async_actors: Optional[bool] = None) -> Dict[str, Any]:
+    """Train for ``learner_steps`` updates.  Actors stop after ``max_actor_steps``
+    group steps (default ``Actor.T``: every env takes T steps, ``actor.py:159``); the
+    learner keeps going on the replay, as the reference's learner process does.
+
+    ``async_actors`` (default ``Runtime.async_actors``): the actor group steps on its
+    own host thread (runtime/actor_thread.py) once the replay holds
+    ``min_replay_mem_size``; otherwise actor and learner alternate
+    (``actor_steps_per_update`` group steps per update; deterministic, for tests)."""
     device = torch.device(device)
     rank = comm.rank if comm is not None else 0
     world = comm.world_size if comm is not None else 1
@@ -66,82 +76,166 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     else:   # graph-captured torch-autograd learner on the same HBM replay
         from ..learner.graph_learner import GraphLearner
         learner = GraphLearner(cfg, device, replay, comm=comm)
-    group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed)
-    min_local = max(L.min_replay_mem_size // world, L.replay_sample_size)
-    started = False
-    t0 = time.time()
-    actor_steps = 0
-    max_actor_steps = max_actor_steps or 10 ** 12
-    losses = []
     ckpt_path = os.path.join(rt.ckpt_dir, "checkpoint.pt") if rt.ckpt_dir else None
     # restart after a learner-rank failure (torchrun --max-restarts / run_elastic):
-    # every rank resumes the same checkpoint, so the DP replicas stay identical
+    # every rank resumes the same checkpoint, so the DP replicas stay identical.
+    # Loaded before the actor group is built: its parameter slot copies the learner's.
     if ckpt_path and rt.resume and os.path.exists(ckpt_path):
         learner.load(ckpt_path)
         if metrics is not None:
             metrics.log("resume", step=learner.num_q_updates, path=ckpt_path)
-    prof = None
-    n_ep_seen = 0
-    t_last, n_last, ins_last, steps_last = t0, learner.num_q_updates, 0, 0
-    while learner.num_q_updates < learner_steps and actor_steps < max_actor_steps:
-        for _ in range(actor_steps_per_update):
+    group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed)
+    min_local = max(L.min_replay_mem_size // world, L.replay_sample_size)
+    max_actor_steps = int(max_actor_steps if max_actor_steps is not None else cfg.Actor.T)
+    if async_actors is None:
+        async_actors = bool(rt.async_actors) and device.type == "cuda"
+    t0 = time.time()
+    st = _LoopState(t0, learner.num_q_updates)
+    # ---- fill: the actors alone until every shard holds min_replay_mem_size / world
+    while True:
+        if st.actor_steps < max_actor_steps:
             group.step()
-            actor_steps += 1
-        if not started:
-            ready = float(replay.size() > min_local)
-            if comm is not None and comm.active:
-                ready = comm.allreduce_scalar(ready, "min")
-            if ready < 1.0:
-                continue
-            started = True
-            learner.refresh_replay_stats()
-        if rt.torch_profile_dir and learner.num_q_updates == rt.torch_profile_start and prof is None:
-            prof = _start_torch_profiler(device)
-        learner.step()
-        n = learner.num_q_updates
-        if prof is not None and n >= rt.torch_profile_start + rt.torch_profile_steps:
-            prof.stop()
-            os.makedirs(rt.torch_profile_dir, exist_ok=True)
-            prof.export_chrome_trace(os.path.join(rt.torch_profile_dir, f"trace_rank{rank}.json"))
-            prof, rt.torch_profile_dir = None, None
-        if n % L.remove_old_xp_freq == 0:
-            replay.remove_to_fit()
-            replay.rebuild()
-            learner.refresh_replay_stats()
-        if rt.log_every and n % rt.log_every == 0:
-            m = learner.last_metrics()
-            losses.append(m["loss"])
-            if metrics is not None:
-                now = time.time()
-                dt = max(now - t_last, 1e-9)
-                eps_ = group.eps.float()
-                new_eps = group.episodes[n_ep_seen:]
-                rets = [r for (_, _, r) in group.episodes[-50:]]
-                lens = [ln for (_, ln, _) in group.episodes[-50:]]
-                metrics.log("learner", step=n, loss=m["loss"], td_abs=m["td_abs_mean"], grad_norm=m["grad_norm"],
-                            is_weight_mean=float(learner.S["weights"].mean()),
-                            learner_kind=getattr(learner, "kind", "fused"),
-                            replay=replay.size(), actor_steps=actor_steps, inserted=group.inserted,
-                            episodes=len(group.episodes),
-                            mean_return=float(np.mean(rets)) if rets else float("nan"),
-                            mean_ep_len=float(np.mean(lens)) if lens else float("nan"),
-                            eps_min=float(eps_.min()), eps_max=float(eps_.max()),
-                            grad_steps_per_s=(n - n_last) / dt,
-                            env_frames_per_s=(actor_steps - steps_last) * group.E * world / dt,
-                            inserts_per_s=(group.inserted - ins_last) * world / dt,
-                            steps_per_s=n / max(now - t0, 1e-9))
-                for (env_id, ep_len, ep_ret) in new_eps[:rt.episode_lines_per_log]:
-                    metrics.episode(env_id, actor_steps, ep_len, ep_ret)
-                n_ep_seen = len(group.episodes)
-                if rt.profile_phases and device.type == "cuda":
-                    metrics.log("phases_ms", step=n, **learner.profile_step())
-                t_last, n_last, ins_last, steps_last = time.time(), learner.num_q_updates, group.inserted, actor_steps
-        if ckpt_path and rt.ckpt_freq and n % rt.ckpt_freq == 0 and rank == 0:
-            learner.save(ckpt_path)
-    if device.type == "cuda":
+            st.actor_steps += 1
+        ready = float(replay.size() > min_local or st.actor_steps >= max_actor_steps)
+        if comm is not None and comm.active:
+            ready = comm.allreduce_scalar(ready, "min")
+        if ready >= 1.0:
+            break
+    learner.refresh_replay_stats()
+    runner = None
+    if async_actors:
+        from .actor_thread import ActorRunner
+        # every graph the loop replays is captured before the actor thread starts
+        # launching work (a capture must not see other threads' launches)
+        if hasattr(learner, "prepare_graphs"):
+            learner.prepare_graphs()
+        runner = ActorRunner(group, max_actor_steps - st.actor_steps, timeout=rt.heartbeat_timeout,
+                             on_event=(lambda kind, **kw: metrics.log(kind, **kw)) if metrics is not None else None)
+        st.actor_base = st.actor_steps
+        st.runner = runner
+        old_switch = sys.getswitchinterval()
+        sys.setswitchinterval(5e-4)      # the learner thread only needs the GIL briefly per chunk
+        runner.start()
+    prof = None
+    inflight: Deque = collections.deque()
+    on_cuda = device.type == "cuda"
+    try:
+        while learner.num_q_updates < learner_steps:
+            n = learner.num_q_updates
+            if runner is not None:
+                runner.check()
+                st.actor_steps = st.actor_base + runner.steps
+                # chunk: up to the next eviction / log / checkpoint / profiler boundary
+                k = min(learner_steps - n, _to_boundary(n, L.remove_old_xp_freq),
+                        _to_boundary(n, rt.log_every) if rt.log_every else learner_steps,
+                        _to_boundary(n, rt.ckpt_freq) if (ckpt_path and rt.ckpt_freq) else learner_steps,
+                        max(1, 2 * int(getattr(rt, "graph_steps", 1) or 1)))
+                if rt.torch_profile_dir and prof is None and n < rt.torch_profile_start:
+                    k = min(k, rt.torch_profile_start - n)
+            else:
+                for _ in range(actor_steps_per_update):
+                    if st.actor_steps < max_actor_steps:
+                        group.step()
+                        st.actor_steps += 1
+                k = 1
+            if rt.torch_profile_dir and learner.num_q_updates == rt.torch_profile_start and prof is None:
+                prof = _start_torch_profiler(device)
+            if runner is not None and not on_cuda:
+                with replay.lock:       # CPU tensors: no stream ordering between the threads
+                    _learn(learner, k)
+            else:
+                _learn(learner, k)
+            if runner is not None and on_cuda:
+                # at most two chunks queued: the actor's inserts never wait long behind them
+                ev = torch.cuda.Event()
+                ev.record()
+                inflight.append(ev)
+                while len(inflight) > 2:
+                    inflight.popleft().synchronize()
+            n = learner.num_q_updates
+            if prof is not None and n >= rt.torch_profile_start + rt.torch_profile_steps:
+                prof.stop()
+                os.makedirs(rt.torch_profile_dir, exist_ok=True)
+                prof.export_chrome_trace(os.path.join(rt.torch_profile_dir, f"trace_rank{rank}.json"))
+                prof, rt.torch_profile_dir = None, None
+            if n % L.remove_old_xp_freq == 0:
+                replay.remove_to_fit()
+                replay.rebuild()
+                learner.refresh_replay_stats()
+            if rt.log_every and n % rt.log_every == 0:
+                if runner is not None:
+                    st.actor_steps = st.actor_base + runner.steps
+                _log(metrics, learner, group, replay, st, rt, world, device)
+            if ckpt_path and rt.ckpt_freq and n % rt.ckpt_freq == 0 and rank == 0:
+                learner.save(ckpt_path)
+    finally:
+        if runner is not None:
+            runner.stop()
+            st.actor_steps = st.actor_base + runner.steps
+            sys.setswitchinterval(old_switch)
+    if on_cuda:
         torch.cuda.synchronize(device)
     rets = [r for (_, _, r) in group.episodes]
-    return {"learner": learner, "replay": replay, "actors": group, "losses": losses,
-            "episodes": group.episodes, "actor_steps": actor_steps,
+    return {"learner": learner, "replay": replay, "actors": group, "losses": st.losses,
+            "episodes": group.episodes, "actor_steps": st.actor_steps,
+            "actor_restarts": runner.restarts if runner is not None else 0,
             "mean_return_last": float(np.mean(rets[-20:])) if rets else float("nan"),
             "wall_s": time.time() - t0}
+
+
+class _LoopState:
+    def __init__(self, t0: float, n0: int):
+        self.t0 = t0
+        self.actor_steps = 0
+        self.actor_base = 0
+        self.runner = None
+        self.losses = []
+        self.n_ep_seen = 0
+        self.t_last, self.n_last, self.ins_last, self.steps_last = t0, n0, 0, 0
+
+
+def _to_boundary(n: int, every: int) -> int:
+    return every - n % every if every and every > 0 else 1 << 62
+
+
+def _learn(learner, k: int) -> None:
+    if k > 1 and hasattr(learner, "steps"):
+        learner.steps(k)
+    else:
+        for _ in range(k):
+            learner.step()
+
+
+def _log(metrics, learner, group, replay, st: "_LoopState", rt, world: int, device) -> None:
+    m = learner.last_metrics()
+    st.losses.append(m["loss"])
+    if metrics is None:
+        return
+    n = learner.num_q_updates
+    now = time.time()
+    dt = max(now - st.t_last, 1e-9)
+    eps_ = group.eps.float()
+    eps_list = list(group.episodes)
+    new_eps = eps_list[st.n_ep_seen:]
+    rets = [r for (_, _, r) in eps_list[-50:]]
+    lens = [ln for (_, ln, _) in eps_list[-50:]]
+    metrics.log("learner", step=n, loss=m["loss"], td_abs=m["td_abs_mean"], grad_norm=m["grad_norm"],
+                is_weight_mean=float(learner.S["weights"].mean()),
+                learner_kind=getattr(learner, "kind", "fused"),
+                replay=replay.size(), actor_steps=st.actor_steps, inserted=group.inserted,
+                episodes=len(eps_list),
+                mean_return=float(np.mean(rets)) if rets else float("nan"),
+                mean_ep_len=float(np.mean(lens)) if lens else float("nan"),
+                eps_min=float(eps_.min()), eps_max=float(eps_.max()),
+                grad_steps_per_s=(n - st.n_last) / dt,
+                env_frames_per_s=(st.actor_steps - st.steps_last) * group.E * world / dt,
+                inserts_per_s=(group.inserted - st.ins_last) * world / dt,
+                steps_per_s=n / max(now - st.t0, 1e-9),
+                actor_thread=st.runner is not None,
+                actor_restarts=st.runner.restarts if st.runner is not None else 0)
+    for (env_id, ep_len, ep_ret) in new_eps[:rt.episode_lines_per_log]:
+        metrics.episode(env_id, st.actor_steps, ep_len, ep_ret)
+    st.n_ep_seen = len(eps_list)
+    if rt.profile_phases and device.type == "cuda":
+        metrics.log("phases_ms", step=n, **learner.profile_step())
+    st.t_last, st.n_last, st.ins_last, st.steps_last = time.time(), n, group.inserted, st.actor_steps

@@ -244,8 +244,10 @@ def test_ddqn_head_prio_matches_head_plus_tree_update():
     torch.testing.assert_close(n1, n0, rtol=1e-12, atol=1e-9)
 
 
-def test_rmsprop_sample_matches_separate_launches():
-    """Optimizer launch carrying the next batch's draw == rmsprop + tree_sample."""
+@pytest.mark.parametrize("sharded", [False, True])
+def test_rmsprop_sample_matches_separate_launches(sharded):
+    """Optimizer launch carrying the next batch's draw == rmsprop + tree_sample
+    (also in sharded mode: rank 1 of 3 shards of one global replay)."""
     from apex_dqn_amd.ops.fused_ops import HipBackend
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
     n, B = 100_003, 128
@@ -253,6 +255,10 @@ def test_rmsprop_sample_matches_separate_launches():
     p0, gr = torch.randn(n, generator=g).to(DEV), torch.randn(n, generator=g).to(DEV) * 1e-2
     rp = GpuReplayShard(2000, 2000, 2100, 4, device=DEV, seed=4)
     _fill_replay(rp, 1500, seed=2)
+    if sharded:
+        rp.enable_sharding(1, 3, 99)
+        t = rp.total()
+        rp.shard_stats.copy_(torch.tensor([0.7 * t, 0.05, t, rp.min_leaf(), 1.6 * t, 0.2], dtype=torch.float64))
     be = HipBackend()
     res = {}
     for fused in (False, True):
@@ -263,7 +269,7 @@ def test_rmsprop_sample_matches_separate_launches():
         nxt2 = torch.zeros(B, 4, dtype=torch.int32, device=DEV)
         args = (p, gr, v, m, pbf, 2.5e-4, 0.95, 1.5e-7, 40.0, True, part, gn)
         if fused:
-            be.optimizer(*args, sample=(rp, B, S, None, nxt2))
+            be.optimizer(*args, sample=(rp, B, S, nxt2))
         else:
             be.optimizer(*args)
             rp.sample(B, out=S, nxt2=nxt2)

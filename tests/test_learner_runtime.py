@@ -187,3 +187,77 @@ def test_image_learner_loops_on_cpu(tmp_path, net, hip, kind):
         assert L.Q.state_dict()[next(iter(L.Q.state_dict()))].data_ptr() >= L.p32.data_ptr()
     out2 = train_frames(cfg, "cpu", 10)          # resumes the step-6 checkpoint
     assert out2["learner"].num_q_updates == 10
+
+
+def _small_image_cfg(**rt):
+    return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 4, "name": "Synthetic"},
+                                 "Actor": {"num_actors": 6, "n_step_transition_batch_size": 6,
+                                           "Q_network_sync_freq": 5},
+                                 "Learner": {"min_replay_mem_size": 40, "replay_sample_size": 8,
+                                             "remove_old_xp_freq": 4, "q_target_sync_freq": 5},
+                                 "Replay_Memory": {"soft_capacity": 120},
+                                 "Runtime": {"replay_capacity": 150, "log_every": 4, "use_graphs": False, **rt}})
+
+
+def test_gpu_loop_async_actor_thread_on_cpu(tmp_path):
+    """The actor group steps on its own thread while the learner trains (reference
+    main.py:46-58 runs actors and learner concurrently)."""
+    from apex_dqn_amd.runtime.gpu_loop import train_frames
+    from apex_dqn_amd.utils.metrics import MetricsLogger
+    mpath = str(tmp_path / "m.jsonl")
+    ml = MetricsLogger(mpath)
+    out = train_frames(_small_image_cfg(), "cpu", 16, metrics=ml, async_actors=True)
+    ml.close()
+    assert out["learner"].num_q_updates == 16
+    assert out["actor_steps"] > 0 and out["actors"].inserted >= 40
+    import json
+    lrn = [json.loads(x) for x in open(mpath) if '"learner"' in x]
+    assert lrn and lrn[-1]["actor_thread"] is True and lrn[-1]["actor_restarts"] == 0
+
+
+def test_actor_T_bounds_env_steps():
+    """Actor.T (reference actor.py:104,159) stops the actors; the learner finishes its steps."""
+    from apex_dqn_amd.runtime.gpu_loop import train_frames
+    cfg = _small_image_cfg()
+    cfg.Actor.T = 12
+    out = train_frames(cfg, "cpu", 10)
+    assert out["actor_steps"] == 12 and out["learner"].num_q_updates == 10
+    out = train_frames(cfg, "cpu", 10, async_actors=True)
+    assert out["actor_steps"] == 12 and out["learner"].num_q_updates == 10
+
+
+class _FlakyGroup:
+    def __init__(self, fail_at=3, sleep_at=None):
+        self.n, self.fail_at, self.sleep_at, self.resets = 0, fail_at, sleep_at, 0
+
+    def step(self):
+        import time
+        self.n += 1
+        if self.n == self.fail_at:
+            raise ValueError("env crashed")
+        if self.sleep_at is not None and self.n >= self.sleep_at:
+            time.sleep(0.5)
+        time.sleep(0.001)
+
+    def reset_episodes(self):
+        self.resets += 1
+
+
+def test_actor_runner_restarts_crashed_thread_and_detects_stall():
+    import time
+    from apex_dqn_amd.runtime.actor_thread import ActorRunner
+    g = _FlakyGroup(fail_at=3)
+    events = []
+    r = ActorRunner(g, 50, timeout=5.0, on_event=lambda k, **kw: events.append(k)).start()
+    t0 = time.time()
+    while not r.done and time.time() - t0 < 20:
+        r.check()
+        time.sleep(0.005)
+    r.stop()
+    assert r.done and r.restarts == 1 and g.resets == 1 and events == ["actor_restart"]
+    g2 = _FlakyGroup(fail_at=-1, sleep_at=2)
+    r2 = ActorRunner(g2, 100, timeout=0.2).start()
+    time.sleep(0.8)
+    with pytest.raises(RuntimeError, match="stalled"):
+        r2.check()
+    r2.stop()
