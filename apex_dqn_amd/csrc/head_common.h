@@ -1,9 +1,8 @@
 // Device code shared by the dueling-head kernels: the q-values of one activation
 // row (head_row) and the fused DDQN loss / priority / head-backward body
-// (ddqn_head_body), used by csrc/ddqn_head.hip (ddqn_head_kernel) and by
-// csrc/sumtree.hip (ddqn_head_prio_kernel: the same body + the priority
-// write-back into the sum-tree), and the head weight gradient (head_wgrad_body,
-// also run by sumtree.hip head_wgrad_prio_kernel beside the tree update).
+// (ddqn_head_body), used by csrc/ddqn_head.hip (ddqn_head_kernel), and the head
+// weight gradient (head_wgrad_body, run by csrc/sumtree.hip head_wgrad_prio_kernel
+// and fc_wgrad_head_prio_kernel beside the priority write-back).
 #pragma once
 #include "apex_common.h"
 

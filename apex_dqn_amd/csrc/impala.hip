@@ -52,7 +52,6 @@ struct SconvDesc {
   int relu_in, relu_out;
   float scale;                // applied to the accumulator before the bias
   int pad0;                   // POOL: argmax codes for images < pad0 only (0 = all)
-  const uint8_t* amax_in;     // MODE 4: argmax codes of the pooled gradient x (same image stride, bytes)
 };
 
 struct SconvWgDesc {
@@ -64,7 +63,6 @@ struct SconvWgDesc {
   int64_t dy_img, x_img;
   int N, relu_in;
   int imgs_per_group, cin_real;
-  const uint8_t* dy_amax;     // DYP: dy is the POOLED gradient, these its argmax codes (dy_img bytes/image)
 };
 
 __device__ __forceinline__ uint4 relu_u4(uint4 v) {
@@ -73,9 +71,8 @@ __device__ __forceinline__ uint4 relu_u4(uint4 v) {
 
 // Gradient of a pre-pool conv output (h, w), channels 8 hf .. 8 hf + 7 of plane p,
 // from the pooled gradient dp and argmax codes am of one image (3x3 / s2 / pad 1):
-// the sum over the <= 4 windows whose argmax is (h, w).  The max-pool backward as
-// a gather, evaluated where the consumer stages its operand, so the
-// full-resolution gradient is never written to HBM.
+// the sum over the <= 4 windows whose argmax is (h, w): the max-pool backward as a
+// gather, one output element per thread, no atomics (maxpool_bwd_kernel).
 template <int H, int W>
 __device__ __forceinline__ uint4 pool_grad8(const bf16_t* __restrict__ dp, const uint8_t* __restrict__ am, int p,
                                             int h, int w, int hf) {
@@ -121,8 +118,7 @@ __device__ __forceinline__ uint4 pool_grad8(const bf16_t* __restrict__ dp, const
 // thread has BATCH global loads in flight instead of one load-use round trip.
 template <int P, int H, int W, int SROWS, int MODE, int NTHR, int BATCH>
 __device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const void* x, int64_t x_img,
-                                           const int32_t* slots, int n, int row0, int relu, int tid,
-                                           const uint8_t* amax = nullptr) {
+                                           const int32_t* slots, int n, int row0, int relu, int tid) {
   constexpr int WP = W + 2, BLK = SROWS * WP;
   if constexpr (MODE == 2) {
     const uint8_t* ring = reinterpret_cast<const uint8_t*>(x);
@@ -166,12 +162,8 @@ __device__ __forceinline__ void stage_rows(uint8_t* xs, int plane_pix, const voi
         const int lr = rem / WP, c = rem - (rem / WP) * WP;
         const int h = row0 + lr, w = c - 1;
         v[k] = make_uint4(0, 0, 0, 0);
-        if (i < NCK && h >= 0 && h < H && w >= 0 && w < W) {
-          if constexpr (MODE == 4)   // x = pooled gradient of this (pre-pool) tensor
-            v[k] = pool_grad8<H, W>(xi, amax + (int64_t)n * x_img, p, h, w, hf);
-          else
-            v[k] = *reinterpret_cast<const uint4*>(xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
-        }
+        if (i < NCK && h >= 0 && h < H && w >= 0 && w < W)
+          v[k] = *reinterpret_cast<const uint4*>(xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
       }
 #pragma unroll
       for (int k = 0; k < BATCH; ++k) {
@@ -273,8 +265,7 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
   if constexpr (MODE == 3)
     stage_ring4<H, W, SROWS, NTHR>(xs, PLANE, reinterpret_cast<const uint8_t*>(d.x), d.slots, n, o0 - 1, tid);
   else
-    stage_rows<P, H, W, SROWS, MODE, NTHR, 8>(xs, PLANE, d.x, d.x_img, d.slots, n, o0 - 1, d.relu_in, tid,
-                                              d.amax_in);
+    stage_rows<P, H, W, SROWS, MODE, NTHR, 8>(xs, PLANE, d.x, d.x_img, d.slots, n, o0 - 1, d.relu_in, tid);
   __syncthreads();
 
   // per-lane LDS byte offset of each K chunk: lane group kg = lane >> 4 reads
@@ -615,7 +606,7 @@ __device__ __forceinline__ bf16x8 tr_pix_frag(const uint8_t* plane, int pix0, in
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int CIN, int COUT, int H, int W, int R, int MODE, int DYP>
+template <int CIN, int COUT, int H, int W, int R, int MODE>
 __global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
   constexpr int P = CIN / 16, NT = COUT / 16;
   constexpr int WP = W + 2;
@@ -656,8 +647,7 @@ __global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
         const int h = r0 + lh;
         v[k] = make_uint4(0, 0, 0, 0);
         if (i < NDC && lh < R && w < W && h < H)
-          v[k] = DYP ? pool_grad8<H, W>(dyi, d.dy_amax + (int64_t)n * d.dy_img, p, h, w, hf)
-                     : *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+          v[k] = *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
       }
 #pragma unroll
       for (int k = 0; k < DB; ++k) {
@@ -911,8 +901,6 @@ __global__ void __launch_bounds__(256) sconv_pack_kernel(PackDesc d) {
   X(16, 16, 42, 42, 42, 0, 0)   \
   X(16, 32, 42, 42, 42, 0, 0)   \
   X(32, 16, 42, 42, 21, 0, 0)   \
-  X(32, 16, 42, 42, 21, 4, 0)   \
-  X(32, 32, 21, 21, 21, 4, 0)   \
   X(32, 32, 21, 21, 21, 0, 0)   \
   X(32, 32, 11, 11, 11, 0, 0)
 
@@ -932,18 +920,15 @@ APEX_EXPORT int apex_sconv_fwd(SconvDesc d, int cin, int cout, int H, int W, int
 }
 
 // wgrad bands (LDS: dY band + x band with halo; 2 workgroups per CU)
-#define SCONV_WG_SHAPES(X)      \
-  X(16, 16, 84, 84, 12, 2, 1)   \
-  X(16, 16, 84, 84, 12, 2, 0)   \
-  X(16, 16, 42, 42, 21, 0, 0)   \
-  X(16, 32, 42, 42, 14, 0, 1)   \
-  X(16, 32, 42, 42, 14, 0, 0)   \
-  X(32, 32, 21, 21, 21, 0, 1)   \
-  X(32, 32, 21, 21, 21, 0, 0)   \
-  X(32, 32, 11, 11, 11, 0, 0)
+#define SCONV_WG_SHAPES(X)   \
+  X(16, 16, 84, 84, 12, 2)   \
+  X(16, 16, 42, 42, 21, 0)   \
+  X(16, 32, 42, 42, 14, 0)   \
+  X(32, 32, 21, 21, 21, 0)   \
+  X(32, 32, 11, 11, 11, 0)
 
 APEX_EXPORT int apex_sconv_wgrad_bands(int cin, int cout, int H, int W, int mode) {
-#define SCONV_WG_BANDS(CI, CO, HH, WW, RR, MM, DP) \
+#define SCONV_WG_BANDS(CI, CO, HH, WW, RR, MM) \
   if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) return (HH + RR - 1) / RR;
   SCONV_WG_SHAPES(SCONV_WG_BANDS)
 #undef SCONV_WG_BANDS
@@ -953,9 +938,9 @@ APEX_EXPORT int apex_sconv_wgrad_bands(int cin, int cout, int H, int W, int mode
 APEX_EXPORT int apex_sconv_wgrad(SconvWgDesc d, int cin, int cout, int H, int W, int mode, int groups,
                                  hipStream_t st) {
   if (d.N <= 0 || groups <= 0) return (int)hipErrorInvalidValue;
-#define SCONV_WG_CASE(CI, CO, HH, WW, RR, MM, DP)                                                       \
-  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM && (d.dy_amax != nullptr) == (DP != 0)) { \
-    sconv_wgrad_kernel<CI, CO, HH, WW, RR, MM, DP><<<dim3((HH + RR - 1) / RR, groups), 256, 0, st>>>(d);   \
+#define SCONV_WG_CASE(CI, CO, HH, WW, RR, MM)                                                          \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) {                                   \
+    sconv_wgrad_kernel<CI, CO, HH, WW, RR, MM><<<dim3((HH + RR - 1) / RR, groups), 256, 0, st>>>(d);     \
     APEX_CHECK_LAUNCH();                                                                                \
   }
   SCONV_WG_SHAPES(SCONV_WG_CASE)

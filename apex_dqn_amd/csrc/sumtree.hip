@@ -438,70 +438,6 @@ __global__ void gather_frames_kernel(const uint8_t* __restrict__ ring, const int
 // critical path (a lone tree_update / tree_sample launch is a few waves running
 // dependent global loads while the rest of the chip idles).
 
-struct PrioArgs {
-  TreeDesc t;
-  const int64_t* idx;        // sampled leaves of the batch [B]
-  const int32_t* gen_expect; // their slot generations at sampling time (or null)
-  const int32_t* gen;        // current slot generations
-  uint64_t* ctr_to_bump;     // sampler RNG counter (+1 per update batch, as tree_update)
-  float alpha, eps;
-  int B;
-};
-
-// ddqn_head + priority write-back.  Wave 0 of block b, after the head body, writes
-// leaf idx[b] = (|delta_b| + eps)^alpha unless a later sample of the batch has the
-// same leaf (last occurrence wins, as tree_update's dedupe), the slot was evicted
-// (leaf 0) or re-used since sampling (generation), then adds the fp64 delta to the
-// leaf's ancestors with hardware atomics and folds the value into the running min.
-template <int HS>
-__global__ void __launch_bounds__(192) ddqn_head_prio_kernel(
-    const bf16_t* __restrict__ Hon, const bf16_t* __restrict__ Htg, HeadParams Pon, HeadParams Ptg,
-    const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
-    const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
-    float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
-    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, PrioArgs pr,
-    HeadLo lo) {
-  // wave 0 issues the write-back's loads (the leaf index, the dedupe scan of the
-  // later samples, the leaf and its generations) before the head body, so their
-  // latency hides under the head math instead of trailing it
-  const int lane = threadIdx.x & 63, b = blockIdx.x;
-  const TreeDesc& t = pr.t;
-  int64_t s = 0;
-  bool dup = false, live = false;
-  float old = 0.f;
-  if (threadIdx.x < 64) {
-    s = pr.idx[b];
-    for (int j0 = b + 1; j0 < pr.B; j0 += 512) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int j = j0 + 64 * k + lane;
-        if (j < pr.B) dup |= pr.idx[j] == s;
-      }
-    }
-    if (lane == 0 && APEX_DBG_OK(s, t.n[0], 0)) {
-      old = t.leaf[s];
-      live = old > 0.f && (pr.gen_expect == nullptr || pr.gen[s] == pr.gen_expect[b]);
-    }
-  }
-  float ad;
-  if (!ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs, loss,
-                          q_out, dH, dhead, zero_ptr, zero_n, &ad, lo))
-    return;
-  if (b == 0 && lane == 0 && pr.ctr_to_bump != nullptr) pr.ctr_to_bump[0] += 1;
-  if (__ballot(dup) != 0ull || lane != 0 || !live) return;
-  const float v = powf(ad + pr.eps, pr.alpha);
-  t.leaf[s] = v;
-  const double d = (double)v - (double)old;
-  if (d != 0.0) {
-    int64_t node = s;
-    for (int k = 1; k <= t.L; ++k) {
-      node >>= 6;
-      atomicAdd(&t.nodes[t.off[k] + node], d);
-    }
-  }
-  if (v > 0.f) atomicMin(t.min_bits, __float_as_uint(v));
-}
-
 // Single-block priority write-back (tree_update mode 1 with dedupe) for n <= 1024
 // leaves and n <= TU_MAXR * blockDim (the launchers check both): items tid,
 // tid + blockDim, ...; the LDS hash keeps the last occurrence of a duplicated leaf;
@@ -610,7 +546,7 @@ __global__ void __launch_bounds__(256) fc_wgrad_head_prio_kernel(WgradDesc d, in
 
 // optimizer + the next step's prioritized draw: blocks [0, nsb) sample, the rest
 // run the clip + centered RMSprop + bf16 pack over the flat parameters.  The tree
-// already holds this step's priorities (written by ddqn_head_prio_kernel), so the
+// already holds this step's priorities (written by fc_wgrad_head_prio_kernel), so the
 // draw equals the one a sample launch at the head of the next step would make.
 template <int NT>
 __global__ void __launch_bounds__(NT) rmsprop_sample_kernel(RmspropArgs a, SampleArgs s, int nsb) {
@@ -721,27 +657,6 @@ APEX_EXPORT int apex_debug_errors(int* counts, long long* first, int reset) {
   }
   return 0;
 #endif
-}
-
-APEX_EXPORT int apex_ddqn_head_prio(const bf16_t* Hon, const bf16_t* Htg, HeadParams Pon, HeadParams Ptg,
-                                    const int32_t* act, const float* rew, const float* gam, const float* isw,
-                                    int B, int A, int huber, float kappa, float grad_scale, float* td_abs,
-                                    float* loss, float* q_out, bf16_t* dH, float* dhead, float* zero_ptr,
-                                    int zero_n, int hidden, TreeDesc t, const int64_t* idx,
-                                    const int32_t* gen_expect, const int32_t* gen, float alpha, float eps,
-                                    uint64_t* ctr_to_bump, HeadLo lo, hipStream_t st) {
-  if (A < 1 || A > HEAD_MAXA || B < 1 || idx == nullptr) return (int)hipErrorInvalidValue;
-  if (lo.Hon != nullptr && (lo.Htg == nullptr || lo.dH == nullptr)) return (int)hipErrorInvalidValue;
-  const PrioArgs pr{t, idx, gen_expect, gen, ctr_to_bump, alpha, eps, B};
-  if (hidden == 512)
-    ddqn_head_prio_kernel<512><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
-                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr, lo);
-  else if (hidden == 256)
-    ddqn_head_prio_kernel<256><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
-                                                  grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, pr, lo);
-  else
-    return (int)hipErrorInvalidValue;
-  APEX_CHECK_LAUNCH();
 }
 
 // rmsprop (clip norm from `npart` partials, as apex_rmsprop_step_np) + tree_sample of B

@@ -45,7 +45,7 @@ from ..models.dueling import DuellingDQN
 from ..models.flat_params import (FlatLayout, flat_to_reference_state, nature_segments,
                                   reference_state_to_flat)
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
-from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
 
 
 def _enable_sharding(replay, comm, rt) -> None:
@@ -554,6 +554,8 @@ class FusedNatureLearner:
         ck = load_checkpoint(path)
         if ck is None:
             return False
+        if adopt_obs_scale(ck, self.rt):
+            self._graphs = self._multi = None    # the input scale is a kernel argument: recapture
         self.load_reference_state_dict(ck["Q_state"])
         if "Q_target_state" in ck:
             reference_state_to_flat(ck["Q_target_state"], self.T)

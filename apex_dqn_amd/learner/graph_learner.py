@@ -31,7 +31,7 @@ import torch
 from ..config import ApexConfig
 from ..models.dueling import build_network
 from ..ops.fused_ops import HipBackend, TorchBackend
-from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
 from .fused_learner import _enable_sharding
 from .losses import ddqn_loss
 
@@ -222,15 +222,22 @@ class GraphLearner:
         with torch.no_grad(), amp:
             return net(frames)[2].float()
 
-    def save(self, path: str) -> None:
+    def save(self, path: str, extra: Optional[Dict] = None) -> None:
         save_checkpoint(path, self.Q.state_dict(), Q_target_state=self.Q_target.state_dict(),
                         optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
-                        num_q_updates=self.num_q_updates, config=self.cfg.to_dict())
+                        num_q_updates=self.num_q_updates, config=self.cfg.to_dict(),
+                        rng={"replay_ctr": int(self.replay.ctr.item()), "replay_seed": int(self.replay.seed)},
+                        **(extra or {}))
 
     def load(self, path: str) -> bool:
         ck = load_checkpoint(path)
         if ck is None:
             return False
+        if adopt_obs_scale(ck, self.rt):
+            for net in (self.Q, self.Q_target):
+                if hasattr(net, "pre"):
+                    net.pre.scale = self.rt.obs_scale
+            self._graphs = None
         with torch.no_grad():
             for p, v in zip(self.Q.state_dict().values(), ck["Q_state"].values()):
                 p.copy_(v)
@@ -244,4 +251,7 @@ class GraphLearner:
                 self.rms_v.copy_(opt["rms_v"])
                 self.rms_m.copy_(opt["rms_m"])
         self.num_q_updates = int(ck.get("num_q_updates", 0))
+        rng = ck.get("rng")
+        if isinstance(rng, dict) and "replay_ctr" in rng:
+            self.replay.ctr.fill_(int(rng["replay_ctr"]))
         return True

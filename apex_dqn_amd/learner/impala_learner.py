@@ -28,22 +28,17 @@ defects fixed, exactly as the NatureCNN learner.
 from __future__ import annotations
 
 import contextlib
-import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
 import torch
 
 from ..config import ApexConfig
-
-# priority write-back: in the head-wgrad launch (one extra single-block tree update);
-# the in-head variant measured ~1 % slower (512 same-address fp64 root atomics)
-_PRIO_IN_HEAD = False
 from ..models.dueling import ImpalaDuellingDQN
 from ..models.flat_params import FlatLayout
 from ..ops.fused_ops import HipBackend, TorchBackend
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
-from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
 from .fused_learner import _enable_sharding
 
 CH = (16, 32, 32)
@@ -85,9 +80,6 @@ class FusedImpalaLearner:
             raise ValueError("the IMPALA kernels are built for 4 x 84 x 84 inputs")
         self.A = int(cfg.env_conf.action_dim)
         self.B = int(batch_size or cfg.Learner.replay_sample_size)
-        # max-pool backward: gathered inside the consumers' staging (1) or materialised (0)
-        import os
-        self.fuse_pool_grad = os.environ.get("APEX_IMPALA_FUSE_POOLGRAD", "0") != "0"
         if backend is None:
             backend = "hip" if (self.device.type == "cuda" and self.rt.use_hip_kernels) else "torch"
         on_gpu = backend == "hip"
@@ -178,9 +170,7 @@ class FusedImpalaLearner:
                      amax=torch.zeros(N3, P, php, php, 16, dtype=torch.uint8, device=d))
             f["o"] = (self.feat[:, :FEAT].view(N3, P, php, php, 16) if s == 2 else t(N3, php))
             self.fw.append(f)
-            b = dict(d_yb=t(B, php), d_ra=t(B, php), d_ya=t(B, php), d_p=t(B, php))
-            if not self.fuse_pool_grad:
-                b["d_c0"] = t(B, hw)
+            b = dict(d_yb=t(B, php), d_ra=t(B, php), d_ya=t(B, php), d_p=t(B, php), d_c0=t(B, hw))
             if s < 2:
                 b["d_o"] = t(B, php)    # gradient of this stack's output (the next stack's conv0 dgrad)
             self.bw.append(b)
@@ -304,11 +294,10 @@ class FusedImpalaLearner:
         isw = S["weights"] if self._isw else None
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
-                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
-                 prio=(self.replay, S["idx"], S["gen"]) if _PRIO_IN_HEAD else None)
+                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
+        # priority write-back in the head-wgrad launch (csrc/sumtree.hip head_wgrad_prio_kernel)
         with self._on_side():
-            ops.head_wgrad(self.h, self.dhead, self.G,
-                           prio=None if _PRIO_IN_HEAD else (self.replay, S["idx"], S["gen"], self.td_abs))
+            ops.head_wgrad(self.h, self.dhead, self.G, prio=(self.replay, S["idx"], S["gen"], self.td_abs))
         ops.fc_wgrad(self.dH, self.feat[:B], self.G["wfc"], self.G["bfc"])
         self._join_side()
 
@@ -334,22 +323,18 @@ class FusedImpalaLearner:
             io.wgrad(b["d_ra"], f["ya"][:B], r0b, *gw(r0b), jobs, relu_in=True)
             io.conv(b["d_ya"], r0a, b["d_p"], transpose=True, mask=f["p"][:B], add=b["d_ra"])
             io.wgrad(b["d_ya"], f["p"][:B], r0a, *gw(r0a), jobs, relu_in=True)
-            am = f["amax"][:B]
-            if self.fuse_pool_grad:
-                # the max-pool backward is gathered by the two consumers while they stage
-                # their operand: the full-resolution gradient never reaches HBM
-                dc, kw_w, kw_c = b["d_p"], dict(dy_pool_amax=am), dict(pool_grad=am)
-            else:
-                io.maxpool_bwd(b["d_p"], am, b["d_c0"])
-                dc, kw_w, kw_c = b["d_c0"], {}, {}
+            # max-pool backward (gather form, csrc/impala.hip maxpool_bwd_kernel); staging
+            # it inside the two consumers measured slower (round 1) and was removed
+            io.maxpool_bwd(b["d_p"], f["amax"][:B], b["d_c0"])
+            dc = b["d_c0"]
             if s == 0:
                 io.wgrad(dc, None, c0, *gw(c0), jobs, ring=self.replay.frames, slots=self.slots[:B],
-                         scale=self.rt.obs_scale, **kw_w)
+                         scale=self.rt.obs_scale)
             else:
                 prev = self.fw[s - 1]["o"][:B]
-                io.wgrad(dc, prev, c0, *gw(c0), jobs, **kw_w)
+                io.wgrad(dc, prev, c0, *gw(c0), jobs)
                 dO = self.bw[s - 1]["d_o"]
-                io.conv(dc, c0, dO, transpose=True, **kw_c)
+                io.conv(dc, c0, dO, transpose=True)
         io.finalize(jobs)
 
     def _seg3(self) -> None:
@@ -520,15 +505,19 @@ class FusedImpalaLearner:
         with torch.no_grad():
             return net(frames_u8.to(self.device))[2]
 
-    def save(self, path: str) -> None:
+    def save(self, path: str, extra: Optional[Dict] = None) -> None:
         save_checkpoint(path, self.module_state(), Q_target_state=self.module_state(self.T),
                         optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
-                        num_q_updates=self.num_q_updates, config=self.cfg.to_dict())
+                        num_q_updates=self.num_q_updates, config=self.cfg.to_dict(),
+                        rng={"replay_ctr": int(self.replay.ctr.item()), "replay_seed": int(self.replay.seed)},
+                        **(extra or {}))
 
     def load(self, path: str) -> bool:
         ck = load_checkpoint(path)
         if ck is None:
             return False
+        if adopt_obs_scale(ck, self.rt):
+            self._graphs = None                   # the input scale is a kernel argument: recapture
         self.load_module_state(ck["Q_state"])
         self.pbf.copy_(self.p32)
         if "Q_target_state" in ck:
@@ -542,4 +531,7 @@ class FusedImpalaLearner:
             self.rms_v.copy_(opt["rms_v"])
             self.rms_m.copy_(opt["rms_m"])
         self.num_q_updates = int(ck.get("num_q_updates", 0))
+        rng = ck.get("rng")
+        if isinstance(rng, dict) and "replay_ctr" in rng:
+            self.replay.ctr.fill_(int(rng["replay_ctr"]))
         return True

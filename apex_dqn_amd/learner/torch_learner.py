@@ -19,7 +19,7 @@ import torch
 
 from ..config import ApexConfig
 from ..models.dueling import build_network
-from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
 from .losses import ddqn_loss
 
 
@@ -114,6 +114,10 @@ class TorchLearner:
         ck = load_checkpoint(path)
         if ck is None:
             return False
+        if adopt_obs_scale(ck, self.rt):
+            for net in (self.Q, self.Q_target):
+                if hasattr(net, "pre"):
+                    net.pre.scale = self.rt.obs_scale
         self.Q.load_state_dict(ck["Q_state"])
         if "Q_target_state" in ck:
             self.Q_target.load_state_dict(ck["Q_target_state"])

@@ -117,9 +117,6 @@ _SIGS = {
     "apex_norm_total": ([c_p, c_i, c_p, c_p], c_i),
     "apex_ddqn_head": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
                         c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, c_p], c_i),
-    "apex_ddqn_head_prio": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
-                             c_p, c_p, c_p, c_p, c_p, c_i, c_i, TreeDesc, c_p, c_p, c_p, c_f, c_f, c_p, HeadLo, c_p],
-                            c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                              c_p, c_p, c_i, c_i, c_u64, c_p, c_p], c_i),

@@ -97,10 +97,8 @@ class TorchBackend:
     # ---------------------------------------------------------------- head
     def head(self, Hon, Htg, Pon: Dict[str, torch.Tensor], Ptg: Dict[str, torch.Tensor], act, rew, gam, isw,
              huber: bool, kappa: float, grad_scale: float, td_abs, loss, dH, dhead, q_out=None,
-             zero: Optional[torch.Tensor] = None, prio=None, lo=None):
-        """``prio = (replay, idx, gen)``: also write the batch's priorities back
-        (the HIP backend fuses it into the head kernel).  ``lo = (Hon_lo, Htg_lo,
-        dH_lo)`` in split mode."""
+             zero: Optional[torch.Tensor] = None, lo=None):
+        """``lo = (Hon_lo, Htg_lo, dH_lo)`` in split mode."""
         B = act.shape[0]
         A = Pon["wa"].shape[0]
         Hon = join(Hon, None if lo is None else lo[0])
@@ -143,8 +141,6 @@ class TorchBackend:
             q_out.copy_(q_t)
         if zero is not None:
             zero.zero_()
-        if prio is not None:
-            prio[0].update_priorities(prio[1], td_abs, prio[2])
 
     def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor], prio=None, Hon_lo=None):
         """``prio = (replay, idx, gen, td_abs)``: also write the batch's priorities back
@@ -354,7 +350,7 @@ class HipBackend(TorchBackend):
         return h
 
     def head(self, Hon, Htg, Pon, Ptg, act, rew, gam, isw, huber, kappa, grad_scale, td_abs, loss, dH,
-             dhead, q_out=None, zero=None, prio=None, lo=None):
+             dhead, q_out=None, zero=None, lo=None):
         B = act.shape[0]
         A = Pon["wa"].shape[0]
         args = (Hon.data_ptr(), Htg.data_ptr(), self._hp(Pon), self._hp(Ptg), act.data_ptr(), rew.data_ptr(),
@@ -362,14 +358,7 @@ class HipBackend(TorchBackend):
                 td_abs.data_ptr(), loss.data_ptr(), _lib.ptr(q_out), dH.data_ptr(), dhead.data_ptr(),
                 _lib.ptr(zero), 0 if zero is None else zero.numel(), Pon["wv"].numel())
         hl = _lib.head_lo(*(lo if lo is not None else (None, None, None)))
-        if prio is not None and prio[0].use_hip:
-            # priority write-back in the head kernel (csrc/sumtree.hip: ddqn_head_prio_kernel)
-            _lib.check(self.lib.apex_ddqn_head_prio(*args, *prio[0].prio_launch_args(prio[1], prio[2]), hl,
-                                                    _lib.stream_ptr()), "ddqn_head_prio")
-            return
         _lib.check(self.lib.apex_ddqn_head(*args, hl, _lib.stream_ptr()), "ddqn_head")
-        if prio is not None:
-            prio[0].update_priorities(prio[1], td_abs, prio[2])
 
     def head_wgrad(self, Hon, dhead, g, prio=None, Hon_lo=None):
         B, A1 = dhead.shape

@@ -28,13 +28,13 @@ class SconvDesc(ctypes.Structure):
     _fields_ = [("x", c_p), ("slots", c_p), ("wf", c_p), ("wf2", c_p), ("bias", c_p), ("bias2", c_p),
                 ("add", c_p), ("mask", c_p), ("y", c_p), ("mask_out", c_p), ("x_img", c_i64), ("y_img", c_i64),
                 ("add_img", c_i64), ("mask_img", c_i64), ("N", c_i), ("n_switch", c_i),
-                ("relu_in", c_i), ("relu_out", c_i), ("scale", c_f), ("pad0", c_i), ("amax_in", c_p)]
+                ("relu_in", c_i), ("relu_out", c_i), ("scale", c_f), ("pad0", c_i)]
 
 
 class SconvWgDesc(ctypes.Structure):
     _fields_ = [("dy", c_p), ("x", c_p), ("slots", c_p), ("slab", c_p), ("bslab", c_p),
                 ("dy_img", c_i64), ("x_img", c_i64), ("N", c_i), ("relu_in", c_i),
-                ("imgs_per_group", c_i), ("cin_real", c_i), ("dy_amax", c_p)]
+                ("imgs_per_group", c_i), ("cin_real", c_i)]
 
 
 class ResDesc(ctypes.Structure):
@@ -177,12 +177,10 @@ class HipImpalaOps:
             self._amax_rows = 0
 
     def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
-             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None, pool_grad=None,
+             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None,
              _pool_amax=False) -> None:
         """y = epi(corr3x3(x', W')): W' = W (forward) or transposed + flipped (data
-        gradient); x' = relu(x) if relu_in; epi = *scale + bias, * (mask > 0), + add, relu.
-        ``pool_grad`` = argmax codes: x is the POOLED gradient and x' its max-pool
-        backward (gathered while staging; never materialised)."""
+        gradient); x' = relu(x) if relu_in; epi = *scale + bias, * (mask > 0), + add, relu."""
         d = SconvDesc()
         pool = _pool_amax is not False
         if pool:
@@ -197,9 +195,6 @@ class HipImpalaOps:
             assert x.shape[0] == N
             d.x, d.x_img = x.data_ptr(), img_stride(x)
             mode = 0
-            if pool_grad is not None:
-                assert pool_grad.shape == x.shape and x.is_contiguous() and pool_grad.dtype == torch.uint8
-                d.amax_in, mode = pool_grad.data_ptr(), 4
         d.wf = (spec.fragT if transpose else spec.frag).data_ptr()
         if second is not None:
             d.wf2 = spec.frag_tgt.data_ptr()
@@ -236,10 +231,9 @@ class HipImpalaOps:
         _lib.check(self.lib.apex_resblock_fwd(d, c0.cin, c0.H, R, _lib.stream_ptr()), f"resblock_fwd[{c0.name}]")
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
-              groups: int = 0, scale: float = 1.0, dy_pool_amax=None) -> None:
+              groups: int = 0, scale: float = 1.0) -> None:
         """gw = scale * sum dy (x) im2col(x') (x' = relu(x) if relu_in), gb = sum dy:
-        partials now, reduced by ``finalize(jobs)``.  ``dy_pool_amax``: dy is the
-        pooled gradient, unpooled (gathered) while staging."""
+        partials now, reduced by ``finalize(jobs)``."""
         N = dy.shape[0]
         mode = 2 if ring is not None else 0
         bands = self.lib.apex_sconv_wgrad_bands(spec.cin, spec.cout, spec.H, spec.W, mode)
@@ -262,9 +256,6 @@ class HipImpalaOps:
             d.x, d.x_img = x.data_ptr(), img_stride(x)
         d.slab = slab.data_ptr()
         d.N, d.relu_in, d.imgs_per_group, d.cin_real = N, int(relu_in), ipg, spec.cin_real
-        if dy_pool_amax is not None:
-            assert dy_pool_amax.shape == dy.shape and dy.is_contiguous()
-            d.dy_amax = dy_pool_amax.data_ptr()
         _lib.check(self.lib.apex_sconv_wgrad(d, spec.cin, spec.cout, spec.H, spec.W, mode, G, _lib.stream_ptr()),
                    f"sconv_wgrad[{spec.name}]")
         jobs.append(dict(slab=slab, out=gw, bout=gb, nsplit=nsplit, NT=NT, P=P, cin_real=spec.cin_real,
@@ -337,16 +328,9 @@ class TorchImpalaOps:
         if ysave is not None:
             ysave[:n_save].copy_(y[:n_save])
 
-    def _unpool(self, dp, amax, spec: ConvSpec, planes: int):
-        full = torch.zeros(dp.shape[0], planes, spec.H, spec.W, 16, dtype=dp.dtype, device=dp.device)
-        self.maxpool_bwd(dp, amax, full)
-        return full
-
     def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
-             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None, pool_grad=None) -> None:
+             bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None) -> None:
         N = y.shape[0]
-        if pool_grad is not None:
-            x = self._unpool(x, pool_grad, spec, x.shape[1])
         if ring is not None:
             xin = F.pad(ring_frames(ring, slots).float(), (0, 0, 0, 0, 0, 12))
         else:
@@ -375,9 +359,7 @@ class TorchImpalaOps:
         y.copy_(o.to(y.dtype))
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
-              groups: int = 0, scale: float = 1.0, dy_pool_amax=None) -> None:
-        if dy_pool_amax is not None:
-            dy = self._unpool(dy, dy_pool_amax, spec, dy.shape[1])
+              groups: int = 0, scale: float = 1.0) -> None:
         if ring is not None:
             xin = ring_frames(ring, slots).float()
         else:

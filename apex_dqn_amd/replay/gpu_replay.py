@@ -390,13 +390,6 @@ class GpuReplayShard:
                 out["nxt"].data_ptr(), out["act"].data_ptr(), out["rew"].data_ptr(), out["gam"].data_ptr(),
                 _lib.ptr(nxt2), _lib.ptr(self.shard_stats), self.shard_rank, self.shard_world, self.shard_seed)
 
-    def prio_launch_args(self, idx: torch.Tensor, gen: Optional[torch.Tensor] = None,
-                         bump_ctr: bool = True) -> tuple:
-        """The priority write-back arguments of :meth:`update_priorities` (TreeDesc, idx,
-        generations, alpha, eps, counter) for ``apex_ddqn_head_prio``."""
-        return (self.tree_desc(), idx.data_ptr(), _lib.ptr(gen), self.gen.data_ptr(), self.alpha, self.eps,
-                self.ctr.data_ptr() if bump_ctr else None)
-
     def alloc_sample_buffers(self, B: int) -> Dict[str, torch.Tensor]:
         d = self.device
         return dict(idx=torch.zeros(B, dtype=torch.int64, device=d),

@@ -85,6 +85,8 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
         if metrics is not None:
             metrics.log("resume", step=learner.num_q_updates, path=ckpt_path)
     group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed)
+    if ckpt_path and rt.resume and os.path.exists(ckpt_path):
+        _restore_actor_rng(group, ckpt_path)
     min_local = max(L.min_replay_mem_size // world, L.replay_sample_size)
     max_actor_steps = int(max_actor_steps if max_actor_steps is not None else cfg.Actor.T)
     if async_actors is None:
@@ -167,7 +169,7 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                     st.actor_steps = st.actor_base + runner.steps
                 _log(metrics, learner, group, replay, st, rt, world, device)
             if ckpt_path and rt.ckpt_freq and n % rt.ckpt_freq == 0 and rank == 0:
-                learner.save(ckpt_path)
+                learner.save(ckpt_path, extra=_actor_rng(group))
     finally:
         if runner is not None:
             runner.stop()
@@ -192,6 +194,20 @@ class _LoopState:
         self.losses = []
         self.n_ep_seen = 0
         self.t_last, self.n_last, self.ins_last, self.steps_last = t0, n0, 0, 0
+
+
+def _actor_rng(group) -> Dict[str, Any]:
+    """The actor group's device RNG counter (epsilon-greedy draws) for the checkpoint."""
+    ctr = getattr(group, "ctr", None)
+    return {"actor_rng": {"ctr": int(ctr.item())}} if ctr is not None else {}
+
+
+def _restore_actor_rng(group, path: str) -> None:
+    from ..utils.checkpoint import load_checkpoint
+    ck = load_checkpoint(path) or {}
+    a = ck.get("actor_rng")
+    if isinstance(a, dict) and getattr(group, "ctr", None) is not None:
+        group.ctr.fill_(int(a["ctr"]))
 
 
 def _to_boundary(n: int, every: int) -> int:

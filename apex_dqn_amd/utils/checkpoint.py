@@ -33,3 +33,33 @@ def load_checkpoint(path: str) -> Optional[Dict[str, Any]]:
     except FileNotFoundError:
         print("WARNING: No trained model found. Training from scratch")
         return None
+
+
+REFERENCE_OBS_SCALE = 1.0   # the reference feeds raw 0..255 floats (actor.py:117-119,161, learner.py:37)
+
+
+def checkpoint_obs_scale(ck: Dict[str, Any]) -> float:
+    """Input scale the checkpoint's weights were trained with: ``config`` holds it
+    for checkpoints written here; a checkpoint without ``config`` comes from the
+    reference, whose networks see raw 0..255 pixels."""
+    cfg = ck.get("config")
+    if isinstance(cfg, dict):
+        rt = cfg.get("Runtime") or {}
+        if "obs_scale" in rt:
+            return float(rt["obs_scale"])
+    return REFERENCE_OBS_SCALE
+
+
+def adopt_obs_scale(ck: Dict[str, Any], runtime_conf) -> bool:
+    """Set ``runtime_conf.obs_scale`` to the checkpoint's input scale (with a loud
+    warning when it changes); returns True if it changed."""
+    new = checkpoint_obs_scale(ck)
+    old = float(runtime_conf.obs_scale)
+    if abs(new - old) <= 1e-12 * max(abs(old), 1.0):
+        return False
+    origin = "reference-format checkpoint (no config): raw 0..255 pixel input" if "config" not in ck \
+        else "checkpoint config"
+    print(f"WARNING: Runtime.obs_scale {old:g} -> {new:g} from the {origin}; the loaded weights expect it")
+    runtime_conf.obs_scale = new
+    return True
+

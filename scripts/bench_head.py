@@ -51,7 +51,6 @@ def main():
     be = HipBackend()
     args = (Hon, Htg, Pon, Ptg, act, rew, gam, isw, True, 1.0, 1.0 / B, td, loss, dH, dhead)
     for name, fn in [("head", lambda: be.head(*args, zero=zero)),
-                     ("head_prio", lambda: be.head(*args, zero=zero, prio=(rp, S["idx"], S["gen"]))),
                      ("head_wgrad", lambda: be.head_wgrad(Hon, dhead, gr)),
                      ("head_wgrad_prio", lambda: be.head_wgrad(Hon, dhead, gr, prio=(rp, S["idx"], S["gen"], td))),
                      ("tree_update", lambda: rp.update_priorities(S["idx"], td, S["gen"])),

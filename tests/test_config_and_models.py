@@ -115,3 +115,45 @@ def test_params_file_is_json():
     with open(os.path.join(ROOT, "parameters.json")) as f:
         d = json.load(f)
     assert set(d) >= {"env_conf", "Actor", "Learner", "Replay_Memory"}
+
+
+def _reference_forward_q(sd, x):
+    """Plain fp32 functional forward of the reference DuellingDQN (duelling_network.py:21-28)
+    on raw float pixels, with the dueling mean taken per row (defect A-mean fixed)."""
+    import torch.nn.functional as F
+    h = F.relu(F.conv2d(x, sd["layer1.0.weight"], sd["layer1.0.bias"], stride=4))
+    h = F.relu(F.conv2d(h, sd["layer2.0.weight"], sd["layer2.0.bias"], stride=2))
+    h = F.relu(F.conv2d(h, sd["layer3.0.weight"], sd["layer3.0.bias"], stride=1)).reshape(x.shape[0], -1)
+    v = F.linear(F.relu(F.linear(h, sd["value_stream_layer.0.weight"], sd["value_stream_layer.0.bias"])),
+                 sd["value.weight"], sd["value.bias"])
+    a = F.linear(F.relu(F.linear(h, sd["advantage_stream_layer.0.weight"], sd["advantage_stream_layer.0.bias"])),
+                 sd["advantage.weight"], sd["advantage.bias"])
+    return v + a - a.mean(1, keepdim=True)
+
+
+@pytest.mark.parametrize("with_config", [False, True])
+def test_reference_checkpoint_q_values_at_raw_pixel_scale(tmp_path, with_config):
+    """A reference-format checkpoint ({'Q_state'} only, learner.py:18-23) loads with
+    the reference's raw 0..255 input scale and reproduces its Q-values; a checkpoint
+    written here keeps the scale recorded in its config."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    torch.manual_seed(3)
+    sd = {k: v * 0.2 for k, v in DuellingDQN((4, 84, 84), 6).state_dict().items()}
+    p = str(tmp_path / "ref.pt")
+    if with_config:
+        save_checkpoint(p, sd, config={"Runtime": {"obs_scale": 1.0 / 255.0}})
+    else:
+        torch.save({"Q_state": sd}, p)
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 4, "load_saved_state": p},
+                                "Runtime": {"use_graphs": False}})
+    rp = GpuReplayShard(16, 16, 32, 4, device="cpu")
+    L = FusedNatureLearner(cfg, "cpu", rp)
+    scale = 1.0 / 255.0 if with_config else 1.0
+    assert L.rt.obs_scale == pytest.approx(scale)
+    x = torch.randint(0, 256, (5, 4, 84, 84), dtype=torch.uint8)
+    q = L.q_values(x)
+    q_ref = _reference_forward_q(sd, x.float() * scale)
+    torch.testing.assert_close(q, q_ref, rtol=1e-4, atol=1e-4 * float(q_ref.abs().max()))

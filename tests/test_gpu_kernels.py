@@ -207,43 +207,6 @@ def test_ddqn_head_kernel_vs_torch(huber, A):
         torch.testing.assert_close(h[5][k], r[5][k], rtol=1e-3, atol=1e-6)
 
 
-def test_ddqn_head_prio_matches_head_plus_tree_update():
-    """The head kernel with the fused priority write-back (duplicates: last wins;
-    stale generation / evicted slot: skipped) leaves the tree exactly as the head
-    kernel followed by tree_update, with identical head outputs."""
-    from apex_dqn_amd.ops.fused_ops import HipBackend
-    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
-    B, A = 64, 6
-    Hon, Htg, Pon, Ptg, act, rew, gam, isw = _head_inputs(B, A, seed=3)
-    g = torch.Generator(device="cpu").manual_seed(5)
-    idx = torch.randint(0, 300, (B,), generator=g).to(DEV)
-    idx[10] = idx[40] = idx[63] = 17          # triple duplicate: sample 63 wins
-    res = {}
-    for fused in (False, True):
-        rp = GpuReplayShard(1000, 700, 1200, 4, device=DEV, alpha=0.6, eps=1e-6)
-        _fill_replay(rp, 900, seed=9)
-        rp.remove_to_fit()                    # slots 0..199 evicted: their updates must be dropped
-        gen = rp.gen[idx].clone()
-        gen[5] += 1                           # stale generation: dropped
-        be = HipBackend()
-        out = [torch.zeros(B, device=DEV), torch.zeros(B, device=DEV),
-               torch.zeros(B, 1024, device=DEV, dtype=torch.bfloat16), torch.zeros(B, A + 1, device=DEV)]
-        ctr0 = int(rp.ctr[0])
-        if fused:
-            be.head(Hon, Htg, Pon, Ptg, act, rew, gam, isw, True, 1.0, 1.0 / B, *out, prio=(rp, idx, gen))
-        else:
-            be.head(Hon, Htg, Pon, Ptg, act, rew, gam, isw, True, 1.0, 1.0 / B, *out)
-            rp.update_priorities(idx, out[0], gen)
-        torch.cuda.synchronize()
-        res[fused] = ([t.clone() for t in out], rp.leaf.clone(), rp.nodes.clone(), int(rp.min_bits[0]),
-                      int(rp.ctr[0]) - ctr0)
-    (o0, l0, n0, m0, c0), (o1, l1, n1, m1, c1) = res[False], res[True]
-    for a, b in zip(o0, o1):
-        assert torch.equal(a, b)
-    assert torch.equal(l0, l1) and m0 == m1 and c0 == c1 == 1
-    torch.testing.assert_close(n1, n0, rtol=1e-12, atol=1e-9)
-
-
 @pytest.mark.parametrize("sharded", [False, True])
 def test_rmsprop_sample_matches_separate_launches(sharded):
     """Optimizer launch carrying the next batch's draw == rmsprop + tree_sample

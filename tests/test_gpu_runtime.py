@@ -171,6 +171,51 @@ def test_fused_norm_equals_gradient_norm():
         assert abs(float(L.gnorm[0]) - true) <= 1e-4 * true + 1e-12, (float(L.gnorm[0]), true)
 
 
+def _filled_replay(seed=5, K=1800):
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(3000, 3000, 3600, 4, device=DEV, seed=seed)
+    rng = np.random.default_rng(seed)
+    seqs = rp.append_frames(rng.integers(0, 255, (2000, 84, 84), dtype=np.uint8))
+    st = np.stack([seqs[i:i + 4] for i in range(K)])
+    rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 6, K), R=rng.normal(size=K).astype(np.float32),
+                   Gamma=np.full(K, 0.97, np.float32), priority=rng.random(K).astype(np.float32) + 0.01))
+    return rp
+
+
+def test_gpu_resume_matches_uninterrupted_run(tmp_path):
+    """Checkpoint at update 4, resume in a fresh learner on the replay as it was at
+    that update: updates 5..9 are bit-identical to the uninterrupted run (params,
+    RMSprop state, target net, sampling counter; graphs on, pre-sampling on)."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 128, "q_target_sync_freq": 3},
+                                "Runtime": {"use_graphs": True}})
+    rp = _filled_replay()
+    L = FusedNatureLearner(cfg, DEV, rp)
+    for _ in range(4):
+        L.step()
+    torch.cuda.synchronize()
+    ck = str(tmp_path / "ck.pt")
+    L.save(ck)
+    tree = [t.clone() for t in (rp.leaf, rp.nodes, rp.min_bits, rp.ctr)]
+    for _ in range(5):
+        L.step()
+    torch.cuda.synchronize()
+    rp2 = _filled_replay()
+    for dst, src in zip((rp2.leaf, rp2.nodes, rp2.min_bits, rp2.ctr), tree):
+        dst.copy_(src)
+    cfg2 = ApexConfig.from_dict({**cfg.to_dict(), "Learner": {**cfg.to_dict()["Learner"], "load_saved_state": ck}})
+    L2 = FusedNatureLearner(cfg2, DEV, rp2)
+    assert L2.num_q_updates == 4
+    for _ in range(5):
+        L2.step()
+    torch.cuda.synchronize()
+    for a, b in ((L.p32, L2.p32), (L.rms_v, L2.rms_v), (L.rms_m, L2.rms_m), (L.t32, L2.t32),
+                 (rp.leaf, rp2.leaf), (rp.ctr, rp2.ctr)):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B", [32, 48])
 def test_fused_learner_unaligned_batch(B):
     """Batches whose online/target split is not a 128-row tile boundary (2B % 128 != 0)

@@ -285,44 +285,6 @@ def test_gpu_resblock_fused(C, H):
 
 
 @pytest.mark.gpu
-def test_gpu_pool_grad_staging():
-    """Max-pool backward gathered inside the consumers' staging (conv data gradient
-    and weight gradient) == materialised maxpool_bwd followed by the plain kernels."""
-    from apex_dqn_amd.ops.impala import HipImpalaOps
-    dev = torch.device("cuda")
-    hops = HipImpalaOps()
-    for (cin, cout, H, ring) in ((32, 32, 21, False), (16, 32, 42, False), (16, 16, 84, True)):
-        N, Ho, P = 9, (H + 1) // 2, cout // 16
-        cs = _spec(cin, cout, H, dev, cin_real=4 if ring else None)
-        _hip_pack(hops, cs, dev)
-        x = torch.randn(N, P, H, H, 16, device=dev).to(torch.bfloat16)
-        pooled = torch.zeros(N, P, Ho, Ho, 16, dtype=torch.bfloat16, device=dev)
-        amax = torch.zeros(N, P, Ho, Ho, 16, dtype=torch.uint8, device=dev)
-        hops.maxpool(x, pooled, amax)
-        dp = torch.randn(N, P, Ho, Ho, 16, device=dev).to(torch.bfloat16)
-        full = torch.zeros(N, P, H, H, 16, dtype=torch.bfloat16, device=dev)
-        hops.maxpool_bwd(dp, amax, full)
-        if not ring:   # data gradient
-            dx, dx2 = (torch.zeros(N, cin // 16, H, H, 16, dtype=torch.bfloat16, device=dev) for _ in range(2))
-            hops.conv(full, cs, dx, transpose=True)
-            hops.conv(dp, cs, dx2, transpose=True, pool_grad=amax)
-            assert torch.equal(dx, dx2)
-        xin = torch.randn(N, cin // 16, H, H, 16, device=dev).to(torch.bfloat16)
-        slots = torch.randint(0, 100, (N, 4), dtype=torch.int32, device=dev)
-        rp = _setup(device=dev)[1] if ring else None
-        kw = dict(ring=rp.frames, slots=slots) if ring else {}
-        outs = []
-        for dy, am in ((full, None), (dp, amax)):
-            gw, gb = torch.zeros(cout, cs.cin_real, 3, 3, device=dev), torch.zeros(cout, device=dev)
-            jobs = []
-            hops.wgrad(dy, None if ring else xin, cs, gw, gb, jobs, dy_pool_amax=am, **kw)
-            hops.finalize(jobs)
-            outs.append((gw, gb))
-        torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-5)
-        torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5)
-
-
-@pytest.mark.gpu
 def test_gpu_maxpool():
     from apex_dqn_amd.ops.impala import HipImpalaOps
     dev = torch.device("cuda")
