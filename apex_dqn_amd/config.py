@@ -104,6 +104,8 @@ class RuntimeConf:
     replay_capacity: Optional[int] = None  # physical capacity, global over the ranks' shards
                                            # (default: soft_capacity * 1.25 + 1024)
     heartbeat_timeout: float = 60.0
+    force_dp: bool = False          # run the data-parallel step (collectives + sharded replay) even at
+                                    # world 1 (needs an initialised process group; checks / overhead)
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
                                     # (runtime/actor_thread.py), concurrent with the learner
 

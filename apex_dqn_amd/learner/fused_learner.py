@@ -120,6 +120,10 @@ class FusedNatureLearner:
         self.sync_target()
         self.num_q_updates = 0
         self.world = comm.world_size if comm is not None else 1
+        # the data-parallel step (collectives, sharded replay); Runtime.force_dp runs it
+        # at world 1 too (an initialised process group of one rank: RCCL capture checks
+        # and the segmented-step overhead on a single GPU)
+        self._dp = self.world > 1 or (bool(self.rt.force_dp) and comm is not None)
         self._alloc(self.B)
         self._graphs = None     # one-update graph
         self._multi = None      # Runtime.graph_steps-update graph (steps())
@@ -130,25 +134,25 @@ class FusedNatureLearner:
         # by RCCL in bf16, cast back before the optimizer)
         if self.rt.allreduce_dtype not in ("fp32", "bf16"):
             raise ValueError("Runtime.allreduce_dtype must be fp32 or bf16")
-        self._comm_bf16 = self.world > 1 and self.rt.allreduce_dtype == "bf16"
+        self._comm_bf16 = self._dp and self.rt.allreduce_dtype == "bf16"
         self.gcomm = torch.zeros(n, dtype=torch.bfloat16, device=d) if self._comm_bf16 else self.g32
         # producer-summed clip norm: the fc wgrad epilogue and the grad_finalize blocks
         # write squared-norm partials of the values they store, the optimizer launch sums
         # them.  With DP the norm is of the all-reduced gradient: the optimizer's own pass.
-        self._fuse_norm = self.world == 1 and self.ops.name == "hip" and getattr(self.ops, "native_conv", False)
+        self._fuse_norm = not self._dp and self.ops.name == "hip" and getattr(self.ops, "native_conv", False)
         # DP: the rank-local replay shards form ONE prioritized replay (replay/gpu_replay.py
         # enable_sharding): every step all-gathers the shards' (sum p^alpha, min p^alpha)
         # right after the priority write-back and the next batch is one global draw,
         # identical on every rank, of which each rank keeps the part in its own shard.
         # Rows drawn elsewhere carry IS weight 0, so the IS weights always enter the loss
         # (with use_is_weights off: beta = 0, i.e. weights 0 / W B / M only).
-        self._isw = bool(self.rt.use_is_weights) or self.world > 1
-        if self.world > 1:
+        self._isw = bool(self.rt.use_is_weights) or self._dp
+        if self._dp:
             _enable_sharding(replay, comm, self.rt)
             replay.gather_shard_stats()
         # DP step as ONE captured graph including the RCCL collectives (backend nccl);
         # gloo (CPU tests, one-GPU rehearsals) cannot be captured: eager DP steps
-        self._dp_graphs = self.world > 1 and cuda and self._backend_name() == "nccl"
+        self._dp_graphs = self._dp and cuda and self._backend_name() == "nccl"
         # next-batch pre-sampling: the batch of step t+1 is drawn at the end of step t,
         # after the priority write-back -- on the HIP backend inside the optimizer launch
         # (its first blocks run the sampler: csrc/sumtree.hip rmsprop_sample_kernel), so
@@ -328,7 +332,7 @@ class FusedNatureLearner:
         start.record()
         self._marks = []
         try:
-            if self.world > 1:
+            if self._dp:
                 self._dp_body()
             else:
                 self._step_body()
@@ -384,13 +388,13 @@ class FusedNatureLearner:
         self._seg3()
 
     def _body(self) -> None:
-        if self.world > 1:
+        if self._dp:
             self._dp_body()
         else:
             self._step_body()
 
     def _graphs_enabled(self) -> bool:
-        return bool(self.rt.use_graphs) and self.device.type == "cuda" and (self.world == 1 or self._dp_graphs)
+        return bool(self.rt.use_graphs) and self.device.type == "cuda" and (not self._dp or self._dp_graphs)
 
     def step(self) -> None:
         """One learner update (asynchronous on the current stream)."""
@@ -495,7 +499,7 @@ class FusedNatureLearner:
     def refresh_replay_stats(self) -> None:
         """Re-gather the shard statistics (after host-side inserts / eviction; a
         collective: every rank calls it at the same point)."""
-        if self.world > 1:
+        if self._dp:
             self.replay.gather_shard_stats()
 
     def _snapshot(self):

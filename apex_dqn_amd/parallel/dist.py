@@ -41,10 +41,14 @@ class Comm:
     # ------------------------------------------------------------ setup
     @classmethod
     def from_env(cls, backend: Optional[str] = None, device: Optional[torch.device] = None,
-                 timeout_s: float = 300.0) -> "Comm":
+                 timeout_s: float = 300.0, force: bool = False) -> "Comm":
+        """``force``: initialise the process group even for one rank (the DP step at
+        world 1, ``Runtime.force_dp``; needs MASTER_ADDR / MASTER_PORT)."""
         ws = int(os.environ.get("WORLD_SIZE", "1"))
-        if ws <= 1:
+        if ws <= 1 and not force:
             return cls(0, 1, device)
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("MASTER_PORT", "29511")
         rank = int(os.environ["RANK"])
         if backend is None:
             backend = "nccl" if (device is not None and torch.device(device).type == "cuda") else "gloo"
@@ -59,8 +63,8 @@ class Comm:
 
     @classmethod
     def init(cls, rank: int, world_size: int, init_method: str, backend: str = "gloo",
-             device: Optional[torch.device] = None) -> "Comm":
-        if world_size > 1 and not dist.is_initialized():
+             device: Optional[torch.device] = None, force: bool = False) -> "Comm":
+        if (world_size > 1 or force) and not dist.is_initialized():
             dist.init_process_group(backend=backend, init_method=init_method, rank=rank,
                                     world_size=world_size,
                                     timeout=datetime.timedelta(seconds=300))
@@ -79,7 +83,7 @@ class Comm:
                 dist.barrier()
 
     def shutdown(self) -> None:
-        if self.active and dist.is_initialized():
+        if dist.is_initialized():
             dist.destroy_process_group()
 
     # ------------------------------------------------------ collectives

@@ -75,7 +75,7 @@ def make_learner(args, dtype, device, comm, rank, replay):
         "Replay_Memory": {"soft_capacity": args.replay},
         "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
                     "seed": 1234 + rank, "network": args.network, "dtype": dtype,
-                    "presample": not args.no_presample,
+                    "presample": not args.no_presample, "force_dp": args.force_dp,
                     **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
     })
     if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
@@ -148,6 +148,9 @@ def main():
                     help="sample at the head of each step instead of inside the previous step's optimizer launch")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (rehearsing several ranks on one GPU)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="run the data-parallel step (RCCL collectives captured in the graphs, sharded "
+                         "replay) even on one rank: capture check and segmented-step overhead")
     ap.add_argument("--graph-steps", type=int, default=None,
                     help="learner updates per HIP-graph launch (Runtime.graph_steps; 1 = one graph per update)")
     ap.add_argument("--graph-impala", action="store_true",
@@ -168,7 +171,7 @@ def main():
     dev_idx = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_idx)
     device = torch.device("cuda", dev_idx)
-    comm = Comm.from_env(backend=args.dist_backend, device=device)
+    comm = Comm.from_env(backend=args.dist_backend, device=device, force=args.force_dp)
 
     replay = make_replay(args, device, rank)
     cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay)
@@ -197,7 +200,8 @@ def main():
                                   if args.network == "nature64" else
                                   "dueling %s, 4x84x84, A=%d" % (args.network, args.actions)),
                        "global_batch": args.batch * world, "seq_len": 1,
-                       "parallelism": "dp%d" % world, "per_gpu_batch": args.batch,
+                       "parallelism": "dp%d" % world + ("-dp-step" if args.force_dp and world == 1 else ""),
+                       "per_gpu_batch": args.batch,
                        "replay_per_gpu": args.replay,
                        "learner": kind + ("/" + ops.name if ops is not None and args.learner == "fused" else
                                           "/torch-autograd"),

@@ -16,10 +16,11 @@ import torch.multiprocessing as mp
 from apex_dqn_amd.config import ApexConfig
 
 
-def _cfg(ar="fp32"):
+def _cfg(ar="fp32", force_dp=False):
     return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
                                  "Learner": {"replay_sample_size": 6},
-                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0, "allreduce_dtype": ar}})
+                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0, "allreduce_dtype": ar,
+                                             "force_dp": force_dp}})
 
 
 def _replay(rank):
@@ -38,8 +39,8 @@ def _worker(rank, world, path, q, ar="fp32"):
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.parallel.dist import Comm
     torch.set_num_threads(2)
-    comm = Comm.init(rank, world, f"file://{path}", backend="gloo")
-    cfg = _cfg(ar)
+    comm = Comm.init(rank, world, f"file://{path}", backend="gloo", force=world == 1)
+    cfg = _cfg(ar, force_dp=world == 1)   # world 1: the DP step forced on one rank
     torch.manual_seed(1234 + rank)  # different local init: rank 0's params must be broadcast
     rp = _replay(rank)
     L = FusedNatureLearner(cfg, "cpu", rp, comm=comm)
@@ -72,14 +73,14 @@ def _worker(rank, world, path, q, ar="fp32"):
     g_mean = torch.stack(gl).mean(0)
     pl = [torch.zeros_like(L.p32) for _ in range(world)]
     torch.distributed.all_gather(pl, L.p32.clone())
-    perr = max(float((pl[0] - p).abs().max()) for p in pl[1:])
+    perr = max([float((pl[0] - p).abs().max()) for p in pl[1:]], default=0.0)
     q.put((rank, float((g_dp - g_mean).abs().max()), float(g_mean.abs().max()), perr, stats.numpy(),
            own, n_valid))
     comm.shutdown()
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("ar,world", [("fp32", 2), ("bf16", 2), ("fp32", 4)])
+@pytest.mark.parametrize("ar,world", [("fp32", 1), ("fp32", 2), ("bf16", 2), ("fp32", 4)])
 def test_dp_learner_gloo(ar, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
