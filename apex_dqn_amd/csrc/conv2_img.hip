@@ -34,6 +34,11 @@ struct Conv2ImgDesc {
   const float* bias2;
   bf16_t* y;            // [N][9][9][64]
   int N, img_switch;    // images >= img_switch use (w2, bias2)
+  // fp32-accurate ("split") mode: lo planes (value = hi + lo) of x, w, w2 and y, or all null
+  const bf16_t* x_lo;
+  const bf16_t* w_lo;
+  const bf16_t* w2_lo;
+  bf16_t* y_lo;
 };
 
 #define C2_THREADS 512
@@ -164,15 +169,190 @@ __global__ void __launch_bounds__(C2_THREADS, 1) conv2_img_fwd_kernel(Conv2ImgDe
 #undef C2_PREFETCH
 }
 
+
+// Split ("fp32-accurate") forward: x = x_hi + x_lo, w = w_hi + w_lo (csrc/mfma_common.h
+// split_pk_bf16), products x_hi w_hi + x_hi w_lo + x_lo w_hi.  Four waves (one per
+// SIMD): wave w owns output-channel half w & 1 and kernel rows 2 (w >> 1) and
+// 2 (w >> 1) + 1, i.e. K 512 whose hi and lo weight fragments (2 x 32 x 8 registers)
+// stay in registers; the two kernel-row pairs meet in a 48 KB fp32 LDS reduction.
+// Every image runs two phases: phase 0 reads x_hi and issues two MFMAs per fragment
+// pair (w_hi, w_lo), phase 1 reads x_lo and issues one (w_hi).  The planes are
+// double-buffered in LDS and filled by LDS-DMA (global_load_lds_dwordx4, no registers):
+// each lane fetches the global 16-B chunk that belongs at its LDS slot, so the next
+// plane streams in under the current phase's MFMA chain.
+// Bank-conflict-free A reads with coalesced DMA: M rows are output pixels on a 10-wide
+// grid (r = 10 oh + ow; ow = 9 and r >= 90 are padding, 96 rows = 3 tiles as before);
+// the plane stores its pixels class-major, P = (input stride-parity class) * 100 +
+// (ih >> 1) * 10 + (iw >> 1), 128 B each with 16-B chunk c at c ^ ((P >> 1) & 7).  The
+// 16 lanes of a ds_read_b128 lane group read 16 pixels whose P are distinct mod 16, i.e.
+// 8 of each parity with distinct (P >> 1) & 7: 16 distinct bank groups (the 9-wide
+// grid of the bf16 kernel measured 41 % conflict cycles), while 8 consecutive DMA
+// lanes still fetch one pixel's whole 128-B NHWC row.
+#define C2S_THREADS 256
+#define C2S_BLOCKS 50           // 64-slot DMA blocks per plane (3200 slots)
+#define C2S_NB 13               // blocks per wave (waves 2, 3: 12)
+#define C2S_PLANE 52224         // 3264 slots: padding rows read past the last pixel
+
+__global__ void __launch_bounds__(C2S_THREADS, 1) conv2_img_fwd_split_kernel(Conv2ImgDesc d) {
+  // three plane buffers: planes run two phases ahead of the MFMAs; the fp32 reduction
+  // tiles (48 KB) reuse the buffer the phase-1 MFMAs just finished reading
+  __shared__ __attribute__((aligned(16))) uint8_t simg[3 * C2S_PLANE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nh = wv & 1, kp = wv >> 1;
+  const int rr = lane & 31, kg = lane >> 5;
+  const int step = gridDim.x, img0 = blockIdx.x, img1 = d.N;
+  if (img0 >= img1) return;
+  const int nimg = (img1 - img0 + step - 1) / step;          // images of this workgroup
+  const int ndma = wv < C2S_BLOCKS - 4 * (C2S_NB - 1) ? C2S_NB : C2S_NB - 1;   // this wave's DMAs per plane
+
+  // DMA source of LDS slot j = 64 b + lane: pixel P = j >> 3, chunk (j & 7) ^ swizzle
+  int srcc[C2S_NB];
+#pragma unroll
+  for (int k = 0; k < C2S_NB; ++k) {
+    const int b = wv + 4 * k, j = min(b, C2S_BLOCKS - 1) * 64 + lane;
+    const int P = j >> 3, c = (j & 7) ^ ((P >> 1) & 7), cls = P / 100, q = P - cls * 100;
+    const int a = q / 10, bb = q - a * 10;
+    srcc[k] = ((2 * a + (cls >> 1)) * 20 + 2 * bb + (cls & 1)) * 8 + c;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)simg;
+  // plane g of this workgroup: image img0 + (g >> 1) step, x_hi (g even) / x_lo (g odd),
+  // into buffer g % 3
+  auto dma_plane = [&](int g) {
+    if ((g >> 1) >= nimg) return;
+    const bf16_t* plane = (g & 1) ? d.x_lo : d.x;
+    const uint4* base = reinterpret_cast<const uint4*>(plane + (int64_t)(img0 + (g >> 1) * step) * (C2_IMG / 2));
+    const uint32_t dst = lds0 + (uint32_t)(g % 3) * C2S_PLANE;
+#pragma unroll
+    for (int k = 0; k < C2S_NB; ++k) {
+      const int b = wv + 4 * k;
+      if (b < C2S_BLOCKS) dma16(base + srcc[k], __builtin_amdgcn_readfirstlane(dst + b * 1024));
+    }
+  };
+  // A row -> pixel slot of kernel-row pair kp: (oh + kp) * 10 + ow (+ (kh & 1) block,
+  // + (kw >> 1) column per K step)
+  int q0[3];
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt) {
+    const int r = mt * 32 + rr, oh = r / 10, ow = r - oh * 10;
+    q0[mt] = (oh + kp) * 10 + ow;
+  }
+  bf16x8 bh[32], bl[32];      // [kernel row of the pair][16 K steps]
+  int cur_set = -1;
+
+  dma_plane(0);
+  dma_plane(1);
+  for (int i = 0; i < nimg; ++i) {
+    const int img = img0 + i * step;
+    const int set = (d.w2 != nullptr && img >= d.img_switch) ? 1 : 0;
+    if (set != cur_set) {
+      const bf16_t* W = set ? d.w2 : d.w;
+      const bf16_t* WL = set ? d.w2_lo : d.w_lo;
+      const int co = nh * 32 + rr;
+#pragma unroll
+      for (int s = 0; s < 32; ++s) {
+        const int kh = 2 * kp + (s >> 4), kw = (s >> 2) & 3, ci0 = ((s & 3) << 4) + kg * 8;
+        const int64_t o = ((co * 4 + kh) * 4 + kw) * 64 + ci0;
+        bh[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(W + o));
+        bl[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(WL + o));
+      }
+      cur_set = set;
+    }
+    f32x16 acc[3];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[mt][j] = 0.f;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      const int g = 2 * i + ph;
+      // plane g landed (this wave's DMAs of plane g + 1 -- issued later -- may still
+      // be in flight; loads return in order, extra completions only over-wait) ...
+      if ((g >> 1) < nimg && ((g + 1) >> 1) < nimg) vmcnt_le(ndma);
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // ... for every wave; and buffer (g + 2) % 3 is free (read in phase g - 1)
+      dma_plane(g + 2);
+      const uint8_t* cur = simg + (g % 3) * C2S_PLANE;
+      // A fragments one K step ahead (explicit; the scheduler barrier per step keeps
+      // the compiler from hoisting all 96 reads and spilling).  K step s: kernel row
+      // kh = 2 kp + (s >> 4), column kw = (s >> 2) & 3, chunk ((s & 3) << 1) | kg.
+      bf16x8 af[2][3];
+#define C2S_LDA(s_, dst_)                                                                   \
+      _Pragma("unroll") for (int mt = 0; mt < 3; ++mt) {                                   \
+        const int P_ = (((s_) >> 4) * 2 + (((s_) >> 2) & 1)) * 100 + q0[mt] + (((s_) >> 3) & 1); \
+        const int c_ = (((s_) & 3) << 1) | kg;                                               \
+        dst_[mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(cur + P_ * 128 + ((c_ ^ ((P_ >> 1) & 7)) << 4))); \
+      }
+      C2S_LDA(0, af[0])
+#pragma unroll
+      for (int s = 0; s < 32; ++s) {
+        if (s + 1 < 32) C2S_LDA(s + 1, af[(s + 1) & 1])
+        __builtin_amdgcn_sched_barrier(0);   // step s + 1's reads issue ahead of step s's MFMAs
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt) {
+          if (ph == 0) acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][mt], bl[s], acc[mt], 0, 0, 0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s & 1][mt], bh[s], acc[mt], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#undef C2S_LDA
+    }
+    __syncthreads();                        // phase-1 reads of buffer (2 i + 1) % 3 done
+    float* red = reinterpret_cast<float*>(simg + ((2 * i + 1) % 3) * C2S_PLANE);
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int row = 8 * (j >> 2) + 4 * kg + (j & 3);
+        red[((wv * 3 + mt) * 32 + row) * 32 + rr] = acc[mt][j];
+      }
+    __syncthreads();
+    // wave (nh, kp) finishes grid rows 48 kp .. 48 kp + 47 of channel half nh: the two
+    // kernel-row pairs (waves nh and nh + 2) in fixed order, bias, ReLU, hi / lo split
+    const float* bias = set ? d.bias2 : d.bias;
+    const int c4 = (lane & 7) * 4;
+    const float4 bv = make_float4(bias[nh * 32 + c4], bias[nh * 32 + c4 + 1], bias[nh * 32 + c4 + 2],
+                                  bias[nh * 32 + c4 + 3]);
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+      const int r = 48 * kp + 8 * it + (lane >> 3), oh = r / 10, ow = r - oh * 10;
+      if (ow < 9 && oh < 9) {
+        const int mt = r >> 5, row = r & 31;
+        float4 sum = bv;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(red + (((nh + 2 * q) * 3 + mt) * 32 + row) * 32 + c4);
+          sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+        }
+        uint32_t h01, l01, h23, l23;
+        split_pk_bf16(fmaxf(sum.x, 0.f), fmaxf(sum.y, 0.f), h01, l01);
+        split_pk_bf16(fmaxf(sum.z, 0.f), fmaxf(sum.w, 0.f), h23, l23);
+        const int64_t o = ((int64_t)img * 81 + oh * 9 + ow) * 64 + nh * 32 + c4;
+        *reinterpret_cast<uint2*>(d.y + o) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(d.y_lo + o) = make_uint2(l01, l23);
+      }
+    }
+    // the next phase's barrier orders these red reads before the DMA into this buffer
+  }
+}
+
 APEX_EXPORT int apex_conv2_img_fwd(Conv2ImgDesc d, int grid, hipStream_t st) {
   if (d.N <= 0 || d.x == nullptr || d.w == nullptr || d.y == nullptr || d.bias == nullptr)
     return (int)hipErrorInvalidValue;
   if (d.w2 != nullptr && d.bias2 == nullptr) return (int)hipErrorInvalidValue;
   if (((uintptr_t)d.x | (uintptr_t)d.w | (uintptr_t)(d.w2 ? d.w2 : d.w)) & 15) return (int)hipErrorInvalidValue;
   if ((uintptr_t)d.y & 7) return (int)hipErrorInvalidValue;
+  const bool split = d.x_lo != nullptr;
+  if (split) {
+    if (d.w_lo == nullptr || d.y_lo == nullptr || (d.w2 != nullptr && d.w2_lo == nullptr))
+      return (int)hipErrorInvalidValue;
+    if ((((uintptr_t)d.x_lo | (uintptr_t)d.w_lo | (uintptr_t)(d.w2_lo ? d.w2_lo : d.w_lo)) & 15) ||
+        ((uintptr_t)d.y_lo & 7))
+      return (int)hipErrorInvalidValue;
+  }
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
-  conv2_img_fwd_kernel<<<G, C2_THREADS, 0, st>>>(d);
+  if (split) conv2_img_fwd_split_kernel<<<G, C2S_THREADS, 0, st>>>(d);
+  else conv2_img_fwd_kernel<<<G, C2_THREADS, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }
 
@@ -198,6 +378,10 @@ struct Conv2DgradImgDesc {
   const bf16_t* mask;   // y1 [N][20][20][64] (ReLU mask source)
   bf16_t* dx;           // [N][20][20][64]
   int N;
+  // split mode: lo planes of dy, w and dx (value = hi + lo), or all null
+  const bf16_t* dy_lo;
+  const bf16_t* w_lo;
+  bf16_t* dx_lo;
 };
 
 #define C2D_SLOTS 121   // 11 x 11 padded dY slots, 128 B each
@@ -302,13 +486,148 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
   }
 }
 
+
+// Split ("fp32-accurate") conv2 data gradient: the same per-class GEMMs with
+// dY = dY_hi + dY_lo (both planes staged in LDS inside their zero rings) and
+// w = w_hi + w_lo, w_hi dY_hi + w_lo dY_hi + w_hi dY_lo per fragment pair.  Four
+// waves, one per stride-parity class and SIMD, each owning both channel halves: its
+// hi and lo weight fragments (2 x 2 x 16 x 8 registers) and the 8 accumulators fit the
+// 512 registers of a lone wave.  The fp32 result leaves as masked hi / lo planes.
+__global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2DgradImgDesc d) {
+  __shared__ __attribute__((aligned(16))) uint8_t sdy[2 * C2D_SLOTS * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sout[2 * 400 * 128];   // hi image, lo image
+  const int tid = threadIdx.x, lane = tid & 63, cls = tid >> 6, p = cls >> 1, q = cls & 1;
+  const int rr = lane & 31, kg = lane >> 5;
+  for (int i = tid; i < 2 * C2D_SLOTS * 8; i += 256) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
+  bf16x8 wh[2][16], wl[2][16];
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int a = (s >> 3) & 1, b = (s >> 2) & 1, co0 = ((s & 3) << 4) + kg * 8;
+      const int kh = p + 2 * a, kw = q + 2 * b, ci = nh * 32 + rr;
+      uint32_t u[4], v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o0 = ((co0 + 2 * e) * 16 + kh * 4 + kw) * 64 + ci, o1 = o0 + 16 * 64;
+        u[e] = (uint32_t)d.w[o0] | ((uint32_t)d.w[o1] << 16);
+        v[e] = (uint32_t)d.w_lo[o0] | ((uint32_t)d.w_lo[o1] << 16);
+      }
+      wh[nh][s] = __builtin_bit_cast(bf16x8, make_uint4(u[0], u[1], u[2], u[3]));
+      wl[nh][s] = __builtin_bit_cast(bf16x8, make_uint4(v[0], v[1], v[2], v[3]));
+    }
+  int pi[4], pj[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int r = min(t * 32 + rr, 99);
+    pi[t] = r / 10;
+    pj[t] = r - pi[t] * 10;
+  }
+  for (int img = blockIdx.x; img < d.N; img += gridDim.x) {
+    __syncthreads();   // previous image: LDS reads and output copy-out done
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(d.dy + (int64_t)img * 81 * 64);
+      const uint4* srl = reinterpret_cast<const uint4*>(d.dy_lo + (int64_t)img * 81 * 64);
+      for (int k = tid; k < 2 * 81 * 8; k += 256) {
+        const int pl = k >= 81 * 8 ? 1 : 0, kk = k - pl * 81 * 8;
+        const int px = kk >> 3, c = kk & 7, oh = px / 9, ow = px - oh * 9;
+        *reinterpret_cast<uint4*>(sdy + pl * C2D_SLOTS * 128 + c2d_off((oh + 1) * 11 + ow + 1, c)) =
+            pl ? srl[kk] : src[kk];
+      }
+    }
+    __syncthreads();
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[nh][t][j] = 0.f;
+    // B fragments (dY hi, lo) of step u + 1 = (s, t) are read while step u's six
+    // MFMAs run (explicit order: scheduler barriers around each step)
+    bf16x8 xf[2][2];
+#define C2DS_LDX(u_, dst_)                                                                   \
+    {                                                                                        \
+      const int s_ = (u_) >> 2, t_ = (u_) & 3;                                              \
+      const int off_ = c2d_off((pi[t_] - ((s_ >> 3) & 1) + 1) * 11 + (pj[t_] - ((s_ >> 2) & 1) + 1), \
+                               ((s_ & 3) << 1) | kg);                                        \
+      dst_[0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + off_));    \
+      dst_[1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + C2D_SLOTS * 128 + off_)); \
+    }
+    C2DS_LDX(0, xf[0])
+#pragma unroll
+    for (int u = 0; u < 64; ++u) {
+      const int s = u >> 2, t = u & 3;
+      if (u + 1 < 64) C2DS_LDX(u + 1, xf[(u + 1) & 1])
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {
+        acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[nh][s], xf[u & 1][0], acc[nh][t], 0, 0, 0);
+        acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[nh][s], xf[u & 1][1], acc[nh][t], 0, 0, 0);
+        acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[nh][s], xf[u & 1][0], acc[nh][t], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#undef C2DS_LDX
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t * 32 + rr >= 100) continue;
+      const int ih = 2 * pi[t] + p, iw = 2 * pj[t] + q, px = ih * 20 + iw;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int ch = nh * 32 + 8 * g + 4 * kg;
+          uint32_t h01, l01, h23, l23;
+          split_pk_bf16(acc[nh][t][4 * g], acc[nh][t][4 * g + 1], h01, l01);
+          split_pk_bf16(acc[nh][t][4 * g + 2], acc[nh][t][4 * g + 3], h23, l23);
+          const int o = c2d_off(px, ch >> 3) + (ch & 7) * 2;
+          *reinterpret_cast<uint2*>(sout + o) = make_uint2(h01, h23);
+          *reinterpret_cast<uint2*>(sout + 400 * 128 + o) = make_uint2(l01, l23);
+        }
+    }
+    __syncthreads();
+    const uint4* msrc = reinterpret_cast<const uint4*>(d.mask + (int64_t)img * 400 * 64);
+    uint4* dst = reinterpret_cast<uint4*>(d.dx + (int64_t)img * 400 * 64);
+    uint4* dsl = reinterpret_cast<uint4*>(d.dx_lo + (int64_t)img * 400 * 64);
+#pragma unroll
+    for (int i0 = 0; i0 < 13; i0 += 7) {     // 3200 chunks / 256 threads: 13 rounds, mask loads 7 ahead
+      uint4 mv[7];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const int k = tid + 256 * (i0 + i);
+        if (i0 + i < 13 && k < 3200) mv[i] = msrc[k];
+      }
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const int k = tid + 256 * (i0 + i);
+        if (i0 + i < 13 && k < 3200) {
+          const int o = c2d_off(k >> 3, k & 7);
+          uint4 v = *reinterpret_cast<const uint4*>(sout + o);
+          uint4 vl = *reinterpret_cast<const uint4*>(sout + 400 * 128 + o);
+          v = make_uint4(mask_bf16x2(v.x, mv[i].x), mask_bf16x2(v.y, mv[i].y), mask_bf16x2(v.z, mv[i].z),
+                         mask_bf16x2(v.w, mv[i].w));
+          vl = make_uint4(mask_bf16x2(vl.x, mv[i].x), mask_bf16x2(vl.y, mv[i].y), mask_bf16x2(vl.z, mv[i].z),
+                          mask_bf16x2(vl.w, mv[i].w));
+          dst[k] = v;
+          dsl[k] = vl;
+        }
+      }
+    }
+  }
+}
+
 APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t st) {
   if (d.N <= 0 || d.dy == nullptr || d.w == nullptr || d.mask == nullptr || d.dx == nullptr)
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)d.dy | (uintptr_t)d.w | (uintptr_t)d.mask | (uintptr_t)d.dx) & 15) return (int)hipErrorInvalidValue;
+  const bool split = d.dy_lo != nullptr;
+  if (split && (d.w_lo == nullptr || d.dx_lo == nullptr || (((uintptr_t)d.dy_lo | (uintptr_t)d.dx_lo) & 15)))
+    return (int)hipErrorInvalidValue;
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
-  conv2_dgrad_img_kernel<<<G, 512, 0, st>>>(d);
+  if (split) conv2_dgrad_img_split_kernel<<<G, 256, 0, st>>>(d);
+  else conv2_dgrad_img_kernel<<<G, 512, 0, st>>>(d);
   APEX_CHECK_LAUNCH();
 }
 

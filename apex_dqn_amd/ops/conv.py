@@ -141,9 +141,11 @@ CONV2_IMG = _os.environ.get("APEX_CONV2_IMG", "1") != "0"
 
 
 def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
-                  w2=None, b2=None, rows_first: int = 0, grid: int = 0) -> None:
+                  w2=None, b2=None, rows_first: int = 0, grid: int = 0, x_lo=None, w_lo=None, w2_lo=None,
+                  out_lo=None) -> None:
     """conv2 + bias + ReLU, one persistent workgroup per CU walking whole images
-    (image staged once in LDS, weights in VGPRs); online/target switch per image."""
+    (image staged once in LDS, weights in VGPRs); online/target switch per image.
+    Split mode (``x_lo`` .. ``out_lo``): the hi / lo plane kernel."""
     from .conv_sigs import Conv2ImgDesc
     N = x.shape[0]
     assert tuple(x.shape[1:]) == (20, 20, 64) and tuple(w.shape) == (64, 4, 4, 64) and tuple(out.shape) == (N, 9, 9, 64)
@@ -154,6 +156,10 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
         assert w2.is_contiguous() and tuple(w2.shape) == (64, 4, 4, 64)
         d.w2, d.bias2 = w2.data_ptr(), b2.data_ptr()
     d.N, d.img_switch = N, int(rows_first) if w2 is not None else N
+    if x_lo is not None:
+        for t in (x_lo, w_lo, out_lo) + ((w2_lo,) if w2 is not None else ()):
+            assert t is not None and t.is_contiguous() and t.dtype == torch.bfloat16
+        d.x_lo, d.w_lo, d.w2_lo, d.y_lo = x_lo.data_ptr(), w_lo.data_ptr(), _lib.ptr(w2_lo), out_lo.data_ptr()
     _lib.check(lib.apex_conv2_img_fwd(d, int(grid), _lib.stream_ptr()), "conv2_img_fwd")
 
 
@@ -165,9 +171,9 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
     Cout, KH, KW, _ = w.shape
     OH, OW = out.shape[1], out.shape[2]
     split = x_lo is not None
-    if CONV2_IMG and not split and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
+    if CONV2_IMG and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
             hasattr(lib, "apex_conv2_img_fwd"):
-        conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first)
+        conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo, out_lo=out_lo)
         return
     if not _split_ok(w2, rows_first, OH * OW):   # batch not tile-aligned: one launch per weight set
         r = rows_first
@@ -261,9 +267,10 @@ CONV2_DGRAD_IMG = _os.environ.get("APEX_CONV2_DGRAD_IMG", "1") != "0"
 
 
 def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor,
-                    grid: int = 0) -> None:
+                    grid: int = 0, dy_lo=None, w_lo=None, out_lo=None) -> None:
     """conv2 data gradient on the image-resident kernel (csrc/conv2_img.hip): one wave
-    per (stride-parity class, channel half), dY staged in LDS inside a zero ring."""
+    per (stride-parity class, channel half), dY staged in LDS inside a zero ring.
+    Split mode (``dy_lo``, ``w_lo``, ``out_lo``): the hi / lo plane kernel."""
     from .conv_sigs import Conv2DgradImgDesc
     N = dy.shape[0]
     assert tuple(dy.shape) == (N, 9, 9, 64) and tuple(out.shape) == (N, 20, 20, 64)
@@ -271,6 +278,10 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
     assert dy.is_contiguous() and out.is_contiguous() and mask.is_contiguous() and w2.is_contiguous()
     d = Conv2DgradImgDesc()
     d.dy, d.w, d.mask, d.dx, d.N = dy.data_ptr(), w2.data_ptr(), mask.data_ptr(), out.data_ptr(), N
+    if dy_lo is not None:
+        for t in (dy_lo, w_lo, out_lo):
+            assert t is not None and t.is_contiguous() and t.dtype == torch.bfloat16
+        d.dy_lo, d.w_lo, d.dx_lo = dy_lo.data_ptr(), w_lo.data_ptr(), out_lo.data_ptr()
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 
@@ -281,8 +292,8 @@ def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out
     K-major from the OHWI tensor per class."""
     N = dy.shape[0]
     assert w2.shape == (64, 4, 4, 64)
-    if CONV2_DGRAD_IMG and dy_lo is None and hasattr(lib, "apex_conv2_dgrad_img"):
-        conv2_dgrad_img(lib, dy, w2, mask, out)
+    if CONV2_DGRAD_IMG and hasattr(lib, "apex_conv2_dgrad_img"):
+        conv2_dgrad_img(lib, dy, w2, mask, out, dy_lo=dy_lo, w_lo=w_lo, out_lo=out_lo)
         return
     d = _conv_desc(x=dy.data_ptr(), w=w2.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
                    Cin=64, OH=10, OW=10, Cout=64, KH=2, KW=2, stride=1, pad=1, mode=1, K=256, ncls=4,

@@ -12,12 +12,13 @@ c_f = ctypes.c_float
 class Conv2ImgDesc(ctypes.Structure):
     """Image-resident conv2 forward (mirrors ``Conv2ImgDesc`` in csrc/conv2_img.hip)."""
     _fields_ = [("x", c_p), ("w", c_p), ("w2", c_p), ("bias", c_p), ("bias2", c_p), ("y", c_p),
-                ("N", c_i), ("img_switch", c_i)]
+                ("N", c_i), ("img_switch", c_i), ("x_lo", c_p), ("w_lo", c_p), ("w2_lo", c_p), ("y_lo", c_p)]
 
 
 class Conv2DgradImgDesc(ctypes.Structure):
     """Image-resident conv2 data gradient (mirrors ``Conv2DgradImgDesc`` in csrc/conv2_img.hip)."""
-    _fields_ = [("dy", c_p), ("w", c_p), ("mask", c_p), ("dx", c_p), ("N", c_i)]
+    _fields_ = [("dy", c_p), ("w", c_p), ("mask", c_p), ("dx", c_p), ("N", c_i), ("dy_lo", c_p), ("w_lo", c_p),
+                ("dx_lo", c_p)]
 
 
 class Conv3DgradImgDesc(ctypes.Structure):

@@ -335,3 +335,42 @@ def test_whole_step_fp32_split_matches_fp64_oracle():
     assert max(e.values()) < 1e-3, e
     # the split path is a different precision class from the bf16-operand path
     assert max(e.values()) < 0.2 * max(errs_all["bf16"].values())
+
+
+@pytest.mark.parametrize("grid", [0, 5])
+def test_conv2_image_resident_split_kernels_vs_generic(monkeypatch, grid):
+    """The image-resident conv2 forward / data-gradient kernels in split mode (LDS-DMA
+    double-buffered planes; four-wave class-owning dgrad) match fp64 and the generic
+    implicit-GEMM split path; small grids walk several images per workgroup across
+    the online / target switch."""
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(grid + 3)
+    lib = _lib()
+    N1, N2 = 23, 14
+    x = torch.relu(torch.randn(N1 + N2, 20, 20, 64, generator=g))
+    wa, wb = torch.randn(64, 4, 4, 64, generator=g) * 0.03, torch.randn(64, 4, 4, 64, generator=g) * 0.03
+    ba, bb = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    (xh, xl), (wah, wal), (wbh, wbl) = _split(x), _split(wa), _split(wb)
+    hi, lo = _empty2(N1 + N2, 9, 9, 64)
+    C.conv2_img_fwd(lib, xh, wah, ba, hi, wbh, bb, N1, grid=grid, x_lo=xl, w_lo=wal, w2_lo=wbl, out_lo=lo)
+    xd = _c(x)
+    ref = torch.cat([R.conv_fwd(xd[:N1], _c(wa), _c(ba), 2, torch.float64),
+                     R.conv_fwd(xd[N1:], _c(wb), _c(bb), 2, torch.float64)])
+    assert _rel(_join(hi, lo), ref) < TOL
+    monkeypatch.setattr(C, "CONV2_IMG", False)
+    gh, gl = _empty2(N1 + N2, 9, 9, 64)
+    C.conv_fwd(lib, xh, wah, ba, 2, gh, wbh, bb, N1, x_lo=xl, w_lo=wal, w2_lo=wbl, out_lo=gl)
+    assert _rel(_join(hi, lo), _join(gh, gl)) < TOL
+    # data gradient
+    N = N1 + N2
+    dy = torch.randn(N, 9, 9, 64, generator=g)
+    y1 = torch.randn(N, 20, 20, 64, generator=g).to(DEV, torch.bfloat16)
+    dh, dl = _split(dy)
+    h1, l1 = _empty2(N, 20, 20, 64)
+    C.conv2_dgrad_img(lib, dh, wah, y1, h1, grid=grid, dy_lo=dl, w_lo=wal, out_lo=l1)
+    ref1 = R.conv_dgrad(_c(dy), _c(wa), (N, 20, 20, 64), 2, _c(y1), torch.float64)
+    assert _rel(_join(h1, l1), ref1) < TOL
+    monkeypatch.setattr(C, "CONV2_DGRAD_IMG", False)
+    g1h, g1l = _empty2(N, 20, 20, 64)
+    C.conv2_dgrad(lib, dh, wah, y1, g1h, dy_lo=dl, w_lo=wal, out_lo=g1l)
+    assert _rel(_join(h1, l1), _join(g1h, g1l)) < TOL
