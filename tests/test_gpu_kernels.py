@@ -389,13 +389,15 @@ def test_head_wgrad_prio_matches_separate_launches():
     torch.testing.assert_close(n1, n0, rtol=1e-12, atol=1e-9)
 
 
-def test_fc_head_wgrad_prio_matches_separate_launches():
+@pytest.mark.parametrize("B", [512, 1024])
+def test_fc_head_wgrad_prio_matches_separate_launches(B):
     """fc wgrad + head wgrad + priority write-back in one launch == the three ops
     launched separately (fc gradient, its squared-norm partials and the tree equal;
-    head gradient up to summation order)."""
+    head gradient up to summation order).  B = 1024: four write-back items per thread
+    of the 256-thread block (TU_MAXR), heavy duplicate indices."""
     from apex_dqn_amd.ops.fused_ops import HipBackend
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
-    B, A = 512, 4
+    A = 4
     Hon, Htg, Pon, Ptg, act, rew, gam, isw = _head_inputs(B, A, seed=8)
     g = torch.Generator(device="cpu").manual_seed(9)
     dH = (torch.randn(B, 1024, generator=g) * 0.01).to(DEV, torch.bfloat16)
