@@ -16,10 +16,13 @@
 //     staged image (an output pixel's 8 channels of one tap are 16 contiguous bytes);
 //   * the four kernel-row partial sums meet in LDS (fp32, fixed order), then bias,
 //     ReLU, bf16 pack and 8-byte NHWC stores.
-// LDS image layout: column-parity planes (the stride-2 taps of one kw only touch one
-// parity), pixel (ih, iw) at slot ih * 10 + iw / 2 of plane iw & 1, 128 B per pixel,
-// 16-B channel chunk c stored at c ^ ((slot >> 1) & 7): the 16 lanes of a
-// ds_read_b128 phase (16 consecutive output pixels) mostly hit distinct bank groups.
+// LDS image layout (bank-conflict-free A reads): M rows are output pixels on a 10-wide
+// grid (r = 10 oh + ow; ow = 9 and r >= 90 are padding, 96 rows = 3 tiles), and the
+// staged image stores its pixels class-major, P = (input stride-parity class) * 100 +
+// (ih >> 1) * 10 + (iw >> 1), 128 B each with 16-B chunk c at c ^ ((P >> 1) & 7).  The
+// 16 lanes of a ds_read_b128 lane group read 16 pixels whose P are distinct mod 16 (8 of
+// each parity, distinct (P >> 1) & 7): 16 distinct bank groups.  (The 9-wide grid over
+// column-parity planes measured 29-41 % bank-conflict cycles.)
 // Online / target weights switch per image (img_switch), so any batch works in one
 // launch.
 #include "mfma_common.h"
@@ -42,17 +45,18 @@ struct Conv2ImgDesc {
 };
 
 #define C2_THREADS 512
-#define C2_IMG 51200            // staged image bytes
+#define C2_IMG 51200            // image bytes (global)
+#define C2_LDSIMG 52224         // staged image bytes: 408 class-major pixel slots (padding rows read past 400)
 #define C2_CHUNKS 3200          // 16-B chunks per image
 #define C2_PF 7                 // prefetch chunks per thread (ceil(3200 / 512))
 
-__device__ __forceinline__ int c2_lds_off(int ih, int iw, int c) {
-  const int slot = ih * 10 + (iw >> 1);
-  return ((((iw & 1) * 200 + slot)) << 7) + ((c ^ ((slot >> 1) & 7)) << 4);
-}
+// class-major pixel index of input pixel (ih, iw) and the byte offset of its chunk c
+__device__ __forceinline__ int c2_pix(int ih, int iw) { return ((ih & 1) * 2 + (iw & 1)) * 100 + (ih >> 1) * 10 + (iw >> 1); }
+__device__ __forceinline__ int c2_off(int P, int c) { return (P << 7) + ((c ^ ((P >> 1) & 7)) << 4); }
+__device__ __forceinline__ int c2_lds_off(int ih, int iw, int c) { return c2_off(c2_pix(ih, iw), c); }
 
 __global__ void __launch_bounds__(C2_THREADS, 1) conv2_img_fwd_kernel(Conv2ImgDesc d) {
-  __shared__ __attribute__((aligned(16))) uint8_t simg[C2_IMG];
+  __shared__ __attribute__((aligned(16))) uint8_t simg[C2_LDSIMG];
   __shared__ __attribute__((aligned(16))) float red[8 * 3 * 32 * 32];   // 96 KB of partial tiles
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nh = wv & 1, kq = wv >> 1;          // output-channel half, kernel row kh
@@ -75,13 +79,13 @@ __global__ void __launch_bounds__(C2_THREADS, 1) conv2_img_fwd_kernel(Conv2ImgDe
     pf5 = src_[5 * C2_THREADS];                                                           \
     if (last) pf6 = src_[6 * C2_THREADS];                                                 \
   }
-  // per m-tile: the output pixel of this lane's A row (rows past 80 repeat pixel 80)
+  // per m-tile: class-major pixel of this lane's A row at kernel row kq, column kw = 0
+  // (10-wide grid; padding rows read in-range garbage that is never stored)
   int slot0[3];
 #pragma unroll
   for (int mt = 0; mt < 3; ++mt) {
-    const int r = min(mt * 32 + rr, 80);
-    const int oh = r / 9, ow = r - oh * 9;
-    slot0[mt] = (2 * oh + kq) * 10 + ow;
+    const int r = mt * 32 + rr, oh = r / 10, ow = r - oh * 10;
+    slot0[mt] = (kq & 1) * 200 + (oh + (kq >> 1)) * 10 + ow;
   }
   bf16x8 bfr[16];
   int cur_set = -1;
@@ -125,12 +129,13 @@ __global__ void __launch_bounds__(C2_THREADS, 1) conv2_img_fwd_kernel(Conv2ImgDe
       for (int j = 0; j < 16; ++j) acc[mt][j] = 0.f;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      const int par = (s >> 2) & 1, c = ((s & 3) << 1) | kg;
+      // K step s: column kw = s >> 2 (parity kw & 1 -> class +100, kw >> 1 -> pixel +1),
+      // chunk ((s & 3) << 1) | kg
+      const int c = ((s & 3) << 1) | kg;
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt) {
-        const int slot = slot0[mt] + (s >> 3);
-        const int off = ((par * 200 + slot) << 7) + ((c ^ ((slot >> 1) & 7)) << 4);
-        const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(simg + off));
+        const int P = slot0[mt] + ((s >> 2) & 1) * 100 + (s >> 3);
+        const bf16x8 a = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(simg + c2_off(P, c)));
         acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr[s], acc[mt], 0, 0, 0);
       }
     }
@@ -151,18 +156,18 @@ __global__ void __launch_bounds__(C2_THREADS, 1) conv2_img_fwd_kernel(Conv2ImgDe
                                   bias[nh * 32 + c4 + 3]);
 #pragma unroll
     for (int it = 0; it < 3; ++it) {
-      const int r = 24 * kq + 8 * it + (lane >> 3);
+      const int r = 24 * kq + 8 * it + (lane >> 3), oh = r / 10, ow = r - oh * 10;
       const int mt = r >> 5, row = r & 31;
-      float4 sum = bv;
+      if (ow < 9 && oh < 9) {
+        float4 sum = bv;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(red + (((nh + 2 * q) * 3 + mt) * 32 + row) * 32 + c4);
-        sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
-      }
-      if (r < 81) {
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(red + (((nh + 2 * q) * 3 + mt) * 32 + row) * 32 + c4);
+          sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+        }
         const uint2 o = make_uint2(cvt_pk_bf16(fmaxf(sum.x, 0.f), fmaxf(sum.y, 0.f)),
                                    cvt_pk_bf16(fmaxf(sum.z, 0.f), fmaxf(sum.w, 0.f)));
-        *reinterpret_cast<uint2*>(d.y + ((int64_t)img * 81 + r) * 64 + nh * 32 + c4) = o;
+        *reinterpret_cast<uint2*>(d.y + ((int64_t)img * 81 + oh * 9 + ow) * 64 + nh * 32 + c4) = o;
       }
     }
   }
