@@ -104,6 +104,8 @@ class RuntimeConf:
     replay_capacity: Optional[int] = None  # physical capacity, global over the ranks' shards
                                            # (default: soft_capacity * 1.25 + 1024)
     heartbeat_timeout: float = 60.0
+    comm_backend: str = "torch"     # DP collectives: "torch" (torch.distributed / RCCL process group) |
+                                    # "native" (parallel/rccl.py: own RCCL communicator + comm stream)
     force_dp: bool = False          # run the data-parallel step (collectives + sharded replay) even at
                                     # world 1 (needs an initialised process group; checks / overhead)
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
@@ -174,6 +176,8 @@ class ApexConfig:
             raise ValueError("Learner.replay_sample_size must be >= 1")
         if self.Runtime.world_size < 1:
             raise ValueError("Runtime.world_size must be >= 1")
+        if self.Runtime.comm_backend not in ("torch", "native"):
+            raise ValueError("Runtime.comm_backend must be 'torch' or 'native'")
         if self.Runtime.loss not in ("huber", "mse"):
             raise ValueError("Runtime.loss must be 'huber' or 'mse'")
         net = self.network

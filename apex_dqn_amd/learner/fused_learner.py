@@ -147,9 +147,15 @@ class FusedNatureLearner:
         # Rows drawn elsewhere carry IS weight 0, so the IS weights always enter the loss
         # (with use_is_weights off: beta = 0, i.e. weights 0 / W B / M only).
         self._isw = bool(self.rt.use_is_weights) or self._dp
+        # the DP step's collectives: torch.distributed (RCCL process group / gloo) or the
+        # native RCCL communicator on its own stream (Runtime.comm_backend, parallel/rccl.py)
+        self.coll = None
         if self._dp:
+            from ..parallel.rccl import make_collectives
+            backend = self.rt.comm_backend if cuda else "torch"
+            self.coll = make_collectives(comm, backend, self.device)
             _enable_sharding(replay, comm, self.rt)
-            replay.gather_shard_stats()
+            replay.gather_shard_stats(coll=self.coll)
         # DP step as ONE captured graph including the RCCL collectives (backend nccl);
         # gloo (CPU tests, one-GPU rehearsals) cannot be captured: eager DP steps
         self._dp_graphs = self._dp and cuda and self._backend_name() == "nccl"
@@ -374,13 +380,12 @@ class FusedNatureLearner:
         this step's priority write-back, consumed by the next batch's global draw
         inside the optimizer launch) are exchanged while the conv backward runs; the
         conv bucket follows; the optimizer waits for all three."""
-        import torch.distributed as dist
         cut = self.layout.offsets["wfc"]
         self._seg1()
-        w_fc = dist.all_reduce(self.gcomm[cut:], op=dist.ReduceOp.SUM, async_op=True)
-        w_r = self.replay.gather_shard_stats(async_op=True)
+        w_fc = self.coll.all_reduce(self.gcomm[cut:])
+        w_r = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
         self._seg2()     # conv backward overlaps the fc/head bucket all-reduce
-        w_cv = dist.all_reduce(self.gcomm[:cut], op=dist.ReduceOp.SUM, async_op=True)
+        w_cv = self.coll.all_reduce(self.gcomm[:cut])
         w_fc.wait()
         w_r.wait()
         w_cv.wait()
@@ -500,7 +505,7 @@ class FusedNatureLearner:
         """Re-gather the shard statistics (after host-side inserts / eviction; a
         collective: every rank calls it at the same point)."""
         if self._dp:
-            self.replay.gather_shard_stats()
+            self.replay.gather_shard_stats(coll=self.coll)
 
     def _snapshot(self):
         rp = self.replay

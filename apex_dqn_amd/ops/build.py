@@ -4,6 +4,8 @@
   --offload-arch=gfx950`` into one shared library with a C ABI (ctypes).
 * ``libapex_runtime.so`` -- host C++ runtime (``csrc/runtime/*.cpp``: sum-tree,
   n-step builder, frame ring bookkeeping) built with g++.
+* ``libapex_comm.so`` -- the native RCCL communicator (``csrc/comm/rccl_comm.cpp``),
+  host code built with hipcc against the RCCL / HIP headers (librccl is dlopen()ed).
 
 Objects are rebuilt only when their source (or a header) is newer.  The
 libraries land in ``apex_dqn_amd/ops/_build/`` which ships to the GPU box
@@ -25,6 +27,7 @@ OUT = os.path.join(HERE, "_build")
 KERNEL_LIB = os.path.join(OUT, "libapex_kernels.so")
 KERNEL_DEBUG_LIB = os.path.join(OUT, "libapex_kernels_debug.so")
 RUNTIME_LIB = os.path.join(OUT, "libapex_runtime.so")
+COMM_LIB = os.path.join(OUT, "libapex_comm.so")
 ARCH = os.environ.get("APEX_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -95,8 +98,19 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     return RUNTIME_LIB
 
 
+def build_comm(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(OUT, exist_ok=True)
+    src = os.path.join(CSRC, "comm", "rccl_comm.cpp")
+    if force or _newer([src], COMM_LIB):
+        _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", "-I", "/opt/rocm/include", src, "-o", COMM_LIB, "-ldl"])
+        if verbose:
+            print(f"built {COMM_LIB}")
+    return COMM_LIB
+
+
 def build_all(force: bool = False, verbose: bool = True, debug: bool = True) -> None:
     build_runtime(force=force, verbose=verbose)
+    build_comm(force=force, verbose=verbose)
     build_kernels(force=force, verbose=verbose)
     if debug:
         build_kernels(force=force, verbose=verbose, debug=True)

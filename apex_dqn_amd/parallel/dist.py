@@ -9,8 +9,10 @@ SURVEY §2.4.1 M1-M11) -- with collectives:
   (mean) for the data-parallel learner (M-DP, new);
 * ``broadcast_flat`` / ``broadcast_module``: parameter broadcast from rank 0
   (replaces M1-M4 weight publish);
-* ``allgather_scalars``: replay-shard statistics (sum p^alpha, min p^alpha,
-  live count) for global IS weights (replaces M8's size RPC).
+* ``allgather_scalars``: small host-side statistics;
+* the DP learner step's collectives (bucketed gradient all-reduce, replay-shard
+  statistics all-gather) go through ``parallel/rccl.py``: torch.distributed or the
+  native RCCL communicator (``Runtime.comm_backend``).
 
 Backend ``nccl`` is RCCL on ROCm; ``gloo`` serves CPU configs and the
 multi-process CPU tests.  Rendezvous comes from torchrun's env vars
@@ -83,8 +85,20 @@ class Comm:
                 dist.barrier()
 
     def shutdown(self) -> None:
+        native = getattr(self, "_native", None)
+        if native is not None:
+            native.close()
+            self._native = None
         if dist.is_initialized():
             dist.destroy_process_group()
+
+    def abort(self) -> None:
+        """Failure path: abort the native communicator (outstanding collectives are
+        cancelled) so the process can exit and torchrun restart the group."""
+        native = getattr(self, "_native", None)
+        if native is not None:
+            native.abort()
+            self._native = None
 
     # ------------------------------------------------------ collectives
     def allreduce_flat(self, flat: torch.Tensor, average: bool = True, async_op: bool = False):

@@ -1,0 +1,246 @@
+"""Native RCCL communicator (``csrc/comm/rccl_comm.cpp``) and the collectives
+interface of the data-parallel learner step.
+
+SURVEY §5.8 plans the learner's collectives as a thin native communicator over
+librccl with explicit HIP streams, the unique id exchanged through the
+torch.distributed rendezvous; §5.3 adds a communicator abort for failure
+recovery.  ``RcclComm`` is that communicator: ``ncclCommInitRank`` over the same
+librccl torch already loaded (one RCCL instance per process), collectives
+enqueued on a dedicated comm stream that waits on the compute stream through
+events -- inside a HIP-graph capture these waits become graph edges, so the
+learner's DP step stays ONE captured graph -- and ``abort()`` /
+``check()`` on the communicator's asynchronous error state.
+
+``make_collectives(comm, backend)`` returns the object the learner step uses:
+``TorchCollectives`` (torch.distributed: RCCL via the ``nccl`` process group, or
+gloo on CPU) or ``NativeCollectives`` (this communicator).  Both expose
+``all_reduce(t, op)`` and ``all_gather_into(out, inp)`` returning a handle whose
+``wait()`` makes the current stream wait for the result.
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+import os
+from typing import Optional
+
+import torch
+
+_DTYPES = {torch.float32: 7, torch.float64: 8, torch.bfloat16: 9, torch.float16: 6, torch.int32: 2,
+           torch.int64: 4, torch.uint8: 1}
+_OPS = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
+_LIB = None
+
+
+def _torch_rccl_path() -> Optional[str]:
+    cands = glob.glob(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so*"))
+    return cands[0] if cands else None
+
+
+def load_comm_lib() -> ctypes.CDLL:
+    """libapex_comm.so with librccl resolved (torch's bundled copy first)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    from ..ops.build import COMM_LIB
+    if not os.path.exists(COMM_LIB):
+        raise RuntimeError(f"{COMM_LIB} missing: run `python -m apex_dqn_amd.ops.build`")
+    lib = ctypes.CDLL(COMM_LIB)
+    c_p, c_i, c_sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    sigs = {
+        "apex_comm_load": ([ctypes.c_char_p], c_i),
+        "apex_comm_version": ([], c_i),
+        "apex_comm_error_string": ([c_i], ctypes.c_char_p),
+        "apex_comm_unique_id": ([ctypes.c_char_p], c_i),
+        "apex_comm_id_bytes": ([], c_i),
+        "apex_comm_init": ([ctypes.POINTER(c_p), c_i, ctypes.c_char_p, c_i], c_i),
+        "apex_comm_all_reduce": ([c_p, c_p, c_p, c_sz, c_i, c_i, c_p], c_i),
+        "apex_comm_all_gather": ([c_p, c_p, c_p, c_sz, c_i, c_p], c_i),
+        "apex_comm_broadcast": ([c_p, c_p, c_p, c_sz, c_i, c_i, c_p], c_i),
+        "apex_comm_group_start": ([], c_i),
+        "apex_comm_group_end": ([], c_i),
+        "apex_comm_async_error": ([c_p], c_i),
+        "apex_comm_abort": ([c_p], c_i),
+        "apex_comm_destroy": ([c_p], c_i),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(lib, name)
+        fn.argtypes, fn.restype = args, res
+    path = _torch_rccl_path()
+    rc = lib.apex_comm_load(path.encode() if path else None)
+    if rc != 0:
+        raise RuntimeError(f"apex_comm_load({path}): {lib.apex_comm_error_string(rc).decode()}")
+    _LIB = lib
+    return lib
+
+
+class RcclError(RuntimeError):
+    pass
+
+
+class RcclComm:
+    """One RCCL communicator for ``rank`` of ``world`` on ``device``.  The unique id
+    comes from rank 0 through ``exchange(id_tensor)`` -- by default a broadcast over
+    the initialised torch.distributed default group."""
+
+    def __init__(self, rank: int, world: int, device, exchange=None):
+        self.lib = load_comm_lib()
+        self.rank, self.world = int(rank), int(world)
+        self.device = torch.device(device)
+        nb = self.lib.apex_comm_id_bytes()
+        buf = ctypes.create_string_buffer(nb)
+        if self.rank == 0:
+            self._check(self.lib.apex_comm_unique_id(buf), "unique_id")
+        idt = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+        if self.world > 1:
+            if exchange is None:
+                import torch.distributed as dist
+                dev = self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+                t = idt.to(dev)
+                dist.broadcast(t, src=0)
+                idt = t.cpu()
+            else:
+                idt = exchange(idt)
+        self._id = bytes(idt.numpy().tobytes())
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            self._check(self.lib.apex_comm_init(ctypes.byref(h), self.world, self._id, self.rank), "comm_init")
+        self.handle = h
+        self.stream = torch.cuda.Stream(self.device)
+        self._closed = False
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise RcclError(f"rccl {what} failed: {self.lib.apex_comm_error_string(rc).decode()} ({rc})")
+
+    @property
+    def version(self) -> int:
+        return int(self.lib.apex_comm_version())
+
+    # ----------------------------------------------------------- raw enqueue
+    def _enqueue(self, fn, what: str, *args) -> None:
+        self._check(fn(self.handle, *args), what)
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum", stream=None) -> None:
+        """In-place all-reduce on ``stream`` (default: the current stream)."""
+        s = stream or torch.cuda.current_stream(self.device)
+        self._enqueue(self.lib.apex_comm_all_reduce, "all_reduce", t.data_ptr(), t.data_ptr(), t.numel(),
+                      _DTYPES[t.dtype], _OPS[op], s.cuda_stream)
+
+    def all_gather_(self, out: torch.Tensor, inp: torch.Tensor, stream=None) -> None:
+        assert out.numel() == inp.numel() * self.world and out.dtype == inp.dtype
+        s = stream or torch.cuda.current_stream(self.device)
+        self._enqueue(self.lib.apex_comm_all_gather, "all_gather", inp.data_ptr(), out.data_ptr(), inp.numel(),
+                      _DTYPES[inp.dtype], s.cuda_stream)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0, stream=None) -> None:
+        s = stream or torch.cuda.current_stream(self.device)
+        self._enqueue(self.lib.apex_comm_broadcast, "broadcast", t.data_ptr(), t.data_ptr(), t.numel(),
+                      _DTYPES[t.dtype], int(src), s.cuda_stream)
+
+    # ------------------------------------------------------------- health
+    def check(self) -> None:
+        """Raise if the communicator has an asynchronous error (peer failure)."""
+        rc = self.lib.apex_comm_async_error(self.handle)
+        if rc != 0:
+            raise RcclError(f"rccl async error: {self.lib.apex_comm_error_string(rc).decode()} ({rc})")
+
+    def abort(self) -> None:
+        """Cancel outstanding collectives and free the communicator (a rank whose
+        peer died must not block in teardown; the elastic restart rebuilds it)."""
+        if not self._closed:
+            self.lib.apex_comm_abort(self.handle)
+            self._closed = True
+
+    def close(self) -> None:
+        if not self._closed:
+            torch.cuda.synchronize(self.device)
+            self.lib.apex_comm_destroy(self.handle)
+            self._closed = True
+
+
+# ------------------------------------------------------------------ collectives
+class _Done:
+    def wait(self) -> None:
+        pass
+
+
+class _TorchWork:
+    def __init__(self, work):
+        self.work = work
+
+    def wait(self) -> None:
+        if self.work is not None:
+            self.work.wait()
+
+
+class _StreamWork:
+    """Completion of a collective enqueued on the comm stream: ``wait`` makes the
+    current stream wait for it (a graph edge under capture)."""
+
+    def __init__(self, comm_stream, device):
+        self.comm_stream, self.device = comm_stream, device
+
+    def wait(self) -> None:
+        torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+
+
+class TorchCollectives:
+    name = "torch"
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum"):
+        import torch.distributed as dist
+        rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+        return _TorchWork(dist.all_reduce(t, op=rop, group=self.group, async_op=True))
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
+        import torch.distributed as dist
+        if dist.get_backend(self.group) == "nccl":
+            return _TorchWork(dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True))
+        # gloo (CPU tests, one-GPU rehearsals; its all_gather takes no CUDA tensors): a
+        # SUM all-reduce of the rank-placed rows, exact (every other row is zero)
+        W, n = dist.get_world_size(self.group), inp.numel()
+        r = dist.get_rank(self.group)
+        out.zero_()
+        out.view(W, n)[r].copy_(inp.reshape(-1))
+        return _TorchWork(dist.all_reduce(out, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+
+class NativeCollectives:
+    """The DP step's collectives on the native communicator's own stream."""
+    name = "native"
+
+    def __init__(self, comm: RcclComm):
+        self.comm = comm
+
+    def _fork(self):
+        cur = torch.cuda.current_stream(self.comm.device)
+        self.comm.stream.wait_stream(cur)
+        return self.comm.stream
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum"):
+        s = self._fork()
+        self.comm.all_reduce_(t, op, stream=s)
+        return _StreamWork(s, self.comm.device)
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
+        s = self._fork()
+        self.comm.all_gather_(out, inp, stream=s)
+        return _StreamWork(s, self.comm.device)
+
+
+def make_collectives(comm, backend: str = "torch", device=None):
+    """Collectives for the learner's DP step: ``torch`` (torch.distributed) or
+    ``native`` (RcclComm; GPU ranks with an initialised process group)."""
+    if backend == "native":
+        nc = getattr(comm, "_native", None)
+        if nc is None:
+            nc = RcclComm(comm.rank, comm.world_size, device if device is not None else comm.device)
+            comm._native = nc
+        return NativeCollectives(nc)
+    if backend != "torch":
+        raise ValueError("Runtime.comm_backend must be 'torch' or 'native'")
+    return TorchCollectives(getattr(comm, "group", None))

@@ -199,22 +199,21 @@ class GpuReplayShard:
     def sharded(self) -> bool:
         return self.shard_stats is not None
 
-    def gather_shard_stats(self, async_op: bool = False):
+    def gather_shard_stats(self, async_op: bool = False, coll=None):
         """All-gather every shard's (sum p^alpha, min p^alpha) into ``shard_stats``
         (a collective; device-side, HIP-graph capturable over RCCL).  Call it after
-        the last tree mutation that the next draw must see."""
-        import torch.distributed as dist
+        the last tree mutation that the next draw must see.  ``coll``: the learner's
+        collectives (parallel/rccl.py; torch.distributed by default).  With
+        ``async_op`` the returned handle's ``wait()`` orders the result."""
+        from ..parallel.rccl import TorchCollectives
         root = self.offs[self.L]
         self.local_stats[0:1].copy_(self.nodes[root:root + 1])
         self.local_stats[1:2].copy_(self.min_bits.view(torch.float32))
-        if dist.get_backend(self.shard_group) == "nccl":
-            return dist.all_gather_into_tensor(self.shard_stats, self.local_stats, group=self.shard_group,
-                                               async_op=async_op)
-        # gloo (CPU tests, one-GPU rehearsals; its all_gather takes no CUDA tensors): a
-        # SUM all-reduce of the rank-placed rows, exact (every other row is zero)
-        self.shard_stats.zero_()
-        self.shard_stats[2 * self.shard_rank:2 * self.shard_rank + 2].copy_(self.local_stats)
-        return dist.all_reduce(self.shard_stats, op=dist.ReduceOp.SUM, group=self.shard_group, async_op=async_op)
+        work = (coll or TorchCollectives(self.shard_group)).all_gather_into(self.shard_stats, self.local_stats)
+        if async_op:
+            return work
+        work.wait()
+        return None
 
     # ----------------------------------------------------------- descriptors
     def tree_desc(self) -> "_lib.TreeDesc":

@@ -75,7 +75,7 @@ def make_learner(args, dtype, device, comm, rank, replay):
         "Replay_Memory": {"soft_capacity": args.replay},
         "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
                     "seed": 1234 + rank, "network": args.network, "dtype": dtype,
-                    "presample": not args.no_presample, "force_dp": args.force_dp,
+                    "presample": not args.no_presample, "force_dp": args.force_dp, "comm_backend": args.comm,
                     **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
     })
     if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
@@ -148,6 +148,9 @@ def main():
                     help="sample at the head of each step instead of inside the previous step's optimizer launch")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (rehearsing several ranks on one GPU)")
+    ap.add_argument("--comm", default="torch", choices=["torch", "native"],
+                    help="DP collectives: torch.distributed (RCCL process group) or the native RCCL "
+                         "communicator (csrc/comm/rccl_comm.cpp)")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel step (RCCL collectives captured in the graphs, sharded "
                          "replay) even on one rank: capture check and segmented-step overhead")
@@ -205,6 +208,7 @@ def main():
                        "replay_per_gpu": args.replay,
                        "learner": kind + ("/" + ops.name if ops is not None and args.learner == "fused" else
                                           "/torch-autograd"),
+                       "dp_collectives": args.comm if (world > 1 or args.force_dp) else None,
                        "hip_graphs": not args.no_graphs},
             "math": ("fp32 master weights, gradients and optimizer; GEMM operands as bf16 hi + lo "
                      "(hi*hi + lo*hi + hi*lo MFMAs, fp32 accumulation)" if args.dtype == "fp32"

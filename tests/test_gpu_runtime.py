@@ -287,3 +287,64 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     out = _bench_json(r.stdout)
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1024 and out["config"]["parallelism"] == "dp2"
+
+
+def _native_rccl_worker(q, port):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0")
+    import torch
+    from apex_dqn_amd.parallel.dist import Comm
+    from apex_dqn_amd.parallel.rccl import make_collectives
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comm = Comm.from_env(device=dev, force=True)
+    coll = make_collectives(comm, "native", dev)
+    nc = comm._native
+    out = {"version": nc.version}
+    x = torch.arange(1000, dtype=torch.float32, device=dev)
+    w = coll.all_reduce(x)
+    w.wait()
+    g_out = torch.zeros(4, dtype=torch.float64, device=dev)
+    coll.all_gather_into(g_out, torch.tensor([1.5, 2.5, 3.5, 4.5], dtype=torch.float64, device=dev)).wait()
+    b = torch.full((7,), 3.0, device=dev, dtype=torch.bfloat16)
+    nc.broadcast_(b, 0)
+    # captured: all-reduce on the comm stream inside a HIP graph, replayed twice
+    y = torch.ones(4096, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        coll.all_reduce(y).wait()
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y.mul_(2.0)
+        coll.all_reduce(y).wait()
+        y.add_(1.0)
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    nc.check()
+    out.update(x_ok=bool(torch.equal(x, torch.arange(1000, dtype=torch.float32, device=dev))),
+               gather=g_out.cpu().tolist(), bcast=float(b.float().min()), bmax=float(b.float().max()), y=float(y[0]))
+    comm.shutdown()
+    q.put(out)
+
+
+@pytest.mark.gpu
+def test_native_rccl_communicator_world1():
+    """csrc/comm/rccl_comm.cpp over the process's librccl: init from a unique id,
+    all-reduce / all-gather / broadcast on explicit streams, capture in a HIP graph,
+    async-error check (world 1: one rank per GPU, the box has one)."""
+    import random
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_rccl_worker, args=(q, 29600 + random.randint(0, 300)))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert out["version"] > 0 and out["x_ok"]
+    assert out["gather"] == [1.5, 2.5, 3.5, 4.5] and out["bcast"] == out["bmax"] == 3.0
+    assert out["y"] == 7.0          # (1*2+1)*2+1: two replays of mul / all-reduce / add
