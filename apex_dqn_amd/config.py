@@ -108,6 +108,8 @@ class RuntimeConf:
                                     # "native" (parallel/rccl.py: own RCCL communicator + comm stream)
     force_dp: bool = False          # run the data-parallel step (collectives + sharded replay) even at
                                     # world 1 (needs an initialised process group; checks / overhead)
+    replica_check_every: int = 5000  # DP: learner steps between replica checksum checks (0 = off)
+    step_timeout: float = 300.0     # GPU loop watchdog: seconds a queued learner chunk may take
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
                                     # (runtime/actor_thread.py), concurrent with the learner
 

@@ -501,6 +501,30 @@ class FusedNatureLearner:
         self._graphs_warm = False
         # capture recorded the step without executing it; state is as before
 
+    def check_replicas(self) -> bool:
+        """Data-parallel replicas must stay bit-identical (same all-reduced gradient,
+        deterministic optimizer).  Compare a checksum of the fp32 master weights
+        across ranks; on a mismatch (silent data corruption, a rank that skipped an
+        update) re-broadcast rank 0's weights and optimizer state.  A collective:
+        every rank calls it at the same step.  Returns True if the replicas agreed."""
+        if not self._dp or self.world <= 1:
+            return True
+        import torch.distributed as dist
+        w = torch.arange(1, 65, device=self.device, dtype=torch.float64)
+        p = self.p32.double()
+        n = p.numel() // 64 * 64
+        sig = torch.stack([p.sum(), (p[:n].view(-1, 64) * w).sum(), self.rms_v.double().sum()])
+        lo, hi = sig.clone(), sig.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        if torch.equal(lo, hi):
+            return True
+        for t in (self.p32, self.rms_v, self.rms_m, self.t32):
+            dist.broadcast(t, src=0)
+        self._refresh_bf16()
+        split_into(self.t32, self.tbf, self.tbf_lo)
+        return False
+
     def refresh_replay_stats(self) -> None:
         """Re-gather the shard statistics (after host-side inserts / eviction; a
         collective: every rank calls it at the same point)."""

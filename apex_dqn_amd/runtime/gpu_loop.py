@@ -131,6 +131,8 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                 k = min(learner_steps - n, _to_boundary(n, L.remove_old_xp_freq),
                         _to_boundary(n, rt.log_every) if rt.log_every else learner_steps,
                         _to_boundary(n, rt.ckpt_freq) if (ckpt_path and rt.ckpt_freq) else learner_steps,
+                        _to_boundary(n, rt.replica_check_every) if (world > 1 and rt.replica_check_every)
+                        else learner_steps,
                         max(1, 2 * int(getattr(rt, "graph_steps", 1) or 1)))
                 if rt.torch_profile_dir and prof is None and n < rt.torch_profile_start:
                     k = min(k, rt.torch_profile_start - n)
@@ -153,13 +155,16 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                 ev.record()
                 inflight.append(ev)
                 while len(inflight) > 2:
-                    inflight.popleft().synchronize()
+                    _wait_event(inflight.popleft(), rt.step_timeout, comm)
             n = learner.num_q_updates
             if prof is not None and n >= rt.torch_profile_start + rt.torch_profile_steps:
                 prof.stop()
                 os.makedirs(rt.torch_profile_dir, exist_ok=True)
                 prof.export_chrome_trace(os.path.join(rt.torch_profile_dir, f"trace_rank{rank}.json"))
                 prof, rt.torch_profile_dir = None, None
+            if world > 1 and rt.replica_check_every and n % rt.replica_check_every == 0 and \
+                    hasattr(learner, "check_replicas") and not learner.check_replicas() and metrics is not None:
+                metrics.log("replica_divergence", step=n, action="re-broadcast from rank 0")
             if n % L.remove_old_xp_freq == 0:
                 replay.remove_to_fit()
                 replay.rebuild()
@@ -208,6 +213,19 @@ def _restore_actor_rng(group, path: str) -> None:
     a = ck.get("actor_rng")
     if isinstance(a, dict) and getattr(group, "ctr", None) is not None:
         group.ctr.fill_(int(a["ctr"]))
+
+
+def _wait_event(ev, timeout: float, comm=None) -> None:
+    """Wait for a queued learner chunk, at most ``timeout`` seconds (watchdog: a hung
+    kernel or collective fails the rank -- the native communicator is aborted first --
+    so torchrun's elastic restart resumes the group from the last checkpoint)."""
+    deadline = time.time() + float(timeout)
+    while not ev.query():
+        if time.time() > deadline:
+            if comm is not None and hasattr(comm, "abort"):
+                comm.abort()
+            raise RuntimeError(f"learner step watchdog: queued GPU work did not finish in {timeout:.0f} s")
+        time.sleep(2e-4)
 
 
 def _to_boundary(n: int, every: int) -> int:

@@ -144,3 +144,39 @@ def test_elastic_restart_resumes_from_checkpoint():
         r1 = torch.load(os.path.join(out, "rank1.pt"), weights_only=True)
         assert r0["n"] == r1["n"] == 12
         assert torch.equal(r0["p"], r1["p"])   # replicas identical after the restart
+
+
+def _replica_worker(rank, world, path, q):
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.parallel.dist import Comm
+    torch.set_num_threads(2)
+    comm = Comm.init(rank, world, f"file://{path}", backend="gloo")
+    L = FusedNatureLearner(_cfg(), "cpu", _replay(rank), comm=comm)
+    L.step()
+    ok_before = L.check_replicas()
+    if rank == 1:                       # a corrupted replica
+        L.p32[123] += 1e-3
+        L.rms_v[7] += 1.0
+    ok_corrupt = L.check_replicas()
+    pl = [torch.zeros_like(L.p32) for _ in range(world)]
+    torch.distributed.all_gather(pl, L.p32.clone())
+    same = all(torch.equal(pl[0], p) for p in pl[1:])
+    q.put((rank, ok_before, ok_corrupt, same, L.check_replicas()))
+    comm.shutdown()
+
+
+@pytest.mark.slow
+def test_replica_check_detects_and_repairs_divergence():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as td:
+        procs = [ctx.Process(target=_replica_worker, args=(r, 2, os.path.join(td, "s"), q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=240) for _ in range(2)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    for _, ok_before, ok_corrupt, same, ok_after in res:
+        assert ok_before and not ok_corrupt and same and ok_after
+

@@ -261,3 +261,27 @@ def test_actor_runner_restarts_crashed_thread_and_detects_stall():
     with pytest.raises(RuntimeError, match="stalled"):
         r2.check()
     r2.stop()
+
+
+def test_loop_watchdog_aborts_on_hung_gpu_work():
+    from apex_dqn_amd.runtime.gpu_loop import _wait_event
+
+    class Hung:
+        def query(self):
+            return False
+
+    class Done:
+        def query(self):
+            return True
+
+    class FakeComm:
+        aborted = False
+
+        def abort(self):
+            FakeComm.aborted = True
+
+    _wait_event(Done(), 0.1, FakeComm())
+    assert not FakeComm.aborted
+    with pytest.raises(RuntimeError, match="watchdog"):
+        _wait_event(Hung(), 0.05, FakeComm())
+    assert FakeComm.aborted
