@@ -205,7 +205,10 @@ __global__ void __launch_bounds__(C2S_THREADS, 1) conv2_img_fwd_split_kernel(Con
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nh = wv & 1, kp = wv >> 1;
   const int rr = lane & 31, kg = lane >> 5;
-  const int step = gridDim.x, img0 = blockIdx.x, img1 = d.N;
+  // a contiguous image range per workgroup: most workgroups see one weight set, so
+  // they load the 256 KB of hi / lo fragments once (strided ranges switched twice)
+  const int per = (d.N + (int)gridDim.x - 1) / (int)gridDim.x, step = 1;
+  const int img0 = blockIdx.x * per, img1 = min(d.N, img0 + per);
   if (img0 >= img1) return;
   const int nimg = (img1 - img0 + step - 1) / step;          // images of this workgroup
   const int ndma = wv < C2S_BLOCKS - 4 * (C2S_NB - 1) ? C2S_NB : C2S_NB - 1;   // this wave's DMAs per plane
