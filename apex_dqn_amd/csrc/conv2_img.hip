@@ -393,11 +393,18 @@ struct Conv2DgradImgDesc {
 };
 
 #define C2D_SLOTS 121   // 11 x 11 padded dY slots, 128 B each
+// The M rows of the dgrad GEMMs are output pixels on an 11-wide grid (the slot grid's
+// width; columns past the image are padding rows, never stored), so the 16 lanes of a
+// ds_read_b128 lane group read 16 slots whose indices are distinct mod 16: with the
+// chunk swizzle c ^ ((slot >> 1) & 7) that is 16 distinct bank groups (a 10- or 9-wide
+// grid wraps inside a lane group: 37-43 % bank-conflict cycles measured).  Padding rows
+// read up to slot 143: the LDS image is 144 slots, zeroed once.
+#define C2D_PSLOTS 144
 
 __device__ __forceinline__ int c2d_off(int slot, int c) { return (slot << 7) + ((c ^ ((slot >> 1) & 7)) << 4); }
 
 __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDesc d) {
-  __shared__ __attribute__((aligned(16))) uint8_t sdy[C2D_SLOTS * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sdy[C2D_PSLOTS * 128];
   __shared__ __attribute__((aligned(16))) uint8_t sout[400 * 128];      // one output image, pixel rows
   const bf16_t* __restrict__ dyp = d.dy;
   const bf16_t* __restrict__ wp = d.w;
@@ -406,7 +413,7 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int cls = wv >> 1, nh = wv & 1, p = cls >> 1, q = cls & 1;
   const int rr = lane & 31, kg = lane >> 5;
-  for (int i = tid; i < C2D_SLOTS * 8; i += 512) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < C2D_PSLOTS * 8; i += 512) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
   // weight fragments: row = input channel ci = nh*32 + rr, K step s = (a, b, co group)
   // (direct 2-byte gathers from L2, once per workgroup: staging them through LDS in
   // coalesced rounds measured slower, 22.7 vs 18.8 us for 512 images)
@@ -427,9 +434,9 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
   int pi[4], pj[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const int r = min(t * 32 + rr, 99);
-    pi[t] = r / 10;
-    pj[t] = r - pi[t] * 10;
+    const int r = t * 32 + rr;
+    pi[t] = r / 11;
+    pj[t] = r - pi[t] * 11;
   }
   for (int img = blockIdx.x; img < d.N; img += gridDim.x) {
     __syncthreads();   // previous image: LDS reads and output copy-out done
@@ -459,7 +466,7 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
     // unmasked bf16 runs -> LDS output image (pixel-major, chunk-swizzled like sdy)
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      if (t * 32 + rr >= 100) continue;
+      if (pi[t] >= 10 || pj[t] >= 10) continue;
       const int ih = 2 * pi[t] + p, iw = 2 * pj[t] + q, px = ih * 20 + iw;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -502,11 +509,11 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
 // hi and lo weight fragments (2 x 2 x 16 x 8 registers) and the 8 accumulators fit the
 // 512 registers of a lone wave.  The fp32 result leaves as masked hi / lo planes.
 __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2DgradImgDesc d) {
-  __shared__ __attribute__((aligned(16))) uint8_t sdy[2 * C2D_SLOTS * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sdy[2 * C2D_PSLOTS * 128];
   __shared__ __attribute__((aligned(16))) uint8_t sout[2 * 400 * 128];   // hi image, lo image
   const int tid = threadIdx.x, lane = tid & 63, cls = tid >> 6, p = cls >> 1, q = cls & 1;
   const int rr = lane & 31, kg = lane >> 5;
-  for (int i = tid; i < 2 * C2D_SLOTS * 8; i += 256) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 2 * C2D_PSLOTS * 8; i += 256) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
   bf16x8 wh[2][16], wl[2][16];
 #pragma unroll
   for (int nh = 0; nh < 2; ++nh)
@@ -527,6 +534,8 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
   int pi[4], pj[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
+    // 10-wide pixel grid here: the 11-wide one (C2D_PSLOTS) removes the dY-read bank
+    // conflicts but measured no gain for this four-wave kernel (47.7 vs 47.4 us)
     const int r = min(t * 32 + rr, 99);
     pi[t] = r / 10;
     pj[t] = r - pi[t] * 10;
@@ -539,7 +548,7 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
       for (int k = tid; k < 2 * 81 * 8; k += 256) {
         const int pl = k >= 81 * 8 ? 1 : 0, kk = k - pl * 81 * 8;
         const int px = kk >> 3, c = kk & 7, oh = px / 9, ow = px - oh * 9;
-        *reinterpret_cast<uint4*>(sdy + pl * C2D_SLOTS * 128 + c2d_off((oh + 1) * 11 + ow + 1, c)) =
+        *reinterpret_cast<uint4*>(sdy + pl * C2D_PSLOTS * 128 + c2d_off((oh + 1) * 11 + ow + 1, c)) =
             pl ? srl[kk] : src[kk];
       }
     }
@@ -560,7 +569,7 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
       const int off_ = c2d_off((pi[t_] - ((s_ >> 3) & 1) + 1) * 11 + (pj[t_] - ((s_ >> 2) & 1) + 1), \
                                ((s_ & 3) << 1) | kg);                                        \
       dst_[0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + off_));    \
-      dst_[1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + C2D_SLOTS * 128 + off_)); \
+      dst_[1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + C2D_PSLOTS * 128 + off_)); \
     }
     C2DS_LDX(0, xf[0])
 #pragma unroll
@@ -645,7 +654,9 @@ APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t 
 // duelling_network.py:12-13): per image an 81 x 64 x 576 GEMM.  Six waves = 3 pixel
 // tiles (32 of the 81 pixels) x 2 channel halves; each owns its 32 x 32 output tile
 // over the full K (no reduction), with its 36 weight fragments (32 input channels x
-// 16 K) in 144 VGPRs, transposed once per workgroup through LDS.  dY3 (7 x 7 x 64)
+// 16 K) in 144 VGPRs, transposed once per workgroup through LDS.  (An 11-wide pixel
+// grid makes its dY reads conflict-free -- 37 -> 4 % conflict cycles -- but needs a
+// fourth, mostly padding, row tile: 8 waves, 11.3 vs 9.5 us.)  dY3 (7 x 7 x 64)
 // sits in LDS inside a 2-pixel zero ring (the same 11 x 11 slot geometry as the conv2
 // kernel) and the next image's dY3 and this image's mask load under the MFMA chain;
 // results go through LDS and leave as coalesced 16-B rows with the y2 mask applied.
