@@ -120,7 +120,7 @@ class SyntheticAtariVec:
         self.ep_ret = np.zeros(self.E, np.float64)
 
     def _frames(self) -> np.ndarray:
-        f = self.bank[self.s].copy()
+        f = self.bank[self.s]       # the gather already returns a fresh array (no extra copy)
         col = (self.t * 3) % self.obs_shape[1]
         f[np.arange(self.E), :, col] = 255
         return f

@@ -177,6 +177,7 @@ class GpuReplayShard:
         # evicts (runtime/actor_thread.py); the kernels each section enqueues land on the
         # stream in the order the sections run
         self.lock = threading.RLock()
+        self._pin_ev = None                 # pinned frame staging (append_frames)
         self._tdesc = None
         self._rdesc = None
         # sharding (enable_sharding): all-gathered (total, min p) of every shard, fp64
@@ -260,11 +261,15 @@ class GpuReplayShard:
 
     def _append_frames_locked(self, frames) -> np.ndarray:
         """Store new frames (n, H, W) uint8; returns their sequence numbers."""
+        if isinstance(frames, np.ndarray) and self.device.type == "cuda":
+            frames = self._pinned(frames)      # async H2D from a pinned staging buffer
         frames = torch.as_tensor(frames)
         n = frames.shape[0]
         seqs = self.frame_head + np.arange(n, dtype=np.int64)
         skip = max(0, n - self.F)  # only the newest F frames survive a wrap
         src = frames[skip:].to(self.device, non_blocking=True).contiguous()
+        if self._pin_ev is not None and frames.is_pinned():
+            self._pin_ev[self._pin_k].record()
         start = (self.frame_head + skip) % self.F
         if self.use_hip and self.frame_shape == (84, 84):
             # s2d permutation + ring scatter (with wrap) in one kernel
@@ -280,6 +285,24 @@ class GpuReplayShard:
                 pos = 0
         self.frame_head += n
         return seqs
+
+    def _pinned(self, frames: np.ndarray) -> torch.Tensor:
+        """Copy host frames into one of two pinned staging buffers (the copy of the
+        buffer's previous use must have finished: its event is waited on first)."""
+        shape = tuple(frames.shape)
+        if getattr(self, "_pin_shape", None) != shape:
+            self._pin_buf = [torch.empty(shape, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            self._pin_ev = [torch.cuda.Event(), torch.cuda.Event()]
+            self._pin_used = [False, False]
+            self._pin_shape, self._pin_k = shape, 1
+        self._pin_k ^= 1
+        k = self._pin_k
+        if self._pin_used[k]:
+            self._pin_ev[k].synchronize()
+        self._pin_used[k] = True
+        buf = self._pin_buf[k]
+        np.copyto(buf.numpy(), frames)
+        return buf
 
     def _insert_locked(self, batch: Dict[str, np.ndarray]) -> np.ndarray:
         """Insert n-step transitions whose S_t/S_tpn payloads are frame seqs (K, C)."""
