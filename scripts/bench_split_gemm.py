@@ -47,16 +47,16 @@ def main():
     e2h = torch.empty(B, 9, 9, 64, device=dev, dtype=torch.bfloat16)
     e2l = torch.empty_like(e2h)
     C.CONV3_DGRAD_IMG = False
-    for hint in (0, 1, 2):
-        C._HINTS["tile"] = hint
-        r = {"hint": hint}
+    for hint, order in ((0, 0), (1, 0), (2, 0), (2, 1), (2, 2), (1, 1), (1, 2)):
+        C._HINTS["tile"], C._HINTS["order"] = hint, order
+        r = {"hint": hint, "order": order}
         r["fc_fwd"] = timed(lambda: C.dense_fwd(lib, xh, wh, b, oh, True, None, w2h, b2, 1024, x_lo=xl, w_lo=wl,
                                                  w2_lo=w2l, out_lo=ol))
         r["conv3_fwd"] = timed(lambda: C.conv_fwd(lib, x3h, w3h, b, 1, o3h, w32h, b2, 1024, x_lo=x3l, w_lo=w3l,
                                                   w2_lo=w32l, out_lo=o3l))
         r["conv3_dgrad"] = timed(lambda: C.conv3_dgrad(lib, d3h, w3h, y2, e2h, dy_lo=d3l, w_lo=w3l, out_lo=e2l))
         print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
-    C._HINTS["tile"] = 0
+    C._HINTS["tile"] = C._HINTS["order"] = 0
 
 
 if __name__ == "__main__":

@@ -124,10 +124,12 @@ def test_dp_learner_two_ranks_on_one_gpu(tmp_path):
     assert res[0][4] == res[1][4]                        # same shard statistics on both ranks
 
 
-@pytest.mark.parametrize("hip,kind", [(True, "impala"), (False, "graph")])
-def test_impala_loop_with_hip_graph(hip, kind):
+@pytest.mark.parametrize("hip,dtype,kind", [(True, "bf16", "impala"), (False, "bf16", "graph"),
+                                            (True, "fp32", "graph")])
+def test_impala_loop_with_hip_graph(hip, dtype, kind):
     """IMPALA-deep on the GPU loop (actors + HBM replay + graph-captured step): the
-    hand-written csrc/impala.hip learner, and the torch-autograd graph learner."""
+    hand-written csrc/impala.hip learner (bf16 operands), and the torch-autograd graph
+    learner (also what Runtime.dtype=fp32 selects: the IMPALA kernels have no split path)."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.runtime.gpu_loop import train_frames
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
@@ -137,7 +139,7 @@ def test_impala_loop_with_hip_graph(hip, kind):
                                             "remove_old_xp_freq": 10, "q_target_sync_freq": 20},
                                 "Replay_Memory": {"soft_capacity": 2000},
                                 "Runtime": {"replay_capacity": 2500, "log_every": 0, "use_graphs": True,
-                                            "network": "impala", "use_hip_kernels": hip}})
+                                            "network": "impala", "use_hip_kernels": hip, "dtype": dtype}})
     out = train_frames(cfg, DEV, 30)
     L = out["learner"]
     assert L.kind == kind and L.num_q_updates == 30 and L._graphs is not None
