@@ -46,7 +46,7 @@ struct ConvDesc {
   int bt;
   int ldb;
   int koff[16];
-  int tile_hint;              // 0 auto, 1 BM=128, 2 BM=64
+  int tile_hint;              // 0 auto, 1 BM=128, 2 BM=64 (register-staged), 3 LDS-DMA
   int order_hint;             // 0 auto, 1 M tiles fastest per XCD, 2 N tiles fastest
   // fp32-accurate ("split") mode, all four set: the lo planes of A, B (both weight
   // sets) and the output; every operand is hi + lo (csrc/mfma_common.h split_pk_bf16)
@@ -70,10 +70,6 @@ struct FwdRegs {
 };
 
 
-// Epilogue image: 32 rows x 128 B per wave; 16-B chunk c of row r at c ^ ((r>>1)&7)
-__device__ __forceinline__ int epi_off(int r, int byte) {
-  return (r << 7) + ((((byte >> 4) ^ ((r >> 1) & 7))) << 4) + (byte & 15);
-}
 
 // MODE: A-operand source (0 dense rows, 1 NHWC implicit im2col).
 // PAD: im2col taps may fall outside the input (padding / dgrad): per-row tap
@@ -357,6 +353,260 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   }
 }
 
+// =====================================================================================
+// forward / dgrad implicit GEMM, LDS-DMA staged (the default for 128-row tiles)
+// =====================================================================================
+// The same GEMM, LDS images, fragments and epilogue as igemm_fwd_kernel at BM = 128
+// (4 waves x 32 rows x 64 channels), but the operand tiles travel global -> LDS by
+// global_load_lds_dwordx4 into an NS-deep ring of stages.  The register-staged
+// kernel moves every operand byte through VGPRs and a ds_write_b128 (13 LDS-path
+// cycles per wave-instruction, under 80 B/clk/CU): at 64-row tiles that costs more
+// LDS cycles than the fragment reads, and it needs the 64-row tiles to fill the
+// chip with a 2-deep pipeline.  Here no VALU or ds_write touches the staging: each
+// lane's DMA source is chosen so its fixed LDS slot (M0 + 16 lane) receives the
+// chunk that the swizzled image (swz_row / swz_tr) wants there, and the tile a wave
+// computes on was issued NS - 1 tiles earlier (one barrier per K tile).
+//   slot p of 128-B row r holds chunk p ^ ((r >> 1) & 7)   (swz_row: A, and B rows)
+//   slot p of K-major row k holds chunk p ^ (s(k) << 1)     (swz_tr: K-major B)
+// Padding taps (dgrad) read a zero row instead of predicating the load.
+__device__ __attribute__((aligned(16))) uint8_t apex_zero_row[128];
+
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC, bool SPLIT, int NS>
+__global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
+  constexpr int BM = 128, MT = 2, WR = 32;
+  constexpr int HALF = BM * 128 + FWD_BN * 128;   // one precision plane of a stage
+  constexpr int STAGE = SPLIT ? 2 * HALF : HALF;
+  constexpr int NA = BM / 32;                     // A DMA instructions per wave per plane
+  constexpr int NB = FWD_BN / 32;                 // B DMA instructions per wave per plane
+  constexpr int DPT = (NA + NB) * (SPLIT ? 2 : 1);   // DMAs per wave per K tile
+  static_assert(NS >= 2 && NS * STAGE <= 163840, "LDS ring");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wg = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+                             gridDim.x * gridDim.y * gridDim.z);
+  int bx, by, bz;
+  if (d.order_hint == 2) {
+    by = wg % gridDim.y;
+    const int r = wg / gridDim.y;
+    bx = r % gridDim.x;
+    bz = r / gridDim.x;
+  } else {
+    bx = wg % gridDim.x;
+    const int r = wg / gridDim.x;
+    by = r % gridDim.y;
+    bz = r / gridDim.y;
+  }
+  const int cls = bz;
+  const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
+  const uint32_t OWv = OWC ? OWC : d.OW;
+  const int M = d.N * OHW;
+  const int m0 = bx * BM;
+  const int n0 = by * FWD_BN;
+  const bool second = d.w2 != nullptr && m0 >= d.m_switch;
+  const uint8_t* wb = reinterpret_cast<const uint8_t*>((second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride);
+  const uint8_t* wl = SPLIT ? reinterpret_cast<const uint8_t*>((second ? d.w2_lo : d.w_lo) + (int64_t)cls * d.w_cls_stride)
+                            : wb;
+  const uint8_t* xa = reinterpret_cast<const uint8_t*>(d.x);
+  const uint8_t* xl = SPLIT ? reinterpret_cast<const uint8_t*>(d.x_lo) : xa;
+  const float* __restrict__ bias = second ? d.bias2 : d.bias;
+  const int KT = d.K >> 6;
+  const int cpb = d.Cin >> 6;
+
+  // per-lane DMA sources: A instruction i of this wave fills rows 8 (wv + 4 i) .. +7
+  // (lane >> 3 picks the row, lane & 7 the LDS slot), B likewise with 64 rows
+  uint32_t a_off[NA], vmask[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int r = 8 * (wv + 4 * i) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int m = m0 + r;
+    const int mm = m < M ? m : 0;
+    if (MODE == 0) {
+      a_off[i] = ((uint32_t)mm * d.K + c * 8) * 2u;
+      vmask[i] = 0;
+    } else {
+      const int img = udiv<OHWC>(mm, OHW), rem = mm - img * OHW;
+      const int oh = udiv<OWC>(rem, OWv), ow = rem - oh * OWv;
+      const int ih0 = oh * d.stride - d.pad_h, iw0 = ow * d.stride - d.pad_w;
+      a_off[i] = (uint32_t)(((img * d.H + ih0) * d.W + iw0) * d.Cin + c * 8) * 2u;
+      uint32_t vm = 0;
+      if (PAD) {
+        const int kh0 = max(0, -ih0), kh1 = min(d.KH, d.H - ih0);
+        const int kw0 = max(0, -iw0), kw1 = min(d.KW, d.W - iw0);
+        const uint32_t colbits = kw1 > kw0 ? ((1u << kw1) - 1u) & ~((1u << kw0) - 1u) : 0u;
+        for (int kh = kh0; kh < kh1; ++kh) vm |= colbits << (kh * d.KW);
+      }
+      vmask[i] = vm;
+    }
+  }
+  uint32_t b_off[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int r = 8 * (wv + 4 * i) + (lane >> 3);
+    if (BT) {
+      const int s = ((r >> 1) & 1) | (((r >> 3) & 1) << 1);
+      const int c = (lane & 7) ^ (s << 1);
+      b_off[i] = (uint32_t)((r * d.ldb + n0 + c * 8) * 2);
+    } else {
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      b_off[i] = (uint32_t)(((n0 + r) * d.K + c * 8) * 2);
+    }
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  // tiles are issued strictly in order: the im2col tap is a scalar cursor
+  int lt = 0, c_cb = 0, c_kw = 0, c_kh = 0;
+  auto issue = [&]() {
+    const int kt = lt;
+    const uint32_t dst = lds0 + (uint32_t)(kt % NS) * STAGE;
+    const uint32_t bso = BT ? (uint32_t)(d.bt == 2 ? kt * 128 * d.ldb : 2 * d.koff[cls * KT + kt]) : (uint32_t)kt * 128u;
+    uint32_t toff;
+    int tap = 0;
+    if (MODE == 0) {
+      toff = (uint32_t)kt * 128u;
+    } else {
+      tap = c_kh * d.KW + c_kw;
+      toff = (uint32_t)(((c_kh * d.W + c_kw) * d.Cin + (c_cb << 6)) * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const uint32_t ldsa = __builtin_amdgcn_readfirstlane(dst + (wv + 4 * i) * 1024);
+      const bool ok = !PAD || ((vmask[i] >> tap) & 1u);
+      const uint32_t ao = a_off[i] + toff;   // 32-bit: a padded row's tap-(0,0) offset wraps
+      dma16(ok ? (const void*)(xa + ao) : (const void*)apex_zero_row, ldsa);
+      if (SPLIT) dma16(ok ? (const void*)(xl + ao) : (const void*)apex_zero_row, ldsa + HALF);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const uint32_t ldsb = __builtin_amdgcn_readfirstlane(dst + BM * 128 + (wv + 4 * i) * 1024);
+      const uint32_t bo = b_off[i] + bso;
+      dma16(wb + bo, ldsb);
+      if (SPLIT) dma16(wl + bo, ldsb + HALF);
+    }
+    ++lt;
+    if (MODE == 1 && ++c_cb == cpb) {
+      c_cb = 0;
+      if (++c_kw == d.KW) { c_kw = 0; ++c_kh; }
+    }
+  };
+
+  f32x4 acc[MT][4];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const uint8_t* As = smem + buf * STAGE;
+    const uint8_t* Bs = As + BM * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 4 * s + (lane >> 4);
+      bf16x8 a[MT], b[4], al[MT], bl[4];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        a[mt] = *reinterpret_cast<const bf16x8*>(As + swz_row(WR * wv + 16 * mt + (lane & 15), c));
+        if (SPLIT) al[mt] = *reinterpret_cast<const bf16x8*>(As + HALF + swz_row(WR * wv + 16 * mt + (lane & 15), c));
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        b[nt] = BT ? tr_frag8(Bs, s, 16 * nt, lane)
+                   : *reinterpret_cast<const bf16x8*>(Bs + swz_row(16 * nt + (lane & 15), c));
+        if (SPLIT)
+          bl[nt] = BT ? tr_frag8(Bs + HALF, s, 16 * nt, lane)
+                      : *reinterpret_cast<const bf16x8*>(Bs + HALF + swz_row(16 * nt + (lane & 15), c));
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          if (SPLIT) {
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[nt], a[mt], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], al[mt], acc[mt][nt], 0, 0, 0);
+          }
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+        }
+    }
+  };
+
+  // ring: tiles 0 .. NS-2 in flight before the loop; iteration kt waits for its own
+  // DMAs of tile kt (later tiles may stay in flight: completions are in order), the
+  // barrier publishes everyone's, and frees stage (kt - 1) % NS for tile kt + NS - 1
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < KT) issue();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int ahead = min(NS - 2, KT - 1 - kt);
+    vmcnt_le(ahead * DPT);
+    __syncthreads();
+    if (kt + NS - 1 < KT) issue();
+    compute(kt % NS);
+  }
+  __syncthreads();
+
+  // ---- epilogue (as igemm_fwd_kernel)
+  uint8_t* Es = smem + wv * (WR * 128);
+  uint8_t* El = smem + BM * 128 + wv * (WR * 128);
+  const int g = lane >> 4, pl = lane & 15;
+  const bool relu32 = SPLIT && d.relu && d.mask == nullptr;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int ch = 16 * nt + 4 * g;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+      const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + ch);
+      b4[0] = bb.x; b4[1] = bb.y; b4[2] = bb.z; b4[3] = bb.w;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = 16 * mt + pl;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[mt][nt][r] * d.in_scale + b4[r];
+        if (relu32) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (SPLIT) {
+        uint32_t h01, l01, h23, l23;
+        split_pk_bf16(v[0], v[1], h01, l01);
+        split_pk_bf16(v[2], v[3], h23, l23);
+        *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(El + epi_off(row, ch * 2)) = make_uint2(l01, l23);
+      } else {
+        *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) =
+            make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
+      }
+    }
+  }
+  __syncthreads();
+  const int ooh = (d.ncls == 4) ? (cls >> 1) : 0;
+  const int oow = (d.ncls == 4) ? (cls & 1) : 0;
+#pragma unroll
+  for (int p = 0; p < WR / 8; ++p) {
+    const int row = 8 * p + (lane >> 3), ch = lane & 7;
+    const int m = m0 + WR * wv + row;
+    if (m >= M) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
+    uint4 vl = make_uint4(0, 0, 0, 0);
+    if (SPLIT) vl = *reinterpret_cast<const uint4*>(El + epi_off(row, ch * 16));
+    const int img = udiv<OHWC>(m, OHW), rem = m - img * OHW;
+    const int oh = udiv<OWC>(rem, OWv), ow = rem - oh * OWv;
+    const int64_t orow = ((int64_t)img * d.OHfull + oh * d.ostride_h + ooh) * d.OWfull + ow * d.ostride_w + oow;
+    const int64_t off = orow * d.ldy + n0 + ch * 8;
+    if (d.mask) {
+      const uint4 mk = *reinterpret_cast<const uint4*>(d.mask + off);
+      v = make_uint4(mask_bf16x2(v.x, mk.x), mask_bf16x2(v.y, mk.y), mask_bf16x2(v.z, mk.z),
+                     mask_bf16x2(v.w, mk.w));
+      if (SPLIT)
+        vl = make_uint4(mask_bf16x2(vl.x, mk.x), mask_bf16x2(vl.y, mk.y), mask_bf16x2(vl.z, mk.z),
+                        mask_bf16x2(vl.w, mk.w));
+    } else if (d.relu && !SPLIT) {
+      v = make_uint4(relu_bf16x2(v.x), relu_bf16x2(v.y), relu_bf16x2(v.z), relu_bf16x2(v.w));
+    }
+    *reinterpret_cast<uint4*>(d.y + off) = v;
+    if (SPLIT) *reinterpret_cast<uint4*>(d.y_lo + off) = vl;
+  }
+}
+
 // weight gradient: csrc/igemm_wgrad.h (igemm_wgrad_body)
 template <int MODE, int OWC, int OHWC, int CT, int NT, int SP>
 __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
@@ -474,6 +724,23 @@ static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
   else igemm_fwd_kernel<1, false, false, 0, 0, BM, SPLIT><<<grid, 256, 0, st>>>(d);
 }
 
+template <bool SPLIT, int NS>
+static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
+  const bool pad = d.pad_h > 0 || d.pad_w > 0;
+  const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
+  if (d.mode == 0 && d.bt) igemm_dma_kernel<0, false, true, 1, 1, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0) igemm_dma_kernel<0, false, false, 1, 1, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  else if (pad && d.bt) {
+    if (g9) igemm_dma_kernel<1, true, true, 9, 81, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+    else if (g10) igemm_dma_kernel<1, true, true, 10, 100, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+    else igemm_dma_kernel<1, true, true, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  } else if (pad) igemm_dma_kernel<1, true, false, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  else if (d.bt) igemm_dma_kernel<1, false, true, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  else if (g9) igemm_dma_kernel<1, false, false, 9, 81, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  else if (g7) igemm_dma_kernel<1, false, false, 7, 49, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  else igemm_dma_kernel<1, false, false, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+}
+
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if ((d.K & 63) || (d.Cout & 63) || d.K <= 0) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.Cin & 63)) return (int)hipErrorInvalidValue;
@@ -503,7 +770,15 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
   const dim3 g64((M + 63) / 64, d.Cout / FWD_BN, ncls), g128((M + 127) / 128, d.Cout / FWD_BN, ncls);
-  if (split) {
+  // LDS-DMA kernel (scripts/bench_dma_gemm.py, fc at batch 512): fc forward 24.8 vs
+  // 27.9 us (bf16) and 46.5 vs 54.0 (split), fc dgrad split 21.1 vs 22.7; the conv3
+  // GEMMs and the bf16 fc dgrad stay on the register-staged 64/128-row tiles, where
+  // two or more blocks per CU beat the deeper ring.  tile_hint 3 forces it.
+  const bool dma = d.tile_hint == 3 || (d.tile_hint == 0 && d.mode == 0 && (!d.bt || split));
+  if (dma) {
+    if (split) launch_dma<true, 3>(d, g128, st);
+    else launch_dma<false, 3>(d, g128, st);
+  } else if (split) {
     if (bm64) launch_fwd<64, true>(d, g64, st);
     else launch_fwd<128, true>(d, g128, st);
   } else {

@@ -34,6 +34,10 @@ __device__ __forceinline__ uint32_t relu_pk16(uint32_t v) {
 // 128-byte LDS rows, 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7):
 // a 16-lane ds_read_b128 group (16 rows, one chunk) hits 16 distinct 16-B slots.
 __device__ __forceinline__ int swz_row(int r, int c) { return (r << 7) + ((c ^ ((r >> 1) & 7)) << 4); }
+// GEMM epilogue image: 128-B rows, 16-B chunk of byte `byte` in row r at chunk ^ ((r>>1)&7)
+__device__ __forceinline__ int epi_off(int r, int byte) {
+  return (r << 7) + ((((byte >> 4) ^ ((r >> 1) & 7))) << 4) + (byte & 15);
+}
 // transposed-read image: chunk16 c of row r at c ^ (s(r) << 1), s(r) = bit1(r) | bit3(r)<<1;
 // both ds_read_b64_tr_b16 halves (rows 8g+q, 8(g+1)+q) then cover 64 distinct banks.
 __device__ __forceinline__ int swz_tr(int r, int c) {
