@@ -51,6 +51,10 @@ struct WgradDesc {
 // SP: fp32-accurate operands.  0: bf16; 1: dY and X both hi + lo (three MFMAs per
 // fragment pair: hi.hi + lo.hi + hi.lo); 2: dY hi + lo, X exact in bf16 (uint8
 // frames: two MFMAs).  The lo images sit after the hi images of each stage.
+// Two-tile blocks (CT * NT == 2, split mode's conv2 shape: the hi + lo images of a
+// 4-tile block do not fit two stages) pair the waves instead of idling two: waves w
+// and w + 2 own the same tile and take the two 32-row halves of every 64-row step,
+// and the pair's accumulators are summed through LDS at the end (fixed order).
 template <int MODE, int OWC, int OHWC, int CT, int NT, int SP = 0>
 __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, int gx, int gy, int gz) {
   static_assert(CT * NT <= 4, "at most 4 output tiles per block");
@@ -218,8 +222,11 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
     }
   };
 
-  const bool active = wv < CT * NT;
-  const int wc = active ? wv / NT : 0, wn = active ? wv - (wv / NT) * NT : 0;   // this wave's (co, kc) tile
+  constexpr bool PAIR = CT * NT == 2;
+  const int tw = PAIR ? (wv & 1) : wv;
+  const bool active = PAIR || wv < CT * NT;
+  const int wc = active ? tw / NT : 0, wn = active ? tw - (tw / NT) * NT : 0;   // this wave's (co, kc) tile
+  const int kk0 = PAIR ? (wv >> 1) : 0, kk1 = PAIR ? kk0 + 1 : 2;              // 32-row halves of a step
   const bool do_bias = active && d.bias_slab != nullptr && kcb + wn == 0;
   // acc[i][j] = D[kc][co] (swapped operands): lane holds kc 16j + 4g + {0..3} of co 16i + (lane&15)
   f32x4 acc[4][4], accb[4];
@@ -238,7 +245,7 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
     const uint8_t* DL = img(stg, CT + NT + wc);
     const uint8_t* XL = img(stg, 2 * CT + NT + wn);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = kk0; kk < kk1; ++kk) {
       bf16x8 a[4], b[4], al[4], bl[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -294,6 +301,26 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
 
   // ---------------- this wave's fp32 partial tile -> slab[split][co][kc] (float4 along kc)
   const int lin_blk = lin;
+  if (PAIR) {
+    // waves 2, 3 hand their half-step sums to waves 0, 1 (acc then accb, lane-major)
+    __syncthreads();                       // every wave is done reading the stages
+    f32x4* red = reinterpret_cast<f32x4*>(smem) + (wv & 1) * (20 * 64) + lane;
+    if (wv >= 2) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) red[q * 64] = acc[q >> 2][q & 3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(16 + i) * 64] = accb[i];
+    }
+    __syncthreads();
+    if (wv >= 2) {
+      if (d.norm_part != nullptr && lane == 0) d.norm_part[d.norm_slot0 + 4 * lin_blk + wv] = 0.0;
+      return;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q >> 2][q & 3] += red[q * 64];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) accb[i] += red[(16 + i) * 64];
+  }
   if (!active) {
     if (d.norm_part != nullptr && lane == 0) d.norm_part[d.norm_slot0 + 4 * lin_blk + wv] = 0.0;
     return;
