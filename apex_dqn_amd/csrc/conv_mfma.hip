@@ -608,9 +608,16 @@ __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
 }
 
 // weight gradient: csrc/igemm_wgrad.h (igemm_wgrad_body)
+// three-stage LDS-DMA ring where it fits next to the row table (else two)
+template <int MODE, int CT, int NT, int SP>
+constexpr int wgrad_stages() {
+  constexpr int nimg = CT + NT + (SP == 0 ? 0 : (SP == 1 ? CT + NT : CT));
+  return SP != 0 && 3 * nimg * WG_IMG + (MODE == 0 ? 0 : WG_TBL * 4) <= 163840 ? 3 : 2;
+}
+
 template <int MODE, int OWC, int OHWC, int CT, int NT, int SP>
 __global__ void __launch_bounds__(256) igemm_wgrad_kernel(WgradDesc d) {
-  igemm_wgrad_body<MODE, OWC, OHWC, CT, NT, SP>(d, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
+  igemm_wgrad_body<MODE, OWC, OHWC, CT, NT, SP, wgrad_stages<MODE, CT, NT, SP>()>(d, blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                                                 gridDim.x, gridDim.y, gridDim.z);
 }
 

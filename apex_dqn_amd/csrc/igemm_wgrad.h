@@ -55,7 +55,12 @@ struct WgradDesc {
 // 4-tile block do not fit two stages) pair the waves instead of idling two: waves w
 // and w + 2 own the same tile and take the two 32-row halves of every 64-row step,
 // and the pair's accumulators are summed through LDS at the end (fixed order).
-template <int MODE, int OWC, int OHWC, int CT, int NT, int SP = 0>
+// NSW: LDS stages.  Split-mode MODE 0 / 1 operands go global -> LDS by buffer LDS-DMA
+// (lane sources chosen so the fixed slots receive the swz_tr image; rows past the split
+// end read zeros through the buffer range check) into an NSW-deep ring (conv2 / conv3 /
+// fc weight gradients 36 / 19 / 29 -> 34 / 15 / 26 us); MODE 2's uint8 frames are
+// converted on the way, so it stays register-staged (two stages), as does bf16.
+template <int MODE, int OWC, int OHWC, int CT, int NT, int SP = 0, int NSW = 2>
 __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, int gx, int gy, int gz) {
   static_assert(CT * NT <= 4, "at most 4 output tiles per block");
   static_assert(SP != 1 || MODE != 2, "mode 2 X is exact: SP = 2");
@@ -65,8 +70,12 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
   constexpr int NTHR = 256;
   // dense rows (MODE 0) need no row table: 80 KB for a 4-tile block, two blocks per CU
   constexpr int TBL = MODE == 0 ? 0 : WG_TBL;
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * STAGE + TBL * 4];
-  uint32_t* tbl = reinterpret_cast<uint32_t*>(smem + 2 * STAGE);
+  // bf16 (SP 0) stays register-staged too: measured tie / 1-5 % slower with the ring
+  constexpr bool DMA = MODE != 2 && SP != 0;
+  constexpr int NS = DMA ? NSW : 2;
+  static_assert(NS * STAGE + TBL * 4 <= 163840, "LDS");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NS * STAGE + TBL * 4];
+  uint32_t* tbl = reinterpret_cast<uint32_t*>(smem + NS * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // XCD-contiguous order: the Kc / Co blocks of one split (same dY rows, overlapping
   // input pixels) and neighbouring splits run on one XCD's L2
@@ -109,8 +118,11 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
   }
   __syncthreads();
 
-  // ---------------- staging geometry (each image: 64 rows; thread rows srow, srow + 32; chunk sc)
-  const int sc = tid & 7, srow = tid >> 3;
+  // ---------------- staging geometry (each image: 64 rows; thread rows srow, srow + 32;
+  // chunk sc -- with DMA, the chunk that lands in the thread's fixed slot tid & 7 of
+  // the swz_tr image: (tid & 7) ^ (s(srow) << 1), the same for srow + 32)
+  const int srow = tid >> 3;
+  const int sc = DMA ? ((tid & 7) ^ ((((srow >> 1) & 1) | (((srow >> 3) & 1) << 1)) << 1)) : (tid & 7);
   const __amdgpu_buffer_rsrc_t dy_rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(d.dy), (short)0, r_end * d.ldd * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t x_rs = MODE == 0
@@ -275,11 +287,61 @@ __device__ __forceinline__ void igemm_wgrad_body(const WgradDesc& d, int lin, in
     }
   };
 
-  // two register stages + two LDS stages, straight-line (loads past the end re-read
-  // the last step -- never computed)
+  // DMA: step st's images into stage st % NS, NS - 1 steps ahead; one barrier per step
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  auto issue_step = [&](int st) {
+    const uint32_t base = lds0 + (uint32_t)(st % NS) * STAGE + (uint32_t)wv * 1024u;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const uint32_t o = dy_off + st * dy_step + c * 128;
+      const uint32_t l = __builtin_amdgcn_readfirstlane(base + c * WG_IMG);
+      bdma16(dy_rs, o, l);
+      bdma16(dy_rs, o + dy_r32, l + 4096);
+      if (SP) {
+        const uint32_t ll = __builtin_amdgcn_readfirstlane(base + (CT + NT + c) * WG_IMG);
+        bdma16(dyl_rs, o, ll);
+        bdma16(dyl_rs, o + dy_r32, ll + 4096);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      uint32_t o0, o1;
+      if (MODE == 0) {
+        o0 = x_off + st * x_step + t * 128;
+        o1 = o0 + x_r32;
+      } else {
+        const uint32_t* tb = tbl + st * WG_ROWS + srow;
+        o0 = tb[0] + x_tap[t];
+        o1 = tb[32] + x_tap[t];
+      }
+      const uint32_t l = __builtin_amdgcn_readfirstlane(base + (CT + t) * WG_IMG);
+      bdma16(x_rs, o0, l);
+      bdma16(x_rs, o1, l + 4096);
+      if (SP == 1) {
+        const uint32_t ll = __builtin_amdgcn_readfirstlane(base + (2 * CT + NT + t) * WG_IMG);
+        bdma16(xl_rs, o0, ll);
+        bdma16(xl_rs, o1, ll + 4096);
+      }
+    }
+  };
+  constexpr int DPW = 2 * (CT + NT + NLO);   // DMAs per wave per step
+  if (DMA && nst > 0) {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < nst) issue_step(p);
+    for (int st = 0; st < nst; ++st) {
+      vmcnt_le(min(NS - 2, nst - 1 - st) * DPW);
+      __syncthreads();
+      if (st + NS - 1 < nst) issue_step(st + NS - 1);
+      compute(st % NS);
+    }
+  }
+
+  // MODE 2: two register stages + two LDS stages, straight-line (loads past the end
+  // re-read the last step -- never computed)
   Regs RA, RB;
   const int SL = nst - 1;
-  if (nst > 0) {
+  if (!DMA && nst > 0) {
     load_step(0, RA);
     load_step(min(1, SL), RB);
     write_step(0, RA);

@@ -148,6 +148,16 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_off) {
                : "memory");
 }
 
+// 16-byte LDS-DMA through a buffer resource (buffer_load_dwordx4 ... lds): like dma16,
+// but offsets past the resource's range read zeros (rows past a GEMM's end).
+__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t lds_off) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(lds_off)
+               : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a run-time n (immediate operand: one branch per value;
 // n is wave-uniform, larger values clamp to 63 = no wait)
 __device__ __forceinline__ void vmcnt_le(int n) {
