@@ -46,7 +46,7 @@ struct ConvDesc {
   int bt;
   int ldb;
   int koff[16];
-  int tile_hint;              // 0 auto, 1 BM=128, 2 BM=64 (register-staged), 3 LDS-DMA
+  int tile_hint;              // 0 auto, 1 / 2 register-staged BM=128 / 64, 3-5 LDS-DMA (apex_conv_fwd)
   int order_hint;             // 0 auto, 1 M tiles fastest per XCD, 2 N tiles fastest
   // fp32-accurate ("split") mode, all four set: the lo planes of A, B (both weight
   // sets) and the output; every operand is hi + lo (csrc/mfma_common.h split_pk_bf16)
@@ -371,9 +371,9 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 // Padding taps (dgrad) read a zero row instead of predicating the load.
 __device__ __attribute__((aligned(16))) uint8_t apex_zero_row[128];
 
-template <int MODE, bool PAD, bool BT, int OWC, int OHWC, bool SPLIT, int NS>
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC, bool SPLIT, int NS, int BM = 128>
 __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
-  constexpr int BM = 128, MT = 2, WR = 32;
+  constexpr int MT = BM / 64, WR = BM / 4;
   constexpr int HALF = BM * 128 + FWD_BN * 128;   // one precision plane of a stage
   constexpr int STAGE = SPLIT ? 2 * HALF : HALF;
   constexpr int NA = BM / 32;                     // A DMA instructions per wave per plane
@@ -731,21 +731,21 @@ static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
   else igemm_fwd_kernel<1, false, false, 0, 0, BM, SPLIT><<<grid, 256, 0, st>>>(d);
 }
 
-template <bool SPLIT, int NS>
+template <bool SPLIT, int NS, int BM>
 static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
   const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
-  if (d.mode == 0 && d.bt) igemm_dma_kernel<0, false, true, 1, 1, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-  else if (d.mode == 0) igemm_dma_kernel<0, false, false, 1, 1, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+  if (d.mode == 0 && d.bt) igemm_dma_kernel<0, false, true, 1, 1, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0) igemm_dma_kernel<0, false, false, 1, 1, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
   else if (pad && d.bt) {
-    if (g9) igemm_dma_kernel<1, true, true, 9, 81, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-    else if (g10) igemm_dma_kernel<1, true, true, 10, 100, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-    else igemm_dma_kernel<1, true, true, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-  } else if (pad) igemm_dma_kernel<1, true, false, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-  else if (d.bt) igemm_dma_kernel<1, false, true, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-  else if (g9) igemm_dma_kernel<1, false, false, 9, 81, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-  else if (g7) igemm_dma_kernel<1, false, false, 7, 49, SPLIT, NS><<<grid, 256, 0, st>>>(d);
-  else igemm_dma_kernel<1, false, false, 0, 0, SPLIT, NS><<<grid, 256, 0, st>>>(d);
+    if (g9) igemm_dma_kernel<1, true, true, 9, 81, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+    else if (g10) igemm_dma_kernel<1, true, true, 10, 100, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+    else igemm_dma_kernel<1, true, true, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  } else if (pad) igemm_dma_kernel<1, true, false, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (d.bt) igemm_dma_kernel<1, false, true, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (g9) igemm_dma_kernel<1, false, false, 9, 81, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (g7) igemm_dma_kernel<1, false, false, 7, 49, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else igemm_dma_kernel<1, false, false, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
 }
 
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
@@ -777,14 +777,26 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
   const dim3 g64((M + 63) / 64, d.Cout / FWD_BN, ncls), g128((M + 127) / 128, d.Cout / FWD_BN, ncls);
-  // LDS-DMA kernel (scripts/bench_dma_gemm.py, fc at batch 512): fc forward 24.8 vs
-  // 27.9 us (bf16) and 46.5 vs 54.0 (split), fc dgrad split 21.1 vs 22.7; the conv3
-  // GEMMs and the bf16 fc dgrad stay on the register-staged 64/128-row tiles, where
-  // two or more blocks per CU beat the deeper ring.  tile_hint 3 forces it.
-  const bool dma = d.tile_hint == 3 || (d.tile_hint == 0 && d.mode == 0 && (!d.bt || split));
-  if (dma) {
-    if (split) launch_dma<true, 3>(d, g128, st);
-    else launch_dma<false, 3>(d, g128, st);
+  // LDS-DMA kernel (scripts/bench_dma_gemm.py, learner shapes at batch 512, us):
+  //   split: 64-row tiles, 2 stages (two blocks per CU) win everywhere -- fc fwd 39.6
+  //     (register-staged 51.5), fc dgrad 17.9 (22.7), conv3 fwd 27.9 (32.0), conv3
+  //     dgrad 20.4 (22.3), generic conv2 dgrad 46.1 (52.8; the image-resident kernel
+  //     ties at 45.9 and stays);
+  //   bf16: fc fwd 64-row, 3 stages 22.4 (26.6), fc dgrad 64-row, 2 stages 10.3 (11.5);
+  //     the conv GEMMs tie or lose and stay register-staged.
+  // tile_hint 3 / 4 / 5 force 128-row 3-stage / 64-row 2-stage / 64-row 3-stage.
+  const int dma = d.tile_hint >= 3 ? d.tile_hint
+                : d.tile_hint != 0 ? 0
+                : split ? 4 : (d.mode == 0 ? (d.bt ? 4 : 5) : 0);
+  if (dma == 3) {
+    if (split) launch_dma<true, 3, 128>(d, g128, st);
+    else launch_dma<false, 3, 128>(d, g128, st);
+  } else if (dma == 4) {
+    if (split) launch_dma<true, 2, 64>(d, g64, st);
+    else launch_dma<false, 2, 64>(d, g64, st);
+  } else if (dma == 5) {
+    if (split) launch_dma<true, 3, 64>(d, g64, st);
+    else launch_dma<false, 3, 64>(d, g64, st);
   } else if (split) {
     if (bm64) launch_fwd<64, true>(d, g64, st);
     else launch_fwd<128, true>(d, g128, st);

@@ -71,7 +71,7 @@ def main():
         for name, (o, fn) in cases.items():
             r = {"op": name, "split": split}
             ref = None
-            for hint in (2, 1, 3):
+            for hint in (2, 1, 4, 5):
                 C._HINTS["tile"], C._HINTS["order"] = hint, 0
                 for t in o:
                     t.zero_()
@@ -83,6 +83,11 @@ def main():
                 else:
                     r[f"maxdiff_h{hint}"] = max(float((a.float() - c.float()).abs().max()) for a, c in zip(got, ref))
                 r[f"us_h{hint}"] = round(timed(lambda: fn(o, split)), 2)
+            if name in ("conv3_dgrad", "conv2_dgrad") and not (name == "conv3_dgrad" and split):
+                C.CONV3_DGRAD_IMG = C.CONV2_DGRAD_IMG = True      # image-resident kernels
+                C._HINTS["tile"] = 0
+                r["us_img"] = round(timed(lambda: fn(o, split)), 2)
+                C.CONV3_DGRAD_IMG = C.CONV2_DGRAD_IMG = False
             print(json.dumps(r), flush=True)
             res[f"{name}_{'split' if split else 'bf16'}"] = r
     C._HINTS["tile"] = C._HINTS["order"] = 0
