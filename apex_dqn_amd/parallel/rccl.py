@@ -191,9 +191,19 @@ class TorchCollectives:
     def __init__(self, group=None):
         self.group = group
 
+    def _sync(self, t: torch.Tensor) -> bool:
+        """gloo on device tensors (one-GPU rehearsals): run the collective synchronously.
+        Several async gloo collectives on device tensors in flight at once deadlocked
+        4 ranks sharing one GPU (scripts/rehearse_dp.sh 4); gloo has nothing to overlap."""
+        import torch.distributed as dist
+        return t.is_cuda and dist.get_backend(self.group) != "nccl"
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         import torch.distributed as dist
         rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+        if self._sync(t):
+            dist.all_reduce(t, op=rop, group=self.group)
+            return _Done()
         return _TorchWork(dist.all_reduce(t, op=rop, group=self.group, async_op=True))
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
@@ -206,7 +216,7 @@ class TorchCollectives:
         r = dist.get_rank(self.group)
         out.zero_()
         out.view(W, n)[r].copy_(inp.reshape(-1))
-        return _TorchWork(dist.all_reduce(out, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        return self.all_reduce(out, "sum")
 
 
 class NativeCollectives:

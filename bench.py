@@ -130,6 +130,11 @@ def measure(cfg, learner, replay, comm, warmup: int, steps: int) -> dict:
 
 
 def main():
+    # diagnostics: APEX_TRACEBACK_AFTER=<s> dumps every thread's stack to stderr after s
+    # seconds (a hung multi-rank run names its blocking call instead of going silent)
+    if os.environ.get("APEX_TRACEBACK_AFTER"):
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["APEX_TRACEBACK_AFTER"]), repeat=True)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
