@@ -111,6 +111,7 @@ class RuntimeConf:
     replica_check_every: int = 5000  # DP: learner steps between replica checksum checks (0 = off)
     step_timeout: float = 300.0     # GPU loop watchdog: seconds a queued learner chunk may take
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
+    learner_stream_priority: bool = True   # async GPU actors: learner on a high-priority HIP stream
                                     # (runtime/actor_thread.py), concurrent with the learner
 
 

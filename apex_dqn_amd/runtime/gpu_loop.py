@@ -53,6 +53,32 @@ def train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                  metrics: Optional[MetricsLogger] = None, num_envs: Optional[int] = None,
                  actor_steps_per_update: int = 1, max_actor_steps: Optional[int] = None,
                  backend: Optional[str] = None, async_actors: Optional[bool] = None) -> Dict[str, Any]:
+    """See :func:`_train_frames`.  With asynchronous actors on a GPU the learner (and
+    the compute stream the actors' inserts ride on) runs on a HIGH-priority HIP stream:
+    the actor thread's inference kernels (its own, default-priority stream) fill the gaps
+    between learner kernels instead of delaying them (Runtime.learner_stream_priority)."""
+    device = torch.device(device)
+    if async_actors is None:
+        async_actors = bool(cfg.Runtime.async_actors) and device.type == "cuda"
+    if not (async_actors and device.type == "cuda" and cfg.Runtime.learner_stream_priority):
+        return _train_frames(cfg, device, learner_steps, comm, metrics, num_envs, actor_steps_per_update,
+                             max_actor_steps, backend, async_actors)
+    prev = torch.cuda.current_stream(device)
+    hi = torch.cuda.Stream(device, priority=torch.cuda.Stream.priority_range()[1])
+    hi.wait_stream(prev)
+    torch.cuda.set_stream(hi)
+    try:
+        return _train_frames(cfg, device, learner_steps, comm, metrics, num_envs, actor_steps_per_update,
+                             max_actor_steps, backend, async_actors)
+    finally:
+        prev.wait_stream(hi)
+        torch.cuda.set_stream(prev)
+
+
+def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
+                  metrics: Optional[MetricsLogger] = None, num_envs: Optional[int] = None,
+                  actor_steps_per_update: int = 1, max_actor_steps: Optional[int] = None,
+                  backend: Optional[str] = None, async_actors: Optional[bool] = None) -> Dict[str, Any]:
     """Train for ``learner_steps`` updates.  Actors stop after ``max_actor_steps``
     group steps (default ``Actor.T``: every env takes T steps, ``actor.py:159``); the
     learner keeps going on the replay, as the reference's learner process does.
