@@ -159,6 +159,7 @@ class FusedNatureLearner:
         # DP step as ONE captured graph including the RCCL collectives (backend nccl);
         # gloo (CPU tests, one-GPU rehearsals) cannot be captured: eager DP steps
         self._dp_graphs = self._dp and cuda and self._backend_name() == "nccl"
+        self._ordered_coll = self._dp and cuda and (self.coll.name == "native" or self._backend_name() == "nccl")
         # next-batch pre-sampling: the batch of step t+1 is drawn at the end of step t,
         # after the priority write-back -- on the HIP backend inside the optimizer launch
         # (its first blocks run the sampler: csrc/sumtree.hip rmsprop_sample_kernel), so
@@ -386,9 +387,14 @@ class FusedNatureLearner:
         w_r = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
         self._seg2()     # conv backward overlaps the fc/head bucket all-reduce
         w_cv = self.coll.all_reduce(self.gcomm[:cut])
-        w_fc.wait()
-        w_r.wait()
-        w_cv.wait()
+        if self._ordered_coll:
+            # RCCL runs a communicator's collectives in issue order on one stream: the
+            # last one's completion covers the others (one join edge in the graph)
+            w_cv.wait()
+        else:
+            w_fc.wait()
+            w_r.wait()
+            w_cv.wait()
         self._mark("allreduce_wait")
         self._seg3()
 

@@ -176,13 +176,19 @@ class _TorchWork:
 
 class _StreamWork:
     """Completion of a collective enqueued on the comm stream: ``wait`` makes the
-    current stream wait for it (a graph edge under capture)."""
+    current stream wait for it (a graph edge under capture).  The collectives of one
+    ``NativeCollectives`` run in order on one stream, so a join covers every op
+    enqueued before it: later waits with nothing new enqueued add no edge (each
+    cross-queue edge of a captured graph costs several microseconds)."""
 
-    def __init__(self, comm_stream, device):
-        self.comm_stream, self.device = comm_stream, device
+    def __init__(self, coll: "NativeCollectives"):
+        self.coll = coll
 
     def wait(self) -> None:
-        torch.cuda.current_stream(self.device).wait_stream(self.comm_stream)
+        c = self.coll
+        if c._unjoined:
+            torch.cuda.current_stream(c.comm.device).wait_stream(c.comm.stream)
+            c._unjoined = False
 
 
 class TorchCollectives:
@@ -225,21 +231,23 @@ class NativeCollectives:
 
     def __init__(self, comm: RcclComm):
         self.comm = comm
+        self._unjoined = False
 
     def _fork(self):
         cur = torch.cuda.current_stream(self.comm.device)
         self.comm.stream.wait_stream(cur)
+        self._unjoined = True
         return self.comm.stream
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         s = self._fork()
         self.comm.all_reduce_(t, op, stream=s)
-        return _StreamWork(s, self.comm.device)
+        return _StreamWork(self)
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
         s = self._fork()
         self.comm.all_gather_(out, inp, stream=s)
-        return _StreamWork(s, self.comm.device)
+        return _StreamWork(self)
 
 
 def make_collectives(comm, backend: str = "torch", device=None):
