@@ -623,6 +623,23 @@ APEX_EXPORT int apex_gather_frames(const uint8_t* ring, const int32_t* slots, in
   APEX_CHECK_LAUNCH();
 }
 
+// Cache-policy probe (scripts/bench_cold_mall.py): fill n 16-B words with plain or
+// non-temporal stores -- does a streaming write evict the Infinity Cache?
+__global__ void fill16_kernel(uint4* p, int64_t n, int nt) {
+  typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+  const uint4 v = make_uint4(1u, 1u, 1u, 1u);
+  const u32x4v vv = {1u, 1u, 1u, 1u};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (nt) __builtin_nontemporal_store(vv, reinterpret_cast<u32x4v*>(p + i));
+    else p[i] = v;
+  }
+}
+
+APEX_EXPORT int apex_fill16(void* p, int64_t n, int nt, hipStream_t st) {
+  fill16_kernel<<<2048, 256, 0, st>>>(reinterpret_cast<uint4*>(p), n, nt);
+  APEX_CHECK_LAUNCH();
+}
+
 APEX_EXPORT int apex_abi_version() { return 2; }
 
 // 1 if this library was built with -DAPEX_DEBUG_BOUNDS

@@ -98,6 +98,7 @@ class Conv1S2DDesc(ctypes.Structure):
 
 _SIGS = {
     "apex_abi_version": ([], c_i),
+    "apex_fill16": ([c_p, c_i64, c_i, c_p], c_i),
     "apex_tree_update": ([TreeDesc, c_p, c_p, c_i, c_i, c_f, c_f, c_p, c_p, c_i, c_p, c_p], c_i),
     "apex_tree_zero_range": ([TreeDesc, c_i64, c_i64, c_p], c_i),
     "apex_replay_insert": ([TreeDesc, RecordDesc, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p],
