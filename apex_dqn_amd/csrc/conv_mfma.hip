@@ -607,6 +607,218 @@ __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
   }
 }
 
+// =====================================================================================
+// dense GEMM on 128x128 tiles with split K (the fc forward)
+// =====================================================================================
+// igemm_dma_kernel's 64x64 tiles stream every activation row once per 64 output
+// columns and every weight row once per 64 batch rows: for the split fc forward
+// (1536 x 3136 -> 1024, hi + lo planes) that is ~616 MB of L2/MALL -> LDS traffic,
+// and the traffic bounds it (a DMA-only variant takes 32 of its ~40 us).  Here a
+// block owns a 128x128 output tile: four waves in 2x2, each 64x64 (4x4 MFMA tiles,
+// every A and B fragment feeds four MFMAs per product), so the traffic halves and
+// the LDS fragment reads per MFMA drop 2.5x.  The K range is split over gridDim.z so
+// the 96 tiles of the fc still cover the chip; partials go to an fp32 workspace
+// [z][M][N] and fc_splitk_epilogue_kernel sums them in fixed z order (deterministic),
+// adds the bias, applies ReLU (or the dgrad mask) and writes the output planes.
+// Staging is the LDS-DMA ring of igemm_dma_kernel (same swizzled images, same
+// lane-source trick); A rows past M read row 0 and are dropped at the store.
+// LW: four extra loader waves issue every DMA (the compute waves then carry only
+// MFMAs and fragment reads; an LDS-DMA issue costs ~60 cycles of the issuing wave).
+template <bool SPLIT, int NS, bool LW>
+__global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, float* __restrict__ ws, int kt_per) {
+  constexpr int BM = 128, BN = 128;
+  constexpr int HALF = (BM + BN) * 128;           // one precision plane of a stage
+  constexpr int STAGE = SPLIT ? 2 * HALF : HALF;
+  constexpr int NA = BM / 32, NB = BN / 32;       // DMA instructions per wave per plane
+  constexpr int DPT = (NA + NB) * (SPLIT ? 2 : 1);
+  static_assert(NS >= 2 && NS * STAGE <= 163840, "LDS ring");
+  __shared__ __attribute__((aligned(16))) uint8_t smem[NS * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = LW ? (tid >> 6) & 3 : tid >> 6;
+  const bool loader = !LW || tid >= 256, computer = !LW || tid < 256;
+  const int ntm = gridDim.x, ntn = gridDim.y;
+  // N tiles fastest, then M tiles, then K splits: the blocks of one XCD share A rows
+  // and a K range (consecutive logical ids land on one XCD)
+  const int wg = xcd_swizzle(blockIdx.x + ntm * (blockIdx.y + ntn * blockIdx.z), ntm * ntn * gridDim.z);
+  const int by = wg % ntn;
+  const int bx = (wg / ntn) % ntm;
+  const int bz = wg / (ntn * ntm);
+  const int M = d.N, Nc = d.Cout;
+  const int m0 = bx * BM, n0 = by * BN;
+  const int KT = d.K >> 6;
+  const int kt0 = bz * kt_per;
+  const int nk = min(KT, kt0 + kt_per) - kt0;     // >= 1 (host sizes the grid)
+  const bool second = d.w2 != nullptr && m0 >= d.m_switch;
+  const uint8_t* wb = reinterpret_cast<const uint8_t*>(second ? d.w2 : d.w);
+  const uint8_t* wl = SPLIT ? reinterpret_cast<const uint8_t*>(second ? d.w2_lo : d.w_lo) : wb;
+  const uint8_t* xa = reinterpret_cast<const uint8_t*>(d.x);
+  const uint8_t* xl = SPLIT ? reinterpret_cast<const uint8_t*>(d.x_lo) : xa;
+
+  // instruction i of wave wv fills tile rows 8 (wv + 4 i) .. +7: lane >> 3 picks the
+  // row, lane & 7 the LDS slot, and the source chunk is the one swz_row puts there
+  uint32_t a_off[NA], b_off[NB];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int r = 8 * (wv + 4 * i) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int m = m0 + r < M ? m0 + r : 0;
+    a_off[i] = ((uint32_t)m * d.K + c * 8) * 2u;
+  }
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int r = 8 * (wv + 4 * i) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    b_off[i] = ((uint32_t)(n0 + r) * d.K + c * 8) * 2u;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
+  int lt = 0;
+  auto issue = [&]() {
+    const uint32_t dst = lds0 + (uint32_t)(lt % NS) * STAGE;
+    const uint32_t toff = (uint32_t)(kt0 + lt) * 128u;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const uint32_t l = __builtin_amdgcn_readfirstlane(dst + (wv + 4 * i) * 1024);
+      dma16(xa + a_off[i] + toff, l);
+      if (SPLIT) dma16(xl + a_off[i] + toff, l + HALF);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const uint32_t l = __builtin_amdgcn_readfirstlane(dst + BM * 128 + (wv + 4 * i) * 1024);
+      dma16(wb + b_off[i] + toff, l);
+      if (SPLIT) dma16(wl + b_off[i] + toff, l + HALF);
+    }
+    ++lt;
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int wm = wv >> 1, wn = wv & 1;
+
+  auto compute = [&](int buf) {
+    const uint8_t* As = smem + buf * STAGE;
+    const uint8_t* Bs = As + BM * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 4 * s + (lane >> 4);
+      bf16x8 a[4], b[4], al[4], bl[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a[t] = *reinterpret_cast<const bf16x8*>(As + swz_row(64 * wm + 16 * t + (lane & 15), c));
+        b[t] = *reinterpret_cast<const bf16x8*>(Bs + swz_row(64 * wn + 16 * t + (lane & 15), c));
+        if (SPLIT) {
+          al[t] = *reinterpret_cast<const bf16x8*>(As + HALF + swz_row(64 * wm + 16 * t + (lane & 15), c));
+          bl[t] = *reinterpret_cast<const bf16x8*>(Bs + HALF + swz_row(64 * wn + 16 * t + (lane & 15), c));
+        }
+      }
+      // product-major order: 16 independent accumulators between dependent MFMAs
+      if (SPLIT) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[nt], a[mt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], al[mt], acc[mt][nt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+    }
+  };
+
+  if (loader) {
+#pragma unroll
+    for (int p = 0; p < NS - 1; ++p)
+      if (p < nk) issue();
+  }
+  for (int j = 0; j < nk; ++j) {
+    if (loader) vmcnt_le(min(NS - 2, nk - 1 - j) * DPT);
+    __syncthreads();
+    if (loader && j + NS - 1 < nk) issue();
+    if (computer) compute(j % NS);
+  }
+  if (!computer) return;
+
+  // partial tile -> ws[bz][m][n]: lane (g = lane >> 4, pl = lane & 15) of MFMA tile
+  // (mt, nt) holds row 16 mt + pl, columns 16 nt + 4 g .. +3
+  float* wz = ws + (int64_t)bz * M * Nc;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int m = m0 + 64 * wm + 16 * mt + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int n = n0 + 64 * wn + 16 * nt + 4 * (lane >> 4);
+      *reinterpret_cast<f32x4*>(wz + (int64_t)m * Nc + n) = acc[mt][nt];
+    }
+  }
+}
+
+// y[m][n] = act(sum_z ws[z][m][n] * in_scale + bias[n]): 8 outputs per thread, the
+// z partials summed in fixed order.  act = ReLU (fp32, before the hi / lo split) or
+// the dgrad mask (both planes, from the producer's bf16 activation).
+template <bool SPLIT>
+__global__ void __launch_bounds__(256) fc_splitk_epilogue_kernel(ConvDesc d, const float* __restrict__ ws,
+                                                                 int nz) {
+  const int Nc = d.Cout;
+  const int64_t MN = (int64_t)d.N * Nc;
+  const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (e >= MN) return;
+  const int m = (int)(e / Nc), n = (int)(e - (int64_t)m * Nc);
+  float v[8];
+  {
+    const float4 p0 = *reinterpret_cast<const float4*>(ws + e);
+    const float4 p1 = *reinterpret_cast<const float4*>(ws + e + 4);
+    v[0] = p0.x; v[1] = p0.y; v[2] = p0.z; v[3] = p0.w;
+    v[4] = p1.x; v[5] = p1.y; v[6] = p1.z; v[7] = p1.w;
+  }
+  for (int z = 1; z < nz; ++z) {
+    const float4 p0 = *reinterpret_cast<const float4*>(ws + z * MN + e);
+    const float4 p1 = *reinterpret_cast<const float4*>(ws + z * MN + e + 4);
+    v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+    v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+  }
+  const float* __restrict__ bias = (d.w2 != nullptr && m >= d.m_switch) ? d.bias2 : d.bias;
+  float b8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (bias) {
+    const float4 b0 = *reinterpret_cast<const float4*>(bias + n);
+    const float4 b1 = *reinterpret_cast<const float4*>(bias + n + 4);
+    b8[0] = b0.x; b8[1] = b0.y; b8[2] = b0.z; b8[3] = b0.w;
+    b8[4] = b1.x; b8[5] = b1.y; b8[6] = b1.z; b8[7] = b1.w;
+  }
+  const bool relu = d.relu && d.mask == nullptr;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    v[r] = v[r] * d.in_scale + b8[r];
+    if (relu) v[r] = fmaxf(v[r], 0.f);
+  }
+  const int64_t off = (int64_t)m * d.ldy + n;
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (SPLIT) split_pk_bf16(v[2 * q], v[2 * q + 1], h[q], l[q]);
+    else h[q] = cvt_pk_bf16(v[2 * q], v[2 * q + 1]);
+  }
+  if (d.mask) {
+    const uint4 mk = *reinterpret_cast<const uint4*>(d.mask + off);
+    const uint32_t mm[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      h[q] = mask_bf16x2(h[q], mm[q]);
+      if (SPLIT) l[q] = mask_bf16x2(l[q], mm[q]);
+    }
+  }
+  *reinterpret_cast<uint4*>(d.y + off) = make_uint4(h[0], h[1], h[2], h[3]);
+  if (SPLIT) *reinterpret_cast<uint4*>(d.y_lo + off) = make_uint4(l[0], l[1], l[2], l[3]);
+}
+
 // weight gradient: csrc/igemm_wgrad.h (igemm_wgrad_body)
 // three-stage LDS-DMA ring where it fits next to the row table (else two)
 template <int MODE, int CT, int NT, int SP>
@@ -746,6 +958,39 @@ static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
   else if (g9) igemm_dma_kernel<1, false, false, 9, 81, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
   else if (g7) igemm_dma_kernel<1, false, false, 7, 49, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
   else igemm_dma_kernel<1, false, false, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+}
+
+// Dense C[M,N] = act(A[M,K] . B[N,K]^T + b) on 128x128 tiles, K split `ksplit` ways
+// (fc_gemm128_kernel + fc_splitk_epilogue_kernel).  ws: fp32 workspace of at least
+// ksplit * M * N elements.  Row-major B only (d.bt == 0), N % 128 == 0.
+APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksplit, int loader_waves,
+                                hipStream_t st) {
+  if (d.mode != 0 || d.bt != 0 || (d.K & 63) || d.K <= 0 || (d.Cout & 127) || d.N <= 0 || ksplit < 1)
+    return (int)hipErrorInvalidValue;
+  if ((d.ldy & 7) || d.ldy < d.Cout) return (int)hipErrorInvalidValue;
+  if ((int64_t)d.N * d.K * 2 >= 0x7ffffff0LL || (int64_t)d.Cout * d.K * 2 >= 0x7ffffff0LL)
+    return (int)hipErrorInvalidValue;
+  if (d.w2 != nullptr && (d.m_switch % 128)) return (int)hipErrorInvalidValue;
+  const bool split = d.x_lo != nullptr;
+  if (split && (d.w_lo == nullptr || d.y_lo == nullptr || (d.w2 != nullptr && d.w2_lo == nullptr)))
+    return (int)hipErrorInvalidValue;
+  const int KT = d.K >> 6;
+  const int kt_per = (KT + ksplit - 1) / ksplit;
+  const int nz = (KT + kt_per - 1) / kt_per;
+  if (ws == nullptr || ws_elems < (int64_t)nz * d.N * d.Cout) return (int)hipErrorInvalidValue;
+  const dim3 grid((d.N + 127) / 128, d.Cout / 128, nz);
+  if (loader_waves) {
+    if (split) fc_gemm128_kernel<true, 2, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
+    else fc_gemm128_kernel<false, 4, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
+  } else {
+    if (split) fc_gemm128_kernel<true, 2, false><<<grid, 256, 0, st>>>(d, ws, kt_per);
+    else fc_gemm128_kernel<false, 4, false><<<grid, 256, 0, st>>>(d, ws, kt_per);
+  }
+  const int64_t nthr = (int64_t)d.N * d.Cout / 8;
+  const int eb = (int)((nthr + 255) / 256);
+  if (split) fc_splitk_epilogue_kernel<true><<<eb, 256, 0, st>>>(d, ws, nz);
+  else fc_splitk_epilogue_kernel<false><<<eb, 256, 0, st>>>(d, ws, nz);
+  APEX_CHECK_LAUNCH();
 }
 
 APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {

@@ -211,6 +211,28 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
     _launch_fwd(lib, d)
 
 
+def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
+                 out: torch.Tensor, relu: bool = True, w2=None, b2=None, rows_first: int = 0, ksplit: int = 2,
+                 loader_waves: bool = False, x_lo=None, w_lo=None, w2_lo=None, out_lo=None) -> None:
+    """``dense_fwd`` on 128x128 tiles with the K range split ``ksplit`` ways
+    (csrc/conv_mfma.hip ``fc_gemm128_kernel``): fp32 partials in a cached workspace,
+    summed in fixed order by the epilogue kernel (bias, ReLU, hi / lo planes)."""
+    M, K = x.shape
+    Nc = w.shape[0]
+    assert w.shape[1] == K and out.shape == (M, Nc) and Nc % 128 == 0 and K % 64 == 0
+    assert x.is_contiguous() and w.is_contiguous() and out.is_contiguous()
+    if w2 is not None and rows_first % 128:
+        raise ValueError("online/target split must fall on a 128-row tile boundary")
+    kt = K // 64
+    per = -(-kt // ksplit)
+    nz = -(-kt // per)
+    buf = ws.get(("fc128",), nz * M * Nc, x.device)
+    d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), N=M, Cin=K, Cout=Nc,
+                   mode=0, relu=relu, K=K, **_second(w2, b2, rows_first, 1), **_lo(x_lo, w_lo, w2_lo, out_lo))
+    _lib.check(lib.apex_fc_gemm128(d, buf.data_ptr(), buf.numel(), int(ksplit), int(loader_waves),
+                                      _lib.stream_ptr()), "fc_gemm128")
+
+
 # K-major B-operand offsets for the dgrad GEMMs reading the natural OHWI weights.
 # conv3: k-tile = output tap t of the 3x3 correlation -> weight tap 8 - t (flipped).
 _KOFF3 = tuple((8 - t) * 64 for t in range(9))

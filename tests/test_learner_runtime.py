@@ -223,7 +223,9 @@ def test_actor_T_bounds_env_steps():
     out = train_frames(cfg, "cpu", 10)
     assert out["actor_steps"] == 12 and out["learner"].num_q_updates == 10
     out = train_frames(cfg, "cpu", 10, async_actors=True)
-    assert out["actor_steps"] == 12 and out["learner"].num_q_updates == 10
+    # the actor thread never passes T; the learner may finish its 10 updates (and stop
+    # the thread) before the thread's last step on a loaded host
+    assert out["actor_steps"] <= 12 and out["learner"].num_q_updates == 10
 
 
 class _FlakyGroup:
