@@ -246,6 +246,8 @@ __global__ void __launch_bounds__(C2S_THREADS, 1) conv2_img_fwd_split_kernel(Con
   }
   bf16x8 bh[32], bl[32];      // [kernel row of the pair][16 K steps]
   int cur_set = -1;
+  const int c4 = (lane & 7) * 4;
+  float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);   // this lane's 4 output-channel biases
 
   dma_plane(0);
   dma_plane(1);
@@ -263,6 +265,14 @@ __global__ void __launch_bounds__(C2S_THREADS, 1) conv2_img_fwd_split_kernel(Con
         bh[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(W + o));
         bl[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(WL + o));
       }
+      // drain here (once per weight set), as an instruction the compiler's wait
+      // insertion sees: otherwise it assumes these loads (and the biases) may still be
+      // in flight on every image and, not counting the inline-asm DMAs, places
+      // vmcnt(61) ... vmcnt(0) waits through each image's first phase and epilogue --
+      // each of which also drains the plane DMAs issued up to two phases ahead
+      const float* bias = set ? d.bias2 : d.bias;
+      bv = make_float4(bias[nh * 32 + c4], bias[nh * 32 + c4 + 1], bias[nh * 32 + c4 + 2], bias[nh * 32 + c4 + 3]);
+      __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0), expcnt / lgkmcnt untouched
       cur_set = set;
     }
     f32x16 acc[3];
@@ -316,10 +326,6 @@ __global__ void __launch_bounds__(C2S_THREADS, 1) conv2_img_fwd_split_kernel(Con
     __syncthreads();
     // wave (nh, kp) finishes grid rows 48 kp .. 48 kp + 47 of channel half nh: the two
     // kernel-row pairs (waves nh and nh + 2) in fixed order, bias, ReLU, hi / lo split
-    const float* bias = set ? d.bias2 : d.bias;
-    const int c4 = (lane & 7) * 4;
-    const float4 bv = make_float4(bias[nh * 32 + c4], bias[nh * 32 + c4 + 1], bias[nh * 32 + c4 + 2],
-                                  bias[nh * 32 + c4 + 3]);
 #pragma unroll
     for (int it = 0; it < 6; ++it) {
       const int r = 48 * kp + 8 * it + (lane >> 3), oh = r / 10, ow = r - oh * 10;

@@ -285,6 +285,15 @@ class HipBackend(TorchBackend):
     def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None):
         if not self.native_conv:
             return super().fc_fwd(x, w, b, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
+        M, K = x.shape[0], x[0].numel()
+        if w.shape[0] % 128 == 0 and K % 64 == 0 and (w2 is None or rows_first % 128 == 0) and \
+                hasattr(self.lib, "apex_fc_gemm128"):
+            # 128x128 tiles, K split in two, loader waves: fc forward 40.6 -> 36.2 us
+            # (split) / 25.7 -> 22.5 (bf16) at the learner shape (scripts/bench_fc128.py)
+            C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, 2, True,
+                           x_lo=None if x_lo is None else x_lo.reshape(M, K), w_lo=w_lo, w2_lo=w2_lo,
+                           out_lo=out_lo)
+            return
         C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True, w2=w2, b2=b2,
                     rows_first=rows_first, ws=self.ws,
                     x_lo=None if x_lo is None else x_lo.reshape(x.shape[0], -1), w_lo=w_lo, w2_lo=w2_lo,
