@@ -371,10 +371,8 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 // Padding taps (dgrad) read a zero row instead of predicating the load.
 __device__ __attribute__((aligned(16))) uint8_t apex_zero_row[128];
 
-// LW: four extra loader waves (512 threads) issue the DMAs; the four compute waves
-// then run only fragment reads and MFMAs (an LDS-DMA issue costs its wave ~60 cycles).
-template <int MODE, bool PAD, bool BT, int OWC, int OHWC, bool SPLIT, int NS, int BM = 128, bool LW = false>
-__global__ void __launch_bounds__(LW ? 512 : 256) igemm_dma_kernel(ConvDesc d) {
+template <int MODE, bool PAD, bool BT, int OWC, int OHWC, bool SPLIT, int NS, int BM = 128>
+__global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
   constexpr int MT = BM / 64, WR = BM / 4;
   constexpr int HALF = BM * 128 + FWD_BN * 128;   // one precision plane of a stage
   constexpr int STAGE = SPLIT ? 2 * HALF : HALF;
@@ -383,8 +381,7 @@ __global__ void __launch_bounds__(LW ? 512 : 256) igemm_dma_kernel(ConvDesc d) {
   constexpr int DPT = (NA + NB) * (SPLIT ? 2 : 1);   // DMAs per wave per K tile
   static_assert(NS >= 2 && NS * STAGE <= 163840, "LDS ring");
   __shared__ __attribute__((aligned(16))) uint8_t smem[NS * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wv = LW ? (tid >> 6) & 3 : tid >> 6;
-  const bool loader = !LW || tid >= 256, computer = !LW || tid < 256;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wg = xcd_swizzle(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z),
                              gridDim.x * gridDim.y * gridDim.z);
   int bx, by, bz;
@@ -534,59 +531,55 @@ __global__ void __launch_bounds__(LW ? 512 : 256) igemm_dma_kernel(ConvDesc d) {
   // ring: tiles 0 .. NS-2 in flight before the loop; iteration kt waits for its own
   // DMAs of tile kt (later tiles may stay in flight: completions are in order), the
   // barrier publishes everyone's, and frees stage (kt - 1) % NS for tile kt + NS - 1
-  if (loader) {
 #pragma unroll
-    for (int p = 0; p < NS - 1; ++p)
-      if (p < KT) issue();
-  }
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < KT) issue();
   for (int kt = 0; kt < KT; ++kt) {
-    if (loader) vmcnt_le(min(NS - 2, KT - 1 - kt) * DPT);
+    const int ahead = min(NS - 2, KT - 1 - kt);
+    vmcnt_le(ahead * DPT);
     __syncthreads();
-    if (loader && kt + NS - 1 < KT) issue();
-    if (computer) compute(kt % NS);
+    if (kt + NS - 1 < KT) issue();
+    compute(kt % NS);
   }
   __syncthreads();
 
-  // ---- epilogue (as igemm_fwd_kernel); loader waves only take part in its barrier
+  // ---- epilogue (as igemm_fwd_kernel)
   uint8_t* Es = smem + wv * (WR * 128);
   uint8_t* El = smem + BM * 128 + wv * (WR * 128);
   const int g = lane >> 4, pl = lane & 15;
   const bool relu32 = SPLIT && d.relu && d.mask == nullptr;
-  if (computer) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int ch = 16 * nt + 4 * g;
-      float b4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (bias) {
-        const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + ch);
-        b4[0] = bb.x; b4[1] = bb.y; b4[2] = bb.z; b4[3] = bb.w;
+  for (int nt = 0; nt < 4; ++nt) {
+    const int ch = 16 * nt + 4 * g;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+      const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + ch);
+      b4[0] = bb.x; b4[1] = bb.y; b4[2] = bb.z; b4[3] = bb.w;
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = 16 * mt + pl;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[mt][nt][r] * d.in_scale + b4[r];
+        if (relu32) v[r] = fmaxf(v[r], 0.f);
       }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int row = 16 * mt + pl;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = acc[mt][nt][r] * d.in_scale + b4[r];
-          if (relu32) v[r] = fmaxf(v[r], 0.f);
-        }
-        if (SPLIT) {
-          uint32_t h01, l01, h23, l23;
-          split_pk_bf16(v[0], v[1], h01, l01);
-          split_pk_bf16(v[2], v[3], h23, l23);
-          *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) = make_uint2(h01, h23);
-          *reinterpret_cast<uint2*>(El + epi_off(row, ch * 2)) = make_uint2(l01, l23);
-        } else {
-          *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) =
-              make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
-        }
+      if (SPLIT) {
+        uint32_t h01, l01, h23, l23;
+        split_pk_bf16(v[0], v[1], h01, l01);
+        split_pk_bf16(v[2], v[3], h23, l23);
+        *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(El + epi_off(row, ch * 2)) = make_uint2(l01, l23);
+      } else {
+        *reinterpret_cast<uint2*>(Es + epi_off(row, ch * 2)) =
+            make_uint2(cvt_pk_bf16(v[0], v[1]), cvt_pk_bf16(v[2], v[3]));
       }
     }
   }
   __syncthreads();
   const int ooh = (d.ncls == 4) ? (cls >> 1) : 0;
   const int oow = (d.ncls == 4) ? (cls & 1) : 0;
-  if (!computer) return;
 #pragma unroll
   for (int p = 0; p < WR / 8; ++p) {
     const int row = 8 * p + (lane >> 3), ch = lane & 7;
@@ -950,22 +943,21 @@ static void launch_fwd(const ConvDesc& d, dim3 grid, hipStream_t st) {
   else igemm_fwd_kernel<1, false, false, 0, 0, BM, SPLIT><<<grid, 256, 0, st>>>(d);
 }
 
-template <bool SPLIT, int NS, int BM, bool LW = false>
+template <bool SPLIT, int NS, int BM>
 static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
   const bool pad = d.pad_h > 0 || d.pad_w > 0;
   const bool g9 = d.OH == 9 && d.OW == 9, g7 = d.OH == 7 && d.OW == 7, g10 = d.OH == 10 && d.OW == 10;
-  constexpr int NT = LW ? 512 : 256;
-  if (d.mode == 0 && d.bt) igemm_dma_kernel<0, false, true, 1, 1, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-  else if (d.mode == 0) igemm_dma_kernel<0, false, false, 1, 1, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
+  if (d.mode == 0 && d.bt) igemm_dma_kernel<0, false, true, 1, 1, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (d.mode == 0) igemm_dma_kernel<0, false, false, 1, 1, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
   else if (pad && d.bt) {
-    if (g9) igemm_dma_kernel<1, true, true, 9, 81, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-    else if (g10) igemm_dma_kernel<1, true, true, 10, 100, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-    else igemm_dma_kernel<1, true, true, 0, 0, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-  } else if (pad) igemm_dma_kernel<1, true, false, 0, 0, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-  else if (d.bt) igemm_dma_kernel<1, false, true, 0, 0, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-  else if (g9) igemm_dma_kernel<1, false, false, 9, 81, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-  else if (g7) igemm_dma_kernel<1, false, false, 7, 49, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
-  else igemm_dma_kernel<1, false, false, 0, 0, SPLIT, NS, BM, LW><<<grid, NT, 0, st>>>(d);
+    if (g9) igemm_dma_kernel<1, true, true, 9, 81, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+    else if (g10) igemm_dma_kernel<1, true, true, 10, 100, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+    else igemm_dma_kernel<1, true, true, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  } else if (pad) igemm_dma_kernel<1, true, false, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (d.bt) igemm_dma_kernel<1, false, true, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (g9) igemm_dma_kernel<1, false, false, 9, 81, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else if (g7) igemm_dma_kernel<1, false, false, 7, 49, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
+  else igemm_dma_kernel<1, false, false, 0, 0, SPLIT, NS, BM><<<grid, 256, 0, st>>>(d);
 }
 
 // Dense C[M,N] = act(A[M,K] . B[N,K]^T + b) on 128x128 tiles, K split `ksplit` ways
@@ -1037,8 +1029,10 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   //     ties at 45.9 and stays);
   //   bf16: fc fwd 64-row, 3 stages 22.4 (26.6), fc dgrad 64-row, 2 stages 10.3 (11.5);
   //     the conv GEMMs tie or lose and stay register-staged.
-  // tile_hint 3 / 4 / 5 force 128-row 3-stage / 64-row 2-stage / 64-row 3-stage;
-  // 6 / 7: 64-row 2- / 3-stage with loader waves.
+  // tile_hint 3 / 4 / 5 force 128-row 3-stage / 64-row 2-stage / 64-row 3-stage.
+  // (Loader waves -- 4 extra waves issuing the DMAs -- measured no gain on these
+  // 64-row tiles: split fc fwd 40.7 vs 40.1, conv3 fwd 29.3 vs 28.9 us,
+  // profiles/r2_dma_gemm_loader_waves.json; they pay on the 128x128 fc tiles.)
   const int dma = d.tile_hint >= 3 ? d.tile_hint
                 : d.tile_hint != 0 ? 0
                 : split ? 4 : (d.mode == 0 ? (d.bt ? 4 : 5) : 0);
@@ -1051,12 +1045,6 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   } else if (dma == 5) {
     if (split) launch_dma<true, 3, 64>(d, g64, st);
     else launch_dma<false, 3, 64>(d, g64, st);
-  } else if (dma == 6) {
-    if (split) launch_dma<true, 2, 64, true>(d, g64, st);
-    else launch_dma<false, 2, 64, true>(d, g64, st);
-  } else if (dma == 7) {
-    if (split) launch_dma<true, 3, 64, true>(d, g64, st);
-    else launch_dma<false, 3, 64, true>(d, g64, st);
   } else if (split) {
     if (bm64) launch_fwd<64, true>(d, g64, st);
     else launch_fwd<128, true>(d, g128, st);

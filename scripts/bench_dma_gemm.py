@@ -71,7 +71,7 @@ def main():
         for name, (o, fn) in cases.items():
             r = {"op": name, "split": split}
             ref = None
-            for hint in (4, 5, 6, 7):
+            for hint in (2, 1, 4, 5):
                 C._HINTS["tile"], C._HINTS["order"] = hint, 0
                 for t in o:
                     t.zero_()
