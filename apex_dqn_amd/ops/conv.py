@@ -28,6 +28,9 @@ class Workspace:
         return t
 
 
+# scratch for launchers called without a workspace (tests, microbenchmarks)
+_DEFAULT_WS = Workspace()
+
 # launch-shape overrides for tuning sweeps (scripts/bench_kernels.py); 0 = kernel's choice
 _HINTS: Dict[str, int] = {}
 
@@ -289,9 +292,10 @@ CONV2_DGRAD_IMG = _os.environ.get("APEX_CONV2_DGRAD_IMG", "1") != "0"
 
 
 def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor,
-                    grid: int = 0, dy_lo=None, w_lo=None, out_lo=None) -> None:
+                    grid: int = 0, dy_lo=None, w_lo=None, out_lo=None, ws: Optional["Workspace"] = None) -> None:
     """conv2 data gradient on the image-resident kernel (csrc/conv2_img.hip): one wave
-    per (stride-parity class, channel half), dY staged in LDS inside a zero ring.
+    per (stride-parity class, channel half), dY staged in LDS inside a zero ring; the
+    weights are packed into per-lane fragment order first (``ws``: cached 256 KB buffer).
     Split mode (``dy_lo``, ``w_lo``, ``out_lo``): the hi / lo plane kernel."""
     from .conv_sigs import Conv2DgradImgDesc
     N = dy.shape[0]
@@ -304,18 +308,20 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
         for t in (dy_lo, w_lo, out_lo):
             assert t is not None and t.is_contiguous() and t.dtype == torch.bfloat16
         d.dy_lo, d.w_lo, d.dx_lo = dy_lo.data_ptr(), w_lo.data_ptr(), out_lo.data_ptr()
+    ws = ws if ws is not None else _DEFAULT_WS
+    d.wfrag = ws.get(("c2d_wfrag",), 2 * 8192 * 8, dy.device, torch.bfloat16).data_ptr()
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 
 def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor, dy_lo=None,
-                w_lo=None, out_lo=None) -> None:
+                w_lo=None, out_lo=None, ws: Optional["Workspace"] = None) -> None:
     """dX1 (20x20) from dY2 (9x9), 4x4 stride 2: four stride-parity classes, each a
     2x2 stride-1 correlation (pad 1) writing every other output pixel; weights read
     K-major from the OHWI tensor per class."""
     N = dy.shape[0]
     assert w2.shape == (64, 4, 4, 64)
     if CONV2_DGRAD_IMG and hasattr(lib, "apex_conv2_dgrad_img"):
-        conv2_dgrad_img(lib, dy, w2, mask, out, dy_lo=dy_lo, w_lo=w_lo, out_lo=out_lo)
+        conv2_dgrad_img(lib, dy, w2, mask, out, dy_lo=dy_lo, w_lo=w_lo, out_lo=out_lo, ws=ws)
         return
     d = _conv_desc(x=dy.data_ptr(), w=w2.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
                    Cin=64, OH=10, OW=10, Cout=64, KH=2, KW=2, stride=1, pad=1, mode=1, K=256, ncls=4,

@@ -339,7 +339,7 @@ class HipBackend(TorchBackend):
         if stride == 1:
             C.conv3_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo)
         else:
-            C.conv2_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo)
+            C.conv2_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo, ws=self.ws)
 
     def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None, dy_lo=None, x_lo=None):
         if not self.native_conv:
