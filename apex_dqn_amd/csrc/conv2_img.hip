@@ -26,6 +26,7 @@
 // Online / target weights switch per image (img_switch), so any batch works in one
 // launch.
 #include "mfma_common.h"
+#include "conv2_wfrag.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -397,36 +398,11 @@ struct Conv2DgradImgDesc {
   const bf16_t* w_lo;
   bf16_t* dx_lo;
   // workspace for the weights in per-lane fragment order (C2D_FRAGS uint4 per plane,
-  // hi then lo), written by pack_c2d_wfrag_kernel in the same launch sequence
+  // hi then lo, csrc/conv2_wfrag.h): packed by this launcher, or already packed earlier
+  // in the step (wfrag_ready: the fc forward's epilogue launch does it in spare blocks)
   uint4* wfrag;
+  int wfrag_ready;
 };
-#define C2D_FRAGS 8192   // (class, channel half, K step, lane)
-
-// The data-gradient kernels hold the conv2 weights as MFMA A fragments: wave (class,
-// channel half), K step s, lane -> 8 bf16 of input channel nh*32 + (lane & 31) over
-// output channels co0 .. co0 + 7 at one kernel tap, i.e. 8 two-byte gathers strided by
-// 2 KB.  Done in every workgroup that is 256 x 512 (split: 1024) such gathers per lane,
-// ~10 us of the launch; here one 8192-thread pass writes the fragments once per
-// launch and each workgroup reads them back as coalesced 16-B loads.
-__global__ void __launch_bounds__(256) pack_c2d_wfrag_kernel(const bf16_t* __restrict__ w,
-                                                             const bf16_t* __restrict__ w_lo,
-                                                             uint4* __restrict__ out) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= C2D_FRAGS) return;
-  const int lane = t & 63, s = (t >> 6) & 15, nh = (t >> 10) & 1, cls = t >> 11;
-  const int p = cls >> 1, q = cls & 1, rr = lane & 31, kg = lane >> 5;
-  const int a = (s >> 3) & 1, b = (s >> 2) & 1, co0 = ((s & 3) << 4) + kg * 8;
-  const int kh = p + 2 * a, kw = q + 2 * b, ci = nh * 32 + rr;
-  uint32_t u[4], v[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int o0 = ((co0 + 2 * e) * 16 + kh * 4 + kw) * 64 + ci, o1 = o0 + 16 * 64;
-    u[e] = (uint32_t)w[o0] | ((uint32_t)w[o1] << 16);
-    if (w_lo) v[e] = (uint32_t)w_lo[o0] | ((uint32_t)w_lo[o1] << 16);
-  }
-  out[t] = make_uint4(u[0], u[1], u[2], u[3]);
-  if (w_lo) out[C2D_FRAGS + t] = make_uint4(v[0], v[1], v[2], v[3]);
-}
 
 #define C2D_SLOTS 121   // 11 x 11 padded dY slots, 128 B each
 // The M rows of the dgrad GEMMs are output pixels on an 11-wide grid (the slot grid's
@@ -438,6 +414,12 @@ __global__ void __launch_bounds__(256) pack_c2d_wfrag_kernel(const bf16_t* __res
 #define C2D_PSLOTS 144
 
 __device__ __forceinline__ int c2d_off(int slot, int c) { return (slot << 7) + ((c ^ ((slot >> 1) & 7)) << 4); }
+
+__global__ void __launch_bounds__(256) pack_c2d_wfrag_kernel(const bf16_t* __restrict__ w,
+                                                             const bf16_t* __restrict__ w_lo,
+                                                             uint32_t* __restrict__ out) {
+  pack_c2d_wfrag_word(blockIdx.x * 256 + threadIdx.x, w, w_lo, out);
+}
 
 __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDesc d) {
   __shared__ __attribute__((aligned(16))) uint8_t sdy[C2D_PSLOTS * 128];
@@ -661,7 +643,9 @@ APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t 
   const bool split = d.dy_lo != nullptr;
   if (split && (d.w_lo == nullptr || d.dx_lo == nullptr || (((uintptr_t)d.dy_lo | (uintptr_t)d.dx_lo) & 15)))
     return (int)hipErrorInvalidValue;
-  pack_c2d_wfrag_kernel<<<C2D_FRAGS / 256, 256, 0, st>>>(d.w, split ? d.w_lo : nullptr, d.wfrag);
+  if (!d.wfrag_ready)
+    pack_c2d_wfrag_kernel<<<C2D_PACK_THREADS / 256, 256, 0, st>>>(d.w, split ? d.w_lo : nullptr,
+                                                                  reinterpret_cast<uint32_t*>(d.wfrag));
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
   if (split) conv2_dgrad_img_split_kernel<<<G, 256, 0, st>>>(d);

@@ -1,0 +1,33 @@
+// conv2 weights in the per-lane MFMA fragment order of the conv2 data-gradient
+// kernels (csrc/conv2_img.hip): shared by their own launcher and by the fc forward's
+// split-K epilogue launch (csrc/conv_mfma.hip), which packs them in spare blocks.
+#pragma once
+#include "apex_common.h"
+
+#define C2D_FRAGS 8192   // (class, channel half, K step, lane)
+
+// The data-gradient kernels hold the conv2 weights as MFMA A fragments: wave (class,
+// channel half), K step s, lane -> 8 bf16 of input channel nh*32 + (lane & 31) over
+// output channels co0 .. co0 + 7 at one kernel tap, i.e. 8 two-byte gathers strided by
+// 2 KB.  Done in every workgroup that is 256 x 512 (split: 1024) such gathers per lane,
+// ~10 us of the launch; here one pass writes the fragments once per step and each
+// workgroup reads them back as coalesced 16-B loads.
+#define C2D_PACK_THREADS (2 * 4 * C2D_FRAGS)   // one per 4-byte word of both planes
+__device__ __forceinline__ void pack_c2d_wfrag_word(int i, const bf16_t* __restrict__ w,
+                                                   const bf16_t* __restrict__ w_lo, uint32_t* __restrict__ out) {
+  // one thread per 4-byte word (two output channels) of one plane: 64 K threads.  As a
+  // launch of its own this takes ~5.8 us of the step (the launch, not the work), so
+  // the step runs it in spare blocks of the fc forward's epilogue launch.
+  if (i >= C2D_PACK_THREADS) return;
+  const int pl = i / (4 * C2D_FRAGS), j = i - pl * 4 * C2D_FRAGS;
+  const int t = j >> 2, e = j & 3;
+  const int lane = t & 63, s = (t >> 6) & 15, nh = (t >> 10) & 1, cls = t >> 11;
+  const int p = cls >> 1, q = cls & 1, rr = lane & 31, kg = lane >> 5;
+  const int a = (s >> 3) & 1, b = (s >> 2) & 1, co0 = ((s & 3) << 4) + kg * 8;
+  const int kh = p + 2 * a, kw = q + 2 * b, ci = nh * 32 + rr;
+  const bf16_t* __restrict__ src = pl ? w_lo : w;
+  if (src == nullptr) return;
+  const int o0 = ((co0 + 2 * e) * 16 + kh * 4 + kw) * 64 + ci, o1 = o0 + 16 * 64;
+  out[i] = (uint32_t)src[o0] | ((uint32_t)src[o1] << 16);
+}
+

@@ -21,6 +21,7 @@
 // next tile's loads are issued before the current tile's MFMAs.
 #include "mfma_common.h"
 #include "igemm_wgrad.h"
+#include "conv2_wfrag.h"
 
 struct ConvDesc {
   const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]
@@ -764,9 +765,22 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
 // y[m][n] = act(sum_z ws[z][m][n] * in_scale + bias[n]): 8 outputs per thread, the
 // z partials summed in fixed order.  act = ReLU (fp32, before the hi / lo split) or
 // the dgrad mask (both planes, from the producer's bf16 activation).
+// Side job (pk.out != null): blocks past the epilogue's grid pack the conv2 weights
+// for the step's conv2 data gradient (csrc/conv2_wfrag.h) -- a launch of its own costs
+// ~5 us in the step's graph; here it rides on an elementwise pass.
+struct C2dPackJob {
+  const bf16_t* w;
+  const bf16_t* w_lo;
+  uint32_t* out;
+};
+
 template <bool SPLIT>
 __global__ void __launch_bounds__(256) fc_splitk_epilogue_kernel(ConvDesc d, const float* __restrict__ ws,
-                                                                 int nz) {
+                                                                 int nz, int eb, C2dPackJob pk) {
+  if ((int)blockIdx.x >= eb) {
+    pack_c2d_wfrag_word(((int)blockIdx.x - eb) * 256 + threadIdx.x, pk.w, pk.w_lo, pk.out);
+    return;
+  }
   const int Nc = d.Cout;
   const int64_t MN = (int64_t)d.N * Nc;
   const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
@@ -962,9 +976,10 @@ static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
 
 // Dense C[M,N] = act(A[M,K] . B[N,K]^T + b) on 128x128 tiles, K split `ksplit` ways
 // (fc_gemm128_kernel + fc_splitk_epilogue_kernel).  ws: fp32 workspace of at least
-// ksplit * M * N elements.  Row-major B only (d.bt == 0), N % 128 == 0.
+// ksplit * M * N elements.  Row-major B only (d.bt == 0), N % 128 == 0.  pk: optional
+// conv2 weight-fragment pack riding on the epilogue launch (fc_splitk_epilogue_kernel).
 APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksplit, int loader_waves,
-                                hipStream_t st) {
+                                C2dPackJob pk, hipStream_t st) {
   if (d.mode != 0 || d.bt != 0 || (d.K & 63) || d.K <= 0 || (d.Cout & 127) || d.N <= 0 || ksplit < 1)
     return (int)hipErrorInvalidValue;
   if ((d.ldy & 7) || d.ldy < d.Cout) return (int)hipErrorInvalidValue;
@@ -988,8 +1003,10 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   }
   const int64_t nthr = (int64_t)d.N * d.Cout / 8;
   const int eb = (int)((nthr + 255) / 256);
-  if (split) fc_splitk_epilogue_kernel<true><<<eb, 256, 0, st>>>(d, ws, nz);
-  else fc_splitk_epilogue_kernel<false><<<eb, 256, 0, st>>>(d, ws, nz);
+  if (pk.out != nullptr && (pk.w == nullptr || ((uintptr_t)pk.out & 15))) return (int)hipErrorInvalidValue;
+  const int pb = pk.out != nullptr ? C2D_PACK_THREADS / 256 : 0;
+  if (split) fc_splitk_epilogue_kernel<true><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk);
+  else fc_splitk_epilogue_kernel<false><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk);
   APEX_CHECK_LAUNCH();
 }
 

@@ -240,6 +240,7 @@ class FusedNatureLearner:
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
                      **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
         ops.fc_fwd(self.y3.reshape(n, 3136), Pb["wfc"], P["bfc"], self.h, Tb["wfc"], T["bfc"], 2 * B,
+                   c2d=(Pb["w2"], Pl["w2"] if sp else None),
                    **self._lo(x_lo=sp and self.y3_lo.reshape(n, 3136), w_lo=sp and Pl["wfc"],
                               w2_lo=sp and Tl["wfc"], out_lo=self.h_lo))
 

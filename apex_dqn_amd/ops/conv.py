@@ -216,10 +216,13 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
 
 def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
                  out: torch.Tensor, relu: bool = True, w2=None, b2=None, rows_first: int = 0, ksplit: int = 2,
-                 loader_waves: bool = False, x_lo=None, w_lo=None, w2_lo=None, out_lo=None) -> None:
+                 loader_waves: bool = False, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
+                 c2d_pack: Optional[Tuple[torch.Tensor, Optional[torch.Tensor]]] = None) -> None:
     """``dense_fwd`` on 128x128 tiles with the K range split ``ksplit`` ways
     (csrc/conv_mfma.hip ``fc_gemm128_kernel``): fp32 partials in a cached workspace,
-    summed in fixed order by the epilogue kernel (bias, ReLU, hi / lo planes)."""
+    summed in fixed order by the epilogue kernel (bias, ReLU, hi / lo planes).
+    ``c2d_pack = (w2, w2_lo)``: the epilogue launch also packs conv2's weights for this
+    step's conv2 data gradient (``conv2_dgrad_img(..., packed=True)``)."""
     M, K = x.shape
     Nc = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, Nc) and Nc % 128 == 0 and K % 64 == 0
@@ -229,11 +232,21 @@ def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Opti
     kt = K // 64
     per = -(-kt // ksplit)
     nz = -(-kt // per)
-    buf = ws.get(("fc128",), nz * M * Nc, x.device)
+    buf = ws.get(("fc128", _lib.stream_ptr()), nz * M * Nc, x.device)   # per stream: actors share the backend
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), N=M, Cin=K, Cout=Nc,
                    mode=0, relu=relu, K=K, **_second(w2, b2, rows_first, 1), **_lo(x_lo, w_lo, w2_lo, out_lo))
-    _lib.check(lib.apex_fc_gemm128(d, buf.data_ptr(), buf.numel(), int(ksplit), int(loader_waves),
+    from .conv_sigs import C2dPackJob
+    pk = C2dPackJob()
+    if c2d_pack is not None:
+        pk.w, pk.w_lo = c2d_pack[0].data_ptr(), _lib.ptr(c2d_pack[1])
+        pk.out = c2d_wfrag_buffer(ws, x.device).data_ptr()
+    _lib.check(lib.apex_fc_gemm128(d, buf.data_ptr(), buf.numel(), int(ksplit), int(loader_waves), pk,
                                       _lib.stream_ptr()), "fc_gemm128")
+
+
+def c2d_wfrag_buffer(ws: "Workspace", device) -> torch.Tensor:
+    """conv2 weights in the data-gradient kernels' fragment order (hi + lo planes, 256 KB)."""
+    return ws.get(("c2d_wfrag",), 2 * 8192 * 8, device, torch.bfloat16)
 
 
 # K-major B-operand offsets for the dgrad GEMMs reading the natural OHWI weights.
@@ -292,10 +305,12 @@ CONV2_DGRAD_IMG = _os.environ.get("APEX_CONV2_DGRAD_IMG", "1") != "0"
 
 
 def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor,
-                    grid: int = 0, dy_lo=None, w_lo=None, out_lo=None, ws: Optional["Workspace"] = None) -> None:
+                    grid: int = 0, dy_lo=None, w_lo=None, out_lo=None, ws: Optional["Workspace"] = None,
+                    packed: bool = False) -> None:
     """conv2 data gradient on the image-resident kernel (csrc/conv2_img.hip): one wave
     per (stride-parity class, channel half), dY staged in LDS inside a zero ring; the
-    weights are packed into per-lane fragment order first (``ws``: cached 256 KB buffer).
+    weights are packed into per-lane fragment order first (``ws``: cached 256 KB buffer;
+    ``packed``: already done earlier in the step by ``dense_fwd128(c2d_pack=...)``).
     Split mode (``dy_lo``, ``w_lo``, ``out_lo``): the hi / lo plane kernel."""
     from .conv_sigs import Conv2DgradImgDesc
     N = dy.shape[0]
@@ -309,19 +324,20 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
             assert t is not None and t.is_contiguous() and t.dtype == torch.bfloat16
         d.dy_lo, d.w_lo, d.dx_lo = dy_lo.data_ptr(), w_lo.data_ptr(), out_lo.data_ptr()
     ws = ws if ws is not None else _DEFAULT_WS
-    d.wfrag = ws.get(("c2d_wfrag",), 2 * 8192 * 8, dy.device, torch.bfloat16).data_ptr()
+    d.wfrag = c2d_wfrag_buffer(ws, dy.device).data_ptr()
+    d.wfrag_ready = int(packed)
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 
 def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor, dy_lo=None,
-                w_lo=None, out_lo=None, ws: Optional["Workspace"] = None) -> None:
+                w_lo=None, out_lo=None, ws: Optional["Workspace"] = None, packed: bool = False) -> None:
     """dX1 (20x20) from dY2 (9x9), 4x4 stride 2: four stride-parity classes, each a
     2x2 stride-1 correlation (pad 1) writing every other output pixel; weights read
     K-major from the OHWI tensor per class."""
     N = dy.shape[0]
     assert w2.shape == (64, 4, 4, 64)
     if CONV2_DGRAD_IMG and hasattr(lib, "apex_conv2_dgrad_img"):
-        conv2_dgrad_img(lib, dy, w2, mask, out, dy_lo=dy_lo, w_lo=w_lo, out_lo=out_lo, ws=ws)
+        conv2_dgrad_img(lib, dy, w2, mask, out, dy_lo=dy_lo, w_lo=w_lo, out_lo=out_lo, ws=ws, packed=packed)
         return
     d = _conv_desc(x=dy.data_ptr(), w=w2.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
                    Cin=64, OH=10, OW=10, Cout=64, KH=2, KW=2, stride=1, pad=1, mode=1, K=256, ncls=4,

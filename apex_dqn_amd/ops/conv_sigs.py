@@ -18,7 +18,12 @@ class Conv2ImgDesc(ctypes.Structure):
 class Conv2DgradImgDesc(ctypes.Structure):
     """Image-resident conv2 data gradient (mirrors ``Conv2DgradImgDesc`` in csrc/conv2_img.hip)."""
     _fields_ = [("dy", c_p), ("w", c_p), ("mask", c_p), ("dx", c_p), ("N", c_i), ("dy_lo", c_p), ("w_lo", c_p),
-                ("dx_lo", c_p), ("wfrag", c_p)]
+                ("dx_lo", c_p), ("wfrag", c_p), ("wfrag_ready", c_i)]
+
+
+class C2dPackJob(ctypes.Structure):
+    """conv2 weight-fragment pack riding on the fc epilogue launch (``C2dPackJob``)."""
+    _fields_ = [("w", c_p), ("w_lo", c_p), ("out", c_p)]
 
 
 class Conv3DgradImgDesc(ctypes.Structure):
@@ -33,7 +38,7 @@ def declare(lib: ctypes.CDLL) -> None:
         "apex_conv2_dgrad_img": ([Conv2DgradImgDesc, c_i, c_p], c_i),
         "apex_conv3_dgrad_img": ([Conv3DgradImgDesc, c_i, c_p], c_i),
         "apex_conv_fwd": ([ConvDesc, c_p], c_i),
-        "apex_fc_gemm128": ([ConvDesc, c_p, c_i64, c_i, c_i, c_p], c_i),
+        "apex_fc_gemm128": ([ConvDesc, c_p, c_i64, c_i, c_i, C2dPackJob, c_p], c_i),
         "apex_conv_wgrad": ([WgradDesc, c_p, c_p, c_i, c_f, c_p], c_i),
         "apex_pack_dgrad_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     }

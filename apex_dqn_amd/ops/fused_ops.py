@@ -83,7 +83,10 @@ class TorchBackend:
             split_into(R.conv_fwd(xf[r:], join(w2, w2_lo), b2, stride, dt), out[r:],
                        None if out_lo is None else out_lo[r:])
 
-    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None):
+    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
+               c2d=None):
+        """``c2d = (conv2 weight, lo plane)``: weights of this step's conv2 data gradient,
+        which the HIP backend pre-packs inside the fc launch (ignored here)."""
         dt = torch.float32 if x_lo is not None else self.dtype
         x = x.reshape(x.shape[0], -1)
         xf = join(x, x_lo.reshape(x.shape)) if x_lo is not None else x
@@ -282,7 +285,8 @@ class HipBackend(TorchBackend):
         C.conv_fwd(self.lib, x, w, b, stride, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo,
                    out_lo=out_lo)
 
-    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None):
+    def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
+               c2d=None):
         if not self.native_conv:
             return super().fc_fwd(x, w, b, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
         M, K = x.shape[0], x[0].numel()
@@ -292,7 +296,11 @@ class HipBackend(TorchBackend):
             # (split) / 25.7 -> 22.5 (bf16) at the learner shape (scripts/bench_fc128.py)
             C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, 2, True,
                            x_lo=None if x_lo is None else x_lo.reshape(M, K), w_lo=w_lo, w2_lo=w2_lo,
-                           out_lo=out_lo)
+                           out_lo=out_lo, c2d_pack=c2d)
+            # the conv2 data gradient of this step finds its weights packed (the key is
+            # checked there, so a different weight tensor still packs its own)
+            if c2d is not None:
+                self._c2d_packed = (c2d[0].data_ptr(), _lib.ptr(c2d[1]))
             return
         C.dense_fwd(self.lib, x.reshape(x.shape[0], -1), w, b, out, relu=True, w2=w2, b2=b2,
                     rows_first=rows_first, ws=self.ws,
@@ -339,7 +347,11 @@ class HipBackend(TorchBackend):
         if stride == 1:
             C.conv3_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo)
         else:
-            C.conv2_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo, ws=self.ws)
+            key = (w.data_ptr(), _lib.ptr(w_lo))
+            packed = getattr(self, "_c2d_packed", None) == key
+            self._c2d_packed = None
+            C.conv2_dgrad(self.lib, dy, w, x_src, dx_out, dy_lo=dy_lo, w_lo=w_lo, out_lo=dx_lo, ws=self.ws,
+                          packed=packed)
 
     def conv_wgrad(self, dy, x, k, stride, dw_out, db_out, jobs=None, dy_lo=None, x_lo=None):
         if not self.native_conv:

@@ -80,3 +80,33 @@ def test_backend_fc_fwd_routes_to_fc128(split):
     c = outs[2].double() + (outs[3].double() if split else 0)
     err = ((a - c).abs() / (c.abs() + 1e-1)).max().item()
     assert err < (1e-4 if split else 8e-3), err
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_c2d_pack_in_fc_epilogue_matches_own_pack(split):
+    """The conv2 weight-fragment pack that rides on the fc epilogue launch gives the
+    conv2 data gradient bit-identical results to the launcher's own pack."""
+    from apex_dqn_amd.ops import _lib as L, conv as C
+    lib = L.require_kernels()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    ws = C.Workspace()
+    B = 64
+    (xh, xl) = _sp(torch.relu(torch.randn(256, 3136, generator=g)).to(DEV))
+    (wh, wl) = _sp((torch.randn(128, 3136, generator=g) * 0.02).to(DEV))
+    b = torch.zeros(128, device=DEV)
+    fo = [torch.zeros(256, 128, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+    (c2h, c2l) = _sp((torch.randn(64, 4, 4, 64, generator=g) * 0.03).to(DEV))
+    (dyh, dyl) = _sp(torch.randn(B, 9, 9, 64, generator=g).to(DEV))
+    y1 = torch.relu(torch.randn(B, 20, 20, 64, generator=g)).to(DEV).to(torch.bfloat16)
+    outs = [torch.zeros(B, 20, 20, 64, device=DEV, dtype=torch.bfloat16) for _ in range(4)]
+    lo = lambda o: dict(dy_lo=dyl, w_lo=c2l, out_lo=o) if split else {}
+    C.conv2_dgrad_img(lib, dyh, c2h, y1, outs[0], ws=ws, **lo(outs[1]))
+    C.c2d_wfrag_buffer(ws, DEV).fill_(3.0)     # stale contents must be overwritten by the fc launch
+    C.dense_fwd128(lib, ws, xh, wh, b, fo[0], True, ksplit=2, loader_waves=True,
+                   c2d_pack=(c2h, c2l if split else None),
+                   **(dict(x_lo=xl, w_lo=wl, out_lo=fo[1]) if split else {}))
+    C.conv2_dgrad_img(lib, dyh, c2h, y1, outs[2], ws=ws, packed=True, **lo(outs[3]))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[2])
+    if split:
+        assert torch.equal(outs[1], outs[3])
