@@ -43,7 +43,26 @@ struct Conv2ImgDesc {
   const bf16_t* w_lo;
   const bf16_t* w2_lo;
   bf16_t* y_lo;
+  // split mode: workspace for both weight sets in per-lane fragment order (4 x C2F_FRAGS
+  // uint4: set 0 hi, lo, set 1 hi, lo), packed by the launcher; null: gather in-kernel
+  uint4* wfrag;
 };
+#define C2F_FRAGS 8192   // (wave, K step, lane) of the split forward
+
+// Split forward weights in fragment order: wave (nh, kp), K step s, lane -> the 16 B of
+// w[co = nh*32 + (lane & 31)][kh = 2 kp + (s >> 4)][kw = (s >> 2) & 3][ci0 ..], read back
+// by each workgroup as one coalesced 1-KB load per wave instead of 32 lines per load.
+__global__ void __launch_bounds__(256) pack_c2f_wfrag_kernel(Conv2ImgDesc d) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 4 * C2F_FRAGS) return;
+  const int q = i / C2F_FRAGS, t = i - q * C2F_FRAGS;   // q = set * 2 + plane
+  const bf16_t* src = q == 0 ? d.w : q == 1 ? d.w_lo : q == 2 ? d.w2 : d.w2_lo;
+  if (src == nullptr) return;
+  const int lane = t & 63, s = (t >> 6) & 31, wv = t >> 11;
+  const int nh = wv & 1, kp = wv >> 1, rr = lane & 31, kg = lane >> 5;
+  const int co = nh * 32 + rr, kh = 2 * kp + (s >> 4), kw = (s >> 2) & 3, ci0 = ((s & 3) << 4) + kg * 8;
+  d.wfrag[i] = *reinterpret_cast<const uint4*>(src + ((co * 4 + kh) * 4 + kw) * 64 + ci0);
+}
 
 #define C2_THREADS 512
 #define C2_IMG 51200            // image bytes (global)
@@ -256,15 +275,24 @@ __global__ void __launch_bounds__(C2S_THREADS, 1) conv2_img_fwd_split_kernel(Con
     const int img = img0 + i * step;
     const int set = (d.w2 != nullptr && img >= d.img_switch) ? 1 : 0;
     if (set != cur_set) {
-      const bf16_t* W = set ? d.w2 : d.w;
-      const bf16_t* WL = set ? d.w2_lo : d.w_lo;
-      const int co = nh * 32 + rr;
+      if (d.wfrag != nullptr) {   // pack_c2f_wfrag_kernel order
+        const uint4* wf = d.wfrag + set * 2 * C2F_FRAGS + wv * 32 * 64 + lane;
 #pragma unroll
-      for (int s = 0; s < 32; ++s) {
-        const int kh = 2 * kp + (s >> 4), kw = (s >> 2) & 3, ci0 = ((s & 3) << 4) + kg * 8;
-        const int64_t o = ((co * 4 + kh) * 4 + kw) * 64 + ci0;
-        bh[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(W + o));
-        bl[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(WL + o));
+        for (int s = 0; s < 32; ++s) {
+          bh[s] = __builtin_bit_cast(bf16x8, wf[s * 64]);
+          bl[s] = __builtin_bit_cast(bf16x8, wf[C2F_FRAGS + s * 64]);
+        }
+      } else {
+        const bf16_t* W = set ? d.w2 : d.w;
+        const bf16_t* WL = set ? d.w2_lo : d.w_lo;
+        const int co = nh * 32 + rr;
+#pragma unroll
+        for (int s = 0; s < 32; ++s) {
+          const int kh = 2 * kp + (s >> 4), kw = (s >> 2) & 3, ci0 = ((s & 3) << 4) + kg * 8;
+          const int64_t o = ((co * 4 + kh) * 4 + kw) * 64 + ci0;
+          bh[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(W + o));
+          bl[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(WL + o));
+        }
       }
       // drain here (once per weight set), as an instruction the compiler's wait
       // insertion sees: otherwise it assumes these loads (and the biases) may still be
@@ -366,6 +394,10 @@ APEX_EXPORT int apex_conv2_img_fwd(Conv2ImgDesc d, int grid, hipStream_t st) {
   }
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
+  if (split && d.wfrag != nullptr) {
+    if ((uintptr_t)d.wfrag & 15) return (int)hipErrorInvalidValue;
+    pack_c2f_wfrag_kernel<<<4 * C2F_FRAGS / 256, 256, 0, st>>>(d);
+  }
   if (split) conv2_img_fwd_split_kernel<<<G, C2S_THREADS, 0, st>>>(d);
   else conv2_img_fwd_kernel<<<G, C2_THREADS, 0, st>>>(d);
   APEX_CHECK_LAUNCH();

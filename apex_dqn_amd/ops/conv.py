@@ -143,6 +143,13 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
 CONV2_IMG = _os.environ.get("APEX_CONV2_IMG", "1") != "0"
 
 
+# split conv2 forward: the launcher packs both weight sets into per-lane fragment order
+# first (pack_c2f_wfrag_kernel; 76.2 -> 71.0 us at 1536 images including the pack,
+# profiles/r2_split_conv2_packed_fwd.jsonl).  False = in-kernel gathers (the A/B of
+# scripts/bench_split_conv2.py).
+C2F_PACK = True
+
+
 def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
                   w2=None, b2=None, rows_first: int = 0, grid: int = 0, x_lo=None, w_lo=None, w2_lo=None,
                   out_lo=None) -> None:
@@ -163,6 +170,9 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
         for t in (x_lo, w_lo, out_lo) + ((w2_lo,) if w2 is not None else ()):
             assert t is not None and t.is_contiguous() and t.dtype == torch.bfloat16
         d.x_lo, d.w_lo, d.w2_lo, d.y_lo = x_lo.data_ptr(), w_lo.data_ptr(), _lib.ptr(w2_lo), out_lo.data_ptr()
+        if C2F_PACK:
+            d.wfrag = _DEFAULT_WS.get(("c2f_wfrag", _lib.stream_ptr()), 4 * 8192 * 8, x.device,
+                                      torch.bfloat16).data_ptr()
     _lib.check(lib.apex_conv2_img_fwd(d, int(grid), _lib.stream_ptr()), "conv2_img_fwd")
 
 

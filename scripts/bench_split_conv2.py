@@ -40,13 +40,15 @@ def main():
         us = timed(lambda: C.conv_fwd(lib, xh, wh, b, 2, oh, w2h, b2, 1024, x_lo=xl, w_lo=wl, w2_lo=w2l, out_lo=ol))
         print(json.dumps({"op": "conv2_fwd_split_igemm", "us": round(us, 2), "tflops_eff": round(fl / us / 1e6, 1)}),
               flush=True)
-    for n in ((256, 512, 1024, 1536) if not only else (1536,)):
-        if only and only != "fwd":
-            break
-        us = timed(lambda: C.conv2_img_fwd(lib, xh[:n], wh, b, oh[:n], w2h, b2, 2 * n // 3, x_lo=xl[:n], w_lo=wl,
-                                           w2_lo=w2l, out_lo=ol[:n]))
-        print(json.dumps({"op": "conv2_fwd_split_img", "images": n, "us": round(us, 2),
-                          "tflops_eff": round(3 * 2.0 * n * 81 * 64 * 1024 / us / 1e6, 1)}), flush=True)
+    for pack in (False, True):
+        C.C2F_PACK = pack
+        for n in ((256, 512, 1024, 1536) if not only else (1536,)):
+            if only and only != "fwd":
+                break
+            us = timed(lambda: C.conv2_img_fwd(lib, xh[:n], wh, b, oh[:n], w2h, b2, 2 * n // 3, x_lo=xl[:n],
+                                               w_lo=wl, w2_lo=w2l, out_lo=ol[:n]))
+            print(json.dumps({"op": "conv2_fwd_split_img", "packed_w": pack, "images": n, "us": round(us, 2),
+                              "tflops_eff": round(3 * 2.0 * n * 81 * 64 * 1024 / us / 1e6, 1)}), flush=True)
     B = 512
     dy = torch.randn(B, 9, 9, 64, device=dev)
     dyh, dyl = sp(dy)
