@@ -146,8 +146,8 @@ CONV2_IMG = _os.environ.get("APEX_CONV2_IMG", "1") != "0"
 # split conv2 forward: the launcher packs both weight sets into per-lane fragment order
 # first (pack_c2f_wfrag_kernel; 76.2 -> 71.0 us at 1536 images including the pack,
 # profiles/r2_split_conv2_packed_fwd.jsonl).  False = in-kernel gathers (the A/B of
-# scripts/bench_split_conv2.py).
-C2F_PACK = True
+# scripts/bench_split_conv2.py; APEX_C2F_PACK=0 for scripts/ab.sh).
+C2F_PACK = _os.environ.get("APEX_C2F_PACK", "1") != "0"
 
 
 def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
