@@ -15,6 +15,7 @@
 // uint8 -> bf16 conversion happens at fragment-read time (values 0..255 are
 // exact in bf16; the 1/255 input scale is applied in the epilogue).
 #include "mfma_common.h"
+#include "conv2_wfrag.h"
 
 #define S2D_FRAME 7056
 
@@ -36,6 +37,10 @@ struct Conv1S2DDesc {
   const float* w32;
   const float* w2_32;
   bf16_t* y_lo;
+  // side job: pack the split conv2 forward's weights for this step (csrc/conv2_wfrag.h)
+  // at the start of the workgroups -- behind their first frame DMAs' latency instead of
+  // a launch of its own (~5 us in the step)
+  C2fPack c2f;
 };
 
 // ---------------------------------------------------------------------------
@@ -105,6 +110,7 @@ __global__ void __launch_bounds__(C1_THREADS, 1) conv1_s2d_fwd_kernel(Conv1S2DDe
   __shared__ int32_t slot_tbl[C1_MAXIMG * C];   // this block's frame slots (prologue)
   uint8_t* Sg = smem + 2 * IMG;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (d.c2f.out != nullptr) c2f_pack_range(d.c2f, blockIdx.x * C1_THREADS + tid, gridDim.x * C1_THREADS);
   const int g = lane >> 4, pl = lane & 15;
   const bool two = d.w2 != nullptr;
   const int img_switch = two ? d.m_switch / 400 : 1 << 30;

@@ -44,24 +44,15 @@ struct Conv2ImgDesc {
   const bf16_t* w2_lo;
   bf16_t* y_lo;
   // split mode: workspace for both weight sets in per-lane fragment order (4 x C2F_FRAGS
-  // uint4: set 0 hi, lo, set 1 hi, lo), packed by the launcher; null: gather in-kernel
+  // uint4: set 0 hi, lo, set 1 hi, lo), packed by the launcher -- or already packed earlier
+  // in the step (wfrag_ready: by the conv1 launch) -- ; null: gather in-kernel
   uint4* wfrag;
+  int wfrag_ready;
 };
-#define C2F_FRAGS 8192   // (wave, K step, lane) of the split forward
-
-// Split forward weights in fragment order: wave (nh, kp), K step s, lane -> the 16 B of
-// w[co = nh*32 + (lane & 31)][kh = 2 kp + (s >> 4)][kw = (s >> 2) & 3][ci0 ..], read back
-// by each workgroup as one coalesced 1-KB load per wave instead of 32 lines per load.
-__global__ void __launch_bounds__(256) pack_c2f_wfrag_kernel(Conv2ImgDesc d) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= 4 * C2F_FRAGS) return;
-  const int q = i / C2F_FRAGS, t = i - q * C2F_FRAGS;   // q = set * 2 + plane
-  const bf16_t* src = q == 0 ? d.w : q == 1 ? d.w_lo : q == 2 ? d.w2 : d.w2_lo;
-  if (src == nullptr) return;
-  const int lane = t & 63, s = (t >> 6) & 31, wv = t >> 11;
-  const int nh = wv & 1, kp = wv >> 1, rr = lane & 31, kg = lane >> 5;
-  const int co = nh * 32 + rr, kh = 2 * kp + (s >> 4), kw = (s >> 2) & 3, ci0 = ((s & 3) << 4) + kg * 8;
-  d.wfrag[i] = *reinterpret_cast<const uint4*>(src + ((co * 4 + kh) * 4 + kw) * 64 + ci0);
+// Split forward weights -> fragment order (csrc/conv2_wfrag.h c2f_src_off): each
+// workgroup then reads them as one coalesced 1-KB load per wave instead of 32 lines per load.
+__global__ void __launch_bounds__(256) pack_c2f_wfrag_kernel(C2fPack p) {
+  c2f_pack_range(p, blockIdx.x * 256 + threadIdx.x, 4 * C2F_FRAGS);
 }
 
 #define C2_THREADS 512
@@ -396,7 +387,8 @@ APEX_EXPORT int apex_conv2_img_fwd(Conv2ImgDesc d, int grid, hipStream_t st) {
   if (G > d.N) G = d.N;
   if (split && d.wfrag != nullptr) {
     if ((uintptr_t)d.wfrag & 15) return (int)hipErrorInvalidValue;
-    pack_c2f_wfrag_kernel<<<4 * C2F_FRAGS / 256, 256, 0, st>>>(d);
+    if (!d.wfrag_ready)
+      pack_c2f_wfrag_kernel<<<4 * C2F_FRAGS / 256, 256, 0, st>>>(C2fPack{{d.w, d.w_lo, d.w2, d.w2_lo}, d.wfrag});
   }
   if (split) conv2_img_fwd_split_kernel<<<G, C2S_THREADS, 0, st>>>(d);
   else conv2_img_fwd_kernel<<<G, C2_THREADS, 0, st>>>(d);

@@ -31,3 +31,27 @@ __device__ __forceinline__ void pack_c2d_wfrag_word(int i, const bf16_t* __restr
   out[i] = (uint32_t)src[o0] | ((uint32_t)src[o1] << 16);
 }
 
+
+// Split conv2 forward weights in fragment order (csrc/conv2_img.hip
+// conv2_img_fwd_split_kernel): fragment t = (wave (nh, kp), K step s, lane) holds the 16 B
+// of w[co = nh*32 + (lane & 31)][kh = 2 kp + (s >> 4)][kw = (s >> 2) & 3][ci0 ..]; four
+// planes (set 0 hi, lo, set 1 hi, lo) of C2F_FRAGS uint4.  Packed by the conv2 launcher or
+// at the start of the step's conv1 launch (csrc/conv1_s2d.hip).
+#define C2F_FRAGS 8192
+__device__ __forceinline__ int c2f_src_off(int t) {
+  const int lane = t & 63, s = (t >> 6) & 31, wv = t >> 11;
+  const int nh = wv & 1, kp = wv >> 1, rr = lane & 31, kg = lane >> 5;
+  const int co = nh * 32 + rr, kh = 2 * kp + (s >> 4), kw = (s >> 2) & 3, ci0 = ((s & 3) << 4) + kg * 8;
+  return ((co * 4 + kh) * 4 + kw) * 64 + ci0;
+}
+struct C2fPack {
+  const bf16_t* src[4];   // set 0 hi, lo, set 1 hi, lo (null planes are skipped)
+  uint4* out;             // 4 * C2F_FRAGS, or null: no pack
+};
+__device__ __forceinline__ void c2f_pack_range(const C2fPack& p, int i0, int stride) {
+  for (int i = i0; i < 4 * C2F_FRAGS; i += stride) {
+    const int q = i / C2F_FRAGS;
+    const bf16_t* src = p.src[q];
+    if (src != nullptr) p.out[i] = *reinterpret_cast<const uint4*>(src + c2f_src_off(i - q * C2F_FRAGS));
+  }
+}

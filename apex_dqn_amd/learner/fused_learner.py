@@ -234,7 +234,8 @@ class FusedNatureLearner:
         sp = self.split
         n = 3 * B
         ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
-                           Tb["w1"], T["b1"], 2 * B, **self._lo(w32=P["w1"], w2_32=T["w1"], out_lo=self.y1_lo))
+                           Tb["w1"], T["b1"], 2 * B, **self._lo(w32=P["w1"], w2_32=T["w1"], out_lo=self.y1_lo,
+                                                                c2f=sp and (Pb["w2"], Pl["w2"], Tb["w2"], Tl["w2"])))
         ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B,
                      **self._lo(x_lo=self.y1_lo, w_lo=sp and Pl["w2"], w2_lo=sp and Tl["w2"], out_lo=self.y2_lo))
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,

@@ -109,10 +109,13 @@ def pack_w1_s2d(lib, ws: "Workspace", w1: torch.Tensor, tag: str) -> torch.Tenso
 def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
                   b1: torch.Tensor, scale: float, out: torch.Tensor, w2=None, b2=None, rows_first: int = 0,
                   grid: int = 0, probe: Optional[torch.Tensor] = None, w32: Optional[torch.Tensor] = None,
-                  w2_32: Optional[torch.Tensor] = None, out_lo: Optional[torch.Tensor] = None) -> None:
+                  w2_32: Optional[torch.Tensor] = None, out_lo: Optional[torch.Tensor] = None,
+                  c2f: Optional[Tuple] = None) -> None:
     """conv1 on the space-to-depth replay ring (persistent LDS-DMA kernel, csrc/conv1_s2d.hip).
     Split mode (``out_lo`` given): the fp32 master weights ``w32`` / ``w2_32`` (OIHW) are
-    read and the output leaves as hi (``out``) / lo (``out_lo``) bf16 planes."""
+    read and the output leaves as hi (``out``) / lo (``out_lo``) bf16 planes.
+    ``c2f = (w2 hi, lo, target hi, lo)``: the launch also packs the split conv2 forward's
+    weights for ``conv2_img_fwd(..., packed=True)`` on the same stream."""
     N, C = slots.shape
     assert out.shape == (N, 20, 20, 64) and w1.shape[1] == C and slots.dtype == torch.int32
     d = _lib.Conv1S2DDesc()
@@ -135,7 +138,16 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
     if out_lo is not None:
         assert w32 is not None and w32.dtype == torch.float32 and (w2 is None or w2_32 is not None)
         d.w32, d.w2_32, d.y_lo = w32.data_ptr(), _lib.ptr(w2_32), out_lo.data_ptr()
+    if c2f is not None:
+        for i, t in enumerate(c2f):
+            d.c2f_src[i] = _lib.ptr(t)
+        d.c2f_out = c2f_wfrag_fwd_buffer(ring.device).data_ptr()
     _lib.check(lib.apex_conv1_s2d_fwd(d, int(grid), _lib.stream_ptr()), "conv1_s2d_fwd")
+
+
+def c2f_wfrag_fwd_buffer(device) -> torch.Tensor:
+    """Split conv2 forward weights of both sets in fragment order (512 KB, per stream)."""
+    return _DEFAULT_WS.get(("c2f_wfrag", _lib.stream_ptr()), 4 * 8192 * 8, device, torch.bfloat16)
 
 
 # conv2 (20x20x64 -> 9x9x64, 4x4/s2) on the image-resident kernel (csrc/conv2_img.hip);
@@ -152,7 +164,7 @@ C2F_PACK = _os.environ.get("APEX_C2F_PACK", "1") != "0"
 
 def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
                   w2=None, b2=None, rows_first: int = 0, grid: int = 0, x_lo=None, w_lo=None, w2_lo=None,
-                  out_lo=None) -> None:
+                  out_lo=None, packed: bool = False) -> None:
     """conv2 + bias + ReLU, one persistent workgroup per CU walking whole images
     (image staged once in LDS, weights in VGPRs); online/target switch per image.
     Split mode (``x_lo`` .. ``out_lo``): the hi / lo plane kernel."""
@@ -170,14 +182,15 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
         for t in (x_lo, w_lo, out_lo) + ((w2_lo,) if w2 is not None else ()):
             assert t is not None and t.is_contiguous() and t.dtype == torch.bfloat16
         d.x_lo, d.w_lo, d.w2_lo, d.y_lo = x_lo.data_ptr(), w_lo.data_ptr(), _lib.ptr(w2_lo), out_lo.data_ptr()
-        if C2F_PACK:
-            d.wfrag = _DEFAULT_WS.get(("c2f_wfrag", _lib.stream_ptr()), 4 * 8192 * 8, x.device,
-                                      torch.bfloat16).data_ptr()
+        if C2F_PACK or packed:
+            d.wfrag = c2f_wfrag_fwd_buffer(x.device).data_ptr()
+            d.wfrag_ready = int(packed)
     _lib.check(lib.apex_conv2_img_fwd(d, int(grid), _lib.stream_ptr()), "conv2_img_fwd")
 
 
 def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int, out: torch.Tensor,
-             w2=None, b2=None, rows_first: int = 0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None) -> None:
+             w2=None, b2=None, rows_first: int = 0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
+             packed: bool = False) -> None:
     """NHWC conv + bias + ReLU with OHWI weights (conv2 / conv3).  Split mode
     (``x_lo`` ... ``out_lo``): fp32-accurate operands as hi + lo bf16 planes."""
     N, H, W, Cin = x.shape
@@ -186,7 +199,8 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
     split = x_lo is not None
     if CONV2_IMG and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
             hasattr(lib, "apex_conv2_img_fwd"):
-        conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo, out_lo=out_lo)
+        conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo, out_lo=out_lo,
+                      packed=packed)
         return
     if not _split_ok(w2, rows_first, OH * OW):   # batch not tile-aligned: one launch per weight set
         r = rows_first

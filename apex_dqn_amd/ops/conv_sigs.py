@@ -13,7 +13,7 @@ class Conv2ImgDesc(ctypes.Structure):
     """Image-resident conv2 forward (mirrors ``Conv2ImgDesc`` in csrc/conv2_img.hip)."""
     _fields_ = [("x", c_p), ("w", c_p), ("w2", c_p), ("bias", c_p), ("bias2", c_p), ("y", c_p),
                 ("N", c_i), ("img_switch", c_i), ("x_lo", c_p), ("w_lo", c_p), ("w2_lo", c_p), ("y_lo", c_p),
-                ("wfrag", c_p)]
+                ("wfrag", c_p), ("wfrag_ready", c_i)]
 
 
 class Conv2DgradImgDesc(ctypes.Structure):

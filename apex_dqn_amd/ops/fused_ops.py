@@ -55,10 +55,11 @@ class TorchBackend:
         split_into(R.conv1_fwd(frames, w, b, scale, dt), out, out_lo)
 
     def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0, w32=None,
-                       w2_32=None, out_lo=None):
+                       w2_32=None, out_lo=None, c2f=None):
         """conv1 on frame stacks addressed by replay-ring slots (N, C); rows >=
         ``rows_first`` use the second weight set (w2, b2) when given.  Split mode reads
-        the fp32 master weights ``w32`` / ``w2_32``."""
+        the fp32 master weights ``w32`` / ``w2_32``.  ``c2f``: conv2 weights the HIP
+        backend pre-packs inside this launch (ignored here)."""
         from ..replay.gpu_replay import from_s2d
         frames = frames_buf[:slots.shape[0]]
         n, c = slots.shape
@@ -271,19 +272,26 @@ class HipBackend(TorchBackend):
 
     # --------------------------------------------------- native conv family
     def conv1_fwd_ring(self, ring, slots, frames_buf, w, b, scale, out, w2=None, b2=None, rows_first=0, w32=None,
-                       w2_32=None, out_lo=None):
+                       w2_32=None, out_lo=None, c2f=None):
         if not self.native_conv:
             return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out, w2, b2, rows_first, w32, w2_32,
                                           out_lo)
+        c2f = c2f if (c2f is not None and out_lo is not None and C.C2F_PACK) else None
         C.conv1_s2d_fwd(self.lib, self.ws, ring, slots, w, b, scale, out, w2, b2, rows_first, w32=w32, w2_32=w2_32,
-                        out_lo=out_lo)
+                        out_lo=out_lo, c2f=c2f)
+        if c2f is not None:   # this step's split conv2 forward finds its weights packed
+            self._c2f_packed = tuple(_lib.ptr(t) for t in c2f)
 
     def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
                  out_lo=None):
         if not self.native_conv:
             return super().conv_fwd(x, w, b, stride, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
+        key = (_lib.ptr(w), _lib.ptr(w_lo), _lib.ptr(w2), _lib.ptr(w2_lo))
+        packed = stride == 2 and x_lo is not None and getattr(self, "_c2f_packed", None) == key
+        if packed:
+            self._c2f_packed = None
         C.conv_fwd(self.lib, x, w, b, stride, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo,
-                   out_lo=out_lo)
+                   out_lo=out_lo, packed=packed)
 
     def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
                c2d=None):

@@ -374,3 +374,35 @@ def test_conv2_image_resident_split_kernels_vs_generic(monkeypatch, grid):
     g1h, g1l = _empty2(N, 20, 20, 64)
     C.conv2_dgrad(lib, dh, wah, y1, g1h, dy_lo=dl, w_lo=wal, out_lo=g1l)
     assert _rel(_join(h1, l1), _join(g1h, g1l)) < TOL
+
+
+@pytest.mark.parametrize("grid_images", [64, 600])
+def test_conv2_fwd_weights_packed_in_conv1_launch(grid_images):
+    """The split conv2 forward's weight-fragment pack that rides on the conv1 launch
+    (csrc/conv2_wfrag.h c2f_pack_range; fewer and more conv1 workgroups than fragment
+    blocks) gives bit-identical conv2 outputs to the conv2 launcher's own pack."""
+    from apex_dqn_amd.ops import conv as C
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    g = torch.Generator(device="cpu").manual_seed(21)
+    raw = torch.randint(0, 256, (60, 84, 84), generator=g, dtype=torch.uint8).to(DEV)
+    ring = to_s2d(raw)
+    N = grid_images
+    slots = torch.randint(0, 60, (N, 4), generator=g, dtype=torch.int32).to(DEV)
+    w1 = (torch.randn(64, 4, 8, 8, generator=g) * 0.05).to(DEV)
+    b1 = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    y1, y1l = _empty2(N, 20, 20, 64)
+    (wh, wl), (w2h, w2l) = _split((torch.randn(64, 4, 4, 64, generator=g) * 0.03).to(DEV)), \
+        _split((torch.randn(64, 4, 4, 64, generator=g) * 0.03).to(DEV))
+    b2a, b2b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    sw = 2 * N // 3
+    outs = [_empty2(N, 9, 9, 64) for _ in range(2)]
+    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, w1.to(torch.bfloat16), b1, 1 / 255.0, y1, w32=w1,
+                    out_lo=y1l)
+    C.conv2_img_fwd(_lib(), y1, wh, b2a, outs[0][0], w2h, b2b, sw, x_lo=y1l, w_lo=wl, w2_lo=w2l, out_lo=outs[0][1])
+    C.c2f_wfrag_fwd_buffer(DEV).fill_(3.0)    # stale contents: the conv1 launch must overwrite them
+    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, w1.to(torch.bfloat16), b1, 1 / 255.0, y1, w32=w1,
+                    out_lo=y1l, c2f=(wh, wl, w2h, w2l))
+    C.conv2_img_fwd(_lib(), y1, wh, b2a, outs[1][0], w2h, b2b, sw, x_lo=y1l, w_lo=wl, w2_lo=w2l,
+                    out_lo=outs[1][1], packed=True)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
