@@ -160,6 +160,7 @@ class FusedNatureLearner:
         # gloo (CPU tests, one-GPU rehearsals) cannot be captured: eager DP steps
         self._dp_graphs = self._dp and cuda and self._backend_name() == "nccl"
         self._ordered_coll = self._dp and cuda and (self.coll.name == "native" or self._backend_name() == "nccl")
+        self._fork_stream = torch.cuda.Stream(self.device) if (self._dp and cuda) else None
         # next-batch pre-sampling: the batch of step t+1 is drawn at the end of step t,
         # after the priority write-back -- on the HIP backend inside the optimizer launch
         # (its first blocks run the sampler: csrc/sumtree.hip rmsprop_sample_kernel), so
@@ -295,14 +296,17 @@ class FusedNatureLearner:
         self.replay.sample(self.B, out=self.S, nxt2=self.slots[2 * self.B:])
         self._sample_ver = self.replay.version
 
-    def _seg2(self) -> None:
+    def _seg2(self, after_first=None) -> None:
         """fc dgrad + conv backward (with DP, all of it overlaps the fc/heads bucket
-        all-reduce): the dgrad chain, conv3/conv2 wgrad, conv1 wgrad last."""
+        all-reduce): the dgrad chain, conv3/conv2 wgrad, conv1 wgrad last.
+        ``after_first``: called once the first kernel (fc dgrad) is enqueued."""
         B, rt, ops, G, Pb, Pl = self.B, self.rt, self.ops, self.G, self.Pb, self.Pl
         sp = self.split
         jobs = []    # split-K reductions, finalised in ONE launch at the end
         ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
                      **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
+        if after_first is not None:
+            after_first()
         ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"], jobs=jobs,
                        **self._lo(dy_lo=self.dY3_lo, x_lo=sp and self.y2_lo[:B]))
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2,
@@ -385,9 +389,32 @@ class FusedNatureLearner:
         conv bucket follows; the optimizer waits for all three."""
         cut = self.layout.offsets["wfc"]
         self._seg1()
-        w_fc = self.coll.all_reduce(self.gcomm[cut:])
-        w_r = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
-        self._seg2()     # conv backward overlaps the fc/head bucket all-reduce
+        works = []
+        on_cuda = self.device.type == "cuda"
+        fork = None
+        if on_cuda:
+            fork = torch.cuda.Event()
+            fork.record()
+
+        def issue_fc_bucket():
+            # The fc/head bucket and the shard statistics leave from a side stream that
+            # waits on the fork event recorded after segment 1, and are enqueued only after
+            # the compute stream's next kernel: in the captured graph the compute child of
+            # the fork comes first, so the executor keeps the backward chain on the step's
+            # hardware queue (comm captured first moved the chain to a second queue: a
+            # 6-10 us gap at each switch, profiles/r2_step_timeline_fp32_forced_dp_fc128.txt)
+            if on_cuda:
+                side = self._fork_stream
+                side.wait_event(fork)
+                with torch.cuda.stream(side):
+                    works.append(self.coll.all_reduce(self.gcomm[cut:]))
+                    works.append(self.replay.gather_shard_stats(async_op=True, coll=self.coll))
+            else:
+                works.append(self.coll.all_reduce(self.gcomm[cut:]))
+                works.append(self.replay.gather_shard_stats(async_op=True, coll=self.coll))
+
+        self._seg2(after_first=issue_fc_bucket)     # conv backward overlaps the fc/head bucket all-reduce
+        w_fc, w_r = works
         w_cv = self.coll.all_reduce(self.gcomm[:cut])
         if self._ordered_coll:
             # RCCL runs a communicator's collectives in issue order on one stream: the
@@ -397,6 +424,8 @@ class FusedNatureLearner:
             w_fc.wait()
             w_r.wait()
             w_cv.wait()
+            if on_cuda:   # gloo on device tensors: the results are ordered on the side stream
+                torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
         self._mark("allreduce_wait")
         self._seg3()
 
