@@ -19,9 +19,13 @@ learner/fused_learner.py).  The JSON's ``value`` is that fp32 number; unless
 it as ``value_bf16``.
 
 Timing: ``--warmup`` untimed updates, then every HIP graph the timed region
-replays is captured (``learner.prepare_graphs``: state-preserving, no updates),
-then EXACTLY ``--steps`` updates between barrier + synchronize brackets; the
-max over ranks is reported.  ``graph_captures_in_timed`` must be 0.
+replays is captured (``learner.prepare_graphs``: state-preserving, no updates) and
+replayed ``--prep-warm`` times from a snapshot that is then restored
+(``learner.rewarm``: no update is kept; without it a 20-step window after a 5-step
+warm-up read 1.5-2 % below a 400-step window, with it they agree within 0.5 %:
+``scripts/warm_ab.sh``, ``profiles/r2_prep_warm_ab.txt``), then EXACTLY ``--steps``
+updates between barrier + synchronize brackets; the max over ranks is reported.
+``graph_captures_in_timed`` must be 0.
 
 ``value`` = whole-job batch-512 gradient steps per second
           = N x (data-parallel steps/s)  (each DP step consumes N x 512 samples).
@@ -90,7 +94,7 @@ def make_learner(args, dtype, device, comm, rank, replay):
     return cfg, FusedImpalaLearner(cfg, device, replay, comm=comm, backend=args.backend)
 
 
-def measure(cfg, learner, replay, comm, warmup: int, steps: int) -> dict:
+def measure(cfg, learner, replay, comm, warmup: int, steps: int, prep_warm: int = 0) -> dict:
     L = cfg.Learner
 
     def run(n):
@@ -114,6 +118,8 @@ def measure(cfg, learner, replay, comm, warmup: int, steps: int) -> dict:
     run(warmup)
     # every graph the timed region replays, captured now (no learner updates)
     caps = learner.prepare_graphs() if hasattr(learner, "prepare_graphs") else 0
+    if hasattr(learner, "rewarm"):
+        learner.rewarm(prep_warm)     # state-preserving: no update is kept
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -126,6 +132,7 @@ def measure(cfg, learner, replay, comm, warmup: int, steps: int) -> dict:
     dt = comm.allreduce_scalar(dt, "max") if comm.active else dt
     caps_after = getattr(learner, "graph_captures", 0)
     return dict(dt=dt, prep_graph_captures=int(caps), graph_captures_in_timed=int(caps_after - caps),
+                prep_warm_replays=int(prep_warm) if hasattr(learner, "rewarm") else 0,
                 metrics=learner.last_metrics())
 
 
@@ -165,6 +172,9 @@ def main():
                     help="learner updates per HIP-graph launch (Runtime.graph_steps; 1 = one graph per update)")
     ap.add_argument("--graph-impala", action="store_true",
                     help="IMPALA on the torch-autograd graph learner (MIOpen) instead of the HIP kernels")
+    ap.add_argument("--prep-warm", type=int, default=4,
+                    help="untimed, state-preserving replays of the multi-step graph right before the timed "
+                         "window (learner.rewarm: no update is kept; reported as prep_warm_replays)")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
                     help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala.hip")
     args = ap.parse_args()
@@ -185,13 +195,13 @@ def main():
 
     replay = make_replay(args, device, rank)
     cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay)
-    res = measure(cfg, learner, replay, comm, args.warmup, args.steps)
+    res = measure(cfg, learner, replay, comm, args.warmup, args.steps, args.prep_warm)
     extra = None
     if not args.no_bf16_extra and args.dtype == "fp32":
         del learner
         torch.cuda.empty_cache()
         cfg_b, learner_b = make_learner(args, "bf16", device, comm, rank, replay)
-        extra = measure(cfg_b, learner_b, replay, comm, args.warmup, args.steps)
+        extra = measure(cfg_b, learner_b, replay, comm, args.warmup, args.steps, args.prep_warm)
         learner = learner_b
     dt = res["dt"]
     ms = 1e3 * dt / args.steps
@@ -224,6 +234,7 @@ def main():
                       "bf16 operands, fp32 accumulation / master weights / optimizer")),
             "prep_graph_captures": res["prep_graph_captures"],
             "graph_captures_in_timed": res["graph_captures_in_timed"],
+            "prep_warm_replays": res["prep_warm_replays"],
             "loss": round(m["loss"], 5), "grad_norm": round(m["grad_norm"], 5),
         }
         if extra is not None:
