@@ -350,3 +350,27 @@ def test_native_rccl_communicator_world1():
     assert out["version"] > 0 and out["x_ok"]
     assert out["gather"] == [1.5, 2.5, 3.5, 4.5] and out["bcast"] == out["bmax"] == 3.0
     assert out["y"] == 7.0          # (1*2+1)*2+1: two replays of mul / all-reduce / add
+
+
+def test_rewarm_preserves_state():
+    """learner.rewarm (bench.py's untimed warm replays before the timed window) keeps no
+    update: after it the next updates equal those of a learner that never rewarmed."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 128},
+                                "Runtime": {"use_graphs": True, "graph_steps": 4}})
+    outs = []
+    for warm in (0, 3):
+        torch.manual_seed(0)
+        rp = _filled_replay(seed=7)
+        L = FusedNatureLearner(cfg, DEV, rp)
+        L.steps(5)
+        if warm:
+            L.rewarm(warm)
+        assert L.num_q_updates == 5
+        L.steps(8)
+        torch.cuda.synchronize()
+        outs.append((L.p32.clone(), L.rms_v.clone(), rp.leaf.clone(), rp.ctr.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
