@@ -113,12 +113,18 @@ __global__ void __launch_bounds__(C2_THREADS, 1) conv2_img_fwd_kernel(Conv2ImgDe
   for (; img < d.N; img += G) {
     const int set = (d.w2 != nullptr && img >= d.img_switch) ? 1 : 0;
     if (set != cur_set) {
-      const bf16_t* W = set ? d.w2 : d.w;
-      const int co = nh * 32 + rr;
+      if (d.wfrag != nullptr) {   // packed by the step's conv1 launch (csrc/conv2_wfrag.h c2b_src_off)
+        const uint4* wf = d.wfrag + set * C2F_FRAGS + wv * 16 * 64 + lane;
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int kw = s >> 2, ci0 = ((s & 3) << 4) + kg * 8;
-        bfr[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(W + ((co * 4 + kq) * 4 + kw) * 64 + ci0));
+        for (int s = 0; s < 16; ++s) bfr[s] = __builtin_bit_cast(bf16x8, wf[s * 64]);
+      } else {
+        const bf16_t* W = set ? d.w2 : d.w;
+        const int co = nh * 32 + rr;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int kw = s >> 2, ci0 = ((s & 3) << 4) + kg * 8;
+          bfr[s] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(W + ((co * 4 + kq) * 4 + kw) * 64 + ci0));
+        }
       }
       cur_set = set;
     }
@@ -385,10 +391,12 @@ APEX_EXPORT int apex_conv2_img_fwd(Conv2ImgDesc d, int grid, hipStream_t st) {
   }
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
+  if (!split && d.wfrag != nullptr && (!d.wfrag_ready || ((uintptr_t)d.wfrag & 15)))
+    return (int)hipErrorInvalidValue;   // bf16: fragments come pre-packed (conv1 launch) only
   if (split && d.wfrag != nullptr) {
     if ((uintptr_t)d.wfrag & 15) return (int)hipErrorInvalidValue;
     if (!d.wfrag_ready)
-      pack_c2f_wfrag_kernel<<<4 * C2F_FRAGS / 256, 256, 0, st>>>(C2fPack{{d.w, d.w_lo, d.w2, d.w2_lo}, d.wfrag});
+      pack_c2f_wfrag_kernel<<<4 * C2F_FRAGS / 256, 256, 0, st>>>(C2fPack{{d.w, d.w_lo, d.w2, d.w2_lo}, d.wfrag, 0});
   }
   if (split) conv2_img_fwd_split_kernel<<<G, C2S_THREADS, 0, st>>>(d);
   else conv2_img_fwd_kernel<<<G, C2_THREADS, 0, st>>>(d);

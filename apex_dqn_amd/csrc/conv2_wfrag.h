@@ -44,12 +44,28 @@ __device__ __forceinline__ int c2f_src_off(int t) {
   const int co = nh * 32 + rr, kh = 2 * kp + (s >> 4), kw = (s >> 2) & 3, ci0 = ((s & 3) << 4) + kg * 8;
   return ((co * 4 + kh) * 4 + kw) * 64 + ci0;
 }
+// bf16 forward (conv2_img_fwd_kernel, 8 waves): fragment t = (wave (nh, kq), K step s <
+// 16, lane) holds w[co = nh*32 + (lane & 31)][kh = kq][kw = s >> 2][ci0 ..]; planes: set 0, set 1
+__device__ __forceinline__ int c2b_src_off(int t) {
+  const int lane = t & 63, s = (t >> 6) & 15, wv = t >> 10;
+  const int nh = wv & 1, kq = wv >> 1, rr = lane & 31, kg = lane >> 5;
+  const int co = nh * 32 + rr, kw = s >> 2, ci0 = ((s & 3) << 4) + kg * 8;
+  return ((co * 4 + kq) * 4 + kw) * 64 + ci0;
+}
 struct C2fPack {
   const bf16_t* src[4];   // set 0 hi, lo, set 1 hi, lo (null planes are skipped)
   uint4* out;             // 4 * C2F_FRAGS, or null: no pack
+  int bf16;               // bf16 forward layout: two planes (set 0, set 1 = src[0], src[2])
 };
 __device__ __forceinline__ void c2f_pack_range(const C2fPack& p, int i0, int stride) {
   for (int i = i0; i < 4 * C2F_FRAGS; i += stride) {
+    if (p.bf16) {
+      if (i >= 2 * C2F_FRAGS) break;
+      const int q = i / C2F_FRAGS;
+      const bf16_t* src = p.src[2 * q];
+      if (src != nullptr) p.out[i] = *reinterpret_cast<const uint4*>(src + c2b_src_off(i - q * C2F_FRAGS));
+      continue;
+    }
     const int q = i / C2F_FRAGS;
     const bf16_t* src = p.src[q];
     if (src != nullptr) p.out[i] = *reinterpret_cast<const uint4*>(src + c2f_src_off(i - q * C2F_FRAGS));

@@ -234,9 +234,11 @@ class FusedNatureLearner:
         Pb, P, Tb, T, Pl, Tl = self.Pb, self.P, self.Tb, self.T, self.Pl, self.Tl
         sp = self.split
         n = 3 * B
+        # c2f: conv2's weights packed for its forward in the same launch (csrc/conv2_wfrag.h)
+        c2f = (Pb["w2"], Pl["w2"], Tb["w2"], Tl["w2"]) if sp else (Pb["w2"], None, Tb["w2"], None)
         ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
-                           Tb["w1"], T["b1"], 2 * B, **self._lo(w32=P["w1"], w2_32=T["w1"], out_lo=self.y1_lo,
-                                                                c2f=sp and (Pb["w2"], Pl["w2"], Tb["w2"], Tl["w2"])))
+                           Tb["w1"], T["b1"], 2 * B, c2f=c2f,
+                           **self._lo(w32=P["w1"], w2_32=T["w1"], out_lo=self.y1_lo))
         ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B,
                      **self._lo(x_lo=self.y1_lo, w_lo=sp and Pl["w2"], w2_lo=sp and Tl["w2"], out_lo=self.y2_lo))
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,

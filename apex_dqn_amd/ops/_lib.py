@@ -94,7 +94,7 @@ class Conv1S2DDesc(ctypes.Structure):
     _fields_ = [("ring", c_p), ("slots", c_p), ("w", c_p), ("w2", c_p), ("bias", c_p), ("bias2", c_p),
                 ("y", c_p), ("zero16", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("m_switch", c_i),
                 ("in_scale", c_f), ("probe", c_p), ("w32", c_p), ("w2_32", c_p), ("y_lo", c_p),
-                ("c2f_src", c_p * 4), ("c2f_out", c_p)]
+                ("c2f_src", c_p * 4), ("c2f_out", c_p), ("c2f_bf16", c_i)]
 
 
 _SIGS = {

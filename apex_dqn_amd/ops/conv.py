@@ -142,6 +142,7 @@ def conv1_s2d_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor,
         for i, t in enumerate(c2f):
             d.c2f_src[i] = _lib.ptr(t)
         d.c2f_out = c2f_wfrag_fwd_buffer(ring.device).data_ptr()
+        d.c2f_bf16 = int(out_lo is None)     # bf16 forward layout: (w2, None, target w2, None)
     _lib.check(lib.apex_conv1_s2d_fwd(d, int(grid), _lib.stream_ptr()), "conv1_s2d_fwd")
 
 
@@ -185,6 +186,9 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
         if C2F_PACK or packed:
             d.wfrag = c2f_wfrag_fwd_buffer(x.device).data_ptr()
             d.wfrag_ready = int(packed)
+    elif packed:   # bf16: fragments packed by this step's conv1 launch
+        d.wfrag = c2f_wfrag_fwd_buffer(x.device).data_ptr()
+        d.wfrag_ready = 1
     _lib.check(lib.apex_conv2_img_fwd(d, int(grid), _lib.stream_ptr()), "conv2_img_fwd")
 
 

@@ -276,7 +276,7 @@ class HipBackend(TorchBackend):
         if not self.native_conv:
             return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out, w2, b2, rows_first, w32, w2_32,
                                           out_lo)
-        c2f = c2f if (c2f is not None and out_lo is not None and C.C2F_PACK) else None
+        c2f = c2f if (c2f is not None and C.C2F_PACK) else None
         C.conv1_s2d_fwd(self.lib, self.ws, ring, slots, w, b, scale, out, w2, b2, rows_first, w32=w32, w2_32=w2_32,
                         out_lo=out_lo, c2f=c2f)
         if c2f is not None:   # this step's split conv2 forward finds its weights packed
@@ -287,7 +287,7 @@ class HipBackend(TorchBackend):
         if not self.native_conv:
             return super().conv_fwd(x, w, b, stride, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
         key = (_lib.ptr(w), _lib.ptr(w_lo), _lib.ptr(w2), _lib.ptr(w2_lo))
-        packed = stride == 2 and x_lo is not None and getattr(self, "_c2f_packed", None) == key
+        packed = stride == 2 and getattr(self, "_c2f_packed", None) == key
         if packed:
             self._c2f_packed = None
         C.conv_fwd(self.lib, x, w, b, stride, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo,

@@ -376,8 +376,9 @@ def test_conv2_image_resident_split_kernels_vs_generic(monkeypatch, grid):
     assert _rel(_join(h1, l1), _join(g1h, g1l)) < TOL
 
 
+@pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("grid_images", [64, 600])
-def test_conv2_fwd_weights_packed_in_conv1_launch(grid_images):
+def test_conv2_fwd_weights_packed_in_conv1_launch(grid_images, split):
     """The split conv2 forward's weight-fragment pack that rides on the conv1 launch
     (csrc/conv2_wfrag.h c2f_pack_range; fewer and more conv1 workgroups than fragment
     blocks) gives bit-identical conv2 outputs to the conv2 launcher's own pack."""
@@ -396,13 +397,15 @@ def test_conv2_fwd_weights_packed_in_conv1_launch(grid_images):
     b2a, b2b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
     sw = 2 * N // 3
     outs = [_empty2(N, 9, 9, 64) for _ in range(2)]
-    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, w1.to(torch.bfloat16), b1, 1 / 255.0, y1, w32=w1,
-                    out_lo=y1l)
-    C.conv2_img_fwd(_lib(), y1, wh, b2a, outs[0][0], w2h, b2b, sw, x_lo=y1l, w_lo=wl, w2_lo=w2l, out_lo=outs[0][1])
+    c1lo = dict(w32=w1, out_lo=y1l) if split else {}
+    c2lo = (lambda o: dict(x_lo=y1l, w_lo=wl, w2_lo=w2l, out_lo=o)) if split else (lambda o: {})
+    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, w1.to(torch.bfloat16), b1, 1 / 255.0, y1, **c1lo)
+    C.conv2_img_fwd(_lib(), y1, wh, b2a, outs[0][0], w2h, b2b, sw, **c2lo(outs[0][1]))
     C.c2f_wfrag_fwd_buffer(DEV).fill_(3.0)    # stale contents: the conv1 launch must overwrite them
-    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, w1.to(torch.bfloat16), b1, 1 / 255.0, y1, w32=w1,
-                    out_lo=y1l, c2f=(wh, wl, w2h, w2l))
-    C.conv2_img_fwd(_lib(), y1, wh, b2a, outs[1][0], w2h, b2b, sw, x_lo=y1l, w_lo=wl, w2_lo=w2l,
-                    out_lo=outs[1][1], packed=True)
+    C.conv1_s2d_fwd(_lib(), C.Workspace(), ring, slots, w1.to(torch.bfloat16), b1, 1 / 255.0, y1,
+                    c2f=(wh, wl, w2h, w2l) if split else (wh, None, w2h, None), **c1lo)
+    C.conv2_img_fwd(_lib(), y1, wh, b2a, outs[1][0], w2h, b2b, sw, packed=True, **c2lo(outs[1][1]))
     torch.cuda.synchronize()
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][0], outs[1][0])
+    if split:
+        assert torch.equal(outs[0][1], outs[1][1])
