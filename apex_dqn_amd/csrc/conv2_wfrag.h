@@ -12,6 +12,12 @@
 // 2 KB.  Done in every workgroup that is 256 x 512 (split: 1024) such gathers per lane,
 // ~10 us of the launch; here one pass writes the fragments once per step and each
 // workgroup reads them back as coalesced 16-B loads.
+// a pack riding on another launch (fc_splitk_epilogue_kernel / ddqn_head_kernel spare blocks)
+struct C2dPackJob {
+  const bf16_t* w;
+  const bf16_t* w_lo;
+  uint32_t* out;
+};
 #define C2D_PACK_THREADS (2 * 4 * C2D_FRAGS)   // one per 4-byte word of both planes
 __device__ __forceinline__ void pack_c2d_wfrag_word(int i, const bf16_t* __restrict__ w,
                                                    const bf16_t* __restrict__ w_lo, uint32_t* __restrict__ out) {

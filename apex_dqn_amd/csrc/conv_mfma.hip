@@ -768,11 +768,6 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
 // Side job (pk.out != null): blocks past the epilogue's grid pack the conv2 weights
 // for the step's conv2 data gradient (csrc/conv2_wfrag.h) -- a launch of its own costs
 // ~5 us in the step's graph; here it rides on an elementwise pass.
-struct C2dPackJob {
-  const bf16_t* w;
-  const bf16_t* w_lo;
-  uint32_t* out;
-};
 
 template <bool SPLIT>
 __global__ void __launch_bounds__(256) fc_splitk_epilogue_kernel(ConvDesc d, const float* __restrict__ ws,
@@ -978,8 +973,9 @@ static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
 // (fc_gemm128_kernel + fc_splitk_epilogue_kernel).  ws: fp32 workspace of at least
 // ksplit * M * N elements.  Row-major B only (d.bt == 0), N % 128 == 0.  pk: optional
 // conv2 weight-fragment pack riding on the epilogue launch (fc_splitk_epilogue_kernel).
+// no_epilogue: only the GEMM runs; the caller consumes the ws partials.
 APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksplit, int loader_waves,
-                                C2dPackJob pk, hipStream_t st) {
+                                int no_epilogue, C2dPackJob pk, hipStream_t st) {
   if (d.mode != 0 || d.bt != 0 || (d.K & 63) || d.K <= 0 || (d.Cout & 127) || d.N <= 0 || ksplit < 1)
     return (int)hipErrorInvalidValue;
   if ((d.ldy & 7) || d.ldy < d.Cout) return (int)hipErrorInvalidValue;
@@ -1003,6 +999,12 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   }
   const int64_t nthr = (int64_t)d.N * d.Cout / 8;
   const int eb = (int)((nthr + 255) / 256);
+  // no_epilogue: the partials stay in ws for the consumer (csrc/head_common.h
+  // load_row_part: the DDQN head sums them itself)
+  if (no_epilogue) {
+    if (pk.out != nullptr) return (int)hipErrorInvalidValue;
+    APEX_CHECK_LAUNCH();
+  }
   if (pk.out != nullptr && (pk.w == nullptr || ((uintptr_t)pk.out & 15))) return (int)hipErrorInvalidValue;
   const int pb = pk.out != nullptr ? C2D_PACK_THREADS / 256 : 0;
   if (split) fc_splitk_epilogue_kernel<true><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk);

@@ -20,17 +20,27 @@
 // Outputs: td_abs[B], loss[B], q_t[B,A] (optional), dH[B,1024] bf16 (gradient
 // at the pre-ReLU stream outputs), dhead[B,1+A] fp32 (d value, d advantage).
 #include "head_common.h"
+#include "conv2_wfrag.h"
 
+// hp.part != null: the fc forward's split-K epilogue runs inside (head_common.h
+// load_row_part); blocks >= B run the conv2 weight-fragment pack job (pk.out != null)
+// that otherwise rides on that epilogue's launch.
 template <int HS>
 __global__ void __launch_bounds__(192) ddqn_head_kernel(
     const bf16_t* __restrict__ Hon, const bf16_t* __restrict__ Htg, HeadParams Pon, HeadParams Ptg,
     const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
-    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, HeadLo lo) {
+    bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, HeadLo lo,
+    HeadPart hp, C2dPackJob pk) {
+  if ((int)blockIdx.x >= B) {
+    for (int i = ((int)blockIdx.x - B) * 192 + (int)threadIdx.x; i < C2D_PACK_THREADS; i += ((int)gridDim.x - B) * 192)
+      pack_c2d_wfrag_word(i, pk.w, pk.w_lo, pk.out);
+    return;
+  }
   float ad;
   (void)ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs, loss,
-                           q_out, dH, dhead, zero_ptr, zero_n, &ad, lo);
+                           q_out, dH, dhead, zero_ptr, zero_n, &ad, lo, hp);
 }
 
 __global__ void __launch_bounds__(512) head_wgrad_kernel(HeadWgArgs h) { head_wgrad_body(h, blockIdx.x, blockIdx.y); }
@@ -39,15 +49,24 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
                                const int32_t* act, const float* rew, const float* gam, const float* isw,
                                int B, int A, int huber, float kappa, float grad_scale, float* td_abs,
                                float* loss, float* q_out, bf16_t* dH, float* dhead, float* zero_ptr,
-                               int zero_n, int hidden, HeadLo lo, hipStream_t st) {
+                               int zero_n, int hidden, HeadLo lo, HeadPart hp, C2dPackJob pk, hipStream_t st) {
   if (A < 1 || A > HEAD_MAXA || B < 1) return (int)hipErrorInvalidValue;
   if (lo.Hon != nullptr && (lo.Htg == nullptr || lo.dH == nullptr)) return (int)hipErrorInvalidValue;
+  if (hp.part != nullptr) {   // split-K partials [nz][3B][2 hidden]; rows [0, B) of h written to hp.hon
+    if (hp.nz < 1 || hp.hon == nullptr || hp.bias_on == nullptr || hp.bias_tg == nullptr || hp.two_b != 2 * B ||
+        (lo.Hon != nullptr) != (hp.hon_lo != nullptr) || (((uintptr_t)hp.part | (uintptr_t)hp.hon) & 15))
+      return (int)hipErrorInvalidValue;
+  }
+  if (pk.out != nullptr && (pk.w == nullptr || ((uintptr_t)pk.out & 15))) return (int)hipErrorInvalidValue;
+  const int grid = B + (pk.out != nullptr ? 128 : 0);
   if (hidden == 512)
-    ddqn_head_kernel<512><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale,
-                                             td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo);
+    ddqn_head_kernel<512><<<grid, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
+                                                grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo,
+                                                hp, pk);
   else if (hidden == 256)
-    ddqn_head_kernel<256><<<B, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale,
-                                             td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo);
+    ddqn_head_kernel<256><<<grid, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
+                                                grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo,
+                                                hp, pk);
   else
     return (int)hipErrorInvalidValue;
   APEX_CHECK_LAUNCH();

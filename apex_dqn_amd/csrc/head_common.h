@@ -66,6 +66,10 @@ __device__ __forceinline__ void load_row_streams(const bf16_t* __restrict__ row,
 // q-values of one row; `row_lo` (split mode, else null) adds the lo plane: the
 // activations are then fp32-accurate (hi + lo)
 template <int HS>
+__device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, float* q, const float* hv,
+                                       const float* ha);
+
+template <int HS>
 __device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const bf16_t* __restrict__ row_lo,
                                          const HeadParams& P, int A, int lane, float* q, float* hv, float* ha) {
   constexpr int NPL = HS / 64;
@@ -79,6 +83,86 @@ __device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const b
       ha[k] += la[k];
     }
   }
+  head_q<HS>(P, A, lane, q, hv, ha);
+}
+
+// The fc forward's split-K epilogue fused into the head (csrc/conv_mfma.hip
+// fc_gemm128_kernel leaves fp32 partials [nz][3B][2 HS]): a wave builds its row from
+// the partials exactly as fc_splitk_epilogue_kernel would (z-ordered sum, + bias,
+// ReLU, bf16 or hi / lo rounding) and uses the rounded values, so the step is
+// bit-identical to the two-launch path; wave 0 stores its S_t row for the head
+// weight gradient.  Saves the epilogue launch and its 19 MB pass over h.
+struct HeadPart {
+  const float* part;      // null: the head reads h (Hon / Htg) as usual
+  int64_t zstride;        // floats between partial planes
+  int nz;
+  const float* bias_on;   // fc bias of rows < two_b (online), of rows >= two_b (target)
+  const float* bias_tg;
+  int two_b;
+  bf16_t* hon;            // rows [0, B) of h written back (hi plane / bf16)
+  bf16_t* hon_lo;         // split mode: lo plane (else null)
+};
+
+template <int HS>
+__device__ __forceinline__ void load_row_part(const HeadPart& hp, int row, int lane, float* hv, float* ha,
+                                              bool store) {
+  constexpr int NPL = HS / 64, ROW = 2 * HS;
+  const bool split = hp.hon_lo != nullptr;
+  const float* __restrict__ bias = row < hp.two_b ? hp.bias_on : hp.bias_tg;
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {       // value stream, advantage stream
+    const int c0 = st * HS + lane * NPL;
+    float v[NPL];
+    const float* p0 = hp.part + (int64_t)row * ROW + c0;
+#pragma unroll
+    for (int k = 0; k < NPL; k += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p0 + k);
+      v[k] = a.x; v[k + 1] = a.y; v[k + 2] = a.z; v[k + 3] = a.w;
+    }
+    for (int z = 1; z < hp.nz; ++z) {
+#pragma unroll
+      for (int k = 0; k < NPL; k += 4) {
+        const float4 a = *reinterpret_cast<const float4*>(p0 + z * hp.zstride + k);
+        v[k] += a.x; v[k + 1] += a.y; v[k + 2] += a.z; v[k + 3] += a.w;
+      }
+    }
+    uint32_t hh[NPL / 2], ll[NPL / 2];
+#pragma unroll
+    for (int k = 0; k < NPL; k += 4) {
+      const float4 b = *reinterpret_cast<const float4*>(bias + c0 + k);
+      v[k] = v[k] * 1.0f + b.x; v[k + 1] = v[k + 1] * 1.0f + b.y;
+      v[k + 2] = v[k + 2] * 1.0f + b.z; v[k + 3] = v[k + 3] * 1.0f + b.w;
+    }
+#pragma unroll
+    for (int k = 0; k < NPL / 2; ++k) {
+      // fc_splitk_epilogue_kernel: ReLU in fp32, then the (hi / lo) bf16 rounding
+      if (split) {
+        split_pk_bf16_h(fmaxf(v[2 * k], 0.f), fmaxf(v[2 * k + 1], 0.f), hh[k], ll[k]);
+      } else {
+        hh[k] = pack_bf16x2(fmaxf(v[2 * k], 0.f), fmaxf(v[2 * k + 1], 0.f));
+        ll[k] = 0;
+      }
+    }
+    float* out = st ? ha : hv;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) out[k] = bf16_at(hh, k) + (split ? bf16_at(ll, k) : 0.f);
+    if (store) {
+      bf16_t* o = hp.hon + (int64_t)row * ROW + c0;
+      if constexpr (NPL == 8) {
+        *reinterpret_cast<uint4*>(o) = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+        if (split) *reinterpret_cast<uint4*>(hp.hon_lo + (int64_t)row * ROW + c0) = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+      } else {
+        *reinterpret_cast<uint2*>(o) = make_uint2(hh[0], hh[1]);
+        if (split) *reinterpret_cast<uint2*>(hp.hon_lo + (int64_t)row * ROW + c0) = make_uint2(ll[0], ll[1]);
+      }
+    }
+  }
+}
+
+template <int HS>
+__device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, float* q, const float* hv,
+                                       const float* ha) {
+  constexpr int NPL = HS / 64;
   float part[HEAD_MAXA + 1];
   {
     float w[NPL], s = 0.f;
@@ -124,23 +208,32 @@ __device__ __forceinline__ bool ddqn_head_body(
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
     bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n,
-    float* ad_out, HeadLo lo) {
+    float* ad_out, HeadLo lo, const HeadPart& hp) {
   __shared__ float qs[2][HEAD_MAXA];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.x;
   // zero the head-gradient region that head_wgrad accumulates into (stream-ordered)
-  if (zero_ptr != nullptr) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += gridDim.x * blockDim.x) zero_ptr[i] = 0.f;
+  if (zero_ptr != nullptr) {   // B blocks (a launch may carry extra side-job blocks)
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += B * blockDim.x) zero_ptr[i] = 0.f;
   }
   constexpr int NPL = HS / 64, ROW = 2 * HS;
   float q_t[HEAD_MAXA], q_n[HEAD_MAXA], q_g[HEAD_MAXA];
   float hv_t[NPL], ha_t[NPL];
   const bool split = lo.Hon != nullptr;
   if (wv == 0) {
-    head_row<HS>(Hon + (int64_t)b * ROW, split ? lo.Hon + (int64_t)b * ROW : nullptr, Pon, A, lane, q_t, hv_t, ha_t);
+    if (hp.part != nullptr) {
+      load_row_part<HS>(hp, b, lane, hv_t, ha_t, true);
+      head_q<HS>(Pon, A, lane, q_t, hv_t, ha_t);
+    } else {
+      head_row<HS>(Hon + (int64_t)b * ROW, split ? lo.Hon + (int64_t)b * ROW : nullptr, Pon, A, lane, q_t, hv_t,
+                   ha_t);
+    }
   } else {
     float hv_x[NPL], ha_x[NPL], q[HEAD_MAXA];
-    if (wv == 1)
+    if (hp.part != nullptr) {
+      load_row_part<HS>(hp, wv == 1 ? B + b : hp.two_b + b, lane, hv_x, ha_x, false);
+      head_q<HS>(wv == 1 ? Pon : Ptg, A, lane, q, hv_x, ha_x);
+    } else if (wv == 1)
       head_row<HS>(Hon + (int64_t)(B + b) * ROW, split ? lo.Hon + (int64_t)(B + b) * ROW : nullptr, Pon, A, lane, q,
                    hv_x, ha_x);
     else

@@ -36,6 +36,8 @@ The step is captured once and replayed as a HIP graph (``use_graphs``).
 """
 from __future__ import annotations
 
+import os
+
 from typing import Any, Dict, Optional
 
 import torch
@@ -161,6 +163,9 @@ class FusedNatureLearner:
         self._dp_graphs = self._dp and cuda and self._backend_name() == "nccl"
         self._ordered_coll = self._dp and cuda and (self.coll.name == "native" or self._backend_name() == "nccl")
         self._fork_stream = torch.cuda.Stream(self.device) if (self._dp and cuda) else None
+        # the fc layer's split-K epilogue runs inside the head launch (ops.fc_fwd defer_head;
+        # APEX_FC_EPI_IN_HEAD=0 keeps the separate epilogue launch, the A/B of scripts/ab.sh)
+        self._defer_fc_epilogue = os.environ.get("APEX_FC_EPI_IN_HEAD", "1") != "0"
         # next-batch pre-sampling: the batch of step t+1 is drawn at the end of step t,
         # after the priority write-back -- on the HIP backend inside the optimizer launch
         # (its first blocks run the sampler: csrc/sumtree.hip rmsprop_sample_kernel), so
@@ -227,9 +232,11 @@ class FusedNatureLearner:
         return kw if self.split else {}
 
     # ------------------------------------------------------------ forward
-    def forward_all(self) -> None:
+    def forward_all(self, defer_head: bool = False) -> None:
         """Online net on rows [0,2B), target net on rows [2B,3B): one launch per layer.
-        bf16 weights (Pb / Tb, + Pl / Tl lo planes in split mode), fp32 biases (P / T)."""
+        bf16 weights (Pb / Tb, + Pl / Tl lo planes in split mode), fp32 biases (P / T).
+        ``defer_head``: the fc layer's split-K epilogue may be left to the step's head
+        launch (which then writes h rows [0, B) only)."""
         ops, rt, B = self.ops, self.rt, self.B
         Pb, P, Tb, T, Pl, Tl = self.Pb, self.P, self.Tb, self.T, self.Pl, self.Tl
         sp = self.split
@@ -244,7 +251,7 @@ class FusedNatureLearner:
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
                      **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
         ops.fc_fwd(self.y3.reshape(n, 3136), Pb["wfc"], P["bfc"], self.h, Tb["wfc"], T["bfc"], 2 * B,
-                   c2d=(Pb["w2"], Pl["w2"] if sp else None),
+                   c2d=(Pb["w2"], Pl["w2"] if sp else None), defer_head=defer_head,
                    **self._lo(x_lo=sp and self.y3_lo.reshape(n, 3136), w_lo=sp and Pl["wfc"],
                               w2_lo=sp and Tl["wfc"], out_lo=self.h_lo))
 
@@ -270,7 +277,7 @@ class FusedNatureLearner:
         S = self.S
         self._mark("sample")
         # conv1 reads the uint8 frame stacks straight from the replay ring by slot
-        self.forward_all()
+        self.forward_all(defer_head=self._defer_fc_epilogue)
         self._mark("forward")
         isw = S["weights"] if self._isw else None
         sp = self.split

@@ -46,6 +46,17 @@ class HeadLo(ctypes.Structure):
     _fields_ = [("Hon", c_p), ("Htg", c_p), ("dH", c_p)]
 
 
+class HeadPart(ctypes.Structure):
+    """fc split-K partials consumed by the DDQN head (mirrors ``HeadPart``, csrc/head_common.h)."""
+    _fields_ = [("part", c_p), ("zstride", c_i64), ("nz", c_i), ("bias_on", c_p), ("bias_tg", c_p),
+                ("two_b", c_i), ("hon", c_p), ("hon_lo", c_p)]
+
+
+class C2dPack(ctypes.Structure):
+    """conv2 weight-fragment pack job riding on another launch (``C2dPackJob``, csrc/conv2_wfrag.h)."""
+    _fields_ = [("w", c_p), ("w_lo", c_p), ("out", c_p)]
+
+
 class ConvDesc(ctypes.Structure):
     """Implicit-GEMM forward/dgrad problem (mirrors ``ConvDesc`` in csrc/conv_mfma.hip)."""
     _fields_ = [("x", c_p), ("frame_slots", c_p), ("w", c_p), ("bias", c_p), ("y", c_p), ("mask", c_p),
@@ -118,7 +129,7 @@ _SIGS = {
     "apex_grad_finalize": ([FinalizeDesc, c_p], c_i),
     "apex_norm_total": ([c_p, c_i, c_p, c_p], c_i),
     "apex_ddqn_head": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
-                        c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, c_p], c_i),
+                        c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, c_p], c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                              c_p, c_p, c_i, c_i, c_u64, c_p, c_p], c_i),

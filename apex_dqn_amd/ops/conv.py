@@ -245,12 +245,15 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
 def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
                  out: torch.Tensor, relu: bool = True, w2=None, b2=None, rows_first: int = 0, ksplit: int = 2,
                  loader_waves: bool = False, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
-                 c2d_pack: Optional[Tuple[torch.Tensor, Optional[torch.Tensor]]] = None) -> None:
+                 c2d_pack: Optional[Tuple[torch.Tensor, Optional[torch.Tensor]]] = None,
+                 no_epilogue: bool = False):
     """``dense_fwd`` on 128x128 tiles with the K range split ``ksplit`` ways
     (csrc/conv_mfma.hip ``fc_gemm128_kernel``): fp32 partials in a cached workspace,
     summed in fixed order by the epilogue kernel (bias, ReLU, hi / lo planes).
     ``c2d_pack = (w2, w2_lo)``: the epilogue launch also packs conv2's weights for this
-    step's conv2 data gradient (``conv2_dgrad_img(..., packed=True)``)."""
+    step's conv2 data gradient (``conv2_dgrad_img(..., packed=True)``).
+    ``no_epilogue``: only the GEMM runs; returns ``(partials, nz)`` for a consumer that
+    finishes the epilogue itself (the DDQN head, csrc/head_common.h load_row_part)."""
     M, K = x.shape
     Nc = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, Nc) and Nc % 128 == 0 and K % 64 == 0
@@ -268,8 +271,9 @@ def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Opti
     if c2d_pack is not None:
         pk.w, pk.w_lo = c2d_pack[0].data_ptr(), _lib.ptr(c2d_pack[1])
         pk.out = c2d_wfrag_buffer(ws, x.device).data_ptr()
-    _lib.check(lib.apex_fc_gemm128(d, buf.data_ptr(), buf.numel(), int(ksplit), int(loader_waves), pk,
-                                      _lib.stream_ptr()), "fc_gemm128")
+    _lib.check(lib.apex_fc_gemm128(d, buf.data_ptr(), buf.numel(), int(ksplit), int(loader_waves),
+                                      int(no_epilogue), pk, _lib.stream_ptr()), "fc_gemm128")
+    return (buf, nz) if no_epilogue else None
 
 
 def c2d_wfrag_buffer(ws: "Workspace", device) -> torch.Tensor:

@@ -85,9 +85,10 @@ class TorchBackend:
                        None if out_lo is None else out_lo[r:])
 
     def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
-               c2d=None):
+               c2d=None, defer_head=False):
         """``c2d = (conv2 weight, lo plane)``: weights of this step's conv2 data gradient,
-        which the HIP backend pre-packs inside the fc launch (ignored here)."""
+        which the HIP backend pre-packs inside the fc launch; ``defer_head``: the HIP
+        backend may leave the epilogue to the next :meth:`head` (both ignored here)."""
         dt = torch.float32 if x_lo is not None else self.dtype
         x = x.reshape(x.shape[0], -1)
         xf = join(x, x_lo.reshape(x.shape)) if x_lo is not None else x
@@ -294,7 +295,7 @@ class HipBackend(TorchBackend):
                    out_lo=out_lo, packed=packed)
 
     def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
-               c2d=None):
+               c2d=None, defer_head=False):
         if not self.native_conv:
             return super().fc_fwd(x, w, b, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
         M, K = x.shape[0], x[0].numel()
@@ -302,9 +303,16 @@ class HipBackend(TorchBackend):
                 hasattr(self.lib, "apex_fc_gemm128"):
             # 128x128 tiles, K split in two, loader waves: fc forward 40.6 -> 36.2 us
             # (split) / 25.7 -> 22.5 (bf16) at the learner shape (scripts/bench_fc128.py)
-            C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, 2, True,
-                           x_lo=None if x_lo is None else x_lo.reshape(M, K), w_lo=w_lo, w2_lo=w2_lo,
-                           out_lo=out_lo, c2d_pack=c2d)
+            defer = defer_head and w2 is not None and b is not None and b2 is not None and \
+                2 * (M // 3) == rows_first and M % 3 == 0
+            r = C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, 2, True,
+                               x_lo=None if x_lo is None else x_lo.reshape(M, K), w_lo=w_lo, w2_lo=w2_lo,
+                               out_lo=out_lo, c2d_pack=None if defer else c2d, no_epilogue=defer)
+            if defer:
+                # the split-K epilogue (and the conv2 pack) move into the next head launch
+                self._fc_part = dict(part=r[0], nz=r[1], zstride=M * w.shape[0], b=b, b2=b2, two_b=rows_first,
+                                     out=out, c2d=c2d)
+                return
             # the conv2 data gradient of this step finds its weights packed (the key is
             # checked there, so a different weight tensor still packs its own)
             if c2d is not None:
@@ -387,7 +395,20 @@ class HipBackend(TorchBackend):
                 td_abs.data_ptr(), loss.data_ptr(), _lib.ptr(q_out), dH.data_ptr(), dhead.data_ptr(),
                 _lib.ptr(zero), 0 if zero is None else zero.numel(), Pon["wv"].numel())
         hl = _lib.head_lo(*(lo if lo is not None else (None, None, None)))
-        _lib.check(self.lib.apex_ddqn_head(*args, hl, _lib.stream_ptr()), "ddqn_head")
+        hp, pk = _lib.HeadPart(), _lib.C2dPack()
+        fp = getattr(self, "_fc_part", None)
+        if fp is not None:
+            # the deferred fc epilogue: h rows [0, B) (+ lo plane) are written by this launch
+            self._fc_part = None
+            assert fp["out"].data_ptr() == Hon.data_ptr() and fp["two_b"] == 2 * B
+            hp.part, hp.zstride, hp.nz = fp["part"].data_ptr(), int(fp["zstride"]), int(fp["nz"])
+            hp.bias_on, hp.bias_tg, hp.two_b = fp["b"].data_ptr(), fp["b2"].data_ptr(), int(fp["two_b"])
+            hp.hon, hp.hon_lo = Hon.data_ptr(), _lib.ptr(None if lo is None else lo[0])
+            if fp["c2d"] is not None:
+                pk.w, pk.w_lo = fp["c2d"][0].data_ptr(), _lib.ptr(fp["c2d"][1])
+                pk.out = C.c2d_wfrag_buffer(self.ws, Hon.device).data_ptr()
+                self._c2d_packed = (fp["c2d"][0].data_ptr(), _lib.ptr(fp["c2d"][1]))
+        _lib.check(self.lib.apex_ddqn_head(*args, hl, hp, pk, _lib.stream_ptr()), "ddqn_head")
 
     def head_wgrad(self, Hon, dhead, g, prio=None, Hon_lo=None):
         B, A1 = dhead.shape

@@ -374,3 +374,33 @@ def test_rewarm_preserves_state():
         outs.append((L.p32.clone(), L.rms_v.clone(), rp.leaf.clone(), rp.ctr.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fc_epilogue_in_head_matches_separate_launch(dtype):
+    """The fc forward's split-K epilogue (and the conv2 weight pack) folded into the DDQN
+    head launch (ops.fc_fwd(defer_head=True) + head_common.h load_row_part): the stream
+    activations h are computed with the same sums, bias, ReLU and rounding as the
+    separate epilogue launch (bit-identical at equal parameters: scripts/diag_fc_head.py);
+    the head's dot products compile to a different instruction order, so |delta| and the
+    update agree to fp32 rounding.  (Later updates are not compared: early centered-RMSprop
+    steps scale a gradient difference by up to lr / eps ~ 400, so ulp-level differences
+    compound within a few updates -- scripts/diag_fc_head.py.)"""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 128},
+                                "Runtime": {"use_graphs": True, "graph_steps": 4, "dtype": dtype}})
+    outs = []
+    for defer in (True, False):
+        torch.manual_seed(0)
+        rp = _filled_replay(seed=11)
+        L = FusedNatureLearner(cfg, DEV, rp)
+        L._defer_fc_epilogue = defer
+        L.step()                      # the one-update graph (captured + replayed)
+        torch.cuda.synchronize()
+        outs.append((L.h[:128].clone(), L.p32.clone(), L.rms_v.clone(), L.td_abs.clone()))
+        del L
+    assert torch.equal(outs[0][0], outs[1][0])     # h: same parameters, same sums and rounding
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        assert torch.allclose(a.double(), b.double(), rtol=1e-5, atol=1e-8), float((a - b).abs().max())
