@@ -15,9 +15,23 @@ Here one step of the group:
   4. the sliding-window n-step builder emits transitions with initial
      priorities, inserted into the local replay shard by one kernel.
 
-The actor keeps its own parameter slot (bf16 weights + fp32 biases/heads),
-refreshed from the learner with a D2D copy every ``Q_network_sync_freq``
-steps (reference ``actor.py:189-191``).
+The actor keeps its own parameter slot (fp32 master weights + the bf16 compute
+copy, with its lo plane when the learner is fp32), refreshed from the learner with
+a D2D copy every ``Q_network_sync_freq`` steps (reference ``actor.py:189-191``).
+
+Precision: the reference actor runs the fp32 network (``actor.py:161`` ``.float()``)
+and derives the initial priorities from those q-values (``actor.py:127-143``).  With
+the fp32 learner (``Runtime.dtype = fp32``, split hi / lo operands) the actor runs the
+same split kernels on its batch -- conv1 on the fp32 weights, hi / lo activation
+planes through conv2 / conv3 / fc, ``actor_head`` on hi + lo -- so its q-values, the
+epsilon-greedy argmax and the initial |delta| priorities carry fp32-class error,
+not bf16's 2^-9.
+
+Epsilon ladder over ranks: env i of rank r is actor ``i * world + r`` of the global
+ladder eps^(1 + alpha k / (N - 1)) (interleaved), so every rank's replay shard holds a
+mix of exploratory and greedy actors -- with contiguous slices rank 0 would hold all
+the most exploratory ones and the shards' priority mass would differ systematically,
+which shrinks the global batch M of the sharded draw.
 
 Actor and learner overlap (the reference runs them as separate processes): the
 group's frame appends, inference and D2H copies run on its own stream, and
@@ -43,7 +57,7 @@ from .nstep import make_nstep_builder
 
 class GpuActorGroup:
     def __init__(self, cfg, learner, replay, env, num_envs: int, global_offset: int = 0,
-                 total_actors: Optional[int] = None, seed: int = 0):
+                 total_actors: Optional[int] = None, seed: int = 0, rank: int = 0, world: int = 1):
         self.cfg = cfg
         self.learner = learner
         self.replay = replay
@@ -55,30 +69,38 @@ class GpuActorGroup:
         d = learner.device
         self.device = d
         a = cfg.Actor
-        total = total_actors or self.E
-        ladder = epsilon_ladder(total, a.epsilon, a.alpha)
-        self.eps = torch.tensor(ladder[global_offset:global_offset + self.E], dtype=torch.float32, device=d)
+        self.eps = torch.tensor(ladder_slice(cfg, self.E, rank, world, total_actors), dtype=torch.float32, device=d)
         self.seed = int(seed) * 7919 + global_offset
         self.ctr = torch.zeros(1, dtype=torch.int64, device=d)
         ad = learner.act_dtype
+        # fp32 learner (split operands): the actor runs the split kernels too
+        self.split = bool(getattr(learner, "split", False))
         self.slots = torch.zeros(self.E, self.C, dtype=torch.int32, device=d)
         self.frames_buf = torch.zeros(self.E, self.C, 84, 84, dtype=torch.uint8, device=d) \
             if self.ops.name != "hip" else torch.zeros(1, self.C, 84, 84, dtype=torch.uint8, device=d)
-        self.y1 = torch.zeros(self.E, 20, 20, 64, dtype=ad, device=d)
-        self.y2 = torch.zeros(self.E, 9, 9, 64, dtype=ad, device=d)
-        self.y3 = torch.zeros(self.E, 7, 7, 64, dtype=ad, device=d)
-        self.h = torch.zeros(self.E, 1024, dtype=ad, device=d)
+
+        def act(*shape):
+            return (torch.zeros(*shape, dtype=ad, device=d),
+                    torch.zeros(*shape, dtype=ad, device=d) if self.split else None)
+
+        self.y1, self.y1_lo = act(self.E, 20, 20, 64)
+        self.y2, self.y2_lo = act(self.E, 9, 9, 64)
+        self.y3, self.y3_lo = act(self.E, 7, 7, 64)
+        self.h, self.h_lo = act(self.E, 1024)
         self.q = torch.zeros(self.E, self.A, dtype=torch.float32, device=d)
         self.act = torch.zeros(self.E, dtype=torch.int32, device=d)
         self.q_host = torch.zeros(self.E, self.A, dtype=torch.float32).pin_memory() \
             if d.type == "cuda" else torch.zeros(self.E, self.A)
         self.a_host = torch.zeros(self.E, dtype=torch.int32).pin_memory() \
             if d.type == "cuda" else torch.zeros(self.E, dtype=torch.int32)
-        # actor parameter slot
+        # actor parameter slot: fp32 master copy + the bf16 compute copy [hi | lo]
         self.p32 = learner.p32.clone()
-        self.pbf = learner.pbf.clone()
+        n = self.p32.numel()
+        self._pbf_all = (learner._pbf_all if self.split else learner.pbf).clone()
+        self.pbf = self._pbf_all[:n]
         self.P = learner.layout.views(self.p32)
         self.Pb = learner.layout.views(self.pbf)
+        self.Pl = learner.layout.views(self._pbf_all[n:]) if self.split else None
         self.builder = make_nstep_builder(self.E, a.num_steps, a.gamma, (self.C,), np.int64, env_id_offset=global_offset)
         self.global_offset = global_offset
         self.payload: Optional[np.ndarray] = None
@@ -126,7 +148,7 @@ class GpuActorGroup:
 
     def _copy_params(self) -> None:
         self.p32.copy_(self.learner.p32)
-        self.pbf.copy_(self.learner.pbf)
+        self._pbf_all.copy_(self.learner._pbf_all if self.split else self.learner.pbf)
 
     def reset_episodes(self) -> None:
         """Drop the partial n-step windows and start fresh episodes (actor restart)."""
@@ -159,15 +181,23 @@ class GpuActorGroup:
         return self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64)
 
     def _policy(self, payload: np.ndarray):
-        ops, P, Pb = self.ops, self.P, self.Pb
+        ops, P, Pb, Pl, E = self.ops, self.P, self.Pb, self.Pl, self.E
         self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
-        ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
-                           self.cfg.Runtime.obs_scale, self.y1)
-        ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2)
-        ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3)
-        ops.fc_fwd(self.y3.reshape(self.E, 3136), Pb["wfc"], P["bfc"], self.h)
+        if self.split:   # fp32-class: the learner's split kernels (hi / lo planes throughout)
+            ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
+                               self.cfg.Runtime.obs_scale, self.y1, w32=P["w1"], out_lo=self.y1_lo)
+            ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, x_lo=self.y1_lo, w_lo=Pl["w2"], out_lo=self.y2_lo)
+            ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, x_lo=self.y2_lo, w_lo=Pl["w3"], out_lo=self.y3_lo)
+            ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h, x_lo=self.y3_lo.reshape(E, 3136),
+                       w_lo=Pl["wfc"], out_lo=self.h_lo)
+        else:
+            ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
+                               self.cfg.Runtime.obs_scale, self.y1)
+            ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2)
+            ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3)
+            ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h)
         heads = {k: P[k] for k in ("wv", "bv", "wa", "ba")}
-        ops.actor_head(self.h, heads, self.eps, self.ctr, self.seed, self.q, self.act)
+        ops.actor_head(self.h, heads, self.eps, self.ctr, self.seed, self.q, self.act, H_lo=self.h_lo)
         self.ctr += 1
         self.q_host.copy_(self.q, non_blocking=True)
         self.a_host.copy_(self.act, non_blocking=True)
@@ -201,6 +231,15 @@ class GpuActorGroup:
         return n
 
 
+def ladder_slice(cfg, E: int, rank: int, world: int, total_actors: Optional[int] = None) -> List[float]:
+    """The epsilons of rank ``rank``'s E envs: actors ``i * world + rank`` of the global
+    ladder over ``total_actors`` (default E * world) actors, interleaved across ranks."""
+    a = cfg.Actor
+    total = max(int(total_actors or E * world), E * world)
+    ladder = epsilon_ladder(total, a.epsilon, a.alpha)
+    return [ladder[i * world + rank] for i in range(E)]
+
+
 class GraphActorGroup(GpuActorGroup):
     """Actor group for ``GraphLearner`` networks (IMPALA-deep): the
     frame stacks are gathered from the replay ring on the device, the actor's own
@@ -208,16 +247,14 @@ class GraphActorGroup(GpuActorGroup):
     epsilon-greedy is drawn on the device; one small D2H copy per step."""
 
     def __init__(self, cfg, learner, replay, env, num_envs: int, global_offset: int = 0,
-                 total_actors: Optional[int] = None, seed: int = 0):
+                 total_actors: Optional[int] = None, seed: int = 0, rank: int = 0, world: int = 1):
         import copy
         self.cfg, self.learner, self.replay, self.env = cfg, learner, replay, env
         self.E, self.C, self.A = int(num_envs), learner.C, learner.A
         d = learner.device
         self.device = d
         a = cfg.Actor
-        total = total_actors or self.E
-        ladder = epsilon_ladder(total, a.epsilon, a.alpha)
-        self.eps = torch.tensor(ladder[global_offset:global_offset + self.E], dtype=torch.float32, device=d)
+        self.eps = torch.tensor(ladder_slice(cfg, self.E, rank, world, total_actors), dtype=torch.float32, device=d)
         self.gen = torch.Generator(device=d)
         self.gen.manual_seed(int(seed) * 7919 + global_offset)
         self.slots = torch.zeros(self.E, self.C, dtype=torch.int32, device=d)
@@ -260,16 +297,15 @@ class ImpalaActorGroup(GpuActorGroup):
     own parameter slot, then the ``actor_head`` kernel draws epsilon-greedy."""
 
     def __init__(self, cfg, learner, replay, env, num_envs: int, global_offset: int = 0,
-                 total_actors: Optional[int] = None, seed: int = 0):
+                 total_actors: Optional[int] = None, seed: int = 0, rank: int = 0, world: int = 1):
         self.cfg, self.learner, self.replay, self.env = cfg, learner, replay, env
         self.E, self.C, self.A = int(num_envs), learner.C, learner.A
         self.ops = learner.ops
         d = learner.device
         self.device = d
         a = cfg.Actor
-        total = total_actors or self.E
-        ladder = epsilon_ladder(total, a.epsilon, a.alpha)
-        self.eps = torch.tensor(ladder[global_offset:global_offset + self.E], dtype=torch.float32, device=d)
+        self.eps = torch.tensor(ladder_slice(cfg, self.E, rank, world, total_actors), dtype=torch.float32, device=d)
+        self.h_lo = None
         self.seed = int(seed) * 7919 + global_offset
         self.ctr = torch.zeros(1, dtype=torch.int64, device=d)
         self.slots = torch.zeros(self.E, self.C, dtype=torch.int32, device=d)
@@ -311,4 +347,4 @@ def make_gpu_actor_group(cfg, learner, replay, num_envs: int, rank: int = 0, wor
     kind = getattr(learner, "kind", "")
     cls = {"graph": GraphActorGroup, "impala": ImpalaActorGroup}.get(kind, GpuActorGroup)
     return cls(cfg, learner, replay, env, num_envs, global_offset=rank * num_envs,
-               total_actors=total, seed=seed + rank)
+               total_actors=total, seed=seed + rank, rank=rank, world=world)

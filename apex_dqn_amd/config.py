@@ -80,8 +80,12 @@ class RuntimeConf:
     grad_clip: float = 40.0
     loss: str = "huber"             # "huber" | "mse" (0.5*delta^2, reference learner.py:48)
     huber_delta: float = 1.0
-    priority_eps: float = 1e-6
+    priority_eps: float = 1e-6      # priority floor: leaves hold (|delta| + priority_eps)^alpha
     use_is_weights: bool = True
+    is_normalise: str = "batch_max"  # IS weights (N P(i))^-beta divided by their max over the sampled batch
+                                    # ("batch_max", the PER / Ape-X papers' 1 / max_i w_i; with DP the global
+                                    # batch) or over the whole replay ("global_min": (p / p_min)^-beta, which
+                                    # shrinks every update when a few priorities sit at the floor)
     ckpt_dir: Optional[str] = None
     ckpt_freq: int = 0              # learner steps between checkpoints (0 = off)
     metrics_path: Optional[str] = None
@@ -181,6 +185,8 @@ class ApexConfig:
             raise ValueError("Runtime.world_size must be >= 1")
         if self.Runtime.comm_backend not in ("torch", "native"):
             raise ValueError("Runtime.comm_backend must be 'torch' or 'native'")
+        if self.Runtime.is_normalise not in ("batch_max", "global_min"):
+            raise ValueError("Runtime.is_normalise must be 'batch_max' or 'global_min'")
         if self.Runtime.loss not in ("huber", "mse"):
             raise ValueError("Runtime.loss must be 'huber' or 'mse'")
         net = self.network

@@ -22,6 +22,17 @@
 #include "head_common.h"
 #include "conv2_wfrag.h"
 
+// Batch-max IS normalisation (Runtime.is_normalise = "batch_max"): block 0's second
+// wave also leaves m = max_b isw[b] / wscale -- the largest (p / p_min)^-beta of the
+// batch, the sampler's W B / M factor taken out -- for the optimizer, which scales the
+// gradient by 1 / m (csrc/rmsprop_common.h is_grad_scale).  With DP `out` is this
+// rank's slot of the shard statistics that are all-gathered later in the step.
+struct IsNorm {
+  const float* wscale;   // sampler's W B / M (null: 1)
+  double* out;           // null: off
+  unsigned long long* valid_count;   // DP: += rows of this batch the rank drew (weight > 0); or null
+};
+
 // hp.part != null: the fc forward's split-K epilogue runs inside (head_common.h
 // load_row_part); blocks >= B run the conv2 weight-fragment pack job (pk.out != null)
 // that otherwise rides on that epilogue's launch.
@@ -32,15 +43,30 @@ __global__ void __launch_bounds__(192) ddqn_head_kernel(
     const float* __restrict__ isw, int B, int A, int huber, float kappa, float grad_scale,
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
     bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n, HeadLo lo,
-    HeadPart hp, C2dPackJob pk) {
+    HeadPart hp, C2dPackJob pk, IsNorm isn) {
   if ((int)blockIdx.x >= B) {
     for (int i = ((int)blockIdx.x - B) * 192 + (int)threadIdx.x; i < C2D_PACK_THREADS; i += ((int)gridDim.x - B) * 192)
       pack_c2d_wfrag_word(i, pk.w, pk.w_lo, pk.out);
     return;
   }
   float ad;
-  (void)ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs, loss,
-                           q_out, dH, dhead, zero_ptr, zero_n, &ad, lo, hp);
+  const bool w0 = ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs,
+                                     loss, q_out, dH, dhead, zero_ptr, zero_n, &ad, lo, hp);
+  if (!w0 && (isn.out != nullptr || isn.valid_count != nullptr) && blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {
+    float m = 0.f;
+    int nv = 0;
+    for (int i = threadIdx.x & 63; i < B; i += 64) {
+      m = fmaxf(m, isw[i]);
+      nv += isw[i] > 0.f ? 1 : 0;
+    }
+    m = wave_max(m);
+    nv = wave_sum(nv);
+    if ((threadIdx.x & 63) == 0) {
+      const float ws = isn.wscale != nullptr ? isn.wscale[0] : 1.f;
+      if (isn.out != nullptr) isn.out[0] = ws > 0.f ? (double)m / (double)ws : 0.0;
+      if (isn.valid_count != nullptr) atomicAdd(isn.valid_count, (unsigned long long)nv);
+    }
+  }
 }
 
 __global__ void __launch_bounds__(512) head_wgrad_kernel(HeadWgArgs h) { head_wgrad_body(h, blockIdx.x, blockIdx.y); }
@@ -49,8 +75,10 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
                                const int32_t* act, const float* rew, const float* gam, const float* isw,
                                int B, int A, int huber, float kappa, float grad_scale, float* td_abs,
                                float* loss, float* q_out, bf16_t* dH, float* dhead, float* zero_ptr,
-                               int zero_n, int hidden, HeadLo lo, HeadPart hp, C2dPackJob pk, hipStream_t st) {
+                               int zero_n, int hidden, HeadLo lo, HeadPart hp, C2dPackJob pk, IsNorm isn,
+                               hipStream_t st) {
   if (A < 1 || A > HEAD_MAXA || B < 1) return (int)hipErrorInvalidValue;
+  if ((isn.out != nullptr || isn.valid_count != nullptr) && isw == nullptr) return (int)hipErrorInvalidValue;
   if (lo.Hon != nullptr && (lo.Htg == nullptr || lo.dH == nullptr)) return (int)hipErrorInvalidValue;
   if (hp.part != nullptr) {   // split-K partials [nz][3B][2 hidden]; rows [0, B) of h written to hp.hon
     if (hp.nz < 1 || hp.hon == nullptr || hp.bias_on == nullptr || hp.bias_tg == nullptr || hp.two_b != 2 * B ||
@@ -62,11 +90,11 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
   if (hidden == 512)
     ddqn_head_kernel<512><<<grid, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
                                                 grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo,
-                                                hp, pk);
+                                                hp, pk, isn);
   else if (hidden == 256)
     ddqn_head_kernel<256><<<grid, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
                                                 grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo,
-                                                hp, pk);
+                                                hp, pk, isn);
   else
     return (int)hipErrorInvalidValue;
   APEX_CHECK_LAUNCH();
@@ -82,16 +110,19 @@ APEX_EXPORT int apex_head_wgrad(const bf16_t* Hon, const float* dhead, int B, in
 
 // Actor-side: dueling q from stream activations + epsilon-greedy selection.
 // One wave per env row. eps per row; uniform draws from the counter RNG.
+// H_lo (fp32 learner, split mode): the lo plane of the stream activations, so the
+// actor's q-values (and the initial priorities built from them) are fp32-accurate.
 template <int HS>
 __global__ void __launch_bounds__(256) actor_head_kernel(const bf16_t* __restrict__ H, HeadParams P, int E,
                                                          int A, const float* __restrict__ eps, uint64_t seed,
                                                          const uint64_t* __restrict__ ctr,
-                                                         float* __restrict__ q_out, int32_t* __restrict__ a_out) {
+                                                         float* __restrict__ q_out, int32_t* __restrict__ a_out,
+                                                         const bf16_t* __restrict__ H_lo) {
   const int lane = threadIdx.x & 63;
   const int e = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (e >= E) return;
   float q[HEAD_MAXA], hv[HS / 64], ha[HS / 64];
-  head_row<HS>(H + (int64_t)e * 2 * HS, nullptr, P, A, lane, q, hv, ha);
+  head_row<HS>(H + (int64_t)e * 2 * HS, H_lo != nullptr ? H_lo + (int64_t)e * 2 * HS : nullptr, P, A, lane, q, hv, ha);
   int best = 0;
   float bq = -3.4e38f;
 #pragma unroll
@@ -115,10 +146,13 @@ __global__ void __launch_bounds__(256) actor_head_kernel(const bf16_t* __restric
 }
 
 APEX_EXPORT int apex_actor_head(const bf16_t* H, HeadParams P, int E, int A, const float* eps, uint64_t seed,
-                                const uint64_t* ctr, float* q_out, int32_t* a_out, int hidden, hipStream_t st) {
+                                const uint64_t* ctr, float* q_out, int32_t* a_out, int hidden, const bf16_t* H_lo,
+                                hipStream_t st) {
   if (A < 1 || A > HEAD_MAXA || E < 1) return (int)hipErrorInvalidValue;
-  if (hidden == 512) actor_head_kernel<512><<<(E + 3) / 4, 256, 0, st>>>(H, P, E, A, eps, seed, ctr, q_out, a_out);
-  else if (hidden == 256) actor_head_kernel<256><<<(E + 3) / 4, 256, 0, st>>>(H, P, E, A, eps, seed, ctr, q_out, a_out);
+  if (hidden == 512)
+    actor_head_kernel<512><<<(E + 3) / 4, 256, 0, st>>>(H, P, E, A, eps, seed, ctr, q_out, a_out, H_lo);
+  else if (hidden == 256)
+    actor_head_kernel<256><<<(E + 3) / 4, 256, 0, st>>>(H, P, E, A, eps, seed, ctr, q_out, a_out, H_lo);
   else return (int)hipErrorInvalidValue;
   APEX_CHECK_LAUNCH();
 }

@@ -49,13 +49,14 @@ APEX_EXPORT int apex_grad_sqnorm_partials(const float* g, int64_t n, double* par
 
 APEX_EXPORT int apex_rmsprop_step(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
                                   const double* partials, float lr, float alpha, float eps, float clip,
-                                  int centered, float* norm_out, bf16_t* pb_lo, hipStream_t st) {
+                                  int centered, float* norm_out, bf16_t* pb_lo, const double* wnorm, int wn,
+                                  int wstride, hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
   if (((uintptr_t)pb | (uintptr_t)pb_lo) & 7) return (int)hipErrorInvalidValue;
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, NPART, lr, alpha, eps, clip, centered,
-                                                 norm_out, pb_lo});
+                                                 norm_out, pb_lo, wnorm, wn, wstride});
   APEX_CHECK_LAUNCH();
 }
 
@@ -63,13 +64,14 @@ APEX_EXPORT int apex_rmsprop_step(float* p, const float* g, float* v, float* m, 
 // (fc wgrad epilogue + grad_finalize blocks): no separate squared-norm pass
 APEX_EXPORT int apex_rmsprop_step_np(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
                                      const double* partials, int npart, float lr, float alpha, float eps, float clip,
-                                     int centered, float* norm_out, bf16_t* pb_lo, hipStream_t st) {
+                                     int centered, float* norm_out, bf16_t* pb_lo, const double* wnorm, int wn,
+                                  int wstride, hipStream_t st) {
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
   if (((uintptr_t)pb | (uintptr_t)pb_lo) & 7) return (int)hipErrorInvalidValue;
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, npart, lr, alpha, eps, clip, centered,
-                                                 norm_out, pb_lo});
+                                                 norm_out, pb_lo, wnorm, wn, wstride});
   APEX_CHECK_LAUNCH();
 }
 

@@ -5,10 +5,24 @@
 #pragma once
 #include "apex_common.h"
 
+// Batch-max IS-weight normalisation (Runtime.is_normalise = "batch_max"): the head
+// kernel leaves m = max_j (p_j / p_min)^-beta over the batch (DP: one per rank, in the
+// all-gathered shard statistics, stride `wstride`); the loss used the global-min
+// weights w_j, so the batch-max weights w_j / m give the gradient g / m -- one scalar
+// applied here, before the clip, instead of a second pass over the weights.
+__device__ __forceinline__ float is_grad_scale(const double* wnorm, int wn, int wstride) {
+  if (wnorm == nullptr) return 1.0f;
+  double m = 0.0;
+  for (int k = 0; k < wn; ++k) m = fmax(m, wnorm[(int64_t)k * wstride]);
+  return m > 0.0 ? (float)(1.0 / m) : 1.0f;
+}
+
 // Clip coefficient from the squared-norm partials: every thread of the block sums a
 // fixed strided subset, then a fixed-order wave / LDS reduction -- deterministic.
+// `gscale` multiplies the gradient first (is_grad_scale); the returned coefficient
+// includes it and sh[1] is the norm of the scaled gradient.
 __device__ __forceinline__ float clip_coef_from_partials(const double* partials, int npart, float clip,
-                                                         float* sh) {
+                                                         float* sh, float gscale = 1.0f) {
   __shared__ double red[16];
   double s = 0.0;
   for (int i = threadIdx.x; i < npart; i += blockDim.x) s += partials[i];
@@ -18,8 +32,8 @@ __device__ __forceinline__ float clip_coef_from_partials(const double* partials,
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
-    const float norm = (float)sqrt(t);
-    sh[0] = (clip > 0.f) ? fminf(1.0f, clip / (norm + 1e-6f)) : 1.0f;
+    const float norm = (float)sqrt(t) * gscale;
+    sh[0] = gscale * ((clip > 0.f) ? fminf(1.0f, clip / (norm + 1e-6f)) : 1.0f);
     sh[1] = norm;
   }
   __syncthreads();
@@ -39,6 +53,8 @@ struct RmspropArgs {
   int centered;
   float* norm_out;
   bf16_t* pb_lo;     // fp32-accurate mode: lo plane of the bf16 copy (p = pb + pb_lo), else null
+  const double* wnorm;  // batch-max IS normalisation (is_grad_scale), or null
+  int wn, wstride;
 };
 
 // one 256-thread block `bid` of `nblk` (grid-stride over float4 chunks)
@@ -70,7 +86,8 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
     gg = g4[i]; pp = p4[i]; vv = v4[i];
     if (centered) mm = m4[i];
   }
-  const float coef = clip_coef_from_partials(A_.partials, A_.npart, A_.clip, sh);
+  const float coef = clip_coef_from_partials(A_.partials, A_.npart, A_.clip, sh,
+                                             is_grad_scale(A_.wnorm, A_.wn, A_.wstride));
   if (bid == 0 && threadIdx.x == 0 && A_.norm_out) A_.norm_out[0] = sh[1];
   const float a1 = 1.0f - alpha;
   for (; i < n4; i += stride) {

@@ -142,6 +142,10 @@ __global__ void __launch_bounds__(1024) tree_update_kernel(TreeDesc t, const int
   if (act) {
     s = idx[i];
     act = APEX_DBG_OK(s, t.n[0], 0);
+    // rows of a sharded draw that landed in another shard (generation -1) write
+    // nothing, so they must not take part in the dedupe either: a foreign row on
+    // the same leaf as a valid row would otherwise win and then be dropped
+    if (gen_expect != nullptr && gen_expect[i] < 0) act = false;
   }
   if (dedupe) {  // host guarantees gridDim.x == 1 and n <= 1024
     for (int j = threadIdx.x; j < 2048; j += blockDim.x) {
@@ -256,6 +260,9 @@ static int tree_kfirst(const TreeDesc& t) {
 // (their priority write-back is dropped).  IS weights use the global minimum:
 // w = (p / p_min)^-beta * (W B / M), the last factor turning the head's 1/(W B)
 // gradient scale into the 1/M mean over the draws actually taken.
+// all-gathered per-shard statistics: (sum p^alpha, min p^alpha, max IS weight of the
+// shard's rows in the current batch -- written by the head kernel, read by the optimizer)
+#define SHARD_STATS 3
 struct SampleArgs {
   TreeDesc t;
   RecordDesc r;
@@ -272,9 +279,10 @@ struct SampleArgs {
   float* out_rew;
   float* out_gam;
   int32_t* out_nxt2;
-  const double* shard_stats;   // sharded mode: [W][2] (total, min p) of every shard, or null
+  const double* shard_stats;   // sharded mode: [W][SHARD_STATS] (total, min p, batch IS max) per shard, or null
   int shard_rank, shard_world;
   uint64_t shard_seed;         // common to all ranks (the local `seed` is per shard)
+  float* out_wscale;           // the batch's W B / M factor (1 unsharded), for the IS batch-max; or null
 };
 
 // block `bid` of 4 waves: samples 4 bid .. 4 bid + 3
@@ -306,14 +314,14 @@ __device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
     double sum = 0.0, c0 = 0.0, tmax = 0.0;
     float pm = __uint_as_float(0x7f800000u);
     for (int q = 0; q < W; ++q) {
-      const double Tq = S.shard_stats[2 * q];
+      const double Tq = S.shard_stats[SHARD_STATS * q];
       if (q < r) c0 += Tq;
       sum += Tq;
       tmax = fmax(tmax, Tq);
-      const float mq = (float)S.shard_stats[2 * q + 1];
+      const float mq = (float)S.shard_stats[SHARD_STATS * q + 1];
       if (Tq > 0.0 && mq > 0.f) pm = fminf(pm, mq);
     }
-    const double Tr = S.shard_stats[2 * r];
+    const double Tr = S.shard_stats[SHARD_STATS * r];
     const double c1 = c0 + Tr;
     int64_t M = 0;
     if (tmax > 0.0) {
@@ -367,6 +375,7 @@ __device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
     const float w = (valid && p > 0.f && pmin > 0.f) ? fminf(powf(p / pmin, -beta), 1.0f) * wscale : 0.f;
     out_idx[b] = s;
     out_w[b] = w;
+    if (b == 0 && S.out_wscale != nullptr) S.out_wscale[0] = wscale;
     out_gen[b] = valid ? r.gen[s] : -1;
     out_act[b] = r.act[s];
     out_rew[b] = r.rew[s];
@@ -478,7 +487,8 @@ __device__ __forceinline__ void tree_update_block(const TreeUpdArgs& a) {
     h[r] = -1;
     if (i < a.n) {
       s[r] = a.idx[i];
-      if (APEX_DBG_OK(s[r], t.n[0], 0)) {
+      // foreign rows of a sharded draw (generation -1) stay out of the dedupe
+      if (APEX_DBG_OK(s[r], t.n[0], 0) && (a.gen_expect == nullptr || a.gen_expect[i] >= 0)) {
         const uint32_t key = (uint32_t)s[r] + 1u;
         int hh = (int)(hash32(key) & 2047u);
         while (true) {
@@ -592,14 +602,15 @@ APEX_EXPORT int apex_tree_sample(TreeDesc t, RecordDesc r, int B, uint64_t seed,
                                  float beta, int64_t* out_idx, float* out_w,
                                  int32_t* out_gen, int32_t* out_obs, int32_t* out_nxt, int32_t* out_act,
                                  float* out_rew, float* out_gam, int32_t* out_nxt2, const double* shard_stats,
-                                 int shard_rank, int shard_world, uint64_t shard_seed, hipStream_t st) {
+                                 int shard_rank, int shard_world, uint64_t shard_seed, float* out_wscale,
+                                 hipStream_t st) {
   if (B <= 0) return 0;
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   const int waves_per_block = 4;
   tree_sample_kernel<<<blocks_for(B, waves_per_block), 64 * waves_per_block, 0, st>>>(
       SampleArgs{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
-                 out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed});
+                 out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed, out_wscale});
   APEX_CHECK_LAUNCH();
 }
 
@@ -684,7 +695,8 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int64_t* out_idx, float* out_w, int32_t* out_gen, int32_t* out_obs,
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
-                                    uint64_t shard_seed, bf16_t* pb_lo, hipStream_t st) {
+                                    uint64_t shard_seed, float* out_wscale, bf16_t* pb_lo, const double* wnorm,
+                                    int wn, int wstride, hipStream_t st) {
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
@@ -706,9 +718,11 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   int nb = (int)((n / 4 + nt - 1) / nt);
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
   const int nsb = blocks_for(B, nt / 64);
-  const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo};
+  const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,
+                      wnorm, wn, wstride};
   const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
-                      out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed};
+                      out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed,
+                      out_wscale};
   if (nt == 1024) rmsprop_sample_kernel<1024><<<nb + nsb, 1024, 0, st>>>(ra, sa, nsb);
   else if (nt == 512) rmsprop_sample_kernel<512><<<nb + nsb, 512, 0, st>>>(ra, sa, nsb);
   else rmsprop_sample_kernel<256><<<nb + nsb, 256, 0, st>>>(ra, sa, nsb);

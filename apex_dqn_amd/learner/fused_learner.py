@@ -48,6 +48,7 @@ from ..models.flat_params import (FlatLayout, flat_to_reference_state, nature_se
                                   reference_state_to_flat)
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
+from .is_norm import IsNormMixin
 
 
 def _enable_sharding(replay, comm, rt) -> None:
@@ -59,7 +60,7 @@ def _enable_sharding(replay, comm, rt) -> None:
         replay.beta = 0.0
 
 
-class FusedNatureLearner:
+class FusedNatureLearner(IsNormMixin):
     kind = "fused"
 
     def __init__(self, cfg: ApexConfig, device, replay, comm=None, backend: Optional[str] = None,
@@ -127,6 +128,7 @@ class FusedNatureLearner:
         # and the segmented-step overhead on a single GPU)
         self._dp = self.world > 1 or (bool(self.rt.force_dp) and comm is not None)
         self._alloc(self.B)
+        self._init_is_norm()
         self._graphs = None     # one-update graph
         self._multi = None      # Runtime.graph_steps-update graph (steps())
         self.graph_captures = 0  # HIP graphs captured so far (the bench asserts none in its timed region)
@@ -149,6 +151,10 @@ class FusedNatureLearner:
         # Rows drawn elsewhere carry IS weight 0, so the IS weights always enter the loss
         # (with use_is_weights off: beta = 0, i.e. weights 0 / W B / M only).
         self._isw = bool(self.rt.use_is_weights) or self._dp
+        # batch-max IS normalisation (Runtime.is_normalise): the head kernel leaves the
+        # batch's largest (p / p_min)^-beta -- with DP in this rank's slot of the shard
+        # statistics, all-gathered later in the step -- and the optimizer divides the
+        # gradient by the maximum (csrc/ddqn_head.hip IsNorm, rmsprop_common.h)
         # the DP step's collectives: torch.distributed (RCCL process group / gloo) or the
         # native RCCL communicator on its own stream (Runtime.comm_backend, parallel/rccl.py)
         self.coll = None
@@ -284,7 +290,7 @@ class FusedNatureLearner:
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
-                 **self._lo(lo=sp and (self.h_lo[:2 * B], self.h_lo[2 * B:], self.dH_lo)))
+                 isn=self._isn(), **self._lo(lo=sp and (self.h_lo[:2 * B], self.h_lo[2 * B:], self.dH_lo)))
         self._mark("head")
         # fc wgrad + head wgrad + priority write-back: one launch on the HIP backend
         # (csrc/sumtree.hip fc_wgrad_head_prio_kernel)
@@ -380,7 +386,7 @@ class FusedNatureLearner:
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else None, sample=nxt,
-                      **self._lo(pb_lo=self.pbf_lo))
+                      wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo))
         if self._presample:
             self._sample_ver = self.replay.version
         self._mark("optimizer")
@@ -620,8 +626,7 @@ class FusedNatureLearner:
 
     # ------------------------------------------------------------ metrics
     def last_metrics(self) -> Dict[str, float]:
-        return {"loss": float(self.loss_b.mean()), "td_abs_mean": float(self.td_abs.mean()),
-                "grad_norm": float(self.gnorm[0])}
+        return self._is_metrics()
 
     def q_values(self, frames_u8: torch.Tensor) -> torch.Tensor:
         """Greedy-evaluation helper: q for a (N, C, 84, 84) uint8 batch (fp32 module,

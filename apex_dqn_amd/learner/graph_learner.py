@@ -91,6 +91,11 @@ class GraphLearner:
         self.loss_b = torch.zeros(1, dtype=torch.float32, device=d)
         # DP: one global prioritized replay over the rank shards (see fused_learner)
         self._isw = bool(self.rt.use_is_weights) or self.world > 1
+        # batch-max IS normalisation (learner/is_norm.py): the loss keeps the sampler's
+        # global-min weights, the optimizer divides the gradient by the batch's largest
+        # (p / p_min)^-beta (with DP its max over the ranks, all-reduced beside the gradient)
+        self._is_bmax = bool(self.rt.use_is_weights) and self.rt.is_normalise == "batch_max"
+        self.wmax = torch.zeros(1, dtype=torch.float64, device=d)
         if self.world > 1:
             _enable_sharding(replay, comm, self.rt)
             replay.gather_shard_stats()
@@ -124,6 +129,8 @@ class GraphLearner:
                 q_n = self.Q(nxt)[2]
                 q_g = self.Q_target(nxt)[2]
         w = S["weights"] if self._isw else None
+        if self._is_bmax:
+            self.wmax.copy_(S["weights"].max().double() / S["wscale"].double().clamp_min(1e-30))
         loss, td = ddqn_loss(q_t.float(), q_n.float(), q_g.float(), S["act"], S["rew"], S["gam"], w,
                              loss=rt.loss, kappa=rt.huber_delta)
         (loss / self.world).backward()     # SUM all-reduce of 1/world-scaled grads = mean
@@ -133,12 +140,15 @@ class GraphLearner:
     def _apply(self) -> None:
         rt = self.rt
         self.ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
-                           rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm)
+                           rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
+                           wnorm=(self.wmax, 1, 1) if self._is_bmax else None)
         self.replay.update_priorities(self.S["idx"], self.td_abs, self.S["gen"])
 
     def _allreduce(self) -> None:
         import torch.distributed as dist
         dist.all_reduce(self.g32, op=dist.ReduceOp.SUM)
+        if self._is_bmax:
+            dist.all_reduce(self.wmax, op=dist.ReduceOp.MAX)
 
     def _capture(self) -> None:
         s = torch.cuda.Stream(self.device)

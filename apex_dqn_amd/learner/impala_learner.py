@@ -40,6 +40,7 @@ from ..ops.fused_ops import HipBackend, TorchBackend
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
 from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
 from .fused_learner import _enable_sharding
+from .is_norm import IsNormMixin
 
 CH = (16, 32, 32)
 HIDDEN = 256
@@ -64,7 +65,7 @@ def fc_column_perm(device=None) -> torch.Tensor:
     return k.reshape(-1).to(device)
 
 
-class FusedImpalaLearner:
+class FusedImpalaLearner(IsNormMixin):
     kind = "impala"
 
     def __init__(self, cfg: ApexConfig, device, replay, comm=None, backend: Optional[str] = None,
@@ -145,6 +146,8 @@ class FusedImpalaLearner:
         self.gnorm = torch.zeros(1, dtype=torch.float32, device=d)
         # DP: one global prioritized replay over the rank shards (see fused_learner)
         self._isw = bool(self.rt.use_is_weights) or self.world > 1
+        self._dp = self.world > 1
+        self._init_is_norm()
         if self.world > 1:
             _enable_sharding(replay, comm, self.rt)
             replay.gather_shard_stats()
@@ -294,7 +297,7 @@ class FusedImpalaLearner:
         isw = S["weights"] if self._isw else None
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
-                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region)
+                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region, isn=self._isn())
         # priority write-back in the head-wgrad launch (csrc/sumtree.hip head_wgrad_prio_kernel)
         with self._on_side():
             ops.head_wgrad(self.h, self.dhead, self.G, prio=(self.replay, S["idx"], S["gen"], self.td_abs))
@@ -341,7 +344,7 @@ class FusedImpalaLearner:
         rt, ops = self.rt, self.ops
         nxt = (self.replay, self.B, self.S, self.slots[2 * self.B:]) if self._presample else None
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
-                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm, sample=nxt)
+                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm, sample=nxt, wnorm=self._wnorm())
         if self._presample:
             self._sample_ver = self.replay.version
 
@@ -442,8 +445,7 @@ class FusedImpalaLearner:
 
     # ------------------------------------------------------------ metrics
     def last_metrics(self) -> Dict[str, float]:
-        return {"loss": float(self.loss_b.mean()), "td_abs_mean": float(self.td_abs.mean()),
-                "grad_norm": float(self.gnorm[0])}
+        return self._is_metrics()
 
     def profile_step(self) -> Dict[str, float]:
         if self.device.type != "cuda":

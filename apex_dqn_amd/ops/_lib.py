@@ -52,6 +52,11 @@ class HeadPart(ctypes.Structure):
                 ("two_b", c_i), ("hon", c_p), ("hon_lo", c_p)]
 
 
+class IsNorm(ctypes.Structure):
+    """Batch-max IS normalisation output of the head kernel (``IsNorm``, csrc/ddqn_head.hip)."""
+    _fields_ = [("wscale", c_p), ("out", c_p), ("valid_count", c_p)]
+
+
 class C2dPack(ctypes.Structure):
     """conv2 weight-fragment pack job riding on another launch (``C2dPackJob``, csrc/conv2_wfrag.h)."""
     _fields_ = [("w", c_p), ("w_lo", c_p), ("out", c_p)]
@@ -116,29 +121,30 @@ _SIGS = {
     "apex_replay_insert": ([TreeDesc, RecordDesc, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p],
                            c_i),
     "apex_tree_sample": ([TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                          c_p, c_p, c_p, c_i, c_i, c_u64, c_p], c_i),
+                          c_p, c_p, c_p, c_i, c_i, c_u64, c_p, c_p], c_i),
     "apex_tree_rebuild": ([TreeDesc, c_p], c_i),
     "apex_gather_frames": ([c_p, c_p, c_i, c_i64, c_i64, c_p, c_p], c_i),
     "apex_debug_bounds_enabled": ([], c_i),
     "apex_debug_errors": ([c_p, c_p, c_i], c_i),
     "apex_grad_sqnorm_partials": ([c_p, c_i64, c_p, c_p], c_i),
-    "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p], c_i),
+    "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p, c_i, c_i,
+                           c_p], c_i),
     "apex_cast_bf16": ([c_p, c_p, c_i64, c_p, c_p], c_i),
-    "apex_rmsprop_step_np": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p],
-                             c_i),
+    "apex_rmsprop_step_np": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p,
+                              c_i, c_i, c_p], c_i),
     "apex_grad_finalize": ([FinalizeDesc, c_p], c_i),
     "apex_norm_total": ([c_p, c_i, c_p, c_p], c_i),
     "apex_ddqn_head": ([c_p, c_p, HeadParams, HeadParams, c_p, c_p, c_p, c_p, c_i, c_i, c_i, c_f, c_f, c_p,
-                        c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, c_p], c_i),
+                        c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, IsNorm, c_p], c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p, c_i, c_i, c_u64, c_p, c_p], c_i),
+                             c_p, c_p, c_i, c_i, c_u64, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
                               c_p, c_p, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,
                                  c_p, c_f, c_f, c_p, c_p, c_p], c_i),
     "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p], c_i),
-    "apex_actor_head": ([c_p, HeadParams, c_i, c_i, c_p, c_u64, c_p, c_p, c_p, c_i, c_p], c_i),
+    "apex_actor_head": ([c_p, HeadParams, c_i, c_i, c_p, c_u64, c_p, c_p, c_p, c_i, c_p, c_p], c_i),
     "apex_conv1_s2d_fwd": ([Conv1S2DDesc, c_i, c_p], c_i),
     "apex_conv1_wgrad_img": ([Conv1WgDesc, c_i, c_p], c_i),
     "apex_slab_reduce": ([c_p, c_i, c_i64, c_f, c_p, c_p, c_i, c_p, c_i, c_i, c_p], c_i),

@@ -8,11 +8,16 @@
   host code built with hipcc against the RCCL / HIP headers (librccl is dlopen()ed).
 
 Objects are rebuilt only when their source (or a header) is newer.  The
-libraries land in ``apex_dqn_amd/ops/_build/`` which ships to the GPU box
-with the repo snapshot (git-ignored, not gpurun-ignored).
+libraries land in ``apex_dqn_amd/ops/_build/`` (``APEX_BUILD_DIR`` overrides it)
+which ships to the GPU box with the repo snapshot (git-ignored, not
+gpurun-ignored).  Builds hold an exclusive ``fcntl`` lock on ``_build/.lock``: the
+ranks of a torchrun job that all find the library missing build it once -- the
+first takes the lock and compiles, the others wait and then find it fresh.
 """
 from __future__ import annotations
 
+import contextlib
+import fcntl
 import glob
 import os
 import subprocess
@@ -23,7 +28,7 @@ from typing import List
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
-OUT = os.path.join(HERE, "_build")
+OUT = os.environ.get("APEX_BUILD_DIR") or os.path.join(HERE, "_build")
 KERNEL_LIB = os.path.join(OUT, "libapex_kernels.so")
 KERNEL_DEBUG_LIB = os.path.join(OUT, "libapex_kernels_debug.so")
 RUNTIME_LIB = os.path.join(OUT, "libapex_runtime.so")
@@ -54,10 +59,40 @@ def _run(cmd: List[str]) -> None:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}")
 
 
+@contextlib.contextmanager
+def build_lock():
+    """Exclusive inter-process lock over the build directory (re-entrant per process
+    through the depth counter: build_all -> build_kernels)."""
+    os.makedirs(OUT, exist_ok=True)
+    if _LOCK["depth"] > 0:
+        _LOCK["depth"] += 1
+        try:
+            yield
+        finally:
+            _LOCK["depth"] -= 1
+        return
+    with open(os.path.join(OUT, ".lock"), "a+") as f:
+        fcntl.flock(f.fileno(), fcntl.LOCK_EX)
+        _LOCK["depth"] = 1
+        try:
+            yield
+        finally:
+            _LOCK["depth"] = 0
+            fcntl.flock(f.fileno(), fcntl.LOCK_UN)
+
+
+_LOCK = {"depth": 0}
+
+
 def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool = False) -> str:
     """``debug=True`` builds ``libapex_kernels_debug.so`` with ``-DAPEX_DEBUG_BOUNDS``
     (device-side index checks in the replay kernels, see csrc/sumtree.hip) and
     ``-DAPEX_PROBE`` (in-kernel phase stamps, csrc/mfma_common.h)."""
+    with build_lock():
+        return _build_kernels(force, jobs, verbose, debug)
+
+
+def _build_kernels(force: bool, jobs: int, verbose: bool, debug: bool) -> str:
     os.makedirs(OUT, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.cuh"))
@@ -81,14 +116,22 @@ def build_kernels(force: bool = False, jobs: int = 8, verbose: bool = False, deb
         with ThreadPoolExecutor(max_workers=jobs) as ex:
             list(ex.map(_run, todo))
     if force or todo or _newer(objs, lib_path):
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib_path] + objs)
+        # link to a temporary name, then rename: a process that maps the library
+        # never sees a half-written file
+        tmp = lib_path + f".tmp{os.getpid()}"
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)
+        os.replace(tmp, lib_path)
     if verbose:
         print(f"built {lib_path} ({len(todo)} objects recompiled)")
     return lib_path
 
 
 def build_runtime(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(OUT, exist_ok=True)
+    with build_lock():
+        return _build_runtime(force, verbose)
+
+
+def _build_runtime(force: bool, verbose: bool) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     hdrs = glob.glob(os.path.join(CSRC, "runtime", "*.h"))
     if srcs and (force or _newer(srcs + hdrs, RUNTIME_LIB)):
@@ -99,7 +142,11 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_comm(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(OUT, exist_ok=True)
+    with build_lock():
+        return _build_comm(force, verbose)
+
+
+def _build_comm(force: bool, verbose: bool) -> str:
     src = os.path.join(CSRC, "comm", "rccl_comm.cpp")
     if force or _newer([src], COMM_LIB):
         _run([HIPCC, "-O2", "-std=c++17", "-fPIC", "-shared", "-I", "/opt/rocm/include", src, "-o", COMM_LIB, "-ldl"])
@@ -109,11 +156,12 @@ def build_comm(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_all(force: bool = False, verbose: bool = True, debug: bool = True) -> None:
-    build_runtime(force=force, verbose=verbose)
-    build_comm(force=force, verbose=verbose)
-    build_kernels(force=force, verbose=verbose)
-    if debug:
-        build_kernels(force=force, verbose=verbose, debug=True)
+    with build_lock():
+        build_runtime(force=force, verbose=verbose)
+        build_comm(force=force, verbose=verbose)
+        build_kernels(force=force, verbose=verbose)
+        if debug:
+            build_kernels(force=force, verbose=verbose, debug=True)
 
 
 if __name__ == "__main__":

@@ -102,8 +102,11 @@ class TorchBackend:
     # ---------------------------------------------------------------- head
     def head(self, Hon, Htg, Pon: Dict[str, torch.Tensor], Ptg: Dict[str, torch.Tensor], act, rew, gam, isw,
              huber: bool, kappa: float, grad_scale: float, td_abs, loss, dH, dhead, q_out=None,
-             zero: Optional[torch.Tensor] = None, lo=None):
-        """``lo = (Hon_lo, Htg_lo, dH_lo)`` in split mode."""
+             zero: Optional[torch.Tensor] = None, lo=None, isn=None):
+        """``lo = (Hon_lo, Htg_lo, dH_lo)`` in split mode.  ``isn = (wscale, out[, count])``:
+        batch-max IS normalisation, ``out[0] = max(isw) / wscale`` (the optimizer divides the
+        gradient by it; csrc/ddqn_head.hip ``IsNorm``; ``out`` may be None), and ``count``
+        (int64) += the rows with a non-zero weight (DP: the rows this rank drew)."""
         B = act.shape[0]
         A = Pon["wa"].shape[0]
         Hon = join(Hon, None if lo is None else lo[0])
@@ -146,6 +149,12 @@ class TorchBackend:
             q_out.copy_(q_t)
         if zero is not None:
             zero.zero_()
+        if isn is not None:
+            if isn[1] is not None:
+                ws = float(isn[0].reshape(-1)[0]) if isn[0] is not None else 1.0
+                isn[1].reshape(-1)[0] = (w.max().double() / ws) if ws > 0 else 0.0
+            if len(isn) > 2 and isn[2] is not None:
+                isn[2].add_((w > 0).sum())
 
     def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor], prio=None, Hon_lo=None):
         """``prio = (replay, idx, gen, td_abs)``: also write the batch's priorities back
@@ -160,9 +169,10 @@ class TorchBackend:
         g["wa"].add_(dhead[:, 1:].t() @ h[:, HS:])
         g["ba"].add_(dhead[:, 1:].sum(0))
 
-    def actor_head(self, H, P, eps, ctr, seed, q_out, a_out):
-        """Dueling q + epsilon-greedy per row (the oracle of csrc actor_head_kernel)."""
-        h = H.float()
+    def actor_head(self, H, P, eps, ctr, seed, q_out, a_out, H_lo=None):
+        """Dueling q + epsilon-greedy per row (the oracle of csrc actor_head_kernel);
+        ``H_lo``: split mode, the activations' lo plane."""
+        h = join(H, H_lo)
         HS = P["wv"].numel()
         v = h[:, :HS] @ P["wv"].float() + P["bv"].float()
         a = h[:, HS:] @ P["wa"].float().t() + P["ba"].float()
@@ -229,19 +239,26 @@ class TorchBackend:
 
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None):
+                  sample=None, pb_lo=None, wnorm=None):
         """``sample = (replay, B, out, nxt2)``: also draw the next
         batch after the update (the HIP backend fuses it into the optimizer launch).
-        ``pb_lo``: split mode, the lo plane of the bf16 copy."""
-        self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo)
+        ``pb_lo``: split mode, the lo plane of the bf16 copy.  ``wnorm = (stats, n,
+        stride)``: batch-max IS normalisation, the gradient is divided by the largest of
+        the n per-rank maxima ``stats[k * stride]`` (csrc/rmsprop_common.h is_grad_scale)."""
+        self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo, wnorm)
         if sample is not None:
             rp, B, out, nxt2 = sample
             rp.sample(B, out=out, nxt2=nxt2)
 
-    def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo=None):
-        norm = g32.double().pow(2).sum().sqrt().float()
+    def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo=None, wnorm=None):
+        sc = torch.ones((), dtype=torch.float32, device=g32.device)
+        if wnorm is not None:     # tensor ops only: no host sync (graph-capturable)
+            st, n, stride = wnorm
+            mx = st.reshape(-1)[0:n * stride:stride].max().float()
+            sc = torch.where(mx > 0, 1.0 / mx.clamp_min(1e-30), sc)
+        norm = g32.double().pow(2).sum().sqrt().float() * sc
         coef = torch.clamp(clip / (norm + 1e-6), max=1.0) if clip > 0 else torch.ones_like(norm)
-        g = g32 * coef
+        g = g32 * (coef * sc)
         v.mul_(alpha).add_((1 - alpha) * g * g)
         if centered:
             m.mul_(alpha).add_((1 - alpha) * g)
@@ -387,7 +404,7 @@ class HipBackend(TorchBackend):
         return h
 
     def head(self, Hon, Htg, Pon, Ptg, act, rew, gam, isw, huber, kappa, grad_scale, td_abs, loss, dH,
-             dhead, q_out=None, zero=None, lo=None):
+             dhead, q_out=None, zero=None, lo=None, isn=None):
         B = act.shape[0]
         A = Pon["wa"].shape[0]
         args = (Hon.data_ptr(), Htg.data_ptr(), self._hp(Pon), self._hp(Ptg), act.data_ptr(), rew.data_ptr(),
@@ -408,7 +425,11 @@ class HipBackend(TorchBackend):
                 pk.w, pk.w_lo = fp["c2d"][0].data_ptr(), _lib.ptr(fp["c2d"][1])
                 pk.out = C.c2d_wfrag_buffer(self.ws, Hon.device).data_ptr()
                 self._c2d_packed = (fp["c2d"][0].data_ptr(), _lib.ptr(fp["c2d"][1]))
-        _lib.check(self.lib.apex_ddqn_head(*args, hl, hp, pk, _lib.stream_ptr()), "ddqn_head")
+        isn_s = _lib.IsNorm()
+        if isn is not None:
+            isn_s.wscale, isn_s.out = _lib.ptr(isn[0]), _lib.ptr(isn[1])
+            isn_s.valid_count = _lib.ptr(isn[2]) if len(isn) > 2 else None
+        _lib.check(self.lib.apex_ddqn_head(*args, hl, hp, pk, isn_s, _lib.stream_ptr()), "ddqn_head")
 
     def head_wgrad(self, Hon, dhead, g, prio=None, Hon_lo=None):
         B, A1 = dhead.shape
@@ -426,17 +447,18 @@ class HipBackend(TorchBackend):
                                             g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(),
                                             g["wv"].numel(), _lib.ptr(Hon_lo), _lib.stream_ptr()), "head_wgrad")
 
-    def actor_head(self, H, P, eps, ctr, seed, q_out, a_out):
+    def actor_head(self, H, P, eps, ctr, seed, q_out, a_out, H_lo=None):
         E, A = q_out.shape
         _lib.check(self.lib.apex_actor_head(H.data_ptr(), self._hp(P), E, A, eps.data_ptr(), int(seed),
                                             ctr.data_ptr(), q_out.data_ptr(), a_out.data_ptr(),
-                                            P["wv"].numel(), _lib.stream_ptr()), "actor_head")
+                                            P["wv"].numel(), _lib.ptr(H_lo), _lib.stream_ptr()), "actor_head")
 
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None):
+                  sample=None, pb_lo=None, wnorm=None):
         n = p32.numel()
         st = _lib.stream_ptr()
         lo = _lib.ptr(pb_lo)
+        wn = (wnorm[0].data_ptr(), int(wnorm[1]), int(wnorm[2])) if wnorm is not None else (None, 0, 0)
         if sample is not None and sample[0].use_hip:
             # the next batch's draw rides in the optimizer launch (csrc/sumtree.hip: rmsprop_sample_kernel)
             rp, B, out, nxt2 = sample
@@ -450,11 +472,11 @@ class HipBackend(TorchBackend):
             _lib.check(self.lib.apex_rmsprop_sample(
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
-                *rp.sample_launch_args(B, out, nxt2), lo, st), "rmsprop_sample")
+                *rp.sample_launch_args(B, out, nxt2), lo, *wn, st), "rmsprop_sample")
             return
         if sample is not None:
             self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,
-                           pb_lo=pb_lo)
+                           pb_lo=pb_lo, wnorm=wnorm)
             rp, B, out, nxt2 = sample
             rp.sample(B, out=out, nxt2=nxt2)
             return
@@ -463,12 +485,13 @@ class HipBackend(TorchBackend):
             _lib.check(self.lib.apex_rmsprop_step_np(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
                                                      pbf.data_ptr(), n, part.data_ptr(), npart, float(lr),
                                                      float(alpha), float(eps), float(clip), int(centered),
-                                                     norm_out.data_ptr(), lo, st), "rmsprop_np")
+                                                     norm_out.data_ptr(), lo, *wn, st), "rmsprop_np")
             return
         _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), n, partials.data_ptr(), st), "sqnorm")
         _lib.check(self.lib.apex_rmsprop_step(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
                                               pbf.data_ptr(), n, partials.data_ptr(), float(lr), float(alpha),
-                                              float(eps), float(clip), int(centered), norm_out.data_ptr(), lo, st),
+                                              float(eps), float(clip), int(centered), norm_out.data_ptr(), lo, *wn,
+                                              st),
                    "rmsprop")
 
     def cast_bf16(self, x32, hi, lo=None) -> None:

@@ -93,12 +93,18 @@ class Comm:
             dist.destroy_process_group()
 
     def abort(self) -> None:
-        """Failure path: abort the native communicator (outstanding collectives are
-        cancelled) so the process can exit and torchrun restart the group."""
+        """Failure path: abort the native communicator and the torch.distributed
+        process group (outstanding collectives are cancelled, ncclCommAbort under
+        RCCL) so the process can exit and torchrun restart the group."""
         native = getattr(self, "_native", None)
         if native is not None:
             native.abort()
             self._native = None
+        if dist.is_initialized():
+            try:
+                dist.distributed_c10d._abort_process_group()
+            except Exception:  # pragma: no cover - best effort on the failure path
+                pass
 
     # ------------------------------------------------------ collectives
     def allreduce_flat(self, flat: torch.Tensor, average: bool = True, async_op: bool = False):

@@ -77,10 +77,15 @@ def apex_uniform(seed: int, ctr: int, idx) -> np.ndarray:
     return (r >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
 
 
+# per-shard statistics all-gathered every DP step (csrc/sumtree.hip SHARD_STATS):
+# (sum p^alpha, min p^alpha, max IS weight of the shard's rows in the current batch)
+SHARD_STATS = 3
+
+
 def global_draw(stats: np.ndarray, rank: int, B: int, seed: int, ctr: int):
     """The sharded sampler's global stratified draw as seen by ``rank`` (mirror of
     csrc/sumtree.hip ``tree_sample_body``): returns (u_local (B,) float64, valid (B,)
-    bool, wscale, pmin_global) for the all-gathered ``stats`` [W, 2] = (total, min p)."""
+    bool, wscale, pmin_global) for the all-gathered ``stats`` [W, >=2] = (total, min p, ...)."""
     W = stats.shape[0]
     sm = c0 = tmax = 0.0
     pm = math.inf
@@ -193,17 +198,18 @@ class GpuReplayShard:
         d = self.device
         self.shard_rank, self.shard_world = int(rank), int(world)
         self.shard_seed, self.shard_group = int(shard_seed), group
-        self.local_stats = torch.zeros(2, dtype=torch.float64, device=d)
-        self.shard_stats = torch.zeros(2 * self.shard_world, dtype=torch.float64, device=d)
+        self.local_stats = torch.zeros(SHARD_STATS, dtype=torch.float64, device=d)
+        self.shard_stats = torch.zeros(SHARD_STATS * self.shard_world, dtype=torch.float64, device=d)
 
     @property
     def sharded(self) -> bool:
         return self.shard_stats is not None
 
     def gather_shard_stats(self, async_op: bool = False, coll=None):
-        """All-gather every shard's (sum p^alpha, min p^alpha) into ``shard_stats``
+        """All-gather every shard's (sum p^alpha, min p^alpha, batch IS max) into ``shard_stats``
         (a collective; device-side, HIP-graph capturable over RCCL).  Call it after
-        the last tree mutation that the next draw must see.  ``coll``: the learner's
+        the last tree mutation that the next draw must see (the third field is written
+        by the learner's head kernel: ``local_stats[2]``).  ``coll``: the learner's
         collectives (parallel/rccl.py; torch.distributed by default).  With
         ``async_op`` the returned handle's ``wait()`` orders the result."""
         from ..parallel.rccl import TorchCollectives
@@ -372,7 +378,7 @@ class GpuReplayShard:
         valid = np.ones(B, bool)
         wscale = 1.0
         if self.sharded:
-            st = self.shard_stats.double().cpu().numpy().reshape(self.shard_world, 2)
+            st = self.shard_stats.double().cpu().numpy().reshape(self.shard_world, SHARD_STATS)
             u, valid, wscale, pmin = global_draw(st, self.shard_rank, B, self.shard_seed, ctr)
             u = torch.from_numpy(u).clamp_(0.0, float(total))
         else:
@@ -400,6 +406,8 @@ class GpuReplayShard:
         out["act"].copy_(self.act[idx])
         out["rew"].copy_(self.rew[idx])
         out["gam"].copy_(self.gam[idx])
+        if "wscale" in out:
+            out["wscale"].fill_(wscale)
         if nxt2 is not None:
             nxt2.copy_(out["nxt"])
         return out
@@ -410,7 +418,8 @@ class GpuReplayShard:
         return (self.tree_desc(), self.record_desc(), B, self.seed, self.ctr.data_ptr(), self.beta,
                 out["idx"].data_ptr(), out["weights"].data_ptr(), out["gen"].data_ptr(), out["obs"].data_ptr(),
                 out["nxt"].data_ptr(), out["act"].data_ptr(), out["rew"].data_ptr(), out["gam"].data_ptr(),
-                _lib.ptr(nxt2), _lib.ptr(self.shard_stats), self.shard_rank, self.shard_world, self.shard_seed)
+                _lib.ptr(nxt2), _lib.ptr(self.shard_stats), self.shard_rank, self.shard_world, self.shard_seed,
+                _lib.ptr(out.get("wscale")))
 
     def alloc_sample_buffers(self, B: int) -> Dict[str, torch.Tensor]:
         d = self.device
@@ -421,7 +430,8 @@ class GpuReplayShard:
                     nxt=torch.zeros(B, self.C, dtype=torch.int32, device=d),
                     act=torch.zeros(B, dtype=torch.int32, device=d),
                     rew=torch.zeros(B, dtype=torch.float32, device=d),
-                    gam=torch.zeros(B, dtype=torch.float32, device=d))
+                    gam=torch.zeros(B, dtype=torch.float32, device=d),
+                    wscale=torch.ones(1, dtype=torch.float32, device=d))
 
     def gather_frames(self, slots: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """slots (B, C) int32 -> stacked frames (B, C, H, W) uint8 in natural pixel order."""
@@ -450,10 +460,13 @@ class GpuReplayShard:
                        "tree_update")
         else:
             idx_c = idx.long()
-            keep = torch.ones(n, dtype=torch.bool, device=idx.device)
-            # last occurrence wins
+            # rows of a sharded draw that fell in another shard (generation -1) write
+            # nothing and take no part in the dedupe
+            valid = torch.ones(n, dtype=torch.bool, device=idx.device) if gen is None else gen >= 0
+            keep = valid.clone()
+            # last occurrence (among the valid rows) wins
             for i in range(n):
-                if (idx_c[i + 1:] == idx_c[i]).any():
+                if keep[i] and (valid[i + 1:] & (idx_c[i + 1:] == idx_c[i])).any():
                     keep[i] = False
             keep &= self.leaf[idx_c] > 0
             if gen is not None:

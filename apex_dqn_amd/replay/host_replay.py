@@ -6,7 +6,9 @@ Reference parity (``replay.py:8-84``): ``add`` (:59), ``sample`` (:44),
 ``size`` (:82).  Intended semantics instead of the
 defects: P(i) = p_i^alpha / sum p^alpha through a sum-tree, IS weights
 w_i = (N P(i))^-beta / max_j w_j (``importance_sampling_exponent`` is never
-read by the reference), and eviction that also drops the priority (A5).
+read by the reference) -- max over the sampled batch (``is_normalise =
+"batch_max"``, the default) or over the whole replay (``"global_min"``) -- and
+eviction that also drops the priority (A5).
 """
 from __future__ import annotations
 
@@ -26,12 +28,15 @@ def _make_tree(cap: int) -> SumTree:
 class PrioritizedReplay:
     def __init__(self, soft_capacity: int, priority_exponent: float = 0.6,
                  importance_sampling_exponent: float = 0.4, capacity: Optional[int] = None,
-                 priority_eps: float = 1e-6, seed: int = 0):
+                 priority_eps: float = 1e-6, seed: int = 0, is_normalise: str = "batch_max"):
         self.soft_capacity = int(soft_capacity)
         self.cap = int(capacity or max(soft_capacity + 1, int(soft_capacity * 1.25)))
         self.alpha = float(priority_exponent)
         self.beta = float(importance_sampling_exponent)
         self.eps = float(priority_eps)
+        if is_normalise not in ("batch_max", "global_min"):
+            raise ValueError("is_normalise must be 'batch_max' or 'global_min'")
+        self.is_normalise = is_normalise
         self.tree = _make_tree(self.cap)
         self.rng = np.random.default_rng(seed)
         self.storage: Dict[str, np.ndarray] = {}
@@ -94,7 +99,7 @@ class PrioritizedReplay:
         N = self.live
         prob = p / total
         w = (N * prob) ** (-self.beta)
-        wmax = (N * pmin / total) ** (-self.beta)
+        wmax = w.max() if self.is_normalise == "batch_max" else (N * pmin / total) ** (-self.beta)
         out["weights"] = (w / wmax).astype(np.float32)
         out["idx"] = idx.astype(np.int64)
         out["prob"] = prob.astype(np.float32)

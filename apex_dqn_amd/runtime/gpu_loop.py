@@ -27,6 +27,10 @@ from ..replay.gpu_replay import GpuReplayShard
 from ..utils.metrics import MetricsLogger
 
 
+FILL_CHECK_EVERY = 16      # fill phase: group steps between readiness all-reduces (DP)
+WATCHDOG_EXIT_CODE = 75    # a multi-rank watchdog timeout exits the process with this code
+
+
 def build_replay(cfg: ApexConfig, device, num_envs: int, seed: int = 0, world: int = 1) -> GpuReplayShard:
     """This rank's shard of the global replay: ``soft_capacity / world`` transitions
     (the learners turn the shards into one prioritized replay, replay/gpu_replay.py)."""
@@ -123,13 +127,20 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
         async_actors = bool(rt.async_actors) and device.type == "cuda"
     t0 = time.time()
     st = _LoopState(t0, learner.num_q_updates)
-    # ---- fill: the actors alone until every shard holds min_replay_mem_size / world
+    # ---- fill: the actors alone until every shard holds min_replay_mem_size / world.
+    # With several ranks readiness is agreed on every FILL_CHECK_EVERY group steps (a
+    # host-blocking all-reduce per step would serialise the fill); every rank steps its
+    # group once per iteration, so all ranks reach the checks together.
+    it = 0
     while True:
         if st.actor_steps < max_actor_steps:
             group.step()
             st.actor_steps += 1
+        it += 1
         ready = float(replay.size() > min_local or st.actor_steps >= max_actor_steps)
         if comm is not None and comm.active:
+            if it % FILL_CHECK_EVERY:
+                continue
             ready = comm.allreduce_scalar(ready, "min")
         if ready >= 1.0:
             break
@@ -179,8 +190,9 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                     _learn(learner, k)
             else:
                 _learn(learner, k)
-            if runner is not None and on_cuda:
-                # at most two chunks queued: the actor's inserts never wait long behind them
+            if on_cuda:
+                # at most two chunks queued (the actor's inserts never wait long behind
+                # them); the wait is the step watchdog in both actor modes
                 ev = torch.cuda.Event()
                 ev.record()
                 inflight.append(ev)
@@ -247,14 +259,21 @@ def _restore_actor_rng(group, path: str) -> None:
 
 def _wait_event(ev, timeout: float, comm=None) -> None:
     """Wait for a queued learner chunk, at most ``timeout`` seconds (watchdog: a hung
-    kernel or collective fails the rank -- the native communicator is aborted first --
-    so torchrun's elastic restart resumes the group from the last checkpoint)."""
+    kernel or collective fails the rank -- the communicators are aborted first -- so
+    torchrun's elastic restart resumes the group from the last checkpoint).  With
+    several ranks the process exits at once (``os._exit``): a rank blocked in a hung
+    collective would otherwise hang again in the teardown."""
     deadline = time.time() + float(timeout)
     while not ev.query():
         if time.time() > deadline:
+            msg = f"learner step watchdog: queued GPU work did not finish in {timeout:.0f} s"
             if comm is not None and hasattr(comm, "abort"):
                 comm.abort()
-            raise RuntimeError(f"learner step watchdog: queued GPU work did not finish in {timeout:.0f} s")
+            if comm is not None and getattr(comm, "active", False):
+                sys.stderr.write(f"[rank {comm.rank}] {msg}; exiting for an elastic restart\n")
+                sys.stderr.flush()
+                os._exit(WATCHDOG_EXIT_CODE)
+            raise RuntimeError(msg)
         time.sleep(2e-4)
 
 
@@ -284,7 +303,8 @@ def _log(metrics, learner, group, replay, st: "_LoopState", rt, world: int, devi
     rets = [r for (_, _, r) in eps_list[-50:]]
     lens = [ln for (_, ln, _) in eps_list[-50:]]
     metrics.log("learner", step=n, loss=m["loss"], td_abs=m["td_abs_mean"], grad_norm=m["grad_norm"],
-                is_weight_mean=float(learner.S["weights"].mean()),
+                is_weight_mean=m.get("is_weight_mean", float(learner.S["weights"].mean())),
+                valid_rows=m.get("valid_rows", learner.B),
                 learner_kind=getattr(learner, "kind", "fused"),
                 replay=replay.size(), actor_steps=st.actor_steps, inserted=group.inserted,
                 episodes=len(eps_list),

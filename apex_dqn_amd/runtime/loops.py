@@ -61,7 +61,7 @@ def train_inline(cfg: ApexConfig, learner_steps: int, device="cpu",
     replay = PrioritizedReplay(cfg.Replay_Memory.soft_capacity, cfg.Replay_Memory.priority_exponent,
                                cfg.Replay_Memory.importance_sampling_exponent,
                                capacity=cfg.replay_capacity, priority_eps=cfg.Runtime.priority_eps,
-                               seed=cfg.Runtime.seed)
+                               seed=cfg.Runtime.seed, is_normalise=cfg.Runtime.is_normalise)
     learner = TorchLearner(cfg, device)
     actor_net = copy.deepcopy(learner.Q).eval()
     policy = _make_policy(actor_net, device)
@@ -154,7 +154,7 @@ def train_multiprocess(cfg: ApexConfig, learner_steps: int, num_procs: Optional[
     replay = PrioritizedReplay(cfg.Replay_Memory.soft_capacity, cfg.Replay_Memory.priority_exponent,
                                cfg.Replay_Memory.importance_sampling_exponent,
                                capacity=cfg.replay_capacity, priority_eps=cfg.Runtime.priority_eps,
-                               seed=cfg.Runtime.seed)
+                               seed=cfg.Runtime.seed, is_normalise=cfg.Runtime.is_normalise)
     episodes, losses, restarts = [], [], 0
     t0 = time.time()
     try:

@@ -27,8 +27,12 @@ warm-up read 1.5-2 % below a 400-step window, with it they agree within 0.5 %:
 updates between barrier + synchronize brackets; the max over ranks is reported.
 ``graph_captures_in_timed`` must be 0.
 
-``value`` = whole-job batch-512 gradient steps per second
-          = N x (data-parallel steps/s)  (each DP step consumes N x 512 samples).
+``value`` = whole-job batch-512 gradient steps per second.  One rank: steps/s.  With
+data parallelism a step's global batch is the M rows the ranks' shards actually
+drew (one global prioritized draw, M <= N (512 - 2): replay/gpu_replay.py), counted
+on the device by the head kernel: ``value`` = (sum of M over the timed steps) / 512
+/ time, reported with ``samples_per_dp_step`` (mean M) and ``value_nominal`` = N x
+(DP steps/s).
 """
 from __future__ import annotations
 
@@ -120,6 +124,9 @@ def measure(cfg, learner, replay, comm, warmup: int, steps: int, prep_warm: int 
     caps = learner.prepare_graphs() if hasattr(learner, "prepare_graphs") else 0
     if hasattr(learner, "rewarm"):
         learner.rewarm(prep_warm)     # state-preserving: no update is kept
+    vr = getattr(learner, "valid_rows_total", None)
+    if vr is not None:
+        vr.zero_()                    # DP: rows each rank actually drew, counted by the head kernel
     torch.cuda.synchronize()
     comm.barrier()
     torch.cuda.synchronize()
@@ -131,7 +138,12 @@ def measure(cfg, learner, replay, comm, warmup: int, steps: int, prep_warm: int 
     dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, "max") if comm.active else dt
     caps_after = getattr(learner, "graph_captures", 0)
+    dp = bool(getattr(learner, "_dp", False)) and vr is not None
+    valid = float(vr.item()) if dp else None
+    if dp and comm.active:
+        valid = comm.allreduce_scalar(valid, "sum")
     return dict(dt=dt, prep_graph_captures=int(caps), graph_captures_in_timed=int(caps_after - caps),
+                valid_rows=valid,
                 prep_warm_replays=int(prep_warm) if hasattr(learner, "rewarm") else 0,
                 metrics=learner.last_metrics())
 
@@ -206,6 +218,11 @@ def main():
     dt = res["dt"]
     ms = 1e3 * dt / args.steps
     value = args.steps / dt * world
+    # DP: a step's global batch is M = the rows the W ranks drew from their shards
+    # (<= W (B - 2), replay/gpu_replay.py); count batch-512 steps as M / 512 samples
+    samples_per_step = res["valid_rows"] / args.steps if res["valid_rows"] is not None else None
+    if samples_per_step is not None:
+        value = samples_per_step / args.batch * args.steps / dt
     m = res["metrics"]
     if rank == 0:
         kind = getattr(learner, "kind", "fused")
@@ -236,9 +253,16 @@ def main():
             "graph_captures_in_timed": res["graph_captures_in_timed"],
             "prep_warm_replays": res["prep_warm_replays"],
             "loss": round(m["loss"], 5), "grad_norm": round(m["grad_norm"], 5),
+            "is_weight_mean": round(m.get("is_weight_mean", float("nan")), 5),
         }
+        if samples_per_step is not None:
+            out["samples_per_dp_step"] = round(samples_per_step, 2)
+            out["value_nominal"] = round(args.steps / dt * world, 2)
         if extra is not None:
-            out["value_bf16"] = round(args.steps / extra["dt"] * world, 2)
+            vb = args.steps / extra["dt"] * world
+            if extra["valid_rows"] is not None:
+                vb = extra["valid_rows"] / args.batch / extra["dt"]
+            out["value_bf16"] = round(vb, 2)
             out["ms_per_step_bf16"] = round(1e3 * extra["dt"] / args.steps, 4)
             out["graph_captures_in_timed_bf16"] = extra["graph_captures_in_timed"]
         print(json.dumps(out), flush=True)

@@ -44,7 +44,7 @@ def _worker(rank, world, path, q, ar="fp32"):
     torch.manual_seed(1234 + rank)  # different local init: rank 0's params must be broadcast
     rp = _replay(rank)
     L = FusedNatureLearner(cfg, "cpu", rp, comm=comm)
-    stats = rp.shard_stats.view(world, 2).clone()
+    stats = rp.shard_stats.view(world, 3)[:, :2].clone()
     own = (rp.total(), rp.min_leaf())
     # the global draw of step 1 (what L.step() consumes: presampled, version unchanged)
     L._sample()
@@ -65,6 +65,7 @@ def _worker(rank, world, path, q, ar="fp32"):
     g_local = Lref.g32.clone()
     n_valid = int((L.S["gen"] >= 0).sum())
     L.step()
+    counted = int(L.valid_rows_total.item())     # the head's device-side count (bench.py's M)
     g_dp = L.g32.clone()
     for _ in range(3):
         L.step()
@@ -75,7 +76,7 @@ def _worker(rank, world, path, q, ar="fp32"):
     torch.distributed.all_gather(pl, L.p32.clone())
     perr = max([float((pl[0] - p).abs().max()) for p in pl[1:]], default=0.0)
     q.put((rank, float((g_dp - g_mean).abs().max()), float(g_mean.abs().max()), perr, stats.numpy(),
-           own, n_valid))
+           own, n_valid, counted))
     comm.shutdown()
 
 
@@ -96,7 +97,8 @@ def test_dp_learner_gloo(ar, world):
     tol = 1e-6 if ar == "fp32" else 1e-2          # bf16 payload: ~3 significant digits
     res.sort(key=lambda r: r[0])
     own = np.array([r[5] for r in res])
-    for rank, gerr, gmax, perr, stats, _, _ in res:
+    for rank, gerr, gmax, perr, stats, _, nv, counted in res:
+        assert counted == nv                          # the counted rows are the rows drawn
         assert gerr <= tol * max(gmax, 1e-6) + 1e-9, (rank, gerr, gmax)
         assert perr == 0.0
         # every rank holds every shard's (total, min p) in rank order

@@ -144,3 +144,52 @@ def test_split_mode_plumbing_matches_fp32_autograd():
     # the optimizer rewrites both planes: hi + lo == fp32 master to ~2^-17 relative
     L._seg3()
     torch.testing.assert_close(L.pbf.float() + L.pbf_lo.float(), L.p32, rtol=2e-5, atol=1e-9)
+
+
+def test_batch_max_is_normalisation_matches_autograd_on_normalised_weights():
+    """Runtime.is_normalise = batch_max (learner/is_norm.py): the fused step keeps the
+    sampler's global-min weights in the loss and divides the gradient by the batch's
+    largest weight inside the optimizer.  The update must equal centered RMSprop + clip
+    applied to the autograd gradient of the loss with weights w / max_batch(w)."""
+    import copy
+    from apex_dqn_amd.models.flat_params import reference_state_to_flat
+    from apex_dqn_amd.ops.fused_ops import TorchBackend
+    cfg, rp = _setup("huber")
+    rp.leaf[3] = 1e-6 ** 0.6          # a leaf at the priority floor: global-min weights are tiny
+    rp._torch_rebuild()
+    cfg = copy.deepcopy(cfg)
+    cfg.Runtime.is_normalise = "batch_max"
+    L = FusedNatureLearner(cfg, "cpu", rp)
+    T = TorchLearner(cfg, "cpu")
+    T.Q.load_state_dict(L.reference_state_dict())
+    T.Q_target.load_state_dict(L.reference_state_dict())
+    p0, v0, m0 = L.p32.clone(), L.rms_v.clone(), L.rms_m.clone()
+    L._seg1()
+    L._seg2()
+    B, S = L.B, L.S
+    w = S["weights"].clone()
+    assert float(w.max()) < 0.1                       # the floor leaf shrinks the global-min weights
+    batch = dict(S_t=L.frames[:B], S_tpn=L.frames[B:2 * B], A_t=S["act"], R=S["rew"], Gamma=S["gam"],
+                 weights=w / w.max())
+    lref, _ = T.compute_loss_and_priorities(batch)
+    T.optimizer.zero_grad()
+    lref.backward()
+    g_ref = torch.zeros_like(L.g32)
+    reference_state_to_flat({k: p.grad for k, p in T.Q.named_parameters()}, L.layout.views(g_ref))
+    L._seg3()
+    assert abs(L.is_scale() - 1.0 / float(w.max())) < 1e-6 / float(w.max())
+    rt = cfg.Runtime
+    p, v, m = p0.clone(), v0.clone(), m0.clone()
+    nrm = torch.zeros(1)
+    TorchBackend()._optimizer(p, g_ref, v, m, p.clone(), rt.lr, rt.rms_decay, rt.rms_eps, rt.grad_clip,
+                              rt.centered_rmsprop, nrm)
+    # the clip norm is the norm of the batch-max gradient (20x+ the global-min one here:
+    # the scale is visible there -- a centered RMSprop step itself is nearly invariant
+    # to a constant gradient scale, up to eps)
+    torch.testing.assert_close(L.gnorm, nrm, rtol=1e-4, atol=1e-9)
+    assert float(L.gnorm) > 10 * float(L.g32.double().norm())
+    # updates agree to 0.1 % of the per-step move lr / sqrt(alpha (1 - alpha))
+    step = rt.lr / (rt.rms_decay * (1 - rt.rms_decay)) ** 0.5
+    torch.testing.assert_close(L.p32 - p0, p - p0, rtol=0, atol=1e-3 * step)
+    met = L.last_metrics()
+    assert abs(met["is_weight_mean"] - float((w / w.max()).mean())) < 1e-5

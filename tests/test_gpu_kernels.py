@@ -96,7 +96,7 @@ def test_sharded_sample_hip_matches_global_draw():
     rps = [GpuReplayShard(4096, 4096, 4200, 4, device=DEV, alpha=0.6, beta=0.4, seed=r) for r in range(W)]
     for r, rp in enumerate(rps):
         _fill_replay(rp, 700 + 900 * r, seed=r)
-    stats = torch.tensor([[rp.total(), rp.min_leaf()] for rp in rps], dtype=torch.float64)
+    stats = torch.tensor([[rp.total(), rp.min_leaf(), 0.0] for rp in rps], dtype=torch.float64)
     n_valid = 0
     for r, rp in enumerate(rps):
         rp.enable_sharding(r, W, seed)
@@ -134,6 +134,39 @@ def test_sumtree_update_duplicates_last_wins_and_generation():
     assert float(rp.leaf[5]) == pytest.approx(7.0)
     assert float(rp.leaf[7]) == pytest.approx(2.0)
     assert float(rp.leaf[9]) == pytest.approx(old9)
+    leaf = rp.leaf.double().cpu().numpy()
+    assert abs(rp.total() - leaf.sum()) / leaf.sum() < 1e-9
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_sumtree_update_foreign_rows_do_not_win_the_dedupe(fused):
+    """Sharded draws: rows that fell in another shard (generation -1) sit on the first
+    live leaf; a VALID row that drew that leaf before them keeps its new priority --
+    through the stand-alone tree update and the block update of the fused head-wgrad
+    launch (csrc/sumtree.hip tree_update_block)."""
+    from apex_dqn_amd.ops.fused_ops import HipBackend
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(1000, 1000, 1200, 4, device=DEV, alpha=1.0, eps=0.0)
+    _fill_replay(rp, 900)
+    B = 64
+    idx = torch.arange(B, dtype=torch.int64, device=DEV) + 10
+    idx[3] = 0                                    # a valid draw of leaf 0 ...
+    idx[40:] = 0                                  # ... and 24 foreign rows on it afterwards
+    gen = rp.gen[idx].clone()
+    gen[40:] = -1
+    td = torch.rand(B, device=DEV) + 0.5
+    if fused:
+        A = 4
+        H = torch.rand(B, 1024, device=DEV).to(torch.bfloat16)
+        dhead = torch.randn(B, A + 1, device=DEV) * 1e-3
+        g = {"wv": torch.zeros(512, device=DEV), "bv": torch.zeros(1, device=DEV),
+             "wa": torch.zeros(A, 512, device=DEV), "ba": torch.zeros(A, device=DEV)}
+        HipBackend().head_wgrad(H, dhead, g, prio=(rp, idx, gen, td))
+    else:
+        rp.update_priorities(idx, td, gen)
+    torch.cuda.synchronize()
+    assert float(rp.leaf[0]) == pytest.approx(float(td[3]), rel=1e-6)
+    assert torch.allclose(rp.leaf[idx[:40]], td[:40].abs(), rtol=1e-6)
     leaf = rp.leaf.double().cpu().numpy()
     assert abs(rp.total() - leaf.sum()) / leaf.sum() < 1e-9
 
@@ -221,7 +254,8 @@ def test_rmsprop_sample_matches_separate_launches(sharded):
     if sharded:
         rp.enable_sharding(1, 3, 99)
         t = rp.total()
-        rp.shard_stats.copy_(torch.tensor([0.7 * t, 0.05, t, rp.min_leaf(), 1.6 * t, 0.2], dtype=torch.float64))
+        rp.shard_stats.copy_(torch.tensor([0.7 * t, 0.05, 0.0, t, rp.min_leaf(), 0.0, 1.6 * t, 0.2, 0.0],
+                                          dtype=torch.float64))
     be = HipBackend()
     res = {}
     for fused in (False, True):

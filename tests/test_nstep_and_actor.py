@@ -84,3 +84,16 @@ def test_actor_group_cartpole_and_frames():
     b2 = g2.drain()
     assert b2["S_t"].shape[1:] == (4, 84, 84) and b2["S_t"].dtype == np.uint8
     assert np.all(g2.eps <= 0.4)
+
+
+def test_interleaved_epsilon_ladder_over_ranks():
+    """Env i of rank r is actor i * W + r of the global ladder: every rank holds a mix of
+    exploratory and greedy actors, and the union over ranks is the whole ladder."""
+    from apex_dqn_amd.actors.gpu_actor import ladder_slice
+    from apex_dqn_amd.config import ApexConfig, epsilon_ladder
+    cfg = ApexConfig()
+    W, E = 4, 8
+    sl = [ladder_slice(cfg, E, r, W) for r in range(W)]
+    full = epsilon_ladder(W * E, cfg.Actor.epsilon, cfg.Actor.alpha)
+    assert sorted(sum(sl, [])) == sorted(full)
+    assert all(max(s) > 0.1 and min(s) < 0.01 for s in sl)

@@ -55,7 +55,7 @@ def _batch(K, rng, obs_dim=4):
 
 def test_host_replay_semantics():
     rng = np.random.default_rng(0)
-    r = PrioritizedReplay(100, 0.6, 0.4, capacity=150)
+    r = PrioritizedReplay(100, 0.6, 0.4, capacity=150, is_normalise="global_min")
     r.add(_batch(120, rng))
     assert r.size() == 120
     s = r.sample(32)
@@ -69,6 +69,27 @@ def test_host_replay_semantics():
     assert np.all(r.tree.get(np.arange(5)) == 0)
     for _ in range(10):  # never samples evicted slots
         assert np.all(r.sample(64)["idx"] >= 20)
+
+
+def test_host_replay_is_normalise_modes():
+    """batch_max: w_i = (N P(i))^-beta / max over the sampled batch (max weight exactly 1);
+    global_min: / max over the whole replay = (p_i / p_min)^-beta (numpy oracle)."""
+    rng = np.random.default_rng(1)
+    b = _batch(200, rng)
+    b["priority"][0] = 0.0           # one leaf at the priority floor: p_min = eps^alpha
+    for mode in ("batch_max", "global_min"):
+        r = PrioritizedReplay(500, 0.6, 0.4, capacity=600, seed=3, is_normalise=mode)
+        r.add(b)
+        s = r.sample(64)
+        leaf = r.tree.get(s["idx"])
+        N, tot = r.size(), r.tree.total
+        w = (N * leaf / tot) ** -0.4
+        ref = w / (w.max() if mode == "batch_max" else (N * r.tree.min_positive / tot) ** -0.4)
+        np.testing.assert_allclose(s["weights"], ref, rtol=1e-5)
+        if mode == "batch_max":
+            assert abs(s["weights"].max() - 1.0) < 1e-6 and s["weights"].mean() > 0.2
+        else:
+            assert s["weights"].mean() < 0.05    # the floor leaf shrinks every weight
 
 
 def _shard_fill(rp, K, seed=0):

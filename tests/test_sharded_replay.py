@@ -18,7 +18,7 @@ import torch.multiprocessing as mp
 from scipy import stats as sstats
 
 from apex_dqn_amd.config import ApexConfig
-from apex_dqn_amd.replay.gpu_replay import GpuReplayShard, apex_uniform, global_draw
+from apex_dqn_amd.replay.gpu_replay import SHARD_STATS, GpuReplayShard, apex_uniform, global_draw
 
 ALPHA, BETA = 0.6, 0.4
 
@@ -35,7 +35,7 @@ def _shard(rank, n_items, scale, seed=0):
 def _link(shards, seed=77):
     """The all-gather, emulated in one process: every shard gets every shard's stats."""
     W = len(shards)
-    st = torch.tensor([[s.total(), s.min_leaf()] for s in shards], dtype=torch.float64).reshape(-1)
+    st = torch.tensor([[s.total(), s.min_leaf(), 0.0] for s in shards], dtype=torch.float64).reshape(-1)
     for r, s in enumerate(shards):
         s.enable_sharding(r, W, seed)
         s.shard_stats.copy_(st)
@@ -71,7 +71,7 @@ def test_global_sampling_distribution_chi2(W):
             v = (out["gen"] >= 0).numpy()
             M_seen += int(v.sum())
             np.add.at(counts, offs[r] + out["idx"].numpy()[v], 1.0)
-        st = shards[0].shard_stats.view(W, 2).numpy()
+        st = shards[0].shard_stats.view(W, SHARD_STATS)[:, :2].numpy()
         M = min(W * B, int(np.floor((B - 2) * st[:, 0].sum() / st[:, 0].max())))
         assert M_seen == M          # each global draw in exactly one shard
         n_draws += M
@@ -89,7 +89,7 @@ def test_sharded_is_weights_use_global_min_and_batch_correction():
     _link(shards)
     W, B = 2, 16
     pmin = min(s.min_leaf() for s in shards)
-    st = shards[0].shard_stats.view(W, 2).numpy()
+    st = shards[0].shard_stats.view(W, SHARD_STATS)[:, :2].numpy()
     M = min(W * B, int(np.floor((B - 2) * st[:, 0].sum() / st[:, 0].max())))
     for r, s in enumerate(shards):
         out = s.sample(B)
@@ -98,6 +98,21 @@ def test_sharded_is_weights_use_global_min_and_batch_correction():
         w_exp = torch.clamp((p / pmin) ** -BETA, max=1.0) * (W * B / M)
         torch.testing.assert_close(out["weights"][v].double(), w_exp[v], rtol=1e-5, atol=1e-7)
         assert torch.all(out["weights"][~v] == 0)
+
+
+def test_sharded_priority_writeback_ignores_foreign_rows():
+    """A row of a sharded draw that fell in another shard (generation -1) sits on the
+    first live leaf (u = 0); a VALID row that drew the same leaf earlier in the batch
+    must keep its new priority (the foreign row takes no part in the last-writer dedupe)."""
+    rp = _shard(0, 20, 1.0)
+    idx = torch.tensor([0, 5, 0, 0], dtype=torch.int64)
+    gen = rp.gen[idx].clone()
+    gen[2:] = -1                      # two foreign rows on leaf 0, after the valid one
+    td = torch.tensor([3.0, 0.5, 9.0, 9.0])
+    rp.update_priorities(idx, td, gen)
+    want = (3.0 + rp.eps) ** ALPHA
+    assert abs(float(rp.leaf[0]) - want) < 1e-5 * want
+    assert abs(float(rp.leaf[5]) - (0.5 + rp.eps) ** ALPHA) < 1e-5
 
 
 def test_global_draw_partition_is_rank_consistent():
@@ -125,7 +140,7 @@ def _gloo_worker(rank, world, path, q):
         rp.ctr.fill_(it)
         out = rp.sample(12)
         res.append(int((out["gen"] >= 0).sum()))
-    q.put((rank, rp.shard_stats.view(world, 2).numpy().copy(), (rp.total(), rp.min_leaf()), res))
+    q.put((rank, rp.shard_stats.view(world, SHARD_STATS)[:, :2].numpy().copy(), (rp.total(), rp.min_leaf()), res))
     comm.shutdown()
 
 
