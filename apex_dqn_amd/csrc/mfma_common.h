@@ -159,7 +159,7 @@ __device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, 
 }
 
 // s_waitcnt vmcnt(n) for a run-time n (immediate operand: one branch per value;
-// n is wave-uniform, larger values clamp to 63 = no wait)
+// n is wave-uniform, values >= 63 = no wait)
 __device__ __forceinline__ void vmcnt_le(int n) {
 #define APEX_VMCNT_CASE(k) \
   case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
@@ -171,7 +171,12 @@ __device__ __forceinline__ void vmcnt_le(int n) {
     APEX_VMCNT_CASE(20) APEX_VMCNT_CASE(21) APEX_VMCNT_CASE(22) APEX_VMCNT_CASE(23) APEX_VMCNT_CASE(24)
     APEX_VMCNT_CASE(25) APEX_VMCNT_CASE(26) APEX_VMCNT_CASE(27) APEX_VMCNT_CASE(28) APEX_VMCNT_CASE(29)
     APEX_VMCNT_CASE(30) APEX_VMCNT_CASE(31) APEX_VMCNT_CASE(32) APEX_VMCNT_CASE(33) APEX_VMCNT_CASE(34)
-    APEX_VMCNT_CASE(35) APEX_VMCNT_CASE(36)
+    APEX_VMCNT_CASE(35) APEX_VMCNT_CASE(36) APEX_VMCNT_CASE(37) APEX_VMCNT_CASE(38) APEX_VMCNT_CASE(39)
+    APEX_VMCNT_CASE(40) APEX_VMCNT_CASE(41) APEX_VMCNT_CASE(42) APEX_VMCNT_CASE(43) APEX_VMCNT_CASE(44)
+    APEX_VMCNT_CASE(45) APEX_VMCNT_CASE(46) APEX_VMCNT_CASE(47) APEX_VMCNT_CASE(48) APEX_VMCNT_CASE(49)
+    APEX_VMCNT_CASE(50) APEX_VMCNT_CASE(51) APEX_VMCNT_CASE(52) APEX_VMCNT_CASE(53) APEX_VMCNT_CASE(54)
+    APEX_VMCNT_CASE(55) APEX_VMCNT_CASE(56) APEX_VMCNT_CASE(57) APEX_VMCNT_CASE(58) APEX_VMCNT_CASE(59)
+    APEX_VMCNT_CASE(60) APEX_VMCNT_CASE(61) APEX_VMCNT_CASE(62)
     default: break;
   }
 #undef APEX_VMCNT_CASE

@@ -248,12 +248,17 @@ class FusedNatureLearner(IsNormMixin):
         sp = self.split
         n = 3 * B
         # c2f: conv2's weights packed for its forward in the same launch (csrc/conv2_wfrag.h)
-        c2f = (Pb["w2"], Pl["w2"], Tb["w2"], Tl["w2"]) if sp else (Pb["w2"], None, Tb["w2"], None)
-        ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
-                           Tb["w1"], T["b1"], 2 * B, c2f=c2f,
-                           **self._lo(w32=P["w1"], w2_32=T["w1"], out_lo=self.y1_lo))
-        ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B,
-                     **self._lo(x_lo=self.y1_lo, w_lo=sp and Pl["w2"], w2_lo=sp and Tl["w2"], out_lo=self.y2_lo))
+        if sp:
+            # conv1 -> conv2 in one launch, y1 kept in LDS; only the S_t rows' y1 (the
+            # backward's input) is written out (csrc/conv12_fused.hip)
+            ops.conv12_fwd(self.replay.frames, self.slots, self.frames, rt.obs_scale, self.y1, self.y1_lo, self.y2,
+                           self.y2_lo, (P["w1"], P["b1"], T["w1"], T["b1"]),
+                           (Pb["w2"], Pl["w2"], P["b2"], Tb["w2"], Tl["w2"], T["b2"]), rows_first=2 * B, copy_n=B)
+        else:
+            c2f = (Pb["w2"], None, Tb["w2"], None)
+            ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
+                               Tb["w1"], T["b1"], 2 * B, c2f=c2f)
+            ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B)
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
                      **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
         ops.fc_fwd(self.y3.reshape(n, 3136), Pb["wfc"], P["bfc"], self.h, Tb["wfc"], T["bfc"], 2 * B,

@@ -72,6 +72,18 @@ class TorchBackend:
             self.conv1_fwd(frames[:r], wa, b, scale, out[:r], None if out_lo is None else out_lo[:r])
             self.conv1_fwd(frames[r:], wb, b2, scale, out[r:], None if out_lo is None else out_lo[r:])
 
+    def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None):
+        """conv1 -> conv2 in split mode: ``c1 = (w1 fp32, b1, w1 target, b1 target)``, ``c2 =
+        (w2, w2_lo, b2, w2 target, w2_lo target, b2 target)`` (target entries None: one
+        set).  y1 rows < ``copy_n`` must hold conv1's output afterwards (the backward's
+        input); the HIP backend keeps the other rows in LDS (csrc/conv12_fused.hip)."""
+        w1, b1, w1b, b1b = c1
+        w2, w2l, b2, w2b, w2bl, b2b = c2
+        self.conv1_fwd_ring(ring, slots, frames_buf, w1.to(y1.dtype), b1, scale, y1,
+                            None if w1b is None else w1b.to(y1.dtype), b1b, rows_first, w32=w1, w2_32=w1b,
+                            out_lo=y1_lo)
+        self.conv_fwd(y1, w2, b2, 2, y2, w2b, b2b, rows_first, x_lo=y1_lo, w_lo=w2l, w2_lo=w2bl, out_lo=y2_lo)
+
     def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
                  out_lo=None):
         dt = torch.float32 if x_lo is not None else self.dtype
@@ -299,6 +311,16 @@ class HipBackend(TorchBackend):
                         out_lo=out_lo, c2f=c2f)
         if c2f is not None:   # this step's split conv2 forward finds its weights packed
             self._c2f_packed = tuple(_lib.ptr(t) for t in c2f)
+
+    def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None):
+        if not (self.native_conv and C.CONV12_FUSED and hasattr(self.lib, "apex_conv12_fused_fwd")):
+            return super().conv12_fwd(ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first,
+                                      copy_n)
+        w1, b1, w1b, b1b = c1
+        w2, w2l, b2, w2b, w2bl, b2b = c2
+        n = slots.shape[0] if copy_n is None else int(copy_n)
+        C.conv12_fused_fwd(self.lib, self.ws, ring, slots, w1, b1, w2, w2l, b2, scale, y2, y2_lo, y1=y1, y1_lo=y1_lo,
+                           copy_n=n, w1b=w1b, b1b=b1b, w2b=w2b, w2b_lo=w2bl, b2b=b2b, rows_first=rows_first)
 
     def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
                  out_lo=None):

@@ -1,0 +1,90 @@
+#!/usr/bin/env python
+"""Phase timing of the fused conv1 -> conv2 kernel (csrc/conv12_fused.hip) from its
+in-kernel s_memtime probes (diagnostic library, PROBE in csrc/mfma_common.h), plus
+wall time of the release kernel for a few variants (copy_n, grid).
+Phases per image: conv1 (MFMA loop), wait+barrier+copy-out, conv2 (MFMA loop),
+tail (reduction, y2 epilogue, barriers, next DMA issue)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def setup(B, dev):
+    g = torch.Generator(device=dev).manual_seed(0)
+    N = 3 * B
+    ring = torch.randint(0, 256, (20000, 84, 84), device=dev, dtype=torch.uint8, generator=g)
+    slots = torch.randint(0, 20000, (N, 4), device=dev, dtype=torch.int32, generator=g)
+    w1 = torch.randn(64, 4, 8, 8, device=dev, generator=g) * 0.05
+    w2 = torch.randn(64, 4, 4, 64, device=dev, generator=g) * 0.03
+    w2h = w2.to(torch.bfloat16)
+    w2l = (w2 - w2h.float()).to(torch.bfloat16)
+    b = torch.randn(64, device=dev, generator=g) * 0.1
+    y1 = torch.empty(B, 20, 20, 64, device=dev, dtype=torch.bfloat16)
+    y1l = torch.empty_like(y1)
+    y2 = torch.empty(N, 9, 9, 64, device=dev, dtype=torch.bfloat16)
+    y2l = torch.empty_like(y2)
+    return dict(ring=ring, slots=slots, w1=w1, w2h=w2h, w2l=w2l, b=b, y1=y1, y1l=y1l, y2=y2, y2l=y2l, N=N)
+
+
+def launch(lib, C, ws, t, B, copy=True, grid=0, probe=None):
+    C.conv12_fused_fwd(lib, ws, t["ring"], t["slots"], t["w1"], t["b"], t["w2h"], t["w2l"], t["b"], 1 / 255.0,
+                       t["y2"], t["y2l"], y1=t["y1"], y1_lo=t["y1l"], copy_n=B if copy else 0, w1b=t["w1"],
+                       b1b=t["b"], w2b=t["w2h"], w2b_lo=t["w2l"], b2b=t["b"], rows_first=2 * B, grid=grid,
+                       probe=probe)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=512)
+    ap.add_argument("--probe", action="store_true")
+    a = ap.parse_args()
+    if a.probe:
+        os.environ["APEX_DEBUG_BOUNDS"] = "1"
+    from apex_dqn_amd.ops import _lib, conv as C
+    lib = _lib.require_kernels()
+    dev = torch.device("cuda", 0)
+    t = setup(a.B, dev)
+    ws = C.Workspace()
+    if a.probe:
+        buf = torch.zeros(4 * 4 * 16 * 4, dtype=torch.int64, device=dev)
+        for _ in range(3):
+            launch(lib, C, ws, t, a.B)
+        buf.zero_()
+        launch(lib, C, ws, t, a.B, probe=buf)
+        torch.cuda.synchronize()
+        st = buf.cpu().numpy().reshape(4, 4, 16, 4)
+        names = ["conv1", "wait_copy", "conv2"]
+        for it in range(16):
+            row = st[:, :, it, :]
+            if not np.all(row > 0):
+                continue
+            rec = {"it": it}
+            for k in range(1, 4):
+                rec[names[k - 1]] = int(np.median(row[:, :, k] - row[:, :, k - 1]))
+            if it + 1 < 16 and np.all(st[:, :, it + 1, 0] > 0):
+                rec["tail"] = int(np.median(st[:, :, it + 1, 0] - row[:, :, 3]))
+            print(json.dumps(rec))
+        return
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for name, kw in (("copy", dict(copy=True)), ("nocopy", dict(copy=False)), ("copy_g240", dict(copy=True, grid=240))):
+        for _ in range(5):
+            launch(lib, C, ws, t, a.B, **kw)
+        ts = []
+        for _ in range(20):
+            ev[0].record()
+            launch(lib, C, ws, t, a.B, **kw)
+            ev[1].record()
+            torch.cuda.synchronize()
+            ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
+        print(json.dumps({"variant": name, "us_median": round(float(np.median(ts)), 1),
+                          "us_min": round(float(np.min(ts)), 1)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -409,3 +409,56 @@ def test_conv2_fwd_weights_packed_in_conv1_launch(grid_images, split):
     assert torch.equal(outs[0][0], outs[1][0])
     if split:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("N,switch,copy_n,C,grid", [(1536, 1024, 512, 4, 0), (96, 64, 32, 4, 0), (37, 20, 9, 4, 5),
+                                                    (50, 50, 50, 1, 0), (40, 24, 0, 2, 7)])
+def test_conv12_fused_split_vs_fp64_and_separate_kernels(N, switch, copy_n, C, grid):
+    """conv1 -> conv2 fused (csrc/conv12_fused.hip: y1 kept in LDS, conv2 weights streamed
+    from L2 in fragment order) against fp64 and against the two separate split kernels:
+    the online / target switch inside a workgroup's range (small grids), the S_t rows'
+    y1 written out (copy_n), C in {1, 2, 4}."""
+    from apex_dqn_amd.ops import conv as C_
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    g = torch.Generator(device="cpu").manual_seed(N + C)
+    raw = torch.randint(0, 256, (80, 84, 84), generator=g, dtype=torch.uint8)
+    ring = to_s2d(raw.to(DEV))
+    slots = torch.randint(0, 80, (N, C), generator=g, dtype=torch.int32).to(DEV)
+    w1a, w1b = (torch.randn(64, C, 8, 8, generator=g) * 0.05).to(DEV), (torch.randn(64, C, 8, 8, generator=g) * 0.05).to(DEV)
+    b1a, b1b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    w2a, w2b = torch.randn(64, 4, 4, 64, generator=g) * 0.03, torch.randn(64, 4, 4, 64, generator=g) * 0.03
+    b2a, b2b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    (w2ah, w2al), (w2bh, w2bl) = _split(w2a), _split(w2b)
+    scale = 1 / 255.0
+    ws = C_.Workspace()
+    y2h, y2l = _empty2(N, 9, 9, 64)
+    y1h, y1l = _empty2(max(copy_n, 1), 20, 20, 64)
+    two = switch < N
+    kw2 = dict(w1b=w1b, b1b=b1b, w2b=w2bh, w2b_lo=w2bl, b2b=b2b, rows_first=switch) if two else {}
+    C_.conv12_fused_fwd(_lib(), ws, ring, slots, w1a, b1a, w2ah, w2al, b2a, scale, y2h, y2l, y1=y1h, y1_lo=y1l,
+                        copy_n=copy_n, grid=grid, **kw2)
+    torch.cuda.synchronize()
+    # fp64 reference
+    fr = torch.stack([raw[slots[i].long().cpu()] for i in range(N)]).double() * scale
+    ref1 = torch.empty(N, 64, 20, 20, dtype=torch.float64)
+    for lo, hi, w, b in ((0, switch, w1a, b1a), (switch, N, w1b, b1b)):
+        if hi > lo:
+            ref1[lo:hi] = torch.relu(torch.nn.functional.conv2d(fr[lo:hi], _c(w), _c(b), stride=4))
+    x1 = ref1.permute(0, 2, 3, 1)      # NHWC
+    ref2 = torch.cat([R.conv_fwd(x1[:switch], _c(w2a), _c(b2a), 2, torch.float64)] +
+                     ([R.conv_fwd(x1[switch:], _c(w2b), _c(b2b), 2, torch.float64)] if two else []))
+    assert _rel(_join(y2h, y2l), ref2) < TOL, _rel(_join(y2h, y2l), ref2)
+    if copy_n:
+        assert _rel(_join(y1h, y1l)[:copy_n], x1[:copy_n]) < TOL
+    # the separate split kernels on the same data (conv1 -> HBM -> conv2)
+    s1h, s1l = _empty2(N, 20, 20, 64)
+    s2h, s2l = _empty2(N, 9, 9, 64)
+    C_.conv1_s2d_fwd(_lib(), ws, ring, slots, w1a.to(torch.bfloat16), b1a, scale, s1h,
+                     w1b.to(torch.bfloat16) if two else None, b1b if two else None, switch if two else 0,
+                     w32=w1a, w2_32=w1b if two else None, out_lo=s1l)
+    C_.conv2_img_fwd(_lib(), s1h, w2ah, b2a, s2h, w2bh if two else None, b2b if two else None, switch if two else 0,
+                     x_lo=s1l, w_lo=w2al, w2_lo=w2bl if two else None, out_lo=s2l)
+    torch.cuda.synchronize()
+    assert _rel(_join(y2h, y2l), _join(s2h, s2l)) < TOL
+    if copy_n:
+        assert _rel(_join(y1h, y1l)[:copy_n], _join(s1h, s1l)[:copy_n]) < 1e-5
