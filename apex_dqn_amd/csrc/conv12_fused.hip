@@ -45,13 +45,8 @@
 #define CF_MAXIMG 64         // images per workgroup (slot table)
 #define CF_FRAME 7056        // s2d frame: 441 blocks of 16 B
 #define CF_LO_SCALE 4096.f
-#define CF_NY2 12            // y2 epilogue store instructions per wave and image (3 mt x 2 jq x 2 planes)
+#define CF_NY2 12            // y2 store instructions per wave and image (3 mt x 2 jh x 2 planes)
 #define CF_WAHEAD 3          // conv2 weight fragments in flight ahead of their MFMAs (K steps)
-
-// both conv2 weight sets -> C2F fragment order (csrc/conv2_wfrag.h), when not packed yet
-__global__ void __launch_bounds__(256) cf_pack_c2f_kernel(C2fPack p) {
-  c2f_pack_range(p, blockIdx.x * 256 + threadIdx.x, 4 * C2F_FRAGS);
-}
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -74,12 +69,83 @@ struct Conv12Desc {
   bf16_t* y1_lo;
   bf16_t* y2;              // [N][9][9][64] hi / lo
   bf16_t* y2_lo;
-  const uint8_t* zero16;   // >= 16 zero bytes (DMA source of the staging tail)
+  uint4* w1frag;           // conv1 f16 hi / lo fragments + folded biases of both sets (CF_W1FRAG_U4
+                           // uint4), written by cf_pack_kernel ahead of the fused launch
   uint8_t* scratch;        // >= 512 B: target of the y2 stores of padding pixels
   int N, C, img_switch, copy_n;
   float in_scale;
   uint64_t* probe;         // phase stamps (diagnostic build, csrc/mfma_common.h PROBE), or null
 };
+
+// conv1 fragments per (set, cp, nt, K step s, hi / lo) as 64 lanes x 16 B, then the folded
+// biases per (set, cp, nt) x 64 lanes (float4)
+#define CF_W1FRAG(C_) (2 * 2 * 2 * 2 * (C_) * 2 * 64)
+#define CF_W1FRAG_U4 (CF_W1FRAG(4) + 2 * 2 * 2 * 64)
+
+// One launch ahead of the fused kernel: blocks [0, nc2f) pack both conv2 weight sets into
+// C2F fragment order (csrc/conv2_wfrag.h; nc2f = 0 when the step packed them already), the
+// last block the conv1 operands of both sets exactly as the MFMA lanes consume them:
+// lane (g, pl) of wave role cp, tile nt, K step s holds channel 32 cp + 16 nt + pl, K
+// 32 s + 8 g .. + 7 (s2d K order k = (tap C + c) 16 + r4 4 + c4, tap = 2 a + b) as f16
+// hi + lo * 2^-12 of w * in_scale, and the bias the hi accumulation chain starts from:
+// bias - 1024 * sum_k w16[n][k] (pixels enter the MFMAs as 1024 + x).  Per workgroup this
+// replaces ~13k cycles of loads and conversions at each weight-set switch by 34 loads.
+struct CfPack {
+  C2fPack c2f;
+  int nc2f;                // C2F blocks
+  const float* w1[2];      // fp32 OIHW [64][C][8][8] (set 1 may be null)
+  const float* b1[2];
+  float in_scale;
+  uint4* w1frag;
+};
+
+template <int C>
+__global__ void __launch_bounds__(256) cf_pack_kernel(CfPack p) {
+  if ((int)blockIdx.x < p.nc2f) {
+    c2f_pack_range(p.c2f, blockIdx.x * 256 + threadIdx.x, 4 * C2F_FRAGS);
+    return;
+  }
+  const int t = threadIdx.x, set = t >> 7, cp = (t >> 6) & 1, lane = t & 63;
+  const int g = lane >> 4, pl = lane & 15;
+  const float* W1 = p.w1[set];
+  if (W1 == nullptr) return;                          // (whole waves)
+  const float sc = p.in_scale;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = 32 * cp + 16 * nt + pl;
+    float ws = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2 * C; ++s) {
+      const int q = 2 * s + (g >> 1), tap = q / C, c = q - tap * C, h = g & 1;
+      const int kh = 4 * (tap >> 1) + 2 * h, kw = 4 * (tap & 1);
+      const float4 r0 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh) * 8 + kw);
+      const float4 r1 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh + 1) * 8 + kw);
+      const float w8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      f16x8 hv, lv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float w = w8[j] * sc;                    // the input scale rides in the weights
+        const _Float16 hi = (_Float16)w;
+        const _Float16 lo = (_Float16)((w - (float)hi) * CF_LO_SCALE);
+        hv[j] = hi;
+        lv[j] = lo;
+        ws += (float)hi + (float)lo * (1.f / CF_LO_SCALE);
+      }
+      uint4* o = p.w1frag + ((((set * 2 + cp) * 2 + nt) * 2 * C + s) * 2) * 64 + lane;
+      o[0] = __builtin_bit_cast(uint4, hv);
+      o[64] = __builtin_bit_cast(uint4, lv);
+    }
+    // channel sums over the four K-group lanes; lane (g, .) takes channels 4 g + i
+    ws += __shfl_xor(ws, 16, 64);
+    ws += __shfl_xor(ws, 32, 64);
+    float c4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c4[i] = __shfl(ws, 4 * g + i, 64);
+    const float4 bb = *reinterpret_cast<const float4*>(p.b1[set] + 32 * cp + 16 * nt + 4 * g);
+    reinterpret_cast<float4*>(p.w1frag + CF_W1FRAG(4))[((set * 2 + cp) * 2 + nt) * 64 + lane] =
+        make_float4(bb.x - 1024.f * c4[0], bb.y - 1024.f * c4[1], bb.z - 1024.f * c4[2], bb.w - 1024.f * c4[3]);
+  }
+}
 
 // class-major y1 pixel slot of input pixel (ih, iw) and the byte offset of its 16-B chunk c
 __device__ __forceinline__ int cf_pix(int ih, int iw) { return ((ih & 1) * 2 + (iw & 1)) * 100 + (ih >> 1) * 10 + (iw >> 1); }
@@ -87,50 +153,58 @@ __device__ __forceinline__ int cf_off(int P, int c) { return (P << 7) + ((c ^ ((
 
 template <int C>
 __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv12Desc d) {
-  constexpr int NCHUNK = C * 441;                 // 16-B s2d blocks per image
-  constexpr int NDMA = (NCHUNK + 63) / 64;        // 1-KB LDS-DMA instructions per image
-  constexpr int NDW = (NDMA + 3) / 4;             // per wave (max)
-  // staging buffer (also the conv2 reduction's 24 KB of partials once its image is read)
-  constexpr int STGB = NDMA * 1024 > 2 * 3 * 4 * 64 * 16 ? NDMA * 1024 : 2 * 3 * 4 * 64 * 16;
+  // staging buffer: an image's C frames (s2d, 7056 B each), then the conv2 reduction's
+  // 24 KB of partials once conv1 has read them
+  constexpr int STGB = C * CF_FRAME > 2 * 3 * 4 * 64 * 16 ? C * CF_FRAME : 2 * 3 * 4 * 64 * 16;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * CF_PLANE + 2 * STGB];
   __shared__ int32_t slot_tbl[CF_MAXIMG * C];
   uint8_t* Y1 = smem;                              // hi plane; lo plane at + CF_PLANE
   uint8_t* STG = smem + 2 * CF_PLANE;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: branches on wave
+                                                             // roles stay scalar
   const int g = lane >> 4, pl = lane & 15;         // conv1 (16x16 MFMA) lane roles
   const int rr = lane & 31, kg = lane >> 5;        // conv2 (32x32 MFMA) lane roles
   const int nh = wv & 1, kp = wv >> 1;             // conv2 wave roles
-  const int per = (d.N + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int img0 = blockIdx.x * per, img1 = min(d.N, img0 + per);
-  if (img0 >= img1) return;
-  const int nimg = img1 - img0;
-  for (int i = tid; i < nimg * C; i += CF_THREADS) slot_tbl[i] = d.slots[(int64_t)img0 * C + i];
+  // images strided over the grid (local image i = blockIdx.x + i * gridDim.x): every
+  // workgroup gets its share of the S_t images -- the ones whose y1 also leaves for HBM
+  // (~4k cycles of store issue each) -- instead of the first workgroups getting all
+  const int G = (int)gridDim.x, img0 = blockIdx.x;
+  if (img0 >= d.N) return;
+  const int nimg = (d.N - img0 + G - 1) / G;
+  for (int i = tid; i < nimg * C; i += CF_THREADS) {
+    const int li = i / C;
+    slot_tbl[i] = d.slots[(int64_t)(img0 + li * G) * C + (i - li * C)];
+  }
   __syncthreads();
 
-  // ---- LDS-DMA of image `li` (local index) into staging buffer `buf`: this wave's
-  // instructions k = wv + 4 j (1 KB each; lanes past the frames read zeros)
-  auto issue_dma = [&](int li, int buf) {
-    int sl[4] = {0, 0, 0, 0};
+  // ---- LDS-DMA of image `li` into staging buffer `buf`: piece k = wv + 4 j (1 KB) copies
+  // bytes 1024 r .. of frame c = k / 7 (r = k % 7; the frame's 7056 bytes end 48 lanes into
+  // piece 6).  Frame slots of the image in SGPRs (`sl`), the address a scalar base plus
+  // the lane's 16 B: a piece is a handful of scalar instructions and one DMA.
+  constexpr int NPF = (CF_FRAME + 1023) / 1024;   // pieces per frame (7)
+  constexpr int NDMA = C * NPF;
+  constexpr int NDW = (NDMA + 3) / 4;             // per wave (max)
+  auto image_slots = [&](int li, int* sl) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) sl[c] = slot_tbl[li * C + c];
-    const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(STG + buf * STGB);
-#pragma unroll
-    for (int j = 0; j < NDW; ++j) {
-      const int k = wv + 4 * j;
-      if (k < NDMA) {
-        const int ch = 64 * k + lane;
-        const uint8_t* src = d.zero16;
-        if (ch < NCHUNK) {
-          const int c = ch / 441, blk = ch - c * 441;
-          int s = sl[0];
-#pragma unroll
-          for (int cc = 1; cc < C; ++cc)
-            if (c == cc) s = sl[cc];
-          src = d.ring + (int64_t)s * CF_FRAME + (blk << 4);
-        }
-        dma16(src, __builtin_amdgcn_readfirstlane(base + (uint32_t)k * 1024u));
-      }
+    for (int c = 0; c < 4; ++c) sl[c] = c < C ? slot_tbl[li * C + c] : 0;   // (VGPRs: SGPRs are short)
+  };
+  auto issue_dma_piece = [&](const int* sl, int buf, int j) {
+    const int k = wv + 4 * j;
+    if (k < NDMA) {
+      const int c = k / NPF, r = k - c * NPF;
+      const int s = c == 0 ? sl[0] : c == 1 ? sl[1] : c == 2 ? sl[2] : sl[3];
+      const uint8_t* src = d.ring + (int64_t)s * CF_FRAME + r * 1024;
+      const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(STG + buf * STGB) +
+                           (uint32_t)(c * CF_FRAME + r * 1024);
+      if (r * 1024 + lane * 16 < CF_FRAME) dma16_s(src, (uint32_t)lane * 16u, dst);
     }
+  };
+  auto issue_dma = [&](int li, int buf) {
+    int sl[4];
+    image_slots(li, sl);
+#pragma unroll
+    for (int j = 0; j < NDW; ++j) issue_dma_piece(sl, buf, j);
   };
 
   // ---- conv1: wave w owns output channels 32 cp .. 32 cp + 31 (cp = w & 1; two 16-channel
@@ -140,7 +214,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   // hi + lo * 2^-12
   const int cp = wv & 1, th = wv >> 1;
   f16x8 w1h[2][2 * C], w1l[2][2 * C];
-  f32x2v bias1[2][2];                                // [nt]: channels 32 cp + 16 nt + 4 g + {0..3}
+  f32x4 bias1[2];                                    // [nt]: channels 32 cp + 16 nt + 4 g + {0..3}
   int aoff[2 * C];                                   // staging byte offset of step s's 8-B fragment
 #pragma unroll
   for (int s = 0; s < 2 * C; ++s) {
@@ -151,39 +225,15 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
                                                      // channels 32 nh + 8 (2 kp + jh) + 4 kg .. + 3
   const uint4* wf = nullptr;                         // this wave's conv2 fragments (hi; lo at + C2F_FRAGS)
   auto load_weights = [&](int set) {
-    const float* W1 = set ? d.w1b : d.w1;
-    const float* B1 = set ? d.b1b : d.b1;
-    const float k = 1024.f * d.in_scale;
+    const uint4* F = d.w1frag + (((set * 2 + cp) * 2) * 2 * C * 2) * 64 + lane;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
-      const int n = 32 * cp + 16 * nt + pl;
-      float ws = 0.f;
 #pragma unroll
       for (int s = 0; s < 2 * C; ++s) {
-        const int q = 2 * s + (g >> 1), tap = q / C, c = q - tap * C, h = g & 1;
-        const int kh = 4 * (tap >> 1) + 2 * h, kw = 4 * (tap & 1);
-        const float4 r0 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh) * 8 + kw);
-        const float4 r1 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh + 1) * 8 + kw);
-        const float w8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const _Float16 hi = (_Float16)w8[j];
-          const _Float16 lo = (_Float16)((w8[j] - (float)hi) * CF_LO_SCALE);
-          w1h[nt][s][j] = hi;
-          w1l[nt][s][j] = lo;
-          ws += (float)hi + (float)lo * (1.f / CF_LO_SCALE);
-        }
+        w1h[nt][s] = __builtin_bit_cast(f16x8, F[((nt * 2 * C + s) * 2) * 64]);
+        w1l[nt][s] = __builtin_bit_cast(f16x8, F[((nt * 2 * C + s) * 2 + 1) * 64]);
       }
-      // channel sums over the four K-group lanes; the epilogue's channels 4 g + i take
-      // theirs: bias' = bias - 1024 * in_scale * sum_k w16[n][k] (pixels enter as 1024 + x)
-      ws += __shfl_xor(ws, 16, 64);
-      ws += __shfl_xor(ws, 32, 64);
-      float c4[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) c4[i] = __shfl(ws, 4 * g + i, 64);
-      const float4 bb = *reinterpret_cast<const float4*>(B1 + 32 * cp + 16 * nt + 4 * g);
-      bias1[nt][0] = (f32x2v){bb.x - k * c4[0], bb.y - k * c4[1]};
-      bias1[nt][1] = (f32x2v){bb.z - k * c4[2], bb.w - k * c4[3]};
+      bias1[nt] = __builtin_bit_cast(f32x4, d.w1frag[CF_W1FRAG(4) + ((set * 2 + cp) * 2 + nt) * 64 + lane]);
     }
     wf = d.wfrag + set * 2 * C2F_FRAGS + wv * 32 * 64 + lane;
     const float* B2 = set ? d.b2b : d.b2;
@@ -205,91 +255,142 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
 
   const bool two = d.w1b != nullptr;
   int cur_set = -1;
+  // y2 of the previous image waits in registers (hi, lo of channels .. + 3 per (mt, jh)) and
+  // leaves during the next conv1, one store per tile among the MFMAs: a wave's store issue
+  // moves ~7-25 B per cycle, so 12 stores in a row after the reduction cost ~3k cycles
+  uint4 pend[3][2];
+  int pend_img = -1;
+  auto store_y2 = [&](int q) {       // q = 2 (2 mt + jh) + plane, 0 .. 11
+    const int mt = q >> 2, jh = (q >> 1) & 1, plane = q & 1;
+    const int jq = 2 * kp + jh;
+    const int r = mt * 32 + rr, oh = r / 10, ow = r - oh * 10;
+    const bool valid = oh < 9 && ow < 9;
+    // every lane stores (padding pixels into scratch): 12 store instructions per wave and
+    // image, which the vmcnt wait after conv1 counts
+    const int64_t o2 = ((int64_t)pend_img * 81 + oh * 9 + ow) * 64 + nh * 32 + 8 * jq + 4 * kg;
+    bf16_t* dst = valid ? (plane ? d.y2_lo : d.y2) + o2 : reinterpret_cast<bf16_t*>(d.scratch + lane * 8);
+    const uint4 v = pend[mt][jh];
+    *reinterpret_cast<uint2*>(dst) = plane ? make_uint2(v.z, v.w) : make_uint2(v.x, v.y);
+  };
+  // image i's frames land in staging(i & 1): image 0's here, image i + 1's during conv1(i)
   issue_dma(0, 0);
-  if (nimg > 1) issue_dma(1, 1);
   for (int i = 0; i < nimg; ++i) {
-    const int img = img0 + i;
+    const int img = img0 + i * G;
     const int set = (two && img >= d.img_switch) ? 1 : 0;
     if (set != cur_set) {
       load_weights(set);      // vmcnt(0): every DMA issued so far has landed as well
       cur_set = set;
       __syncthreads();
     }
+    int nsl[4];                                       // image i + 1's frame slots
+    if (i + 1 < nimg) image_slots(i + 1, nsl);
     PROBE(d.probe, 4, i, 0);
     const uint8_t* S = STG + (i & 1) * STGB;
-    // ================= conv1: this wave's pixel tiles T = th, th + 2, .. (16 pixels each)
-    // x 32 channels.  Software-pipelined over tiles (one wave per SIMD hides nothing by
-    // itself): the 2C fragment reads of the next tile are in flight while this tile's
-    // MFMAs issue, and the previous tile's epilogue runs behind them.
+    // ================= conv1: this wave's pixel tiles T = th + 2 j, j = 0 .. 12 (16 pixels
+    // each; th = 1's 13th tile lies past pixel 399: it reads pixel 399 and writes the
+    // spare slots 400..407, which only conv2's invalid rows read) x 32 channels.
+    // Software-pipelined: tile j + 1's fragment reads are in flight while tile j's MFMAs
+    // issue with tile j - 1's epilogue between them -- every epilogue shares its tile with
+    // MFMAs (one wave per SIMD: the vector issue slots an MFMA leaves free are the only
+    // free ones).
     {
-      const int nT = th == 0 ? 13 : 12;
       auto load_tile = [&](int j, uint2* u) {
-        const int p = 16 * (th + 2 * j) + pl, oh = p / 20, ow = p - 20 * oh;
+        int p = 16 * (th + 2 * j) + pl;
+        if (j == 12) p = min(p, 399);
+        const int oh = p / 20, ow = p - 20 * oh;
         const uint8_t* A = S + ((oh * 21 + ow) << 4);
 #pragma unroll
         for (int s2 = 0; s2 < 2 * C; ++s2) u[s2] = *reinterpret_cast<const uint2*>(A + aoff[s2]);
       };
-      auto mfma_tile = [&](const uint2* u, f32x4* acc, f32x4* accl) {
+      // tile j - 1's epilogue in 8 pieces (per 16-channel half nt: combine + ReLU of
+      // rows 0-1, of rows 2-3, bf16 hi / lo split, LDS stores); lane: channels
+      // 32 cp + 16 nt + 4 g .. + 3 of pixel p -> y1 hi / lo planes
+      float ev[2][4];
+      uint32_t eh[2][2], el[2][2];
+      auto epi_piece = [&](int k, int j, const f32x4* acc, const f32x4* accl) {
+#ifdef CF_EXP_NOEPI
+        if (k == 0 && acc[0][0] + accl[1][3] == 1234.5f) Y1[tid] = 1;
+        return;
+#endif
+        const int nt = k >> 2, part = k & 3;
+        if (part < 2) {
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[nt] = accl[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s2 = 0; s2 < 2 * C; ++s2) {
-          const f16x8 a = __builtin_bit_cast(f16x8, u8x8_to_f16off(u[s2].x, u[s2].y));
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt) {
-            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1h[nt][s2], a, acc[nt], 0, 0, 0);
-            accl[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1l[nt][s2], a, accl[nt], 0, 0, 0);
-          }
-        }
-      };
-      // lane: channels 32 cp + 16 nt + 4 g .. + 3 of pixel (oh, ow) -> y1 hi / lo planes
-      auto epi = [&](int j, const f32x4* acc, const f32x4* accl) {
-        const int p = 16 * (th + 2 * j) + pl, oh = p / 20, ow = p - 20 * oh;
-        const int P = cf_pix(oh, ow);
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            v[r] = fmaxf((acc[nt][r] + accl[nt][r] * (1.f / CF_LO_SCALE)) * d.in_scale + bias1[nt][r >> 1][r & 1],
-                         0.f);
-          uint32_t h01, l01, h23, l23;
-          split_pk_bf16(v[0], v[1], h01, l01);
-          split_pk_bf16(v[2], v[3], h23, l23);
+          for (int r = 2 * part; r < 2 * part + 2; ++r)
+            ev[nt][r] = fmaxf(fmaf(accl[nt][r], 1.f / CF_LO_SCALE, acc[nt][r]), 0.f);
+        } else if (part == 2) {
+          split_pk_bf16(ev[nt][0], ev[nt][1], eh[nt][0], el[nt][0]);
+          split_pk_bf16(ev[nt][2], ev[nt][3], eh[nt][1], el[nt][1]);
+        } else {
+          const int p = 16 * (th + 2 * j) + pl, oh = p / 20, ow = p - 20 * oh;
+          const int P = (j == 12 && p >= 400) ? 400 + (pl & 7) : cf_pix(oh, ow);
           const int ch = 32 * cp + 16 * nt + 4 * g;
           const int off = cf_off(P, ch >> 3) + (ch & 7) * 2;
-          *reinterpret_cast<uint2*>(Y1 + off) = make_uint2(h01, h23);
-          *reinterpret_cast<uint2*>(Y1 + CF_PLANE + off) = make_uint2(l01, l23);
+          *reinterpret_cast<uint2*>(Y1 + off) = make_uint2(eh[nt][0], eh[nt][1]);
+          *reinterpret_cast<uint2*>(Y1 + CF_PLANE + off) = make_uint2(el[nt][0], el[nt][1]);
         }
       };
-      uint2 uA[2 * C], uB[2 * C];
-      f32x4 aA[2], aAl[2], aB[2], aBl[2];
-      load_tile(0, uA);
-      load_tile(1, uB);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_tile(uA, aA, aAl);                    // tile 0
-      for (int j = 1; j < nT; j += 2) {          // uA: tile j - 1 (consumed), uB: tile j
-        if (j + 1 < nT) load_tile(j + 1, uA);
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_tile(uB, aB, aBl);                  // tile j
-        epi(j - 1, aA, aAl);
-        __builtin_amdgcn_sched_barrier(0);
-        if (j + 1 < nT) {
-          if (j + 2 < nT) load_tile(j + 2, uB);
+      auto cvt = [&](const uint2 v) {
+#ifdef CF_EXP_NOPERM
+        return __builtin_bit_cast(f16x8, make_uint4(v.x, v.y, v.x, v.y));
+#else
+        return __builtin_bit_cast(f16x8, u8x8_to_f16off(v.x, v.y));
+#endif
+      };
+      // tile j's 2C K steps (4 MFMAs each); step s2 + 1's fragment conversion and 8 / 2C
+      // epilogue pieces of tile j - 1 (pj >= 0) go between them, one scheduling region
+      // per step, so the vector work rides in the MFMAs' free issue slots
+      auto mfma_tile = [&](const uint2* u, f32x4* acc, f32x4* accl, int pj, const f32x4* pacc,
+                           const f32x4* paccl) {
+        f16x8 av[2];
+        av[0] = cvt(u[0]);
+#pragma unroll
+        for (int s2 = 0; s2 < 2 * C; ++s2) {
+          if (s2 + 1 < 2 * C) av[(s2 + 1) & 1] = cvt(u[s2 + 1]);
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1h[nt][s2], av[s2 & 1], s2 ? acc[nt] : bias1[nt], 0, 0, 0);
+            accl[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1l[nt][s2], av[s2 & 1],
+                                                              s2 ? accl[nt] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          }
+          if (pj >= 0) {
+#pragma unroll
+            for (int k = s2 * 8 / (2 * C); k < (s2 + 1) * 8 / (2 * C); ++k) epi_piece(k, pj, pacc, paccl);
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);    // VALU
+          }
           __builtin_amdgcn_sched_barrier(0);
-          mfma_tile(uA, aA, aAl);                // tile j + 1
         }
-        epi(j, aB, aBl);
+      };
+      uint2 u[2][2 * C];
+      f32x4 a[2][2], al[2][2];
+      load_tile(0, u[0]);
+      load_tile(1, u[1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_tile(u[0], a[0], al[0], -1, nullptr, nullptr);
+#pragma unroll
+      for (int j = 1; j < 13; ++j) {
+        if (j + 1 < 13) load_tile(j + 1, u[(j + 1) & 1]);     // tile j - 1's registers
+        // image i + 1's frames -> staging((i + 1) & 1), one 1-KB DMA per tile among the
+        // MFMAs (that buffer's last readers -- conv1(i - 1), the reduction of image i - 1
+        // -- finished before the barrier that closed image i - 1)
+        if (j - 1 < NDW && i + 1 < nimg) issue_dma_piece(nsl, (i + 1) & 1, j - 1);
+        if (i > 0) store_y2(j - 1);                           // image i - 1's y2
         __builtin_amdgcn_sched_barrier(0);
+        mfma_tile(u[j & 1], a[j & 1], al[j & 1], j - 1, a[(j - 1) & 1], al[(j - 1) & 1]);
       }
-      if (nT & 1) epi(nT - 1, aA, aAl);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) epi_piece(k, 12, a[0], al[0]);
     }
     PROBE(d.probe, 4, i, 1);
-    // image i + 1's frames (issued during image i - 1) have landed: only the CF_NY2 y2
-    // stores of image i - 1 are younger (their acks are not waited for)
-    static_assert(CF_NY2 == 12, "the vmcnt below counts the y2 epilogue stores");
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    __syncthreads();          // y1 complete; staging(i) read; staging(i + 1) visible
+    // image i + 1's frames (DMA pieces at tiles 1 .. NDW, each before that tile's y2 store)
+    // have landed: only the y2 stores of tiles NDW .. 12 are younger than the last piece
+    static_assert(NDW <= 7, "the vmcnt below assumes the last DMA piece at tile <= 7");
+    if (i > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(13 - NDW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();          // y1 complete; staging(i) read (free: the reduction's); staging(i + 1) visible
     const bool copy = img < d.copy_n;
     // S_t rows: y1 (hi, lo) leaves for HBM (the backward's input).  Thread tid copies LDS
     // chunks k = tid + 256 r in LDS order (pixel slot P = k >> 3, stored chunk k & 7):
@@ -366,11 +467,11 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
 #undef CF_LDA
     }
     PROBE(d.probe, 4, i, 3);
-    __syncthreads();          // every read of y1 is done: its LDS takes the partial sums
-    // the two kernel-row pairs meet in LDS: wave (nh, kp) finishes output channels
-    // 32 nh + 16 kp .. + 15 (jq = 2 kp, 2 kp + 1) and hands the other half of its partial
-    // sums to its partner; sum = (bias + pair 0) + pair 1 in both waves (fixed order)
-    float4* red = reinterpret_cast<float4*>(Y1);
+    // the two kernel-row pairs meet in LDS (staging(i), read by conv1(i) before the barrier
+    // above): wave (nh, kp) finishes output channels 32 nh + 16 kp .. + 15 (jq = 2 kp,
+    // 2 kp + 1) and hands the other half of its partial sums to its partner;
+    // sum = (bias + pair 0) + pair 1 in both waves (fixed order)
+    float4* red = reinterpret_cast<float4*>(STG + (i & 1) * STGB);
     // (kp is wave-uniform: both branches index the accumulators with constants)
     auto give = [&](const int jq0) {
 #pragma unroll
@@ -383,16 +484,11 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
     };
     if (kp == 0) give(2);
     else give(0);
-    // staging(i) is free (read by conv1(i)): image i + 2's frames go there now, ahead of
-    // this image's epilogue stores (the wait after the next conv1 counts only those)
-    if (i + 2 < nimg) issue_dma(i + 2, i & 1);
-    __syncthreads();          // partials visible
+    __syncthreads();          // partials visible; every read of y1 is done
     // acc2[mt][4 jq + i] = D[channel 32 nh + 8 jq + 4 kg + i][pixel mt * 32 + rr]
     auto finish = [&](const int jq0, const bool own_first) {
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt) {
-        const int r = mt * 32 + rr, oh = r / 10, ow = r - oh * 10;
-        const bool valid = oh < 9 && ow < 9;
 #pragma unroll
         for (int jh = 0; jh < 2; ++jh) {
           const int jq = jq0 + jh;
@@ -408,27 +504,24 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
           uint32_t h01, l01, h23, l23;
           split_pk_bf16(v0, v1, h01, l01);
           split_pk_bf16(v2, v3, h23, l23);
-          // every lane stores (padding pixels into scratch): a fixed count of CF_NY2 store
-          // instructions per wave keeps the vmcnt wait of the next image exact
-          const int64_t o2 = ((int64_t)img * 81 + oh * 9 + ow) * 64 + nh * 32 + 8 * jq + 4 * kg;
-          bf16_t* dh = valid ? d.y2 + o2 : reinterpret_cast<bf16_t*>(d.scratch + lane * 8);
-          bf16_t* dl = valid ? d.y2_lo + o2 : reinterpret_cast<bf16_t*>(d.scratch + lane * 8);
-          *reinterpret_cast<uint2*>(dh) = make_uint2(h01, h23);
-          *reinterpret_cast<uint2*>(dl) = make_uint2(l01, l23);
+          pend[mt][jh] = make_uint4(h01, h23, l01, l23);
         }
       }
     };
     if (kp == 0) finish(0, true);        // (bias + own pair 0) + pair 1
     else finish(2, false);               // (bias + pair 0) + own pair 1
-    __syncthreads();          // the partials are read: y1's LDS is free for the next conv1
+    pend_img = img;
+    __syncthreads();          // the partials are read: staging(i) may take image i + 2's frames
   }
+#pragma unroll
+  for (int q = 0; q < 12; ++q) store_y2(q);   // the last image's y2
 }
 
 APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if (d.N < 1) return 0;
   if (d.ring == nullptr || d.slots == nullptr || d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr ||
-      d.w2_lo == nullptr || d.b2 == nullptr || d.y2 == nullptr || d.y2_lo == nullptr || d.zero16 == nullptr ||
-      d.wfrag == nullptr || d.scratch == nullptr)
+      d.w2_lo == nullptr || d.b2 == nullptr || d.y2 == nullptr || d.y2_lo == nullptr ||
+      d.wfrag == nullptr || d.scratch == nullptr || d.w1frag == nullptr)
     return (int)hipErrorInvalidValue;
   const bool two = d.w1b != nullptr;
   if (two && (d.b1b == nullptr || d.w2b == nullptr || d.w2b_lo == nullptr || d.b2b == nullptr))
@@ -441,12 +534,21 @@ APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
   if ((d.N + G - 1) / G > CF_MAXIMG) G = (d.N + CF_MAXIMG - 1) / CF_MAXIMG;
-  if (!d.wfrag_ready)
-    cf_pack_c2f_kernel<<<4 * C2F_FRAGS / 256, 256, 0, st>>>(C2fPack{{d.w2, d.w2_lo, d.w2b, d.w2b_lo}, d.wfrag, 0});
+  CfPack pk{C2fPack{{d.w2, d.w2_lo, d.w2b, d.w2b_lo}, d.wfrag, 0}, d.wfrag_ready ? 0 : 4 * C2F_FRAGS / 256,
+            {d.w1, d.w1b}, {d.b1, d.b1b}, d.in_scale, d.w1frag};
   switch (d.C) {
-    case 1: conv12_fused_split_kernel<1><<<G, CF_THREADS, 0, st>>>(d); break;
-    case 2: conv12_fused_split_kernel<2><<<G, CF_THREADS, 0, st>>>(d); break;
-    case 4: conv12_fused_split_kernel<4><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 1:
+      cf_pack_kernel<1><<<pk.nc2f + 1, 256, 0, st>>>(pk);
+      conv12_fused_split_kernel<1><<<G, CF_THREADS, 0, st>>>(d);
+      break;
+    case 2:
+      cf_pack_kernel<2><<<pk.nc2f + 1, 256, 0, st>>>(pk);
+      conv12_fused_split_kernel<2><<<G, CF_THREADS, 0, st>>>(d);
+      break;
+    case 4:
+      cf_pack_kernel<4><<<pk.nc2f + 1, 256, 0, st>>>(pk);
+      conv12_fused_split_kernel<4><<<G, CF_THREADS, 0, st>>>(d);
+      break;
     default: return (int)hipErrorInvalidValue;
   }
   APEX_CHECK_LAUNCH();

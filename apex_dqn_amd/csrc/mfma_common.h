@@ -140,6 +140,20 @@ __device__ __forceinline__ uint32_t relu2(uint32_t v) {
 // 16-byte LDS-DMA issued from inline asm: hipcc does not track it, so it emits no
 // conservative vmcnt(0) before later ds_reads; completion is counted by hand with
 // explicit s_waitcnt vmcnt(N) + s_barrier (M0 is written inside the statement).
+// the same with a wave-uniform 64-bit base (SGPR pair) and a per-lane 32-bit offset:
+// no per-lane address arithmetic
+__device__ __forceinline__ void dma16_s(const void* base, uint32_t voff, uint32_t lds_off) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  // (readfirstlane returns int: through uint32_t, or bit 31 of the low half sign-extends)
+  const uint64_t sbase = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_off)
+               : "memory");
+}
+
 __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_off) {
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"

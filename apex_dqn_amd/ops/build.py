@@ -98,7 +98,10 @@ def _build_kernels(force: bool, jobs: int, verbose: bool, debug: bool) -> str:
     headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.cuh"))
     lib_path = KERNEL_DEBUG_LIB if debug else KERNEL_LIB
     suffix = ".dbg.o" if debug else ".o"
-    flags = HIP_FLAGS + (["-DAPEX_DEBUG_BOUNDS", "-DAPEX_PROBE"] if debug else [])
+    # APEX_DEBUG_DEFS: extra space-separated -D flags for the diagnostic library only
+    # (kernel experiments behind #ifdef, e.g. scripts/probe_conv12.py)
+    extra = [f for f in os.environ.get("APEX_DEBUG_DEFS", "").split() if f.startswith("-D")]
+    flags = HIP_FLAGS + (["-DAPEX_DEBUG_BOUNDS", "-DAPEX_PROBE"] + extra if debug else [])
     objs = []
     todo = []
     if debug:

@@ -195,6 +195,7 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
 # fp32 learner: conv1 -> conv2 fused with y1 kept in LDS (csrc/conv12_fused.hip);
 # APEX_CONV12_FUSED=0 runs the two image-resident kernels
 CONV12_FUSED = _os.environ.get("APEX_CONV12_FUSED", "1") != "0"
+CF_W1FRAG_BYTES = (2 * 2 * 2 * 2 * 4 * 2 * 64 + 2 * 2 * 2 * 64) * 16
 
 
 def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
@@ -226,11 +227,9 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
         d.y1, d.y1_lo = y1.data_ptr(), y1_lo.data_ptr()
     d.copy_n = int(copy_n)
     d.y2, d.y2_lo = y2.data_ptr(), y2_lo.data_ptr()
-    zero = ws.get(("zero16",), 64, ring.device, torch.uint8)
-    if not getattr(ws, "_zeroed", False):
-        zero.zero_()
-        ws._zeroed = True
-    d.zero16 = zero.data_ptr()
+    # conv1 fragments + folded biases of both sets (csrc/conv12_fused.hip CF_W1FRAG_U4 uint4),
+    # rewritten by the launch's pack kernel
+    d.w1frag = ws.get(("cf_w1frag",), CF_W1FRAG_BYTES, ring.device, torch.uint8).data_ptr()
     d.scratch = ws.get(("scratch1k",), 2048, ring.device, torch.uint8).data_ptr()
     d.wfrag = c2f_wfrag_fwd_buffer(ring.device).data_ptr()
     d.wfrag_ready = 0

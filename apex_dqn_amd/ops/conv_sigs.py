@@ -21,7 +21,7 @@ class Conv12Desc(ctypes.Structure):
     _fields_ = [("ring", c_p), ("slots", c_p), ("w1", c_p), ("w1b", c_p), ("b1", c_p), ("b1b", c_p),
                 ("w2", c_p), ("w2_lo", c_p), ("w2b", c_p), ("w2b_lo", c_p), ("wfrag", c_p), ("wfrag_ready", c_i),
                 ("b2", c_p), ("b2b", c_p), ("y1", c_p), ("y1_lo", c_p), ("y2", c_p), ("y2_lo", c_p),
-                ("zero16", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("img_switch", c_i), ("copy_n", c_i),
+                ("w1frag", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("img_switch", c_i), ("copy_n", c_i),
                 ("in_scale", ctypes.c_float), ("probe", c_p)]
 
 
