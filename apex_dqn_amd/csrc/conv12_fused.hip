@@ -62,7 +62,8 @@ struct Conv12Desc {
   const bf16_t* w2b;       //   target, or null
   const bf16_t* w2b_lo;
   uint4* wfrag;            // both sets in C2F fragment order (4 x C2F_FRAGS uint4: set 0 hi, lo, set 1 hi, lo)
-  int wfrag_ready;         // packed earlier in the step; else the launcher packs them first
+  int pack_sets;           // weight sets the launcher (re)packs first (wfrag, w1frag): bit 0 online,
+                           // bit 1 target; the others' fragments are current (cf_pack_kernel)
   const float* b2;
   const float* b2b;
   bf16_t* y1;              // [copy_n][20][20][64] hi / lo (rows < copy_n only)
@@ -82,18 +83,21 @@ struct Conv12Desc {
 #define CF_W1FRAG(C_) (2 * 2 * 2 * 2 * (C_) * 2 * 64)
 #define CF_W1FRAG_U4 (CF_W1FRAG(4) + 2 * 2 * 2 * 64)
 
-// One launch ahead of the fused kernel: blocks [0, nc2f) pack both conv2 weight sets into
-// C2F fragment order (csrc/conv2_wfrag.h; nc2f = 0 when the step packed them already), the
-// last block the conv1 operands of both sets exactly as the MFMA lanes consume them:
-// lane (g, pl) of wave role cp, tile nt, K step s holds channel 32 cp + 16 nt + pl, K
-// 32 s + 8 g .. + 7 (s2d K order k = (tap C + c) 16 + r4 4 + c4, tap = 2 a + b) as f16
-// hi + lo * 2^-12 of w * in_scale, and the bias the hi accumulation chain starts from:
-// bias - 1024 * sum_k w16[n][k] (pixels enter the MFMAs as 1024 + x).  Per workgroup this
-// replaces ~13k cycles of loads and conversions at each weight-set switch by 34 loads.
+// The pack launch ahead of the fused kernel (or alone, apex_conv12_pack): blocks
+// [0, nc2f) pack the requested conv2 weight sets into C2F fragment order
+// (csrc/conv2_wfrag.h), the next 4 per requested set the conv1 operands exactly as the MFMA
+// lanes consume them: block (set, cp, nt), lane (g, pl), K step s holds channel
+// 32 cp + 16 nt + pl, K 32 s + 8 g .. + 7 (s2d K order k = (tap C + c) 16 + r4 4 + c4,
+// tap = 2 a + b) as f16 hi + lo * 2^-12 of w * in_scale, and the bias the hi accumulation
+// chain starts from: bias - 1024 * sum_k w16[n][k] (pixels enter the MFMAs as 1024 + x).
+// The fused kernel's weight-set switch is then 34 coalesced loads instead of ~13k cycles of
+// gathers and conversions.  The target set changes only at a target sync: the learner
+// repacks it then (pack_sets bit 1) and the step's launch packs the online set alone.
 struct CfPack {
   C2fPack c2f;
   int nc2f;                // C2F blocks
-  const float* w1[2];      // fp32 OIHW [64][C][8][8] (set 1 may be null)
+  int sets;                // bit 0: online, bit 1: target
+  const float* w1[2];      // fp32 OIHW [64][C][8][8]
   const float* b1[2];
   float in_scale;
   uint4* w1frag;
@@ -102,47 +106,52 @@ struct CfPack {
 template <int C>
 __global__ void __launch_bounds__(256) cf_pack_kernel(CfPack p) {
   if ((int)blockIdx.x < p.nc2f) {
-    c2f_pack_range(p.c2f, blockIdx.x * 256 + threadIdx.x, 4 * C2F_FRAGS);
+    c2f_pack_range(p.c2f, blockIdx.x * 256 + threadIdx.x, p.nc2f * 256);
     return;
   }
-  const int t = threadIdx.x, set = t >> 7, cp = (t >> 6) & 1, lane = t & 63;
-  const int g = lane >> 4, pl = lane & 15;
+  __shared__ float part[4][64];
+  __shared__ float tot[64];
+  const int jb = (int)blockIdx.x - p.nc2f;
+  const int set = p.sets == 2 ? 1 : jb >> 2, cp = (jb >> 1) & 1, nt = jb & 1;
+  const int t = threadIdx.x, lane = t & 63, sq = t >> 6, g = lane >> 4, pl = lane & 15;
   const float* W1 = p.w1[set];
-  if (W1 == nullptr) return;                          // (whole waves)
   const float sc = p.in_scale;
+  const int n = 32 * cp + 16 * nt + pl;
+  float ws = 0.f;
+  for (int s = sq; s < 2 * C; s += 4) {
+    const int q = 2 * s + (g >> 1), tap = q / C, c = q - tap * C, h = g & 1;
+    const int kh = 4 * (tap >> 1) + 2 * h, kw = 4 * (tap & 1);
+    const float4 r0 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh) * 8 + kw);
+    const float4 r1 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh + 1) * 8 + kw);
+    const float w8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+    f16x8 hv, lv;
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int n = 32 * cp + 16 * nt + pl;
-    float ws = 0.f;
-#pragma unroll
-    for (int s = 0; s < 2 * C; ++s) {
-      const int q = 2 * s + (g >> 1), tap = q / C, c = q - tap * C, h = g & 1;
-      const int kh = 4 * (tap >> 1) + 2 * h, kw = 4 * (tap & 1);
-      const float4 r0 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh) * 8 + kw);
-      const float4 r1 = *reinterpret_cast<const float4*>(W1 + ((n * C + c) * 8 + kh + 1) * 8 + kw);
-      const float w8[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-      f16x8 hv, lv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float w = w8[j] * sc;                    // the input scale rides in the weights
-        const _Float16 hi = (_Float16)w;
-        const _Float16 lo = (_Float16)((w - (float)hi) * CF_LO_SCALE);
-        hv[j] = hi;
-        lv[j] = lo;
-        ws += (float)hi + (float)lo * (1.f / CF_LO_SCALE);
-      }
-      uint4* o = p.w1frag + ((((set * 2 + cp) * 2 + nt) * 2 * C + s) * 2) * 64 + lane;
-      o[0] = __builtin_bit_cast(uint4, hv);
-      o[64] = __builtin_bit_cast(uint4, lv);
+    for (int j = 0; j < 8; ++j) {
+      const float w = w8[j] * sc;                      // the input scale rides in the weights
+      const _Float16 hi = (_Float16)w;
+      const _Float16 lo = (_Float16)((w - (float)hi) * CF_LO_SCALE);
+      hv[j] = hi;
+      lv[j] = lo;
+      ws += (float)hi + (float)lo * (1.f / CF_LO_SCALE);
     }
-    // channel sums over the four K-group lanes; lane (g, .) takes channels 4 g + i
-    ws += __shfl_xor(ws, 16, 64);
-    ws += __shfl_xor(ws, 32, 64);
+    uint4* o = p.w1frag + ((((set * 2 + cp) * 2 + nt) * 2 * C + s) * 2) * 64 + lane;
+    o[0] = __builtin_bit_cast(uint4, hv);
+    o[64] = __builtin_bit_cast(uint4, lv);
+  }
+  part[sq][lane] = ws;
+  __syncthreads();
+  if (t < 64) tot[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+  __syncthreads();
+  if (t < 64) {
+    // channel 4 g + i: its sum over the four K-group lanes (fixed order)
     float c4[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) c4[i] = __shfl(ws, 4 * g + i, 64);
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 4 * g + i;
+      c4[i] = ((tot[ch] + tot[16 + ch]) + tot[32 + ch]) + tot[48 + ch];
+    }
     const float4 bb = *reinterpret_cast<const float4*>(p.b1[set] + 32 * cp + 16 * nt + 4 * g);
-    reinterpret_cast<float4*>(p.w1frag + CF_W1FRAG(4))[((set * 2 + cp) * 2 + nt) * 64 + lane] =
+    reinterpret_cast<float4*>(p.w1frag + CF_W1FRAG(4))[((set * 2 + cp) * 2 + nt) * 64 + t] =
         make_float4(bb.x - 1024.f * c4[0], bb.y - 1024.f * c4[1], bb.z - 1024.f * c4[2], bb.w - 1024.f * c4[3]);
   }
 }
@@ -517,6 +526,32 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   for (int q = 0; q < 12; ++q) store_y2(q);   // the last image's y2
 }
 
+static int cf_launch_pack(const Conv12Desc& d, hipStream_t st) {
+  const int sets = d.pack_sets & ((d.w1b != nullptr) ? 3 : 1);
+  if (sets == 0) return 0;
+  const bool s0 = sets & 1, s1 = (sets & 2) != 0;
+  CfPack pk{C2fPack{{s0 ? d.w2 : nullptr, s0 ? d.w2_lo : nullptr, s1 ? d.w2b : nullptr, s1 ? d.w2b_lo : nullptr},
+                    d.wfrag, 0},
+            (s1 ? 4 : 2) * C2F_FRAGS / 256, sets, {d.w1, d.w1b}, {d.b1, d.b1b}, d.in_scale, d.w1frag};
+  const int nb = pk.nc2f + 4 * (s0 + s1);
+  switch (d.C) {
+    case 1: cf_pack_kernel<1><<<nb, 256, 0, st>>>(pk); break;
+    case 2: cf_pack_kernel<2><<<nb, 256, 0, st>>>(pk); break;
+    case 4: cf_pack_kernel<4><<<nb, 256, 0, st>>>(pk); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return 0;
+}
+
+// pack only (the learner's target sync): d.pack_sets of d's weights
+APEX_EXPORT int apex_conv12_pack(Conv12Desc d, hipStream_t st) {
+  if (d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr || d.w2_lo == nullptr || d.wfrag == nullptr ||
+      d.w1frag == nullptr || ((d.pack_sets & 2) && (d.w1b == nullptr || d.b1b == nullptr || d.w2b == nullptr ||
+                                                   d.w2b_lo == nullptr)))
+    return (int)hipErrorInvalidValue;
+  return cf_launch_pack(d, st);
+}
+
 APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if (d.N < 1) return 0;
   if (d.ring == nullptr || d.slots == nullptr || d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr ||
@@ -534,21 +569,12 @@ APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
   if ((d.N + G - 1) / G > CF_MAXIMG) G = (d.N + CF_MAXIMG - 1) / CF_MAXIMG;
-  CfPack pk{C2fPack{{d.w2, d.w2_lo, d.w2b, d.w2b_lo}, d.wfrag, 0}, d.wfrag_ready ? 0 : 4 * C2F_FRAGS / 256,
-            {d.w1, d.w1b}, {d.b1, d.b1b}, d.in_scale, d.w1frag};
+  const int err = cf_launch_pack(d, st);
+  if (err) return err;
   switch (d.C) {
-    case 1:
-      cf_pack_kernel<1><<<pk.nc2f + 1, 256, 0, st>>>(pk);
-      conv12_fused_split_kernel<1><<<G, CF_THREADS, 0, st>>>(d);
-      break;
-    case 2:
-      cf_pack_kernel<2><<<pk.nc2f + 1, 256, 0, st>>>(pk);
-      conv12_fused_split_kernel<2><<<G, CF_THREADS, 0, st>>>(d);
-      break;
-    case 4:
-      cf_pack_kernel<4><<<pk.nc2f + 1, 256, 0, st>>>(pk);
-      conv12_fused_split_kernel<4><<<G, CF_THREADS, 0, st>>>(d);
-      break;
+    case 1: conv12_fused_split_kernel<1><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 2: conv12_fused_split_kernel<2><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 4: conv12_fused_split_kernel<4><<<G, CF_THREADS, 0, st>>>(d); break;
     default: return (int)hipErrorInvalidValue;
   }
   APEX_CHECK_LAUNCH();

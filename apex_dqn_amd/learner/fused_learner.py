@@ -120,6 +120,7 @@ class FusedNatureLearner(IsNormMixin):
         if comm is not None and comm.world_size > 1:
             comm.broadcast_flat(self.p32)
         self._refresh_bf16()
+        self._tgt_packed = False
         self.sync_target()
         self.num_q_updates = 0
         self.world = comm.world_size if comm is not None else 1
@@ -251,9 +252,11 @@ class FusedNatureLearner(IsNormMixin):
         if sp:
             # conv1 -> conv2 in one launch, y1 kept in LDS; only the S_t rows' y1 (the
             # backward's input) is written out (csrc/conv12_fused.hip)
+            # (the target set's weight fragments are repacked at each target change:
+            # _target_changed; the step packs the online set only)
+            c1, c2 = self._conv12_weights()
             ops.conv12_fwd(self.replay.frames, self.slots, self.frames, rt.obs_scale, self.y1, self.y1_lo, self.y2,
-                           self.y2_lo, (P["w1"], P["b1"], T["w1"], T["b1"]),
-                           (Pb["w2"], Pl["w2"], P["b2"], Tb["w2"], Tl["w2"], T["b2"]), rows_first=2 * B, copy_n=B)
+                           self.y2_lo, c1, c2, rows_first=2 * B, copy_n=B, pack_sets=1 if self._tgt_packed else 3)
         else:
             c2f = (Pb["w2"], None, Tb["w2"], None)
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
@@ -265,6 +268,18 @@ class FusedNatureLearner(IsNormMixin):
                    c2d=(Pb["w2"], Pl["w2"] if sp else None), defer_head=defer_head,
                    **self._lo(x_lo=sp and self.y3_lo.reshape(n, 3136), w_lo=sp and Pl["wfc"],
                               w2_lo=sp and Tl["wfc"], out_lo=self.h_lo))
+
+    def _conv12_weights(self):
+        P, T, Pb, Tb, Pl, Tl = self.P, self.T, self.Pb, self.Tb, self.Pl, self.Tl
+        return ((P["w1"], P["b1"], T["w1"], T["b1"]), (Pb["w2"], Pl["w2"], P["b2"], Tb["w2"], Tl["w2"], T["b2"]))
+
+    def _target_changed(self) -> None:
+        """The target weights (t32 / tbf) changed: repack the fused forward's target
+        fragments (split mode)."""
+        if self.split:
+            c1, c2 = self._conv12_weights()
+            self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=2)
+            self._tgt_packed = True
 
     def _head_params(self, V):
         return {k: V[k] for k in ("wv", "bv", "wa", "ba")}
@@ -600,6 +615,7 @@ class FusedNatureLearner(IsNormMixin):
             dist.broadcast(t, src=0)
         self._refresh_bf16()
         split_into(self.t32, self.tbf, self.tbf_lo)
+        self._target_changed()
         return False
 
     def refresh_replay_stats(self) -> None:
@@ -628,6 +644,7 @@ class FusedNatureLearner(IsNormMixin):
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)
         self._tbf_all.copy_(self._pbf_all)
+        self._target_changed()
 
     # ------------------------------------------------------------ metrics
     def last_metrics(self) -> Dict[str, float]:
@@ -669,6 +686,7 @@ class FusedNatureLearner(IsNormMixin):
         if "Q_target_state" in ck:
             reference_state_to_flat(ck["Q_target_state"], self.T)
             split_into(self.t32, self.tbf, self.tbf_lo)
+            self._target_changed()
         else:
             self.sync_target()
         opt = ck.get("optimizer_state")

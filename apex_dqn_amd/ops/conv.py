@@ -198,42 +198,66 @@ CONV12_FUSED = _os.environ.get("APEX_CONV12_FUSED", "1") != "0"
 CF_W1FRAG_BYTES = (2 * 2 * 2 * 2 * 4 * 2 * 64 + 2 * 2 * 2 * 64) * 16
 
 
-def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
-                     b1: torch.Tensor, w2: torch.Tensor, w2_lo: torch.Tensor, b2: torch.Tensor, scale: float,
-                     y2: torch.Tensor, y2_lo: torch.Tensor, y1: Optional[torch.Tensor] = None,
-                     y1_lo: Optional[torch.Tensor] = None, copy_n: int = 0, w1b=None, b1b=None, w2b=None,
-                     w2b_lo=None, b2b=None, rows_first: int = 0, grid: int = 0,
-                     probe: Optional[torch.Tensor] = None) -> None:
-    """conv1 (fp32 OIHW weights ``w1``, exact uint8 frames from the s2d ring) + ReLU ->
-    conv2 (hi / lo bf16 OHWI ``w2``, ``w2_lo``) + ReLU in one persistent launch, y1 kept
-    in LDS; rows < ``copy_n`` also store y1 (hi / lo) for the backward.  Rows >=
-    ``rows_first`` use the second weight set (``w1b`` ..) when given."""
+def _conv12_desc(ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1, b1, w2, w2_lo, b2, scale, w1b, b1b,
+                 w2b, w2b_lo, b2b):
     from .conv_sigs import Conv12Desc
-    N, C = slots.shape
-    assert slots.dtype == torch.int32 and slots.is_contiguous()
+    C = int(w1.shape[1])
     assert tuple(w1.shape) == (64, C, 8, 8) and w1.dtype == torch.float32 and w1.is_contiguous()
     assert tuple(w2.shape) == (64, 4, 4, 64) and w2.dtype == torch.bfloat16 and w2_lo.dtype == torch.bfloat16
-    assert tuple(y2.shape) == (N, 9, 9, 64) and tuple(y2_lo.shape) == (N, 9, 9, 64)
     d = Conv12Desc()
-    d.ring, d.slots = ring.data_ptr(), slots.data_ptr()
+    d.ring, d.slots = _lib.ptr(ring), _lib.ptr(slots)
     d.w1, d.b1, d.w2, d.w2_lo, d.b2 = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), w2_lo.data_ptr(), b2.data_ptr()
     if w1b is not None:
         assert tuple(w1b.shape) == tuple(w1.shape) and tuple(w2b.shape) == tuple(w2.shape)
         d.w1b, d.b1b, d.w2b, d.w2b_lo, d.b2b = (w1b.data_ptr(), b1b.data_ptr(), w2b.data_ptr(), w2b_lo.data_ptr(),
                                                  b2b.data_ptr())
+    dev = w1.device
+    # conv1 fragments + folded biases of both sets (csrc/conv12_fused.hip CF_W1FRAG_U4 uint4)
+    # and the conv2 C2F fragments: written by the pack launch, read by every fused launch
+    d.w1frag = ws.get(("cf_w1frag",), CF_W1FRAG_BYTES, dev, torch.uint8).data_ptr()
+    d.scratch = ws.get(("scratch1k",), 2048, dev, torch.uint8).data_ptr()
+    # (in ``ws``, not per stream: the target set packed at a sync, outside the step's
+    # captured graph, must be the buffer the graph's launches read)
+    d.wfrag = ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, dev, torch.uint8).data_ptr()
+    d.C, d.in_scale = C, float(scale)
+    return d
+
+
+def conv12_pack(lib, ws: "Workspace", w1, b1, w2, w2_lo, b2, scale: float, w1b=None, b1b=None, w2b=None,
+                w2b_lo=None, b2b=None, sets: int = 2) -> None:
+    """(Re)pack the fused kernel's weight fragments of ``sets`` (bit 0 online, bit 1 target)
+    alone -- the learner's target sync; the step's fused launch then packs the online set
+    only (``conv12_fused_fwd(pack_sets=1)``).  The input scale is folded into the conv1
+    fragments: pack with the scale the forward uses."""
+    d = _conv12_desc(ws, None, None, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b)
+    d.pack_sets = int(sets)
+    _lib.check(lib.apex_conv12_pack(d, _lib.stream_ptr()), "conv12_pack")
+
+
+def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
+                     b1: torch.Tensor, w2: torch.Tensor, w2_lo: torch.Tensor, b2: torch.Tensor, scale: float,
+                     y2: torch.Tensor, y2_lo: torch.Tensor, y1: Optional[torch.Tensor] = None,
+                     y1_lo: Optional[torch.Tensor] = None, copy_n: int = 0, w1b=None, b1b=None, w2b=None,
+                     w2b_lo=None, b2b=None, rows_first: int = 0, grid: int = 0,
+                     probe: Optional[torch.Tensor] = None, pack_sets: int = 3) -> None:
+    """conv1 (fp32 OIHW weights ``w1``, exact uint8 frames from the s2d ring) + ReLU ->
+    conv2 (hi / lo bf16 OHWI ``w2``, ``w2_lo``) + ReLU in one persistent launch, y1 kept
+    in LDS; rows < ``copy_n`` also store y1 (hi / lo) for the backward.  Rows >=
+    ``rows_first`` use the second weight set (``w1b`` ..) when given.  ``pack_sets``: the
+    weight sets whose fragments the launch repacks first (the others' must be current,
+    see ``conv12_pack``)."""
+    N, C = slots.shape
+    assert slots.dtype == torch.int32 and slots.is_contiguous() and int(w1.shape[1]) == C
+    assert tuple(y2.shape) == (N, 9, 9, 64) and tuple(y2_lo.shape) == (N, 9, 9, 64)
+    d = _conv12_desc(ws, ring, slots, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b)
     d.img_switch = int(rows_first) if w1b is not None else N
     if copy_n > 0:
         assert y1 is not None and y1_lo is not None and y1.shape[0] >= copy_n and tuple(y1.shape[1:]) == (20, 20, 64)
         d.y1, d.y1_lo = y1.data_ptr(), y1_lo.data_ptr()
     d.copy_n = int(copy_n)
     d.y2, d.y2_lo = y2.data_ptr(), y2_lo.data_ptr()
-    # conv1 fragments + folded biases of both sets (csrc/conv12_fused.hip CF_W1FRAG_U4 uint4),
-    # rewritten by the launch's pack kernel
-    d.w1frag = ws.get(("cf_w1frag",), CF_W1FRAG_BYTES, ring.device, torch.uint8).data_ptr()
-    d.scratch = ws.get(("scratch1k",), 2048, ring.device, torch.uint8).data_ptr()
-    d.wfrag = c2f_wfrag_fwd_buffer(ring.device).data_ptr()
-    d.wfrag_ready = 0
-    d.N, d.C, d.in_scale = N, C, float(scale)
+    d.pack_sets = int(pack_sets)
+    d.N = N
     d.probe = _lib.ptr(probe)
     _lib.check(lib.apex_conv12_fused_fwd(d, int(grid), _lib.stream_ptr()), "conv12_fused_fwd")
 

@@ -19,7 +19,7 @@ class Conv2ImgDesc(ctypes.Structure):
 class Conv12Desc(ctypes.Structure):
     """Fused conv1 -> conv2 split forward (mirrors ``Conv12Desc`` in csrc/conv12_fused.hip)."""
     _fields_ = [("ring", c_p), ("slots", c_p), ("w1", c_p), ("w1b", c_p), ("b1", c_p), ("b1b", c_p),
-                ("w2", c_p), ("w2_lo", c_p), ("w2b", c_p), ("w2b_lo", c_p), ("wfrag", c_p), ("wfrag_ready", c_i),
+                ("w2", c_p), ("w2_lo", c_p), ("w2b", c_p), ("w2b_lo", c_p), ("wfrag", c_p), ("pack_sets", c_i),
                 ("b2", c_p), ("b2b", c_p), ("y1", c_p), ("y1_lo", c_p), ("y2", c_p), ("y2_lo", c_p),
                 ("w1frag", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("img_switch", c_i), ("copy_n", c_i),
                 ("in_scale", ctypes.c_float), ("probe", c_p)]
@@ -46,6 +46,7 @@ def declare(lib: ctypes.CDLL) -> None:
     sigs = {
         "apex_conv2_img_fwd": ([Conv2ImgDesc, c_i, c_p], c_i),
         "apex_conv12_fused_fwd": ([Conv12Desc, c_i, c_p], c_i),
+        "apex_conv12_pack": ([Conv12Desc, c_p], c_i),
         "apex_conv2_dgrad_img": ([Conv2DgradImgDesc, c_i, c_p], c_i),
         "apex_conv3_dgrad_img": ([Conv3DgradImgDesc, c_i, c_p], c_i),
         "apex_conv_fwd": ([ConvDesc, c_p], c_i),

@@ -72,11 +72,18 @@ class TorchBackend:
             self.conv1_fwd(frames[:r], wa, b, scale, out[:r], None if out_lo is None else out_lo[:r])
             self.conv1_fwd(frames[r:], wb, b2, scale, out[r:], None if out_lo is None else out_lo[r:])
 
-    def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None):
+    def conv12_pack(self, c1, c2, scale, sets=2):
+        """Repack the fused conv12 kernel's weight fragments of ``sets`` (bit 0 online, bit
+        1 target; HIP backend only) -- after the target weights change."""
+
+    def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None,
+                   pack_sets=3):
         """conv1 -> conv2 in split mode: ``c1 = (w1 fp32, b1, w1 target, b1 target)``, ``c2 =
         (w2, w2_lo, b2, w2 target, w2_lo target, b2 target)`` (target entries None: one
         set).  y1 rows < ``copy_n`` must hold conv1's output afterwards (the backward's
-        input); the HIP backend keeps the other rows in LDS (csrc/conv12_fused.hip)."""
+        input); the HIP backend keeps the other rows in LDS (csrc/conv12_fused.hip) and
+        repacks the weight fragments of ``pack_sets`` first (the others come from the last
+        ``conv12_pack``)."""
         w1, b1, w1b, b1b = c1
         w2, w2l, b2, w2b, w2bl, b2b = c2
         self.conv1_fwd_ring(ring, slots, frames_buf, w1.to(y1.dtype), b1, scale, y1,
@@ -312,15 +319,28 @@ class HipBackend(TorchBackend):
         if c2f is not None:   # this step's split conv2 forward finds its weights packed
             self._c2f_packed = tuple(_lib.ptr(t) for t in c2f)
 
-    def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None):
-        if not (self.native_conv and C.CONV12_FUSED and hasattr(self.lib, "apex_conv12_fused_fwd")):
+    def _conv12_native(self) -> bool:
+        return self.native_conv and C.CONV12_FUSED and hasattr(self.lib, "apex_conv12_fused_fwd")
+
+    def conv12_pack(self, c1, c2, scale, sets=2):
+        if not self._conv12_native():
+            return
+        w1, b1, w1b, b1b = c1
+        w2, w2l, b2, w2b, w2bl, b2b = c2
+        C.conv12_pack(self.lib, self.ws, w1, b1, w2, w2l, b2, scale, w1b=w1b, b1b=b1b, w2b=w2b, w2b_lo=w2bl,
+                      b2b=b2b, sets=sets)
+
+    def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None,
+                   pack_sets=3):
+        if not self._conv12_native():
             return super().conv12_fwd(ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first,
                                       copy_n)
         w1, b1, w1b, b1b = c1
         w2, w2l, b2, w2b, w2bl, b2b = c2
         n = slots.shape[0] if copy_n is None else int(copy_n)
         C.conv12_fused_fwd(self.lib, self.ws, ring, slots, w1, b1, w2, w2l, b2, scale, y2, y2_lo, y1=y1, y1_lo=y1_lo,
-                           copy_n=n, w1b=w1b, b1b=b1b, w2b=w2b, w2b_lo=w2bl, b2b=b2b, rows_first=rows_first)
+                           copy_n=n, w1b=w1b, b1b=b1b, w2b=w2b, w2b_lo=w2bl, b2b=b2b, rows_first=rows_first,
+                           pack_sets=pack_sets)
 
     def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
                  out_lo=None):
