@@ -76,6 +76,8 @@ struct Conv12Desc {
   int N, C, img_switch, copy_n;
   float in_scale;
   uint64_t* probe;         // phase stamps (diagnostic build, csrc/mfma_common.h PROBE), or null
+  int* wq;                 // work queue {next image, finished workgroups}: zero before the first
+                           // launch; the last workgroup to finish zeroes it again (wq_done)
 };
 
 // conv1 fragments per (set, cp, nt, K step s, hi / lo) as 64 lanes x 16 B, then the folded
@@ -166,7 +168,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   // 24 KB of partials once conv1 has read them
   constexpr int STGB = C * CF_FRAME > 2 * 3 * 4 * 64 * 16 ? C * CF_FRAME : 2 * 3 * 4 * 64 * 16;
   __shared__ __attribute__((aligned(16))) uint8_t smem[2 * CF_PLANE + 2 * STGB];
-  __shared__ int32_t slot_tbl[CF_MAXIMG * C];
+  __shared__ int q_img;                            // the work queue's next-but-one image
   uint8_t* Y1 = smem;                              // hi plane; lo plane at + CF_PLANE
   uint8_t* STG = smem + 2 * CF_PLANE;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -175,16 +177,20 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   const int g = lane >> 4, pl = lane & 15;         // conv1 (16x16 MFMA) lane roles
   const int rr = lane & 31, kg = lane >> 5;        // conv2 (32x32 MFMA) lane roles
   const int nh = wv & 1, kp = wv >> 1;             // conv2 wave roles
-  // images strided over the grid (local image i = blockIdx.x + i * gridDim.x): every
-  // workgroup gets its share of the S_t images -- the ones whose y1 also leaves for HBM
-  // (~4k cycles of store issue each) -- instead of the first workgroups getting all
-  const int G = (int)gridDim.x, img0 = blockIdx.x;
-  if (img0 >= d.N) return;
-  const int nimg = (d.N - img0 + G - 1) / G;
-  for (int i = tid; i < nimg * C; i += CF_THREADS) {
-    const int li = i / C;
-    slot_tbl[i] = d.slots[(int64_t)(img0 + li * G) * C + (i - li * C)];
+  // Images come from a device-side work queue (d.wq, csrc/mfma_common.h wq_*), two ahead
+  // of the one in flight: a workgroup that starts late -- its CU held by another kernel,
+  // e.g. RCCL's beside a data-parallel step -- takes fewer images instead of holding the
+  // launch up (scripts/bench_cu_steal.py).  Every image is computed whole by one
+  // workgroup, so the outputs do not depend on the assignment.  Images leave the queue in
+  // order: the S_t rows (y1 also copied out) spread over all workgroups first.
+  if (tid == 0) {
+    const int a = wq_fetch(d.wq), b = wq_fetch(d.wq);
+    reinterpret_cast<volatile int*>(&q_img)[0] = a;
+    reinterpret_cast<volatile int*>(Y1)[0] = b;     // (y1 is free until the first conv1)
   }
+  __syncthreads();
+  int cur = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_img)[0]);
+  int nxt = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(Y1)[0]);
   __syncthreads();
 
   // ---- LDS-DMA of image `li` into staging buffer `buf`: piece k = wv + 4 j (1 KB) copies
@@ -194,10 +200,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   constexpr int NPF = (CF_FRAME + 1023) / 1024;   // pieces per frame (7)
   constexpr int NDMA = C * NPF;
   constexpr int NDW = (NDMA + 3) / 4;             // per wave (max)
-  auto image_slots = [&](int li, int* sl) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) sl[c] = c < C ? slot_tbl[li * C + c] : 0;   // (VGPRs: SGPRs are short)
-  };
+  auto image_slots = [&](int img, int* sl) { sload_slots<C>(d.slots + (int64_t)img * C, *reinterpret_cast<int(*)[4]>(sl)); };
   auto issue_dma_piece = [&](const int* sl, int buf, int j) {
     const int k = wv + 4 * j;
     if (k < NDMA) {
@@ -209,9 +212,9 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
       if (r * 1024 + lane * 16 < CF_FRAME) dma16_s(src, (uint32_t)lane * 16u, dst);
     }
   };
-  auto issue_dma = [&](int li, int buf) {
+  auto issue_dma = [&](int img, int buf) {
     int sl[4];
-    image_slots(li, sl);
+    image_slots(img, sl);
 #pragma unroll
     for (int j = 0; j < NDW; ++j) issue_dma_piece(sl, buf, j);
   };
@@ -269,30 +272,44 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   // moves ~7-25 B per cycle, so 12 stores in a row after the reduction cost ~3k cycles
   uint4 pend[3][2];
   int pend_img = -1;
+  // byte offset of this lane's y2 quad at (mt, jq = 0) within an image, -1 for padding
+  // rows (their lanes skip; every wave has valid lanes in each mt, so the 12 store
+  // instructions per wave and image that the vmcnt wait after conv1 counts always issue)
+  int yoff[3];
+#pragma unroll
+  for (int mt = 0; mt < 3; ++mt) {
+    const int r = mt * 32 + rr, oh = r / 10, ow = r - oh * 10;
+    yoff[mt] = (oh < 9 && ow < 9) ? ((oh * 9 + ow) * 64 + nh * 32 + 4 * kg) * 2 : -1;
+  }
   auto store_y2 = [&](int q) {       // q = 2 (2 mt + jh) + plane, 0 .. 11
     const int mt = q >> 2, jh = (q >> 1) & 1, plane = q & 1;
     const int jq = 2 * kp + jh;
-    const int r = mt * 32 + rr, oh = r / 10, ow = r - oh * 10;
-    const bool valid = oh < 9 && ow < 9;
-    // every lane stores (padding pixels into scratch): 12 store instructions per wave and
-    // image, which the vmcnt wait after conv1 counts
-    const int64_t o2 = ((int64_t)pend_img * 81 + oh * 9 + ow) * 64 + nh * 32 + 8 * jq + 4 * kg;
-    bf16_t* dst = valid ? (plane ? d.y2_lo : d.y2) + o2 : reinterpret_cast<bf16_t*>(d.scratch + lane * 8);
-    const uint4 v = pend[mt][jh];
-    *reinterpret_cast<uint2*>(dst) = plane ? make_uint2(v.z, v.w) : make_uint2(v.x, v.y);
+    // uniform base (image) + 32-bit lane offset: the saddr store form, no 64-bit math
+    const uint8_t* base = reinterpret_cast<const uint8_t*>((plane ? d.y2_lo : d.y2) + (int64_t)pend_img * 5184);
+    if (yoff[mt] >= 0) {
+      const uint4 v = pend[mt][jh];
+      *reinterpret_cast<uint2*>(const_cast<uint8_t*>(base) + (uint32_t)(yoff[mt] + 16 * jq)) =
+          plane ? make_uint2(v.z, v.w) : make_uint2(v.x, v.y);
+    }
   };
   // image i's frames land in staging(i & 1): image 0's here, image i + 1's during conv1(i)
-  issue_dma(0, 0);
-  for (int i = 0; i < nimg; ++i) {
-    const int img = img0 + i * G;
+  if (cur < d.N) issue_dma(cur, 0);
+  for (int i = 0; cur < d.N; ++i) {
+    const int img = cur;
+    const bool more = nxt < d.N;
     const int set = (two && img >= d.img_switch) ? 1 : 0;
     if (set != cur_set) {
       load_weights(set);      // vmcnt(0): every DMA issued so far has landed as well
       cur_set = set;
       __syncthreads();
     }
-    int nsl[4];                                       // image i + 1's frame slots
-    if (i + 1 < nimg) image_slots(i + 1, nsl);
+    int nsl[4] = {0, 0, 0, 0};                        // image i + 1's frame slots
+    if (more) image_slots(nxt, nsl);
+    // the image after next (read after this image's last barrier).  The fetch's return is
+    // waited for here, before any DMA is in flight: ~0.5 us of one wave per image (the
+    // compiler moves the value into a register of its choosing at once, so a later use
+    // does not hide the atomic's latency)
+    if (tid == 0) reinterpret_cast<volatile int*>(&q_img)[0] = more ? wq_fetch(d.wq) : d.N;
     PROBE(d.probe, 4, i, 0);
     const uint8_t* S = STG + (i & 1) * STGB;
     // ================= conv1: this wave's pixel tiles T = th + 2 j, j = 0 .. 12 (16 pixels
@@ -327,8 +344,8 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
           for (int r = 2 * part; r < 2 * part + 2; ++r)
             ev[nt][r] = fmaxf(fmaf(accl[nt][r], 1.f / CF_LO_SCALE, acc[nt][r]), 0.f);
         } else if (part == 2) {
-          split_pk_bf16(ev[nt][0], ev[nt][1], eh[nt][0], el[nt][0]);
-          split_pk_bf16(ev[nt][2], ev[nt][3], eh[nt][1], el[nt][1]);
+          split_pk_bf16_s(ev[nt][0], ev[nt][1], eh[nt][0], el[nt][0]);
+          split_pk_bf16_s(ev[nt][2], ev[nt][3], eh[nt][1], el[nt][1]);
         } else {
           const int p = 16 * (th + 2 * j) + pl, oh = p / 20, ow = p - 20 * oh;
           const int P = (j == 12 && p >= 400) ? 400 + (pl & 7) : cf_pix(oh, ow);
@@ -385,7 +402,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
         // image i + 1's frames -> staging((i + 1) & 1), one 1-KB DMA per tile among the
         // MFMAs (that buffer's last readers -- conv1(i - 1), the reduction of image i - 1
         // -- finished before the barrier that closed image i - 1)
-        if (j - 1 < NDW && i + 1 < nimg) issue_dma_piece(nsl, (i + 1) & 1, j - 1);
+        if (j - 1 < NDW && more) issue_dma_piece(nsl, (i + 1) & 1, j - 1);
         if (i > 0) store_y2(j - 1);                           // image i - 1's y2
         __builtin_amdgcn_sched_barrier(0);
         mfma_tile(u[j & 1], a[j & 1], al[j & 1], j - 1, a[(j - 1) & 1], al[(j - 1) & 1]);
@@ -494,6 +511,8 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
     if (kp == 0) give(2);
     else give(0);
     __syncthreads();          // partials visible; every read of y1 is done
+    // (read before the closing barrier: thread 0 rewrites it at the next image's start)
+    const int nn = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_img)[0]);
     // acc2[mt][4 jq + i] = D[channel 32 nh + 8 jq + 4 kg + i][pixel mt * 32 + rr]
     auto finish = [&](const int jq0, const bool own_first) {
 #pragma unroll
@@ -521,9 +540,14 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
     else finish(2, false);               // (bias + pair 0) + own pair 1
     pend_img = img;
     __syncthreads();          // the partials are read: staging(i) may take image i + 2's frames
+    cur = nxt;
+    nxt = nn;
   }
+  if (pend_img >= 0) {
 #pragma unroll
-  for (int q = 0; q < 12; ++q) store_y2(q);   // the last image's y2
+    for (int q = 0; q < 12; ++q) store_y2(q);   // the last image's y2
+  }
+  if (tid == 0) wq_done(d.wq);
 }
 
 static int cf_launch_pack(const Conv12Desc& d, hipStream_t st) {
@@ -556,7 +580,7 @@ APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if (d.N < 1) return 0;
   if (d.ring == nullptr || d.slots == nullptr || d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr ||
       d.w2_lo == nullptr || d.b2 == nullptr || d.y2 == nullptr || d.y2_lo == nullptr ||
-      d.wfrag == nullptr || d.scratch == nullptr || d.w1frag == nullptr)
+      d.wfrag == nullptr || d.scratch == nullptr || d.w1frag == nullptr || d.wq == nullptr)
     return (int)hipErrorInvalidValue;
   const bool two = d.w1b != nullptr;
   if (two && (d.b1b == nullptr || d.w2b == nullptr || d.w2b_lo == nullptr || d.b2b == nullptr))

@@ -434,7 +434,20 @@ struct Conv2DgradImgDesc {
   // in the step (wfrag_ready: the fc forward's epilogue launch does it in spare blocks)
   uint4* wfrag;
   int wfrag_ready;
+  int* wq;         // image work queue {next, finished workgroups} (csrc/mfma_common.h wq_*), zero
+                   // before the first launch and left zero by each launch
 };
+
+// Images come from the work queue: thread 0 fetches the next image while this one's
+// MFMAs run (after its dY loads, so no vmcnt wait on those covers the atomic) and hands
+// it over through LDS before the copy-out barrier.  A workgroup whose CU is taken by
+// another kernel (RCCL beside a data-parallel step) simply does fewer images; every
+// image is computed whole by one workgroup, so the outputs do not depend on who did it.
+#define C2D_WQ_BEGIN(q_next_, img_)                                      \
+  if (threadIdx.x == 0) reinterpret_cast<volatile int*>(&(q_next_))[0] = wq_fetch(d.wq); \
+  __syncthreads();                                                       \
+  int img_ = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&(q_next_))[0]); \
+  int wq_fetched_ = 0;
 
 #define C2D_SLOTS 121   // 11 x 11 padded dY slots, 128 B each
 // The M rows of the dgrad GEMMs are output pixels on an 11-wide grid (the slot grid's
@@ -478,7 +491,9 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
     pi[t] = r / 11;
     pj[t] = r - pi[t] * 11;
   }
-  for (int img = blockIdx.x; img < d.N; img += gridDim.x) {
+  __shared__ int q_next;
+  C2D_WQ_BEGIN(q_next, img)
+  while (img < d.N) {
     __syncthreads();   // previous image: LDS reads and output copy-out done
     {
       const uint4* src = reinterpret_cast<const uint4*>(dyp + (int64_t)img * 81 * 64);
@@ -488,6 +503,7 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
       }
     }
     __syncthreads();
+    if (tid == 0) wq_fetched_ = wq_fetch(d.wq);
     f32x16 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -515,6 +531,7 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
             make_uint2(cvt_pk_bf16(acc[t][4 * g], acc[t][4 * g + 1]), cvt_pk_bf16(acc[t][4 * g + 2], acc[t][4 * g + 3]));
       }
     }
+    if (tid == 0) reinterpret_cast<volatile int*>(&q_next)[0] = wq_fetched_;
     __syncthreads();
     // coalesced copy-out with the ReLU mask of y1 applied per 16-B chunk (mask loads
     // issued together, then the stores)
@@ -538,7 +555,9 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
         dst[k] = v;
       }
     }
+    img = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_next)[0]);
   }
+  if (tid == 0) wq_done(d.wq);
 }
 
 
@@ -574,7 +593,9 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
     pi[t] = r / 10;
     pj[t] = r - pi[t] * 10;
   }
-  for (int img = blockIdx.x; img < d.N; img += gridDim.x) {
+  __shared__ int q_next;
+  C2D_WQ_BEGIN(q_next, img)
+  while (img < d.N) {
     __syncthreads();   // previous image: LDS reads and output copy-out done
     {
       const uint4* src = reinterpret_cast<const uint4*>(d.dy + (int64_t)img * 81 * 64);
@@ -587,6 +608,7 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
       }
     }
     __syncthreads();
+    if (tid == 0) wq_fetched_ = wq_fetch(d.wq);
     f32x16 acc[2][4];
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh)
@@ -637,6 +659,7 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
           *reinterpret_cast<uint2*>(sout + 400 * 128 + o) = make_uint2(l01, l23);
         }
     }
+    if (tid == 0) reinterpret_cast<volatile int*>(&q_next)[0] = wq_fetched_;
     __syncthreads();
     const uint4* msrc = reinterpret_cast<const uint4*>(d.mask + (int64_t)img * 400 * 64);
     uint4* dst = reinterpret_cast<uint4*>(d.dx + (int64_t)img * 400 * 64);
@@ -665,14 +688,16 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
         }
       }
     }
+    img = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_next)[0]);
   }
+  if (tid == 0) wq_done(d.wq);
 }
 
 APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t st) {
   if (d.N <= 0 || d.dy == nullptr || d.w == nullptr || d.mask == nullptr || d.dx == nullptr)
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)d.dy | (uintptr_t)d.w | (uintptr_t)d.mask | (uintptr_t)d.dx) & 15) return (int)hipErrorInvalidValue;
-  if (d.wfrag == nullptr || ((uintptr_t)d.wfrag & 15)) return (int)hipErrorInvalidValue;
+  if (d.wfrag == nullptr || ((uintptr_t)d.wfrag & 15) || d.wq == nullptr) return (int)hipErrorInvalidValue;
   const bool split = d.dy_lo != nullptr;
   if (split && (d.w_lo == nullptr || d.dx_lo == nullptr || (((uintptr_t)d.dy_lo | (uintptr_t)d.dx_lo) & 15)))
     return (int)hipErrorInvalidValue;

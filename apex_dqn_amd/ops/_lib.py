@@ -130,6 +130,7 @@ _SIGS = {
     "apex_rmsprop_step": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p, c_i, c_i,
                            c_p], c_i),
     "apex_cast_bf16": ([c_p, c_p, c_i64, c_p, c_p], c_i),
+    "apex_spin_hold": ([c_i, c_i, c_i, c_p, c_p], c_i),
     "apex_rmsprop_step_np": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p,
                               c_i, c_i, c_p], c_i),
     "apex_grad_finalize": ([FinalizeDesc, c_p], c_i),

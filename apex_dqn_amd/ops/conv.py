@@ -27,6 +27,16 @@ class Workspace:
             self.bufs[k] = t
         return t
 
+    def get_zeroed(self, key, numel: int, device, dtype=torch.int32) -> torch.Tensor:
+        """A buffer zeroed when first made (work-queue counters: the kernels leave them
+        zero again at their end)."""
+        k = (key, numel, str(device), dtype)
+        t = self.bufs.get(k)
+        if t is None:
+            t = torch.zeros(numel, dtype=dtype, device=device)
+            self.bufs[k] = t
+        return t
+
 
 # scratch for launchers called without a workspace (tests, microbenchmarks)
 _DEFAULT_WS = Workspace()
@@ -259,6 +269,7 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     d.pack_sets = int(pack_sets)
     d.N = N
     d.probe = _lib.ptr(probe)
+    d.wq = ws.get_zeroed(("cf_wq",), 2, ring.device).data_ptr()
     _lib.check(lib.apex_conv12_fused_fwd(d, int(grid), _lib.stream_ptr()), "conv12_fused_fwd")
 
 
@@ -428,6 +439,7 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
     ws = ws if ws is not None else _DEFAULT_WS
     d.wfrag = c2d_wfrag_buffer(ws, dy.device).data_ptr()
     d.wfrag_ready = int(packed)
+    d.wq = ws.get_zeroed(("c2d_wq",), 2, dy.device).data_ptr()
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 

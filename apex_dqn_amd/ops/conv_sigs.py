@@ -22,13 +22,13 @@ class Conv12Desc(ctypes.Structure):
                 ("w2", c_p), ("w2_lo", c_p), ("w2b", c_p), ("w2b_lo", c_p), ("wfrag", c_p), ("pack_sets", c_i),
                 ("b2", c_p), ("b2b", c_p), ("y1", c_p), ("y1_lo", c_p), ("y2", c_p), ("y2_lo", c_p),
                 ("w1frag", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("img_switch", c_i), ("copy_n", c_i),
-                ("in_scale", ctypes.c_float), ("probe", c_p)]
+                ("in_scale", ctypes.c_float), ("probe", c_p), ("wq", c_p)]
 
 
 class Conv2DgradImgDesc(ctypes.Structure):
     """Image-resident conv2 data gradient (mirrors ``Conv2DgradImgDesc`` in csrc/conv2_img.hip)."""
     _fields_ = [("dy", c_p), ("w", c_p), ("mask", c_p), ("dx", c_p), ("N", c_i), ("dy_lo", c_p), ("w_lo", c_p),
-                ("dx_lo", c_p), ("wfrag", c_p), ("wfrag_ready", c_i)]
+                ("dx_lo", c_p), ("wfrag", c_p), ("wfrag_ready", c_i), ("wq", c_p)]
 
 
 class C2dPackJob(ctypes.Structure):
