@@ -332,7 +332,7 @@ class ImpalaActorGroup(GpuActorGroup):
         self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
         h = self.learner.trunk_forward(self.slots, self.ps, self.bufs)
         heads = {k: self.ps["V"][k] for k in ("wv", "bv", "wa", "ba")}
-        self.ops.actor_head(h, heads, self.eps, self.ctr, self.seed, self.q, self.act)
+        self.ops.actor_head(h, heads, self.eps, self.ctr, self.seed, self.q, self.act, H_lo=self.bufs.get("h_lo"))
         self.ctr += 1
         self.q_host.copy_(self.q, non_blocking=True)
         self.a_host.copy_(self.act, non_blocking=True)

@@ -77,7 +77,8 @@ struct Conv12Desc {
   float in_scale;
   uint64_t* probe;         // phase stamps (diagnostic build, csrc/mfma_common.h PROBE), or null
   int* wq;                 // work queue {next image, finished workgroups}: zero before the first
-                           // launch; the last workgroup to finish zeroes it again (wq_done)
+                           // launch; the last workgroup to finish zeroes it again (wq_done);
+                           // null: static strided image order (mfma_common.h wq_next)
 };
 
 // conv1 fragments per (set, cp, nt, K step s, hi / lo) as 64 lanes x 16 B, then the folded
@@ -183,8 +184,9 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   // launch up (scripts/bench_cu_steal.py).  Every image is computed whole by one
   // workgroup, so the outputs do not depend on the assignment.  Images leave the queue in
   // order: the S_t rows (y1 also copied out) spread over all workgroups first.
+  int wq_seq = 0;                                  // (thread 0: static order, d.wq null)
   if (tid == 0) {
-    const int a = wq_fetch(d.wq), b = wq_fetch(d.wq);
+    const int a = wq_next(d.wq, wq_seq), b = wq_next(d.wq, wq_seq);
     reinterpret_cast<volatile int*>(&q_img)[0] = a;
     reinterpret_cast<volatile int*>(Y1)[0] = b;     // (y1 is free until the first conv1)
   }
@@ -309,7 +311,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
     // waited for here, before any DMA is in flight: ~0.5 us of one wave per image (the
     // compiler moves the value into a register of its choosing at once, so a later use
     // does not hide the atomic's latency)
-    if (tid == 0) reinterpret_cast<volatile int*>(&q_img)[0] = more ? wq_fetch(d.wq) : d.N;
+    if (tid == 0) reinterpret_cast<volatile int*>(&q_img)[0] = more ? wq_next(d.wq, wq_seq) : d.N;
     PROBE(d.probe, 4, i, 0);
     const uint8_t* S = STG + (i & 1) * STGB;
     // ================= conv1: this wave's pixel tiles T = th + 2 j, j = 0 .. 12 (16 pixels
@@ -580,7 +582,7 @@ APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if (d.N < 1) return 0;
   if (d.ring == nullptr || d.slots == nullptr || d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr ||
       d.w2_lo == nullptr || d.b2 == nullptr || d.y2 == nullptr || d.y2_lo == nullptr ||
-      d.wfrag == nullptr || d.scratch == nullptr || d.w1frag == nullptr || d.wq == nullptr)
+      d.wfrag == nullptr || d.scratch == nullptr || d.w1frag == nullptr)
     return (int)hipErrorInvalidValue;
   const bool two = d.w1b != nullptr;
   if (two && (d.b1b == nullptr || d.w2b == nullptr || d.w2b_lo == nullptr || d.b2b == nullptr))

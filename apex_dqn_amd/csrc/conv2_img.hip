@@ -435,7 +435,7 @@ struct Conv2DgradImgDesc {
   uint4* wfrag;
   int wfrag_ready;
   int* wq;         // image work queue {next, finished workgroups} (csrc/mfma_common.h wq_*), zero
-                   // before the first launch and left zero by each launch
+                   // before the first launch and left zero by each launch; null: static order
 };
 
 // Images come from the work queue: thread 0 fetches the next image while this one's
@@ -444,7 +444,8 @@ struct Conv2DgradImgDesc {
 // another kernel (RCCL beside a data-parallel step) simply does fewer images; every
 // image is computed whole by one workgroup, so the outputs do not depend on who did it.
 #define C2D_WQ_BEGIN(q_next_, img_)                                      \
-  if (threadIdx.x == 0) reinterpret_cast<volatile int*>(&(q_next_))[0] = wq_fetch(d.wq); \
+  int wq_seq_ = 0;                                                       \
+  if (threadIdx.x == 0) reinterpret_cast<volatile int*>(&(q_next_))[0] = wq_next(d.wq, wq_seq_); \
   __syncthreads();                                                       \
   int img_ = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&(q_next_))[0]); \
   int wq_fetched_ = 0;
@@ -503,7 +504,7 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
       }
     }
     __syncthreads();
-    if (tid == 0) wq_fetched_ = wq_fetch(d.wq);
+    if (tid == 0) wq_fetched_ = wq_next(d.wq, wq_seq_);
     f32x16 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -608,7 +609,7 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
       }
     }
     __syncthreads();
-    if (tid == 0) wq_fetched_ = wq_fetch(d.wq);
+    if (tid == 0) wq_fetched_ = wq_next(d.wq, wq_seq_);
     f32x16 acc[2][4];
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh)
@@ -697,7 +698,7 @@ APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t 
   if (d.N <= 0 || d.dy == nullptr || d.w == nullptr || d.mask == nullptr || d.dx == nullptr)
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)d.dy | (uintptr_t)d.w | (uintptr_t)d.mask | (uintptr_t)d.dx) & 15) return (int)hipErrorInvalidValue;
-  if (d.wfrag == nullptr || ((uintptr_t)d.wfrag & 15) || d.wq == nullptr) return (int)hipErrorInvalidValue;
+  if (d.wfrag == nullptr || ((uintptr_t)d.wfrag & 15)) return (int)hipErrorInvalidValue;
   const bool split = d.dy_lo != nullptr;
   if (split && (d.w_lo == nullptr || d.dx_lo == nullptr || (((uintptr_t)d.dy_lo | (uintptr_t)d.dx_lo) & 15)))
     return (int)hipErrorInvalidValue;

@@ -221,7 +221,18 @@ __device__ __forceinline__ int wq_fetch(int* ctr) {
   asm volatile("v_mov_b32 %0, 0" : "=v"(z));
   return atomicAdd(ctr + z, 1);
 }
+// Item source of a persistent kernel: ctr == nullptr gives the static strided order
+// (the k-th item of workgroup b is b + k * gridDim.x; `seq` counts k, no atomics); else
+// the work queue.  The queue costs a device-scope atomic round trip per item (all
+// workgroups on one counter: ~15 us on the fused forward, ~11 us on the conv2 data
+// gradient of the fp32 step), so the learner enables it only where another kernel can
+// hold CUs during the launch (the data-parallel step's RCCL collectives).
+__device__ __forceinline__ int wq_next(int* ctr, int& seq) {
+  if (ctr == nullptr) return (int)blockIdx.x + (seq++) * (int)gridDim.x;
+  return wq_fetch(ctr);
+}
 __device__ __forceinline__ void wq_done(int* ctr) {
+  if (ctr == nullptr) return;
   __threadfence();
   if (atomicAdd(ctr + 1, 1) == (int)gridDim.x - 1) {
     atomicExch(ctr, 0);

@@ -128,6 +128,10 @@ class FusedNatureLearner(IsNormMixin):
         # at world 1 too (an initialised process group of one rank: RCCL capture checks
         # and the segmented-step overhead on a single GPU)
         self._dp = self.world > 1 or (bool(self.rt.force_dp) and comm is not None)
+        # image work queues in the persistent kernels (ops/conv.py Workspace.work_queue):
+        # only where RCCL's kernels may hold CUs during the step
+        if hasattr(self.ops, "ws"):
+            self.ops.ws.work_queue = self._dp
         self._alloc(self.B)
         self._init_is_norm()
         self._graphs = None     # one-update graph

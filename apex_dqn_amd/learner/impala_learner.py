@@ -36,7 +36,7 @@ import torch
 from ..config import ApexConfig
 from ..models.dueling import ImpalaDuellingDQN
 from ..models.flat_params import FlatLayout
-from ..ops.fused_ops import HipBackend, TorchBackend
+from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
 from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
 from .fused_learner import _enable_sharding
@@ -84,10 +84,23 @@ class FusedImpalaLearner(IsNormMixin):
         if backend is None:
             backend = "hip" if (self.device.type == "cuda" and self.rt.use_hip_kernels) else "torch"
         on_gpu = backend == "hip"
+        if self.rt.dtype not in ("fp32", "bf16"):
+            raise ValueError("Runtime.dtype must be fp32 or bf16")
+        bf16_torch = self.device.type == "cuda" and self.rt.dtype == "bf16"
         self.ops = HipBackend(native_conv=True) if on_gpu else TorchBackend(
-            torch.bfloat16 if self.device.type == "cuda" else torch.float32)
+            torch.bfloat16 if bf16_torch else torch.float32)
         self.iops = HipImpalaOps() if on_gpu else TorchImpalaOps()
-        self.act_dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+        # split mode (Runtime.dtype fp32 on the HIP kernels): fp32 trunk activations and
+        # gradients, bf16 hi + lo weight fragments, three MFMAs per product
+        # (csrc/impala_split.hip); the fc / heads run the NatureCNN split kernels on the
+        # bf16 hi / lo planes of feat and h.  The torch backend is the fp32 oracle (bf16
+        # on the GPU when asked for).
+        self.split = on_gpu and self.rt.dtype == "fp32"
+        if on_gpu:
+            self.act_dtype = torch.float32 if self.split else torch.bfloat16
+            self.op_dtype = torch.bfloat16                  # GEMM operand planes
+        else:
+            self.act_dtype = self.op_dtype = torch.bfloat16 if bf16_torch else torch.float32
         d = self.device
 
         # ---- flat parameter layout (conv trunk first: the DP fc/heads bucket starts at wfc)
@@ -106,17 +119,24 @@ class FusedImpalaLearner(IsNormMixin):
         self.layout = FlatLayout(segs)
         n = self.layout.numel
         self.p32 = torch.zeros(n, dtype=torch.float32, device=d)
-        self.pbf = torch.zeros(n, dtype=self.act_dtype, device=d)
+        # bf16 compute copies [hi | lo] of the online / target parameters (lo: split mode)
+        nb = 2 * n if self.split else n
+        self._pbf_all = torch.zeros(nb, dtype=self.op_dtype, device=d)
+        self._tbf_all = torch.zeros(nb, dtype=self.op_dtype, device=d)
+        self.pbf, self.tbf = self._pbf_all[:n], self._tbf_all[:n]
+        self.pbf_lo = self._pbf_all[n:] if self.split else None
+        self.tbf_lo = self._tbf_all[n:] if self.split else None
         self.g32 = torch.zeros(n, dtype=torch.float32, device=d)
         self.rms_v = torch.zeros(n, dtype=torch.float32, device=d)
         self.rms_m = torch.zeros(n, dtype=torch.float32, device=d)
         self.t32 = torch.zeros(n, dtype=torch.float32, device=d)
-        self.tbf = torch.zeros(n, dtype=self.act_dtype, device=d)
         self.P = self.layout.views(self.p32)
         self.Pb = self.layout.views(self.pbf)
         self.G = self.layout.views(self.g32)
         self.T = self.layout.views(self.t32)
         self.Tb = self.layout.views(self.tbf)
+        self.Pl = self.layout.views(self.pbf_lo) if self.split else None
+        self.Tl = self.layout.views(self.tbf_lo) if self.split else None
         self._perm = fc_column_perm(d)
         for convs in self.specs:
             for cs in convs:
@@ -126,11 +146,15 @@ class FusedImpalaLearner(IsNormMixin):
                     cs.frag = torch.zeros(frag_elems(cs.cin, cs.cout), dtype=torch.bfloat16, device=d)
                     cs.fragT = torch.zeros(frag_elems(cs.cout, cs.cin), dtype=torch.bfloat16, device=d)
                     cs.frag_tgt = torch.zeros_like(cs.frag)
+                if self.split:
+                    cs.extra["wl"], cs.extra["w_tgt_lo"] = self.Pl[cs.name + ".w"], self.Tl[cs.name + ".w"]
+                    cs.frag_lo, cs.fragT_lo = torch.zeros_like(cs.frag), torch.zeros_like(cs.fragT)
+                    cs.frag_tgt_lo = torch.zeros_like(cs.frag)
         init = ImpalaDuellingDQN((self.C, 84, 84), self.A, channels=CH, hidden=HIDDEN)
         self.load_module_state(init.state_dict(), self.P)
         if comm is not None and comm.world_size > 1:
             comm.broadcast_flat(self.p32)
-        self.pbf.copy_(self.p32)
+        self._refresh_bf16()
         self.num_q_updates = 0
         self._alloc(self.B)
         self.sync_target()
@@ -164,21 +188,31 @@ class FusedImpalaLearner(IsNormMixin):
         self.S["obs"] = self.slots[:B]
         self.S["nxt"] = self.slots[B:2 * B]
         self.fw, self.bw = [], []
-        self.feat = torch.zeros(N3, FEAT_LD, dtype=ad, device=d)     # pad columns stay 0
-        self.dfeat = torch.zeros(B, FEAT_LD, dtype=ad, device=d)
+        od = self.op_dtype
+        # fc operand rows (pad columns stay 0); split mode: bf16 hi + lo planes written by
+        # the last residual block, and the fc data gradient's planes merged to fp32
+        self.feat = torch.zeros(N3, FEAT_LD, dtype=od if self.split else ad, device=d)
+        self.feat_lo = torch.zeros(N3, FEAT_LD, dtype=od, device=d) if self.split else None
+        self.dfeat = torch.zeros(B, FEAT_LD, dtype=od if self.split else ad, device=d)
+        self.dfeat_lo = torch.zeros(B, FEAT_LD, dtype=od, device=d) if self.split else None
+        self.dfeat32 = torch.zeros(B, FEAT_LD, dtype=torch.float32, device=d) if self.split else self.dfeat
         for s, (cin, cout, hw, php) in enumerate(_stack_dims()):
             P = cout // 16
             t = lambda n, h: torch.zeros(n, P, h, h, 16, dtype=ad, device=d)  # noqa: E731
             f = dict(p=t(N3, php), ya=t(N3, php), ra=t(N3, php), yb=t(N3, php),
                      amax=torch.zeros(N3, P, php, php, 16, dtype=torch.uint8, device=d))
             f["o"] = (self.feat[:, :FEAT].view(N3, P, php, php, 16) if s == 2 else t(N3, php))
+            if s == 2 and self.split:
+                f["o_lo"] = self.feat_lo[:, :FEAT].view(N3, P, php, php, 16)
             self.fw.append(f)
             b = dict(d_yb=t(B, php), d_ra=t(B, php), d_ya=t(B, php), d_p=t(B, php), d_c0=t(B, hw))
             if s < 2:
                 b["d_o"] = t(B, php)    # gradient of this stack's output (the next stack's conv0 dgrad)
             self.bw.append(b)
-        self.h = torch.zeros(N3, 2 * HIDDEN, dtype=ad, device=d)
-        self.dH = torch.zeros(B, 2 * HIDDEN, dtype=ad, device=d)
+        self.h = torch.zeros(N3, 2 * HIDDEN, dtype=od, device=d)
+        self.dH = torch.zeros(B, 2 * HIDDEN, dtype=od, device=d)
+        self.h_lo = torch.zeros(N3, 2 * HIDDEN, dtype=od, device=d) if self.split else None
+        self.dH_lo = torch.zeros(B, 2 * HIDDEN, dtype=od, device=d) if self.split else None
         self.dhead = torch.zeros(B, self.A + 1, dtype=torch.float32, device=d)
         self.td_abs = torch.zeros(B, dtype=torch.float32, device=d)
         self.loss_b = torch.zeros(B, dtype=torch.float32, device=d)
@@ -191,9 +225,13 @@ class FusedImpalaLearner(IsNormMixin):
         jobs = []
         for convs in self.specs:
             for cs in convs:
-                jobs.append((cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs)))
-                if cs.cin_real == cs.cin:   # the ring conv needs no data gradient
-                    jobs.append((cs.wb, cs.fragT, cs.cin, cs.cout, cs.cin_real, 1))
+                planes = [(cs.wb, cs.frag, cs.fragT)]
+                if self.split:
+                    planes.append((cs.extra["wl"], cs.frag_lo, cs.fragT_lo))
+                for w, f, fT in planes:
+                    jobs.append((w, f, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs)))
+                    if cs.cin_real == cs.cin:   # the ring conv needs no data gradient
+                        jobs.append((w, fT, cs.cin, cs.cout, cs.cin_real, 1))
         self.iops.pack(jobs)
 
     @staticmethod
@@ -201,8 +239,14 @@ class FusedImpalaLearner(IsNormMixin):
         return 2 if cs.cin_real < cs.cin else 0     # 4-frame ring conv: tap-pair fragments
 
     def _pack_target(self) -> None:
-        self.iops.pack([(cs.extra["w_tgt"], cs.frag_tgt, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs))
-                        for convs in self.specs for cs in convs])
+        jobs = []
+        for convs in self.specs:
+            for cs in convs:
+                jobs.append((cs.extra["w_tgt"], cs.frag_tgt, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs)))
+                if self.split:
+                    jobs.append((cs.extra["w_tgt_lo"], cs.frag_tgt_lo, cs.cin, cs.cout, cs.cin_real,
+                                 self._fwd_kind(cs)))
+        self.iops.pack(jobs)
 
     # ------------------------------------------------------------ forward
     def forward_all(self) -> None:
@@ -222,17 +266,29 @@ class FusedImpalaLearner(IsNormMixin):
             # B training rows only (the backward's ReLU masks / weight-gradient inputs)
             io.resblock(f["p"], r0a, r0b, f["ra"], ysave=f["ya"], n_save=B, target=True, n_switch=2 * B)
             io.resblock(f["ra"], r1a, r1b, f["o"], ysave=f["yb"], n_save=B, target=True, n_switch=2 * B,
-                        relu_out=(s == 2))
+                        relu_out=(s == 2), **self._lo(out_lo=f.get("o_lo")))
             x = f["o"]
-        self.ops.fc_fwd(self.feat, self.Pb["wfc"], self.P["bfc"], self.h, self.Tb["wfc"], self.T["bfc"], 2 * B)
+        self.ops.fc_fwd(self.feat, self.Pb["wfc"], self.P["bfc"], self.h, self.Tb["wfc"], self.T["bfc"], 2 * B,
+                        **self._lo(x_lo=self.feat_lo, w_lo=self.Pl and self.Pl["wfc"],
+                                   w2_lo=self.Tl and self.Tl["wfc"], out_lo=self.h_lo))
+
+    def _lo(self, **kw):
+        """Split-mode keyword arguments of an op (empty with bf16 operands)."""
+        return kw if self.split else {}
+
+    def _refresh_bf16(self) -> None:
+        """bf16 compute copy (and its lo plane) from the fp32 master weights."""
+        split_into(self.p32, self.pbf, self.pbf_lo)
 
     # ------------------------------------------------- actor-side inference
     def actor_param_set(self) -> Dict:
         """A private parameter slot for an actor group (fp32 + bf16 copies and, on
         the HIP path, packed fragments); refreshed by ``refresh_param_set``."""
         import dataclasses
-        p32, pbf = self.p32.clone(), self.pbf.clone()
-        V, Vb = self.layout.views(p32), self.layout.views(pbf)
+        n = self.layout.numel
+        p32, pall = self.p32.clone(), self._pbf_all.clone()
+        V, Vb = self.layout.views(p32), self.layout.views(pall[:n])
+        Vl = self.layout.views(pall[n:]) if self.split else None
         specs = []
         for convs in self.specs:
             row = []
@@ -241,28 +297,41 @@ class FusedImpalaLearner(IsNormMixin):
                                          extra=dict(cs.extra))
                 if cs.frag is not None:
                     c2.frag = torch.zeros_like(cs.frag)
-                    c2.fragT = c2.frag_tgt = None
+                    c2.fragT = c2.frag_tgt = c2.fragT_lo = c2.frag_tgt_lo = None
+                if self.split:
+                    c2.extra["wl"] = Vl[cs.name + ".w"]
+                    c2.frag_lo = torch.zeros_like(cs.frag_lo)
                 row.append(c2)
             specs.append(row)
-        ps = dict(p32=p32, pbf=pbf, V=V, Vb=Vb, specs=specs)
+        ps = dict(p32=p32, pbf=pall, V=V, Vb=Vb, Vl=Vl, specs=specs)
         self.refresh_param_set(ps)
         return ps
 
     def refresh_param_set(self, ps: Dict) -> None:
         ps["p32"].copy_(self.p32)
-        ps["pbf"].copy_(self.pbf)
-        self.iops.pack([(cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs))
-                        for row in ps["specs"] for cs in row])
+        ps["pbf"].copy_(self._pbf_all)
+        jobs = []
+        for row in ps["specs"]:
+            for cs in row:
+                jobs.append((cs.wb, cs.frag, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs)))
+                if self.split:
+                    jobs.append((cs.extra["wl"], cs.frag_lo, cs.cin, cs.cout, cs.cin_real, self._fwd_kind(cs)))
+        self.iops.pack(jobs)
 
     def alloc_trunk(self, E: int) -> Dict:
-        d, ad = self.device, self.act_dtype
-        bufs = dict(stacks=[], feat=torch.zeros(E, FEAT_LD, dtype=ad, device=d),
-                    h=torch.zeros(E, 2 * HIDDEN, dtype=ad, device=d))
+        d, ad, od = self.device, self.act_dtype, self.op_dtype
+        sp = self.split
+        bufs = dict(stacks=[], feat=torch.zeros(E, FEAT_LD, dtype=od if sp else ad, device=d),
+                    h=torch.zeros(E, 2 * HIDDEN, dtype=od, device=d),
+                    feat_lo=torch.zeros(E, FEAT_LD, dtype=od, device=d) if sp else None,
+                    h_lo=torch.zeros(E, 2 * HIDDEN, dtype=od, device=d) if sp else None)
         for s, (cin, cout, hw, php) in enumerate(_stack_dims()):
             P = cout // 16
             t = lambda: torch.zeros(E, P, php, php, 16, dtype=ad, device=d)  # noqa: E731
             st = dict(p=t(), ya=t(), ra=t(), yb=t())
             st["o"] = bufs["feat"][:, :FEAT].view(E, P, php, php, 16) if s == 2 else t()
+            if s == 2 and sp:
+                st["o_lo"] = bufs["feat_lo"][:, :FEAT].view(E, P, php, php, 16)
             bufs["stacks"].append(st)
         return bufs
 
@@ -278,9 +347,10 @@ class FusedImpalaLearner(IsNormMixin):
             else:
                 io.conv_pool(x, c0, f["p"], None)
             io.resblock(f["p"], r0a, r0b, f["ra"])
-            io.resblock(f["ra"], r1a, r1b, f["o"], relu_out=(s == 2))
+            io.resblock(f["ra"], r1a, r1b, f["o"], relu_out=(s == 2), **self._lo(out_lo=f.get("o_lo")))
             x = f["o"]
-        self.ops.fc_fwd(bufs["feat"], ps["Vb"]["wfc"], ps["V"]["bfc"], bufs["h"])
+        self.ops.fc_fwd(bufs["feat"], ps["Vb"]["wfc"], ps["V"]["bfc"], bufs["h"],
+                        **self._lo(x_lo=bufs["feat_lo"], w_lo=ps["Vl"] and ps["Vl"]["wfc"], out_lo=bufs["h_lo"]))
         return bufs["h"]
 
     def _head_params(self, V):
@@ -295,13 +365,17 @@ class FusedImpalaLearner(IsNormMixin):
         S = self.S
         self.forward_all()
         isw = S["weights"] if self._isw else None
+        sp = self.split
         ops.head(self.h[:2 * B], self.h[2 * B:], self._head_params(self.P), self._head_params(self.T), S["act"],
                  S["rew"], S["gam"], isw, rt.loss == "huber", rt.huber_delta, 1.0 / (B * self.world),
-                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region, isn=self._isn())
+                 self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region, isn=self._isn(),
+                 **self._lo(lo=sp and (self.h_lo[:2 * B], self.h_lo[2 * B:], self.dH_lo)))
         # priority write-back in the head-wgrad launch (csrc/sumtree.hip head_wgrad_prio_kernel)
         with self._on_side():
-            ops.head_wgrad(self.h, self.dhead, self.G, prio=(self.replay, S["idx"], S["gen"], self.td_abs))
-        ops.fc_wgrad(self.dH, self.feat[:B], self.G["wfc"], self.G["bfc"])
+            ops.head_wgrad(self.h, self.dhead, self.G, prio=(self.replay, S["idx"], S["gen"], self.td_abs),
+                           **self._lo(Hon_lo=self.h_lo))
+        ops.fc_wgrad(self.dH, self.feat[:B], self.G["wfc"], self.G["bfc"],
+                     **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.feat_lo[:B]))
         self._join_side()
 
     def _sample(self) -> None:
@@ -311,9 +385,13 @@ class FusedImpalaLearner(IsNormMixin):
     def _seg2(self) -> None:
         """fc data gradient, then the three stacks backwards."""
         B, io, G = self.B, self.iops, self.G
-        self.ops.fc_dgrad(self.dH, self.feat[:B], self.Pb["wfc"], self.dfeat)
+        sp = self.split
+        self.ops.fc_dgrad(self.dH, self.feat[:B], self.Pb["wfc"], self.dfeat,
+                          **self._lo(dh_lo=self.dH_lo, w_lo=sp and self.Pl["wfc"], dx_lo=self.dfeat_lo))
+        if sp:
+            io.merge(self.dfeat, self.dfeat_lo, self.dfeat32)
         jobs: list = []
-        dO = self.dfeat[:, :FEAT].view(B, 2, 11, 11, 16)
+        dO = self.dfeat32[:, :FEAT].view(B, 2, 11, 11, 16)
         for s in (2, 1, 0):
             f, b = self.fw[s], self.bw[s]
             c0, r0a, r0b, r1a, r1b = self.specs[s]
@@ -344,7 +422,8 @@ class FusedImpalaLearner(IsNormMixin):
         rt, ops = self.rt, self.ops
         nxt = (self.replay, self.B, self.S, self.slots[2 * self.B:]) if self._presample else None
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
-                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm, sample=nxt, wnorm=self._wnorm())
+                      rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm, sample=nxt, wnorm=self._wnorm(),
+                      **self._lo(pb_lo=self.pbf_lo))
         if self._presample:
             self._sample_ver = self.replay.version
 
@@ -425,12 +504,12 @@ class FusedImpalaLearner(IsNormMixin):
 
     def _snapshot(self):
         rp = self.replay
-        return [t.clone() for t in (self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes,
+        return [t.clone() for t in (self.p32, self._pbf_all, self.rms_v, self.rms_m, rp.leaf, rp.nodes,
                                     rp.min_bits, rp.ctr)] + ([rp.shard_stats.clone()] if rp.sharded else [])
 
     def _restore(self, snap) -> None:
         rp = self.replay
-        for dst, src in zip((self.p32, self.pbf, self.rms_v, self.rms_m, rp.leaf, rp.nodes, rp.min_bits,
+        for dst, src in zip((self.p32, self._pbf_all, self.rms_v, self.rms_m, rp.leaf, rp.nodes, rp.min_bits,
                              rp.ctr) + ((rp.shard_stats,) if rp.sharded else ()), snap):
             dst.copy_(src)
 
@@ -440,7 +519,7 @@ class FusedImpalaLearner(IsNormMixin):
 
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)
-        self.tbf.copy_(self.pbf)
+        self._tbf_all.copy_(self._pbf_all)
         self._pack_target()
 
     # ------------------------------------------------------------ metrics
@@ -521,10 +600,10 @@ class FusedImpalaLearner(IsNormMixin):
         if adopt_obs_scale(ck, self.rt):
             self._graphs = None                   # the input scale is a kernel argument: recapture
         self.load_module_state(ck["Q_state"])
-        self.pbf.copy_(self.p32)
+        self._refresh_bf16()
         if "Q_target_state" in ck:
             self.load_module_state(ck["Q_target_state"], self.T)
-            self.tbf.copy_(self.t32)
+            split_into(self.t32, self.tbf, self.tbf_lo)
             self._pack_target()
         else:
             self.sync_target()

@@ -27,6 +27,18 @@ class Workspace:
             self.bufs[k] = t
         return t
 
+    # device-side image work queues in the persistent kernels (csrc/mfma_common.h wq_next):
+    # off by default (static order: each queue item costs a contended device-scope
+    # atomic); the data-parallel learner turns them on, where RCCL's kernels hold CUs
+    # during the conv backward.  APEX_WORK_QUEUE=1 / 0 forces them on / off.
+    work_queue = False
+
+    def wq(self, key, device) -> int:
+        """Counter pair of a work queue, or 0 (null: static order) when queues are off."""
+        env = _os.environ.get("APEX_WORK_QUEUE", "")
+        on = (env == "1") or (env != "0" and self.work_queue)
+        return self.get_zeroed(key, 2, device).data_ptr() if on else 0
+
     def get_zeroed(self, key, numel: int, device, dtype=torch.int32) -> torch.Tensor:
         """A buffer zeroed when first made (work-queue counters: the kernels leave them
         zero again at their end)."""
@@ -269,7 +281,7 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     d.pack_sets = int(pack_sets)
     d.N = N
     d.probe = _lib.ptr(probe)
-    d.wq = ws.get_zeroed(("cf_wq",), 2, ring.device).data_ptr()
+    d.wq = ws.wq(("cf_wq",), ring.device)
     _lib.check(lib.apex_conv12_fused_fwd(d, int(grid), _lib.stream_ptr()), "conv12_fused_fwd")
 
 
@@ -439,7 +451,7 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
     ws = ws if ws is not None else _DEFAULT_WS
     d.wfrag = c2d_wfrag_buffer(ws, dy.device).data_ptr()
     d.wfrag_ready = int(packed)
-    d.wq = ws.get_zeroed(("c2d_wq",), 2, dy.device).data_ptr()
+    d.wq = ws.wq(("c2d_wq",), dy.device)
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 

@@ -60,6 +60,27 @@ class PackDesc(ctypes.Structure):
     _fields_ = [("job", PackJob * 32), ("njobs", c_i)]
 
 
+# split (fp32-class) kernels: csrc/impala_split.hip
+class SconvSDesc(ctypes.Structure):
+    _fields_ = [("x", c_p), ("slots", c_p), ("wf", c_p), ("wf_lo", c_p), ("wf2", c_p), ("wf2_lo", c_p),
+                ("bias", c_p), ("bias2", c_p), ("add", c_p), ("mask", c_p), ("y", c_p), ("mask_out", c_p),
+                ("x_img", c_i64), ("y_img", c_i64), ("add_img", c_i64), ("mask_img", c_i64), ("N", c_i),
+                ("n_switch", c_i), ("relu_in", c_i), ("relu_out", c_i), ("scale", c_f), ("pad0", c_i)]
+
+
+class ResSDesc(ctypes.Structure):
+    _fields_ = [("x", c_p), ("wf0", c_p), ("wf0_lo", c_p), ("wf0b", c_p), ("wf0b_lo", c_p), ("b0", c_p),
+                ("b0b", c_p), ("wf1", c_p), ("wf1_lo", c_p), ("wf1b", c_p), ("wf1b_lo", c_p), ("b1", c_p),
+                ("b1b", c_p), ("ysave", c_p), ("out", c_p), ("out_lo", c_p), ("x_img", c_i64),
+                ("ysave_img", c_i64), ("out_img", c_i64), ("N", c_i), ("n_switch", c_i), ("n_save", c_i),
+                ("relu_out", c_i)]
+
+
+class SconvWgSDesc(ctypes.Structure):
+    _fields_ = [("dy", c_p), ("x", c_p), ("slots", c_p), ("slab", c_p), ("dy_img", c_i64), ("x_img", c_i64),
+                ("N", c_i), ("relu_in", c_i), ("imgs_per_group", c_i), ("cin_real", c_i)]
+
+
 _SIGS = {
     "apex_sconv_fwd": ([SconvDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
     "apex_sconv_wgrad": ([SconvWgDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
@@ -70,6 +91,11 @@ _SIGS = {
     "apex_resblock_fwd": ([ResDesc, c_i, c_i, c_i, c_p], c_i),
     "apex_sconv_wgrad_reduce": ([WgRedDesc, c_p], c_i),
     "apex_sconv_frag_elems": ([c_i, c_i], c_i64),
+    "apex_sconv_fwd_split": ([SconvSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_resblock_fwd_split": ([ResSDesc, c_i, c_i, c_p], c_i),
+    "apex_sconv_wgrad_split": ([SconvWgSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_maxpool_bwd_split": ([c_p, c_i64, c_p, c_i, c_i, c_i, c_p, c_i64, c_i, c_p], c_i),
+    "apex_merge_split": ([c_p, c_p, c_p, c_i64, c_p], c_i),
 }
 
 
@@ -118,6 +144,11 @@ class ConvSpec:
     frag: torch.Tensor = None       # forward fragments (online)
     fragT: torch.Tensor = None      # data-gradient fragments (online)
     frag_tgt: torch.Tensor = None   # forward fragments (target)
+    # split mode (fp32-class): fragments of the lo plane of the bf16 weight copy
+    # (v = hi + lo); the lo weight views are extra["wl"] / extra["w_tgt_lo"]
+    frag_lo: torch.Tensor = None
+    fragT_lo: torch.Tensor = None
+    frag_tgt_lo: torch.Tensor = None
     extra: Dict = field(default_factory=dict)
 
 
@@ -180,7 +211,11 @@ class HipImpalaOps:
              bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None,
              _pool_amax=False) -> None:
         """y = epi(corr3x3(x', W')): W' = W (forward) or transposed + flipped (data
-        gradient); x' = relu(x) if relu_in; epi = *scale + bias, * (mask > 0), + add, relu."""
+        gradient); x' = relu(x) if relu_in; epi = *scale + bias, * (mask > 0), + add, relu.
+        fp32 ``y``: the split (fp32-class) kernel, fp32 x / add / mask, hi + lo fragments."""
+        if y.dtype == torch.float32:
+            return self._conv_split(x, spec, y, transpose, relu_in, relu_out, add, mask, bias, second, n_switch,
+                                    scale, ring, slots, _pool_amax)
         d = SconvDesc()
         pool = _pool_amax is not False
         if pool:
@@ -211,11 +246,50 @@ class HipImpalaOps:
         _lib.check(self.lib.apex_sconv_fwd(d, cin, cout, spec.H, spec.W, mode, int(pool), _lib.stream_ptr()),
                    f"sconv_fwd[{spec.name}{'^T' if transpose else ''}{'+pool' if pool else ''}]")
 
+    def _conv_split(self, x, spec, y, transpose, relu_in, relu_out, add, mask, bias, second, n_switch, scale, ring,
+                    slots, _pool_amax) -> None:
+        d = SconvSDesc()
+        pool = _pool_amax is not False
+        if pool:
+            d.mask_out = _lib.ptr(_pool_amax)
+            d.pad0 = getattr(self, "_amax_rows", 0)
+        N = y.shape[0]
+        if ring is not None:
+            d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
+            mode = 3
+            assert slots.shape == (N, 4) and slots.dtype == torch.int32 and spec.cin == 16 and not transpose
+        else:
+            assert x.shape[0] == N and x.dtype == torch.float32
+            d.x, d.x_img = x.data_ptr(), img_stride(x)
+            mode = 0
+        f, fl = (spec.fragT, spec.fragT_lo) if transpose else (spec.frag, spec.frag_lo)
+        assert fl is not None, f"{spec.name}: no lo fragments (split mode packs them)"
+        d.wf, d.wf_lo = f.data_ptr(), fl.data_ptr()
+        if second is not None:
+            d.wf2, d.wf2_lo = spec.frag_tgt.data_ptr(), spec.frag_tgt_lo.data_ptr()
+            d.bias2 = second.data_ptr() if bias else None
+            d.n_switch = int(n_switch)
+        d.bias = spec.b.data_ptr() if (bias and not transpose) else None
+        if transpose:
+            d.bias2 = None
+        for t in (add, mask):
+            assert t is None or t.dtype == torch.float32
+        d.add, d.add_img = _lib.ptr(add), (img_stride(add) if add is not None else 0)
+        d.mask, d.mask_img = _lib.ptr(mask), (img_stride(mask) if mask is not None else 0)
+        d.y, d.y_img = y.data_ptr(), img_stride(y)
+        d.N, d.relu_in, d.relu_out, d.scale = N, int(relu_in), int(relu_out), float(scale)
+        cin, cout = (spec.cout, spec.cin) if transpose else (spec.cin, spec.cout)
+        _lib.check(self.lib.apex_sconv_fwd_split(d, cin, cout, spec.H, spec.W, mode, int(pool), _lib.stream_ptr()),
+                   f"sconv_fwd_split[{spec.name}{'^T' if transpose else ''}{'+pool' if pool else ''}]")
+
     def resblock(self, x, c0: ConvSpec, c1: ConvSpec, out, *, ysave=None, n_save=0, target=False, n_switch=0,
-                 relu_out=False) -> None:
+                 relu_out=False, out_lo=None) -> None:
         """out = x + conv1(relu(conv0(relu(x)))) (+ ReLU) in one kernel; conv0's output
         goes to ``ysave`` for images < ``n_save`` only; images >= ``n_switch`` use the
-        target weights when ``target``."""
+        target weights when ``target``.  fp32 ``x``: the split kernel; with ``out_lo`` the
+        output is written as bf16 hi (``out``) + lo planes (the fc GEMM's split operand)."""
+        if x.dtype == torch.float32:
+            return self._resblock_split(x, c0, c1, out, ysave, n_save, target, n_switch, relu_out, out_lo)
         d = ResDesc()
         d.x, d.x_img = x.data_ptr(), img_stride(x)
         d.wf0, d.b0, d.wf1, d.b1 = c0.frag.data_ptr(), c0.b.data_ptr(), c1.frag.data_ptr(), c1.b.data_ptr()
@@ -229,6 +303,34 @@ class HipImpalaOps:
         d.N, d.relu_out = x.shape[0], int(relu_out)
         R = RESBLOCK_BANDS.get((c0.cin, c0.H), 0)
         _lib.check(self.lib.apex_resblock_fwd(d, c0.cin, c0.H, R, _lib.stream_ptr()), f"resblock_fwd[{c0.name}]")
+
+    def _resblock_split(self, x, c0, c1, out, ysave, n_save, target, n_switch, relu_out, out_lo) -> None:
+        d = ResSDesc()
+        d.x, d.x_img = x.data_ptr(), img_stride(x)
+        assert c0.frag_lo is not None and c1.frag_lo is not None
+        d.wf0, d.wf0_lo, d.b0 = c0.frag.data_ptr(), c0.frag_lo.data_ptr(), c0.b.data_ptr()
+        d.wf1, d.wf1_lo, d.b1 = c1.frag.data_ptr(), c1.frag_lo.data_ptr(), c1.b.data_ptr()
+        if target:
+            d.wf0b, d.wf0b_lo, d.b0b = c0.frag_tgt.data_ptr(), c0.frag_tgt_lo.data_ptr(), c0.extra["b_tgt"].data_ptr()
+            d.wf1b, d.wf1b_lo, d.b1b = c1.frag_tgt.data_ptr(), c1.frag_tgt_lo.data_ptr(), c1.extra["b_tgt"].data_ptr()
+            d.n_switch = int(n_switch)
+        if ysave is not None:
+            assert ysave.dtype == torch.float32
+            d.ysave, d.ysave_img, d.n_save = ysave.data_ptr(), img_stride(ysave), int(n_save)
+        if out_lo is not None:
+            assert out.dtype == torch.bfloat16 and out_lo.dtype == torch.bfloat16 and out.stride() == out_lo.stride()
+        else:
+            assert out.dtype == torch.float32
+        d.out, d.out_lo, d.out_img = out.data_ptr(), _lib.ptr(out_lo), img_stride(out)
+        d.N, d.relu_out = x.shape[0], int(relu_out)
+        _lib.check(self.lib.apex_resblock_fwd_split(d, c0.cin, c0.H, _lib.stream_ptr()),
+                   f"resblock_fwd_split[{c0.name}]")
+
+    def merge(self, hi, lo, out) -> None:
+        """out (fp32) = hi + lo (bf16 planes of the same shape)."""
+        assert hi.is_contiguous() and lo.is_contiguous() and out.is_contiguous() and hi.numel() == out.numel()
+        _lib.check(self.lib.apex_merge_split(hi.data_ptr(), lo.data_ptr(), out.data_ptr(), out.numel(),
+                                             _lib.stream_ptr()), "merge_split")
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
               groups: int = 0, scale: float = 1.0) -> None:
@@ -248,7 +350,8 @@ class HipImpalaOps:
         G = (N + ipg - 1) // ipg
         nsplit = bands * G
         slab = self._buf(("slab", spec.name), nsplit * n, dy.device)
-        d = SconvWgDesc()
+        split = dy.dtype == torch.float32
+        d = SconvWgSDesc() if split else SconvWgDesc()
         d.dy, d.dy_img = dy.data_ptr(), img_stride(dy)
         if ring is not None:
             d.x, d.slots, d.x_img = ring.data_ptr(), slots.data_ptr(), 0
@@ -256,8 +359,13 @@ class HipImpalaOps:
             d.x, d.x_img = x.data_ptr(), img_stride(x)
         d.slab = slab.data_ptr()
         d.N, d.relu_in, d.imgs_per_group, d.cin_real = N, int(relu_in), ipg, spec.cin_real
-        _lib.check(self.lib.apex_sconv_wgrad(d, spec.cin, spec.cout, spec.H, spec.W, mode, G, _lib.stream_ptr()),
-                   f"sconv_wgrad[{spec.name}]")
+        if split:
+            assert x is None or x.dtype == torch.float32
+            _lib.check(self.lib.apex_sconv_wgrad_split(d, spec.cin, spec.cout, spec.H, spec.W, mode, G,
+                                                       _lib.stream_ptr()), f"sconv_wgrad_split[{spec.name}]")
+        else:
+            _lib.check(self.lib.apex_sconv_wgrad(d, spec.cin, spec.cout, spec.H, spec.W, mode, G, _lib.stream_ptr()),
+                       f"sconv_wgrad[{spec.name}]")
         jobs.append(dict(slab=slab, out=gw, bout=gb, nsplit=nsplit, NT=NT, P=P, cin_real=spec.cin_real,
                          scale=float(scale), cols=(NT * 9 * P + NT) * 64))
 
@@ -283,6 +391,12 @@ class HipImpalaOps:
 
     def maxpool_bwd(self, dy, amax, dx) -> None:
         N, P, H, W, _ = dx.shape
+        if dx.dtype == torch.float32:
+            assert dy.dtype == torch.float32
+            _lib.check(self.lib.apex_maxpool_bwd_split(dy.data_ptr(), img_stride(dy), amax.data_ptr(), P, H, W,
+                                                       dx.data_ptr(), img_stride(dx), N, _lib.stream_ptr()),
+                       "maxpool_bwd_split")
+            return
         _lib.check(self.lib.apex_maxpool_bwd(dy.data_ptr(), img_stride(dy), amax.data_ptr(), P, H, W, dx.data_ptr(),
                                              img_stride(dx), N, _lib.stream_ptr()), "maxpool_bwd")
 
@@ -319,54 +433,66 @@ class TorchImpalaOps:
         self.maxpool(c0, y, amax)
 
     def resblock(self, x, c0: ConvSpec, c1: ConvSpec, out, *, ysave=None, n_save=0, target=False, n_switch=0,
-                 relu_out=False) -> None:
-        y = torch.zeros(x.shape[0], c0.cout // 16, c0.H, c0.W, 16, dtype=out.dtype, device=out.device)
+                 relu_out=False, out_lo=None) -> None:
+        dt = x.dtype if out_lo is not None else out.dtype
+        y = torch.zeros(x.shape[0], c0.cout // 16, c0.H, c0.W, 16, dtype=dt, device=out.device)
         t0 = dict(second=c0.extra["b_tgt"], n_switch=n_switch) if target else {}
         t1 = dict(second=c1.extra["b_tgt"], n_switch=n_switch) if target else {}
         self.conv(x, c0, y, relu_in=True, **t0)
-        self.conv(y, c1, out, relu_in=True, add=x, relu_out=relu_out, **t1)
+        if out_lo is None:
+            self.conv(y, c1, out, relu_in=True, add=x, relu_out=relu_out, **t1)
+        else:    # bf16 hi / lo planes of the block output
+            o = torch.zeros_like(y)
+            self.conv(y, c1, o, relu_in=True, add=x, relu_out=relu_out, **t1)
+            out.copy_(o.to(out.dtype))
+            out_lo.copy_((o - out.to(o.dtype)).to(out_lo.dtype))
         if ysave is not None:
             ysave[:n_save].copy_(y[:n_save])
+
+    def merge(self, hi, lo, out) -> None:
+        out.copy_(hi.to(out.dtype) + lo.to(out.dtype))
 
     def conv(self, x, spec: ConvSpec, y, *, transpose=False, relu_in=False, relu_out=False, add=None, mask=None,
              bias=True, second=None, n_switch=0, scale=1.0, ring=None, slots=None) -> None:
         N = y.shape[0]
+        cdt = torch.float64 if y.dtype == torch.float64 else torch.float32
         if ring is not None:
-            xin = F.pad(ring_frames(ring, slots).float(), (0, 0, 0, 0, 0, 12))
+            xin = F.pad(ring_frames(ring, slots).to(cdt), (0, 0, 0, 0, 0, 12))
         else:
-            xin = from_planar(x.float())
+            xin = from_planar(x.to(cdt))
         if relu_in:
             xin = xin.clamp_min(0)
         outs = []
         for lo, hi, sec in ((0, n_switch if second is not None else N, False), (n_switch, N, True)):
             if hi <= lo or (sec and second is None):
                 continue
-            w = self._w(spec, transpose, sec)
+            w = self._w(spec, transpose, sec).to(cdt)
             b = None
             if bias and not transpose:
-                b = (second if sec else spec.b).float()
+                b = (second if sec else spec.b).to(cdt)
             o = F.conv2d(xin[lo:hi], w, None, padding=1) * scale
             if b is not None:
                 o = o + b[None, :, None, None]
             outs.append(o)
         o = to_planar(torch.cat(outs))
         if mask is not None:
-            o = o * (mask.float() > 0)
+            o = o * (mask.to(cdt) > 0)
         if add is not None:
-            o = o + add.float()
+            o = o + add.to(cdt)
         if relu_out:
             o = o.clamp_min(0)
         y.copy_(o.to(y.dtype))
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
               groups: int = 0, scale: float = 1.0) -> None:
+        cdt = torch.float64 if gw.dtype == torch.float64 else torch.float32
         if ring is not None:
-            xin = ring_frames(ring, slots).float()
+            xin = ring_frames(ring, slots).to(cdt)
         else:
-            xin = from_planar(x.float())[:, :spec.cin_real]
+            xin = from_planar(x.to(cdt))[:, :spec.cin_real]
         if relu_in:
             xin = xin.clamp_min(0)
-        g = from_planar(dy.float())
+        g = from_planar(dy.to(cdt))
         gw.copy_(torch.nn.grad.conv2d_weight(xin, gw.shape, g, padding=1) * scale)
         gb.copy_(g.sum((0, 2, 3)))
 
@@ -374,7 +500,7 @@ class TorchImpalaOps:
         pass
 
     def maxpool(self, x, y, amax) -> None:
-        xn = from_planar(x.float())
+        xn = from_planar(x if x.dtype == torch.float64 else x.float())
         o, idx = F.max_pool2d(xn, 3, 2, 1, return_indices=True)
         y.copy_(to_planar(o).to(y.dtype))
         if amax is not None:
@@ -388,7 +514,8 @@ class TorchImpalaOps:
 
     def maxpool_bwd(self, dy, amax, dx) -> None:
         N, P, H, W, _ = dx.shape
-        g = from_planar(dy.float())
+        cdt = torch.float64 if dx.dtype == torch.float64 else torch.float32
+        g = from_planar(dy.to(cdt))
         code = from_planar(amax.long())
         Ho, Wo = g.shape[2:]
         oh = torch.arange(Ho, device=dy.device)[:, None]
@@ -396,6 +523,6 @@ class TorchImpalaOps:
         ih = 2 * oh - 1 + code // 3
         iw = 2 * ow - 1 + code % 3
         flat = (ih * W + iw).reshape(N, P * 16, -1)
-        out = torch.zeros(N, P * 16, H * W, dtype=torch.float32, device=dy.device)
+        out = torch.zeros(N, P * 16, H * W, dtype=cdt, device=dy.device)
         out.scatter_add_(2, flat, g.reshape(N, P * 16, -1))
         dx.copy_(to_planar(out.reshape(N, P * 16, H, W)).to(dx.dtype))

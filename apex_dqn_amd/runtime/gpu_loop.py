@@ -100,14 +100,13 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     replay = build_replay(cfg, device, E, seed=rt.seed + rank, world=world)
     if cfg.network in ("nature64", "nature32"):
         learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=backend)
-    elif cfg.network == "impala" and cfg.Runtime.use_hip_kernels and \
-            (cfg.Runtime.dtype == "bf16" or device.type != "cuda"):
-        # csrc/impala.hip learner: bf16 operands (fp32 accumulation / master weights)
+    elif cfg.network == "impala" and cfg.Runtime.use_hip_kernels:
+        # hand-written IMPALA learner: csrc/impala_split.hip (Runtime.dtype fp32: split
+        # hi / lo operands) or csrc/impala.hip (bf16 operands), fp32 accumulation / master weights
         from ..learner.impala_learner import FusedImpalaLearner
         learner = FusedImpalaLearner(cfg, device, replay, comm=comm, backend=backend)
     else:
-        # graph-captured torch-autograd learner on the same HBM replay (IMPALA at
-        # Runtime.dtype=fp32: the hand-written IMPALA kernels have no split-operand path)
+        # graph-captured torch-autograd learner on the same HBM replay (use_hip_kernels off)
         from ..learner.graph_learner import GraphLearner
         learner = GraphLearner(cfg, device, replay, comm=comm)
     ckpt_path = os.path.join(rt.ckpt_dir, "checkpoint.pt") if rt.ckpt_dir else None

@@ -86,9 +86,7 @@ def make_learner(args, dtype, device, comm, rank, replay):
                     "presample": not args.no_presample, "force_dp": args.force_dp, "comm_backend": args.comm,
                     **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
     })
-    if args.learner == "graph" or (args.network == "impala" and (args.graph_impala or dtype == "fp32")):
-        # (the hand-written IMPALA kernels are bf16-operand only: fp32 IMPALA runs the
-        # torch-autograd learner)
+    if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
         from apex_dqn_amd.learner.graph_learner import GraphLearner
         return cfg, GraphLearner(cfg, device, replay, comm=comm)
     if args.network in ("nature64", "nature32"):

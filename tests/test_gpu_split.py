@@ -462,3 +462,43 @@ def test_conv12_fused_split_vs_fp64_and_separate_kernels(N, switch, copy_n, C, g
     assert _rel(_join(y2h, y2l), _join(s2h, s2l)) < TOL
     if copy_n:
         assert _rel(_join(y1h, y1l)[:copy_n], _join(s1h, s1l)[:copy_n]) < 1e-5
+
+
+@pytest.mark.parametrize("N,grid", [(1536, 0), (37, 5)])
+def test_work_queue_outputs_bit_identical_to_static_order(N, grid):
+    """The persistent kernels' image work queue (csrc/mfma_common.h wq_next, enabled by the
+    data-parallel learner) computes every image whole in one workgroup: the fused conv1 ->
+    conv2 forward and the split conv2 data gradient give bit-identical outputs with the
+    queue on or off, and three queued launches in a row (the counters reset by the last
+    workgroup of each launch) agree too."""
+    from apex_dqn_amd.ops import conv as C_
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    g = torch.Generator(device="cpu").manual_seed(N + 11)
+    raw = torch.randint(0, 256, (80, 84, 84), generator=g, dtype=torch.uint8)
+    ring = to_s2d(raw.to(DEV))
+    slots = torch.randint(0, 80, (N, 4), generator=g, dtype=torch.int32).to(DEV)
+    w1 = (torch.randn(64, 4, 8, 8, generator=g) * 0.05).to(DEV)
+    b1, b2 = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    w2h, w2l = _split(torch.randn(64, 4, 4, 64, generator=g) * 0.03)
+    copy_n = N // 3
+    dy = torch.randn(N, 9, 9, 64, generator=g)
+    dh, dl = _split(dy)
+    mask = torch.randn(N, 20, 20, 64, generator=g).to(DEV, torch.bfloat16)
+    outs = []
+    for wq, reps in ((False, 1), (True, 3)):
+        ws = C_.Workspace()
+        ws.work_queue = wq
+        for _ in range(reps):
+            y2h, y2l = _empty2(N, 9, 9, 64)
+            y1h, y1l = _empty2(copy_n, 20, 20, 64)
+            C_.conv12_fused_fwd(_lib(), ws, ring, slots, w1, b1, w2h, w2l, b2, 1 / 255.0, y2h, y2l, y1=y1h,
+                                y1_lo=y1l, copy_n=copy_n, grid=grid)
+            dxh, dxl = _empty2(N, 20, 20, 64)
+            C_.conv2_dgrad_img(_lib(), dh, w2h, mask, dxh, grid=grid, dy_lo=dl, w_lo=w2l, out_lo=dxl, ws=ws)
+            torch.cuda.synchronize()
+            outs.append((y2h, y2l, y1h, y1l, dxh, dxl))
+        if wq:
+            assert int(ws.get_zeroed(("cf_wq",), 2, DEV).abs().sum()) == 0    # counters left at zero
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)

@@ -12,12 +12,12 @@ from apex_dqn_amd.ops.impala import ConvSpec, TorchImpalaOps, from_planar, to_pl
 from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
 
 
-def _setup(B=4, A=6, device="cpu", loss="huber"):
+def _setup(B=4, A=6, device="cpu", loss="huber", dtype="fp32"):
     torch.manual_seed(0)
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": A, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": B},
                                 "Runtime": {"grad_clip": 40.0, "loss": loss, "network": "impala",
-                                            "use_graphs": False}})
+                                            "use_graphs": False, "dtype": dtype}})
     rp = GpuReplayShard(256, 256, 400, 4, device=device)
     rng = np.random.default_rng(0)
     seqs = rp.append_frames(rng.integers(0, 255, (200, 84, 84), dtype=np.uint8))
@@ -309,9 +309,9 @@ def test_gpu_impala_learner_matches_torch_backend():
     """Whole hand-written step (HIP) vs the same step on the torch ops (both bf16
     activations on the GPU): loss, priorities and gradients."""
     dev = torch.device("cuda")
-    cfg, rp = _setup(B=64, device=dev)
+    cfg, rp = _setup(B=64, device=dev, dtype="bf16")
     Lh = FusedImpalaLearner(cfg, dev, rp, backend="hip")
-    cfg2, rp2 = _setup(B=64, device=dev)
+    cfg2, rp2 = _setup(B=64, device=dev, dtype="bf16")
     Lt = FusedImpalaLearner(cfg2, dev, rp2, backend="torch")
     Lt.p32.copy_(Lh.p32)
     Lt.pbf.copy_(Lh.pbf)
@@ -336,9 +336,10 @@ def test_gpu_impala_learner_matches_torch_backend():
 
 
 @pytest.mark.gpu
-def test_gpu_impala_graph_step_runs():
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_gpu_impala_graph_step_runs(dtype):
     dev = torch.device("cuda")
-    cfg, rp = _setup(B=64, device=dev)
+    cfg, rp = _setup(B=64, device=dev, dtype=dtype)
     cfg.Runtime.use_graphs = True
     L = FusedImpalaLearner(cfg, dev, rp, backend="hip")
     for _ in range(3):
