@@ -67,7 +67,7 @@ class RuntimeConf:
     seed: int = 0
     learner_T: int = 500000         # reference hard-codes 500000 (main.py:46)
     network: str = "auto"           # "auto" | "nature64" | "nature32" | "mlp" | "impala"
-    env_backend: str = "auto"       # "auto" | "synthetic" | "cartpole" | "ale" | "fake_ale"
+    env_backend: str = "auto"       # "auto" | "synthetic" | "cartpole" | "ale" | "fake_ale" | "fake_ale_target"
     frame_stack: Optional[int] = None  # defaults to state_shape[0]
     actors_per_rank: Optional[int] = None  # defaults to num_actors / world_size
     obs_scale: float = 1.0 / 255.0  # uint8 -> float scale fed to conv nets
@@ -102,7 +102,8 @@ class RuntimeConf:
     allreduce_dtype: str = "fp32"   # DP gradient all-reduce payload: "fp32" (exact) | "bf16" (half the bytes)
     presample: bool = True          # draw step t+1's batch at the end of step t (fused learner; on the HIP
                                     # backend inside the optimizer launch)
-    graph_steps: int = 10           # learner updates per HIP-graph launch in learner.steps(n) (1 rank;
+    graph_steps: int = 10           # learner updates per HIP-graph launch in learner.steps(n) (single
+                                    # rank and DP alike: the DP step's collectives are captured too;
                                     # 10 divides the default eviction cadence: 3505 vs 3472 steps/s at 4)
     actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)
     replay_capacity: Optional[int] = None  # physical capacity, global over the ranks' shards

@@ -76,9 +76,8 @@ struct Conv12Desc {
   int N, C, img_switch, copy_n;
   float in_scale;
   uint64_t* probe;         // phase stamps (diagnostic build, csrc/mfma_common.h PROBE), or null
-  int* wq;                 // work queue {next image, finished workgroups}: zero before the first
-                           // launch; the last workgroup to finish zeroes it again (wq_done);
-                           // null: static strided image order (mfma_common.h wq_next)
+  unsigned long long* wq;  // image work queue counter (mfma_common.h wq_next), or null: static
+                           // strided image order
 };
 
 // conv1 fragments per (set, cp, nt, K step s, hi / lo) as 64 lanes x 16 B, then the folded
@@ -186,7 +185,8 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
   // order: the S_t rows (y1 also copied out) spread over all workgroups first.
   int wq_seq = 0;                                  // (thread 0: static order, d.wq null)
   if (tid == 0) {
-    const int a = wq_next(d.wq, wq_seq), b = wq_next(d.wq, wq_seq);
+    // (the second fetch only after an item: each workgroup stops at its first value >= N)
+    const int a = wq_next(d.wq, wq_seq, d.N), b = a < d.N ? wq_next(d.wq, wq_seq, d.N) : d.N;
     reinterpret_cast<volatile int*>(&q_img)[0] = a;
     reinterpret_cast<volatile int*>(Y1)[0] = b;     // (y1 is free until the first conv1)
   }
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
     // waited for here, before any DMA is in flight: ~0.5 us of one wave per image (the
     // compiler moves the value into a register of its choosing at once, so a later use
     // does not hide the atomic's latency)
-    if (tid == 0) reinterpret_cast<volatile int*>(&q_img)[0] = more ? wq_next(d.wq, wq_seq) : d.N;
+    if (tid == 0) reinterpret_cast<volatile int*>(&q_img)[0] = more ? wq_next(d.wq, wq_seq, d.N) : d.N;
     PROBE(d.probe, 4, i, 0);
     const uint8_t* S = STG + (i & 1) * STGB;
     // ================= conv1: this wave's pixel tiles T = th + 2 j, j = 0 .. 12 (16 pixels
@@ -549,7 +549,6 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
 #pragma unroll
     for (int q = 0; q < 12; ++q) store_y2(q);   // the last image's y2
   }
-  if (tid == 0) wq_done(d.wq);
 }
 
 static int cf_launch_pack(const Conv12Desc& d, hipStream_t st) {

@@ -434,8 +434,7 @@ struct Conv2DgradImgDesc {
   // in the step (wfrag_ready: the fc forward's epilogue launch does it in spare blocks)
   uint4* wfrag;
   int wfrag_ready;
-  int* wq;         // image work queue {next, finished workgroups} (csrc/mfma_common.h wq_*), zero
-                   // before the first launch and left zero by each launch; null: static order
+  unsigned long long* wq;   // image work queue counter (csrc/mfma_common.h wq_next); null: static order
 };
 
 // Images come from the work queue: thread 0 fetches the next image while this one's
@@ -445,7 +444,7 @@ struct Conv2DgradImgDesc {
 // image is computed whole by one workgroup, so the outputs do not depend on who did it.
 #define C2D_WQ_BEGIN(q_next_, img_)                                      \
   int wq_seq_ = 0;                                                       \
-  if (threadIdx.x == 0) reinterpret_cast<volatile int*>(&(q_next_))[0] = wq_next(d.wq, wq_seq_); \
+  if (threadIdx.x == 0) reinterpret_cast<volatile int*>(&(q_next_))[0] = wq_next(d.wq, wq_seq_, d.N); \
   __syncthreads();                                                       \
   int img_ = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&(q_next_))[0]); \
   int wq_fetched_ = 0;
@@ -504,7 +503,7 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
       }
     }
     __syncthreads();
-    if (tid == 0) wq_fetched_ = wq_next(d.wq, wq_seq_);
+    if (tid == 0) wq_fetched_ = wq_next(d.wq, wq_seq_, d.N);
     f32x16 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -558,7 +557,6 @@ __global__ void __launch_bounds__(512, 1) conv2_dgrad_img_kernel(Conv2DgradImgDe
     }
     img = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_next)[0]);
   }
-  if (tid == 0) wq_done(d.wq);
 }
 
 
@@ -609,7 +607,7 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
       }
     }
     __syncthreads();
-    if (tid == 0) wq_fetched_ = wq_next(d.wq, wq_seq_);
+    if (tid == 0) wq_fetched_ = wq_next(d.wq, wq_seq_, d.N);
     f32x16 acc[2][4];
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh)
@@ -691,7 +689,6 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
     }
     img = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_next)[0]);
   }
-  if (tid == 0) wq_done(d.wq);
 }
 
 APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t st) {

@@ -206,38 +206,30 @@ __device__ __forceinline__ void vmcnt_le(int n) {
 #undef APEX_VMCNT_CASE
 }
 
-// ---- device-side work queue of a persistent kernel: ctr[0] = next item, ctr[1] =
-// finished workgroups.  One thread per workgroup fetches (vector atomics: this is one
-// lane's global_atomic_add with return); each workgroup calls wq_done once after its
-// last fetch (which returned >= the item count), and the last one to finish zeroes both
-// counters for the next launch -- no memset node between launches.  Items are handed
-// out in increasing order, so a workgroup's items increase too.
+// ---- device-side work queue of a persistent kernel.  One thread per workgroup fetches
+// (vector atomics: one lane's global_atomic_add_x2 with return) from a 64-bit counter
+// that is never reset: a launch over n items with G workgroups consumes exactly n + G
+// values -- every workgroup fetches until its first value >= n and then stops -- so
+// value v means item v mod (n + G) in every launch (no end-of-launch atomics, no memset
+// node).  The counter belongs to one (call site, n, G).  Items leave in increasing order.
 // (the address goes through an opaque zero in a VGPR: with a uniform address the
 // compiler's atomic optimizer broadcasts the result with a readfirstlane right after the
-// atomic, i.e. waits for its return there -- microseconds under load; this way the
-// wait lands where the value is first used, after work that hides it)
-__device__ __forceinline__ int wq_fetch(int* ctr) {
+// atomic, i.e. waits for its return there; this way the wait lands where the value is
+// first used, after work that hides it)
+__device__ __forceinline__ int wq_fetch(unsigned long long* ctr, int n_items) {
   int z;
   asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  return atomicAdd(ctr + z, 1);
+  const unsigned long long v = atomicAdd(ctr + z, 1ull);
+  return (int)(v % (unsigned long long)(n_items + (int)gridDim.x));
 }
 // Item source of a persistent kernel: ctr == nullptr gives the static strided order
 // (the k-th item of workgroup b is b + k * gridDim.x; `seq` counts k, no atomics); else
-// the work queue.  The queue costs a device-scope atomic round trip per item (all
-// workgroups on one counter: ~15 us on the fused forward, ~11 us on the conv2 data
-// gradient of the fp32 step), so the learner enables it only where another kernel can
-// hold CUs during the launch (the data-parallel step's RCCL collectives).
-__device__ __forceinline__ int wq_next(int* ctr, int& seq) {
+// the work queue.  A queue item costs a device-scope atomic round trip, so the learner
+// enables the queue only where another kernel can hold CUs during the launch (the conv
+// backward beside the data-parallel step's RCCL collectives).
+__device__ __forceinline__ int wq_next(unsigned long long* ctr, int& seq, int n_items) {
   if (ctr == nullptr) return (int)blockIdx.x + (seq++) * (int)gridDim.x;
-  return wq_fetch(ctr);
-}
-__device__ __forceinline__ void wq_done(int* ctr) {
-  if (ctr == nullptr) return;
-  __threadfence();
-  if (atomicAdd(ctr + 1, 1) == (int)gridDim.x - 1) {
-    atomicExch(ctr, 0);
-    atomicExch(ctr + 1, 0);
-  }
+  return wq_fetch(ctr, n_items);
 }
 
 // Scalar (SMEM) load of the C frame slots of one image: counted by lgkmcnt, so it

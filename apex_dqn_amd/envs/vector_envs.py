@@ -189,10 +189,14 @@ class FakeALE:
     wrapper stack below run (and be tested) without ROMs."""
 
     def __init__(self, seed: int = 0, lives: int = 3, life_frames: int = 60, reward_scale: float = 5.0,
-                 n_actions: int = 6):
+                 n_actions: int = 6, target: bool = False):
         self.rng = np.random.default_rng(seed)
         self.max_lives, self.life_frames, self.reward_scale = lives, life_frames, reward_scale
         self.n_actions = n_actions
+        # target mode (backend "fake_ale_target"): the 7th-frame reward is paid only while
+        # the block is in the right third of the screen -- a policy to learn (move right
+        # and stay), observable only through the frames (learning-parity runs)
+        self.target = bool(target)
         self.frames_total = 0
         self.reset_game()
 
@@ -218,6 +222,8 @@ class FakeALE:
         self.x = int(np.clip(self.x + (int(a) % 3 - 1) * 3, 0, 150))
         if self.t % self.life_frames == 0:
             self._lives -= 1
+        if self.target and self.x < 100:
+            return 0.0
         return self.reward_scale if self.t % 7 == 0 else 0.0
 
     def getScreenRGB(self) -> np.ndarray:  # noqa: N802
@@ -340,8 +346,9 @@ def make_vec_env(backend: str, name: str, num_envs: int, action_dim: int,
     if backend == "synthetic":
         return SyntheticAtariVec(num_envs, action_dim=action_dim, seed=seed,
                                  frame_hw=frame_hw or (84, 84))
-    if backend == "fake_ale":
-        return AtariWrapperVec([FakeALE(seed=seed + i, n_actions=action_dim) for i in range(num_envs)], seed=seed)
+    if backend in ("fake_ale", "fake_ale_target"):
+        return AtariWrapperVec([FakeALE(seed=seed + i, n_actions=action_dim, target=backend == "fake_ale_target")
+                                for i in range(num_envs)], seed=seed)
     if backend == "ale":  # pragma: no cover
         return ALEVec(name, num_envs, seed=seed)
     raise ValueError(f"unknown env backend {backend!r}")

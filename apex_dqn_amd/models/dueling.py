@@ -1,10 +1,11 @@
 """Dueling Q-networks (PyTorch reference implementations).
 
 These modules are the *semantic* definition of every network family and the
-CPU / oracle path.  The MI355X training path (``models/fused_nature.py``)
-runs the same math through hand-written HIP kernels on a flat parameter
-buffer and converts to/from these modules' ``state_dict`` so checkpoints stay
-interchangeable.
+CPU / oracle path.  The MI355X training paths (``learner/fused_learner.py``
+for the NatureCNN, ``learner/impala_learner.py`` for IMPALA-deep) run the same
+math through hand-written HIP kernels on a flat parameter buffer
+(``models/flat_params.py``) and convert to/from these modules' ``state_dict``
+so checkpoints stay interchangeable.
 
 ``DuellingDQN`` keeps the reference key names exactly
 (``duelling_network.py:8-19``: ``layer1.0.weight`` ... ``advantage.bias``)

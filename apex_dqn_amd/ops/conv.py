@@ -33,11 +33,16 @@ class Workspace:
     # during the conv backward.  APEX_WORK_QUEUE=1 / 0 forces them on / off.
     work_queue = False
 
-    def wq(self, key, device) -> int:
-        """Counter pair of a work queue, or 0 (null: static order) when queues are off."""
+    def wq(self, key, device, overlapped: bool = True) -> int:
+        """Counter pair of a work queue, or 0 (null: static order) when queues are off.
+        ``overlapped``: the launch can run beside the step's collectives (the conv
+        backward); the forward never does (it follows the optimizer's join), so it keeps
+        the static order unless APEX_WORK_QUEUE=1."""
         env = _os.environ.get("APEX_WORK_QUEUE", "")
-        on = (env == "1") or (env != "0" and self.work_queue)
-        return self.get_zeroed(key, 2, device).data_ptr() if on else 0
+        on = (env == "1") or (env != "0" and self.work_queue and overlapped)
+        # one never-reset 64-bit counter per (call site, items, grid): a launch consumes
+        # exactly items + grid values (csrc/mfma_common.h wq_fetch)
+        return self.get_zeroed(key, 1, device, dtype=torch.int64).data_ptr() if on else 0
 
     def get_zeroed(self, key, numel: int, device, dtype=torch.int32) -> torch.Tensor:
         """A buffer zeroed when first made (work-queue counters: the kernels leave them
@@ -281,7 +286,7 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     d.pack_sets = int(pack_sets)
     d.N = N
     d.probe = _lib.ptr(probe)
-    d.wq = ws.wq(("cf_wq",), ring.device)
+    d.wq = ws.wq(("cf_wq", N, int(grid)), ring.device, overlapped=False)
     _lib.check(lib.apex_conv12_fused_fwd(d, int(grid), _lib.stream_ptr()), "conv12_fused_fwd")
 
 
@@ -451,7 +456,7 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
     ws = ws if ws is not None else _DEFAULT_WS
     d.wfrag = c2d_wfrag_buffer(ws, dy.device).data_ptr()
     d.wfrag_ready = int(packed)
-    d.wq = ws.wq(("c2d_wq",), dy.device)
+    d.wq = ws.wq(("c2d_wq", N, int(grid)), dy.device)
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 

@@ -240,10 +240,26 @@ def _learner(dtype, backend, B=64):
 
 def test_split_impala_step_matches_fp32_torch_step():
     """Whole split step (HIP, Runtime.dtype fp32) vs the fp32 torch step on the same
-    parameters and batch: |delta| and every gradient tensor at fp32-class error; the
-    bf16-operand HIP step on the same data is the contrast (>= 10x worse)."""
+    parameters and batch.  Every backward data-gradient op of the HIP step, re-run in
+    fp64 on the HIP step's own inputs, is within 2e-5 (measured ~4e-6; torch fp32 ~3e-7).
+    End to end, |delta| and the fc / head gradients match at fp32 class (< 1e-4); the
+    trunk weight gradients differ by up to ~5e-3 because ReLU masks and max-pool winners
+    flip where an activation lies within the two forwards' ~1e-6 difference of a tie (a
+    handful of units per layer, each moving one O(1) term of a sum over ~1e5;
+    scripts/diag_impala_split.py) -- the bf16-operand HIP step on the same data is the
+    contrast (>= 10x worse)."""
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
+    cudnn_was = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False      # oracle convs: torch's native fp32 path
+    try:
+        _step_vs_torch()
+    finally:
+        torch.backends.cudnn.enabled = cudnn_was
+
+
+def _step_vs_torch():
+    tops = TorchImpalaOps()
     Lt = _learner("fp32", "torch")
     errs = {}
     for dt in ("fp32", "bf16"):
@@ -255,6 +271,8 @@ def test_split_impala_step_matches_fp32_torch_step():
         Lh._seg2()
         if dt == "fp32":
             Lt._seg1()
+            for s in range(3):     # the oracle backward routes through the kernels' pool winners
+                Lt.fw[s]["amax"].copy_(Lh.fw[s]["amax"])
             Lt._seg2()
         torch.cuda.synchronize()
         assert torch.equal(Lh.slots, Lt.slots)
@@ -262,10 +280,32 @@ def test_split_impala_step_matches_fp32_torch_step():
         e = {k: float((gh[k] - gt[k]).norm() / (gt[k].norm() + 1e-12)) for k in gh}
         e["td_abs"] = _rel(Lh.td_abs, Lt.td_abs)
         errs[dt] = e
+        if dt == "fp32":
+            # per-op: each data-gradient kernel of the step in fp64 on its own HIP inputs
+            B = Lh.B
+            dO = Lh.dfeat32[:, :3872].view(B, 2, 11, 11, 16)
+            for s in (2, 1, 0):
+                f, b = Lh.fw[s], Lh.bw[s]
+                c0, r0a, r0b, r1a, r1b = Lh.specs[s]
+                for name, cs, dy, mask, add in (("d_yb", r1b, dO, f["yb"][:B], None),
+                                                ("d_ra", r1a, b["d_yb"], f["ra"][:B], dO),
+                                                ("d_ya", r0b, b["d_ra"], f["ya"][:B], None),
+                                                ("d_p", r0a, b["d_ya"], f["p"][:B], b["d_ra"])):
+                    ref = ConvSpec(cs.name, cs.cin, cs.cout, cs.cin_real, cs.H, cs.W, w=cs.w, b=cs.b,
+                                   wb=cs.w.double())
+                    y = torch.zeros(b[name].shape, dtype=torch.float64, device=DEV)
+                    tops.conv(dy.double(), ref, y, transpose=True, mask=mask.double(),
+                              add=None if add is None else add.double())
+                    assert _rel(b[name], y) < 2e-5, (s, name, _rel(b[name], y))
+                if s > 0:
+                    dO = Lh.bw[s - 1]["d_o"]
         Lh._seg3()
         torch.cuda.synchronize()
         assert torch.isfinite(Lh.p32).all()
-    worst32 = max(errs["fp32"].values())
-    print("impala split step vs fp32 torch: worst", worst32, "bf16 worst", max(errs["bf16"].values()))
-    assert worst32 < 2e-3, errs["fp32"]
-    assert worst32 < 0.1 * max(errs["bf16"].values()), errs
+    e32 = errs["fp32"]
+    print({k: f"{v:.2e}" for k, v in e32.items()})
+    print("bf16 worst", max(errs["bf16"].values()))
+    head = {k: v for k, v in e32.items() if not k.startswith("stacks.")}
+    assert max(head.values()) < 1e-4, head
+    assert max(e32.values()) < 1e-2, e32
+    assert max(e32.values()) < 0.1 * max(errs["bf16"].values()), errs
