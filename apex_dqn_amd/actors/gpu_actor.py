@@ -74,7 +74,9 @@ class GpuActorGroup:
         self.ctr = torch.zeros(1, dtype=torch.int64, device=d)
         ad = learner.act_dtype
         # fp32 learner (split operands): the actor runs the split kernels too
-        self.split = bool(getattr(learner, "split", False))
+        # (Runtime.actor_precision = "bf16": the hi planes only -- cheaper inference, bf16-class
+        # q-values and initial priorities)
+        self.split = bool(getattr(learner, "split", False)) and cfg.Runtime.actor_precision != "bf16"
         self.slots = torch.zeros(self.E, self.C, dtype=torch.int32, device=d)
         self.frames_buf = torch.zeros(self.E, self.C, 84, 84, dtype=torch.uint8, device=d) \
             if self.ops.name != "hip" else torch.zeros(1, self.C, 84, 84, dtype=torch.uint8, device=d)

@@ -116,6 +116,9 @@ class RuntimeConf:
     replica_check_every: int = 5000  # DP: learner steps between replica checksum checks (0 = off)
     step_timeout: float = 300.0     # GPU loop watchdog: seconds a queued learner chunk may take
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
+    actor_precision: str = "learner"  # GPU actor inference: "learner" (the learner's precision; fp32-class
+                                      # split kernels with dtype fp32, as the reference's fp32 actors) |
+                                      # "bf16" (hi planes only: faster, bf16-class q-values / priorities)
     learner_stream_priority: bool = True   # async GPU actors: learner on a high-priority HIP stream
                                     # (runtime/actor_thread.py), concurrent with the learner
 
@@ -186,6 +189,8 @@ class ApexConfig:
             raise ValueError("Runtime.world_size must be >= 1")
         if self.Runtime.comm_backend not in ("torch", "native"):
             raise ValueError("Runtime.comm_backend must be 'torch' or 'native'")
+        if self.Runtime.actor_precision not in ("learner", "bf16"):
+            raise ValueError("Runtime.actor_precision must be 'learner' or 'bf16'")
         if self.Runtime.is_normalise not in ("batch_max", "global_min"):
             raise ValueError("Runtime.is_normalise must be 'batch_max' or 'global_min'")
         if self.Runtime.loss not in ("huber", "mse"):

@@ -169,9 +169,12 @@ class TorchBackend:
         if zero is not None:
             zero.zero_()
         if isn is not None:
-            if isn[1] is not None:
-                ws = float(isn[0].reshape(-1)[0]) if isn[0] is not None else 1.0
-                isn[1].reshape(-1)[0] = (w.max().double() / ws) if ws > 0 else 0.0
+            if isn[1] is not None:   # tensor ops only: no host sync (graph-capturable)
+                ws = isn[0].reshape(-1)[0].double() if isn[0] is not None else torch.ones((), dtype=torch.float64,
+                                                                                           device=w.device)
+                m = w.max().double()
+                isn[1].reshape(-1)[0] = torch.where(ws > 0, m / torch.where(ws > 0, ws, torch.ones_like(ws)),
+                                                    torch.zeros_like(m))
             if len(isn) > 2 and isn[2] is not None:
                 isn[2].add_((w > 0).sum())
 

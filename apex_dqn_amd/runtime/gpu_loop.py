@@ -98,7 +98,7 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
     E = num_envs or cfg.Runtime.actors_per_rank or max(1, cfg.Actor.num_actors // world)
     torch.manual_seed(rt.seed)
     replay = build_replay(cfg, device, E, seed=rt.seed + rank, world=world)
-    if cfg.network in ("nature64", "nature32"):
+    if cfg.network in ("nature64", "nature32") and (cfg.Runtime.use_hip_kernels or device.type != "cuda"):
         learner = FusedNatureLearner(cfg, device, replay, comm=comm, backend=backend)
     elif cfg.network == "impala" and cfg.Runtime.use_hip_kernels:
         # hand-written IMPALA learner: csrc/impala_split.hip (Runtime.dtype fp32: split
