@@ -125,11 +125,12 @@ def test_dp_learner_two_ranks_on_one_gpu(tmp_path):
 
 
 @pytest.mark.parametrize("hip,dtype,kind", [(True, "bf16", "impala"), (False, "bf16", "graph"),
-                                            (True, "fp32", "graph")])
+                                            (True, "fp32", "impala"), (False, "fp32", "graph")])
 def test_impala_loop_with_hip_graph(hip, dtype, kind):
     """IMPALA-deep on the GPU loop (actors + HBM replay + graph-captured step): the
-    hand-written csrc/impala.hip learner (bf16 operands), and the torch-autograd graph
-    learner (also what Runtime.dtype=fp32 selects: the IMPALA kernels have no split path)."""
+    hand-written learner -- csrc/impala_split.hip (fp32: split operands, fp32-class actors)
+    or csrc/impala.hip (bf16 operands) -- and the torch-autograd graph learner
+    (use_hip_kernels off)."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.runtime.gpu_loop import train_frames
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
@@ -444,3 +445,46 @@ def test_actor_q_values_precision_vs_fp32_module(dtype):
     else:
         assert rel > 1e-4        # the bf16 actor is measurably coarser (the reason for the split path)
 
+
+
+def test_optimizer_pack_tail_matches_pack_launch():
+    """fp32 learner: the optimizer launch's tail blocks (csrc/cf_pack.h, waiting on the
+    optimizer blocks that store w1 / b1 / w2) leave the fused forward's online operands
+    bit-identical to a separate pack launch of the updated weights, after graph-replayed
+    multi-step chunks; and a learner without the tail (pack in every forward) takes the
+    same updates bit for bit."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.ops import conv as C
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 128},
+                                "Runtime": {"use_graphs": True, "graph_steps": 4}})
+    outs = []
+    for tail in (True, False):
+        torch.manual_seed(0)
+        rp = _filled_replay(seed=5)
+        L = FusedNatureLearner(cfg, DEV, rp)
+        assert L._cf_tail is not None
+        if not tail:
+            L._cf_tail = None
+        L.steps(9)
+        torch.cuda.synchronize()
+        if tail:
+            ws = L.ops.ws
+            got = [ws.get(("cf_w1frag",), C.CF_W1FRAG_BYTES, DEV, torch.uint8).clone(),
+                   ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, DEV, torch.uint8).clone()]
+            ws2 = C.Workspace()
+            c1, c2 = L._conv12_weights()
+            C.conv12_pack(L.ops.lib, ws2, c1[0], c1[1], c2[0], c2[1], c2[2], L.rt.obs_scale, sets=1)
+            torch.cuda.synchronize()
+            ref = [ws2.get(("cf_w1frag",), C.CF_W1FRAG_BYTES, DEV, torch.uint8),
+                   ws2.get(("cf_c2f_wfrag",), 4 * 8192 * 16, DEV, torch.uint8)]
+            frag0 = 2 * 2 * 8 * 2 * 64 * 16               # set 0 (online) conv1 fragments (C = 4)
+            bias0 = 2 * 2 * 2 * 2 * 4 * 2 * 64 * 16       # folded biases after both sets' fragments
+            assert torch.equal(got[0][:frag0], ref[0][:frag0])
+            assert torch.equal(got[0][bias0:bias0 + 4 * 64 * 16], ref[0][bias0:bias0 + 4 * 64 * 16])
+            assert torch.equal(got[1][:2 * 8192 * 16], ref[1][:2 * 8192 * 16])       # set 0 hi, lo planes
+        outs.append((L.p32.clone(), L.rms_v.clone(), rp.leaf.clone()))
+        del L
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
