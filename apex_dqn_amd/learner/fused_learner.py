@@ -200,6 +200,8 @@ class FusedNatureLearner(IsNormMixin):
         changes repack eagerly (_online_changed)."""
         self._cf_tail = None
         ops = self.ops
+        if os.environ.get("APEX_CF_TAIL", "1") == "0":    # A/B switch: pack launch in every forward
+            return
         if not (self.split and self._presample and getattr(self.replay, "use_hip", False)
                 and getattr(ops, "_conv12_native", lambda: False)()):
             return

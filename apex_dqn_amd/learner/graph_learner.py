@@ -212,8 +212,12 @@ class GraphLearner:
 
     # ------------------------------------------------------------- metrics
     def last_metrics(self) -> Dict[str, float]:
+        w = float(self.S["weights"].mean()) if self._isw else 1.0
+        if self._is_bmax:    # the effective weights: the optimizer divides the gradient by wmax
+            wm = float(self.wmax[0])
+            w = w / wm if wm > 0 else w
         return {"loss": float(self.loss_b[0]), "td_abs_mean": float(self.td_abs.mean()),
-                "grad_norm": float(self.gnorm[0])}
+                "grad_norm": float(self.gnorm[0]), "is_weight_mean": w}
 
     def profile_step(self) -> Dict[str, float]:
         if self.device.type != "cuda":
