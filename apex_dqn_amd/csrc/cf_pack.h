@@ -1,7 +1,5 @@
-// Weight-fragment pack of the fused conv1 -> conv2 forward (csrc/conv12_fused.hip), shared
-// by its own pack launch (cf_pack_kernel) and the optimizer launch (csrc/sumtree.hip
-// rmsprop_sample_kernel), whose tail blocks repack the online set from the weights the
-// launch has just written, so the next step's forward finds its operands ready.
+// Weight-fragment pack of the fused conv1 -> conv2 forward (csrc/conv12_fused.hip): the
+// pack launch's block bodies (cf_pack_kernel).
 #pragma once
 #include "mfma_common.h"
 #include "conv2_wfrag.h"
@@ -83,16 +81,3 @@ __device__ __forceinline__ void cf_pack_w1_block(const CfPack& p, int C, int jb,
         make_float4(bb.x - 1024.f * c4[0], bb.y - 1024.f * c4[1], bb.z - 1024.f * c4[2], bb.w - 1024.f * c4[3]);
   }
 }
-
-// The optimizer launch's pack tail (csrc/sumtree.hip): `nblk` blocks after the optimizer's,
-// the first `nc2f` (of the launch's block size) for the C2F part, then 4 conv1 blocks.
-// They wait until the `sig_blocks` optimizer blocks whose first grid-stride chunk holds
-// every element the pack reads (w1, b1, w2: the head of the flat parameter vector) have
-// stored it: sig[0] counts those blocks, sig[1] the finished tail blocks (the last resets
-// both for the next launch).
-struct CfPackTail {
-  CfPack pk;
-  int nblk, nc2f, C;
-  int* sig;
-  int sig_blocks;
-};

@@ -499,23 +499,6 @@ static int cf_launch_pack(const Conv12Desc& d, hipStream_t st) {
   return 0;
 }
 
-// The optimizer launch's pack tail for d's online set (csrc/cf_pack.h CfPackTail; the
-// launcher sizes its blocks): filled into `out` (apex_cf_tail_size bytes) for the host to
-// hand to apex_rmsprop_sample.  `sig`: two ints, zero before the first launch.
-APEX_EXPORT int apex_cf_tail_size() { return (int)sizeof(CfPackTail); }
-APEX_EXPORT int apex_cf_tail_plan(Conv12Desc d, int* sig, void* out) {
-  if (d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr || d.w2_lo == nullptr || d.wfrag == nullptr ||
-      d.w1frag == nullptr || sig == nullptr || out == nullptr || (d.C != 1 && d.C != 2 && d.C != 4))
-    return (int)hipErrorInvalidValue;
-  CfPackTail t{};
-  t.pk = CfPack{C2fPack{{d.w2, d.w2_lo, nullptr, nullptr}, d.wfrag, 0}, 2 * C2F_FRAGS / 256, 1, {d.w1, nullptr},
-                {d.b1, nullptr}, d.in_scale, d.w1frag};
-  t.C = d.C;
-  t.sig = sig;
-  *reinterpret_cast<CfPackTail*>(out) = t;
-  return 0;
-}
-
 // pack only (the learner's target sync): d.pack_sets of d's weights
 APEX_EXPORT int apex_conv12_pack(Conv12Desc d, hipStream_t st) {
   if (d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr || d.w2_lo == nullptr || d.wfrag == nullptr ||

@@ -709,24 +709,34 @@ __global__ void __launch_bounds__(256) merge_split_kernel(const bf16_t* __restri
 
 // ------------------------------------------------------------------ launchers
 // (shapes and row bands of csrc/impala.hip; the pooled stack-2 entry uses R = 22)
+// (row bands R: the first listed per shape is the default; the others are LDS-occupancy
+// variants -- fewer staged rows per workgroup, more workgroups per CU -- chosen by the
+// host, ops/impala.py SPLIT_BANDS)
 #define SCONV_S_SHAPES(X)       \
   X(16, 16, 84, 84, 10, 3, 1)   \
   X(16, 32, 42, 42, 14, 0, 1)   \
+  X(16, 32, 42, 42, 6, 0, 1)    \
   X(32, 32, 21, 21, 22, 0, 1)   \
+  X(32, 32, 21, 21, 8, 0, 1)    \
   X(16, 16, 84, 84, 21, 3, 0)   \
   X(16, 16, 42, 42, 42, 0, 0)   \
+  X(16, 16, 42, 42, 21, 0, 0)   \
+  X(16, 16, 42, 42, 14, 0, 0)   \
   X(16, 32, 42, 42, 42, 0, 0)   \
   X(32, 16, 42, 42, 21, 0, 0)   \
+  X(32, 16, 42, 42, 11, 0, 0)   \
   X(32, 32, 21, 21, 21, 0, 0)   \
+  X(32, 32, 21, 21, 11, 0, 0)   \
+  X(32, 32, 21, 21, 7, 0, 0)    \
   X(32, 32, 11, 11, 11, 0, 0)
 
-APEX_EXPORT int apex_sconv_fwd_split(SconvSDesc d, int cin, int cout, int H, int W, int mode, int pool,
+APEX_EXPORT int apex_sconv_fwd_split(SconvSDesc d, int cin, int cout, int H, int W, int mode, int pool, int R,
                                      hipStream_t st) {
   if (d.N <= 0) return 0;
   if (d.wf == nullptr || d.wf_lo == nullptr || (d.wf2 != nullptr && d.wf2_lo == nullptr)) return (int)hipErrorInvalidValue;
   if (pool && (d.add || d.mask || d.relu_out)) return (int)hipErrorInvalidValue;
 #define SCONV_S_FWD_CASE(CI, CO, HH, WW, RR, MM, PP)                                                     \
-  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM && pool == PP) {                       \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM && pool == PP && (R == 0 || R == RR)) { \
     const int bands = PP ? ((HH + 1) / 2 + RR / 2 - 1) / (RR / 2) : (HH + RR - 1) / RR;                  \
     sconv_fwd_split_kernel<CI, CO, HH, WW, RR, MM, PP><<<dim3(bands, d.N), 512, 0, st>>>(d);             \
     APEX_CHECK_LAUNCH();                                                                                 \
@@ -738,15 +748,20 @@ APEX_EXPORT int apex_sconv_fwd_split(SconvSDesc d, int cin, int cout, int H, int
 
 #define RESBLOCK_S_SHAPES(X) \
   X(16, 42, 14)              \
+  X(16, 42, 10)              \
+  X(16, 42, 7)               \
   X(32, 21, 21)              \
-  X(32, 11, 11)
+  X(32, 21, 11)              \
+  X(32, 21, 7)               \
+  X(32, 11, 11)              \
+  X(32, 11, 6)
 
-APEX_EXPORT int apex_resblock_fwd_split(ResSDesc d, int C, int HW, hipStream_t st) {
+APEX_EXPORT int apex_resblock_fwd_split(ResSDesc d, int C, int HW, int R, hipStream_t st) {
   if (d.N <= 0) return 0;
   if (d.wf0_lo == nullptr || d.wf1_lo == nullptr || (d.wf0b != nullptr && (d.wf0b_lo == nullptr || d.wf1b_lo == nullptr)))
     return (int)hipErrorInvalidValue;
 #define RESBLOCK_S_CASE(CC, HH, RR)                                                           \
-  if (C == CC && HW == HH) {                                                                  \
+  if (C == CC && HW == HH && (R == 0 || R == RR)) {                                          \
     resblock_fwd_split_kernel<CC, HH, RR><<<dim3((HH + RR - 1) / RR, d.N), 512, 0, st>>>(d);  \
     APEX_CHECK_LAUNCH();                                                                      \
   }

@@ -57,11 +57,8 @@ struct RmspropArgs {
   int wn, wstride;
 };
 
-// one block `bid` of `nblk` (grid-stride over float4 chunks).  Blocks bid < sig_blocks
-// signal `sig` once their first chunk is stored (device-scope release): the optimizer
-// launch's pack tail (csrc/cf_pack.h) reads the head of the parameter vector after it.
-__device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int nblk, int* sig = nullptr,
-                                             int sig_blocks = 0) {
+// one block `bid` of `nblk` (grid-stride over float4 chunks)
+__device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int nblk) {
   float* __restrict__ p = A_.p;
   const float* __restrict__ g = A_.g;
   float* __restrict__ v = A_.v;
@@ -127,12 +124,6 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
       pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
     }
     gg = gn; pp = pn; vv = vn; mm = mn;
-    if (sig != nullptr && bid < sig_blocks) {       // (block-uniform; first chunk only)
-      __threadfence();
-      __syncthreads();
-      if (threadIdx.x == 0) atomicAdd(sig, 1);
-      sig = nullptr;
-    }
   }
   for (int64_t i = n4 * 4 + (int64_t)bid * blockDim.x + threadIdx.x; i < n; i += (int64_t)nblk * blockDim.x) {
     float gg = g[i] * coef;

@@ -17,7 +17,6 @@
 #include "head_common.h"
 #include "igemm_wgrad.h"
 #include "rmsprop_common.h"
-#include "cf_pack.h"
 
 // Bounds-checking debug build (SURVEY §5.2 "race / bounds detection"): built as a
 // separate library with -DAPEX_DEBUG_BOUNDS and selected by APEX_DEBUG_BOUNDS=1.
@@ -560,40 +559,12 @@ __global__ void __launch_bounds__(256) fc_wgrad_head_prio_kernel(WgradDesc d, in
 // already holds this step's priorities (written by fc_wgrad_head_prio_kernel), so the
 // draw equals the one a sample launch at the head of the next step would make.
 template <int NT>
-__global__ void __launch_bounds__(NT) rmsprop_sample_kernel(RmspropArgs a, SampleArgs s, int nsb, CfPackTail tl) {
+__global__ void __launch_bounds__(NT) rmsprop_sample_kernel(RmspropArgs a, SampleArgs s, int nsb) {
   if ((int)blockIdx.x < nsb) {
     tree_sample_body(s, blockIdx.x);
     return;
   }
-  const int nb = (int)gridDim.x - nsb - tl.nblk;
-  const int b = (int)blockIdx.x - nsb;
-  if (b < nb) {
-    rmsprop_body(a, b, nb, tl.sig, tl.sig_blocks);
-    return;
-  }
-  // ---- pack tail (csrc/cf_pack.h): wait for the optimizer blocks that store w1, b1, w2
-  // (dispatched before this block: lower ids), then repack the fused forward's online
-  // operands.  The wait is bounded -- a lost signal leaves stale fragments, never a hang.
-  const int j = b - nb;
-  if (threadIdx.x == 0) {
-    int z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));        // vector (not scalar-cache) loads
-    int* sg = tl.sig + z;
-    for (int spin = 0; spin < (1 << 22); ++spin) {
-      if (__hip_atomic_load(sg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= tl.sig_blocks) break;
-      __builtin_amdgcn_s_sleep(4);
-    }
-  }
-  __syncthreads();
-  __threadfence();
-  if (j < tl.nc2f) c2f_pack_range(tl.pk.c2f, j * NT + threadIdx.x, tl.nc2f * NT);
-  else cf_pack_w1_block(tl.pk, tl.C, j - tl.nc2f, threadIdx.x);
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(tl.sig + 1, 1) == tl.nblk - 1) {
-    atomicExch(tl.sig, 0);
-    atomicExch(tl.sig + 1, 0);
-  }
+  rmsprop_body(a, blockIdx.x - nsb, gridDim.x - nsb);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -725,8 +696,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
                                     uint64_t shard_seed, float* out_wscale, bf16_t* pb_lo, const double* wnorm,
-                                    int wn, int wstride, const void* cf_tail, int64_t cf_region,
-                                    hipStream_t st) {
+                                    int wn, int wstride, hipStream_t st) {
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
@@ -753,22 +723,9 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
                       out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed,
                       out_wscale};
-  // optional pack tail: the fused forward's online operands repacked from this launch's
-  // updated weights (`cf_region` = elements at the head of p / pb / pb_lo the pack reads)
-  CfPackTail tl{};
-  if (cf_tail != nullptr) {
-    tl = *reinterpret_cast<const CfPackTail*>(cf_tail);
-    tl.nc2f = (2 * C2F_FRAGS + nt - 1) / nt;
-    tl.nblk = tl.nc2f + 4;
-    tl.sig_blocks = (int)(((cf_region + 3) / 4 + nt - 1) / nt);
-    if (cf_region <= 0 || cf_region > n || tl.sig_blocks > nb || (int64_t)tl.sig_blocks * nt > n / 4 ||
-        tl.sig == nullptr)
-      return (int)hipErrorInvalidValue;
-  }
-  const int grid = nb + nsb + tl.nblk;
-  if (nt == 1024) rmsprop_sample_kernel<1024><<<grid, 1024, 0, st>>>(ra, sa, nsb, tl);
-  else if (nt == 512) rmsprop_sample_kernel<512><<<grid, 512, 0, st>>>(ra, sa, nsb, tl);
-  else rmsprop_sample_kernel<256><<<grid, 256, 0, st>>>(ra, sa, nsb, tl);
+  if (nt == 1024) rmsprop_sample_kernel<1024><<<nb + nsb, 1024, 0, st>>>(ra, sa, nsb);
+  else if (nt == 512) rmsprop_sample_kernel<512><<<nb + nsb, 512, 0, st>>>(ra, sa, nsb);
+  else rmsprop_sample_kernel<256><<<nb + nsb, 256, 0, st>>>(ra, sa, nsb);
   APEX_CHECK_LAUNCH();
 }
 

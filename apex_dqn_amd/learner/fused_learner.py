@@ -107,7 +107,6 @@ class FusedNatureLearner(IsNormMixin):
         self.rms_v = torch.zeros(n, dtype=torch.float32, device=d)
         self.rms_m = torch.zeros(n, dtype=torch.float32, device=d)
         self.t32 = torch.zeros(n, dtype=torch.float32, device=d)
-        self._cf_tail = None     # optimizer-launch pack of the fused forward's online operands
         self.P = self.layout.views(self.p32)
         self.Pb = self.layout.views(self.pbf)
         self.G = self.layout.views(self.g32)
@@ -187,39 +186,9 @@ class FusedNatureLearner(IsNormMixin):
         # the head of t+1.
         self._presample = bool(self.rt.presample)
         self._sample_ver = None
-        self._setup_cf_tail()
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
-
-    def _setup_cf_tail(self) -> None:
-        """Split mode on the fused conv1 -> conv2 forward with pre-sampling: the optimizer
-        launch (csrc/sumtree.hip rmsprop_sample_kernel) repacks the forward's online weight
-        fragments in tail blocks that wait for the blocks storing w1 / b1 / w2, so no step
-        runs a pack launch of its own (pack_sets 0 in forward_all).  Host-side weight
-        changes repack eagerly (_online_changed)."""
-        self._cf_tail = None
-        ops = self.ops
-        if os.environ.get("APEX_CF_TAIL", "1") == "0":    # A/B switch: pack launch in every forward
-            return
-        if not (self.split and self._presample and getattr(self.replay, "use_hip", False)
-                and getattr(ops, "_conv12_native", lambda: False)()):
-            return
-        from ..ops import conv as C
-        c1, c2 = self._conv12_weights()
-        off, P = self.layout.offsets, self.P
-        region = max(off[k] + P[k].numel() for k in ("w1", "b1", "w2"))
-        self._cf_tail = (C.conv12_pack_tail(ops.lib, ops.ws, c1[0], c1[1], c2[0], c2[1], c2[2], self.rt.obs_scale),
-                         region)
-        self._online_changed()
-
-    def _online_changed(self) -> None:
-        """The online weights changed outside a step (init, load, restore, replica fix):
-        repack the fused forward's online fragments now (the optimizer launch keeps them
-        current from step to step)."""
-        if getattr(self, "_cf_tail", None) is not None:
-            c1, c2 = self._conv12_weights()
-            self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=1)
 
     def _backend_name(self) -> str:
         try:
@@ -290,10 +259,8 @@ class FusedNatureLearner(IsNormMixin):
             # (the target set's weight fragments are repacked at each target change:
             # _target_changed; the step packs the online set only)
             c1, c2 = self._conv12_weights()
-            online = 0 if self._cf_tail is not None else 1      # (packed by the last optimizer launch)
             ops.conv12_fwd(self.replay.frames, self.slots, self.frames, rt.obs_scale, self.y1, self.y1_lo, self.y2,
-                           self.y2_lo, c1, c2, rows_first=2 * B, copy_n=B,
-                           pack_sets=online | (0 if self._tgt_packed else 2))
+                           self.y2_lo, c1, c2, rows_first=2 * B, copy_n=B, pack_sets=1 if self._tgt_packed else 3)
         else:
             c2f = (Pb["w2"], None, Tb["w2"], None)
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
@@ -443,8 +410,7 @@ class FusedNatureLearner(IsNormMixin):
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else None, sample=nxt,
-                      wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo),
-                      **({"cf_tail": self._cf_tail} if (self._cf_tail is not None and self._presample) else {}))
+                      wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo))
         if self._presample:
             self._sample_ver = self.replay.version
         self._mark("optimizer")
@@ -674,12 +640,10 @@ class FusedNatureLearner(IsNormMixin):
             dst.append(rp.shard_stats)
         for t, src in zip(dst, snap):
             t.copy_(src)
-        self._online_changed()
 
     def _refresh_bf16(self) -> None:
         """bf16 compute copy (and its lo plane) from the fp32 master weights."""
         split_into(self.p32, self.pbf, self.pbf_lo)
-        self._online_changed()
 
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)
@@ -722,7 +686,6 @@ class FusedNatureLearner(IsNormMixin):
             return False
         if adopt_obs_scale(ck, self.rt):
             self._graphs = self._multi = None    # the input scale is a kernel argument: recapture
-            self._setup_cf_tail()                # (and folded into the packed conv1 operands)
         self.load_reference_state_dict(ck["Q_state"])
         if "Q_target_state" in ck:
             reference_state_to_flat(ck["Q_target_state"], self.T)

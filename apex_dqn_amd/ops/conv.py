@@ -261,19 +261,6 @@ def conv12_pack(lib, ws: "Workspace", w1, b1, w2, w2_lo, b2, scale: float, w1b=N
     _lib.check(lib.apex_conv12_pack(d, _lib.stream_ptr()), "conv12_pack")
 
 
-def conv12_pack_tail(lib, ws: "Workspace", w1, b1, w2, w2_lo, b2, scale: float):
-    """Plan of the optimizer launch's pack tail (csrc/cf_pack.h CfPackTail) for the online
-    weights (views into the flat parameter buffers the optimizer writes): the launch then
-    leaves the fused forward's online fragments current, and the step's forward packs
-    nothing (``conv12_fused_fwd(pack_sets=0)``).  Returns an opaque ctypes buffer."""
-    import ctypes
-    d = _conv12_desc(ws, None, None, w1, b1, w2, w2_lo, b2, scale, None, None, None, None, None)
-    sig = ws.get_zeroed(("cf_tail_sig",), 2, w1.device)
-    buf = ctypes.create_string_buffer(int(lib.apex_cf_tail_size()))
-    _lib.check(lib.apex_cf_tail_plan(d, ctypes.c_void_p(sig.data_ptr()), buf), "cf_tail_plan")
-    return buf
-
-
 def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,
                      b1: torch.Tensor, w2: torch.Tensor, w2_lo: torch.Tensor, b2: torch.Tensor, scale: float,
                      y2: torch.Tensor, y2_lo: torch.Tensor, y1: Optional[torch.Tensor] = None,

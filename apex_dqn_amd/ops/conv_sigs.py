@@ -47,8 +47,6 @@ def declare(lib: ctypes.CDLL) -> None:
         "apex_conv2_img_fwd": ([Conv2ImgDesc, c_i, c_p], c_i),
         "apex_conv12_fused_fwd": ([Conv12Desc, c_i, c_p], c_i),
         "apex_conv12_pack": ([Conv12Desc, c_p], c_i),
-        "apex_cf_tail_size": ([], c_i),
-        "apex_cf_tail_plan": ([Conv12Desc, c_p, c_p], c_i),
         "apex_conv2_dgrad_img": ([Conv2DgradImgDesc, c_i, c_p], c_i),
         "apex_conv3_dgrad_img": ([Conv3DgradImgDesc, c_i, c_p], c_i),
         "apex_conv_fwd": ([ConvDesc, c_p], c_i),

@@ -261,7 +261,7 @@ class TorchBackend:
 
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None, cf_tail=None):
+                  sample=None, pb_lo=None, wnorm=None):
         """``sample = (replay, B, out, nxt2)``: also draw the next
         batch after the update (the HIP backend fuses it into the optimizer launch).
         ``pb_lo``: split mode, the lo plane of the bf16 copy.  ``wnorm = (stats, n,
@@ -499,10 +499,7 @@ class HipBackend(TorchBackend):
                                             P["wv"].numel(), _lib.ptr(H_lo), _lib.stream_ptr()), "actor_head")
 
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None, cf_tail=None):
-        """``cf_tail = (plan, region)``: the launch also repacks the fused forward's online
-        fragments from the weights it writes (ops/conv.py conv12_pack_tail; the fused
-        rmsprop + sample launch only -- returns False when it could not)."""
+                  sample=None, pb_lo=None, wnorm=None):
         n = p32.numel()
         st = _lib.stream_ptr()
         lo = _lib.ptr(pb_lo)
@@ -520,10 +517,8 @@ class HipBackend(TorchBackend):
             _lib.check(self.lib.apex_rmsprop_sample(
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
-                *rp.sample_launch_args(B, out, nxt2), lo, *wn,
-                None if cf_tail is None else cf_tail[0], 0 if cf_tail is None else int(cf_tail[1]), st),
-                "rmsprop_sample")
-            return True
+                *rp.sample_launch_args(B, out, nxt2), lo, *wn, st), "rmsprop_sample")
+            return
         if sample is not None:
             self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,
                            pb_lo=pb_lo, wnorm=wnorm)

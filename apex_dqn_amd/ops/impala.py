@@ -91,8 +91,8 @@ _SIGS = {
     "apex_resblock_fwd": ([ResDesc, c_i, c_i, c_i, c_p], c_i),
     "apex_sconv_wgrad_reduce": ([WgRedDesc, c_p], c_i),
     "apex_sconv_frag_elems": ([c_i, c_i], c_i64),
-    "apex_sconv_fwd_split": ([SconvSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
-    "apex_resblock_fwd_split": ([ResSDesc, c_i, c_i, c_p], c_i),
+    "apex_sconv_fwd_split": ([SconvSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_resblock_fwd_split": ([ResSDesc, c_i, c_i, c_i, c_p], c_i),
     "apex_sconv_wgrad_split": ([SconvWgSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
     "apex_maxpool_bwd_split": ([c_p, c_i64, c_p, c_i, c_i, c_i, c_p, c_i64, c_i, c_p], c_i),
     "apex_merge_split": ([c_p, c_p, c_p, c_i64, c_p], c_i),
@@ -161,6 +161,31 @@ WGRAD_TUNING = {"target_wgs": int(_os.environ.get("APEX_IMPALA_WG_TARGET", "512"
 
 # fused residual block: rows per workgroup band per (channels, size); 0 = kernel default
 RESBLOCK_BANDS = {(16, 42): int(_os.environ.get("APEX_RESBLOCK_R16", "14"))}   # swept: 21 777, 14 786, 11 778
+
+
+def _split_bands() -> Dict[tuple, int]:
+    """Row bands of the split kernels (csrc/impala_split.hip: 0 = the kernel default):
+    resblock (C, HW) and sconv (cin, cout, HW, pool); APEX_ISPLIT_BANDS="key=R,..." with
+    keys like rb16x42 / sc16x16x42p0 overrides (the sweep of scripts/experiments)."""
+    # defaults from the band sweep (profiles/r3_impala_split_band_sweep.txt: each +0.6 to
+    # +2.4 % on the fp32 IMPALA step; 2 workgroups per CU where the 16-channel shapes fit)
+    out: Dict[tuple, int] = {("rb", 16, 42): 7, ("sc", 16, 16, 42, 0): 21, ("sc", 32, 16, 42, 0): 11,
+                             ("sc", 16, 32, 42, 1): 6}
+    for item in _os.environ.get("APEX_ISPLIT_BANDS", "").split(","):
+        if "=" not in item:
+            continue
+        k, v = item.split("=")
+        if k.startswith("rb"):
+            c, hw = k[2:].split("x")
+            out[("rb", int(c), int(hw))] = int(v)
+        elif k.startswith("sc"):
+            a, p = k[2:].split("p")
+            ci, co, hw = a.split("x")
+            out[("sc", int(ci), int(co), int(hw), int(p))] = int(v)
+    return out
+
+
+SPLIT_BANDS = _split_bands()
 
 
 # ------------------------------------------------------------------ HIP backend
@@ -279,7 +304,8 @@ class HipImpalaOps:
         d.y, d.y_img = y.data_ptr(), img_stride(y)
         d.N, d.relu_in, d.relu_out, d.scale = N, int(relu_in), int(relu_out), float(scale)
         cin, cout = (spec.cout, spec.cin) if transpose else (spec.cin, spec.cout)
-        _lib.check(self.lib.apex_sconv_fwd_split(d, cin, cout, spec.H, spec.W, mode, int(pool), _lib.stream_ptr()),
+        R = SPLIT_BANDS.get(("sc", cin, cout, spec.H, int(pool)), 0)
+        _lib.check(self.lib.apex_sconv_fwd_split(d, cin, cout, spec.H, spec.W, mode, int(pool), R, _lib.stream_ptr()),
                    f"sconv_fwd_split[{spec.name}{'^T' if transpose else ''}{'+pool' if pool else ''}]")
 
     def resblock(self, x, c0: ConvSpec, c1: ConvSpec, out, *, ysave=None, n_save=0, target=False, n_switch=0,
@@ -323,7 +349,8 @@ class HipImpalaOps:
             assert out.dtype == torch.float32
         d.out, d.out_lo, d.out_img = out.data_ptr(), _lib.ptr(out_lo), img_stride(out)
         d.N, d.relu_out = x.shape[0], int(relu_out)
-        _lib.check(self.lib.apex_resblock_fwd_split(d, c0.cin, c0.H, _lib.stream_ptr()),
+        R = SPLIT_BANDS.get(("rb", c0.cin, c0.H), 0)
+        _lib.check(self.lib.apex_resblock_fwd_split(d, c0.cin, c0.H, R, _lib.stream_ptr()),
                    f"resblock_fwd_split[{c0.name}]")
 
     def merge(self, hi, lo, out) -> None:

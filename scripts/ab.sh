@@ -10,7 +10,7 @@ out=gpurun_out/ab_$TAG.log
 for rep in 1 2; do
   for v in "$@"; do
     envs="${v%%::*}"; flags="${v#*::}"; [ "$envs" = "$v" ] && flags=""
-    r=$(env $envs timeout -k 10 200 python bench.py --steps 600 --warmup 50 $flags 2>/dev/null | tail -1) || { echo "FAIL $v" >> $out; exit 1; }
+    r=$(env $envs timeout -k 10 200 python bench.py --steps ${AB_STEPS:-600} --warmup ${AB_WARMUP:-50} $flags 2>/dev/null | tail -1) || { echo "FAIL $v" >> $out; exit 1; }
     echo "$v => $(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> $out
   done
 done

@@ -11,6 +11,6 @@ for dt in fp32 bf16; do
   cd $R && python scripts/prof_summary.py gpurun_out/r3impala_$dt --steps 50 --top 40 > gpurun_out/r3impala_$dt.md 2>&1
 done
 head -12 gpurun_out/r3impala_fp32.md
-bash scripts/ab.sh cftail "APEX_CF_TAIL=1 ::" "APEX_CF_TAIL=0 ::" || exit 1
+
 timeout -k 10 180 python -u bench.py --gpus 1 --steps 200 --warmup 20 --force-dp --no-bf16-extra > gpurun_out/bench_dp_r3e.json 2> gpurun_out/bench_dp_r3e.err || exit 1
 cat gpurun_out/bench_dp_r3e.json

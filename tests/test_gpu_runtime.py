@@ -444,47 +444,3 @@ def test_actor_q_values_precision_vs_fp32_module(dtype):
         assert np.array_equal(a, q.argmax(1))
     else:
         assert rel > 1e-4        # the bf16 actor is measurably coarser (the reason for the split path)
-
-
-
-def test_optimizer_pack_tail_matches_pack_launch():
-    """fp32 learner: the optimizer launch's tail blocks (csrc/cf_pack.h, waiting on the
-    optimizer blocks that store w1 / b1 / w2) leave the fused forward's online operands
-    bit-identical to a separate pack launch of the updated weights, after graph-replayed
-    multi-step chunks; and a learner without the tail (pack in every forward) takes the
-    same updates bit for bit."""
-    from apex_dqn_amd.config import ApexConfig
-    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
-    from apex_dqn_amd.ops import conv as C
-    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
-                                "Learner": {"replay_sample_size": 128},
-                                "Runtime": {"use_graphs": True, "graph_steps": 4}})
-    outs = []
-    for tail in (True, False):
-        torch.manual_seed(0)
-        rp = _filled_replay(seed=5)
-        L = FusedNatureLearner(cfg, DEV, rp)
-        assert L._cf_tail is not None
-        if not tail:
-            L._cf_tail = None
-        L.steps(9)
-        torch.cuda.synchronize()
-        if tail:
-            ws = L.ops.ws
-            got = [ws.get(("cf_w1frag",), C.CF_W1FRAG_BYTES, DEV, torch.uint8).clone(),
-                   ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, DEV, torch.uint8).clone()]
-            ws2 = C.Workspace()
-            c1, c2 = L._conv12_weights()
-            C.conv12_pack(L.ops.lib, ws2, c1[0], c1[1], c2[0], c2[1], c2[2], L.rt.obs_scale, sets=1)
-            torch.cuda.synchronize()
-            ref = [ws2.get(("cf_w1frag",), C.CF_W1FRAG_BYTES, DEV, torch.uint8),
-                   ws2.get(("cf_c2f_wfrag",), 4 * 8192 * 16, DEV, torch.uint8)]
-            frag0 = 2 * 2 * 8 * 2 * 64 * 16               # set 0 (online) conv1 fragments (C = 4)
-            bias0 = 2 * 2 * 2 * 2 * 4 * 2 * 64 * 16       # folded biases after both sets' fragments
-            assert torch.equal(got[0][:frag0], ref[0][:frag0])
-            assert torch.equal(got[0][bias0:bias0 + 4 * 64 * 16], ref[0][bias0:bias0 + 4 * 64 * 16])
-            assert torch.equal(got[1][:2 * 8192 * 16], ref[1][:2 * 8192 * 16])       # set 0 hi, lo planes
-        outs.append((L.p32.clone(), L.rms_v.clone(), rp.leaf.clone()))
-        del L
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)

@@ -309,3 +309,55 @@ def _step_vs_torch():
     assert max(head.values()) < 1e-4, head
     assert max(e32.values()) < 1e-2, e32
     assert max(e32.values()) < 0.1 * max(errs["bf16"].values()), errs
+
+
+@pytest.mark.parametrize("kind,key,R", [("rb", (16, 42), 10), ("rb", (16, 42), 7), ("rb", (32, 21), 11),
+                                        ("rb", (32, 21), 7), ("rb", (32, 11), 6),
+                                        ("sc", (16, 16, 42, 0), 21), ("sc", (16, 16, 42, 0), 14),
+                                        ("sc", (32, 16, 42, 0), 11), ("sc", (32, 32, 21, 0), 11),
+                                        ("sc", (32, 32, 21, 0), 7), ("sc", (16, 32, 42, 1), 6),
+                                        ("sc", (32, 32, 21, 1), 8)])
+def test_split_band_variants_vs_fp64(kind, key, R, monkeypatch):
+    """The row-band variants of the split kernels (ops/impala.py SPLIT_BANDS: fewer staged
+    rows per workgroup, more workgroups per CU) compute the same convolutions."""
+    from apex_dqn_amd.ops import impala as I
+    hops, tops = _hops(), TorchImpalaOps()
+    monkeypatch.setattr(I, "SPLIT_BANDS", {(kind,) + key: R})
+    g = torch.Generator(device=DEV).manual_seed(R)
+    N = 5
+    if kind == "rb":
+        C, H = key
+        x = _t(N, C // 16, H, g)
+        (c0, r0), (c1, r1) = _spec(C, C, H, seed=3), _spec(C, C, H, seed=4)
+        out = torch.zeros(N, C // 16, H, H, 16, device=DEV)
+        ys = torch.zeros_like(out)
+        outr = torch.zeros(out.shape, dtype=torch.float64, device=DEV)
+        ysr = torch.zeros_like(outr)
+        kw = dict(n_save=3, target=True, n_switch=4, relu_out=True)
+        hops.resblock(x, c0, c1, out, ysave=ys, **kw)
+        tops.resblock(x.double(), r0, r1, outr, ysave=ysr, **kw)
+        assert _rel(out, outr) < TOL and _rel(ys[:3], ysr[:3]) < TOL
+        return
+    cin, cout, H, pool = key
+    cs, ref = _spec(cin, cout, H, seed=6)
+    x = _t(N, cin // 16, H, g)
+    if pool:
+        Ho = (H + 1) // 2
+        p = torch.zeros(N, cout // 16, Ho, Ho, 16, device=DEV)
+        a = torch.zeros(N, cout // 16, Ho, Ho, 16, dtype=torch.uint8, device=DEV)
+        hops.conv_pool(x, cs, p, a, second=cs.extra["b_tgt"], n_switch=2)
+        y = torch.zeros(N, cout // 16, H, H, 16, dtype=torch.float64, device=DEV)
+        tops.conv(x.double(), ref, y, second=ref.extra["b_tgt"], n_switch=2)
+        pr, ar = torch.zeros(p.shape, dtype=torch.float64, device=DEV), torch.zeros_like(a)
+        tops.maxpool(y, pr, ar)
+        assert _rel(p, pr) < TOL and (a == ar).float().mean().item() > 0.999
+        return
+    # the data-gradient use: (cin, cout) is the transposed conv's (spec cout, spec cin)
+    cs, ref = _spec(cout, cin, H, seed=6)
+    dy = _t(N, cin // 16, H, g)
+    m2, a2 = _t(N, cout // 16, H, g), _t(N, cout // 16, H, g)
+    dx = torch.zeros(N, cout // 16, H, H, 16, device=DEV)
+    dxr = torch.zeros(dx.shape, dtype=torch.float64, device=DEV)
+    hops.conv(dy, cs, dx, transpose=True, mask=m2, add=a2)
+    tops.conv(dy.double(), ref, dxr, transpose=True, mask=m2.double(), add=a2.double())
+    assert _rel(dx, dxr) < TOL, _rel(dx, dxr)
