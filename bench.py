@@ -186,7 +186,7 @@ def main():
                     help="untimed, state-preserving replays of the multi-step graph right before the timed "
                          "window (learner.rewarm: no update is kept; reported as prep_warm_replays)")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
-                    help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala.hip")
+                    help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala_split.hip (fp32) / csrc/impala.hip (bf16)")
     args = ap.parse_args()
 
     from apex_dqn_amd.parallel.dist import Comm
