@@ -70,8 +70,8 @@ struct Conv12Desc {
   bf16_t* y1_lo;
   bf16_t* y2;              // [N][9][9][64] hi / lo
   bf16_t* y2_lo;
-  uint4* w1frag;           // conv1 f16 hi / lo fragments + folded biases of both sets (CF_W1FRAG_U4
-                           // uint4), written by cf_pack_kernel ahead of the fused launch
+  uint4* w1frag;           // conv1 f16 hi / lo fragments of both sets (CF_W1FRAG_U4 uint4), written
+                           // by cf_pack_kernel or (online set) by the previous optimizer launch
   uint8_t* scratch;        // >= 512 B: target of the y2 stores of padding pixels
   int N, C, img_switch, copy_n;
   float in_scale;
@@ -178,7 +178,22 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
         w1h[nt][s] = __builtin_bit_cast(f16x8, F[((nt * 2 * C + s) * 2) * 64]);
         w1l[nt][s] = __builtin_bit_cast(f16x8, F[((nt * 2 * C + s) * 2 + 1) * 64]);
       }
-      bias1[nt] = __builtin_bit_cast(f32x4, d.w1frag[CF_W1FRAG(4) + ((set * 2 + cp) * 2 + nt) * 64 + lane]);
+      // the bias the hi chain starts from: b - 1024 * sum_k w16[n][k] (pixels enter as
+      // 1024 + x): this lane's 2C x 8 K values of channel 32 cp + 16 nt + pl, summed over
+      // the four K-group lanes (fixed order), then gathered into the accumulator layout
+      // (lane (g, pl) holds channels 4 g .. 4 g + 3 of its pixel)
+      float ws = 0.f;
+#pragma unroll
+      for (int s = 0; s < 2 * C; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ws += (float)w1h[nt][s][j] + (float)w1l[nt][s][j] * (1.f / CF_LO_SCALE);
+      ws += __shfl_xor(ws, 16, 64);
+      ws += __shfl_xor(ws, 32, 64);
+      const float* B1 = set ? d.b1b : d.b1;
+      const float4 bb = *reinterpret_cast<const float4*>(B1 + 32 * cp + 16 * nt + 4 * g);
+      const float s0 = __shfl(ws, 4 * g, 64), s1 = __shfl(ws, 4 * g + 1, 64);
+      const float s2 = __shfl(ws, 4 * g + 2, 64), s3 = __shfl(ws, 4 * g + 3, 64);
+      bias1[nt] = (f32x4){bb.x - 1024.f * s0, bb.y - 1024.f * s1, bb.z - 1024.f * s2, bb.w - 1024.f * s3};
     }
     wf = d.wfrag + set * 2 * C2F_FRAGS + wv * 32 * 64 + lane;
     const float* B2 = set ? d.b2b : d.b2;

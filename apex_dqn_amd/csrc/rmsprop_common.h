@@ -4,6 +4,7 @@
 // next step's prioritized batch in its first blocks).
 #pragma once
 #include "apex_common.h"
+#include "cf_pack.h"
 
 // Batch-max IS-weight normalisation (Runtime.is_normalise = "batch_max"): the head
 // kernel leaves m = max_j (p_j / p_min)^-beta over the batch (DP: one per rank, in the
@@ -55,6 +56,7 @@ struct RmspropArgs {
   bf16_t* pb_lo;     // fp32-accurate mode: lo plane of the bf16 copy (p = pb + pb_lo), else null
   const double* wnorm;  // batch-max IS normalisation (is_grad_scale), or null
   int wn, wstride;
+  CfFragOut fo;         // the fused forward's online operands in fragment order (w1frag null: off)
 };
 
 // one block `bid` of `nblk` (grid-stride over float4 chunks)
@@ -120,6 +122,7 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
       split_pk_bf16_h(px[2], px[3], h23, l23);
       pb4[i] = make_uint2(h01, h23);
       pbl4[i] = make_uint2(l01, l23);
+      if (A_.fo.w1frag != nullptr) cf_frag_store(A_.fo, 4 * i, px, make_uint2(h01, h23), make_uint2(l01, l23));
     } else {
       pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
     }

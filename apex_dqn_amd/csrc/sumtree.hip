@@ -696,7 +696,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
                                     uint64_t shard_seed, float* out_wscale, bf16_t* pb_lo, const double* wnorm,
-                                    int wn, int wstride, hipStream_t st) {
+                                    int wn, int wstride, CfFragOut fo, hipStream_t st) {
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
@@ -718,8 +718,12 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   int nb = (int)((n / 4 + nt - 1) / nt);
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
   const int nsb = blocks_for(B, nt / 64);
+  if (fo.w1frag != nullptr && (pb_lo == nullptr || fo.c2f == nullptr || (fo.C != 1 && fo.C != 2 && fo.C != 4) ||
+                               (fo.w1_off & 3) || (fo.w2_off & 7) || fo.w1_off + 4096LL * fo.C > n ||
+                               fo.w2_off + 65536 > n))
+    return (int)hipErrorInvalidValue;
   const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,
-                      wnorm, wn, wstride};
+                      wnorm, wn, wstride, fo};
   const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
                       out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed,
                       out_wscale};

@@ -107,6 +107,7 @@ class FusedNatureLearner(IsNormMixin):
         self.rms_v = torch.zeros(n, dtype=torch.float32, device=d)
         self.rms_m = torch.zeros(n, dtype=torch.float32, device=d)
         self.t32 = torch.zeros(n, dtype=torch.float32, device=d)
+        self._frag_out = None    # the optimizer stores the fused forward's online operands
         self.P = self.layout.views(self.p32)
         self.Pb = self.layout.views(self.pbf)
         self.G = self.layout.views(self.g32)
@@ -129,9 +130,10 @@ class FusedNatureLearner(IsNormMixin):
         # and the segmented-step overhead on a single GPU)
         self._dp = self.world > 1 or (bool(self.rt.force_dp) and comm is not None)
         # image work queues in the persistent kernels (ops/conv.py Workspace.work_queue):
-        # only where RCCL's kernels may hold CUs during the step
+        # only where RCCL's kernels may hold CUs during the step -- world > 1 (a forced-DP
+        # step on one rank has no peer traffic beside it: static order)
         if hasattr(self.ops, "ws"):
-            self.ops.ws.work_queue = self._dp
+            self.ops.ws.work_queue = self.world > 1
         self._alloc(self.B)
         self._init_is_norm()
         self._graphs = None     # one-update graph
@@ -186,9 +188,35 @@ class FusedNatureLearner(IsNormMixin):
         # the head of t+1.
         self._presample = bool(self.rt.presample)
         self._sample_ver = None
+        self._setup_frag_out()
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
+
+    def _setup_frag_out(self) -> None:
+        """Split mode on the fused conv1 -> conv2 forward with pre-sampling: the optimizer +
+        sample launch stores the updated w1 / w2 in the forward's fragment order
+        (csrc/cf_pack.h cf_frag_store; elementwise, no hand-off between workgroups), so the
+        step runs no pack launch for the online set (forward_all pack_sets).  Host-side
+        weight changes repack eagerly (_online_changed).  APEX_OPT_FRAGS=0: pack launch."""
+        self._frag_out = None
+        ops = self.ops
+        if os.environ.get("APEX_OPT_FRAGS", "1") == "0":
+            return
+        if not (self.split and self._presample and getattr(self.replay, "use_hip", False)
+                and getattr(ops, "_conv12_native", lambda: False)()):
+            return
+        from ..ops import conv as C
+        off = self.layout.offsets
+        self._frag_out = C.conv12_frag_out(ops.ws, self.P["w1"], off["w1"], off["w2"], self.rt.obs_scale)
+        self._online_changed()
+
+    def _online_changed(self) -> None:
+        """Online weights changed outside a step (init, load, restore, replica fix): repack
+        the fused forward's online operands now (the optimizer keeps them current)."""
+        if getattr(self, "_frag_out", None) is not None:
+            c1, c2 = self._conv12_weights()
+            self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=1)
 
     def _backend_name(self) -> str:
         try:
@@ -259,8 +287,10 @@ class FusedNatureLearner(IsNormMixin):
             # (the target set's weight fragments are repacked at each target change:
             # _target_changed; the step packs the online set only)
             c1, c2 = self._conv12_weights()
+            online = 0 if self._frag_out is not None else 1     # (stored by the last optimizer launch)
             ops.conv12_fwd(self.replay.frames, self.slots, self.frames, rt.obs_scale, self.y1, self.y1_lo, self.y2,
-                           self.y2_lo, c1, c2, rows_first=2 * B, copy_n=B, pack_sets=1 if self._tgt_packed else 3)
+                           self.y2_lo, c1, c2, rows_first=2 * B, copy_n=B,
+                           pack_sets=online | (0 if self._tgt_packed else 2))
         else:
             c2f = (Pb["w2"], None, Tb["w2"], None)
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
@@ -410,7 +440,8 @@ class FusedNatureLearner(IsNormMixin):
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else None, sample=nxt,
-                      wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo))
+                      wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo),
+                      **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}))
         if self._presample:
             self._sample_ver = self.replay.version
         self._mark("optimizer")
@@ -640,10 +671,12 @@ class FusedNatureLearner(IsNormMixin):
             dst.append(rp.shard_stats)
         for t, src in zip(dst, snap):
             t.copy_(src)
+        self._online_changed()
 
     def _refresh_bf16(self) -> None:
         """bf16 compute copy (and its lo plane) from the fp32 master weights."""
         split_into(self.p32, self.pbf, self.pbf_lo)
+        self._online_changed()
 
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)
@@ -686,6 +719,7 @@ class FusedNatureLearner(IsNormMixin):
             return False
         if adopt_obs_scale(ck, self.rt):
             self._graphs = self._multi = None    # the input scale is a kernel argument: recapture
+            self._setup_frag_out()               # (and folded into the conv1 operands)
         self.load_reference_state_dict(ck["Q_state"])
         if "Q_target_state" in ck:
             reference_state_to_flat(ck["Q_target_state"], self.T)

@@ -57,6 +57,13 @@ class IsNorm(ctypes.Structure):
     _fields_ = [("wscale", c_p), ("out", c_p), ("valid_count", c_p)]
 
 
+class CfFragOut(ctypes.Structure):
+    """The optimizer's stores of the fused forward's online operands (``CfFragOut``,
+    csrc/cf_pack.h); all-zero = off."""
+    _fields_ = [("w1frag", c_p), ("c2f", c_p), ("w1_off", c_i64), ("w2_off", c_i64), ("C", c_i),
+                ("in_scale", c_f)]
+
+
 class C2dPack(ctypes.Structure):
     """conv2 weight-fragment pack job riding on another launch (``C2dPackJob``, csrc/conv2_wfrag.h)."""
     _fields_ = [("w", c_p), ("w_lo", c_p), ("out", c_p)]
@@ -139,7 +146,7 @@ _SIGS = {
                         c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, IsNorm, c_p], c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p, c_i, c_i, c_u64, c_p, c_p, c_p, c_i, c_i, c_p], c_i),
+                             c_p, c_p, c_i, c_i, c_u64, c_p, c_p, c_p, c_i, c_i, CfFragOut, c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
                               c_p, c_p, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,

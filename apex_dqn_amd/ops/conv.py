@@ -222,7 +222,7 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
 # fp32 learner: conv1 -> conv2 fused with y1 kept in LDS (csrc/conv12_fused.hip);
 # APEX_CONV12_FUSED=0 runs the two image-resident kernels
 CONV12_FUSED = _os.environ.get("APEX_CONV12_FUSED", "1") != "0"
-CF_W1FRAG_BYTES = (2 * 2 * 2 * 2 * 4 * 2 * 64 + 2 * 2 * 2 * 64) * 16
+CF_W1FRAG_BYTES = 2 * 2 * 2 * 2 * 4 * 2 * 64 * 16
 
 
 def _conv12_desc(ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1, b1, w2, w2_lo, b2, scale, w1b, b1b,
@@ -259,6 +259,19 @@ def conv12_pack(lib, ws: "Workspace", w1, b1, w2, w2_lo, b2, scale: float, w1b=N
     d = _conv12_desc(ws, None, None, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b)
     d.pack_sets = int(sets)
     _lib.check(lib.apex_conv12_pack(d, _lib.stream_ptr()), "conv12_pack")
+
+
+def conv12_frag_out(ws: "Workspace", w1: torch.Tensor, w1_off: int, w2_off: int, scale: float):
+    """``CfFragOut`` for the optimizer launch: the fused forward's online conv1 / conv2
+    operand buffers of ``ws`` and the flat offsets of w1 / w2 in the parameter vector the
+    optimizer updates (csrc/cf_pack.h cf_frag_store)."""
+    C = int(w1.shape[1])
+    dev = w1.device
+    fo = _lib.CfFragOut()
+    fo.w1frag = ws.get(("cf_w1frag",), CF_W1FRAG_BYTES, dev, torch.uint8).data_ptr()
+    fo.c2f = ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, dev, torch.uint8).data_ptr()
+    fo.w1_off, fo.w2_off, fo.C, fo.in_scale = int(w1_off), int(w2_off), C, float(scale)
+    return fo
 
 
 def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1: torch.Tensor,

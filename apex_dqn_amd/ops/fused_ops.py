@@ -261,7 +261,7 @@ class TorchBackend:
 
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None):
+                  sample=None, pb_lo=None, wnorm=None, frag_out=None):
         """``sample = (replay, B, out, nxt2)``: also draw the next
         batch after the update (the HIP backend fuses it into the optimizer launch).
         ``pb_lo``: split mode, the lo plane of the bf16 copy.  ``wnorm = (stats, n,
@@ -499,11 +499,16 @@ class HipBackend(TorchBackend):
                                             P["wv"].numel(), _lib.ptr(H_lo), _lib.stream_ptr()), "actor_head")
 
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None):
+                  sample=None, pb_lo=None, wnorm=None, frag_out=None) -> bool:
+        """``frag_out`` (ops/conv.py conv12_frag_out): the launch also stores the updated
+        w1 / w2 in the fused forward's fragment order.  Returns whether it did (the fused
+        optimizer + sample launch only)."""
         n = p32.numel()
         st = _lib.stream_ptr()
         lo = _lib.ptr(pb_lo)
         wn = (wnorm[0].data_ptr(), int(wnorm[1]), int(wnorm[2])) if wnorm is not None else (None, 0, 0)
+        if frag_out is not None and not (sample is not None and sample[0].use_hip):
+            raise ValueError("frag_out needs the fused optimizer + sample launch (a HIP replay)")
         if sample is not None and sample[0].use_hip:
             # the next batch's draw rides in the optimizer launch (csrc/sumtree.hip: rmsprop_sample_kernel)
             rp, B, out, nxt2 = sample
@@ -517,8 +522,9 @@ class HipBackend(TorchBackend):
             _lib.check(self.lib.apex_rmsprop_sample(
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
-                *rp.sample_launch_args(B, out, nxt2), lo, *wn, st), "rmsprop_sample")
-            return
+                *rp.sample_launch_args(B, out, nxt2), lo, *wn, frag_out if frag_out is not None else _lib.CfFragOut(),
+                st), "rmsprop_sample")
+            return frag_out is not None
         if sample is not None:
             self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,
                            pb_lo=pb_lo, wnorm=wnorm)

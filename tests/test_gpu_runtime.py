@@ -402,11 +402,15 @@ def test_fc_epilogue_in_head_matches_separate_launch(dtype):
         L._defer_fc_epilogue = defer
         L.step()                      # the one-update graph (captured + replayed)
         torch.cuda.synchronize()
-        outs.append((L.h[:128].clone(), L.p32.clone(), L.rms_v.clone(), L.td_abs.clone()))
+        outs.append((L.h[:128].clone(), L.g32.clone(), L.rms_v.clone(), L.td_abs.clone(), L.p32.clone()))
         del L
     assert torch.equal(outs[0][0], outs[1][0])     # h: same parameters, same sums and rounding
-    for a, b in zip(outs[0][1:], outs[1][1:]):
+    for a, b in zip(outs[0][1:4], outs[1][1:4]):
         assert torch.allclose(a.double(), b.double(), rtol=1e-5, atol=1e-8), float((a - b).abs().max())
+    # the first centered-RMSprop update is lr * g / (sqrt(a (1 - a)) |g| + eps): an element
+    # whose |g| is near eps moves by up to lr / eps times its gradient's rounding difference
+    a, b = outs[0][4], outs[1][4]
+    assert torch.allclose(a.double(), b.double(), rtol=1e-5, atol=1e-6), float((a - b).abs().max())
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])

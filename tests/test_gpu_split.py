@@ -503,3 +503,51 @@ def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
+
+
+def _presample_learner(monkeypatch, opt_frags: bool):
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    monkeypatch.setenv("APEX_OPT_FRAGS", "1" if opt_frags else "0")
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Learner": {"replay_sample_size": 128},
+                                "Runtime": {"use_graphs": False, "presample": True, "dtype": "fp32"}})
+    torch.manual_seed(0)
+    rp = GpuReplayShard(2000, 2000, 2100, 4, device=DEV, seed=7)
+    rng = np.random.default_rng(11)
+    seqs = rp.append_frames(rng.integers(0, 255, (1800, 84, 84), dtype=np.uint8))
+    K = 1500
+    st = np.stack([seqs[i:i + 4] for i in range(K)])
+    rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 6, K), R=rng.normal(size=K) * 2,
+                   Gamma=np.where(rng.random(K) < 0.1, 0.0, 0.97), priority=rng.random(K)))
+    return FusedNatureLearner(cfg, DEV, rp, backend="hip")
+
+
+def test_optimizer_stores_conv12_fragments_bit_identical_to_pack(monkeypatch):
+    """The optimizer + sample launch stores the updated w1 / w2 in the fused forward's
+    fragment order (csrc/cf_pack.h cf_frag_store): after real steps the online fragments
+    are byte-identical to a fresh pack launch, and the run's weights are bit-identical to
+    the pack-launch variant's (APEX_OPT_FRAGS=0)."""
+    from apex_dqn_amd.ops import conv as C
+    out = {}
+    for opt in (True, False):
+        L = _presample_learner(monkeypatch, opt)
+        assert (L._frag_out is not None) == opt
+        for _ in range(3):
+            L.step()
+        torch.cuda.synchronize()
+        out[opt] = L.p32.clone()
+        if opt:
+            ws, dev = L.ops.ws, L.device
+            w1f = ws.get(("cf_w1frag",), C.CF_W1FRAG_BYTES, dev, torch.uint8)
+            c2f = ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, dev, torch.uint8)
+            half = C.CF_W1FRAG_BYTES // 2          # set 0 (online) of w1; hi + lo planes of set 0 of w2
+            got = (w1f[:half].clone(), c2f[:2 * 8192 * 16].clone())
+            c1, c2 = L._conv12_weights()
+            L.ops.conv12_pack(c1, c2, L.rt.obs_scale, sets=1)
+            torch.cuda.synchronize()
+            assert torch.equal(got[0], w1f[:half]), "conv1 fragments differ from the pack launch"
+            assert torch.equal(got[1], c2f[:2 * 8192 * 16]), "conv2 C2F fragments differ from the pack launch"
+        del L
+    assert torch.equal(out[True], out[False])
