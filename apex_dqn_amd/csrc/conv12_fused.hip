@@ -37,6 +37,11 @@
 //
 // Online / target weights switch at image img_switch; each workgroup takes a contiguous
 // image range, so at most one workgroup reloads its weights.
+//
+// bf16 learner (SPLIT = false, d.bf16): the same pipeline with one operand plane -- conv1
+// runs the f16 hi chain only (w * in_scale rounded to f16: at least bf16's precision), y1
+// is one bf16 plane in LDS (and in HBM for the S_t rows), conv2 issues one product per
+// fragment (x w, the bf16 weights) and y2 is one bf16 plane.
 #include "mfma_common.h"
 #include "conv2_wfrag.h"
 #include "cf_pack.h"
@@ -78,6 +83,7 @@ struct Conv12Desc {
   uint64_t* probe;         // phase stamps (diagnostic build, csrc/mfma_common.h PROBE), or null
   unsigned long long* wq;  // image work queue counter (mfma_common.h wq_next), or null: static
                            // strided image order
+  int bf16;                // 1: one bf16 plane everywhere (w2_lo, y1_lo, y2_lo unused)
 };
 
 template <int C>
@@ -93,8 +99,16 @@ __global__ void __launch_bounds__(256) cf_pack_kernel(CfPack p) {
 __device__ __forceinline__ int cf_pix(int ih, int iw) { return ((ih & 1) * 2 + (iw & 1)) * 100 + (ih >> 1) * 10 + (iw >> 1); }
 __device__ __forceinline__ int cf_off(int P, int c) { return (P << 7) + ((c ^ ((P >> 1) & 7)) << 4); }
 
-template <int C>
-__global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv12Desc d) {
+// y2 stores younger than the last frame DMA piece after conv1 (store of tile q = j - 1 at
+// tile j >= 1, after that tile's piece; the bf16 kernel stores plane 0 only: even q)
+__host__ __device__ constexpr int cf_young_stores(int ndw, bool split) {
+  int n = 0;
+  for (int q = ndw - 1; q < 12; ++q) n += (split || (q & 1) == 0) ? 1 : 0;
+  return n;
+}
+
+template <int C, bool SPLIT>
+__global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc d) {
   // staging buffer: an image's C frames (s2d, 7056 B each), then the conv2 reduction's
   // 24 KB of partials once conv1 has read them
   constexpr int STGB = C * CF_FRAME > 2 * 3 * 4 * 64 * 16 ? C * CF_FRAME : 2 * 3 * 4 * 64 * 16;
@@ -176,7 +190,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
 #pragma unroll
       for (int s = 0; s < 2 * C; ++s) {
         w1h[nt][s] = __builtin_bit_cast(f16x8, F[((nt * 2 * C + s) * 2) * 64]);
-        w1l[nt][s] = __builtin_bit_cast(f16x8, F[((nt * 2 * C + s) * 2 + 1) * 64]);
+        if (SPLIT) w1l[nt][s] = __builtin_bit_cast(f16x8, F[((nt * 2 * C + s) * 2 + 1) * 64]);
       }
       // the bias the hi chain starts from: b - 1024 * sum_k w16[n][k] (pixels enter as
       // 1024 + x): this lane's 2C x 8 K values of channel 32 cp + 16 nt + pl, summed over
@@ -186,7 +200,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
 #pragma unroll
       for (int s = 0; s < 2 * C; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ws += (float)w1h[nt][s][j] + (float)w1l[nt][s][j] * (1.f / CF_LO_SCALE);
+        for (int j = 0; j < 8; ++j) ws += (float)w1h[nt][s][j] + (SPLIT ? (float)w1l[nt][s][j] * (1.f / CF_LO_SCALE) : 0.f);
       ws += __shfl_xor(ws, 16, 64);
       ws += __shfl_xor(ws, 32, 64);
       const float* B1 = set ? d.b1b : d.b1;
@@ -233,6 +247,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
     const int mt = q >> 2, jh = (q >> 1) & 1, plane = q & 1;
     const int jq = 2 * kp + jh;
     // uniform base (image) + 32-bit lane offset: the saddr store form, no 64-bit math
+    if (!SPLIT && plane) return;
     const uint8_t* base = reinterpret_cast<const uint8_t*>((plane ? d.y2_lo : d.y2) + (int64_t)pend_img * 5184);
     if (yoff[mt] >= 0) {
       const uint4 v = pend[mt][jh];
@@ -290,17 +305,22 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
         if (part < 2) {
 #pragma unroll
           for (int r = 2 * part; r < 2 * part + 2; ++r)
-            ev[nt][r] = fmaxf(fmaf(accl[nt][r], 1.f / CF_LO_SCALE, acc[nt][r]), 0.f);
+            ev[nt][r] = SPLIT ? fmaxf(fmaf(accl[nt][r], 1.f / CF_LO_SCALE, acc[nt][r]), 0.f) : fmaxf(acc[nt][r], 0.f);
         } else if (part == 2) {
-          split_pk_bf16_s(ev[nt][0], ev[nt][1], eh[nt][0], el[nt][0]);
-          split_pk_bf16_s(ev[nt][2], ev[nt][3], eh[nt][1], el[nt][1]);
+          if (SPLIT) {
+            split_pk_bf16_s(ev[nt][0], ev[nt][1], eh[nt][0], el[nt][0]);
+            split_pk_bf16_s(ev[nt][2], ev[nt][3], eh[nt][1], el[nt][1]);
+          } else {
+            eh[nt][0] = cvt_pk_bf16(ev[nt][0], ev[nt][1]);
+            eh[nt][1] = cvt_pk_bf16(ev[nt][2], ev[nt][3]);
+          }
         } else {
           const int p = 16 * (th + 2 * j) + pl, oh = p / 20, ow = p - 20 * oh;
           const int P = (j == 12 && p >= 400) ? 400 + (pl & 7) : cf_pix(oh, ow);
           const int ch = 32 * cp + 16 * nt + 4 * g;
           const int off = cf_off(P, ch >> 3) + (ch & 7) * 2;
           *reinterpret_cast<uint2*>(Y1 + off) = make_uint2(eh[nt][0], eh[nt][1]);
-          *reinterpret_cast<uint2*>(Y1 + CF_PLANE + off) = make_uint2(el[nt][0], el[nt][1]);
+          if (SPLIT) *reinterpret_cast<uint2*>(Y1 + CF_PLANE + off) = make_uint2(el[nt][0], el[nt][1]);
         }
       };
       auto cvt = [&](const uint2 v) {
@@ -323,17 +343,18 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt) {
             acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1h[nt][s2], av[s2 & 1], s2 ? acc[nt] : bias1[nt], 0, 0, 0);
-            accl[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1l[nt][s2], av[s2 & 1],
-                                                              s2 ? accl[nt] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            if (SPLIT)
+              accl[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1l[nt][s2], av[s2 & 1],
+                                                                s2 ? accl[nt] : (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
           }
           if (pj >= 0) {
 #pragma unroll
             for (int k = s2 * 8 / (2 * C); k < (s2 + 1) * 8 / (2 * C); ++k) epi_piece(k, pj, pacc, paccl);
           }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < (SPLIT ? 4 : 2); ++q) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);    // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);    // VALU
+            __builtin_amdgcn_sched_group_barrier(0x002, SPLIT ? 3 : 5, 0);    // VALU
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -362,7 +383,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
     // image i + 1's frames (DMA pieces at tiles 1 .. NDW, each before that tile's y2 store)
     // have landed: only the y2 stores of tiles NDW .. 12 are younger than the last piece
     static_assert(NDW <= 7, "the vmcnt below assumes the last DMA piece at tile <= 7");
-    if (i > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(13 - NDW) : "memory");
+    if (i > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(cf_young_stores(NDW, SPLIT)) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();          // y1 complete; staging(i) read (free: the reduction's); staging(i + 1) visible
     const bool copy = img < d.copy_n;
@@ -376,16 +397,20 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
       int tq = tid;
       asm volatile("" : "+v"(tq));
       const int cst = tq & 7;
+      // (bf16: 3200 chunks of one plane, 12.5 rounds)
+      constexpr int NR = SPLIT ? 25 : 13, NB = 5;
 #pragma unroll
-      for (int r0 = 0; r0 < 25; r0 += 5) {
-        uint4 v[5];
+      for (int r0 = 0; r0 < NR; r0 += NB) {
+        uint4 v[NB];
 #pragma unroll
-        for (int r = 0; r < 5; ++r)
-          v[r] = *reinterpret_cast<const uint4*>(
-              Y1 + (r0 + r) * 4096 + tq * 16 +
-              ((r0 + r > 12 || (r0 + r == 12 && tq >= 128)) ? CF_PLANE - 51200 : 0));    // lo plane
+        for (int r = 0; r < NB; ++r)
+          if (r0 + r < NR && (SPLIT || r0 + r < 12 || tq < 128))
+            v[r] = *reinterpret_cast<const uint4*>(
+                Y1 + (r0 + r) * 4096 + tq * 16 +
+                ((r0 + r > 12 || (r0 + r == 12 && tq >= 128)) ? CF_PLANE - 51200 : 0));    // lo plane
 #pragma unroll
-        for (int r = 0; r < 5; ++r) {
+        for (int r = 0; r < NB; ++r) {
+          if (r0 + r >= NR || (!SPLIT && r0 + r == 12 && tq >= 128)) continue;
           const int k = tq + CF_THREADS * (r0 + r);
           const int plane = k >= 3200 ? 1 : 0, kk = k - plane * 3200;
           const int P = kk >> 3, c = cst ^ ((P >> 1) & 7);      // the chunk stored at slot cst
@@ -410,7 +435,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
 #pragma unroll
       for (int s = 0; s < CF_WAHEAD; ++s) {
         wh[s] = __builtin_bit_cast(bf16x8, wf[s * 64]);
-        wl[s] = __builtin_bit_cast(bf16x8, wf[C2F_FRAGS + s * 64]);
+        if (SPLIT) wl[s] = __builtin_bit_cast(bf16x8, wf[C2F_FRAGS + s * 64]);
       }
       bf16x8 ah[2][3], al[2][3];
 #define CF_LDA(s_, buf_)                                                                     \
@@ -418,22 +443,25 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
         const int P_ = (((s_) >> 4) * 2 + (((s_) >> 2) & 1)) * 100 + q0[mt] + (((s_) >> 3) & 1); \
         const int o_ = cf_off(P_, (((s_) & 3) << 1) | kg);                                   \
         ah[buf_][mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Y1 + o_)); \
-        al[buf_][mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Y1 + CF_PLANE + o_)); \
+        if (SPLIT) al[buf_][mt] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(Y1 + CF_PLANE + o_)); \
       }
       CF_LDA(0, 0)
 #pragma unroll
       for (int s = 0; s < 32; ++s) {
         if (s + CF_WAHEAD < 32) {
           wh[(s + CF_WAHEAD) % (CF_WAHEAD + 1)] = __builtin_bit_cast(bf16x8, wf[(s + CF_WAHEAD) * 64]);
-          wl[(s + CF_WAHEAD) % (CF_WAHEAD + 1)] = __builtin_bit_cast(bf16x8, wf[C2F_FRAGS + (s + CF_WAHEAD) * 64]);
+          if (SPLIT)
+            wl[(s + CF_WAHEAD) % (CF_WAHEAD + 1)] = __builtin_bit_cast(bf16x8, wf[C2F_FRAGS + (s + CF_WAHEAD) * 64]);
         }
         if (s + 1 < 32) CF_LDA(s + 1, (s + 1) & 1)
         __builtin_amdgcn_sched_barrier(0);
         const bf16x8 bh = wh[s % (CF_WAHEAD + 1)], bl = wl[s % (CF_WAHEAD + 1)];
 #pragma unroll
         for (int mt = 0; mt < 3; ++mt) {
-          acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl, ah[s & 1][mt], acc2[mt], 0, 0, 0);
-          acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, al[s & 1][mt], acc2[mt], 0, 0, 0);
+          if (SPLIT) {
+            acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl, ah[s & 1][mt], acc2[mt], 0, 0, 0);
+            acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, al[s & 1][mt], acc2[mt], 0, 0, 0);
+          }
           acc2[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh, ah[s & 1][mt], acc2[mt], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -477,9 +505,14 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_split_kernel(Conv1
           const float v1 = fmaxf((bb.y + p0.y) + p1.y, 0.f);
           const float v2 = fmaxf((bb.z + p0.z) + p1.z, 0.f);
           const float v3 = fmaxf((bb.w + p0.w) + p1.w, 0.f);
-          uint32_t h01, l01, h23, l23;
-          split_pk_bf16(v0, v1, h01, l01);
-          split_pk_bf16(v2, v3, h23, l23);
+          uint32_t h01, l01 = 0, h23, l23 = 0;
+          if (SPLIT) {
+            split_pk_bf16(v0, v1, h01, l01);
+            split_pk_bf16(v2, v3, h23, l23);
+          } else {
+            h01 = cvt_pk_bf16(v0, v1);
+            h23 = cvt_pk_bf16(v2, v3);
+          }
           pend[mt][jh] = make_uint4(h01, h23, l01, l23);
         }
       }
@@ -516,23 +549,26 @@ static int cf_launch_pack(const Conv12Desc& d, hipStream_t st) {
 
 // pack only (the learner's target sync): d.pack_sets of d's weights
 APEX_EXPORT int apex_conv12_pack(Conv12Desc d, hipStream_t st) {
-  if (d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr || d.w2_lo == nullptr || d.wfrag == nullptr ||
+  const bool sp = d.bf16 == 0;
+  if (d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr || (sp && d.w2_lo == nullptr) || d.wfrag == nullptr ||
       d.w1frag == nullptr || ((d.pack_sets & 2) && (d.w1b == nullptr || d.b1b == nullptr || d.w2b == nullptr ||
-                                                   d.w2b_lo == nullptr)))
+                                                   (sp && d.w2b_lo == nullptr))))
     return (int)hipErrorInvalidValue;
   return cf_launch_pack(d, st);
 }
 
 APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if (d.N < 1) return 0;
+  const bool sp = d.bf16 == 0;
   if (d.ring == nullptr || d.slots == nullptr || d.w1 == nullptr || d.b1 == nullptr || d.w2 == nullptr ||
-      d.w2_lo == nullptr || d.b2 == nullptr || d.y2 == nullptr || d.y2_lo == nullptr ||
+      (sp && d.w2_lo == nullptr) || d.b2 == nullptr || d.y2 == nullptr || (sp && d.y2_lo == nullptr) ||
       d.wfrag == nullptr || d.scratch == nullptr || d.w1frag == nullptr)
     return (int)hipErrorInvalidValue;
   const bool two = d.w1b != nullptr;
-  if (two && (d.b1b == nullptr || d.w2b == nullptr || d.w2b_lo == nullptr || d.b2b == nullptr))
+  if (two && (d.b1b == nullptr || d.w2b == nullptr || (sp && d.w2b_lo == nullptr) || d.b2b == nullptr))
     return (int)hipErrorInvalidValue;
-  if (d.copy_n > 0 && (d.y1 == nullptr || d.y1_lo == nullptr || d.copy_n > d.N)) return (int)hipErrorInvalidValue;
+  if (d.copy_n > 0 && (d.y1 == nullptr || (sp && d.y1_lo == nullptr) || d.copy_n > d.N))
+    return (int)hipErrorInvalidValue;
   if ((((uintptr_t)d.w1 | (uintptr_t)(two ? d.w1b : d.w1) | (uintptr_t)d.b1 | (uintptr_t)(two ? d.b1b : d.b1) |
         (uintptr_t)d.w2 | (uintptr_t)d.w2_lo | (uintptr_t)d.b2 | (uintptr_t)d.y1 | (uintptr_t)d.y1_lo) & 15) ||
       (((uintptr_t)d.y2 | (uintptr_t)d.y2_lo | (uintptr_t)d.scratch) & 7) || ((uintptr_t)d.wfrag & 15))
@@ -542,10 +578,13 @@ APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if ((d.N + G - 1) / G > CF_MAXIMG) G = (d.N + CF_MAXIMG - 1) / CF_MAXIMG;
   const int err = cf_launch_pack(d, st);
   if (err) return err;
-  switch (d.C) {
-    case 1: conv12_fused_split_kernel<1><<<G, CF_THREADS, 0, st>>>(d); break;
-    case 2: conv12_fused_split_kernel<2><<<G, CF_THREADS, 0, st>>>(d); break;
-    case 4: conv12_fused_split_kernel<4><<<G, CF_THREADS, 0, st>>>(d); break;
+  switch (d.C * 2 + (sp ? 1 : 0)) {
+    case 3: conv12_fused_kernel<1, true><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 5: conv12_fused_kernel<2, true><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 9: conv12_fused_kernel<4, true><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 2: conv12_fused_kernel<1, false><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 4: conv12_fused_kernel<2, false><<<G, CF_THREADS, 0, st>>>(d); break;
+    case 8: conv12_fused_kernel<4, false><<<G, CF_THREADS, 0, st>>>(d); break;
     default: return (int)hipErrorInvalidValue;
   }
   APEX_CHECK_LAUNCH();

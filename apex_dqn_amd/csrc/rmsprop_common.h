@@ -124,7 +124,9 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
       pbl4[i] = make_uint2(l01, l23);
       if (A_.fo.w1frag != nullptr) cf_frag_store(A_.fo, 4 * i, px, make_uint2(h01, h23), make_uint2(l01, l23));
     } else {
-      pb4[i] = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
+      const uint2 hb = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
+      pb4[i] = hb;
+      if (A_.fo.w1frag != nullptr) cf_frag_store(A_.fo, 4 * i, px, hb, make_uint2(0u, 0u));
     }
     gg = gn; pp = pn; vv = vn; mm = mn;
   }

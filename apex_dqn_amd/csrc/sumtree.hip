@@ -718,7 +718,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   int nb = (int)((n / 4 + nt - 1) / nt);
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
   const int nsb = blocks_for(B, nt / 64);
-  if (fo.w1frag != nullptr && (pb_lo == nullptr || fo.c2f == nullptr || (fo.C != 1 && fo.C != 2 && fo.C != 4) ||
+  if (fo.w1frag != nullptr && (fo.c2f == nullptr || (fo.C != 1 && fo.C != 2 && fo.C != 4) ||
                                (fo.w1_off & 3) || (fo.w2_off & 7) || fo.w1_off + 4096LL * fo.C > n ||
                                fo.w2_off + 65536 > n))
     return (int)hipErrorInvalidValue;

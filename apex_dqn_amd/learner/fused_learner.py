@@ -92,6 +92,12 @@ class FusedNatureLearner(IsNormMixin):
         self.split = (self.precision == "fp32" and backend == "hip") if split is None else bool(split)
         self.act_dtype = torch.bfloat16 if (self.split or (cuda and self.ops.name == "hip")
                                             or (cuda and self.precision == "bf16")) else torch.float32
+        # conv1 -> conv2 forward in one launch, y1 kept in LDS (csrc/conv12_fused.hip): the
+        # split kernel in fp32 mode, its one-plane variant for the bf16 learner
+        # (APEX_CONV12_BF16=0: the bf16 learner runs the two image-resident kernels)
+        # (the torch backend emulates the split kernel's contract: ops.conv12_fwd)
+        self._c12 = self.split or (backend == "hip" and self.ops._conv12_native()
+                                   and os.environ.get("APEX_CONV12_BF16", "1") != "0")
         d = self.device
         self.layout = FlatLayout(nature_segments(self.C, self.A, 64))
         n = self.layout.numel
@@ -203,7 +209,7 @@ class FusedNatureLearner(IsNormMixin):
         ops = self.ops
         if os.environ.get("APEX_OPT_FRAGS", "1") == "0":
             return
-        if not (self.split and self._presample and getattr(self.replay, "use_hip", False)
+        if not (self._c12 and self._presample and getattr(self.replay, "use_hip", False)
                 and getattr(ops, "_conv12_native", lambda: False)()):
             return
         from ..ops import conv as C
@@ -281,7 +287,7 @@ class FusedNatureLearner(IsNormMixin):
         sp = self.split
         n = 3 * B
         # c2f: conv2's weights packed for its forward in the same launch (csrc/conv2_wfrag.h)
-        if sp:
+        if self._c12:
             # conv1 -> conv2 in one launch, y1 kept in LDS; only the S_t rows' y1 (the
             # backward's input) is written out (csrc/conv12_fused.hip)
             # (the target set's weight fragments are repacked at each target change:
@@ -305,12 +311,14 @@ class FusedNatureLearner(IsNormMixin):
 
     def _conv12_weights(self):
         P, T, Pb, Tb, Pl, Tl = self.P, self.T, self.Pb, self.Tb, self.Pl, self.Tl
-        return ((P["w1"], P["b1"], T["w1"], T["b1"]), (Pb["w2"], Pl["w2"], P["b2"], Tb["w2"], Tl["w2"], T["b2"]))
+        sp = self.split
+        return ((P["w1"], P["b1"], T["w1"], T["b1"]),
+                (Pb["w2"], Pl["w2"] if sp else None, P["b2"], Tb["w2"], Tl["w2"] if sp else None, T["b2"]))
 
     def _target_changed(self) -> None:
         """The target weights (t32 / tbf) changed: repack the fused forward's target
-        fragments (split mode)."""
-        if self.split:
+        fragments (fused conv1 -> conv2 forward)."""
+        if self._c12:
             c1, c2 = self._conv12_weights()
             self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=2)
             self._tgt_packed = True

@@ -230,13 +230,16 @@ def _conv12_desc(ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1, b
     from .conv_sigs import Conv12Desc
     C = int(w1.shape[1])
     assert tuple(w1.shape) == (64, C, 8, 8) and w1.dtype == torch.float32 and w1.is_contiguous()
-    assert tuple(w2.shape) == (64, 4, 4, 64) and w2.dtype == torch.bfloat16 and w2_lo.dtype == torch.bfloat16
+    assert tuple(w2.shape) == (64, 4, 4, 64) and w2.dtype == torch.bfloat16
+    assert w2_lo is None or w2_lo.dtype == torch.bfloat16
     d = Conv12Desc()
+    d.bf16 = int(w2_lo is None)          # one bf16 plane (the bf16 learner)
     d.ring, d.slots = _lib.ptr(ring), _lib.ptr(slots)
-    d.w1, d.b1, d.w2, d.w2_lo, d.b2 = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), w2_lo.data_ptr(), b2.data_ptr()
+    d.w1, d.b1, d.w2, d.w2_lo, d.b2 = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), _lib.ptr(w2_lo), b2.data_ptr()
     if w1b is not None:
         assert tuple(w1b.shape) == tuple(w1.shape) and tuple(w2b.shape) == tuple(w2.shape)
-        d.w1b, d.b1b, d.w2b, d.w2b_lo, d.b2b = (w1b.data_ptr(), b1b.data_ptr(), w2b.data_ptr(), w2b_lo.data_ptr(),
+        assert (w2b_lo is None) == (w2_lo is None)
+        d.w1b, d.b1b, d.w2b, d.w2b_lo, d.b2b = (w1b.data_ptr(), b1b.data_ptr(), w2b.data_ptr(), _lib.ptr(w2b_lo),
                                                  b2b.data_ptr())
     dev = w1.device
     # conv1 fragments + folded biases of both sets (csrc/conv12_fused.hip CF_W1FRAG_U4 uint4)
@@ -285,17 +288,21 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     in LDS; rows < ``copy_n`` also store y1 (hi / lo) for the backward.  Rows >=
     ``rows_first`` use the second weight set (``w1b`` ..) when given.  ``pack_sets``: the
     weight sets whose fragments the launch repacks first (the others' must be current,
-    see ``conv12_pack``)."""
+    see ``conv12_pack``).  ``w2_lo`` None: the bf16 kernel (one plane; ``y1_lo``,
+    ``y2_lo`` unused)."""
     N, C = slots.shape
+    sp = w2_lo is not None
     assert slots.dtype == torch.int32 and slots.is_contiguous() and int(w1.shape[1]) == C
-    assert tuple(y2.shape) == (N, 9, 9, 64) and tuple(y2_lo.shape) == (N, 9, 9, 64)
+    assert tuple(y2.shape[:4]) == (N, 9, 9, 64) and y2.is_contiguous() and y2.dtype == torch.bfloat16
+    assert not sp or (y2_lo is not None and tuple(y2_lo.shape) == (N, 9, 9, 64))
     d = _conv12_desc(ws, ring, slots, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b)
     d.img_switch = int(rows_first) if w1b is not None else N
     if copy_n > 0:
-        assert y1 is not None and y1_lo is not None and y1.shape[0] >= copy_n and tuple(y1.shape[1:]) == (20, 20, 64)
-        d.y1, d.y1_lo = y1.data_ptr(), y1_lo.data_ptr()
+        assert y1 is not None and (y1_lo is not None or not sp) and y1.shape[0] >= copy_n and \
+            tuple(y1.shape[1:]) == (20, 20, 64) and y1.is_contiguous()
+        d.y1, d.y1_lo = y1.data_ptr(), (y1_lo.data_ptr() if sp else 0)
     d.copy_n = int(copy_n)
-    d.y2, d.y2_lo = y2.data_ptr(), y2_lo.data_ptr()
+    d.y2, d.y2_lo = y2.data_ptr(), (y2_lo.data_ptr() if sp else 0)
     d.pack_sets = int(pack_sets)
     d.N = N
     d.probe = _lib.ptr(probe)

@@ -17,12 +17,12 @@ class Conv2ImgDesc(ctypes.Structure):
 
 
 class Conv12Desc(ctypes.Structure):
-    """Fused conv1 -> conv2 split forward (mirrors ``Conv12Desc`` in csrc/conv12_fused.hip)."""
+    """Fused conv1 -> conv2 forward, split or bf16 (mirrors ``Conv12Desc`` in csrc/conv12_fused.hip)."""
     _fields_ = [("ring", c_p), ("slots", c_p), ("w1", c_p), ("w1b", c_p), ("b1", c_p), ("b1b", c_p),
                 ("w2", c_p), ("w2_lo", c_p), ("w2b", c_p), ("w2b_lo", c_p), ("wfrag", c_p), ("pack_sets", c_i),
                 ("b2", c_p), ("b2b", c_p), ("y1", c_p), ("y1_lo", c_p), ("y2", c_p), ("y2_lo", c_p),
                 ("w1frag", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("img_switch", c_i), ("copy_n", c_i),
-                ("in_scale", ctypes.c_float), ("probe", c_p), ("wq", c_p)]
+                ("in_scale", ctypes.c_float), ("probe", c_p), ("wq", c_p), ("bf16", c_i)]
 
 
 class Conv2DgradImgDesc(ctypes.Structure):

@@ -464,6 +464,57 @@ def test_conv12_fused_split_vs_fp64_and_separate_kernels(N, switch, copy_n, C, g
         assert _rel(_join(y1h, y1l)[:copy_n], _join(s1h, s1l)[:copy_n]) < 1e-5
 
 
+@pytest.mark.parametrize("N,switch,copy_n,C,grid", [(1536, 1024, 512, 4, 0), (37, 20, 9, 4, 5), (50, 50, 50, 1, 0),
+                                                    (40, 24, 0, 2, 7)])
+def test_conv12_fused_bf16_vs_fp64_and_separate_kernels(N, switch, copy_n, C, grid):
+    """The bf16 learner's fused conv1 -> conv2 forward (one plane: f16 conv1 operands, bf16
+    y1 in LDS, bf16 conv2 weights) against fp64 at bf16-class tolerance and against the
+    two separate bf16 kernels (conv1 -> HBM -> conv2)."""
+    from apex_dqn_amd.ops import conv as C_
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+    g = torch.Generator(device="cpu").manual_seed(N + C + 100)
+    raw = torch.randint(0, 256, (80, 84, 84), generator=g, dtype=torch.uint8)
+    ring = to_s2d(raw.to(DEV))
+    slots = torch.randint(0, 80, (N, C), generator=g, dtype=torch.int32).to(DEV)
+    w1a, w1b = (torch.randn(64, C, 8, 8, generator=g) * 0.05).to(DEV), (torch.randn(64, C, 8, 8, generator=g) * 0.05).to(DEV)
+    b1a, b1b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    w2a = (torch.randn(64, 4, 4, 64, generator=g) * 0.03).to(DEV, torch.bfloat16)
+    w2b = (torch.randn(64, 4, 4, 64, generator=g) * 0.03).to(DEV, torch.bfloat16)
+    b2a, b2b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    scale = 1 / 255.0
+    ws = C_.Workspace()
+    y2 = torch.full((N, 9, 9, 64), float("nan"), device=DEV, dtype=torch.bfloat16)
+    y1 = torch.full((max(copy_n, 1), 20, 20, 64), float("nan"), device=DEV, dtype=torch.bfloat16)
+    two = switch < N
+    kw2 = dict(w1b=w1b, b1b=b1b, w2b=w2b, w2b_lo=None, b2b=b2b, rows_first=switch) if two else {}
+    C_.conv12_fused_fwd(_lib(), ws, ring, slots, w1a, b1a, w2a, None, b2a, scale, y2, None, y1=y1, y1_lo=None,
+                        copy_n=copy_n, grid=grid, **kw2)
+    torch.cuda.synchronize()
+    assert not torch.isnan(y2).any()
+    fr = torch.stack([raw[slots[i].long().cpu()] for i in range(N)]).double() * scale
+    ref1 = torch.empty(N, 64, 20, 20, dtype=torch.float64)
+    for lo, hi, w, b in ((0, switch, w1a, b1a), (switch, N, w1b, b1b)):
+        if hi > lo:
+            ref1[lo:hi] = torch.relu(torch.nn.functional.conv2d(fr[lo:hi], _c(w), _c(b), stride=4))
+    x1 = ref1.permute(0, 2, 3, 1)
+    ref2 = torch.cat([R.conv_fwd(x1[:switch], _c(w2a), _c(b2a), 2, torch.float64)] +
+                     ([R.conv_fwd(x1[switch:], _c(w2b), _c(b2b), 2, torch.float64)] if two else []))
+    e2 = _rel(_c(y2), ref2)
+    assert e2 < 1e-2, e2                      # bf16 y1 and y2 roundings (2^-9 each)
+    if copy_n:
+        e1 = _rel(_c(y1)[:copy_n], x1[:copy_n])
+        assert e1 < 5e-3, e1
+    s1 = torch.empty(N, 20, 20, 64, device=DEV, dtype=torch.bfloat16)
+    s2 = torch.empty(N, 9, 9, 64, device=DEV, dtype=torch.bfloat16)
+    C_.conv1_s2d_fwd(_lib(), ws, ring, slots, w1a.to(torch.bfloat16), b1a, scale, s1,
+                     w1b.to(torch.bfloat16) if two else None, b1b if two else None, switch if two else 0)
+    C_.conv2_img_fwd(_lib(), s1, w2a, b2a, s2, w2b if two else None, b2b if two else None, switch if two else 0)
+    torch.cuda.synchronize()
+    es = _rel(_c(s2), ref2)
+    print(f"bf16 conv2 output vs fp64: fused {e2:.2e}, separate kernels {es:.2e}")
+    assert e2 < 1.5 * es + 1e-4               # f16 conv1 operands: no worse than the bf16 kernels
+
+
 @pytest.mark.parametrize("N,grid", [(1536, 0), (37, 5)])
 def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
     """The persistent kernels' image work queue (csrc/mfma_common.h wq_next, enabled by the
@@ -505,14 +556,14 @@ def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
             assert torch.equal(a, b)
 
 
-def _presample_learner(monkeypatch, opt_frags: bool):
+def _presample_learner(monkeypatch, opt_frags: bool, dtype: str = "fp32"):
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
     monkeypatch.setenv("APEX_OPT_FRAGS", "1" if opt_frags else "0")
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": 128},
-                                "Runtime": {"use_graphs": False, "presample": True, "dtype": "fp32"}})
+                                "Runtime": {"use_graphs": False, "presample": True, "dtype": dtype}})
     torch.manual_seed(0)
     rp = GpuReplayShard(2000, 2000, 2100, 4, device=DEV, seed=7)
     rng = np.random.default_rng(11)
@@ -524,7 +575,8 @@ def _presample_learner(monkeypatch, opt_frags: bool):
     return FusedNatureLearner(cfg, DEV, rp, backend="hip")
 
 
-def test_optimizer_stores_conv12_fragments_bit_identical_to_pack(monkeypatch):
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_optimizer_stores_conv12_fragments_bit_identical_to_pack(monkeypatch, dtype):
     """The optimizer + sample launch stores the updated w1 / w2 in the fused forward's
     fragment order (csrc/cf_pack.h cf_frag_store): after real steps the online fragments
     are byte-identical to a fresh pack launch, and the run's weights are bit-identical to
@@ -532,8 +584,8 @@ def test_optimizer_stores_conv12_fragments_bit_identical_to_pack(monkeypatch):
     from apex_dqn_amd.ops import conv as C
     out = {}
     for opt in (True, False):
-        L = _presample_learner(monkeypatch, opt)
-        assert (L._frag_out is not None) == opt
+        L = _presample_learner(monkeypatch, opt, dtype)
+        assert L._c12 and (L._frag_out is not None) == opt
         for _ in range(3):
             L.step()
         torch.cuda.synchronize()
@@ -543,11 +595,12 @@ def test_optimizer_stores_conv12_fragments_bit_identical_to_pack(monkeypatch):
             w1f = ws.get(("cf_w1frag",), C.CF_W1FRAG_BYTES, dev, torch.uint8)
             c2f = ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, dev, torch.uint8)
             half = C.CF_W1FRAG_BYTES // 2          # set 0 (online) of w1; hi + lo planes of set 0 of w2
-            got = (w1f[:half].clone(), c2f[:2 * 8192 * 16].clone())
+            planes = 2 if dtype == "fp32" else 1   # (bf16: the hi plane only is read)
+            got = (w1f[:half].clone(), c2f[:planes * 8192 * 16].clone())
             c1, c2 = L._conv12_weights()
             L.ops.conv12_pack(c1, c2, L.rt.obs_scale, sets=1)
             torch.cuda.synchronize()
             assert torch.equal(got[0], w1f[:half]), "conv1 fragments differ from the pack launch"
-            assert torch.equal(got[1], c2f[:2 * 8192 * 16]), "conv2 C2F fragments differ from the pack launch"
+            assert torch.equal(got[1], c2f[:planes * 8192 * 16]), "conv2 C2F fragments differ from the pack launch"
         del L
     assert torch.equal(out[True], out[False])
