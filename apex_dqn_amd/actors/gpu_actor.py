@@ -183,8 +183,35 @@ class GpuActorGroup:
         return self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64)
 
     def _policy(self, payload: np.ndarray):
+        """Inference for the payload's frame stacks (on the actor stream): slots in, the
+        kernels (one HIP graph replay with Runtime.actor_graph: captured once, outside the
+        actor thread -- the fill phase's first step), q / actions out to pinned memory."""
+        sl = torch.from_numpy((payload % self.replay.F).astype(np.int32))
+        if self.device.type == "cuda":
+            if getattr(self, "_slots_host", None) is None:
+                self._slots_host = torch.zeros(self.E, self.C, dtype=torch.int32).pin_memory()
+            self._slots_host.copy_(sl)
+            sl = self._slots_host
+        self.slots.copy_(sl, non_blocking=True)
+        if self._use_graph():
+            if getattr(self, "_graph", None) is None:
+                self._policy_kernels()            # warm: kernel library, workspaces
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.stream):
+                    self._policy_kernels()
+                self._graph = g
+            self._graph.replay()
+        else:
+            self._policy_kernels()
+        self.q_host.copy_(self.q, non_blocking=True)
+        self.a_host.copy_(self.act, non_blocking=True)
+
+    def _use_graph(self) -> bool:
+        return bool(getattr(self.cfg.Runtime, "actor_graph", False)) and self.stream is not None \
+            and type(self)._policy_kernels is GpuActorGroup._policy_kernels
+
+    def _policy_kernels(self) -> None:
         ops, P, Pb, Pl, E = self.ops, self.P, self.Pb, self.Pl, self.E
-        self.slots.copy_(torch.from_numpy((payload % self.replay.F).astype(np.int32)), non_blocking=True)
         if self.split:   # fp32-class: the learner's split kernels (hi / lo planes throughout)
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
                                self.cfg.Runtime.obs_scale, self.y1, w32=P["w1"], out_lo=self.y1_lo)
@@ -201,14 +228,34 @@ class GpuActorGroup:
         heads = {k: P[k] for k in ("wv", "bv", "wa", "ba")}
         ops.actor_head(self.h, heads, self.eps, self.ctr, self.seed, self.q, self.act, H_lo=self.h_lo)
         self.ctr += 1
-        self.q_host.copy_(self.q, non_blocking=True)
-        self.a_host.copy_(self.act, non_blocking=True)
 
     def step(self) -> int:
         """One env step for all E envs; returns the number of transitions inserted."""
         if self.payload is None:
             self.reset()
         q, actions = self.policy(self.payload)
+        return self._env_step(q, actions)
+
+    # split step (PipelinedActorGroups): the policy launch returns at once; the finish
+    # waits for its q / actions, steps the envs and inserts
+    def launch_policy(self) -> None:
+        if self.payload is None:
+            self.reset()
+        with self._on_stream():
+            self._policy(self.payload)
+        self._pending = torch.cuda.Event() if self.stream is not None else None
+        if self._pending is not None:
+            self._pending.record(self.stream)
+
+    def finish_step(self) -> int:
+        """Wait for the launched inference, step the envs, append the frames, insert."""
+        ev = getattr(self, "_pending", None)
+        if ev is not None:
+            ev.synchronize()
+        self._pending = None
+        return self._env_step(self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64))
+
+    def _env_step(self, q: np.ndarray, actions: np.ndarray) -> int:
         frames, rew, done, info = self.env.step(actions)
         prev = self.payload
         self.payload = self._ingest(frames, done)
@@ -231,6 +278,53 @@ class GpuActorGroup:
                 n = len(b["A_t"])
                 self.inserted += n
         return n
+
+
+class PipelinedActorGroups:
+    """A rank's envs as K actor groups (own envs, HIP stream and buffers each) stepped in
+    turn: group k's q / actions are read back, its envs stepped, its frames appended and
+    its transitions inserted while the inference of the groups after it runs on the GPU.
+    A single group waits for its own inference every step (~0.3 ms of a ~0.6 ms step on
+    the Pong-shaped config, the kernels queued behind the learner's: scripts/diag_e2e_actor.py);
+    here the host's env work hides it.  Each env still acts on its latest frame stack
+    (every group's policy is launched after its previous env step), so the transitions are
+    those of one group of K * E envs; the groups take consecutive env ids and slices of
+    the rank's epsilon ladder.  Exposes the GpuActorGroup attributes the GPU loop and the
+    actor thread use (E, eps, episodes, inserted, ctr, step, reset_episodes)."""
+
+    def __init__(self, groups: List["GpuActorGroup"]):
+        self.groups = list(groups)
+        self.E = sum(g.E for g in self.groups)
+        self.eps = torch.cat([g.eps for g in self.groups])
+        self.episodes = self.groups[0].episodes
+        for g in self.groups[1:]:
+            g.episodes = self.episodes          # one time-ordered episode list
+        self.ctr = self.groups[0].ctr           # checkpointed RNG counter (group k's draws use their own seed)
+        self._launched = False
+
+    @property
+    def inserted(self) -> int:
+        return sum(g.inserted for g in self.groups)
+
+    def step(self) -> int:
+        if not self._launched:
+            for g in self.groups:
+                g.launch_policy()
+            self._launched = True
+        n = 0
+        for g in self.groups:
+            n += g.finish_step()
+            g.launch_policy()
+        return n
+
+    def reset_episodes(self) -> None:
+        for g in self.groups:
+            ev = getattr(g, "_pending", None)
+            if ev is not None:       # a launched inference: let it land, drop its result
+                ev.synchronize()
+                g._pending = None
+            g.reset_episodes()
+        self._launched = False
 
 
 def ladder_slice(cfg, E: int, rank: int, world: int, total_actors: Optional[int] = None) -> List[float]:
@@ -341,9 +435,25 @@ class ImpalaActorGroup(GpuActorGroup):
 
 
 def make_gpu_actor_group(cfg, learner, replay, num_envs: int, rank: int = 0, world: int = 1,
-                         seed: int = 0) -> GpuActorGroup:
+                         seed: int = 0, pipeline: int = 1):
+    """The rank's actor group; ``pipeline`` K > 1 (NatureCNN learners on a GPU): K groups
+    of num_envs / K envs stepped in turn (PipelinedActorGroups)."""
     from ..envs.vector_envs import make_vec_env
     total = max(cfg.Actor.num_actors, num_envs * world)
+    K = int(pipeline)
+    if K > 1 and num_envs % K == 0 and num_envs // K >= 1 and getattr(learner, "kind", "") not in ("graph", "impala") \
+            and learner.device.type == "cuda":
+        h = num_envs // K
+        eps_all = ladder_slice(cfg, num_envs, rank, world, total)
+        groups = []
+        for k in range(K):
+            env = make_vec_env(cfg.env_backend, cfg.env_conf.name, h, cfg.env_conf.action_dim,
+                               seed=seed + 1000 * rank + 100003 * k)
+            g = GpuActorGroup(cfg, learner, replay, env, h, global_offset=rank * num_envs + k * h,
+                              total_actors=total, seed=seed + rank, rank=rank, world=world)
+            g.eps = torch.tensor(eps_all[k * h:(k + 1) * h], dtype=torch.float32, device=learner.device)
+            groups.append(g)
+        return PipelinedActorGroups(groups)
     env = make_vec_env(cfg.env_backend, cfg.env_conf.name, num_envs, cfg.env_conf.action_dim,
                        seed=seed + 1000 * rank)
     kind = getattr(learner, "kind", "")

@@ -92,13 +92,7 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
                                              is_grad_scale(A_.wnorm, A_.wn, A_.wstride));
   if (bid == 0 && threadIdx.x == 0 && A_.norm_out) A_.norm_out[0] = sh[1];
   const float a1 = 1.0f - alpha;
-  for (; i < n4; i += stride) {
-    const int64_t inx = i + stride;
-    float4 gn = z4, pn = z4, vn = z4, mn = z4;
-    if (inx < n4) {
-      gn = g4[inx]; pn = p4[inx]; vn = v4[inx];
-      if (centered) mn = m4[inx];
-    }
+  auto update = [&](int64_t i, const float4 gg, const float4 pp, const float4 vv, const float4 mm, const bool frag) {
     float gx[4] = {gg.x * coef, gg.y * coef, gg.z * coef, gg.w * coef};
     float px[4] = {pp.x, pp.y, pp.z, pp.w};
     float vx[4] = {vv.x, vv.y, vv.z, vv.w};
@@ -122,12 +116,33 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
       split_pk_bf16_h(px[2], px[3], h23, l23);
       pb4[i] = make_uint2(h01, h23);
       pbl4[i] = make_uint2(l01, l23);
-      if (A_.fo.w1frag != nullptr) cf_frag_store(A_.fo, 4 * i, px, make_uint2(h01, h23), make_uint2(l01, l23));
+      if (frag) cf_frag_store(A_.fo, 4 * i, px, make_uint2(h01, h23), make_uint2(l01, l23));
     } else {
       const uint2 hb = make_uint2(pack_bf16x2(px[0], px[1]), pack_bf16x2(px[2], px[3]));
       pb4[i] = hb;
-      if (A_.fo.w1frag != nullptr) cf_frag_store(A_.fo, 4 * i, px, hb, make_uint2(0u, 0u));
+      if (frag) cf_frag_store(A_.fo, 4 * i, px, hb, make_uint2(0u, 0u));
     }
+  };
+  // The first chunk is peeled: the fused forward's operand stores (A_.fo, the launcher
+  // checks that w1 / w2 lie within every thread's first chunk) run before the next
+  // chunk's loads are issued, so the steady loop keeps 6 waves per SIMD (every block of
+  // the launch resident at once; with the stores inside the loop it held 85 VGPRs)
+  if (i < n4) {
+    update(i, gg, pp, vv, mm, A_.fo.w1frag != nullptr);
+    i += stride;
+    if (i < n4) {
+      gg = g4[i]; pp = p4[i]; vv = v4[i];
+      if (centered) mm = m4[i];
+    }
+  }
+  for (; i < n4; i += stride) {
+    const int64_t inx = i + stride;
+    float4 gn = z4, pn = z4, vn = z4, mn = z4;
+    if (inx < n4) {
+      gn = g4[inx]; pn = p4[inx]; vn = v4[inx];
+      if (centered) mn = m4[inx];
+    }
+    update(i, gg, pp, vv, mm, false);
     gg = gn; pp = pn; vv = vn; mm = mn;
   }
   for (int64_t i = n4 * 4 + (int64_t)bid * blockDim.x + threadIdx.x; i < n; i += (int64_t)nblk * blockDim.x) {

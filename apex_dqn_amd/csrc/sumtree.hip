@@ -720,7 +720,9 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   const int nsb = blocks_for(B, nt / 64);
   if (fo.w1frag != nullptr && (fo.c2f == nullptr || (fo.C != 1 && fo.C != 2 && fo.C != 4) ||
                                (fo.w1_off & 3) || (fo.w2_off & 7) || fo.w1_off + 4096LL * fo.C > n ||
-                               fo.w2_off + 65536 > n))
+                               fo.w2_off + 65536 > n ||
+                               // (stored in each thread's first chunk: rmsprop_body's peel)
+                               (fo.w1_off + 4096LL * fo.C) / 4 > (int64_t)nb * nt || (fo.w2_off + 65536) / 4 > (int64_t)nb * nt))
     return (int)hipErrorInvalidValue;
   const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,
                       wnorm, wn, wstride, fo};

@@ -117,13 +117,16 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
         learner.load(ckpt_path)
         if metrics is not None:
             metrics.log("resume", step=learner.num_q_updates, path=ckpt_path)
-    group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed)
+    if async_actors is None:
+        async_actors = bool(rt.async_actors) and device.type == "cuda"
+    # async actors: the envs as Runtime.actor_pipeline groups stepped in turn (the host's env
+    # work of one group hides another's inference); the lock-step loop keeps one group
+    group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed,
+                                 pipeline=int(rt.actor_pipeline) if async_actors else 1)
     if ckpt_path and rt.resume and os.path.exists(ckpt_path):
         _restore_actor_rng(group, ckpt_path)
     min_local = max(L.min_replay_mem_size // world, L.replay_sample_size)
     max_actor_steps = int(max_actor_steps if max_actor_steps is not None else cfg.Actor.T)
-    if async_actors is None:
-        async_actors = bool(rt.async_actors) and device.type == "cuda"
     t0 = time.time()
     st = _LoopState(t0, learner.num_q_updates)
     # ---- fill: the actors alone until every shard holds min_replay_mem_size / world.

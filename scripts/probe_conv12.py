@@ -32,10 +32,11 @@ def setup(B, dev):
     return dict(ring=ring, slots=slots, w1=w1, w2h=w2h, w2l=w2l, b=b, y1=y1, y1l=y1l, y2=y2, y2l=y2l, N=N)
 
 
-def launch(lib, C, ws, t, B, copy=True, grid=0, probe=None):
-    C.conv12_fused_fwd(lib, ws, t["ring"], t["slots"], t["w1"], t["b"], t["w2h"], t["w2l"], t["b"], 1 / 255.0,
-                       t["y2"], t["y2l"], y1=t["y1"], y1_lo=t["y1l"], copy_n=B if copy else 0, w1b=t["w1"],
-                       b1b=t["b"], w2b=t["w2h"], w2b_lo=t["w2l"], b2b=t["b"], rows_first=2 * B, grid=grid,
+def launch(lib, C, ws, t, B, copy=True, grid=0, probe=None, bf16=False):
+    lo = (lambda k: None) if bf16 else (lambda k: t[k])      # noqa: E731
+    C.conv12_fused_fwd(lib, ws, t["ring"], t["slots"], t["w1"], t["b"], t["w2h"], lo("w2l"), t["b"], 1 / 255.0,
+                       t["y2"], lo("y2l"), y1=t["y1"], y1_lo=lo("y1l"), copy_n=B if copy else 0, w1b=t["w1"],
+                       b1b=t["b"], w2b=t["w2h"], w2b_lo=lo("w2l"), b2b=t["b"], rows_first=2 * B, grid=grid,
                        probe=probe)
 
 
@@ -43,6 +44,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=512)
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--bf16", action="store_true", help="the bf16 learner's one-plane kernel")
     a = ap.parse_args()
     if a.probe:
         os.environ["APEX_DEBUG_BOUNDS"] = "1"
@@ -54,9 +56,9 @@ def main():
     if a.probe:
         buf = torch.zeros(4 * 4 * 16 * 4, dtype=torch.int64, device=dev)
         for _ in range(3):
-            launch(lib, C, ws, t, a.B)
+            launch(lib, C, ws, t, a.B, bf16=a.bf16)
         buf.zero_()
-        launch(lib, C, ws, t, a.B, probe=buf)
+        launch(lib, C, ws, t, a.B, probe=buf, bf16=a.bf16)
         torch.cuda.synchronize()
         st = buf.cpu().numpy().reshape(4, 4, 16, 4)
         names = ["conv1", "wait_copy", "conv2"]
@@ -74,11 +76,11 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for name, kw in (("copy", dict(copy=True)), ("nocopy", dict(copy=False)), ("copy_g240", dict(copy=True, grid=240))):
         for _ in range(5):
-            launch(lib, C, ws, t, a.B, **kw)
+            launch(lib, C, ws, t, a.B, bf16=a.bf16, **kw)
         ts = []
         for _ in range(20):
             ev[0].record()
-            launch(lib, C, ws, t, a.B, **kw)
+            launch(lib, C, ws, t, a.B, bf16=a.bf16, **kw)
             ev[1].record()
             torch.cuda.synchronize()
             ts.append(ev[0].elapsed_time(ev[1]) * 1e3)

@@ -6,7 +6,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows = [r for r in rows]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # find last occurrences of tree_sample_kernel as step starts
-first = sys.argv[2] if len(sys.argv) > 2 else "void cf_pack_kernel"
+first = sys.argv[2] if len(sys.argv) > 2 else "void conv12_fused_kernel"
 starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(first)]
 i0, i1 = starts[-6], starts[-5]
 t0 = int(rows[i0]["Start_Timestamp"])

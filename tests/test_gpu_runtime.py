@@ -448,3 +448,37 @@ def test_actor_q_values_precision_vs_fp32_module(dtype):
         assert np.array_equal(a, q.argmax(1))
     else:
         assert rel > 1e-4        # the bf16 actor is measurably coarser (the reason for the split path)
+
+
+def test_pipelined_actor_groups_step_all_envs():
+    """Runtime.actor_pipeline: the rank's envs as two groups stepped in turn (one group's
+    host env step overlaps the other's inference): every env acts once per step, the
+    groups take consecutive env ids and the rank's epsilon-ladder slices, episodes land
+    in one list, and the transitions reach the replay."""
+    from apex_dqn_amd.actors.gpu_actor import PipelinedActorGroups, ladder_slice, make_gpu_actor_group
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    E = 64
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                "Actor": {"num_actors": E, "n_step_transition_batch_size": 32},
+                                "Learner": {"replay_sample_size": 64},
+                                "Runtime": {"use_graphs": False, "env_backend": "fake_ale"}})
+    torch.manual_seed(3)
+    rp = GpuReplayShard(4000, 4000, 4200, 4, device=DEV)
+    L = FusedNatureLearner(cfg, DEV, rp)
+    grp = make_gpu_actor_group(cfg, L, rp, E, pipeline=2)
+    assert isinstance(grp, PipelinedActorGroups) and grp.E == E and len(grp.groups) == 2
+    assert grp.groups[0].stream is not grp.groups[1].stream
+    assert [g.global_offset for g in grp.groups] == [0, E // 2]
+    np.testing.assert_allclose(grp.eps.cpu().numpy(), np.array(ladder_slice(cfg, E, 0, 1, E), dtype=np.float32))
+    n0 = rp.size()
+    ins = sum(grp.step() for _ in range(40))
+    torch.cuda.synchronize()
+    assert all(g.t == 40 for g in grp.groups)
+    assert ins == grp.inserted > 0 and rp.size() - n0 == ins
+    assert all(g.episodes is grp.episodes for g in grp.groups)
+    grp.reset_episodes()
+    assert all(g.payload is None for g in grp.groups)
+    grp.step()                                        # fresh episodes after an actor restart
+    assert all(g.t == 41 for g in grp.groups)
