@@ -582,16 +582,9 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
       wl[nh][s] = __builtin_bit_cast(bf16x8, wf[C2D_FRAGS + s * 64]);
     }
   }
-  int pi[4], pj[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    // 10-wide pixel grid here: the 11-wide one (C2D_PSLOTS) removes the dY-read bank
-    // conflicts but measured no gain for this four-wave kernel (47.7 vs 47.4 us; again
-    // with packed weights: 45.2 vs 41.4 us, although PMC shows 44 % conflict cycles here)
-    const int r = min(t * 32 + rr, 99);
-    pi[t] = r / 10;
-    pj[t] = r - pi[t] * 10;
-  }
+  // (10-wide pixel grid here: the 11-wide one (C2D_PSLOTS) removes the dY-read bank
+  // conflicts but measured no gain for this four-wave kernel (47.7 vs 47.4 us; again
+  // with packed weights: 45.2 vs 41.4 us, although PMC shows 44 % conflict cycles here)
   __shared__ int q_next;
   C2D_WQ_BEGIN(q_next, img)
   while (img < d.N) {
@@ -608,55 +601,76 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
     }
     __syncthreads();
     if (tid == 0) wq_fetched_ = wq_next(d.wq, wq_seq_, d.N);
-    f32x16 acc[2][4];
+    // two passes of two pixel tiles each: 64 accumulator registers instead of 128, so the
+    // hi / lo weight fragments (128) stay in registers without spills (one pass over all
+    // four tiles spilled ~100 registers per lane to scratch)
 #pragma unroll
-    for (int nh = 0; nh < 2; ++nh)
+    for (int tp = 0; tp < 2; ++tp) {
+      // (the dY fragment offsets are recomputed per pass from an opaque copy of the lane
+      // row: hoisted out of the image loop, the compiler kept all 64 in registers it does
+      // not have and spilled)
+      int pi[4], pj[4];
+      {
+        int rq = rr;
+        asm volatile("" : "+v"(rq));
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[nh][t][j] = 0.f;
-    // B fragments (dY hi, lo) of step u + 1 = (s, t) are read while step u's six
-    // MFMAs run (explicit order: scheduler barriers around each step)
-    bf16x8 xf[2][2];
-#define C2DS_LDX(u_, dst_)                                                                   \
-    {                                                                                        \
-      const int s_ = (u_) >> 2, t_ = (u_) & 3;                                              \
-      const int off_ = c2d_off((pi[t_] - ((s_ >> 3) & 1) + 1) * 11 + (pj[t_] - ((s_ >> 2) & 1) + 1), \
-                               ((s_ & 3) << 1) | kg);                                        \
-      dst_[0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + off_));    \
-      dst_[1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + C2D_PSLOTS * 128 + off_)); \
-    }
-    C2DS_LDX(0, xf[0])
-#pragma unroll
-    for (int u = 0; u < 64; ++u) {
-      const int s = u >> 2, t = u & 3;
-      if (u + 1 < 64) C2DS_LDX(u + 1, xf[(u + 1) & 1])
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int nh = 0; nh < 2; ++nh) {
-        acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[nh][s], xf[u & 1][0], acc[nh][t], 0, 0, 0);
-        acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[nh][s], xf[u & 1][1], acc[nh][t], 0, 0, 0);
-        acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[nh][s], xf[u & 1][0], acc[nh][t], 0, 0, 0);
+        for (int t = 0; t < 4; ++t) {
+          const int r = min(t * 32 + rq, 99);
+          pi[t] = r / 10;
+          pj[t] = r - pi[t] * 10;
+        }
       }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#undef C2DS_LDX
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t * 32 + rr >= 100) continue;
-      const int ih = 2 * pi[t] + p, iw = 2 * pj[t] + q, px = ih * 20 + iw;
+      f32x16 acc[2][2];
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int ch = nh * 32 + 8 * g + 4 * kg;
-          uint32_t h01, l01, h23, l23;
-          split_pk_bf16(acc[nh][t][4 * g], acc[nh][t][4 * g + 1], h01, l01);
-          split_pk_bf16(acc[nh][t][4 * g + 2], acc[nh][t][4 * g + 3], h23, l23);
-          const int o = c2d_off(px, ch >> 3) + (ch & 7) * 2;
-          *reinterpret_cast<uint2*>(sout + o) = make_uint2(h01, h23);
-          *reinterpret_cast<uint2*>(sout + 400 * 128 + o) = make_uint2(l01, l23);
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[nh][t][j] = 0.f;
+      // B fragments (dY hi, lo) of step u + 1 = (s, t) are read while step u's six
+      // MFMAs run (explicit order: scheduler barriers around each step)
+      bf16x8 xf[2][2];
+#define C2DS_LDX(u_, dst_)                                                                   \
+      {                                                                                      \
+        const int s_ = (u_) >> 1, t_ = 2 * tp + ((u_) & 1);                                 \
+        const int off_ = c2d_off((pi[t_] - ((s_ >> 3) & 1) + 1) * 11 + (pj[t_] - ((s_ >> 2) & 1) + 1), \
+                                 ((s_ & 3) << 1) | kg);                                      \
+        dst_[0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + off_));  \
+        dst_[1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + C2D_PSLOTS * 128 + off_)); \
+      }
+      C2DS_LDX(0, xf[0])
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int s = u >> 1, t = u & 1;
+        if (u + 1 < 32) C2DS_LDX(u + 1, xf[(u + 1) & 1])
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh) {
+          acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[nh][s], xf[u & 1][0], acc[nh][t], 0, 0, 0);
+          acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[nh][s], xf[u & 1][1], acc[nh][t], 0, 0, 0);
+          acc[nh][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[nh][s], xf[u & 1][0], acc[nh][t], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#undef C2DS_LDX
+#pragma unroll
+      for (int t2 = 0; t2 < 2; ++t2) {
+        const int t = 2 * tp + t2;
+        if (t * 32 + rr >= 100) continue;
+        const int ih = 2 * pi[t] + p, iw = 2 * pj[t] + q, px = ih * 20 + iw;
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int ch = nh * 32 + 8 * g + 4 * kg;
+            uint32_t h01, l01, h23, l23;
+            split_pk_bf16(acc[nh][t2][4 * g], acc[nh][t2][4 * g + 1], h01, l01);
+            split_pk_bf16(acc[nh][t2][4 * g + 2], acc[nh][t2][4 * g + 3], h23, l23);
+            const int o = c2d_off(px, ch >> 3) + (ch & 7) * 2;
+            *reinterpret_cast<uint2*>(sout + o) = make_uint2(h01, h23);
+            *reinterpret_cast<uint2*>(sout + 400 * 128 + o) = make_uint2(l01, l23);
+          }
+      }
     }
     if (tid == 0) reinterpret_cast<volatile int*>(&q_next)[0] = wq_fetched_;
     __syncthreads();
