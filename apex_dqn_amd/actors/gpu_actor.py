@@ -110,6 +110,23 @@ class GpuActorGroup:
         self.episodes: List[tuple] = []
         self.inserted = 0
         self._init_stream()
+        # conv1 -> conv2 as the learner's fused kernel (csrc/conv12_fused.hip, y1 kept in LDS)
+        # on a backend of the group's own: its weight fragments are the actor slot's, packed
+        # at every parameter sync on the actor stream
+        self.c12_ops = None
+        if getattr(learner, "_c12", False) and self.ops.name == "hip" and self.ops._conv12_native():
+            from ..ops.fused_ops import HipBackend
+            self.c12_ops = HipBackend()
+            with self._on_stream():
+                self._pack_c12()
+
+    def _c12_weights(self):
+        P, Pb, Pl = self.P, self.Pb, self.Pl
+        return ((P["w1"], P["b1"], None, None), (Pb["w2"], Pl["w2"] if self.split else None, P["b2"], None, None, None))
+
+    def _pack_c12(self) -> None:
+        c1, c2 = self._c12_weights()
+        self.c12_ops.conv12_pack(c1, c2, self.cfg.Runtime.obs_scale, sets=1)
 
     # ---------------------------------------------------------------- stream
     def _init_stream(self) -> None:
@@ -151,6 +168,8 @@ class GpuActorGroup:
     def _copy_params(self) -> None:
         self.p32.copy_(self.learner.p32)
         self._pbf_all.copy_(self.learner._pbf_all if self.split else self.learner.pbf)
+        if getattr(self, "c12_ops", None) is not None:
+            self._pack_c12()
 
     def reset_episodes(self) -> None:
         """Drop the partial n-step windows and start fresh episodes (actor restart)."""
@@ -212,17 +231,23 @@ class GpuActorGroup:
 
     def _policy_kernels(self) -> None:
         ops, P, Pb, Pl, E = self.ops, self.P, self.Pb, self.Pl, self.E
-        if self.split:   # fp32-class: the learner's split kernels (hi / lo planes throughout)
+        if self.c12_ops is not None:
+            c1, c2 = self._c12_weights()
+            self.c12_ops.conv12_fwd(self.replay.frames, self.slots, self.frames_buf, self.cfg.Runtime.obs_scale,
+                                    None, None, self.y2, self.y2_lo, c1, c2, rows_first=E, copy_n=0, pack_sets=0)
+        elif self.split:   # fp32-class: the learner's split kernels (hi / lo planes throughout)
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
                                self.cfg.Runtime.obs_scale, self.y1, w32=P["w1"], out_lo=self.y1_lo)
             ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, x_lo=self.y1_lo, w_lo=Pl["w2"], out_lo=self.y2_lo)
-            ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, x_lo=self.y2_lo, w_lo=Pl["w3"], out_lo=self.y3_lo)
-            ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h, x_lo=self.y3_lo.reshape(E, 3136),
-                       w_lo=Pl["wfc"], out_lo=self.h_lo)
         else:
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
                                self.cfg.Runtime.obs_scale, self.y1)
             ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2)
+        if self.split:
+            ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, x_lo=self.y2_lo, w_lo=Pl["w3"], out_lo=self.y3_lo)
+            ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h, x_lo=self.y3_lo.reshape(E, 3136),
+                       w_lo=Pl["wfc"], out_lo=self.h_lo)
+        else:
             ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3)
             ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h)
         heads = {k: P[k] for k in ("wv", "bv", "wa", "ba")}

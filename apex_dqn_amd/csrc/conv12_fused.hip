@@ -147,12 +147,20 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
   constexpr int NPF = (CF_FRAME + 1023) / 1024;   // pieces per frame (7)
   constexpr int NDMA = C * NPF;
   constexpr int NDW = (NDMA + 3) / 4;             // per wave (max)
-  auto image_slots = [&](int img, int* sl) { sload_slots<C>(d.slots + (int64_t)img * C, *reinterpret_cast<int(*)[4]>(sl)); };
-  auto issue_dma_piece = [&](const int* sl, int buf, int j) {
+  // (the slots travel as a vector VALUE: an int[4] whose element was picked by a runtime
+  // frame index became a scratch array, and each scratch load's vmcnt(0) waited for every
+  // DMA piece and y2 store in flight)
+  typedef int sl4_t __attribute__((ext_vector_type(4)));
+  auto image_slots = [&](int img) -> sl4_t {
+    int a[4];
+    sload_slots<C>(d.slots + (int64_t)img * C, a);
+    return (sl4_t){a[0], a[1], a[2], a[3]};
+  };
+  auto issue_dma_piece = [&](const sl4_t sl, int buf, int j) {
     const int k = wv + 4 * j;
     if (k < NDMA) {
       const int c = k / NPF, r = k - c * NPF;
-      const int s = c == 0 ? sl[0] : c == 1 ? sl[1] : c == 2 ? sl[2] : sl[3];
+      const int s = __builtin_amdgcn_readfirstlane(c == 0 ? sl.x : c == 1 ? sl.y : c == 2 ? sl.z : sl.w);
       const uint8_t* src = d.ring + (int64_t)s * CF_FRAME + r * 1024;
       const uint32_t dst = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(STG + buf * STGB) +
                            (uint32_t)(c * CF_FRAME + r * 1024);
@@ -160,8 +168,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
     }
   };
   auto issue_dma = [&](int img, int buf) {
-    int sl[4];
-    image_slots(img, sl);
+    const sl4_t sl = image_slots(img);
 #pragma unroll
     for (int j = 0; j < NDW; ++j) issue_dma_piece(sl, buf, j);
   };
@@ -266,8 +273,8 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
       cur_set = set;
       __syncthreads();
     }
-    int nsl[4] = {0, 0, 0, 0};                        // image i + 1's frame slots
-    if (more) image_slots(nxt, nsl);
+    sl4_t nsl = (sl4_t){0, 0, 0, 0};                  // image i + 1's frame slots
+    if (more) nsl = image_slots(nxt);
     // the image after next (read after this image's last barrier).  The fetch's return is
     // waited for here, before any DMA is in flight: ~0.5 us of one wave per image (the
     // compiler moves the value into a register of its choosing at once, so a later use
@@ -397,29 +404,28 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
       int tq = tid;
       asm volatile("" : "+v"(tq));
       const int cst = tq & 7;
-      // (bf16: 3200 chunks of one plane, 12.5 rounds)
-      constexpr int NR = SPLIT ? 25 : 13, NB = 5;
+      auto store_chunk = [&](const int r, const uint4 v) {
+        const int k = tq + CF_THREADS * r;
+        const int plane = k >= 3200 ? 1 : 0, kk = k - plane * 3200;
+        const int P = kk >> 3, c = cst ^ ((P >> 1) & 7);      // the chunk stored at slot cst
+        const int cls = P / 100, q = P - cls * 100, a = q / 10, b = q - a * 10;
+        const int ih = 2 * a + (cls >> 1), iw = 2 * b + (cls & 1);
+        *reinterpret_cast<uint4*>((plane ? d.y1_lo : d.y1) + (int64_t)img * 25600 + (ih * 20 + iw) * 64 + c * 8) = v;
+      };
+      // (bf16: 3200 chunks of one plane = 12 full rounds + half a round)
+      constexpr int NR = SPLIT ? 25 : 12, NB = SPLIT ? 5 : 4;
 #pragma unroll
       for (int r0 = 0; r0 < NR; r0 += NB) {
         uint4 v[NB];
 #pragma unroll
         for (int r = 0; r < NB; ++r)
-          if (r0 + r < NR && (SPLIT || r0 + r < 12 || tq < 128))
-            v[r] = *reinterpret_cast<const uint4*>(
-                Y1 + (r0 + r) * 4096 + tq * 16 +
-                ((r0 + r > 12 || (r0 + r == 12 && tq >= 128)) ? CF_PLANE - 51200 : 0));    // lo plane
+          v[r] = *reinterpret_cast<const uint4*>(
+              Y1 + (r0 + r) * 4096 + tq * 16 +
+              ((SPLIT && (r0 + r > 12 || (r0 + r == 12 && tq >= 128))) ? CF_PLANE - 51200 : 0));    // lo plane
 #pragma unroll
-        for (int r = 0; r < NB; ++r) {
-          if (r0 + r >= NR || (!SPLIT && r0 + r == 12 && tq >= 128)) continue;
-          const int k = tq + CF_THREADS * (r0 + r);
-          const int plane = k >= 3200 ? 1 : 0, kk = k - plane * 3200;
-          const int P = kk >> 3, c = cst ^ ((P >> 1) & 7);      // the chunk stored at slot cst
-          const int cls = P / 100, q = P - cls * 100, a = q / 10, b = q - a * 10;
-          const int ih = 2 * a + (cls >> 1), iw = 2 * b + (cls & 1);
-          *reinterpret_cast<uint4*>((plane ? d.y1_lo : d.y1) + (int64_t)img * 25600 + (ih * 20 + iw) * 64 + c * 8) =
-              v[r];
-        }
+        for (int r = 0; r < NB; ++r) store_chunk(r0 + r, v[r]);
       }
+      if (!SPLIT && tq < 128) store_chunk(12, *reinterpret_cast<const uint4*>(Y1 + 12 * 4096 + tq * 16));
     }
     PROBE(d.probe, 4, i, 2);
     // ================= conv2 over the resident hi / lo planes, weights streamed from L2
