@@ -466,8 +466,7 @@ def make_gpu_actor_group(cfg, learner, replay, num_envs: int, rank: int = 0, wor
     from ..envs.vector_envs import make_vec_env
     total = max(cfg.Actor.num_actors, num_envs * world)
     K = int(pipeline)
-    if K > 1 and num_envs % K == 0 and num_envs // K >= 1 and getattr(learner, "kind", "") not in ("graph", "impala") \
-            and learner.device.type == "cuda":
+    if K > 1 and num_envs % K == 0 and num_envs // K >= 1 and getattr(learner, "kind", "") not in ("graph", "impala"):
         h = num_envs // K
         eps_all = ladder_slice(cfg, num_envs, rank, world, total)
         groups = []

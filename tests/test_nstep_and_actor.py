@@ -97,3 +97,34 @@ def test_interleaved_epsilon_ladder_over_ranks():
     full = epsilon_ladder(W * E, cfg.Actor.epsilon, cfg.Actor.alpha)
     assert sorted(sum(sl, [])) == sorted(full)
     assert all(max(s) > 0.1 and min(s) < 0.01 for s in sl)
+
+
+def test_pipelined_actor_groups_cpu():
+    """Runtime.actor_pipeline's group wrapper (actors/gpu_actor.py PipelinedActorGroups) on
+    the CPU backend: two groups of E / 2 envs stepped in turn, consecutive env ids, the
+    rank's epsilon-ladder slices, one episode list, inserts from both groups."""
+    import torch
+    from apex_dqn_amd.actors.gpu_actor import PipelinedActorGroups, ladder_slice, make_gpu_actor_group
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    E = 8
+    cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 4, "name": "Synthetic"},
+                                "Actor": {"num_actors": E, "n_step_transition_batch_size": 8},
+                                "Learner": {"replay_sample_size": 16},
+                                "Runtime": {"use_graphs": False, "env_backend": "synthetic"}})
+    torch.manual_seed(0)
+    rp = GpuReplayShard(600, 600, 700, 4, device="cpu")
+    L = FusedNatureLearner(cfg, "cpu", rp)
+    grp = make_gpu_actor_group(cfg, L, rp, E, pipeline=2)
+    assert isinstance(grp, PipelinedActorGroups) and grp.E == E
+    assert [g.global_offset for g in grp.groups] == [0, E // 2]
+    np.testing.assert_allclose(grp.eps.numpy(), np.array(ladder_slice(cfg, E, 0, 1, E), dtype=np.float32))
+    ins = sum(grp.step() for _ in range(12))
+    assert all(g.t == 12 for g in grp.groups)
+    assert ins == grp.inserted > 0 and all(g.inserted > 0 for g in grp.groups)
+    assert all(g.episodes is grp.episodes for g in grp.groups)
+    assert len(set(grp.groups[0].builder.env_ids) & set(grp.groups[1].builder.env_ids)) == 0
+    grp.reset_episodes()
+    grp.step()
+    assert all(g.t == 13 for g in grp.groups)
