@@ -315,7 +315,9 @@ class PipelinedActorGroups:
     (every group's policy is launched after its previous env step), so the transitions are
     those of one group of K * E envs; the groups take consecutive env ids and slices of
     the rank's epsilon ladder.  Exposes the GpuActorGroup attributes the GPU loop and the
-    actor thread use (E, eps, episodes, inserted, ctr, step, reset_episodes)."""
+    actor thread use (E, eps, episodes, inserted, ctr, step, reset_episodes).  (The
+    reference runs one process per actor, ``main.py:50-54``; here a rank's actors are
+    batched rows of these groups.)"""
 
     def __init__(self, groups: List["GpuActorGroup"]):
         self.groups = list(groups)
