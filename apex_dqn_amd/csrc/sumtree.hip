@@ -704,7 +704,9 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   // block size APEX_OPT_THREADS (256 / 512 / 1024), grid capped at APEX_OPT_BLOCKS:
   // every block first sums the ~2.6 K clip-norm partials, so fewer, fatter blocks
   // cut those L2 reads (measured 512 x 512: 3543-3576 steps/s vs 3497-3520 at
-  // 256 x 2048)
+  // 256 x 2048; round 3, with the sample blocks and the operand stores: 256 x 512
+  // 2,540 / 4,175 vs 512 x 512 2,528 / 4,107 fp32 / bf16,
+  // profiles/r3_ab_optimizer_blocks_512_384_256.txt)
   static const int nt = [] {
     const char* e = getenv("APEX_OPT_THREADS");
     const int v = e ? atoi(e) : 512;
@@ -712,8 +714,8 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   }();
   static const int maxb = [] {
     const char* e = getenv("APEX_OPT_BLOCKS");
-    const int v = e ? atoi(e) : 512;
-    return v > 0 ? v : 512;
+    const int v = e ? atoi(e) : 256;
+    return v > 0 ? v : 256;
   }();
   int nb = (int)((n / 4 + nt - 1) / nt);
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
