@@ -20,6 +20,8 @@ import json
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 
 @dataclass
 class EnvConf:
@@ -113,6 +115,14 @@ class RuntimeConf:
                                     # "native" (parallel/rccl.py: own RCCL communicator + comm stream)
     force_dp: bool = False          # run the data-parallel step (collectives + sharded replay) even at
                                     # world 1 (needs an initialised process group; checks / overhead)
+    batch_scope: str = "global"     # DP: "global" = Learner.replay_sample_size is the batch of ONE update
+                                    # summed over all ranks (the reference's / Ape-X's update, learner.py:68:
+                                    # strong scaling; each rank computes the rows of the global draw that fall
+                                    # in its shard) | "per_rank" = every rank draws up to that many rows (a
+                                    # W-rank update averages up to W x the batch: weak scaling)
+    dp_batch_slack: float = 0.125   # global scope: rows a rank can hold beyond B/W, as a fraction of B/W (plus
+                                    # 2): the draw takes exactly B strata while no shard holds more than
+                                    # (rows - 2) / B of the total priority mass, fewer otherwise
     replica_check_every: int = 5000  # DP: learner steps between replica checksum checks (0 = off)
     step_timeout: float = 300.0     # GPU loop watchdog: seconds a queued learner chunk may take
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
@@ -200,6 +210,10 @@ class ApexConfig:
             raise ValueError("Runtime.actor_precision must be 'learner' or 'bf16'")
         if self.Runtime.is_normalise not in ("batch_max", "global_min"):
             raise ValueError("Runtime.is_normalise must be 'batch_max' or 'global_min'")
+        if self.Runtime.batch_scope not in ("global", "per_rank"):
+            raise ValueError("Runtime.batch_scope must be 'global' or 'per_rank'")
+        if not self.Runtime.dp_batch_slack >= 0.0:
+            raise ValueError("Runtime.dp_batch_slack must be >= 0")
         if self.Runtime.loss not in ("huber", "mse"):
             raise ValueError("Runtime.loss must be 'huber' or 'mse'")
         net = self.network
@@ -254,6 +268,28 @@ class ApexConfig:
         else:
             phys = int(soft * 1.25) + 1024
         return soft, max(phys, soft)
+
+    def dp_batch(self, world: int, dp: bool = True) -> Tuple[int, int]:
+        """(rows per rank, cap on the global batch M) of a learner update on ``world``
+        data-parallel ranks (``dp``: the sharded DP step runs, world > 1 or forced).
+
+        * no DP: (B, B);
+        * ``batch_scope = "per_rank"``: (B, W B) -- every rank draws up to B rows;
+        * ``batch_scope = "global"``: one update takes B = ``replay_sample_size`` draws
+          over all shards, as the reference's single learner (``learner.py:68``); rank r
+          holds ceil(B / W (1 + dp_batch_slack)) + 2 rows (B at W = 1), enough for its
+          share of the global draw while its shard carries at most (rows - 2) / B of
+          the total mass (replay/gpu_replay.py ``enable_sharding``)."""
+        B = int(self.Learner.replay_sample_size)
+        W = max(int(world), 1)
+        if not dp:
+            return B, B
+        if self.Runtime.batch_scope == "per_rank":
+            return B, W * B
+        if W == 1:
+            return B, B
+        rows = int(np.ceil(B / W * (1.0 + float(self.Runtime.dp_batch_slack)) - 1e-9)) + 2
+        return min(rows, B + 2), B
 
     def copy(self) -> "ApexConfig":
         return copy.deepcopy(self)

@@ -304,10 +304,6 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
       float ev[2][4];
       uint32_t eh[2][2], el[2][2];
       auto epi_piece = [&](int k, int j, const f32x4* acc, const f32x4* accl) {
-#ifdef CF_EXP_NOEPI
-        if (k == 0 && acc[0][0] + accl[1][3] == 1234.5f) Y1[tid] = 1;
-        return;
-#endif
         const int nt = k >> 2, part = k & 3;
         if (part < 2) {
 #pragma unroll
@@ -331,11 +327,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
         }
       };
       auto cvt = [&](const uint2 v) {
-#ifdef CF_EXP_NOPERM
-        return __builtin_bit_cast(f16x8, make_uint4(v.x, v.y, v.x, v.y));
-#else
         return __builtin_bit_cast(f16x8, u8x8_to_f16off(v.x, v.y));
-#endif
       };
       // tile j's 2C K steps (4 MFMAs each); step s2 + 1's fragment conversion and 8 / 2C
       // epilogue pieces of tile j - 1 (pj >= 0) go between them, one scheduling region

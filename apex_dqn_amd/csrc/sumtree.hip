@@ -283,6 +283,8 @@ struct SampleArgs {
   int shard_rank, shard_world;
   uint64_t shard_seed;         // common to all ranks (the local `seed` is per shard)
   float* out_wscale;           // the batch's W B / M factor (1 unsharded), for the IS batch-max; or null
+  int64_t mcap;                // sharded: cap on the global batch M (W B: per-rank batches; the
+                               // configured global batch: Runtime.batch_scope = "global")
 };
 
 // block `bid` of 4 waves: samples 4 bid .. 4 bid + 3
@@ -325,8 +327,10 @@ __device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
     const double c1 = c0 + Tr;
     int64_t M = 0;
     if (tmax > 0.0) {
-      const double mb = floor((double)(B - 2) * sum / tmax);
-      M = (int64_t)fmin((double)W * (double)B, fmax(mb, 0.0));
+      // one shard holds every stratum: B rows suffice; otherwise an interval of mass T
+      // catches at most floor(T M / sum) + 2 strata
+      const double mb = W == 1 ? (double)B : floor((double)(B - 2) * sum / tmax);
+      M = (int64_t)fmin((double)S.mcap, fmax(mb, 0.0));
     }
     const uint64_t cc = ctr[0];
     double ul = 0.0;
@@ -336,7 +340,8 @@ __device__ __forceinline__ void tree_sample_body(const SampleArgs& S, int bid) {
       if (((double)j0 + (double)apex_uniform(S.shard_seed, cc, (uint64_t)j0)) * delta < c0) ++j0;
       const int64_t j = j0 + b;
       const double uj = ((double)j + (double)apex_uniform(S.shard_seed, cc, (uint64_t)j)) * delta;
-      valid = j < M && uj < c1;
+      // (the last interval ends at the total: strata rounded past it are still its own)
+      valid = j < M && (r == W - 1 || uj < c1);
       ul = uj - c0;
       wscale = (float)((double)W * (double)B / (double)M);
     } else {
@@ -603,14 +608,16 @@ APEX_EXPORT int apex_tree_sample(TreeDesc t, RecordDesc r, int B, uint64_t seed,
                                  int32_t* out_gen, int32_t* out_obs, int32_t* out_nxt, int32_t* out_act,
                                  float* out_rew, float* out_gam, int32_t* out_nxt2, const double* shard_stats,
                                  int shard_rank, int shard_world, uint64_t shard_seed, float* out_wscale,
-                                 hipStream_t st) {
+                                 int64_t mcap, hipStream_t st) {
   if (B <= 0) return 0;
+  if (mcap <= 0) mcap = (int64_t)shard_world * B;
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   const int waves_per_block = 4;
   tree_sample_kernel<<<blocks_for(B, waves_per_block), 64 * waves_per_block, 0, st>>>(
       SampleArgs{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt, out_act,
-                 out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed, out_wscale});
+                 out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed, out_wscale,
+                 mcap});
   APEX_CHECK_LAUNCH();
 }
 
@@ -651,7 +658,7 @@ APEX_EXPORT int apex_fill16(void* p, int64_t n, int nt, hipStream_t st) {
   APEX_CHECK_LAUNCH();
 }
 
-APEX_EXPORT int apex_abi_version() { return 2; }
+APEX_EXPORT int apex_abi_version() { return 3; }
 
 // 1 if this library was built with -DAPEX_DEBUG_BOUNDS
 APEX_EXPORT int apex_debug_bounds_enabled() {
@@ -695,28 +702,18 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int64_t* out_idx, float* out_w, int32_t* out_gen, int32_t* out_obs,
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
-                                    uint64_t shard_seed, float* out_wscale, bf16_t* pb_lo, const double* wnorm,
-                                    int wn, int wstride, CfFragOut fo, hipStream_t st) {
+                                    uint64_t shard_seed, float* out_wscale, int64_t mcap, bf16_t* pb_lo,
+                                    const double* wnorm, int wn, int wstride, CfFragOut fo, hipStream_t st) {
+  if (mcap <= 0) mcap = (int64_t)shard_world * B;
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
   if ((((uintptr_t)pb | (uintptr_t)pb_lo) & 7) || B < 1) return (int)hipErrorInvalidValue;
-  // block size APEX_OPT_THREADS (256 / 512 / 1024), grid capped at APEX_OPT_BLOCKS:
-  // every block first sums the ~2.6 K clip-norm partials, so fewer, fatter blocks
-  // cut those L2 reads (measured 512 x 512: 3543-3576 steps/s vs 3497-3520 at
-  // 256 x 2048; round 3, with the sample blocks and the operand stores: 256 x 512
-  // 2,540 / 4,175 vs 512 x 512 2,528 / 4,107 fp32 / bf16,
-  // profiles/r3_ab_optimizer_blocks_512_384_256.txt)
-  static const int nt = [] {
-    const char* e = getenv("APEX_OPT_THREADS");
-    const int v = e ? atoi(e) : 512;
-    return (v == 512 || v == 1024) ? v : 256;
-  }();
-  static const int maxb = [] {
-    const char* e = getenv("APEX_OPT_BLOCKS");
-    const int v = e ? atoi(e) : 256;
-    return v > 0 ? v : 256;
-  }();
+  // 512-thread blocks, grid capped at 256: every block first sums the ~2.6 K clip-norm
+  // partials, so fewer, fatter blocks cut those L2 reads (256 x 512 measured 2,540 / 4,175
+  // fp32 / bf16 steps/s vs 2,528 / 4,107 at 512 x 512 and 3497-3520 vs 3543-3576 at
+  // 256 x 2048 before; profiles/r3_ab_optimizer_blocks_512_384_256.txt)
+  constexpr int nt = 512, maxb = 256;
   int nb = (int)((n / 4 + nt - 1) / nt);
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
   const int nsb = blocks_for(B, nt / 64);
@@ -730,10 +727,8 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                       wnorm, wn, wstride, fo};
   const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
                       out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed,
-                      out_wscale};
-  if (nt == 1024) rmsprop_sample_kernel<1024><<<nb + nsb, 1024, 0, st>>>(ra, sa, nsb);
-  else if (nt == 512) rmsprop_sample_kernel<512><<<nb + nsb, 512, 0, st>>>(ra, sa, nsb);
-  else rmsprop_sample_kernel<256><<<nb + nsb, 256, 0, st>>>(ra, sa, nsb);
+                      out_wscale, mcap};
+  rmsprop_sample_kernel<nt><<<nb + nsb, nt, 0, st>>>(ra, sa, nsb);
   APEX_CHECK_LAUNCH();
 }
 

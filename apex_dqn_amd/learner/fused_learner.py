@@ -36,8 +36,6 @@ The step is captured once and replayed as a HIP graph (``use_graphs``).
 """
 from __future__ import annotations
 
-import os
-
 from typing import Any, Dict, Optional
 
 import torch
@@ -47,17 +45,34 @@ from ..models.dueling import DuellingDQN
 from ..models.flat_params import (FlatLayout, flat_to_reference_state, nature_segments,
                                   reference_state_to_flat)
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
+from ..ops.switches import SW
 from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
 from .is_norm import IsNormMixin
 
 
-def _enable_sharding(replay, comm, rt) -> None:
-    """Turn the rank-local replay into one shard of the global replay (idempotent)."""
+def _enable_sharding(replay, comm, rt, mcap: int = 0) -> None:
+    """Turn the rank-local replay into one shard of the global replay (idempotent;
+    ``mcap``: the cap on a draw's global batch, ``ApexConfig.dp_batch``)."""
     if not replay.sharded:
         replay.enable_sharding(comm.rank, comm.world_size, shard_seed=(int(rt.seed) << 20) ^ 0x5EED,
-                               group=comm.group)
+                               group=comm.group, mcap=mcap)
+    replay.shard_mcap = int(mcap)
     if not rt.use_is_weights:
         replay.beta = 0.0
+
+
+def dp_layout(cfg: ApexConfig, comm, batch_size: Optional[int] = None, allow_force: bool = True):
+    """(world, dp, rows per rank, global-batch cap) of a learner on ``comm``: the DP
+    step runs at world > 1 or with ``Runtime.force_dp``; ``Runtime.batch_scope`` decides
+    whether ``replay_sample_size`` is the update's global batch or every rank's
+    (``ApexConfig.dp_batch``).  ``batch_size`` overrides the rows per rank."""
+    world = comm.world_size if comm is not None else 1
+    dp = world > 1 or (allow_force and bool(cfg.Runtime.force_dp) and comm is not None)
+    rows, mcap = cfg.dp_batch(world, dp)
+    if batch_size:
+        rows = int(batch_size)
+        mcap = mcap if cfg.Runtime.batch_scope == "global" else world * rows
+    return world, dp, rows, mcap
 
 
 class FusedNatureLearner(IsNormMixin):
@@ -72,7 +87,9 @@ class FusedNatureLearner(IsNormMixin):
         self.comm = comm
         self.C = cfg.frame_stack
         self.A = int(cfg.env_conf.action_dim)
-        self.B = int(batch_size or cfg.Learner.replay_sample_size)
+        # B = the rows this rank computes: replay_sample_size, or with a global-batch DP
+        # step (Runtime.batch_scope) its share of the global draw plus slack (dp_layout)
+        self.world, self._dp, self.B, self.mcap = dp_layout(cfg, comm, batch_size)
         if self.rt.dtype not in ("fp32", "bf16"):
             raise ValueError("Runtime.dtype must be fp32 or bf16")
         self.precision = self.rt.dtype
@@ -94,10 +111,9 @@ class FusedNatureLearner(IsNormMixin):
                                             or (cuda and self.precision == "bf16")) else torch.float32
         # conv1 -> conv2 forward in one launch, y1 kept in LDS (csrc/conv12_fused.hip): the
         # split kernel in fp32 mode, its one-plane variant for the bf16 learner
-        # (APEX_CONV12_BF16=0: the bf16 learner runs the two image-resident kernels)
+        # (SW.conv12_bf16 = False: the bf16 learner runs the two image-resident kernels)
         # (the torch backend emulates the split kernel's contract: ops.conv12_fwd)
-        self._c12 = self.split or (backend == "hip" and self.ops._conv12_native()
-                                   and os.environ.get("APEX_CONV12_BF16", "1") != "0")
+        self._c12 = self.split or (backend == "hip" and self.ops._conv12_native() and SW.conv12_bf16)
         d = self.device
         self.layout = FlatLayout(nature_segments(self.C, self.A, 64))
         n = self.layout.numel
@@ -130,11 +146,9 @@ class FusedNatureLearner(IsNormMixin):
         self._tgt_packed = False
         self.sync_target()
         self.num_q_updates = 0
-        self.world = comm.world_size if comm is not None else 1
-        # the data-parallel step (collectives, sharded replay); Runtime.force_dp runs it
-        # at world 1 too (an initialised process group of one rank: RCCL capture checks
-        # and the segmented-step overhead on a single GPU)
-        self._dp = self.world > 1 or (bool(self.rt.force_dp) and comm is not None)
+        # self._dp: the data-parallel step (collectives, sharded replay); Runtime.force_dp
+        # runs it at world 1 too (an initialised process group of one rank: RCCL capture
+        # checks and the segmented-step overhead on a single GPU)
         # image work queues in the persistent kernels (ops/conv.py Workspace.work_queue):
         # only where RCCL's kernels may hold CUs during the step -- world > 1 (a forced-DP
         # step on one rank has no peer traffic beside it: static order)
@@ -175,7 +189,7 @@ class FusedNatureLearner(IsNormMixin):
             from ..parallel.rccl import make_collectives
             backend = self.rt.comm_backend if cuda else "torch"
             self.coll = make_collectives(comm, backend, self.device)
-            _enable_sharding(replay, comm, self.rt)
+            _enable_sharding(replay, comm, self.rt, self.mcap)
             replay.gather_shard_stats(coll=self.coll)
         # DP step as ONE captured graph including the RCCL collectives (backend nccl);
         # gloo (CPU tests, one-GPU rehearsals) cannot be captured: eager DP steps
@@ -183,8 +197,8 @@ class FusedNatureLearner(IsNormMixin):
         self._ordered_coll = self._dp and cuda and (self.coll.name == "native" or self._backend_name() == "nccl")
         self._fork_stream = torch.cuda.Stream(self.device) if (self._dp and cuda) else None
         # the fc layer's split-K epilogue runs inside the head launch (ops.fc_fwd defer_head;
-        # APEX_FC_EPI_IN_HEAD=0 keeps the separate epilogue launch, the A/B of scripts/ab.sh)
-        self._defer_fc_epilogue = os.environ.get("APEX_FC_EPI_IN_HEAD", "1") != "0"
+        # SW.fc_epi_in_head = False keeps the separate epilogue launch)
+        self._defer_fc_epilogue = SW.fc_epi_in_head
         # next-batch pre-sampling: the batch of step t+1 is drawn at the end of step t,
         # after the priority write-back -- on the HIP backend inside the optimizer launch
         # (its first blocks run the sampler: csrc/sumtree.hip rmsprop_sample_kernel), so
@@ -204,10 +218,10 @@ class FusedNatureLearner(IsNormMixin):
         sample launch stores the updated w1 / w2 in the forward's fragment order
         (csrc/cf_pack.h cf_frag_store; elementwise, no hand-off between workgroups), so the
         step runs no pack launch for the online set (forward_all pack_sets).  Host-side
-        weight changes repack eagerly (_online_changed).  APEX_OPT_FRAGS=0: pack launch."""
+        weight changes repack eagerly (_online_changed).  SW.opt_frags = False: pack launch."""
         self._frag_out = None
         ops = self.ops
-        if os.environ.get("APEX_OPT_FRAGS", "1") == "0":
+        if not SW.opt_frags:
             return
         if not (self._c12 and self._presample and getattr(self.replay, "use_hip", False)
                 and getattr(ops, "_conv12_native", lambda: False)()):

@@ -32,7 +32,7 @@ from ..config import ApexConfig
 from ..models.dueling import build_network
 from ..ops.fused_ops import HipBackend, TorchBackend
 from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
-from .fused_learner import _enable_sharding
+from .fused_learner import _enable_sharding, dp_layout
 from .losses import ddqn_loss
 
 
@@ -60,10 +60,9 @@ class GraphLearner:
         self.device = torch.device(device)
         self.replay = replay
         self.comm = comm
-        self.world = comm.world_size if comm is not None else 1
+        self.world, _, self.B, self.mcap = dp_layout(cfg, comm, batch_size, allow_force=False)
         self.C = cfg.frame_stack
         self.A = int(cfg.env_conf.action_dim)
-        self.B = int(batch_size or cfg.Learner.replay_sample_size)
         d = self.device
         self.Q = build_network(cfg.network, cfg.env_conf.state_shape, self.A, obs_scale=self.rt.obs_scale).to(d)
         self.p32 = _flatten_module(self.Q, d)
@@ -97,7 +96,7 @@ class GraphLearner:
         self._is_bmax = bool(self.rt.use_is_weights) and self.rt.is_normalise == "batch_max"
         self.wmax = torch.zeros(1, dtype=torch.float64, device=d)
         if self.world > 1:
-            _enable_sharding(replay, comm, self.rt)
+            _enable_sharding(replay, comm, self.rt, self.mcap)
             replay.gather_shard_stats()
         self.num_q_updates = 0
         self._graphs: Optional[List[torch.cuda.CUDAGraph]] = None

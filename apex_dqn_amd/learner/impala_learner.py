@@ -39,7 +39,7 @@ from ..models.flat_params import FlatLayout
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
 from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
-from .fused_learner import _enable_sharding
+from .fused_learner import _enable_sharding, dp_layout
 from .is_norm import IsNormMixin
 
 CH = (16, 32, 32)
@@ -75,12 +75,11 @@ class FusedImpalaLearner(IsNormMixin):
         self.device = torch.device(device)
         self.replay = replay
         self.comm = comm
-        self.world = comm.world_size if comm is not None else 1
+        self.world, _, self.B, self.mcap = dp_layout(cfg, comm, batch_size, allow_force=False)
         self.C = cfg.frame_stack
         if self.C != 4 or tuple(cfg.env_conf.state_shape[1:]) != (84, 84):
             raise ValueError("the IMPALA kernels are built for 4 x 84 x 84 inputs")
         self.A = int(cfg.env_conf.action_dim)
-        self.B = int(batch_size or cfg.Learner.replay_sample_size)
         if backend is None:
             backend = "hip" if (self.device.type == "cuda" and self.rt.use_hip_kernels) else "torch"
         on_gpu = backend == "hip"
@@ -173,7 +172,7 @@ class FusedImpalaLearner(IsNormMixin):
         self._dp = self.world > 1
         self._init_is_norm()
         if self.world > 1:
-            _enable_sharding(replay, comm, self.rt)
+            _enable_sharding(replay, comm, self.rt, self.mcap)
             replay.gather_shard_stats()
         ls = cfg.Learner.load_saved_state
         if ls:

@@ -122,13 +122,14 @@ class Conv1S2DDesc(ctypes.Structure):
 
 _SIGS = {
     "apex_abi_version": ([], c_i),
+    "apex_build_id": ([], ctypes.c_char_p),
     "apex_fill16": ([c_p, c_i64, c_i, c_p], c_i),
     "apex_tree_update": ([TreeDesc, c_p, c_p, c_i, c_i, c_f, c_f, c_p, c_p, c_i, c_p, c_p], c_i),
     "apex_tree_zero_range": ([TreeDesc, c_i64, c_i64, c_p], c_i),
     "apex_replay_insert": ([TreeDesc, RecordDesc, c_i64, c_i, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_f, c_p],
                            c_i),
     "apex_tree_sample": ([TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                          c_p, c_p, c_p, c_i, c_i, c_u64, c_p, c_p], c_i),
+                          c_p, c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p], c_i),
     "apex_tree_rebuild": ([TreeDesc, c_p], c_i),
     "apex_gather_frames": ([c_p, c_p, c_i, c_i64, c_i64, c_p, c_p], c_i),
     "apex_debug_bounds_enabled": ([], c_i),
@@ -146,7 +147,7 @@ _SIGS = {
                         c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, IsNorm, c_p], c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p, c_i, c_i, c_u64, c_p, c_p, c_p, c_i, c_i, CfFragOut, c_p], c_i),
+                             c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut, c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
                               c_p, c_p, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,
@@ -177,17 +178,23 @@ def _declare(lib: ctypes.CDLL) -> None:
     conv_sigs.declare(lib)
 
 
+ABI_VERSION = 3      # csrc/sumtree.hip apex_abi_version(): the launchers' argument lists
+
+
 def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:
+    """Load the kernel library, after checking the build id compiled into it against
+    the tree (ops/build.py: sources, headers, flags, compiler): a stale library is
+    rebuilt first (``build_if_missing``) or refused -- never run."""
     global _LIB, _LOAD_ERROR
     if _LIB is not None:
         return _LIB
     debug = debug_bounds_requested()
-    path = _build.KERNEL_DEBUG_LIB if debug else _build.KERNEL_LIB
     try:
-        if build_if_missing and not os.path.exists(path):
-            _build.build_kernels(debug=debug)
+        path = _build.ensure_current("kernels_debug" if debug else "kernels", allow_build=build_if_missing)
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
         _declare(lib)
+        if lib.apex_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"{path}: ABI {lib.apex_abi_version()} != {ABI_VERSION}")
         _LIB = lib
     except Exception as e:  # pragma: no cover - depends on toolchain
         _LOAD_ERROR = repr(e)

@@ -8,11 +8,11 @@ from __future__ import annotations
 
 from typing import Dict, Optional, Tuple
 
-import os as _os
 
 import torch
 
 from . import _lib
+from .switches import SW
 
 
 class Workspace:
@@ -30,23 +30,25 @@ class Workspace:
     # device-side image work queues in the persistent kernels (csrc/mfma_common.h wq_next):
     # off by default (static order: each queue item costs a contended device-scope
     # atomic); the data-parallel learner turns them on, where RCCL's kernels hold CUs
-    # during the conv backward.  APEX_WORK_QUEUE=1 / 0 forces them on / off.
+    # during the conv backward.  SW.work_queue = "on" / "off" forces them on / off.
     work_queue = False
 
     def wq(self, key, device, overlapped: bool = True) -> int:
         """Counter pair of a work queue, or 0 (null: static order) when queues are off.
         ``overlapped``: the launch can run beside the step's collectives (the conv
         backward); the forward never does (it follows the optimizer's join), so it keeps
-        the static order unless APEX_WORK_QUEUE=1."""
-        env = _os.environ.get("APEX_WORK_QUEUE", "")
-        on = (env == "1") or (env != "0" and self.work_queue and overlapped)
+        the static order unless SW.work_queue = "on"."""
+        mode = SW.work_queue
+        on = mode == "on" or (mode != "off" and self.work_queue and overlapped)
         # one never-reset 64-bit counter per (call site, items, grid): a launch consumes
         # exactly items + grid values (csrc/mfma_common.h wq_fetch)
         return self.get_zeroed(key, 1, device, dtype=torch.int64).data_ptr() if on else 0
 
     def get_zeroed(self, key, numel: int, device, dtype=torch.int32) -> torch.Tensor:
-        """A buffer zeroed when first made (work-queue counters: the kernels leave them
-        zero again at their end)."""
+        """A buffer zeroed once, when first made, and never reset: a work-queue counter
+        (csrc/mfma_common.h wq_fetch) is a 64-bit count that every launch advances by
+        exactly items + grid and reads modulo that, so it must serve ONE (call site,
+        items, grid) on one stream -- resetting it would break the modular item map."""
         k = (key, numel, str(device), dtype)
         t = self.bufs.get(k)
         if t is None:
@@ -179,15 +181,11 @@ def c2f_wfrag_fwd_buffer(device) -> torch.Tensor:
 
 
 # conv2 (20x20x64 -> 9x9x64, 4x4/s2) on the image-resident kernel (csrc/conv2_img.hip);
-# APEX_CONV2_IMG=0 selects the generic implicit GEMM
-CONV2_IMG = _os.environ.get("APEX_CONV2_IMG", "1") != "0"
+# (SW.conv2_img = False selects the generic implicit GEMM)
 
 
 # split conv2 forward: the launcher packs both weight sets into per-lane fragment order
-# first (pack_c2f_wfrag_kernel; 76.2 -> 71.0 us at 1536 images including the pack,
-# profiles/r2_split_conv2_packed_fwd.jsonl).  False = in-kernel gathers (the A/B of
-# scripts/bench_split_conv2.py; APEX_C2F_PACK=0 for scripts/ab.sh).
-C2F_PACK = _os.environ.get("APEX_C2F_PACK", "1") != "0"
+# first (SW.c2f_pack; False = in-kernel gathers, the A/B of scripts/bench_split_conv2.py)
 
 
 def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: torch.Tensor,
@@ -210,7 +208,7 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
         for t in (x_lo, w_lo, out_lo) + ((w2_lo,) if w2 is not None else ()):
             assert t is not None and t.is_contiguous() and t.dtype == torch.bfloat16
         d.x_lo, d.w_lo, d.w2_lo, d.y_lo = x_lo.data_ptr(), w_lo.data_ptr(), _lib.ptr(w2_lo), out_lo.data_ptr()
-        if C2F_PACK or packed:
+        if SW.c2f_pack or packed:
             d.wfrag = c2f_wfrag_fwd_buffer(x.device).data_ptr()
             d.wfrag_ready = int(packed)
     elif packed:   # bf16: fragments packed by this step's conv1 launch
@@ -220,8 +218,7 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
 
 
 # fp32 learner: conv1 -> conv2 fused with y1 kept in LDS (csrc/conv12_fused.hip);
-# APEX_CONV12_FUSED=0 runs the two image-resident kernels
-CONV12_FUSED = _os.environ.get("APEX_CONV12_FUSED", "1") != "0"
+# (SW.conv12_fused = False runs the two image-resident kernels)
 CF_W1FRAG_BYTES = 2 * 2 * 2 * 2 * 4 * 2 * 64 * 16
 
 
@@ -319,7 +316,7 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
     Cout, KH, KW, _ = w.shape
     OH, OW = out.shape[1], out.shape[2]
     split = x_lo is not None
-    if CONV2_IMG and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
+    if SW.conv2_img and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
             hasattr(lib, "apex_conv2_img_fwd"):
         conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo, out_lo=out_lo,
                       packed=packed)
@@ -419,9 +416,6 @@ def dense_dgrad(lib, dh: torch.Tensor, w: torch.Tensor, out: torch.Tensor, mask:
     _launch_fwd(lib, d)
 
 
-CONV3_DGRAD_IMG = _os.environ.get("APEX_CONV3_DGRAD_IMG", "1") != "0"
-
-
 def conv3_dgrad_img(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out: torch.Tensor,
                     grid: int = 0) -> None:
     """conv3 data gradient on the image-resident kernel (csrc/conv2_img.hip): six waves
@@ -442,16 +436,13 @@ def conv3_dgrad(lib, dy: torch.Tensor, w3: torch.Tensor, mask: torch.Tensor, out
     K-major from the OHWI weight (co rows, ci columns)."""
     N = dy.shape[0]
     assert w3.shape == (64, 3, 3, 64)
-    if CONV3_DGRAD_IMG and dy_lo is None and hasattr(lib, "apex_conv3_dgrad_img"):
+    if SW.conv3_dgrad_img and dy_lo is None and hasattr(lib, "apex_conv3_dgrad_img"):
         conv3_dgrad_img(lib, dy, w3, mask, out)
         return
     d = _conv_desc(x=dy.data_ptr(), w=w3.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=7, W=7,
                    Cin=64, OH=9, OW=9, Cout=64, KH=3, KW=3, stride=1, pad=2, mode=1, K=576,
                    bt=1, ldb=576, koff=_KOFF3, **_lo(dy_lo, w_lo, None, out_lo))
     _launch_fwd(lib, d)
-
-
-CONV2_DGRAD_IMG = _os.environ.get("APEX_CONV2_DGRAD_IMG", "1") != "0"
 
 
 def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out: torch.Tensor,
@@ -487,7 +478,7 @@ def conv2_dgrad(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor, out
     K-major from the OHWI tensor per class."""
     N = dy.shape[0]
     assert w2.shape == (64, 4, 4, 64)
-    if CONV2_DGRAD_IMG and hasattr(lib, "apex_conv2_dgrad_img"):
+    if SW.conv2_dgrad_img and hasattr(lib, "apex_conv2_dgrad_img"):
         conv2_dgrad_img(lib, dy, w2, mask, out, dy_lo=dy_lo, w_lo=w_lo, out_lo=out_lo, ws=ws, packed=packed)
         return
     d = _conv_desc(x=dy.data_ptr(), w=w2.data_ptr(), y=out.data_ptr(), mask=mask.data_ptr(), N=N, H=9, W=9,
@@ -510,7 +501,6 @@ def _wg_desc(**kw) -> "_lib.WgradDesc":
     return d
 
 
-_WG_ROWS_ENV = {3: int(_os.environ.get("APEX_WG_ROWS3", "0")), 4: int(_os.environ.get("APEX_WG_ROWS2", "0"))}
 _WG_ROWS = 64       # reduction rows per kernel step (csrc/conv_mfma.hip WG_ROWS)
 _WG_TBL = 1024      # per-block row-offset table entries (WG_TBL)
 
@@ -530,11 +520,11 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     ``target_rows``: reduction rows per split-K block (0 = tuned default: fewer
     rows for the small 3x3 layer, whose 9 output tiles need more splits (384: two
     68 KB blocks per CU); 704 for conv2 keeps its 4 x 59 blocks (84 KB LDS each,
-    one per CU) in a single wave on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  APEX_WG_ROWS3 / APEX_WG_ROWS2
+    one per CU) in a single wave on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  SW.wg_rows3 / SW.wg_rows2
     override for sweeps."""
     N, OH, OW, Co = dy.shape
     if target_rows <= 0:
-        target_rows = _WG_ROWS_ENV.get(KH) or (384 if KH == 3 else 704)
+        target_rows = {3: SW.wg_rows3, 4: SW.wg_rows2}.get(KH) or (384 if KH == 3 else 704)
     _, H, W, Cin = x.shape
     Kc = KH * KH * Cin
     Mred = N * OH * OW

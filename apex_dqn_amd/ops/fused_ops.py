@@ -25,6 +25,7 @@ import torch
 from . import _lib
 from . import conv as C
 from . import reference as R
+from .switches import SW
 
 
 def join(hi: torch.Tensor, lo: Optional[torch.Tensor]) -> torch.Tensor:
@@ -316,14 +317,14 @@ class HipBackend(TorchBackend):
         if not self.native_conv:
             return super().conv1_fwd_ring(ring, slots, frames_buf, w, b, scale, out, w2, b2, rows_first, w32, w2_32,
                                           out_lo)
-        c2f = c2f if (c2f is not None and C.C2F_PACK) else None
+        c2f = c2f if (c2f is not None and SW.c2f_pack) else None
         C.conv1_s2d_fwd(self.lib, self.ws, ring, slots, w, b, scale, out, w2, b2, rows_first, w32=w32, w2_32=w2_32,
                         out_lo=out_lo, c2f=c2f)
         if c2f is not None:   # this step's split conv2 forward finds its weights packed
             self._c2f_packed = tuple(_lib.ptr(t) for t in c2f)
 
     def _conv12_native(self) -> bool:
-        return self.native_conv and C.CONV12_FUSED and hasattr(self.lib, "apex_conv12_fused_fwd")
+        return self.native_conv and SW.conv12_fused and hasattr(self.lib, "apex_conv12_fused_fwd")
 
     def conv12_pack(self, c1, c2, scale, sets=2):
         if not self._conv12_native():

@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from .switches import SW
 
 c_p, c_i, c_i64, c_f = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 
@@ -154,24 +155,22 @@ class ConvSpec:
 
 # weight-gradient launch shape: workgroups per conv (images are split into groups, one
 # fp32 partial per workgroup and band) and the cap on the partial slab (floats)
-import os as _os
-WGRAD_TUNING = {"target_wgs": int(_os.environ.get("APEX_IMPALA_WG_TARGET", "512")),
-                "slab_cap": int(_os.environ.get("APEX_IMPALA_SLAB_CAP", str(2 << 20)))}
+WGRAD_TUNING = {"target_wgs": SW.impala_wg_target, "slab_cap": SW.impala_slab_cap}
 
 
 # fused residual block: rows per workgroup band per (channels, size); 0 = kernel default
-RESBLOCK_BANDS = {(16, 42): int(_os.environ.get("APEX_RESBLOCK_R16", "14"))}   # swept: 21 777, 14 786, 11 778
+RESBLOCK_BANDS = {(16, 42): SW.resblock_r16}   # swept: 21 777, 14 786, 11 778
 
 
 def _split_bands() -> Dict[tuple, int]:
     """Row bands of the split kernels (csrc/impala_split.hip: 0 = the kernel default):
-    resblock (C, HW) and sconv (cin, cout, HW, pool); APEX_ISPLIT_BANDS="key=R,..." with
-    keys like rb16x42 / sc16x16x42p0 overrides (the sweep of scripts/experiments)."""
+    resblock (C, HW) and sconv (cin, cout, HW, pool); SW.isplit_bands = "key=R;..." with
+    keys like rb16x42 / sc16x16x42p0 overrides (APEX_SWITCHES sweeps)."""
     # defaults from the band sweep (profiles/r3_impala_split_band_sweep.txt: each +0.6 to
     # +2.4 % on the fp32 IMPALA step; 2 workgroups per CU where the 16-channel shapes fit)
     out: Dict[tuple, int] = {("rb", 16, 42): 7, ("sc", 16, 16, 42, 0): 21, ("sc", 32, 16, 42, 0): 11,
                              ("sc", 16, 32, 42, 1): 6}
-    for item in _os.environ.get("APEX_ISPLIT_BANDS", "").split(","):
+    for item in SW.isplit_bands.split(";"):
         if "=" not in item:
             continue
         k, v = item.split("=")

@@ -1,0 +1,90 @@
+"""Kernel-path switches: ONE registry.
+
+Every alternative kernel path that survived as an A/B knob lives here with its
+measured winner as the default (the measurements are cited per field; the history is
+in docs/PERF_NOTES.md).  Production code reads ``SW.<name>``; tests flip a path with
+``monkeypatch.setattr(SW, name, value)``; experiments override from the environment
+with ONE variable::
+
+    APEX_SWITCHES="conv2_img=0,wg_rows3=384" python bench.py
+
+``bench.py`` prints every non-default value in its JSON (``switches``), so a number
+measured off the defaults is labelled as such.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass
+from typing import Any, Dict
+
+
+@dataclass
+class Switches:
+    # conv2 forward on the image-resident kernel (csrc/conv2_img.hip) instead of the generic
+    # implicit GEMM (bf16 learner without the fused conv1 -> conv2 kernel, actors)
+    conv2_img: bool = True
+    # split conv2 forward: weights packed into per-lane fragment order by the launcher
+    # (76.2 -> 71.0 us at 1536 images, profiles/r2_split_conv2_packed_fwd.jsonl)
+    c2f_pack: bool = True
+    # conv1 -> conv2 forward fused with y1 in LDS (csrc/conv12_fused.hip), split mode
+    conv12_fused: bool = True
+    # the fused forward's one-plane variant for the bf16 learner (4,105 vs 3,790 steps/s,
+    # profiles/r3_ab_conv12_bf16_fused_4105_vs_3790.txt)
+    conv12_bf16: bool = True
+    # image-resident conv3 / conv2 data gradients (csrc/conv2_img.hip)
+    conv3_dgrad_img: bool = True
+    conv2_dgrad_img: bool = True
+    # the optimizer + sample launch stores the fused forward's online weight fragments
+    # (+0.5-1 %, profiles/r3_ab_optimizer_frag_stores_*.txt)
+    opt_frags: bool = True
+    # the fc layer's split-K epilogue runs inside the DDQN head launch
+    fc_epi_in_head: bool = True
+    # device-side image work queues in the persistent kernels: "auto" = only where RCCL's
+    # kernels may hold CUs (the DP conv backward at world > 1), "on" / "off" force them
+    work_queue: str = "auto"
+    # split-K reduction rows per workgroup of the conv3 / conv2 weight gradients (0: the
+    # tuned defaults in ops/conv.py)
+    wg_rows3: int = 0
+    wg_rows2: int = 0
+    # IMPALA weight gradients: workgroups per conv and the partial-slab cap (floats)
+    impala_wg_target: int = 512
+    impala_slab_cap: int = 2 << 20
+    # IMPALA bf16 fused residual block rows per band at 16 ch x 42 (swept: 21 777, 14 786, 11 778)
+    resblock_r16: int = 14
+    # IMPALA split kernels' row bands "key=R;..." (rb16x42 / sc16x16x42p0 ...; '' = defaults)
+    isplit_bands: str = ""
+
+    @classmethod
+    def from_env(cls, spec: str = None) -> "Switches":
+        sw = cls()
+        spec = os.environ.get("APEX_SWITCHES", "") if spec is None else spec
+        for item in spec.split(","):
+            item = item.strip()
+            if not item:
+                continue
+            if "=" not in item:
+                raise ValueError(f"APEX_SWITCHES item must be name=value, got {item!r}")
+            k, v = item.split("=", 1)
+            f = {f.name: f for f in dataclasses.fields(cls)}.get(k)
+            if f is None:
+                raise ValueError(f"unknown kernel switch {k!r}")
+            setattr(sw, k, _parse(f.type, v))
+        return sw
+
+    def non_default(self) -> Dict[str, Any]:
+        d = Switches()
+        return {f.name: getattr(self, f.name) for f in dataclasses.fields(self)
+                if getattr(self, f.name) != getattr(d, f.name)}
+
+
+def _parse(typ, v: str):
+    t = typ if isinstance(typ, str) else typ.__name__
+    if t == "bool":
+        return v.lower() not in ("0", "false", "off", "no")
+    if t == "int":
+        return int(v)
+    return v
+
+
+SW = Switches.from_env()

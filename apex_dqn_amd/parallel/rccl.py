@@ -42,10 +42,9 @@ def load_comm_lib() -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    from ..ops.build import COMM_LIB
-    if not os.path.exists(COMM_LIB):
-        raise RuntimeError(f"{COMM_LIB} missing: run `python -m apex_dqn_amd.ops.build`")
-    lib = ctypes.CDLL(COMM_LIB)
+    from ..ops.build import ensure_current
+    # content-addressed (ops/build.py): a stale or missing library is rebuilt, never run
+    lib = ctypes.CDLL(ensure_current("comm"))
     c_p, c_i, c_sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     sigs = {
         "apex_comm_load": ([ctypes.c_char_p], c_i),

@@ -82,11 +82,13 @@ def apex_uniform(seed: int, ctr: int, idx) -> np.ndarray:
 SHARD_STATS = 3
 
 
-def global_draw(stats: np.ndarray, rank: int, B: int, seed: int, ctr: int):
+def global_draw(stats: np.ndarray, rank: int, B: int, seed: int, ctr: int, mcap: Optional[int] = None):
     """The sharded sampler's global stratified draw as seen by ``rank`` (mirror of
     csrc/sumtree.hip ``tree_sample_body``): returns (u_local (B,) float64, valid (B,)
-    bool, wscale, pmin_global) for the all-gathered ``stats`` [W, >=2] = (total, min p, ...)."""
+    bool, wscale, pmin_global) for the all-gathered ``stats`` [W, >=2] = (total, min p, ...).
+    ``mcap`` caps the global batch M (default W B)."""
     W = stats.shape[0]
+    mcap = W * B if not mcap or mcap <= 0 else int(mcap)
     sm = c0 = tmax = 0.0
     pm = math.inf
     for q in range(W):
@@ -100,7 +102,11 @@ def global_draw(stats: np.ndarray, rank: int, B: int, seed: int, ctr: int):
             pm = min(pm, mq)
     tr = float(stats[rank, 0])
     c1 = c0 + tr
-    M = int(min(W * B, max(math.floor((B - 2) * sm / tmax), 0))) if tmax > 0.0 else 0
+    if tmax > 0.0:
+        mb = B if W == 1 else math.floor((B - 2) * sm / tmax)
+        M = int(min(mcap, max(mb, 0)))
+    else:
+        M = 0
     u = np.zeros(B, np.float64)
     valid = np.zeros(B, bool)
     wscale = 1.0
@@ -111,7 +117,7 @@ def global_draw(stats: np.ndarray, rank: int, B: int, seed: int, ctr: int):
             j0 += 1
         j = j0 + np.arange(B, dtype=np.int64)
         uj = (j.astype(np.float64) + apex_uniform(seed, ctr, j).astype(np.float64)) * delta
-        valid = (j < M) & (uj < c1)
+        valid = (j < M) & ((uj < c1) | (rank == W - 1))
         u = np.where(valid, uj - c0, 0.0)
         wscale = float(np.float32(W * B / M))
     return u, valid, wscale, pm
@@ -187,17 +193,24 @@ class GpuReplayShard:
         self._rdesc = None
         # sharding (enable_sharding): all-gathered (total, min p) of every shard, fp64
         self.shard_rank, self.shard_world, self.shard_seed, self.shard_group = 0, 1, 0, None
+        self.shard_mcap = 0     # cap on a draw's global batch M (0: W x the per-rank batch)
         self.local_stats = None
         self.shard_stats = None
 
     # -------------------------------------------------------------- sharding
-    def enable_sharding(self, rank: int, world: int, shard_seed: int, group=None) -> None:
+    def enable_sharding(self, rank: int, world: int, shard_seed: int, group=None, mcap: int = 0) -> None:
         """Make this shard part of ONE global prioritized replay over ``world`` ranks
         (see the module docstring).  ``shard_seed`` must be equal on every rank;
-        the sampling counter ``ctr`` advances in lock-step with the DP updates."""
+        the sampling counter ``ctr`` advances in lock-step with the DP updates.
+        ``mcap``: the global batch of a draw is M = min(mcap, floor((B - 2) sum / max_r
+        T_r)) strata (B = the per-rank row buffer); 0 = W B (per-rank batches).  With
+        ``Runtime.batch_scope = "global"`` mcap is ``replay_sample_size`` and B holds
+        ceil(mcap / W) rows plus slack, so M = mcap unless one shard carries more than
+        (B - 2) / mcap of the total mass (then M shrinks, identically on every rank)."""
         d = self.device
         self.shard_rank, self.shard_world = int(rank), int(world)
         self.shard_seed, self.shard_group = int(shard_seed), group
+        self.shard_mcap = int(mcap)
         self.local_stats = torch.zeros(SHARD_STATS, dtype=torch.float64, device=d)
         self.shard_stats = torch.zeros(SHARD_STATS * self.shard_world, dtype=torch.float64, device=d)
 
@@ -379,7 +392,7 @@ class GpuReplayShard:
         wscale = 1.0
         if self.sharded:
             st = self.shard_stats.double().cpu().numpy().reshape(self.shard_world, SHARD_STATS)
-            u, valid, wscale, pmin = global_draw(st, self.shard_rank, B, self.shard_seed, ctr)
+            u, valid, wscale, pmin = global_draw(st, self.shard_rank, B, self.shard_seed, ctr, self.shard_mcap)
             u = torch.from_numpy(u).clamp_(0.0, float(total))
         else:
             uu = torch.from_numpy(apex_uniform(self.seed, ctr, np.arange(B))).double()
@@ -419,7 +432,7 @@ class GpuReplayShard:
                 out["idx"].data_ptr(), out["weights"].data_ptr(), out["gen"].data_ptr(), out["obs"].data_ptr(),
                 out["nxt"].data_ptr(), out["act"].data_ptr(), out["rew"].data_ptr(), out["gam"].data_ptr(),
                 _lib.ptr(nxt2), _lib.ptr(self.shard_stats), self.shard_rank, self.shard_world, self.shard_seed,
-                _lib.ptr(out.get("wscale")))
+                _lib.ptr(out.get("wscale")), int(self.shard_mcap))
 
     def alloc_sample_buffers(self, B: int) -> Dict[str, torch.Tensor]:
         d = self.device

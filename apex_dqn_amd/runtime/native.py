@@ -48,9 +48,8 @@ def lib() -> Optional[ctypes.CDLL]:
         return None
     try:
         from ..ops import build
-        path = build.RUNTIME_LIB
-        if not os.path.exists(path):
-            build.build_runtime()
+        # content-addressed: a library whose build id does not match the sources is rebuilt
+        path = build.ensure_current("runtime")
         L = ctypes.CDLL(path)
         for name, (args, res) in _SIGS.items():
             f = getattr(L, name)

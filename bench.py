@@ -28,11 +28,20 @@ updates between barrier + synchronize brackets; the max over ranks is reported.
 ``graph_captures_in_timed`` must be 0.
 
 ``value`` = whole-job batch-512 gradient steps per second.  One rank: steps/s.  With
-data parallelism a step's global batch is the M rows the ranks' shards actually
-drew (one global prioritized draw, M <= N (512 - 2): replay/gpu_replay.py), counted
-on the device by the head kernel: ``value`` = (sum of M over the timed steps) / 512
-/ time, reported with ``samples_per_dp_step`` (mean M) and ``value_nominal`` = N x
-(DP steps/s).
+data parallelism (``--batch-scope``):
+
+* ``global`` (default; ``scaling: "strong"``): every update is ONE global prioritized
+  draw of exactly 512 samples over the N replay shards -- the reference learner's update
+  (``learner.py:68``, ``replay_sample_size``) -- and each rank computes the rows that
+  landed in its shard (ceil(512/N (1 + slack)) + 2 row buffers, ``ApexConfig.dp_batch``).
+  ``value`` = updates/s (``value_strong``); ``samples_per_dp_step`` is the mean global
+  batch M actually drawn (512 unless a shard held more than its slack of the mass).
+* ``per_rank`` (``scaling: "weak"``): every rank draws up to 512 rows, so an update
+  averages up to N x 512 samples; ``value`` = (sum of M over the timed steps) / 512 /
+  time (``value_weak``), ``value_nominal`` = N x (DP steps/s).
+
+At N > 1 the run also measures the other scope (fp32) and prints both ``value_strong``
+and ``value_weak`` with the rows each rank computed (``per_rank_rows``).
 """
 from __future__ import annotations
 
@@ -74,7 +83,7 @@ def make_replay(args, device, rank):
     return replay
 
 
-def make_learner(args, dtype, device, comm, rank, replay):
+def make_learner(args, dtype, device, comm, rank, replay, scope=None):
     from apex_dqn_amd.config import ApexConfig
     cfg = ApexConfig.from_dict({
         "env_conf": {"state_shape": [4, 84, 84], "action_dim": args.actions, "name": "SyntheticPong"},
@@ -84,6 +93,7 @@ def make_learner(args, dtype, device, comm, rank, replay):
         "Runtime": {"use_graphs": not args.no_graphs, "use_hip_kernels": args.backend == "hip",
                     "seed": 1234 + rank, "network": args.network, "dtype": dtype,
                     "presample": not args.no_presample, "force_dp": args.force_dp, "comm_backend": args.comm,
+                    "batch_scope": scope or args.batch_scope, "allreduce_dtype": args.allreduce_dtype,
                     **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
     })
     if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
@@ -152,6 +162,11 @@ def main():
     if os.environ.get("APEX_TRACEBACK_AFTER"):
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["APEX_TRACEBACK_AFTER"]), repeat=True)
+    args = parser().parse_args()
+    run(args)
+
+
+def parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -175,6 +190,13 @@ def main():
     ap.add_argument("--comm", default="torch", choices=["torch", "native"],
                     help="DP collectives: torch.distributed (RCCL process group) or the native RCCL "
                          "communicator (csrc/comm/rccl_comm.cpp)")
+    ap.add_argument("--batch-scope", default="global", choices=["global", "per_rank"],
+                    help="DP: global = one 512-sample update over all ranks (strong scaling, the reference's "
+                         "update); per_rank = 512 rows per rank (weak scaling)")
+    ap.add_argument("--no-scope-extra", action="store_true",
+                    help="N > 1: skip measuring the other --batch-scope (value_weak / value_strong)")
+    ap.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="DP gradient all-reduce payload (Runtime.allreduce_dtype)")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel step (RCCL collectives captured in the graphs, sharded "
                          "replay) even on one rank: capture check and segmented-step overhead")
@@ -187,8 +209,12 @@ def main():
                          "window (learner.rewarm: no update is kept; reported as prep_warm_replays)")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
                     help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala_split.hip (fp32) / csrc/impala.hip (bf16)")
-    args = ap.parse_args()
+    return ap
 
+
+def run(args) -> None:
+
+    from apex_dqn_amd.ops.switches import SW
     from apex_dqn_amd.parallel.dist import Comm
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,23 +230,45 @@ def main():
     comm = Comm.from_env(backend=args.dist_backend, device=device, force=args.force_dp)
 
     replay = make_replay(args, device, rank)
-    cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay)
+    dp = world > 1 or args.force_dp
+    scope = args.batch_scope if dp else "global"
+
+    def value_of(r, sc):
+        """whole-job batch-512 grad-steps/s of a measurement at scope ``sc``: updates/s
+        (global: every update is one 512-sample draw over all shards), or the drawn
+        samples in units of 512 per second (per_rank: an update averages M <= N 512)."""
+        if r["valid_rows"] is None:
+            return args.steps / r["dt"] * world
+        if sc == "global":
+            return args.steps / r["dt"]
+        return r["valid_rows"] / args.batch / r["dt"]
+
+    cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay, scope)
+    rows = learner.B
     res = measure(cfg, learner, replay, comm, args.warmup, args.steps, args.prep_warm)
+    other = None
+    if world > 1 and not args.no_scope_extra:
+        # the other batch scope, fp32: both scalings from one run
+        osc = "per_rank" if scope == "global" else "global"
+        del learner
+        torch.cuda.empty_cache()
+        cfg_o, learner_o = make_learner(args, args.dtype, device, comm, rank, replay, osc)
+        other = dict(measure(cfg_o, learner_o, replay, comm, args.warmup, args.steps, args.prep_warm),
+                     scope=osc, rows=learner_o.B)
+        learner = learner_o
     extra = None
     if not args.no_bf16_extra and args.dtype == "fp32":
         del learner
         torch.cuda.empty_cache()
-        cfg_b, learner_b = make_learner(args, "bf16", device, comm, rank, replay)
+        cfg_b, learner_b = make_learner(args, "bf16", device, comm, rank, replay, scope)
         extra = measure(cfg_b, learner_b, replay, comm, args.warmup, args.steps, args.prep_warm)
         learner = learner_b
     dt = res["dt"]
     ms = 1e3 * dt / args.steps
-    value = args.steps / dt * world
+    value = value_of(res, scope)
     # DP: a step's global batch is M = the rows the W ranks drew from their shards
-    # (<= W (B - 2), replay/gpu_replay.py); count batch-512 steps as M / 512 samples
+    # (global scope: 512 unless a shard outgrew its slack; per_rank: <= W (B - 2))
     samples_per_step = res["valid_rows"] / args.steps if res["valid_rows"] is not None else None
-    if samples_per_step is not None:
-        value = samples_per_step / args.batch * args.steps / dt
     m = res["metrics"]
     if rank == 0:
         kind = getattr(learner, "kind", "fused")
@@ -229,14 +277,17 @@ def main():
             "metric": METRIC,
             "value": round(value, 2), "unit": "grad-steps/s (batch 512)", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
-            "higher_is_better": True, "scaling": "weak",
+            "higher_is_better": True, "scaling": "strong" if scope == "global" else "weak",
             "vs_baseline": round(value / BASELINE_STEPS_PER_S, 2), "dtype": args.dtype, "data": "synthetic",
             "config": {"model": ("dueling NatureCNN (reference DuellingDQN, conv1=64), 4x84x84, A=%d" % args.actions
                                   if args.network == "nature64" else
                                   "dueling %s, 4x84x84, A=%d" % (args.network, args.actions)),
-                       "global_batch": args.batch * world, "seq_len": 1,
+                       "global_batch": args.batch * (world if scope == "per_rank" else 1), "seq_len": 1,
                        "parallelism": "dp%d" % world + ("-dp-step" if args.force_dp and world == 1 else ""),
-                       "per_gpu_batch": args.batch,
+                       "batch_scope": scope,
+                       "per_gpu_batch": args.batch if scope == "per_rank" else round(args.batch / world, 2),
+                       "per_rank_rows": rows,
+                       "allreduce_dtype": args.allreduce_dtype if dp else None,
                        "replay_per_gpu": args.replay,
                        "learner": kind + ("/" + ops.name if ops is not None and args.learner == "fused" else
                                           "/torch-autograd"),
@@ -247,6 +298,7 @@ def main():
                      and args.learner == "fused" else
                      ("torch fp32 (MIOpen / hipBLASLt)" if args.learner == "graph" and args.dtype == "fp32" else
                       "bf16 operands, fp32 accumulation / master weights / optimizer")),
+            "switches": SW.non_default(),      # kernel-path switches off their defaults (ops/switches.py)
             "prep_graph_captures": res["prep_graph_captures"],
             "graph_captures_in_timed": res["graph_captures_in_timed"],
             "prep_warm_replays": res["prep_warm_replays"],
@@ -256,11 +308,16 @@ def main():
         if samples_per_step is not None:
             out["samples_per_dp_step"] = round(samples_per_step, 2)
             out["value_nominal"] = round(args.steps / dt * world, 2)
+            out["value_" + ("strong" if scope == "global" else "weak")] = round(value, 2)
+        if other is not None:
+            k = "strong" if other["scope"] == "global" else "weak"
+            out["value_" + k] = round(value_of(other, other["scope"]), 2)
+            out["ms_per_step_" + k] = round(1e3 * other["dt"] / args.steps, 4)
+            out["samples_per_dp_step_" + k] = round(other["valid_rows"] / args.steps, 2)
+            out["per_rank_rows_" + k] = other["rows"]
+            out["graph_captures_in_timed_" + k] = other["graph_captures_in_timed"]
         if extra is not None:
-            vb = args.steps / extra["dt"] * world
-            if extra["valid_rows"] is not None:
-                vb = extra["valid_rows"] / args.batch / extra["dt"]
-            out["value_bf16"] = round(vb, 2)
+            out["value_bf16"] = round(value_of(extra, scope), 2)
             out["ms_per_step_bf16"] = round(1e3 * extra["dt"] / args.steps, 4)
             out["graph_captures_in_timed_bf16"] = extra["graph_captures_in_timed"]
         print(json.dumps(out), flush=True)

@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from bench_tree import timed  # noqa: E402
 from apex_dqn_amd.ops import _lib, conv as C  # noqa: E402
+from apex_dqn_amd.ops.switches import SW  # noqa: E402
 
 
 def main():
@@ -26,7 +27,7 @@ def main():
     b, b2 = torch.randn(64, device=dev), torch.randn(64, device=dev)
     out = torch.empty(N, 9, 9, 64, device=dev, dtype=torch.bfloat16)
     fl = 2.0 * N * 81 * 64 * 1024
-    C.CONV2_IMG = False
+    SW.conv2_img = False
     us = timed(lambda: C.conv_fwd(lib, x, w, b, 2, out, w2, b2, 2 * N // 3))
     print(json.dumps({"op": "conv2_fwd_igemm", "us": round(us, 2), "tflops": round(fl / us / 1e6, 1)}), flush=True)
     B = N // 2       # 768: the per-image sweep below uses 256 / 512 / 768 of them
@@ -34,7 +35,7 @@ def main():
     y1 = torch.relu(torch.randn(B, 20, 20, 64, device=dev)).to(torch.bfloat16)
     dx = torch.empty(B, 20, 20, 64, device=dev, dtype=torch.bfloat16)
     fl2 = 2.0 * B * 400 * 64 * 256
-    C.CONV2_DGRAD_IMG = False
+    SW.conv2_dgrad_img = False
     us = timed(lambda: C.conv2_dgrad(lib, dy, w, y1, dx))
     print(json.dumps({"op": "conv2_dgrad_igemm", "us": round(us, 2), "tflops": round(fl2 / us / 1e6, 1)}), flush=True)
     for nimg in (256, 512, 768):
@@ -48,7 +49,7 @@ def main():
     w3 = (torch.randn(64, 3, 3, 64, device=dev) * 0.04).to(torch.bfloat16)
     y2 = torch.relu(torch.randn(B, 9, 9, 64, device=dev)).to(torch.bfloat16)
     dx2 = torch.empty(B, 9, 9, 64, device=dev, dtype=torch.bfloat16)
-    C.CONV3_DGRAD_IMG = False
+    SW.conv3_dgrad_img = False
     us = timed(lambda: C.conv3_dgrad(lib, dy3[:512], w3, y2[:512], dx2[:512]))
     print(json.dumps({"op": "conv3_dgrad_igemm", "images": 512, "us": round(us, 2)}), flush=True)
     for g3 in (256, 128, 512):

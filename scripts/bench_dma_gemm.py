@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from bench_tree import timed  # noqa: E402
 from apex_dqn_amd.ops import _lib, conv as C  # noqa: E402
+from apex_dqn_amd.ops.switches import SW  # noqa: E402
 
 
 def sp(t):
@@ -50,8 +51,8 @@ def main():
     def outs(*shape):
         return [torch.zeros(*shape, device=dev, dtype=torch.bfloat16) for _ in range(2)]
 
-    C.CONV3_DGRAD_IMG = False
-    C.CONV2_DGRAD_IMG = False
+    SW.conv3_dgrad_img = False
+    SW.conv2_dgrad_img = False
     cases = {
         "fc_fwd": (outs(N, 1024), lambda o, s: C.dense_fwd(
             lib, xh, wh, b, o[0], True, None, w2h, b2, 1024,
@@ -84,15 +85,15 @@ def main():
                     r[f"maxdiff_h{hint}"] = max(float((a.float() - c.float()).abs().max()) for a, c in zip(got, ref))
                 r[f"us_h{hint}"] = round(timed(lambda: fn(o, split)), 2)
             if name in ("conv3_dgrad", "conv2_dgrad") and not (name == "conv3_dgrad" and split):
-                C.CONV3_DGRAD_IMG = C.CONV2_DGRAD_IMG = True      # image-resident kernels
+                SW.conv3_dgrad_img = SW.conv2_dgrad_img = True      # image-resident kernels
                 C._HINTS["tile"] = 0
                 r["us_img"] = round(timed(lambda: fn(o, split)), 2)
-                C.CONV3_DGRAD_IMG = C.CONV2_DGRAD_IMG = False
+                SW.conv3_dgrad_img = SW.conv2_dgrad_img = False
             print(json.dumps(r), flush=True)
             res[f"{name}_{'split' if split else 'bf16'}"] = r
     C._HINTS["tile"] = C._HINTS["order"] = 0
-    C.CONV3_DGRAD_IMG = True
-    C.CONV2_DGRAD_IMG = True
+    SW.conv3_dgrad_img = True
+    SW.conv2_dgrad_img = True
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/dma_gemm.json", "w") as f:
         json.dump(res, f, indent=1)

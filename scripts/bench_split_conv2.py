@@ -15,6 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from bench_tree import timed  # noqa: E402
 from apex_dqn_amd.ops import _lib, conv as C  # noqa: E402
+from apex_dqn_amd.ops.switches import SW  # noqa: E402
 
 
 def sp(t):
@@ -36,12 +37,12 @@ def main():
     fl = 3 * 2.0 * N * 81 * 64 * 1024
     only = os.environ.get("ONLY", "")
     if not only:
-        C.CONV2_IMG = False
+        SW.conv2_img = False
         us = timed(lambda: C.conv_fwd(lib, xh, wh, b, 2, oh, w2h, b2, 1024, x_lo=xl, w_lo=wl, w2_lo=w2l, out_lo=ol))
         print(json.dumps({"op": "conv2_fwd_split_igemm", "us": round(us, 2), "tflops_eff": round(fl / us / 1e6, 1)}),
               flush=True)
     for pack in (False, True):
-        C.C2F_PACK = pack
+        SW.c2f_pack = pack
         for n in ((256, 512, 1024, 1536) if not only else (1536,)):
             if only and only != "fwd":
                 break
@@ -56,7 +57,7 @@ def main():
     dxh = torch.empty(B, 20, 20, 64, device=dev, dtype=torch.bfloat16)
     dxl = torch.empty_like(dxh)
     if not only:
-        C.CONV2_DGRAD_IMG = False
+        SW.conv2_dgrad_img = False
         us = timed(lambda: C.conv2_dgrad(lib, dyh, wh, y1, dxh, dy_lo=dyl, w_lo=wl, out_lo=dxl))
         print(json.dumps({"op": "conv2_dgrad_split_igemm", "us": round(us, 2)}), flush=True)
     for n in ((256, 512) if not only else (512,)):

@@ -13,6 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from bench_tree import timed  # noqa: E402
 from apex_dqn_amd.ops import _lib, conv as C  # noqa: E402
+from apex_dqn_amd.ops.switches import SW  # noqa: E402
 
 
 def sp(t):
@@ -46,7 +47,7 @@ def main():
     y2 = torch.relu(torch.randn(B, 9, 9, 64, device=dev)).to(torch.bfloat16)
     e2h = torch.empty(B, 9, 9, 64, device=dev, dtype=torch.bfloat16)
     e2l = torch.empty_like(e2h)
-    C.CONV3_DGRAD_IMG = False
+    SW.conv3_dgrad_img = False
     for hint, order in ((0, 0), (1, 0), (2, 0), (2, 1), (2, 2), (1, 1), (1, 2)):
         C._HINTS["tile"], C._HINTS["order"] = hint, order
         r = {"hint": hint, "order": order}

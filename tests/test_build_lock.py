@@ -1,6 +1,7 @@
 """Multi-rank launch hygiene: four ranks that start on a checkout with no built
 kernel library build it ONCE (``ops/build.py`` holds an ``fcntl`` lock over the
-build directory; the waiters then find the objects fresh).  A stub compiler
+build directory; the waiters then find the objects' content keys and the library's
+build-id stamp current).  A stub compiler
 (``HIPCC``) records every invocation, so the test needs no toolchain time."""
 import os
 import stat
@@ -9,16 +10,21 @@ import tempfile
 import torch.multiprocessing as mp
 
 STUB = r'''#!/bin/sh
-# record the call, then create the -o target like a compiler would
+# record the call, then create the -o target like a compiler would (a link
+# concatenates its objects, so the build-id stamp object's marker survives)
+[ "$1" = "--version" ] && {{ echo "stub hipcc"; exit 0; }}
 echo "$PPID $*" >> "{log}"
 sleep 0.2
 out=""
 prev=""
+objs=""
 for a in "$@"; do
-  if [ "$prev" = "-o" ]; then out="$a"; fi
+  if [ "$prev" = "-o" ]; then out="$a";
+  else case "$a" in *.o) objs="$objs $a";; esac; fi
   prev="$a"
 done
 [ -n "$out" ] && : > "$out"
+case " $* " in *" -shared "*) [ -n "$objs" ] && cat $objs > "$out";; esac
 exit 0
 '''
 

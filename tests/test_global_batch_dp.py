@@ -1,0 +1,128 @@
+"""Global-batch data parallelism (``Runtime.batch_scope = "global"``) on the gloo fake
+cluster: W ranks that each compute their share of ONE global prioritized draw of B
+samples take the same update as one rank with batch B over the same replay contents
+and RNG counter ("W ranks with batch B/W must match 1 rank with batch B").
+
+The one-rank run holds the W shards concatenated in rank order (leaves, records and
+frame rings), so the global stratified draw -- identical uniforms, identical strata --
+picks the same transitions; the parameters after several updates agree to fp32
+round-off (only the order of the gradient sums differs).
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from apex_dqn_amd.config import ApexConfig
+
+CAP, FR = 300, 400
+BG, STEPS = 16, 3
+
+
+def _cfg(slack):
+    return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
+                                 "Learner": {"replay_sample_size": BG, "q_target_sync_freq": 2},
+                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0, "force_dp": True,
+                                             "batch_scope": "global", "dp_batch_slack": slack}})
+
+
+def _shard(rank):
+    """Rank ``rank``'s replay shard: deliberately unequal priority mass per shard."""
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    rp = GpuReplayShard(CAP, CAP, FR, 4, device="cpu", seed=rank + 3)
+    rng = np.random.default_rng(100 + rank)
+    seqs = rp.append_frames(rng.integers(0, 255, (120, 84, 84), dtype=np.uint8))
+    K = 100
+    st = np.stack([seqs[i:i + 4] for i in range(K)])
+    rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 5, K), R=rng.normal(size=K),
+                   Gamma=np.where(rng.random(K) < 0.2, 0.0, 0.97), priority=rng.random(K) * (1 + 0.5 * rank)))
+    return rp
+
+
+def _concat(world):
+    """One replay holding the ``world`` shards back to back (rank order)."""
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    shards = [_shard(r) for r in range(world)]
+    rp = GpuReplayShard(CAP * world, CAP * world, FR * world, 4, device="cpu", seed=3)
+    rp.frames.copy_(torch.cat([s.frames for s in shards]))
+    for name in ("act", "rew", "gam", "gen", "leaf"):
+        getattr(rp, name).copy_(torch.cat([getattr(s, name) for s in shards]))
+    rp.obs.copy_(torch.cat([s.obs + r * FR for r, s in enumerate(shards)]))
+    rp.nxt.copy_(torch.cat([s.nxt + r * FR for r, s in enumerate(shards)]))
+    rp.live = rp.head = CAP * world
+    rp._torch_rebuild()
+    return rp
+
+
+def _worker(rank, world, concat, slack, path, q):
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.parallel.dist import Comm
+    torch.set_num_threads(2)
+    comm = Comm.init(rank, world, f"file://{path}", backend="gloo", force=True)
+    torch.manual_seed(1234)          # identical initial parameters in every run
+    rp = _concat(concat) if concat else _shard(rank)
+    L = FusedNatureLearner(_cfg(slack), "cpu", rp, comm=comm)
+    draws, grads = [], []
+    p0 = L.p32.numpy().copy()
+    for _ in range(STEPS):
+        L._sample()
+        valid = L.S["gen"] >= 0
+        # global leaf id of every row this rank drew (the concatenated replay's numbering)
+        draws.append((L.S["idx"][valid] + (0 if concat else rank * CAP)).tolist())
+        L.step()
+        grads.append(L.g32.numpy().copy())
+    q.put((rank, L.B, int(L.valid_rows_total.item()), draws, grads, L.p32.numpy().copy(), L.t32.numpy().copy(), p0))
+    comm.shutdown()
+
+
+def _run(world, concat, slack):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "store")
+        procs = [ctx.Process(target=_worker, args=(r, world, concat, slack, path, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=300) for _ in range(world)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_dp_batch_rows():
+    cfg = ApexConfig.from_dict({"Learner": {"replay_sample_size": 512}})
+    assert [cfg.dp_batch(w) for w in (1, 2, 4, 8)] == [(512, 512), (290, 512), (146, 512), (74, 512)]
+    assert cfg.dp_batch(8, dp=False) == (512, 512)
+    cfg.Runtime.batch_scope = "per_rank"
+    assert cfg.dp_batch(8) == (512, 8 * 512)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 4])
+def test_global_batch_dp_equals_one_rank(world):
+    slack = 1.0
+    multi = _run(world, 0, slack)
+    one = _run(1, world, slack)[0]
+    rows = multi[0][1]
+    assert rows == int(np.ceil(BG / world * (1 + slack))) + 2 and one[1] == BG
+    # every update drew exactly BG samples over the shards, and one rank drew the same BG
+    assert sum(r[2] for r in multi) == STEPS * BG == one[2]
+    for s in range(STEPS):
+        glob = [i for r in multi for i in r[3][s]]
+        assert glob == one[3][s], (s, glob, one[3][s])
+    # the same updates: all-reduced gradient and parameters to fp32 round-off
+    for r in multi:
+        for s in range(STEPS):
+            g1, gw = one[4][s], r[4][s]
+            assert np.abs(gw - g1).max() <= 2e-6 * np.abs(g1).max() + 1e-10, s
+        # parameters: RMSprop divides by sqrt(centered variance), which amplifies the
+        # summation-order round-off of the first updates a little
+        upd = np.abs(one[5] - one[7]).max()
+        dp = np.abs(r[5] - one[5]).max()
+        assert dp <= 1e-3 * upd, (dp, upd)
+        assert np.array_equal(r[5], multi[0][5])            # replicas bit-identical
+        assert np.abs(r[6] - one[6]).max() <= 1e-3 * upd

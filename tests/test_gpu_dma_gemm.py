@@ -8,6 +8,8 @@ that are not tile multiples exercise the clamped rows."""
 import pytest
 import torch
 
+from apex_dqn_amd.ops.switches import SW
+
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
@@ -34,8 +36,8 @@ def _run(C, hint, fn, outs):
 def test_dma_kernel_matches_register_staged(op, split, monkeypatch):
     from apex_dqn_amd.ops import _lib as L, conv as C
     lib = L.require_kernels()
-    monkeypatch.setattr(C, "CONV3_DGRAD_IMG", False)
-    monkeypatch.setattr(C, "CONV2_DGRAD_IMG", False)
+    monkeypatch.setattr(SW, "conv3_dgrad_img", False)
+    monkeypatch.setattr(SW, "conv2_dgrad_img", False)
     g = torch.Generator(device="cpu").manual_seed(3)
 
     def rnd(*shape, s=1.0, relu=False):

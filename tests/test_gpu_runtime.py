@@ -291,7 +291,13 @@ def test_bench_two_ranks_gloo_rehearsal():
                        cwd=ROOT)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     out = _bench_json(r.stdout)
-    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 1024 and out["config"]["parallelism"] == "dp2"
+    # default: one global 512-sample update per step (strong scaling), each rank computing
+    # its share (290 rows at W = 2); the per-rank scope rides along as value_weak
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 512 and out["config"]["parallelism"] == "dp2"
+    assert out["scaling"] == "strong" and out["config"]["per_rank_rows"] == 290
+    assert out["samples_per_dp_step"] == 512.0 and out["value"] == out["value_strong"] > 0
+    assert out["value_weak"] > 0 and out["per_rank_rows_weak"] == 512 and out["samples_per_dp_step_weak"] > 512
+    assert out["graph_captures_in_timed"] == 0
 
 
 def _native_rccl_worker(q, port):

@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 import torch
 
+from apex_dqn_amd.ops.switches import SW
+
 from apex_dqn_amd.ops import reference as R
 
 pytestmark = pytest.mark.gpu
@@ -297,11 +299,14 @@ def _fp64_reference_grads(L):
     return {k: t.grad for k, t in sd.items()}, a.detach(), flips
 
 
-def test_whole_step_fp32_split_matches_fp64_oracle():
+@pytest.mark.parametrize("B", [128, 74, 36])
+def test_whole_step_fp32_split_matches_fp64_oracle(B):
     """The whole fused learner step in its default fp32 (split) mode: every gradient
     segment within 1e-3 relative (norm-wise; measured ~1e-5) of fp64 CPU autograd on the
     same batch in the same ReLU region; the bf16-operand mode and the torch fp32 backend
-    (MIOpen / hipBLASLt) are measured against the same oracle and printed."""
+    (MIOpen / hipBLASLt) are measured against the same oracle and printed.  B = 74 / 36:
+    the per-rank row counts of a global-batch DP step (ApexConfig.dp_batch), whose
+    online / target switch is not on a 128-row tile (two launches per weight set)."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.models.flat_params import flat_to_reference_state
@@ -309,7 +314,7 @@ def test_whole_step_fp32_split_matches_fp64_oracle():
     errs_all = {}
     for mode, be, dtype in (("fp32_split", "hip", "fp32"), ("bf16", "hip", "bf16"), ("torch_fp32", "torch", "fp32")):
         cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
-                                    "Learner": {"replay_sample_size": 128},
+                                    "Learner": {"replay_sample_size": B},
                                     "Runtime": {"use_graphs": False, "presample": False, "dtype": dtype}})
         torch.manual_seed(0)
         rp = GpuReplayShard(2000, 2000, 2100, 4, device=DEV, seed=7)
@@ -357,7 +362,7 @@ def test_conv2_image_resident_split_kernels_vs_generic(monkeypatch, grid):
     ref = torch.cat([R.conv_fwd(xd[:N1], _c(wa), _c(ba), 2, torch.float64),
                      R.conv_fwd(xd[N1:], _c(wb), _c(bb), 2, torch.float64)])
     assert _rel(_join(hi, lo), ref) < TOL
-    monkeypatch.setattr(C, "CONV2_IMG", False)
+    monkeypatch.setattr(SW, "conv2_img", False)
     gh, gl = _empty2(N1 + N2, 9, 9, 64)
     C.conv_fwd(lib, xh, wah, ba, 2, gh, wbh, bb, N1, x_lo=xl, w_lo=wal, w2_lo=wbl, out_lo=gl)
     assert _rel(_join(hi, lo), _join(gh, gl)) < TOL
@@ -370,7 +375,7 @@ def test_conv2_image_resident_split_kernels_vs_generic(monkeypatch, grid):
     C.conv2_dgrad_img(lib, dh, wah, y1, h1, grid=grid, dy_lo=dl, w_lo=wal, out_lo=l1)
     ref1 = R.conv_dgrad(_c(dy), _c(wa), (N, 20, 20, 64), 2, _c(y1), torch.float64)
     assert _rel(_join(h1, l1), ref1) < TOL
-    monkeypatch.setattr(C, "CONV2_DGRAD_IMG", False)
+    monkeypatch.setattr(SW, "conv2_dgrad_img", False)
     g1h, g1l = _empty2(N, 20, 20, 64)
     C.conv2_dgrad(lib, dh, wah, y1, g1h, dy_lo=dl, w_lo=wal, out_lo=g1l)
     assert _rel(_join(h1, l1), _join(g1h, g1l)) < TOL
@@ -538,7 +543,7 @@ def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
     outs = []
     for wq, reps in ((False, 1), (True, 3)):
         ws = C_.Workspace()
-        monkeypatch.setenv("APEX_WORK_QUEUE", "1" if wq else "0")   # (the forward's queue is env-only)
+        monkeypatch.setattr(SW, "work_queue", "on" if wq else "off")   # (the forward's queue is switch-only)
         for _ in range(reps):
             y2h, y2l = _empty2(N, 9, 9, 64)
             y1h, y1l = _empty2(copy_n, 20, 20, 64)
@@ -560,7 +565,7 @@ def _presample_learner(monkeypatch, opt_frags: bool, dtype: str = "fp32"):
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
-    monkeypatch.setenv("APEX_OPT_FRAGS", "1" if opt_frags else "0")
+    monkeypatch.setattr(SW, "opt_frags", opt_frags)
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": 128},
                                 "Runtime": {"use_graphs": False, "presample": True, "dtype": dtype}})
@@ -580,7 +585,7 @@ def test_optimizer_stores_conv12_fragments_bit_identical_to_pack(monkeypatch, dt
     """The optimizer + sample launch stores the updated w1 / w2 in the fused forward's
     fragment order (csrc/cf_pack.h cf_frag_store): after real steps the online fragments
     are byte-identical to a fresh pack launch, and the run's weights are bit-identical to
-    the pack-launch variant's (APEX_OPT_FRAGS=0)."""
+    the pack-launch variant's (SW.opt_frags = False)."""
     from apex_dqn_amd.ops import conv as C
     out = {}
     for opt in (True, False):
