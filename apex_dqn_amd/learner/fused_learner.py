@@ -527,6 +527,10 @@ class FusedNatureLearner(IsNormMixin):
         else:
             self._step_body()
 
+    # called after update i of the multi-step graph's capture (its work is captured into
+    # the graph): tests record every update's state and next batch from inside the graph
+    _step_hook = None
+
     def _graphs_enabled(self) -> bool:
         return bool(self.rt.use_graphs) and self.device.type == "cuda" and (not self._dp or self._dp_graphs)
 
@@ -586,8 +590,10 @@ class FusedNatureLearner(IsNormMixin):
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.device)
             with torch.cuda.graph(g):
-                for _ in range(k):
+                for i in range(k):
                     self._body()
+                    if self._step_hook is not None:
+                        self._step_hook(i)      # captured too (tests: per-update state copies)
             self._multi = g
             self.graph_captures += 1
             self._graphs_warm = False

@@ -245,18 +245,32 @@ class _LoopState:
         self.t_last, self.n_last, self.ins_last, self.steps_last = t0, n0, 0, 0
 
 
+def _rng_groups(group) -> list:
+    """The actor groups whose device RNG counters drive the epsilon-greedy draws (every
+    group of a pipelined actor, ``Runtime.actor_pipeline``)."""
+    gs = getattr(group, "groups", None) or [group]
+    return [g for g in gs if getattr(g, "ctr", None) is not None]
+
+
 def _actor_rng(group) -> Dict[str, Any]:
-    """The actor group's device RNG counter (epsilon-greedy draws) for the checkpoint."""
-    ctr = getattr(group, "ctr", None)
-    return {"actor_rng": {"ctr": int(ctr.item())}} if ctr is not None else {}
+    """Every actor group's device RNG counter for the checkpoint (``ctrs``, one per
+    pipelined group; ``ctr`` = group 0's, the older single-counter format)."""
+    ctrs = [int(g.ctr.item()) for g in _rng_groups(group)]
+    return {"actor_rng": {"ctr": ctrs[0], "ctrs": ctrs}} if ctrs else {}
 
 
 def _restore_actor_rng(group, path: str) -> None:
+    """Restore every group's counter (a checkpoint with one counter restores group 0's
+    and leaves the others at their fresh state)."""
     from ..utils.checkpoint import load_checkpoint
     ck = load_checkpoint(path) or {}
     a = ck.get("actor_rng")
-    if isinstance(a, dict) and getattr(group, "ctr", None) is not None:
-        group.ctr.fill_(int(a["ctr"]))
+    if not isinstance(a, dict):
+        return
+    gs = _rng_groups(group)
+    ctrs = a.get("ctrs") or [a["ctr"]]
+    for g, c in zip(gs, ctrs):
+        g.ctr.fill_(int(c))
 
 
 def _wait_event(ev, timeout: float, comm=None) -> None:

@@ -115,18 +115,89 @@ def _state(L):
             cpu(flat_to_reference_state(L.layout.views(L.rms_m), L.c1)))
 
 
-def _run(dtype, defer=True):
+class _GraphTrace:
+    """Records, from INSIDE the learner's multi-step HIP graph (``_step_hook``), every
+    update's resulting state (p32, RMSprop v / m) and the batch it drew for the next
+    update (the optimizer launch's pre-sample), so the oracles replay the production
+    path's own batches and one-step errors start from its own states."""
+
+    KEYS = ("idx", "weights", "gen", "obs", "nxt", "act", "rew", "gam")
+
+    def __init__(self, L, k):
+        self.L = L
+        self.S = [{n: torch.zeros_like(L.S[n]) for n in self.KEYS} for _ in range(k)]
+        self.st = [tuple(torch.zeros_like(t) for t in (L.p32, L.rms_v, L.rms_m)) for _ in range(k)]
+
+    def __call__(self, i):
+        for n in self.KEYS:
+            self.S[i][n].copy_(self.L.S[n])
+        for dst, src in zip(self.st[i], (self.L.p32, self.L.rms_v, self.L.rms_m)):
+            dst.copy_(src)
+
+
+def _state_of(L, p32, v, m):
+    """Reference-keyed CPU state dicts of flat (p32, v, m) and the learner's target."""
+    from apex_dqn_amd.models.flat_params import flat_to_reference_state
+    cpu = lambda d: {k: x.detach().cpu() for k, x in d.items()}       # noqa: E731
+    return (cpu(flat_to_reference_state(L.layout.views(p32), L.c1)), cpu(flat_to_reference_state(L.T, L.c1)),
+            cpu(flat_to_reference_state(L.layout.views(v), L.c1)),
+            cpu(flat_to_reference_state(L.layout.views(m), L.c1)))
+
+
+def _graph_updates(L):
+    """The production path: ``L.steps(SYNC)`` replays ONE captured graph of SYNC updates
+    (pre-sampling inside the optimizer launch, optimizer-written fused-forward operands),
+    then the target sync; yields (state before, batch, state after) per update."""
+    tr = _GraphTrace(L, SYNC)
+    L._step_hook = tr
+    L.prepare_graphs(multi=True)
+    for _ in range(STEPS // SYNC):
+        if L._sample_ver != L.replay.version:
+            L._sample()
+        torch.cuda.synchronize()
+        before = _state(L)
+        tgt = before[1]                   # the target of the chunk's updates (synced after it)
+        S0 = {k: v.clone() for k, v in L.S.items()}
+        L.steps(SYNC)                     # one multi-step graph launch, then sync_target()
+        torch.cuda.synchronize()
+        for i in range(SYNC):
+            S = S0 if i == 0 else tr.S[i - 1]
+            a = _state_of(L, *tr.st[i])
+            after = (a[0], tgt, a[2], a[3])
+            yield before, S, after, i == SYNC - 1
+            before = after
+
+
+def _eager_updates(L):
+    for t in range(1, STEPS + 1):
+        st0 = _state(L)
+        L._seg1()
+        S = {k: v.clone() for k, v in L.S.items()}
+        L._seg2()
+        L._seg3()
+        L.num_q_updates += 1
+        sync = t % SYNC == 0
+        yield st0, S, None, sync
+        if sync:
+            L.sync_target()
+
+
+def _run(dtype, defer=True, graph=False):
     """24 updates; returns (trajectory errors of the fused learner and of the torch-fp32
-    oracle vs fp64: parameters, q on a probe batch; median one-step update errors)."""
+    oracle vs fp64: parameters, q on a probe batch; median one-step update errors).
+    ``graph``: the production path (multi-step HIP graphs, pre-sampling, optimizer-written
+    operands) instead of eager segments."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": A, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": B, "q_target_sync_freq": SYNC},
-                                "Runtime": {"use_graphs": False, "presample": False, "dtype": dtype}})
+                                "Runtime": {"use_graphs": graph, "presample": graph, "dtype": dtype,
+                                            "graph_steps": SYNC}})
     torch.manual_seed(0)
     rp = _replay()
     L = FusedNatureLearner(cfg, DEV, rp)
     L._defer_fc_epilogue = defer
+    assert not graph or L._frag_out is not None       # optimizer-written operands on
     rt = cfg.Runtime
     sd0 = {k: v.detach().cpu() for k, v in L.reference_state_dict().items()}
     o64, o32 = _Oracle(sd0, rt, torch.float64), _Oracle(sd0, rt, torch.float32)
@@ -139,13 +210,7 @@ def _run(dtype, defer=True):
     probe = L.replay.gather_frames(probe_slots).double().cpu() * scale
     q0 = o64.q(probe)
     local_f, local_32 = [], []
-    for t in range(1, STEPS + 1):
-        st0 = _state(L)
-        L._seg1()
-        S = {k: v.clone() for k, v in L.S.items()}
-        L._seg2()
-        L._seg3()
-        L.num_q_updates += 1
+    for st0, S, st1, sync in (_graph_updates(L) if graph else _eager_updates(L)):
         s_t = L.replay.gather_frames(S["obs"]).double().cpu() * scale
         s_n = L.replay.gather_frames(S["nxt"]).double().cpu() * scale
         w = S["weights"].double().cpu()
@@ -157,12 +222,12 @@ def _run(dtype, defer=True):
             o.step(*args)
         d64 = l64.flat() - _flat(st0[0], keys)
         dn = float(d64.norm())
-        local_f.append(float((_flat(L.reference_state_dict(), keys) - _flat(st0[0], keys) - d64).norm()) / dn)
+        p1 = _flat(L.reference_state_dict() if st1 is None else st1[0], keys)
+        local_f.append(float((p1 - _flat(st0[0], keys) - d64).norm()) / dn)
         local_32.append(float((l32.flat() - _flat(st0[0], keys) - d64).norm()) / dn)
         for o in (o64, o32):
             o.step(*args)
-        if t % SYNC == 0:
-            L.sync_target()
+        if sync:
             o64.sync()
             o32.sync()
     torch.cuda.synchronize()
@@ -199,3 +264,19 @@ def test_fused_learner_trajectory_vs_fp64():
         # 5.7e-2, torch fp32 2.1e-2, bf16 2.0e-1
         assert r["q"] < 4.0 * r["q32"] + 1e-6, (k, r)
         assert r["q"] < 0.5 * bf["q"], (k, r, bf)
+
+
+def test_graph_path_trajectory_vs_fp64():
+    """The production path -- 8-update HIP graphs with the next batch drawn inside the
+    optimizer launch and the fused forward's operands written by the optimizer -- over
+    24 updates with a target sync after every graph: the same fp64 bounds as the eager
+    segments above (one-step and function-space), on the batches and states recorded
+    from inside the graph."""
+    res = {"fp32_graph": _run("fp32", graph=True), "bf16_graph": _run("bf16", graph=True)}
+    for k, r in res.items():
+        print(k, {n: f"{v:.3e}" for n, v in r.items()})
+    r, bf = res["fp32_graph"], res["bf16_graph"]
+    assert r["local"] < 1e-3, r
+    assert r["local"] < 0.02 * bf["local"], (r, bf)
+    assert r["q"] < 4.0 * r["q32"] + 1e-6, r
+    assert r["q"] < 0.5 * bf["q"], (r, bf)
