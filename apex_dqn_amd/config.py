@@ -123,6 +123,11 @@ class RuntimeConf:
     dp_batch_slack: float = 0.125   # global scope: rows a rank can hold beyond B/W, as a fraction of B/W (plus
                                     # 2): the draw takes exactly B strata while no shard holds more than
                                     # (rows - 2) / B of the total priority mass, fewer otherwise
+    dp_fc_exchange: str = "auto"    # DP exchange of the fc layer's gradient: "allreduce" (the 1024 x 3136 fp32
+                                    # gradient) | "factors" (all-gather every rank's dH / fc-input rows -- the
+                                    # operands the kernels use -- and form the gradient of the whole global
+                                    # batch on each rank: ~(B_total x 4160) values instead of 3.2 M, exact and
+                                    # bit-identical across ranks) | "auto" (factors while W x rows <= 1024)
     replica_check_every: int = 5000  # DP: learner steps between replica checksum checks (0 = off)
     step_timeout: float = 300.0     # GPU loop watchdog: seconds a queued learner chunk may take
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
@@ -214,6 +219,8 @@ class ApexConfig:
             raise ValueError("Runtime.batch_scope must be 'global' or 'per_rank'")
         if not self.Runtime.dp_batch_slack >= 0.0:
             raise ValueError("Runtime.dp_batch_slack must be >= 0")
+        if self.Runtime.dp_fc_exchange not in ("auto", "factors", "allreduce"):
+            raise ValueError("Runtime.dp_fc_exchange must be 'auto', 'factors' or 'allreduce'")
         if self.Runtime.loss not in ("huber", "mse"):
             raise ValueError("Runtime.loss must be 'huber' or 'mse'")
         net = self.network

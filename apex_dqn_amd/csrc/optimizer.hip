@@ -81,3 +81,91 @@ APEX_EXPORT int apex_cast_bf16(const float* x, bf16_t* y, int64_t n, bf16_t* lo,
   cast_bf16_kernel<<<nb, 256, 0, st>>>(x, y, lo, n);
   APEX_CHECK_LAUNCH();
 }
+
+// ------------------------------------------------ data-parallel fc-gradient factors
+// Row pack of up to 4 (src, src row stride, cols) segments of 16-bit values into one
+// [rows][ld] buffer: the send rows of the factored fc-gradient exchange
+// (learner/fused_learner.py _dp_body: [dH | dH lo | y3 | y3 lo] per sample, one
+// all-gather instead of an all-reduce of the 1024 x 3136 gradient).  16-B chunks,
+// every column count and stride a multiple of 8.
+struct PackRows {
+  const uint16_t* src[4];
+  int64_t ld[4];
+  int cols[4];
+  int nseg, rows;
+  uint16_t* dst;
+  int64_t dld;
+};
+
+__global__ void __launch_bounds__(256) pack_rows_kernel(PackRows p) {
+  int tot = 0;
+  for (int s = 0; s < p.nseg; ++s) tot += p.cols[s] >> 3;
+  const int64_t nchunks = (int64_t)p.rows * tot;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(c / tot);
+    int k = (int)(c - (int64_t)r * tot), s = 0, col0 = 0;
+    while (k >= (p.cols[s] >> 3)) {
+      k -= p.cols[s] >> 3;
+      col0 += p.cols[s];
+      ++s;
+    }
+    const uint4 v = *reinterpret_cast<const uint4*>(p.src[s] + (int64_t)r * p.ld[s] + 8 * k);
+    *reinterpret_cast<uint4*>(p.dst + (int64_t)r * p.dld + col0 + 8 * k) = v;
+  }
+}
+
+APEX_EXPORT int apex_pack_rows(const uint16_t* const* src, const int64_t* ld, const int* cols, int nseg, int rows,
+                               uint16_t* dst, int64_t dld, hipStream_t st) {
+  if (nseg < 1 || nseg > 4 || rows < 0 || (dld & 7) || ((uintptr_t)dst & 15)) return (int)hipErrorInvalidValue;
+  PackRows p{};
+  int tot = 0;
+  for (int s = 0; s < nseg; ++s) {
+    if ((cols[s] & 7) || (ld[s] & 7) || ((uintptr_t)src[s] & 15)) return (int)hipErrorInvalidValue;
+    p.src[s] = src[s];
+    p.ld[s] = ld[s];
+    p.cols[s] = cols[s];
+    tot += cols[s];
+  }
+  if (tot > dld) return (int)hipErrorInvalidValue;
+  p.nseg = nseg;
+  p.rows = rows;
+  p.dst = dst;
+  p.dld = dld;
+  if (rows == 0) return 0;
+  const int64_t nchunks = (int64_t)rows * (tot >> 3);
+  int nb = (int)((nchunks + 255) / 256);
+  nb = nb > 1024 ? 1024 : nb;
+  pack_rows_kernel<<<nb, 256, 0, st>>>(p);
+  APEX_CHECK_LAUNCH();
+}
+
+// Squared-norm partials of two fp32 ranges (the all-reduced conv + head gradient
+// regions of the factored DP step; the fc part's partials come from its wgrad
+// epilogue): `nblk` partials into `partials`.
+__global__ void __launch_bounds__(256) sqnorm_ranges_kernel(const float* __restrict__ p0, int64_t n0,
+                                                            const float* __restrict__ p1, int64_t n1,
+                                                            double* __restrict__ partials) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int r = 0; r < 2; ++r) {
+    const float* g = r ? p1 : p0;
+    const int64_t n = r ? n1 : n0;
+    if (g == nullptr) continue;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const float v = g[i];
+      acc += (double)v * v;
+    }
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+APEX_EXPORT int apex_sqnorm_ranges(const float* p0, int64_t n0, const float* p1, int64_t n1, double* partials,
+                                   int nblk, hipStream_t st) {
+  if (nblk < 1 || nblk > 1024) return (int)hipErrorInvalidValue;
+  sqnorm_ranges_kernel<<<nblk, 256, 0, st>>>(p0, n0, p1, n1, partials);
+  APEX_CHECK_LAUNCH();
+}

@@ -167,6 +167,23 @@ class FusedNatureLearner(IsNormMixin):
             raise ValueError("Runtime.allreduce_dtype must be fp32 or bf16")
         self._comm_bf16 = self._dp and self.rt.allreduce_dtype == "bf16"
         self.gcomm = torch.zeros(n, dtype=torch.bfloat16, device=d) if self._comm_bf16 else self.g32
+        # DP exchange of the fc weight gradient (Runtime.dp_fc_exchange).  Its gradient is
+        # dW = dH^T X over the global batch: rank r holds rows (dH_r, X_r), rank <= its row
+        # count.  "factors" all-gathers those rows -- exactly the bf16 (hi / lo) operands
+        # the kernels multiply -- and every rank forms dW of the WHOLE global batch with the
+        # same kernel in the same order: W x rows x (1024 + 3136) values move instead of the
+        # 3.2 M-float gradient (a global-batch step at W = 8: 1.2 MB sent per rank vs 12.9 MB
+        # all-reduced), the result is bit-identical on every rank, and only the conv and
+        # head gradients (0.48 MB) are all-reduced.  "auto": factors while W x rows <= 1024.
+        mode = self.rt.dp_fc_exchange
+        self._fc_factors = self._dp and not self._comm_bf16 and (
+            mode == "factors" or (mode == "auto" and self.world * self.B <= 1024))
+        if self._fc_factors:
+            planes = 2 if self.split else 1
+            self._fx_cols = [1024] * planes + [3136] * planes      # [dH | dH lo | X | X lo]
+            ncol = sum(self._fx_cols)
+            self.fx_send = torch.zeros(self.B, ncol, dtype=self.act_dtype, device=d)
+            self.fx_recv = torch.zeros(self.world * self.B, ncol, dtype=self.act_dtype, device=d)
         # producer-summed clip norm: the fc wgrad epilogue and the grad_finalize blocks
         # write squared-norm partials of the values they store, the optimizer launch sums
         # them.  With DP the norm is of the all-reduced gradient: the optimizer's own pass.
@@ -368,9 +385,19 @@ class FusedNatureLearner(IsNormMixin):
                  self.td_abs, self.loss_b, self.dH, self.dhead, zero=self.g_head_region,
                  isn=self._isn(), **self._lo(lo=sp and (self.h_lo[:2 * B], self.h_lo[2 * B:], self.dH_lo)))
         self._mark("head")
+        prio = (self.replay, S["idx"], S["gen"], self.td_abs)
+        if getattr(self, "_fc_factors", False):
+            # factored DP exchange: the head weight gradient + priority write-back now, the
+            # fc weight gradient after the all-gather of every rank's (dH, X) rows (_dp_body)
+            ops.head_wgrad(self.h, self.dhead, self._head_params(self.G), prio=prio,
+                           **self._lo(Hon_lo=self.h_lo))
+            segs = [self.dH, self.dH_lo, self.y3[:B].reshape(B, 3136), self.y3_lo[:B].reshape(B, 3136)] \
+                if sp else [self.dH, self.y3[:B].reshape(B, 3136)]
+            ops.pack_rows(self.fx_send, segs)
+            self._mark("fc_wgrad")
+            return
         # fc wgrad + head wgrad + priority write-back: one launch on the HIP backend
         # (csrc/sumtree.hip fc_wgrad_head_prio_kernel)
-        prio = (self.replay, S["idx"], S["gen"], self.td_abs)
         nrm = (self.norm_part, 0) if self._fuse_norm else None
         self._fc_slots = ops.fc_head_wgrad(self.dH, self.y3[:B], self.G["wfc"], self.G["bfc"], self.h,
                                            self.dhead, self.G, prio, norm=nrm,
@@ -451,8 +478,10 @@ class FusedNatureLearner(IsNormMixin):
         self.num_q_updates += 1
         return out
 
-    def _seg3(self) -> None:
-        """clip + centered RMSprop (+ bf16 hi / lo pack) with the next batch's draw."""
+    def _seg3(self, norm_slots: Optional[int] = None) -> None:
+        """clip + centered RMSprop (+ bf16 hi / lo pack) with the next batch's draw.
+        ``norm_slots``: the clip norm is the sum of ``norm_part[:norm_slots]`` (written by
+        the gradient producers of the factored DP step)."""
         rt, ops = self.rt, self.ops
         if self._comm_bf16:
             self.g32.copy_(self.gcomm)
@@ -461,7 +490,8 @@ class FusedNatureLearner(IsNormMixin):
         nxt = (self.replay, self.B, self.S, self.slots[2 * self.B:]) if self._presample else None
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
-                      norm_total=(self.norm_part, self._npart) if self._fuse_norm else None, sample=nxt,
+                      norm_total=(self.norm_part, self._npart) if self._fuse_norm else
+                      ((self.norm_part, norm_slots) if norm_slots else None), sample=nxt,
                       wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo),
                       **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}))
         if self._presample:
@@ -479,6 +509,8 @@ class FusedNatureLearner(IsNormMixin):
         this step's priority write-back, consumed by the next batch's global draw
         inside the optimizer launch) are exchanged while the conv backward runs; the
         conv bucket follows; the optimizer waits for all three."""
+        if self._fc_factors:
+            return self._dp_body_factors()
         cut = self.layout.offsets["wfc"]
         self._seg1()
         works = []
@@ -520,6 +552,73 @@ class FusedNatureLearner(IsNormMixin):
                 torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
         self._mark("allreduce_wait")
         self._seg3()
+
+    def _dp_body_factors(self) -> None:
+        """The data-parallel step with the factored fc-gradient exchange (see __init__):
+
+          compute stream                           comm stream (RCCL, in issue order)
+          forward, head, head wgrad + prio, pack
+          fc dgrad                           -->   all-gather (dH, X) rows of all ranks
+          conv backward, split-K finalize          all-reduce head gradient; shard stats
+                                             -->   all-reduce conv gradient (0.48 MB)
+          wait all-gather; fc wgrad over the W x rows gathered rows (+ clip-norm partials)
+          wait; clip-norm partials of the all-reduced regions; clip + RMSprop + next draw
+
+        The fc wgrad of the global batch runs while the conv all-reduce is in flight."""
+        cut = self.layout.offsets["wfc"]
+        o0 = self.layout.offsets["wv"]
+        o1 = self.layout.offsets["ba"] + self.A
+        self._seg1()
+        on_cuda = self.device.type == "cuda"
+        works = {}
+        fork = None
+        if on_cuda:
+            fork = torch.cuda.Event()
+            fork.record()
+
+        def issue_early():
+            # (after the fc dgrad is enqueued: the backward stays the fork's first child on
+            # the step's hardware queue, as in _dp_body)
+            ctx = torch.cuda.stream(self._fork_stream) if on_cuda else None
+            if on_cuda:
+                self._fork_stream.wait_event(fork)
+                ctx.__enter__()
+            try:
+                works["ag"] = self.coll.all_gather_into(self.fx_recv, self.fx_send)
+                works["head"] = self.coll.all_reduce(self.g32[o0:o1])
+                works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
+            finally:
+                if on_cuda:
+                    ctx.__exit__(None, None, None)
+
+        self._seg2(after_first=issue_early)
+        w_cv = self.coll.all_reduce(self.g32[:cut])
+        works["ag"].wait()
+        if on_cuda and not self._ordered_coll:
+            torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
+        self._mark("allgather_wait")
+        # the fc weight gradient of the global batch from the gathered rows (identical on
+        # every rank), with its clip-norm partials
+        R, sp = self.fx_recv, self.split
+        c = [0]
+        for w in self._fx_cols:
+            c.append(c[-1] + w)
+        cols = [R[:, c[i]:c[i + 1]] for i in range(len(self._fx_cols))]
+        dy, dy_lo, x, x_lo = (cols[0], cols[1], cols[2], cols[3]) if sp else (cols[0], None, cols[1], None)
+        nfc = self.ops.fc_wgrad(dy, x, self.G["wfc"], self.G["bfc"], norm=(self.norm_part, 0),
+                                **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
+        self._mark("fc_wgrad_global")
+        if self._ordered_coll:
+            w_cv.wait()          # RCCL runs the collectives in issue order: covers head + stats
+        else:
+            works["head"].wait()
+            works["stats"].wait()
+            w_cv.wait()
+            if on_cuda:
+                torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
+        self._mark("allreduce_wait")
+        nr = self.ops.sqnorm_ranges((self.g32[:cut], self.g32[o0:o1]), self.norm_part[nfc:], 64)
+        self._seg3(norm_slots=nfc + nr)
 
     def _body(self) -> None:
         if self._dp:

@@ -627,10 +627,15 @@ def _dense_wgrad_desc(dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, d
                       norm: Optional[Tuple[torch.Tensor, int]] = None, dy_lo=None, x_lo=None):
     M, Nc = dy.shape
     K = x.shape[1]
+    # row-strided operands (the gathered factor rows of the DP exchange: columns of one
+    # [rows][ld] buffer); a lo plane shares its hi plane's row stride
+    assert dy.stride(1) == 1 and x.stride(1) == 1
+    assert dy_lo is None or dy_lo.stride() == dy.stride()
+    assert x_lo is None or x_lo.stride() == x.stride()
     extra = {} if norm is None else dict(norm_part=norm[0].data_ptr(), norm_slot0=int(norm[1]))
     return _wg_desc(dy=dy.data_ptr(), x=x.data_ptr(), slab=dw_out.data_ptr(), bias_slab=db_out.data_ptr(),
-                    mode=0, Co=Nc, Kc=K, ldd=Nc, ldx=K, rows_per_split=M, Mred=M, dy_lo=_lib.ptr(dy_lo),
-                    x_lo=_lib.ptr(x_lo), **extra)
+                    mode=0, Co=Nc, Kc=K, ldd=dy.stride(0), ldx=x.stride(0), rows_per_split=M, Mred=M,
+                    dy_lo=_lib.ptr(dy_lo), x_lo=_lib.ptr(x_lo), **extra)
 
 
 def dense_wgrad(lib, dy: torch.Tensor, x: torch.Tensor, dw_out: torch.Tensor, db_out: torch.Tensor,

@@ -295,6 +295,21 @@ class TorchBackend:
     def gather_frames(self, replay, slots, out):
         replay.gather_frames(slots, out)
 
+    # ------------------------------------------- data-parallel gradient factors
+    def pack_rows(self, dst: torch.Tensor, segs) -> None:
+        """dst[:, c0:c0 + n] = seg for the 2-D ``segs`` laid side by side (same row count)."""
+        c0 = 0
+        for t in segs:
+            t2 = t.reshape(t.shape[0], -1)
+            dst[:t2.shape[0], c0:c0 + t2.shape[1]].copy_(t2)
+            c0 += t2.shape[1]
+
+    def sqnorm_ranges(self, ranges, partials: torch.Tensor, nblk: int) -> int:
+        """Squared-norm partials of the fp32 ``ranges`` into ``partials[:nblk]`` (the HIP
+        optimizer sums producer partials; the torch optimizer takes the norm of the whole
+        gradient itself: nothing to do).  Returns the slots written."""
+        return 0
+
 
 class HipBackend(TorchBackend):
     """MI355X backend: the hand-written gfx950 kernels (``kernels`` lists the op
@@ -545,6 +560,26 @@ class HipBackend(TorchBackend):
                                               float(eps), float(clip), int(centered), norm_out.data_ptr(), lo, *wn,
                                               st),
                    "rmsprop")
+
+    def pack_rows(self, dst: torch.Tensor, segs) -> None:
+        import ctypes
+        if dst.dtype not in (torch.bfloat16, torch.float16) or len(segs) > 4:
+            return super().pack_rows(dst, segs)
+        n = len(segs)
+        src = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in segs])
+        ld = (ctypes.c_int64 * 4)(*[t.stride(0) for t in segs])
+        cols = (ctypes.c_int * 4)(*[t.reshape(t.shape[0], -1).shape[1] for t in segs])
+        for t in segs:
+            assert t.dtype == dst.dtype and t.reshape(t.shape[0], -1).stride(1) == 1 and t.shape[0] == segs[0].shape[0]
+        _lib.check(self.lib.apex_pack_rows(ctypes.addressof(src), ctypes.addressof(ld), ctypes.addressof(cols), n,
+                                           int(segs[0].shape[0]), dst.data_ptr(), int(dst.stride(0)),
+                                           _lib.stream_ptr()), "pack_rows")
+
+    def sqnorm_ranges(self, ranges, partials: torch.Tensor, nblk: int) -> int:
+        (a, b) = (list(ranges) + [None])[:2]
+        _lib.check(self.lib.apex_sqnorm_ranges(a.data_ptr(), a.numel(), _lib.ptr(b), 0 if b is None else b.numel(),
+                                               partials.data_ptr(), int(nblk), _lib.stream_ptr()), "sqnorm_ranges")
+        return int(nblk)
 
     def cast_bf16(self, x32, hi, lo=None) -> None:
         """hi = bf16(x32) (and lo = bf16(x32 - hi)) with one kernel."""

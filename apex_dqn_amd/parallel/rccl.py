@@ -175,19 +175,25 @@ class _TorchWork:
 
 class _StreamWork:
     """Completion of a collective enqueued on the comm stream: ``wait`` makes the
-    current stream wait for it (a graph edge under capture).  The collectives of one
-    ``NativeCollectives`` run in order on one stream, so a join covers every op
-    enqueued before it: later waits with nothing new enqueued add no edge (each
-    cross-queue edge of a captured graph costs several microseconds)."""
+    current stream wait for an event recorded right after it (a graph edge under
+    capture), so a later collective still in flight is not waited for.  The
+    collectives of one ``NativeCollectives`` run in order on one stream, so a join
+    covers every op enqueued before it: a wait on an op already covered by an earlier
+    join adds no edge (each cross-queue edge of a captured graph costs several
+    microseconds)."""
 
     def __init__(self, coll: "NativeCollectives"):
         self.coll = coll
+        coll._seq += 1
+        self.seq = coll._seq
+        self.event = torch.cuda.Event()
+        self.event.record(coll.comm.stream)
 
     def wait(self) -> None:
         c = self.coll
-        if c._unjoined:
-            torch.cuda.current_stream(c.comm.device).wait_stream(c.comm.stream)
-            c._unjoined = False
+        if self.seq > c._joined:
+            torch.cuda.current_stream(c.comm.device).wait_event(self.event)
+            c._joined = self.seq
 
 
 class TorchCollectives:
@@ -230,12 +236,12 @@ class NativeCollectives:
 
     def __init__(self, comm: RcclComm):
         self.comm = comm
-        self._unjoined = False
+        self._seq = 0          # collectives enqueued
+        self._joined = 0       # the last one a join covers
 
     def _fork(self):
         cur = torch.cuda.current_stream(self.comm.device)
         self.comm.stream.wait_stream(cur)
-        self._unjoined = True
         return self.comm.stream
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):

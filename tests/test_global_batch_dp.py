@@ -22,11 +22,12 @@ CAP, FR = 300, 400
 BG, STEPS = 16, 3
 
 
-def _cfg(slack):
+def _cfg(slack, exchange="auto"):
     return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
                                  "Learner": {"replay_sample_size": BG, "q_target_sync_freq": 2},
                                  "Runtime": {"use_graphs": False, "grad_clip": 40.0, "force_dp": True,
-                                             "batch_scope": "global", "dp_batch_slack": slack}})
+                                             "batch_scope": "global", "dp_batch_slack": slack,
+                                             "dp_fc_exchange": exchange}})
 
 
 def _shard(rank):
@@ -57,14 +58,15 @@ def _concat(world):
     return rp
 
 
-def _worker(rank, world, concat, slack, path, q):
+def _worker(rank, world, concat, slack, path, q, exchange="auto"):
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.parallel.dist import Comm
     torch.set_num_threads(2)
     comm = Comm.init(rank, world, f"file://{path}", backend="gloo", force=True)
     torch.manual_seed(1234)          # identical initial parameters in every run
     rp = _concat(concat) if concat else _shard(rank)
-    L = FusedNatureLearner(_cfg(slack), "cpu", rp, comm=comm)
+    L = FusedNatureLearner(_cfg(slack, exchange), "cpu", rp, comm=comm)
+    assert L._fc_factors == (exchange != "allreduce")
     draws, grads = [], []
     p0 = L.p32.numpy().copy()
     for _ in range(STEPS):
@@ -78,12 +80,12 @@ def _worker(rank, world, concat, slack, path, q):
     comm.shutdown()
 
 
-def _run(world, concat, slack):
+def _run(world, concat, slack, exchange="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "store")
-        procs = [ctx.Process(target=_worker, args=(r, world, concat, slack, path, q)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, concat, slack, path, q, exchange)) for r in range(world)]
         for p in procs:
             p.start()
         res = [q.get(timeout=300) for _ in range(world)]
@@ -102,11 +104,13 @@ def test_dp_batch_rows():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world", [2, 4])
-def test_global_batch_dp_equals_one_rank(world):
+@pytest.mark.parametrize("world,exchange", [(2, "factors"), (4, "factors"), (2, "allreduce")])
+def test_global_batch_dp_equals_one_rank(world, exchange):
+    """``exchange``: the fc gradient as all-gathered factor rows (every rank forms the
+    global batch's gradient) or all-reduced -- both equal the one-rank update."""
     slack = 1.0
-    multi = _run(world, 0, slack)
-    one = _run(1, world, slack)[0]
+    multi = _run(world, 0, slack, exchange)
+    one = _run(1, world, slack, "allreduce")[0]
     rows = multi[0][1]
     assert rows == int(np.ceil(BG / world * (1 + slack))) + 2 and one[1] == BG
     # every update drew exactly BG samples over the shards, and one rank drew the same BG

@@ -70,7 +70,7 @@ def test_main_cli_gpu_mode(tmp_path):
     assert os.path.exists(os.path.join(str(tmp_path), "checkpoint.pt"))
 
 
-def _dp_gpu_worker(rank, world, path, q):
+def _dp_gpu_worker(rank, world, path, q, exchange="auto"):
     """One rank of a 2-process data-parallel learner sharing cuda:0 (gloo carries
     the CUDA-tensor all-reduces; RCCL refuses two ranks on one GPU).  Exercises the
     DP step exactly as on a node: three captured HIP-graph segments, async bucket
@@ -86,7 +86,7 @@ def _dp_gpu_worker(rank, world, path, q):
     comm = Comm.init(rank, world, f"file://{path}", backend="gloo", device=dev)
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
                                 "Learner": {"replay_sample_size": 128},
-                                "Runtime": {"use_graphs": True}})
+                                "Runtime": {"use_graphs": True, "dp_fc_exchange": exchange}})
     rp = GpuReplayShard(2000, 2000, 2600, 4, device=dev, seed=rank + 3)
     rng = np.random.default_rng(100 + rank)
     seqs = rp.append_frames(rng.integers(0, 255, (1200, 84, 84), dtype=np.uint8))
@@ -96,6 +96,7 @@ def _dp_gpu_worker(rank, world, path, q):
                    Gamma=np.full(K, 0.97, np.float32), priority=rng.random(K).astype(np.float32) + 0.01 * (rank + 1)))
     torch.manual_seed(1234 + rank)            # different local init: rank 0's params are broadcast
     L = FusedNatureLearner(cfg, dev, rp, comm=comm)
+    assert L._fc_factors == (exchange != "allreduce")
     for _ in range(4):
         L.step()
     torch.cuda.synchronize()
@@ -107,12 +108,16 @@ def _dp_gpu_worker(rank, world, path, q):
 
 
 @pytest.mark.gpu
-def test_dp_learner_two_ranks_on_one_gpu(tmp_path):
+@pytest.mark.parametrize("exchange", ["factors", "allreduce"])
+def test_dp_learner_two_ranks_on_one_gpu(tmp_path, exchange):
+    """Global-batch DP step (128 samples over two shards, 74 rows per rank) with the fc
+    gradient exchanged as all-gathered factor rows (HIP row pack, strided fc wgrad of
+    the gathered batch, clip-norm partials of the all-reduced regions) or all-reduced."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     path = str(tmp_path / "store")
-    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, path, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, path, q, exchange)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(2)]
@@ -122,6 +127,65 @@ def test_dp_learner_two_ranks_on_one_gpu(tmp_path):
     for rank, perr, finite, gnorm, ratio in res:
         assert perr == 0.0 and finite and gnorm > 0      # replicas bit-identical after 4 DP steps
     assert res[0][4] == res[1][4]                        # same shard statistics on both ranks
+
+
+def _forced_dp_worker(path, q, dtype):
+    """One process: the same update as a single-rank step and as the forced DP step
+    (world 1 process group, factored fc exchange), from identical state and batch."""
+    import numpy as np
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.parallel.dist import Comm
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comm = Comm.init(0, 1, f"file://{path}", backend="gloo", device=dev, force=True)
+    out = {}
+    for dp in (False, True):
+        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                    "Learner": {"replay_sample_size": 256},
+                                    "Runtime": {"use_graphs": False, "presample": True, "dtype": dtype,
+                                                "force_dp": dp, "dp_fc_exchange": "factors"}})
+        # the sharded draw at world 1 is the single-rank draw with the shard seed
+        # ((Runtime.seed << 20) ^ 0x5EED): the same seed here gives both runs one batch
+        rp = GpuReplayShard(4000, 4000, 4100, 4, device=dev, seed=0x5EED)
+        rng = np.random.default_rng(9)
+        seqs = rp.append_frames(rng.integers(0, 255, (3000, 84, 84), dtype=np.uint8))
+        K = 2800
+        st = np.stack([seqs[i:i + 4] for i in range(K)])
+        rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 6, K), R=rng.normal(size=K).astype(np.float32),
+                       Gamma=np.full(K, 0.97, np.float32), priority=rng.random(K).astype(np.float32) + 0.01))
+        torch.manual_seed(3)
+        L = FusedNatureLearner(cfg, dev, rp, comm=comm if dp else None)
+        assert L._fc_factors == dp
+        L.step()
+        L.step()
+        torch.cuda.synchronize()
+        out[dp] = (L.g32.cpu().numpy(), L.p32.cpu().numpy(), float(L.gnorm[0]))
+    comm.shutdown()
+    (g0, p0, n0), (g1, p1, n1) = out[False], out[True]
+    q.put((float(np.abs(g1 - g0).max()), float(np.abs(g0).max()), float(np.abs(p1 - p0).max()),
+           float(np.abs(p0).max()), n0, n1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_forced_dp_factored_step_matches_single_rank(tmp_path, dtype):
+    """The factored DP step on one rank (all-gather = copy) takes the single-rank update:
+    gradient, clip norm and parameters agree (the fc gradient runs on the strided
+    gathered rows instead of inside the fused fc + head + priority launch: summation
+    order only)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_forced_dp_worker, args=(str(tmp_path / "store"), q, dtype))
+    p.start()
+    gerr, gmax, perr, pmax, n0, n1 = q.get(timeout=300)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert gerr <= 1e-5 * gmax, (gerr, gmax)
+    assert abs(n1 - n0) <= 1e-5 * n0, (n0, n1)
+    assert perr <= 1e-6 * pmax + 1e-9, (perr, pmax)
 
 
 @pytest.mark.parametrize("hip,dtype,kind", [(True, "bf16", "impala"), (False, "bf16", "graph"),
