@@ -40,7 +40,7 @@ struct ConvDesc {
   int64_t w_cls_stride;
   const bf16_t* w2;           // weights for output rows >= m_switch (target network), or null
   const float* bias2;
-  int m_switch;               // multiple of 128 rows
+  int m_switch;               // first output row of the second weight set (any row: row_tile)
   // B operand stored K-major (bt != 0): element (k, n) at w + koff(cls, k/64) + (k%64)*ldb + n.
   // Lets the dgrad GEMMs read the natural weight tensors (no transposed / flipped copies):
   // bt = 1: koff from the table koff[cls * KT + kt]; bt = 2: koff = kt * 64 * ldb.
@@ -86,6 +86,28 @@ struct FwdRegs {
 // accumulator), and the epilogue writes the fp32 result as hi / lo bf16 planes
 // (ReLU applied in fp32 before the split: a ReLU on the lo plane alone would be
 // wrong; the dgrad mask zeroes both planes).
+// Row tiles of a launch whose rows >= m_switch use a second weight set (online /
+// target networks in one launch): [0, m_switch) and [m_switch, M) are tiled from their
+// own starts, so no tile straddles the switch and the weight set stays block-uniform;
+// rows past a segment's end read row 0 and are never stored.  With m_switch a
+// multiple of BM this is the plain tiling.  row_tiles() is the host-side tile count.
+struct RowTile {
+  int m0, mend;
+  bool second;
+};
+
+__device__ __forceinline__ RowTile row_tile(const ConvDesc& d, int bx, int BM, int M) {
+  if (d.w2 == nullptr) return RowTile{bx * BM, M, false};
+  const int t1 = (d.m_switch + BM - 1) / BM;
+  if (bx < t1) return RowTile{bx * BM, d.m_switch, false};
+  return RowTile{d.m_switch + (bx - t1) * BM, M, true};
+}
+
+static inline int row_tiles(const ConvDesc& d, int M, int BM) {
+  if (d.w2 == nullptr) return (M + BM - 1) / BM;
+  return (d.m_switch + BM - 1) / BM + (M - d.m_switch + BM - 1) / BM;
+}
+
 template <int MODE, bool PAD, bool BT, int OWC, int OHWC, int BM, bool SPLIT>
 __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   constexpr int AR = BM / 32;            // A rows staged per thread
@@ -116,10 +138,11 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
   const uint32_t OWv = OWC ? OWC : d.OW;
   const int M = d.N * OHW;
-  const int m0 = bx * BM;
+  const RowTile rt = row_tile(d, bx, BM, M);
+  const int m0 = rt.m0, mend = rt.mend;
   const int n0 = by * FWD_BN;
   // online / target weight sets in one launch: the switch row is block-uniform
-  const bool second = d.w2 != nullptr && m0 >= d.m_switch;
+  const bool second = rt.second;
   const bf16_t* __restrict__ wb = (second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride;
   const float* __restrict__ bias = second ? d.bias2 : d.bias;
   const int KT = d.K >> 6;
@@ -137,7 +160,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int m = m0 + srow + 32 * i;
-    const int mm = m < M ? m : 0;
+    const int mm = m < mend ? m : 0;
     if (MODE == 0) {
       a_off[i] = ((uint32_t)mm * d.K + sc * 8) * 2u;
       vmask[i] = 0;
@@ -331,7 +354,7 @@ __global__ void __launch_bounds__(256) igemm_fwd_kernel(ConvDesc d) {
   for (int p = 0; p < WR / 8; ++p) {
     const int row = 8 * p + (lane >> 3), ch = lane & 7;
     const int m = m0 + WR * wv + row;
-    if (m >= M) continue;
+    if (m >= mend) continue;
     uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
     uint4 vl = make_uint4(0, 0, 0, 0);
     if (SPLIT) vl = *reinterpret_cast<const uint4*>(El + epi_off(row, ch * 16));
@@ -401,9 +424,10 @@ __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
   const uint32_t OHW = OHWC ? OHWC : d.OH * d.OW;
   const uint32_t OWv = OWC ? OWC : d.OW;
   const int M = d.N * OHW;
-  const int m0 = bx * BM;
+  const RowTile rt = row_tile(d, bx, BM, M);
+  const int m0 = rt.m0, mend = rt.mend;
   const int n0 = by * FWD_BN;
-  const bool second = d.w2 != nullptr && m0 >= d.m_switch;
+  const bool second = rt.second;
   const uint8_t* wb = reinterpret_cast<const uint8_t*>((second ? d.w2 : d.w) + (int64_t)cls * d.w_cls_stride);
   const uint8_t* wl = SPLIT ? reinterpret_cast<const uint8_t*>((second ? d.w2_lo : d.w_lo) + (int64_t)cls * d.w_cls_stride)
                             : wb;
@@ -421,7 +445,7 @@ __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
     const int r = 8 * (wv + 4 * i) + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
     const int m = m0 + r;
-    const int mm = m < M ? m : 0;
+    const int mm = m < mend ? m : 0;
     if (MODE == 0) {
       a_off[i] = ((uint32_t)mm * d.K + c * 8) * 2u;
       vmask[i] = 0;
@@ -585,7 +609,7 @@ __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
   for (int p = 0; p < WR / 8; ++p) {
     const int row = 8 * p + (lane >> 3), ch = lane & 7;
     const int m = m0 + WR * wv + row;
-    if (m >= M) continue;
+    if (m >= mend) continue;
     uint4 v = *reinterpret_cast<const uint4*>(Es + epi_off(row, ch * 16));
     uint4 vl = make_uint4(0, 0, 0, 0);
     if (SPLIT) vl = *reinterpret_cast<const uint4*>(El + epi_off(row, ch * 16));
@@ -644,11 +668,12 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
   const int bx = (wg / ntn) % ntm;
   const int bz = wg / (ntn * ntm);
   const int M = d.N, Nc = d.Cout;
-  const int m0 = bx * BM, n0 = by * BN;
+  const RowTile rt = row_tile(d, bx, BM, M);
+  const int m0 = rt.m0, mend = rt.mend, n0 = by * BN;
   const int KT = d.K >> 6;
   const int kt0 = bz * kt_per;
   const int nk = min(KT, kt0 + kt_per) - kt0;     // >= 1 (host sizes the grid)
-  const bool second = d.w2 != nullptr && m0 >= d.m_switch;
+  const bool second = rt.second;
   const uint8_t* wb = reinterpret_cast<const uint8_t*>(second ? d.w2 : d.w);
   const uint8_t* wl = SPLIT ? reinterpret_cast<const uint8_t*>(second ? d.w2_lo : d.w_lo) : wb;
   const uint8_t* xa = reinterpret_cast<const uint8_t*>(d.x);
@@ -661,7 +686,7 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
   for (int i = 0; i < NA; ++i) {
     const int r = 8 * (wv + 4 * i) + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const int m = m0 + r < M ? m0 + r : 0;
+    const int m = m0 + r < mend ? m0 + r : 0;
     a_off[i] = ((uint32_t)m * d.K + c * 8) * 2u;
   }
 #pragma unroll
@@ -753,7 +778,7 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
     const int m = m0 + 64 * wm + 16 * mt + (lane & 15);
-    if (m >= M) continue;
+    if (m >= mend) continue;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int n = n0 + 64 * wn + 16 * nt + 4 * (lane >> 4);
@@ -981,7 +1006,7 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   if ((d.ldy & 7) || d.ldy < d.Cout) return (int)hipErrorInvalidValue;
   if ((int64_t)d.N * d.K * 2 >= 0x7ffffff0LL || (int64_t)d.Cout * d.K * 2 >= 0x7ffffff0LL)
     return (int)hipErrorInvalidValue;
-  if (d.w2 != nullptr && (d.m_switch % 128)) return (int)hipErrorInvalidValue;
+  if (d.w2 != nullptr && (d.m_switch < 0 || d.m_switch > d.N)) return (int)hipErrorInvalidValue;
   const bool split = d.x_lo != nullptr;
   if (split && (d.w_lo == nullptr || d.y_lo == nullptr || (d.w2 != nullptr && d.w2_lo == nullptr)))
     return (int)hipErrorInvalidValue;
@@ -989,7 +1014,7 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   const int kt_per = (KT + ksplit - 1) / ksplit;
   const int nz = (KT + kt_per - 1) / kt_per;
   if (ws == nullptr || ws_elems < (int64_t)nz * d.N * d.Cout) return (int)hipErrorInvalidValue;
-  const dim3 grid((d.N + 127) / 128, d.Cout / 128, nz);
+  const dim3 grid(row_tiles(d, d.N, 128), d.Cout / 128, nz);
   if (loader_waves) {
     if (split) fc_gemm128_kernel<true, 2, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
     else fc_gemm128_kernel<false, 4, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
@@ -1020,7 +1045,7 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   const int64_t xbytes = d.mode == 0 ? (int64_t)d.N * d.K * 2 : (int64_t)d.N * d.H * d.W * d.Cin * 2;
   if (xbytes >= 0x7ffffff0LL) return (int)hipErrorInvalidValue;
   if (d.mode == 1 && (d.pad_h > 0 || d.pad_w > 0) && d.KH * d.KW > 32) return (int)hipErrorInvalidValue;
-  if (d.w2 != nullptr && (d.m_switch % 128)) return (int)hipErrorInvalidValue;
+  if (d.w2 != nullptr && (d.m_switch < 0 || d.m_switch > d.N * d.OH * d.OW)) return (int)hipErrorInvalidValue;
   if (d.bt == 1 && (d.K >> 6) * (d.ncls > 0 ? d.ncls : 1) > 16) return (int)hipErrorInvalidValue;
   // split mode: every lo plane present (and the target set's when there is one)
   const bool split = d.x_lo != nullptr;
@@ -1040,7 +1065,7 @@ APEX_EXPORT int apex_conv_fwd(ConvDesc d, hipStream_t st) {
   if (d.tile_hint == 1) bm64 = false;
   if (d.tile_hint == 2) bm64 = true;
   if (d.order_hint == 0) d.order_hint = (d.mode == 0 && !d.bt && d.Cout >= 512) ? 2 : 1;
-  const dim3 g64((M + 63) / 64, d.Cout / FWD_BN, ncls), g128((M + 127) / 128, d.Cout / FWD_BN, ncls);
+  const dim3 g64(row_tiles(d, M, 64), d.Cout / FWD_BN, ncls), g128(row_tiles(d, M, 128), d.Cout / FWD_BN, ncls);
   // LDS-DMA kernel (scripts/bench_dma_gemm.py, learner shapes at batch 512, us):
   //   split: 64-row tiles, 2 stages (two blocks per CU) win everywhere -- fc fwd 39.6
   //     (register-staged 51.5), fc dgrad 17.9 (22.7), conv3 fwd 27.9 (32.0), conv3

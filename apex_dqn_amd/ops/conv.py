@@ -108,19 +108,20 @@ def _lo(x_lo=None, w_lo=None, w2_lo=None, out_lo=None) -> dict:
 
 
 def _second(w2, b2, rows_first, per_row):
-    """Descriptor fields for a second weight set on rows >= rows_first (images)."""
+    """Descriptor fields for a second weight set on rows >= rows_first (images); the
+    kernels tile the two row ranges separately (csrc/conv_mfma.hip row_tile), so the
+    switch may fall on any row."""
     if w2 is None:
         return {}
-    m_switch = rows_first * per_row
-    if m_switch % 128:
-        raise ValueError("online/target split must fall on a 128-row tile boundary")
-    return dict(w2=w2.data_ptr(), bias2=_lib.ptr(b2), m_switch=m_switch)
+    return dict(w2=w2.data_ptr(), bias2=_lib.ptr(b2), m_switch=rows_first * per_row)
 
 
-def _split_ok(w2, rows_first: int, per_row: int) -> bool:
-    """One launch can switch weight sets at rows_first only on a 128-row tile
-    boundary (the switch is block-uniform); otherwise the caller issues two."""
-    return w2 is None or (rows_first * per_row) % 128 == 0
+def row_tiles_host(M: int, m_switch: Optional[int], bm: int) -> int:
+    """Row tiles of a launch (csrc/conv_mfma.hip row_tiles): the rows before and after a
+    weight switch are tiled separately."""
+    if m_switch is None:
+        return -(-M // bm)
+    return -(-m_switch // bm) + -(-(M - m_switch) // bm)
 
 
 def _launch_fwd(lib, d) -> None:
@@ -315,18 +316,10 @@ def conv_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int
     N, H, W, Cin = x.shape
     Cout, KH, KW, _ = w.shape
     OH, OW = out.shape[1], out.shape[2]
-    split = x_lo is not None
     if SW.conv2_img and (H, W, Cin, Cout, KH, KW, stride) == (20, 20, 64, 64, 4, 4, 2) and \
             hasattr(lib, "apex_conv2_img_fwd"):
         conv2_img_fwd(lib, x, w, b, out, w2, b2, rows_first, x_lo=x_lo, w_lo=w_lo, w2_lo=w2_lo, out_lo=out_lo,
                       packed=packed)
-        return
-    if not _split_ok(w2, rows_first, OH * OW):   # batch not tile-aligned: one launch per weight set
-        r = rows_first
-        conv_fwd(lib, x[:r], w, b, stride, out[:r], x_lo=None if not split else x_lo[:r], w_lo=w_lo,
-                 out_lo=None if not split else out_lo[:r])
-        conv_fwd(lib, x[r:], w2, b2, stride, out[r:], x_lo=None if not split else x_lo[r:], w_lo=w2_lo,
-                 out_lo=None if not split else out_lo[r:])
         return
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=b.data_ptr(), y=out.data_ptr(), N=N, H=H, W=W,
                    Cin=Cin, OH=OH, OW=OW, Cout=Cout, KH=KH, KW=KW, stride=stride, mode=1, relu=1,
@@ -342,15 +335,6 @@ def dense_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], 
     M, K = x.shape
     Nc = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, Nc)
-    if not _split_ok(w2, rows_first, 1):         # batch not tile-aligned: one launch per weight set
-        r = rows_first
-        m1, m2 = (None, None) if mask is None else (mask[:r], mask[r:])
-        sp = x_lo is not None
-        dense_fwd(lib, x[:r], w, b, out[:r], relu, m1, ws=ws, x_lo=x_lo[:r] if sp else None, w_lo=w_lo,
-                  out_lo=out_lo[:r] if sp else None)
-        dense_fwd(lib, x[r:], w2, b2, out[r:], relu, m2, ws=ws, x_lo=x_lo[r:] if sp else None, w_lo=w2_lo,
-                  out_lo=out_lo[r:] if sp else None)
-        return
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), mask=_lib.ptr(mask),
                    N=M, Cin=K, Cout=Nc, mode=0, relu=relu and mask is None, K=K,
                    **_second(w2, b2, rows_first, 1), **_lo(x_lo, w_lo, w2_lo, out_lo))
@@ -373,8 +357,6 @@ def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Opti
     Nc = w.shape[0]
     assert w.shape[1] == K and out.shape == (M, Nc) and Nc % 128 == 0 and K % 64 == 0
     assert x.is_contiguous() and w.is_contiguous() and out.is_contiguous()
-    if w2 is not None and rows_first % 128:
-        raise ValueError("online/target split must fall on a 128-row tile boundary")
     kt = K // 64
     per = -(-kt // ksplit)
     nz = -(-kt // per)

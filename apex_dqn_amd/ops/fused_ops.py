@@ -377,13 +377,17 @@ class HipBackend(TorchBackend):
         if not self.native_conv:
             return super().fc_fwd(x, w, b, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
         M, K = x.shape[0], x[0].numel()
-        if w.shape[0] % 128 == 0 and K % 64 == 0 and (w2 is None or rows_first % 128 == 0) and \
-                hasattr(self.lib, "apex_fc_gemm128"):
+        if w.shape[0] % 128 == 0 and K % 64 == 0 and hasattr(self.lib, "apex_fc_gemm128"):
             # 128x128 tiles, K split in two, loader waves: fc forward 40.6 -> 36.2 us
             # (split) / 25.7 -> 22.5 (bf16) at the learner shape (scripts/bench_fc128.py)
             defer = defer_head and w2 is not None and b is not None and b2 is not None and \
                 2 * (M // 3) == rows_first and M % 3 == 0
-            r = C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, 2, True,
+            # K splits so the launch fills the chip: 2 at the learner's 1536 rows (96 tiles,
+            # 192 blocks), more for the few row tiles of a small per-rank batch (global-batch
+            # DP: 74 rows per rank -> 24 tiles x 10 splits)
+            tiles = C.row_tiles_host(M, rows_first if w2 is not None else None, 128) * (w.shape[0] // 128)
+            ks = max(2, 256 // max(tiles, 1))
+            r = C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, ks, True,
                                x_lo=None if x_lo is None else x_lo.reshape(M, K), w_lo=w_lo, w2_lo=w2_lo,
                                out_lo=out_lo, c2d_pack=None if defer else c2d, no_epilogue=defer)
             if defer:
