@@ -54,7 +54,10 @@ def _enable_sharding(replay, comm, rt, mcap: int = 0) -> None:
     """Turn the rank-local replay into one shard of the global replay (idempotent;
     ``mcap``: the cap on a draw's global batch, ``ApexConfig.dp_batch``)."""
     if not replay.sharded:
-        replay.enable_sharding(comm.rank, comm.world_size, shard_seed=(int(rt.seed) << 20) ^ 0x5EED,
+        # the global draw must use ONE seed on every rank (rank 0's Runtime.seed: the
+        # ranks may seed their local RNGs differently, e.g. bench.py's 1234 + rank)
+        seed0 = comm.broadcast_int(int(rt.seed)) if hasattr(comm, "broadcast_int") else int(rt.seed)
+        replay.enable_sharding(comm.rank, comm.world_size, shard_seed=(seed0 << 20) ^ 0x5EED,
                                group=comm.group, mcap=mcap)
     replay.shard_mcap = int(mcap)
     if not rt.use_is_weights:

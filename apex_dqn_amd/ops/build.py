@@ -88,6 +88,10 @@ def _digest(files: Sequence[str], extra: Sequence[str]) -> str:
     return h.hexdigest()
 
 
+def _rel_flag(f: str) -> str:
+    return f.replace(CSRC, "<csrc>").replace(PKG, "<pkg>")
+
+
 def read_stamp(lib_path: str) -> Optional[str]:
     """The build id compiled into a library (``APEX_BUILD_ID:<hex>``), read from the
     file without loading it; None if missing / unstamped."""
@@ -138,10 +142,13 @@ class _Plan:
         self.link_libs = list(link_libs)
         cid = compiler_id(cc)
         hdrs = sorted(hdrs)
+        # the checkout's absolute path (an include flag) is not content: the tree builds
+        # to the same keys wherever it is copied (a GPU box runs it from a scratch path)
+        kflags = [_rel_flag(f) for f in self.flags]
         self.objs = []
         for s in srcs:
             o = os.path.join(OUT, os.path.basename(s) + obj_suffix)
-            self.objs.append((s, o, _digest([s] + hdrs, self.flags + [cid])))
+            self.objs.append((s, o, _digest([s] + hdrs, kflags + [cid])))
         h = hashlib.sha256((BUILD_SCHEMA + tag).encode())
         for _, o, k in self.objs:
             h.update(os.path.basename(o).encode() + b"=" + k.encode())

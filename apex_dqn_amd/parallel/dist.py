@@ -157,6 +157,16 @@ class Comm:
         dist.all_gather(out, values.contiguous(), group=self.group)
         return torch.stack(out)
 
+    def broadcast_int(self, x: int, src: int = 0) -> int:
+        """Rank ``src``'s integer on every rank (int64)."""
+        if not self.active:
+            return int(x)
+        dev = self.device if (self.device is not None and dist.get_backend(self.group) == "nccl") \
+            else torch.device("cpu")
+        t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+        dist.broadcast(t, src=src, group=self.group)
+        return int(t.item())
+
     def allreduce_scalar(self, x: float, op: str = "sum") -> float:
         if not self.active:
             return float(x)

@@ -73,3 +73,19 @@ def test_kernel_library_header_edit_detected(tmp_path, monkeypatch):
     assert build.library_stale("kernels")
     lib = build.ensure_current("kernels")
     assert not build.library_stale("kernels") and _call(lib, "apex_probe_value") == 8
+
+
+def test_keys_do_not_depend_on_the_checkout_path(monkeypatch):
+    """The same sources under another absolute path (a GPU box runs the tree from a
+    scratch directory) build to the same keys: the shipped libraries stay current."""
+    ids = build.kernel_plan().build_id, build.runtime_plan().build_id
+    import shutil
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        csrc = os.path.join(td, "pkg", "csrc")
+        shutil.copytree(build.CSRC, csrc, ignore=shutil.ignore_patterns("__pycache__"))
+        monkeypatch.setattr(build, "CSRC", csrc)
+        monkeypatch.setattr(build, "PKG", os.path.dirname(csrc))
+        monkeypatch.setattr(build, "HIP_FLAGS", [csrc if f.endswith("/csrc") else f for f in build.HIP_FLAGS])
+        monkeypatch.setattr(build, "CXX_FLAGS", [csrc if f.endswith("/csrc") else f for f in build.CXX_FLAGS])
+        assert (build.kernel_plan().build_id, build.runtime_plan().build_id) == ids

@@ -22,10 +22,10 @@ CAP, FR = 300, 400
 BG, STEPS = 16, 3
 
 
-def _cfg(slack, exchange="auto"):
+def _cfg(slack, exchange="auto", seed=0):
     return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
                                  "Learner": {"replay_sample_size": BG, "q_target_sync_freq": 2},
-                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0, "force_dp": True,
+                                 "Runtime": {"use_graphs": False, "grad_clip": 40.0, "force_dp": True, "seed": seed,
                                              "batch_scope": "global", "dp_batch_slack": slack,
                                              "dp_fc_exchange": exchange}})
 
@@ -65,7 +65,8 @@ def _worker(rank, world, concat, slack, path, q, exchange="auto"):
     comm = Comm.init(rank, world, f"file://{path}", backend="gloo", force=True)
     torch.manual_seed(1234)          # identical initial parameters in every run
     rp = _concat(concat) if concat else _shard(rank)
-    L = FusedNatureLearner(_cfg(slack, exchange), "cpu", rp, comm=comm)
+    # per-rank Runtime.seed (as bench.py sets it): the draw's seed is rank 0's on every rank
+    L = FusedNatureLearner(_cfg(slack, exchange, seed=7 * rank), "cpu", rp, comm=comm)
     assert L._fc_factors == (exchange != "allreduce")
     draws, grads = [], []
     p0 = L.p32.numpy().copy()

@@ -97,13 +97,19 @@ def _dp_gpu_worker(rank, world, path, q, exchange="auto"):
     torch.manual_seed(1234 + rank)            # different local init: rank 0's params are broadcast
     L = FusedNatureLearner(cfg, dev, rp, comm=comm)
     assert L._fc_factors == (exchange != "allreduce")
+    drawn = []
     for _ in range(4):
+        if L._sample_ver != rp.version:
+            L._sample()
+        torch.cuda.synchronize()
+        drawn.append((int((L.S["weights"] > 0).sum()), int((L.S["gen"] >= 0).sum())))
         L.step()
     torch.cuda.synchronize()
     pl = [torch.zeros_like(L.p32) for _ in range(world)]
     torch.distributed.all_gather(pl, L.p32.clone())
     ok_finite = bool(torch.isfinite(L.p32).all())
-    q.put((rank, float((pl[0] - pl[1]).abs().max()), ok_finite, float(L.gnorm[0]), rp.shard_stats.cpu().tolist()))
+    q.put((rank, float((pl[0] - pl[1]).abs().max()), ok_finite, float(L.gnorm[0]), rp.shard_stats.cpu().tolist(),
+           drawn))
     comm.shutdown()
 
 
@@ -124,9 +130,15 @@ def test_dp_learner_two_ranks_on_one_gpu(tmp_path, exchange):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    for rank, perr, finite, gnorm, ratio in res:
+    res.sort(key=lambda r: r[0])
+    for rank, perr, finite, gnorm, ratio, _ in res:
         assert perr == 0.0 and finite and gnorm > 0      # replicas bit-identical after 4 DP steps
     assert res[0][4] == res[1][4]                        # same shard statistics on both ranks
+    # every update drew exactly the global batch over the two shards (rows with IS weight > 0
+    # = rows with a valid generation)
+    for t in range(4):
+        (w0, g0), (w1, g1) = res[0][5][t], res[1][5][t]
+        assert w0 == g0 and w1 == g1 and w0 + w1 == 128, (t, res[0][5], res[1][5])
 
 
 def _forced_dp_worker(path, q, dtype):
@@ -355,6 +367,7 @@ def test_bench_two_ranks_gloo_rehearsal():
                        cwd=ROOT)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     out = _bench_json(r.stdout)
+    print(r.stdout[-3000:])
     # default: one global 512-sample update per step (strong scaling), each rank computing
     # its share (290 rows at W = 2); the per-rank scope rides along as value_weak
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 512 and out["config"]["parallelism"] == "dp2"
