@@ -216,6 +216,9 @@ class FusedNatureLearner(IsNormMixin):
         self._dp_graphs = self._dp and cuda and self._backend_name() == "nccl"
         self._ordered_coll = self._dp and cuda and (self.coll.name == "native" or self._backend_name() == "nccl")
         self._fork_stream = torch.cuda.Stream(self.device) if (self._dp and cuda) else None
+        # single rank: the weight gradients beside the data-gradient chain (SW.bwd_branches)
+        self._branched = (not self._dp) and cuda and SW.bwd_branches
+        self._wg_stream = torch.cuda.Stream(self.device) if self._branched else None
         # the fc layer's split-K epilogue runs inside the head launch (ops.fc_fwd defer_head;
         # SW.fc_epi_in_head = False keeps the separate epilogue launch)
         self._defer_fc_epilogue = SW.fc_epi_in_head
@@ -227,11 +230,36 @@ class FusedNatureLearner(IsNormMixin):
         # mutations (eviction, rebuild) bump replay.version and force a fresh sample at
         # the head of t+1.
         self._presample = bool(self.rt.presample)
+        self._setup_spec()
         self._sample_ver = None
         self._setup_frag_out()
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
+
+    def _setup_spec(self) -> None:
+        """Speculative fc update (SW.spec_fc_opt, branched single-rank HIP step with the
+        producer-summed clip norm and pre-sampling): the fc layer -- the flat buffer's
+        3.2 M-parameter suffix [wfc, end) -- is updated as soon as its gradient exists, with
+        the clip coefficient taken as 1, beside the rest of the backward; the final
+        optimizer launch updates the prefix and, only when ||g|| > clip, redoes the fc
+        suffix from the saved state (bit-identical to the one-pass update either way)."""
+        mode = SW.spec_fc_opt
+        self._spec = None
+        if mode == "off" or not (self._branched and self._presample and self._fuse_norm
+                                 and getattr(self.replay, "use_hip", False)):
+            return
+        off = self.layout.offsets["wfc"]
+        nfc = self.layout.numel - off
+        where = mode if mode in ("side", "main") else ("main" if self.B >= 256 else "side")
+        bk = tuple(torch.zeros(nfc, dtype=torch.float32, device=self.device) for _ in range(3))
+        self._spec = dict(off=off, n=nfc, where=where, bk=bk)
+
+    def _spec_update(self) -> None:
+        sp, rt, o = self._spec, self.rt, self._spec["off"]
+        self.ops.spec_update(self.p32[o:], self.g32[o:], self.rms_v[o:], self.rms_m[o:], self.pbf[o:], rt.lr,
+                             rt.rms_decay, rt.rms_eps, rt.centered_rmsprop,
+                             None if self.pbf_lo is None else self.pbf_lo[o:], self._wnorm(), sp["bk"])
 
     def _setup_frag_out(self) -> None:
         """Split mode on the fused conv1 -> conv2 forward with pre-sampling: the optimizer +
@@ -389,6 +417,8 @@ class FusedNatureLearner(IsNormMixin):
                  isn=self._isn(), **self._lo(lo=sp and (self.h_lo[:2 * B], self.h_lo[2 * B:], self.dH_lo)))
         self._mark("head")
         prio = (self.replay, S["idx"], S["gen"], self.td_abs)
+        if getattr(self, "_branched", False):
+            return           # the weight gradients run on the branch stream (_seg2_branched)
         if getattr(self, "_fc_factors", False):
             # factored DP exchange: the head weight gradient + priority write-back now, the
             # fc weight gradient after the all-gather of every rank's (dH, X) rows (_dp_body)
@@ -496,15 +526,89 @@ class FusedNatureLearner(IsNormMixin):
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else
                       ((self.norm_part, norm_slots) if norm_slots else None), sample=nxt,
                       wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo),
-                      **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}))
+                      **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}),
+                      **self._spec_final_args())
         if self._presample:
             self._sample_ver = self.replay.version
         self._mark("optimizer")
 
+    def _seg2_branched(self) -> None:
+        """Backward with the weight gradients on a second stream (SW.bwd_branches): the
+        step's critical path is the data-gradient chain (fc dgrad -> conv3 dgrad -> conv2
+        dgrad -> conv1 wgrad); fc wgrad (+ head wgrad + priority write-back), conv3 wgrad
+        and conv2 wgrad need only its intermediate dY and run beside it -- in the captured
+        graph, a branch forked after the head and joined before the split-K finalisation.
+        Each main-stream kernel is enqueued before the branch work that waits on it, so the
+        chain stays the fork's first child (on the step's hardware queue)."""
+        B, rt, ops, G, Pb, Pl, S = self.B, self.rt, self.ops, self.G, self.Pb, self.Pl, self.S
+        sp = self.split
+        main, side = torch.cuda.current_stream(self.device), self._wg_stream
+        jobs = []
+        ev = torch.cuda.Event()
+        ev.record(main)
+        ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
+                     **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
+        side.wait_event(ev)
+        spec = self._spec
+        ev_fcw = torch.cuda.Event() if spec is not None else None
+        with torch.cuda.stream(side):
+            prio = (self.replay, S["idx"], S["gen"], self.td_abs)
+            nrm = (self.norm_part, 0) if self._fuse_norm else None
+            self._fc_slots = ops.fc_head_wgrad(self.dH, self.y3[:B], G["wfc"], G["bfc"], self.h, self.dhead, G,
+                                               prio, norm=nrm,
+                                               **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B],
+                                                          Hon_lo=self.h_lo))
+            if ev_fcw is not None:
+                ev_fcw.record(side)
+        ev3 = torch.cuda.Event()
+        ev3.record(main)
+        ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2,
+                       **self._lo(dy_lo=self.dY3_lo, w_lo=sp and Pl["w3"], dx_lo=self.dY2_lo))
+        side.wait_event(ev3)
+        with torch.cuda.stream(side):
+            if spec is not None and spec["where"] == "side":
+                self._spec_update()    # after the fc dgrad (ev3): it read the old fc weights
+            ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"], jobs=jobs,
+                           **self._lo(dy_lo=self.dY3_lo, x_lo=sp and self.y2_lo[:B]))
+        ev2 = torch.cuda.Event()
+        ev2.record(main)
+        ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1,
+                       **self._lo(dy_lo=self.dY2_lo, w_lo=sp and Pl["w2"], dx_lo=self.dY1_lo))
+        side.wait_event(ev2)
+        with torch.cuda.stream(side):
+            ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"], jobs=jobs,
+                           **self._lo(dy_lo=self.dY2_lo, x_lo=sp and self.y1_lo[:B]))
+        ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
+                             G["b1"], jobs=jobs, **self._lo(dy_lo=self.dY1_lo))
+        if spec is not None and spec["where"] == "main":
+            main.wait_event(ev_fcw)
+            self._spec_update()
+        main.wait_stream(side)
+        norm = dict(part=self.norm_part, slot0=self._fc_slots) if self._fuse_norm else None
+        self._npart = ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
+        self._mark("conv_backward")
+
+    def _spec_final_args(self) -> Dict[str, Any]:
+        """The final optimizer launch of a step whose fc suffix was updated speculatively:
+        the prefix only, plus the clip fix-up range (eager _seg2 steps never speculate)."""
+        sp = self._spec
+        if sp is None or not self._branched_step:
+            return {}
+        return dict(n_update=sp["off"], fix=(sp["bk"][0], sp["bk"][1], sp["bk"][2], sp["off"], sp["n"]))
+
+    _branched_step = False
+
     def _step_body(self) -> None:
         self._seg1()
-        self._seg2()
-        self._seg3()
+        if self._branched:
+            self._seg2_branched()
+        else:
+            self._seg2()
+        self._branched_step = self._branched
+        try:
+            self._seg3()
+        finally:
+            self._branched_step = False
 
     def _dp_body(self) -> None:
         """One data-parallel step (graph-capturable with RCCL): the fc/heads gradient
@@ -562,15 +666,13 @@ class FusedNatureLearner(IsNormMixin):
           compute stream                           comm stream (RCCL, in issue order)
           forward, head, head wgrad + prio, pack
           fc dgrad                           -->   all-gather (dH, X) rows of all ranks
-          conv backward, split-K finalize          all-reduce head gradient; shard stats
-                                             -->   all-reduce conv gradient (0.48 MB)
+          conv backward, split-K finalize          shard stats
+                                             -->   all-reduce conv + head gradients (0.48 MB)
           wait all-gather; fc wgrad over the W x rows gathered rows (+ clip-norm partials)
           wait; clip-norm partials of the all-reduced regions; clip + RMSprop + next draw
 
         The fc wgrad of the global batch runs while the conv all-reduce is in flight."""
-        cut = self.layout.offsets["wfc"]
-        o0 = self.layout.offsets["wv"]
-        o1 = self.layout.offsets["ba"] + self.A
+        cut = self.layout.offsets["wfc"]      # [0, cut): conv + head gradients (all-reduced)
         self._seg1()
         on_cuda = self.device.type == "cuda"
         works = {}
@@ -588,7 +690,6 @@ class FusedNatureLearner(IsNormMixin):
                 ctx.__enter__()
             try:
                 works["ag"] = self.coll.all_gather_into(self.fx_recv, self.fx_send)
-                works["head"] = self.coll.all_reduce(self.g32[o0:o1])
                 works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
             finally:
                 if on_cuda:
@@ -612,15 +713,14 @@ class FusedNatureLearner(IsNormMixin):
                                 **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
         self._mark("fc_wgrad_global")
         if self._ordered_coll:
-            w_cv.wait()          # RCCL runs the collectives in issue order: covers head + stats
+            w_cv.wait()          # RCCL runs the collectives in issue order: covers the stats
         else:
-            works["head"].wait()
             works["stats"].wait()
             w_cv.wait()
             if on_cuda:
                 torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
         self._mark("allreduce_wait")
-        nr = self.ops.sqnorm_ranges((self.g32[:cut], self.g32[o0:o1]), self.norm_part[nfc:], 64)
+        nr = self.ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[nfc:], 64)
         self._seg3(norm_slots=nfc + nr)
 
     def _body(self) -> None:

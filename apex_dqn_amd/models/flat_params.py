@@ -21,13 +21,17 @@ ALIGN = 64  # elements (256 B): every segment starts 16-B aligned for dwordx4 ac
 
 
 def nature_segments(C: int, A: int, c1: int = 64) -> List[Tuple[str, Tuple[int, ...]]]:
+    """Flat order: the small tensors (convs, heads) first, the 3.2 M-parameter fc layer
+    last, so the fc weights are one contiguous suffix: the data-parallel exchange treats
+    [0, wfc) and [wfc, end) as its two buckets and the single-rank step updates the fc
+    suffix early (learner/fused_learner.py)."""
     return [
         ("w1", (c1, C, 8, 8)), ("b1", (c1,)),
         ("w2", (64, 4, 4, c1)), ("b2", (64,)),
         ("w3", (64, 3, 3, 64)), ("b3", (64,)),
-        ("wfc", (1024, 3136)), ("bfc", (1024,)),
         ("wv", (512,)), ("bv", (1,)),
         ("wa", (A, 512)), ("ba", (A,)),
+        ("wfc", (1024, 3136)), ("bfc", (1024,)),
     ]
 
 

@@ -40,6 +40,15 @@ class Switches:
     opt_frags: bool = True
     # the fc layer's split-K epilogue runs inside the DDQN head launch
     fc_epi_in_head: bool = True
+    # single-rank step: the weight gradients (fc + heads + priority write-back, conv3,
+    # conv2) on a second stream beside the data-gradient chain (graph branches)
+    bwd_branches: bool = True
+    # with the branched backward: the fc layer's RMSprop update runs early, beside the
+    # backward, with the clip coefficient assumed 1 (redone exactly by the final optimizer
+    # launch when ||g|| > clip); "side" = after the fc wgrad on the branch stream, "main" =
+    # after conv1's wgrad, "auto" = main from 256 rows per rank up (the branch is then the
+    # longer chain), "off"
+    spec_fc_opt: str = "auto"
     # device-side image work queues in the persistent kernels: "auto" = only where RCCL's
     # kernels may hold CUs (the DP conv backward at world > 1), "on" / "off" force them
     work_queue: str = "auto"

@@ -469,3 +469,64 @@ def test_fc_head_wgrad_prio_matches_separate_launches(B):
     torch.testing.assert_close(a[6], b[6], rtol=1e-12, atol=1e-9)
     ref = dH.float().t() @ y3.float()
     torch.testing.assert_close(b[1], ref, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_branched_backward_matches_serial(monkeypatch, dtype):
+    """SW.bwd_branches: the weight gradients on a second stream beside the data-gradient
+    chain (a captured graph branch) give the same updates as the one-stream step --
+    the same kernels on the same inputs, only scheduled side by side."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.ops.switches import SW
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    res = {}
+    for br in (False, True):
+        monkeypatch.setattr(SW, "bwd_branches", br)
+        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                    "Learner": {"replay_sample_size": 128},
+                                    "Runtime": {"use_graphs": True, "graph_steps": 4, "dtype": dtype}})
+        torch.manual_seed(0)
+        rp = GpuReplayShard(4000, 4000, 4100, 4, device=DEV, seed=3)
+        _fill_replay(rp, 3800, seed=1)
+        L = FusedNatureLearner(cfg, DEV, rp, backend="hip")
+        assert L._branched == br
+        L.steps(6)
+        torch.cuda.synchronize()
+        res[br] = (L.g32.clone(), L.p32.clone(), rp.leaf.clone(), L.S["idx"].clone())
+    assert torch.equal(res[False][3], res[True][3])
+    for a, b in zip(res[False][:3], res[True][:3]):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("where,clip", [("side", 40.0), ("main", 40.0), ("side", 1e-4)])
+def test_speculative_fc_update_matches_one_pass(monkeypatch, where, clip):
+    """SW.spec_fc_opt: the fc layer updated early with the clip coefficient assumed 1
+    (old state saved), the final launch redoing it when ||g|| > clip -- the same
+    parameters and RMSprop state as the one-pass optimizer, with the clip inactive (40)
+    and active on every update (1e-4: the fix-up path)."""
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.ops.switches import SW
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    res = {}
+    for spec in ("off", where):
+        monkeypatch.setattr(SW, "spec_fc_opt", spec)
+        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                    "Learner": {"replay_sample_size": 128},
+                                    "Runtime": {"use_graphs": True, "graph_steps": 4, "grad_clip": clip}})
+        torch.manual_seed(0)
+        rp = GpuReplayShard(4000, 4000, 4100, 4, device=DEV, seed=3)
+        _fill_replay(rp, 3800, seed=1)
+        L = FusedNatureLearner(cfg, DEV, rp, backend="hip")
+        assert (L._spec is not None) == (spec != "off")
+        L.steps(6)
+        torch.cuda.synchronize()
+        res[spec] = (L.p32.clone(), L.rms_v.clone(), L.rms_m.clone(), L._pbf_all.clone(), L.S["idx"].clone(),
+                     float(L.gnorm[0]))
+    a, b = res["off"], res[where]
+    assert torch.equal(a[4], b[4])
+    if clip < 1.0:
+        assert a[5] > clip                  # the clip was active: the fix-up path ran
+    for x, y in zip(a[:4], b[:4]):
+        assert torch.equal(x, y)
