@@ -69,6 +69,10 @@ struct RmspropArgs {
 
 // one block `bid` of `nblk` (grid-stride over float4 chunks)
 __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int nblk) {
+  // no FMA contraction: every inlined copy of the update (steady loop, peeled chunk, the
+  // clip fix-up of a speculative update, other launches) rounds identically, so a
+  // speculative update redone by the fix-up is bit-identical to the one-pass update
+#pragma clang fp contract(off)
   float* __restrict__ p = A_.p;
   const float* __restrict__ g = A_.g;
   float* __restrict__ v = A_.v;

@@ -450,7 +450,11 @@ class FusedNatureLearner(IsNormMixin):
     def _seg2(self, after_first=None) -> None:
         """fc dgrad + conv backward (with DP, all of it overlaps the fc/heads bucket
         all-reduce): the dgrad chain, conv3/conv2 wgrad, conv1 wgrad last.
-        ``after_first``: called once the first kernel (fc dgrad) is enqueued."""
+        ``after_first``: called once the first kernel (fc dgrad) is enqueued.  The
+        single-rank branched step (SW.bwd_branches) runs :meth:`_seg2_branched`."""
+        if self._branched:
+            assert after_first is None
+            return self._seg2_branched()
         B, rt, ops, G, Pb, Pl = self.B, self.rt, self.ops, self.G, self.Pb, self.Pl
         sp = self.split
         jobs = []    # split-K reductions, finalised in ONE launch at the end
@@ -583,32 +587,27 @@ class FusedNatureLearner(IsNormMixin):
         if spec is not None and spec["where"] == "main":
             main.wait_event(ev_fcw)
             self._spec_update()
+        self._spec_pending = spec is not None   # the next _seg3 updates the prefix + fix-up
         main.wait_stream(side)
         norm = dict(part=self.norm_part, slot0=self._fc_slots) if self._fuse_norm else None
         self._npart = ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
         self._mark("conv_backward")
 
     def _spec_final_args(self) -> Dict[str, Any]:
-        """The final optimizer launch of a step whose fc suffix was updated speculatively:
-        the prefix only, plus the clip fix-up range (eager _seg2 steps never speculate)."""
+        """The final optimizer launch of a step whose fc suffix was updated speculatively
+        (by this step's _seg2_branched): the prefix only, plus the clip fix-up range."""
         sp = self._spec
-        if sp is None or not self._branched_step:
+        if sp is None or not self._spec_pending:
             return {}
+        self._spec_pending = False
         return dict(n_update=sp["off"], fix=(sp["bk"][0], sp["bk"][1], sp["bk"][2], sp["off"], sp["n"]))
 
-    _branched_step = False
+    _spec_pending = False
 
     def _step_body(self) -> None:
         self._seg1()
-        if self._branched:
-            self._seg2_branched()
-        else:
-            self._seg2()
-        self._branched_step = self._branched
-        try:
-            self._seg3()
-        finally:
-            self._branched_step = False
+        self._seg2()
+        self._seg3()
 
     def _dp_body(self) -> None:
         """One data-parallel step (graph-capturable with RCCL): the fc/heads gradient
