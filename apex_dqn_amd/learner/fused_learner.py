@@ -218,7 +218,10 @@ class FusedNatureLearner(IsNormMixin):
         self._fork_stream = torch.cuda.Stream(self.device) if (self._dp and cuda) else None
         # single rank: the weight gradients beside the data-gradient chain (SW.bwd_branches)
         self._branched = (not self._dp) and cuda and SW.bwd_branches
-        self._wg_stream = torch.cuda.Stream(self.device) if self._branched else None
+        # the DP step's backward on the same two chains, its collectives issued from the
+        # branch as their inputs complete (_dp_body_branched)
+        self._dp_branched = self._dp and cuda and SW.bwd_branches
+        self._wg_stream = torch.cuda.Stream(self.device) if (self._branched or self._dp_branched) else None
         # the fc layer's split-K epilogue runs inside the head launch (ops.fc_fwd defer_head;
         # SW.fc_epi_in_head = False keeps the separate epilogue launch)
         self._defer_fc_epilogue = SW.fc_epi_in_head
@@ -417,7 +420,7 @@ class FusedNatureLearner(IsNormMixin):
                  isn=self._isn(), **self._lo(lo=sp and (self.h_lo[:2 * B], self.h_lo[2 * B:], self.dH_lo)))
         self._mark("head")
         prio = (self.replay, S["idx"], S["gen"], self.td_abs)
-        if getattr(self, "_branched", False):
+        if getattr(self, "_branched", False) or getattr(self, "_dp_branched", False):
             return           # the weight gradients run on the branch stream (_seg2_branched)
         if getattr(self, "_fc_factors", False):
             # factored DP exchange: the head weight gradient + priority write-back now, the
@@ -615,6 +618,8 @@ class FusedNatureLearner(IsNormMixin):
         this step's priority write-back, consumed by the next batch's global draw
         inside the optimizer launch) are exchanged while the conv backward runs; the
         conv bucket follows; the optimizer waits for all three."""
+        if self._dp_branched:
+            return self._dp_body_branched()
         if self._fc_factors:
             return self._dp_body_factors()
         cut = self.layout.offsets["wfc"]
@@ -658,6 +663,95 @@ class FusedNatureLearner(IsNormMixin):
                 torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
         self._mark("allreduce_wait")
         self._seg3()
+
+    def _dp_body_branched(self) -> None:
+        """The data-parallel step on the branched backward (SW.bwd_branches):
+
+          main stream          fc dgrad -> conv3 dgrad -> conv2 dgrad -> conv1 wgrad -> finalize
+          branch stream        head wgrad + priorities (+ fc wgrad)  conv3 wgrad  conv2 wgrad
+          comm (RCCL, in order) fc factors all-gather (or fc bucket all-reduce) + shard
+                               stats, issued from the branch as soon as they exist;
+                               conv + head all-reduce after the split-K finalisation,
+                               [factors: the fc wgrad of the gathered rows beside it]
+
+        then the clip norm of the reduced gradient and the optimizer + next draw."""
+        B, rt, ops, G, Pb, Pl, S = self.B, self.rt, self.ops, self.G, self.Pb, self.Pl, self.S
+        sp = self.split
+        cut = self.layout.offsets["wfc"]
+        self._seg1()                      # forward + head (the weight gradients come below)
+        main, side = torch.cuda.current_stream(self.device), self._wg_stream
+        factors = self._fc_factors
+        jobs, works = [], {}
+        ev = torch.cuda.Event()
+        ev.record(main)
+        ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
+                     **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
+        side.wait_event(ev)
+        prio = (self.replay, S["idx"], S["gen"], self.td_abs)
+        with torch.cuda.stream(side):
+            if factors:
+                ops.head_wgrad(self.h, self.dhead, self._head_params(self.G), prio=prio, **self._lo(Hon_lo=self.h_lo))
+                segs = [self.dH, self.dH_lo, self.y3[:B].reshape(B, 3136), self.y3_lo[:B].reshape(B, 3136)] \
+                    if sp else [self.dH, self.y3[:B].reshape(B, 3136)]
+                ops.pack_rows(self.fx_send, segs)
+                works["fc"] = self.coll.all_gather_into(self.fx_recv, self.fx_send)
+            else:
+                ops.fc_head_wgrad(self.dH, self.y3[:B], G["wfc"], G["bfc"], self.h, self.dhead, G, prio,
+                                  **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B], Hon_lo=self.h_lo))
+                if self._comm_bf16:
+                    self.gcomm[cut:].copy_(self.g32[cut:])
+                works["fc"] = self.coll.all_reduce(self.gcomm[cut:])
+            works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
+        ev3 = torch.cuda.Event()
+        ev3.record(main)
+        ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2,
+                       **self._lo(dy_lo=self.dY3_lo, w_lo=sp and Pl["w3"], dx_lo=self.dY2_lo))
+        side.wait_event(ev3)
+        with torch.cuda.stream(side):
+            ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"], jobs=jobs,
+                           **self._lo(dy_lo=self.dY3_lo, x_lo=sp and self.y2_lo[:B]))
+        ev2 = torch.cuda.Event()
+        ev2.record(main)
+        ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1,
+                       **self._lo(dy_lo=self.dY2_lo, w_lo=sp and Pl["w2"], dx_lo=self.dY1_lo))
+        side.wait_event(ev2)
+        nfc = 0
+        with torch.cuda.stream(side):
+            ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"], jobs=jobs,
+                           **self._lo(dy_lo=self.dY2_lo, x_lo=sp and self.y1_lo[:B]))
+        ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
+                             G["b1"], jobs=jobs, **self._lo(dy_lo=self.dY1_lo))
+        main.wait_stream(side)
+        self._npart = ops.finalize_grads(jobs, None, None)
+        self._mark("conv_backward")
+        if self._comm_bf16:
+            self.gcomm[:cut].copy_(self.g32[:cut])
+        w_cv = self.coll.all_reduce(self.gcomm[:cut])
+        if factors:
+            # the fc weight gradient of the global batch from the gathered rows (identical
+            # on every rank, with its clip-norm partials), beside the conv all-reduce
+            # (waited for on the main stream: a wait on the branch inside a captured
+            # graph crashed the capture of the world-1 all-gather)
+            works["fc"].wait()
+            R, c = self.fx_recv, [0]
+            for w in self._fx_cols:
+                c.append(c[-1] + w)
+            cols = [R[:, c[i]:c[i + 1]] for i in range(len(self._fx_cols))]
+            dy, dy_lo, x, x_lo = (cols[0], cols[1], cols[2], cols[3]) if sp else (cols[0], None, cols[1], None)
+            nfc = ops.fc_wgrad(dy, x, G["wfc"], G["bfc"], norm=(self.norm_part, 0),
+                               **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
+        if self._ordered_coll:
+            w_cv.wait()          # RCCL runs the collectives in issue order: covers fc + stats
+        else:
+            works["fc"].wait()
+            works["stats"].wait()
+            w_cv.wait()
+        self._mark("allreduce_wait")
+        if factors:
+            nr = self.ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[nfc:], 64)
+            self._seg3(norm_slots=nfc + nr)
+        else:
+            self._seg3()         # (the optimizer's own clip-norm pass over the reduced gradient)
 
     def _dp_body_factors(self) -> None:
         """The data-parallel step with the factored fc-gradient exchange (see __init__):

@@ -46,9 +46,11 @@ class Switches:
     # with the branched backward: the fc layer's RMSprop update runs early, beside the
     # backward, with the clip coefficient assumed 1 (redone exactly by the final optimizer
     # launch when ||g|| > clip); "side" = after the fc wgrad on the branch stream, "main" =
-    # after conv1's wgrad, "auto" = main from 256 rows per rank up (the branch is then the
-    # longer chain), "off"
-    spec_fc_opt: str = "auto"
+    # after conv1's wgrad, "auto" = main from 256 rows per rank up, "off".  Measured slower
+    # everywhere (its 44 B / parameter of traffic competes with the backward kernels:
+    # 2,564 / 2,495 vs 2,640 steps/s at 512 rows, 5,750 / 5,757 vs 6,130 at 74,
+    # profiles/r4_ab_spec_fc_update.txt): off
+    spec_fc_opt: str = "off"
     # device-side image work queues in the persistent kernels: "auto" = only where RCCL's
     # kernels may hold CUs (the DP conv backward at world > 1), "on" / "off" force them
     work_queue: str = "auto"

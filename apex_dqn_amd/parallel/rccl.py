@@ -179,7 +179,7 @@ class _StreamWork:
     capture), so a later collective still in flight is not waited for.  The
     collectives of one ``NativeCollectives`` run in order on one stream, so a join
     covers every op enqueued before it: a wait on an op already covered by an earlier
-    join adds no edge (each cross-queue edge of a captured graph costs several
+    join of the same stream adds no edge (each cross-queue edge of a captured graph costs several
     microseconds)."""
 
     def __init__(self, coll: "NativeCollectives"):
@@ -191,9 +191,11 @@ class _StreamWork:
 
     def wait(self) -> None:
         c = self.coll
-        if self.seq > c._joined:
-            torch.cuda.current_stream(c.comm.device).wait_event(self.event)
-            c._joined = self.seq
+        cur = torch.cuda.current_stream(c.comm.device)
+        key = cur.cuda_stream
+        if self.seq > c._joined.get(key, 0):
+            cur.wait_event(self.event)
+            c._joined[key] = self.seq
 
 
 class TorchCollectives:
@@ -237,7 +239,7 @@ class NativeCollectives:
     def __init__(self, comm: RcclComm):
         self.comm = comm
         self._seq = 0          # collectives enqueued
-        self._joined = 0       # the last one a join covers
+        self._joined = {}      # per waiting stream: the last collective a join covers
 
     def _fork(self):
         cur = torch.cuda.current_stream(self.comm.device)

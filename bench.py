@@ -94,6 +94,7 @@ def make_learner(args, dtype, device, comm, rank, replay, scope=None):
                     "seed": 1234 + rank, "network": args.network, "dtype": dtype,
                     "presample": not args.no_presample, "force_dp": args.force_dp, "comm_backend": args.comm,
                     "batch_scope": scope or args.batch_scope, "allreduce_dtype": args.allreduce_dtype,
+                    "dp_fc_exchange": args.dp_fc_exchange,
                     **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
     })
     if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
@@ -195,6 +196,8 @@ def parser() -> argparse.ArgumentParser:
                          "update); per_rank = 512 rows per rank (weak scaling)")
     ap.add_argument("--no-scope-extra", action="store_true",
                     help="N > 1: skip measuring the other --batch-scope (value_weak / value_strong)")
+    ap.add_argument("--dp-fc-exchange", default="auto", choices=["auto", "factors", "allreduce"],
+                    help="DP exchange of the fc gradient (Runtime.dp_fc_exchange)")
     ap.add_argument("--allreduce-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="DP gradient all-reduce payload (Runtime.allreduce_dtype)")
     ap.add_argument("--force-dp", action="store_true",
@@ -288,6 +291,8 @@ def run(args) -> None:
                        "per_gpu_batch": args.batch if scope == "per_rank" else round(args.batch / world, 2),
                        "per_rank_rows": rows,
                        "allreduce_dtype": args.allreduce_dtype if dp else None,
+                       "dp_fc_exchange": ("factors" if getattr(learner, "_fc_factors", False) else "allreduce")
+                       if dp else None,
                        "replay_per_gpu": args.replay,
                        "learner": kind + ("/" + ops.name if ops is not None and args.learner == "fused" else
                                           "/torch-autograd"),
