@@ -127,7 +127,8 @@ class RuntimeConf:
                                     # gradient) | "factors" (all-gather every rank's dH / fc-input rows -- the
                                     # operands the kernels use -- and form the gradient of the whole global
                                     # batch on each rank: ~(B_total x 4160) values instead of 3.2 M, exact and
-                                    # bit-identical across ranks) | "auto" (factors while W x rows <= 1024)
+                                    # bit-identical across ranks) | "auto" (factors while 1 < W and W x rows
+                                    # <= 1024)
     replica_check_every: int = 5000  # DP: learner steps between replica checksum checks (0 = off)
     step_timeout: float = 300.0     # GPU loop watchdog: seconds a queued learner chunk may take
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread

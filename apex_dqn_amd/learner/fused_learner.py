@@ -177,10 +177,13 @@ class FusedNatureLearner(IsNormMixin):
         # same kernel in the same order: W x rows x (1024 + 3136) values move instead of the
         # 3.2 M-float gradient (a global-batch step at W = 8: 1.2 MB sent per rank vs 12.9 MB
         # all-reduced), the result is bit-identical on every rank, and only the conv and
-        # head gradients (0.48 MB) are all-reduced.  "auto": factors while W x rows <= 1024.
+        # head gradients (0.48 MB) are all-reduced.  "auto": factors while W x rows <= 1024
+        # and W > 1 (at world 1 -- the forced-DP rehearsal -- there is no traffic to save and
+        # the all-gather, separate head wgrad and pack cost ~20 us more than the copy-like
+        # all-reduce: 2,319 vs 2,441 steps/s, profiles/r4_bench_forced_dp_*).
         mode = self.rt.dp_fc_exchange
         self._fc_factors = self._dp and not self._comm_bf16 and (
-            mode == "factors" or (mode == "auto" and self.world * self.B <= 1024))
+            mode == "factors" or (mode == "auto" and 1 < self.world and self.world * self.B <= 1024))
         if self._fc_factors:
             planes = 2 if self.split else 1
             self._fx_cols = [1024] * planes + [3136] * planes      # [dH | dH lo | X | X lo]
