@@ -56,8 +56,7 @@ APEX_EXPORT int apex_rmsprop_step(float* p, const float* g, float* v, float* m, 
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, NPART, lr, alpha, eps, clip, centered,
-                                                 norm_out, pb_lo, wnorm, wn, wstride, CfFragOut{}, nullptr,
-                                                 nullptr, nullptr, 0, 0});
+                                                 norm_out, pb_lo, wnorm, wn, wstride, CfFragOut{}});
   APEX_CHECK_LAUNCH();
 }
 
@@ -72,29 +71,7 @@ APEX_EXPORT int apex_rmsprop_step_np(float* p, const float* g, float* v, float* 
   int nb = (int)((n / 4 + 255) / 256);
   nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
   rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, partials, npart, lr, alpha, eps, clip, centered,
-                                                 norm_out, pb_lo, wnorm, wn, wstride, CfFragOut{}, nullptr,
-                                                 nullptr, nullptr, 0, 0});
-  APEX_CHECK_LAUNCH();
-}
-
-// Speculative update of a parameter range (the fc suffix) with the clip coefficient
-// taken as 1 (only the batch-max IS scale applied): the old p / v / m go to bk_* first,
-// so the final optimizer launch can redo the range exactly if the global norm turns
-// out above the clip (apex_rmsprop_sample fix_off / fix_n).  Pointers are the range's.
-APEX_EXPORT int apex_rmsprop_spec(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n, float lr,
-                                  float alpha, float eps, int centered, bf16_t* pb_lo, const double* wnorm, int wn,
-                                  int wstride, float* bk_p, float* bk_v, float* bk_m, hipStream_t st) {
-  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
-  if (((uintptr_t)bk_p | (uintptr_t)bk_v | (uintptr_t)bk_m) & 15 || bk_p == nullptr || bk_v == nullptr ||
-      bk_m == nullptr || (n & 3))
-    return (int)hipErrorInvalidValue;
-  if (((uintptr_t)pb | (uintptr_t)pb_lo) & 7) return (int)hipErrorInvalidValue;
-  int nb = (int)((n / 4 + 255) / 256);
-  nb = nb < 1 ? 1 : (nb > 2048 ? 2048 : nb);
-  // no partials: the clip coefficient is 1 (times the IS scale); clip > 0 is irrelevant here
-  rmsprop_kernel<<<nb, 256, 0, st>>>(RmspropArgs{p, g, v, m, pb, n, nullptr, 0, lr, alpha, eps, 0.f, centered,
-                                                 nullptr, pb_lo, wnorm, wn, wstride, CfFragOut{}, bk_p, bk_v, bk_m,
-                                                 0, 0});
+                                                 norm_out, pb_lo, wnorm, wn, wstride, CfFragOut{}});
   APEX_CHECK_LAUNCH();
 }
 

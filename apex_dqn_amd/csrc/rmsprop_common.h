@@ -57,21 +57,12 @@ struct RmspropArgs {
   const double* wnorm;  // batch-max IS normalisation (is_grad_scale), or null
   int wn, wstride;
   CfFragOut fo;         // the fused forward's online operands in fragment order (w1frag null: off)
-  // speculative fc update (learner/fused_learner.py _spec): the fc suffix of the flat
-  // parameters is updated early with the clip coefficient assumed 1 (clipping is inactive
-  // unless ||g|| > clip), its old state saved in bk_* first; the final launch, which knows
-  // the norm, redoes [fix_off, fix_off + fix_n) from bk_* when the clip is active.
-  float* bk_p;          // spec launch: old p / v / m of the range written here (null: off)
-  float* bk_v;
-  float* bk_m;
-  int64_t fix_off, fix_n;   // final launch: the range to redo from bk_* if clipping (0: none)
 };
 
 // one block `bid` of `nblk` (grid-stride over float4 chunks)
 __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int nblk) {
   // no FMA contraction: every inlined copy of the update (steady loop, peeled chunk, the
-  // clip fix-up of a speculative update, other launches) rounds identically, so a
-  // speculative update redone by the fix-up is bit-identical to the one-pass update
+  // other launches) rounds identically
 #pragma clang fp contract(off)
   float* __restrict__ p = A_.p;
   const float* __restrict__ g = A_.g;
@@ -90,10 +81,6 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
   float4* m4 = reinterpret_cast<float4*>(m);
   uint2* pb4 = reinterpret_cast<uint2*>(pb);
   uint2* pbl4 = reinterpret_cast<uint2*>(pbl);
-  float4* bkp4 = reinterpret_cast<float4*>(A_.bk_p);
-  float4* bkv4 = reinterpret_cast<float4*>(A_.bk_v);
-  float4* bkm4 = reinterpret_cast<float4*>(A_.bk_m);
-  const bool save = bkp4 != nullptr && A_.fix_n == 0;    // the speculative launch
   const int64_t stride = (int64_t)nblk * blockDim.x;
   int64_t i = (int64_t)bid * blockDim.x + threadIdx.x;
   // the first chunk's loads are in flight while the block sums the clip-norm
@@ -122,11 +109,6 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
         var = vx[j] - mx[j] * mx[j];
       }
       px[j] -= lr * gx[j] / (sqrtf(fmaxf(var, 0.f)) + eps);
-    }
-    if (save) {                // speculative update: keep the old state for a clip fix-up
-      bkp4[i] = pp;
-      bkv4[i] = vv;
-      if (centered) bkm4[i] = mm;
     }
     p4[i] = make_float4(px[0], px[1], px[2], px[3]);
     v4[i] = make_float4(vx[0], vx[1], vx[2], vx[3]);
@@ -165,17 +147,6 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
     }
     update(i, gg, pp, vv, mm, false);
     gg = gn; pp = pn; vv = vn; mm = mn;
-  }
-  // clip fix-up of a speculatively updated range (rare: ||g|| > clip): redo it from the
-  // saved state with the real coefficient (the same arithmetic as the update above)
-  if (A_.fix_n > 0 && A_.clip > 0.f && A_.clip / (sh[1] + 1e-6f) < 1.0f) {
-    const int64_t f0 = A_.fix_off / 4, fn4 = A_.fix_n / 4;
-    const float4* ob = reinterpret_cast<const float4*>(A_.bk_p);
-    const float4* ov = reinterpret_cast<const float4*>(A_.bk_v);
-    const float4* om = reinterpret_cast<const float4*>(A_.bk_m);
-    for (int64_t k = (int64_t)bid * blockDim.x + threadIdx.x; k < fn4; k += stride) {
-      update(f0 + k, g4[f0 + k], ob[k], ov[k], centered ? om[k] : z4, false);
-    }
   }
   for (int64_t i = n4 * 4 + (int64_t)bid * blockDim.x + threadIdx.x; i < n; i += (int64_t)nblk * blockDim.x) {
     float gg = g[i] * coef;

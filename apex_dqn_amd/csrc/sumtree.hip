@@ -658,7 +658,7 @@ APEX_EXPORT int apex_fill16(void* p, int64_t n, int nt, hipStream_t st) {
   APEX_CHECK_LAUNCH();
 }
 
-APEX_EXPORT int apex_abi_version() { return 4; }
+APEX_EXPORT int apex_abi_version() { return 5; }
 
 // 1 if this library was built with -DAPEX_DEBUG_BOUNDS
 APEX_EXPORT int apex_debug_bounds_enabled() {
@@ -703,14 +703,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
                                     uint64_t shard_seed, float* out_wscale, int64_t mcap, bf16_t* pb_lo,
-                                    const double* wnorm, int wn, int wstride, CfFragOut fo, float* bk_p,
-                                    float* bk_v, float* bk_m, int64_t fix_off, int64_t fix_n, hipStream_t st) {
-  // fix_n > 0: [fix_off, fix_off + fix_n) was updated speculatively (apex_rmsprop_spec);
-  // redone here from bk_* if the clip is active.  It must lie beyond the range updated here.
-  if (fix_n > 0 && (bk_p == nullptr || bk_v == nullptr || bk_m == nullptr || fix_off < n || (fix_off & 3) ||
-                    (fix_n & 3) || (((uintptr_t)bk_p | (uintptr_t)bk_v | (uintptr_t)bk_m) & 15)))
-    return (int)hipErrorInvalidValue;
-  if (mcap <= 0) mcap = (int64_t)shard_world * B;
+                                    const double* wnorm, int wn, int wstride, CfFragOut fo, hipStream_t st) {
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
@@ -730,8 +723,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                (fo.w1_off + 4096LL * fo.C) / 4 > (int64_t)nb * nt || (fo.w2_off + 65536) / 4 > (int64_t)nb * nt))
     return (int)hipErrorInvalidValue;
   const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,
-                      wnorm, wn, wstride, fo, fix_n > 0 ? bk_p : nullptr, bk_v, bk_m, fix_off,
-                      fix_n > 0 ? fix_n : 0};
+                      wnorm, wn, wstride, fo};
   const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
                       out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed,
                       out_wscale, mcap};

@@ -236,36 +236,11 @@ class FusedNatureLearner(IsNormMixin):
         # mutations (eviction, rebuild) bump replay.version and force a fresh sample at
         # the head of t+1.
         self._presample = bool(self.rt.presample)
-        self._setup_spec()
         self._sample_ver = None
         self._setup_frag_out()
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
-
-    def _setup_spec(self) -> None:
-        """Speculative fc update (SW.spec_fc_opt, branched single-rank HIP step with the
-        producer-summed clip norm and pre-sampling): the fc layer -- the flat buffer's
-        3.2 M-parameter suffix [wfc, end) -- is updated as soon as its gradient exists, with
-        the clip coefficient taken as 1, beside the rest of the backward; the final
-        optimizer launch updates the prefix and, only when ||g|| > clip, redoes the fc
-        suffix from the saved state (bit-identical to the one-pass update either way)."""
-        mode = SW.spec_fc_opt
-        self._spec = None
-        if mode == "off" or not (self._branched and self._presample and self._fuse_norm
-                                 and getattr(self.replay, "use_hip", False)):
-            return
-        off = self.layout.offsets["wfc"]
-        nfc = self.layout.numel - off
-        where = mode if mode in ("side", "main") else ("main" if self.B >= 256 else "side")
-        bk = tuple(torch.zeros(nfc, dtype=torch.float32, device=self.device) for _ in range(3))
-        self._spec = dict(off=off, n=nfc, where=where, bk=bk)
-
-    def _spec_update(self) -> None:
-        sp, rt, o = self._spec, self.rt, self._spec["off"]
-        self.ops.spec_update(self.p32[o:], self.g32[o:], self.rms_v[o:], self.rms_m[o:], self.pbf[o:], rt.lr,
-                             rt.rms_decay, rt.rms_eps, rt.centered_rmsprop,
-                             None if self.pbf_lo is None else self.pbf_lo[o:], self._wnorm(), sp["bk"])
 
     def _setup_frag_out(self) -> None:
         """Split mode on the fused conv1 -> conv2 forward with pre-sampling: the optimizer +
@@ -536,8 +511,7 @@ class FusedNatureLearner(IsNormMixin):
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else
                       ((self.norm_part, norm_slots) if norm_slots else None), sample=nxt,
                       wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo),
-                      **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}),
-                      **self._spec_final_args())
+                      **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}))
         if self._presample:
             self._sample_ver = self.replay.version
         self._mark("optimizer")
@@ -559,8 +533,6 @@ class FusedNatureLearner(IsNormMixin):
         ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
                      **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
         side.wait_event(ev)
-        spec = self._spec
-        ev_fcw = torch.cuda.Event() if spec is not None else None
         with torch.cuda.stream(side):
             prio = (self.replay, S["idx"], S["gen"], self.td_abs)
             nrm = (self.norm_part, 0) if self._fuse_norm else None
@@ -568,16 +540,12 @@ class FusedNatureLearner(IsNormMixin):
                                                prio, norm=nrm,
                                                **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B],
                                                           Hon_lo=self.h_lo))
-            if ev_fcw is not None:
-                ev_fcw.record(side)
         ev3 = torch.cuda.Event()
         ev3.record(main)
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2,
                        **self._lo(dy_lo=self.dY3_lo, w_lo=sp and Pl["w3"], dx_lo=self.dY2_lo))
         side.wait_event(ev3)
         with torch.cuda.stream(side):
-            if spec is not None and spec["where"] == "side":
-                self._spec_update()    # after the fc dgrad (ev3): it read the old fc weights
             ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"], jobs=jobs,
                            **self._lo(dy_lo=self.dY3_lo, x_lo=sp and self.y2_lo[:B]))
         ev2 = torch.cuda.Event()
@@ -590,25 +558,10 @@ class FusedNatureLearner(IsNormMixin):
                            **self._lo(dy_lo=self.dY2_lo, x_lo=sp and self.y1_lo[:B]))
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"], jobs=jobs, **self._lo(dy_lo=self.dY1_lo))
-        if spec is not None and spec["where"] == "main":
-            main.wait_event(ev_fcw)
-            self._spec_update()
-        self._spec_pending = spec is not None   # the next _seg3 updates the prefix + fix-up
         main.wait_stream(side)
         norm = dict(part=self.norm_part, slot0=self._fc_slots) if self._fuse_norm else None
         self._npart = ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
         self._mark("conv_backward")
-
-    def _spec_final_args(self) -> Dict[str, Any]:
-        """The final optimizer launch of a step whose fc suffix was updated speculatively
-        (by this step's _seg2_branched): the prefix only, plus the clip fix-up range."""
-        sp = self._spec
-        if sp is None or not self._spec_pending:
-            return {}
-        self._spec_pending = False
-        return dict(n_update=sp["off"], fix=(sp["bk"][0], sp["bk"][1], sp["bk"][2], sp["off"], sp["n"]))
-
-    _spec_pending = False
 
     def _step_body(self) -> None:
         self._seg1()

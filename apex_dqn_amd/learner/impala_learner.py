@@ -39,6 +39,7 @@ from ..models.flat_params import FlatLayout
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
 from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
+from ..ops.switches import SW
 from .fused_learner import _enable_sharding, dp_layout
 from .is_norm import IsNormMixin
 
@@ -163,6 +164,9 @@ class FusedImpalaLearner(IsNormMixin):
         # cost more than the overlap); the head kernel writes the priorities back and
         # the optimizer launch draws the next batch (Runtime.presample)
         self._side = None
+        # the conv weight gradients beside the data-gradient chain (SW.bwd_branches, one rank)
+        self._wg_stream = torch.cuda.Stream(self.device) if (on_gpu and SW.impala_bwd_branches and self.world == 1) \
+            else None
         self._presample = bool(self.rt.presample)
         self._sample_ver = None
         self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
@@ -382,7 +386,11 @@ class FusedImpalaLearner(IsNormMixin):
         self._sample_ver = self.replay.version
 
     def _seg2(self) -> None:
-        """fc data gradient, then the three stacks backwards."""
+        """fc data gradient, then the three stacks backwards.  With the branched backward
+        (SW.bwd_branches, one rank on a GPU) the 15 conv weight gradients run on a second
+        stream, each after the data gradient it reads (an event per wgrad), beside the
+        data-gradient chain that is the step's critical path; joined before the split-K
+        finalisation (SW.impala_bwd_branches: off, measured no gain)."""
         B, io, G = self.B, self.iops, self.G
         sp = self.split
         self.ops.fc_dgrad(self.dH, self.feat[:B], self.Pb["wfc"], self.dfeat,
@@ -390,31 +398,46 @@ class FusedImpalaLearner(IsNormMixin):
         if sp:
             io.merge(self.dfeat, self.dfeat_lo, self.dfeat32)
         jobs: list = []
+        side = self._wg_stream
+        if side is not None:
+            main = torch.cuda.current_stream(self.device)
+            wgrad0 = io.wgrad
+
+            def wgrad(*a, **kw):
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+                with torch.cuda.stream(side):
+                    wgrad0(*a, **kw)
+        else:
+            wgrad = io.wgrad
         dO = self.dfeat32[:, :FEAT].view(B, 2, 11, 11, 16)
         for s in (2, 1, 0):
             f, b = self.fw[s], self.bw[s]
             c0, r0a, r0b, r1a, r1b = self.specs[s]
             gw = lambda cs: (G[cs.name + ".w"], G[cs.name + ".b"])  # noqa: E731
             io.conv(dO, r1b, b["d_yb"], transpose=True, mask=f["yb"][:B])
-            io.wgrad(dO, f["yb"][:B], r1b, *gw(r1b), jobs, relu_in=True)
+            wgrad(dO, f["yb"][:B], r1b, *gw(r1b), jobs, relu_in=True)
             io.conv(b["d_yb"], r1a, b["d_ra"], transpose=True, mask=f["ra"][:B], add=dO)
-            io.wgrad(b["d_yb"], f["ra"][:B], r1a, *gw(r1a), jobs, relu_in=True)
+            wgrad(b["d_yb"], f["ra"][:B], r1a, *gw(r1a), jobs, relu_in=True)
             io.conv(b["d_ra"], r0b, b["d_ya"], transpose=True, mask=f["ya"][:B])
-            io.wgrad(b["d_ra"], f["ya"][:B], r0b, *gw(r0b), jobs, relu_in=True)
+            wgrad(b["d_ra"], f["ya"][:B], r0b, *gw(r0b), jobs, relu_in=True)
             io.conv(b["d_ya"], r0a, b["d_p"], transpose=True, mask=f["p"][:B], add=b["d_ra"])
-            io.wgrad(b["d_ya"], f["p"][:B], r0a, *gw(r0a), jobs, relu_in=True)
+            wgrad(b["d_ya"], f["p"][:B], r0a, *gw(r0a), jobs, relu_in=True)
             # max-pool backward (gather form, csrc/impala.hip maxpool_bwd_kernel); staging
             # it inside the two consumers measured slower (round 1) and was removed
             io.maxpool_bwd(b["d_p"], f["amax"][:B], b["d_c0"])
             dc = b["d_c0"]
             if s == 0:
-                io.wgrad(dc, None, c0, *gw(c0), jobs, ring=self.replay.frames, slots=self.slots[:B],
+                wgrad(dc, None, c0, *gw(c0), jobs, ring=self.replay.frames, slots=self.slots[:B],
                          scale=self.rt.obs_scale)
             else:
                 prev = self.fw[s - 1]["o"][:B]
-                io.wgrad(dc, prev, c0, *gw(c0), jobs)
+                wgrad(dc, prev, c0, *gw(c0), jobs)
                 dO = self.bw[s - 1]["d_o"]
                 io.conv(dc, c0, dO, transpose=True)
+        if side is not None:
+            main.wait_stream(side)
         io.finalize(jobs)
 
     def _seg3(self) -> None:

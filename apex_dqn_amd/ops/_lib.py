@@ -147,10 +147,7 @@ _SIGS = {
                         c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, IsNorm, c_p], c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut,
-                             c_p, c_p, c_p, c_i64, c_i64, c_p], c_i),
-    "apex_rmsprop_spec": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_i, c_p, c_p, c_i, c_i, c_p, c_p, c_p,
-                           c_p], c_i),
+                             c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut, c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
                               c_p, c_p, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,
@@ -183,7 +180,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     conv_sigs.declare(lib)
 
 
-ABI_VERSION = 4      # csrc/sumtree.hip apex_abi_version(): the launchers' argument lists
+ABI_VERSION = 5      # csrc/sumtree.hip apex_abi_version(): the launchers' argument lists
 
 
 def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:

@@ -387,6 +387,8 @@ class HipBackend(TorchBackend):
             # DP: 74 rows per rank -> 24 tiles x 10 splits)
             tiles = C.row_tiles_host(M, rows_first if w2 is not None else None, 128) * (w.shape[0] // 128)
             ks = max(2, 256 // max(tiles, 1))
+            if SW.fc_ksplit_max > 0:
+                ks = max(1, min(ks, SW.fc_ksplit_max))
             r = C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, ks, True,
                                x_lo=None if x_lo is None else x_lo.reshape(M, K), w_lo=w_lo, w2_lo=w2_lo,
                                out_lo=out_lo, c2d_pack=None if defer else c2d, no_epilogue=defer)
@@ -518,32 +520,17 @@ class HipBackend(TorchBackend):
                                             ctr.data_ptr(), q_out.data_ptr(), a_out.data_ptr(),
                                             P["wv"].numel(), _lib.ptr(H_lo), _lib.stream_ptr()), "actor_head")
 
-    def spec_update(self, p32, g32, v, m, pbf, lr, alpha, eps, centered, pb_lo, wnorm, bk) -> None:
-        """Speculative RMSprop update of a parameter range (views of the flat buffers) with
-        the clip coefficient assumed 1; the old p / v / m go to ``bk = (p, v, m)`` for the
-        final launch's fix-up (``optimizer(fix=...)``)."""
-        wn = (wnorm[0].data_ptr(), int(wnorm[1]), int(wnorm[2])) if wnorm is not None else (None, 0, 0)
-        _lib.check(self.lib.apex_rmsprop_spec(p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(),
-                                              pbf.data_ptr(), p32.numel(), float(lr), float(alpha), float(eps),
-                                              int(centered), _lib.ptr(pb_lo), *wn, bk[0].data_ptr(),
-                                              bk[1].data_ptr(), bk[2].data_ptr(), _lib.stream_ptr()), "rmsprop_spec")
-
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None, frag_out=None, n_update=None, fix=None) -> bool:
+                  sample=None, pb_lo=None, wnorm=None, frag_out=None) -> bool:
         """``frag_out`` (ops/conv.py conv12_frag_out): the launch also stores the updated
         w1 / w2 in the fused forward's fragment order.  Returns whether it did (the fused
-        optimizer + sample launch only).  ``n_update``: update only the first n parameters;
-        ``fix = (bk_p, bk_v, bk_m, off, n)``: [off, off + n) was updated by
-        :meth:`spec_update` -- redone from the saved state if the clip is active (the fused
         optimizer + sample launch only)."""
-        n = p32.numel() if n_update is None else int(n_update)
+        n = p32.numel()
         st = _lib.stream_ptr()
         lo = _lib.ptr(pb_lo)
         wn = (wnorm[0].data_ptr(), int(wnorm[1]), int(wnorm[2])) if wnorm is not None else (None, 0, 0)
-        if (frag_out is not None or fix is not None) and not (sample is not None and sample[0].use_hip):
-            raise ValueError("frag_out / fix need the fused optimizer + sample launch (a HIP replay)")
-        fx = (fix[0].data_ptr(), fix[1].data_ptr(), fix[2].data_ptr(), int(fix[3]), int(fix[4])) if fix is not None \
-            else (None, None, None, 0, 0)
+        if frag_out is not None and not (sample is not None and sample[0].use_hip):
+            raise ValueError("frag_out needs the fused optimizer + sample launch (a HIP replay)")
         if sample is not None and sample[0].use_hip:
             # the next batch's draw rides in the optimizer launch (csrc/sumtree.hip: rmsprop_sample_kernel)
             rp, B, out, nxt2 = sample
@@ -558,7 +545,7 @@ class HipBackend(TorchBackend):
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
                 *rp.sample_launch_args(B, out, nxt2), lo, *wn, frag_out if frag_out is not None else _lib.CfFragOut(),
-                *fx, st), "rmsprop_sample")
+                st), "rmsprop_sample")
             return frag_out is not None
         if sample is not None:
             self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,

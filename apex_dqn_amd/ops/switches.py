@@ -43,14 +43,12 @@ class Switches:
     # single-rank step: the weight gradients (fc + heads + priority write-back, conv3,
     # conv2) on a second stream beside the data-gradient chain (graph branches)
     bwd_branches: bool = True
-    # with the branched backward: the fc layer's RMSprop update runs early, beside the
-    # backward, with the clip coefficient assumed 1 (redone exactly by the final optimizer
-    # launch when ||g|| > clip); "side" = after the fc wgrad on the branch stream, "main" =
-    # after conv1's wgrad, "auto" = main from 256 rows per rank up, "off".  Measured slower
-    # everywhere (its 44 B / parameter of traffic competes with the backward kernels:
-    # 2,564 / 2,495 vs 2,640 steps/s at 512 rows, 5,750 / 5,757 vs 6,130 at 74,
-    # profiles/r4_ab_spec_fc_update.txt): off
-    spec_fc_opt: str = "off"
+    # the IMPALA learner's 15 conv weight gradients beside its data-gradient chain: no gain
+    # (392.5 / 393.9 vs 395.6 / 395.4 steps/s fp32, profiles/r4_ab_impala_bwd_branches.txt)
+    impala_bwd_branches: bool = False
+    # cap on the fc forward's K splits (0: fill the chip, ops/fused_ops.py fc_fwd); the DDQN
+    # head sums the splits' partials (the deferred epilogue)
+    fc_ksplit_max: int = 0
     # device-side image work queues in the persistent kernels: "auto" = only where RCCL's
     # kernels may hold CUs (the DP conv backward at world > 1), "on" / "off" force them
     work_queue: str = "auto"

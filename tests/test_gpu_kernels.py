@@ -497,90 +497,3 @@ def test_branched_backward_matches_serial(monkeypatch, dtype):
     assert torch.equal(res[False][3], res[True][3])
     for a, b in zip(res[False][:3], res[True][:3]):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9)
-
-
-@pytest.mark.parametrize("where,clip", [("side", 40.0), ("main", 40.0), ("side", 1e-4)])
-def test_speculative_fc_update_matches_one_pass(monkeypatch, where, clip):
-    """SW.spec_fc_opt: the fc layer updated early with the clip coefficient assumed 1
-    (old state saved), the final launch redoing it when ||g|| > clip -- the same
-    parameters and RMSprop state as the one-pass optimizer, with the clip inactive (40)
-    and active on every update (1e-4: the fix-up path)."""
-    from apex_dqn_amd.config import ApexConfig
-    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
-    from apex_dqn_amd.ops.switches import SW
-    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
-    res = {}
-    for spec in ("off", where):
-        monkeypatch.setattr(SW, "spec_fc_opt", spec)
-        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
-                                    "Learner": {"replay_sample_size": 128},
-                                    "Runtime": {"use_graphs": True, "graph_steps": 4, "grad_clip": clip}})
-        torch.manual_seed(0)
-        rp = GpuReplayShard(4000, 4000, 4100, 4, device=DEV, seed=3)
-        _fill_replay(rp, 3800, seed=1)
-        L = FusedNatureLearner(cfg, DEV, rp, backend="hip")
-        assert (L._spec is not None) == (spec != "off")
-        L.steps(6)
-        torch.cuda.synchronize()
-        res[spec] = (L.p32.clone(), L.rms_v.clone(), L.rms_m.clone(), L._pbf_all.clone(), L.S["idx"].clone(),
-                     float(L.gnorm[0]))
-    a, b = res["off"], res[where]
-    assert torch.equal(a[4], b[4])
-    if clip < 1.0:
-        assert a[5] > clip                  # the clip was active: the fix-up path ran
-    off = L.layout.offsets["wfc"]
-    for name, x, y in zip(("p", "v", "m", "pbf"), a[:4], b[:4]):
-        d = (x.float() - y.float()).abs()
-        n = x.numel() if name != "pbf" else L.p32.numel()
-        print(name, "prefix", float(d[:off].max()), "fc", float(d[off:n].max()),
-              "lo", float(d[n:].max()) if d.numel() > n else 0.0, "first fc diff",
-              int(torch.nonzero(d[off:n])[0]) if bool((d[off:n] > 0).any()) else -1)
-    for x, y in zip(a[:4], b[:4]):
-        assert torch.equal(x, y)
-
-
-@pytest.mark.parametrize("clip", [40.0, 1e-3])
-def test_spec_update_then_fixup_equals_one_pass(clip):
-    """Kernel level: apex_rmsprop_spec on a suffix + the fused final launch (prefix +
-    clip fix-up) == one fused launch over everything."""
-    from apex_dqn_amd.ops.fused_ops import HipBackend
-    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
-    be = HipBackend()
-    g = torch.Generator(device="cpu").manual_seed(5)
-    n, off = 200_000, 70_016
-    base = [torch.randn(n, generator=g).to(DEV) * s for s in (0.05, 0.01, 1e-4, 1e-3)]
-    base[2] = base[2].abs()
-    rp = GpuReplayShard(1000, 1000, 1200, 4, device=DEV)
-    _fill_replay(rp, 900, seed=2)
-    out = {}
-    for mode in ("one", "spec"):
-        p, gr, v, m = (t.clone() for t in base)
-        pb = torch.zeros(n, dtype=torch.bfloat16, device=DEV)
-        pl = torch.zeros_like(pb)
-        part = torch.zeros(64, dtype=torch.float64, device=DEV)
-        part[:7] = (gr.double() ** 2).sum() / 7      # the producers' squared-norm partials
-        nout = torch.zeros(1, device=DEV)
-        S = rp.alloc_sample_buffers(32)
-        kw = {}
-        if mode == "spec":
-            bk = tuple(torch.zeros(n - off, device=DEV) for _ in range(3))
-            be.spec_update(p[off:], gr[off:], v[off:], m[off:], pb[off:], 2.5e-4, 0.95, 1.5e-7, True, pl[off:], None,
-                           bk)
-            kw = dict(n_update=off, fix=(bk[0], bk[1], bk[2], off, n - off))
-        be.optimizer(p, gr, v, m, pb, 2.5e-4, 0.95, 1.5e-7, clip, True, None, nout, norm_total=(part, 7),
-                     sample=(rp, 32, S, None), pb_lo=pl, **kw)
-        torch.cuda.synchronize()
-        out[mode] = (p, v, m, pb, pl, float(nout[0]))
-    assert (out["one"][5] > clip) == (clip < 1.0)
-    # (diagnostics) the torch update with the real and with a unit clip coefficient
-    p0, g0, v0, m0 = (t.clone() for t in base)
-    for name, c in (("real", min(1.0, clip / (out["one"][5] + 1e-6))), ("unit", 1.0)):
-        gg = g0 * c
-        vv = 0.95 * v0 + 0.05 * gg * gg
-        mm = 0.95 * m0 + 0.05 * gg
-        pp = p0 - 2.5e-4 * gg / ((vv - mm * mm).clamp_min(0).sqrt() + 1.5e-7)
-        for mode in ("one", "spec"):
-            print(name, mode, "prefix", float((out[mode][0][:off] - pp[:off]).abs().max()),
-                  "suffix", float((out[mode][0][off:] - pp[off:]).abs().max()))
-    for a, b in zip(out["one"][:5], out["spec"][:5]):
-        assert torch.equal(a, b)
