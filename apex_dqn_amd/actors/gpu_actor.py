@@ -281,7 +281,11 @@ class GpuActorGroup:
         return self._env_step(self.q_host.numpy().copy(), self.a_host.numpy().astype(np.int64))
 
     def _env_step(self, q: np.ndarray, actions: np.ndarray) -> int:
-        frames, rew, done, info = self.env.step(actions)
+        # frame-producing envs write straight into the replay's pinned staging buffer (the
+        # frame append then starts its H2D copy from it: no staging copy on the host thread)
+        stage = getattr(self.replay, "stage_frames", None) if getattr(self.env, "frame_out", False) else None
+        buf = stage(self.E) if stage is not None else None
+        frames, rew, done, info = self.env.step(actions, out=buf) if buf is not None else self.env.step(actions)
         prev = self.payload
         self.payload = self._ingest(frames, done)
         self.builder.step(prev, q, actions, rew, done, self.payload)

@@ -97,6 +97,7 @@ class SyntheticAtariVec:
 
     obs_dtype = np.uint8
     frame_based = True
+    frame_out = True          # step(actions, out=...) writes the frames into ``out``
 
     def __init__(self, num_envs: int, action_dim: int = 6, seed: int = 0,
                  num_states: int = 32, p_end: float = 0.01, max_len: int = 1000,
@@ -119,8 +120,10 @@ class SyntheticAtariVec:
         self.t = np.zeros(self.E, np.int64)
         self.ep_ret = np.zeros(self.E, np.float64)
 
-    def _frames(self) -> np.ndarray:
-        f = self.bank[self.s]       # the gather already returns a fresh array (no extra copy)
+    def _frames(self, out: Optional[np.ndarray] = None) -> np.ndarray:
+        # the gather returns a fresh array, or fills ``out`` (e.g. the replay's pinned staging;
+        # mode 'clip': numpy buffers ``out`` under the default 'raise')
+        f = self.bank[self.s] if out is None else np.take(self.bank, self.s, axis=0, out=out, mode="clip")
         col = (self.t * 3) % self.obs_shape[1]
         f[np.arange(self.E), :, col] = 255
         return f
@@ -131,7 +134,7 @@ class SyntheticAtariVec:
         self.ep_ret[:] = 0
         return self._frames()
 
-    def step(self, actions: np.ndarray):
+    def step(self, actions: np.ndarray, out: Optional[np.ndarray] = None):
         actions = np.asarray(actions, np.int64)
         rew = (actions == (self.s % self.action_dim)).astype(np.float32)
         self.s = (self.s * 7 + actions + 1 + self.rng.integers(0, 2, size=self.E)) % self.S
@@ -145,7 +148,7 @@ class SyntheticAtariVec:
             self.s[idx] = self.rng.integers(0, self.S, size=len(idx))
             self.t[idx] = 0
             self.ep_ret[idx] = 0
-        return self._frames(), rew, done, info
+        return self._frames(out), rew, done, info
 
 
 def _area_matrix(n_out: int, n_in: int) -> np.ndarray:
@@ -252,6 +255,7 @@ class AtariWrapperVec:
     obs_dtype = np.uint8
     frame_based = True
     obs_shape = (84, 84)
+    frame_out = True          # step(actions, out=...) writes the frames into ``out``
 
     def __init__(self, emulators, frame_skip: int = 4, noop_max: int = 30, clip_rewards: bool = True,
                  episodic_life: bool = True, fire_reset: bool = False, seed: int = 0):
@@ -284,8 +288,8 @@ class AtariWrapperVec:
         self.ep_len[:] = 0
         return np.stack([self._reset_one(i) for i in range(self.E)])
 
-    def step(self, actions):
-        obs = np.zeros((self.E, 84, 84), np.uint8)
+    def step(self, actions, out: Optional[np.ndarray] = None):
+        obs = np.zeros((self.E, 84, 84), np.uint8) if out is None else out    # every row is written below
         rew = np.zeros(self.E, np.float32)
         done = np.zeros(self.E, bool)
         real_done = np.zeros(self.E, bool)

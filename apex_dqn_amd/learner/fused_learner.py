@@ -553,14 +553,21 @@ class FusedNatureLearner(IsNormMixin):
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1,
                        **self._lo(dy_lo=self.dY2_lo, w_lo=sp and Pl["w2"], dx_lo=self.dY1_lo))
         side.wait_event(ev2)
+        fuse = self._fuse_norm
         with torch.cuda.stream(side):
             ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"], jobs=jobs,
                            **self._lo(dy_lo=self.dY2_lo, x_lo=sp and self.y1_lo[:B]))
+        jobs1 = []
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
-                             G["b1"], jobs=jobs, **self._lo(dy_lo=self.dY1_lo))
+                             G["b1"], jobs=jobs1, **self._lo(dy_lo=self.dY1_lo))
+        with torch.cuda.stream(side):
+            # conv3 / conv2 split-K reductions (+ the head region's norm partials) on the
+            # branch, beside conv1's weight gradient
+            n_side = ops.finalize_grads(jobs, self.g_head_region if fuse else None,
+                                        dict(part=self.norm_part, slot0=self._fc_slots) if fuse else None)
+        n_main = ops.finalize_grads(jobs1, None, dict(part=self.norm_part, slot0=n_side) if fuse else None)
         main.wait_stream(side)
-        norm = dict(part=self.norm_part, slot0=self._fc_slots) if self._fuse_norm else None
-        self._npart = ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
+        self._npart = n_main
         self._mark("conv_backward")
 
     def _step_body(self) -> None:
@@ -623,12 +630,15 @@ class FusedNatureLearner(IsNormMixin):
     def _dp_body_branched(self) -> None:
         """The data-parallel step on the branched backward (SW.bwd_branches):
 
-          main stream          fc dgrad -> conv3 dgrad -> conv2 dgrad -> conv1 wgrad -> finalize
+          main stream          fc dgrad -> conv3 dgrad -> conv2 dgrad -> conv1 wgrad -> finalize (conv1)
           branch stream        head wgrad + priorities (+ fc wgrad)  conv3 wgrad  conv2 wgrad
+                               -> finalize (conv3 / conv2)
           comm (RCCL, in order) fc factors all-gather (or fc bucket all-reduce) + shard
                                stats, issued from the branch as soon as they exist;
-                               conv + head all-reduce after the split-K finalisation,
-                               [factors: the fc wgrad of the gathered rows beside it]
+                               the [w2, wfc) bucket (conv2 / conv3 / head) from the branch
+                               after its finalisation; conv1's bucket from the main stream
+          [factors] the fc wgrad of the gathered rows on the branch after its conv2 wgrad
+                               (SW.dp_fc_wgrad_branch; off: on the main stream after conv1)
 
         then the clip norm of the reduced gradient and the optimizer + next draw."""
         B, rt, ops, G, Pb, Pl, S = self.B, self.rt, self.ops, self.G, self.Pb, self.Pl, self.S
@@ -672,35 +682,48 @@ class FusedNatureLearner(IsNormMixin):
                        **self._lo(dy_lo=self.dY2_lo, w_lo=sp and Pl["w2"], dx_lo=self.dY1_lo))
         side.wait_event(ev2)
         nfc = 0
+        o2 = self.layout.offsets["w2"]
+        fc_branch = factors and SW.dp_fc_wgrad_branch
+        if fc_branch:
+            # the branch's fc wgrad needs the all-gather: waited for on the main stream
+            # (long done by now) and handed over by an event -- a wait on the torch work
+            # from the branch inside a captured graph crashed the capture (world 1)
+            works["fc"].wait()
+            ev1 = torch.cuda.Event()
+            ev1.record(main)
         with torch.cuda.stream(side):
             ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, G["w2"], G["b2"], jobs=jobs,
                            **self._lo(dy_lo=self.dY2_lo, x_lo=sp and self.y1_lo[:B]))
+        jobs1 = []
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
-                             G["b1"], jobs=jobs, **self._lo(dy_lo=self.dY1_lo))
-        main.wait_stream(side)
-        self._npart = ops.finalize_grads(jobs, None, None)
+                             G["b1"], jobs=jobs1, **self._lo(dy_lo=self.dY1_lo))
+        with torch.cuda.stream(side):
+            # conv2 / conv3 / head bucket [w2, wfc): reduced on the branch and all-reduced
+            # from it while conv1's weight gradient runs -- only conv1's bucket follows the
+            # last backward kernel
+            ops.finalize_grads(jobs, None, None)
+            if self._comm_bf16:
+                self.gcomm[o2:cut].copy_(self.g32[o2:cut])
+            works["cv2"] = self.coll.all_reduce(self.gcomm[o2:cut])
+            if fc_branch:
+                side.wait_event(ev1)
+                nfc = self._fc_wgrad_gathered(None)
+        ops.finalize_grads(jobs1, None, None)
+        self._npart = 0
         self._mark("conv_backward")
         if self._comm_bf16:
-            self.gcomm[:cut].copy_(self.g32[:cut])
-        w_cv = self.coll.all_reduce(self.gcomm[:cut])
-        if factors:
-            # the fc weight gradient of the global batch from the gathered rows (identical
-            # on every rank, with its clip-norm partials), beside the conv all-reduce
-            # (waited for on the main stream: a wait on the branch inside a captured
-            # graph crashed the capture of the world-1 all-gather)
-            works["fc"].wait()
-            R, c = self.fx_recv, [0]
-            for w in self._fx_cols:
-                c.append(c[-1] + w)
-            cols = [R[:, c[i]:c[i + 1]] for i in range(len(self._fx_cols))]
-            dy, dy_lo, x, x_lo = (cols[0], cols[1], cols[2], cols[3]) if sp else (cols[0], None, cols[1], None)
-            nfc = ops.fc_wgrad(dy, x, G["wfc"], G["bfc"], norm=(self.norm_part, 0),
-                               **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
+            self.gcomm[:o2].copy_(self.g32[:o2])
+        w_cv = self.coll.all_reduce(self.gcomm[:o2])
+        main.wait_stream(side)
+        if factors and not fc_branch:
+            # (on the main stream, after conv1: SW.dp_fc_wgrad_branch off)
+            nfc = self._fc_wgrad_gathered(works["fc"])
         if self._ordered_coll:
             w_cv.wait()          # RCCL runs the collectives in issue order: covers fc + stats
         else:
             works["fc"].wait()
             works["stats"].wait()
+            works["cv2"].wait()
             w_cv.wait()
         self._mark("allreduce_wait")
         if factors:
@@ -708,6 +731,22 @@ class FusedNatureLearner(IsNormMixin):
             self._seg3(norm_slots=nfc + nr)
         else:
             self._seg3()         # (the optimizer's own clip-norm pass over the reduced gradient)
+
+    def _fc_wgrad_gathered(self, work) -> int:
+        """The fc weight gradient of the global batch from the all-gathered (dH, X) rows
+        (identical on every rank), with its clip-norm partials in norm_part[0:]; waits for
+        the all-gather ``work`` on the current stream (None: already ordered after it).
+        Returns the partial slots written."""
+        G, sp = self.G, self.split
+        if work is not None:
+            work.wait()
+        R, c = self.fx_recv, [0]
+        for w in self._fx_cols:
+            c.append(c[-1] + w)
+        cols = [R[:, c[i]:c[i + 1]] for i in range(len(self._fx_cols))]
+        dy, dy_lo, x, x_lo = (cols[0], cols[1], cols[2], cols[3]) if sp else (cols[0], None, cols[1], None)
+        return self.ops.fc_wgrad(dy, x, G["wfc"], G["bfc"], norm=(self.norm_part, 0),
+                                 **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
 
     def _dp_body_factors(self) -> None:
         """The data-parallel step with the factored fc-gradient exchange (see __init__):

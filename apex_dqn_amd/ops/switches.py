@@ -46,6 +46,9 @@ class Switches:
     # the IMPALA learner's 15 conv weight gradients beside its data-gradient chain: no gain
     # (392.5 / 393.9 vs 395.6 / 395.4 steps/s fp32, profiles/r4_ab_impala_bwd_branches.txt)
     impala_bwd_branches: bool = False
+    # DP step, factored fc exchange: the global batch's fc wgrad on the branch stream (after
+    # its conv2 wgrad, beside conv1's) instead of on the main stream after conv1
+    dp_fc_wgrad_branch: bool = True
     # cap on the fc forward's K splits (0: fill the chip, ops/fused_ops.py fc_fwd); the DDQN
     # head sums the splits' partials (the deferred epilogue)
     fc_ksplit_max: int = 0

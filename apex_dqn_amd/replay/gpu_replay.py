@@ -305,10 +305,10 @@ class GpuReplayShard:
         self.frame_head += n
         return seqs
 
-    def _pinned(self, frames: np.ndarray) -> torch.Tensor:
-        """Copy host frames into one of two pinned staging buffers (the copy of the
-        buffer's previous use must have finished: its event is waited on first)."""
-        shape = tuple(frames.shape)
+    def _acquire_pin(self, shape) -> torch.Tensor:
+        """The next of two pinned staging buffers of ``shape`` (the copy of its previous
+        use must have finished: its event is waited on first)."""
+        shape = tuple(shape)
         if getattr(self, "_pin_shape", None) != shape:
             self._pin_buf = [torch.empty(shape, dtype=torch.uint8).pin_memory() for _ in range(2)]
             self._pin_ev = [torch.cuda.Event(), torch.cuda.Event()]
@@ -319,7 +319,29 @@ class GpuReplayShard:
         if self._pin_used[k]:
             self._pin_ev[k].synchronize()
         self._pin_used[k] = True
-        buf = self._pin_buf[k]
+        return self._pin_buf[k]
+
+    def stage_frames(self, n: int) -> Optional[np.ndarray]:
+        """A pinned host buffer for the next append of ``n`` frames (GPU shards): an env
+        that writes its frames straight into it (``step(actions, out=...)``) saves the
+        staging copy -- append_frames of exactly that array starts its H2D copy from it.
+        None off the GPU."""
+        if self.device.type != "cuda" or self.frame_shape is None:
+            return None
+        with self.lock:
+            buf = self._acquire_pin((int(n),) + tuple(self.frame_shape))
+            arr = buf.numpy()
+            self._staged = (buf, arr)
+            return arr
+
+    def _pinned(self, frames: np.ndarray) -> torch.Tensor:
+        """Host frames in a pinned staging buffer: the buffer itself when ``frames`` is the
+        array stage_frames handed out, else a copy into the next one."""
+        st = getattr(self, "_staged", None)
+        if st is not None and frames is st[1]:
+            self._staged = None
+            return st[0]
+        buf = self._acquire_pin(frames.shape)
         np.copyto(buf.numpy(), frames)
         return buf
 

@@ -92,3 +92,4 @@ class ActorRunner:
             return
         if self.alive and not self.done and time.time() - self.beat > self.timeout:
             raise RuntimeError("actor thread stalled: no group step for %.0f s" % (time.time() - self.beat))
+

@@ -10,6 +10,7 @@
 #   bash scripts/gpu.sh pmc TAG COUNTERS [bench args]  # one rocprofv3 --pmc pass (<= 8 SQ counters), summarised
 #   bash scripts/gpu.sh ab TAG "ENV=1 :: --flag" ...   # interleaved A/B of bench variants (each twice)
 #   bash scripts/gpu.sh steal TAG                      # CU-steal proxy of the DP step (scripts/bench_cu_steal.py)
+#   bash scripts/gpu.sh e2e TAG [main.py --set args]   # actor + learner loop, Pong-shaped config
 #   bash scripts/gpu.sh py TAG SCRIPT [args]           # any python script under a 300 s limit
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -73,6 +74,13 @@ steal)
   TAG=$1
   timeout -k 10 300 python -u scripts/bench_cu_steal.py > gpurun_out/steal_$TAG.jsonl 2> gpurun_out/steal_$TAG.err
   rc=$?; cat gpurun_out/steal_$TAG.jsonl; exit $rc ;;
+e2e)
+  TAG=$1; shift
+  timeout -k 10 400 python -u main.py --params-file configs/pong_1gpu.json --mode gpu \
+      --learner-steps ${E2E_STEPS:-8000} --metrics gpurun_out/e2e_$TAG.jsonl --set Runtime.log_every=500 "$@" \
+      > gpurun_out/e2e_$TAG.log 2>&1
+  rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/e2e_$TAG.log; exit $rc; }
+  python scripts/e2e_summary.py gpurun_out/e2e_$TAG.jsonl ;;
 py)
   TAG=$1; shift
   timeout -k 10 300 python -u "$@" > gpurun_out/py_$TAG.log 2>&1

@@ -76,3 +76,24 @@ def test_factory_fake_ale_shapes():
     assert obs.shape == (3, 84, 84) and obs.dtype == np.uint8 and env.action_dim == 6
     obs, r, d, info = env.step(np.zeros(3, np.int64))
     assert obs.shape == (3, 84, 84) and r.shape == (3,) and d.shape == (3,)
+
+
+def test_envs_write_frames_into_a_given_buffer():
+    """``step(actions, out=buf)`` (the actor's zero-copy path into the replay's pinned
+    staging buffer, actors/gpu_actor.py _env_step) returns ``buf`` holding exactly the
+    frames a plain step returns, for the synthetic env and the ALE wrapper stack."""
+    from apex_dqn_amd.envs.vector_envs import make_vec_env
+    for backend in ("synthetic", "fake_ale"):
+        a, b = (make_vec_env(backend, "PongNoFrameskip-v4", 6, 6, seed=3) for _ in range(2))
+        assert a.frame_out and b.frame_out
+        np.testing.assert_array_equal(a.reset(), b.reset())
+        rng = np.random.default_rng(0)
+        for _ in range(40):
+            act = rng.integers(0, 6, 6)
+            buf = np.full((6, 84, 84), 7, np.uint8)
+            fa, ra, da, _ = a.step(act)
+            fb, rb, db, _ = b.step(act, out=buf)
+            assert fb is buf
+            np.testing.assert_array_equal(fa, fb)
+            np.testing.assert_array_equal(ra, rb)
+            np.testing.assert_array_equal(da, db)

@@ -565,3 +565,26 @@ def test_pipelined_actor_groups_step_all_envs():
     assert all(g.payload is None for g in grp.groups)
     grp.step()                                        # fresh episodes after an actor restart
     assert all(g.t == 41 for g in grp.groups)
+
+
+@pytest.mark.gpu
+def test_staged_frame_append_matches_copy():
+    """GpuReplayShard.stage_frames: frames written straight into the pinned staging
+    buffer and appended from it land in the HBM ring exactly as a copied append does,
+    across both staging buffers and a ring wrap."""
+    import numpy as np
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    dev = torch.device("cuda", 0)
+    a = GpuReplayShard(100, 100, 64, 4, device=dev, seed=1)
+    b = GpuReplayShard(100, 100, 64, 4, device=dev, seed=1)
+    rng = np.random.default_rng(0)
+    for it in range(9):
+        f = rng.integers(0, 255, (24, 84, 84), dtype=np.uint8)
+        buf = a.stage_frames(24)
+        assert buf is not None and buf.shape == (24, 84, 84)
+        buf[...] = f
+        sa = a.append_frames(buf)
+        sb = b.append_frames(f)
+        np.testing.assert_array_equal(sa, sb)
+    torch.cuda.synchronize()
+    assert torch.equal(a.frames, b.frames)

@@ -128,3 +128,4 @@ def test_pipelined_actor_groups_cpu():
     grp.reset_episodes()
     grp.step()
     assert all(g.t == 13 for g in grp.groups)
+
