@@ -36,7 +36,7 @@ struct IsNorm {
 // hp.part != null: the fc forward's split-K epilogue runs inside (head_common.h
 // load_row_part); blocks >= B run the conv2 weight-fragment pack job (pk.out != null)
 // that otherwise rides on that epilogue's launch.
-template <int HS>
+template <int HS, int MAXA>
 __global__ void __launch_bounds__(192) ddqn_head_kernel(
     const bf16_t* __restrict__ Hon, const bf16_t* __restrict__ Htg, HeadParams Pon, HeadParams Ptg,
     const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(192) ddqn_head_kernel(
     return;
   }
   float ad;
-  const bool w0 = ddqn_head_body<HS>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs,
+  const bool w0 = ddqn_head_body<HS, MAXA>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa, grad_scale, td_abs,
                                      loss, q_out, dH, dhead, zero_ptr, zero_n, &ad, lo, hp);
   if (!w0 && (isn.out != nullptr || isn.valid_count != nullptr) && blockIdx.x == 0 && (threadIdx.x >> 6) == 1) {
     float m = 0.f;
@@ -87,16 +87,19 @@ APEX_EXPORT int apex_ddqn_head(const bf16_t* Hon, const bf16_t* Htg, HeadParams 
   }
   if (pk.out != nullptr && (pk.w == nullptr || ((uintptr_t)pk.out & 15))) return (int)hipErrorInvalidValue;
   const int grid = B + (pk.out != nullptr ? 128 : 0);
-  if (hidden == 512)
-    ddqn_head_kernel<512><<<grid, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
-                                                grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo,
-                                                hp, pk, isn);
-  else if (hidden == 256)
-    ddqn_head_kernel<256><<<grid, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,
-                                                grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo,
-                                                hp, pk, isn);
+#define APEX_HEAD_LAUNCH(HS_, MA_)                                                                              \
+  ddqn_head_kernel<HS_, MA_><<<grid, 192, 0, st>>>(Hon, Htg, Pon, Ptg, act, rew, gam, isw, B, A, huber, kappa,     \
+                                                   grad_scale, td_abs, loss, q_out, dH, dhead, zero_ptr, zero_n, lo, \
+                                                   hp, pk, isn)
+  // the q arrays in registers: 8 actions (every ALE minimal action set but the full
+  // 18) keep the kernel free of scratch
+  if (hidden == 512 && A <= 8) APEX_HEAD_LAUNCH(512, 8);
+  else if (hidden == 512) APEX_HEAD_LAUNCH(512, HEAD_MAXA);
+  else if (hidden == 256 && A <= 8) APEX_HEAD_LAUNCH(256, 8);
+  else if (hidden == 256) APEX_HEAD_LAUNCH(256, HEAD_MAXA);
   else
     return (int)hipErrorInvalidValue;
+#undef APEX_HEAD_LAUNCH
   APEX_CHECK_LAUNCH();
 }
 

@@ -65,11 +65,16 @@ __device__ __forceinline__ void load_row_streams(const bf16_t* __restrict__ row,
 
 // q-values of one row; `row_lo` (split mode, else null) adds the lo plane: the
 // activations are then fp32-accurate (hi + lo)
-template <int HS>
+// MAXA: compile-time bound on the action count (the q arrays live in registers; the
+// launchers pick 8 when A <= 8, else HEAD_MAXA).  KEEP: also leave the weights the head
+// backward needs (wave 0 of ddqn_head_body) -- wv, the column sums of wa and wa's row
+// for action a_sel -- so the backward issues no second round of weight loads.
+template <int HS, int MAXA = HEAD_MAXA, bool KEEP = false>
 __device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, float* q, const float* hv,
-                                       const float* ha);
+                                       const float* ha, float* kwv = nullptr, float* kcs = nullptr,
+                                       float* kws = nullptr, int a_sel = 0);
 
-template <int HS>
+template <int HS, int MAXA = HEAD_MAXA>
 __device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const bf16_t* __restrict__ row_lo,
                                          const HeadParams& P, int A, int lane, float* q, float* hv, float* ha) {
   constexpr int NPL = HS / 64;
@@ -83,7 +88,7 @@ __device__ __forceinline__ void head_row(const bf16_t* __restrict__ row, const b
       ha[k] += la[k];
     }
   }
-  head_q<HS>(P, A, lane, q, hv, ha);
+  head_q<HS, MAXA>(P, A, lane, q, hv, ha);
 }
 
 // The fc forward's split-K epilogue fused into the head (csrc/conv_mfma.hip
@@ -106,46 +111,70 @@ struct HeadPart {
 template <int HS>
 __device__ __forceinline__ void load_row_part(const HeadPart& hp, int row, int lane, float* hv, float* ha,
                                               bool store) {
-  constexpr int NPL = HS / 64, ROW = 2 * HS;
+  // Every load of a group of ZU partial planes (both streams) is issued before any of
+  // them is summed -- at a small per-rank batch the fc forward runs ~10 K splits and a
+  // plane-by-plane loop paid one memory round trip per plane -- and the sum keeps the
+  // z order of fc_splitk_epilogue_kernel (bit-identical).
+  constexpr int NPL = HS / 64, ROW = 2 * HS, ZU = 4;
   const bool split = hp.hon_lo != nullptr;
   const float* __restrict__ bias = row < hp.two_b ? hp.bias_on : hp.bias_tg;
+  float v[2][NPL], bs[2][NPL];
+  const float* p0 = hp.part + (int64_t)row * ROW + lane * NPL;
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int k = 0; k < NPL; k += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p0 + st * HS + k);
+      const float4 b = *reinterpret_cast<const float4*>(bias + st * HS + lane * NPL + k);
+      v[st][k] = a.x; v[st][k + 1] = a.y; v[st][k + 2] = a.z; v[st][k + 3] = a.w;
+      bs[st][k] = b.x; bs[st][k + 1] = b.y; bs[st][k + 2] = b.z; bs[st][k + 3] = b.w;
+    }
+  for (int z0 = 1; z0 < hp.nz; z0 += ZU) {
+    float4 t[ZU][2][NPL / 4];
+#pragma unroll
+    for (int u = 0; u < ZU; ++u)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int k = 0; k < NPL / 4; ++k)
+          t[u][st][k] = z0 + u < hp.nz
+                            ? *reinterpret_cast<const float4*>(p0 + (int64_t)(z0 + u) * hp.zstride + st * HS + 4 * k)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      if (z0 + u >= hp.nz) break;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int k = 0; k < NPL / 4; ++k) {
+          v[st][4 * k] += t[u][st][k].x; v[st][4 * k + 1] += t[u][st][k].y;
+          v[st][4 * k + 2] += t[u][st][k].z; v[st][4 * k + 3] += t[u][st][k].w;
+        }
+    }
+  }
 #pragma unroll
   for (int st = 0; st < 2; ++st) {       // value stream, advantage stream
     const int c0 = st * HS + lane * NPL;
-    float v[NPL];
-    const float* p0 = hp.part + (int64_t)row * ROW + c0;
-#pragma unroll
-    for (int k = 0; k < NPL; k += 4) {
-      const float4 a = *reinterpret_cast<const float4*>(p0 + k);
-      v[k] = a.x; v[k + 1] = a.y; v[k + 2] = a.z; v[k + 3] = a.w;
-    }
-    for (int z = 1; z < hp.nz; ++z) {
-#pragma unroll
-      for (int k = 0; k < NPL; k += 4) {
-        const float4 a = *reinterpret_cast<const float4*>(p0 + z * hp.zstride + k);
-        v[k] += a.x; v[k + 1] += a.y; v[k + 2] += a.z; v[k + 3] += a.w;
-      }
-    }
     uint32_t hh[NPL / 2], ll[NPL / 2];
 #pragma unroll
-    for (int k = 0; k < NPL; k += 4) {
-      const float4 b = *reinterpret_cast<const float4*>(bias + c0 + k);
-      v[k] = v[k] * 1.0f + b.x; v[k + 1] = v[k + 1] * 1.0f + b.y;
-      v[k + 2] = v[k + 2] * 1.0f + b.z; v[k + 3] = v[k + 3] * 1.0f + b.w;
-    }
+    for (int k = 0; k < NPL; ++k) v[st][k] = v[st][k] * 1.0f + bs[st][k];
 #pragma unroll
     for (int k = 0; k < NPL / 2; ++k) {
       // fc_splitk_epilogue_kernel: ReLU in fp32, then the (hi / lo) bf16 rounding
       if (split) {
-        split_pk_bf16_h(fmaxf(v[2 * k], 0.f), fmaxf(v[2 * k + 1], 0.f), hh[k], ll[k]);
+        split_pk_bf16_h(fmaxf(v[st][2 * k], 0.f), fmaxf(v[st][2 * k + 1], 0.f), hh[k], ll[k]);
       } else {
-        hh[k] = pack_bf16x2(fmaxf(v[2 * k], 0.f), fmaxf(v[2 * k + 1], 0.f));
+        hh[k] = pack_bf16x2(fmaxf(v[st][2 * k], 0.f), fmaxf(v[st][2 * k + 1], 0.f));
         ll[k] = 0;
       }
     }
-    float* out = st ? ha : hv;
+    // (no pointer select between hv / ha: that put both arrays in scratch)
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) out[k] = bf16_at(hh, k) + (split ? bf16_at(ll, k) : 0.f);
+    for (int k = 0; k < NPL; ++k) {
+      const float x = bf16_at(hh, k) + (split ? bf16_at(ll, k) : 0.f);
+      if (st) ha[k] = x;
+      else hv[k] = x;
+    }
     if (store) {
       bf16_t* o = hp.hon + (int64_t)row * ROW + c0;
       if constexpr (NPL == 8) {
@@ -159,26 +188,41 @@ __device__ __forceinline__ void load_row_part(const HeadPart& hp, int row, int l
   }
 }
 
-template <int HS>
+template <int HS, int MAXA, bool KEEP>
 __device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, float* q, const float* hv,
-                                       const float* ha) {
+                                       const float* ha, float* kwv, float* kcs, float* kws, int a_sel) {
   constexpr int NPL = HS / 64;
-  float part[HEAD_MAXA + 1];
+  float part[MAXA + 1];
   {
     float w[NPL], s = 0.f;
     load_w<NPL>(P.wv + lane * NPL, w);
 #pragma unroll
     for (int k = 0; k < NPL; ++k) s += hv[k] * w[k];
     part[0] = s;
+    if constexpr (KEEP) {
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        kwv[k] = w[k];
+        kcs[k] = 0.f;
+        kws[k] = 0.f;
+      }
+    }
   }
 #pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
+  for (int j = 0; j < MAXA; ++j) {
     if (j < A) {
       float w[NPL], s = 0.f;
       load_w<NPL>(P.wa + j * HS + lane * NPL, w);
 #pragma unroll
       for (int k = 0; k < NPL; ++k) s += ha[k] * w[k];
       part[j + 1] = s;
+      if constexpr (KEEP) {
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) {
+          kcs[k] += w[k];
+          if (j == a_sel) kws[k] = w[k];
+        }
+      }
     } else {
       part[j + 1] = 0.f;
     }
@@ -186,7 +230,7 @@ __device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, flo
   float v = wave_sum_dpp(part[0]) + P.bv[0];
   float amean = 0.f;
 #pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
+  for (int j = 0; j < MAXA; ++j) {
     if (j < A) {
       float a = wave_sum_dpp(part[j + 1]) + P.ba[j];
       part[j + 1] = a;
@@ -195,13 +239,13 @@ __device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, flo
   }
   amean /= (float)A;
 #pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j)
+  for (int j = 0; j < MAXA; ++j)
     if (j < A) q[j] = v + part[j + 1] - amean;
 }
 
 // One block of three waves per sample (blockIdx.x = b).  Returns true in wave 0,
 // which finishes the sample and holds |delta| (wave-uniform) in *ad_out.
-template <int HS>
+template <int HS, int MAXA = HEAD_MAXA>
 __device__ __forceinline__ bool ddqn_head_body(
     const bf16_t* __restrict__ Hon, const bf16_t* __restrict__ Htg, HeadParams Pon, HeadParams Ptg,
     const int32_t* __restrict__ act, const float* __restrict__ rew, const float* __restrict__ gam,
@@ -209,7 +253,7 @@ __device__ __forceinline__ bool ddqn_head_body(
     float* __restrict__ td_abs, float* __restrict__ loss, float* __restrict__ q_out,
     bf16_t* __restrict__ dH, float* __restrict__ dhead, float* __restrict__ zero_ptr, int zero_n,
     float* ad_out, HeadLo lo, const HeadPart& hp) {
-  __shared__ float qs[2][HEAD_MAXA];
+  __shared__ float qs[2][MAXA];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.x;
   // zero the head-gradient region that head_wgrad accumulates into (stream-ordered)
@@ -217,53 +261,70 @@ __device__ __forceinline__ bool ddqn_head_body(
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_n; i += B * blockDim.x) zero_ptr[i] = 0.f;
   }
   constexpr int NPL = HS / 64, ROW = 2 * HS;
-  float q_t[HEAD_MAXA], q_n[HEAD_MAXA], q_g[HEAD_MAXA];
+  float q_t[MAXA], q_n[MAXA], q_g[MAXA];
   float hv_t[NPL], ha_t[NPL];
   const bool split = lo.Hon != nullptr;
+  // the sample's scalars are loaded up front (wave 0 consumes them after the barrier)
+  float kwv[NPL], kcs[NPL], kws[NPL];     // kept by head_q for the backward
+  int a_b = 0;
+  float rew_b = 0.f, gam_b = 0.f, w_b = 1.f;
   if (wv == 0) {
+    a_b = act[b];
+    rew_b = rew[b];
+    gam_b = gam[b];
+    if (isw) w_b = isw[b];
     if (hp.part != nullptr) {
       load_row_part<HS>(hp, b, lane, hv_t, ha_t, true);
-      head_q<HS>(Pon, A, lane, q_t, hv_t, ha_t);
+      head_q<HS, MAXA, true>(Pon, A, lane, q_t, hv_t, ha_t, kwv, kcs, kws, a_b);
     } else {
-      head_row<HS>(Hon + (int64_t)b * ROW, split ? lo.Hon + (int64_t)b * ROW : nullptr, Pon, A, lane, q_t, hv_t,
-                   ha_t);
+      const bf16_t* row = Hon + (int64_t)b * ROW;
+      load_row_streams<HS>(row, lane, hv_t, ha_t);
+      if (split) {
+        float lv[NPL], la[NPL];
+        load_row_streams<HS>(lo.Hon + (int64_t)b * ROW, lane, lv, la);
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) {
+          hv_t[k] += lv[k];
+          ha_t[k] += la[k];
+        }
+      }
+      head_q<HS, MAXA, true>(Pon, A, lane, q_t, hv_t, ha_t, kwv, kcs, kws, a_b);
     }
   } else {
-    float hv_x[NPL], ha_x[NPL], q[HEAD_MAXA];
+    float hv_x[NPL], ha_x[NPL], q[MAXA];
     if (hp.part != nullptr) {
       load_row_part<HS>(hp, wv == 1 ? B + b : hp.two_b + b, lane, hv_x, ha_x, false);
-      head_q<HS>(wv == 1 ? Pon : Ptg, A, lane, q, hv_x, ha_x);
+      head_q<HS, MAXA>(wv == 1 ? Pon : Ptg, A, lane, q, hv_x, ha_x);
     } else if (wv == 1)
-      head_row<HS>(Hon + (int64_t)(B + b) * ROW, split ? lo.Hon + (int64_t)(B + b) * ROW : nullptr, Pon, A, lane, q,
+      head_row<HS, MAXA>(Hon + (int64_t)(B + b) * ROW, split ? lo.Hon + (int64_t)(B + b) * ROW : nullptr, Pon, A, lane, q,
                    hv_x, ha_x);
     else
-      head_row<HS>(Htg + (int64_t)b * ROW, split ? lo.Htg + (int64_t)b * ROW : nullptr, Ptg, A, lane, q, hv_x, ha_x);
+      head_row<HS, MAXA>(Htg + (int64_t)b * ROW, split ? lo.Htg + (int64_t)b * ROW : nullptr, Ptg, A, lane, q, hv_x, ha_x);
     if (lane == 0) {
 #pragma unroll
-      for (int j = 0; j < HEAD_MAXA; ++j)
+      for (int j = 0; j < MAXA; ++j)
         if (j < A) qs[wv - 1][j] = q[j];
     }
   }
   __syncthreads();
   if (wv != 0) return false;
 #pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
+  for (int j = 0; j < MAXA; ++j) {
     q_n[j] = j < A ? qs[0][j] : 0.f;
     q_g[j] = j < A ? qs[1][j] : 0.f;
   }
   // double DQN: argmax from the online net, value from the target net
   int astar = 0;
   float best = -3.4e38f, qg_star = 0.f, q_sa = 0.f;
-  const int a_b = act[b];
 #pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j) {
+  for (int j = 0; j < MAXA; ++j) {
     if (j < A) {
       if (q_n[j] > best) { best = q_n[j]; astar = j; qg_star = q_g[j]; }
       if (j == a_b) q_sa = q_t[j];
     }
   }
   (void)astar;
-  const float G = rew[b] + gam[b] * qg_star;
+  const float G = rew_b + gam_b * qg_star;
   const float delta = G - q_sa;
   const float ad = fabsf(delta);
   float l, dl;
@@ -274,7 +335,7 @@ __device__ __forceinline__ bool ddqn_head_body(
     l = 0.5f * delta * delta;
     dl = delta;
   }
-  const float w = isw ? isw[b] : 1.0f;
+  const float w = w_b;
   // d loss_mean / d q(S_t, a_b) = -w * dl / B  (grad_scale = 1/B)
   const float dq = -w * dl * grad_scale;
   if (lane == 0) {
@@ -285,32 +346,19 @@ __device__ __forceinline__ bool ddqn_head_body(
   if (q_out != nullptr && lane < A) {
     float qv = 0.f;
 #pragma unroll
-    for (int j = 0; j < HEAD_MAXA; ++j)
+    for (int j = 0; j < MAXA; ++j)
       if (j == lane) qv = q_t[j];
     q_out[(int64_t)b * A + lane] = qv;
   }
   const float invA = 1.0f / (float)A;
   if (lane < A) dhead[(int64_t)b * (A + 1) + 1 + lane] = dq * ((lane == a_b ? 1.f : 0.f) - invA);
   // back through the heads and the stream ReLUs
-  float dv[NPL], da[NPL], wvv[NPL];
-  load_w<NPL>(Pon.wv + lane * NPL, wvv);
+  // (wv, wa's column sums and the taken action's row: kept by head_q)
+  float dv[NPL], da[NPL];
 #pragma unroll
-  for (int k = 0; k < NPL; ++k) dv[k] = hv_t[k] > 0.f ? dq * wvv[k] : 0.f;
-  float colsum[NPL], wsel[NPL];
+  for (int k = 0; k < NPL; ++k) dv[k] = hv_t[k] > 0.f ? dq * kwv[k] : 0.f;
 #pragma unroll
-  for (int k = 0; k < NPL; ++k) { colsum[k] = 0.f; wsel[k] = 0.f; }
-  for (int j = 0; j < A; ++j) {
-    float wr[NPL];
-    load_w<NPL>(Pon.wa + j * HS + lane * NPL, wr);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const float ww = wr[k];
-      colsum[k] += ww;
-      if (j == a_b) wsel[k] = ww;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < NPL; ++k) da[k] = ha_t[k] > 0.f ? dq * (wsel[k] - colsum[k] * invA) : 0.f;
+  for (int k = 0; k < NPL; ++k) da[k] = ha_t[k] > 0.f ? dq * (kws[k] - kcs[k] * invA) : 0.f;
   if (split) {
     // fp32 dH -> hi / lo planes (NPL consecutive columns per stream: 2 per dword)
     uint32_t vh[NPL / 2], vl[NPL / 2], ah[NPL / 2], al[NPL / 2];

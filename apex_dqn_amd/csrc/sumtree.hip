@@ -704,6 +704,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
                                     uint64_t shard_seed, float* out_wscale, int64_t mcap, bf16_t* pb_lo,
                                     const double* wnorm, int wn, int wstride, CfFragOut fo, hipStream_t st) {
+  if (mcap <= 0) mcap = (int64_t)shard_world * B;
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
