@@ -540,6 +540,10 @@ class FusedNatureLearner(IsNormMixin):
                                                prio, norm=nrm,
                                                **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B],
                                                           Hon_lo=self.h_lo))
+        # (conv3's weight gradient after conv1's on the main stream, where the chain has
+        # slack at 512 rows: 2,674 / 2,668 vs 2,677 / 2,675 fp32, 4,271 / 4,312 vs 4,388 /
+        # 4,489 bf16, 6,078 / 6,056 vs 6,478 / 6,437 at 74 rows -- the co-running kernels
+        # stretch instead, profiles/r4_ab_wgrad3_main_rejected.txt)
         self._conv32_branched(main, side, jobs)
         fuse = self._fuse_norm
         jobs1 = []
@@ -560,9 +564,14 @@ class FusedNatureLearner(IsNormMixin):
         self.ops.conv_wgrad(self.dY2, self.y1[:B], 4, 2, self.G["w2"], self.G["b2"], jobs=jobs,
                             **self._lo(dy_lo=self.dY2_lo, x_lo=sp and self.y1_lo[:B]))
 
+    def _conv3_wgrad(self, jobs) -> None:
+        B, sp = self.B, self.split
+        self.ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, self.G["w3"], self.G["b3"], jobs=jobs,
+                            **self._lo(dy_lo=self.dY3_lo, x_lo=sp and self.y2_lo[:B]))
+
     def _conv32_branched(self, main, side, jobs, wgrad2: bool = True) -> None:
         """Branched backward, middle part: conv3 / conv2 data gradients on the main stream,
-        conv3 (and, ``wgrad2``, conv2) weight gradients on the branch, each after a wait for
+        conv3 and (``wgrad2``) conv2 weight gradients on the branch, each after a wait for
         the data gradient it reads.  (One wait before both weight gradients -- one graph
         edge fewer -- measured 5,937 / 6,062 vs 6,240 / 6,437 steps/s at 74 rows and
         neutral at 512, profiles/r4_ab_bwd_one_wait_rejected.txt.)"""
@@ -573,8 +582,7 @@ class FusedNatureLearner(IsNormMixin):
                        **self._lo(dy_lo=self.dY3_lo, w_lo=sp and Pl["w3"], dx_lo=self.dY2_lo))
         side.wait_event(ev3)
         with torch.cuda.stream(side):
-            ops.conv_wgrad(self.dY3, self.y2[:B], 3, 1, G["w3"], G["b3"], jobs=jobs,
-                           **self._lo(dy_lo=self.dY3_lo, x_lo=sp and self.y2_lo[:B]))
+            self._conv3_wgrad(jobs)
         ev2 = torch.cuda.Event()
         ev2.record(main)
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1,

@@ -17,7 +17,6 @@ import json
 import os
 import sys
 import time
-import types
 
 import torch
 
@@ -38,9 +37,7 @@ def main():
     from apex_dqn_amd.ops import _lib
     lib = _lib.require_kernels()
     dev = torch.device("cuda", 0)
-    args = types.SimpleNamespace(replay=100000, actions=4, batch=512, no_graphs=False, backend="hip", network="nature64",
-                                 no_presample=False, force_dp=False, comm="torch", graph_steps=None, learner="fused",
-                                 graph_impala=False)
+    args = bench.parser().parse_args([])
     replay = bench.make_replay(args, dev, 0)
     cfg, L = bench.make_learner(args, a.dtype, dev, None, 0, replay)
     for _ in range(a.warmup):

@@ -3,7 +3,6 @@ fc_wgrad_head_prio_kernel) against its parts, at the learner's shapes (B=512):
 fc weight-gradient GEMM alone, head wgrad alone, the tree update alone."""
 from __future__ import annotations
 
-import argparse
 import json
 import os
 import sys
@@ -21,9 +20,7 @@ def main():
     dev = torch.device("cuda", 0)
     res = {}
     for dtype in ("bf16", "fp32"):
-        args = argparse.Namespace(replay=100000, actions=4, batch=512, no_graphs=False, backend="hip",
-                                  network="nature64", no_presample=False, force_dp=False, comm="torch",
-                                  graph_steps=None, learner="fused", graph_impala=False)
+        args = bench.parser().parse_args(["--batch", os.environ.get("B", "512")])
         from apex_dqn_amd.parallel.dist import Comm
         comm = Comm(0, 1, dev)
         replay = bench.make_replay(args, dev, 0)
