@@ -11,6 +11,11 @@
 //     while this one computes);
 //   * the image's 400 x 64 dY1 rows (+16 zero rows), LDS-DMA'd with the
 //     transposed-read swizzle applied through the SOURCE addresses.
+// Work items: item i (< gridDim.x) is the image group {i, i + G, i + 2G, ...}; its
+// partial goes to slab slot i.  Statically workgroup i does item i; with the work
+// queue (d.wq, the data-parallel step, where RCCL's kernels can hold CUs) a resident
+// workgroup takes the items of workgroups that have no CU yet.  Either way every slot
+// holds the same image group's sum, so the reduction is bit-identical.
 // The reduction runs over pixels (MFMA K = 32 pixels): dY fragments come from
 // ds_read_b64_tr_b16 on the dY image, X fragments from ds_read_b64_tr_b16 with
 // per-lane plane addresses (4 consecutive k of one pixel are 8 contiguous bytes).
@@ -38,6 +43,7 @@ struct Conv1WgDesc {
   const uint8_t* zero16;      // 16 zero bytes (DMA filler)
   int N, C;
   const bf16_t* dy_lo;        // split mode: lo plane of dY (else null)
+  unsigned long long* wq;     // item work queue counter (csrc/mfma_common.h wq_next); null: static order
 };
 
 template <int C, bool SPLIT>
@@ -199,50 +205,65 @@ __global__ void __launch_bounds__(C1W_THREADS, 1) conv1_wgrad_img_kernel(Conv1Wg
   };
 
   const int G = gridDim.x;
-  int img = blockIdx.x;
-  if (img < d.N) issue_frames(img);
-  if constexpr (SPLIT) {
-    for (; img < d.N; img += G) {
-      issue_dy_half(img, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // frames(img) + dY half 0 of this wave
+  __shared__ int q_item;
+  int wq_seq = 0;
+  if (tid == 0) reinterpret_cast<volatile int*>(&q_item)[0] = wq_next(d.wq, wq_seq, G);
+  __syncthreads();
+  int item = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_item)[0]);
+  while (item < G) {
+    int img = item;
+    if (img < d.N) issue_frames(img);
+    if constexpr (SPLIT) {
+      for (; img < d.N; img += G) {
+        issue_dy_half(img, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // frames(img) + dY half 0 of this wave
+        __builtin_amdgcn_s_barrier();
+        convert_frames();
+        __syncthreads();
+        compute_steps(0, DYR / 32, 0);
+        __syncthreads();                                    // dY planes and staging free
+        issue_dy_half(img, 1);
+        if (img + G < d.N) issue_frames(img + G);           // lands under half 1
+        vmcnt_le(img + G < d.N ? nfr_w : 0);                // dY half 1 of this wave
+        __builtin_amdgcn_s_barrier();
+        compute_steps(DYR / 32, 13, DYR);
+        __syncthreads();                                    // planes and dY may be overwritten
+      }
+    }
+    for (; !SPLIT && img < d.N; img += G) {
+      issue_dy(img);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // frames(img) + dY(img) of this wave
       __builtin_amdgcn_s_barrier();
       convert_frames();
       __syncthreads();
+      if (img + G < d.N) issue_frames(img + G);            // staging is free again
       compute_steps(0, DYR / 32, 0);
-      __syncthreads();                                    // dY planes and staging free
-      issue_dy_half(img, 1);
-      if (img + G < d.N) issue_frames(img + G);           // lands under half 1
-      vmcnt_le(img + G < d.N ? nfr_w : 0);                // dY half 1 of this wave
-      __builtin_amdgcn_s_barrier();
-      compute_steps(DYR / 32, 13, DYR);
-      __syncthreads();                                    // planes and dY may be overwritten
+      __syncthreads();   // planes and dY image may be overwritten
     }
-  }
-  for (; !SPLIT && img < d.N; img += G) {
-    issue_dy(img);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // frames(img) + dY(img) of this wave
-    __builtin_amdgcn_s_barrier();
-    convert_frames();
-    __syncthreads();
-    if (img + G < d.N) issue_frames(img + G);            // staging is free again
-    compute_steps(0, DYR / 32, 0);
-    __syncthreads();   // planes and dY image may be overwritten
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the next item (static order: none -- item + G), fetched before this one's stores
+    if (tid == 0) reinterpret_cast<volatile int*>(&q_item)[0] = wq_next(d.wq, wq_seq, G);
 
-  // ---- this block's partial: slab[block][co][k] (s2d K order), float4 along k
-  float* slab = d.slab + (int64_t)blockIdx.x * 64 * K;
-  const int pl = lane & 15;
+    // ---- this item's partial: slab[item][co][k] (s2d K order), float4 along k
+    float* slab = d.slab + (int64_t)item * 64 * K;
+    const int pl = lane & 15;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-      const int co = 16 * (2 * wc + i) + pl;
-      *reinterpret_cast<f32x4*>(slab + (int64_t)co * K + 16 * (C * wk + j) + 4 * g) = acc[i][j];
+      for (int j = 0; j < C; ++j) {
+        const int co = 16 * (2 * wc + i) + pl;
+        *reinterpret_cast<f32x4*>(slab + (int64_t)co * K + 16 * (C * wk + j) + 4 * g) = acc[i][j];
+        acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    if (wk == 0 && g == 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) d.bias_slab[(int64_t)item * 64 + 16 * (2 * wc + i) + pl] = accb[i][0];
     }
-  if (wk == 0 && g == 0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) d.bias_slab[(int64_t)blockIdx.x * 64 + 16 * (2 * wc + i) + pl] = accb[i][0];
+    for (int i = 0; i < 2; ++i) accb[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    item = __builtin_amdgcn_readfirstlane(reinterpret_cast<volatile int*>(&q_item)[0]);
+    __syncthreads();   // every wave has read q_item before thread 0 overwrites it
   }
 }
 

@@ -109,7 +109,7 @@ class FinalizeDesc(ctypes.Structure):
 class Conv1WgDesc(ctypes.Structure):
     """Image-resident conv1 weight gradient (mirrors ``Conv1WgDesc`` in csrc/conv1_wgrad.hip)."""
     _fields_ = [("ring", c_p), ("slots", c_p), ("dy", c_p), ("slab", c_p), ("bias_slab", c_p), ("zero16", c_p),
-                ("N", c_i), ("C", c_i), ("dy_lo", c_p)]
+                ("N", c_i), ("C", c_i), ("dy_lo", c_p), ("wq", c_p)]
 
 
 class Conv1S2DDesc(ctypes.Structure):

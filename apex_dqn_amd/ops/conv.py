@@ -548,6 +548,9 @@ def conv1_wgrad_ring(lib, ws: Workspace, dy: torch.Tensor, ring: torch.Tensor, s
     d.slab, d.bias_slab, d.zero16 = slab.data_ptr(), bslab.data_ptr(), zero.data_ptr()
     d.N, d.C = N, C
     d.dy_lo = _lib.ptr(dy_lo)
+    # item work queue where the launch runs beside the DP step's collectives (per-item
+    # partial slots: the reduction does not depend on which workgroup took an item)
+    d.wq = ws.wq(("c1w_wq", N, int(G)), dy.device)
     st = _lib.stream_ptr()
     _lib.check(lib.apex_conv1_wgrad_img(d, G, st), "conv1_wgrad_img")
     if jobs is not None:

@@ -525,7 +525,8 @@ def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
     """The persistent kernels' image work queue (csrc/mfma_common.h wq_next, enabled by the
     data-parallel learner) computes every image whole in one workgroup: the fused conv1 ->
     conv2 forward and the split conv2 data gradient give bit-identical outputs with the
-    queue on or off, and three queued launches in a row (one never-reset counter, read
+    queue on or off, as does the conv1 weight gradient (items = image groups, one partial
+    slot per item), and three queued launches in a row (one never-reset counter, read
     modulo items + workgroups) agree too."""
     from apex_dqn_amd.ops import conv as C_
     from apex_dqn_amd.replay.gpu_replay import to_s2d
@@ -540,6 +541,7 @@ def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
     dy = torch.randn(N, 9, 9, 64, generator=g)
     dh, dl = _split(dy)
     mask = torch.randn(N, 20, 20, 64, generator=g).to(DEV, torch.bfloat16)
+    d1h, d1l = _split(torch.randn(N, 20, 20, 64, generator=g) * 0.1)
     outs = []
     for wq, reps in ((False, 1), (True, 3)):
         ws = C_.Workspace()
@@ -551,11 +553,14 @@ def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
                                 y1_lo=y1l, copy_n=copy_n, grid=grid)
             dxh, dxl = _empty2(N, 20, 20, 64)
             C_.conv2_dgrad_img(_lib(), dh, w2h, mask, dxh, grid=grid, dy_lo=dl, w_lo=w2l, out_lo=dxl, ws=ws)
+            # conv1 weight gradient: items = image groups with per-item partial slots
+            dw1, db1 = torch.zeros(64, 4, 8, 8, device=DEV), torch.zeros(64, device=DEV)
+            C_.conv1_wgrad_ring(_lib(), ws, d1h, ring, slots, 1 / 255.0, dw1, db1, grid=grid, dy_lo=d1l)
             torch.cuda.synchronize()
-            outs.append((y2h, y2l, y1h, y1l, dxh, dxl))
+            outs.append((y2h, y2l, y1h, y1l, dxh, dxl, dw1, db1))
         if wq:   # each launch consumed exactly items + workgroups values of its counter
-            c = [int(t.item()) for k, t in ws.bufs.items() if k[0][0] in ("cf_wq", "c2d_wq")]
-            assert len(c) == 2 and all(v > 0 and v % 3 == 0 for v in c), c
+            c = [int(t.item()) for k, t in ws.bufs.items() if k[0][0] in ("cf_wq", "c2d_wq", "c1w_wq")]
+            assert len(c) == 3 and all(v > 0 and v % 3 == 0 for v in c), c
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
