@@ -224,6 +224,9 @@ class FusedNatureLearner(IsNormMixin):
         # the DP step's backward on the same two chains, its collectives issued from the
         # branch as their inputs complete (_dp_body_branched)
         self._dp_branched = self._dp and cuda and SW.bwd_branches
+        # (a high-priority branch stream measured neutral: 2,677 / 2,674 vs 2,685 / 2,684,
+        # profiles/r4_ab_branch_priority_neutral.txt -- the captured graph's queues do not
+        # keep it)
         self._wg_stream = torch.cuda.Stream(self.device) if (self._branched or self._dp_branched) else None
         # the fc layer's split-K epilogue runs inside the head launch (ops.fc_fwd defer_head;
         # SW.fc_epi_in_head = False keeps the separate epilogue launch)
