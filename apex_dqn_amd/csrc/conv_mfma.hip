@@ -22,6 +22,7 @@
 #include "mfma_common.h"
 #include "igemm_wgrad.h"
 #include "conv2_wfrag.h"
+#include "fc_sk.h"
 
 struct ConvDesc {
   const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]
@@ -650,7 +651,8 @@ __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
 // LW: four extra loader waves issue every DMA (the compute waves then carry only
 // MFMAs and fragment reads; an LDS-DMA issue costs ~60 cycles of the issuing wave).
 template <bool SPLIT, int NS, bool LW>
-__global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, float* __restrict__ ws, int kt_per) {
+__global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, float* __restrict__ ws, int kt_per,
+                                                                    FcSK sk) {
   constexpr int BM = 128, BN = 128;
   constexpr int HALF = (BM + BN) * 128;           // one precision plane of a stage
   constexpr int STAGE = SPLIT ? 2 * HALF : HALF;
@@ -660,130 +662,157 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
   __shared__ __attribute__((aligned(16))) uint8_t smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = LW ? (tid >> 6) & 3 : tid >> 6;
   const bool loader = !LW || tid >= 256, computer = !LW || tid < 256;
-  const int ntm = gridDim.x, ntn = gridDim.y;
+  const bool streamk = sk.nblk > 0;
+  const int ntm = streamk ? sk.ntm : gridDim.x, ntn = streamk ? sk.ntn : gridDim.y;
   // N tiles fastest, then M tiles, then K splits: the blocks of one XCD share A rows
   // and a K range (consecutive logical ids land on one XCD)
-  const int wg = xcd_swizzle(blockIdx.x + ntm * (blockIdx.y + ntn * blockIdx.z), ntm * ntn * gridDim.z);
-  const int by = wg % ntn;
-  const int bx = (wg / ntn) % ntm;
-  const int bz = wg / (ntn * ntm);
+  const int wg = streamk ? xcd_swizzle(blockIdx.x, gridDim.x)
+                         : xcd_swizzle(blockIdx.x + ntm * (blockIdx.y + ntn * blockIdx.z), ntm * ntn * gridDim.z);
   const int M = d.N, Nc = d.Cout;
-  const RowTile rt = row_tile(d, bx, BM, M);
-  const int m0 = rt.m0, mend = rt.mend, n0 = by * BN;
   const int KT = d.K >> 6;
-  const int kt0 = bz * kt_per;
-  const int nk = min(KT, kt0 + kt_per) - kt0;     // >= 1 (host sizes the grid)
-  const bool second = rt.second;
-  const uint8_t* wb = reinterpret_cast<const uint8_t*>(second ? d.w2 : d.w);
-  const uint8_t* wl = SPLIT ? reinterpret_cast<const uint8_t*>(second ? d.w2_lo : d.w_lo) : wb;
   const uint8_t* xa = reinterpret_cast<const uint8_t*>(d.x);
   const uint8_t* xl = SPLIT ? reinterpret_cast<const uint8_t*>(d.x_lo) : xa;
-
-  // instruction i of wave wv fills tile rows 8 (wv + 4 i) .. +7: lane >> 3 picks the
-  // row, lane & 7 the LDS slot, and the source chunk is the one swz_row puts there
-  uint32_t a_off[NA], b_off[NB];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int r = 8 * (wv + 4 * i) + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    const int m = m0 + r < mend ? m0 + r : 0;
-    a_off[i] = ((uint32_t)m * d.K + c * 8) * 2u;
-  }
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const int r = 8 * (wv + 4 * i) + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    b_off[i] = ((uint32_t)(n0 + r) * d.K + c * 8) * 2u;
-  }
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
-  int lt = 0;
-  auto issue = [&]() {
-    const uint32_t dst = lds0 + (uint32_t)(lt % NS) * STAGE;
-    const uint32_t toff = (uint32_t)(kt0 + lt) * 128u;
+  const int wm = wv >> 1, wn = wv & 1;
+
+  // Segments: one (tile, K range) in the K-split mode; stream-K: the tiles this
+  // workgroup's iteration range [u, uend) touches, each with its partial plane.
+  int64_t u = 0, uend = 1;
+  if (streamk) {
+    u = fc_sk_start(sk, wg);
+    uend = fc_sk_start(sk, wg + 1);
+  }
+  while (u < uend) {
+    int tile, kt0, nk, bz;
+    if (streamk) {
+      tile = (int)(u / KT);
+      kt0 = (int)(u - (int64_t)tile * KT);
+      const int kend = (int)min((int64_t)KT, uend - (int64_t)tile * KT);
+      nk = kend - kt0;
+      bz = wg - fc_sk_owner(sk, (int64_t)tile * KT);
+      u = (int64_t)tile * KT + kend;
+    } else {
+      tile = wg % (ntn * ntm);
+      bz = wg / (ntn * ntm);
+      kt0 = bz * kt_per;
+      nk = min(KT, kt0 + kt_per) - kt0;              // >= 1 (host sizes the grid)
+      u = uend;
+    }
+    const int by = tile % ntn;
+    const int bx = tile / ntn;
+    const RowTile rt = row_tile(d, bx, BM, M);
+    const int m0 = rt.m0, mend = rt.mend, n0 = by * BN;
+    const bool second = rt.second;
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(second ? d.w2 : d.w);
+    const uint8_t* wl = SPLIT ? reinterpret_cast<const uint8_t*>(second ? d.w2_lo : d.w_lo) : wb;
+
+    // instruction i of wave wv fills tile rows 8 (wv + 4 i) .. +7: lane >> 3 picks the
+    // row, lane & 7 the LDS slot, and the source chunk is the one swz_row puts there
+    uint32_t a_off[NA], b_off[NB];
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const uint32_t l = __builtin_amdgcn_readfirstlane(dst + (wv + 4 * i) * 1024);
-      dma16(xa + a_off[i] + toff, l);
-      if (SPLIT) dma16(xl + a_off[i] + toff, l + HALF);
+      const int r = 8 * (wv + 4 * i) + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int m = m0 + r < mend ? m0 + r : 0;
+      a_off[i] = ((uint32_t)m * d.K + c * 8) * 2u;
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      const uint32_t l = __builtin_amdgcn_readfirstlane(dst + BM * 128 + (wv + 4 * i) * 1024);
-      dma16(wb + b_off[i] + toff, l);
-      if (SPLIT) dma16(wl + b_off[i] + toff, l + HALF);
+      const int r = 8 * (wv + 4 * i) + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      b_off[i] = ((uint32_t)(n0 + r) * d.K + c * 8) * 2u;
     }
-    ++lt;
-  };
+    int lt = 0;
+    auto issue = [&]() {
+      const uint32_t dst = lds0 + (uint32_t)(lt % NS) * STAGE;
+      const uint32_t toff = (uint32_t)(kt0 + lt) * 128u;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const uint32_t l = __builtin_amdgcn_readfirstlane(dst + (wv + 4 * i) * 1024);
+        dma16(xa + a_off[i] + toff, l);
+        if (SPLIT) dma16(xl + a_off[i] + toff, l + HALF);
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const uint32_t l = __builtin_amdgcn_readfirstlane(dst + BM * 128 + (wv + 4 * i) * 1024);
+        dma16(wb + b_off[i] + toff, l);
+        if (SPLIT) dma16(wl + b_off[i] + toff, l + HALF);
+      }
+      ++lt;
+    };
 
-  f32x4 acc[4][4];
+    f32x4 acc[4][4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int wm = wv >> 1, wn = wv & 1;
+      for (int b = 0; b < 4; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
-    const uint8_t* As = smem + buf * STAGE;
-    const uint8_t* Bs = As + BM * 128;
+    auto compute = [&](int buf) {
+      const uint8_t* As = smem + buf * STAGE;
+      const uint8_t* Bs = As + BM * 128;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int c = 4 * s + (lane >> 4);
-      bf16x8 a[4], b[4], al[4], bl[4];
+      for (int s = 0; s < 2; ++s) {
+        const int c = 4 * s + (lane >> 4);
+        bf16x8 a[4], b[4], al[4], bl[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        a[t] = *reinterpret_cast<const bf16x8*>(As + swz_row(64 * wm + 16 * t + (lane & 15), c));
-        b[t] = *reinterpret_cast<const bf16x8*>(Bs + swz_row(64 * wn + 16 * t + (lane & 15), c));
+        for (int t = 0; t < 4; ++t) {
+          a[t] = *reinterpret_cast<const bf16x8*>(As + swz_row(64 * wm + 16 * t + (lane & 15), c));
+          b[t] = *reinterpret_cast<const bf16x8*>(Bs + swz_row(64 * wn + 16 * t + (lane & 15), c));
+          if (SPLIT) {
+            al[t] = *reinterpret_cast<const bf16x8*>(As + HALF + swz_row(64 * wm + 16 * t + (lane & 15), c));
+            bl[t] = *reinterpret_cast<const bf16x8*>(Bs + HALF + swz_row(64 * wn + 16 * t + (lane & 15), c));
+          }
+        }
+        // product-major order: 16 independent accumulators between dependent MFMAs
         if (SPLIT) {
-          al[t] = *reinterpret_cast<const bf16x8*>(As + HALF + swz_row(64 * wm + 16 * t + (lane & 15), c));
-          bl[t] = *reinterpret_cast<const bf16x8*>(Bs + HALF + swz_row(64 * wn + 16 * t + (lane & 15), c));
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[nt], a[mt], acc[mt][nt], 0, 0, 0);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], al[mt], acc[mt][nt], 0, 0, 0);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+      }
+    };
+
+    if (loader) {
+#pragma unroll
+      for (int p = 0; p < NS - 1; ++p)
+        if (p < nk) issue();
+    }
+    for (int j = 0; j < nk; ++j) {
+      if (loader) vmcnt_le(min(NS - 2, nk - 1 - j) * DPT);
+      __syncthreads();
+      if (loader && j + NS - 1 < nk) issue();
+      if (computer) compute(j % NS);
+    }
+
+    // partial tile -> ws[bz][m][n]: lane (g = lane >> 4, pl = lane & 15) of MFMA tile
+    // (mt, nt) holds row 16 mt + pl, columns 16 nt + 4 g .. +3
+    if (computer) {
+      float* wz = ws + (int64_t)bz * M * Nc;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = m0 + 64 * wm + 16 * mt + (lane & 15);
+        if (m >= mend) continue;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int n = n0 + 64 * wn + 16 * nt + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(wz + (int64_t)m * Nc + n) = acc[mt][nt];
         }
       }
-      // product-major order: 16 independent accumulators between dependent MFMAs
-      if (SPLIT) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[nt], a[mt], acc[mt][nt], 0, 0, 0);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], al[mt], acc[mt][nt], 0, 0, 0);
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
     }
-  };
-
-  if (loader) {
-#pragma unroll
-    for (int p = 0; p < NS - 1; ++p)
-      if (p < nk) issue();
-  }
-  for (int j = 0; j < nk; ++j) {
-    if (loader) vmcnt_le(min(NS - 2, nk - 1 - j) * DPT);
-    __syncthreads();
-    if (loader && j + NS - 1 < nk) issue();
-    if (computer) compute(j % NS);
-  }
-  if (!computer) return;
-
-  // partial tile -> ws[bz][m][n]: lane (g = lane >> 4, pl = lane & 15) of MFMA tile
-  // (mt, nt) holds row 16 mt + pl, columns 16 nt + 4 g .. +3
-  float* wz = ws + (int64_t)bz * M * Nc;
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    const int m = m0 + 64 * wm + 16 * mt + (lane & 15);
-    if (m >= mend) continue;
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int n = n0 + 64 * wn + 16 * nt + 4 * (lane >> 4);
-      *reinterpret_cast<f32x4*>(wz + (int64_t)m * Nc + n) = acc[mt][nt];
-    }
+    // the next segment's DMA must not land in a stage a compute wave still reads
+    if (u < uend) __syncthreads();
   }
 }
 
@@ -796,7 +825,7 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
 
 template <bool SPLIT>
 __global__ void __launch_bounds__(256) fc_splitk_epilogue_kernel(ConvDesc d, const float* __restrict__ ws,
-                                                                 int nz, int eb, C2dPackJob pk) {
+                                                                 int nz, int eb, C2dPackJob pk, FcSK sk) {
   if ((int)blockIdx.x >= eb) {
     pack_c2d_wfrag_word(((int)blockIdx.x - eb) * 256 + threadIdx.x, pk.w, pk.w_lo, pk.out);
     return;
@@ -806,6 +835,7 @@ __global__ void __launch_bounds__(256) fc_splitk_epilogue_kernel(ConvDesc d, con
   const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (e >= MN) return;
   const int m = (int)(e / Nc), n = (int)(e - (int64_t)m * Nc);
+  if (sk.nblk > 0) nz = fc_sk_count(sk, fc_sk_tile(sk, m, n));   // stream-K: this tile's planes
   float v[8];
   {
     const float4 p0 = *reinterpret_cast<const float4*>(ws + e);
@@ -995,13 +1025,45 @@ static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
 }
 
 // Dense C[M,N] = act(A[M,K] . B[N,K]^T + b) on 128x128 tiles, K split `ksplit` ways
-// (fc_gemm128_kernel + fc_splitk_epilogue_kernel).  ws: fp32 workspace of at least
-// ksplit * M * N elements.  Row-major B only (d.bt == 0), N % 128 == 0.  pk: optional
-// conv2 weight-fragment pack riding on the epilogue launch (fc_splitk_epilogue_kernel).
-// no_epilogue: only the GEMM runs; the caller consumes the ws partials.
+// (fc_gemm128_kernel + fc_splitk_epilogue_kernel), or with ksplit = -nblk a stream-K
+// split over nblk workgroups (csrc/fc_sk.h).  ws: fp32 workspace of at least planes *
+// M * N elements (planes = ksplit, or apex_fc_sk_planes).  Row-major B only (d.bt == 0),
+// N % 128 == 0.  pk: optional conv2 weight-fragment pack riding on the epilogue launch
+// (fc_splitk_epilogue_kernel).  no_epilogue: only the GEMM runs; the caller consumes the
+// ws partials.
+static FcSK fc_sk_of(const ConvDesc& d, int nblk) {
+  FcSK s;
+  s.nblk = nblk;
+  s.kt = d.K >> 6;
+  s.ntm = row_tiles(d, d.N, 128);
+  s.ntn = d.Cout / 128;
+  s.m_switch = d.w2 != nullptr ? d.m_switch : -1;
+  return s;
+}
+
+// partial planes of a stream-K fc forward of M rows (second weight set from row
+// m_switch, or -1) over nblk workgroups; 0 for an invalid shape
+APEX_EXPORT int apex_fc_sk_planes(int M, int Nc, int K, int m_switch, int nblk) {
+  if (M <= 0 || (Nc & 127) || (K & 63) || K <= 0 || nblk < 1) return 0;
+  ConvDesc d{};
+  d.N = M;
+  d.Cout = Nc;
+  d.K = K;
+  d.m_switch = m_switch;
+  d.w2 = m_switch >= 0 ? reinterpret_cast<const bf16_t*>(16) : nullptr;
+  FcSK s = fc_sk_of(d, nblk);
+  if (fc_sk_total(s) < nblk) return 0;
+  int nz = 0;
+  for (int t = 0; t < s.ntm * s.ntn; ++t) {
+    const int c = fc_sk_count(s, t);
+    nz = c > nz ? c : nz;
+  }
+  return nz;
+}
+
 APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksplit, int loader_waves,
                                 int no_epilogue, C2dPackJob pk, hipStream_t st) {
-  if (d.mode != 0 || d.bt != 0 || (d.K & 63) || d.K <= 0 || (d.Cout & 127) || d.N <= 0 || ksplit < 1)
+  if (d.mode != 0 || d.bt != 0 || (d.K & 63) || d.K <= 0 || (d.Cout & 127) || d.N <= 0 || ksplit == 0)
     return (int)hipErrorInvalidValue;
   if ((d.ldy & 7) || d.ldy < d.Cout) return (int)hipErrorInvalidValue;
   if ((int64_t)d.N * d.K * 2 >= 0x7ffffff0LL || (int64_t)d.Cout * d.K * 2 >= 0x7ffffff0LL)
@@ -1011,16 +1073,26 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   if (split && (d.w_lo == nullptr || d.y_lo == nullptr || (d.w2 != nullptr && d.w2_lo == nullptr)))
     return (int)hipErrorInvalidValue;
   const int KT = d.K >> 6;
-  const int kt_per = (KT + ksplit - 1) / ksplit;
-  const int nz = (KT + kt_per - 1) / kt_per;
-  if (ws == nullptr || ws_elems < (int64_t)nz * d.N * d.Cout) return (int)hipErrorInvalidValue;
-  const dim3 grid(row_tiles(d, d.N, 128), d.Cout / 128, nz);
-  if (loader_waves) {
-    if (split) fc_gemm128_kernel<true, 2, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
-    else fc_gemm128_kernel<false, 4, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
+  FcSK sk{};
+  int kt_per = KT, nz;
+  dim3 grid;
+  if (ksplit < 0) {            // stream-K over -ksplit workgroups
+    sk = fc_sk_of(d, -ksplit);
+    if (fc_sk_total(sk) < sk.nblk) return (int)hipErrorInvalidValue;
+    nz = apex_fc_sk_planes(d.N, d.Cout, d.K, sk.m_switch, sk.nblk);
+    grid = dim3(sk.nblk);
   } else {
-    if (split) fc_gemm128_kernel<true, 2, false><<<grid, 256, 0, st>>>(d, ws, kt_per);
-    else fc_gemm128_kernel<false, 4, false><<<grid, 256, 0, st>>>(d, ws, kt_per);
+    kt_per = (KT + ksplit - 1) / ksplit;
+    nz = (KT + kt_per - 1) / kt_per;
+    grid = dim3(row_tiles(d, d.N, 128), d.Cout / 128, nz);
+  }
+  if (ws == nullptr || nz < 1 || ws_elems < (int64_t)nz * d.N * d.Cout) return (int)hipErrorInvalidValue;
+  if (loader_waves) {
+    if (split) fc_gemm128_kernel<true, 2, true><<<grid, 512, 0, st>>>(d, ws, kt_per, sk);
+    else fc_gemm128_kernel<false, 4, true><<<grid, 512, 0, st>>>(d, ws, kt_per, sk);
+  } else {
+    if (split) fc_gemm128_kernel<true, 2, false><<<grid, 256, 0, st>>>(d, ws, kt_per, sk);
+    else fc_gemm128_kernel<false, 4, false><<<grid, 256, 0, st>>>(d, ws, kt_per, sk);
   }
   const int64_t nthr = (int64_t)d.N * d.Cout / 8;
   const int eb = (int)((nthr + 255) / 256);
@@ -1032,8 +1104,8 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   }
   if (pk.out != nullptr && (pk.w == nullptr || ((uintptr_t)pk.out & 15))) return (int)hipErrorInvalidValue;
   const int pb = pk.out != nullptr ? C2D_PACK_THREADS / 256 : 0;
-  if (split) fc_splitk_epilogue_kernel<true><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk);
-  else fc_splitk_epilogue_kernel<false><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk);
+  if (split) fc_splitk_epilogue_kernel<true><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk, sk);
+  else fc_splitk_epilogue_kernel<false><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk, sk);
   APEX_CHECK_LAUNCH();
 }
 

@@ -5,6 +5,7 @@
 // and fc_wgrad_head_prio_kernel beside the priority write-back).
 #pragma once
 #include "apex_common.h"
+#include "fc_sk.h"
 
 #define HEAD_MAXA 32
 
@@ -106,6 +107,7 @@ struct HeadPart {
   int two_b;
   bf16_t* hon;            // rows [0, B) of h written back (hi plane / bf16)
   bf16_t* hon_lo;         // split mode: lo plane (else null)
+  FcSK sk;                // stream-K fc forward (sk.nblk > 0): per-tile plane counts; nz = the most
 };
 
 template <int HS>
@@ -120,6 +122,13 @@ __device__ __forceinline__ void load_row_part(const HeadPart& hp, int row, int l
   const float* __restrict__ bias = row < hp.two_b ? hp.bias_on : hp.bias_tg;
   float v[2][NPL], bs[2][NPL];
   const float* p0 = hp.part + (int64_t)row * ROW + lane * NPL;
+  // partial planes of each stream's columns (stream-K: per 128-column tile)
+  int nzs[2] = {hp.nz, hp.nz};
+  if (hp.sk.nblk > 0) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) nzs[st] = fc_sk_count(hp.sk, fc_sk_tile(hp.sk, row, st * HS + lane * NPL));
+  }
+  const int nzmax = nzs[0] > nzs[1] ? nzs[0] : nzs[1];
 #pragma unroll
   for (int st = 0; st < 2; ++st)
 #pragma unroll
@@ -129,7 +138,7 @@ __device__ __forceinline__ void load_row_part(const HeadPart& hp, int row, int l
       v[st][k] = a.x; v[st][k + 1] = a.y; v[st][k + 2] = a.z; v[st][k + 3] = a.w;
       bs[st][k] = b.x; bs[st][k + 1] = b.y; bs[st][k + 2] = b.z; bs[st][k + 3] = b.w;
     }
-  for (int z0 = 1; z0 < hp.nz; z0 += ZU) {
+  for (int z0 = 1; z0 < nzmax; z0 += ZU) {
     float4 t[ZU][2][NPL / 4];
 #pragma unroll
     for (int u = 0; u < ZU; ++u)
@@ -137,20 +146,20 @@ __device__ __forceinline__ void load_row_part(const HeadPart& hp, int row, int l
       for (int st = 0; st < 2; ++st)
 #pragma unroll
         for (int k = 0; k < NPL / 4; ++k)
-          t[u][st][k] = z0 + u < hp.nz
+          t[u][st][k] = z0 + u < nzs[st]
                             ? *reinterpret_cast<const float4*>(p0 + (int64_t)(z0 + u) * hp.zstride + st * HS + 4 * k)
                             : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int u = 0; u < ZU; ++u) {
-      if (z0 + u >= hp.nz) break;
+    for (int u = 0; u < ZU; ++u)
 #pragma unroll
-      for (int st = 0; st < 2; ++st)
+      for (int st = 0; st < 2; ++st) {
+        if (z0 + u >= nzs[st]) continue;      // (no +0.0: keeps a -0.0 sum bit-exact)
 #pragma unroll
         for (int k = 0; k < NPL / 4; ++k) {
           v[st][4 * k] += t[u][st][k].x; v[st][4 * k + 1] += t[u][st][k].y;
           v[st][4 * k + 2] += t[u][st][k].z; v[st][4 * k + 3] += t[u][st][k].w;
         }
-    }
+      }
   }
 #pragma unroll
   for (int st = 0; st < 2; ++st) {       // value stream, advantage stream

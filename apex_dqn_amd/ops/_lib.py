@@ -46,10 +46,15 @@ class HeadLo(ctypes.Structure):
     _fields_ = [("Hon", c_p), ("Htg", c_p), ("dH", c_p)]
 
 
+class FcSK(ctypes.Structure):
+    """Stream-K split of the fc forward (mirrors ``FcSK``, csrc/fc_sk.h)."""
+    _fields_ = [("nblk", c_i), ("kt", c_i), ("ntm", c_i), ("ntn", c_i), ("m_switch", c_i)]
+
+
 class HeadPart(ctypes.Structure):
     """fc split-K partials consumed by the DDQN head (mirrors ``HeadPart``, csrc/head_common.h)."""
     _fields_ = [("part", c_p), ("zstride", c_i64), ("nz", c_i), ("bias_on", c_p), ("bias_tg", c_p),
-                ("two_b", c_i), ("hon", c_p), ("hon_lo", c_p)]
+                ("two_b", c_i), ("hon", c_p), ("hon_lo", c_p), ("sk", FcSK)]
 
 
 class IsNorm(ctypes.Structure):

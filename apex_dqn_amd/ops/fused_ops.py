@@ -386,16 +386,19 @@ class HipBackend(TorchBackend):
             # 192 blocks), more for the few row tiles of a small per-rank batch (global-batch
             # DP: 74 rows per rank -> 24 tiles x 10 splits)
             tiles = C.row_tiles_host(M, rows_first if w2 is not None else None, 128) * (w.shape[0] // 128)
-            ks = max(2, 256 // max(tiles, 1))
-            if SW.fc_ksplit_max > 0:
-                ks = max(1, min(ks, SW.fc_ksplit_max))
+            if SW.fc_stream_k > 0 and tiles * (K // 64) >= SW.fc_stream_k:
+                ks = -SW.fc_stream_k          # stream-K: every workgroup an equal (tile, K) range
+            else:
+                ks = max(2, 256 // max(tiles, 1))
+                if SW.fc_ksplit_max > 0:
+                    ks = max(1, min(ks, SW.fc_ksplit_max))
             r = C.dense_fwd128(self.lib, self.ws, x.reshape(M, K), w, b, out, True, w2, b2, rows_first, ks, True,
                                x_lo=None if x_lo is None else x_lo.reshape(M, K), w_lo=w_lo, w2_lo=w2_lo,
                                out_lo=out_lo, c2d_pack=None if defer else c2d, no_epilogue=defer)
             if defer:
                 # the split-K epilogue (and the conv2 pack) move into the next head launch
-                self._fc_part = dict(part=r[0], nz=r[1], zstride=M * w.shape[0], b=b, b2=b2, two_b=rows_first,
-                                     out=out, c2d=c2d)
+                self._fc_part = dict(part=r[0], nz=r[1], sk=r[2], zstride=M * w.shape[0], b=b, b2=b2,
+                                     two_b=rows_first, out=out, c2d=c2d)
                 return
             # the conv2 data gradient of this step finds its weights packed (the key is
             # checked there, so a different weight tensor still packs its own)
@@ -486,6 +489,8 @@ class HipBackend(TorchBackend):
             self._fc_part = None
             assert fp["out"].data_ptr() == Hon.data_ptr() and fp["two_b"] == 2 * B
             hp.part, hp.zstride, hp.nz = fp["part"].data_ptr(), int(fp["zstride"]), int(fp["nz"])
+            if fp.get("sk") is not None:
+                hp.sk = fp["sk"]
             hp.bias_on, hp.bias_tg, hp.two_b = fp["b"].data_ptr(), fp["b2"].data_ptr(), int(fp["two_b"])
             hp.hon, hp.hon_lo = Hon.data_ptr(), _lib.ptr(None if lo is None else lo[0])
             if fp["c2d"] is not None:
