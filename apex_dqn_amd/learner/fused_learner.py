@@ -441,7 +441,7 @@ class FusedNatureLearner(IsNormMixin):
             return self._seg2_branched()
         B, rt, ops, G, Pb, Pl = self.B, self.rt, self.ops, self.G, self.Pb, self.Pl
         sp = self.split
-        jobs = []    # split-K reductions, finalised in ONE launch at the end
+        jobs = []    # split-K reductions of conv3 / conv2, finalised at the end
         ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
                      **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
         if after_first is not None:
@@ -454,10 +454,17 @@ class FusedNatureLearner(IsNormMixin):
                        **self._lo(dy_lo=self.dY2_lo, x_lo=sp and self.y1_lo[:B]))
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1,
                        **self._lo(dy_lo=self.dY2_lo, w_lo=sp and Pl["w2"], dx_lo=self.dY1_lo))
+        jobs1 = []
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
-                             G["b1"], jobs=jobs, **self._lo(dy_lo=self.dY1_lo))
-        norm = dict(part=self.norm_part, slot0=self._fc_slots) if self._fuse_norm else None
-        self._npart = ops.finalize_grads(jobs, self.g_head_region if self._fuse_norm else None, norm)
+                             G["b1"], jobs=jobs1, **self._lo(dy_lo=self.dY1_lo))
+        # two finalisations, as the branched step runs them (conv3 / conv2 + the head
+        # region's norm partials, then conv1): the same norm-partial slots, so the two
+        # schedules give bit-identical updates
+        fuse = self._fuse_norm
+        n1 = ops.finalize_grads(jobs, self.g_head_region if fuse else None,
+                                dict(part=self.norm_part, slot0=self._fc_slots) if fuse else None)
+        n2 = ops.finalize_grads(jobs1, None, dict(part=self.norm_part, slot0=n1) if fuse else None)
+        self._npart = n2 if fuse else 0
         if self._comm_bf16:
             cut = self.layout.offsets["wfc"]
             self.gcomm[:cut].copy_(self.g32[:cut])

@@ -46,7 +46,7 @@ trace)
   TAG=$1; shift
   cd /tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${TAG}_step -o run -- \
-      python $R/bench.py --steps 200 --warmup 20 --no-bf16-extra "$@" > $R/gpurun_out/${TAG}_step.log 2>&1 || exit 1
+      python3 $R/bench.py --steps 200 --warmup 20 --no-bf16-extra "$@" > $R/gpurun_out/${TAG}_step.log 2>&1 || exit 1
   cd $R
   python scripts/prof_summary.py gpurun_out/${TAG}_step --steps 220 --top 40 > gpurun_out/${TAG}_step.md 2>&1
   python scripts/step_timeline.py gpurun_out/${TAG}_step/run_kernel_trace.csv > gpurun_out/${TAG}_timeline.txt 2>&1
@@ -55,7 +55,7 @@ pmc)
   TAG=$1; CNT=$2; shift 2
   cd /tmp
   timeout -s KILL 120 rocprofv3 --pmc $CNT --output-format csv -d $R/gpurun_out/${TAG}_pmc -o run -- \
-      python $R/bench.py --steps 50 --warmup 10 --no-bf16-extra "$@" > $R/gpurun_out/${TAG}_pmc.log 2>&1 || exit 1
+      python3 $R/bench.py --steps 50 --warmup 10 --no-bf16-extra "$@" > $R/gpurun_out/${TAG}_pmc.log 2>&1 || exit 1
   cd $R
   python scripts/pmc_summary.py gpurun_out/${TAG}_pmc > gpurun_out/${TAG}_pmc.md 2>&1; head -40 gpurun_out/${TAG}_pmc.md ;;
 ab)

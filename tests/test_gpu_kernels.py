@@ -474,8 +474,10 @@ def test_fc_head_wgrad_prio_matches_separate_launches(B):
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_branched_backward_matches_serial(monkeypatch, dtype):
     """SW.bwd_branches: the weight gradients on a second stream beside the data-gradient
-    chain (a captured graph branch) give the same updates as the one-stream step --
-    the same kernels on the same inputs, only scheduled side by side."""
+    chain (a captured graph branch) give BIT-IDENTICAL updates to the one-stream step --
+    the same kernels on the same inputs with the same norm-partial slots, only scheduled
+    side by side -- over 10 updates of the 4-update graph path that cross two target
+    syncs (q_target_sync_freq = 4)."""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.ops.switches import SW
@@ -484,16 +486,17 @@ def test_branched_backward_matches_serial(monkeypatch, dtype):
     for br in (False, True):
         monkeypatch.setattr(SW, "bwd_branches", br)
         cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
-                                    "Learner": {"replay_sample_size": 128},
+                                    "Learner": {"replay_sample_size": 128, "q_target_sync_freq": 4},
                                     "Runtime": {"use_graphs": True, "graph_steps": 4, "dtype": dtype}})
         torch.manual_seed(0)
         rp = GpuReplayShard(4000, 4000, 4100, 4, device=DEV, seed=3)
         _fill_replay(rp, 3800, seed=1)
         L = FusedNatureLearner(cfg, DEV, rp, backend="hip")
         assert L._branched == br
-        L.steps(6)
+        L.steps(10)
         torch.cuda.synchronize()
-        res[br] = (L.g32.clone(), L.p32.clone(), rp.leaf.clone(), L.S["idx"].clone())
-    assert torch.equal(res[False][3], res[True][3])
-    for a, b in zip(res[False][:3], res[True][:3]):
-        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-9)
+        assert L.num_q_updates == 10
+        res[br] = (L.g32.clone(), L.p32.clone(), L.t32.clone(), L.rms_v.clone(), L.rms_m.clone(),
+                   rp.leaf.clone(), L.S["idx"].clone())
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
