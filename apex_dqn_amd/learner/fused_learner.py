@@ -538,18 +538,32 @@ class FusedNatureLearner(IsNormMixin):
         sp = self.split
         main, side = torch.cuda.current_stream(self.device), self._wg_stream
         jobs = []
-        ev = torch.cuda.Event()
-        ev.record(main)
-        ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
-                     **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
-        side.wait_event(ev)
-        with torch.cuda.stream(side):
-            prio = (self.replay, S["idx"], S["gen"], self.td_abs)
-            nrm = (self.norm_part, 0) if self._fuse_norm else None
+        prio = (self.replay, S["idx"], S["gen"], self.td_abs)
+        nrm = (self.norm_part, 0) if self._fuse_norm else None
+
+        def fc_wgrad():
             self._fc_slots = ops.fc_head_wgrad(self.dH, self.y3[:B], G["wfc"], G["bfc"], self.h, self.dhead, G,
                                                prio, norm=nrm,
                                                **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B],
                                                           Hon_lo=self.h_lo))
+
+        # auto: fp32-class at >= 256 rows, 2,681 / 2,679 vs 2,654 / 2,665 steps/s; bf16 and
+        # 74 rows lose (4,264 / 4,214 vs 4,367 / 4,403; 6,077 vs 6,415),
+        # profiles/r4_ab_fc_wgrad_main.txt
+        fc_main = SW.fc_wgrad_main == "on" or (SW.fc_wgrad_main == "auto" and sp and B >= 256)
+        if not fc_main:
+            ev = torch.cuda.Event()
+            ev.record(main)
+        ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
+                     **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
+        if fc_main:
+            # fc dgrad and the fc weight gradient back to back on the main stream, each on
+            # the whole chip; the branch forks after them (its first wait, conv3's wgrad)
+            fc_wgrad()
+        else:
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                fc_wgrad()
         # (conv3's weight gradient after conv1's on the main stream, where the chain has
         # slack at 512 rows: 2,674 / 2,668 vs 2,677 / 2,675 fp32, 4,271 / 4,312 vs 4,388 /
         # 4,489 bf16, 6,078 / 6,056 vs 6,478 / 6,437 at 74 rows -- the co-running kernels

@@ -46,6 +46,10 @@ class Switches:
     # the IMPALA learner's 15 conv weight gradients beside its data-gradient chain: no gain
     # (392.5 / 393.9 vs 395.6 / 395.4 steps/s fp32, profiles/r4_ab_impala_bwd_branches.txt)
     impala_bwd_branches: bool = False
+    # single-rank branched backward: the fc weight gradient (+ head wgrad + priorities) on
+    # the main stream right after the fc dgrad, the branch forking after it ("on"), on the
+    # branch beside the dgrad chain ("off"), "auto": main for fp32-class at >= 256 rows
+    fc_wgrad_main: str = "auto"
     # fc forward: stream-K over this many workgroups (0: a fixed K split, fc_ksplit_max).
     # Measured slower: fc 43.1 vs 40.5 us at 512 rows, 18.8 vs 12.6 at 74 (segments restart
     # the LDS pipeline, more partial planes for the head), profiles/r4_ab_fc_stream_k_rejected.txt
