@@ -52,6 +52,7 @@ import numpy as np
 import torch
 
 from ..config import epsilon_ladder
+from ..ops.switches import SW
 from .nstep import make_nstep_builder
 
 
@@ -243,13 +244,16 @@ class GpuActorGroup:
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
                                self.cfg.Runtime.obs_scale, self.y1)
             ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2)
+        # (SW.actor_fc_ksplit: the actors' fc forward with few K splits -- a throughput job
+        # beside the learner, where the chip-filling split's partial planes cost HBM traffic)
+        ks = dict(ksplit=SW.actor_fc_ksplit) if SW.actor_fc_ksplit > 0 else {}
         if self.split:
             ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, x_lo=self.y2_lo, w_lo=Pl["w3"], out_lo=self.y3_lo)
             ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h, x_lo=self.y3_lo.reshape(E, 3136),
-                       w_lo=Pl["wfc"], out_lo=self.h_lo)
+                       w_lo=Pl["wfc"], out_lo=self.h_lo, **ks)
         else:
             ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3)
-            ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h)
+            ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h, **ks)
         heads = {k: P[k] for k in ("wv", "bv", "wa", "ba")}
         ops.actor_head(self.h, heads, self.eps, self.ctr, self.seed, self.q, self.act, H_lo=self.h_lo)
         self.ctr += 1

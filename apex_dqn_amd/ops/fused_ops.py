@@ -105,7 +105,7 @@ class TorchBackend:
                        None if out_lo is None else out_lo[r:])
 
     def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
-               c2d=None, defer_head=False):
+               c2d=None, defer_head=False, ksplit=0):
         """``c2d = (conv2 weight, lo plane)``: weights of this step's conv2 data gradient,
         which the HIP backend pre-packs inside the fc launch; ``defer_head``: the HIP
         backend may leave the epilogue to the next :meth:`head` (both ignored here)."""
@@ -373,7 +373,9 @@ class HipBackend(TorchBackend):
                    out_lo=out_lo, packed=packed)
 
     def fc_fwd(self, x, w, b, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
-               c2d=None, defer_head=False):
+               c2d=None, defer_head=False, ksplit=0):
+        """``ksplit`` > 0: that K split instead of the one that fills the chip (the actors:
+        a throughput job beside the learner, where fewer partial planes cost less)."""
         if not self.native_conv:
             return super().fc_fwd(x, w, b, out, w2, b2, rows_first, x_lo, w_lo, w2_lo, out_lo)
         M, K = x.shape[0], x[0].numel()
@@ -386,7 +388,9 @@ class HipBackend(TorchBackend):
             # 192 blocks), more for the few row tiles of a small per-rank batch (global-batch
             # DP: 74 rows per rank -> 24 tiles x 10 splits)
             tiles = C.row_tiles_host(M, rows_first if w2 is not None else None, 128) * (w.shape[0] // 128)
-            if SW.fc_stream_k > 0 and tiles * (K // 64) >= SW.fc_stream_k:
+            if ksplit > 0:
+                ks = int(ksplit)
+            elif SW.fc_stream_k > 0 and tiles * (K // 64) >= SW.fc_stream_k:
                 ks = -SW.fc_stream_k          # stream-K: every workgroup an equal (tile, K) range
             else:
                 ks = max(2, 256 // max(tiles, 1))

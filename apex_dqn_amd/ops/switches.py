@@ -46,6 +46,8 @@ class Switches:
     # the IMPALA learner's 15 conv weight gradients beside its data-gradient chain: no gain
     # (392.5 / 393.9 vs 395.6 / 395.4 steps/s fp32, profiles/r4_ab_impala_bwd_branches.txt)
     impala_bwd_branches: bool = False
+    # the GPU actors' fc forward: this K split (0: the chip-filling split of the learner)
+    actor_fc_ksplit: int = 4
     # single-rank branched backward: the fc weight gradient (+ head wgrad + priorities) on
     # the main stream right after the fc dgrad, the branch forking after it ("on"), on the
     # branch beside the dgrad chain ("off"), "auto": main for fp32-class at >= 256 rows
