@@ -732,6 +732,28 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   APEX_CHECK_LAUNCH();
 }
 
+// clip + centered RMSprop over one range of the flat parameters with the SAME launch
+// shape as apex_rmsprop_sample (512-thread blocks: the clip coefficient's partial sum runs
+// in the same order, so a range updated here is bit-identical to one updated by the fused
+// launch).  The learner updates the fc layer this way on a stream of its own, beside the
+// next update's conv forward (learner/fused_learner.py _seg3, SW.opt_overlap).
+APEX_EXPORT int apex_rmsprop_range(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
+                                   const double* partials, int npart, float lr, float alpha, float eps_opt,
+                                   float clip, int centered, float* norm_out, bf16_t* pb_lo, const double* wnorm,
+                                   int wn, int wstride, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
+  if (((uintptr_t)pb | (uintptr_t)pb_lo) & 7) return (int)hipErrorInvalidValue;
+  constexpr int nt = 512, maxb = 256;
+  int nb = (int)((n / 4 + nt - 1) / nt);
+  nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
+  const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,
+                      wnorm, wn, wstride, CfFragOut{}};
+  const SampleArgs sa{};            // no draw blocks
+  rmsprop_sample_kernel<nt><<<nb, nt, 0, st>>>(ra, sa, 0);
+  APEX_CHECK_LAUNCH();
+}
+
 APEX_EXPORT int apex_head_wgrad_prio(const bf16_t* Hon, const float* dhead, int B, int A, float* gwv, float* gbv,
                                      float* gwa, float* gba, int hidden, TreeDesc t, const int64_t* idx,
                                      const float* td, const int32_t* gen_expect, const int32_t* gen,

@@ -228,6 +228,16 @@ class FusedNatureLearner(IsNormMixin):
         # profiles/r4_ab_branch_priority_neutral.txt -- the captured graph's queues do not
         # keep it)
         self._wg_stream = torch.cuda.Stream(self.device) if (self._branched or self._dp_branched) else None
+        # SW.opt_overlap: inside a multi-update graph the fc layer's RMSprop update (96 % of
+        # the parameters, [wfc, end) of the flat layout) runs on a stream of its own beside
+        # the NEXT update's conv forward, which never reads the fc weights; that update's fc
+        # forward waits for it (_seg3, forward_all).  Bit-identical to the one-launch update.
+        self._opt_cut = self.layout.offsets["wfc"]
+        self._opt_stream = torch.cuda.Stream(self.device) \
+            if (cuda and SW.opt_overlap and self.ops.name == "hip" and self._opt_cut % 4 == 0) else None
+        self._opt_pending = None      # event: the last deferred fc update
+        self._opt_defer = False       # set while capturing an update that another follows
+        self._gnorm_b = torch.zeros(1, dtype=torch.float32, device=d)
         # the fc layer's split-K epilogue runs inside the head launch (ops.fc_fwd defer_head;
         # SW.fc_epi_in_head = False keeps the separate epilogue launch)
         self._defer_fc_epilogue = SW.fc_epi_in_head
@@ -350,6 +360,7 @@ class FusedNatureLearner(IsNormMixin):
             ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B)
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
                      **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
+        self._join_opt()          # the previous update's deferred fc RMSprop (SW.opt_overlap)
         ops.fc_fwd(self.y3.reshape(n, 3136), Pb["wfc"], P["bfc"], self.h, Tb["wfc"], T["bfc"], 2 * B,
                    c2d=(Pb["w2"], Pl["w2"] if sp else None), defer_head=defer_head,
                    **self._lo(x_lo=sp and self.y3_lo.reshape(n, 3136), w_lo=sp and Pl["wfc"],
@@ -506,16 +517,52 @@ class FusedNatureLearner(IsNormMixin):
         self.num_q_updates += 1
         return out
 
+    def _join_opt(self) -> None:
+        """The current stream waits for the deferred fc update, if one is in flight."""
+        if self._opt_pending is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._opt_pending)
+            self._opt_pending = None
+
     def _seg3(self, norm_slots: Optional[int] = None) -> None:
         """clip + centered RMSprop (+ bf16 hi / lo pack) with the next batch's draw.
         ``norm_slots``: the clip norm is the sum of ``norm_part[:norm_slots]`` (written by
-        the gradient producers of the factored DP step)."""
+        the gradient producers of the factored DP step).  With SW.opt_overlap, while
+        capturing an update another one follows (``_opt_defer``), the fc range is updated
+        on its own stream (joined by the next update's fc forward)."""
         rt, ops = self.rt, self.ops
         if self._comm_bf16:
             self.g32.copy_(self.gcomm)
         # with pre-sampling the optimizer launch also draws step t+1's batch (every
         # read of this step's sample buffers is behind us)
         nxt = (self.replay, self.B, self.S, self.slots[2 * self.B:]) if self._presample else None
+        if self._opt_stream is not None and self._opt_defer:
+            if self._fuse_norm:
+                tot = (self.norm_part, self._npart)
+            elif norm_slots:
+                tot = (self.norm_part, norm_slots)
+            else:                  # the norm of the (reduced) gradient: one pass, read by both launches
+                tot = (self.partials, ops.grad_sqnorm_partials(self.g32, self.partials))
+            c = self._opt_cut
+            main, side = torch.cuda.current_stream(self.device), self._opt_stream
+            ev = torch.cuda.Event()
+            ev.record(main)
+            ops.optimizer(self.p32[:c], self.g32[:c], self.rms_v[:c], self.rms_m[:c], self.pbf[:c], rt.lr,
+                          rt.rms_decay, rt.rms_eps, rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
+                          norm_total=tot, sample=nxt, wnorm=self._wnorm(),
+                          **self._lo(pb_lo=self.split and self.pbf_lo[:c]),
+                          **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}))
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                ops.optimizer_range(self.p32[c:], self.g32[c:], self.rms_v[c:], self.rms_m[c:], self.pbf[c:], rt.lr,
+                                    rt.rms_decay, rt.rms_eps, rt.grad_clip, rt.centered_rmsprop, self._gnorm_b, tot,
+                                    pb_lo=self.pbf_lo[c:] if self.split else None, wnorm=self._wnorm())
+                done = torch.cuda.Event()
+                done.record(side)
+            self._opt_pending = done
+            if self._presample:
+                self._sample_ver = self.replay.version
+            self._mark("optimizer")
+            return
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else
@@ -849,6 +896,8 @@ class FusedNatureLearner(IsNormMixin):
             self._dp_body()
         else:
             self._step_body()
+        if not self._opt_defer:
+            self._join_opt()
 
     # called after update i of the multi-step graph's capture (its work is captured into
     # the graph): tests record every update's state and next batch from inside the graph
@@ -913,10 +962,17 @@ class FusedNatureLearner(IsNormMixin):
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.device)
             with torch.cuda.graph(g):
-                for i in range(k):
-                    self._body()
-                    if self._step_hook is not None:
-                        self._step_hook(i)      # captured too (tests: per-update state copies)
+                try:
+                    for i in range(k):
+                        # (SW.opt_overlap: the fc update of every update but the last runs
+                        # beside the next update's conv forward)
+                        self._opt_defer = i + 1 < k and self._step_hook is None
+                        self._body()
+                        if self._step_hook is not None:
+                            self._step_hook(i)      # captured too (tests: per-update state copies)
+                finally:
+                    self._opt_defer = False
+                    self._join_opt()
             self._multi = g
             self.graph_captures += 1
             self._graphs_warm = False

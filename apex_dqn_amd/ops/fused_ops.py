@@ -590,6 +590,25 @@ class HipBackend(TorchBackend):
                                            int(segs[0].shape[0]), dst.data_ptr(), int(dst.stride(0)),
                                            _lib.stream_ptr()), "pack_rows")
 
+    def grad_sqnorm_partials(self, g32, partials) -> int:
+        """Squared-norm partials of the whole gradient (the optimizer's own pass);
+        returns the partial count."""
+        _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), g32.numel(), partials.data_ptr(),
+                                                      _lib.stream_ptr()), "sqnorm")
+        return partials.numel()
+
+    def optimizer_range(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, norm_total,
+                        pb_lo=None, wnorm=None) -> None:
+        """Clip + centered RMSprop over a range of the flat parameters (views), bit-identical
+        to the fused optimizer + sample launch over the same range: ``norm_total =
+        (partials, count)`` of the WHOLE gradient (csrc/sumtree.hip apex_rmsprop_range)."""
+        part, npart = norm_total
+        wn = (wnorm[0].data_ptr(), int(wnorm[1]), int(wnorm[2])) if wnorm is not None else (None, 0, 0)
+        _lib.check(self.lib.apex_rmsprop_range(
+            p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), p32.numel(), part.data_ptr(),
+            int(npart), float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
+            _lib.ptr(pb_lo), *wn, _lib.stream_ptr()), "rmsprop_range")
+
     def sqnorm_ranges(self, ranges, partials: torch.Tensor, nblk: int) -> int:
         (a, b) = (list(ranges) + [None])[:2]
         _lib.check(self.lib.apex_sqnorm_ranges(a.data_ptr(), a.numel(), _lib.ptr(b), 0 if b is None else b.numel(),

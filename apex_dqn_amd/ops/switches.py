@@ -46,6 +46,13 @@ class Switches:
     # the IMPALA learner's 15 conv weight gradients beside its data-gradient chain: no gain
     # (392.5 / 393.9 vs 395.6 / 395.4 steps/s fp32, profiles/r4_ab_impala_bwd_branches.txt)
     impala_bwd_branches: bool = False
+    # inside multi-update graphs: the fc layer's RMSprop update on a stream of its own,
+    # beside the next update's conv forward (learner/fused_learner.py _seg3).  Bit-identical
+    # but slower: the rest of the launch keeps the next batch's draw, a ~20 us latency chain
+    # the fc update used to hide, and the fc forward pays a join edge -- 2,659 / 2,649 vs
+    # 2,669 / 2,677 steps/s, 6,550 / 6,574 vs 6,657 / 6,641 at 74 rows
+    # (profiles/r4_ab_opt_overlap_rejected.txt).  Off.
+    opt_overlap: bool = False
     # the GPU actors' fc forward: this K split (0: the chip-filling split of the learner)
     actor_fc_ksplit: int = 4
     # single-rank branched backward: the fc weight gradient (+ head wgrad + priorities) on
