@@ -115,7 +115,7 @@ APEX_EXPORT int apex_head_wgrad(const bf16_t* Hon, const float* dhead, int B, in
 // One wave per env row. eps per row; uniform draws from the counter RNG.
 // H_lo (fp32 learner, split mode): the lo plane of the stream activations, so the
 // actor's q-values (and the initial priorities built from them) are fp32-accurate.
-template <int HS>
+template <int HS, int MAXA>
 __global__ void __launch_bounds__(256) actor_head_kernel(const bf16_t* __restrict__ H, HeadParams P, int E,
                                                          int A, const float* __restrict__ eps, uint64_t seed,
                                                          const uint64_t* __restrict__ ctr,
@@ -124,17 +124,18 @@ __global__ void __launch_bounds__(256) actor_head_kernel(const bf16_t* __restric
   const int lane = threadIdx.x & 63;
   const int e = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (e >= E) return;
-  float q[HEAD_MAXA], hv[HS / 64], ha[HS / 64];
-  head_row<HS>(H + (int64_t)e * 2 * HS, H_lo != nullptr ? H_lo + (int64_t)e * 2 * HS : nullptr, P, A, lane, q, hv, ha);
+  float q[MAXA], hv[HS / 64], ha[HS / 64];
+  head_row<HS, MAXA>(H + (int64_t)e * 2 * HS, H_lo != nullptr ? H_lo + (int64_t)e * 2 * HS : nullptr, P, A, lane, q,
+                     hv, ha);
   int best = 0;
   float bq = -3.4e38f;
 #pragma unroll
-  for (int j = 0; j < HEAD_MAXA; ++j)
+  for (int j = 0; j < MAXA; ++j)
     if (j < A && q[j] > bq) { bq = q[j]; best = j; }
   if (lane < A) {
     float qv = 0.f;
 #pragma unroll
-    for (int j = 0; j < HEAD_MAXA; ++j)
+    for (int j = 0; j < MAXA; ++j)
       if (j == lane) qv = q[j];
     q_out[(int64_t)e * A + lane] = qv;
   }
@@ -152,10 +153,13 @@ APEX_EXPORT int apex_actor_head(const bf16_t* H, HeadParams P, int E, int A, con
                                 const uint64_t* ctr, float* q_out, int32_t* a_out, int hidden, const bf16_t* H_lo,
                                 hipStream_t st) {
   if (A < 1 || A > HEAD_MAXA || E < 1) return (int)hipErrorInvalidValue;
-  if (hidden == 512)
-    actor_head_kernel<512><<<(E + 3) / 4, 256, 0, st>>>(H, P, E, A, eps, seed, ctr, q_out, a_out, H_lo);
-  else if (hidden == 256)
-    actor_head_kernel<256><<<(E + 3) / 4, 256, 0, st>>>(H, P, E, A, eps, seed, ctr, q_out, a_out, H_lo);
+#define APEX_ACTOR_HEAD(HS_, MA_) \
+  actor_head_kernel<HS_, MA_><<<(E + 3) / 4, 256, 0, st>>>(H, P, E, A, eps, seed, ctr, q_out, a_out, H_lo)
+  if (hidden == 512 && A <= 8) APEX_ACTOR_HEAD(512, 8);
+  else if (hidden == 512) APEX_ACTOR_HEAD(512, HEAD_MAXA);
+  else if (hidden == 256 && A <= 8) APEX_ACTOR_HEAD(256, 8);
+  else if (hidden == 256) APEX_ACTOR_HEAD(256, HEAD_MAXA);
   else return (int)hipErrorInvalidValue;
+#undef APEX_ACTOR_HEAD
   APEX_CHECK_LAUNCH();
 }

@@ -202,16 +202,37 @@ __device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, flo
                                        const float* ha, float* kwv, float* kcs, float* kws, int a_sel) {
   constexpr int NPL = HS / 64;
   float part[MAXA + 1];
-  {
-    float w[NPL], s = 0.f;
-    load_w<NPL>(P.wv + lane * NPL, w);
+  // every weight row of the heads is loaded before the first product (MAXA <= 8: 9 x NPL
+  // registers): issued one row at a time, each row's load waited for before the next --
+  // one memory round trip per action
+  constexpr bool PRE = MAXA <= 8;
+  float wpre[PRE ? MAXA : 1][NPL];
+  float bpre[PRE ? MAXA : 1];           // the advantage biases, with the weights
+  float w0[NPL];
+  load_w<NPL>(P.wv + lane * NPL, w0);
+  const float bv = P.bv[0];
+  if constexpr (PRE) {
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) s += hv[k] * w[k];
+    for (int j = 0; j < MAXA; ++j) {
+      if (j < A) {
+        load_w<NPL>(P.wa + j * HS + lane * NPL, wpre[j]);
+        bpre[j] = P.ba[j];
+      } else {
+        bpre[j] = 0.f;
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) wpre[j][k] = 0.f;
+      }
+    }
+  }
+  {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) s += hv[k] * w0[k];
     part[0] = s;
     if constexpr (KEEP) {
 #pragma unroll
       for (int k = 0; k < NPL; ++k) {
-        kwv[k] = w[k];
+        kwv[k] = w0[k];
         kcs[k] = 0.f;
         kws[k] = 0.f;
       }
@@ -221,7 +242,12 @@ __device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, flo
   for (int j = 0; j < MAXA; ++j) {
     if (j < A) {
       float w[NPL], s = 0.f;
-      load_w<NPL>(P.wa + j * HS + lane * NPL, w);
+      if constexpr (PRE) {
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) w[k] = wpre[j][k];
+      } else {
+        load_w<NPL>(P.wa + j * HS + lane * NPL, w);
+      }
 #pragma unroll
       for (int k = 0; k < NPL; ++k) s += ha[k] * w[k];
       part[j + 1] = s;
@@ -236,12 +262,12 @@ __device__ __forceinline__ void head_q(const HeadParams& P, int A, int lane, flo
       part[j + 1] = 0.f;
     }
   }
-  float v = wave_sum_dpp(part[0]) + P.bv[0];
+  float v = wave_sum_dpp(part[0]) + bv;
   float amean = 0.f;
 #pragma unroll
   for (int j = 0; j < MAXA; ++j) {
     if (j < A) {
-      float a = wave_sum_dpp(part[j + 1]) + P.ba[j];
+      float a = wave_sum_dpp(part[j + 1]) + (PRE ? bpre[PRE ? j : 0] : P.ba[j]);
       part[j + 1] = a;
       amean += a;
     }
