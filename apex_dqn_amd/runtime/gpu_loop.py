@@ -121,6 +121,13 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
         async_actors = bool(rt.async_actors) and device.type == "cuda"
     # async actors: the envs as Runtime.actor_pipeline groups stepped in turn (the host's env
     # work of one group hides another's inference); the lock-step loop keeps one group
+    if async_actors and int(rt.actor_pipeline) > 2 and device.type == "cuda":
+        # measured on MI355X: 4 groups starve (each group's finish waits ~1.2 ms for its
+        # inference, 10-17k env frames/s, profiles/r4_diag_e2e_actor_pipeline4_starved.txt) --
+        # the groups' streams likely share the process's few hardware queues
+        # (GPU_MAX_HW_QUEUES) with the learner's step graphs
+        sys.stderr.write(f"warning: Runtime.actor_pipeline={rt.actor_pipeline} > 2 measured far slower on "
+                         f"MI355X (actor streams share hardware queues with the learner); 2 is the default\n")
     group = make_gpu_actor_group(cfg, learner, replay, E, rank, world, seed=rt.seed,
                                  pipeline=int(rt.actor_pipeline) if async_actors else 1)
     if ckpt_path and rt.resume and os.path.exists(ckpt_path):
