@@ -22,6 +22,13 @@ import json
 import os
 import sys
 
+# HIP maps every stream to one of GPU_MAX_HW_QUEUES hardware queues (4 by default); the
+# learner's two step streams, the data-parallel collective / fork streams and the actor
+# groups' streams exceed four, and a stream that shares a queue runs behind that queue's
+# other work (actor inference queued behind the learner's step graphs starved the actors:
+# profiles/r4_e2e_actor_streams_ab.txt).  Read when HIP initialises, so set before it.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
