@@ -793,12 +793,22 @@ class FusedNatureLearner(IsNormMixin):
         self._mark("conv_backward")
         if self._comm_bf16:
             self.gcomm[:o2].copy_(self.g32[:o2])
-        w_cv = self.coll.all_reduce(self.gcomm[:o2])
-        main.wait_stream(side)
+        inline = SW.dp_inline_last and self._ordered_coll and hasattr(self.coll, "all_reduce_inline")
+        if inline:
+            # conv1's bucket on the main stream itself: one join of the branch and one of
+            # the comm stream (in order: covers fc + stats + cv2), then no fork / join edge
+            main.wait_stream(side)
+            works["cv2"].wait()
+            self.coll.all_reduce_inline(self.gcomm[:o2])
+        else:
+            w_cv = self.coll.all_reduce(self.gcomm[:o2])
+            main.wait_stream(side)
         if factors and not fc_branch:
             # (on the main stream, after conv1: SW.dp_fc_wgrad_branch off)
             nfc = self._fc_wgrad_gathered(works["fc"])
-        if self._ordered_coll:
+        if inline:
+            pass
+        elif self._ordered_coll:
             w_cv.wait()          # RCCL runs the collectives in issue order: covers fc + stats
         else:
             works["fc"].wait()

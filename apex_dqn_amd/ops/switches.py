@@ -66,6 +66,10 @@ class Switches:
     # DP step, factored fc exchange: the global batch's fc wgrad on the branch stream (after
     # its conv2 wgrad, beside conv1's) instead of on the main stream after conv1
     dp_fc_wgrad_branch: bool = True
+    # DP step, native communicator: conv1's (last) gradient bucket all-reduced on the main
+    # stream itself after one join of the comm stream, instead of forked to the comm stream
+    # and joined back (nothing overlaps it; saves a graph edge on the critical path)
+    dp_inline_last: bool = False
     # cap on the fc forward's K splits (0: fill the chip, ops/fused_ops.py fc_fwd); the DDQN
     # head sums the splits' partials (the deferred epilogue)
     fc_ksplit_max: int = 0

@@ -256,6 +256,12 @@ class NativeCollectives:
         self.comm.all_gather_(out, inp, stream=s)
         return _StreamWork(self)
 
+    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum"):
+        """All-reduce enqueued on the CURRENT stream (no fork / join): the caller has
+        already joined every collective issued before it, so RCCL's issue order holds."""
+        self.comm.all_reduce_(t, op)
+        return _Done()
+
 
 def make_collectives(comm, backend: str = "torch", device=None):
     """Collectives for the learner's DP step: ``torch`` (torch.distributed) or

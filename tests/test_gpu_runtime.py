@@ -588,3 +588,60 @@ def test_staged_frame_append_matches_copy():
         np.testing.assert_array_equal(sa, sb)
     torch.cuda.synchronize()
     assert torch.equal(a.frames, b.frames)
+
+
+def _inline_last_worker(q, port):
+    """Forced DP on the native communicator (world 1, captured 4-update graphs): the same
+    updates with conv1's bucket forked to the comm stream and all-reduced inline."""
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0")
+    import numpy as np
+    import torch
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.ops.switches import SW
+    from apex_dqn_amd.parallel.dist import Comm
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    comm = Comm.from_env(device=dev, force=True)
+    out = {}
+    for inline in (False, True):
+        SW.dp_inline_last = inline
+        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
+                                    "Learner": {"replay_sample_size": 256},
+                                    "Runtime": {"use_graphs": True, "graph_steps": 4, "presample": True,
+                                                "force_dp": True, "comm_backend": "native"}})
+        rp = GpuReplayShard(4000, 4000, 4100, 4, device=dev, seed=0x5EED)
+        rng = np.random.default_rng(9)
+        seqs = rp.append_frames(rng.integers(0, 255, (3000, 84, 84), dtype=np.uint8))
+        K = 2800
+        st = np.stack([seqs[i:i + 4] for i in range(K)])
+        rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 6, K), R=rng.normal(size=K).astype(np.float32),
+                       Gamma=np.full(K, 0.97, np.float32), priority=rng.random(K).astype(np.float32) + 0.01))
+        torch.manual_seed(3)
+        L = FusedNatureLearner(cfg, dev, rp, comm=comm)
+        assert L._dp and L.coll.name == "native"
+        L.steps(8)
+        torch.cuda.synchronize()
+        out[inline] = L.p32.cpu()
+    SW.dp_inline_last = False
+    comm._native.check()
+    comm.shutdown()
+    q.put((bool(torch.equal(out[False], out[True])), float((out[False] - out[True]).abs().max())))
+
+
+@pytest.mark.gpu
+def test_dp_inline_last_bucket_bit_identical():
+    """SW.dp_inline_last (conv1's bucket all-reduced on the main stream after one join of
+    the comm stream) takes the same updates as the forked bucket, inside captured graphs."""
+    import random
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_inline_last_worker, args=(q, 29600 + random.randint(301, 600)))
+    p.start()
+    same, diff = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert same, diff
