@@ -111,8 +111,10 @@ class RuntimeConf:
     replay_capacity: Optional[int] = None  # physical capacity, global over the ranks' shards
                                            # (default: soft_capacity * 1.25 + 1024)
     heartbeat_timeout: float = 60.0
-    comm_backend: str = "torch"     # DP collectives: "torch" (torch.distributed / RCCL process group) |
-                                    # "native" (parallel/rccl.py: own RCCL communicator + comm stream)
+    comm_backend: str = "native"    # DP collectives: "native" (parallel/rccl.py: own RCCL communicator on its
+                                    # own comm stream; the step is one captured HIP graph) | "torch"
+                                    # (torch.distributed process group; eager DP steps: its watchdog's
+                                    # event cache is not capture-safe on this ROCm / torch build)
     force_dp: bool = False          # run the data-parallel step (collectives + sharded replay) even at
                                     # world 1 (needs an initialised process group; checks / overhead)
     batch_scope: str = "global"     # DP: "global" = Learner.replay_sample_size is the batch of ONE update
@@ -129,6 +131,9 @@ class RuntimeConf:
                                     # batch on each rank: ~(B_total x 4160) values instead of 3.2 M, exact and
                                     # bit-identical across ranks) | "auto" (factors while 1 < W and W x rows
                                     # <= 1024)
+    dp_shard_update: str = "auto"   # DP: the fc layer's optimizer (96 % of the parameters) sharded by output rows
+                                    # over the ranks, the updated rows all-gathered (learner/dp_step.py):
+                                    # "on" | "off" | "auto" (on at world > 1 when 1024 / (64 W) is whole)
     replica_check_every: int = 5000  # DP: learner steps between replica checksum checks (0 = off)
     step_timeout: float = 300.0     # GPU loop watchdog: seconds a queued learner chunk may take
     async_actors: bool = True       # GPU loop: the actor group steps on its own host thread
@@ -220,6 +225,8 @@ class ApexConfig:
             raise ValueError("Runtime.batch_scope must be 'global' or 'per_rank'")
         if not self.Runtime.dp_batch_slack >= 0.0:
             raise ValueError("Runtime.dp_batch_slack must be >= 0")
+        if self.Runtime.dp_shard_update not in ("auto", "on", "off"):
+            raise ValueError("Runtime.dp_shard_update must be 'auto', 'on' or 'off'")
         if self.Runtime.dp_fc_exchange not in ("auto", "factors", "allreduce"):
             raise ValueError("Runtime.dp_fc_exchange must be 'auto', 'factors' or 'allreduce'")
         if self.Runtime.loss not in ("huber", "mse"):

@@ -33,6 +33,10 @@ struct Api {
                              hipStream_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*reduce_scatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                                 hipStream_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*comm_user_rank)(const ncclComm_t, int*) = nullptr;
   ncclResult_t (*group_start)() = nullptr;
   ncclResult_t (*group_end)() = nullptr;
 };
@@ -63,7 +67,9 @@ APEX_EXPORT int apex_comm_load(const char* path) {
             sym(g.comm_abort, "ncclCommAbort") && sym(g.comm_async_error, "ncclCommGetAsyncError") &&
             sym(g.error_string, "ncclGetErrorString") && sym(g.all_reduce, "ncclAllReduce") &&
             sym(g.all_gather, "ncclAllGather") && sym(g.broadcast, "ncclBroadcast") &&
-            sym(g.group_start, "ncclGroupStart") && sym(g.group_end, "ncclGroupEnd");
+            sym(g.group_start, "ncclGroupStart") && sym(g.group_end, "ncclGroupEnd") &&
+            sym(g.reduce_scatter, "ncclReduceScatter") && sym(g.comm_count, "ncclCommCount") &&
+            sym(g.comm_user_rank, "ncclCommUserRank");
   if (!ok) {
     g = Api{};
     return kNotLoaded;
@@ -122,6 +128,24 @@ APEX_EXPORT int apex_comm_all_gather(void* comm, const void* send, void* recv, s
   if (g.all_gather == nullptr) return kNotLoaded;
   return static_cast<int>(g.all_gather(send, recv, sendcount, static_cast<ncclDataType_t>(dtype),
                                        static_cast<ncclComm_t>(comm), static_cast<hipStream_t>(stream)));
+}
+
+// recv = this rank's `recvcount`-element chunk of the reduction of send (W x recvcount)
+APEX_EXPORT int apex_comm_reduce_scatter(void* comm, const void* send, void* recv, size_t recvcount, int dtype,
+                                         int op, void* stream) {
+  if (g.reduce_scatter == nullptr) return kNotLoaded;
+  return static_cast<int>(g.reduce_scatter(send, recv, recvcount, static_cast<ncclDataType_t>(dtype),
+                                           static_cast<ncclRedOp_t>(op), static_cast<ncclComm_t>(comm),
+                                           static_cast<hipStream_t>(stream)));
+}
+
+// the rank count / this rank as the communicator itself sees them (bench.py reports
+// them next to WORLD_SIZE: a world RCCL never formed cannot hide behind the env)
+APEX_EXPORT int apex_comm_count(void* comm, int* count, int* rank) {
+  if (g.comm_count == nullptr || g.comm_user_rank == nullptr) return kNotLoaded;
+  ncclResult_t r = g.comm_count(static_cast<ncclComm_t>(comm), count);
+  if (r != ncclSuccess) return static_cast<int>(r);
+  return static_cast<int>(g.comm_user_rank(static_cast<ncclComm_t>(comm), rank));
 }
 
 APEX_EXPORT int apex_comm_broadcast(void* comm, const void* send, void* recv, size_t count, int dtype, int root,

@@ -22,7 +22,6 @@
 #include "mfma_common.h"
 #include "igemm_wgrad.h"
 #include "conv2_wfrag.h"
-#include "fc_sk.h"
 
 struct ConvDesc {
   const void* x;              // mode 0: bf16 [M][K]; mode 1: bf16 NHWC [N][H][W][Cin]
@@ -651,8 +650,7 @@ __global__ void __launch_bounds__(256) igemm_dma_kernel(ConvDesc d) {
 // LW: four extra loader waves issue every DMA (the compute waves then carry only
 // MFMAs and fragment reads; an LDS-DMA issue costs ~60 cycles of the issuing wave).
 template <bool SPLIT, int NS, bool LW>
-__global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, float* __restrict__ ws, int kt_per,
-                                                                    FcSK sk) {
+__global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, float* __restrict__ ws, int kt_per) {
   constexpr int BM = 128, BN = 128;
   constexpr int HALF = (BM + BN) * 128;           // one precision plane of a stage
   constexpr int STAGE = SPLIT ? 2 * HALF : HALF;
@@ -662,12 +660,10 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
   __shared__ __attribute__((aligned(16))) uint8_t smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = LW ? (tid >> 6) & 3 : tid >> 6;
   const bool loader = !LW || tid >= 256, computer = !LW || tid < 256;
-  const bool streamk = sk.nblk > 0;
-  const int ntm = streamk ? sk.ntm : gridDim.x, ntn = streamk ? sk.ntn : gridDim.y;
+  const int ntm = gridDim.x, ntn = gridDim.y;
   // N tiles fastest, then M tiles, then K splits: the blocks of one XCD share A rows
   // and a K range (consecutive logical ids land on one XCD)
-  const int wg = streamk ? xcd_swizzle(blockIdx.x, gridDim.x)
-                         : xcd_swizzle(blockIdx.x + ntm * (blockIdx.y + ntn * blockIdx.z), ntm * ntn * gridDim.z);
+  const int wg = xcd_swizzle(blockIdx.x + ntm * (blockIdx.y + ntn * blockIdx.z), ntm * ntn * gridDim.z);
   const int M = d.N, Nc = d.Cout;
   const int KT = d.K >> 6;
   const uint8_t* xa = reinterpret_cast<const uint8_t*>(d.x);
@@ -675,29 +671,12 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)smem;
   const int wm = wv >> 1, wn = wv & 1;
 
-  // Segments: one (tile, K range) in the K-split mode; stream-K: the tiles this
-  // workgroup's iteration range [u, uend) touches, each with its partial plane.
-  int64_t u = 0, uend = 1;
-  if (streamk) {
-    u = fc_sk_start(sk, wg);
-    uend = fc_sk_start(sk, wg + 1);
-  }
-  while (u < uend) {
-    int tile, kt0, nk, bz;
-    if (streamk) {
-      tile = (int)(u / KT);
-      kt0 = (int)(u - (int64_t)tile * KT);
-      const int kend = (int)min((int64_t)KT, uend - (int64_t)tile * KT);
-      nk = kend - kt0;
-      bz = wg - fc_sk_owner(sk, (int64_t)tile * KT);
-      u = (int64_t)tile * KT + kend;
-    } else {
-      tile = wg % (ntn * ntm);
-      bz = wg / (ntn * ntm);
-      kt0 = bz * kt_per;
-      nk = min(KT, kt0 + kt_per) - kt0;              // >= 1 (host sizes the grid)
-      u = uend;
-    }
+  // one (tile, K range) per workgroup
+  {
+    const int tile = wg % (ntn * ntm);
+    const int bz = wg / (ntn * ntm);
+    const int kt0 = bz * kt_per;
+    const int nk = min(KT, kt0 + kt_per) - kt0;      // >= 1 (host sizes the grid)
     const int by = tile % ntn;
     const int bx = tile / ntn;
     const RowTile rt = row_tile(d, bx, BM, M);
@@ -811,8 +790,6 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
         }
       }
     }
-    // the next segment's DMA must not land in a stage a compute wave still reads
-    if (u < uend) __syncthreads();
   }
 }
 
@@ -825,7 +802,7 @@ __global__ void __launch_bounds__(LW ? 512 : 256) fc_gemm128_kernel(ConvDesc d, 
 
 template <bool SPLIT>
 __global__ void __launch_bounds__(256) fc_splitk_epilogue_kernel(ConvDesc d, const float* __restrict__ ws,
-                                                                 int nz, int eb, C2dPackJob pk, FcSK sk) {
+                                                                 int nz, int eb, C2dPackJob pk) {
   if ((int)blockIdx.x >= eb) {
     pack_c2d_wfrag_word(((int)blockIdx.x - eb) * 256 + threadIdx.x, pk.w, pk.w_lo, pk.out);
     return;
@@ -835,7 +812,6 @@ __global__ void __launch_bounds__(256) fc_splitk_epilogue_kernel(ConvDesc d, con
   const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (e >= MN) return;
   const int m = (int)(e / Nc), n = (int)(e - (int64_t)m * Nc);
-  if (sk.nblk > 0) nz = fc_sk_count(sk, fc_sk_tile(sk, m, n));   // stream-K: this tile's planes
   float v[8];
   {
     const float4 p0 = *reinterpret_cast<const float4*>(ws + e);
@@ -1025,45 +1001,15 @@ static void launch_dma(const ConvDesc& d, dim3 grid, hipStream_t st) {
 }
 
 // Dense C[M,N] = act(A[M,K] . B[N,K]^T + b) on 128x128 tiles, K split `ksplit` ways
-// (fc_gemm128_kernel + fc_splitk_epilogue_kernel), or with ksplit = -nblk a stream-K
-// split over nblk workgroups (csrc/fc_sk.h).  ws: fp32 workspace of at least planes *
-// M * N elements (planes = ksplit, or apex_fc_sk_planes).  Row-major B only (d.bt == 0),
-// N % 128 == 0.  pk: optional conv2 weight-fragment pack riding on the epilogue launch
-// (fc_splitk_epilogue_kernel).  no_epilogue: only the GEMM runs; the caller consumes the
-// ws partials.
-static FcSK fc_sk_of(const ConvDesc& d, int nblk) {
-  FcSK s;
-  s.nblk = nblk;
-  s.kt = d.K >> 6;
-  s.ntm = row_tiles(d, d.N, 128);
-  s.ntn = d.Cout / 128;
-  s.m_switch = d.w2 != nullptr ? d.m_switch : -1;
-  return s;
-}
-
-// partial planes of a stream-K fc forward of M rows (second weight set from row
-// m_switch, or -1) over nblk workgroups; 0 for an invalid shape
-APEX_EXPORT int apex_fc_sk_planes(int M, int Nc, int K, int m_switch, int nblk) {
-  if (M <= 0 || (Nc & 127) || (K & 63) || K <= 0 || nblk < 1) return 0;
-  ConvDesc d{};
-  d.N = M;
-  d.Cout = Nc;
-  d.K = K;
-  d.m_switch = m_switch;
-  d.w2 = m_switch >= 0 ? reinterpret_cast<const bf16_t*>(16) : nullptr;
-  FcSK s = fc_sk_of(d, nblk);
-  if (fc_sk_total(s) < nblk) return 0;
-  int nz = 0;
-  for (int t = 0; t < s.ntm * s.ntn; ++t) {
-    const int c = fc_sk_count(s, t);
-    nz = c > nz ? c : nz;
-  }
-  return nz;
-}
-
+// (fc_gemm128_kernel + fc_splitk_epilogue_kernel).  ws: fp32 workspace of at least
+// ksplit * M * N elements.  Row-major B only (d.bt == 0), N % 128 == 0.  pk: optional
+// conv2 weight-fragment pack riding on the epilogue launch (fc_splitk_epilogue_kernel).
+// no_epilogue: only the GEMM runs; the caller consumes the ws partials.
+// (A stream-K split was measured slower -- fc 43.1 vs 40.5 us at 512 rows, 18.8 vs
+// 12.6 at 74, profiles/r4_ab_fc_stream_k_rejected.txt -- and removed.)
 APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksplit, int loader_waves,
                                 int no_epilogue, C2dPackJob pk, hipStream_t st) {
-  if (d.mode != 0 || d.bt != 0 || (d.K & 63) || d.K <= 0 || (d.Cout & 127) || d.N <= 0 || ksplit == 0)
+  if (d.mode != 0 || d.bt != 0 || (d.K & 63) || d.K <= 0 || (d.Cout & 127) || d.N <= 0 || ksplit < 1)
     return (int)hipErrorInvalidValue;
   if ((d.ldy & 7) || d.ldy < d.Cout) return (int)hipErrorInvalidValue;
   if ((int64_t)d.N * d.K * 2 >= 0x7ffffff0LL || (int64_t)d.Cout * d.K * 2 >= 0x7ffffff0LL)
@@ -1073,26 +1019,16 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   if (split && (d.w_lo == nullptr || d.y_lo == nullptr || (d.w2 != nullptr && d.w2_lo == nullptr)))
     return (int)hipErrorInvalidValue;
   const int KT = d.K >> 6;
-  FcSK sk{};
-  int kt_per = KT, nz;
-  dim3 grid;
-  if (ksplit < 0) {            // stream-K over -ksplit workgroups
-    sk = fc_sk_of(d, -ksplit);
-    if (fc_sk_total(sk) < sk.nblk) return (int)hipErrorInvalidValue;
-    nz = apex_fc_sk_planes(d.N, d.Cout, d.K, sk.m_switch, sk.nblk);
-    grid = dim3(sk.nblk);
-  } else {
-    kt_per = (KT + ksplit - 1) / ksplit;
-    nz = (KT + kt_per - 1) / kt_per;
-    grid = dim3(row_tiles(d, d.N, 128), d.Cout / 128, nz);
-  }
+  const int kt_per = (KT + ksplit - 1) / ksplit;
+  const int nz = (KT + kt_per - 1) / kt_per;
+  const dim3 grid(row_tiles(d, d.N, 128), d.Cout / 128, nz);
   if (ws == nullptr || nz < 1 || ws_elems < (int64_t)nz * d.N * d.Cout) return (int)hipErrorInvalidValue;
   if (loader_waves) {
-    if (split) fc_gemm128_kernel<true, 2, true><<<grid, 512, 0, st>>>(d, ws, kt_per, sk);
-    else fc_gemm128_kernel<false, 4, true><<<grid, 512, 0, st>>>(d, ws, kt_per, sk);
+    if (split) fc_gemm128_kernel<true, 2, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
+    else fc_gemm128_kernel<false, 4, true><<<grid, 512, 0, st>>>(d, ws, kt_per);
   } else {
-    if (split) fc_gemm128_kernel<true, 2, false><<<grid, 256, 0, st>>>(d, ws, kt_per, sk);
-    else fc_gemm128_kernel<false, 4, false><<<grid, 256, 0, st>>>(d, ws, kt_per, sk);
+    if (split) fc_gemm128_kernel<true, 2, false><<<grid, 256, 0, st>>>(d, ws, kt_per);
+    else fc_gemm128_kernel<false, 4, false><<<grid, 256, 0, st>>>(d, ws, kt_per);
   }
   const int64_t nthr = (int64_t)d.N * d.Cout / 8;
   const int eb = (int)((nthr + 255) / 256);
@@ -1104,8 +1040,8 @@ APEX_EXPORT int apex_fc_gemm128(ConvDesc d, float* ws, int64_t ws_elems, int ksp
   }
   if (pk.out != nullptr && (pk.w == nullptr || ((uintptr_t)pk.out & 15))) return (int)hipErrorInvalidValue;
   const int pb = pk.out != nullptr ? C2D_PACK_THREADS / 256 : 0;
-  if (split) fc_splitk_epilogue_kernel<true><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk, sk);
-  else fc_splitk_epilogue_kernel<false><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk, sk);
+  if (split) fc_splitk_epilogue_kernel<true><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk);
+  else fc_splitk_epilogue_kernel<false><<<eb + pb, 256, 0, st>>>(d, ws, nz, eb, pk);
   APEX_CHECK_LAUNCH();
 }
 

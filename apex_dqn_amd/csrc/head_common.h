@@ -5,7 +5,6 @@
 // and fc_wgrad_head_prio_kernel beside the priority write-back).
 #pragma once
 #include "apex_common.h"
-#include "fc_sk.h"
 
 #define HEAD_MAXA 32
 
@@ -107,7 +106,6 @@ struct HeadPart {
   int two_b;
   bf16_t* hon;            // rows [0, B) of h written back (hi plane / bf16)
   bf16_t* hon_lo;         // split mode: lo plane (else null)
-  FcSK sk;                // stream-K fc forward (sk.nblk > 0): per-tile plane counts; nz = the most
 };
 
 template <int HS>
@@ -122,13 +120,8 @@ __device__ __forceinline__ void load_row_part(const HeadPart& hp, int row, int l
   const float* __restrict__ bias = row < hp.two_b ? hp.bias_on : hp.bias_tg;
   float v[2][NPL], bs[2][NPL];
   const float* p0 = hp.part + (int64_t)row * ROW + lane * NPL;
-  // partial planes of each stream's columns (stream-K: per 128-column tile)
-  int nzs[2] = {hp.nz, hp.nz};
-  if (hp.sk.nblk > 0) {
-#pragma unroll
-    for (int st = 0; st < 2; ++st) nzs[st] = fc_sk_count(hp.sk, fc_sk_tile(hp.sk, row, st * HS + lane * NPL));
-  }
-  const int nzmax = nzs[0] > nzs[1] ? nzs[0] : nzs[1];
+  const int nzs[2] = {hp.nz, hp.nz};
+  const int nzmax = hp.nz;
 #pragma unroll
   for (int st = 0; st < 2; ++st)
 #pragma unroll

@@ -467,6 +467,7 @@ struct TreeUpdArgs {
   uint64_t* ctr_to_bump;
   float alpha, eps;
   int n, kfirst;
+  double* stats_out;         // sharded replay: (sum p^alpha, min p^alpha) after the update, or null
 };
 
 __device__ __forceinline__ void tree_update_block(const TreeUpdArgs& a) {
@@ -523,6 +524,17 @@ __device__ __forceinline__ void tree_update_block(const TreeUpdArgs& a) {
     tree_block_update(t, act, s[r], v, lacc, &lmin, a.kfirst);
     __syncthreads();
   }
+  if (a.stats_out != nullptr) {
+    // this shard's statistics for the step's all-gather (replay/gpu_replay.py
+    // gather_shard_stats): the root and the min after every update above -- read by
+    // L2 atomics, which see this block's own atomic updates
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      a.stats_out[0] = atomicAdd(t.nodes + t.off[t.L], 0.0);
+      a.stats_out[1] = (double)__uint_as_float(atomicOr(t.min_bits, 0u));
+    }
+  }
 }
 
 // head weight gradient + priority write-back in one launch: block 0 runs the
@@ -563,13 +575,46 @@ __global__ void __launch_bounds__(256) fc_wgrad_head_prio_kernel(WgradDesc d, in
 // run the clip + centered RMSprop + bf16 pack over the flat parameters.  The tree
 // already holds this step's priorities (written by fc_wgrad_head_prio_kernel), so the
 // draw equals the one a sample launch at the head of the next step would make.
-template <int NT>
-__global__ void __launch_bounds__(NT) rmsprop_sample_kernel(RmspropArgs a, SampleArgs s, int nsb) {
+//
+// SEG: the update covers only the listed ranges of the flat arrays (RmsSegs): the
+// data-parallel step with a sharded optimizer (learner/dp_step.py) updates the conv +
+// head range and the rank's own fc rows.  Every element's update is the same
+// arithmetic as in the whole-range launch (the clip coefficient comes from the same
+// partials), so a sharded update equals the unsharded one element for element.
+struct RmsSegs {
+  int nseg;            // 1..3
+  int blk0[4];         // first optimizer block of segment k; blk0[nseg] = the total
+  int64_t off[3];      // element offset of segment k (a multiple of 4)
+  int64_t len[3];
+};
+
+template <int NT, bool SEG>
+__global__ void __launch_bounds__(NT) rmsprop_sample_kernel(RmspropArgs a, SampleArgs s, int nsb, RmsSegs sg) {
   if ((int)blockIdx.x < nsb) {
     tree_sample_body(s, blockIdx.x);
     return;
   }
-  rmsprop_body(a, blockIdx.x - nsb, gridDim.x - nsb);
+  const int b = blockIdx.x - nsb;
+  if constexpr (!SEG) {
+    rmsprop_body(a, b, gridDim.x - nsb);
+  } else {
+    int k = 0;
+    while (k + 1 < sg.nseg && b >= sg.blk0[k + 1]) ++k;
+    RmspropArgs t = a;
+    const int64_t o = sg.off[k];
+    t.p += o;
+    t.g += o;
+    t.v += o;
+    t.m += o;
+    t.pb += o;
+    if (t.pb_lo != nullptr) t.pb_lo += o;
+    t.n = sg.len[k];
+    if (k != 0) {                 // the fused-forward operand stores and the norm live in segment 0
+      t.fo = CfFragOut{};
+      t.norm_out = nullptr;
+    }
+    rmsprop_body(t, b - sg.blk0[k], sg.blk0[k + 1] - sg.blk0[k]);
+  }
 }
 
 // ---------------------------------------------------------------- launchers
@@ -658,7 +703,7 @@ APEX_EXPORT int apex_fill16(void* p, int64_t n, int nt, hipStream_t st) {
   APEX_CHECK_LAUNCH();
 }
 
-APEX_EXPORT int apex_abi_version() { return 5; }
+APEX_EXPORT int apex_abi_version() { return 7; }
 
 // 1 if this library was built with -DAPEX_DEBUG_BOUNDS
 APEX_EXPORT int apex_debug_bounds_enabled() {
@@ -694,7 +739,9 @@ APEX_EXPORT int apex_debug_errors(int* counts, long long* first, int reset) {
 #endif
 }
 
-// rmsprop (clip norm from `npart` partials, as apex_rmsprop_step_np) + tree_sample of B
+// rmsprop (clip norm from `npart` partials, as apex_rmsprop_step_np) + tree_sample of B.
+// `seg` (nullable): update only those ranges (offsets relative to p / g / v / m / pb);
+// blk0 is filled in here.
 APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
                                     const double* partials, int npart, float lr, float alpha, float eps_opt,
                                     float clip, int centered, float* norm_out, TreeDesc t, RecordDesc r, int B,
@@ -703,12 +750,13 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int32_t* out_nxt, int32_t* out_act, float* out_rew, float* out_gam,
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
                                     uint64_t shard_seed, float* out_wscale, int64_t mcap, bf16_t* pb_lo,
-                                    const double* wnorm, int wn, int wstride, CfFragOut fo, hipStream_t st) {
+                                    const double* wnorm, int wn, int wstride, CfFragOut fo, const RmsSegs* seg,
+                                    hipStream_t st) {
   if (mcap <= 0) mcap = (int64_t)shard_world * B;
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
-  if ((((uintptr_t)pb | (uintptr_t)pb_lo) & 7) || B < 1) return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)pb | (uintptr_t)pb_lo) & 7) || B < 0) return (int)hipErrorInvalidValue;
   // 512-thread blocks, grid capped at 256: every block first sums the ~2.6 K clip-norm
   // partials, so fewer, fatter blocks cut those L2 reads (256 x 512 measured 2,540 / 4,175
   // fp32 / bf16 steps/s vs 2,528 / 4,107 at 512 x 512 and 3497-3520 vs 3543-3576 at
@@ -716,10 +764,38 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   constexpr int nt = 512, maxb = 256;
   int nb = (int)((n / 4 + nt - 1) / nt);
   nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
-  const int nsb = blocks_for(B, nt / 64);
+  RmsSegs sg{};
+  if (seg != nullptr) {
+    sg = *seg;
+    if (sg.nseg < 1 || sg.nseg > 3) return (int)hipErrorInvalidValue;
+    int64_t tot = 0;
+    for (int k = 0; k < sg.nseg; ++k) {
+      if ((sg.off[k] & 3) || sg.len[k] <= 0 || sg.off[k] < 0 || sg.off[k] + sg.len[k] > n)
+        return (int)hipErrorInvalidValue;
+      tot += sg.len[k];
+    }
+    // blocks in proportion to the segment sizes (at least one each, at most one float4
+    // per thread), segment 0 enough for the fragment stores' first-chunk rule below
+    const int64_t need0 = fo.w1frag != nullptr ? (fo.w2_off + 65536) / 4 / nt + 1 : 1;
+    int b0 = 0;
+    for (int k = 0; k < sg.nseg; ++k) {
+      const int64_t full = (sg.len[k] / 4 + nt - 1) / nt;
+      int64_t nbk = (int64_t)maxb * sg.len[k] / tot;
+      if (k == 0 && nbk < need0) nbk = need0;
+      if (nbk > full) nbk = full;
+      if (nbk < 1) nbk = 1;
+      sg.blk0[k] = b0;
+      b0 += (int)nbk;
+    }
+    sg.blk0[sg.nseg] = b0;
+    nb = sg.blk0[1];              // segment 0's blocks: the fragment-store check below
+  }
+  const int nsb = B > 0 ? blocks_for(B, nt / 64) : 0;
+  const int64_t n0 = seg != nullptr ? sg.len[0] : n;
+  if (fo.w1frag != nullptr && (seg != nullptr && sg.off[0] != 0)) return (int)hipErrorInvalidValue;
   if (fo.w1frag != nullptr && (fo.c2f == nullptr || (fo.C != 1 && fo.C != 2 && fo.C != 4) ||
-                               (fo.w1_off & 3) || (fo.w2_off & 7) || fo.w1_off + 4096LL * fo.C > n ||
-                               fo.w2_off + 65536 > n ||
+                               (fo.w1_off & 3) || (fo.w2_off & 7) || fo.w1_off + 4096LL * fo.C > n0 ||
+                               fo.w2_off + 65536 > n0 ||
                                // (stored in each thread's first chunk: rmsprop_body's peel)
                                (fo.w1_off + 4096LL * fo.C) / 4 > (int64_t)nb * nt || (fo.w2_off + 65536) / 4 > (int64_t)nb * nt))
     return (int)hipErrorInvalidValue;
@@ -728,29 +804,8 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
   const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
                       out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed,
                       out_wscale, mcap};
-  rmsprop_sample_kernel<nt><<<nb + nsb, nt, 0, st>>>(ra, sa, nsb);
-  APEX_CHECK_LAUNCH();
-}
-
-// clip + centered RMSprop over one range of the flat parameters with the SAME launch
-// shape as apex_rmsprop_sample (512-thread blocks: the clip coefficient's partial sum runs
-// in the same order, so a range updated here is bit-identical to one updated by the fused
-// launch).  The learner updates the fc layer this way on a stream of its own, beside the
-// next update's conv forward (learner/fused_learner.py _seg3, SW.opt_overlap).
-APEX_EXPORT int apex_rmsprop_range(float* p, const float* g, float* v, float* m, bf16_t* pb, int64_t n,
-                                   const double* partials, int npart, float lr, float alpha, float eps_opt,
-                                   float clip, int centered, float* norm_out, bf16_t* pb_lo, const double* wnorm,
-                                   int wn, int wstride, hipStream_t st) {
-  if (n <= 0) return 0;
-  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)v | (uintptr_t)m) & 15) return (int)hipErrorInvalidValue;
-  if (((uintptr_t)pb | (uintptr_t)pb_lo) & 7) return (int)hipErrorInvalidValue;
-  constexpr int nt = 512, maxb = 256;
-  int nb = (int)((n / 4 + nt - 1) / nt);
-  nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
-  const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,
-                      wnorm, wn, wstride, CfFragOut{}};
-  const SampleArgs sa{};            // no draw blocks
-  rmsprop_sample_kernel<nt><<<nb, nt, 0, st>>>(ra, sa, 0);
+  if (seg != nullptr) rmsprop_sample_kernel<nt, true><<<sg.blk0[sg.nseg] + nsb, nt, 0, st>>>(ra, sa, nsb, sg);
+  else rmsprop_sample_kernel<nt, false><<<nb + nsb, nt, 0, st>>>(ra, sa, nsb, sg);
   APEX_CHECK_LAUNCH();
 }
 
@@ -758,14 +813,14 @@ APEX_EXPORT int apex_head_wgrad_prio(const bf16_t* Hon, const float* dhead, int 
                                      float* gwa, float* gba, int hidden, TreeDesc t, const int64_t* idx,
                                      const float* td, const int32_t* gen_expect, const int32_t* gen,
                                      float alpha, float eps, uint64_t* ctr_to_bump, const bf16_t* Hon_lo,
-                                     hipStream_t st) {
+                                     double* stats_out, hipStream_t st) {
   // the single-block tree update holds TU_MAXR items per thread
   if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || B > TU_MAXR * 512 || idx == nullptr)
     return (int)hipErrorInvalidValue;
   const int nblk = 1 + (A + 1) * (hidden / 64);
   head_wgrad_prio_kernel<<<nblk, 512, 0, st>>>(
       HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden, Hon_lo},
-      TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)});
+      TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t), stats_out});
   APEX_CHECK_LAUNCH();
 }
 
@@ -776,7 +831,7 @@ APEX_EXPORT int apex_fc_wgrad_head_prio(WgradDesc d, const bf16_t* Hon, const fl
                                         float* gwv, float* gbv, float* gwa, float* gba, int hidden, TreeDesc t,
                                         const int64_t* idx, const float* td, const int32_t* gen_expect,
                                         const int32_t* gen, float alpha, float eps, uint64_t* ctr_to_bump,
-                                        const bf16_t* Hon_lo, hipStream_t st) {
+                                        const bf16_t* Hon_lo, double* stats_out, hipStream_t st) {
   // 256-thread blocks: the single-block tree update holds TU_MAXR items per thread
   if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || B > TU_MAXR * 256 || idx == nullptr)
     return (int)hipErrorInvalidValue;
@@ -792,7 +847,7 @@ APEX_EXPORT int apex_fc_wgrad_head_prio(WgradDesc d, const bf16_t* Hon, const fl
   const int nhw = (A + 1) * (hidden / 64);
   const int blk0 = (1 + nhw + 7) & ~7;
   const HeadWgArgs hw{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden, Hon_lo};
-  const TreeUpdArgs tu{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t)};
+  const TreeUpdArgs tu{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t), stats_out};
   if (split) fc_wgrad_head_prio_kernel<1><<<blk0 + gx * gy, 256, 0, st>>>(d, gx, gy, hw, tu, nhw, blk0);
   else fc_wgrad_head_prio_kernel<0><<<blk0 + gx * gy, 256, 0, st>>>(d, gx, gy, hw, tu, nhw, blk0);
   APEX_CHECK_LAUNCH();

@@ -9,8 +9,9 @@ Per step (B = local batch), entirely on device, one stream, no host sync:
   (generation-checked, last writer wins)         fc_wgrad_head_prio_kernel)
   backward: fc, conv3, conv2 dgrad+wgrad, conv1  csrc/conv_mfma.hip, conv2_img.hip,
   wgrad, one split-K finalisation                conv1_wgrad.hip
-  (DP) flat-gradient all-reduce over RCCL        two buckets + the all-gather of the
-                                                 replay shards' statistics (one global
+  (DP) gradient exchange over RCCL               learner/dp_step.py: factored fc exchange,
+                                                 bucketed all-reduce, sharded optimizer,
+                                                 the replay shards' statistics (one global
                                                  prioritized replay), captured in the
                                                  step's HIP graph
   grad-norm clip + centered RMSprop + bf16 pack  ONE launch (csrc/sumtree.hip
@@ -46,7 +47,9 @@ from ..models.flat_params import (FlatLayout, flat_to_reference_state, nature_se
                                   reference_state_to_flat)
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..ops.switches import SW
-from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
+from ..utils.checkpoint import (adopt_obs_scale, layout_segments, load_checkpoint, pack_flat_state,
+                                save_checkpoint, unpack_flat_state)
+from .dp_step import DataParallelStep, Streams
 from .is_norm import IsNormMixin
 
 
@@ -78,7 +81,7 @@ def dp_layout(cfg: ApexConfig, comm, batch_size: Optional[int] = None, allow_for
     return world, dp, rows, mcap
 
 
-class FusedNatureLearner(IsNormMixin):
+class FusedNatureLearner(IsNormMixin, DataParallelStep):
     kind = "fused"
 
     def __init__(self, cfg: ApexConfig, device, replay, comm=None, backend: Optional[str] = None,
@@ -188,8 +191,9 @@ class FusedNatureLearner(IsNormMixin):
             planes = 2 if self.split else 1
             self._fx_cols = [1024] * planes + [3136] * planes      # [dH | dH lo | X | X lo]
             ncol = sum(self._fx_cols)
-            self.fx_send = torch.zeros(self.B, ncol, dtype=self.act_dtype, device=d)
             self.fx_recv = torch.zeros(self.world * self.B, ncol, dtype=self.act_dtype, device=d)
+            r = comm.rank
+            self.fx_send = self.fx_recv[r * self.B:(r + 1) * self.B]    # (the all-gather runs in place)
         # producer-summed clip norm: the fc wgrad epilogue and the grad_finalize blocks
         # write squared-norm partials of the values they store, the optimizer launch sums
         # them.  With DP the norm is of the all-reduced gradient: the optimizer's own pass.
@@ -210,34 +214,36 @@ class FusedNatureLearner(IsNormMixin):
         self.coll = None
         if self._dp:
             from ..parallel.rccl import make_collectives
-            backend = self.rt.comm_backend if cuda else "torch"
+            # (the native communicator joins an RCCL process group's ranks; gloo groups -- CPU
+            # tests, several ranks rehearsing on one GPU -- use torch.distributed)
+            backend = self.rt.comm_backend if (cuda and self._backend_name() == "nccl") else "torch"
             self.coll = make_collectives(comm, backend, self.device)
             _enable_sharding(replay, comm, self.rt, self.mcap)
             replay.gather_shard_stats(coll=self.coll)
-        # DP step as ONE captured graph including the RCCL collectives (backend nccl);
-        # gloo (CPU tests, one-GPU rehearsals) cannot be captured: eager DP steps
-        self._dp_graphs = self._dp and cuda and self._backend_name() == "nccl"
-        self._ordered_coll = self._dp and cuda and (self.coll.name == "native" or self._backend_name() == "nccl")
-        self._fork_stream = torch.cuda.Stream(self.device) if (self._dp and cuda) else None
-        # single rank: the weight gradients beside the data-gradient chain (SW.bwd_branches)
+        # DP step as ONE captured graph including the RCCL collectives (the native
+        # communicator, or emulated copies); gloo (CPU tests, one-GPU rehearsals) cannot be
+        # captured, and the torch.distributed RCCL process group is run eagerly: its watchdog
+        # queried events recorded inside the capture (hipErrorCapturedEvent abort,
+        # profiles/r5_dp_capture_probe.txt)
+        self._dp_graphs = self._dp and cuda and self.coll.name in ("native", "emulated")
+        self._ordered_coll = self._dp and cuda and (self.coll.name in ("native", "emulated")
+                                                   or self._backend_name() == "nccl")
+        # single rank: the weight gradients beside the data-gradient chain (SW.bwd_branches);
+        # the DP step always runs them on the branch (learner/dp_step.py)
         self._branched = (not self._dp) and cuda and SW.bwd_branches
-        # the DP step's backward on the same two chains, its collectives issued from the
-        # branch as their inputs complete (_dp_body_branched)
-        self._dp_branched = self._dp and cuda and SW.bwd_branches
         # (a high-priority branch stream measured neutral: 2,677 / 2,674 vs 2,685 / 2,684,
         # profiles/r4_ab_branch_priority_neutral.txt -- the captured graph's queues do not
         # keep it)
-        self._wg_stream = torch.cuda.Stream(self.device) if (self._branched or self._dp_branched) else None
-        # SW.opt_overlap: inside a multi-update graph the fc layer's RMSprop update (96 % of
-        # the parameters, [wfc, end) of the flat layout) runs on a stream of its own beside
-        # the NEXT update's conv forward, which never reads the fc weights; that update's fc
-        # forward waits for it (_seg3, forward_all).  Bit-identical to the one-launch update.
-        self._opt_cut = self.layout.offsets["wfc"]
-        self._opt_stream = torch.cuda.Stream(self.device) \
-            if (cuda and SW.opt_overlap and self.ops.name == "hip" and self._opt_cut % 4 == 0) else None
-        self._opt_pending = None      # event: the last deferred fc update
-        self._opt_defer = False       # set while capturing an update that another follows
-        self._gnorm_b = torch.zeros(1, dtype=torch.float32, device=d)
+        self._wg_stream = torch.cuda.Stream(self.device) if (self._branched or (self._dp and cuda)) else None
+        self._streams = Streams(self.device, self._wg_stream if self._dp else None)
+        if self._dp and cuda and hasattr(self.coll, "use_stream"):
+            # the collectives run on the backward's branch stream itself: the captured step
+            # then has two chains (main, branch) as the single-rank step, which the HIP graph
+            # executor runs on two queues -- with a third (comm) stream it interleaved the
+            # chains' kernels on shared queues and serialized the branch behind the main
+            # chain (profiles/r5_step_timeline_emu8_comm_stream.txt)
+            self.coll.use_stream(self._wg_stream)
+        self._dp_setup()
         # the fc layer's split-K epilogue runs inside the head launch (ops.fc_fwd defer_head;
         # SW.fc_epi_in_head = False keeps the separate epilogue launch)
         self._defer_fc_epilogue = SW.fc_epi_in_head
@@ -360,7 +366,7 @@ class FusedNatureLearner(IsNormMixin):
             ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B)
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
                      **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
-        self._join_opt()          # the previous update's deferred fc RMSprop (SW.opt_overlap)
+        self._wait_params()       # sharded DP update: the last update's fc rows (learner/dp_step.py)
         ops.fc_fwd(self.y3.reshape(n, 3136), Pb["wfc"], P["bfc"], self.h, Tb["wfc"], T["bfc"], 2 * B,
                    c2d=(Pb["w2"], Pl["w2"] if sp else None), defer_head=defer_head,
                    **self._lo(x_lo=sp and self.y3_lo.reshape(n, 3136), w_lo=sp and Pl["wfc"],
@@ -412,18 +418,8 @@ class FusedNatureLearner(IsNormMixin):
                  isn=self._isn(), **self._lo(lo=sp and (self.h_lo[:2 * B], self.h_lo[2 * B:], self.dH_lo)))
         self._mark("head")
         prio = (self.replay, S["idx"], S["gen"], self.td_abs)
-        if getattr(self, "_branched", False) or getattr(self, "_dp_branched", False):
-            return           # the weight gradients run on the branch stream (_seg2_branched)
-        if getattr(self, "_fc_factors", False):
-            # factored DP exchange: the head weight gradient + priority write-back now, the
-            # fc weight gradient after the all-gather of every rank's (dH, X) rows (_dp_body)
-            ops.head_wgrad(self.h, self.dhead, self._head_params(self.G), prio=prio,
-                           **self._lo(Hon_lo=self.h_lo))
-            segs = [self.dH, self.dH_lo, self.y3[:B].reshape(B, 3136), self.y3_lo[:B].reshape(B, 3136)] \
-                if sp else [self.dH, self.y3[:B].reshape(B, 3136)]
-            ops.pack_rows(self.fx_send, segs)
-            self._mark("fc_wgrad")
-            return
+        if self._branched or self._dp:
+            return           # the weight gradients: _seg2_branched / the DP step (dp_step.py)
         # fc wgrad + head wgrad + priority write-back: one launch on the HIP backend
         # (csrc/sumtree.hip fc_wgrad_head_prio_kernel)
         nrm = (self.norm_part, 0) if self._fuse_norm else None
@@ -517,58 +513,24 @@ class FusedNatureLearner(IsNormMixin):
         self.num_q_updates += 1
         return out
 
-    def _join_opt(self) -> None:
-        """The current stream waits for the deferred fc update, if one is in flight."""
-        if self._opt_pending is not None:
-            torch.cuda.current_stream(self.device).wait_event(self._opt_pending)
-            self._opt_pending = None
-
-    def _seg3(self, norm_slots: Optional[int] = None) -> None:
+    def _seg3(self, norm_slots: Optional[int] = None, segs=None) -> None:
         """clip + centered RMSprop (+ bf16 hi / lo pack) with the next batch's draw.
         ``norm_slots``: the clip norm is the sum of ``norm_part[:norm_slots]`` (written by
-        the gradient producers of the factored DP step).  With SW.opt_overlap, while
-        capturing an update another one follows (``_opt_defer``), the fc range is updated
-        on its own stream (joined by the next update's fc forward)."""
+        the gradient producers of the DP step).  ``segs``: the flat ranges to update (the
+        sharded DP update, learner/dp_step.py)."""
         rt, ops = self.rt, self.ops
         if self._comm_bf16:
             self.g32.copy_(self.gcomm)
         # with pre-sampling the optimizer launch also draws step t+1's batch (every
         # read of this step's sample buffers is behind us)
         nxt = (self.replay, self.B, self.S, self.slots[2 * self.B:]) if self._presample else None
-        if self._opt_stream is not None and self._opt_defer:
-            if self._fuse_norm:
-                tot = (self.norm_part, self._npart)
-            elif norm_slots:
-                tot = (self.norm_part, norm_slots)
-            else:                  # the norm of the (reduced) gradient: one pass, read by both launches
-                tot = (self.partials, ops.grad_sqnorm_partials(self.g32, self.partials))
-            c = self._opt_cut
-            main, side = torch.cuda.current_stream(self.device), self._opt_stream
-            ev = torch.cuda.Event()
-            ev.record(main)
-            ops.optimizer(self.p32[:c], self.g32[:c], self.rms_v[:c], self.rms_m[:c], self.pbf[:c], rt.lr,
-                          rt.rms_decay, rt.rms_eps, rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
-                          norm_total=tot, sample=nxt, wnorm=self._wnorm(),
-                          **self._lo(pb_lo=self.split and self.pbf_lo[:c]),
-                          **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}))
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                ops.optimizer_range(self.p32[c:], self.g32[c:], self.rms_v[c:], self.rms_m[c:], self.pbf[c:], rt.lr,
-                                    rt.rms_decay, rt.rms_eps, rt.grad_clip, rt.centered_rmsprop, self._gnorm_b, tot,
-                                    pb_lo=self.pbf_lo[c:] if self.split else None, wnorm=self._wnorm())
-                done = torch.cuda.Event()
-                done.record(side)
-            self._opt_pending = done
-            if self._presample:
-                self._sample_ver = self.replay.version
-            self._mark("optimizer")
-            return
         ops.optimizer(self.p32, self.g32, self.rms_v, self.rms_m, self.pbf, rt.lr, rt.rms_decay, rt.rms_eps,
                       rt.grad_clip, rt.centered_rmsprop, self.partials, self.gnorm,
                       norm_total=(self.norm_part, self._npart) if self._fuse_norm else
                       ((self.norm_part, norm_slots) if norm_slots else None), sample=nxt,
                       wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo),
-                      **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}))
+                      **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}),
+                      **({"segs": segs} if segs is not None else {}))
         if self._presample:
             self._sample_ver = self.replay.version
         self._mark("optimizer")
@@ -668,259 +630,33 @@ class FusedNatureLearner(IsNormMixin):
         self._seg2()
         self._seg3()
 
-    def _dp_body(self) -> None:
-        """One data-parallel step (graph-capturable with RCCL): the fc/heads gradient
-        bucket and the shard statistics (every shard's sum / min p^alpha, taken after
-        this step's priority write-back, consumed by the next batch's global draw
-        inside the optimizer launch) are exchanged while the conv backward runs; the
-        conv bucket follows; the optimizer waits for all three."""
-        if self._dp_branched:
-            return self._dp_body_branched()
-        if self._fc_factors:
-            return self._dp_body_factors()
-        cut = self.layout.offsets["wfc"]
-        self._seg1()
-        works = []
-        on_cuda = self.device.type == "cuda"
-        fork = None
-        if on_cuda:
-            fork = torch.cuda.Event()
-            fork.record()
-
-        def issue_fc_bucket():
-            # The fc/head bucket and the shard statistics leave from a side stream that
-            # waits on the fork event recorded after segment 1, and are enqueued only after
-            # the compute stream's next kernel: in the captured graph the compute child of
-            # the fork comes first, so the executor keeps the backward chain on the step's
-            # hardware queue (comm captured first moved the chain to a second queue: a
-            # 6-10 us gap at each switch, profiles/r2_step_timeline_fp32_forced_dp_fc128.txt)
-            if on_cuda:
-                side = self._fork_stream
-                side.wait_event(fork)
-                with torch.cuda.stream(side):
-                    works.append(self.coll.all_reduce(self.gcomm[cut:]))
-                    works.append(self.replay.gather_shard_stats(async_op=True, coll=self.coll))
-            else:
-                works.append(self.coll.all_reduce(self.gcomm[cut:]))
-                works.append(self.replay.gather_shard_stats(async_op=True, coll=self.coll))
-
-        self._seg2(after_first=issue_fc_bucket)     # conv backward overlaps the fc/head bucket all-reduce
-        w_fc, w_r = works
-        w_cv = self.coll.all_reduce(self.gcomm[:cut])
-        if self._ordered_coll:
-            # RCCL runs a communicator's collectives in issue order on one stream: the
-            # last one's completion covers the others (one join edge in the graph)
-            w_cv.wait()
-        else:
-            w_fc.wait()
-            w_r.wait()
-            w_cv.wait()
-            if on_cuda:   # gloo on device tensors: the results are ordered on the side stream
-                torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
-        self._mark("allreduce_wait")
-        self._seg3()
-
-    def _dp_body_branched(self) -> None:
-        """The data-parallel step on the branched backward (SW.bwd_branches):
-
-          main stream          fc dgrad -> conv3 dgrad -> conv2 dgrad -> conv1 wgrad -> finalize (conv1)
-          branch stream        head wgrad + priorities (+ fc wgrad)  conv3 wgrad  conv2 wgrad
-                               -> finalize (conv3 / conv2)
-          comm (RCCL, in order) fc factors all-gather (or fc bucket all-reduce) + shard
-                               stats, issued from the branch as soon as they exist;
-                               the [w2, wfc) bucket (conv2 / conv3 / head) from the branch
-                               after its finalisation; conv1's bucket from the main stream
-          [factors] the fc wgrad of the gathered rows on the branch after its conv2 wgrad
-                               (SW.dp_fc_wgrad_branch; off: on the main stream after conv1)
-
-        then the clip norm of the reduced gradient and the optimizer + next draw."""
-        B, rt, ops, G, Pb, Pl, S = self.B, self.rt, self.ops, self.G, self.Pb, self.Pl, self.S
-        sp = self.split
-        cut = self.layout.offsets["wfc"]
-        self._seg1()                      # forward + head (the weight gradients come below)
-        main, side = torch.cuda.current_stream(self.device), self._wg_stream
-        factors = self._fc_factors
-        jobs, works = [], {}
-        ev = torch.cuda.Event()
-        ev.record(main)
-        ops.fc_dgrad(self.dH, self.y3[:B], Pb["wfc"], self.dY3,
-                     **self._lo(dh_lo=self.dH_lo, w_lo=sp and Pl["wfc"], dx_lo=self.dY3_lo))
-        side.wait_event(ev)
-        prio = (self.replay, S["idx"], S["gen"], self.td_abs)
-        with torch.cuda.stream(side):
-            if factors:
-                ops.head_wgrad(self.h, self.dhead, self._head_params(self.G), prio=prio, **self._lo(Hon_lo=self.h_lo))
-                segs = [self.dH, self.dH_lo, self.y3[:B].reshape(B, 3136), self.y3_lo[:B].reshape(B, 3136)] \
-                    if sp else [self.dH, self.y3[:B].reshape(B, 3136)]
-                ops.pack_rows(self.fx_send, segs)
-                works["fc"] = self.coll.all_gather_into(self.fx_recv, self.fx_send)
-            else:
-                ops.fc_head_wgrad(self.dH, self.y3[:B], G["wfc"], G["bfc"], self.h, self.dhead, G, prio,
-                                  **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B], Hon_lo=self.h_lo))
-                if self._comm_bf16:
-                    self.gcomm[cut:].copy_(self.g32[cut:])
-                works["fc"] = self.coll.all_reduce(self.gcomm[cut:])
-            works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
-        self._conv32_branched(main, side, jobs, wgrad2=False)
-        nfc = 0
-        o2 = self.layout.offsets["w2"]
-        fc_branch = factors and SW.dp_fc_wgrad_branch
-        if fc_branch:
-            # the branch's fc wgrad needs the all-gather: waited for on the main stream
-            # (long done by now) and handed over by an event -- a wait on the torch work
-            # from the branch inside a captured graph crashed the capture (world 1)
-            works["fc"].wait()
-            ev1 = torch.cuda.Event()
-            ev1.record(main)
-        with torch.cuda.stream(side):
-            self._conv2_wgrad(jobs)
-        jobs1 = []
-        ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
-                             G["b1"], jobs=jobs1, **self._lo(dy_lo=self.dY1_lo))
-        with torch.cuda.stream(side):
-            # conv2 / conv3 / head bucket [w2, wfc): reduced on the branch and all-reduced
-            # from it while conv1's weight gradient runs -- only conv1's bucket follows the
-            # last backward kernel
-            ops.finalize_grads(jobs, None, None)
-            if self._comm_bf16:
-                self.gcomm[o2:cut].copy_(self.g32[o2:cut])
-            works["cv2"] = self.coll.all_reduce(self.gcomm[o2:cut])
-            if fc_branch:
-                side.wait_event(ev1)
-                nfc = self._fc_wgrad_gathered(None)
-        ops.finalize_grads(jobs1, None, None)
-        self._npart = 0
-        self._mark("conv_backward")
-        if self._comm_bf16:
-            self.gcomm[:o2].copy_(self.g32[:o2])
-        inline = SW.dp_inline_last and self._ordered_coll and hasattr(self.coll, "all_reduce_inline")
-        if inline:
-            # conv1's bucket on the main stream itself: one join of the branch and one of
-            # the comm stream (in order: covers fc + stats + cv2), then no fork / join edge
-            main.wait_stream(side)
-            works["cv2"].wait()
-            self.coll.all_reduce_inline(self.gcomm[:o2])
-        else:
-            w_cv = self.coll.all_reduce(self.gcomm[:o2])
-            main.wait_stream(side)
-        if factors and not fc_branch:
-            # (on the main stream, after conv1: SW.dp_fc_wgrad_branch off)
-            nfc = self._fc_wgrad_gathered(works["fc"])
-        if inline:
-            pass
-        elif self._ordered_coll:
-            w_cv.wait()          # RCCL runs the collectives in issue order: covers fc + stats
-        else:
-            works["fc"].wait()
-            works["stats"].wait()
-            works["cv2"].wait()
-            w_cv.wait()
-        self._mark("allreduce_wait")
-        if factors:
-            nr = self.ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[nfc:], 64)
-            self._seg3(norm_slots=nfc + nr)
-        else:
-            self._seg3()         # (the optimizer's own clip-norm pass over the reduced gradient)
-
-    def _fc_wgrad_gathered(self, work) -> int:
-        """The fc weight gradient of the global batch from the all-gathered (dH, X) rows
-        (identical on every rank), with its clip-norm partials in norm_part[0:]; waits for
-        the all-gather ``work`` on the current stream (None: already ordered after it).
-        Returns the partial slots written."""
-        G, sp = self.G, self.split
-        if work is not None:
-            work.wait()
-        R, c = self.fx_recv, [0]
-        for w in self._fx_cols:
-            c.append(c[-1] + w)
-        cols = [R[:, c[i]:c[i + 1]] for i in range(len(self._fx_cols))]
-        dy, dy_lo, x, x_lo = (cols[0], cols[1], cols[2], cols[3]) if sp else (cols[0], None, cols[1], None)
-        return self.ops.fc_wgrad(dy, x, G["wfc"], G["bfc"], norm=(self.norm_part, 0),
-                                 **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
-
-    def _dp_body_factors(self) -> None:
-        """The data-parallel step with the factored fc-gradient exchange (see __init__):
-
-          compute stream                           comm stream (RCCL, in issue order)
-          forward, head, head wgrad + prio, pack
-          fc dgrad                           -->   all-gather (dH, X) rows of all ranks
-          conv backward, split-K finalize          shard stats
-                                             -->   all-reduce conv + head gradients (0.48 MB)
-          wait all-gather; fc wgrad over the W x rows gathered rows (+ clip-norm partials)
-          wait; clip-norm partials of the all-reduced regions; clip + RMSprop + next draw
-
-        The fc wgrad of the global batch runs while the conv all-reduce is in flight."""
-        cut = self.layout.offsets["wfc"]      # [0, cut): conv + head gradients (all-reduced)
-        self._seg1()
-        on_cuda = self.device.type == "cuda"
-        works = {}
-        fork = None
-        if on_cuda:
-            fork = torch.cuda.Event()
-            fork.record()
-
-        def issue_early():
-            # (after the fc dgrad is enqueued: the backward stays the fork's first child on
-            # the step's hardware queue, as in _dp_body)
-            ctx = torch.cuda.stream(self._fork_stream) if on_cuda else None
-            if on_cuda:
-                self._fork_stream.wait_event(fork)
-                ctx.__enter__()
-            try:
-                works["ag"] = self.coll.all_gather_into(self.fx_recv, self.fx_send)
-                works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=self.coll)
-            finally:
-                if on_cuda:
-                    ctx.__exit__(None, None, None)
-
-        self._seg2(after_first=issue_early)
-        w_cv = self.coll.all_reduce(self.g32[:cut])
-        works["ag"].wait()
-        if on_cuda and not self._ordered_coll:
-            torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
-        self._mark("allgather_wait")
-        # the fc weight gradient of the global batch from the gathered rows (identical on
-        # every rank), with its clip-norm partials
-        R, sp = self.fx_recv, self.split
-        c = [0]
-        for w in self._fx_cols:
-            c.append(c[-1] + w)
-        cols = [R[:, c[i]:c[i + 1]] for i in range(len(self._fx_cols))]
-        dy, dy_lo, x, x_lo = (cols[0], cols[1], cols[2], cols[3]) if sp else (cols[0], None, cols[1], None)
-        nfc = self.ops.fc_wgrad(dy, x, self.G["wfc"], self.G["bfc"], norm=(self.norm_part, 0),
-                                **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
-        self._mark("fc_wgrad_global")
-        if self._ordered_coll:
-            w_cv.wait()          # RCCL runs the collectives in issue order: covers the stats
-        else:
-            works["stats"].wait()
-            w_cv.wait()
-            if on_cuda:
-                torch.cuda.current_stream(self.device).wait_stream(self._fork_stream)
-        self._mark("allreduce_wait")
-        nr = self.ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[nfc:], 64)
-        self._seg3(norm_slots=nfc + nr)
-
     def _body(self) -> None:
         if self._dp:
             self._dp_body()
         else:
             self._step_body()
-        if not self._opt_defer:
-            self._join_opt()
+        if not self._defer_params:
+            self._wait_params()
 
     # called after update i of the multi-step graph's capture (its work is captured into
     # the graph): tests record every update's state and next batch from inside the graph
     _step_hook = None
 
+    # set when the DP step's graph capture (or its first replay) failed on some rank: every
+    # rank then runs the eager DP step (prepare_graphs)
+    graph_fallback = None
+    _inject_capture_failure = False    # tests: fail the one-update capture after its body
+
     def _graphs_enabled(self) -> bool:
-        return bool(self.rt.use_graphs) and self.device.type == "cuda" and (not self._dp or self._dp_graphs)
+        return (bool(self.rt.use_graphs) and self.device.type == "cuda" and (not self._dp or self._dp_graphs)
+                and self.graph_fallback is None)
 
     def step(self) -> None:
         """One learner update (asynchronous on the current stream)."""
         graphs = self._graphs_enabled()
         if graphs and self._graphs is None:
-            self._capture()
+            self.prepare_graphs(multi=False)
+            graphs = self._graphs_enabled()
         if graphs and self._presample and self._sample_ver != self.replay.version:
             self._sample()     # host-side replay mutation since the pre-sample: redraw
         if graphs:
@@ -950,6 +686,10 @@ class FusedNatureLearner(IsNormMixin):
                 n -= 1
                 continue
             self.prepare_graphs(multi=True)
+            if not self._graphs_enabled():       # (the DP step fell back to eager)
+                for _ in range(n):
+                    self.step()
+                return
             if self._presample and self._sample_ver != self.replay.version:
                 self._sample()
             self._multi.replay()
@@ -962,9 +702,53 @@ class FusedNatureLearner(IsNormMixin):
         """Capture every graph :meth:`step` / :meth:`steps` will replay (the one-update
         graph and, with ``multi``, the ``Runtime.graph_steps`` graph) now, so no
         capture lands in a timed region.  Learner state is unchanged.  Returns
-        ``graph_captures``."""
+        ``graph_captures``.
+
+        Data parallel: the DP step's graphs hold RCCL collectives.  If capturing them or
+        their first replay raises on ANY rank (the ranks agree by a host all-reduce), every
+        rank drops its graphs, restores its state and runs the eager DP step instead --
+        in process, no restart of a process that has touched the GPU (``graph_fallback``
+        says why; bench.py reports it as ``dp_graphs`` / ``graph_fallback``)."""
         if not self._graphs_enabled():
             return self.graph_captures
+        k = int(self.rt.graph_steps)
+        if not (self._graphs is None or (multi and k > 1 and self._multi is None) or not self._graphs_warm):
+            return self.graph_captures
+        if not self._dp:
+            self._prepare_graphs(multi)
+            return self.graph_captures
+        snap = self._snapshot()
+        err = None
+        try:
+            self._prepare_graphs(multi)
+        except Exception as e:      # capture / first replay of the DP step failed here
+            err = e
+        ok = err is None
+        if self.comm is not None and getattr(self.comm, "active", False):
+            ok = self.comm.allreduce_scalar(1.0 if ok else 0.0, "min") > 0.5
+        if not ok:
+            self._eager_fallback(err, snap)
+        return self.graph_captures
+
+    def _eager_fallback(self, err, snap) -> None:
+        import sys
+        try:
+            torch.cuda.synchronize(self.device)
+        except Exception:  # pragma: no cover - a sticky error is reported below anyway
+            pass
+        self._graphs = self._multi = None
+        self._params_pending, self._defer_params = None, False
+        self._restore(snap)
+        if self._presample:
+            self._sample()
+        torch.cuda.synchronize(self.device)
+        self.graph_fallback = repr(err) if err is not None else "a peer rank's DP graph capture failed"
+        r = self.comm.rank if self.comm is not None else 0
+        sys.stderr.write(f"[rank {r}] DP step graphs unavailable ({self.graph_fallback}); "
+                         f"running the eager DP step\n")
+        sys.stderr.flush()
+
+    def _prepare_graphs(self, multi: bool) -> None:
         if self._graphs is None:
             self._capture()
         k = int(self.rt.graph_steps)
@@ -974,15 +758,15 @@ class FusedNatureLearner(IsNormMixin):
             with torch.cuda.graph(g):
                 try:
                     for i in range(k):
-                        # (SW.opt_overlap: the fc update of every update but the last runs
-                        # beside the next update's conv forward)
-                        self._opt_defer = i + 1 < k and self._step_hook is None
+                        # (sharded DP update: the fc-row all-gather of every update but the
+                        # last is joined by the next update's fc forward)
+                        self._defer_params = i + 1 < k and self._step_hook is None
                         self._body()
                         if self._step_hook is not None:
                             self._step_hook(i)      # captured too (tests: per-update state copies)
                 finally:
-                    self._opt_defer = False
-                    self._join_opt()
+                    self._defer_params = False
+                    self._wait_params()
             self._multi = g
             self.graph_captures += 1
             self._graphs_warm = False
@@ -1001,7 +785,6 @@ class FusedNatureLearner(IsNormMixin):
                 self._sample()     # the pre-drawn batch of the restored state (same draw)
             torch.cuda.synchronize(self.device)
             self._graphs_warm = True
-        return self.graph_captures
 
     def rewarm(self, replays: int) -> None:
         """Untimed, state-preserving GPU warm-up: replay the multi-step graph ``replays``
@@ -1040,6 +823,8 @@ class FusedNatureLearner(IsNormMixin):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._body()
+            if self._inject_capture_failure:
+                raise RuntimeError("injected DP graph capture failure (test)")
         self._graphs = g
         self.graph_captures += 1
         self._graphs_warm = False
@@ -1051,9 +836,10 @@ class FusedNatureLearner(IsNormMixin):
         across ranks; on a mismatch (silent data corruption, a rank that skipped an
         update) re-broadcast rank 0's weights and optimizer state.  A collective:
         every rank calls it at the same step.  Returns True if the replicas agreed."""
-        if not self._dp or self.world <= 1:
+        if not self._dp or self.world <= 1 or getattr(self.comm, "emulated", False):
             return True
         import torch.distributed as dist
+        self.materialize()
         w = torch.arange(1, 65, device=self.device, dtype=torch.float64)
         p = self.p32.double()
         n = p.numel() // 64 * 64
@@ -1123,9 +909,10 @@ class FusedNatureLearner(IsNormMixin):
         self._refresh_bf16()
 
     def save(self, path: str, extra: Optional[Dict[str, Any]] = None) -> None:
+        self._check_materialized()
         tgt = flat_to_reference_state(self.T, self.c1)
         save_checkpoint(path, self.reference_state_dict(), Q_target_state=tgt,
-                        optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
+                        optimizer_state=pack_flat_state(layout_segments(self.layout), rms_v=self.rms_v, rms_m=self.rms_m),
                         num_q_updates=self.num_q_updates, config=self.cfg.to_dict(),
                         rng={"replay_ctr": int(self.replay.ctr.item()), "replay_seed": int(self.replay.seed)},
                         **(extra or {}))
@@ -1145,9 +932,7 @@ class FusedNatureLearner(IsNormMixin):
         else:
             self.sync_target()
         opt = ck.get("optimizer_state")
-        if isinstance(opt, dict) and "rms_v" in opt:
-            self.rms_v.copy_(opt["rms_v"])
-            self.rms_m.copy_(opt["rms_m"])
+        unpack_flat_state(opt, layout_segments(self.layout), rms_v=self.rms_v, rms_m=self.rms_m)
         self.num_q_updates = int(ck.get("num_q_updates", 0))
         rng = ck.get("rng")
         if isinstance(rng, dict) and "replay_ctr" in rng:

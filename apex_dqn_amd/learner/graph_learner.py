@@ -31,7 +31,7 @@ import torch
 from ..config import ApexConfig
 from ..models.dueling import build_network
 from ..ops.fused_ops import HipBackend, TorchBackend
-from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
+from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, pack_flat_state, save_checkpoint, unpack_flat_state
 from .fused_learner import _enable_sharding, dp_layout
 from .losses import ddqn_loss
 
@@ -235,9 +235,17 @@ class GraphLearner:
         with torch.no_grad(), amp:
             return net(frames)[2].float()
 
+    def _segments(self):
+        """(parameter name, flat offset, numel) of the flat buffers (module parameter order)."""
+        out, o = [], 0
+        for name, p in self.Q.named_parameters():
+            out.append((name, o, p.numel()))
+            o += p.numel()
+        return out
+
     def save(self, path: str, extra: Optional[Dict] = None) -> None:
         save_checkpoint(path, self.Q.state_dict(), Q_target_state=self.Q_target.state_dict(),
-                        optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
+                        optimizer_state=pack_flat_state(self._segments(), rms_v=self.rms_v, rms_m=self.rms_m),
                         num_q_updates=self.num_q_updates, config=self.cfg.to_dict(),
                         rng={"replay_ctr": int(self.replay.ctr.item()), "replay_seed": int(self.replay.seed)},
                         **(extra or {}))
@@ -259,10 +267,7 @@ class GraphLearner:
                     p.copy_(v)
             else:
                 self.sync_target()
-            opt = ck.get("optimizer_state") or {}
-            if "rms_v" in opt:
-                self.rms_v.copy_(opt["rms_v"])
-                self.rms_m.copy_(opt["rms_m"])
+            unpack_flat_state(ck.get("optimizer_state"), self._segments(), rms_v=self.rms_v, rms_m=self.rms_m)
         self.num_q_updates = int(ck.get("num_q_updates", 0))
         rng = ck.get("rng")
         if isinstance(rng, dict) and "replay_ctr" in rng:

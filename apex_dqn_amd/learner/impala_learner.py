@@ -38,7 +38,8 @@ from ..models.dueling import ImpalaDuellingDQN
 from ..models.flat_params import FlatLayout
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
-from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, save_checkpoint
+from ..utils.checkpoint import (adopt_obs_scale, layout_segments, load_checkpoint, pack_flat_state,
+                                save_checkpoint, unpack_flat_state)
 from ..ops.switches import SW
 from .fused_learner import _enable_sharding, dp_layout
 from .is_norm import IsNormMixin
@@ -164,9 +165,10 @@ class FusedImpalaLearner(IsNormMixin):
         # cost more than the overlap); the head kernel writes the priorities back and
         # the optimizer launch draws the next batch (Runtime.presample)
         self._side = None
-        # the conv weight gradients beside the data-gradient chain (SW.bwd_branches, one rank)
-        self._wg_stream = torch.cuda.Stream(self.device) if (on_gpu and SW.impala_bwd_branches and self.world == 1) \
-            else None
+        # (the 15 conv weight gradients on a second stream beside the data-gradient chain
+        # measured no gain -- 392.5 / 393.9 vs 395.6 / 395.4 steps/s fp32,
+        # profiles/r4_ab_impala_bwd_branches.txt -- and were removed: the IMPALA kernels
+        # fill the chip on their own)
         self._presample = bool(self.rt.presample)
         self._sample_ver = None
         self.partials = torch.zeros(1024, dtype=torch.float64, device=d)
@@ -386,11 +388,7 @@ class FusedImpalaLearner(IsNormMixin):
         self._sample_ver = self.replay.version
 
     def _seg2(self) -> None:
-        """fc data gradient, then the three stacks backwards.  With the branched backward
-        (SW.bwd_branches, one rank on a GPU) the 15 conv weight gradients run on a second
-        stream, each after the data gradient it reads (an event per wgrad), beside the
-        data-gradient chain that is the step's critical path; joined before the split-K
-        finalisation (SW.impala_bwd_branches: off, measured no gain)."""
+        """fc data gradient, then the three stacks backwards (one stream)."""
         B, io, G = self.B, self.iops, self.G
         sp = self.split
         self.ops.fc_dgrad(self.dH, self.feat[:B], self.Pb["wfc"], self.dfeat,
@@ -398,19 +396,7 @@ class FusedImpalaLearner(IsNormMixin):
         if sp:
             io.merge(self.dfeat, self.dfeat_lo, self.dfeat32)
         jobs: list = []
-        side = self._wg_stream
-        if side is not None:
-            main = torch.cuda.current_stream(self.device)
-            wgrad0 = io.wgrad
-
-            def wgrad(*a, **kw):
-                ev = torch.cuda.Event()
-                ev.record(main)
-                side.wait_event(ev)
-                with torch.cuda.stream(side):
-                    wgrad0(*a, **kw)
-        else:
-            wgrad = io.wgrad
+        wgrad = io.wgrad
         dO = self.dfeat32[:, :FEAT].view(B, 2, 11, 11, 16)
         for s in (2, 1, 0):
             f, b = self.fw[s], self.bw[s]
@@ -436,8 +422,6 @@ class FusedImpalaLearner(IsNormMixin):
                 wgrad(dc, prev, c0, *gw(c0), jobs)
                 dO = self.bw[s - 1]["d_o"]
                 io.conv(dc, c0, dO, transpose=True)
-        if side is not None:
-            main.wait_stream(side)
         io.finalize(jobs)
 
     def _seg3(self) -> None:
@@ -610,7 +594,7 @@ class FusedImpalaLearner(IsNormMixin):
 
     def save(self, path: str, extra: Optional[Dict] = None) -> None:
         save_checkpoint(path, self.module_state(), Q_target_state=self.module_state(self.T),
-                        optimizer_state={"rms_v": self.rms_v.cpu(), "rms_m": self.rms_m.cpu()},
+                        optimizer_state=pack_flat_state(layout_segments(self.layout), rms_v=self.rms_v, rms_m=self.rms_m),
                         num_q_updates=self.num_q_updates, config=self.cfg.to_dict(),
                         rng={"replay_ctr": int(self.replay.ctr.item()), "replay_seed": int(self.replay.seed)},
                         **(extra or {}))
@@ -630,9 +614,7 @@ class FusedImpalaLearner(IsNormMixin):
         else:
             self.sync_target()
         opt = ck.get("optimizer_state")
-        if isinstance(opt, dict) and "rms_v" in opt:
-            self.rms_v.copy_(opt["rms_v"])
-            self.rms_m.copy_(opt["rms_m"])
+        unpack_flat_state(opt, layout_segments(self.layout), rms_v=self.rms_v, rms_m=self.rms_m)
         self.num_q_updates = int(ck.get("num_q_updates", 0))
         rng = ck.get("rng")
         if isinstance(rng, dict) and "replay_ctr" in rng:

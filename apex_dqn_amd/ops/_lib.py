@@ -46,15 +46,10 @@ class HeadLo(ctypes.Structure):
     _fields_ = [("Hon", c_p), ("Htg", c_p), ("dH", c_p)]
 
 
-class FcSK(ctypes.Structure):
-    """Stream-K split of the fc forward (mirrors ``FcSK``, csrc/fc_sk.h)."""
-    _fields_ = [("nblk", c_i), ("kt", c_i), ("ntm", c_i), ("ntn", c_i), ("m_switch", c_i)]
-
-
 class HeadPart(ctypes.Structure):
     """fc split-K partials consumed by the DDQN head (mirrors ``HeadPart``, csrc/head_common.h)."""
     _fields_ = [("part", c_p), ("zstride", c_i64), ("nz", c_i), ("bias_on", c_p), ("bias_tg", c_p),
-                ("two_b", c_i), ("hon", c_p), ("hon_lo", c_p), ("sk", FcSK)]
+                ("two_b", c_i), ("hon", c_p), ("hon_lo", c_p)]
 
 
 class IsNorm(ctypes.Structure):
@@ -67,6 +62,12 @@ class CfFragOut(ctypes.Structure):
     csrc/cf_pack.h); all-zero = off."""
     _fields_ = [("w1frag", c_p), ("c2f", c_p), ("w1_off", c_i64), ("w2_off", c_i64), ("C", c_i),
                 ("in_scale", c_f)]
+
+
+class RmsSegs(ctypes.Structure):
+    """Ranges of the flat parameters one optimizer launch updates (``RmsSegs``,
+    csrc/sumtree.hip; the sharded data-parallel update)."""
+    _fields_ = [("nseg", c_i), ("blk0", c_i * 4), ("off", c_i64 * 3), ("len", c_i64 * 3)]
 
 
 class C2dPack(ctypes.Structure):
@@ -152,13 +153,12 @@ _SIGS = {
                         c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, IsNorm, c_p], c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut, c_p], c_i),
-    "apex_rmsprop_range": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p, c_p, c_p, c_i,
-                            c_i, c_p], c_i),
+                             c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut, c_p, c_p],
+                            c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
-                              c_p, c_p, c_p], c_i),
+                              c_p, c_p, c_p, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,
-                                 c_p, c_f, c_f, c_p, c_p, c_p], c_i),
+                                 c_p, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
     "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p], c_i),
     "apex_actor_head": ([c_p, HeadParams, c_i, c_i, c_p, c_u64, c_p, c_p, c_p, c_i, c_p, c_p], c_i),
     "apex_conv1_s2d_fwd": ([Conv1S2DDesc, c_i, c_p], c_i),
@@ -187,7 +187,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     conv_sigs.declare(lib)
 
 
-ABI_VERSION = 5      # csrc/sumtree.hip apex_abi_version(): the launchers' argument lists
+ABI_VERSION = 7      # csrc/sumtree.hip apex_abi_version(): the launchers' argument lists
 
 
 def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:

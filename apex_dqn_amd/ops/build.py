@@ -65,15 +65,27 @@ _COMPILER_IDS: Dict[str, str] = {}
 
 
 # ------------------------------------------------------------------ keys
+def normalize_compiler_version(text: str) -> str:
+    """The version facts of a ``--version`` banner, without what varies between two
+    installs of the same compiler (install paths, the configuration file line): the
+    lines naming a version, path tokens dropped."""
+    keep = []
+    for line in text.splitlines():
+        if "version" not in line.lower() and not line.startswith(("g++", "gcc", "c++")):
+            continue
+        toks = [t for t in line.split() if "/" not in t]
+        keep.append(" ".join(toks))
+    return "\n".join(keep) if keep else text.strip()
+
+
 def compiler_id(cc: str) -> str:
-    """``cc --version`` (cached per process): part of every key built with ``cc``."""
+    """The normalized ``cc --version`` (cached per process): part of every key built with
+    ``cc``.  A missing compiler raises: the key would not describe what built the
+    shipped objects (and nothing could rebuild them here anyway)."""
     if cc not in _COMPILER_IDS:
-        try:
-            r = subprocess.run([cc, "--version"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
-                               timeout=120)
-            _COMPILER_IDS[cc] = r.stdout.strip()
-        except Exception as e:  # pragma: no cover - missing toolchain
-            _COMPILER_IDS[cc] = f"unavailable: {e!r}"
+        r = subprocess.run([cc, "--version"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=120)
+        _COMPILER_IDS[cc] = normalize_compiler_version(r.stdout)
     return _COMPILER_IDS[cc]
 
 

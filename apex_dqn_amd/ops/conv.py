@@ -346,13 +346,12 @@ def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Opti
                  loader_waves: bool = False, x_lo=None, w_lo=None, w2_lo=None, out_lo=None,
                  c2d_pack: Optional[Tuple[torch.Tensor, Optional[torch.Tensor]]] = None,
                  no_epilogue: bool = False):
-    """``dense_fwd`` on 128x128 tiles with the K range split ``ksplit`` ways, or with
-    ``ksplit = -nblk`` a stream-K split over nblk workgroups (csrc/conv_mfma.hip
-    ``fc_gemm128_kernel``, csrc/fc_sk.h): fp32 partials in a cached workspace, summed in
-    fixed order by the epilogue kernel (bias, ReLU, hi / lo planes).
+    """``dense_fwd`` on 128x128 tiles with the K range split ``ksplit`` ways
+    (csrc/conv_mfma.hip ``fc_gemm128_kernel``): fp32 partials in a cached workspace,
+    summed in fixed order by the epilogue kernel (bias, ReLU, hi / lo planes).
     ``c2d_pack = (w2, w2_lo)``: the epilogue launch also packs conv2's weights for this
     step's conv2 data gradient (``conv2_dgrad_img(..., packed=True)``).
-    ``no_epilogue``: only the GEMM runs; returns ``(partials, nz, FcSK or None)`` for a
+    ``no_epilogue``: only the GEMM runs; returns ``(partials, nz)`` for a
     consumer that finishes the epilogue itself (the DDQN head, csrc/head_common.h
     load_row_part)."""
     M, K = x.shape
@@ -360,17 +359,9 @@ def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Opti
     assert w.shape[1] == K and out.shape == (M, Nc) and Nc % 128 == 0 and K % 64 == 0
     assert x.is_contiguous() and w.is_contiguous() and out.is_contiguous()
     kt = K // 64
-    sk = None
-    if ksplit < 0:
-        # stream-K over -ksplit workgroups (csrc/fc_sk.h): planes = most partials of a tile
-        m_switch = int(rows_first) if w2 is not None else -1
-        nz = int(lib.apex_fc_sk_planes(M, Nc, K, m_switch, -int(ksplit)))
-        assert nz >= 1, "stream-K shape"
-        sk = _lib.FcSK(nblk=-int(ksplit), kt=kt, ntm=row_tiles_host(M, m_switch if w2 is not None else None, 128),
-                       ntn=Nc // 128, m_switch=m_switch)
-    else:
-        per = -(-kt // ksplit)
-        nz = -(-kt // per)
+    assert ksplit >= 1
+    per = -(-kt // ksplit)
+    nz = -(-kt // per)
     buf = ws.get(("fc128", _lib.stream_ptr()), nz * M * Nc, x.device)   # per stream: actors share the backend
     d = _conv_desc(x=x.data_ptr(), w=w.data_ptr(), bias=_lib.ptr(b), y=out.data_ptr(), N=M, Cin=K, Cout=Nc,
                    mode=0, relu=relu, K=K, **_second(w2, b2, rows_first, 1), **_lo(x_lo, w_lo, w2_lo, out_lo))
@@ -381,7 +372,7 @@ def dense_fwd128(lib, ws: "Workspace", x: torch.Tensor, w: torch.Tensor, b: Opti
         pk.out = c2d_wfrag_buffer(ws, x.device).data_ptr()
     _lib.check(lib.apex_fc_gemm128(d, buf.data_ptr(), buf.numel(), int(ksplit), int(loader_waves),
                                       int(no_epilogue), pk, _lib.stream_ptr()), "fc_gemm128")
-    return (buf, nz, sk) if no_epilogue else None
+    return (buf, nz) if no_epilogue else None
 
 
 def c2d_wfrag_buffer(ws: "Workspace", device) -> torch.Tensor:
@@ -656,7 +647,7 @@ def dense_wgrad_head_prio(lib, dy, x, dw_out, db_out, norm, Hon, dhead, g, repla
                                      g["bv"].data_ptr(), g["wa"].data_ptr(), g["ba"].data_ptr(), g["wv"].numel(),
                                      replay.tree_desc(), idx.data_ptr(), td.data_ptr(), _lib.ptr(gen),
                                      replay.gen.data_ptr(), replay.alpha, replay.eps, replay.ctr.data_ptr(),
-                                     _lib.ptr(Hon_lo), _lib.stream_ptr())
+                                     _lib.ptr(Hon_lo), _lib.ptr(replay.local_stats), _lib.stream_ptr())
     if rc == 1:          # hipErrorInvalidValue: not the compiled shape
         return None
     _lib.check(rc, "fc_wgrad_head_prio")

@@ -51,7 +51,6 @@ def declare(lib: ctypes.CDLL) -> None:
         "apex_conv3_dgrad_img": ([Conv3DgradImgDesc, c_i, c_p], c_i),
         "apex_conv_fwd": ([ConvDesc, c_p], c_i),
         "apex_fc_gemm128": ([ConvDesc, c_p, c_i64, c_i, c_i, c_i, C2dPackJob, c_p], c_i),
-        "apex_fc_sk_planes": ([c_i, c_i, c_i, c_i, c_i], c_i),
         "apex_conv_wgrad": ([WgradDesc, c_p, c_p, c_i, c_f, c_p], c_i),
         "apex_pack_dgrad_weights": ([c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_i),
     }

@@ -18,6 +18,7 @@ op of before.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, Optional
 
 import torch
@@ -223,11 +224,17 @@ class TorchBackend:
         dx_out.copy_(dx.reshape(dx_out.shape))
 
     def fc_wgrad(self, dh, x, dw_out, db_out, norm=None, dh_lo=None, x_lo=None):
+        """``norm = (partials, slot0)``: also the squared norm of what it writes, in fp64
+        at ``partials[slot0]`` (one slot; the HIP kernel writes 4 per workgroup)."""
         xf = join(x.reshape(x.shape[0], -1), None if x_lo is None else x_lo.reshape(x.shape[0], -1))
         dhf = join(dh, dh_lo)
         dw_out.copy_(dhf.t() @ xf)
         db_out.copy_(dhf.sum(0))
-        return 0
+        if norm is None:
+            return 0
+        part, s0 = norm
+        part[s0] = dw_out.double().pow(2).sum() + db_out.double().pow(2).sum()
+        return 1
 
     def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None, dh_lo=None, x_lo=None,
                       Hon_lo=None) -> int:
@@ -262,34 +269,49 @@ class TorchBackend:
 
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None, frag_out=None):
+                  sample=None, pb_lo=None, wnorm=None, frag_out=None, segs=None):
         """``sample = (replay, B, out, nxt2)``: also draw the next
         batch after the update (the HIP backend fuses it into the optimizer launch).
         ``pb_lo``: split mode, the lo plane of the bf16 copy.  ``wnorm = (stats, n,
         stride)``: batch-max IS normalisation, the gradient is divided by the largest of
-        the n per-rank maxima ``stats[k * stride]`` (csrc/rmsprop_common.h is_grad_scale)."""
-        self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo, wnorm)
+        the n per-rank maxima ``stats[k * stride]`` (csrc/rmsprop_common.h is_grad_scale).
+        ``norm_total = (partials, n)``: the clip norm is sqrt(sum(partials[:n])) (squared-norm
+        partials written by the gradient producers) instead of a pass over ``g32``.
+        ``segs``: [(offset, length), ...] -- update only these ranges of the flat arrays
+        (the sharded data-parallel update; needs ``norm_total``)."""
+        self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo, wnorm, norm_total,
+                        segs)
         if sample is not None:
             rp, B, out, nxt2 = sample
             rp.sample(B, out=out, nxt2=nxt2)
 
-    def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo=None, wnorm=None):
+    def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo=None, wnorm=None,
+                   norm_total=None, segs=None):
         sc = torch.ones((), dtype=torch.float32, device=g32.device)
         if wnorm is not None:     # tensor ops only: no host sync (graph-capturable)
             st, n, stride = wnorm
             mx = st.reshape(-1)[0:n * stride:stride].max().float()
             sc = torch.where(mx > 0, 1.0 / mx.clamp_min(1e-30), sc)
-        norm = g32.double().pow(2).sum().sqrt().float() * sc
-        coef = torch.clamp(clip / (norm + 1e-6), max=1.0) if clip > 0 else torch.ones_like(norm)
-        g = g32 * (coef * sc)
-        v.mul_(alpha).add_((1 - alpha) * g * g)
-        if centered:
-            m.mul_(alpha).add_((1 - alpha) * g)
-            var = v - m * m
+        if norm_total is not None:
+            part, npart = norm_total if isinstance(norm_total, tuple) else (norm_total, 1)
+            sq = part[:npart].double().sum()
         else:
-            var = v
-        p32.sub_(lr * g / (var.clamp_min(0).sqrt() + eps))
-        split_into(p32, pbf, pb_lo)
+            assert segs is None, "a sharded update needs the clip norm's partials (norm_total)"
+            sq = g32.double().pow(2).sum()
+        norm = sq.sqrt().float() * sc
+        coef = torch.clamp(clip / (norm + 1e-6), max=1.0) if clip > 0 else torch.ones_like(norm)
+        for o, n in (segs if segs is not None else [(0, p32.numel())]):
+            r = slice(o, o + n)
+            g = g32[r] * (coef * sc)
+            vr, mr, pr = v[r], m[r], p32[r]
+            vr.mul_(alpha).add_((1 - alpha) * g * g)
+            if centered:
+                mr.mul_(alpha).add_((1 - alpha) * g)
+                var = vr - mr * mr
+            else:
+                var = vr
+            pr.sub_(lr * g / (var.clamp_min(0).sqrt() + eps))
+            split_into(pr, pbf[r], None if pb_lo is None else pb_lo[r])
         norm_out.copy_(norm.view(1))
 
     def gather_frames(self, replay, slots, out):
@@ -305,10 +327,10 @@ class TorchBackend:
             c0 += t2.shape[1]
 
     def sqnorm_ranges(self, ranges, partials: torch.Tensor, nblk: int) -> int:
-        """Squared-norm partials of the fp32 ``ranges`` into ``partials[:nblk]`` (the HIP
-        optimizer sums producer partials; the torch optimizer takes the norm of the whole
-        gradient itself: nothing to do).  Returns the slots written."""
-        return 0
+        """Squared-norm partials of the fp32 ``ranges`` into ``partials`` (fp64; the HIP
+        kernel writes ``nblk`` block partials, this one slot).  Returns the slots written."""
+        partials[0] = sum(r.double().pow(2).sum() for r in ranges if r is not None)
+        return 1
 
 
 class HipBackend(TorchBackend):
@@ -390,8 +412,6 @@ class HipBackend(TorchBackend):
             tiles = C.row_tiles_host(M, rows_first if w2 is not None else None, 128) * (w.shape[0] // 128)
             if ksplit > 0:
                 ks = int(ksplit)
-            elif SW.fc_stream_k > 0 and tiles * (K // 64) >= SW.fc_stream_k:
-                ks = -SW.fc_stream_k          # stream-K: every workgroup an equal (tile, K) range
             else:
                 ks = max(2, 256 // max(tiles, 1))
                 if SW.fc_ksplit_max > 0:
@@ -401,7 +421,7 @@ class HipBackend(TorchBackend):
                                out_lo=out_lo, c2d_pack=None if defer else c2d, no_epilogue=defer)
             if defer:
                 # the split-K epilogue (and the conv2 pack) move into the next head launch
-                self._fc_part = dict(part=r[0], nz=r[1], sk=r[2], zstride=M * w.shape[0], b=b, b2=b2,
+                self._fc_part = dict(part=r[0], nz=r[1], zstride=M * w.shape[0], b=b, b2=b2,
                                      two_b=rows_first, out=out, c2d=c2d)
                 return
             # the conv2 data gradient of this step finds its weights packed (the key is
@@ -493,8 +513,6 @@ class HipBackend(TorchBackend):
             self._fc_part = None
             assert fp["out"].data_ptr() == Hon.data_ptr() and fp["two_b"] == 2 * B
             hp.part, hp.zstride, hp.nz = fp["part"].data_ptr(), int(fp["zstride"]), int(fp["nz"])
-            if fp.get("sk") is not None:
-                hp.sk = fp["sk"]
             hp.bias_on, hp.bias_tg, hp.two_b = fp["b"].data_ptr(), fp["b2"].data_ptr(), int(fp["two_b"])
             hp.hon, hp.hon_lo = Hon.data_ptr(), _lib.ptr(None if lo is None else lo[0])
             if fp["c2d"] is not None:
@@ -515,7 +533,7 @@ class HipBackend(TorchBackend):
                 Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(), g["bv"].data_ptr(),
                 g["wa"].data_ptr(), g["ba"].data_ptr(), g["wv"].numel(), rp.tree_desc(), idx.data_ptr(),
                 td.data_ptr(), _lib.ptr(gen), rp.gen.data_ptr(), rp.alpha, rp.eps, rp.ctr.data_ptr(),
-                _lib.ptr(Hon_lo), _lib.stream_ptr()), "head_wgrad_prio")
+                _lib.ptr(Hon_lo), _lib.ptr(rp.local_stats), _lib.stream_ptr()), "head_wgrad_prio")
             return
         if prio is not None:
             prio[0].update_priorities(prio[1], prio[3], prio[2])
@@ -530,11 +548,25 @@ class HipBackend(TorchBackend):
                                             P["wv"].numel(), _lib.ptr(H_lo), _lib.stream_ptr()), "actor_head")
 
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None, frag_out=None) -> bool:
+                  sample=None, pb_lo=None, wnorm=None, frag_out=None, segs=None) -> bool:
         """``frag_out`` (ops/conv.py conv12_frag_out): the launch also stores the updated
         w1 / w2 in the fused forward's fragment order.  Returns whether it did (the fused
-        optimizer + sample launch only)."""
+        optimizer + sample launch only).  ``segs``: the ranges to update (the sharded DP
+        update: one launch, csrc/sumtree.hip ``RmsSegs``)."""
         n = p32.numel()
+        if segs is not None:
+            if norm_total is None:
+                raise ValueError("a sharded update needs the clip norm's partials (norm_total)")
+            if sample is None or not sample[0].use_hip:
+                raise ValueError("the sharded update runs in the fused optimizer + sample launch")
+            sg = _lib.RmsSegs()
+            sg.nseg = len(segs)
+            assert 1 <= sg.nseg <= 3
+            for k, (o, ln) in enumerate(segs):
+                sg.off[k], sg.len[k] = int(o), int(ln)
+            segp = ctypes.byref(sg)
+        else:
+            segp = None
         st = _lib.stream_ptr()
         lo = _lib.ptr(pb_lo)
         wn = (wnorm[0].data_ptr(), int(wnorm[1]), int(wnorm[2])) if wnorm is not None else (None, 0, 0)
@@ -554,7 +586,7 @@ class HipBackend(TorchBackend):
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
                 *rp.sample_launch_args(B, out, nxt2), lo, *wn, frag_out if frag_out is not None else _lib.CfFragOut(),
-                st), "rmsprop_sample")
+                segp, st), "rmsprop_sample")
             return frag_out is not None
         if sample is not None:
             self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,
@@ -577,7 +609,6 @@ class HipBackend(TorchBackend):
                    "rmsprop")
 
     def pack_rows(self, dst: torch.Tensor, segs) -> None:
-        import ctypes
         if dst.dtype not in (torch.bfloat16, torch.float16) or len(segs) > 4:
             return super().pack_rows(dst, segs)
         n = len(segs)
@@ -596,18 +627,6 @@ class HipBackend(TorchBackend):
         _lib.check(self.lib.apex_grad_sqnorm_partials(g32.data_ptr(), g32.numel(), partials.data_ptr(),
                                                       _lib.stream_ptr()), "sqnorm")
         return partials.numel()
-
-    def optimizer_range(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, norm_total,
-                        pb_lo=None, wnorm=None) -> None:
-        """Clip + centered RMSprop over a range of the flat parameters (views), bit-identical
-        to the fused optimizer + sample launch over the same range: ``norm_total =
-        (partials, count)`` of the WHOLE gradient (csrc/sumtree.hip apex_rmsprop_range)."""
-        part, npart = norm_total
-        wn = (wnorm[0].data_ptr(), int(wnorm[1]), int(wnorm[2])) if wnorm is not None else (None, 0, 0)
-        _lib.check(self.lib.apex_rmsprop_range(
-            p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), p32.numel(), part.data_ptr(),
-            int(npart), float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
-            _lib.ptr(pb_lo), *wn, _lib.stream_ptr()), "rmsprop_range")
 
     def sqnorm_ranges(self, ranges, partials: torch.Tensor, nblk: int) -> int:
         (a, b) = (list(ranges) + [None])[:2]

@@ -43,33 +43,12 @@ class Switches:
     # single-rank step: the weight gradients (fc + heads + priority write-back, conv3,
     # conv2) on a second stream beside the data-gradient chain (graph branches)
     bwd_branches: bool = True
-    # the IMPALA learner's 15 conv weight gradients beside its data-gradient chain: no gain
-    # (392.5 / 393.9 vs 395.6 / 395.4 steps/s fp32, profiles/r4_ab_impala_bwd_branches.txt)
-    impala_bwd_branches: bool = False
-    # inside multi-update graphs: the fc layer's RMSprop update on a stream of its own,
-    # beside the next update's conv forward (learner/fused_learner.py _seg3).  Bit-identical
-    # but slower: the rest of the launch keeps the next batch's draw, a ~20 us latency chain
-    # the fc update used to hide, and the fc forward pays a join edge -- 2,659 / 2,649 vs
-    # 2,669 / 2,677 steps/s, 6,550 / 6,574 vs 6,657 / 6,641 at 74 rows
-    # (profiles/r4_ab_opt_overlap_rejected.txt).  Off.
-    opt_overlap: bool = False
     # the GPU actors' fc forward: this K split (0: the chip-filling split of the learner)
     actor_fc_ksplit: int = 4
     # single-rank branched backward: the fc weight gradient (+ head wgrad + priorities) on
     # the main stream right after the fc dgrad, the branch forking after it ("on"), on the
     # branch beside the dgrad chain ("off"), "auto": main for fp32-class at >= 256 rows
     fc_wgrad_main: str = "auto"
-    # fc forward: stream-K over this many workgroups (0: a fixed K split, fc_ksplit_max).
-    # Measured slower: fc 43.1 vs 40.5 us at 512 rows, 18.8 vs 12.6 at 74 (segments restart
-    # the LDS pipeline, more partial planes for the head), profiles/r4_ab_fc_stream_k_rejected.txt
-    fc_stream_k: int = 0
-    # DP step, factored fc exchange: the global batch's fc wgrad on the branch stream (after
-    # its conv2 wgrad, beside conv1's) instead of on the main stream after conv1
-    dp_fc_wgrad_branch: bool = True
-    # DP step, native communicator: conv1's (last) gradient bucket all-reduced on the main
-    # stream itself after one join of the comm stream, instead of forked to the comm stream
-    # and joined back (nothing overlaps it; saves a graph edge on the critical path)
-    dp_inline_last: bool = False
     # cap on the fc forward's K splits (0: fill the chip, ops/fused_ops.py fc_fwd); the DDQN
     # head sums the splits' partials (the deferred epilogue)
     fc_ksplit_max: int = 0

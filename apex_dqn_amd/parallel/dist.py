@@ -177,6 +177,38 @@ class Comm:
         return float(t.item())
 
 
+class EmulatedComm(Comm):
+    """Rank ``rank`` of a ``world``-rank data-parallel job, alone on one GPU
+    (``bench.py --emulate-world W``): the learner sizes its step for ``world`` ranks
+    (rows per rank, fc row slice, sharded replay) and its collectives become device
+    copies of their true sizes (``parallel/rccl.py EmulatedCollectives``).  Host-side
+    collectives are identities (no process group); ``active`` is False so callers
+    never wait for peers that do not exist."""
+    emulated = True
+
+    def __init__(self, world_size: int, rank: int = 0, device: Optional[torch.device] = None):
+        super().__init__(rank, world_size, device)
+
+    @property
+    def active(self) -> bool:
+        return False
+
+    def barrier(self) -> None:
+        pass
+
+    def shutdown(self) -> None:
+        pass
+
+    def broadcast_flat(self, flat: torch.Tensor, src: int = 0) -> None:
+        pass
+
+    def broadcast_int(self, x: int, src: int = 0) -> int:
+        return int(x)
+
+    def allreduce_scalar(self, x: float, op: str = "sum") -> float:
+        return float(x)
+
+
 class _Pending:
     def __init__(self, works: List, flat: Optional[torch.Tensor], ws: int):
         self.works, self.flat, self.ws = works, flat, ws

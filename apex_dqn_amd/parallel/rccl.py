@@ -13,9 +13,15 @@ learner's DP step stays ONE captured graph -- and ``abort()`` /
 
 ``make_collectives(comm, backend)`` returns the object the learner step uses:
 ``TorchCollectives`` (torch.distributed: RCCL via the ``nccl`` process group, or
-gloo on CPU) or ``NativeCollectives`` (this communicator).  Both expose
-``all_reduce(t, op)`` and ``all_gather_into(out, inp)`` returning a handle whose
-``wait()`` makes the current stream wait for the result.
+gloo on CPU), ``NativeCollectives`` (this communicator) or ``EmulatedCollectives``
+(``bench.py --emulate-world W``: rank 0's share of a W-rank step on one GPU, every
+collective a device copy of its true size on a comm stream).  All expose
+``all_reduce(t, op)``, ``all_gather_into(out, inp)`` (in place when ``inp`` is this
+rank's chunk of ``out``) and ``reduce_scatter_into(out, inp)``, returning a handle
+whose ``wait()`` makes the current stream wait for the result; on a GPU the handle
+also carries the completion ``event`` (any stream may wait on it: a graph edge under
+capture).  ``all_reduce_inline`` (where ``inline`` is True) enqueues on the current
+stream itself -- no fork / join edge on the step's critical path.
 """
 from __future__ import annotations
 
@@ -56,6 +62,8 @@ def load_comm_lib() -> ctypes.CDLL:
         "apex_comm_all_reduce": ([c_p, c_p, c_p, c_sz, c_i, c_i, c_p], c_i),
         "apex_comm_all_gather": ([c_p, c_p, c_p, c_sz, c_i, c_p], c_i),
         "apex_comm_broadcast": ([c_p, c_p, c_p, c_sz, c_i, c_i, c_p], c_i),
+        "apex_comm_reduce_scatter": ([c_p, c_p, c_p, c_sz, c_i, c_i, c_p], c_i),
+        "apex_comm_count": ([c_p, ctypes.POINTER(c_i), ctypes.POINTER(c_i)], c_i),
         "apex_comm_group_start": ([], c_i),
         "apex_comm_group_end": ([], c_i),
         "apex_comm_async_error": ([c_p], c_i),
@@ -132,6 +140,19 @@ class RcclComm:
         self._enqueue(self.lib.apex_comm_all_gather, "all_gather", inp.data_ptr(), out.data_ptr(), inp.numel(),
                       _DTYPES[inp.dtype], s.cuda_stream)
 
+    def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", stream=None) -> None:
+        """out = this rank's chunk of the reduction of ``inp`` (world x out.numel())."""
+        assert inp.numel() == out.numel() * self.world and out.dtype == inp.dtype
+        s = stream or torch.cuda.current_stream(self.device)
+        self._enqueue(self.lib.apex_comm_reduce_scatter, "reduce_scatter", inp.data_ptr(), out.data_ptr(),
+                      out.numel(), _DTYPES[out.dtype], _OPS[op], s.cuda_stream)
+
+    def count(self):
+        """(ranks, this rank) as the RCCL communicator itself reports them."""
+        n, r = ctypes.c_int(0), ctypes.c_int(-1)
+        self._check(self.lib.apex_comm_count(self.handle, ctypes.byref(n), ctypes.byref(r)), "comm_count")
+        return int(n.value), int(r.value)
+
     def broadcast_(self, t: torch.Tensor, src: int = 0, stream=None) -> None:
         s = stream or torch.cuda.current_stream(self.device)
         self._enqueue(self.lib.apex_comm_broadcast, "broadcast", t.data_ptr(), t.data_ptr(), t.numel(),
@@ -160,49 +181,104 @@ class RcclComm:
 
 # ------------------------------------------------------------------ collectives
 class _Done:
+    event = None
+
     def wait(self) -> None:
         pass
 
 
 class _TorchWork:
-    def __init__(self, work):
+    event = None
+
+    def __init__(self, work, coll=None):
         self.work = work
+        self.coll = coll
+        if coll is not None:
+            coll._seq += 1
+            self.seq = coll._seq
 
     def wait(self) -> None:
-        if self.work is not None:
+        """The current stream waits for the process group's stream (RCCL: in issue order,
+        so a wait covers every earlier collective and later waits on those add no edge)."""
+        if self.work is None:
+            return
+        c = self.coll
+        if c is None:
             self.work.wait()
+            return
+        key = torch.cuda.current_stream(c.device).cuda_stream
+        if self.seq > c._joined.get(key, 0):
+            self.work.wait()
+            c._joined[key] = self.seq
 
 
 class _StreamWork:
-    """Completion of a collective enqueued on the comm stream: ``wait`` makes the
-    current stream wait for an event recorded right after it (a graph edge under
-    capture), so a later collective still in flight is not waited for.  The
-    collectives of one ``NativeCollectives`` run in order on one stream, so a join
-    covers every op enqueued before it: a wait on an op already covered by an earlier
-    join of the same stream adds no edge (each cross-queue edge of a captured graph costs several
+    """Completion of a collective enqueued on a collectives object's comm stream: ``wait``
+    makes the current stream wait for an event recorded right after it (a graph edge
+    under capture), so a later collective still in flight is not waited for.  The
+    collectives of one object run in order on one stream, so a join covers every op
+    enqueued before it: a wait on an op already covered by an earlier join of the same
+    stream adds no edge (each cross-queue edge of a captured graph costs several
     microseconds)."""
 
-    def __init__(self, coll: "NativeCollectives"):
+    def __init__(self, coll):
         self.coll = coll
         coll._seq += 1
         self.seq = coll._seq
         self.event = torch.cuda.Event()
-        self.event.record(coll.comm.stream)
+        self.event.record(coll.stream)
 
     def wait(self) -> None:
         c = self.coll
-        cur = torch.cuda.current_stream(c.comm.device)
+        cur = torch.cuda.current_stream(c.device)
         key = cur.cuda_stream
         if self.seq > c._joined.get(key, 0):
             cur.wait_event(self.event)
             c._joined[key] = self.seq
 
 
-class TorchCollectives:
-    name = "torch"
+class _StreamColl:
+    """Shared plumbing: a comm stream that forks from the current stream per op."""
+    inline = False
 
-    def __init__(self, group=None):
+    def _init_stream(self, device):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        self._seq = 0          # collectives enqueued
+        self._joined = {}      # per waiting stream: the last collective a join covers
+
+    def _fork(self):
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream != self.stream.cuda_stream:
+            self.stream.wait_stream(cur)
+        return self.stream
+
+    def use_stream(self, stream) -> None:
+        """Enqueue the collectives on ``stream`` (the learner's branch stream) instead of a
+        stream of their own."""
+        self.stream = stream
+        self._joined = {}
+
+
+class TorchCollectives:
+    """torch.distributed.  With the RCCL process group the collectives run on the process
+    group's own stream, forked from the current stream; their handles are waited for on
+    the step's main (capture-origin) stream only -- a forked stream that waits on a
+    stream forked from itself crashed HIP graph capture (hipStreamEndCapture segfault,
+    round 5, ``scripts/probe_dp_capture.py``), so the branch receives collective results
+    by a main-stream handover (learner/dp_step.py ``Streams.handover``).  gloo (CPU
+    tests, one-GPU rehearsals) keeps the process group's own handles."""
+    name = "torch"
+    inline = False
+
+    def __init__(self, group=None, device=None):
+        import torch.distributed as dist
         self.group = group
+        self._nccl = (device is not None and torch.device(device).type == "cuda"
+                      and dist.is_initialized() and dist.get_backend(group) == "nccl")
+        self.device = torch.device(device) if device is not None else None
+        self._seq = 0
+        self._joined = {}
 
     def _sync(self, t: torch.Tensor) -> bool:
         """gloo on device tensors (one-GPU rehearsals): run the collective synchronously.
@@ -211,9 +287,14 @@ class TorchCollectives:
         import torch.distributed as dist
         return t.is_cuda and dist.get_backend(self.group) != "nccl"
 
+    def _on_stream(self, fn):
+        return _TorchWork(fn(), self)
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         import torch.distributed as dist
         rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+        if self._nccl:
+            return self._on_stream(lambda: dist.all_reduce(t, op=rop, group=self.group, async_op=True))
         if self._sync(t):
             dist.all_reduce(t, op=rop, group=self.group)
             return _Done()
@@ -221,30 +302,50 @@ class TorchCollectives:
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
         import torch.distributed as dist
-        if dist.get_backend(self.group) == "nccl":
+        if self._nccl:
+            return self._on_stream(lambda: dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True))
+        if dist.get_backend(self.group) == "nccl":      # (no device given: the process group's handle)
             return _TorchWork(dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True))
         # gloo (CPU tests, one-GPU rehearsals; its all_gather takes no CUDA tensors): a
-        # SUM all-reduce of the rank-placed rows, exact (every other row is zero)
+        # SUM all-reduce of the rank-placed rows, exact (every other row is zero); ``inp``
+        # may be this rank's chunk of ``out`` (in place)
         W, n = dist.get_world_size(self.group), inp.numel()
         r = dist.get_rank(self.group)
+        src = inp.reshape(-1).clone()
         out.zero_()
-        out.view(W, n)[r].copy_(inp.reshape(-1))
+        out.view(W, n)[r].copy_(src)
         return self.all_reduce(out, "sum")
 
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum"):
+        import torch.distributed as dist
+        if self._nccl:
+            rop = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}[op]
+            return self._on_stream(lambda: dist.reduce_scatter_tensor(out, inp, op=rop, group=self.group,
+                                                                      async_op=True))
+        # gloo has no reduce-scatter: all-reduce a copy, keep this rank's chunk
+        W, n = dist.get_world_size(self.group), out.numel()
+        r = dist.get_rank(self.group)
+        tmp = inp.reshape(-1).clone()
+        self.all_reduce(tmp, op).wait()
+        out.reshape(-1).copy_(tmp.view(W, n)[r])
+        return _Done()
 
-class NativeCollectives:
+    def world(self) -> int:
+        import torch.distributed as dist
+        return int(dist.get_world_size(self.group))
+
+
+class NativeCollectives(_StreamColl):
     """The DP step's collectives on the native communicator's own stream."""
     name = "native"
+    inline = True
 
     def __init__(self, comm: RcclComm):
         self.comm = comm
-        self._seq = 0          # collectives enqueued
-        self._joined = {}      # per waiting stream: the last collective a join covers
-
-    def _fork(self):
-        cur = torch.cuda.current_stream(self.comm.device)
-        self.comm.stream.wait_stream(cur)
-        return self.comm.stream
+        self.device = comm.device
+        self.stream = comm.stream
+        self._seq = 0
+        self._joined = {}
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         s = self._fork()
@@ -256,22 +357,98 @@ class NativeCollectives:
         self.comm.all_gather_(out, inp, stream=s)
         return _StreamWork(self)
 
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum"):
+        s = self._fork()
+        self.comm.reduce_scatter_(out, inp, op, stream=s)
+        return _StreamWork(self)
+
     def all_reduce_inline(self, t: torch.Tensor, op: str = "sum"):
         """All-reduce enqueued on the CURRENT stream (no fork / join): the caller has
         already joined every collective issued before it, so RCCL's issue order holds."""
         self.comm.all_reduce_(t, op)
         return _Done()
 
+    def world(self) -> int:
+        return self.comm.count()[0]
+
+
+class EmulatedCollectives(_StreamColl):
+    """Rank ``rank``'s view of a ``world``-rank step on ONE GPU (``bench.py
+    --emulate-world``): every collective is a device copy of its true size on a comm
+    stream joined like the real one's -- an all-gather writes this rank's chunk into
+    every slot (the gathered rows / statistics / parameters stay valid data), an
+    all-reduce copies the buffer once, a reduce-scatter copies this rank's chunk.  It
+    measures the per-rank compute, the graph edges and the copies; RCCL's own latency
+    and xGMI transfer time are not in it."""
+    name = "emulated"
+    inline = True
+
+    def __init__(self, device, world: int, rank: int = 0):
+        self._init_stream(device)
+        self.W, self.rank = int(world), int(rank)
+        self._scratch = {}
+
+    def _buf(self, t: torch.Tensor) -> torch.Tensor:
+        key = (t.dtype, t.numel())
+        b = self._scratch.get(key)
+        if b is None:
+            b = self._scratch[key] = torch.empty(t.numel(), dtype=t.dtype, device=self.device)
+        return b
+
+    def _reduce(self, t: torch.Tensor) -> None:
+        self._buf(t).copy_(t.reshape(-1))
+
+    def _gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        W, n, r = self.W, inp.numel(), self.rank
+        rows = out.view(W, n)
+        src = inp.reshape(1, n)
+        if r > 0:
+            rows[:r].copy_(src.expand(r, n))
+        if r + 1 < W:
+            rows[r + 1:].copy_(src.expand(W - r - 1, n))
+        if inp.data_ptr() != rows[r].data_ptr():
+            rows[r].copy_(inp.reshape(-1))
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum"):
+        s = self._fork()
+        with torch.cuda.stream(s):
+            self._reduce(t)
+        return _StreamWork(self)
+
+    def all_reduce_inline(self, t: torch.Tensor, op: str = "sum"):
+        self._reduce(t)
+        return _Done()
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
+        s = self._fork()
+        with torch.cuda.stream(s):
+            self._gather(out, inp)
+        return _StreamWork(self)
+
+    def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum"):
+        s = self._fork()
+        n = out.numel()
+        with torch.cuda.stream(s):
+            out.reshape(-1).copy_(inp.reshape(-1)[self.rank * n:(self.rank + 1) * n])
+        return _StreamWork(self)
+
+    def world(self) -> int:
+        return self.W
+
 
 def make_collectives(comm, backend: str = "torch", device=None):
     """Collectives for the learner's DP step: ``torch`` (torch.distributed) or
-    ``native`` (RcclComm; GPU ranks with an initialised process group)."""
+    ``native`` (RcclComm; GPU ranks with an initialised process group); an emulated
+    communicator (``parallel/dist.py EmulatedComm``) gets ``EmulatedCollectives``."""
+    dev = device if device is not None else getattr(comm, "device", None)
+    if getattr(comm, "emulated", False):
+        return EmulatedCollectives(dev, comm.world_size, comm.rank)
     if backend == "native":
         nc = getattr(comm, "_native", None)
         if nc is None:
-            nc = RcclComm(comm.rank, comm.world_size, device if device is not None else comm.device)
+            nc = RcclComm(comm.rank, comm.world_size, dev)
             comm._native = nc
         return NativeCollectives(nc)
     if backend != "torch":
         raise ValueError("Runtime.comm_backend must be 'torch' or 'native'")
-    return TorchCollectives(getattr(comm, "group", None))
+    return TorchCollectives(getattr(comm, "group", None), dev)

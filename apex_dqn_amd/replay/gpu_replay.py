@@ -211,24 +211,29 @@ class GpuReplayShard:
         self.shard_rank, self.shard_world = int(rank), int(world)
         self.shard_seed, self.shard_group = int(shard_seed), group
         self.shard_mcap = int(mcap)
-        self.local_stats = torch.zeros(SHARD_STATS, dtype=torch.float64, device=d)
         self.shard_stats = torch.zeros(SHARD_STATS * self.shard_world, dtype=torch.float64, device=d)
+        # this shard's slot of the gathered statistics (the all-gather runs in place)
+        r = self.shard_rank
+        self.local_stats = self.shard_stats[SHARD_STATS * r:SHARD_STATS * (r + 1)]
 
     @property
     def sharded(self) -> bool:
         return self.shard_stats is not None
 
-    def gather_shard_stats(self, async_op: bool = False, coll=None):
+    def gather_shard_stats(self, async_op: bool = False, coll=None, fresh_local: bool = False):
         """All-gather every shard's (sum p^alpha, min p^alpha, batch IS max) into ``shard_stats``
-        (a collective; device-side, HIP-graph capturable over RCCL).  Call it after
-        the last tree mutation that the next draw must see (the third field is written
-        by the learner's head kernel: ``local_stats[2]``).  ``coll``: the learner's
-        collectives (parallel/rccl.py; torch.distributed by default).  With
-        ``async_op`` the returned handle's ``wait()`` orders the result."""
+        (a collective; device-side, HIP-graph capturable over RCCL; in place: ``local_stats``
+        is this shard's slot).  Call it after the last tree mutation that the next draw
+        must see (the third field is written by the learner's head kernel:
+        ``local_stats[2]``).  ``fresh_local``: the first two fields are already current
+        (written by the priority write-back kernel, csrc/sumtree.hip ``stats_out``).
+        ``coll``: the learner's collectives (parallel/rccl.py; torch.distributed by
+        default).  With ``async_op`` the returned handle's ``wait()`` orders the result."""
         from ..parallel.rccl import TorchCollectives
-        root = self.offs[self.L]
-        self.local_stats[0:1].copy_(self.nodes[root:root + 1])
-        self.local_stats[1:2].copy_(self.min_bits.view(torch.float32))
+        if not fresh_local:
+            root = self.offs[self.L]
+            self.local_stats[0:1].copy_(self.nodes[root:root + 1])
+            self.local_stats[1:2].copy_(self.min_bits.view(torch.float32))
         work = (coll or TorchCollectives(self.shard_group)).all_gather_into(self.shard_stats, self.local_stats)
         if async_op:
             return work
@@ -307,7 +312,13 @@ class GpuReplayShard:
 
     def _acquire_pin(self, shape) -> torch.Tensor:
         """The next of two pinned staging buffers of ``shape`` (the copy of its previous
-        use must have finished: its event is waited on first)."""
+        use must have finished: its event is waited on first).  Refuses while another
+        thread's staged frames (stage_frames) wait for their append: rotating the
+        buffers then would hand that thread's buffer out again and overwrite its frames."""
+        st = getattr(self, "_staged", None)
+        if st is not None and st[2] != threading.get_ident():
+            raise RuntimeError("GpuReplayShard: frames staged by another thread are not appended yet "
+                               "(stage_frames / append_frames must pair up on one thread)")
         shape = tuple(shape)
         if getattr(self, "_pin_shape", None) != shape:
             self._pin_buf = [torch.empty(shape, dtype=torch.uint8).pin_memory() for _ in range(2)]
@@ -331,7 +342,9 @@ class GpuReplayShard:
         with self.lock:
             buf = self._acquire_pin((int(n),) + tuple(self.frame_shape))
             arr = buf.numpy()
-            self._staged = (buf, arr)
+            # one staging slot per shard: the append of this array must come from the same
+            # thread before anything else takes a pinned buffer (_acquire_pin checks)
+            self._staged = (buf, arr, threading.get_ident())
             return arr
 
     def _pinned(self, frames: np.ndarray) -> torch.Tensor:
@@ -341,6 +354,8 @@ class GpuReplayShard:
         if st is not None and frames is st[1]:
             self._staged = None
             return st[0]
+        if st is not None and st[2] == threading.get_ident():
+            self._staged = None       # this thread staged and then appended other frames: drop it
         buf = self._acquire_pin(frames.shape)
         np.copyto(buf.numpy(), frames)
         return buf

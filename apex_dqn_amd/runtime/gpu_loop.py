@@ -224,8 +224,11 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                 if runner is not None:
                     st.actor_steps = st.actor_base + runner.steps
                 _log(metrics, learner, group, replay, st, rt, world, device)
-            if ckpt_path and rt.ckpt_freq and n % rt.ckpt_freq == 0 and rank == 0:
-                learner.save(ckpt_path, extra=_actor_rng(group))
+            if ckpt_path and rt.ckpt_freq and n % rt.ckpt_freq == 0:
+                if hasattr(learner, "materialize"):
+                    learner.materialize()      # sharded DP update: a collective, every rank
+                if rank == 0:
+                    learner.save(ckpt_path, extra=_actor_rng(group))
     finally:
         if runner is not None:
             runner.stop()

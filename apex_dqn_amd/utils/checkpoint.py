@@ -10,9 +10,12 @@ ignore.  Loading always uses ``weights_only=True`` (no pickle execution).
 from __future__ import annotations
 
 import os
-from typing import Any, Dict, Optional
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import torch
+
+# (segment name, flat offset, element count) of a learner's flat parameter buffer
+Segments = Sequence[Tuple[str, int, int]]
 
 
 def save_checkpoint(path: str, q_state: Dict[str, torch.Tensor], **extras: Any) -> None:
@@ -33,6 +36,54 @@ def load_checkpoint(path: str) -> Optional[Dict[str, Any]]:
     except FileNotFoundError:
         print("WARNING: No trained model found. Training from scratch")
         return None
+
+
+def pack_flat_state(segments: Segments, **flats: torch.Tensor) -> Dict[str, Any]:
+    """Per-parameter state kept in a flat buffer (RMSprop's ``rms_v`` / ``rms_m``), saved
+    per named segment with the layout it came from: a later engine whose flat layout
+    orders or pads the segments differently still restores every value to its parameter
+    (:func:`unpack_flat_state`)."""
+    out: Dict[str, Any] = {"layout": [[str(n), int(o), int(k)] for n, o, k in segments]}
+    for key, flat in flats.items():
+        f = flat.detach().cpu()
+        out[key] = {n: f[o:o + k].clone() for n, o, k in segments}
+    return out
+
+
+def unpack_flat_state(opt: Any, segments: Segments, **dsts: torch.Tensor) -> bool:
+    """Restore :func:`pack_flat_state` output into the flat buffers ``dsts`` of the current
+    layout ``segments``.  Refuses (returns False, with a warning, buffers untouched) state
+    without a layout tag -- an older checkpoint's raw flat vectors, whose layout cannot be
+    verified -- or whose segments do not match by name and size; the caller then starts the
+    optimizer state fresh rather than misaligned."""
+    if not isinstance(opt, dict) or not dsts:
+        return False
+    if "layout" not in opt:
+        print("WARNING: checkpoint optimizer state has no layout tag (an older flat vector); "
+              "RMSprop state not restored (starts fresh)")
+        return False
+    saved = {str(n): int(k) for n, _, k in opt["layout"]}
+    cur = {n: int(k) for n, _, k in segments}
+    if saved != cur or any(not isinstance(opt.get(key), dict) for key in dsts):
+        print("WARNING: checkpoint optimizer state layout does not match this network; "
+              "RMSprop state not restored (starts fresh)")
+        return False
+    for key, dst in dsts.items():
+        src = opt[key]
+        for n, o, k in segments:
+            dst[o:o + k].copy_(src[n].reshape(-1).to(dst.dtype))
+    return True
+
+
+def layout_segments(layout) -> List[Tuple[str, int, int]]:
+    """Segments of a ``models.flat_params.FlatLayout``."""
+    out = []
+    for name, shape in layout.segments:
+        n = 1
+        for d in shape:
+            n *= d
+        out.append((name, layout.offsets[name], n))
+    return out
 
 
 REFERENCE_OBS_SCALE = 1.0   # the reference feeds raw 0..255 floats (actor.py:117-119,161, learner.py:37)

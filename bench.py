@@ -4,12 +4,14 @@ dueling NatureCNN (BASELINE.json metric), on N MI355X of one node.
 
 One process per GPU (torchrun env vars).  Each rank owns an HBM replay shard
 prefilled with synthetic uint8 frames (no datasets on the box) and a
-data-parallel learner replica that takes a full batch of 512 from its shard
-(weak scaling: per-GPU work fixed).  A timed step is the complete learner
-update: prioritized sample + frame gather, online fwd on [S_t;S_t+n] and target
-fwd on S_t+n, DDQN/Huber/IS loss + priorities, full backward, RCCL gradient
-all-reduce (N>1), clip + centered RMSprop, priority write-back, plus the
-periodic target sync / FIFO eviction at their configured cadences.
+data-parallel learner replica.  By default (``--batch-scope global``) the N shards
+form ONE prioritized replay: every update is one global draw of 512 samples and
+each rank computes the rows that landed in its shard (strong scaling; see below).
+A timed step is the complete learner update: prioritized sample + frame gather,
+online fwd on [S_t;S_t+n] and target fwd on S_t+n, DDQN/Huber/IS loss +
+priorities, full backward, the RCCL gradient exchange (N>1; sharded fc optimizer
++ parameter all-gather, learner/dp_step.py), clip + centered RMSprop, priority
+write-back, plus the periodic target sync / FIFO eviction at their cadences.
 
 Precision: ``--dtype fp32`` (default) matches the reference learner
 (``learner.py:37-38`` computes in fp32): the hand-written kernels run split
@@ -42,6 +44,18 @@ data parallelism (``--batch-scope``):
 
 At N > 1 the run also measures the other scope (fp32) and prints both ``value_strong``
 and ``value_weak`` with the rows each rank computed (``per_rank_rows``).
+
+N > 1 diagnostics in the JSON: ``comm_world`` (the rank count the communicator itself
+reports), ``init_allreduce_ok`` (a checked all-reduce of rank + 1 through the DP step's
+collectives, = N (N + 1) / 2), ``dp_graphs`` (the DP step ran as captured HIP graphs;
+``graph_fallback`` names why not).  Every phase runs under a watchdog
+(``--phase-timeout``): a rank stuck in a collective exits non-zero naming its phase.
+
+``--emulate-world W`` (one GPU): rank 0's share of a W-rank global-batch step -- its
+rows, its 1/W fc optimizer slice and fc weight-gradient rows, the sharded replay draw
+-- with every collective a device copy of its true size (``parallel/rccl.py
+EmulatedCollectives``).  ``value`` is then that per-rank step's rate, the W-GPU update
+rate if RCCL's latency hides behind the compute; labelled ``emulated_world``.
 """
 from __future__ import annotations
 
@@ -100,7 +114,7 @@ def make_learner(args, dtype, device, comm, rank, replay, scope=None):
                     "seed": 1234 + rank, "network": args.network, "dtype": dtype,
                     "presample": not args.no_presample, "force_dp": args.force_dp, "comm_backend": args.comm,
                     "batch_scope": scope or args.batch_scope, "allreduce_dtype": args.allreduce_dtype,
-                    "dp_fc_exchange": args.dp_fc_exchange,
+                    "dp_fc_exchange": args.dp_fc_exchange, "dp_shard_update": args.dp_shard_update,
                     **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
     })
     if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
@@ -113,8 +127,13 @@ def make_learner(args, dtype, device, comm, rank, replay, scope=None):
     return cfg, FusedImpalaLearner(cfg, device, replay, comm=comm, backend=args.backend)
 
 
-def measure(cfg, learner, replay, comm, warmup: int, steps: int, prep_warm: int = 0) -> dict:
+def measure(cfg, learner, replay, comm, warmup: int, steps: int, prep_warm: int = 0, wd=None,
+            timeout: float = 0.0, tag: str = "") -> dict:
     L = cfg.Learner
+    from contextlib import nullcontext
+
+    def phase(name):
+        return wd.phase(tag + name, timeout) if wd is not None else nullcontext()
 
     def run(n):
         """n learner updates; the FIFO eviction + tree rebuild at its cadence runs
@@ -134,23 +153,29 @@ def measure(cfg, learner, replay, comm, warmup: int, steps: int, prep_warm: int 
                 if hasattr(learner, "refresh_replay_stats"):
                     learner.refresh_replay_stats()
 
-    run(warmup)
+    with phase("warmup"):
+        run(warmup)
+        torch.cuda.synchronize()
     # every graph the timed region replays, captured now (no learner updates)
-    caps = learner.prepare_graphs() if hasattr(learner, "prepare_graphs") else 0
-    if hasattr(learner, "rewarm"):
-        learner.rewarm(prep_warm)     # state-preserving: no update is kept
+    with phase("graph capture"):
+        caps = learner.prepare_graphs() if hasattr(learner, "prepare_graphs") else 0
+        if hasattr(learner, "rewarm"):
+            learner.rewarm(prep_warm)     # state-preserving: no update is kept
+        torch.cuda.synchronize()
     vr = getattr(learner, "valid_rows_total", None)
     if vr is not None:
         vr.zero_()                    # DP: rows each rank actually drew, counted by the head kernel
-    torch.cuda.synchronize()
-    comm.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(steps)
-    torch.cuda.synchronize()
-    comm.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    with phase("barrier before the timed steps"):
+        torch.cuda.synchronize()
+        comm.barrier()
+        torch.cuda.synchronize()
+    with phase("timed steps"):
+        t0 = time.perf_counter()
+        run(steps)
+        torch.cuda.synchronize()
+        comm.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
     dt = comm.allreduce_scalar(dt, "max") if comm.active else dt
     caps_after = getattr(learner, "graph_captures", 0)
     dp = bool(getattr(learner, "_dp", False)) and vr is not None
@@ -194,9 +219,9 @@ def parser() -> argparse.ArgumentParser:
                     help="sample at the head of each step instead of inside the previous step's optimizer launch")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collectives: nccl (= RCCL over xGMI) or gloo (rehearsing several ranks on one GPU)")
-    ap.add_argument("--comm", default="torch", choices=["torch", "native"],
-                    help="DP collectives: torch.distributed (RCCL process group) or the native RCCL "
-                         "communicator (csrc/comm/rccl_comm.cpp)")
+    ap.add_argument("--comm", default="native", choices=["torch", "native"],
+                    help="DP collectives: the native RCCL communicator (csrc/comm/rccl_comm.cpp; captured "
+                         "graphs) or torch.distributed (RCCL process group; eager DP steps)")
     ap.add_argument("--batch-scope", default="global", choices=["global", "per_rank"],
                     help="DP: global = one 512-sample update over all ranks (strong scaling, the reference's "
                          "update); per_rank = 512 rows per rank (weak scaling)")
@@ -216,6 +241,13 @@ def parser() -> argparse.ArgumentParser:
     ap.add_argument("--prep-warm", type=int, default=4,
                     help="untimed, state-preserving replays of the multi-step graph right before the timed "
                          "window (learner.rewarm: no update is kept; reported as prep_warm_replays)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one GPU: run rank 0's share of a W-rank global-batch DP step, collectives as device "
+                         "copies of their true sizes (reported as emulated_world)")
+    ap.add_argument("--dp-shard-update", default="auto", choices=["auto", "on", "off"],
+                    help="DP: shard the fc optimizer by output rows (Runtime.dp_shard_update)")
+    ap.add_argument("--phase-timeout", type=float, default=600.0,
+                    help="watchdog: seconds any bench phase may take before the rank exits non-zero")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
                     help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala_split.hip (fp32) / csrc/impala.hip (bf16)")
     return ap
@@ -224,21 +256,33 @@ def parser() -> argparse.ArgumentParser:
 def run(args) -> None:
 
     from apex_dqn_amd.ops.switches import SW
-    from apex_dqn_amd.parallel.dist import Comm
+    from apex_dqn_amd.parallel.dist import Comm, EmulatedComm
+    from apex_dqn_amd.runtime.watchdog import PhaseWatchdog
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
+    emu = int(args.emulate_world)
+    if emu and world > 1:
+        raise SystemExit("--emulate-world runs on one process")
+    wd = PhaseWatchdog(rank)
+    to = float(args.phase_timeout)
     # one rank per GPU; the modulo only matters when rehearsing several ranks on
     # fewer GPUs (device_count() does not initialise the GPU)
     dev_idx = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_idx)
     device = torch.device("cuda", dev_idx)
-    comm = Comm.from_env(backend=args.dist_backend, device=device, force=args.force_dp)
-
-    replay = make_replay(args, device, rank)
+    with wd.phase("process group init", to):
+        if emu:
+            comm = EmulatedComm(emu, 0, device)
+            args.force_dp = True
+        else:
+            comm = Comm.from_env(backend=args.dist_backend, device=device, force=args.force_dp)
+    wd.comm = comm
+    with wd.phase("replay prefill", to):
+        replay = make_replay(args, device, rank)
     dp = world > 1 or args.force_dp
     scope = args.batch_scope if dp else "global"
 
@@ -252,9 +296,17 @@ def run(args) -> None:
             return args.steps / r["dt"]
         return r["valid_rows"] / args.batch / r["dt"]
 
-    cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay, scope)
+    with wd.phase("learner init (comm init, parameter broadcast)", to):
+        cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay, scope)
     rows = learner.B
-    res = measure(cfg, learner, replay, comm, args.warmup, args.steps, args.prep_warm)
+    diag = {}
+    if dp and hasattr(learner, "comm_report"):
+        with wd.phase("checked init all-reduce", to):
+            diag = learner.comm_report()
+    res = measure(cfg, learner, replay, comm, args.warmup, args.steps, args.prep_warm, wd, to)
+    dp_graphs = bool(getattr(learner, "_dp", False)) and learner._graphs_enabled() if dp else None
+    fallback = getattr(learner, "graph_fallback", None)
+    shard = bool(getattr(learner, "_shard", False))
     other = None
     if world > 1 and not args.no_scope_extra:
         # the other batch scope, fp32: both scalings from one run
@@ -262,7 +314,8 @@ def run(args) -> None:
         del learner
         torch.cuda.empty_cache()
         cfg_o, learner_o = make_learner(args, args.dtype, device, comm, rank, replay, osc)
-        other = dict(measure(cfg_o, learner_o, replay, comm, args.warmup, args.steps, args.prep_warm),
+        other = dict(measure(cfg_o, learner_o, replay, comm, args.warmup, args.steps, args.prep_warm, wd, to,
+                             "other scope: "),
                      scope=osc, rows=learner_o.B)
         learner = learner_o
     extra = None
@@ -270,7 +323,7 @@ def run(args) -> None:
         del learner
         torch.cuda.empty_cache()
         cfg_b, learner_b = make_learner(args, "bf16", device, comm, rank, replay, scope)
-        extra = measure(cfg_b, learner_b, replay, comm, args.warmup, args.steps, args.prep_warm)
+        extra = measure(cfg_b, learner_b, replay, comm, args.warmup, args.steps, args.prep_warm, wd, to, "bf16: ")
         learner = learner_b
     dt = res["dt"]
     ms = 1e3 * dt / args.steps
@@ -284,7 +337,7 @@ def run(args) -> None:
         ops = getattr(learner, "ops", None)
         out = {
             "metric": METRIC,
-            "value": round(value, 2), "unit": "grad-steps/s (batch 512)", "n_gpus": world,
+            "value": round(value, 2), "unit": "grad-steps/s (batch 512)", "n_gpus": 1 if emu else world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
             "higher_is_better": True, "scaling": "strong" if scope == "global" else "weak",
             "vs_baseline": round(value / BASELINE_STEPS_PER_S, 2), "dtype": args.dtype, "data": "synthetic",
@@ -292,9 +345,10 @@ def run(args) -> None:
                                   if args.network == "nature64" else
                                   "dueling %s, 4x84x84, A=%d" % (args.network, args.actions)),
                        "global_batch": args.batch * (world if scope == "per_rank" else 1), "seq_len": 1,
-                       "parallelism": "dp%d" % world + ("-dp-step" if args.force_dp and world == 1 else ""),
+                       "parallelism": ("dp%d-emulated-rank0" % emu) if emu else
+                       ("dp%d" % world + ("-dp-step" if args.force_dp and world == 1 else "")),
                        "batch_scope": scope,
-                       "per_gpu_batch": args.batch if scope == "per_rank" else round(args.batch / world, 2),
+                       "per_gpu_batch": args.batch if scope == "per_rank" else round(args.batch / (emu or world), 2),
                        "per_rank_rows": rows,
                        "allreduce_dtype": args.allreduce_dtype if dp else None,
                        "dp_fc_exchange": ("factors" if getattr(learner, "_fc_factors", False) else "allreduce")
@@ -302,7 +356,9 @@ def run(args) -> None:
                        "replay_per_gpu": args.replay,
                        "learner": kind + ("/" + ops.name if ops is not None and args.learner == "fused" else
                                           "/torch-autograd"),
-                       "dp_collectives": args.comm if (world > 1 or args.force_dp) else None,
+                       "dp_collectives": getattr(getattr(learner, "coll", None), "name", None)
+                       if (world > 1 or args.force_dp) else None,
+                       "dp_shard_update": shard if dp else None,
                        "hip_graphs": not args.no_graphs},
             "math": ("fp32 master weights, gradients and optimizer; GEMM operands as bf16 hi + lo "
                      "(hi*hi + lo*hi + hi*lo MFMAs, fp32 accumulation)" if args.dtype == "fp32"
@@ -316,7 +372,17 @@ def run(args) -> None:
             "loss": round(m["loss"], 5), "grad_norm": round(m["grad_norm"], 5),
             "is_weight_mean": round(m.get("is_weight_mean", float("nan")), 5),
         }
-        if samples_per_step is not None:
+        if dp:
+            out["dp_graphs"] = dp_graphs
+            out["graph_fallback"] = fallback
+            out.update(diag)
+        if emu:
+            out["emulated_world"] = emu
+            out["emulation"] = ("rank 0 of a %d-rank global-batch step on one GPU; collectives are device copies "
+                                "of their true sizes (RCCL latency / xGMI time not included)" % emu)
+        if samples_per_step is not None and emu:
+            out["rank0_rows_drawn_per_step"] = round(samples_per_step, 2)
+        elif samples_per_step is not None:
             out["samples_per_dp_step"] = round(samples_per_step, 2)
             out["value_nominal"] = round(args.steps / dt * world, 2)
             out["value_" + ("strong" if scope == "global" else "weak")] = round(value, 2)
@@ -332,7 +398,9 @@ def run(args) -> None:
             out["ms_per_step_bf16"] = round(1e3 * extra["dt"] / args.steps, 4)
             out["graph_captures_in_timed_bf16"] = extra["graph_captures_in_timed"]
         print(json.dumps(out), flush=True)
-    comm.shutdown()
+    with wd.phase("shutdown", to):
+        comm.shutdown()
+    wd.close()
 
 
 if __name__ == "__main__":

@@ -69,9 +69,18 @@ def _worker(rank, world, path, q, ar="fp32"):
     g_dp = L.g32.clone()
     for _ in range(3):
         L.step()
+    L.materialize()              # sharded fc update (learner/dp_step.py): gather the fp32 rows
     gl = [torch.zeros_like(g_local) for _ in range(world)]
     torch.distributed.all_gather(gl, g_local)
     g_mean = torch.stack(gl).mean(0)
+    if L._shard:                 # the gradient rows this rank computed: conv + head, its fc rows
+        keep = torch.zeros_like(g_dp, dtype=torch.bool)
+        off = L.layout.offsets
+        keep[:off["wfc"]] = True
+        o = off["wfc"] + L._fc_r0 * 3136
+        keep[o:o + L._fc_S * 3136] = True
+        keep[off["bfc"] + L._fc_r0:off["bfc"] + L._fc_r0 + L._fc_S] = True
+        g_dp, g_mean = g_dp[keep], g_mean[keep]
     pl = [torch.zeros_like(L.p32) for _ in range(world)]
     torch.distributed.all_gather(pl, L.p32.clone())
     perr = max([float((pl[0] - p).abs().max()) for p in pl[1:]], default=0.0)

@@ -22,12 +22,25 @@ CAP, FR = 300, 400
 BG, STEPS = 16, 3
 
 
-def _cfg(slack, exchange="auto", seed=0):
+def _cfg(slack, exchange="auto", seed=0, shard="auto"):
     return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
                                  "Learner": {"replay_sample_size": BG, "q_target_sync_freq": 2},
                                  "Runtime": {"use_graphs": False, "grad_clip": 40.0, "force_dp": True, "seed": seed,
                                              "batch_scope": "global", "dp_batch_slack": slack,
-                                             "dp_fc_exchange": exchange}})
+                                             "dp_fc_exchange": exchange, "dp_shard_update": shard}})
+
+
+def _computed(L):
+    """Mask of the gradient entries this rank computes: all of them, or with the sharded
+    update (learner/dp_step.py) the conv + head range and its own fc rows."""
+    m = np.ones(L.g32.numel(), bool)
+    if L._shard:
+        off = L.layout.offsets
+        m[off["wfc"]:] = False
+        o = off["wfc"] + L._fc_r0 * 3136
+        m[o:o + L._fc_S * 3136] = True
+        m[off["bfc"] + L._fc_r0:off["bfc"] + L._fc_r0 + L._fc_S] = True
+    return m
 
 
 def _shard(rank):
@@ -58,7 +71,7 @@ def _concat(world):
     return rp
 
 
-def _worker(rank, world, concat, slack, path, q, exchange="auto"):
+def _worker(rank, world, concat, slack, path, q, exchange="auto", shard="auto"):
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.parallel.dist import Comm
     torch.set_num_threads(2)
@@ -66,8 +79,10 @@ def _worker(rank, world, concat, slack, path, q, exchange="auto"):
     torch.manual_seed(1234)          # identical initial parameters in every run
     rp = _concat(concat) if concat else _shard(rank)
     # per-rank Runtime.seed (as bench.py sets it): the draw's seed is rank 0's on every rank
-    L = FusedNatureLearner(_cfg(slack, exchange, seed=7 * rank), "cpu", rp, comm=comm)
+    L = FusedNatureLearner(_cfg(slack, exchange, seed=7 * rank, shard=shard), "cpu", rp, comm=comm)
     assert L._fc_factors == (exchange != "allreduce")
+    assert L._shard == (world > 1 and shard != "off")
+    mask = _computed(L)
     draws, grads = [], []
     p0 = L.p32.numpy().copy()
     for _ in range(STEPS):
@@ -76,17 +91,18 @@ def _worker(rank, world, concat, slack, path, q, exchange="auto"):
         # global leaf id of every row this rank drew (the concatenated replay's numbering)
         draws.append((L.S["idx"][valid] + (0 if concat else rank * CAP)).tolist())
         L.step()
-        grads.append(L.g32.numpy().copy())
+        grads.append(np.where(mask, L.g32.numpy(), np.nan))
+    L.materialize()              # (sharded: every rank's fp32 rows gathered)
     q.put((rank, L.B, int(L.valid_rows_total.item()), draws, grads, L.p32.numpy().copy(), L.t32.numpy().copy(), p0))
     comm.shutdown()
 
 
-def _run(world, concat, slack, exchange="auto"):
+def _run(world, concat, slack, exchange="auto", shard="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "store")
-        procs = [ctx.Process(target=_worker, args=(r, world, concat, slack, path, q, exchange)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, concat, slack, path, q, exchange, shard)) for r in range(world)]
         for p in procs:
             p.start()
         res = [q.get(timeout=300) for _ in range(world)]
@@ -105,12 +121,15 @@ def test_dp_batch_rows():
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("world,exchange", [(2, "factors"), (4, "factors"), (2, "allreduce")])
-def test_global_batch_dp_equals_one_rank(world, exchange):
+@pytest.mark.parametrize("world,exchange,shard", [(2, "factors", "auto"), (4, "factors", "auto"),
+                                                  (2, "allreduce", "auto"), (4, "allreduce", "auto"),
+                                                  (2, "factors", "off"), (2, "allreduce", "off")])
+def test_global_batch_dp_equals_one_rank(world, exchange, shard):
     """``exchange``: the fc gradient as all-gathered factor rows (every rank forms the
-    global batch's gradient) or all-reduced -- both equal the one-rank update."""
+    global batch's gradient, or with the sharded update its own fc rows) or all-reduced
+    (sharded: reduce-scattered) -- every variant equals the one-rank update."""
     slack = 1.0
-    multi = _run(world, 0, slack, exchange)
+    multi = _run(world, 0, slack, exchange, shard)
     one = _run(1, world, slack, "allreduce")[0]
     rows = multi[0][1]
     assert rows == int(np.ceil(BG / world * (1 + slack))) + 2 and one[1] == BG
@@ -123,7 +142,8 @@ def test_global_batch_dp_equals_one_rank(world, exchange):
     for r in multi:
         for s in range(STEPS):
             g1, gw = one[4][s], r[4][s]
-            assert np.abs(gw - g1).max() <= 2e-6 * np.abs(g1).max() + 1e-10, s
+            m = ~np.isnan(gw)
+            assert np.abs(gw[m] - g1[m]).max() <= 2e-6 * np.abs(g1).max() + 1e-10, s
         # parameters: RMSprop divides by sqrt(centered variance), which amplifies the
         # summation-order round-off of the first updates a little
         upd = np.abs(one[5] - one[7]).max()

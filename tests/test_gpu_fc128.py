@@ -3,8 +3,7 @@ fc_splitk_epilogue_kernel, ``ops.conv.dense_fwd128``) against an fp64 reference 
 same op: online rows [0, r) on the first weight set, target rows [r, M) on the second,
 bias + ReLU, in bf16 and in split (hi / lo planes, fp32-accurate) mode, for every K
 split and with / without the loader waves; a row count that is not a tile multiple
-exercises the clamped rows.  Negative ``ksplit``: the stream-K split over that many
-workgroups (csrc/fc_sk.h: per-tile partial-plane counts).  Also the step's default path (the fused learner's
+exercises the clamped rows.  Also the step's default path (the fused learner's
 ``fc_fwd`` routes here) against the 64x64-tile kernel it replaced."""
 import pytest
 import torch
@@ -19,8 +18,7 @@ def _sp(t):
 
 
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("ksplit,lw", [(1, False), (2, True), (3, True), (4, False), (49, True),
-                                       (-256, True), (-37, True), (-200, False)])
+@pytest.mark.parametrize("ksplit,lw", [(1, False), (2, True), (3, True), (4, False), (10, True), (49, True)])
 def test_fc128_matches_fp64(split, ksplit, lw):
     from apex_dqn_amd.ops import _lib as L, conv as C
     lib = L.require_kernels()

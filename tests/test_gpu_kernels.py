@@ -501,33 +501,3 @@ def test_branched_backward_matches_serial(monkeypatch, dtype):
     for a, b in zip(res[False], res[True]):
         assert torch.equal(a, b)
 
-
-@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_deferred_fc_update_bit_identical(monkeypatch, dtype):
-    """SW.opt_overlap: inside a multi-update graph the fc layer's RMSprop update runs on its
-    own stream beside the next update's conv forward (csrc/sumtree.hip apex_rmsprop_range,
-    the same launch shape as the fused optimizer + sample launch): 10 updates of the
-    4-update graph path across two target syncs are bit-identical to the one-launch
-    optimizer."""
-    from apex_dqn_amd.config import ApexConfig
-    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
-    from apex_dqn_amd.ops.switches import SW
-    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
-    res = {}
-    for ov in (False, True):
-        monkeypatch.setattr(SW, "opt_overlap", ov)
-        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
-                                    "Learner": {"replay_sample_size": 128, "q_target_sync_freq": 4},
-                                    "Runtime": {"use_graphs": True, "graph_steps": 4, "dtype": dtype}})
-        torch.manual_seed(0)
-        rp = GpuReplayShard(4000, 4000, 4100, 4, device=DEV, seed=3)
-        _fill_replay(rp, 3800, seed=1)
-        L = FusedNatureLearner(cfg, DEV, rp, backend="hip")
-        assert (L._opt_stream is not None) == ov    # (off by default: slower)
-        L.steps(10)
-        torch.cuda.synchronize()
-        res[ov] = (L.g32.clone(), L.p32.clone(), L.t32.clone(), L.rms_v.clone(), L.rms_m.clone(),
-                   L._pbf_all.clone() if hasattr(L, "_pbf_all") else L.pbf.clone(), rp.leaf.clone(),
-                   L.S["idx"].clone())
-    for a, b in zip(res[False], res[True]):
-        assert torch.equal(a, b)

@@ -105,6 +105,8 @@ def _dp_gpu_worker(rank, world, path, q, exchange="auto"):
         drawn.append((int((L.S["weights"] > 0).sum()), int((L.S["gen"] >= 0).sum())))
         L.step()
     torch.cuda.synchronize()
+    assert L._shard                     # (the fc optimizer sharded by rows: gather the fp32 rows)
+    L.materialize()
     pl = [torch.zeros_like(L.p32) for _ in range(world)]
     torch.distributed.all_gather(pl, L.p32.clone())
     ok_finite = bool(torch.isfinite(L.p32).all())
@@ -590,28 +592,55 @@ def test_staged_frame_append_matches_copy():
     assert torch.equal(a.frames, b.frames)
 
 
-def _inline_last_worker(q, port):
-    """Forced DP on the native communicator (world 1, captured 4-update graphs): the same
-    updates with conv1's bucket forked to the comm stream and all-reduced inline."""
+def _get_or_dead(q, p, timeout: float):
+    """The child's result, failing at once (instead of after ``timeout``) if it died."""
+    import queue
+    import time
+    t_end = time.time() + timeout
+    while time.time() < t_end:
+        try:
+            return q.get(timeout=2)
+        except queue.Empty:
+            if not p.is_alive():
+                raise AssertionError(f"worker died with exit code {p.exitcode}")
+    raise AssertionError("worker timed out")
+
+
+def _dp_variants_worker(q, port):
+    """Forced DP at world 1 (RCCL process group of one rank; captured 4-update graphs):
+    the same 8 updates through every DP-step variant -- torch.distributed vs the native
+    communicator (whose conv1 bucket is all-reduced inline), factored vs all-reduced fc
+    exchange, the sharded fc optimizer on / off (learner/dp_step.py), and a DP graph
+    capture that fails (injected) and falls back to the eager DP step."""
+    import faulthandler
     import os
+    faulthandler.enable()
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0")
     import numpy as np
     import torch
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
-    from apex_dqn_amd.ops.switches import SW
     from apex_dqn_amd.parallel.dist import Comm
     from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     comm = Comm.from_env(device=dev, force=True)
+    variants = {
+        "torch_factors": ("torch", "factors", "off", False),
+        "native_factors": ("native", "factors", "off", False),
+        "native_factors_shard": ("native", "factors", "on", False),
+        "torch_factors_shard": ("torch", "factors", "on", False),
+        "native_factors_shard_fallback": ("native", "factors", "on", True),
+        "torch_allreduce": ("torch", "allreduce", "off", False),
+        "torch_allreduce_shard": ("torch", "allreduce", "on", False),
+    }
     out = {}
-    for inline in (False, True):
-        SW.dp_inline_last = inline
+    for name, (cb, ex, sh, inject) in variants.items():
         cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},
-                                    "Learner": {"replay_sample_size": 256},
+                                    "Learner": {"replay_sample_size": 256, "q_target_sync_freq": 6},
                                     "Runtime": {"use_graphs": True, "graph_steps": 4, "presample": True,
-                                                "force_dp": True, "comm_backend": "native"}})
+                                                "force_dp": True, "comm_backend": cb, "dp_fc_exchange": ex,
+                                                "dp_shard_update": sh}})
         rp = GpuReplayShard(4000, 4000, 4100, 4, device=dev, seed=0x5EED)
         rng = np.random.default_rng(9)
         seqs = rp.append_frames(rng.integers(0, 255, (3000, 84, 84), dtype=np.uint8))
@@ -621,27 +650,88 @@ def _inline_last_worker(q, port):
                        Gamma=np.full(K, 0.97, np.float32), priority=rng.random(K).astype(np.float32) + 0.01))
         torch.manual_seed(3)
         L = FusedNatureLearner(cfg, dev, rp, comm=comm)
-        assert L._dp and L.coll.name == "native"
+        assert L._dp and L.coll.name == cb and L._shard == (sh == "on") and L._fc_factors == (ex == "factors")
+        L._inject_capture_failure = inject
         L.steps(8)
         torch.cuda.synchronize()
-        out[inline] = L.p32.cpu()
-    SW.dp_inline_last = False
+        L.materialize()
+        rep = L.comm_report()
+        out[name] = dict(p=L.p32.cpu(), v=L.rms_v.cpu(), t=L.t32.cpu(), pb=L._pbf_all.cpu(), leaf=rp.leaf.cpu(),
+                         graphs=L._graphs_enabled(), fallback=L.graph_fallback, rep=rep)
     comm._native.check()
     comm.shutdown()
-    q.put((bool(torch.equal(out[False], out[True])), float((out[False] - out[True]).abs().max())))
+    same = lambda a, b: all(torch.equal(out[a][k], out[b][k]) for k in ("p", "v", "t", "pb", "leaf"))  # noqa: E731
+    res = {
+        "torch==native": same("torch_factors", "native_factors"),
+        "shard==unsharded": same("native_factors", "native_factors_shard"),
+        "torch shard==native shard": same("torch_factors_shard", "native_factors_shard"),
+        "fallback==graphs": same("native_factors_shard_fallback", "native_factors_shard"),
+        "allreduce shard~unsharded": float((out["torch_allreduce"]["p"] - out["torch_allreduce_shard"]["p"]).abs().max()),
+        "graphs": {k: v["graphs"] for k, v in out.items()},
+        "fallback": {k: v["fallback"] for k, v in out.items()},
+        "rep": {k: v["rep"] for k, v in out.items()},
+    }
+    q.put(res)
 
 
 @pytest.mark.gpu
-def test_dp_inline_last_bucket_bit_identical():
-    """SW.dp_inline_last (conv1's bucket all-reduced on the main stream after one join of
-    the comm stream) takes the same updates as the forked bucket, inside captured graphs."""
+def test_dp_step_variants_bit_identical():
+    """Every DP-step variant takes the same updates at world 1 (see _dp_variants_worker);
+    the sharded all-reduce exchange differs only in the clip norm's summation order.  The
+    injected capture failure leaves that learner on the eager DP step (graph_fallback set,
+    graphs off) with updates identical to the captured ones; the communicator reports one
+    rank and the checked all-reduce of rank + 1 gives 1."""
     import random
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_inline_last_worker, args=(q, 29600 + random.randint(301, 600)))
+    p = ctx.Process(target=_dp_variants_worker, args=(q, 29600 + random.randint(301, 600)))
     p.start()
-    same, diff = q.get(timeout=240)
+    res = _get_or_dead(q, p, 400)
     p.join(timeout=60)
     assert p.exitcode == 0
-    assert same, diff
+    for k in ("torch==native", "shard==unsharded", "torch shard==native shard", "fallback==graphs"):
+        assert res[k] is True, (k, res)
+    assert res["allreduce shard~unsharded"] < 1e-6, res
+    for name, g in res["graphs"].items():
+        # torch.distributed runs eager DP steps (fused_learner: _dp_graphs)
+        assert g == (not name.endswith("fallback") and name.startswith("native")), (name, res)
+        assert (res["fallback"][name] is not None) == name.endswith("fallback"), (name, res)
+    for name, r in res["rep"].items():
+        assert r["comm_world"] == 1 and r["init_allreduce_ok"], (name, r)
+
+
+@pytest.mark.gpu
+def test_emulated_world_step_runs_sharded():
+    """bench.py --emulate-world: rank 0's share of an 8-rank global-batch step on one GPU
+    (parallel/rccl.py EmulatedCollectives) -- 74-row buffers, the sharded fc update over
+    rows [0, 128), captured graphs, finite updates, about 512 / 8 rows drawn per update."""
+    import numpy as np
+    from apex_dqn_amd.config import ApexConfig
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.parallel.dist import EmulatedComm
+    from apex_dqn_amd.replay.gpu_replay import GpuReplayShard
+    dev = torch.device("cuda", 0)
+    for dtype in ("fp32", "bf16"):
+        cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 4, "name": "Synthetic"},
+                                    "Learner": {"replay_sample_size": 512},
+                                    "Runtime": {"use_graphs": True, "graph_steps": 5, "dtype": dtype}})
+        rp = GpuReplayShard(8000, 8000, 8100, 4, device=dev, seed=1)
+        rng = np.random.default_rng(2)
+        seqs = rp.append_frames(rng.integers(0, 255, (7000, 84, 84), dtype=np.uint8))
+        K = 6000
+        st = np.stack([seqs[i:i + 4] for i in range(K)])
+        rp.insert(dict(S_t=st, S_tpn=st + 3, A_t=rng.integers(0, 4, K), R=rng.normal(size=K).astype(np.float32),
+                       Gamma=np.full(K, 0.97, np.float32), priority=rng.random(K).astype(np.float32) + 0.01))
+        L = FusedNatureLearner(cfg, dev, rp, comm=EmulatedComm(8, 0, dev))
+        assert L._dp and L.B == 74 and L._shard and L._fc_S == 128 and L.coll.name == "emulated"
+        assert L.comm_report()["init_allreduce_ok"]
+        L.prepare_graphs()         # (its warm replays count rows too: state-preserving otherwise)
+        p0 = L.p32.clone()
+        L.valid_rows_total.zero_()
+        L.steps(10)
+        torch.cuda.synchronize()
+        assert L._graphs_enabled() and L.graph_captures >= 1
+        assert torch.isfinite(L.p32).all() and not torch.equal(L.p32, p0)
+        rows = int(L.valid_rows_total.item()) / 10
+        assert 40 <= rows <= 74, rows
