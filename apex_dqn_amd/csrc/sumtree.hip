@@ -424,6 +424,37 @@ __global__ void tree_reduce_level_kernel(const float* __restrict__ leaf, const d
   }
 }
 
+// The leaf level of the exact rebuild: parents grid-strided over a bounded grid, the
+// min over positive leaves kept per lane and reduced once per block -- one atomicMin per
+// block instead of one per parent (at 2.5 M leaves the per-parent atomics on the single
+// min word serialised the rebuild: 0.38 ms, profiles/r5_replay_2m.json).
+__global__ void __launch_bounds__(256) tree_reduce_leaf_kernel(const float* __restrict__ leaf, int64_t nsrc,
+                                                               double* __restrict__ dst, int64_t ndst,
+                                                               uint32_t* min_bits) {
+  __shared__ float wmin[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  float mn = __uint_as_float(0x7f800000u);
+  for (int64_t p = (int64_t)blockIdx.x * 4 + w; p < ndst; p += nw) {
+    const int64_t c = p * 64 + lane;
+    double v = 0.0;
+    if (c < nsrc) {
+      const float f = leaf[c];
+      v = (double)f;
+      if (f > 0.f) mn = fminf(mn, f);
+    }
+    v = wave_sum(v);
+    if (lane == 0) dst[p] = v;
+  }
+  mn = wave_min(mn);
+  if (lane == 0) wmin[w] = mn;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fminf(fminf(wmin[0], wmin[1]), fminf(wmin[2], wmin[3]));
+    if (m < __uint_as_float(0x7f800000u)) atomicMin(min_bits, __float_as_uint(m));
+  }
+}
+
 __global__ void fill_u32_kernel(uint32_t* p, uint32_t v, int64_t n) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -671,9 +702,14 @@ APEX_EXPORT int apex_tree_rebuild(TreeDesc t, hipStream_t st) {
   for (int k = 1; k <= t.L; ++k) {
     int64_t nd = t.n[k];
     const int wpb = 4;
+    if (k == 1) {
+      const int nb = blocks_for(nd, wpb);
+      tree_reduce_leaf_kernel<<<nb < 512 ? nb : 512, 64 * wpb, 0, st>>>(t.leaf, t.n[0], t.nodes + t.off[1], nd,
+                                                                       t.min_bits);
+      continue;
+    }
     tree_reduce_level_kernel<<<blocks_for(nd, wpb), 64 * wpb, 0, st>>>(
-        k == 1 ? t.leaf : nullptr, k == 1 ? nullptr : t.nodes + t.off[k - 1], t.n[k - 1],
-        t.nodes + t.off[k], nd, t.min_bits);
+        nullptr, t.nodes + t.off[k - 1], t.n[k - 1], t.nodes + t.off[k], nd, t.min_bits);
   }
   APEX_CHECK_LAUNCH();
 }

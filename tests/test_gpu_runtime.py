@@ -377,6 +377,12 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert out["samples_per_dp_step"] == 512.0 and out["value"] == out["value_strong"] > 0
     assert out["value_weak"] > 0 and out["per_rank_rows_weak"] == 512 and out["samples_per_dp_step_weak"] > 512
     assert out["graph_captures_in_timed"] == 0
+    # what the collectives themselves report: the process group's rank count, the checked
+    # all-reduce of rank + 1 (1 + 2 = 3), and whether the DP step ran as captured graphs
+    # (gloo: eager by design) -- the fields the driver's first N-GPU run is judged by
+    assert out["comm_world"] == 2 and out["init_allreduce"] == 3.0 and out["init_allreduce_ok"] is True
+    assert out["dp_graphs"] is False and out["graph_fallback"] is None
+    assert out["config"]["dp_collectives"] == "torch" and out["config"]["dp_shard_update"] is True
 
 
 def _native_rccl_worker(q, port):
