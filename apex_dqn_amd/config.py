@@ -131,6 +131,9 @@ class RuntimeConf:
                                     # batch on each rank: ~(B_total x 4160) values instead of 3.2 M, exact and
                                     # bit-identical across ranks) | "auto" (factors while 1 < W and W x rows
                                     # <= 1024)
+    dp_rows_adaptive: bool = True   # global scope: grow the per-rank rows (and recapture the step) when a
+                                    # shard's share of the priority mass outgrows them, checked at init and
+                                    # at every eviction (learner/dp_step.py _fit_rows), so M stays B
     dp_shard_update: str = "auto"   # DP: the fc layer's optimizer (96 % of the parameters) sharded by output rows
                                     # over the ranks, the updated rows all-gathered (learner/dp_step.py):
                                     # "on" | "off" | "auto" (on at world > 1 when 1024 / (64 W) is whole)

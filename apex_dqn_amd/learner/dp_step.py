@@ -134,6 +134,61 @@ class DataParallelStep:
         if W * nfc + 64 > self.norm_part.numel():
             raise ValueError(f"norm partials: {W} x {nfc} + 64 slots exceed norm_part")
 
+    def _alloc_factors(self) -> None:
+        """The factored exchange's row buffer: W x rows of [dH | dH lo | X | X lo]; this rank
+        packs into its own block (the all-gather runs in place)."""
+        ncol = sum(self._fx_cols)
+        self.fx_recv = torch.zeros(self.world * self.B, ncol, dtype=self.act_dtype, device=self.device)
+        r = self.comm.rank
+        self.fx_send = self.fx_recv[r * self.B:(r + 1) * self.B]
+
+    # ---------------------------------------------------- adaptive row buffer
+    def rows_needed(self, stats=None) -> int:
+        """Global batch scope: the fewest rows per rank with which the next global draw
+        takes all ``mcap`` samples -- the draw's M = min(mcap, floor((rows - 2) sum T / max T))
+        (replay/gpu_replay.py ``global_draw``, csrc/sumtree.hip) -- for the gathered shard
+        masses T (a host read of the statistics)."""
+        from ..replay.gpu_replay import SHARD_STATS
+        st = self.replay.shard_stats if stats is None else stats
+        T = st.double().reshape(self.world, SHARD_STATS)[:, 0].cpu().numpy()
+        sm, tmax = float(T.sum()), float(T.max())
+        if not (tmax > 0.0):
+            return 0
+        import math
+        r = int(math.ceil(self.mcap * tmax / sm)) + 2
+        while math.floor((r - 2) * sm / tmax) < self.mcap:      # (the kernel's exact rounding)
+            r += 1
+        return r
+
+    def _fit_rows(self) -> bool:
+        """Grow the per-rank row buffer when a shard's share of the priority mass would make
+        the global draw shrink below ``replay_sample_size`` (``Runtime.dp_rows_adaptive``;
+        the default buffer holds B / W (1 + dp_batch_slack) + 2 rows).  Every rank reads the
+        same gathered statistics, so every rank picks the same size; the new size keeps
+        the configured slack above the current need.  Buffers are reallocated and the HIP
+        graphs recaptured (a rare, host-side event at the eviction cadence).  Returns
+        whether the buffer grew."""
+        if not (self._dp and self.world > 1 and self.rt.batch_scope == "global" and self.rt.dp_rows_adaptive):
+            return False
+        need = self.rows_needed()
+        if need <= self.B:
+            return False
+        import math
+        grow = int(math.ceil((need - 2) * (1.0 + float(self.rt.dp_batch_slack)))) + 2
+        self._resize_rows(max(need, min(grow, self.mcap + 2)))
+        return True
+
+    def _resize_rows(self, rows: int) -> None:
+        self.B = int(rows)
+        self._alloc(self.B)
+        if self._fc_factors:
+            self._alloc_factors()
+        self._graphs = self._multi = None
+        self._graphs_warm = False
+        self._params_pending = None
+        self._sample_ver = None
+        self.rows_resized = getattr(self, "rows_resized", 0) + 1
+
     def _fc_rows(self, flat: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         """(whole fc weight range, this rank's rows) of a flat-layout tensor."""
         o = self.layout.offsets["wfc"]

@@ -190,10 +190,7 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         if self._fc_factors:
             planes = 2 if self.split else 1
             self._fx_cols = [1024] * planes + [3136] * planes      # [dH | dH lo | X | X lo]
-            ncol = sum(self._fx_cols)
-            self.fx_recv = torch.zeros(self.world * self.B, ncol, dtype=self.act_dtype, device=d)
-            r = comm.rank
-            self.fx_send = self.fx_recv[r * self.B:(r + 1) * self.B]    # (the all-gather runs in place)
+            self._alloc_factors()
         # producer-summed clip norm: the fc wgrad epilogue and the grad_finalize blocks
         # write squared-norm partials of the values they store, the optimizer launch sums
         # them.  With DP the norm is of the all-reduced gradient: the optimizer's own pass.
@@ -257,6 +254,7 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         self._presample = bool(self.rt.presample)
         self._sample_ver = None
         self._setup_frag_out()
+        self._fit_rows()          # global batch: rows for the largest shard's share (dp_step.py)
         ls = cfg.Learner.load_saved_state
         if ls:
             self.load(ls)
@@ -858,9 +856,11 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
 
     def refresh_replay_stats(self) -> None:
         """Re-gather the shard statistics (after host-side inserts / eviction; a
-        collective: every rank calls it at the same point)."""
+        collective: every rank calls it at the same point), and grow the per-rank rows if
+        a shard's share of the mass outgrew them (:meth:`_fit_rows`)."""
         if self._dp:
             self.replay.gather_shard_stats(coll=self.coll)
+            self._fit_rows()
 
     def _snapshot(self):
         rp = self.replay

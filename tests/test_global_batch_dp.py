@@ -22,12 +22,13 @@ CAP, FR = 300, 400
 BG, STEPS = 16, 3
 
 
-def _cfg(slack, exchange="auto", seed=0, shard="auto"):
+def _cfg(slack, exchange="auto", seed=0, shard="auto", adaptive=True):
     return ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 5, "name": "Synthetic"},
                                  "Learner": {"replay_sample_size": BG, "q_target_sync_freq": 2},
                                  "Runtime": {"use_graphs": False, "grad_clip": 40.0, "force_dp": True, "seed": seed,
                                              "batch_scope": "global", "dp_batch_slack": slack,
-                                             "dp_fc_exchange": exchange, "dp_shard_update": shard}})
+                                             "dp_fc_exchange": exchange, "dp_shard_update": shard,
+                                             "dp_rows_adaptive": adaptive}})
 
 
 def _computed(L):
@@ -71,7 +72,7 @@ def _concat(world):
     return rp
 
 
-def _worker(rank, world, concat, slack, path, q, exchange="auto", shard="auto"):
+def _worker(rank, world, concat, slack, path, q, exchange="auto", shard="auto", adaptive=True):
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     from apex_dqn_amd.parallel.dist import Comm
     torch.set_num_threads(2)
@@ -79,13 +80,16 @@ def _worker(rank, world, concat, slack, path, q, exchange="auto", shard="auto"):
     torch.manual_seed(1234)          # identical initial parameters in every run
     rp = _concat(concat) if concat else _shard(rank)
     # per-rank Runtime.seed (as bench.py sets it): the draw's seed is rank 0's on every rank
-    L = FusedNatureLearner(_cfg(slack, exchange, seed=7 * rank, shard=shard), "cpu", rp, comm=comm)
+    L = FusedNatureLearner(_cfg(slack, exchange, seed=7 * rank, shard=shard, adaptive=adaptive), "cpu", rp,
+                           comm=comm)
     assert L._fc_factors == (exchange != "allreduce")
     assert L._shard == (world > 1 and shard != "off")
     mask = _computed(L)
     draws, grads = [], []
     p0 = L.p32.numpy().copy()
     for _ in range(STEPS):
+        if adaptive:
+            L.refresh_replay_stats()     # (the loop's eviction-cadence check, here every update)
         L._sample()
         valid = L.S["gen"] >= 0
         # global leaf id of every row this rank drew (the concatenated replay's numbering)
@@ -97,12 +101,12 @@ def _worker(rank, world, concat, slack, path, q, exchange="auto", shard="auto"):
     comm.shutdown()
 
 
-def _run(world, concat, slack, exchange="auto", shard="auto"):
+def _run(world, concat, slack, exchange="auto", shard="auto", adaptive=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "store")
-        procs = [ctx.Process(target=_worker, args=(r, world, concat, slack, path, q, exchange, shard)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, concat, slack, path, q, exchange, shard, adaptive)) for r in range(world)]
         for p in procs:
             p.start()
         res = [q.get(timeout=300) for _ in range(world)]
@@ -151,3 +155,25 @@ def test_global_batch_dp_equals_one_rank(world, exchange, shard):
         assert dp <= 1e-3 * upd, (dp, upd)
         assert np.array_equal(r[5], multi[0][5])            # replicas bit-identical
         assert np.abs(r[6] - one[6]).max() <= 1e-3 * upd
+
+
+@pytest.mark.slow
+def test_default_slack_adaptive_rows_keep_the_global_batch():
+    """At the default slack (0.125) a 2-rank buffer holds 11 rows, enough while no shard
+    carries more than 9 / 16 of the priority mass; the priority write-backs push rank 1's
+    share past that.  Without the adaptive buffer the draw shrinks (M < 16, a different
+    update); with it (``Runtime.dp_rows_adaptive``, learner/dp_step.py; checked here before
+    every update, in the loops at the eviction cadence) both ranks grow to the same larger
+    buffer and the updates equal the one-rank update over the concatenated replay."""
+    fixed = _run(2, 0, 0.125, "factors", "auto", adaptive=False)
+    assert fixed[0][1] == 11 and sum(r[2] for r in fixed) < STEPS * BG      # the draw shrank
+    multi = _run(2, 0, 0.125, "factors", "auto", adaptive=True)
+    one = _run(1, 2, 0.125, "allreduce")[0]
+    rows = multi[0][1]
+    assert rows > 11 and multi[1][1] == rows
+    assert sum(r[2] for r in multi) == STEPS * BG == one[2]
+    for s in range(STEPS):
+        assert [i for r in multi for i in r[3][s]] == one[3][s]
+    upd = np.abs(one[5] - one[7]).max()
+    for r in multi:
+        assert np.abs(r[5] - one[5]).max() <= 1e-3 * upd
