@@ -222,23 +222,25 @@ class DataParallelStep:
                 segs = [self.dH, self.dH_lo, self.y3[:B].reshape(B, FC_COLS), self.y3_lo[:B].reshape(B, FC_COLS)] \
                     if sp else [self.dH, self.y3[:B].reshape(B, FC_COLS)]
                 ops.pack_rows(self.fx_send, segs)
-                works["fc"] = coll.all_gather_into(self.fx_recv, self.fx_send)
             else:
                 ops.fc_head_wgrad(self.dH, self.y3[:B], G["wfc"], G["bfc"], self.h, self.dhead, G, prio,
                                   **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B], Hon_lo=self.h_lo))
-                if shard:
+                if self._comm_bf16 and not shard:
+                    self.gcomm[cut:].copy_(self.g32[cut:])
+            # (the HIP priority write-back kernel has left this shard's sum / min in its slot)
+            fresh = self.ops.name == "hip" and getattr(self.replay, "use_hip", False)
+            with coll.fused():        # (RCCL: one launch for the fc exchange + the statistics)
+                if factors:
+                    works["fc"] = coll.all_gather_into(self.fx_recv, self.fx_send)
+                elif shard:
                     # reduce-scatter: this rank's fc rows (in place) and bias entries
                     w_all, w_own = self._fc_rows(self.g32)
                     b_all, b_own = self._fc_bias(self.g32)
                     coll.reduce_scatter_into(w_own, w_all)
                     works["fc"] = coll.reduce_scatter_into(b_own, b_all)
                 else:
-                    if self._comm_bf16:
-                        self.gcomm[cut:].copy_(self.g32[cut:])
                     works["fc"] = coll.all_reduce(self.gcomm[cut:])
-            # (the HIP priority write-back kernel has left this shard's sum / min in its slot)
-            fresh = self.ops.name == "hip" and getattr(self.replay, "use_hip", False)
-            works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=coll, fresh_local=fresh)
+                works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=coll, fresh_local=fresh)
         # conv3 / conv2 data gradients on main, conv3's weight gradient on the branch
         ev3 = br.mark()
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2,
@@ -263,9 +265,8 @@ class DataParallelStep:
         if shard:
             with br.branch(hand):
                 # this rank's fc rows of the global batch's gradient (+ their clip-norm
-                # partials, all-gathered) beside conv1's weight gradient
+                # partials, all-gathered with the next bucket) beside conv1's weight gradient
                 nfc = self._fc_shard_grad_norm()
-                works["fcn"] = coll.all_gather_into(self.norm_part[:self.world * nfc], self.fcn_send[:nfc])
         with br.branch(hand if (factors and not shard) else None):
             # conv2 / conv3 / head bucket [w2, wfc): reduced on the branch and all-reduced
             # from it while conv1's weight gradient runs -- only conv1's bucket follows the
@@ -273,7 +274,10 @@ class DataParallelStep:
             ops.finalize_grads(jobs, None, None)
             if self._comm_bf16:
                 self.gcomm[o2:cut].copy_(self.g32[o2:cut])
-            works["cv2"] = coll.all_reduce(self.gcomm[o2:cut])
+            with coll.fused():
+                if shard:
+                    works["fcn"] = coll.all_gather_into(self.norm_part[:self.world * nfc], self.fcn_send[:nfc])
+                works["cv2"] = coll.all_reduce(self.gcomm[o2:cut])
             if factors and not shard:
                 # the global batch's whole fc weight gradient (identical on every rank)
                 nfc = self._fc_wgrad_gathered()
@@ -348,13 +352,14 @@ class DataParallelStep:
         place; the next forward waits for it at its fc layer (:meth:`_wait_params`)."""
         coll = self.coll
         works = []
-        w_all, w_own = self._fc_rows(self.pbf)
-        works.append(coll.all_gather_into(w_all, w_own))
-        if self.split:
-            l_all, l_own = self._fc_rows(self.pbf_lo)
-            works.append(coll.all_gather_into(l_all, l_own))
-        b_all, b_own = self._fc_bias(self.p32)
-        works.append(coll.all_gather_into(b_all, b_own))
+        with coll.fused():            # (RCCL: one launch)
+            w_all, w_own = self._fc_rows(self.pbf)
+            works.append(coll.all_gather_into(w_all, w_own))
+            if self.split:
+                l_all, l_own = self._fc_rows(self.pbf_lo)
+                works.append(coll.all_gather_into(l_all, l_own))
+            b_all, b_own = self._fc_bias(self.p32)
+            works.append(coll.all_gather_into(b_all, b_own))
         self._params_pending = works
 
     def _wait_params(self) -> None:

@@ -212,6 +212,22 @@ class _TorchWork:
             c._joined[key] = self.seq
 
 
+class _GroupedWork:
+    """A collective issued inside ``NativeCollectives.fused()``: RCCL launches the group's
+    operations at the group's end, so the completion event is recorded there (shared by
+    every member)."""
+
+    def __init__(self):
+        self.work = None
+
+    @property
+    def event(self):
+        return self.work.event if self.work is not None else None
+
+    def wait(self) -> None:
+        self.work.wait()
+
+
 class _StreamWork:
     """Completion of a collective enqueued on a collectives object's comm stream: ``wait``
     makes the current stream wait for an event recorded right after it (a graph edge
@@ -240,6 +256,12 @@ class _StreamWork:
 class _StreamColl:
     """Shared plumbing: a comm stream that forks from the current stream per op."""
     inline = False
+
+    def fused(self):
+        """Context: the collectives issued inside leave as ONE launch where the backend
+        can fuse them (RCCL group); elsewhere a no-op."""
+        from contextlib import nullcontext
+        return nullcontext()
 
     def _init_stream(self, device):
         self.device = torch.device(device)
@@ -334,6 +356,10 @@ class TorchCollectives:
         import torch.distributed as dist
         return int(dist.get_world_size(self.group))
 
+    def fused(self):
+        from contextlib import nullcontext
+        return nullcontext()
+
 
 class NativeCollectives(_StreamColl):
     """The DP step's collectives on the native communicator's own stream."""
@@ -347,20 +373,53 @@ class NativeCollectives(_StreamColl):
         self._seq = 0
         self._joined = {}
 
+    _grouped = None     # handles of the open RCCL group (fused())
+
+    def _done(self):
+        if self._grouped is not None:
+            h = _GroupedWork()
+            self._grouped.append(h)
+            return h
+        return _StreamWork(self)
+
+    def fused(self):
+        """RCCL group: the collectives issued inside launch together at its end (one kernel
+        and one latency instead of one per op: the fc factor rows with the shard
+        statistics, the updated fc rows with their biases)."""
+        from contextlib import contextmanager
+        lib = self.comm.lib
+
+        @contextmanager
+        def ctx():
+            assert self._grouped is None, "RCCL groups do not nest here"
+            self._fork()
+            self._grouped = []
+            self.comm._check(lib.apex_comm_group_start(), "group_start")
+            try:
+                yield
+            finally:
+                members, self._grouped = self._grouped, None
+                self.comm._check(lib.apex_comm_group_end(), "group_end")
+                if members:
+                    w = _StreamWork(self)
+                    for m in members:
+                        m.work = w
+        return ctx()
+
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
         s = self._fork()
         self.comm.all_reduce_(t, op, stream=s)
-        return _StreamWork(self)
+        return self._done()
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
         s = self._fork()
         self.comm.all_gather_(out, inp, stream=s)
-        return _StreamWork(self)
+        return self._done()
 
     def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum"):
         s = self._fork()
         self.comm.reduce_scatter_(out, inp, op, stream=s)
-        return _StreamWork(self)
+        return self._done()
 
     def all_reduce_inline(self, t: torch.Tensor, op: str = "sum"):
         """All-reduce enqueued on the CURRENT stream (no fork / join): the caller has
