@@ -58,6 +58,9 @@ class Streams:
         self.cuda = torch.device(device).type == "cuda" and side is not None
         self.device = device
         self.side = side
+        # a third stream for the sharded update's parameter all-gathers, so the branch's
+        # chain of each update starts at its fork like the single-rank step's
+        self.aside_stream = torch.cuda.Stream(device) if self.cuda else None
 
     @property
     def main(self):
@@ -79,19 +82,14 @@ class Streams:
             self.side.wait_event(after)
         return torch.cuda.stream(self.side)
 
-    def handover(self, work):
-        """A collective's result for the branch: the MAIN stream waits for it (at its current
-        point) and the returned event marks that point; branch work enqueued with
-        ``branch(event)`` then runs after the collective.  The branch cannot wait on the
-        collective's own completion event when the collective was issued from the branch
-        (a forked stream waiting on a stream forked from itself crashed HIP graph capture:
-        segfault in hipStreamEndCapture, round 5 -- ``scripts/probe_dp_capture.py``; round 4
-        saw the same with a torch work handle).  Callers hand over after the main stream has
-        enqueued the data-gradient kernels that the collective overlaps, so the wait rarely
-        stalls it, and enqueue the next main-stream kernel before the branch work: the HIP
-        graph executor keeps a node's first-captured child on the node's queue."""
-        work.wait()
-        return self.mark()
+    def aside(self, after=None):
+        """Context: enqueue on the third stream (after the main-stream point ``after``); the
+        main stream joins it through the work handles of what was issued there."""
+        if not self.cuda:
+            return nullcontext()
+        if after is not None:
+            self.aside_stream.wait_event(after)
+        return torch.cuda.stream(self.aside_stream)
 
     def join(self) -> None:
         if self.cuda:
@@ -114,6 +112,7 @@ class DataParallelStep:
         self._shard = ok and (mode == "on" or (mode == "auto" and W > 1))
         self._params_pending = None     # the last update's fc-row all-gather (sharded)
         self._defer_params = False      # set while capturing an update that another follows
+        self._gather_due = None         # (event,): the optimizer point a deferred gather follows
         if not self._shard:
             return
         off = self.layout.offsets
@@ -185,7 +184,7 @@ class DataParallelStep:
             self._alloc_factors()
         self._graphs = self._multi = None
         self._graphs_warm = False
-        self._params_pending = None
+        self._params_pending = self._gather_due = None
         self._sample_ver = None
         self.rows_resized = getattr(self, "rows_resized", 0) + 1
 
@@ -251,50 +250,60 @@ class DataParallelStep:
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1,
                        **self._lo(dy_lo=self.dY2_lo, w_lo=sp and Pl["w2"], dx_lo=self.dY1_lo))
         nfc = 0
-        # the fc exchange's result for the branch (main waits: see Streams.handover); the
-        # branch's conv2 wgrad, then conv1's wgrad on main.  (Capturing conv1's wgrad
-        # before the handover or before the branch's conv2 wgrad measured the same within
-        # noise: 4,470-4,490 vs 4,540 updates/s emulated at W = 8,
-        # profiles/r5_ab_dp_capture_order.txt.)
-        hand = br.handover(works["fc"]) if (factors or shard) else None
+        # the branch's conv2 wgrad, then conv1's wgrad on main.  The fc exchange's result
+        # reaches the branch by stream order: the collectives were issued from the branch
+        # (graphs: the comm stream IS the branch; eager torch: the work handle's wait).
+        # The main stream does not wait for the exchange before conv1's wgrad: a main-stream
+        # wait there made conv1's wgrad start only after the branch's conv2 wgrad in the
+        # replayed graph (trace r5_emu8e: ~28 us idle; 5,025-5,033 vs 5,128-5,158 updates/s
+        # emulated at W = 8, profiles/r5_ab_dp_capture_order.txt).
         with br.branch(ev2):
             self._conv2_wgrad(jobs)
         jobs1 = []
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
                              G["b1"], jobs=jobs1, **self._lo(dy_lo=self.dY1_lo))
-        if shard:
-            with br.branch(hand):
-                # this rank's fc rows of the global batch's gradient (+ their clip-norm
-                # partials, all-gathered with the next bucket) beside conv1's weight gradient
-                nfc = self._fc_shard_grad_norm()
-        with br.branch(hand if (factors and not shard) else None):
+        with br.branch():
+            if factors and not shard:
+                works["fc"].wait()
             # conv2 / conv3 / head bucket [w2, wfc): reduced on the branch and all-reduced
             # from it while conv1's weight gradient runs -- only conv1's bucket follows the
             # last backward kernel
             ops.finalize_grads(jobs, None, None)
             if self._comm_bf16:
                 self.gcomm[o2:cut].copy_(self.g32[o2:cut])
-            with coll.fused():
-                if shard:
-                    works["fcn"] = coll.all_gather_into(self.norm_part[:self.world * nfc], self.fcn_send[:nfc])
-                works["cv2"] = coll.all_reduce(self.gcomm[o2:cut])
+            works["cv2"] = coll.all_reduce(self.gcomm[o2:cut])
             if factors and not shard:
                 # the global batch's whole fc weight gradient (identical on every rank)
                 nfc = self._fc_wgrad_gathered()
         ops.finalize_grads(jobs1, None, None)
+        if shard:
+            # this rank's fc rows of the global batch's gradient (+ their clip-norm partials)
+            # on main after conv1's: the branch carries the exchange, conv3 / conv2 wgrads
+            # and the [w2, wfc) bucket, the main stream would otherwise idle here (the
+            # exchange finished long before: this wait costs one edge, no stall)
+            works["fc"].wait()
+            nfc = self._fc_shard_grad_norm()
         self._npart = 0
         self._mark("conv_backward")
         if self._comm_bf16:
             self.gcomm[:o2].copy_(self.g32[:o2])
+        fcn = (self.norm_part[:self.world * nfc], self.fcn_send[:nfc]) if shard else None
         if getattr(coll, "inline", False) and self._ordered_coll:
-            # conv1's bucket on the main stream itself: one join of the branch and one of
-            # the comm stream (in order: covers everything issued before), then no fork /
-            # join edge on the critical path
+            # conv1's bucket (+ the fc clip-norm partials) on the main stream itself, one
+            # RCCL launch: one join of the branch (in order: covers every collective issued
+            # from it), then no fork / join edge on the critical path
             br.join()
             works["cv2"].wait()
-            coll.all_reduce_inline(self.gcomm[:o2])
+            with coll.fused(inline=True):
+                coll.all_reduce_inline(self.gcomm[:o2])
+                if fcn is not None:
+                    coll.all_gather_inline(*fcn)
         else:
-            w_cv = coll.all_reduce(self.gcomm[:o2])
+            with coll.fused():
+                w_cv = coll.all_reduce(self.gcomm[:o2])
+                if fcn is not None:
+                    works["cv1"] = w_cv
+                    w_cv = coll.all_gather_into(*fcn)
             br.join()
             if self._ordered_coll:
                 w_cv.wait()          # the collectives run in issue order: covers the rest
@@ -307,7 +316,13 @@ class DataParallelStep:
             n0 = self.world * nfc
             nr = ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[n0:], 64)
             self._seg3(norm_slots=n0 + nr, segs=self._segs)
-            self._gather_params()
+            if self._defer_params and self._streams.cuda:
+                # inside a multi-update capture: issued once the next update's conv12 is
+                # enqueued (forward_all -> _issue_params), so conv12 stays the optimizer's
+                # first-captured child and keeps the main queue (round-5 trace r5_emu8d)
+                self._gather_due = (self._streams.mark(),)
+            else:
+                self._gather_params()
         elif factors:
             nr = ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[nfc:], 64)
             self._seg3(norm_slots=nfc + nr)
@@ -362,10 +377,23 @@ class DataParallelStep:
             works.append(coll.all_gather_into(b_all, b_own))
         self._params_pending = works
 
+    def _issue_params(self) -> None:
+        """Issue a deferred fc-row all-gather (see the end of :meth:`_dp_body`) on the third stream,
+        after the optimizer point it was deferred from."""
+        due = getattr(self, "_gather_due", None)
+        if due is not None:
+            self._gather_due = None
+            with self._streams.aside(due[0]), self.coll.on_stream(self._streams.aside_stream):
+                # (RCCL keeps one communicator's kernels in issue order by itself; the
+                # next collective, the branch's, forks from main after the fc forward
+                # that waits for these)
+                self._gather_params()
+
     def _wait_params(self) -> None:
         """The current stream waits for the last update's fc-row all-gathers, if pending
         (the last first: on an in-order comm stream its join covers the others, which
         then add no edge)."""
+        self._issue_params()
         ws = getattr(self, "_params_pending", None)
         if ws:
             for w in reversed(ws):

@@ -362,6 +362,7 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
                                Tb["w1"], T["b1"], 2 * B, c2f=c2f)
             ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B)
+        self._issue_params()      # sharded DP update: a deferred fc-row all-gather (learner/dp_step.py)
         ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
                      **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
         self._wait_params()       # sharded DP update: the last update's fc rows (learner/dp_step.py)
@@ -735,7 +736,7 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         except Exception:  # pragma: no cover - a sticky error is reported below anyway
             pass
         self._graphs = self._multi = None
-        self._params_pending, self._defer_params = None, False
+        self._params_pending, self._defer_params, self._gather_due = None, False, None
         self._restore(snap)
         if self._presample:
             self._sample()

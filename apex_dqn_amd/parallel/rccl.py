@@ -241,13 +241,16 @@ class _StreamWork:
         self.coll = coll
         coll._seq += 1
         self.seq = coll._seq
+        self.stream = coll.stream
         self.event = torch.cuda.Event()
-        self.event.record(coll.stream)
+        self.event.record(self.stream)
 
     def wait(self) -> None:
         c = self.coll
         cur = torch.cuda.current_stream(c.device)
-        key = cur.cuda_stream
+        if cur.cuda_stream == self.stream.cuda_stream:
+            return               # issued on this very stream: already in order
+        key = (cur.cuda_stream, self.stream.cuda_stream)
         if self.seq > c._joined.get(key, 0):
             cur.wait_event(self.event)
             c._joined[key] = self.seq
@@ -257,7 +260,7 @@ class _StreamColl:
     """Shared plumbing: a comm stream that forks from the current stream per op."""
     inline = False
 
-    def fused(self):
+    def fused(self, inline: bool = False):
         """Context: the collectives issued inside leave as ONE launch where the backend
         can fuse them (RCCL group); elsewhere a no-op."""
         from contextlib import nullcontext
@@ -281,14 +284,28 @@ class _StreamColl:
         self.stream = stream
         self._joined = {}
 
+    def on_stream(self, stream):
+        """Context: the collectives issued inside go to ``stream`` (already ordered after
+        the collectives of the usual stream by the caller's events)."""
+        from contextlib import contextmanager
+
+        @contextmanager
+        def ctx():
+            prev, self.stream = self.stream, stream
+            try:
+                yield
+            finally:
+                self.stream = prev
+        return ctx()
+
 
 class TorchCollectives:
     """torch.distributed.  With the RCCL process group the collectives run on the process
     group's own stream, forked from the current stream; their handles are waited for on
     the step's main (capture-origin) stream only -- a forked stream that waits on a
     stream forked from itself crashed HIP graph capture (hipStreamEndCapture segfault,
-    round 5, ``scripts/probe_dp_capture.py``), so the branch receives collective results
-    by a main-stream handover (learner/dp_step.py ``Streams.handover``).  gloo (CPU
+    round 5, ``scripts/probe_dp_capture.py``), so this backend runs the DP step eagerly
+    (learner/fused_learner.py ``_dp_graphs``).  gloo (CPU
     tests, one-GPU rehearsals) keeps the process group's own handles."""
     name = "torch"
     inline = False
@@ -356,7 +373,7 @@ class TorchCollectives:
         import torch.distributed as dist
         return int(dist.get_world_size(self.group))
 
-    def fused(self):
+    def fused(self, inline: bool = False):
         from contextlib import nullcontext
         return nullcontext()
 
@@ -382,17 +399,19 @@ class NativeCollectives(_StreamColl):
             return h
         return _StreamWork(self)
 
-    def fused(self):
+    def fused(self, inline: bool = False):
         """RCCL group: the collectives issued inside launch together at its end (one kernel
         and one latency instead of one per op: the fc factor rows with the shard
-        statistics, the updated fc rows with their biases)."""
+        statistics, the updated fc rows with their biases).  ``inline``: a group of
+        ``*_inline`` ops on the current stream (no fork)."""
         from contextlib import contextmanager
         lib = self.comm.lib
 
         @contextmanager
         def ctx():
             assert self._grouped is None, "RCCL groups do not nest here"
-            self._fork()
+            if not inline:
+                self._fork()
             self._grouped = []
             self.comm._check(lib.apex_comm_group_start(), "group_start")
             try:
@@ -425,6 +444,11 @@ class NativeCollectives(_StreamColl):
         """All-reduce enqueued on the CURRENT stream (no fork / join): the caller has
         already joined every collective issued before it, so RCCL's issue order holds."""
         self.comm.all_reduce_(t, op)
+        return _Done()
+
+    def all_gather_inline(self, out: torch.Tensor, inp: torch.Tensor):
+        """All-gather on the CURRENT stream (as :meth:`all_reduce_inline`)."""
+        self.comm.all_gather_(out, inp)
         return _Done()
 
     def world(self) -> int:
@@ -476,6 +500,10 @@ class EmulatedCollectives(_StreamColl):
 
     def all_reduce_inline(self, t: torch.Tensor, op: str = "sum"):
         self._reduce(t)
+        return _Done()
+
+    def all_gather_inline(self, out: torch.Tensor, inp: torch.Tensor):
+        self._gather(out, inp)
         return _Done()
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
