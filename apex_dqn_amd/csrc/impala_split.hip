@@ -413,36 +413,17 @@ __device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, 
   }
 }
 
+// conv0 -> ys, barrier, conv1 (+ x, ReLU) -> out for image n, row band `band`, from the
+// staged x rows (LDS x row 0 = image row band R - 2); shared by both kernels below
 template <int C, int HW, int R>
-__global__ void __launch_bounds__(512) resblock_fwd_split_kernel(ResSDesc d) {
+__device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uint8_t* xs, uint8_t* ys, int n, int band,
+                                                    int lane, int wv) {
   constexpr int NTHR = 512, P = C / 16, NT = C / 16, WP = HW + 2;
   constexpr int XROWS = R + 4, YROWS = R + 2;
   constexpr int XPL = XROWS * WP + 24, YPL = YROWS * WP + 24;
   constexpr int XLO = P * XPL * 32, YLO = P * YPL * 32;      // lo set offsets
-  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (XLO + YLO)];
-  uint8_t* xs = smem;
-  uint8_t* ys = smem + 2 * XLO;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int band = blockIdx.x, n = blockIdx.y;
   const int r0 = band * R;
   const bool second = d.wf0b != nullptr && n >= d.n_switch;
-  stage_rows_split<P, HW, HW, XROWS, NTHR, 4>(xs, XPL, d.x, d.x_img, n, r0 - 2, 0, tid);
-  // conv1's zero padding in both y sets: halo columns of every row + the slack past the rows
-  for (int i = tid; i < 2 * P * YROWS * 2; i += NTHR) {
-    const int set = i / (P * YROWS * 2), i1 = i - set * (P * YROWS * 2);
-    const int p = i1 / (YROWS * 2), r = i1 - p * YROWS * 2;
-    const int c = (r & 1) ? WP - 1 : 0;
-    uint8_t* q = ys + set * YLO + (p * YPL + (r >> 1) * WP + c) * 32;
-    *reinterpret_cast<uint4*>(q) = make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(q + 16) = make_uint4(0, 0, 0, 0);
-  }
-  for (int i = tid; i < 2 * P * 24 * 2; i += NTHR) {
-    const int set = i / (P * 48), i1 = i - set * (P * 48);
-    const int p = i1 / 48, r = i1 - p * 48;
-    *reinterpret_cast<uint4*>(ys + set * YLO + (p * YPL + YROWS * WP) * 32 + r * 16) = make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-
   {  // conv0 on rows r0 - 1 + lh, lh in [0, R + 2): LDS x row 0 = image row r0 - 2
     const float* __restrict__ b0 = second ? d.b0b : d.b0;
     const bool save = d.ysave != nullptr && n < d.n_save;
@@ -496,6 +477,42 @@ __global__ void __launch_bounds__(512) resblock_fwd_split_kernel(ResSDesc d) {
       }
     });
   }
+}
+
+// conv1's zero padding in both y sets: halo columns of every row + the slack past the rows
+// (conv0's epilogue never writes them)
+template <int P, int WP, int YROWS, int YPL, int YLO, int NTHR>
+__device__ __forceinline__ void zero_y_halo(uint8_t* ys, int tid) {
+  for (int i = tid; i < 2 * P * YROWS * 2; i += NTHR) {
+    const int set = i / (P * YROWS * 2), i1 = i - set * (P * YROWS * 2);
+    const int p = i1 / (YROWS * 2), r = i1 - p * YROWS * 2;
+    const int c = (r & 1) ? WP - 1 : 0;
+    uint8_t* q = ys + set * YLO + (p * YPL + (r >> 1) * WP + c) * 32;
+    *reinterpret_cast<uint4*>(q) = make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(q + 16) = make_uint4(0, 0, 0, 0);
+  }
+  for (int i = tid; i < 2 * P * 24 * 2; i += NTHR) {
+    const int set = i / (P * 48), i1 = i - set * (P * 48);
+    const int p = i1 / 48, r = i1 - p * 48;
+    *reinterpret_cast<uint4*>(ys + set * YLO + (p * YPL + YROWS * WP) * 32 + r * 16) = make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int C, int HW, int R>
+__global__ void __launch_bounds__(512) resblock_fwd_split_kernel(ResSDesc d) {
+  constexpr int NTHR = 512, P = C / 16, WP = HW + 2;
+  constexpr int XROWS = R + 4, YROWS = R + 2;
+  constexpr int XPL = XROWS * WP + 24, YPL = YROWS * WP + 24;
+  constexpr int XLO = P * XPL * 32, YLO = P * YPL * 32;      // lo set offsets
+  __shared__ __attribute__((aligned(16))) uint8_t smem[2 * (XLO + YLO)];
+  uint8_t* xs = smem;
+  uint8_t* ys = smem + 2 * XLO;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int band = blockIdx.x, n = blockIdx.y;
+  stage_rows_split<P, HW, HW, XROWS, NTHR, 4>(xs, XPL, d.x, d.x_img, n, band * R - 2, 0, tid);
+  zero_y_halo<P, WP, YROWS, YPL, YLO, NTHR>(ys, tid);
+  __syncthreads();
+  resblock_item_split<C, HW, R>(d, xs, ys, n, band, lane, wv);
 }
 
 // =====================================================================================
