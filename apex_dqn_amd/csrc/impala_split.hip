@@ -669,47 +669,60 @@ template <int H, int W>
 __global__ void __launch_bounds__(256) maxpool_bwd_split_kernel(const float* __restrict__ dy, int64_t dy_img,
                                                                 const uint8_t* __restrict__ amax, int P,
                                                                 float* __restrict__ dx, int64_t dx_img, int N) {
-  // one thread per (image, plane, pixel, 4-channel quad); the <= 4 windows whose argmax
-  // may be (h, w) are loaded up front (clamped address, masked when absent)
+  // one thread per (image, plane, pooled pixel (a, b), 4-channel quad): the input pixels
+  // (2a + dh, 2b + dw) of its 2 x 2 block see only the windows (a + i, b + j), i, j in
+  // {0, 1} (i = 1 only for dh = 1: kernel row 0), so each window's gradient and argmax
+  // codes are loaded once for four outputs (the per-pixel form loaded four windows per
+  // output pixel).  Per output the windows are summed in the same (i, j) order as before.
+  constexpr int HO = (H + 1) / 2, WO = (W + 1) / 2;
+  constexpr int64_t PIMG = (int64_t)HO * WO * 16;
   const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
-  const uint32_t total = (uint32_t)N * (uint32_t)P * (uint32_t)(H * W * 4);
+  const uint32_t total = (uint32_t)N * (uint32_t)P * (uint32_t)(HO * WO * 4);
   if (idx >= total) return;
   const int qd = (int)(idx & 3u);
   uint32_t r = idx >> 2;
-  const uint32_t rw = r / (uint32_t)W;
-  const int w = (int)(r - rw * (uint32_t)W);
-  const uint32_t rh = rw / (uint32_t)H;
-  const int h = (int)(rw - rh * (uint32_t)H);
-  const uint32_t rp = rh / (uint32_t)P;
-  const int p = (int)(rh - rp * (uint32_t)P);
+  const uint32_t rb = r / (uint32_t)WO;
+  const int b = (int)(r - rb * (uint32_t)WO);
+  const uint32_t ra = rb / (uint32_t)HO;
+  const int a = (int)(rb - ra * (uint32_t)HO);
+  const uint32_t rp = ra / (uint32_t)P;
+  const int p = (int)(ra - rp * (uint32_t)P);
   const int n = (int)rp;
-  constexpr int HO = (H + 1) / 2, WO = (W + 1) / 2;
-  constexpr int64_t PIMG = (int64_t)HO * WO * 16;
   const float* dp = dy + (int64_t)n * dy_img;
   const uint8_t* am = amax + (int64_t)n * P * PIMG;
-  const int oha = h >> 1, owa = w >> 1;
-  const bool hb = (h & 1) && oha + 1 < HO, wb = (w & 1) && owa + 1 < WO;
-  const int kha = 1 + (h & 1), kwa = 1 + (w & 1);
-  const int ohs[2] = {oha, hb ? oha + 1 : oha}, ows[2] = {owa, wb ? owa + 1 : owa};
-  const int khs[2] = {kha, hb ? 0 : -16}, kws[2] = {kwa, wb ? 0 : -16};
+  const bool i1 = a + 1 < HO, j1 = b + 1 < WO;
   float4 g[4];
   uint32_t cv[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int64_t po = (((int64_t)p * HO + ohs[i >> 1]) * WO + ows[i & 1]) * 16 + 4 * qd;
-    g[i] = ld4(dp + po);
-    cv[i] = *reinterpret_cast<const uint32_t*>(am + po);
+  for (int k = 0; k < 4; ++k) {
+    const int oh = (k >> 1) && i1 ? a + 1 : a, ow = (k & 1) && j1 ? b + 1 : b;
+    const int64_t po = (((int64_t)p * HO + oh) * WO + ow) * 16 + 4 * qd;
+    g[k] = ld4(dp + po);
+    cv[k] = *reinterpret_cast<const uint32_t*>(am + po);
   }
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float* dxi = dx + (int64_t)n * dx_img;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int want = khs[i >> 1] * 3 + kws[i & 1];
-    const float gv[4] = {g[i].x, g[i].y, g[i].z, g[i].w};
+  for (int dh = 0; dh < 2; ++dh) {
+    const int h = 2 * a + dh;
+    if (h >= H) continue;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] += (int)((cv[i] >> (8 * c)) & 0xffu) == want ? gv[c] : 0.f;
+    for (int dw = 0; dw < 2; ++dw) {
+      const int w = 2 * b + dw;
+      if (w >= W) continue;
+      // window (a + i, b + j) holds this pixel at kernel (kh, kw); absent windows never match
+      const int khs[2] = {1 + dh, (dh && i1) ? 0 : -16}, kws[2] = {1 + dw, (dw && j1) ? 0 : -16};
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int want = khs[k >> 1] * 3 + kws[k & 1];
+        const float gv[4] = {g[k].x, g[k].y, g[k].z, g[k].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] += (int)((cv[k] >> (8 * c)) & 0xffu) == want ? gv[c] : 0.f;
+      }
+      *reinterpret_cast<float4*>(dxi + (((int64_t)p * H + h) * W + w) * 16 + 4 * qd) =
+          make_float4(acc[0], acc[1], acc[2], acc[3]);
+    }
   }
-  *reinterpret_cast<float4*>(dx + (int64_t)n * dx_img + (((int64_t)p * H + h) * W + w) * 16 + 4 * qd) =
-      make_float4(acc[0], acc[1], acc[2], acc[3]);
 }
 
 // out[r][c] = hi[r][c] + lo[r][c] (fp32) for c < cols, rows of ld elements
@@ -810,8 +823,8 @@ APEX_EXPORT int apex_sconv_wgrad_split(SconvWgSDesc d, int cin, int cout, int H,
 
 APEX_EXPORT int apex_maxpool_bwd_split(const float* dy, int64_t dy_img, const uint8_t* amax, int P, int H, int W,
                                        float* dx, int64_t dx_img, int N, hipStream_t st) {
-  const int64_t total = (int64_t)N * P * H * W * 4;
-  if (total <= 0 || total >= 0x7fffff00LL) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * P * ((H + 1) / 2) * ((W + 1) / 2) * 4;   // threads: pooled pixels x quads
+  if (total <= 0 || (int64_t)N * P * H * W * 4 >= 0x7fffff00LL) return (int)hipErrorInvalidValue;
   const int blocks = (int)((total + 255) / 256);
   if (H == 84 && W == 84) maxpool_bwd_split_kernel<84, 84><<<blocks, 256, 0, st>>>(dy, dy_img, amax, P, dx, dx_img, N);
   else if (H == 42 && W == 42) maxpool_bwd_split_kernel<42, 42><<<blocks, 256, 0, st>>>(dy, dy_img, amax, P, dx, dx_img, N);
