@@ -435,6 +435,7 @@ struct Conv2DgradImgDesc {
   uint4* wfrag;
   int wfrag_ready;
   unsigned long long* wq;   // image work queue counter (csrc/mfma_common.h wq_next); null: static order
+  int cls_split;            // split mode: one workgroup per (image, stride-parity class) -- small batches
 };
 
 // Images come from the work queue: thread 0 fetches the next image while this one's
@@ -705,6 +706,133 @@ __global__ void __launch_bounds__(256, 1) conv2_dgrad_img_split_kernel(Conv2Dgra
   }
 }
 
+// Split conv2 data gradient for small batches (d.cls_split): one workgroup per (image,
+// stride-parity class) instead of per image, so a 74-image per-rank batch (global-batch
+// DP at 8 ranks) spreads over 296 workgroups rather than 74 CUs.  Workgroup b owns class
+// b & 3 for images b >> 2, (b >> 2) + G / 4, ...; its four waves split the class's GEMM
+// (100 output pixels x 64 channels, K 256) by channel half (w & 1) and pixel-tile pair
+// (w >> 1), each holding its half's hi / lo weight fragments (loaded once) -- the same
+// fragments, K order and fixed-order accumulation as conv2_dgrad_img_split_kernel, so the
+// outputs are bit-identical.  The class's 100 pixel rows go through LDS and leave as full
+// 128-B NHWC rows with the ReLU mask applied.
+__global__ void __launch_bounds__(256, 2) conv2_dgrad_img_split_cls_kernel(Conv2DgradImgDesc d) {
+  __shared__ __attribute__((aligned(16))) uint8_t sdy[2 * C2D_PSLOTS * 128];
+  __shared__ __attribute__((aligned(16))) uint8_t sout[2 * 100 * 128];   // the class's pixels: hi, lo
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int cls = blockIdx.x & 3, p = cls >> 1, q = cls & 1;
+  const int nh = wv & 1, tp = wv >> 1;
+  const int rr = lane & 31, kg = lane >> 5;
+  const int ngrp = (int)gridDim.x >> 2;
+  for (int i = tid; i < 2 * C2D_PSLOTS * 8; i += 256) *reinterpret_cast<uint4*>(sdy + i * 16) = make_uint4(0, 0, 0, 0);
+  bf16x8 wh[16], wl[16];
+  {
+    const uint4* __restrict__ wf = d.wfrag + ((cls * 2 + nh) * 16) * 64 + lane;   // pack_c2d_wfrag_kernel
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      wh[s] = __builtin_bit_cast(bf16x8, wf[s * 64]);
+      wl[s] = __builtin_bit_cast(bf16x8, wf[C2D_FRAGS + s * 64]);
+    }
+  }
+  for (int img = (int)blockIdx.x >> 2; img < d.N; img += ngrp) {
+    __syncthreads();   // previous image: LDS reads and copy-out done
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(d.dy + (int64_t)img * 81 * 64);
+      const uint4* srl = reinterpret_cast<const uint4*>(d.dy_lo + (int64_t)img * 81 * 64);
+      for (int k = tid; k < 2 * 81 * 8; k += 256) {
+        const int pl = k >= 81 * 8 ? 1 : 0, kk = k - pl * 81 * 8;
+        const int px = kk >> 3, c = kk & 7, oh = px / 9, ow = px - oh * 9;
+        *reinterpret_cast<uint4*>(sdy + pl * C2D_PSLOTS * 128 + c2d_off((oh + 1) * 11 + ow + 1, c)) =
+            pl ? srl[kk] : src[kk];
+      }
+    }
+    __syncthreads();
+    int pi[4], pj[4];
+    {
+      int rq = rr;
+      asm volatile("" : "+v"(rq));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = min(t * 32 + rq, 99);
+        pi[t] = r / 10;
+        pj[t] = r - pi[t] * 10;
+      }
+    }
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[t][j] = 0.f;
+    bf16x8 xf[2][2];
+#define C2DC_LDX(u_, dst_)                                                                   \
+    {                                                                                      \
+      const int s_ = (u_) >> 1, t_ = 2 * tp + ((u_) & 1);                                 \
+      const int off_ = c2d_off((pi[t_] - ((s_ >> 3) & 1) + 1) * 11 + (pj[t_] - ((s_ >> 2) & 1) + 1), \
+                               ((s_ & 3) << 1) | kg);                                      \
+      dst_[0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + off_));  \
+      dst_[1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sdy + C2D_PSLOTS * 128 + off_)); \
+    }
+    C2DC_LDX(0, xf[0])
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int s = u >> 1, t = u & 1;
+      if (u + 1 < 32) C2DC_LDX(u + 1, xf[(u + 1) & 1])
+      __builtin_amdgcn_sched_barrier(0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[s], xf[u & 1][0], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[s], xf[u & 1][1], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[s], xf[u & 1][0], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#undef C2DC_LDX
+    // this wave's channel half of its two pixel tiles -> the class's LDS rows (slot r)
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const int r = (2 * tp + t2) * 32 + rr;
+      if (r >= 100) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ch = nh * 32 + 8 * g + 4 * kg;
+        uint32_t h01, l01, h23, l23;
+        split_pk_bf16(acc[t2][4 * g], acc[t2][4 * g + 1], h01, l01);
+        split_pk_bf16(acc[t2][4 * g + 2], acc[t2][4 * g + 3], h23, l23);
+        const int o = c2d_off(r, ch >> 3) + (ch & 7) * 2;
+        *reinterpret_cast<uint2*>(sout + o) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(sout + 100 * 128 + o) = make_uint2(l01, l23);
+      }
+    }
+    __syncthreads();
+    // copy-out: 100 class pixels x 8 chunks, full 128-B rows, with the ReLU mask of y1
+    const uint4* msrc = reinterpret_cast<const uint4*>(d.mask + (int64_t)img * 400 * 64);
+    uint4* dst = reinterpret_cast<uint4*>(d.dx + (int64_t)img * 400 * 64);
+    uint4* dsl = reinterpret_cast<uint4*>(d.dx_lo + (int64_t)img * 400 * 64);
+    uint4 mv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = tid + 256 * i;
+      if (k < 800) {
+        const int r = k >> 3, c = k & 7, a = r / 10, b = r - a * 10;
+        mv[i] = msrc[((2 * a + p) * 20 + 2 * b + q) * 8 + c];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = tid + 256 * i;
+      if (k < 800) {
+        const int r = k >> 3, c = k & 7, a = r / 10, b = r - a * 10;
+        const int o = c2d_off(r, c);
+        uint4 v = *reinterpret_cast<const uint4*>(sout + o);
+        uint4 vl = *reinterpret_cast<const uint4*>(sout + 100 * 128 + o);
+        v = make_uint4(mask_bf16x2(v.x, mv[i].x), mask_bf16x2(v.y, mv[i].y), mask_bf16x2(v.z, mv[i].z),
+                       mask_bf16x2(v.w, mv[i].w));
+        vl = make_uint4(mask_bf16x2(vl.x, mv[i].x), mask_bf16x2(vl.y, mv[i].y), mask_bf16x2(vl.z, mv[i].z),
+                        mask_bf16x2(vl.w, mv[i].w));
+        const int64_t go = ((2 * a + p) * 20 + 2 * b + q) * 8 + c;
+        dst[go] = v;
+        dsl[go] = vl;
+      }
+    }
+  }
+}
+
 APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t st) {
   if (d.N <= 0 || d.dy == nullptr || d.w == nullptr || d.mask == nullptr || d.dx == nullptr)
     return (int)hipErrorInvalidValue;
@@ -716,6 +844,13 @@ APEX_EXPORT int apex_conv2_dgrad_img(Conv2DgradImgDesc d, int grid, hipStream_t 
   if (!d.wfrag_ready)
     pack_c2d_wfrag_kernel<<<C2D_PACK_THREADS / 256, 256, 0, st>>>(d.w, split ? d.w_lo : nullptr,
                                                                   reinterpret_cast<uint32_t*>(d.wfrag));
+  if (split && d.cls_split) {
+    // (image, class) workgroups: 4 per image, up to two per CU
+    int gi = grid > 0 ? grid : 128;
+    if (gi > d.N) gi = d.N;
+    conv2_dgrad_img_split_cls_kernel<<<4 * gi, 256, 0, st>>>(d);
+    APEX_CHECK_LAUNCH();
+  }
   int G = grid > 0 ? grid : 256;
   if (G > d.N) G = d.N;
   if (split) conv2_dgrad_img_split_kernel<<<G, 256, 0, st>>>(d);

@@ -452,6 +452,8 @@ def conv2_dgrad_img(lib, dy: torch.Tensor, w2: torch.Tensor, mask: torch.Tensor,
     d.wfrag = c2d_wfrag_buffer(ws, dy.device).data_ptr()
     d.wfrag_ready = int(packed)
     d.wq = ws.wq(("c2d_wq", N, int(grid)), dy.device)
+    # small batches (a global-batch DP rank's rows): one workgroup per (image, class)
+    d.cls_split = int(dy_lo is not None and N <= SW.conv2_dgrad_cls_max)
     _lib.check(lib.apex_conv2_dgrad_img(d, int(grid), _lib.stream_ptr()), "conv2_dgrad_img")
 
 

@@ -28,7 +28,7 @@ class Conv12Desc(ctypes.Structure):
 class Conv2DgradImgDesc(ctypes.Structure):
     """Image-resident conv2 data gradient (mirrors ``Conv2DgradImgDesc`` in csrc/conv2_img.hip)."""
     _fields_ = [("dy", c_p), ("w", c_p), ("mask", c_p), ("dx", c_p), ("N", c_i), ("dy_lo", c_p), ("w_lo", c_p),
-                ("dx_lo", c_p), ("wfrag", c_p), ("wfrag_ready", c_i), ("wq", c_p)]
+                ("dx_lo", c_p), ("wfrag", c_p), ("wfrag_ready", c_i), ("wq", c_p), ("cls_split", c_i)]
 
 
 class C2dPackJob(ctypes.Structure):

@@ -35,6 +35,9 @@ class Switches:
     # image-resident conv3 / conv2 data gradients (csrc/conv2_img.hip)
     conv3_dgrad_img: bool = True
     conv2_dgrad_img: bool = True
+    # split conv2 data gradient: one workgroup per (image, stride-parity class) up to this
+    # many images (0: never), per image above it
+    conv2_dgrad_cls_max: int = 256
     # the optimizer + sample launch stores the fused forward's online weight fragments
     # (+0.5-1 %, profiles/r3_ab_optimizer_frag_stores_*.txt)
     opt_frags: bool = True

@@ -381,6 +381,32 @@ def test_conv2_image_resident_split_kernels_vs_generic(monkeypatch, grid):
     assert _rel(_join(h1, l1), _join(g1h, g1l)) < TOL
 
 
+@pytest.mark.parametrize("N,grid", [(74, 0), (146, 0), (37, 5)])
+def test_conv2_dgrad_class_split_bit_identical(monkeypatch, N, grid):
+    """The small-batch split conv2 data gradient (one workgroup per (image, stride-parity
+    class), csrc/conv2_img.hip conv2_dgrad_img_split_cls_kernel) writes exactly the bytes of
+    the per-image kernel: same fragments, K order and accumulation; several images per
+    workgroup when the grid is small."""
+    from apex_dqn_amd.ops import conv as C
+    g = torch.Generator(device="cpu").manual_seed(N)
+    lib = _lib()
+    w = torch.randn(64, 4, 4, 64, generator=g) * 0.03
+    dy = torch.randn(N, 9, 9, 64, generator=g)
+    y1 = torch.randn(N, 20, 20, 64, generator=g).to(DEV, torch.bfloat16)
+    (wh, wl), (dh, dl) = _split(w), _split(dy)
+    outs = {}
+    for cmax in (0, 4096):
+        monkeypatch.setattr(SW, "conv2_dgrad_cls_max", cmax)
+        h1, l1 = _empty2(N, 20, 20, 64)
+        C.conv2_dgrad_img(lib, dh, wh, y1, h1, grid=grid, dy_lo=dl, w_lo=wl, out_lo=l1)
+        torch.cuda.synchronize()
+        outs[cmax] = (h1, l1)
+    assert torch.equal(outs[0][0].view(torch.int16), outs[4096][0].view(torch.int16))
+    assert torch.equal(outs[0][1].view(torch.int16), outs[4096][1].view(torch.int16))
+    ref = R.conv_dgrad(_c(dy), _c(w), (N, 20, 20, 64), 2, _c(y1), torch.float64)
+    assert _rel(_join(*outs[4096]), ref) < TOL
+
+
 @pytest.mark.parametrize("split", [True, False])
 @pytest.mark.parametrize("grid_images", [64, 600])
 def test_conv2_fwd_weights_packed_in_conv1_launch(grid_images, split):
