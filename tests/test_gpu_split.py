@@ -569,6 +569,8 @@ def test_work_queue_outputs_bit_identical_to_static_order(N, grid, monkeypatch):
     mask = torch.randn(N, 20, 20, 64, generator=g).to(DEV, torch.bfloat16)
     d1h, d1l = _split(torch.randn(N, 20, 20, 64, generator=g) * 0.1)
     outs = []
+    # (the per-image data-gradient kernel: the small-batch (image, class) variant has no queue)
+    monkeypatch.setattr(SW, "conv2_dgrad_cls_max", 0)
     for wq, reps in ((False, 1), (True, 3)):
         ws = C_.Workspace()
         monkeypatch.setattr(SW, "work_queue", "on" if wq else "off")   # (the forward's queue is switch-only)
