@@ -9,6 +9,7 @@
 // and writes the bf16 compute copy that the MFMA kernels read, so no separate
 // cast kernel runs.  Memory-bound: 16 B read + 14 B written per parameter.
 #include "rmsprop_common.h"
+#include "pack_rows.h"
 
 #define NPART 1024
 
@@ -83,56 +84,16 @@ APEX_EXPORT int apex_cast_bf16(const float* x, bf16_t* y, int64_t n, bf16_t* lo,
 }
 
 // ------------------------------------------------ data-parallel fc-gradient factors
-// Row pack of up to 4 (src, src row stride, cols) segments of 16-bit values into one
-// [rows][ld] buffer: the send rows of the factored fc-gradient exchange
-// (learner/fused_learner.py _dp_body: [dH | dH lo | y3 | y3 lo] per sample, one
-// all-gather instead of an all-reduce of the 1024 x 3136 gradient).  16-B chunks,
-// every column count and stride a multiple of 8.
-struct PackRows {
-  const uint16_t* src[4];
-  int64_t ld[4];
-  int cols[4];
-  int nseg, rows;
-  uint16_t* dst;
-  int64_t dld;
-};
-
-__global__ void __launch_bounds__(256) pack_rows_kernel(PackRows p) {
-  int tot = 0;
-  for (int s = 0; s < p.nseg; ++s) tot += p.cols[s] >> 3;
-  const int64_t nchunks = (int64_t)p.rows * tot;
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(c / tot);
-    int k = (int)(c - (int64_t)r * tot), s = 0, col0 = 0;
-    while (k >= (p.cols[s] >> 3)) {
-      k -= p.cols[s] >> 3;
-      col0 += p.cols[s];
-      ++s;
-    }
-    const uint4 v = *reinterpret_cast<const uint4*>(p.src[s] + (int64_t)r * p.ld[s] + 8 * k);
-    *reinterpret_cast<uint4*>(p.dst + (int64_t)r * p.dld + col0 + 8 * k) = v;
-  }
-}
+// (csrc/pack_rows.h)
+__global__ void __launch_bounds__(256) pack_rows_kernel(PackRows p) { pack_rows_body(p, blockIdx.x, gridDim.x); }
 
 APEX_EXPORT int apex_pack_rows(const uint16_t* const* src, const int64_t* ld, const int* cols, int nseg, int rows,
                                uint16_t* dst, int64_t dld, hipStream_t st) {
-  if (nseg < 1 || nseg > 4 || rows < 0 || (dld & 7) || ((uintptr_t)dst & 15)) return (int)hipErrorInvalidValue;
-  PackRows p{};
-  int tot = 0;
-  for (int s = 0; s < nseg; ++s) {
-    if ((cols[s] & 7) || (ld[s] & 7) || ((uintptr_t)src[s] & 15)) return (int)hipErrorInvalidValue;
-    p.src[s] = src[s];
-    p.ld[s] = ld[s];
-    p.cols[s] = cols[s];
-    tot += cols[s];
-  }
-  if (tot > dld) return (int)hipErrorInvalidValue;
-  p.nseg = nseg;
-  p.rows = rows;
-  p.dst = dst;
-  p.dld = dld;
+  PackRows p;
+  int64_t nchunks = 0;
+  const int err = make_pack_rows(src, ld, cols, nseg, rows, dst, dld, p, nchunks);
+  if (err) return err;
   if (rows == 0) return 0;
-  const int64_t nchunks = (int64_t)rows * (tot >> 3);
   int nb = (int)((nchunks + 255) / 256);
   nb = nb > 1024 ? 1024 : nb;
   pack_rows_kernel<<<nb, 256, 0, st>>>(p);

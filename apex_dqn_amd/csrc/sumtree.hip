@@ -17,6 +17,7 @@
 #include "head_common.h"
 #include "igemm_wgrad.h"
 #include "rmsprop_common.h"
+#include "pack_rows.h"
 
 // Bounds-checking debug build (SURVEY §5.2 "race / bounds detection"): built as a
 // separate library with -DAPEX_DEBUG_BOUNDS and selected by APEX_DEBUG_BOUNDS=1.
@@ -571,9 +572,15 @@ __device__ __forceinline__ void tree_update_block(const TreeUpdArgs& a) {
 // head weight gradient + priority write-back in one launch: block 0 runs the
 // single-block tree update (dispatched first, it is the long pole), blocks 1..
 // the (A+1) x HS/64 head_wgrad blocks.  Both only need the head kernel's outputs.
-__global__ void __launch_bounds__(512) head_wgrad_prio_kernel(HeadWgArgs hw, TreeUpdArgs tu) {
+// (DP step: blocks past 1 + nhw pack the factored exchange's send rows, csrc/pack_rows.h)
+__global__ void __launch_bounds__(512) head_wgrad_prio_kernel(HeadWgArgs hw, TreeUpdArgs tu, PackRows pk, int nhw,
+                                                             int npk) {
   if (blockIdx.x == 0) {
     tree_update_block(tu);
+    return;
+  }
+  if ((int)blockIdx.x > nhw) {
+    pack_rows_body(pk, blockIdx.x - 1 - nhw, npk);
     return;
   }
   const int b = blockIdx.x - 1, nch = hw.HS / 64;
@@ -739,7 +746,7 @@ APEX_EXPORT int apex_fill16(void* p, int64_t n, int nt, hipStream_t st) {
   APEX_CHECK_LAUNCH();
 }
 
-APEX_EXPORT int apex_abi_version() { return 7; }
+APEX_EXPORT int apex_abi_version() { return 8; }
 
 // 1 if this library was built with -DAPEX_DEBUG_BOUNDS
 APEX_EXPORT int apex_debug_bounds_enabled() {
@@ -849,14 +856,26 @@ APEX_EXPORT int apex_head_wgrad_prio(const bf16_t* Hon, const float* dhead, int 
                                      float* gwa, float* gba, int hidden, TreeDesc t, const int64_t* idx,
                                      const float* td, const int32_t* gen_expect, const int32_t* gen,
                                      float alpha, float eps, uint64_t* ctr_to_bump, const bf16_t* Hon_lo,
-                                     double* stats_out, hipStream_t st) {
+                                     double* stats_out, const uint16_t* const* psrc, const int64_t* pld,
+                                     const int* pcols, int pnseg, int prows, uint16_t* pdst, int64_t pdld,
+                                     hipStream_t st) {
   // the single-block tree update holds TU_MAXR items per thread
   if ((hidden != 512 && hidden != 256) || B < 1 || B > 1024 || B > TU_MAXR * 512 || idx == nullptr)
     return (int)hipErrorInvalidValue;
-  const int nblk = 1 + (A + 1) * (hidden / 64);
-  head_wgrad_prio_kernel<<<nblk, 512, 0, st>>>(
+  const int nhw = (A + 1) * (hidden / 64);
+  // optional row pack in the same launch (pnseg > 0): up to 256 tail blocks
+  PackRows pk{};
+  int npk = 0;
+  if (pnseg > 0) {
+    int64_t nchunks = 0;
+    const int err = make_pack_rows(psrc, pld, pcols, pnseg, prows, pdst, pdld, pk, nchunks);
+    if (err) return err;
+    npk = (int)((nchunks + 511) / 512);
+    npk = npk > 256 ? 256 : npk;
+  }
+  head_wgrad_prio_kernel<<<1 + nhw + npk, 512, 0, st>>>(
       HeadWgArgs{Hon, dhead, B, A, gwv, gbv, gwa, gba, hidden, Hon_lo},
-      TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t), stats_out});
+      TreeUpdArgs{t, idx, td, gen_expect, gen, ctr_to_bump, alpha, eps, B, tree_kfirst(t), stats_out}, pk, nhw, npk);
   APEX_CHECK_LAUNCH();
 }
 

@@ -217,10 +217,11 @@ class DataParallelStep:
         prio = (self.replay, S["idx"], S["gen"], self.td_abs)
         with br.branch(fork):
             if factors:
-                ops.head_wgrad(self.h, self.dhead, self._head_params(G), prio=prio, **self._lo(Hon_lo=self.h_lo))
+                # head weight gradient + priority write-back + the factor-row pack, one launch
                 segs = [self.dH, self.dH_lo, self.y3[:B].reshape(B, FC_COLS), self.y3_lo[:B].reshape(B, FC_COLS)] \
                     if sp else [self.dH, self.y3[:B].reshape(B, FC_COLS)]
-                ops.pack_rows(self.fx_send, segs)
+                ops.head_wgrad(self.h, self.dhead, self._head_params(G), prio=prio, pack=(self.fx_send, segs),
+                               **self._lo(Hon_lo=self.h_lo))
             else:
                 ops.fc_head_wgrad(self.dH, self.y3[:B], G["wfc"], G["bfc"], self.h, self.dhead, G, prio,
                                   **self._lo(dh_lo=self.dH_lo, x_lo=sp and self.y3_lo[:B], Hon_lo=self.h_lo))
@@ -293,7 +294,8 @@ class DataParallelStep:
             # RCCL launch: one join of the branch (in order: covers every collective issued
             # from it), then no fork / join edge on the critical path
             br.join()
-            works["cv2"].wait()
+            if getattr(coll, "stream", None) is not br.side:
+                works["cv2"].wait()      # (issued from the branch itself: the join covers it)
             with coll.fused(inline=True):
                 coll.all_reduce_inline(self.gcomm[:o2])
                 if fcn is not None:

@@ -156,7 +156,7 @@ _SIGS = {
                              c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut, c_p, c_p],
                             c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
-                              c_p, c_p, c_p, c_p], c_i),
+                              c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p, c_i64, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,
                                  c_p, c_f, c_f, c_p, c_p, c_p, c_p], c_i),
     "apex_head_wgrad": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, c_p, c_p], c_i),
@@ -187,7 +187,7 @@ def _declare(lib: ctypes.CDLL) -> None:
     conv_sigs.declare(lib)
 
 
-ABI_VERSION = 7      # csrc/sumtree.hip apex_abi_version(): the launchers' argument lists
+ABI_VERSION = 8      # csrc/sumtree.hip apex_abi_version(): the launchers' argument lists
 
 
 def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:

@@ -180,9 +180,13 @@ class TorchBackend:
             if len(isn) > 2 and isn[2] is not None:
                 isn[2].add_((w > 0).sum())
 
-    def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor], prio=None, Hon_lo=None):
+    def head_wgrad(self, Hon, dhead, g: Dict[str, torch.Tensor], prio=None, Hon_lo=None, pack=None):
         """``prio = (replay, idx, gen, td_abs)``: also write the batch's priorities back
-        (the HIP backend runs it as one extra block of the same launch)."""
+        (the HIP backend runs it as one extra block of the same launch).  ``pack = (dst,
+        segs)``: also the :meth:`pack_rows` of the DP step's factor rows (HIP: tail blocks
+        of the same launch)."""
+        if pack is not None:
+            self.pack_rows(*pack)
         if prio is not None:
             prio[0].update_priorities(prio[1], prio[3], prio[2])
         B = dhead.shape[0]
@@ -525,16 +529,19 @@ class HipBackend(TorchBackend):
             isn_s.valid_count = _lib.ptr(isn[2]) if len(isn) > 2 else None
         _lib.check(self.lib.apex_ddqn_head(*args, hl, hp, pk, isn_s, _lib.stream_ptr()), "ddqn_head")
 
-    def head_wgrad(self, Hon, dhead, g, prio=None, Hon_lo=None):
+    def head_wgrad(self, Hon, dhead, g, prio=None, Hon_lo=None, pack=None):
         B, A1 = dhead.shape
         if prio is not None and prio[0].use_hip and B <= 1024:
             rp, idx, gen, td = prio
+            pk = self._pack_args(*pack) if pack is not None else (None, None, None, 0, 0, None, 0)
             _lib.check(self.lib.apex_head_wgrad_prio(
                 Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(), g["bv"].data_ptr(),
                 g["wa"].data_ptr(), g["ba"].data_ptr(), g["wv"].numel(), rp.tree_desc(), idx.data_ptr(),
                 td.data_ptr(), _lib.ptr(gen), rp.gen.data_ptr(), rp.alpha, rp.eps, rp.ctr.data_ptr(),
-                _lib.ptr(Hon_lo), _lib.ptr(rp.local_stats), _lib.stream_ptr()), "head_wgrad_prio")
+                _lib.ptr(Hon_lo), _lib.ptr(rp.local_stats), *pk, _lib.stream_ptr()), "head_wgrad_prio")
             return
+        if pack is not None:
+            self.pack_rows(*pack)
         if prio is not None:
             prio[0].update_priorities(prio[1], prio[3], prio[2])
         _lib.check(self.lib.apex_head_wgrad(Hon.data_ptr(), dhead.data_ptr(), B, A1 - 1, g["wv"].data_ptr(),
@@ -608,18 +615,24 @@ class HipBackend(TorchBackend):
                                               st),
                    "rmsprop")
 
-    def pack_rows(self, dst: torch.Tensor, segs) -> None:
-        if dst.dtype not in (torch.bfloat16, torch.float16) or len(segs) > 4:
-            return super().pack_rows(dst, segs)
+    def _pack_args(self, dst: torch.Tensor, segs):
+        """(src*, ld*, cols*, nseg, rows, dst, dst ld) of a row pack (csrc/pack_rows.h); the
+        ctypes arrays stay referenced by this backend until the next call."""
+        assert dst.dtype in (torch.bfloat16, torch.float16) and len(segs) <= 4
         n = len(segs)
         src = (ctypes.c_void_p * 4)(*[t.data_ptr() for t in segs])
         ld = (ctypes.c_int64 * 4)(*[t.stride(0) for t in segs])
         cols = (ctypes.c_int * 4)(*[t.reshape(t.shape[0], -1).shape[1] for t in segs])
         for t in segs:
             assert t.dtype == dst.dtype and t.reshape(t.shape[0], -1).stride(1) == 1 and t.shape[0] == segs[0].shape[0]
-        _lib.check(self.lib.apex_pack_rows(ctypes.addressof(src), ctypes.addressof(ld), ctypes.addressof(cols), n,
-                                           int(segs[0].shape[0]), dst.data_ptr(), int(dst.stride(0)),
-                                           _lib.stream_ptr()), "pack_rows")
+        self._pack_keep = (src, ld, cols)
+        return (ctypes.addressof(src), ctypes.addressof(ld), ctypes.addressof(cols), n, int(segs[0].shape[0]),
+                dst.data_ptr(), int(dst.stride(0)))
+
+    def pack_rows(self, dst: torch.Tensor, segs) -> None:
+        if dst.dtype not in (torch.bfloat16, torch.float16) or len(segs) > 4:
+            return super().pack_rows(dst, segs)
+        _lib.check(self.lib.apex_pack_rows(*self._pack_args(dst, segs), _lib.stream_ptr()), "pack_rows")
 
     def grad_sqnorm_partials(self, g32, partials) -> int:
         """Squared-norm partials of the whole gradient (the optimizer's own pass);
