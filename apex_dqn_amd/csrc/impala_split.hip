@@ -364,7 +364,9 @@ struct ResSDesc {
 
 // All M tiles of an OROWS x WP output grid from the hi / lo LDS plane sets at img
 // (lo set at img + lo_off bytes), relu on the fragments; epi(lh, w, nt, kg, acc)
-template <int P, int NT, int WP, int OROWS, int PLANE, int NTHR, typename Epi>
+// (RELU: apply relu to the staged planes per fragment; false when they were stored
+// relu'd already)
+template <int P, int NT, int WP, int OROWS, int PLANE, int NTHR, bool RELU = true, typename Epi>
 __device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, const bf16_t* __restrict__ wf,
                                                 const bf16_t* __restrict__ wfl, int lane, int wv, Epi epi) {
   constexpr int NCH = (9 * P + 1) / 2, NW = NTHR / 64;
@@ -395,7 +397,7 @@ __device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, 
     for (int c = 0; c < NCH; ++c) {
       uint4 h = *reinterpret_cast<const uint4*>(img + aoff[c] + q0 * 32);
       uint4 l = *reinterpret_cast<const uint4*>(img + lo_off + aoff[c] + q0 * 32);
-      relu_split(h, l);
+      if (RELU) relu_split(h, l);
       const bf16x8 xh = __builtin_bit_cast(bf16x8, h), xl = __builtin_bit_cast(bf16x8, l);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
@@ -428,8 +430,11 @@ __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uin
     const float* __restrict__ b0 = second ? d.b0b : d.b0;
     const bool save = d.ysave != nullptr && n < d.n_save;
     float* __restrict__ ysv = save ? d.ysave + (int64_t)n * d.ysave_img : nullptr;
-    conv_grid_split<P, NT, WP, YROWS, XPL, NTHR>(xs, XLO, second ? d.wf0b : d.wf0, second ? d.wf0b_lo : d.wf0_lo,
-                                                 lane, wv, [&](int lh, int w, int nt, int kg, f32x4 a) {
+    // (x was staged relu'd; conv1's input -- this conv's output -- is stored relu'd: neither
+    // convolution re-applies relu per fragment read, 9 reads per pixel)
+    conv_grid_split<P, NT, WP, YROWS, XPL, NTHR, false>(xs, XLO, second ? d.wf0b : d.wf0,
+                                                        second ? d.wf0b_lo : d.wf0_lo,
+                                                        lane, wv, [&](int lh, int w, int nt, int kg, f32x4 a) {
       if (w >= HW) return;
       const int h = r0 - 1 + lh;
       const bool inside = h >= 0 && h < HW;
@@ -437,8 +442,8 @@ __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uin
       const float v0 = a[0] + b.x, v1 = a[1] + b.y, v2 = a[2] + b.z, v3 = a[3] + b.w;
       uint2 hi = make_uint2(0, 0), lo = make_uint2(0, 0);
       if (inside) {
-        split_pk_bf16(v0, v1, hi.x, lo.x);
-        split_pk_bf16(v2, v3, hi.y, lo.y);
+        split_pk_bf16(fmaxf(v0, 0.f), fmaxf(v1, 0.f), hi.x, lo.x);
+        split_pk_bf16(fmaxf(v2, 0.f), fmaxf(v3, 0.f), hi.y, lo.y);
       }
       const int o = (nt * YPL + lh * WP + w + 1) * 32 + 8 * kg;
       *reinterpret_cast<uint2*>(ys + o) = hi;
@@ -452,18 +457,17 @@ __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uin
     const float* __restrict__ b1 = second ? d.b1b : d.b1;
     const int relu_out = d.relu_out;
     const bool planes = d.out_lo != nullptr;
-    conv_grid_split<P, NT, WP, R, YPL, NTHR>(ys, YLO, second ? d.wf1b : d.wf1, second ? d.wf1b_lo : d.wf1_lo, lane,
-                                             wv, [&](int lh, int w, int nt, int kg, f32x4 a) {
+    conv_grid_split<P, NT, WP, R, YPL, NTHR, false>(ys, YLO, second ? d.wf1b : d.wf1, second ? d.wf1b_lo : d.wf1_lo,
+                                                    lane, wv, [&](int lh, int w, int nt, int kg, f32x4 a) {
       const int h = r0 + lh;
       if (w >= HW || h >= HW) return;
       const float4 b = ld4(b1 + nt * 16 + 4 * kg);
-      const int xo = (nt * XPL + (lh + 2) * WP + w + 1) * 32 + 8 * kg;
-      const uint2 xh = *reinterpret_cast<const uint2*>(xs + xo);
-      const uint2 xl = *reinterpret_cast<const uint2*>(xs + XLO + xo);
-      float v0 = a[0] + b.x + (bf16_to_f32(xh.x & 0xffff) + bf16_to_f32(xl.x & 0xffff));
-      float v1 = a[1] + b.y + (bf16_to_f32(xh.x >> 16) + bf16_to_f32(xl.x >> 16));
-      float v2 = a[2] + b.z + (bf16_to_f32(xh.y & 0xffff) + bf16_to_f32(xl.y & 0xffff));
-      float v3 = a[3] + b.w + (bf16_to_f32(xh.y >> 16) + bf16_to_f32(xl.y >> 16));
+      // the residual: the block's fp32 input itself (the staged planes hold relu(x))
+      const float4 xr = ld4(d.x + (int64_t)n * d.x_img + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg);
+      float v0 = a[0] + b.x + xr.x;
+      float v1 = a[1] + b.y + xr.y;
+      float v2 = a[2] + b.z + xr.z;
+      float v3 = a[3] + b.w + xr.w;
       if (relu_out) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
       const int64_t off = (int64_t)n * d.out_img + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg;
       if (planes) {
@@ -509,7 +513,7 @@ __global__ void __launch_bounds__(512) resblock_fwd_split_kernel(ResSDesc d) {
   uint8_t* ys = smem + 2 * XLO;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int band = blockIdx.x, n = blockIdx.y;
-  stage_rows_split<P, HW, HW, XROWS, NTHR, 4>(xs, XPL, d.x, d.x_img, n, band * R - 2, 0, tid);
+  stage_rows_split<P, HW, HW, XROWS, NTHR, 4>(xs, XPL, d.x, d.x_img, n, band * R - 2, 1, tid);   // relu(x)
   zero_y_halo<P, WP, YROWS, YPL, YLO, NTHR>(ys, tid);
   __syncthreads();
   resblock_item_split<C, HW, R>(d, xs, ys, n, band, lane, wv);
