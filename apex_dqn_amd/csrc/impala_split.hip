@@ -67,14 +67,15 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // the image) of image n as hi planes at xs and lo planes at xs + P * plane_pix * 32;
 // pixels past the SROWS x (W+2) block up to plane_pix are zeroed in both sets.
 // One item = 8 channels (two float4 loads), BATCH items in flight per thread.
-template <int P, int H, int W, int SROWS, int NTHR, int BATCH>
+// ROLLED keeps the batch loop rolled (a caller holding many live accumulators).
+template <int P, int H, int W, int SROWS, int NTHR, int BATCH, bool ROLLED = false>
 __device__ __forceinline__ void stage_rows_split(uint8_t* xs, int plane_pix, const float* x, int64_t x_img, int n,
                                                  int row0, int relu, int tid) {
   constexpr int WP = W + 2, BLK = SROWS * WP;
   constexpr int NCK = P * BLK * 2;
   const float* xi = x + (int64_t)n * x_img;
   uint8_t* xl = xs + P * plane_pix * 32;
-  for (int base = 0; base < NCK; base += NTHR * BATCH) {
+  auto batch = [&](int base) {
     float4 va[BATCH], vb[BATCH];
 #pragma unroll
     for (int k = 0; k < BATCH; ++k) {
@@ -103,6 +104,12 @@ __device__ __forceinline__ void stage_rows_split(uint8_t* xs, int plane_pix, con
         *reinterpret_cast<uint4*>(xl + o) = lo;
       }
     }
+  };
+  if constexpr (ROLLED) {
+#pragma unroll 1
+    for (int base = 0; base < NCK; base += NTHR * BATCH) batch(base);
+  } else {
+    for (int base = 0; base < NCK; base += NTHR * BATCH) batch(base);
   }
   const int slack = plane_pix - BLK;
   for (int i = tid; i < 2 * P * slack * 2; i += NTHR) {
@@ -112,6 +119,58 @@ __device__ __forceinline__ void stage_rows_split(uint8_t* xs, int plane_pix, con
         make_uint4(0, 0, 0, 0);
   }
 }
+
+// stage_rows_split in two halves, every load of the block in flight at once: load()
+// issues them into registers, the caller zero-fills what it needs meanwhile (zero_slack:
+// the plane slack past the SROWS x (W+2) block), store() splits them into the hi / lo
+// planes (resblock 16 ch x 42²: 171 -> 158 µs against the batched stage_rows_split).
+template <int P, int H, int W, int SROWS, int NTHR>
+struct RowLoads {
+  static constexpr int WP = W + 2, BLK = SROWS * WP, NCK = P * BLK * 2, K = (NCK + NTHR - 1) / NTHR;
+  float4 va[K], vb[K];
+  __device__ __forceinline__ void load(const float* x, int64_t x_img, int n, int row0, int tid) {
+    const float* xi = x + (int64_t)n * x_img;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = k * NTHR + tid;
+      const int hf = i & 1, pix = i >> 1;
+      const int p = pix / BLK, rem = pix - (pix / BLK) * BLK;
+      const int lr = rem / WP, c = rem - (rem / WP) * WP;
+      const int h = row0 + lr, w = c - 1;
+      va[k] = vb[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NCK && h >= 0 && h < H && w >= 0 && w < W) {
+        const float* s = xi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8;
+        va[k] = ld4(s);
+        vb[k] = ld4(s + 4);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(uint8_t* xs, int plane_pix, int relu, int tid) const {
+    uint8_t* xl = xs + P * plane_pix * 32;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = k * NTHR + tid;
+      const int hf = i & 1, pix = i >> 1;
+      const int p = pix / BLK, rem = pix - (pix / BLK) * BLK;
+      if (i < NCK) {
+        uint4 hi, lo;
+        split8s(relu ? relu4s(va[k]) : va[k], relu ? relu4s(vb[k]) : vb[k], hi, lo);
+        const int o = (p * plane_pix + rem) * 32 + hf * 16;
+        *reinterpret_cast<uint4*>(xs + o) = hi;
+        *reinterpret_cast<uint4*>(xl + o) = lo;
+      }
+    }
+  }
+  static __device__ __forceinline__ void zero_slack(uint8_t* xs, int plane_pix, int tid) {
+    const int slack = plane_pix - BLK;
+    for (int i = tid; i < 2 * P * slack * 2; i += NTHR) {
+      const int set = i / (P * slack * 2), r0 = i - set * (P * slack * 2);
+      const int p = r0 / (slack * 2), r = r0 - p * slack * 2;
+      *reinterpret_cast<uint4*>(xs + set * P * plane_pix * 32 + (p * plane_pix + BLK) * 32 + r * 16) =
+          make_uint4(0, 0, 0, 0);
+    }
+  }
+};
 
 // The 4 stacked uint8 frames as 4-channel bf16 pixels (8 bytes; exact), rows [row0,
 // row0 + SROWS) x cols [-1, W] of image n (csrc/impala.hip stage_ring4).
@@ -204,6 +263,13 @@ __global__ void __launch_bounds__(512) sconv_fwd_split_kernel(SconvSDesc d) {
   const bf16_t* __restrict__ wfl = second ? d.wf2_lo : d.wf_lo;
   const float* __restrict__ bias = second ? d.bias2 : d.bias;
 
+  // fp32 input rows: every load in flight before the weight loads when they fit in 4
+  // float4 pairs per thread (RowLoads), batched through stage_rows_split otherwise
+  using Rows = RowLoads<P, H, W, SROWS, NTHR>;
+  constexpr bool ONE_BATCH = MODE != 3 && Rows::K <= 4;
+  Rows rows;
+  if constexpr (ONE_BATCH) rows.load(reinterpret_cast<const float*>(d.x), d.x_img, n, o0 - 1, tid);
+
   bf16x8 wh[NCH][NT], wl[NCH][NT];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
@@ -213,11 +279,15 @@ __global__ void __launch_bounds__(512) sconv_fwd_split_kernel(SconvSDesc d) {
       wl[c][nt] = *reinterpret_cast<const bf16x8*>(wfl + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
     }
 
-  if constexpr (MODE == 3)
+  if constexpr (MODE == 3) {
     stage_ring4_split<H, W, SROWS, NTHR>(xs, PLANE, reinterpret_cast<const uint8_t*>(d.x), d.slots, n, o0 - 1, tid);
-  else
+  } else if constexpr (ONE_BATCH) {
+    Rows::zero_slack(xs, PLANE, tid);
+    rows.store(xs, PLANE, d.relu_in, tid);
+  } else {
     stage_rows_split<P, H, W, SROWS, NTHR, 4>(xs, PLANE, reinterpret_cast<const float*>(d.x), d.x_img, n, o0 - 1,
                                               d.relu_in, tid);
+  }
   __syncthreads();
 
   const int kg = lane >> 4;
@@ -416,7 +486,7 @@ __device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, 
 }
 
 // conv0 -> ys, barrier, conv1 (+ x, ReLU) -> out for image n, row band `band`, from the
-// staged x rows (LDS x row 0 = image row band R - 2); shared by both kernels below
+// staged x rows (LDS x row 0 = image row band R - 2)
 template <int C, int HW, int R>
 __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uint8_t* xs, uint8_t* ys, int n, int band,
                                                     int lane, int wv) {
@@ -513,8 +583,12 @@ __global__ void __launch_bounds__(512) resblock_fwd_split_kernel(ResSDesc d) {
   uint8_t* ys = smem + 2 * XLO;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int band = blockIdx.x, n = blockIdx.y;
-  stage_rows_split<P, HW, HW, XROWS, NTHR, 4>(xs, XPL, d.x, d.x_img, n, band * R - 2, 1, tid);   // relu(x)
+  using Rows = RowLoads<P, HW, HW, XROWS, NTHR>;
+  Rows rows;
+  rows.load(d.x, d.x_img, n, band * R - 2, tid);
+  Rows::zero_slack(xs, XPL, tid);
   zero_y_halo<P, WP, YROWS, YPL, YLO, NTHR>(ys, tid);
+  rows.store(xs, XPL, 1, tid);                                  // relu(x)
   __syncthreads();
   resblock_item_split<C, HW, R>(d, xs, ys, n, band, lane, wv);
 }
@@ -544,8 +618,12 @@ __device__ __forceinline__ bf16x8 tr_pix_frag_s(const uint8_t* plane, int pix0, 
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int CIN, int COUT, int H, int W, int R, int MODE>
-__global__ void __launch_bounds__(256) sconv_wgrad_split_kernel(SconvWgSDesc d) {
+template <int CIN, int COUT, int H, int W, int R, int MODE, int NTHR>
+__global__ void __launch_bounds__(NTHR) sconv_wgrad_split_kernel(SconvWgSDesc d) {
+  // NTHR = 512: 8 waves (2 per SIMD), the per-image staging one batch of loads per thread
+  // and the other wave of a SIMD covering the LDS-read latency of the MFMA chain (the
+  // 4-wave form ran one wave per SIMD at 13 % MFMA busy, profiles/r5_pmc_impala_step.md)
+  constexpr int NW = NTHR / 64;
   constexpr int P = CIN / 16, NT = COUT / 16;
   constexpr int WP = W + 2;
   constexpr int NQ = (R * WP + 31) / 32;
@@ -574,12 +652,13 @@ __global__ void __launch_bounds__(256) sconv_wgrad_split_kernel(SconvWgSDesc d) 
 
   for (int n = n_begin; n < n_end; ++n) {
     const float* dyi = d.dy + (int64_t)n * d.dy_img;
-    constexpr int NDC = NT * DPIX * 2, DB = 4;
-    for (int base = 0; base < NDC; base += 256 * DB) {
+    constexpr int NDC = NT * DPIX * 2, DB = NT * P >= 4 ? 2 : 4;   // 32 x 32: 144 accumulator VGPRs live
+#pragma unroll 1
+    for (int base = 0; base < NDC; base += NTHR * DB) {
       float4 va[DB], vb[DB];
 #pragma unroll
       for (int k = 0; k < DB; ++k) {
-        const int i = base + k * 256 + tid;
+        const int i = base + k * NTHR + tid;
         const int hf = i & 1, pix = i >> 1;
         const int p = pix / DPIX, q = pix - (pix / DPIX) * DPIX;
         const int lh = q / WP, w = q - (q / WP) * WP;
@@ -593,7 +672,7 @@ __global__ void __launch_bounds__(256) sconv_wgrad_split_kernel(SconvWgSDesc d) 
       }
 #pragma unroll
       for (int k = 0; k < DB; ++k) {
-        const int i = base + k * 256 + tid;
+        const int i = base + k * NTHR + tid;
         if (i < NDC) {
           uint4 hi, lo;
           split8s(va[k], vb[k], hi, lo);
@@ -603,12 +682,13 @@ __global__ void __launch_bounds__(256) sconv_wgrad_split_kernel(SconvWgSDesc d) 
       }
     }
     if constexpr (MODE == 2)
-      stage_ring16_split<H, W, R + 2, 256>(xs, XPIX, reinterpret_cast<const uint8_t*>(d.x), d.slots, n, r0 - 1, tid);
+      stage_ring16_split<H, W, R + 2, NTHR>(xs, XPIX, reinterpret_cast<const uint8_t*>(d.x), d.slots, n, r0 - 1, tid);
     else
-      stage_rows_split<P, H, W, R + 2, 256, 4>(xs, XPIX, reinterpret_cast<const float*>(d.x), d.x_img, n, r0 - 1,
+      stage_rows_split<P, H, W, R + 2, NTHR, 4, (NT * P >= 4)>(xs, XPIX, reinterpret_cast<const float*>(d.x), d.x_img, n, r0 - 1,
                                                d.relu_in, tid);
     __syncthreads();
-    for (int j = wv; j < NQ; j += 4) {
+#pragma unroll 1
+    for (int j = wv; j < NQ; j += NW) {
       const int qb = 32 * j;
       bf16x8 ah[NT], al[NT];
 #pragma unroll
@@ -644,6 +724,7 @@ __global__ void __launch_bounds__(256) sconv_wgrad_split_kernel(SconvWgSDesc d) 
   const int split = group * gridDim.x + band;
   f32x4* __restrict__ slab = reinterpret_cast<f32x4*>(d.slab) + (int64_t)split * TT * 64;
   f32x4* red = reinterpret_cast<f32x4*>(smem);
+  static_assert(sizeof(smem) >= NW * 4 * 64 * sizeof(f32x4), "reduction slab exceeds the staging LDS");
 #pragma unroll
   for (int base = 0; base < TT; base += 4) {
 #pragma unroll
@@ -653,12 +734,12 @@ __global__ void __launch_bounds__(256) sconv_wgrad_split_kernel(SconvWgSDesc d) 
       else if (tt < TT) red[(wv * 4 + u) * 64 + lane] = accb[tt - T];
     }
     __syncthreads();
-    {
+    if (tid < 256) {
       const int u = tid >> 6, l = tid & 63, tt = base + u;
       if (tt < TT) {
         f32x4 v = red[u * 64 + l];
 #pragma unroll
-        for (int w = 1; w < 4; ++w) v += red[(w * 4 + u) * 64 + l];
+        for (int w = 1; w < NW; ++w) v += red[(w * 4 + u) * 64 + l];
         slab[tt * 64 + l] = v;
       }
     }
@@ -804,21 +885,34 @@ APEX_EXPORT int apex_resblock_fwd_split(ResSDesc d, int C, int HW, int R, hipStr
   return (int)hipErrorInvalidValue;
 }
 
-// the bf16 kernels' wgrad bands (csrc/impala.hip SCONV_WG_SHAPES)
-#define SCONV_WG_S_SHAPES(X) \
-  X(16, 16, 84, 84, 12, 2)   \
-  X(16, 16, 42, 42, 21, 0)   \
-  X(16, 32, 42, 42, 14, 0)   \
-  X(32, 32, 21, 21, 21, 0)   \
-  X(32, 32, 11, 11, 11, 0)
+// weight-gradient shapes (cin, cout, H, W, rows per band, mode, threads); the launcher
+// takes the first match of the requested (rows, threads), 0 = any (ops/impala.py
+// SPLIT_BANDS "wg" keys).  Swept on the fp32 IMPALA step (PERF_NOTES round 5): 11-row
+// bands (2 workgroups per CU where the LDS allows) beat the 21-row single-workgroup form
+// by 3.4 % together; 8 waves per workgroup except where 256 VGPRs need 4.
+#define SCONV_WG_S_SHAPES(X)      \
+  X(16, 16, 84, 84, 12, 2, 512)   \
+  X(16, 16, 42, 42, 11, 0, 512)   \
+  X(16, 32, 42, 42, 7, 0, 256)    \
+  X(32, 32, 21, 21, 11, 0, 512)   \
+  X(32, 32, 11, 11, 11, 0, 256)
 
-APEX_EXPORT int apex_sconv_wgrad_split(SconvWgSDesc d, int cin, int cout, int H, int W, int mode, int groups,
-                                       hipStream_t st) {
+APEX_EXPORT int apex_sconv_wgrad_split_rows(int cin, int cout, int H, int W, int mode, int R, int nthr) {
+#define SCONV_WG_S_ROWS(CI, CO, HH, WW, RR, MM, NT)                                                        \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM && (R == 0 || R == RR) && (nthr == 0 || nthr == NT)) \
+    return RR;
+  SCONV_WG_S_SHAPES(SCONV_WG_S_ROWS)
+#undef SCONV_WG_S_ROWS
+  return 0;
+}
+
+APEX_EXPORT int apex_sconv_wgrad_split(SconvWgSDesc d, int cin, int cout, int H, int W, int mode, int R, int nthr,
+                                       int groups, hipStream_t st) {
   if (d.N <= 0 || groups <= 0) return (int)hipErrorInvalidValue;
-#define SCONV_WG_S_CASE(CI, CO, HH, WW, RR, MM)                                                         \
-  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM) {                                    \
-    sconv_wgrad_split_kernel<CI, CO, HH, WW, RR, MM><<<dim3((HH + RR - 1) / RR, groups), 256, 0, st>>>(d); \
-    APEX_CHECK_LAUNCH();                                                                                 \
+#define SCONV_WG_S_CASE(CI, CO, HH, WW, RR, MM, NT)                                                            \
+  if (cin == CI && cout == CO && H == HH && W == WW && mode == MM && (R == 0 || R == RR) && (nthr == 0 || nthr == NT)) { \
+    sconv_wgrad_split_kernel<CI, CO, HH, WW, RR, MM, NT><<<dim3((HH + RR - 1) / RR, groups), NT, 0, st>>>(d);    \
+    APEX_CHECK_LAUNCH();                                                                                        \
   }
   SCONV_WG_S_SHAPES(SCONV_WG_S_CASE)
 #undef SCONV_WG_S_CASE

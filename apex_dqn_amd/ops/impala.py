@@ -94,7 +94,8 @@ _SIGS = {
     "apex_sconv_frag_elems": ([c_i, c_i], c_i64),
     "apex_sconv_fwd_split": ([SconvSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
     "apex_resblock_fwd_split": ([ResSDesc, c_i, c_i, c_i, c_p], c_i),
-    "apex_sconv_wgrad_split": ([SconvWgSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_sconv_wgrad_split": ([SconvWgSDesc, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_p], c_i),
+    "apex_sconv_wgrad_split_rows": ([c_i, c_i, c_i, c_i, c_i, c_i, c_i], c_i),
     "apex_maxpool_bwd_split": ([c_p, c_i64, c_p, c_i, c_i, c_i, c_p, c_i64, c_i, c_p], c_i),
     "apex_merge_split": ([c_p, c_p, c_p, c_i64, c_p], c_i),
 }
@@ -181,6 +182,10 @@ def _split_bands() -> Dict[tuple, int]:
             a, p = k[2:].split("p")
             ci, co, hw = a.split("x")
             out[("sc", int(ci), int(co), int(hw), int(p))] = int(v)
+        elif k.startswith("wg"):                 # weight gradient: "wg16x16x42=11/512" (rows / threads)
+            ci, co, hw = k[2:].split("x")
+            r, _, t = v.partition("/")
+            out[("wg", int(ci), int(co), int(hw))] = (int(r), int(t or 0))
     return out
 
 
@@ -364,7 +369,13 @@ class HipImpalaOps:
         partials now, reduced by ``finalize(jobs)``."""
         N = dy.shape[0]
         mode = 2 if ring is not None else 0
-        bands = self.lib.apex_sconv_wgrad_bands(spec.cin, spec.cout, spec.H, spec.W, mode)
+        split = dy.dtype == torch.float32
+        if split:
+            R, nthr = SPLIT_BANDS.get(("wg", spec.cin, spec.cout, spec.H), (0, 0))
+            rows = self.lib.apex_sconv_wgrad_split_rows(spec.cin, spec.cout, spec.H, spec.W, mode, R, nthr)
+            bands = (spec.H + rows - 1) // rows if rows > 0 else 0
+        else:
+            bands = self.lib.apex_sconv_wgrad_bands(spec.cin, spec.cout, spec.H, spec.W, mode)
         if bands <= 0:
             raise ValueError(f"no wgrad kernel for {spec}")
         NT, P = spec.cout // 16, spec.cin // 16
@@ -376,7 +387,6 @@ class HipImpalaOps:
         G = (N + ipg - 1) // ipg
         nsplit = bands * G
         slab = self._buf(("slab", spec.name), nsplit * n, dy.device)
-        split = dy.dtype == torch.float32
         d = SconvWgSDesc() if split else SconvWgDesc()
         d.dy, d.dy_img = dy.data_ptr(), img_stride(dy)
         if ring is not None:
@@ -387,7 +397,7 @@ class HipImpalaOps:
         d.N, d.relu_in, d.imgs_per_group, d.cin_real = N, int(relu_in), ipg, spec.cin_real
         if split:
             assert x is None or x.dtype == torch.float32
-            _lib.check(self.lib.apex_sconv_wgrad_split(d, spec.cin, spec.cout, spec.H, spec.W, mode, G,
+            _lib.check(self.lib.apex_sconv_wgrad_split(d, spec.cin, spec.cout, spec.H, spec.W, mode, R, nthr, G,
                                                        _lib.stream_ptr()), f"sconv_wgrad_split[{spec.name}]")
         else:
             _lib.check(self.lib.apex_sconv_wgrad(d, spec.cin, spec.cout, spec.H, spec.W, mode, G, _lib.stream_ptr()),

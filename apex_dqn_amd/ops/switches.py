@@ -64,7 +64,7 @@ class Switches:
     wg_rows2: int = 0
     # IMPALA weight gradients: workgroups per conv and the partial-slab cap (floats)
     impala_wg_target: int = 512
-    impala_slab_cap: int = 2 << 20
+    impala_slab_cap: int = 8 << 20
     # IMPALA bf16 fused residual block rows per band at 16 ch x 42 (swept: 21 777, 14 786, 11 778)
     resblock_r16: int = 14
     # IMPALA split kernels' row bands "key=R;..." (rb16x42 / sc16x16x42p0 ...; '' = defaults)

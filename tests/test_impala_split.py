@@ -168,6 +168,33 @@ def test_split_sconv_wgrad_vs_fp64(cin, cout, H):
         assert _rel(gw, gwr) < TOL and _rel(gb, gbr) < TOL, (relu, _rel(gw, gwr), _rel(gb, gbr))
 
 
+# every (rows, threads) instantiation of the split weight gradient (SCONV_WG_S_SHAPES)
+WG_VARIANTS = [(16, 16, 42, 11, 512), (16, 32, 42, 7, 256), (32, 32, 21, 11, 512), (32, 32, 11, 11, 256)]
+
+
+@pytest.mark.parametrize("cin,cout,H,R,nthr", WG_VARIANTS)
+def test_split_sconv_wgrad_variants_vs_fp64(cin, cout, H, R, nthr, monkeypatch):
+    from apex_dqn_amd.ops import impala as impala_mod
+    hops, tops = _hops(), TorchImpalaOps()
+    assert hops.lib.apex_sconv_wgrad_split_rows(cin, cout, H, H, 0, R, nthr) == R
+    monkeypatch.setitem(impala_mod.SPLIT_BANDS, ("wg", cin, cout, H), (R, nthr))
+    N = 19
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x, dy = _t(N, cin // 16, H, g), _t(N, cout // 16, H, g)
+    cs, ref = _spec(cin, cout, H)
+    gw, gb = torch.zeros(cout, cin, 3, 3, device=DEV), torch.zeros(cout, device=DEV)
+    gwr = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, device=DEV)
+    gbr = torch.zeros(cout, dtype=torch.float64, device=DEV)
+    for groups in (0, 5):
+        gw.zero_(), gb.zero_()
+        jobs = []
+        hops.wgrad(dy, x, cs, gw, gb, jobs, relu_in=True, groups=groups)
+        hops.finalize(jobs)
+        if groups == 0:
+            tops.wgrad(dy.double(), x.double(), ref, gwr, gbr, [], relu_in=True)
+        assert _rel(gw, gwr) < TOL and _rel(gb, gbr) < TOL, (groups, _rel(gw, gwr), _rel(gb, gbr))
+
+
 @pytest.mark.parametrize("C,H", [(16, 42), (32, 21), (32, 11)])
 def test_split_resblock_vs_fp64(C, H):
     hops, tops = _hops(), TorchImpalaOps()
