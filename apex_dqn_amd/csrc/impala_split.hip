@@ -307,6 +307,9 @@ __global__ void __launch_bounds__(512) sconv_fwd_split_kernel(SconvSDesc d) {
   float* __restrict__ yi = d.y + (int64_t)n * d.y_img;
   const float* __restrict__ addi = d.add ? d.add + (int64_t)n * d.add_img : nullptr;
   const float* __restrict__ mski = d.mask ? d.mask + (int64_t)n * d.mask_img : nullptr;
+  float4 bv[NT];                                                // bias: loaded once, not per tile
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) bv[nt] = bias ? ld4(bias + nt * 16 + 4 * kg) : make_float4(0.f, 0.f, 0.f, 0.f);
 
   for (int tile = wv; tile < NTILE; tile += NW) {
     const int q0 = tile * 16;
@@ -347,12 +350,11 @@ __global__ void __launch_bounds__(512) sconv_fwd_split_kernel(SconvSDesc d) {
     if (!valid) continue;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int co = nt * 16 + 4 * kg;
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] * d.scale;
       if (bias) {
-        const float4 b = ld4(bias + co);
+        const float4 b = bv[nt];
         v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
       }
       if (POOL) {
@@ -436,19 +438,41 @@ struct ResSDesc {
 // (lo set at img + lo_off bytes), relu on the fragments; epi(lh, w, nt, kg, acc)
 // (RELU: apply relu to the staged planes per fragment; false when they were stored
 // relu'd already)
-template <int P, int NT, int WP, int OROWS, int PLANE, int NTHR, bool RELU = true, typename Epi>
-__device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, const bf16_t* __restrict__ wf,
-                                                const bf16_t* __restrict__ wfl, int lane, int wv, Epi epi) {
-  constexpr int NCH = (9 * P + 1) / 2, NW = NTHR / 64;
+// Per-tile operand of an epilogue loaded before the tile's MFMA chain (none by default)
+struct NoPrefetch {
+  struct T {};
+  __device__ __forceinline__ T operator()(int, int, int) const { return T{}; }
+};
+
+// All M tiles of an OROWS x WP output grid from the hi / lo LDS plane sets at img (lo set
+// at img + lo_off bytes); pf(lh, w, kg) is issued before each tile's MFMAs (its global
+// loads overlap them instead of stalling the epilogue), epi(lh, w, nt, kg, acc, pf value).
+// RELU: apply relu to the staged planes per fragment (false when stored relu'd already).
+// A convolution's hi / lo weight fragments in registers (loaded by the caller, so their
+// latency can hide behind other work)
+template <int P, int NT>
+struct WFrags {
+  static constexpr int NCH = (9 * P + 1) / 2;
+  bf16x8 h[NCH][NT], l[NCH][NT];
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ wf, const bf16_t* __restrict__ wfl, int lane) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        h[c][nt] = *reinterpret_cast<const bf16x8*>(wf + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
+        l[c][nt] = *reinterpret_cast<const bf16x8*>(wfl + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
+      }
+  }
+};
+
+template <int P, int NT, int WP, int OROWS, int PLANE, int NTHR, bool RELU = true, typename Epi,
+          typename Pf = NoPrefetch>
+__device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, const WFrags<P, NT>& wfr, int lane,
+                                                int wv, Epi epi, Pf pf = Pf()) {
+  constexpr int NCH = WFrags<P, NT>::NCH, NW = NTHR / 64;
   constexpr int NTILE = (OROWS * WP + 15) / 16;
-  bf16x8 wh[NCH][NT], wl[NCH][NT];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) {
-      wh[c][nt] = *reinterpret_cast<const bf16x8*>(wf + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
-      wl[c][nt] = *reinterpret_cast<const bf16x8*>(wfl + ((int64_t)(c * NT + nt) * 64 + lane) * 8);
-    }
+  const auto& wh = wfr.h;
+  const auto& wl = wfr.l;
   const int kg = lane >> 4;
   int aoff[NCH];
 #pragma unroll
@@ -460,6 +484,9 @@ __device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, 
   }
   for (int tile = wv; tile < NTILE; tile += NW) {
     const int q0 = tile * 16;
+    const int q = q0 + (lane & 15);
+    const int lh = q / WP, w = q - (q / WP) * WP;
+    const auto pre = pf(lh, w, kg);
     f32x4 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -476,11 +503,9 @@ __device__ __forceinline__ void conv_grid_split(const uint8_t* img, int lo_off, 
         acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh[c][nt], xl, acc[nt], 0, 0, 0);
       }
     }
-    const int q = q0 + (lane & 15);
-    const int lh = q / WP, w = q - (q / WP) * WP;
     if (lh < OROWS) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) epi(lh, w, nt, kg, acc[nt]);
+      for (int nt = 0; nt < NT; ++nt) epi(lh, w, nt, kg, acc[nt], pre);
     }
   }
 }
@@ -502,13 +527,17 @@ __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uin
     float* __restrict__ ysv = save ? d.ysave + (int64_t)n * d.ysave_img : nullptr;
     // (x was staged relu'd; conv1's input -- this conv's output -- is stored relu'd: neither
     // convolution re-applies relu per fragment read, 9 reads per pixel)
-    conv_grid_split<P, NT, WP, YROWS, XPL, NTHR, false>(xs, XLO, second ? d.wf0b : d.wf0,
-                                                        second ? d.wf0b_lo : d.wf0_lo,
-                                                        lane, wv, [&](int lh, int w, int nt, int kg, f32x4 a) {
+    float4 bias[NT];                                            // loaded once, not per tile
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bias[nt] = ld4(b0 + nt * 16 + 4 * (lane >> 4));
+    WFrags<P, NT> w0;
+    w0.load(second ? d.wf0b : d.wf0, second ? d.wf0b_lo : d.wf0_lo, lane);
+    conv_grid_split<P, NT, WP, YROWS, XPL, NTHR, false>(xs, XLO, w0, lane, wv, [&](int lh, int w, int nt, int kg,
+                                                                                  f32x4 a, NoPrefetch::T) {
       if (w >= HW) return;
       const int h = r0 - 1 + lh;
       const bool inside = h >= 0 && h < HW;
-      const float4 b = ld4(b0 + nt * 16 + 4 * kg);
+      const float4 b = bias[nt];
       const float v0 = a[0] + b.x, v1 = a[1] + b.y, v2 = a[2] + b.z, v3 = a[3] + b.w;
       uint2 hi = make_uint2(0, 0), lo = make_uint2(0, 0);
       if (inside) {
@@ -527,13 +556,32 @@ __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uin
     const float* __restrict__ b1 = second ? d.b1b : d.b1;
     const int relu_out = d.relu_out;
     const bool planes = d.out_lo != nullptr;
-    conv_grid_split<P, NT, WP, R, YPL, NTHR, false>(ys, YLO, second ? d.wf1b : d.wf1, second ? d.wf1b_lo : d.wf1_lo,
-                                                    lane, wv, [&](int lh, int w, int nt, int kg, f32x4 a) {
+    float4 bias[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bias[nt] = ld4(b1 + nt * 16 + 4 * (lane >> 4));
+    // the residual -- the block's fp32 input itself (the staged planes hold relu(x)) --
+    // loaded before each tile's MFMAs
+    struct Res {
+      float4 v[NT];
+    };
+    const float* __restrict__ xn = d.x + (int64_t)n * d.x_img;
+    auto residual = [&](int lh, int w, int kg) {
+      Res r;
+      const int h = r0 + lh;
+      const bool ok = lh < R && w < HW && h < HW;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        r.v[nt] = ok ? ld4(xn + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg) : make_float4(0.f, 0.f, 0.f, 0.f);
+      return r;
+    };
+    WFrags<P, NT> w1;
+    w1.load(second ? d.wf1b : d.wf1, second ? d.wf1b_lo : d.wf1_lo, lane);
+    conv_grid_split<P, NT, WP, R, YPL, NTHR, false>(ys, YLO, w1, lane, wv, [&](int lh, int w, int nt, int kg, f32x4 a,
+                                                                              const Res& res) {
       const int h = r0 + lh;
       if (w >= HW || h >= HW) return;
-      const float4 b = ld4(b1 + nt * 16 + 4 * kg);
-      // the residual: the block's fp32 input itself (the staged planes hold relu(x))
-      const float4 xr = ld4(d.x + (int64_t)n * d.x_img + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg);
+      const float4 b = bias[nt];
+      const float4 xr = res.v[nt];
       float v0 = a[0] + b.x + xr.x;
       float v1 = a[1] + b.y + xr.y;
       float v2 = a[2] + b.z + xr.z;
@@ -549,7 +597,7 @@ __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uin
       } else {
         *reinterpret_cast<float4*>(reinterpret_cast<float*>(d.out) + off) = make_float4(v0, v1, v2, v3);
       }
-    });
+    }, residual);
   }
 }
 
@@ -828,6 +876,7 @@ __global__ void __launch_bounds__(256) merge_split_kernel(const bf16_t* __restri
 // variants -- fewer staged rows per workgroup, more workgroups per CU -- chosen by the
 // host, ops/impala.py SPLIT_BANDS)
 #define SCONV_S_SHAPES(X)       \
+  X(16, 16, 84, 84, 6, 3, 1)    \
   X(16, 16, 84, 84, 10, 3, 1)   \
   X(16, 32, 42, 42, 14, 0, 1)   \
   X(16, 32, 42, 42, 6, 0, 1)    \

@@ -169,8 +169,10 @@ def _split_bands() -> Dict[tuple, int]:
     keys like rb16x42 / sc16x16x42p0 overrides (APEX_SWITCHES sweeps)."""
     # defaults from the band sweep (profiles/r3_impala_split_band_sweep.txt: each +0.6 to
     # +2.4 % on the fp32 IMPALA step; 2 workgroups per CU where the 16-channel shapes fit)
+    # round 5: the stack-1 pooled conv at 6 rows (3 workgroups per CU; 472.6-473.2 vs
+    # 470.0-470.2 updates/s at 10, 469.4-470.5 at 4)
     out: Dict[tuple, int] = {("rb", 16, 42): 7, ("sc", 16, 16, 42, 0): 21, ("sc", 32, 16, 42, 0): 11,
-                             ("sc", 16, 32, 42, 1): 6}
+                             ("sc", 16, 32, 42, 1): 6, ("sc", 16, 16, 84, 1): 6}
     for item in SW.isplit_bands.split(";"):
         if "=" not in item:
             continue
