@@ -289,6 +289,10 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
   bf16_t* __restrict__ yi = d.y + (int64_t)n * d.y_img;
   const bf16_t* __restrict__ addi = d.add ? d.add + (int64_t)n * d.add_img : nullptr;
   const bf16_t* __restrict__ mski = d.mask ? d.mask + (int64_t)n * d.mask_img : nullptr;
+  float4 bv[NT];                                   // bias: loaded once, not per tile epilogue
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) bv[nt] = bias ? *reinterpret_cast<const float4*>(bias + nt * 16 + 4 * kg)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
 
   for (int tile = wv; tile < NTILE; tile += NW) {
     const int q0 = tile * 16;
@@ -329,12 +333,11 @@ __global__ void __launch_bounds__(512) sconv_fwd_kernel(SconvDesc d) {
     if (!valid) continue;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int co = nt * 16 + 4 * kg;
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] * d.scale;
       if (bias) {
-        const float4 b = *reinterpret_cast<const float4*>(bias + co);
+        const float4 b = bv[nt];
         v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
       }
       if (POOL) {
@@ -534,12 +537,15 @@ __global__ void __launch_bounds__(512) resblock_fwd_kernel(ResDesc d) {
     const float* __restrict__ b0 = second ? d.b0b : d.b0;
     const bool save = d.ysave != nullptr && n < d.n_save;
     bf16_t* __restrict__ ysv = save ? d.ysave + (int64_t)n * d.ysave_img : nullptr;
+    float4 bias[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bias[nt] = *reinterpret_cast<const float4*>(b0 + nt * 16 + 4 * (lane >> 4));
     conv_grid<P, NT, WP, YROWS, XPL, NTHR>(xs, second ? d.wf0b : d.wf0, true, lane, wv,
       [&](int lh, int w, int nt, int kg, f32x4 a) {
         if (w >= HW) return;                   // padded-width garbage columns
         const int h = r0 - 1 + lh;
         const bool inside = h >= 0 && h < HW;
-        const float4 b = *reinterpret_cast<const float4*>(b0 + nt * 16 + 4 * kg);
+        const float4 b = bias[nt];
         const uint2 v = inside ? make_uint2(cvt_pk_bf16(a[0] + b.x, a[1] + b.y), cvt_pk_bf16(a[2] + b.z, a[3] + b.w))
                                : make_uint2(0, 0);
         *reinterpret_cast<uint2*>(ys + (nt * YPL + lh * WP + w + 1) * 32 + 8 * kg) = v;
@@ -553,11 +559,14 @@ __global__ void __launch_bounds__(512) resblock_fwd_kernel(ResDesc d) {
     const float* __restrict__ b1 = second ? d.b1b : d.b1;
     bf16_t* __restrict__ oi = d.out + (int64_t)n * d.out_img;
     const int relu_out = d.relu_out;
+    float4 bias[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) bias[nt] = *reinterpret_cast<const float4*>(b1 + nt * 16 + 4 * (lane >> 4));
     conv_grid<P, NT, WP, R, YPL, NTHR>(ys, second ? d.wf1b : d.wf1, true, lane, wv,
       [&](int lh, int w, int nt, int kg, f32x4 a) {
         const int h = r0 + lh;
         if (w >= HW || h >= HW) return;
-        const float4 b = *reinterpret_cast<const float4*>(b1 + nt * 16 + 4 * kg);
+        const float4 b = bias[nt];
         const uint2 xv = *reinterpret_cast<const uint2*>(xs + (nt * XPL + (lh + 2) * WP + w + 1) * 32 + 8 * kg);
         float v0 = a[0] + b.x + bf16_to_f32(xv.x & 0xffff), v1 = a[1] + b.y + bf16_to_f32(xv.x >> 16);
         float v2 = a[2] + b.z + bf16_to_f32(xv.y & 0xffff), v3 = a[3] + b.w + bf16_to_f32(xv.y >> 16);
