@@ -652,6 +652,10 @@ struct SconvWgSDesc {
   int64_t dy_img, x_img;
   int N, relu_in;
   int imgs_per_group, cin_real;
+  // mode 2 with amax set: dy is the gradient of the 3x3/s2 max pool that follows this conv
+  // ([HO][WO][16] per plane, dy_img its image stride) and amax its argmax codes; the conv
+  // output gradient is formed while staging (maxpool_bwd_split_kernel's sums, same order)
+  const uint8_t* amax;
 };
 
 // csrc/impala.hip tr_pix_frag: channel (lane & 15) of pixels 16h + 4(lane >> 4) + {0..3}
@@ -698,11 +702,74 @@ __global__ void __launch_bounds__(NTHR) sconv_wgrad_split_kernel(SconvWgSDesc d)
   }
   const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u));
 
+  // fused max-pool backward (mode 2): the band's 2 x 2 pixel blocks, one per (block,
+  // 8-channel half); the pad pixels of the dy planes (columns W, W+1 of each row, rows past
+  // the band / image, the tail) are never written by it: zeroed once here
+  constexpr bool POOLED = MODE == 2 && NT == 1 && (R % 2) == 0 && (H % 2) == 0 && (W % 2) == 0;
+  const bool pooled = POOLED && d.amax != nullptr;
+  if (POOLED && pooled) {
+    for (int q = tid; q < DPIX; q += NTHR) {
+      const int lh = q / WP, w = q - (q / WP) * WP;
+      if (lh < R && w < W && r0 + lh < H) continue;
+#pragma unroll
+      for (int set = 0; set < 2; ++set) {
+        *reinterpret_cast<uint4*>(dys + set * DLO + q * 32) = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(dys + set * DLO + q * 32 + 16) = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+
   for (int n = n_begin; n < n_end; ++n) {
     const float* dyi = d.dy + (int64_t)n * d.dy_img;
     constexpr int NDC = NT * DPIX * 2, DB = NT * P >= 4 ? 2 : 4;   // 32 x 32: 144 accumulator VGPRs live
+    if constexpr (POOLED) {
+      if (pooled) {
+        constexpr int HO = H / 2, WO = W / 2, NBLK = (R / 2) * WO * 2;
+        const uint8_t* ami = d.amax + (int64_t)n * HO * WO * 16;
+        for (int it = tid; it < NBLK; it += NTHR) {
+          const int hf = it & 1, rest = it >> 1;
+          const int al = rest / WO, b = rest - (rest / WO) * WO;
+          const int a = (r0 >> 1) + al;
+          if (2 * a >= H) continue;
+          const bool i1 = a + 1 < HO, j1 = b + 1 < WO;
+          float4 g0[4], g1[4];
+          uint2 cv[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int oh = (k >> 1) && i1 ? a + 1 : a, ow = (k & 1) && j1 ? b + 1 : b;
+            const int64_t po = ((int64_t)oh * WO + ow) * 16 + 8 * hf;
+            g0[k] = ld4(dyi + po);
+            g1[k] = ld4(dyi + po + 4);
+            cv[k] = *reinterpret_cast<const uint2*>(ami + po);
+          }
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh)
+#pragma unroll
+            for (int dw = 0; dw < 2; ++dw) {
+              const int khs[2] = {1 + dh, (dh && i1) ? 0 : -16}, kws[2] = {1 + dw, (dw && j1) ? 0 : -16};
+              float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int want = khs[k >> 1] * 3 + kws[k & 1];
+                const float gv[8] = {g0[k].x, g0[k].y, g0[k].z, g0[k].w, g1[k].x, g1[k].y, g1[k].z, g1[k].w};
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                  const uint32_t word = c < 4 ? cv[k].x : cv[k].y;
+                  acc8[c] += (int)((word >> (8 * (c & 3))) & 0xffu) == want ? gv[c] : 0.f;
+                }
+              }
+              uint4 hi, lo;
+              split8s(make_float4(acc8[0], acc8[1], acc8[2], acc8[3]), make_float4(acc8[4], acc8[5], acc8[6], acc8[7]),
+                      hi, lo);
+              const int q = (2 * al + dh) * WP + 2 * b + dw;
+              *reinterpret_cast<uint4*>(dys + q * 32 + hf * 16) = hi;
+              *reinterpret_cast<uint4*>(dys + DLO + q * 32 + hf * 16) = lo;
+            }
+        }
+      }
+    }
 #pragma unroll 1
-    for (int base = 0; base < NDC; base += NTHR * DB) {
+    for (int base = 0; base < (pooled ? 0 : NDC); base += NTHR * DB) {
       float4 va[DB], vb[DB];
 #pragma unroll
       for (int k = 0; k < DB; ++k) {

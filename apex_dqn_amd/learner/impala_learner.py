@@ -410,8 +410,14 @@ class FusedImpalaLearner(IsNormMixin):
             wgrad(b["d_ra"], f["ya"][:B], r0b, *gw(r0b), jobs, relu_in=True)
             io.conv(b["d_ya"], r0a, b["d_p"], transpose=True, mask=f["p"][:B], add=b["d_ra"])
             wgrad(b["d_ya"], f["p"][:B], r0a, *gw(r0a), jobs, relu_in=True)
-            # max-pool backward (gather form, csrc/impala.hip maxpool_bwd_kernel); staging
-            # it inside the two consumers measured slower (round 1) and was removed
+            if s == 0 and SW.impala_pool_wgrad:
+                # stack 1's conv has one consumer of its output gradient (the ring conv's
+                # weight gradient): the max-pool backward runs inside that kernel's staging
+                # (split) and the 84² gradient is never written
+                wgrad(b["d_p"], None, c0, *gw(c0), jobs, ring=self.replay.frames, slots=self.slots[:B],
+                      scale=self.rt.obs_scale, pool_amax=f["amax"][:B])
+                continue
+            # max-pool backward (gather form, csrc/impala_split.hip maxpool_bwd_split_kernel)
             io.maxpool_bwd(b["d_p"], f["amax"][:B], b["d_c0"])
             dc = b["d_c0"]
             if s == 0:

@@ -13,6 +13,7 @@ the CPU path and the numerics oracle of every kernel (tests/test_impala.py).
 from __future__ import annotations
 
 import ctypes
+import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -79,7 +80,7 @@ class ResSDesc(ctypes.Structure):
 
 class SconvWgSDesc(ctypes.Structure):
     _fields_ = [("dy", c_p), ("x", c_p), ("slots", c_p), ("slab", c_p), ("dy_img", c_i64), ("x_img", c_i64),
-                ("N", c_i), ("relu_in", c_i), ("imgs_per_group", c_i), ("cin_real", c_i)]
+                ("N", c_i), ("relu_in", c_i), ("imgs_per_group", c_i), ("cin_real", c_i), ("amax", c_p)]
 
 
 _SIGS = {
@@ -366,12 +367,21 @@ class HipImpalaOps:
                                              _lib.stream_ptr()), "merge_split")
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
-              groups: int = 0, scale: float = 1.0) -> None:
+              groups: int = 0, scale: float = 1.0, pool_amax=None) -> None:
         """gw = scale * sum dy (x) im2col(x') (x' = relu(x) if relu_in), gb = sum dy:
-        partials now, reduced by ``finalize(jobs)``."""
+        partials now, reduced by ``finalize(jobs)``.  pool_amax: dy is the gradient of
+        the 3x3/s2 max pool after this conv (its argmax codes); the split ring conv forms
+        the conv output gradient inside its staging, the others through maxpool_bwd."""
         N = dy.shape[0]
         mode = 2 if ring is not None else 0
         split = dy.dtype == torch.float32
+        fuse_pool = pool_amax is not None and split and mode == 2
+        if pool_amax is not None and not fuse_pool:
+            shape = (N, spec.cout // 16, spec.H, spec.W, 16)
+            full = self._buf(("pool_dx", spec.name), math.prod(shape), dy.device, dy.dtype)[:math.prod(shape)]
+            full = full.view(shape)
+            self.maxpool_bwd(dy, pool_amax, full)
+            dy = full
         if split:
             R, nthr = SPLIT_BANDS.get(("wg", spec.cin, spec.cout, spec.H), (0, 0))
             rows = self.lib.apex_sconv_wgrad_split_rows(spec.cin, spec.cout, spec.H, spec.W, mode, R, nthr)
@@ -398,6 +408,7 @@ class HipImpalaOps:
         d.slab = slab.data_ptr()
         d.N, d.relu_in, d.imgs_per_group, d.cin_real = N, int(relu_in), ipg, spec.cin_real
         if split:
+            d.amax = pool_amax.data_ptr() if fuse_pool else None
             assert x is None or x.dtype == torch.float32
             _lib.check(self.lib.apex_sconv_wgrad_split(d, spec.cin, spec.cout, spec.H, spec.W, mode, R, nthr, G,
                                                        _lib.stream_ptr()), f"sconv_wgrad_split[{spec.name}]")
@@ -522,7 +533,11 @@ class TorchImpalaOps:
         y.copy_(o.to(y.dtype))
 
     def wgrad(self, dy, x, spec: ConvSpec, gw, gb, jobs: list, *, relu_in=False, ring=None, slots=None,
-              groups: int = 0, scale: float = 1.0) -> None:
+              groups: int = 0, scale: float = 1.0, pool_amax=None) -> None:
+        if pool_amax is not None:
+            full = torch.zeros(dy.shape[0], spec.cout // 16, spec.H, spec.W, 16, dtype=dy.dtype, device=dy.device)
+            self.maxpool_bwd(dy, pool_amax, full)
+            dy = full
         cdt = torch.float64 if gw.dtype == torch.float64 else torch.float32
         if ring is not None:
             xin = ring_frames(ring, slots).to(cdt)

@@ -67,6 +67,8 @@ class Switches:
     impala_slab_cap: int = 8 << 20
     # IMPALA bf16 fused residual block rows per band at 16 ch x 42 (swept: 21 777, 14 786, 11 778)
     resblock_r16: int = 14
+    # IMPALA stack 1: the max-pool backward inside the ring conv's weight-gradient staging
+    impala_pool_wgrad: bool = True
     # IMPALA split kernels' row bands "key=R;..." (rb16x42 / sc16x16x42p0 ...; '' = defaults)
     isplit_bands: str = ""
 

@@ -147,6 +147,42 @@ def test_split_ring_conv_pool_and_wgrad_vs_fp64():
     assert _rel(gw, gwr) < TOL and _rel(gb, gbr) < TOL
 
 
+@pytest.mark.parametrize("N,groups", [(5, 0), (37, 0), (37, 6)])
+def test_ring_wgrad_fused_pool_backward_bit_identical(N, groups):
+    """The ring conv's weight gradient straight from the pooled gradient + argmax codes
+    (max-pool backward inside its staging) equals max-pool backward then weight gradient
+    bit for bit, and the fp64 oracle within tolerance."""
+    hops, tops = _hops(), TorchImpalaOps()
+    g = torch.Generator(device=DEV).manual_seed(8)
+    ring = _ring(g)
+    slots = torch.randint(0, 80, (N, 4), generator=g, dtype=torch.int32, device=DEV)
+    cs, ref = _spec(16, 16, 84, cin_real=4, seed=9)
+    # argmax codes from a real max pool (ties make some pixels take several windows)
+    x = torch.randn(N, 1, 84, 84, 16, generator=g, device=DEV).round()
+    p = torch.zeros(N, 1, 42, 42, 16, dtype=torch.float32, device=DEV)
+    a = torch.zeros(N, 1, 42, 42, 16, dtype=torch.uint8, device=DEV)
+    tops.maxpool(x, p, a)
+    dp = _t(N, 1, 42, g)
+    kw = dict(ring=ring, slots=slots, scale=1.0 / 255, groups=groups)
+    outs = []
+    for fused in (True, False):
+        gw, gb = torch.zeros(16, 4, 3, 3, device=DEV), torch.zeros(16, device=DEV)
+        jobs = []
+        if fused:
+            hops.wgrad(dp, None, cs, gw, gb, jobs, pool_amax=a, **kw)
+        else:
+            dc = torch.zeros(N, 1, 84, 84, 16, device=DEV)
+            hops.maxpool_bwd(dp, a, dc)
+            hops.wgrad(dc, None, cs, gw, gb, jobs, **kw)
+        hops.finalize(jobs)
+        outs.append((gw, gb))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    gwr = torch.zeros(16, 4, 3, 3, dtype=torch.float64, device=DEV)
+    gbr = torch.zeros(16, dtype=torch.float64, device=DEV)
+    tops.wgrad(dp.double(), None, ref, gwr, gbr, [], pool_amax=a, ring=ring, slots=slots, scale=1.0 / 255)
+    assert _rel(outs[0][0], gwr) < TOL and _rel(outs[0][1], gbr) < TOL
+
+
 WG_SHAPES = [(16, 16, 42), (16, 32, 42), (32, 32, 21), (32, 32, 11)]
 
 
