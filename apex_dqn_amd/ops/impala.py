@@ -172,8 +172,10 @@ def _split_bands() -> Dict[tuple, int]:
     # +2.4 % on the fp32 IMPALA step; 2 workgroups per CU where the 16-channel shapes fit)
     # round 5: the stack-1 pooled conv at 6 rows (3 workgroups per CU; 472.6-473.2 vs
     # 470.0-470.2 updates/s at 10, 469.4-470.5 at 4)
+    # the 32 x 32 x 21² weight gradients at 256 workgroups (128 per band: half the partial
+    # slab for the reduce; 504.3-505.1 vs 497.9-498.3 at 512, 491.1-492.2 at 128)
     out: Dict[tuple, int] = {("rb", 16, 42): 7, ("sc", 16, 16, 42, 0): 21, ("sc", 32, 16, 42, 0): 11,
-                             ("sc", 16, 32, 42, 1): 6, ("sc", 16, 16, 84, 1): 6}
+                             ("sc", 16, 32, 42, 1): 6, ("sc", 16, 16, 84, 1): 6, ("wt", 32, 32, 21): 256}
     for item in SW.isplit_bands.split(";"):
         if "=" not in item:
             continue
@@ -185,6 +187,9 @@ def _split_bands() -> Dict[tuple, int]:
             a, p = k[2:].split("p")
             ci, co, hw = a.split("x")
             out[("sc", int(ci), int(co), int(hw), int(p))] = int(v)
+        elif k.startswith("wt"):                 # weight-gradient workgroup target: "wt32x32x11=128"
+            ci, co, hw = k[2:].split("x")
+            out[("wt", int(ci), int(co), int(hw))] = int(v)
         elif k.startswith("wg"):                 # weight gradient: "wg16x16x42=11/512" (rows / threads)
             ci, co, hw = k[2:].split("x")
             r, _, t = v.partition("/")
@@ -392,7 +397,8 @@ class HipImpalaOps:
             raise ValueError(f"no wgrad kernel for {spec}")
         NT, P = spec.cout // 16, spec.cin // 16
         n = (NT * 9 * P + NT) * 256          # partial floats per split (accumulator order)
-        G = groups or max(1, min(N, WGRAD_TUNING["target_wgs"] // bands))
+        target = SPLIT_BANDS.get(("wt", spec.cin, spec.cout, spec.H), WGRAD_TUNING["target_wgs"])
+        G = groups or max(1, min(N, target // bands))
         while not groups and G > 32 and bands * G * n > WGRAD_TUNING["slab_cap"]:   # slab floats
             G //= 2
         ipg = (N + G - 1) // G
