@@ -549,7 +549,10 @@ __device__ __forceinline__ void resblock_item_split(const ResSDesc& d, const uin
       *reinterpret_cast<uint2*>(ys + o) = hi;
       *reinterpret_cast<uint2*>(ys + YLO + o) = lo;
       if (ysv != nullptr && lh >= 1 && lh <= R && h < HW)
-        *reinterpret_cast<float4*>(ysv + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg) = make_float4(v0, v1, v2, v3);
+        // (read back only by the backward, after the rest of the forward: a non-temporal
+        // store keeps it out of the caches the forward is using -- +0.7 %)
+        __builtin_nontemporal_store((f32x4){v0, v1, v2, v3},
+                                    reinterpret_cast<f32x4*>(ysv + ((int64_t)(nt * HW + h) * HW + w) * 16 + 4 * kg));
     });
   }
   __syncthreads();
