@@ -69,7 +69,10 @@ class Switches:
     resblock_r16: int = 14
     # IMPALA stack 1: the max-pool backward inside the ring conv's weight-gradient staging
     impala_pool_wgrad: bool = True
-    # IMPALA split kernels' row bands "key=R;..." (rb16x42 / sc16x16x42p0 ...; '' = defaults)
+    # IMPALA split kernels' launch shapes "key=value;..." ('' = the defaults of
+    # ops/impala.py _split_bands): rb<C>x<H>=R (residual block rows), sc<cin>x<cout>x<H>p<pool>=R
+    # (conv rows), wg<cin>x<cout>x<H>=R/threads (weight-gradient variant), wt<cin>x<cout>x<H>=N
+    # (weight-gradient workgroup target)
     isplit_bands: str = ""
 
     @classmethod
