@@ -157,3 +157,22 @@ def test_reference_checkpoint_q_values_at_raw_pixel_scale(tmp_path, with_config)
     q = L.q_values(x)
     q_ref = _reference_forward_q(sd, x.float() * scale)
     torch.testing.assert_close(q, q_ref, rtol=1e-4, atol=1e-4 * float(q_ref.abs().max()))
+
+
+def test_kernel_switches_and_impala_launch_shape_keys(monkeypatch):
+    """APEX_SWITCHES parsing (one registry) and the IMPALA launch-shape keys of
+    SW.isplit_bands (rb / sc / wg / wt), defaults included."""
+    from apex_dqn_amd.ops import impala
+    from apex_dqn_amd.ops.switches import SW, Switches
+    sw = Switches.from_env("impala_wg_target=256,isplit_bands=rb16x42=10;wg32x32x21=11/256;wt32x32x11=128;"
+                           "sc16x32x42p1=14")
+    assert sw.impala_wg_target == 256 and sw.non_default().keys() == {"impala_wg_target", "isplit_bands"}
+    with pytest.raises(ValueError):
+        Switches.from_env("no_such_switch=1")
+    defaults = impala._split_bands()
+    assert defaults[("sc", 16, 16, 84, 1)] == 6 and defaults[("wt", 32, 32, 21)] == 256
+    monkeypatch.setattr(SW, "isplit_bands", sw.isplit_bands)
+    b = impala._split_bands()
+    assert b[("rb", 16, 42)] == 10 and b[("sc", 16, 32, 42, 1)] == 14
+    assert b[("wg", 32, 32, 21)] == (11, 256) and b[("wt", 32, 32, 11)] == 128
+    assert b[("wt", 32, 32, 21)] == 256          # untouched defaults survive an override list
