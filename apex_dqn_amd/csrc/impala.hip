@@ -63,6 +63,10 @@ struct SconvWgDesc {
   int64_t dy_img, x_img;
   int N, relu_in;
   int imgs_per_group, cin_real;
+  // mode 2 with amax set: dy is the gradient of the 3x3/s2 max pool after this conv (its
+  // argmax codes here); the conv output gradient is gathered while staging (pool_grad8,
+  // maxpool_bwd_kernel's arithmetic: bit-identical)
+  const uint8_t* amax;
 };
 
 __device__ __forceinline__ uint4 relu_u4(uint4 v) {
@@ -655,8 +659,12 @@ __global__ void __launch_bounds__(256) sconv_wgrad_kernel(SconvWgDesc d) {
         const int lh = q / WP, w = q - (q / WP) * WP;
         const int h = r0 + lh;
         v[k] = make_uint4(0, 0, 0, 0);
-        if (i < NDC && lh < R && w < W && h < H)
-          v[k] = *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+        if (i < NDC && lh < R && w < W && h < H) {
+          if (MODE == 2 && d.amax != nullptr)
+            v[k] = pool_grad8<H, W>(dyi, d.amax + (int64_t)n * NT * ((H + 1) / 2) * ((W + 1) / 2) * 16, p, h, w, hf);
+          else
+            v[k] = *reinterpret_cast<const uint4*>(dyi + ((int64_t)(p * H + h) * W + w) * 16 + hf * 8);
+        }
       }
 #pragma unroll
       for (int k = 0; k < DB; ++k) {

@@ -36,7 +36,7 @@ class SconvDesc(ctypes.Structure):
 class SconvWgDesc(ctypes.Structure):
     _fields_ = [("dy", c_p), ("x", c_p), ("slots", c_p), ("slab", c_p), ("bslab", c_p),
                 ("dy_img", c_i64), ("x_img", c_i64), ("N", c_i), ("relu_in", c_i),
-                ("imgs_per_group", c_i), ("cin_real", c_i)]
+                ("imgs_per_group", c_i), ("cin_real", c_i), ("amax", c_p)]
 
 
 class ResDesc(ctypes.Structure):
@@ -375,12 +375,13 @@ class HipImpalaOps:
               groups: int = 0, scale: float = 1.0, pool_amax=None) -> None:
         """gw = scale * sum dy (x) im2col(x') (x' = relu(x) if relu_in), gb = sum dy:
         partials now, reduced by ``finalize(jobs)``.  pool_amax: dy is the gradient of
-        the 3x3/s2 max pool after this conv (its argmax codes); the split ring conv forms
-        the conv output gradient inside its staging, the others through maxpool_bwd."""
+        the 3x3/s2 max pool after this conv (its argmax codes); the ring conv (both
+        precisions) forms the conv output gradient inside its staging, the others get it
+        from maxpool_bwd."""
         N = dy.shape[0]
         mode = 2 if ring is not None else 0
         split = dy.dtype == torch.float32
-        fuse_pool = pool_amax is not None and split and mode == 2
+        fuse_pool = pool_amax is not None and mode == 2
         if pool_amax is not None and not fuse_pool:
             shape = (N, spec.cout // 16, spec.H, spec.W, 16)
             full = self._buf(("pool_dx", spec.name), math.prod(shape), dy.device, dy.dtype)[:math.prod(shape)]
@@ -413,8 +414,8 @@ class HipImpalaOps:
             d.x, d.x_img = x.data_ptr(), img_stride(x)
         d.slab = slab.data_ptr()
         d.N, d.relu_in, d.imgs_per_group, d.cin_real = N, int(relu_in), ipg, spec.cin_real
+        d.amax = pool_amax.data_ptr() if fuse_pool else None
         if split:
-            d.amax = pool_amax.data_ptr() if fuse_pool else None
             assert x is None or x.dtype == torch.float32
             _lib.check(self.lib.apex_sconv_wgrad_split(d, spec.cin, spec.cout, spec.H, spec.W, mode, R, nthr, G,
                                                        _lib.stream_ptr()), f"sconv_wgrad_split[{spec.name}]")

@@ -214,6 +214,38 @@ def test_gpu_sconv_ring_input():
     torch.testing.assert_close(gb, gbr, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.gpu
+def test_gpu_ring_wgrad_fused_pool_backward_bit_identical():
+    """bf16: the ring conv's weight gradient straight from the pooled gradient + argmax
+    codes equals max-pool backward then weight gradient bit for bit."""
+    from apex_dqn_amd.ops.impala import HipImpalaOps
+    dev = torch.device("cuda")
+    cfg, rp = _setup(device=dev)
+    hops, tops = HipImpalaOps(), TorchImpalaOps()
+    cs = _spec(16, 16, 84, dev, cin_real=4)
+    _hip_pack(hops, cs, dev)
+    N = 9
+    slots = torch.randint(0, 150, (N, 4), dtype=torch.int32, device=dev)
+    x = torch.randn(N, 1, 84, 84, 16, device=dev).round().to(torch.bfloat16)   # ties: multi-window pixels
+    p = torch.zeros(N, 1, 42, 42, 16, dtype=torch.bfloat16, device=dev)
+    a = torch.zeros(N, 1, 42, 42, 16, dtype=torch.uint8, device=dev)
+    tops.maxpool(x, p, a)
+    dp = torch.randn(N, 1, 42, 42, 16, device=dev).to(torch.bfloat16)
+    outs = []
+    for fused in (True, False):
+        gw, gb = torch.zeros(16, 4, 3, 3, device=dev), torch.zeros(16, device=dev)
+        jobs = []
+        if fused:
+            hops.wgrad(dp, None, cs, gw, gb, jobs, ring=rp.frames, slots=slots, scale=1.0 / 255, pool_amax=a)
+        else:
+            dc = torch.zeros(N, 1, 84, 84, 16, dtype=torch.bfloat16, device=dev)
+            hops.maxpool_bwd(dp, a, dc)
+            hops.wgrad(dc, None, cs, gw, gb, jobs, ring=rp.frames, slots=slots, scale=1.0 / 255)
+        hops.finalize(jobs)
+        outs.append((gw, gb))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
 WG_SHAPES = [(16, 16, 42), (16, 32, 42), (32, 32, 21), (32, 32, 11)]
 
 
