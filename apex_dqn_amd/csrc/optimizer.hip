@@ -130,3 +130,48 @@ APEX_EXPORT int apex_sqnorm_ranges(const float* p0, int64_t n0, const float* p1,
   sqnorm_ranges_kernel<<<nblk, 256, 0, st>>>(p0, n0, p1, n1, partials);
   APEX_CHECK_LAUNCH();
 }
+
+// Several device copies in ONE launch (grid.y = segment): the emulated world's stand-in
+// for an RCCL group (parallel/rccl.py EmulatedCollectives.fused) -- RCCL launches a
+// group's collectives as one kernel, so the emulation issues one copy kernel per group
+// instead of one per member.  16-B chunks where both ends are 16-B aligned, bytes else.
+#define COPY_SEGS 32
+struct CopySegs {
+  const uint8_t* src[COPY_SEGS];
+  uint8_t* dst[COPY_SEGS];
+  int64_t bytes[COPY_SEGS];
+};
+
+__global__ void __launch_bounds__(256) copy_segments_kernel(CopySegs c) {
+  const int s = blockIdx.y;
+  const uint8_t* src = c.src[s];
+  uint8_t* dst = c.dst[s];
+  const int64_t nb = c.bytes[s];
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (int64_t)gridDim.x * blockDim.x;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int64_t n16 = nb >> 4;
+    for (int64_t i = t0; i < n16; i += stride)
+      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (int64_t i = (n16 << 4) + t0; i < nb; i += stride) dst[i] = src[i];
+  } else {
+    for (int64_t i = t0; i < nb; i += stride) dst[i] = src[i];
+  }
+}
+
+APEX_EXPORT int apex_copy_segments(int n, const int64_t* src, const int64_t* dst, const int64_t* bytes,
+                                   hipStream_t st) {
+  if (n < 1 || n > COPY_SEGS) return (int)hipErrorInvalidValue;
+  CopySegs c{};
+  int64_t mx = 0;
+  for (int i = 0; i < n; ++i) {
+    if (bytes[i] < 0 || (bytes[i] > 0 && (src[i] == 0 || dst[i] == 0))) return (int)hipErrorInvalidValue;
+    c.src[i] = reinterpret_cast<const uint8_t*>(src[i]);
+    c.dst[i] = reinterpret_cast<uint8_t*>(dst[i]);
+    c.bytes[i] = bytes[i];
+    mx = bytes[i] > mx ? bytes[i] : mx;
+  }
+  int64_t bx = (mx / 16 + 255) / 256;
+  bx = bx < 1 ? 1 : (bx > 1024 ? 1024 : bx);
+  copy_segments_kernel<<<dim3((unsigned)bx, (unsigned)n), 256, 0, st>>>(c);
+  APEX_CHECK_LAUNCH();
+}

@@ -411,6 +411,10 @@ class DataParallelStep:
         if not getattr(self, "_shard", False):
             return
         self._wait_params()
+        if getattr(self.comm, "emulated", False):
+            # (an emulated world has no other ranks: its all-gathers would overwrite the
+            # other slices with copies of this rank's rows)
+            return
         works = []
         # (t32: every rank's own rows are right -- copies of its p32 rows at the last sync)
         for t in (self.p32, self.t32, self.rms_v, self.rms_m):
@@ -428,7 +432,10 @@ class DataParallelStep:
         """Before reading the whole fp32 state (save): gathered at this update."""
         if not getattr(self, "_shard", False):
             return
-        if self.world == 1 or getattr(self.comm, "emulated", False):
+        if getattr(self.comm, "emulated", False):
+            raise RuntimeError("sharded DP update in an emulated world: only this rank's fc rows exist, "
+                               "there is no whole model to save")
+        if self.world == 1:
             self.materialize()
         elif getattr(self, "_materialized_at", None) != self.num_q_updates:
             raise RuntimeError("sharded DP update: call learner.materialize() on every rank before save()")

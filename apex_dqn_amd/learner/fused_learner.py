@@ -48,7 +48,7 @@ from ..models.flat_params import (FlatLayout, flat_to_reference_state, nature_se
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..ops.switches import SW
 from ..utils.checkpoint import (adopt_obs_scale, layout_segments, load_checkpoint, pack_flat_state,
-                                save_checkpoint, unpack_flat_state)
+                                save_checkpoint, unpack_flat_state, checkpoint_network)
 from .dp_step import DataParallelStep, Streams
 from .is_norm import IsNormMixin
 
@@ -703,30 +703,42 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         capture lands in a timed region.  Learner state is unchanged.  Returns
         ``graph_captures``.
 
-        Data parallel: the DP step's graphs hold RCCL collectives.  If capturing them or
-        their first replay raises on ANY rank (the ranks agree by a host all-reduce), every
-        rank drops its graphs, restores its state and runs the eager DP step instead --
-        in process, no restart of a process that has touched the GPU (``graph_fallback``
-        says why; bench.py reports it as ``dp_graphs`` / ``graph_fallback``)."""
+        Data parallel: the DP step's graphs hold RCCL collectives, and three phases
+        differ in what a failure leaves behind:
+
+        * the eager warm-up (real collectives) and the first replay of fresh graphs
+          (real collectives) are not recoverable in process -- a rank that raises there
+          has skipped collectives its peers are blocked in -- so an error propagates and
+          the caller's watchdog (bench.py's ``PhaseWatchdog``, gpu_loop's chunk phase)
+          aborts the communicator and exits non-zero;
+        * the capture itself enqueues nothing: if it raises on ANY rank (agreed by a host
+          all-reduce that every rank reaches), every rank drops its graphs and runs the
+          eager DP step (``graph_fallback``).
+        A NATIVE crash inside capture is caught before the parent process ever touches
+        the GPU, by the out-of-process probe (``runtime/capture_probe.py``)."""
         if not self._graphs_enabled():
             return self.graph_captures
         k = int(self.rt.graph_steps)
         if not (self._graphs is None or (multi and k > 1 and self._multi is None) or not self._graphs_warm):
             return self.graph_captures
+        if self._graphs is None:
+            self._warmup_eager()
         if not self._dp:
-            self._prepare_graphs(multi)
-            return self.graph_captures
-        snap = self._snapshot()
-        err = None
-        try:
-            self._prepare_graphs(multi)
-        except Exception as e:      # capture / first replay of the DP step failed here
-            err = e
-        ok = err is None
-        if self.comm is not None and getattr(self.comm, "active", False):
-            ok = self.comm.allreduce_scalar(1.0 if ok else 0.0, "min") > 0.5
-        if not ok:
-            self._eager_fallback(err, snap)
+            self._capture_graphs(multi)
+        else:
+            snap = self._snapshot()
+            err = None
+            try:
+                self._capture_graphs(multi)
+            except Exception as e:      # the capture of the DP step failed here
+                err = e
+            ok = err is None
+            if self.comm is not None and getattr(self.comm, "active", False):
+                ok = self.comm.allreduce_scalar(1.0 if ok else 0.0, "min") > 0.5
+            if not ok:
+                self._eager_fallback(err, snap)
+                return self.graph_captures
+        self._warm_graphs()
         return self.graph_captures
 
     def _eager_fallback(self, err, snap) -> None:
@@ -747,9 +759,18 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
                          f"running the eager DP step\n")
         sys.stderr.flush()
 
-    def _prepare_graphs(self, multi: bool) -> None:
+    def _capture_graphs(self, multi: bool) -> None:
+        """Capture the one-update graph (if missing) and, with ``multi``, the
+        ``graph_steps`` graph.  Capture records without executing: state is unchanged."""
         if self._graphs is None:
-            self._capture()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body()
+                if self._inject_capture_failure:
+                    raise RuntimeError("injected DP graph capture failure (test)")
+            self._graphs = g
+            self.graph_captures += 1
+            self._graphs_warm = False
         k = int(self.rt.graph_steps)
         if multi and k > 1 and self._multi is None:
             g = torch.cuda.CUDAGraph()
@@ -769,21 +790,24 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
             self._multi = g
             self.graph_captures += 1
             self._graphs_warm = False
-        if not self._graphs_warm:
-            # the first launch of a fresh graph uploads it (~ms): replay each graph once
-            # and restore the learner / replay state, so the first timed launch is warm
-            snap = self._snapshot()
-            if self._presample and self._sample_ver != self.replay.version:
-                self._sample()
-            for gr in (self._graphs, self._multi):
-                if gr is not None:
-                    gr.replay()
-            torch.cuda.synchronize(self.device)
-            self._restore(snap)
-            if self._presample:
-                self._sample()     # the pre-drawn batch of the restored state (same draw)
-            torch.cuda.synchronize(self.device)
-            self._graphs_warm = True
+
+    def _warm_graphs(self) -> None:
+        """The first launch of a fresh graph uploads it (~ms): replay each graph once and
+        restore the learner / replay state, so the first timed launch is warm."""
+        if self._graphs_warm:
+            return
+        snap = self._snapshot()
+        if self._presample and self._sample_ver != self.replay.version:
+            self._sample()
+        for gr in (self._graphs, self._multi):
+            if gr is not None:
+                gr.replay()
+        torch.cuda.synchronize(self.device)
+        self._restore(snap)
+        if self._presample:
+            self._sample()     # the pre-drawn batch of the restored state (same draw)
+        torch.cuda.synchronize(self.device)
+        self._graphs_warm = True
 
     def rewarm(self, replays: int) -> None:
         """Untimed, state-preserving GPU warm-up: replay the multi-step graph ``replays``
@@ -805,9 +829,9 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
             self._sample()
         torch.cuda.synchronize(self.device)
 
-    def _capture(self) -> None:
-        """Warm up on a side stream (allocator pools, workspaces, the communicator),
-        restore state, then capture the one-update graph."""
+    def _warmup_eager(self) -> None:
+        """Two eager updates on a side stream (allocator pools, workspaces, the
+        communicator), then the state restored: the graphs start from the same state."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         snap = self._snapshot()
@@ -819,15 +843,6 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         if self._presample:    # the graphs start from a drawn batch (their seg1 holds no sample)
             self._sample()
         torch.cuda.synchronize(self.device)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._body()
-            if self._inject_capture_failure:
-                raise RuntimeError("injected DP graph capture failure (test)")
-        self._graphs = g
-        self.graph_captures += 1
-        self._graphs_warm = False
-        # capture recorded the step without executing it; state is as before
 
     def check_replicas(self) -> bool:
         """Data-parallel replicas must stay bit-identical (same all-reduced gradient,
@@ -855,13 +870,48 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         self._target_changed()
         return False
 
-    def refresh_replay_stats(self) -> None:
+    def refresh_replay_stats(self) -> bool:
         """Re-gather the shard statistics (after host-side inserts / eviction; a
         collective: every rank calls it at the same point), and grow the per-rank rows if
-        a shard's share of the mass outgrew them (:meth:`_fit_rows`)."""
+        a shard's share of the mass outgrew them (:meth:`_fit_rows`).  Returns True when
+        the rows grew: the step graphs were dropped, and the caller recaptures them
+        (:meth:`prepare_graphs`) while no other thread launches GPU work."""
         if self._dp:
             self.replay.gather_shard_stats(coll=self.coll)
-            self._fit_rows()
+            return bool(self._fit_rows())
+        return False
+
+    def graph_matches_eager(self) -> Optional[bool]:
+        """One update replayed from the captured one-update graph against the same update
+        run eagerly from the same snapshot: parameters (fp32 + bf16 operands) and RMSprop
+        state bit-identical?  The state is restored afterwards.  A collective with DP
+        (every rank calls it; the answer is agreed by a host all-reduce).  None when the
+        graphs are not in use."""
+        if not self._graphs_enabled() or self._graphs is None:
+            return None
+        self._wait_params()
+        torch.cuda.synchronize(self.device)
+        snap = self._snapshot()
+        state = (self.p32, self._pbf_all, self.rms_v, self.rms_m)
+        if self._presample and self._sample_ver != self.replay.version:
+            self._sample()
+        self._graphs.replay()
+        torch.cuda.synchronize(self.device)
+        g = [t.clone() for t in state]
+        self._restore(snap)
+        if self._presample:
+            self._sample()
+        self._body()
+        self._wait_params()
+        torch.cuda.synchronize(self.device)
+        same = all(torch.equal(a, b) for a, b in zip(g, state))
+        self._restore(snap)
+        if self._presample:
+            self._sample()
+        torch.cuda.synchronize(self.device)
+        if self.comm is not None and getattr(self.comm, "active", False):
+            same = self.comm.allreduce_scalar(1.0 if same else 0.0, "min") > 0.5
+        return bool(same)
 
     def _snapshot(self):
         rp = self.replay
@@ -933,7 +983,8 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         else:
             self.sync_target()
         opt = ck.get("optimizer_state")
-        unpack_flat_state(opt, layout_segments(self.layout), rms_v=self.rms_v, rms_m=self.rms_m)
+        unpack_flat_state(opt, layout_segments(self.layout), untagged_network=checkpoint_network(ck),
+                          network=self.cfg.network, rms_v=self.rms_v, rms_m=self.rms_m)
         self.num_q_updates = int(ck.get("num_q_updates", 0))
         rng = ck.get("rng")
         if isinstance(rng, dict) and "replay_ctr" in rng:

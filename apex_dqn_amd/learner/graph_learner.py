@@ -31,7 +31,8 @@ import torch
 from ..config import ApexConfig
 from ..models.dueling import build_network
 from ..ops.fused_ops import HipBackend, TorchBackend
-from ..utils.checkpoint import adopt_obs_scale, load_checkpoint, pack_flat_state, save_checkpoint, unpack_flat_state
+from ..utils.checkpoint import (adopt_obs_scale, checkpoint_network, load_checkpoint, pack_flat_state, save_checkpoint,
+                                unpack_flat_state)
 from .fused_learner import _enable_sharding, dp_layout
 from .losses import ddqn_loss
 
@@ -202,9 +203,11 @@ class GraphLearner:
             self.sync_target()
 
     # --------------------------------------------------- replay statistics
-    def refresh_replay_stats(self) -> None:
+    def refresh_replay_stats(self) -> bool:
+        """Re-gather the shard statistics (a collective).  Fixed rows: never resizes."""
         if self.world > 1:
             self.replay.gather_shard_stats()
+        return False
 
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)
@@ -267,7 +270,8 @@ class GraphLearner:
                     p.copy_(v)
             else:
                 self.sync_target()
-            unpack_flat_state(ck.get("optimizer_state"), self._segments(), rms_v=self.rms_v, rms_m=self.rms_m)
+            unpack_flat_state(ck.get("optimizer_state"), self._segments(), untagged_network=checkpoint_network(ck),
+                              network=self.cfg.network, rms_v=self.rms_v, rms_m=self.rms_m)
         self.num_q_updates = int(ck.get("num_q_updates", 0))
         rng = ck.get("rng")
         if isinstance(rng, dict) and "replay_ctr" in rng:

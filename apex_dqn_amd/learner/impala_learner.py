@@ -39,7 +39,7 @@ from ..models.flat_params import FlatLayout
 from ..ops.fused_ops import HipBackend, TorchBackend, split_into
 from ..ops.impala import ConvSpec, HipImpalaOps, TorchImpalaOps, frag_elems
 from ..utils.checkpoint import (adopt_obs_scale, layout_segments, load_checkpoint, pack_flat_state,
-                                save_checkpoint, unpack_flat_state)
+                                save_checkpoint, unpack_flat_state, checkpoint_network)
 from ..ops.switches import SW
 from .fused_learner import _enable_sharding, dp_layout
 from .is_norm import IsNormMixin
@@ -525,9 +525,11 @@ class FusedImpalaLearner(IsNormMixin):
                              rp.ctr) + ((rp.shard_stats,) if rp.sharded else ()), snap):
             dst.copy_(src)
 
-    def refresh_replay_stats(self) -> None:
+    def refresh_replay_stats(self) -> bool:
+        """Re-gather the shard statistics (a collective).  Fixed rows: never resizes."""
         if self.world > 1:
             self.replay.gather_shard_stats()
+        return False
 
     def sync_target(self) -> None:
         self.t32.copy_(self.p32)
@@ -620,7 +622,8 @@ class FusedImpalaLearner(IsNormMixin):
         else:
             self.sync_target()
         opt = ck.get("optimizer_state")
-        unpack_flat_state(opt, layout_segments(self.layout), rms_v=self.rms_v, rms_m=self.rms_m)
+        unpack_flat_state(opt, layout_segments(self.layout), untagged_network=checkpoint_network(ck),
+                          network=self.cfg.network, rms_v=self.rms_v, rms_m=self.rms_m)
         self.num_q_updates = int(ck.get("num_q_updates", 0))
         rng = ck.get("rng")
         if isinstance(rng, dict) and "replay_ctr" in rng:

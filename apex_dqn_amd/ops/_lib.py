@@ -169,6 +169,7 @@ _SIGS = {
     "apex_s2d_frames": ([c_p, c_p, c_i64, c_i64, c_i64, c_p], c_i),
     "apex_pack_rows": ([c_p, c_p, c_p, c_i, c_i, c_p, c_i64, c_p], c_i),
     "apex_sqnorm_ranges": ([c_p, c_i64, c_p, c_i64, c_p, c_i, c_p], c_i),
+    "apex_copy_segments": ([c_i, c_p, c_p, c_p, c_p], c_i),
 }
 
 _LIB: Optional[ctypes.CDLL] = None

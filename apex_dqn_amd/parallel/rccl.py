@@ -457,12 +457,15 @@ class NativeCollectives(_StreamColl):
 
 class EmulatedCollectives(_StreamColl):
     """Rank ``rank``'s view of a ``world``-rank step on ONE GPU (``bench.py
-    --emulate-world``): every collective is a device copy of its true size on a comm
-    stream joined like the real one's -- an all-gather writes this rank's chunk into
-    every slot (the gathered rows / statistics / parameters stay valid data), an
-    all-reduce copies the buffer once, a reduce-scatter copies this rank's chunk.  It
-    measures the per-rank compute, the graph edges and the copies; RCCL's own latency
-    and xGMI transfer time are not in it."""
+    --emulate-world``): every collective is a device copy of its true size -- an
+    all-gather writes this rank's chunk into every slot (the gathered rows / statistics /
+    parameters stay valid data), an all-reduce copies the buffer once, a reduce-scatter
+    copies this rank's chunk.  Launches are modelled on RCCL's: one collective is ONE
+    kernel (``csrc/optimizer.hip copy_segments_kernel``, all its copies), and the
+    collectives of a ``fused()`` group leave as ONE kernel at the group's end, as an
+    ``ncclGroupStart / End`` pair launches them; non-inline ones run on a comm stream
+    joined like the real one's.  It measures the per-rank compute, the graph edges and
+    the copies; RCCL's own latency and xGMI transfer time are not in it."""
     name = "emulated"
     inline = True
 
@@ -470,6 +473,7 @@ class EmulatedCollectives(_StreamColl):
         self._init_stream(device)
         self.W, self.rank = int(world), int(rank)
         self._scratch = {}
+        self._group = None          # (segments, handles) of the open fused() group
 
     def _buf(self, t: torch.Tensor) -> torch.Tensor:
         key = (t.dtype, t.numel())
@@ -478,46 +482,94 @@ class EmulatedCollectives(_StreamColl):
             b = self._scratch[key] = torch.empty(t.numel(), dtype=t.dtype, device=self.device)
         return b
 
-    def _reduce(self, t: torch.Tensor) -> None:
-        self._buf(t).copy_(t.reshape(-1))
+    @staticmethod
+    def _seg(dst: torch.Tensor, src: torch.Tensor):
+        assert dst.is_contiguous() and src.is_contiguous() and dst.numel() == src.numel()
+        return (src.data_ptr(), dst.data_ptr(), src.numel() * src.element_size(), dst, src)
 
-    def _gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+    def _reduce_segs(self, t: torch.Tensor):
+        return [self._seg(self._buf(t), t.reshape(-1))]
+
+    def _gather_segs(self, out: torch.Tensor, inp: torch.Tensor):
         W, n, r = self.W, inp.numel(), self.rank
         rows = out.view(W, n)
-        src = inp.reshape(1, n)
-        if r > 0:
-            rows[:r].copy_(src.expand(r, n))
-        if r + 1 < W:
-            rows[r + 1:].copy_(src.expand(W - r - 1, n))
-        if inp.data_ptr() != rows[r].data_ptr():
-            rows[r].copy_(inp.reshape(-1))
+        src = inp.reshape(-1)
+        return [self._seg(rows[j], src) for j in range(W) if j != r or rows[j].data_ptr() != src.data_ptr()]
+
+    def _scatter_segs(self, out: torch.Tensor, inp: torch.Tensor):
+        n = out.numel()
+        return [self._seg(out.reshape(-1), inp.reshape(-1)[self.rank * n:(self.rank + 1) * n])]
+
+    def _launch(self, segs) -> None:
+        """All copies in as few launches as the kernel's 32 segments allow (one, here)."""
+        if not segs:
+            return
+        if self.device.type != "cuda":
+            for _, _, _, dst, src in segs:
+                dst.copy_(src)
+            return
+        from ..ops import _lib
+        lib = _lib.require_kernels()
+        for i in range(0, len(segs), 32):
+            part = segs[i:i + 32]
+            arr = lambda k: (ctypes.c_int64 * len(part))(*[int(x[k]) for x in part])  # noqa: E731
+            _lib.check(lib.apex_copy_segments(len(part), arr(0), arr(1), arr(2), _lib.stream_ptr(self.device)),
+                       "copy_segments")
+
+    def _op(self, segs, inline: bool):
+        if self._group is not None:
+            self._group[0].extend(segs)
+            h = _GroupedWork()
+            self._group[1].append(h)
+            return h
+        if inline:
+            self._launch(segs)
+            return _Done()
+        s = self._fork()
+        with torch.cuda.stream(s):
+            self._launch(segs)
+        return _StreamWork(self)
+
+    def fused(self, inline: bool = False):
+        """The group's collectives leave as one copy launch at its end (inline: on the
+        current stream; else on the comm stream, forked from the current one)."""
+        from contextlib import contextmanager
+
+        @contextmanager
+        def ctx():
+            assert self._group is None, "groups do not nest here"
+            self._group = ([], [])
+            try:
+                yield
+            finally:
+                segs, handles = self._group
+                self._group = None
+                if inline:
+                    self._launch(segs)
+                    w = _Done()
+                else:
+                    s = self._fork()
+                    with torch.cuda.stream(s):
+                        self._launch(segs)
+                    w = _StreamWork(self)
+                for h in handles:
+                    h.work = w
+        return ctx()
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):
-        s = self._fork()
-        with torch.cuda.stream(s):
-            self._reduce(t)
-        return _StreamWork(self)
+        return self._op(self._reduce_segs(t), False)
 
     def all_reduce_inline(self, t: torch.Tensor, op: str = "sum"):
-        self._reduce(t)
-        return _Done()
+        return self._op(self._reduce_segs(t), True)
 
     def all_gather_inline(self, out: torch.Tensor, inp: torch.Tensor):
-        self._gather(out, inp)
-        return _Done()
+        return self._op(self._gather_segs(out, inp), True)
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor):
-        s = self._fork()
-        with torch.cuda.stream(s):
-            self._gather(out, inp)
-        return _StreamWork(self)
+        return self._op(self._gather_segs(out, inp), False)
 
     def reduce_scatter_into(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum"):
-        s = self._fork()
-        n = out.numel()
-        with torch.cuda.stream(s):
-            out.reshape(-1).copy_(inp.reshape(-1)[self.rank * n:(self.rank + 1) * n])
-        return _StreamWork(self)
+        return self._op(self._scatter_segs(out, inp), False)
 
     def world(self) -> int:
         return self.W

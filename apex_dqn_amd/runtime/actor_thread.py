@@ -69,6 +69,18 @@ class ActorRunner:
         if self._thread is not None:
             self._thread.join(timeout)
 
+    def pause(self, timeout: float = 60.0) -> None:
+        """Quiesce: let the thread finish its current group step and end (the learner
+        thread then launches alone, e.g. to recapture its graphs); :meth:`resume` starts a
+        fresh thread that continues the step count."""
+        self.stop(timeout)
+        if self.alive:
+            raise RuntimeError("actor thread did not stop within %.0f s" % timeout)
+
+    def resume(self) -> None:
+        if not self.done:
+            self.start()
+
     # ----------------------------------------------------------------- health
     @property
     def done(self) -> bool:

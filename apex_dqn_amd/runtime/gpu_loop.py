@@ -12,6 +12,7 @@ checkpoints, JSONL metrics, synchronized start across ranks.
 from __future__ import annotations
 
 import collections
+import contextlib
 import os
 import sys
 import time
@@ -154,13 +155,26 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
         if ready >= 1.0:
             break
     learner.refresh_replay_stats()
+    # multi-rank: host calls that can block on peers (graph warm-up / first replays with
+    # their collectives, learner chunks) run under a deadline that aborts the
+    # communicators and exits non-zero naming the phase (learner/fused_learner.py
+    # prepare_graphs: those phases are not recoverable in process)
+    wd = None
+    if world > 1 and device.type == "cuda":
+        from .watchdog import PhaseWatchdog
+        wd = PhaseWatchdog(rank, comm)
+
+    def guard(name):
+        return wd.phase(name, rt.step_timeout) if wd is not None else contextlib.nullcontext()
+
     runner = None
     if async_actors:
         from .actor_thread import ActorRunner
         # every graph the loop replays is captured before the actor thread starts
         # launching work (a capture must not see other threads' launches)
         if hasattr(learner, "prepare_graphs"):
-            learner.prepare_graphs()
+            with guard("graph capture"):
+                learner.prepare_graphs()
         runner = ActorRunner(group, max_actor_steps - st.actor_steps, timeout=rt.heartbeat_timeout,
                              on_event=(lambda kind, **kw: metrics.log(kind, **kw)) if metrics is not None else None)
         st.actor_base = st.actor_steps
@@ -198,7 +212,8 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                 with replay.lock:       # CPU tensors: no stream ordering between the threads
                     _learn(learner, k)
             else:
-                _learn(learner, k)
+                with guard("learner chunk"):
+                    _learn(learner, k)
             if on_cuda:
                 # at most two chunks queued (the actor's inserts never wait long behind
                 # them); the wait is the step watchdog in both actor modes
@@ -219,7 +234,20 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
             if n % L.remove_old_xp_freq == 0:
                 replay.remove_to_fit()
                 replay.rebuild()
-                learner.refresh_replay_stats()
+                if learner.refresh_replay_stats():
+                    # the per-rank rows grew (DP global batch): the step graphs were
+                    # dropped.  Recapture them now with the actor thread quiesced -- a
+                    # capture must not see another thread's launches -- on every rank
+                    # (the same gathered statistics: every rank grew alike)
+                    if runner is not None:
+                        runner.pause()
+                    if hasattr(learner, "prepare_graphs"):
+                        with guard("graph recapture after a row resize"):
+                            learner.prepare_graphs()
+                    if runner is not None:
+                        runner.resume()
+                    if metrics is not None:
+                        metrics.log("rows_resized", step=n, rows=int(learner.B))
             if rt.log_every and n % rt.log_every == 0:
                 if runner is not None:
                     st.actor_steps = st.actor_base + runner.steps
@@ -234,6 +262,8 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
             runner.stop()
             st.actor_steps = st.actor_base + runner.steps
             sys.setswitchinterval(old_switch)
+        if wd is not None:
+            wd.close()
     if on_cuda:
         torch.cuda.synchronize(device)
     rets = [r for (_, _, r) in group.episodes]

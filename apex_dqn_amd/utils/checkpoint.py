@@ -50,17 +50,33 @@ def pack_flat_state(segments: Segments, **flats: torch.Tensor) -> Dict[str, Any]
     return out
 
 
-def unpack_flat_state(opt: Any, segments: Segments, **dsts: torch.Tensor) -> bool:
+def unpack_flat_state(opt: Any, segments: Segments, untagged_network: Optional[str] = None,
+                      network: Optional[str] = None, **dsts: torch.Tensor) -> bool:
     """Restore :func:`pack_flat_state` output into the flat buffers ``dsts`` of the current
-    layout ``segments``.  Refuses (returns False, with a warning, buffers untouched) state
-    without a layout tag -- an older checkpoint's raw flat vectors, whose layout cannot be
-    verified -- or whose segments do not match by name and size; the caller then starts the
-    optimizer state fresh rather than misaligned."""
+    layout ``segments``.  State whose segments do not match by name and size is refused
+    (returns False, with a warning, buffers untouched): the caller then starts the optimizer
+    state fresh rather than misaligned.
+
+    Untagged state -- an older checkpoint's raw flat vectors, written before the tag
+    existed -- is accepted when it was saved by the same network (``untagged_network``,
+    from the checkpoint's config, equals ``network``) and every vector has exactly the
+    current flat buffer's length: this engine's flat layout (``models/flat_params.py``
+    nature segments and their padding) has not changed since, so the vector is the buffer.
+    Dropping it instead would restart centered RMSprop at v = m = 0 -- a several-times
+    larger step on every parameter in mid-training."""
     if not isinstance(opt, dict) or not dsts:
         return False
     if "layout" not in opt:
-        print("WARNING: checkpoint optimizer state has no layout tag (an older flat vector); "
-              "RMSprop state not restored (starts fresh)")
+        raw = all(isinstance(opt.get(key), torch.Tensor) and opt[key].numel() == dst.numel()
+                  for key, dst in dsts.items())
+        if raw and network is not None and untagged_network == network:
+            for key, dst in dsts.items():
+                dst.copy_(opt[key].reshape(-1).to(dst.dtype))
+            print("WARNING: checkpoint optimizer state has no layout tag (an older flat vector); restored by "
+                  "length (same network, %d values)" % next(iter(dsts.values())).numel())
+            return True
+        print("WARNING: checkpoint optimizer state has no layout tag (an older flat vector) and does not match "
+              "this network's flat buffer; RMSprop state not restored (starts fresh)")
         return False
     saved = {str(n): int(k) for n, _, k in opt["layout"]}
     cur = {n: int(k) for n, _, k in segments}
@@ -73,6 +89,19 @@ def unpack_flat_state(opt: Any, segments: Segments, **dsts: torch.Tensor) -> boo
         for n, o, k in segments:
             dst[o:o + k].copy_(src[n].reshape(-1).to(dst.dtype))
     return True
+
+
+def checkpoint_network(ck: Dict[str, Any]) -> Optional[str]:
+    """The network a checkpoint was saved by (its ``config``), or None."""
+    c = ck.get("config") if isinstance(ck, dict) else None
+    if not isinstance(c, dict):
+        return None
+    rt = c.get("Runtime") or {}
+    net = rt.get("network", "auto")
+    if net == "auto":
+        shape = (c.get("env_conf") or {}).get("state_shape") or []
+        net = "nature64" if len(shape) == 3 else "mlp"
+    return str(net)
 
 
 def layout_segments(layout) -> List[Tuple[str, int, int]]:

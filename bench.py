@@ -51,6 +51,16 @@ collectives, = N (N + 1) / 2), ``dp_graphs`` (the DP step ran as captured HIP gr
 ``graph_fallback`` names why not).  Every phase runs under a watchdog
 (``--phase-timeout``): a rank stuck in a collective exits non-zero naming its phase.
 
+Before this process makes any HIP call, each rank at N > 1 captures and replays the DP
+step in ONE child process (``runtime/capture_probe.py``: its own RCCL communicator and
+rendezvous under a separate store prefix); a child that crashes, hangs or fails on any
+rank sends every rank to the eager DP step for that measurement (``dp_capture_probe``:
+exit status per rank, verdict per measurement, seconds).  After the timed region the
+run checks itself: ``replicas_identical`` (checksums of every rank's fp32 master weights
+and RMSprop state agree) and ``graph_matches_eager`` (one captured update equals the same
+update run eagerly from the same snapshot, bit for bit, on every rank); ``param_sha256``
+fingerprints the final fp32 weights.
+
 ``--emulate-world W`` (one GPU): rank 0's share of a W-rank global-batch step -- its
 rows, its 1/W fc optimizer slice and fc weight-gradient rows, the sharded replay draw
 -- with every collective a device copy of its true size (``parallel/rccl.py
@@ -103,9 +113,9 @@ def make_replay(args, device, rank):
     return replay
 
 
-def make_learner(args, dtype, device, comm, rank, replay, scope=None):
-    from apex_dqn_amd.config import ApexConfig
-    cfg = ApexConfig.from_dict({
+def learner_config(args, dtype, rank, scope=None) -> dict:
+    """The learner's config (ApexConfig dict) of one measurement."""
+    return {
         "env_conf": {"state_shape": [4, 84, 84], "action_dim": args.actions, "name": "SyntheticPong"},
         "Learner": {"replay_sample_size": args.batch, "q_target_sync_freq": 2500, "remove_old_xp_freq": 100,
                     "min_replay_mem_size": 0},
@@ -116,13 +126,60 @@ def make_learner(args, dtype, device, comm, rank, replay, scope=None):
                     "batch_scope": scope or args.batch_scope, "allreduce_dtype": args.allreduce_dtype,
                     "dp_fc_exchange": args.dp_fc_exchange, "dp_shard_update": args.dp_shard_update,
                     **({} if args.graph_steps is None else {"graph_steps": args.graph_steps})},
-    })
+    }
+
+
+def measurements(args, world: int):
+    """(name, dtype, batch scope) of every learner this run builds, in order."""
+    dp = world > 1 or args.force_dp
+    scope = args.batch_scope if dp else "global"
+    out = [("headline", args.dtype, scope)]
+    if world > 1 and not args.no_scope_extra:
+        out.append(("other_scope", args.dtype, "per_rank" if scope == "global" else "global"))
+    if not args.no_bf16_extra and args.dtype == "fp32":
+        out.append(("bf16", "bf16", scope))
+    return out
+
+
+def capture_probe(args, world: int, rank: int, local_rank: int):
+    """The DP step's graph capture tried first in a child process per rank
+    (runtime/capture_probe.py), before this process makes any HIP call: a native crash
+    in capture (or a hang in RCCL's first captured collectives) costs the child, and the
+    variants that failed on any rank run the eager DP step here.  Returns the report
+    for the JSON (``dp_capture_probe``), or None when not applicable."""
+    mode = args.capture_probe
+    nature = args.network in ("nature64", "nature32") and args.learner == "fused" and args.backend == "hip"
+    graphs = not args.no_graphs and args.comm == "native" and args.dist_backend == "nccl"
+    if mode == "off" or args.emulate_world or not (nature and graphs):
+        return None
+    if not (world > 1 or (args.force_dp and mode == "on")):
+        return None
+    from apex_dqn_amd.runtime.capture_probe import run_probe
+    variants = [{"name": n, "cfg": learner_config(args, dt, rank, sc), "steps": args.graph_steps or 10}
+                for (n, dt, sc) in measurements(args, world)]
+    log = open(os.path.join(args.capture_probe_log, f"capture_probe_rank{rank}.log"), "wb") \
+        if args.capture_probe_log else None
+    try:
+        return run_probe(variants, rank, world, local_rank, timeout=args.capture_probe_timeout, log=log)
+    finally:
+        if log is not None:
+            log.close()
+
+
+def make_learner(args, dtype, device, comm, rank, replay, scope=None, probe=None, name=None):
+    from apex_dqn_amd.config import ApexConfig
+    cfg = ApexConfig.from_dict(learner_config(args, dtype, rank, scope))
+    torch.manual_seed(cfg.Runtime.seed)       # random-init weights: reproducible runs (DP: rank 0's broadcast)
     if args.learner == "graph" or (args.network == "impala" and args.graph_impala):
         from apex_dqn_amd.learner.graph_learner import GraphLearner
         return cfg, GraphLearner(cfg, device, replay, comm=comm)
     if args.network in ("nature64", "nature32"):
         from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
-        return cfg, FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
+        L = FusedNatureLearner(cfg, device, replay, comm=comm, backend=args.backend)
+        if probe is not None and not probe["ok"].get(name, False):
+            # the out-of-process capture failed on some rank: eager DP step on every rank
+            L.graph_fallback = "capture probe: child exit status per rank %s, captures %s" % (probe["rc"], probe["ok"])
+        return cfg, L
     from apex_dqn_amd.learner.impala_learner import FusedImpalaLearner
     return cfg, FusedImpalaLearner(cfg, device, replay, comm=comm, backend=args.backend)
 
@@ -248,6 +305,13 @@ def parser() -> argparse.ArgumentParser:
                     help="DP: shard the fc optimizer by output rows (Runtime.dp_shard_update)")
     ap.add_argument("--phase-timeout", type=float, default=600.0,
                     help="watchdog: seconds any bench phase may take before the rank exits non-zero")
+    ap.add_argument("--capture-probe", default="auto", choices=["auto", "on", "off"],
+                    help="DP graphs: capture + replay the DP step first in one child process per rank, before "
+                         "this process touches the GPU (auto: at world > 1; on: also --force-dp at world 1)")
+    ap.add_argument("--capture-probe-timeout", type=float, default=150.0,
+                    help="seconds the capture probe's child may take")
+    ap.add_argument("--capture-probe-log", default=None,
+                    help="directory for the probe children's output (capture_probe_rank<r>.log)")
     ap.add_argument("--network", default="nature64", choices=["nature64", "nature32", "impala"],
                     help="nature64 = the headline fused-HIP learner; nature32 runs on it zero-padded; impala on csrc/impala_split.hip (fp32) / csrc/impala.hip (bf16)")
     return ap
@@ -262,13 +326,19 @@ def run(args) -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU")
     emu = int(args.emulate_world)
     if emu and world > 1:
         raise SystemExit("--emulate-world runs on one process")
     wd = PhaseWatchdog(rank)
     to = float(args.phase_timeout)
+    if args.force_dp and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+    # before ANY HIP call of this process (torch.cuda.is_available() initialises HIP)
+    with wd.phase("capture probe", args.capture_probe_timeout + 60.0):
+        probe = capture_probe(args, world, rank, local_rank)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
     # one rank per GPU; the modulo only matters when rehearsing several ranks on
     # fewer GPUs (device_count() does not initialise the GPU)
     dev_idx = local_rank % max(1, torch.cuda.device_count())
@@ -297,7 +367,7 @@ def run(args) -> None:
         return r["valid_rows"] / args.batch / r["dt"]
 
     with wd.phase("learner init (comm init, parameter broadcast)", to):
-        cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay, scope)
+        cfg, learner = make_learner(args, args.dtype, device, comm, rank, replay, scope, probe, "headline")
     rows = learner.B
     diag = {}
     if dp and hasattr(learner, "comm_report"):
@@ -307,13 +377,29 @@ def run(args) -> None:
     dp_graphs = bool(getattr(learner, "_dp", False)) and learner._graphs_enabled() if dp else None
     fallback = getattr(learner, "graph_fallback", None)
     shard = bool(getattr(learner, "_shard", False))
+    if dp:
+        # after the timed region: did the replicas stay bit-identical, and does the
+        # captured update equal the eager one from the same state (both collectives)
+        diag["dp_capture_probe"] = probe if probe is not None else "not run (%s)" % (
+            "emulated world" if emu else "eager DP step" if not dp_graphs else "off" if args.capture_probe == "off"
+            else "world 1")
+        with wd.phase("replica check", to):
+            diag["replicas_identical"] = bool(learner.check_replicas()) if hasattr(learner, "check_replicas") \
+                else None
+        with wd.phase("graph vs eager check", to):
+            diag["graph_matches_eager"] = learner.graph_matches_eager() \
+                if hasattr(learner, "graph_matches_eager") else None
+    if hasattr(learner, "p32") and not emu:
+        learner.materialize()      # (sharded update: every rank's fc rows; a collective)
+        import hashlib
+        diag["param_sha256"] = hashlib.sha256(learner.p32.detach().cpu().numpy().tobytes()).hexdigest()[:16]
     other = None
     if world > 1 and not args.no_scope_extra:
         # the other batch scope, fp32: both scalings from one run
         osc = "per_rank" if scope == "global" else "global"
         del learner
         torch.cuda.empty_cache()
-        cfg_o, learner_o = make_learner(args, args.dtype, device, comm, rank, replay, osc)
+        cfg_o, learner_o = make_learner(args, args.dtype, device, comm, rank, replay, osc, probe, "other_scope")
         other = dict(measure(cfg_o, learner_o, replay, comm, args.warmup, args.steps, args.prep_warm, wd, to,
                              "other scope: "),
                      scope=osc, rows=learner_o.B)
@@ -322,7 +408,7 @@ def run(args) -> None:
     if not args.no_bf16_extra and args.dtype == "fp32":
         del learner
         torch.cuda.empty_cache()
-        cfg_b, learner_b = make_learner(args, "bf16", device, comm, rank, replay, scope)
+        cfg_b, learner_b = make_learner(args, "bf16", device, comm, rank, replay, scope, probe, "bf16")
         extra = measure(cfg_b, learner_b, replay, comm, args.warmup, args.steps, args.prep_warm, wd, to, "bf16: ")
         learner = learner_b
     dt = res["dt"]
@@ -375,7 +461,7 @@ def run(args) -> None:
         if dp:
             out["dp_graphs"] = dp_graphs
             out["graph_fallback"] = fallback
-            out.update(diag)
+        out.update(diag)
         if emu:
             out["emulated_world"] = emu
             out["emulation"] = ("rank 0 of a %d-rank global-batch step on one GPU; collectives are device copies "

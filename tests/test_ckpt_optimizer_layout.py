@@ -1,8 +1,9 @@
 """Checkpointed optimizer state is tagged with the flat layout it came from
 (utils/checkpoint.py pack_flat_state / unpack_flat_state): a resume restores every
-RMSprop value to its own parameter even when the engine's flat layout changed, and an
-untagged flat vector (a checkpoint written before the tag existed, whose layout cannot
-be verified) is refused -- the state starts fresh instead of silently misaligned."""
+RMSprop value to its own parameter even when the engine's flat layout changed.  An
+untagged flat vector (a checkpoint written before the tag existed) is restored by
+length when the same network saved it -- this engine's flat layout is unchanged since --
+and refused otherwise: the state then starts fresh instead of silently misaligned."""
 import torch
 
 from apex_dqn_amd.config import ApexConfig
@@ -39,7 +40,13 @@ def test_mismatched_or_untagged_state_is_refused(capsys):
     dst = torch.full((c.numel,), 5.0)
     assert not unpack_flat_state(st, layout_segments(c), rms_v=dst)
     assert not unpack_flat_state({"rms_v": torch.ones(a.numel)}, layout_segments(a), rms_v=dst)
+    # untagged of this buffer's length: only from the same network
+    assert not unpack_flat_state({"rms_v": torch.ones(c.numel)}, layout_segments(c), untagged_network="impala",
+                                 network="nature64", rms_v=dst)
     assert torch.equal(dst, torch.full((c.numel,), 5.0))
+    assert unpack_flat_state({"rms_v": torch.ones(c.numel)}, layout_segments(c), untagged_network="nature64",
+                             network="nature64", rms_v=dst)
+    assert torch.equal(dst, torch.ones(c.numel))
     assert "not restored" in capsys.readouterr().out
 
 
@@ -56,9 +63,14 @@ def test_fused_learner_resume_restores_rmsprop_state(tmp_path):
     L.save(p)
     L2 = FusedNatureLearner(_cfg(p), "cpu", _replay())
     assert torch.equal(L2.rms_v, L.rms_v) and torch.equal(L2.rms_m, L.rms_m)
-    # an older checkpoint: raw flat vectors with no layout tag -> refused, state fresh
+    # an older checkpoint: raw flat vectors with no layout tag, same network -> restored
     ck = torch.load(p, weights_only=True)
     ck["optimizer_state"] = {"rms_v": L.rms_v.clone(), "rms_m": L.rms_m.clone()}
     torch.save(ck, p)
     L3 = FusedNatureLearner(_cfg(p), "cpu", _replay())
-    assert torch.count_nonzero(L3.rms_v) == 0 and torch.equal(L3.p32, L.p32)
+    assert torch.equal(L3.rms_v, L.rms_v) and torch.equal(L3.rms_m, L.rms_m) and torch.equal(L3.p32, L.p32)
+    # ... of another length (e.g. another network's buffer): refused, state fresh
+    ck["optimizer_state"] = {"rms_v": L.rms_v[:-64].clone(), "rms_m": L.rms_m[:-64].clone()}
+    torch.save(ck, p)
+    L4 = FusedNatureLearner(_cfg(p), "cpu", _replay())
+    assert torch.count_nonzero(L4.rms_v) == 0 and torch.equal(L4.p32, L.p32)

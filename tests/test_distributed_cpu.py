@@ -191,3 +191,40 @@ def test_replica_check_detects_and_repairs_divergence():
     for _, ok_before, ok_corrupt, same, ok_after in res:
         assert ok_before and not ok_corrupt and same and ok_after
 
+
+
+def _probe_parent(rank, world, port, env, q):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **env)
+    from apex_dqn_amd.runtime.capture_probe import run_probe
+    variants = [{"name": "headline", "cfg": {}}, {"name": "bf16", "cfg": {}}]
+    q.put((rank, run_probe(variants, rank, world, 0, timeout=60.0)))
+
+
+@pytest.mark.parametrize("inject", ["", "abort@1"])
+def test_capture_probe_rendezvous_and_agreement(inject):
+    """runtime/capture_probe.py across 2 parent processes (dry children: no GPU work):
+    every parent spawns one child, the children meet in their own gloo group through the
+    parents' TCP store under the probe's key prefix, and every parent reads every rank's
+    exit status.  A child that aborts on rank 1 fails the probe on BOTH ranks (the other
+    rank's child is killed through the store's failure flag or exits cleanly): every
+    variant then runs eagerly everywhere."""
+    import random
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29800 + random.randint(0, 150)
+    env = {"APEX_CAPTURE_PROBE_DRY": "1", "APEX_CAPTURE_PROBE_INJECT": inject}
+    ps = [ctx.Process(target=_probe_parent, args=(r, 2, port, env, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(2))
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert out[0]["rc"] == out[1]["rc"] and out[0]["ok"] == out[1]["ok"]
+    if not inject:
+        assert out[0]["rc"] == [0, 0] and out[0]["ok"] == {"headline": True, "bf16": True}
+    else:
+        assert out[0]["rc"][1] == -6 and out[0]["ok"] == {"headline": False, "bf16": False}
+    assert max(o["seconds"] for o in out.values()) < 60

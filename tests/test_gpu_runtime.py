@@ -1,5 +1,6 @@
 """GPU runtime: actor head kernel, actor group + HBM replay + fused learner loop
 (HIP graphs on), CLI in gpu mode."""
+import json
 import os
 import subprocess
 import sys
@@ -383,6 +384,48 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert out["comm_world"] == 2 and out["init_allreduce"] == 3.0 and out["init_allreduce_ok"] is True
     assert out["dp_graphs"] is False and out["graph_fallback"] is None
     assert out["config"]["dp_collectives"] == "torch" and out["config"]["dp_shard_update"] is True
+    # the self-checks after the timed region: replicas bit-identical across the 2 ranks;
+    # gloo runs the eager DP step, so there is no capture to probe or to compare
+    assert out["replicas_identical"] is True
+    assert out["dp_capture_probe"] == "not run (eager DP step)" and out["graph_matches_eager"] is None
+    assert len(out["param_sha256"]) == 16
+
+
+def _bench_force_dp(extra_env, port, tmp):
+    env = dict(os.environ, **extra_env)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--force-dp", "--capture-probe", "on",
+                        "--steps", "20", "--warmup", "5", "--replay", "20000", "--no-bf16-extra", "--prep-warm", "0",
+                        "--capture-probe-timeout", "120", "--capture-probe-log", str(tmp)],
+                       capture_output=True, text=True, timeout=400, cwd=ROOT,
+                       env=dict(env, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)))
+    log = open(os.path.join(str(tmp), "capture_probe_rank0.log"), errors="replace").read()
+    print(log[-3000:])
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    return _bench_json(r.stdout)
+
+
+@pytest.mark.gpu
+def test_capture_probe_abort_falls_back_to_identical_eager_updates(tmp_path):
+    """bench.py's out-of-process DP capture probe (runtime/capture_probe.py) at world 1
+    (--force-dp: the DP step over a one-rank RCCL communicator).  Clean: the child
+    captures and replays, the parent keeps its graphs, and one captured update equals
+    the eager one bit for bit.  With the child forced to abort (SIGABRT after its
+    captures) the parent runs the eager DP step instead -- and ends at the same fp32
+    weights as the captured run."""
+    import random
+    port = 29900 + random.randint(0, 90)
+    a = _bench_force_dp({}, port, tmp_path)
+    b = _bench_force_dp({"APEX_CAPTURE_PROBE_INJECT": "abort"}, port + 1, tmp_path)
+    print(json.dumps({k: a.get(k) for k in ("dp_capture_probe", "graph_matches_eager", "param_sha256")}))
+    print(json.dumps({k: b.get(k) for k in ("dp_capture_probe", "graph_fallback", "param_sha256")}))
+    assert a["dp_capture_probe"]["rc"] == [0] and a["dp_capture_probe"]["ok"] == {"headline": True}
+    assert a["dp_graphs"] is True and a["graph_fallback"] is None and a["graph_captures_in_timed"] == 0
+    assert a["graph_matches_eager"] is True and a["replicas_identical"] is True
+    assert a["dp_capture_probe"]["seconds"] < 60
+    assert b["dp_capture_probe"]["rc"] == [-6] and b["dp_capture_probe"]["ok"] == {"headline": False}
+    assert b["dp_graphs"] is False and "capture probe" in b["graph_fallback"]
+    assert b["graph_matches_eager"] is None
+    assert a["param_sha256"] == b["param_sha256"]
 
 
 def _native_rccl_worker(q, port):

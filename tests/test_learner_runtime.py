@@ -287,3 +287,40 @@ def test_loop_watchdog_aborts_on_hung_gpu_work():
     with pytest.raises(RuntimeError, match="watchdog"):
         _wait_event(Hung(), 0.05, FakeComm())
     assert FakeComm.aborted
+
+
+def test_row_resize_recaptures_with_actor_thread_quiesced(monkeypatch):
+    """A DP row resize at an eviction (FusedNatureLearner.refresh_replay_stats -> True:
+    the step graphs were dropped) recaptures the graphs while the actor thread is
+    stopped -- a capture must not see another thread's launches -- and the thread then
+    resumes.  Forced here on the CPU loop with the async actor thread on."""
+    import threading
+    from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
+    from apex_dqn_amd.runtime.gpu_loop import train_frames
+    calls = {"refresh": 0, "prepare": [], "resized_at": None}
+    orig_refresh = FusedNatureLearner.refresh_replay_stats
+
+    def refresh(self):
+        orig_refresh(self)
+        calls["refresh"] += 1
+        if calls["refresh"] == 3:            # the second eviction of the training loop
+            calls["resized_at"] = self.num_q_updates
+            return True
+        return False
+
+    def prepare(self, multi=True):
+        alive = any(t.name == "apex-actor" and t.is_alive() for t in threading.enumerate())
+        calls["prepare"].append((self.num_q_updates, alive))
+        return 0
+
+    monkeypatch.setattr(FusedNatureLearner, "refresh_replay_stats", refresh)
+    monkeypatch.setattr(FusedNatureLearner, "prepare_graphs", prepare)
+    out = train_frames(_small_image_cfg(), "cpu", 12, async_actors=True)
+    assert out["learner"].num_q_updates == 12
+    n = calls["resized_at"]
+    assert n is not None and n > 0
+    # the initial capture (before the thread starts) and the recapture at the resize:
+    # the actor thread is never alive during either
+    assert [c for c in calls["prepare"] if c[0] == n] == [(n, False)], calls
+    assert all(alive is False for _, alive in calls["prepare"]), calls
+    assert out["actor_steps"] > 0
