@@ -318,7 +318,7 @@ class PipelinedActorGroups:
     turn: group k's q / actions are read back, its envs stepped, its frames appended and
     its transitions inserted while the inference of the groups after it runs on the GPU.
     A single group waits for its own inference every step (~0.3 ms of a ~0.6 ms step on
-    the Pong-shaped config, the kernels queued behind the learner's: scripts/diag_e2e_actor.py);
+    the Pong-shaped config, the kernels queued behind the learner's: scripts/archive/diag_e2e_actor.py);
     here the host's env work hides it.  Each env still acts on its latest frame stack
     (every group's policy is launched after its previous env step), so the transitions are
     those of one group of K * E envs; the groups take consecutive env ids and slices of

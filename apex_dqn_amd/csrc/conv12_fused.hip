@@ -84,6 +84,8 @@ struct Conv12Desc {
   unsigned long long* wq;  // image work queue counter (mfma_common.h wq_next), or null: static
                            // strided image order
   int bf16;                // 1: one bf16 plane everywhere (w2_lo, y1_lo, y2_lo unused)
+  int probe_split;         // diagnostic build: bit 0 = wait for the first image's frames before
+                           // the weight loads (prologue split); 0 otherwise
 };
 
 template <int C>
@@ -128,6 +130,12 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
   // launch up (scripts/bench_cu_steal.py).  Every image is computed whole by one
   // workgroup, so the outputs do not depend on the assignment.  Images leave the queue in
   // order: the S_t rows (y1 also copied out) spread over all workgroups first.
+  PROBE(d.probe, 4, PROBE_ITERS - 1, 0);          // kernel entry (diagnostic build)
+#ifdef APEX_PROBE
+  if (d.probe != nullptr && blockIdx.x < PROBE_BLOCKS && (threadIdx.x & 63) == 0)
+    d.probe[((blockIdx.x * 4 + (threadIdx.x >> 6)) * PROBE_ITERS + PROBE_ITERS - 1) * 4 + 2] =
+        __builtin_amdgcn_s_memrealtime();
+#endif
   int wq_seq = 0;                                  // (thread 0: static order, d.wq null)
   if (tid == 0) {
     // (the second fetch only after an item: each workgroup stops at its first value >= N)
@@ -263,14 +271,21 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
     }
   };
   // image i's frames land in staging(i & 1): image 0's here, image i + 1's during conv1(i)
+  PROBE(d.probe, 4, PROBE_ITERS - 2, 0);          // (diagnostic build: prologue split)
   if (cur < d.N) issue_dma(cur, 0);
+  PROBE(d.probe, 4, PROBE_ITERS - 2, 1);
   for (int i = 0; cur < d.N; ++i) {
     const int img = cur;
     const bool more = nxt < d.N;
     const int set = (two && img >= d.img_switch) ? 1 : 0;
     if (set != cur_set) {
+#ifdef APEX_PROBE
+      if (i == 0 && (d.probe_split & 1)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (i == 0) PROBE(d.probe, 4, PROBE_ITERS - 2, 2);
+#endif
       load_weights(set);      // vmcnt(0): every DMA issued so far has landed as well
       cur_set = set;
+      if (i == 0) PROBE(d.probe, 4, PROBE_ITERS - 2, 3);
       __syncthreads();
     }
     sl4_t nsl = (sl4_t){0, 0, 0, 0};                  // image i + 1's frame slots
@@ -526,6 +541,13 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
 #pragma unroll
     for (int q = 0; q < 12; ++q) store_y2(q);   // the last image's y2
   }
+  PROBE(d.probe, 4, PROBE_ITERS - 1, 1);          // every store issued (diagnostic build)
+#ifdef APEX_PROBE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (d.probe != nullptr && blockIdx.x < PROBE_BLOCKS && (threadIdx.x & 63) == 0)
+    d.probe[((blockIdx.x * 4 + (threadIdx.x >> 6)) * PROBE_ITERS + PROBE_ITERS - 1) * 4 + 3] =
+        __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 static int cf_launch_pack(const Conv12Desc& d, hipStream_t st) {

@@ -1208,6 +1208,10 @@ struct RedJob {
   int nsplit, nb, s2dC, Kc;
   float scale;
   int blk0;                  // first block of this job
+  int cpb;                   // 16-float4 column chunks per block (>= 1: wide jobs, fewer blocks);
+                             // < 0: direct mode (few splits): one float4 column per thread,
+                             // -cpb passes of 256 columns per block, splits summed in order
+  double* jnorm;             // null, or this job's own squared-norm partials: jnorm[block - blk0]
 };
 
 struct FinalizeDesc {
@@ -1231,56 +1235,94 @@ __global__ void __launch_bounds__(256) grad_finalize_kernel(FinalizeDesc d) {
   for (int k = 0; k < 4; ++k)
     if (k < d.njobs && b >= d.job[k].blk0) j = k;
   const int last_blk = d.nblocks - 1;
+  double* jn = nullptr;                // the block's slot in its job's own partials (RedJob.jnorm)
   if (d.nrm_n > 0 && b == last_blk) {
     for (int i = threadIdx.x; i < d.nrm_n; i += 256) ss += d.nrm_ptr[i] * d.nrm_ptr[i];
-  } else if (j >= 0) {
+  } else if (j >= 0 && d.job[j].cpb < 0) {
+    // direct mode: thread = float4 column, the splits summed in order 0, 1, ... (the same
+    // values as the 16-group reduction when nsplit <= 16)
     const RedJob& J = d.job[j];
-    const int lb = b - J.blk0;
-    const int64_t nwb = (J.n / 4 + 15) / 16;
+    const int lb = b - J.blk0, np = -J.cpb;
+    const int64_t nwb = (J.n / 4 + 256 * np - 1) / (256 * np);
     const bool bias = lb >= nwb;
     const float* src = bias ? J.bslab : J.slab;
     const int64_t stride = bias ? J.nb : J.n;
     const int64_t n4 = bias ? J.nb / 4 : J.n / 4;
-    const int64_t c4 = (bias ? (int64_t)(lb - nwb) : (int64_t)lb) * 16 + lc;
-    float4 s = make_float4(0, 0, 0, 0);
-    if (c4 < n4) {
-#pragma unroll 4
-      for (int k = grp; k < J.nsplit; k += 16) {
+    for (int q = 0; q < np; ++q) {
+      const int64_t c4 = ((bias ? (int64_t)(lb - nwb) : (int64_t)lb) * np + q) * 256 + threadIdx.x;
+      if (c4 >= n4) break;
+      float4 a = *reinterpret_cast<const float4*>(src + c4 * 4);
+      for (int k = 1; k < J.nsplit; ++k) {
         const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)k * stride + c4 * 4);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-    }
-    red[grp][lc] = s;
-    __syncthreads();
-    if (grp == 0 && c4 < n4) {
-      float4 a = red[0][lc];
-#pragma unroll
-      for (int g = 1; g < 16; ++g) {
-        const float4 v = red[g][lc];
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
       }
       if (bias) {
         *reinterpret_cast<float4*>(J.bout + c4 * 4) = a;
       } else {
         a.x *= J.scale; a.y *= J.scale; a.z *= J.scale; a.w *= J.scale;
-        int64_t o = c4 * 4;
-        if (J.s2dC > 0) {
-          const int64_t row = o / J.Kc;
-          const int k = (int)(o - row * J.Kc);
-          const int q = k >> 4, r4 = (k >> 2) & 3;
-          const int tap = q / J.s2dC, c = q - tap * J.s2dC;
-          o = row * J.Kc + (c * 8 + 4 * (tap >> 1) + r4) * 8 + 4 * (tap & 1);
-        }
-        *reinterpret_cast<float4*>(J.out + o) = a;
+        *reinterpret_cast<float4*>(J.out + c4 * 4) = a;
       }
-      ss = a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+      ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
     }
+    jn = J.jnorm != nullptr ? J.jnorm + lb : nullptr;
+  } else if (j >= 0) {
+    const RedJob& J = d.job[j];
+    const int lb = b - J.blk0;
+    const int cpb = J.cpb > 1 ? J.cpb : 1;
+    const int64_t nwb = (J.n / 4 + 16 * cpb - 1) / (16 * cpb);
+    const bool bias = lb >= nwb;
+    const float* src = bias ? J.bslab : J.slab;
+    const int64_t stride = bias ? J.nb : J.n;
+    const int64_t n4 = bias ? J.nb / 4 : J.n / 4;
+    // (block-uniform trip count: every thread reaches the barriers)
+    for (int q = 0; q < cpb; ++q) {
+      const int64_t c4 = ((bias ? (int64_t)(lb - nwb) : (int64_t)lb) * cpb + q) * 16 + lc;
+      float4 s = make_float4(0, 0, 0, 0);
+      if (c4 < n4) {
+#pragma unroll 4
+        for (int k = grp; k < J.nsplit; k += 16) {
+          const float4 v = *reinterpret_cast<const float4*>(src + (int64_t)k * stride + c4 * 4);
+          s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+      }
+      if (q > 0) __syncthreads();          // the previous chunk's red[] reads are done
+      red[grp][lc] = s;
+      __syncthreads();
+      if (grp == 0 && c4 < n4) {
+        float4 a = red[0][lc];
+#pragma unroll
+        for (int g = 1; g < 16; ++g) {
+          const float4 v = red[g][lc];
+          a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        if (bias) {
+          *reinterpret_cast<float4*>(J.bout + c4 * 4) = a;
+        } else {
+          a.x *= J.scale; a.y *= J.scale; a.z *= J.scale; a.w *= J.scale;
+          int64_t o = c4 * 4;
+          if (J.s2dC > 0) {
+            const int64_t row = o / J.Kc;
+            const int k = (int)(o - row * J.Kc);
+            const int qq = k >> 4, r4 = (k >> 2) & 3;
+            const int tap = qq / J.s2dC, c = qq - tap * J.s2dC;
+            o = row * J.Kc + (c * 8 + 4 * (tap >> 1) + r4) * 8 + 4 * (tap & 1);
+          }
+          *reinterpret_cast<float4*>(J.out + o) = a;
+        }
+        ss += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+      }
+    }
+    jn = J.jnorm != nullptr ? J.jnorm + lb : nullptr;
   }
-  if (d.norm_part == nullptr) return;
+  if (d.norm_part == nullptr && jn == nullptr) return;
   ss = wave_sum_dpp(ss);
   if ((threadIdx.x & 63) == 0) nred[threadIdx.x >> 6] = ss;
   __syncthreads();
-  if (threadIdx.x == 0) d.norm_part[d.norm_slot0 + b] = (double)nred[0] + nred[1] + nred[2] + nred[3];
+  if (threadIdx.x == 0) {
+    const double t = (double)nred[0] + nred[1] + nred[2] + nred[3];
+    if (d.norm_part != nullptr) d.norm_part[d.norm_slot0 + b] = t;
+    if (jn != nullptr) jn[0] = t;
+  }
 }
 
 // Sum of the squared-norm partials of the step (fc wgrad epilogue + grad_finalize

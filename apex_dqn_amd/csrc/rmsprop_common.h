@@ -22,10 +22,24 @@ __device__ __forceinline__ float is_grad_scale(const double* wnorm, int wn, int 
 // fixed strided subset, then a fixed-order wave / LDS reduction -- deterministic.
 // `gscale` multiplies the gradient first (is_grad_scale); the returned coefficient
 // includes it and sh[1] is the norm of the scaled gradient.
+// `gpre` (n_pre floats, 16-B aligned, or null): a short gradient range whose squares every
+// block sums itself, in the same fixed thread-strided order (the data-parallel step's conv1
+// bucket, all-reduced right before this launch: no separate norm launch on the critical
+// path, learner/dp_step.py).
 __device__ __forceinline__ float clip_coef_from_partials(const double* partials, int npart, float clip,
-                                                         float* sh, float gscale = 1.0f) {
+                                                         float* sh, float gscale = 1.0f,
+                                                         const float* gpre = nullptr, int64_t npre = 0) {
   __shared__ double red[16];
   double s = 0.0;
+  if (gpre != nullptr) {
+    const float4* g4 = reinterpret_cast<const float4*>(gpre);
+    const int64_t n4 = npre / 4;
+    for (int64_t i = threadIdx.x; i < n4; i += blockDim.x) {
+      const float4 v = g4[i];
+      s += (double)(v.x * v.x + v.y * v.y) + (double)(v.z * v.z + v.w * v.w);
+    }
+    for (int64_t i = n4 * 4 + threadIdx.x; i < npre; i += blockDim.x) s += (double)gpre[i] * gpre[i];
+  }
   for (int i = threadIdx.x; i < npart; i += blockDim.x) s += partials[i];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -57,6 +71,8 @@ struct RmspropArgs {
   const double* wnorm;  // batch-max IS normalisation (is_grad_scale), or null
   int wn, wstride;
   CfFragOut fo;         // the fused forward's online operands in fragment order (w1frag null: off)
+  const float* gpre;    // clip norm: a gradient range summed in every block (clip_coef_from_partials), or null
+  int64_t npre;
 };
 
 // one block `bid` of `nblk` (grid-stride over float4 chunks)
@@ -92,7 +108,7 @@ __device__ __forceinline__ void rmsprop_body(const RmspropArgs& A_, int bid, int
     if (centered) mm = m4[i];
   }
   const float coef = clip_coef_from_partials(A_.partials, A_.npart, A_.clip, sh,
-                                             is_grad_scale(A_.wnorm, A_.wn, A_.wstride));
+                                             is_grad_scale(A_.wnorm, A_.wn, A_.wstride), A_.gpre, A_.npre);
   if (bid == 0 && threadIdx.x == 0 && A_.norm_out) A_.norm_out[0] = sh[1];
   const float a1 = 1.0f - alpha;
   auto update = [&](int64_t i, const float4 gg, const float4 pp, const float4 vv, const float4 mm, const bool frag) {

@@ -794,7 +794,7 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                     int32_t* out_nxt2, const double* shard_stats, int shard_rank, int shard_world,
                                     uint64_t shard_seed, float* out_wscale, int64_t mcap, bf16_t* pb_lo,
                                     const double* wnorm, int wn, int wstride, CfFragOut fo, const RmsSegs* seg,
-                                    hipStream_t st) {
+                                    const float* gpre, int64_t npre, hipStream_t st) {
   if (mcap <= 0) mcap = (int64_t)shard_world * B;
   if (shard_stats != nullptr && (B < 3 || shard_world < 1 || shard_rank < 0 || shard_rank >= shard_world))
     return (int)hipErrorInvalidValue;
@@ -842,8 +842,9 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                // (stored in each thread's first chunk: rmsprop_body's peel)
                                (fo.w1_off + 4096LL * fo.C) / 4 > (int64_t)nb * nt || (fo.w2_off + 65536) / 4 > (int64_t)nb * nt))
     return (int)hipErrorInvalidValue;
+  if (((uintptr_t)gpre & 15) || npre < 0 || (npre > 0 && gpre == nullptr)) return (int)hipErrorInvalidValue;
   const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,
-                      wnorm, wn, wstride, fo};
+                      wnorm, wn, wstride, fo, npre > 0 ? gpre : nullptr, npre};
   const SampleArgs sa{t, r, B, seed, ctr, beta, out_idx, out_w, out_gen, out_obs, out_nxt,
                       out_act, out_rew, out_gam, out_nxt2, shard_stats, shard_rank, shard_world, shard_seed,
                       out_wscale, mcap};

@@ -46,6 +46,8 @@ from typing import List, Optional, Tuple
 
 import torch
 
+from ..ops.switches import SW
+
 FC_ROWS, FC_COLS = 1024, 3136
 
 
@@ -100,6 +102,9 @@ class DataParallelStep:
     """Mixin: the DP step of the fused NatureCNN learner.  Needs the learner's buffers,
     ``self.coll`` (parallel/rccl.py), ``self.layout`` and ``self.ops``."""
 
+    _fc_split = False       # sharded update: the fc rows' gradient as split-K partials (_dp_setup)
+    _fc_cpb = -1
+
     # ------------------------------------------------------------------ setup
     def _dp_setup(self) -> None:
         """Sharding decision and the buffers of the sharded update (after the fc
@@ -113,17 +118,28 @@ class DataParallelStep:
         self._params_pending = None     # the last update's fc-row all-gather (sharded)
         self._defer_params = False      # set while capturing an update that another follows
         self._gather_due = None         # (event,): the optimizer point a deferred gather follows
+        hip = self.ops.name == "hip" and getattr(self.ops, "native_conv", False)
+        # the fc weight gradient from the gathered factor rows as split-K partials reduced in
+        # a grad_finalize launch (one norm partial per finalize block), sharded or not -- the
+        # two stay bit-identical
+        self._fc_split = self._dp and self._fc_factors and SW.dp_fc_split_rows > 0
+        S = FC_ROWS // W if self._shard else FC_ROWS
+        self._fc_cpb = -max(1, S // 128)       # direct finalize: ~393 norm partials at any S
         if not self._shard:
             return
         off = self.layout.offsets
-        S = FC_ROWS // W
         self._fc_S, self._fc_r0 = S, rank * S
         o0 = self._fc_r0
         self._segs = [(0, off["wfc"]), (off["wfc"] + o0 * FC_COLS, S * FC_COLS), (off["bfc"] + o0, S)]
         # this rank's fc-slice clip-norm partials (sent) and the gathered ones (norm_part[:W
         # nfc]): the fc wgrad kernel writes 4 per workgroup (ops/conv.py wgrad_blocks), the
         # torch backend and the sqnorm kernel's 64-block launch fewer
-        if self._fc_factors and self.ops.name == "hip" and getattr(self.ops, "native_conv", False):
+        if self._fc_factors and hip and self._fc_split:
+            # split-K partials reduced in conv1's grad_finalize launch: one norm partial per
+            # finalize block of the fc job (ops/conv.py finalize_job_blocks)
+            from ..ops.conv import finalize_job_blocks
+            nfc = finalize_job_blocks(dict(n=S * FC_COLS, nb=S, cpb=self._fc_cpb))
+        elif self._fc_factors and hip:
             from ..ops.conv import wgrad_blocks
             nfc = 4 * wgrad_blocks(S, FC_COLS, 1 if self.split else 0)
         else:
@@ -241,16 +257,25 @@ class DataParallelStep:
                 else:
                     works["fc"] = coll.all_reduce(self.gcomm[cut:])
                 works["stats"] = self.replay.gather_shard_stats(async_op=True, coll=coll, fresh_local=fresh)
+            nfc = 0
+            fc_on_branch = shard and SW.dp_fc_shard_branch
+            if fc_on_branch:
+                # this rank's fc rows of the global batch's gradient (+ their clip-norm
+                # partials) right behind the exchange, on the branch: no main-stream wait
+                # on the branch's exchange (one cross-queue edge fewer on the critical path)
+                works["fc"].wait()
+                nfc = self._fc_shard_grad_norm()
         # conv3 / conv2 data gradients on main, conv3's weight gradient on the branch
-        ev3 = br.mark()
+        one_wait = SW.dp_branch_one_wait
+        ev3 = None if one_wait else br.mark()
         ops.conv_dgrad(self.dY3, Pb["w3"], 1, self.y2[:B], self.dY2,
                        **self._lo(dy_lo=self.dY3_lo, w_lo=sp and Pl["w3"], dx_lo=self.dY2_lo))
-        with br.branch(ev3):
-            self._conv3_wgrad(jobs)
+        if not one_wait:
+            with br.branch(ev3):
+                self._conv3_wgrad(jobs)
         ev2 = br.mark()
         ops.conv_dgrad(self.dY2, Pb["w2"], 2, self.y1[:B], self.dY1,
                        **self._lo(dy_lo=self.dY2_lo, w_lo=sp and Pl["w2"], dx_lo=self.dY1_lo))
-        nfc = 0
         # the branch's conv2 wgrad, then conv1's wgrad on main.  The fc exchange's result
         # reaches the branch by stream order: the collectives were issued from the branch
         # (graphs: the comm stream IS the branch; eager torch: the work handle's wait).
@@ -259,6 +284,10 @@ class DataParallelStep:
         # replayed graph (trace r5_emu8e: ~28 us idle; 5,025-5,033 vs 5,128-5,158 updates/s
         # emulated at W = 8, profiles/r5_ab_dp_capture_order.txt).
         with br.branch(ev2):
+            if one_wait:
+                # (one main-stream event for both weight gradients: conv2 dgrad's input is
+                # conv3 dgrad's output, so both are ready at this point)
+                self._conv3_wgrad(jobs)
             self._conv2_wgrad(jobs)
         jobs1 = []
         ops.conv1_wgrad_ring(self.dY1, self.replay.frames, self.slots[:B], self.frames, rt.obs_scale, G["w1"],
@@ -266,6 +295,10 @@ class DataParallelStep:
         with br.branch():
             if factors and not shard:
                 works["fc"].wait()
+                if self._fc_split:
+                    # the global batch's whole fc weight gradient as split-K partials,
+                    # reduced in the branch's finalize launch below (norm partials first)
+                    nfc = self._fc_wgrad_gathered(jobs)
             # conv2 / conv3 / head bucket [w2, wfc): reduced on the branch and all-reduced
             # from it while conv1's weight gradient runs -- only conv1's bucket follows the
             # last backward kernel
@@ -273,22 +306,33 @@ class DataParallelStep:
             if self._comm_bf16:
                 self.gcomm[o2:cut].copy_(self.g32[o2:cut])
             works["cv2"] = coll.all_reduce(self.gcomm[o2:cut])
-            if factors and not shard:
+            n_pre = 0
+            if shard and SW.dp_norm_split:
+                # the clip-norm partials of the reduced [w2, wfc) bucket, on the branch right
+                # behind its all-reduce; conv1's bucket -- reduced last, on main -- is summed
+                # inside the optimizer launch (norm_prefix): no norm launch on the critical path
+                works["cv2"].wait()
+                n_pre = ops.sqnorm_ranges((self.g32[o2:cut],), self.norm_part, 64)
+            if factors and not shard and not self._fc_split:
                 # the global batch's whole fc weight gradient (identical on every rank)
                 nfc = self._fc_wgrad_gathered()
+        if shard and not fc_on_branch and self._fc_split:
+            # this rank's fc rows of the global batch's gradient as split-K partials (the
+            # rows fill the chip only when the reduction is split), reduced in conv1's
+            # finalize launch with one clip-norm partial per finalize block
+            works["fc"].wait()
+            nfc = self._fc_shard_grad_norm(jobs1)
         ops.finalize_grads(jobs1, None, None)
-        if shard:
+        if shard and not fc_on_branch and not self._fc_split:
             # this rank's fc rows of the global batch's gradient (+ their clip-norm partials)
-            # on main after conv1's: the branch carries the exchange, conv3 / conv2 wgrads
-            # and the [w2, wfc) bucket, the main stream would otherwise idle here (the
-            # exchange finished long before: this wait costs one edge, no stall)
+            # on main after conv1's (the exchange finished long before: one edge, no stall)
             works["fc"].wait()
             nfc = self._fc_shard_grad_norm()
         self._npart = 0
         self._mark("conv_backward")
         if self._comm_bf16:
             self.gcomm[:o2].copy_(self.g32[:o2])
-        fcn = (self.norm_part[:self.world * nfc], self.fcn_send[:nfc]) if shard else None
+        fcn = (self.norm_part[n_pre:n_pre + self.world * nfc], self.fcn_send[:nfc]) if shard else None
         if getattr(coll, "inline", False) and self._ordered_coll:
             # conv1's bucket (+ the fc clip-norm partials) on the main stream itself, one
             # RCCL launch: one join of the branch (in order: covers every collective issued
@@ -315,9 +359,12 @@ class DataParallelStep:
                 w_cv.wait()
         self._mark("allreduce_wait")
         if shard:
-            n0 = self.world * nfc
-            nr = ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[n0:], 64)
-            self._seg3(norm_slots=n0 + nr, segs=self._segs)
+            if n_pre:
+                self._seg3(norm_slots=n_pre + self.world * nfc, segs=self._segs, norm_prefix=self.g32[:o2])
+            else:
+                n0 = self.world * nfc
+                nr = ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[n0:], 64)
+                self._seg3(norm_slots=n0 + nr, segs=self._segs)
             if self._defer_params and self._streams.cuda:
                 # inside a multi-update capture: issued once the next update's conv12 is
                 # enqueued (forward_all -> _issue_params), so conv12 stays the optimizer's
@@ -338,21 +385,34 @@ class DataParallelStep:
         cols = [R[:, c[i]:c[i + 1]] for i in range(len(self._fx_cols))]
         return (cols[0], cols[1], cols[2], cols[3]) if self.split else (cols[0], None, cols[1], None)
 
-    def _fc_wgrad_gathered(self) -> int:
+    def _fc_wgrad_gathered(self, jobs=None) -> int:
         """The fc weight gradient of the global batch from the all-gathered (dH, X) rows
         (identical on every rank), with its clip-norm partials in norm_part[0:].
-        Returns the partial slots written."""
+        Returns the partial slots written.  With ``jobs``: split-K partials reduced by the
+        finalize launch of ``jobs`` (``SW.dp_fc_split_rows``)."""
         dy, dy_lo, x, x_lo = self._gathered_cols()
+        if jobs is not None:
+            return self.ops.fc_wgrad_split(dy, x, self.G["wfc"], self.G["bfc"], jobs, int(SW.dp_fc_split_rows),
+                                           self.norm_part, cpb=self._fc_cpb, **self._lo(dh_lo=dy_lo, x_lo=x_lo))
         return self.ops.fc_wgrad(dy, x, self.G["wfc"], self.G["bfc"], norm=(self.norm_part, 0),
                                  **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
 
-    def _fc_shard_grad_norm(self) -> int:
+    def _fc_shard_grad_norm(self, jobs=None) -> int:
         """Sharded update: this rank's fc rows of the gradient (factors: computed from the
         gathered rows; allreduce exchange: already reduce-scattered) and their squared-norm
-        partials in ``fcn_send``.  Returns the partial count (equal on every rank)."""
+        partials in ``fcn_send``.  Returns the partial count (equal on every rank).  With
+        ``jobs`` (factors, ``SW.dp_fc_split_rows``): split-K partials, reduced by the
+        finalize launch of ``jobs`` that writes the norm partials."""
         _, w_own = self._fc_rows(self.g32)
         _, b_own = self._fc_bias(self.g32)
-        if self._fc_factors:
+        if self._fc_factors and jobs is not None:
+            dy, dy_lo, x, x_lo = self._gathered_cols()
+            r0, S = self._fc_r0, self._fc_S
+            n = self.ops.fc_wgrad_split(dy[:, r0:r0 + S], x, w_own.view(S, FC_COLS), b_own, jobs,
+                                        int(SW.dp_fc_split_rows), self.fcn_send,
+                                        cpb=self._fc_cpb,
+                                        **self._lo(dh_lo=None if dy_lo is None else dy_lo[:, r0:r0 + S], x_lo=x_lo))
+        elif self._fc_factors:
             dy, dy_lo, x, x_lo = self._gathered_cols()
             r0, S = self._fc_r0, self._fc_S
             n = self.ops.fc_wgrad(dy[:, r0:r0 + S], x, w_own.view(S, FC_COLS), b_own,

@@ -512,11 +512,12 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         self.num_q_updates += 1
         return out
 
-    def _seg3(self, norm_slots: Optional[int] = None, segs=None) -> None:
+    def _seg3(self, norm_slots: Optional[int] = None, segs=None, norm_prefix=None) -> None:
         """clip + centered RMSprop (+ bf16 hi / lo pack) with the next batch's draw.
         ``norm_slots``: the clip norm is the sum of ``norm_part[:norm_slots]`` (written by
-        the gradient producers of the DP step).  ``segs``: the flat ranges to update (the
-        sharded DP update, learner/dp_step.py)."""
+        the gradient producers of the DP step) plus, with ``norm_prefix``, the squares of
+        that gradient range (summed inside the launch).  ``segs``: the flat ranges to
+        update (the sharded DP update, learner/dp_step.py)."""
         rt, ops = self.rt, self.ops
         if self._comm_bf16:
             self.g32.copy_(self.gcomm)
@@ -529,7 +530,8 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
                       ((self.norm_part, norm_slots) if norm_slots else None), sample=nxt,
                       wnorm=self._wnorm(), **self._lo(pb_lo=self.pbf_lo),
                       **({"frag_out": self._frag_out} if (self._frag_out is not None and nxt is not None) else {}),
-                      **({"segs": segs} if segs is not None else {}))
+                      **({"segs": segs} if segs is not None else {}),
+                      **({"norm_prefix": norm_prefix} if norm_prefix is not None else {}))
         if self._presample:
             self._sample_ver = self.replay.version
         self._mark("optimizer")

@@ -103,7 +103,8 @@ class WgradDesc(ctypes.Structure):
 class RedJob(ctypes.Structure):
     """One split-K finalisation job (mirrors ``RedJob`` in csrc/conv_mfma.hip)."""
     _fields_ = [("slab", c_p), ("bslab", c_p), ("out", c_p), ("bout", c_p), ("n", c_i64),
-                ("nsplit", c_i), ("nb", c_i), ("s2dC", c_i), ("Kc", c_i), ("scale", c_f), ("blk0", c_i)]
+                ("nsplit", c_i), ("nb", c_i), ("s2dC", c_i), ("Kc", c_i), ("scale", c_f), ("blk0", c_i),
+                ("cpb", c_i), ("jnorm", c_p)]
 
 
 class FinalizeDesc(ctypes.Structure):
@@ -153,8 +154,8 @@ _SIGS = {
                         c_p, c_p, c_p, c_p, c_p, c_i, c_i, HeadLo, HeadPart, C2dPack, IsNorm, c_p], c_i),
     "apex_rmsprop_sample": ([c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_i, c_f, c_f, c_f, c_f, c_i, c_p,
                              TreeDesc, RecordDesc, c_i, c_u64, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
-                             c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut, c_p, c_p],
-                            c_i),
+                             c_p, c_p, c_i, c_i, c_u64, c_p, c_i64, c_p, c_p, c_i, c_i, CfFragOut, c_p, c_p, c_i64,
+                             c_p], c_i),
     "apex_head_wgrad_prio": ([c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p, c_p, c_f, c_f,
                               c_p, c_p, c_p, c_p, c_p, c_p, c_i, c_i, c_p, c_i64, c_p], c_i),
     "apex_fc_wgrad_head_prio": ([WgradDesc, c_p, c_p, c_i, c_i, c_p, c_p, c_p, c_p, c_i, TreeDesc, c_p, c_p, c_p,

@@ -175,21 +175,29 @@ class _Plan:
         return read_stamp(self.lib) == self.build_id
 
 
+DEBUG_ONLY_SOURCES = ("cu_steal.hip",)
+
+
 def kernel_plan(debug: bool = False) -> _Plan:
     """``libapex_kernels(.debug).so``: every csrc/*.hip; the debug library builds the
     sources with debug checks or probes with -DAPEX_DEBUG_BOUNDS -DAPEX_PROBE (plus
     ``APEX_DEBUG_DEFS``), the rest are the release objects."""
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    every = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    # benchmark-only kernels (cu_steal.hip: the CU-steal proxy of scripts/bench_cu_steal.py)
+    # ship in the diagnostic library only
+    srcs = [s for s in every if os.path.basename(s) not in DEBUG_ONLY_SOURCES]
     hdrs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.cuh"))
     if not debug:
         return _Plan(KERNEL_LIB, HIPCC, HIP_FLAGS, srcs, hdrs, "kernels",
                      link=["-shared", "-fPIC", f"--offload-arch={ARCH}"])
+    srcs = every
     # APEX_DEBUG_DEFS: extra space-separated -D flags for the diagnostic library only
-    # (kernel experiments behind #ifdef, e.g. scripts/probe_conv12.py); part of the keys
+    # (kernel experiments behind #ifdef, e.g. scripts/archive/probe_conv12.py); part of the keys
     extra = [f for f in os.environ.get("APEX_DEBUG_DEFS", "").split() if f.startswith("-D")]
     dflags = HIP_FLAGS + ["-DAPEX_DEBUG_BOUNDS", "-DAPEX_PROBE"] + extra
     rel = kernel_plan(False)
-    dbg_srcs = [s for s in srcs if ("APEX_DEBUG_BOUNDS" in open(s).read() or "PROBE(" in open(s).read())]
+    dbg_srcs = [s for s in srcs if ("APEX_DEBUG_BOUNDS" in open(s).read() or "PROBE(" in open(s).read()
+                                    or os.path.basename(s) in DEBUG_ONLY_SOURCES)]
     dp = _Plan(KERNEL_DEBUG_LIB, HIPCC, dflags, dbg_srcs, hdrs, "kernels_debug", obj_suffix=".dbg.o",
                link=["-shared", "-fPIC", f"--offload-arch={ARCH}"])
     # the release objects of the other sources join the debug library

@@ -280,7 +280,7 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
                      y2: torch.Tensor, y2_lo: torch.Tensor, y1: Optional[torch.Tensor] = None,
                      y1_lo: Optional[torch.Tensor] = None, copy_n: int = 0, w1b=None, b1b=None, w2b=None,
                      w2b_lo=None, b2b=None, rows_first: int = 0, grid: int = 0,
-                     probe: Optional[torch.Tensor] = None, pack_sets: int = 3) -> None:
+                     probe: Optional[torch.Tensor] = None, pack_sets: int = 3, probe_split: int = 0) -> None:
     """conv1 (fp32 OIHW weights ``w1``, exact uint8 frames from the s2d ring) + ReLU ->
     conv2 (hi / lo bf16 OHWI ``w2``, ``w2_lo``) + ReLU in one persistent launch, y1 kept
     in LDS; rows < ``copy_n`` also store y1 (hi / lo) for the backward.  Rows >=
@@ -304,6 +304,7 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     d.pack_sets = int(pack_sets)
     d.N = N
     d.probe = _lib.ptr(probe)
+    d.probe_split = int(probe_split)
     d.wq = ws.wq(("cf_wq", N, int(grid)), ring.device, overlapped=False)
     _lib.check(lib.apex_conv12_fused_fwd(d, int(grid), _lib.stream_ptr()), "conv12_fused_fwd")
 
@@ -661,6 +662,39 @@ def finalize_blocks(jobs: list, norm_range: Optional[torch.Tensor]) -> int:
     return n + (1 if norm_range is not None else 0)
 
 
+def finalize_job_blocks(j: dict) -> int:
+    """grad_finalize blocks of one job: 16 float4 columns per block, ``cpb`` times that
+    for a wide job (csrc/conv_mfma.hip RedJob)."""
+    c = int(j.get("cpb", 1))
+    w = 256 * -c if c < 0 else 16 * max(1, c)       # (cpb < 0: direct mode, 256 columns per pass)
+    return (j["n"] // 4 + w - 1) // w + (j["nb"] // 4 + w - 1) // w
+
+
+def dense_wgrad_split(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, nsplit: int, dw_out: torch.Tensor,
+                      db_out: torch.Tensor, jobs: list, dy_lo=None, x_lo=None, cpb: int = -1,
+                      jnorm: Optional[torch.Tensor] = None) -> int:
+    """dW[N,K] = dy[M,N]^T @ x[M,K] as ``nsplit`` split-K partial slabs (the small-batch DP
+    step's fc rows: a few row tiles over a long reduction fill the chip only when the
+    reduction rows are split), reduced by the step's ``grad_finalize`` launch: the job is
+    appended to ``jobs`` (``cpb``: finalize blocks of -cpb x 256 columns, one thread per
+    column, the splits summed in order; with ``jnorm`` the job's squared-norm partials, one
+    per finalize block).  Returns that block count."""
+    M, Nc = dy.shape
+    K = x.shape[1]
+    rows = -(-M // nsplit)
+    rows = -(-rows // 64) * 64
+    nsplit = -(-M // rows)
+    slab = ws.get(("wgd", Nc, K, nsplit), nsplit * Nc * K, dy.device)
+    bslab = ws.get(("wgdb", Nc, nsplit), nsplit * Nc, dy.device)
+    d = _dense_wgrad_desc(dy, x, slab, bslab, None, dy_lo, x_lo)
+    d.rows_per_split = rows
+    _lib.check(lib.apex_conv_wgrad(d, None, None, nsplit, 1.0, _lib.stream_ptr()), "dense_wgrad_split")
+    j = dict(slab=slab, bslab=bslab, out=dw_out, bout=db_out, n=Nc * K, nsplit=nsplit, nb=Nc, s2dC=0, Kc=K,
+             scale=1.0, cpb=int(cpb), jnorm=jnorm)
+    jobs.append(j)
+    return finalize_job_blocks(j)
+
+
 def finalize_grads(lib, jobs: list, norm_range: Optional[torch.Tensor] = None, norm_part=None, slot0: int = 0,
                    total=None) -> int:
     """One launch for every deferred split-K reduction; with ``norm_part`` also the
@@ -676,7 +710,9 @@ def finalize_grads(lib, jobs: list, norm_range: Optional[torch.Tensor] = None, n
             j["bout"].data_ptr()
         J.n, J.nsplit, J.nb, J.s2dC, J.Kc, J.scale, J.blk0 = j["n"], j["nsplit"], j["nb"], j["s2dC"], j["Kc"], \
             j["scale"], blk
-        blk += (j["n"] // 4 + 15) // 16 + (j["nb"] // 4 + 15) // 16
+        J.cpb = int(j.get("cpb", 1))
+        J.jnorm = _lib.ptr(j.get("jnorm"))
+        blk += finalize_job_blocks(j)
     d.njobs = len(jobs)
     if norm_range is not None and norm_part is not None:
         d.nrm_ptr, d.nrm_n = norm_range.data_ptr(), norm_range.numel()

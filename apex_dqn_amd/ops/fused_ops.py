@@ -240,6 +240,14 @@ class TorchBackend:
         part[s0] = dw_out.double().pow(2).sum() + db_out.double().pow(2).sum()
         return 1
 
+    def fc_wgrad_split(self, dh, x, dw_out, db_out, jobs, split_rows: int, jnorm, dh_lo=None, x_lo=None,
+                       cpb: int = -1) -> int:
+        """The fc weight gradient as split-K partials reduced by the step's
+        ``finalize_grads`` (HIP: a job appended to ``jobs``); its squared-norm partials go
+        to ``jnorm`` (one per finalize block).  Returns the partial count.  The torch
+        path computes it at once (one partial)."""
+        return self.fc_wgrad(dh, x, dw_out, db_out, norm=(jnorm, 0), dh_lo=dh_lo, x_lo=x_lo)
+
     def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None, dh_lo=None, x_lo=None,
                       Hon_lo=None) -> int:
         """fc weight gradient + head weight gradient (+ the priority write-back,
@@ -273,7 +281,7 @@ class TorchBackend:
 
     # ----------------------------------------------------------- optimizer
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None, frag_out=None, segs=None):
+                  sample=None, pb_lo=None, wnorm=None, frag_out=None, segs=None, norm_prefix=None):
         """``sample = (replay, B, out, nxt2)``: also draw the next
         batch after the update (the HIP backend fuses it into the optimizer launch).
         ``pb_lo``: split mode, the lo plane of the bf16 copy.  ``wnorm = (stats, n,
@@ -282,15 +290,16 @@ class TorchBackend:
         ``norm_total = (partials, n)``: the clip norm is sqrt(sum(partials[:n])) (squared-norm
         partials written by the gradient producers) instead of a pass over ``g32``.
         ``segs``: [(offset, length), ...] -- update only these ranges of the flat arrays
-        (the sharded data-parallel update; needs ``norm_total``)."""
+        (the sharded data-parallel update; needs ``norm_total``).  ``norm_prefix``: a
+        gradient range whose squares join the partials' sum (summed inside the launch)."""
         self._optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo, wnorm, norm_total,
-                        segs)
+                        segs, norm_prefix)
         if sample is not None:
             rp, B, out, nxt2 = sample
             rp.sample(B, out=out, nxt2=nxt2)
 
     def _optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, norm_out, pb_lo=None, wnorm=None,
-                   norm_total=None, segs=None):
+                   norm_total=None, segs=None, norm_prefix=None):
         sc = torch.ones((), dtype=torch.float32, device=g32.device)
         if wnorm is not None:     # tensor ops only: no host sync (graph-capturable)
             st, n, stride = wnorm
@@ -299,6 +308,8 @@ class TorchBackend:
         if norm_total is not None:
             part, npart = norm_total if isinstance(norm_total, tuple) else (norm_total, 1)
             sq = part[:npart].double().sum()
+            if norm_prefix is not None:
+                sq = sq + norm_prefix.double().pow(2).sum()
         else:
             assert segs is None, "a sharded update needs the clip norm's partials (norm_total)"
             sq = g32.double().pow(2).sum()
@@ -451,6 +462,15 @@ class HipBackend(TorchBackend):
         return C.dense_wgrad(self.lib, dh, x.reshape(x.shape[0], -1), dw_out, db_out, norm=norm, dy_lo=dh_lo,
                              x_lo=None if x_lo is None else x_lo.reshape(x.shape[0], -1))
 
+    def fc_wgrad_split(self, dh, x, dw_out, db_out, jobs, split_rows: int, jnorm, dh_lo=None, x_lo=None,
+                       cpb: int = -1) -> int:
+        if not self.native_conv:
+            return super().fc_wgrad_split(dh, x, dw_out, db_out, jobs, split_rows, jnorm, dh_lo, x_lo, cpb)
+        M = dh.shape[0]
+        return C.dense_wgrad_split(self.lib, self.ws, dh, x.reshape(M, -1), max(1, -(-M // int(split_rows))),
+                                   dw_out, db_out, jobs, dy_lo=dh_lo,
+                                   x_lo=None if x_lo is None else x_lo.reshape(M, -1), cpb=cpb, jnorm=jnorm)
+
     def fc_head_wgrad(self, dh, x, dw_out, db_out, Hon, dhead, g_head, prio, norm=None, dh_lo=None, x_lo=None,
                       Hon_lo=None) -> int:
         if self.native_conv and prio is not None and prio[0].use_hip:
@@ -555,7 +575,7 @@ class HipBackend(TorchBackend):
                                             P["wv"].numel(), _lib.ptr(H_lo), _lib.stream_ptr()), "actor_head")
 
     def optimizer(self, p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total=None,
-                  sample=None, pb_lo=None, wnorm=None, frag_out=None, segs=None) -> bool:
+                  sample=None, pb_lo=None, wnorm=None, frag_out=None, segs=None, norm_prefix=None) -> bool:
         """``frag_out`` (ops/conv.py conv12_frag_out): the launch also stores the updated
         w1 / w2 in the fused forward's fragment order.  Returns whether it did (the fused
         optimizer + sample launch only).  ``segs``: the ranges to update (the sharded DP
@@ -593,8 +613,10 @@ class HipBackend(TorchBackend):
                 p32.data_ptr(), g32.data_ptr(), v.data_ptr(), m.data_ptr(), pbf.data_ptr(), n, part.data_ptr(), npart,
                 float(lr), float(alpha), float(eps), float(clip), int(centered), norm_out.data_ptr(),
                 *rp.sample_launch_args(B, out, nxt2), lo, *wn, frag_out if frag_out is not None else _lib.CfFragOut(),
-                segp, st), "rmsprop_sample")
+                segp, _lib.ptr(norm_prefix), 0 if norm_prefix is None else norm_prefix.numel(), st), "rmsprop_sample")
             return frag_out is not None
+        if norm_prefix is not None:
+            raise ValueError("norm_prefix runs in the fused optimizer + sample launch")
         if sample is not None:
             self.optimizer(p32, g32, v, m, pbf, lr, alpha, eps, clip, centered, partials, norm_out, norm_total,
                            pb_lo=pb_lo, wnorm=wnorm)

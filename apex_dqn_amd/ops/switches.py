@@ -74,6 +74,21 @@ class Switches:
     # (conv rows), wg<cin>x<cout>x<H>=R/threads (weight-gradient variant), wt<cin>x<cout>x<H>=N
     # (weight-gradient workgroup target)
     isplit_bands: str = ""
+    # DP step (learner/dp_step.py): the sharded update's fc weight gradient on the branch
+    # right behind the factor exchange (True) or on main after conv1's weight gradient
+    # (False: emulated W = 8 160.5-162.1 vs 178.6-180.7 us, W = 4 201.5-202.0 vs
+    # 199.7-203.6 -- the branch becomes the critical chain; profiles/r6_ab_dp_switches.txt)
+    dp_fc_shard_branch: bool = False
+    # DP step: one main-stream event for the branch's conv3 + conv2 weight gradients
+    dp_branch_one_wait: bool = False
+    # DP step, sharded update with the factored exchange: this rank's fc weight-gradient rows
+    # as split-K partials of this many reduction rows each, reduced in conv1's finalize
+    # launch (0: one launch over all rows writing the gradient itself)
+    dp_fc_split_rows: int = 128
+    # DP step, sharded update: the [w2, wfc) bucket's clip-norm partials on the branch and
+    # conv1's bucket summed inside the optimizer launch (no norm launch on main; emulated W =
+    # 8 with the fc gradient on main: 160.5-162.1 us vs 166-169 before)
+    dp_norm_split: bool = True
 
     @classmethod
     def from_env(cls, spec: str = None) -> "Switches":

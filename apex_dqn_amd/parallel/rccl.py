@@ -304,7 +304,7 @@ class TorchCollectives:
     group's own stream, forked from the current stream; their handles are waited for on
     the step's main (capture-origin) stream only -- a forked stream that waits on a
     stream forked from itself crashed HIP graph capture (hipStreamEndCapture segfault,
-    round 5, ``scripts/probe_dp_capture.py``), so this backend runs the DP step eagerly
+    round 5, ``scripts/archive/probe_dp_capture.py``), so this backend runs the DP step eagerly
     (learner/fused_learner.py ``_dp_graphs``).  gloo (CPU
     tests, one-GPU rehearsals) keeps the process group's own handles."""
     name = "torch"

@@ -10,7 +10,8 @@ So before the parent process makes ANY HIP call, every rank spawns ONE fresh chi
 
 * joins its own rendezvous -- the same TCP store as torch.distributed (the torchrun
   agent's store, or rank 0's), under the key prefix ``apex_capture_probe/<restart>`` --
-  with a gloo process group for host-side collectives and its own RCCL communicator,
+  with an RCCL process group for host-side collectives and its own native RCCL
+  communicator for the step, as the parent will have,
 * builds each learner variant the parent will run on a small synthetic replay,
   captures the DP step's graphs and replays them once, checks the update is finite,
 * writes a per-variant verdict into the store and exits.
@@ -131,12 +132,15 @@ def _child() -> int:
     from ..config import ApexConfig
     from ..parallel.dist import Comm
     store = _store(rank, world, 120.0, client=True)
-    dist.init_process_group("gloo", store=dist.PrefixStore(pre + "/pg", store), rank=rank, world_size=world,
-                            timeout=datetime.timedelta(seconds=120))
     res = {v["name"]: True for v in spec["variants"]} if dry else {}
     dev = torch.device("cuda", int(spec["local_rank"])) if not dry else torch.device("cpu")
+    # the parent's arrangement: an RCCL process group (host-side collectives, the native
+    # communicator's id exchange) beside the native communicator of the step
+    kw = {} if dry else {"device_id": dev}
     if not dry:
         torch.cuda.set_device(dev)
+    dist.init_process_group("gloo" if dry else "nccl", store=dist.PrefixStore(pre + "/pg", store), rank=rank,
+                            world_size=world, timeout=datetime.timedelta(seconds=120), **kw)
     comm = Comm(rank, world, dev)
     for v in ([] if dry else spec["variants"]):
         cfg = ApexConfig.from_dict(v["cfg"])

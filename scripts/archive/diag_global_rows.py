@@ -10,7 +10,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import bench  # noqa: E402
 from apex_dqn_amd.parallel.dist import Comm  # noqa: E402
 from apex_dqn_amd.replay.gpu_replay import SHARD_STATS, global_draw  # noqa: E402

@@ -8,7 +8,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from apex_dqn_amd.config import ApexConfig  # noqa: E402
 from apex_dqn_amd.learner.fused_learner import FusedNatureLearner  # noqa: E402

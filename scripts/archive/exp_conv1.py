@@ -2,7 +2,7 @@
 """conv1 s2d forward experiments: locality of the frame ring and grid size."""
 import json, os, sys
 import torch
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from apex_dqn_amd.ops import _lib, conv as C
 
 lib = _lib.require_kernels()

@@ -12,7 +12,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def setup(B, dev):
@@ -32,18 +32,19 @@ def setup(B, dev):
     return dict(ring=ring, slots=slots, w1=w1, w2h=w2h, w2l=w2l, b=b, y1=y1, y1l=y1l, y2=y2, y2l=y2l, N=N)
 
 
-def launch(lib, C, ws, t, B, copy=True, grid=0, probe=None, bf16=False):
+def launch(lib, C, ws, t, B, copy=True, grid=0, probe=None, bf16=False, split=0):
     lo = (lambda k: None) if bf16 else (lambda k: t[k])      # noqa: E731
     C.conv12_fused_fwd(lib, ws, t["ring"], t["slots"], t["w1"], t["b"], t["w2h"], lo("w2l"), t["b"], 1 / 255.0,
                        t["y2"], lo("y2l"), y1=t["y1"], y1_lo=lo("y1l"), copy_n=B if copy else 0, w1b=t["w1"],
                        b1b=t["b"], w2b=t["w2h"], w2b_lo=lo("w2l"), b2b=t["b"], rows_first=2 * B, grid=grid,
-                       probe=probe)
+                       probe=probe, probe_split=split)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=512)
     ap.add_argument("--probe", action="store_true")
+    ap.add_argument("--split", type=int, default=0, help="probe: wait for the first frames before the weights")
     ap.add_argument("--bf16", action="store_true", help="the bf16 learner's one-plane kernel")
     a = ap.parse_args()
     if a.probe:
@@ -58,11 +59,23 @@ def main():
         for _ in range(3):
             launch(lib, C, ws, t, a.B, bf16=a.bf16)
         buf.zero_()
-        launch(lib, C, ws, t, a.B, probe=buf, bf16=a.bf16)
+        launch(lib, C, ws, t, a.B, probe=buf, bf16=a.bf16, split=a.split)
         torch.cuda.synchronize()
         st = buf.cpu().numpy().reshape(4, 4, 16, 4)
+        p14 = st[:, :, 14, :]        # prologue: dma issue, [frames landed], weights landed
+        print(json.dumps({"split": a.split, "entry_to_dma_issue": int(np.median(p14[:, :, 0] - st[:, :, 15, 0])),
+                          "dma_issue": int(np.median(p14[:, :, 1] - p14[:, :, 0])),
+                          "to_before_weights": int(np.median(p14[:, :, 2] - p14[:, :, 1])),
+                          "weights": int(np.median(p14[:, :, 3] - p14[:, :, 2])),
+                          "barrier_to_conv1": int(np.median(st[:, :, 0, 0] - p14[:, :, 3]))}))
         names = ["conv1", "wait_copy", "conv2"]
-        for it in range(16):
+        sp = st[:, :, 15, :]          # kernel entry / exit stamps (csrc/conv12_fused.hip)
+        last = max(it for it in range(15) if np.all(st[:, :, it, 0] > 0))
+        print(json.dumps({"prologue_to_conv1_it0": int(np.median(st[:, :, 0, 0] - sp[:, :, 0])),
+                          "last_conv2_end_to_exit": int(np.median(sp[:, :, 1] - st[:, :, last, 3])),
+                          "block_wall_us_realtime": float(np.median(sp[:, :, 3] - sp[:, :, 2])) / 100.0,
+                          "entry_skew_us": float(sp[:, :, 2].max() - sp[:, :, 2].min()) / 100.0}))
+        for it in range(14):
             row = st[:, :, it, :]
             if not np.all(row > 0):
                 continue

@@ -13,7 +13,7 @@ VARIANTS = ["emu_noshard", "emu_shard", "native_w1", "native_w1_shard", "native_
 
 
 def child(name: str) -> None:
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
     import numpy as np
     import torch
     from apex_dqn_amd.config import ApexConfig

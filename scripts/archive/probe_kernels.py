@@ -14,7 +14,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 os.environ["APEX_DEBUG_BOUNDS"] = "1"   # the diagnostic library carries the PROBE stamps
 
 PROBE_BLOCKS, PROBE_ITERS = 4, 16

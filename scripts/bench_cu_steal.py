@@ -34,8 +34,13 @@ def main():
     ap.add_argument("--lds", type=int, default=96 * 1024)
     a = ap.parse_args()
     import bench
-    from apex_dqn_amd.ops import _lib
-    lib = _lib.require_kernels()
+    from apex_dqn_amd.ops import _lib, build
+    _lib.require_kernels()
+    # the spin kernel ships in the diagnostic library only (ops/build.py DEBUG_ONLY_SOURCES);
+    # the learner keeps the release kernels
+    lib = ctypes.CDLL(build.ensure_current("kernels_debug"))
+    lib.apex_spin_hold.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.apex_spin_hold.restype = ctypes.c_int
     dev = torch.device("cuda", 0)
     args = bench.parser().parse_args([])
     replay = bench.make_replay(args, dev, 0)

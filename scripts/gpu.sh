@@ -64,7 +64,7 @@ ab)
   for rep in 1 2; do
     for v in "$@"; do
       envs="${v%%::*}"; flags="${v#*::}"; [ "$envs" = "$v" ] && flags=""
-      r=$(env $envs timeout -k 10 300 python bench.py --steps ${AB_STEPS:-600} --warmup ${AB_WARMUP:-50} $flags \
+      r=$(env $envs timeout -k 10 150 python bench.py --steps ${AB_STEPS:-600} --warmup ${AB_WARMUP:-50} $flags \
           2>>gpurun_out/ab_$TAG.err | tail -1) || { echo "FAIL $v" >> $out; cat $out; exit 1; }
       echo "$v => $(echo "$r" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("value_bf16"))')" >> $out
     done

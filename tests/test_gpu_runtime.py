@@ -518,11 +518,11 @@ def test_fc_epilogue_in_head_matches_separate_launch(dtype):
     """The fc forward's split-K epilogue (and the conv2 weight pack) folded into the DDQN
     head launch (ops.fc_fwd(defer_head=True) + head_common.h load_row_part): the stream
     activations h are computed with the same sums, bias, ReLU and rounding as the
-    separate epilogue launch (bit-identical at equal parameters: scripts/diag_fc_head.py);
+    separate epilogue launch (bit-identical at equal parameters: scripts/archive/diag_fc_head.py);
     the head's dot products compile to a different instruction order, so |delta| and the
     update agree to fp32 rounding.  (Later updates are not compared: early centered-RMSprop
     steps scale a gradient difference by up to lr / eps ~ 400, so ulp-level differences
-    compound within a few updates -- scripts/diag_fc_head.py.)"""
+    compound within a few updates -- scripts/archive/diag_fc_head.py.)"""
     from apex_dqn_amd.config import ApexConfig
     from apex_dqn_amd.learner.fused_learner import FusedNatureLearner
     cfg = ApexConfig.from_dict({"env_conf": {"state_shape": [4, 84, 84], "action_dim": 6, "name": "Synthetic"},

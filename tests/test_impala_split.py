@@ -309,7 +309,7 @@ def test_split_impala_step_matches_fp32_torch_step():
     trunk weight gradients differ by up to ~5e-3 because ReLU masks and max-pool winners
     flip where an activation lies within the two forwards' ~1e-6 difference of a tie (a
     handful of units per layer, each moving one O(1) term of a sum over ~1e5;
-    scripts/diag_impala_split.py) -- the bf16-operand HIP step on the same data is the
+    scripts/archive/diag_impala_split.py) -- the bf16-operand HIP step on the same data is the
     contrast (>= 10x worse)."""
     torch.backends.cudnn.allow_tf32 = False
     torch.backends.cuda.matmul.allow_tf32 = False
