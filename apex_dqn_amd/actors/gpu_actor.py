@@ -232,10 +232,14 @@ class GpuActorGroup:
 
     def _policy_kernels(self) -> None:
         ops, P, Pb, Pl, E = self.ops, self.P, self.Pb, self.Pl, self.E
+        c3 = None
         if self.c12_ops is not None:
             c1, c2 = self._c12_weights()
+            if 0 < E <= SW.conv123_max_images:      # conv3 in the same launch, from y2 in LDS
+                c3 = (Pb["w3"], Pl["w3"] if self.split else None, P["b3"], None, None, None)
             self.c12_ops.conv12_fwd(self.replay.frames, self.slots, self.frames_buf, self.cfg.Runtime.obs_scale,
-                                    None, None, self.y2, self.y2_lo, c1, c2, rows_first=E, copy_n=0, pack_sets=0)
+                                    None, None, self.y2, self.y2_lo, c1, c2, rows_first=E, copy_n=0, pack_sets=0,
+                                    c3=c3, y3=self.y3, y3_lo=self.y3_lo if self.split else None)
         elif self.split:   # fp32-class: the learner's split kernels (hi / lo planes throughout)
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames_buf, Pb["w1"], P["b1"],
                                self.cfg.Runtime.obs_scale, self.y1, w32=P["w1"], out_lo=self.y1_lo)
@@ -248,11 +252,14 @@ class GpuActorGroup:
         # beside the learner, where the chip-filling split's partial planes cost HBM traffic)
         ks = dict(ksplit=SW.actor_fc_ksplit) if SW.actor_fc_ksplit > 0 else {}
         if self.split:
-            ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, x_lo=self.y2_lo, w_lo=Pl["w3"], out_lo=self.y3_lo)
+            if c3 is None:
+                ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, x_lo=self.y2_lo, w_lo=Pl["w3"],
+                             out_lo=self.y3_lo)
             ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h, x_lo=self.y3_lo.reshape(E, 3136),
                        w_lo=Pl["wfc"], out_lo=self.h_lo, **ks)
         else:
-            ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3)
+            if c3 is None:
+                ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3)
             ops.fc_fwd(self.y3.reshape(E, 3136), Pb["wfc"], P["bfc"], self.h, **ks)
         heads = {k: P[k] for k in ("wv", "bv", "wa", "ba")}
         ops.actor_head(self.h, heads, self.eps, self.ctr, self.seed, self.q, self.act, H_lo=self.h_lo)

@@ -52,6 +52,8 @@
 #define CF_FRAME 7056        // s2d frame: 441 blocks of 16 B
 #define CF_NY2 12            // y2 store instructions per wave and image (3 mt x 2 jh x 2 planes)
 #define CF_WAHEAD 3          // conv2 weight fragments in flight ahead of their MFMAs (K steps)
+#define CF_W3AHEAD 5         // fused conv3: weight fragments in flight ahead of their MFMAs
+#define CF_W3EARLY 0         // 1: the first ones issued before conv2's epilogue (spills at C = 4)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -86,6 +88,16 @@ struct Conv12Desc {
   int bf16;                // 1: one bf16 plane everywhere (w2_lo, y1_lo, y2_lo unused)
   int probe_split;         // diagnostic build: bit 0 = wait for the first image's frames before
                            // the weight loads (prologue split); 0 otherwise
+  // conv3 fused (w3 non-null): 3x3 / s1, OHWI [64][3][3][64] bf16 hi / lo planes per set,
+  // fp32 biases; y3 [N][7][7][64] hi / lo (ReLU'd) -- conv3 reads y2 from LDS
+  const bf16_t* w3;
+  const bf16_t* w3_lo;
+  const bf16_t* w3b;
+  const bf16_t* w3b_lo;
+  const float* b3;
+  const float* b3b;
+  bf16_t* y3;
+  bf16_t* y3_lo;
 };
 
 template <int C>
@@ -270,6 +282,154 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
           plane ? make_uint2(v.z, v.w) : make_uint2(v.x, v.y);
     }
   };
+  // ---- conv3 (fused, d.w3 != null): after image img's conv2 epilogue, its y2 (this wave's
+  // quads in `pend`) goes into the image's spent staging buffer as hi / lo planes of 96
+  // pixel slots (slot oh * 9 + ow; conv2's class swizzle cf_off), then conv3 runs from
+  // there: wave (nt = wv & 1, kh3 = wv >> 1) takes output channels 32 nt .. + 31 over all
+  // 64 rows r = 32 mt + rr (output pixel (r / 9, r % 9), valid < 7 x 7: the input slot of
+  // tap (kh, kw) is r + 9 kh + kw) and K steps 18 kh3 .. + 17 of 36 (tap s >> 2, 16
+  // channels 16 (s & 3) ..); weights straight from OHWI (L2-resident, CF_WAHEAD steps
+  // ahead).  The two K halves meet in the (free) y1 planes; kh3 = 0 sums them in fixed
+  // order, + bias, ReLU, hi / lo split, stores y3.  Padding slots and invalid rows only
+  // feed output columns that are never stored (MFMA columns are independent).
+  // conv3 weights: lane's row = output channel 32 nt + rr (nt = wv & 1), K chunk kg of each
+  // 16-channel step; step s of this wave's 18 (kh3 = wv >> 1: steps 18 kh3 ..) lives in
+  // slot s % (CF_W3AHEAD + 1) (6 in flight spill at C = 4; issued before conv2 s epilogue, 4 do).
+  bf16x8 wh3[CF_W3AHEAD + 1], wl3[CF_W3AHEAD + 1];
+  auto w3row = [&](const int set3, const bool lo) -> const bf16_t* {
+    const bf16_t* W = lo ? (set3 ? d.w3b_lo : d.w3_lo) : (set3 ? d.w3b : d.w3);
+    return W + (32 * (wv & 1) + rr) * 576 + 8 * kg;
+  };
+  // K step s: tap = s >> 2 (kh = tap / 3, kw = tap % 3), channels 16 (s & 3) + 8 kg ..
+  auto wofs3 = [](int s) { return (s >> 2) * 64 + (s & 3) * 16; };
+  auto conv3_prefetch = [&](const int set3) {
+    const bf16_t* wr = w3row(set3, false);
+    const bf16_t* wrl = SPLIT ? w3row(set3, true) : wr;
+    const int s0 = 18 * (wv >> 1);
+#pragma unroll
+    for (int q = 0; q < CF_W3AHEAD; ++q) {
+      wh3[q] = *reinterpret_cast<const bf16x8*>(wr + wofs3(s0 + q));
+      if (SPLIT) wl3[q] = *reinterpret_cast<const bf16x8*>(wrl + wofs3(s0 + q));
+    }
+  };
+  auto conv3_image = [&](const int img, const int set3, uint8_t* Y2S, const int it) {
+    const int nt = wv & 1, kh3 = wv >> 1;
+    if (it == 0) PROBE(d.probe, 4, PROBE_ITERS - 3, 0);   // (diagnostic build: conv3 phases, image 0)
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) {
+#pragma unroll
+      for (int jh = 0; jh < 2; ++jh) {
+        const int r = mt * 32 + rr, oh = r / 10, ow = r - oh * 10;
+        if (oh < 9 && ow < 9) {
+          const int jq = 2 * kp + jh;
+          const int off = cf_off(oh * 9 + ow, 4 * nh + jq) + 8 * kg;
+          const uint4 v = pend[mt][jh];
+          *reinterpret_cast<uint2*>(Y2S + off) = make_uint2(v.x, v.y);
+          if (SPLIT) *reinterpret_cast<uint2*>(Y2S + 12288 + off) = make_uint2(v.z, v.w);
+        }
+      }
+    }
+    __syncthreads();          // y2 of the image complete in LDS
+    if (it == 0) PROBE(d.probe, 4, PROBE_ITERS - 3, 1);
+    const bf16_t* wr = w3row(set3, false);
+    const bf16_t* wrl = SPLIT ? w3row(set3, true) : wr;
+    f32x16 acc3[2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc3[mt][j] = 0.f;
+    const int s0 = 18 * kh3;
+    if (!CF_W3EARLY) conv3_prefetch(set3);
+    bf16x8 bh3[2][2], bl3[2][2];
+    auto lda3 = [&](int s, int buf) {
+      const int tap = s >> 2, kh = tap / 3, kw = tap - 3 * kh;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int o = cf_off(mt * 32 + rr + 9 * kh + kw, ((s & 3) << 1) | kg);
+        bh3[buf][mt] = *reinterpret_cast<const bf16x8*>(Y2S + o);
+        if (SPLIT) bl3[buf][mt] = *reinterpret_cast<const bf16x8*>(Y2S + 12288 + o);
+      }
+    };
+    lda3(s0, 0);
+#pragma unroll
+    for (int q = 0; q < 18; ++q) {
+      const int s = s0 + q;
+      if (q + CF_W3AHEAD < 18) {
+        wh3[(q + CF_W3AHEAD) % (CF_W3AHEAD + 1)] = *reinterpret_cast<const bf16x8*>(wr + wofs3(s + CF_W3AHEAD));
+        if (SPLIT)
+          wl3[(q + CF_W3AHEAD) % (CF_W3AHEAD + 1)] = *reinterpret_cast<const bf16x8*>(wrl + wofs3(s + CF_W3AHEAD));
+      }
+      if (q + 1 < 18) lda3(s + 1, (q + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x8 ah = wh3[q % (CF_W3AHEAD + 1)], al = wl3[q % (CF_W3AHEAD + 1)];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        if (SPLIT) {
+          acc3[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh3[q & 1][mt], acc3[mt], 0, 0, 0);
+          acc3[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl3[q & 1][mt], acc3[mt], 0, 0, 0);
+        }
+        acc3[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh3[q & 1][mt], acc3[mt], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (it == 0) PROBE(d.probe, 4, PROBE_ITERS - 3, 2);
+    // K halves meet in the y1 planes (conv2 has read them; conv1 of the next image writes
+    // them only after the barrier that closes this image)
+    // each wave hands the other K half the channel quads it does not finish: kh3 = 0
+    // finishes jq 0, 1 and kh3 = 1 jq 2, 3 of its nt; sum = (bias + half 0) + half 1
+    float4* red3 = reinterpret_cast<float4*>(Y1);
+    const int jgive = kh3 ? 0 : 2;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int jq = jgive + jj;
+        red3[((nt * 2 + mt) * 4 + jq) * 64 + lane] =
+            make_float4(acc3[mt][4 * jq], acc3[mt][4 * jq + 1], acc3[mt][4 * jq + 2], acc3[mt][4 * jq + 3]);
+      }
+    __syncthreads();
+    {
+      const float* B3 = set3 ? d.b3b : d.b3;
+      uint8_t* y3h = reinterpret_cast<uint8_t*>(d.y3) + (int64_t)img * 6272;
+      uint8_t* y3l = SPLIT ? reinterpret_cast<uint8_t*>(d.y3_lo) + (int64_t)img * 6272 : y3h;
+      const int jown = kh3 ? 2 : 0;
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int jq = jown + jj;
+        // acc3[mt][4 jq + e] = D[channel 32 nt + 8 jq + 4 kg + e][pixel 32 mt + rr]
+        const int c0 = 32 * nt + 8 * jq + 4 * kg;
+        const float4 bb = *reinterpret_cast<const float4*>(B3 + c0);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const int r = mt * 32 + rr, oh = r / 9, ow = r - oh * 9;
+          const float4 o = red3[((nt * 2 + mt) * 4 + jq) * 64 + lane];
+          const float4 own = make_float4(acc3[mt][4 * jq], acc3[mt][4 * jq + 1], acc3[mt][4 * jq + 2],
+                                         acc3[mt][4 * jq + 3]);
+          const float4 p0 = kh3 ? o : own, p1 = kh3 ? own : o;
+          const float v0 = fmaxf((bb.x + p0.x) + p1.x, 0.f);
+          const float v1 = fmaxf((bb.y + p0.y) + p1.y, 0.f);
+          const float v2 = fmaxf((bb.z + p0.z) + p1.z, 0.f);
+          const float v3 = fmaxf((bb.w + p0.w) + p1.w, 0.f);
+          uint32_t h01, l01 = 0, h23, l23 = 0;
+          if (SPLIT) {
+            split_pk_bf16(v0, v1, h01, l01);
+            split_pk_bf16(v2, v3, h23, l23);
+          } else {
+            h01 = cvt_pk_bf16(v0, v1);
+            h23 = cvt_pk_bf16(v2, v3);
+          }
+          if (oh < 7 && ow < 7) {
+            const uint32_t off = (uint32_t)(((oh * 7 + ow) * 64 + c0) * 2);
+            *reinterpret_cast<uint2*>(y3h + off) = make_uint2(h01, h23);
+            if (SPLIT) *reinterpret_cast<uint2*>(y3l + off) = make_uint2(l01, l23);
+          }
+        }
+      }
+    }
+    __syncthreads();          // staging(i) and the y1 planes are free again
+    if (it == 0) PROBE(d.probe, 4, PROBE_ITERS - 3, 3);
+  };
+
   // image i's frames land in staging(i & 1): image 0's here, image i + 1's during conv1(i)
   PROBE(d.probe, 4, PROBE_ITERS - 2, 0);          // (diagnostic build: prologue split)
   if (cur < d.N) issue_dma(cur, 0);
@@ -482,6 +642,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
 #undef CF_LDA
     }
     PROBE(d.probe, 4, i, 3);
+    if (d.w3 != nullptr && CF_W3EARLY) conv3_prefetch(set);   // (latency hidden behind conv2's epilogue)
     // the two kernel-row pairs meet in LDS (staging(i), read by conv1(i) before the barrier
     // above): wave (nh, kp) finishes output channels 32 nh + 16 kp .. + 15 (jq = 2 kp,
     // 2 kp + 1) and hands the other half of its partial sums to its partner;
@@ -534,6 +695,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
     else finish(2, false);               // (bias + pair 0) + own pair 1
     pend_img = img;
     __syncthreads();          // the partials are read: staging(i) may take image i + 2's frames
+    if (d.w3 != nullptr) conv3_image(img, set, STG + (i & 1) * STGB, i);
     cur = nxt;
     nxt = nn;
   }
@@ -588,6 +750,13 @@ APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if (two && (d.b1b == nullptr || d.w2b == nullptr || (sp && d.w2b_lo == nullptr) || d.b2b == nullptr))
     return (int)hipErrorInvalidValue;
   if (d.copy_n > 0 && (d.y1 == nullptr || (sp && d.y1_lo == nullptr) || d.copy_n > d.N))
+    return (int)hipErrorInvalidValue;
+  if (d.w3 != nullptr &&
+      (d.b3 == nullptr || d.y3 == nullptr || (sp && (d.w3_lo == nullptr || d.y3_lo == nullptr)) ||
+       (two && (d.w3b == nullptr || d.b3b == nullptr || (sp && d.w3b_lo == nullptr))) ||
+       (((uintptr_t)d.w3 | (uintptr_t)(sp ? d.w3_lo : d.w3) | (uintptr_t)(two ? d.w3b : d.w3) |
+         (uintptr_t)(two && sp ? d.w3b_lo : d.w3) | (uintptr_t)d.b3 | (uintptr_t)(two ? d.b3b : d.b3)) & 15) ||
+       (((uintptr_t)d.y3 | (uintptr_t)(sp ? d.y3_lo : d.y3)) & 7)))
     return (int)hipErrorInvalidValue;
   if ((((uintptr_t)d.w1 | (uintptr_t)(two ? d.w1b : d.w1) | (uintptr_t)d.b1 | (uintptr_t)(two ? d.b1b : d.b1) |
         (uintptr_t)d.w2 | (uintptr_t)d.w2_lo | (uintptr_t)d.b2 | (uintptr_t)d.y1 | (uintptr_t)d.y1_lo) & 15) ||

@@ -337,6 +337,11 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         return kw if self.split else {}
 
     # ------------------------------------------------------------ forward
+    @property
+    def _conv123(self) -> bool:
+        """conv3 inside the fused conv1 -> conv2 launch (small launches only, SW.conv123_max_images)."""
+        return bool(self._c12) and 0 < 3 * self.B <= SW.conv123_max_images
+
     def forward_all(self, defer_head: bool = False) -> None:
         """Online net on rows [0,2B), target net on rows [2B,3B): one launch per layer.
         bf16 weights (Pb / Tb, + Pl / Tl lo planes in split mode), fp32 biases (P / T).
@@ -354,17 +359,21 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
             # _target_changed; the step packs the online set only)
             c1, c2 = self._conv12_weights()
             online = 0 if self._frag_out is not None else 1     # (stored by the last optimizer launch)
+            # conv3 in the same launch from y2 in LDS (SW.conv123_fused)
+            c3 = (Pb["w3"], Pl["w3"] if sp else None, P["b3"], Tb["w3"], Tl["w3"] if sp else None, T["b3"]) \
+                if self._conv123 else None
             ops.conv12_fwd(self.replay.frames, self.slots, self.frames, rt.obs_scale, self.y1, self.y1_lo, self.y2,
                            self.y2_lo, c1, c2, rows_first=2 * B, copy_n=B,
-                           pack_sets=online | (0 if self._tgt_packed else 2))
+                           pack_sets=online | (0 if self._tgt_packed else 2), c3=c3, y3=self.y3, y3_lo=self.y3_lo)
         else:
             c2f = (Pb["w2"], None, Tb["w2"], None)
             ops.conv1_fwd_ring(self.replay.frames, self.slots, self.frames, Pb["w1"], P["b1"], rt.obs_scale, self.y1,
                                Tb["w1"], T["b1"], 2 * B, c2f=c2f)
             ops.conv_fwd(self.y1, Pb["w2"], P["b2"], 2, self.y2, Tb["w2"], T["b2"], 2 * B)
         self._issue_params()      # sharded DP update: a deferred fc-row all-gather (learner/dp_step.py)
-        ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
-                     **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
+        if not self._conv123:
+            ops.conv_fwd(self.y2, Pb["w3"], P["b3"], 1, self.y3, Tb["w3"], T["b3"], 2 * B,
+                         **self._lo(x_lo=self.y2_lo, w_lo=sp and Pl["w3"], w2_lo=sp and Tl["w3"], out_lo=self.y3_lo))
         self._wait_params()       # sharded DP update: the last update's fc rows (learner/dp_step.py)
         ops.fc_fwd(self.y3.reshape(n, 3136), Pb["wfc"], P["bfc"], self.h, Tb["wfc"], T["bfc"], 2 * B,
                    c2d=(Pb["w2"], Pl["w2"] if sp else None), defer_head=defer_head,

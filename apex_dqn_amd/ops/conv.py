@@ -280,14 +280,17 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
                      y2: torch.Tensor, y2_lo: torch.Tensor, y1: Optional[torch.Tensor] = None,
                      y1_lo: Optional[torch.Tensor] = None, copy_n: int = 0, w1b=None, b1b=None, w2b=None,
                      w2b_lo=None, b2b=None, rows_first: int = 0, grid: int = 0,
-                     probe: Optional[torch.Tensor] = None, pack_sets: int = 3, probe_split: int = 0) -> None:
+                     probe: Optional[torch.Tensor] = None, pack_sets: int = 3, probe_split: int = 0,
+                     c3=None, y3: Optional[torch.Tensor] = None, y3_lo: Optional[torch.Tensor] = None) -> None:
     """conv1 (fp32 OIHW weights ``w1``, exact uint8 frames from the s2d ring) + ReLU ->
     conv2 (hi / lo bf16 OHWI ``w2``, ``w2_lo``) + ReLU in one persistent launch, y1 kept
     in LDS; rows < ``copy_n`` also store y1 (hi / lo) for the backward.  Rows >=
     ``rows_first`` use the second weight set (``w1b`` ..) when given.  ``pack_sets``: the
     weight sets whose fragments the launch repacks first (the others' must be current,
     see ``conv12_pack``).  ``w2_lo`` None: the bf16 kernel (one plane; ``y1_lo``,
-    ``y2_lo`` unused)."""
+    ``y2_lo`` unused).  ``c3 = (w3, w3_lo, b3, w3 target, w3_lo target, b3 target)``:
+    conv3 (3x3 / s1, OHWI bf16 planes) + ReLU fused too, from y2 in LDS, into ``y3``
+    (``y3_lo``) [N, 7, 7, 64]; y2 is still written for every row."""
     N, C = slots.shape
     sp = w2_lo is not None
     assert slots.dtype == torch.int32 and slots.is_contiguous() and int(w1.shape[1]) == C
@@ -306,6 +309,17 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     d.probe = _lib.ptr(probe)
     d.probe_split = int(probe_split)
     d.wq = ws.wq(("cf_wq", N, int(grid)), ring.device, overlapped=False)
+    if c3 is not None:
+        w3, w3l, b3, w3b, w3bl, b3t = c3
+        assert tuple(w3.shape) == (64, 3, 3, 64) and w3.dtype == torch.bfloat16 and w3.is_contiguous()
+        assert y3 is not None and tuple(y3.shape[:4]) == (N, 7, 7, 64) and y3.is_contiguous()
+        assert not sp or (w3l is not None and y3_lo is not None and tuple(y3_lo.shape[:4]) == (N, 7, 7, 64))
+        two = w1b is not None
+        assert not two or (w3b is not None and b3t is not None and (not sp or w3bl is not None))
+        d.w3, d.w3_lo, d.b3 = w3.data_ptr(), (w3l.data_ptr() if sp else 0), b3.data_ptr()
+        d.w3b, d.w3b_lo, d.b3b = (w3b.data_ptr() if two else 0), (w3bl.data_ptr() if two and sp else 0), \
+            (b3t.data_ptr() if two else 0)
+        d.y3, d.y3_lo = y3.data_ptr(), (y3_lo.data_ptr() if sp else 0)
     _lib.check(lib.apex_conv12_fused_fwd(d, int(grid), _lib.stream_ptr()), "conv12_fused_fwd")
 
 

@@ -79,19 +79,23 @@ class TorchBackend:
         1 target; HIP backend only) -- after the target weights change."""
 
     def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None,
-                   pack_sets=3):
+                   pack_sets=3, c3=None, y3=None, y3_lo=None):
         """conv1 -> conv2 in split mode: ``c1 = (w1 fp32, b1, w1 target, b1 target)``, ``c2 =
         (w2, w2_lo, b2, w2 target, w2_lo target, b2 target)`` (target entries None: one
         set).  y1 rows < ``copy_n`` must hold conv1's output afterwards (the backward's
         input); the HIP backend keeps the other rows in LDS (csrc/conv12_fused.hip) and
         repacks the weight fragments of ``pack_sets`` first (the others come from the last
-        ``conv12_pack``)."""
+        ``conv12_pack``).  ``c3 = (w3, w3_lo, b3, w3 target, w3_lo target, b3 target)``:
+        conv3 too, into ``y3`` / ``y3_lo``."""
         w1, b1, w1b, b1b = c1
         w2, w2l, b2, w2b, w2bl, b2b = c2
         self.conv1_fwd_ring(ring, slots, frames_buf, w1.to(y1.dtype), b1, scale, y1,
                             None if w1b is None else w1b.to(y1.dtype), b1b, rows_first, w32=w1, w2_32=w1b,
                             out_lo=y1_lo)
         self.conv_fwd(y1, w2, b2, 2, y2, w2b, b2b, rows_first, x_lo=y1_lo, w_lo=w2l, w2_lo=w2bl, out_lo=y2_lo)
+        if c3 is not None:
+            w3, w3l, b3, w3b, w3bl, b3b = c3
+            self.conv_fwd(y2, w3, b3, 1, y3, w3b, b3b, rows_first, x_lo=y2_lo, w_lo=w3l, w2_lo=w3bl, out_lo=y3_lo)
 
     def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
                  out_lo=None):
@@ -387,16 +391,16 @@ class HipBackend(TorchBackend):
                       b2b=b2b, sets=sets)
 
     def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None,
-                   pack_sets=3):
+                   pack_sets=3, c3=None, y3=None, y3_lo=None):
         if not self._conv12_native():
             return super().conv12_fwd(ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first,
-                                      copy_n)
+                                      copy_n, c3=c3, y3=y3, y3_lo=y3_lo)
         w1, b1, w1b, b1b = c1
         w2, w2l, b2, w2b, w2bl, b2b = c2
         n = slots.shape[0] if copy_n is None else int(copy_n)
         C.conv12_fused_fwd(self.lib, self.ws, ring, slots, w1, b1, w2, w2l, b2, scale, y2, y2_lo, y1=y1, y1_lo=y1_lo,
                            copy_n=n, w1b=w1b, b1b=b1b, w2b=w2b, w2b_lo=w2bl, b2b=b2b, rows_first=rows_first,
-                           pack_sets=pack_sets)
+                           pack_sets=pack_sets, c3=c3, y3=y3, y3_lo=y3_lo)
 
     def conv_fwd(self, x, w, b, stride, out, w2=None, b2=None, rows_first=0, x_lo=None, w_lo=None, w2_lo=None,
                  out_lo=None):

@@ -29,6 +29,13 @@ class Switches:
     c2f_pack: bool = True
     # conv1 -> conv2 forward fused with y1 in LDS (csrc/conv12_fused.hip), split mode
     conv12_fused: bool = True
+    # conv3 fused into the conv1 -> conv2 kernel (y2 read from LDS; csrc/conv12_fused.hip) for
+    # launches of at most this many images (0: never).  The fused conv3 costs ~6.7 us per
+    # image against ~5 us per image in the separate implicit GEMM, so it wins only where the
+    # separate launch's latency dominates: emulated W = 8 (222 images) 160-168 vs 173-174
+    # us, while at 512 rows (1,536 images) it lost 381.6 vs 371.8 us
+    # (profiles/r6_ab_conv123_fused.txt)
+    conv123_max_images: int = 512
     # the fused forward's one-plane variant for the bf16 learner (4,105 vs 3,790 steps/s,
     # profiles/r3_ab_conv12_bf16_fused_4105_vs_3790.txt)
     conv12_bf16: bool = True

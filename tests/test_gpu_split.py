@@ -642,3 +642,66 @@ def test_optimizer_stores_conv12_fragments_bit_identical_to_pack(monkeypatch, dt
             assert torch.equal(got[1], c2f[:planes * 8192 * 16]), "conv2 C2F fragments differ from the pack launch"
         del L
     assert torch.equal(out[True], out[False])
+
+
+@pytest.mark.parametrize("N,switch,C,grid,split", [(1536, 1024, 4, 0, True), (222, 148, 4, 0, True),
+                                                   (37, 20, 4, 5, True), (50, 50, 1, 0, True),
+                                                   (1536, 1024, 4, 0, False), (37, 20, 2, 5, False)])
+def test_conv123_fused_vs_fp64_and_separate_conv3(N, switch, C, grid, split):
+    """conv3 fused into the conv1 -> conv2 kernel (csrc/conv12_fused.hip conv3_image: y2 from
+    LDS, weights straight from OHWI, two K halves summed in fixed order) against fp64 on
+    the kernel's own y2, and against the separate implicit-GEMM conv3 on that y2 (split:
+    fp32-class tolerance; bf16: one plane).  y2 itself is unchanged by the fusion."""
+    from apex_dqn_amd.ops import conv as C_
+    from apex_dqn_amd.replay.gpu_replay import to_s2d
+
+    def _j3(hi, lo):
+        return hi.double() + (lo.double() if lo is not None else 0.0)
+    g = torch.Generator(device="cpu").manual_seed(N + C + 7)
+    raw = torch.randint(0, 256, (80, 84, 84), generator=g, dtype=torch.uint8)
+    ring = to_s2d(raw.to(DEV))
+    slots = torch.randint(0, 80, (N, C), generator=g, dtype=torch.int32).to(DEV)
+    w1a, w1b = (torch.randn(64, C, 8, 8, generator=g) * 0.05).to(DEV), (torch.randn(64, C, 8, 8, generator=g) * 0.05).to(DEV)
+    b1a, b1b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    w2a, w2b = torch.randn(64, 4, 4, 64, generator=g) * 0.03, torch.randn(64, 4, 4, 64, generator=g) * 0.03
+    b2a, b2b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    w3a, w3b = torch.randn(64, 3, 3, 64, generator=g) * 0.04, torch.randn(64, 3, 3, 64, generator=g) * 0.04
+    b3a, b3b = (torch.randn(64, generator=g) * 0.1).to(DEV), (torch.randn(64, generator=g) * 0.1).to(DEV)
+    if split:
+        (w2ah, w2al), (w2bh, w2bl) = _split(w2a), _split(w2b)
+        (w3ah, w3al), (w3bh, w3bl) = _split(w3a), _split(w3b)
+    else:
+        w2ah, w2bh = w2a.to(DEV).to(torch.bfloat16), w2b.to(DEV).to(torch.bfloat16)
+        w3ah, w3bh = w3a.to(DEV).to(torch.bfloat16), w3b.to(DEV).to(torch.bfloat16)
+        w2al = w2bl = w3al = w3bl = None
+    ws = C_.Workspace()
+    y2h, y2l = _empty2(N, 9, 9, 64)
+    y3h, y3l = _empty2(N, 7, 7, 64)
+    y1h, y1l = _empty2(N, 20, 20, 64)
+    kw2 = dict(w1b=w1b, b1b=b1b, w2b=w2bh, w2b_lo=w2bl, b2b=b2b, rows_first=switch) if switch < N else {}
+    c3 = (w3ah, w3al, b3a, w3bh, w3bl, b3b)
+    C_.conv12_fused_fwd(_lib(), ws, ring, slots, w1a, b1a, w2ah, w2al, b2a, 1 / 255.0, y2h, y2l if split else None,
+                        y1=y1h, y1_lo=y1l if split else None, copy_n=N // 3, grid=grid, c3=c3, y3=y3h,
+                        y3_lo=y3l if split else None, **kw2)
+    # the same launch without conv3: y2 must be bit-identical
+    z2h, z2l = _empty2(N, 9, 9, 64)
+    C_.conv12_fused_fwd(_lib(), ws, ring, slots, w1a, b1a, w2ah, w2al, b2a, 1 / 255.0, z2h, z2l if split else None,
+                        y1=y1h, y1_lo=y1l if split else None, copy_n=N // 3, grid=grid, **kw2)
+    torch.cuda.synchronize()
+    assert torch.equal(y2h, z2h) and (not split or torch.equal(y2l, z2l))
+    x2 = _j3(y2h, y2l if split else None).double().cpu()
+    w3s = (_j3(w3ah, w3al) if split else w3ah.float()).double().cpu()
+    w3t = (_j3(w3bh, w3bl) if split else w3bh.float()).double().cpu()
+    ref3 = torch.cat([R.conv_fwd(x2[:switch], w3s, _c(b3a), 1, torch.float64)] +
+                     ([R.conv_fwd(x2[switch:], w3t, _c(b3b), 1, torch.float64)] if switch < N else []))
+    got = _j3(y3h, y3l if split else None)
+    tol = TOL if split else 1e-2
+    assert _rel(got, ref3) < tol, _rel(got, ref3)
+    # the separate conv3 kernel on the same y2
+    s3h, s3l = _empty2(N, 7, 7, 64)
+    C_.conv_fwd(_lib(), y2h, w3ah, b3a, 1, s3h, w3bh if switch < N else None, b3b if switch < N else None,
+                switch if switch < N else 0, **(dict(x_lo=y2l, w_lo=w3al, w2_lo=w3bl if switch < N else None,
+                                                     out_lo=s3l) if split else {}))
+    torch.cuda.synchronize()
+    sep = _j3(s3h, s3l if split else None)
+    assert _rel(got, sep) < (TOL if split else 1e-2), _rel(got, sep)
