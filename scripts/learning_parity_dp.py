@@ -86,9 +86,19 @@ def run_one(world, steps, seed, variant):
     for p in ps:
         p.start()
     got = {}
-    for _ in range(world):
-        r, res = q.get(timeout=1800)
-        got[r] = res
+    import queue
+    t0 = time.time()
+    while len(got) < world:
+        try:
+            r, res = q.get(timeout=50)
+            got[r] = res
+        except queue.Empty:
+            # (a heartbeat: a GPU command that prints nothing for minutes is taken for hung)
+            print(f"  ... world {world} seed {seed}: {time.time() - t0:.0f} s", flush=True)
+            if time.time() - t0 > 1800:
+                raise SystemExit("timed out")
+            if any(p.exitcode not in (None, 0) for p in ps):
+                raise SystemExit("a rank died")
     for p in ps:
         p.join(timeout=120)
         if p.exitcode != 0:
