@@ -127,7 +127,9 @@ class GpuActorGroup:
 
     def _pack_c12(self) -> None:
         c1, c2 = self._c12_weights()
-        self.c12_ops.conv12_pack(c1, c2, self.cfg.Runtime.obs_scale, sets=1)
+        P, Pb, Pl = self.P, self.Pb, self.Pl
+        c3 = (Pb["w3"], Pl["w3"] if self.split else None, P["b3"], None, None, None)
+        self.c12_ops.conv12_pack(c1, c2, self.cfg.Runtime.obs_scale, sets=1, c3=c3)
 
     # ---------------------------------------------------------------- stream
     def _init_stream(self) -> None:
@@ -217,7 +219,7 @@ class GpuActorGroup:
             if getattr(self, "_graph", None) is None:
                 self._policy_kernels()            # warm: kernel library, workspaces
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=self.stream):
+                with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                     self._policy_kernels()
                 self._graph = g
             self._graph.replay()

@@ -21,6 +21,8 @@
 struct CfPack {
   C2fPack c2f;
   int nc2f;                // C2F blocks (of 256 threads)
+  C3fPack c3f;             // fused conv3's fragments (out null: none)
+  int nc3f;                // C3F blocks, after the C2F ones
   int sets;                // bit 0: online, bit 1: target
   const float* w1[2];      // fp32 OIHW [64][C][8][8]
   const float* b1[2];
@@ -46,6 +48,8 @@ struct CfFragOut {
   int64_t w1_off, w2_off;  // flat offsets of w1 (OIHW [64][C][8][8]) and w2 (OHWI [64][4][4][64])
   int C;
   float in_scale;
+  uint4* c3f;              // fused conv3's C3F fragments (set 0 hi; lo at + C3F_FRAGS), or null
+  int64_t w3_off;          // flat offset of w3 (OHWI [64][3][3][64])
 };
 
 // 4 consecutive updated weights e .. e + 3 (e % 4 == 0): fp32 values px, bf16 hi / lo words
@@ -70,6 +74,16 @@ __device__ __forceinline__ void cf_frag_store(const CfFragOut& fo, int64_t e, co
     *reinterpret_cast<uint2*>(base) = make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
     a = (f16x2v){l0, l1}; b = (f16x2v){l2, l3};
     *reinterpret_cast<uint2*>(base + 64 * 16) = make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+    return;
+  }
+  if (fo.c3f != nullptr && e >= fo.w3_off && e < fo.w3_off + 36864) {
+    // 4 of the 8 K values of fragment (nt, s, lane) (csrc/conv2_wfrag.h c3f_src_off)
+    const int k = (int)(e - fo.w3_off);
+    const int ci = k & 63, tap = (k >> 6) % 9, co = k / 576;
+    const int t = ((co >> 5) * 36 + tap * 4 + (ci >> 4)) * 64 + ((ci >> 3) & 1) * 32 + (co & 31);
+    uint8_t* base = reinterpret_cast<uint8_t*>(fo.c3f + t) + (ci & 4) * 2;
+    *reinterpret_cast<uint2*>(base) = hi;
+    *reinterpret_cast<uint2*>(base + C3F_FRAGS * 16) = lo;
     return;
   }
   if (e >= fo.w2_off && e < fo.w2_off + 65536) {

@@ -98,6 +98,8 @@ struct Conv12Desc {
   const float* b3b;
   bf16_t* y3;
   bf16_t* y3_lo;
+  uint4* w3frag;           // both sets' conv3 weights in C3F fragment order (csrc/conv2_wfrag.h:
+                           // set 0 hi, lo, set 1 hi, lo), packed with the other fragments
 };
 
 template <int C>
@@ -106,7 +108,11 @@ __global__ void __launch_bounds__(256) cf_pack_kernel(CfPack p) {
     c2f_pack_range(p.c2f, blockIdx.x * 256 + threadIdx.x, p.nc2f * 256);
     return;
   }
-  cf_pack_w1_block(p, C, (int)blockIdx.x - p.nc2f, threadIdx.x);
+  if ((int)blockIdx.x < p.nc2f + p.nc3f) {
+    c3f_pack_range(p.c3f, (blockIdx.x - p.nc2f) * 256 + threadIdx.x, p.nc3f * 256);
+    return;
+  }
+  cf_pack_w1_block(p, C, (int)blockIdx.x - p.nc2f - p.nc3f, threadIdx.x);
 }
 
 // class-major y1 pixel slot of input pixel (ih, iw) and the byte offset of its 16-B chunk c
@@ -296,15 +302,15 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
   // 16-channel step; step s of this wave's 18 (kh3 = wv >> 1: steps 18 kh3 ..) lives in
   // slot s % (CF_W3AHEAD + 1) (6 in flight spill at C = 4; issued before conv2 s epilogue, 4 do).
   bf16x8 wh3[CF_W3AHEAD + 1], wl3[CF_W3AHEAD + 1];
-  auto w3row = [&](const int set3, const bool lo) -> const bf16_t* {
-    const bf16_t* W = lo ? (set3 ? d.w3b_lo : d.w3_lo) : (set3 ? d.w3b : d.w3);
-    return W + (32 * (wv & 1) + rr) * 576 + 8 * kg;
+  // (the C3F fragments: one coalesced 1-KB load per wave and K step; the OHWI rows were 32
+  // scattered 32-B pieces per load)
+  auto w3row = [&](const int set3, const bool lo) -> const uint4* {
+    return d.w3frag + (2 * set3 + (lo ? 1 : 0)) * C3F_FRAGS + (wv & 1) * 36 * 64 + lane;
   };
-  // K step s: tap = s >> 2 (kh = tap / 3, kw = tap % 3), channels 16 (s & 3) + 8 kg ..
-  auto wofs3 = [](int s) { return (s >> 2) * 64 + (s & 3) * 16; };
+  auto wofs3 = [](int s) { return s * 64; };
   auto conv3_prefetch = [&](const int set3) {
-    const bf16_t* wr = w3row(set3, false);
-    const bf16_t* wrl = SPLIT ? w3row(set3, true) : wr;
+    const uint4* wr = w3row(set3, false);
+    const uint4* wrl = SPLIT ? w3row(set3, true) : wr;
     const int s0 = 18 * (wv >> 1);
 #pragma unroll
     for (int q = 0; q < CF_W3AHEAD; ++q) {
@@ -331,8 +337,8 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
     }
     __syncthreads();          // y2 of the image complete in LDS
     if (it == 0) PROBE(d.probe, 4, PROBE_ITERS - 3, 1);
-    const bf16_t* wr = w3row(set3, false);
-    const bf16_t* wrl = SPLIT ? w3row(set3, true) : wr;
+    const uint4* wr = w3row(set3, false);
+    const uint4* wrl = SPLIT ? w3row(set3, true) : wr;
     f32x16 acc3[2];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
@@ -340,6 +346,12 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
       for (int j = 0; j < 16; ++j) acc3[mt][j] = 0.f;
     const int s0 = 18 * kh3;
     if (!CF_W3EARLY) conv3_prefetch(set3);
+    // the biases of the two channel quads this wave finishes, loaded ahead of the MFMA loop
+    // (an epilogue load is one exposed L2 round trip)
+    const float* B3 = set3 ? d.b3b : d.b3;
+    float4 bias3[2];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) bias3[jj] = *reinterpret_cast<const float4*>(B3 + 32 * nt + 8 * ((kh3 ? 2 : 0) + jj) + 4 * kg);
     bf16x8 bh3[2][2], bl3[2][2];
     auto lda3 = [&](int s, int buf) {
       const int tap = s >> 2, kh = tap / 3, kw = tap - 3 * kh;
@@ -389,7 +401,6 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
       }
     __syncthreads();
     {
-      const float* B3 = set3 ? d.b3b : d.b3;
       uint8_t* y3h = reinterpret_cast<uint8_t*>(d.y3) + (int64_t)img * 6272;
       uint8_t* y3l = SPLIT ? reinterpret_cast<uint8_t*>(d.y3_lo) + (int64_t)img * 6272 : y3h;
       const int jown = kh3 ? 2 : 0;
@@ -398,7 +409,7 @@ __global__ void __launch_bounds__(CF_THREADS, 1) conv12_fused_kernel(Conv12Desc 
         const int jq = jown + jj;
         // acc3[mt][4 jq + e] = D[channel 32 nt + 8 jq + 4 kg + e][pixel 32 mt + rr]
         const int c0 = 32 * nt + 8 * jq + 4 * kg;
-        const float4 bb = *reinterpret_cast<const float4*>(B3 + c0);
+        const float4 bb = bias3[jj];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const int r = mt * 32 + rr, oh = r / 9, ow = r - oh * 9;
@@ -716,10 +727,15 @@ static int cf_launch_pack(const Conv12Desc& d, hipStream_t st) {
   const int sets = d.pack_sets & ((d.w1b != nullptr) ? 3 : 1);
   if (sets == 0) return 0;
   const bool s0 = sets & 1, s1 = (sets & 2) != 0;
+  const bool c3 = d.w3 != nullptr && d.w3frag != nullptr;
   CfPack pk{C2fPack{{s0 ? d.w2 : nullptr, s0 ? d.w2_lo : nullptr, s1 ? d.w2b : nullptr, s1 ? d.w2b_lo : nullptr},
                     d.wfrag, 0},
-            (s1 ? 4 : 2) * C2F_FRAGS / 256, sets, {d.w1, d.w1b}, {d.b1, d.b1b}, d.in_scale, d.w1frag};
-  const int nb = pk.nc2f + 4 * (s0 + s1);
+            (s1 ? 4 : 2) * C2F_FRAGS / 256,
+            C3fPack{{c3 && s0 ? d.w3 : nullptr, c3 && s0 ? d.w3_lo : nullptr, c3 && s1 ? d.w3b : nullptr,
+                     c3 && s1 ? d.w3b_lo : nullptr}, d.w3frag},
+            c3 ? (s1 ? 4 : 2) * C3F_FRAGS / 256 : 0,
+            sets, {d.w1, d.w1b}, {d.b1, d.b1b}, d.in_scale, d.w1frag};
+  const int nb = pk.nc2f + pk.nc3f + 4 * (s0 + s1);
   switch (d.C) {
     case 1: cf_pack_kernel<1><<<nb, 256, 0, st>>>(pk); break;
     case 2: cf_pack_kernel<2><<<nb, 256, 0, st>>>(pk); break;
@@ -752,7 +768,7 @@ APEX_EXPORT int apex_conv12_fused_fwd(Conv12Desc d, int grid, hipStream_t st) {
   if (d.copy_n > 0 && (d.y1 == nullptr || (sp && d.y1_lo == nullptr) || d.copy_n > d.N))
     return (int)hipErrorInvalidValue;
   if (d.w3 != nullptr &&
-      (d.b3 == nullptr || d.y3 == nullptr || (sp && (d.w3_lo == nullptr || d.y3_lo == nullptr)) ||
+      (d.b3 == nullptr || d.y3 == nullptr || d.w3frag == nullptr || ((uintptr_t)d.w3frag & 15) || (sp && (d.w3_lo == nullptr || d.y3_lo == nullptr)) ||
        (two && (d.w3b == nullptr || d.b3b == nullptr || (sp && d.w3b_lo == nullptr))) ||
        (((uintptr_t)d.w3 | (uintptr_t)(sp ? d.w3_lo : d.w3) | (uintptr_t)(two ? d.w3b : d.w3) |
          (uintptr_t)(two && sp ? d.w3b_lo : d.w3) | (uintptr_t)d.b3 | (uintptr_t)(two ? d.b3b : d.b3)) & 15) ||

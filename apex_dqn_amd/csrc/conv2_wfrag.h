@@ -58,6 +58,28 @@ __device__ __forceinline__ int c2b_src_off(int t) {
   const int co = nh * 32 + rr, kw = s >> 2, ci0 = ((s & 3) << 4) + kg * 8;
   return ((co * 4 + kq) * 4 + kw) * 64 + ci0;
 }
+// Fused conv3 forward weights in fragment order (csrc/conv12_fused.hip conv3_image):
+// fragment t = (nt, K step s < 36, lane) holds the 16 B of w[co = 32 nt + (lane & 31)][tap =
+// s >> 2][ci0 = 16 (s & 3) + 8 (lane >> 5) ..] of OHWI [64][3][3][64]; four planes (set 0 hi,
+// lo, set 1 hi, lo) of C3F_FRAGS uint4 -- one coalesced 1-KB load per wave and K step
+// instead of 32 scattered rows.
+#define C3F_FRAGS 4608
+__device__ __forceinline__ int c3f_src_off(int t) {
+  const int lane = t & 63, s = (t >> 6) % 36, nt = t / 2304;
+  return (32 * nt + (lane & 31)) * 576 + (s >> 2) * 64 + 16 * (s & 3) + 8 * (lane >> 5);
+}
+struct C3fPack {
+  const bf16_t* src[4];   // set 0 hi, lo, set 1 hi, lo (null planes are skipped)
+  uint4* out;             // 4 * C3F_FRAGS, or null: no pack
+};
+__device__ __forceinline__ void c3f_pack_range(const C3fPack& p, int i0, int stride) {
+  for (int i = i0; i < 4 * C3F_FRAGS; i += stride) {
+    const int q = i / C3F_FRAGS;
+    const bf16_t* src = p.src[q];
+    if (src != nullptr) p.out[i] = *reinterpret_cast<const uint4*>(src + c3f_src_off(i - q * C3F_FRAGS));
+  }
+}
+
 struct C2fPack {
   const bf16_t* src[4];   // set 0 hi, lo, set 1 hi, lo (null planes are skipped)
   uint4* out;             // 4 * C2F_FRAGS, or null: no pack

@@ -819,7 +819,9 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
     }
     // blocks in proportion to the segment sizes (at least one each, at most one float4
     // per thread), segment 0 enough for the fragment stores' first-chunk rule below
-    const int64_t need0 = fo.w1frag != nullptr ? (fo.w2_off + 65536) / 4 / nt + 1 : 1;
+    const int64_t fend = fo.c3f != nullptr && fo.w3_off + 36864 > fo.w2_off + 65536 ? fo.w3_off + 36864
+                                                                                     : fo.w2_off + 65536;
+    const int64_t need0 = fo.w1frag != nullptr ? fend / 4 / nt + 1 : 1;
     int b0 = 0;
     for (int k = 0; k < sg.nseg; ++k) {
       const int64_t full = (sg.len[k] / 4 + nt - 1) / nt;
@@ -841,6 +843,9 @@ APEX_EXPORT int apex_rmsprop_sample(float* p, const float* g, float* v, float* m
                                fo.w2_off + 65536 > n0 ||
                                // (stored in each thread's first chunk: rmsprop_body's peel)
                                (fo.w1_off + 4096LL * fo.C) / 4 > (int64_t)nb * nt || (fo.w2_off + 65536) / 4 > (int64_t)nb * nt))
+    return (int)hipErrorInvalidValue;
+  if (fo.w1frag != nullptr && fo.c3f != nullptr &&
+      ((fo.w3_off & 3) || fo.w3_off + 36864 > n0 || (fo.w3_off + 36864) / 4 > (int64_t)nb * nt || ((uintptr_t)fo.c3f & 15)))
     return (int)hipErrorInvalidValue;
   if (((uintptr_t)gpre & 15) || npre < 0 || (npre > 0 && gpre == nullptr)) return (int)hipErrorInvalidValue;
   const RmspropArgs ra{p, g, v, m, pb, n, partials, npart, lr, alpha, eps_opt, clip, centered, norm_out, pb_lo,

@@ -306,16 +306,23 @@ class DataParallelStep:
             if self._comm_bf16:
                 self.gcomm[o2:cut].copy_(self.g32[o2:cut])
             works["cv2"] = coll.all_reduce(self.gcomm[o2:cut])
-            n_pre = 0
-            if shard and SW.dp_norm_split:
-                # the clip-norm partials of the reduced [w2, wfc) bucket, on the branch right
-                # behind its all-reduce; conv1's bucket -- reduced last, on main -- is summed
-                # inside the optimizer launch (norm_prefix): no norm launch on the critical path
-                works["cv2"].wait()
-                n_pre = ops.sqnorm_ranges((self.g32[o2:cut],), self.norm_part, 64)
             if factors and not shard and not self._fc_split:
                 # the global batch's whole fc weight gradient (identical on every rank)
                 nfc = self._fc_wgrad_gathered()
+            n_pre = 0
+            if SW.dp_norm_split and self._presample and not self._comm_bf16:
+                # the clip-norm partials of the reduced buckets on the branch, right behind
+                # their all-reduces (first in norm_part, after the fc partials of the unsharded
+                # factored exchange); conv1's bucket -- reduced last, on main -- is summed inside
+                # the optimizer launch (norm_prefix): no norm launch on the critical path
+                works["cv2"].wait()
+                if shard:
+                    n_pre = ops.sqnorm_ranges((self.g32[o2:cut],), self.norm_part, 64)
+                elif factors:
+                    n_pre = nfc + ops.sqnorm_ranges((self.g32[o2:cut],), self.norm_part[nfc:], 64)
+                else:
+                    works["fc"].wait()
+                    n_pre = ops.sqnorm_ranges((self.g32[o2:cut], self.g32[cut:]), self.norm_part, 64)
         if shard and not fc_on_branch and self._fc_split:
             # this rank's fc rows of the global batch's gradient as split-K partials (the
             # rows fill the chip only when the reduction is split), reduced in conv1's
@@ -372,6 +379,8 @@ class DataParallelStep:
                 self._gather_due = (self._streams.mark(),)
             else:
                 self._gather_params()
+        elif n_pre:
+            self._seg3(norm_slots=n_pre, norm_prefix=self.g32[:o2])
         elif factors:
             nr = ops.sqnorm_ranges((self.g32[:cut],), self.norm_part[nfc:], 64)
             self._seg3(norm_slots=nfc + nr)

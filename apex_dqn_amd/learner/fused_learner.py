@@ -274,7 +274,8 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
             return
         from ..ops import conv as C
         off = self.layout.offsets
-        self._frag_out = C.conv12_frag_out(ops.ws, self.P["w1"], off["w1"], off["w2"], self.rt.obs_scale)
+        self._frag_out = C.conv12_frag_out(ops.ws, self.P["w1"], off["w1"], off["w2"], self.rt.obs_scale,
+                                           w3_off=off["w3"])
         self._online_changed()
 
     def _online_changed(self) -> None:
@@ -282,7 +283,7 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         the fused forward's online operands now (the optimizer keeps them current)."""
         if getattr(self, "_frag_out", None) is not None:
             c1, c2 = self._conv12_weights()
-            self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=1)
+            self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=1, c3=self._conv3_weights())
 
     def _backend_name(self) -> str:
         try:
@@ -360,8 +361,7 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
             c1, c2 = self._conv12_weights()
             online = 0 if self._frag_out is not None else 1     # (stored by the last optimizer launch)
             # conv3 in the same launch from y2 in LDS (SW.conv123_fused)
-            c3 = (Pb["w3"], Pl["w3"] if sp else None, P["b3"], Tb["w3"], Tl["w3"] if sp else None, T["b3"]) \
-                if self._conv123 else None
+            c3 = self._conv3_weights() if self._conv123 else None
             ops.conv12_fwd(self.replay.frames, self.slots, self.frames, rt.obs_scale, self.y1, self.y1_lo, self.y2,
                            self.y2_lo, c1, c2, rows_first=2 * B, copy_n=B,
                            pack_sets=online | (0 if self._tgt_packed else 2), c3=c3, y3=self.y3, y3_lo=self.y3_lo)
@@ -386,12 +386,19 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         return ((P["w1"], P["b1"], T["w1"], T["b1"]),
                 (Pb["w2"], Pl["w2"] if sp else None, P["b2"], Tb["w2"], Tl["w2"] if sp else None, T["b2"]))
 
+    def _conv3_weights(self):
+        """The fused conv3's weights (both sets): packed with the conv1 / conv2 fragments
+        whenever those are (the fused launch may or may not run conv3, SW.conv123_max_images)."""
+        P, T, Pb, Tb, Pl, Tl = self.P, self.T, self.Pb, self.Tb, self.Pl, self.Tl
+        sp = self.split
+        return (Pb["w3"], Pl["w3"] if sp else None, P["b3"], Tb["w3"], Tl["w3"] if sp else None, T["b3"])
+
     def _target_changed(self) -> None:
         """The target weights (t32 / tbf) changed: repack the fused forward's target
         fragments (fused conv1 -> conv2 forward)."""
         if self._c12:
             c1, c2 = self._conv12_weights()
-            self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=2)
+            self.ops.conv12_pack(c1, c2, self.rt.obs_scale, sets=2, c3=self._conv3_weights())
             self._tgt_packed = True
 
     def _head_params(self, V):
@@ -772,10 +779,13 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
 
     def _capture_graphs(self, multi: bool) -> None:
         """Capture the one-update graph (if missing) and, with ``multi``, the
-        ``graph_steps`` graph.  Capture records without executing: state is unchanged."""
+        ``graph_steps`` graph.  Capture records without executing: state is unchanged.
+        Thread-local capture mode: the torch.distributed RCCL watchdog thread queries its
+        events at any time (in global mode one such query inside a capture invalidated it
+        and aborted the process: hipErrorStreamCaptureUnsupported on the watchdog)."""
         if self._graphs is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._body()
                 if self._inject_capture_failure:
                     raise RuntimeError("injected DP graph capture failure (test)")
@@ -786,7 +796,7 @@ class FusedNatureLearner(IsNormMixin, DataParallelStep):
         if multi and k > 1 and self._multi is None:
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.device)
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 try:
                     for i in range(k):
                         # (sharded DP update: the fc-row all-gather of every update but the

@@ -171,7 +171,7 @@ class GraphLearner:
         self._graphs = []
         for seg in segs:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 seg()
             self._graphs.append(g)
             self.graph_captures += 1

@@ -503,7 +503,7 @@ class FusedImpalaLearner(IsNormMixin):
         self._graphs = []
         for seg in segs:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 seg()
             self._graphs.append(g)
             self.graph_captures += 1

@@ -61,7 +61,7 @@ class CfFragOut(ctypes.Structure):
     """The optimizer's stores of the fused forward's online operands (``CfFragOut``,
     csrc/cf_pack.h); all-zero = off."""
     _fields_ = [("w1frag", c_p), ("c2f", c_p), ("w1_off", c_i64), ("w2_off", c_i64), ("C", c_i),
-                ("in_scale", c_f)]
+                ("in_scale", c_f), ("c3f", c_p), ("w3_off", c_i64)]
 
 
 class RmsSegs(ctypes.Structure):

@@ -223,8 +223,11 @@ def conv2_img_fwd(lib, x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, out: t
 CF_W1FRAG_BYTES = 2 * 2 * 2 * 2 * 4 * 2 * 64 * 16
 
 
+C3F_BYTES = 4 * 4608 * 16      # csrc/conv2_wfrag.h C3F_FRAGS x 4 planes
+
+
 def _conv12_desc(ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1, b1, w2, w2_lo, b2, scale, w1b, b1b,
-                 w2b, w2b_lo, b2b):
+                 w2b, w2b_lo, b2b, c3=None):
     from .conv_sigs import Conv12Desc
     C = int(w1.shape[1])
     assert tuple(w1.shape) == (64, C, 8, 8) and w1.dtype == torch.float32 and w1.is_contiguous()
@@ -248,21 +251,34 @@ def _conv12_desc(ws: "Workspace", ring: torch.Tensor, slots: torch.Tensor, w1, b
     # captured graph, must be the buffer the graph's launches read)
     d.wfrag = ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, dev, torch.uint8).data_ptr()
     d.C, d.in_scale = C, float(scale)
+    if c3 is not None:
+        # fused conv3: both sets' weights (packed into C3F fragments with the others)
+        w3, w3l, b3, w3b, w3bl, b3t = c3
+        sp = w2_lo is not None
+        two = w1b is not None
+        assert tuple(w3.shape) == (64, 3, 3, 64) and w3.dtype == torch.bfloat16 and w3.is_contiguous()
+        assert not sp or w3l is not None
+        assert not two or (w3b is not None and b3t is not None and (not sp or w3bl is not None))
+        d.w3, d.w3_lo, d.b3 = w3.data_ptr(), (w3l.data_ptr() if sp else 0), b3.data_ptr()
+        d.w3b, d.w3b_lo, d.b3b = (w3b.data_ptr() if two else 0), (w3bl.data_ptr() if two and sp else 0), \
+            (b3t.data_ptr() if two else 0)
+        d.w3frag = ws.get(("cf_c3f",), C3F_BYTES, dev, torch.uint8).data_ptr()
     return d
 
 
 def conv12_pack(lib, ws: "Workspace", w1, b1, w2, w2_lo, b2, scale: float, w1b=None, b1b=None, w2b=None,
-                w2b_lo=None, b2b=None, sets: int = 2) -> None:
+                w2b_lo=None, b2b=None, sets: int = 2, c3=None) -> None:
     """(Re)pack the fused kernel's weight fragments of ``sets`` (bit 0 online, bit 1 target)
     alone -- the learner's target sync; the step's fused launch then packs the online set
     only (``conv12_fused_fwd(pack_sets=1)``).  The input scale is folded into the conv1
     fragments: pack with the scale the forward uses."""
-    d = _conv12_desc(ws, None, None, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b)
+    d = _conv12_desc(ws, None, None, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b, c3)
     d.pack_sets = int(sets)
     _lib.check(lib.apex_conv12_pack(d, _lib.stream_ptr()), "conv12_pack")
 
 
-def conv12_frag_out(ws: "Workspace", w1: torch.Tensor, w1_off: int, w2_off: int, scale: float):
+def conv12_frag_out(ws: "Workspace", w1: torch.Tensor, w1_off: int, w2_off: int, scale: float,
+                    w3_off: Optional[int] = None):
     """``CfFragOut`` for the optimizer launch: the fused forward's online conv1 / conv2
     operand buffers of ``ws`` and the flat offsets of w1 / w2 in the parameter vector the
     optimizer updates (csrc/cf_pack.h cf_frag_store)."""
@@ -272,6 +288,9 @@ def conv12_frag_out(ws: "Workspace", w1: torch.Tensor, w1_off: int, w2_off: int,
     fo.w1frag = ws.get(("cf_w1frag",), CF_W1FRAG_BYTES, dev, torch.uint8).data_ptr()
     fo.c2f = ws.get(("cf_c2f_wfrag",), 4 * 8192 * 16, dev, torch.uint8).data_ptr()
     fo.w1_off, fo.w2_off, fo.C, fo.in_scale = int(w1_off), int(w2_off), C, float(scale)
+    if w3_off is not None:      # the fused conv3's C3F fragments (csrc/cf_pack.h)
+        fo.c3f = ws.get(("cf_c3f",), C3F_BYTES, dev, torch.uint8).data_ptr()
+        fo.w3_off = int(w3_off)
     return fo
 
 
@@ -296,7 +315,7 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     assert slots.dtype == torch.int32 and slots.is_contiguous() and int(w1.shape[1]) == C
     assert tuple(y2.shape[:4]) == (N, 9, 9, 64) and y2.is_contiguous() and y2.dtype == torch.bfloat16
     assert not sp or (y2_lo is not None and tuple(y2_lo.shape) == (N, 9, 9, 64))
-    d = _conv12_desc(ws, ring, slots, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b)
+    d = _conv12_desc(ws, ring, slots, w1, b1, w2, w2_lo, b2, scale, w1b, b1b, w2b, w2b_lo, b2b, c3)
     d.img_switch = int(rows_first) if w1b is not None else N
     if copy_n > 0:
         assert y1 is not None and (y1_lo is not None or not sp) and y1.shape[0] >= copy_n and \
@@ -310,15 +329,8 @@ def conv12_fused_fwd(lib, ws: "Workspace", ring: torch.Tensor, slots: torch.Tens
     d.probe_split = int(probe_split)
     d.wq = ws.wq(("cf_wq", N, int(grid)), ring.device, overlapped=False)
     if c3 is not None:
-        w3, w3l, b3, w3b, w3bl, b3t = c3
-        assert tuple(w3.shape) == (64, 3, 3, 64) and w3.dtype == torch.bfloat16 and w3.is_contiguous()
         assert y3 is not None and tuple(y3.shape[:4]) == (N, 7, 7, 64) and y3.is_contiguous()
-        assert not sp or (w3l is not None and y3_lo is not None and tuple(y3_lo.shape[:4]) == (N, 7, 7, 64))
-        two = w1b is not None
-        assert not two or (w3b is not None and b3t is not None and (not sp or w3bl is not None))
-        d.w3, d.w3_lo, d.b3 = w3.data_ptr(), (w3l.data_ptr() if sp else 0), b3.data_ptr()
-        d.w3b, d.w3b_lo, d.b3b = (w3b.data_ptr() if two else 0), (w3bl.data_ptr() if two and sp else 0), \
-            (b3t.data_ptr() if two else 0)
+        assert not sp or (y3_lo is not None and tuple(y3_lo.shape[:4]) == (N, 7, 7, 64))
         d.y3, d.y3_lo = y3.data_ptr(), (y3_lo.data_ptr() if sp else 0)
     _lib.check(lib.apex_conv12_fused_fwd(d, int(grid), _lib.stream_ptr()), "conv12_fused_fwd")
 

@@ -24,7 +24,7 @@ class Conv12Desc(ctypes.Structure):
                 ("w1frag", c_p), ("scratch", c_p), ("N", c_i), ("C", c_i), ("img_switch", c_i), ("copy_n", c_i),
                 ("in_scale", ctypes.c_float), ("probe", c_p), ("wq", c_p), ("bf16", c_i), ("probe_split", c_i),
                 ("w3", c_p), ("w3_lo", c_p), ("w3b", c_p), ("w3b_lo", c_p), ("b3", c_p), ("b3b", c_p),
-                ("y3", c_p), ("y3_lo", c_p)]
+                ("y3", c_p), ("y3_lo", c_p), ("w3frag", c_p)]
 
 
 class Conv2DgradImgDesc(ctypes.Structure):

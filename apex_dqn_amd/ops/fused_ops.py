@@ -74,9 +74,10 @@ class TorchBackend:
             self.conv1_fwd(frames[:r], wa, b, scale, out[:r], None if out_lo is None else out_lo[:r])
             self.conv1_fwd(frames[r:], wb, b2, scale, out[r:], None if out_lo is None else out_lo[r:])
 
-    def conv12_pack(self, c1, c2, scale, sets=2):
+    def conv12_pack(self, c1, c2, scale, sets=2, c3=None):
         """Repack the fused conv12 kernel's weight fragments of ``sets`` (bit 0 online, bit
-        1 target; HIP backend only) -- after the target weights change."""
+        1 target; HIP backend only) -- after the target weights change; ``c3``: the fused
+        conv3's too."""
 
     def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None,
                    pack_sets=3, c3=None, y3=None, y3_lo=None):
@@ -382,13 +383,13 @@ class HipBackend(TorchBackend):
     def _conv12_native(self) -> bool:
         return self.native_conv and SW.conv12_fused and hasattr(self.lib, "apex_conv12_fused_fwd")
 
-    def conv12_pack(self, c1, c2, scale, sets=2):
+    def conv12_pack(self, c1, c2, scale, sets=2, c3=None):
         if not self._conv12_native():
             return
         w1, b1, w1b, b1b = c1
         w2, w2l, b2, w2b, w2bl, b2b = c2
         C.conv12_pack(self.lib, self.ws, w1, b1, w2, w2l, b2, scale, w1b=w1b, b1b=b1b, w2b=w2b, w2b_lo=w2bl,
-                      b2b=b2b, sets=sets)
+                      b2b=b2b, sets=sets, c3=c3)
 
     def conv12_fwd(self, ring, slots, frames_buf, scale, y1, y1_lo, y2, y2_lo, c1, c2, rows_first=0, copy_n=None,
                    pack_sets=3, c3=None, y3=None, y3_lo=None):

@@ -30,12 +30,13 @@ class Switches:
     # conv1 -> conv2 forward fused with y1 in LDS (csrc/conv12_fused.hip), split mode
     conv12_fused: bool = True
     # conv3 fused into the conv1 -> conv2 kernel (y2 read from LDS; csrc/conv12_fused.hip) for
-    # launches of at most this many images (0: never).  The fused conv3 costs ~6.7 us per
-    # image against ~5 us per image in the separate implicit GEMM, so it wins only where the
-    # separate launch's latency dominates: emulated W = 8 (222 images) 160-168 vs 173-174
-    # us, while at 512 rows (1,536 images) it lost 381.6 vs 371.8 us
-    # (profiles/r6_ab_conv123_fused.txt)
-    conv123_max_images: int = 512
+    # launches of at most this many images (0: never).  With its weights in coalesced C3F
+    # fragments (written by the optimizer) and its biases loaded ahead, the fused conv3 takes
+    # ~3.7 k cycles per image and wins at every size: 512 rows 2,733-2,740 vs 2,678-2,692
+    # fp32 updates/s (bf16 4,523-4,529 vs 4,433-4,451), emulated W = 8 157.1-157.3 vs
+    # 163.1-169.7 us, W = 4 192.7-193.5 vs 198.1-202.9 us (profiles/r6_ab_conv123_fused_c3f.txt;
+    # with the weights read from OHWI rows it lost at 512 rows, r6_ab_conv123_fused.txt)
+    conv123_max_images: int = 1 << 20
     # the fused forward's one-plane variant for the bf16 learner (4,105 vs 3,790 steps/s,
     # profiles/r3_ab_conv12_bf16_fused_4105_vs_3790.txt)
     conv12_bf16: bool = True
