@@ -316,13 +316,15 @@ class DataParallelStep:
                 # factored exchange); conv1's bucket -- reduced last, on main -- is summed inside
                 # the optimizer launch (norm_prefix): no norm launch on the critical path
                 works["cv2"].wait()
+                # (not with the all-reduce exchange: the 3.2 M-float fc bucket's norm on the
+                # branch -- the chain that also carries that bucket -- lengthened the forced-DP
+                # step at world 1 by 73 us at 64 blocks and still cost 0.7 % at 1,024:
+                # 2,636 vs 2,656 updates/s, profiles/r6_ab_forced_dp_norm_split.txt; the
+                # optimizer's own norm pass stays there)
                 if shard:
                     n_pre = ops.sqnorm_ranges((self.g32[o2:cut],), self.norm_part, 64)
                 elif factors:
                     n_pre = nfc + ops.sqnorm_ranges((self.g32[o2:cut],), self.norm_part[nfc:], 64)
-                else:
-                    works["fc"].wait()
-                    n_pre = ops.sqnorm_ranges((self.g32[o2:cut], self.g32[cut:]), self.norm_part, 64)
         if shard and not fc_on_branch and self._fc_split:
             # this rank's fc rows of the global batch's gradient as split-K partials (the
             # rows fill the chip only when the reduction is split), reduced in conv1's

@@ -87,8 +87,11 @@ class Switches:
     # (False: emulated W = 8 160.5-162.1 vs 178.6-180.7 us, W = 4 201.5-202.0 vs
     # 199.7-203.6 -- the branch becomes the critical chain; profiles/r6_ab_dp_switches.txt)
     dp_fc_shard_branch: bool = False
-    # DP step: one main-stream event for the branch's conv3 + conv2 weight gradients
-    dp_branch_one_wait: bool = False
+    # DP step: one main-stream event for the branch's conv3 + conv2 weight gradients (one
+    # cross-queue edge fewer on the critical path; with the fused conv3: emulated W = 4
+    # 195.0 / 195.1 vs 197.2 / 197.6 us, W = 8 164.1 / 163.2 vs 170.0 / 166.2,
+    # profiles/r6_ab_misc.txt)
+    dp_branch_one_wait: bool = True
     # DP step, sharded update with the factored exchange: this rank's fc weight-gradient rows
     # as split-K partials of this many reduction rows each, reduced in conv1's finalize
     # launch (0: one launch over all rows writing the gradient itself)
