@@ -390,7 +390,8 @@ def run(args) -> None:
             diag["graph_matches_eager"] = learner.graph_matches_eager() \
                 if hasattr(learner, "graph_matches_eager") else None
     if hasattr(learner, "p32") and not emu:
-        learner.materialize()      # (sharded update: every rank's fc rows; a collective)
+        if hasattr(learner, "materialize"):
+            learner.materialize()      # (sharded update: every rank's fc rows; a collective)
         import hashlib
         diag["param_sha256"] = hashlib.sha256(learner.p32.detach().cpu().numpy().tobytes()).hexdigest()[:16]
     other = None
