@@ -310,7 +310,7 @@ class DataParallelStep:
                 # the global batch's whole fc weight gradient (identical on every rank)
                 nfc = self._fc_wgrad_gathered()
             n_pre = 0
-            if SW.dp_norm_split and self._presample and not self._comm_bf16:
+            if SW.dp_norm_split and self._presample and not self._comm_bf16 and (shard or factors):
                 # the clip-norm partials of the reduced buckets on the branch, right behind
                 # their all-reduces (first in norm_part, after the fc partials of the unsharded
                 # factored exchange); conv1's bucket -- reduced last, on main -- is summed inside
@@ -319,8 +319,8 @@ class DataParallelStep:
                 # (not with the all-reduce exchange: the 3.2 M-float fc bucket's norm on the
                 # branch -- the chain that also carries that bucket -- lengthened the forced-DP
                 # step at world 1 by 73 us at 64 blocks and still cost 0.7 % at 1,024:
-                # 2,636 vs 2,656 updates/s, profiles/r6_ab_forced_dp_norm_split.txt; the
-                # optimizer's own norm pass stays there)
+                # 2,636 vs 2,656 updates/s, profiles/r6_ab_forced_dp_norm_split.txt, the 0.7 %
+                # being this block's branch wait alone; the optimizer's own norm pass stays there)
                 if shard:
                     n_pre = ops.sqnorm_ranges((self.g32[o2:cut],), self.norm_part, 64)
                 elif factors:
