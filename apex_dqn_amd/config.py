@@ -104,9 +104,11 @@ class RuntimeConf:
     allreduce_dtype: str = "fp32"   # DP gradient all-reduce payload: "fp32" (exact) | "bf16" (half the bytes)
     presample: bool = True          # draw step t+1's batch at the end of step t (fused learner; on the HIP
                                     # backend inside the optimizer launch)
-    graph_steps: int = 10           # learner updates per HIP-graph launch in learner.steps(n) (single
+    graph_steps: int = 20           # learner updates per HIP-graph launch in learner.steps(n) (single
                                     # rank and DP alike: the DP step's collectives are captured too;
-                                    # 10 divides the default eviction cadence: 3505 vs 3472 steps/s at 4)
+                                    # divides the default eviction cadence; 20 vs 10: 2,732 / 2,726 vs
+                                    # 2,703 / 2,684 steps/s at 20 / 5, 2,729 / 2,744 vs 2,718 / 2,717 at
+                                    # 200 / 20, profiles/r6_ab_graph_steps.txt; 10 vs 4: 3505 vs 3472)
     actor_learner_ratio: float = 0.0  # in-process actor steps per learner step (0 = separate)
     replay_capacity: Optional[int] = None  # physical capacity, global over the ranks' shards
                                            # (default: soft_capacity * 1.25 + 1024)

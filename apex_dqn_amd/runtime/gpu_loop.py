@@ -32,6 +32,14 @@ FILL_CHECK_EVERY = 16      # fill phase: group steps between readiness all-reduc
 WATCHDOG_EXIT_CODE = 75    # a multi-rank watchdog timeout exits the process with this code
 
 
+def _chunk_cap(graph_steps: int) -> int:
+    """Learner updates per loop chunk with an actor thread: whole multi-update graphs,
+    about 20 updates (two chunks in flight bound how long an actor insert waits behind
+    the learner)."""
+    g = max(1, graph_steps)
+    return g * max(1, 20 // g)
+
+
 def build_replay(cfg: ApexConfig, device, num_envs: int, seed: int = 0, world: int = 1) -> GpuReplayShard:
     """This rank's shard of the global replay: ``soft_capacity / world`` transitions
     (the learners turn the shards into one prioritized replay, replay/gpu_replay.py)."""
@@ -197,7 +205,7 @@ def _train_frames(cfg: ApexConfig, device, learner_steps: int, comm=None,
                         _to_boundary(n, rt.ckpt_freq) if (ckpt_path and rt.ckpt_freq) else learner_steps,
                         _to_boundary(n, rt.replica_check_every) if (world > 1 and rt.replica_check_every)
                         else learner_steps,
-                        max(1, 2 * int(getattr(rt, "graph_steps", 1) or 1)))
+                        _chunk_cap(int(getattr(rt, "graph_steps", 1) or 1)))
                 if rt.torch_profile_dir and prof is None and n < rt.torch_profile_start:
                     k = min(k, rt.torch_profile_start - n)
             else:

@@ -154,8 +154,9 @@ def capture_probe(args, world: int, rank: int, local_rank: int):
         return None
     if not (world > 1 or (args.force_dp and mode == "on")):
         return None
+    from apex_dqn_amd.config import RuntimeConf
     from apex_dqn_amd.runtime.capture_probe import run_probe
-    variants = [{"name": n, "cfg": learner_config(args, dt, rank, sc), "steps": args.graph_steps or 10}
+    variants = [{"name": n, "cfg": learner_config(args, dt, rank, sc), "steps": args.graph_steps or RuntimeConf.graph_steps}
                 for (n, dt, sc) in measurements(args, world)]
     log = open(os.path.join(args.capture_probe_log, f"capture_probe_rank{rank}.log"), "wb") \
         if args.capture_probe_log else None

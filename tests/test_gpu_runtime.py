@@ -346,8 +346,8 @@ def _bench_json(stdout: str) -> dict:
 def test_bench_contract_one_gpu():
     """bench.py prints exactly one JSON line with the driver's keys; the headline is
     the fp32 (reference-precision) learner, bf16 rides along as value_bf16, and no
-    HIP graph is captured inside either timed window (warmup 5 < graph_steps 10:
-    the 10-update graph is captured by prepare_graphs, before the clock starts)."""
+    HIP graph is captured inside either timed window (warmup 5 < graph_steps 20:
+    the 20-update graph is captured by prepare_graphs, before the clock starts)."""
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "30", "--warmup", "5",
                         "--replay", "20000"], capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
