@@ -160,6 +160,7 @@ class FusedImpalaLearner(IsNormMixin):
         self._alloc(self.B)
         self.sync_target()
         self._graphs = None
+        self._multi = None      # one rank: Runtime.graph_steps updates in one graph (steps())
         self.graph_captures = 0
         # one stream by default (see fused_learner: cross-stream edges in the HIP graph
         # cost more than the overlap); the head kernel writes the priorities back and
@@ -487,6 +488,31 @@ class FusedImpalaLearner(IsNormMixin):
         if self.num_q_updates % self.cfg.Learner.q_target_sync_freq == 0:
             self.sync_target()
 
+    def steps(self, n: int) -> None:
+        """``n`` updates.  On one rank with HIP graphs, chunks of ``Runtime.graph_steps``
+        updates replay one graph holding that many steps (no launch boundary between
+        them), never straddling a target sync -- learner/fused_learner.py ``steps``."""
+        k = int(self.rt.graph_steps)
+        if k <= 1 or self.world > 1 or not (self.rt.use_graphs and self.device.type == "cuda"):
+            for _ in range(n):
+                self.step()
+            return
+        f = self.cfg.Learner.q_target_sync_freq
+        while n > 0:
+            if n < k or f - self.num_q_updates % f < k:
+                self.step()
+                n -= 1
+                continue
+            if self._multi is None:
+                self.prepare_graphs(multi=True)
+            if self._presample and self._sample_ver != self.replay.version:
+                self._sample()
+            self._multi.replay()
+            self.num_q_updates += k
+            n -= k
+            if self.num_q_updates % f == 0:
+                self.sync_target()
+
     def _capture(self) -> None:
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -509,10 +535,43 @@ class FusedImpalaLearner(IsNormMixin):
             self.graph_captures += 1
 
     def prepare_graphs(self, multi: bool = True) -> int:
-        """Capture the step's graphs now (outside any timed region)."""
-        if self.rt.use_graphs and self.device.type == "cuda" and self._graphs is None:
+        """Capture the step's graphs now (outside any timed region); with ``multi`` on one
+        rank also the ``graph_steps``-update graph, replayed once from a snapshot so its
+        first timed launch is warm (the first launch of a fresh graph uploads it)."""
+        if not (self.rt.use_graphs and self.device.type == "cuda"):
+            return self.graph_captures
+        if self._graphs is None:
             self._capture()
+        k = int(self.rt.graph_steps)
+        if multi and self.world == 1 and k > 1 and self._multi is None:
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                for _ in range(k):
+                    self._step_body()
+            self._multi = g
+            self.graph_captures += 1
+            self.rewarm(1)
         return self.graph_captures
+
+    def rewarm(self, replays: int) -> None:
+        """Untimed, state-preserving warm-up: replay the multi-update graph ``replays``
+        times from a snapshot, then restore the learner / replay state (bench.py, before
+        its timed window; no update is kept)."""
+        gr = self._multi if self._multi is not None else (self._graphs[0] if self._graphs and self.world == 1
+                                                          else None)
+        if replays <= 0 or gr is None:
+            return
+        snap = self._snapshot()
+        if self._presample and self._sample_ver != self.replay.version:
+            self._sample()
+        for _ in range(replays):
+            gr.replay()
+        torch.cuda.synchronize(self.device)
+        self._restore(snap)
+        if self._presample:
+            self._sample()     # the pre-drawn batch of the restored state (same draw)
+        torch.cuda.synchronize(self.device)
 
     def _snapshot(self):
         rp = self.replay
@@ -612,7 +671,7 @@ class FusedImpalaLearner(IsNormMixin):
         if ck is None:
             return False
         if adopt_obs_scale(ck, self.rt):
-            self._graphs = None                   # the input scale is a kernel argument: recapture
+            self._graphs = self._multi = None     # the input scale is a kernel argument: recapture
         self.load_module_state(ck["Q_state"])
         self._refresh_bf16()
         if "Q_target_state" in ck:

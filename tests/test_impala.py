@@ -379,3 +379,30 @@ def test_gpu_impala_graph_step_runs(dtype):
     torch.cuda.synchronize()
     m = L.last_metrics()
     assert np.isfinite(m["loss"]) and np.isfinite(m["grad_norm"])
+
+
+@pytest.mark.gpu
+def test_gpu_impala_multi_step_graph_matches_single_step_graphs():
+    """steps(n) replaying 4-update graphs (with a target sync inside the run and a
+    host-side replay mutation between calls) == n one-update graph replays (fp32)."""
+    dev = torch.device("cuda")
+    res = {}
+    for k in (1, 4):
+        cfg, rp = _setup(B=64, device=dev, dtype="fp32")
+        cfg.Runtime.use_graphs = True
+        cfg.Runtime.graph_steps = k
+        cfg.Learner.q_target_sync_freq = 6
+        L = FusedImpalaLearner(cfg, dev, rp, backend="hip")
+        L.prepare_graphs()
+        assert (L._multi is not None) == (k > 1)
+        L.steps(9)
+        rp.remove_to_fit()
+        rp.rebuild()
+        L.steps(8)
+        torch.cuda.synchronize()
+        assert L.num_q_updates == 17
+        res[k] = (L.p32.clone(), L.t32.clone(), rp.leaf.clone(), L.S["idx"].clone())
+    # same draws; parameters equal up to the order of the fp32 head-wgrad atomics
+    assert torch.equal(res[1][3], res[4][3])
+    for a, b in zip(res[1][:3], res[4][:3]):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
