@@ -758,7 +758,7 @@ __global__ void __launch_bounds__(256) sconv_wgrad_reduce_kernel(WgRedDesc d) {
   const int64_t stride = (int64_t)TT * 64;
   f32x4 v = (f32x4){0.f, 0.f, 0.f, 0.f};
   if (col < TT * 64) {
-#pragma unroll 4
+#pragma unroll 8
     for (int k = grp; k < J.nsplit; k += 16) v += src[(int64_t)k * stride + col];
   }
   red[grp][lc] = v;
