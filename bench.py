@@ -253,7 +253,23 @@ def main():
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["APEX_TRACEBACK_AFTER"]), repeat=True)
     args = parser().parse_args()
+    global _RESULT_OUT
+    _RESULT_OUT = _claim_stdout()
     run(args)
+
+
+_RESULT_OUT = sys.stdout
+
+
+def _claim_stdout():
+    """The driver reads ONE JSON line from stdout, but libraries print there too (RCCL
+    writes its version banner to stdout when a communicator initialises): point fd 1 at
+    stderr for the whole run (child processes inherit that) and keep a private handle on
+    the real stdout for the result line."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
 
 
 def parser() -> argparse.ArgumentParser:
@@ -485,7 +501,7 @@ def run(args) -> None:
             out["value_bf16"] = round(value_of(extra, scope), 2)
             out["ms_per_step_bf16"] = round(1e3 * extra["dt"] / args.steps, 4)
             out["graph_captures_in_timed_bf16"] = extra["graph_captures_in_timed"]
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=_RESULT_OUT, flush=True)
     with wd.phase("shutdown", to):
         comm.shutdown()
     wd.close()
