@@ -533,11 +533,16 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     ``target_rows``: reduction rows per split-K block (0 = tuned default: fewer
     rows for the small 3x3 layer, whose 9 output tiles need more splits (384: two
     68 KB blocks per CU); 704 for conv2 keeps its 4 x 59 blocks (84 KB LDS each,
-    one per CU) in a single wave on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  SW.wg_rows3 / SW.wg_rows2
-    override for sweeps."""
+    one per CU) in a single wave on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  Below 256
+    images (the per-rank rows of a global batch over 4+ ranks) half those rows, so the few
+    images still make enough blocks: emulated W = 8 rank step 167.8 / 168.4 / 168.3 ->
+    159.9 / 161.5 / 159.6 us, W = 4 ~1 % (profiles/r6_ab_wgrad_rows_small_batch.txt).
+    SW.wg_rows3 / SW.wg_rows2 override for sweeps."""
     N, OH, OW, Co = dy.shape
     if target_rows <= 0:
-        target_rows = {3: SW.wg_rows3, 4: SW.wg_rows2}.get(KH) or (384 if KH == 3 else 704)
+        small = N < 256
+        target_rows = {3: SW.wg_rows3, 4: SW.wg_rows2}.get(KH) or \
+            ((192 if small else 384) if KH == 3 else (352 if small else 704))
     _, H, W, Cin = x.shape
     Kc = KH * KH * Cin
     Mred = N * OH * OW
