@@ -536,7 +536,8 @@ def conv_wgrad(lib, ws: Workspace, dy: torch.Tensor, x: torch.Tensor, KH: int, s
     one per CU) in a single wave on 256 CUs: 3507-3572 -> 3562-3611 steps/s).  Below 256
     images (the per-rank rows of a global batch over 4+ ranks) half those rows, so the few
     images still make enough blocks: emulated W = 8 rank step 167.8 / 168.4 / 168.3 ->
-    159.9 / 161.5 / 159.6 us, W = 4 ~1 % (profiles/r6_ab_wgrad_rows_small_batch.txt).
+    159.9 / 161.5 / 159.6 us, W = 4 ~1 %; at 290 images (W = 2) halving loses 2.5 %
+    (profiles/r6_ab_wgrad_rows_small_batch.txt).
     SW.wg_rows3 / SW.wg_rows2 override for sweeps."""
     N, OH, OW, Co = dy.shape
     if target_rows <= 0:
