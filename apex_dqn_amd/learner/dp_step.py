@@ -103,6 +103,7 @@ class DataParallelStep:
     ``self.coll`` (parallel/rccl.py), ``self.layout`` and ``self.ops``."""
 
     _fc_split = False       # sharded update: the fc rows' gradient as split-K partials (_dp_setup)
+    _fc_split_rows = 128    # their reduction rows per split (SW.dp_fc_split_rows, _dp_setup)
     _fc_cpb = -1
 
     # ------------------------------------------------------------------ setup
@@ -122,7 +123,8 @@ class DataParallelStep:
         # the fc weight gradient from the gathered factor rows as split-K partials reduced in
         # a grad_finalize launch (one norm partial per finalize block), sharded or not -- the
         # two stay bit-identical
-        self._fc_split = self._dp and self._fc_factors and SW.dp_fc_split_rows > 0
+        self._fc_split_rows = int(SW.dp_fc_split_rows) if SW.dp_fc_split_rows >= 0 else (256 if W >= 8 else 128)
+        self._fc_split = self._dp and self._fc_factors and self._fc_split_rows > 0
         S = FC_ROWS // W if self._shard else FC_ROWS
         self._fc_cpb = -max(1, S // 128)       # direct finalize: ~393 norm partials at any S
         if not self._shard:
@@ -403,7 +405,7 @@ class DataParallelStep:
         finalize launch of ``jobs`` (``SW.dp_fc_split_rows``)."""
         dy, dy_lo, x, x_lo = self._gathered_cols()
         if jobs is not None:
-            return self.ops.fc_wgrad_split(dy, x, self.G["wfc"], self.G["bfc"], jobs, int(SW.dp_fc_split_rows),
+            return self.ops.fc_wgrad_split(dy, x, self.G["wfc"], self.G["bfc"], jobs, self._fc_split_rows,
                                            self.norm_part, cpb=self._fc_cpb, **self._lo(dh_lo=dy_lo, x_lo=x_lo))
         return self.ops.fc_wgrad(dy, x, self.G["wfc"], self.G["bfc"], norm=(self.norm_part, 0),
                                  **self._lo(dh_lo=dy_lo, x_lo=x_lo)) or 0
@@ -420,7 +422,7 @@ class DataParallelStep:
             dy, dy_lo, x, x_lo = self._gathered_cols()
             r0, S = self._fc_r0, self._fc_S
             n = self.ops.fc_wgrad_split(dy[:, r0:r0 + S], x, w_own.view(S, FC_COLS), b_own, jobs,
-                                        int(SW.dp_fc_split_rows), self.fcn_send,
+                                        self._fc_split_rows, self.fcn_send,
                                         cpb=self._fc_cpb,
                                         **self._lo(dh_lo=None if dy_lo is None else dy_lo[:, r0:r0 + S], x_lo=x_lo))
         elif self._fc_factors:

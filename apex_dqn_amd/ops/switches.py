@@ -94,8 +94,10 @@ class Switches:
     dp_branch_one_wait: bool = True
     # DP step, sharded update with the factored exchange: this rank's fc weight-gradient rows
     # as split-K partials of this many reduction rows each, reduced in conv1's finalize
-    # launch (0: one launch over all rows writing the gradient itself)
-    dp_fc_split_rows: int = 128
+    # launch (0: one launch over all rows writing the gradient itself; -1: 256 at 8+ ranks,
+    # else 128 -- emulated W = 8 157.3 vs 159.0 us, W = 4 193.9 vs 190.5 at 256,
+    # profiles/r6_ab_dp_fc_split_rows.txt)
+    dp_fc_split_rows: int = -1
     # DP step, sharded update: the [w2, wfc) bucket's clip-norm partials on the branch and
     # conv1's bucket summed inside the optimizer launch (no norm launch on main; emulated W =
     # 8 with the fc gradient on main: 160.5-162.1 us vs 166-169 before)
